@@ -1,0 +1,111 @@
+"""ctypes binding of libgreedymml_hip.so (the C ABI in include/greedymml.h).
+
+The library is loaded AFTER `import torch` so that it binds to PyTorch's HIP
+runtime instance (same SONAME libamdhip64.so.7).  There is no fallback: if the
+library is missing or fails to load, every op raises.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL: shared HIP runtime)
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "libgreedymml_hip.so")
+
+GM_F32, GM_BF16 = 0, 1
+GM_NCHW, GM_NHWC = 0, 1
+ABI_VERSION = 1
+
+c_int, c_float, c_void_p, c_size_t = ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
+c_float_p = ctypes.c_void_p  # device pointers are opaque
+
+
+class SpatialReduce(ctypes.Structure):
+    _fields_ = [("x", c_void_p), ("dy", c_void_p), ("C", c_int), ("HW", c_int),
+                ("out", c_void_p), ("ld_out", c_int), ("e", c_void_p), ("ld_e", c_int),
+                ("scale", c_float)]
+
+
+class ChannelScale(ctypes.Structure):
+    _fields_ = [("x", c_void_p), ("y", c_void_p), ("C", c_int), ("HW", c_int),
+                ("s", c_void_p), ("ld_s", c_int), ("a", c_void_p), ("ld_a", c_int),
+                ("alpha", c_float)]
+
+
+class Operand(ctypes.Structure):
+    _fields_ = [("ptr", c_void_p), ("ld0", c_int), ("ld1", c_int)]
+
+
+class Gemm(ctypes.Structure):
+    _fields_ = [("M", c_int), ("N", c_int), ("K", c_int * 2), ("A", Operand * 2),
+                ("B", Operand * 2), ("bias", c_void_p), ("mask", c_void_p), ("ld_mask", c_int),
+                ("C", c_void_p), ("ld_c", c_int), ("act", c_int), ("accumulate", c_int)]
+
+
+class Tensor(ctypes.Structure):
+    _fields_ = [("param", c_void_p), ("grad", c_void_p), ("n", ctypes.c_longlong),
+                ("offset", ctypes.c_longlong), ("group_mask", ctypes.c_uint),
+                ("pad", ctypes.c_uint)]
+
+
+EXPORTS = {
+    "gm_abi_version": (c_int, []),
+    "gm_last_error": (ctypes.c_char_p, []),
+    "gm_spatial_reduce_scratch": (c_size_t, [c_void_p, c_int, c_int, c_int, c_int]),
+    "gm_mmtm_spatial_reduce": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_size_t,
+                                       c_void_p]),
+    "gm_mmtm_channel_scale": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
+    "gm_gemm_f32": (c_int, [c_void_p, c_int, c_void_p]),
+    "gm_mmtm_running_avg": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                    c_void_p, c_int, c_void_p]),
+    "gm_group_sumsq_scratch": (c_size_t, [ctypes.c_longlong]),
+    "gm_group_sumsq": (c_int, [c_void_p, c_int, ctypes.c_longlong, c_int, c_float, c_float,
+                               c_void_p, c_void_p, c_size_t, c_void_p]),
+}
+
+_lib = None
+
+
+class GreedyMMLError(RuntimeError):
+    pass
+
+
+def load():
+    """Load (once) and return the CDLL; raises if the HIP library is unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise GreedyMMLError(
+            f"{LIB_PATH} not built: run `python -m greedy_multimodal_learning_amd.build` "
+            "(no CPU fallback exists)")
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_LOCAL)
+    for name, (res, args) in EXPORTS.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    v = lib.gm_abi_version()
+    if v != ABI_VERSION:
+        raise GreedyMMLError(f"ABI mismatch: library {v}, bindings {ABI_VERSION}")
+    _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = load().gm_last_error().decode(errors="replace")
+        raise GreedyMMLError(f"{what} failed (rc={rc}): {msg}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (0 for None)."""
+    return 0 if t is None else t.data_ptr()
+
+
+def stream_of(device=None):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def arr(struct_type, items):
+    a = (struct_type * len(items))(*items)
+    return a

@@ -1,0 +1,287 @@
+"""Conditional-learning-speed gating on MI355X: drop-in for the gating classes
+of the reference's `src.callbacks`.
+
+`Bias_Mitigation_Strong(epsilon, curation_windowsize, branchnames,
+starting_epoch=2, MMTMnames=['visual','skeleton'])` and
+`Bias_Mitigation_Random()` keep the reference's gin parameters, hook protocol
+(`set_model`, `set_model_pytoune`, `on_train_begin`, `on_epoch_begin`,
+`on_backward_end`, `on_batch_end`; src/callbacks.py:94-170) and state machine
+(src/callbacks.py:173-302).  `compute_BDR` replaces the reference's per-tensor
+`(p**2).sum().item()` / `(g**2).sum().item()` loop (284 host syncs per step,
+:203-205) by ONE multi-tensor HIP pass (`gm_group_sumsq`) that produces every
+group's sums at once, followed by a single 8-double device->host copy.
+
+Group semantics (:207-223): names containing 'mmtm' go to bypass[i] when they
+contain MMTMnames[i], to all bypass groups when they contain none (the shared
+fc_squeeze); other names go to main[i] when they contain branchnames[i].
+"""
+import ctypes
+import random
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from .gin_lite import configurable
+
+
+class Callback(object):
+    """Hook protocol of the reference (src/callbacks.py:94-170)."""
+
+    def __init__(self):
+        pass
+
+    def set_config(self, config):
+        self.config = config
+
+    def set_meta_data(self, meta_data):
+        self.meta_data = meta_data
+
+    def set_save_path(self, save_path):
+        self.save_path = save_path
+
+    def set_optimizer(self, optimizer):
+        self.optimizer = optimizer
+
+    def set_model(self, model, ignore=True):
+        if ignore:
+            return
+        self.model = model
+
+    def set_model_pytoune(self, model_pytoune):
+        self.model_pytoune = model_pytoune
+
+    def set_params(self, params):
+        self.params = params
+
+    def set_dataloader(self, data):
+        self.data = data
+
+    def on_epoch_begin(self, epoch, logs):
+        pass
+
+    def on_epoch_end(self, epoch, logs):
+        pass
+
+    def on_batch_begin(self, batch, logs):
+        pass
+
+    def on_batch_end(self, batch, logs):
+        pass
+
+    def on_forward_begin(self, batch, data):
+        pass
+
+    def on_backward_end(self, batch):
+        pass
+
+    def on_train_begin(self, logs):
+        pass
+
+    def on_train_end(self, logs):
+        pass
+
+    def on_val_batch_end(self, batch, logs):
+        pass
+
+
+def group_masks(names, branchnames, MMTMnames):
+    """Bit i = main[i] (i < len(branchnames)); bit nb+j = bypass[j]."""
+    nb = len(branchnames)
+    out = []
+    for name in names:
+        m = 0
+        if "mmtm" in name:
+            hit = [j for j, mod in enumerate(MMTMnames) if mod in name]
+            for j in (hit if hit else range(len(MMTMnames))):
+                m |= 1 << (nb + j)
+        else:
+            for i, b in enumerate(branchnames):
+                if b in name:
+                    m |= 1 << i
+        out.append(m)
+    return out
+
+
+class GroupNorms:
+    """Device-side per-group sum(w^2), sum(g^2) over a fixed parameter list.
+
+    `sums(grad_scale=1.0, lr=0.0)` launches gm_group_sumsq (optionally fused with
+    the SGD update) and returns a float64 device tensor [2*ngroups] (no sync).
+    """
+
+    def __init__(self, named_params, branchnames, MMTMnames):
+        self.names = [n for n, _ in named_params]
+        self.params = [p for _, p in named_params]
+        self.ngroups = len(branchnames) + len(MMTMnames)
+        self.masks = group_masks(self.names, branchnames, MMTMnames)
+        self.total = int(sum(p.numel() for p in self.params))
+        self.device = self.params[0].device
+        self._key = None
+        self._table = None
+        self._scratch = None
+        self._out = None
+
+    def _build(self):
+        key = tuple((p.data_ptr(), 0 if p.grad is None else p.grad.data_ptr()) for p in self.params)
+        if key == self._key:
+            return
+        for p in self.params:
+            if p.dtype != torch.float32 or not p.is_contiguous():
+                raise L.GreedyMMLError("group norms need contiguous fp32 parameters")
+            if p.grad is not None and (p.grad.dtype != torch.float32 or not p.grad.is_contiguous()):
+                raise L.GreedyMMLError("group norms need contiguous fp32 gradients")
+        n = len(self.params)
+        tab = (L.Tensor * n)()
+        off = 0
+        for i, p in enumerate(self.params):
+            tab[i] = L.Tensor(p.data_ptr(), 0 if p.grad is None else p.grad.data_ptr(),
+                              p.numel(), off, self.masks[i], 0)
+            off += p.numel()
+        host = torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8)
+        self._table = host.to(self.device)
+        self._key = key
+        if self._scratch is None:
+            need = L.load().gm_group_sumsq_scratch(self.total)
+            self._scratch = torch.empty(need, dtype=torch.uint8, device=self.device)
+            self._out = torch.empty(2 * self.ngroups, dtype=torch.float64, device=self.device)
+
+    def sums(self, grad_scale=1.0, lr=0.0):
+        L.load()
+        if not self.params[0].is_cuda:
+            raise L.GreedyMMLError("group norms run on HIP devices only (no CPU fallback)")
+        self._build()
+        out = torch.empty(2 * self.ngroups, dtype=torch.float64, device=self.device)
+        L.check(L.load().gm_group_sumsq(self._table.data_ptr(), len(self.params), self.total,
+                                        self.ngroups, float(grad_scale), float(lr), out.data_ptr(),
+                                        self._scratch.data_ptr(), self._scratch.numel(),
+                                        L.stream_of(self.device)), "gm_group_sumsq")
+        return out
+
+
+def bdr_update(M_bypass, M_main, s, nb):
+    """Accumulate the M's from one step's group sums (host float64) and return d_BDR.
+    s = [w_main0, g_main0, w_main1, g_main1, w_by0, g_by0, w_by1, g_by1]."""
+    for i in range(nb):
+        M_main[i] += s[2 * i + 1] / s[2 * i]
+        M_bypass[i] += s[2 * (nb + i) + 1] / s[2 * (nb + i)]
+    bdr0 = np.log10(M_bypass[0] / M_main[0])
+    bdr1 = np.log10(M_bypass[1] / M_main[1])
+    return bdr0 - bdr1
+
+
+@configurable
+class Bias_Mitigation_Strong(Callback):
+    def __init__(self, epsilon, curation_windowsize, branchnames, starting_epoch=2,
+                 MMTMnames=['visual', 'skeleton']):
+        self.epsilon = epsilon
+        self.branchnames = list(branchnames)
+        self.MMTMnames = list(MMTMnames)
+        self.curation_windowsize = curation_windowsize
+        self.starting_epoch = starting_epoch
+        self._norms = None
+        # set by a fused engine: group sums already computed this step (device tensor)
+        self.pending_sums = None
+        super().__init__()
+
+    def on_train_begin(self, logs):
+        self.M_bypass_modal_0 = 0
+        self.M_bypass_modal_1 = 0
+        self.M_main_modal_0 = 0
+        self.M_main_modal_1 = 0
+        self.model_pytoune.curation_mode = False
+        self.model_pytoune.caring_modality = None
+        self.unlock = False
+
+    def group_sums(self):
+        """Device float64 [8]: (w, g) sums of main0, main1, bypass0, bypass1."""
+        if self.pending_sums is not None:
+            s, self.pending_sums = self.pending_sums, None
+            return s
+        named = list(self.model.named_parameters())
+        if self._norms is None or self._norms.names != [n for n, _ in named]:
+            self._norms = GroupNorms(named, self.branchnames, self.MMTMnames)
+        return self._norms.sums()
+
+    def compute_BDR(self):
+        s = self.group_sums().cpu().numpy()  # the step's single host sync
+        M_by = [self.M_bypass_modal_0, self.M_bypass_modal_1]
+        M_main = [self.M_main_modal_0, self.M_main_modal_1]
+        d = bdr_update(M_by, M_main, s, len(self.branchnames))
+        self.M_bypass_modal_0, self.M_bypass_modal_1 = M_by
+        self.M_main_modal_0, self.M_main_modal_1 = M_main
+        return d
+
+    def on_batch_end(self, batch, logs):
+        logs['curation_mode'] = float(self.model_pytoune.curation_mode)
+        logs['caring_modality'] = self.model_pytoune.caring_modality
+        logs['d_BDR'] = self.d_BDR
+
+    def needs_bdr(self):
+        """True when on_backward_end of this step will call compute_BDR."""
+        return (not self.unlock) or (not self.model_pytoune.curation_mode)
+
+    def on_backward_end(self, batch):
+        mp = self.model_pytoune
+        if self.unlock:
+            if not mp.curation_mode:
+                self.d_BDR = self.compute_BDR()
+                if abs(self.d_BDR) > self.epsilon:
+                    biased_direction = np.sign(self.d_BDR)
+                    mp.curation_mode = True
+                    self.curation_step = 0
+                    if biased_direction == -1:
+                        mp.caring_modality = 1
+                    elif biased_direction == 1:
+                        mp.caring_modality = 0
+                else:
+                    mp.curation_mode = False
+                    mp.caring_modality = 0
+            else:
+                self.pending_sums = None
+                self.curation_step += 1
+                if self.curation_step == self.curation_windowsize:
+                    mp.curation_mode = False
+        else:
+            self.d_BDR = self.compute_BDR()
+            mp.curation_mode = False
+            mp.caring_modality = 0
+
+    def on_epoch_begin(self, epoch, logs):
+        if epoch >= self.starting_epoch:
+            self.unlock = True
+
+
+@configurable
+class Bias_Mitigation_Random(Callback):
+    """Random gating (src/callbacks.py:269-302): python `random` global RNG."""
+
+    def on_train_begin(self, logs):
+        self.model_pytoune.curation_mode = False
+        self.model_pytoune.caring_modality = None
+        self.unlock = False
+        self.starting_epoch = 2
+
+    def on_batch_end(self, batch, logs):
+        logs['curation_mode'] = float(self.model_pytoune.curation_mode)
+        logs['caring_modality'] = self.model_pytoune.caring_modality
+
+    def needs_bdr(self):
+        return False
+
+    def on_backward_end(self, batch):
+        mp = self.model_pytoune
+        if self.unlock:
+            mode = random.choice([0, 1, 2])
+            if mode == 0:
+                mp.curation_mode, mp.caring_modality = False, 0
+            elif mode == 1:
+                mp.curation_mode, mp.caring_modality = True, 1
+            else:
+                mp.curation_mode, mp.caring_modality = True, 0
+        else:
+            mp.curation_mode, mp.caring_modality = False, 0
+
+    def on_epoch_begin(self, epoch, logs):
+        if epoch >= self.starting_epoch:
+            self.unlock = True

@@ -1,0 +1,78 @@
+// Internal helpers shared by the HIP translation units of libgreedymml_hip.so.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstdint>
+
+#include "greedymml.h"
+
+namespace gm {
+
+// ---- error reporting (thread-local text, no exceptions across the ABI) ----
+void set_error(const char* fmt, ...);
+int check_launch(const char* what);
+
+#define GM_REQUIRE(cond, ...)                 \
+    do {                                      \
+        if (!(cond)) {                        \
+            ::gm::set_error(__VA_ARGS__);     \
+            return GM_E_ARG;                  \
+        }                                     \
+    } while (0)
+
+// ---- element access ----
+template <typename T> struct Elem;
+template <> struct Elem<float> {
+    static __device__ __forceinline__ float ld(const float* p) { return *p; }
+    static __device__ __forceinline__ void st(float* p, float v) { *p = v; }
+};
+// bf16 stored as raw uint16 (upper half of an f32)
+template <> struct Elem<uint16_t> {
+    static __device__ __forceinline__ float ld(const uint16_t* p) {
+        return __uint_as_float(((uint32_t)*p) << 16);
+    }
+    static __device__ __forceinline__ void st(uint16_t* p, float v) { *p = f2bf(v); }
+    static __device__ __forceinline__ uint16_t f2bf(float v) {
+        __bf16 h = (__bf16)v;  // v_cvt_pk_bf16_f32: RNE, NaN-preserving
+        return __builtin_bit_cast(uint16_t, h);
+    }
+};
+
+__device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+__device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
+    return (uint32_t)Elem<uint16_t>::f2bf(lo) | ((uint32_t)Elem<uint16_t>::f2bf(hi) << 16);
+}
+
+// 64-lane wave sum (gfx950 wave64)
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// unsigned fast division by a runtime constant (host-side precomputed magic)
+struct FastDiv {
+    uint32_t d, m, s;
+    FastDiv() : d(1), m(0), s(0) {}
+    explicit FastDiv(uint32_t div) : d(div) {
+        s = 0;
+        while ((1ull << s) < div) ++s;
+        m = (uint32_t)((((1ull << 32) * ((1ull << s) - div)) / div) + 1);
+    }
+    __device__ __forceinline__ uint32_t div(uint32_t n) const {
+        uint32_t t = __umulhi(n, m);
+        return (uint32_t)(((uint64_t)t + n) >> s);
+    }
+};
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+}  // namespace gm

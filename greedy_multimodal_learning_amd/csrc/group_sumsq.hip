@@ -1,0 +1,157 @@
+// Per-branch weight/gradient norms (+ fused SGD) for the conditional-learning-
+// speed gate: one multi-tensor pass over all parameters and gradients.
+//
+// Reference: Bias_Mitigation_Strong.compute_BDR (src/callbacks.py:199-233) runs
+// `(p**2).sum().item()` and `(g**2).sum().item()` for each of the 142 parameter
+// tensors (284 host syncs per step) and then torch.optim.SGD updates them
+// (train.py:48-51).  Here: ONE streaming pass.  The virtual concatenation of all
+// tensors is cut into fixed chunks; each workgroup streams its chunk with 16-byte
+// loads, accumulates per-thread fp32 partials per tensor segment, folds them into
+// fp64 per-group sums, and writes one fp64 row per workgroup; a second 1-block
+// pass adds the rows in fixed order.  HBM bytes/step: 8*N (read p, g) without the
+// update, 12*N with it (read p, g; write p).  Deterministic.
+#include "gm_common.h"
+
+namespace gm {
+
+constexpr int kChunk = 16384;     // elements per workgroup
+constexpr int kMaxGroups = 8;
+
+__device__ __forceinline__ int find_tensor(const gm_tensor* t, int nt, long long e) {
+    int lo = 0, hi = nt - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (t[mid].offset <= e) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+template <bool SGD>
+__global__ __launch_bounds__(256) void k_group_sumsq(const gm_tensor* __restrict__ tab, int nt,
+                                                     long long total, int ngroups, float gscale,
+                                                     float lr, double* __restrict__ rows) {
+    __shared__ double sred[4][2 * kMaxGroups];
+    const long long e0 = (long long)blockIdx.x * kChunk;
+    const long long e1 = min(total, e0 + kChunk);
+    double gw[kMaxGroups], gg[kMaxGroups];
+#pragma unroll
+    for (int g = 0; g < kMaxGroups; ++g) { gw[g] = 0.0; gg[g] = 0.0; }
+    int ti = find_tensor(tab, nt, e0);
+    long long e = e0;
+    while (e < e1) {
+        const gm_tensor T = tab[ti];
+        const long long tb = e - T.offset;                       // first local element
+        const long long te = min(T.n, e1 - T.offset);            // end (exclusive)
+        float* __restrict__ p = T.param;
+        const float* __restrict__ gr = T.grad;
+        float sw = 0.f, sg = 0.f;
+        // scalar head up to 16-byte alignment of p (and g)
+        long long a = tb;
+        const bool vec_ok = gr == nullptr || (((uintptr_t)(p + a) ^ (uintptr_t)(gr + a)) & 15) == 0;
+        long long head = a;
+        if (vec_ok) {
+            while (head < te && ((uintptr_t)(p + head) & 15)) ++head;
+        } else {
+            head = te;
+        }
+        for (long long i = a + threadIdx.x; i < head; i += 256) {
+            const float w = p[i];
+            const float g = gr ? gr[i] * gscale : 0.f;
+            sw = fmaf(w, w, sw);
+            sg = fmaf(g, g, sg);
+            if (SGD && gr) p[i] = fmaf(-lr, g, w);
+        }
+        const long long nv = (te - head) >> 2;
+        float4* pv = (float4*)(p + head);
+        const float4* gv = (const float4*)(gr ? gr + head : nullptr);
+        for (long long i = threadIdx.x; i < nv; i += 256) {
+            const float4 w = pv[i];
+            sw = fmaf(w.x, w.x, sw); sw = fmaf(w.y, w.y, sw);
+            sw = fmaf(w.z, w.z, sw); sw = fmaf(w.w, w.w, sw);
+            if (gr) {
+                float4 g = gv[i];
+                g.x *= gscale; g.y *= gscale; g.z *= gscale; g.w *= gscale;
+                sg = fmaf(g.x, g.x, sg); sg = fmaf(g.y, g.y, sg);
+                sg = fmaf(g.z, g.z, sg); sg = fmaf(g.w, g.w, sg);
+                if (SGD)
+                    pv[i] = make_float4(fmaf(-lr, g.x, w.x), fmaf(-lr, g.y, w.y),
+                                        fmaf(-lr, g.z, w.z), fmaf(-lr, g.w, w.w));
+            }
+        }
+        for (long long i = head + nv * 4 + threadIdx.x; i < te; i += 256) {
+            const float w = p[i];
+            const float g = gr ? gr[i] * gscale : 0.f;
+            sw = fmaf(w, w, sw);
+            sg = fmaf(g, g, sg);
+            if (SGD && gr) p[i] = fmaf(-lr, g, w);
+        }
+        const unsigned m = T.group_mask;
+#pragma unroll
+        for (int g = 0; g < kMaxGroups; ++g)
+            if (g < ngroups && ((m >> g) & 1u)) { gw[g] += (double)sw; gg[g] += (double)sg; }
+        e = T.offset + te;
+        ++ti;
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int g = 0; g < kMaxGroups; ++g) {
+        if (g >= ngroups) break;
+        const double w = wave_sum_d(gw[g]);
+        const double s = wave_sum_d(gg[g]);
+        if (lane == 0) { sred[wave][2 * g] = w; sred[wave][2 * g + 1] = s; }
+    }
+    __syncthreads();
+    if (threadIdx.x < 2 * ngroups) {
+        const int j = threadIdx.x;
+        rows[(size_t)blockIdx.x * 2 * ngroups + j] = ((sred[0][j] + sred[1][j]) + sred[2][j]) + sred[3][j];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_group_finalize(const double* __restrict__ rows, int nrows,
+                                                        int ngroups, double* __restrict__ out) {
+    __shared__ double s[256];
+    const int w = 2 * ngroups;
+    for (int j = 0; j < w; ++j) {
+        double acc = 0.0;
+        for (int r = threadIdx.x; r < nrows; r += 256) acc += rows[(size_t)r * w + j];
+        s[threadIdx.x] = acc;
+        __syncthreads();
+        for (int o = 128; o > 0; o >>= 1) {
+            if ((int)threadIdx.x < o) s[threadIdx.x] += s[threadIdx.x + o];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) out[j] = s[0];
+        __syncthreads();
+    }
+}
+
+}  // namespace gm
+
+using namespace gm;
+
+extern "C" size_t gm_group_sumsq_scratch(long long total) {
+    if (total <= 0) return 0;
+    const long long nb = (total + kChunk - 1) / kChunk;
+    return (size_t)nb * 2 * kMaxGroups * sizeof(double);
+}
+
+extern "C" int gm_group_sumsq(const gm_tensor* table, int nt, long long total, int ngroups, float gscale,
+                              float lr, double* out, void* scratch, size_t scratch_bytes, void* stream) {
+    GM_REQUIRE(table && nt >= 1 && total >= 1, "group_sumsq: empty tensor table");
+    GM_REQUIRE(ngroups >= 1 && ngroups <= kMaxGroups, "group_sumsq: ngroups must be 1..%d", kMaxGroups);
+    GM_REQUIRE(out, "group_sumsq: null output");
+    const long long nb = (total + kChunk - 1) / kChunk;
+    GM_REQUIRE(nb < (1ll << 31), "group_sumsq: too many elements");
+    GM_REQUIRE(scratch && scratch_bytes >= gm_group_sumsq_scratch(total),
+               "group_sumsq: scratch %zu < %zu bytes", scratch_bytes, gm_group_sumsq_scratch(total));
+    hipStream_t st = as_stream(stream);
+    double* rows = (double*)scratch;
+    if (lr != 0.f)
+        k_group_sumsq<true><<<(int)nb, 256, 0, st>>>(table, nt, total, ngroups, gscale, lr, rows);
+    else
+        k_group_sumsq<false><<<(int)nb, 256, 0, st>>>(table, nt, total, ngroups, gscale, lr, rows);
+    int rc = check_launch("k_group_sumsq");
+    if (rc) return rc;
+    k_group_finalize<<<1, 256, 0, st>>>(rows, (int)nb, ngroups, out);
+    return check_launch("k_group_finalize");
+}

@@ -1,0 +1,479 @@
+// MMTM squeeze / excitation-scale kernels for gfx950 (wave64).
+//
+// Spatial reduction (squeeze and its backward) and channel re-scale of
+// MMTM_mitigate (reference src/balanced_mmtm.py:49-154).  HBM-bound: every
+// kernel streams its activations exactly once with 16-byte vector loads where
+// alignment allows, accumulates in fp32 and reduces with wave shuffles + LDS.
+//
+//   NCHW: one wave per (b,c) row of HW contiguous elements; the row is read with
+//         the widest aligned vector (2..16 B/lane) and reduced by wave shuffles.
+//   NHWC: a 256-thread workgroup per (b, HW-split); each thread owns 16 B of
+//         channels, walks pixels, then the pixel lanes are reduced through LDS.
+//         Splits write fp32 partials which a second pass sums in fixed order
+//         (deterministic, no float atomics).
+#include <cstring>
+
+#include "gm_common.h"
+
+namespace gm {
+
+constexpr int kMaxProb = 4;
+
+struct RedProb {
+    const void* x;
+    const void* dy;
+    float* out;
+    const float* e;
+    int C, HW, ld_out, ld_e;
+    float scale;
+    int row_start;   // NCHW: first global row (b*C + c) of this problem
+    int wg_start;    // NHWC: first workgroup of this problem
+    int S;           // NHWC: HW splits
+    int hw_per;      // NHWC: pixels per split
+    float* part;     // NHWC partials [B][S][C] (S > 1)
+};
+struct RedArgs {
+    RedProb p[kMaxProb];
+    int nprob, B;
+};
+
+__device__ __forceinline__ float epilogue(float g, const RedProb& p, int b, int c) {
+    g *= p.scale;
+    if (p.e) {
+        float e = p.e[(size_t)b * p.ld_e + c];
+        g = g * ((1.0f - e) * e);
+    }
+    return g;
+}
+
+// ---- vector loaders: VB bytes per lane -> N floats ----
+template <typename T, int VB> struct VecLd;
+template <int VB> struct VecLd<float, VB> {
+    static constexpr int N = VB / 4;
+    static __device__ __forceinline__ void ld(const float* p, float* v) {
+        if constexpr (VB == 16) { float4 t = *(const float4*)p; v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w; }
+        else if constexpr (VB == 8) { float2 t = *(const float2*)p; v[0] = t.x; v[1] = t.y; }
+        else { v[0] = *p; }
+    }
+};
+template <int VB> struct VecLd<uint16_t, VB> {
+    static constexpr int N = VB / 2;
+    static __device__ __forceinline__ void ld(const uint16_t* p, float* v) {
+        if constexpr (VB == 16) {
+            uint4 t = *(const uint4*)p;
+            v[0] = bf_lo(t.x); v[1] = bf_hi(t.x); v[2] = bf_lo(t.y); v[3] = bf_hi(t.y);
+            v[4] = bf_lo(t.z); v[5] = bf_hi(t.z); v[6] = bf_lo(t.w); v[7] = bf_hi(t.w);
+        } else if constexpr (VB == 8) {
+            uint2 t = *(const uint2*)p;
+            v[0] = bf_lo(t.x); v[1] = bf_hi(t.x); v[2] = bf_lo(t.y); v[3] = bf_hi(t.y);
+        } else if constexpr (VB == 4) {
+            uint32_t t = *(const uint32_t*)p;
+            v[0] = bf_lo(t); v[1] = bf_hi(t);
+        } else {
+            v[0] = __uint_as_float(((uint32_t)*p) << 16);
+        }
+    }
+};
+
+// ---------------- NCHW: one wave per row ----------------
+template <typename T, int VB, bool BWD>
+__global__ __launch_bounds__(256) void k_rowreduce_nchw(RedArgs a, int total_rows) {
+    using L = VecLd<T, VB>;
+    constexpr int N = L::N;
+    const int lane = threadIdx.x & 63;
+    const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int nwaves = (gridDim.x * blockDim.x) >> 6;
+    for (int row = wave; row < total_rows; row += nwaves) {
+        int pi = 0;
+#pragma unroll
+        for (int q = 1; q < kMaxProb; ++q)
+            if (q < a.nprob && row >= a.p[q].row_start) pi = q;
+        const RedProb& p = a.p[pi];
+        const int r = row - p.row_start;
+        const size_t base = (size_t)r * p.HW;
+        const T* x = (const T*)p.x + base;
+        const T* dy = BWD ? (const T*)p.dy + base : nullptr;
+        const int nvec = p.HW / N;
+        float acc = 0.f;
+        for (int i = lane; i < nvec; i += 64) {
+            float vx[N];
+            L::ld(x + (size_t)i * N, vx);
+            if constexpr (BWD) {
+                float vd[N];
+                L::ld(dy + (size_t)i * N, vd);
+#pragma unroll
+                for (int j = 0; j < N; ++j) acc = fmaf(vx[j], vd[j], acc);
+            } else {
+#pragma unroll
+                for (int j = 0; j < N; ++j) acc += vx[j];
+            }
+        }
+        acc = wave_sum(acc);
+        if (lane == 0) {
+            const int b = r / p.C, c = r - b * p.C;
+            p.out[(size_t)b * p.ld_out + c] = epilogue(acc, p, b, c);
+        }
+    }
+}
+
+// ---------------- NHWC: workgroup per (b, split) ----------------
+template <typename T, bool BWD>
+__global__ __launch_bounds__(256) void k_colreduce_nhwc(RedArgs a) {
+    constexpr int N = 16 / (int)sizeof(T);  // channels per thread (16 B)
+    __shared__ float red[256 * N];
+    int pi = 0;
+#pragma unroll
+    for (int q = 1; q < kMaxProb; ++q)
+        if (q < a.nprob && (int)blockIdx.x >= a.p[q].wg_start) pi = q;
+    const RedProb& p = a.p[pi];
+    const int w = blockIdx.x - p.wg_start;
+    const int b = w / p.S, s = w - b * p.S;
+    const int tpp = p.C / N;          // threads per pixel
+    const int ppi = 256 / tpp;        // pixels per iteration
+    const int t = threadIdx.x;
+    const int cc = t % tpp, pl = t / tpp;
+    const int hw0 = s * p.hw_per, hw1 = min(p.HW, hw0 + p.hw_per);
+    float acc[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) acc[j] = 0.f;
+    if (pl < ppi) {
+        const size_t bbase = (size_t)b * p.HW * p.C + (size_t)cc * N;
+        for (int hw = hw0 + pl; hw < hw1; hw += ppi) {
+            const size_t off = bbase + (size_t)hw * p.C;
+            float vx[N];
+            VecLd<T, 16>::ld((const T*)p.x + off, vx);
+            if constexpr (BWD) {
+                float vd[N];
+                VecLd<T, 16>::ld((const T*)p.dy + off, vd);
+#pragma unroll
+                for (int j = 0; j < N; ++j) acc[j] = fmaf(vx[j], vd[j], acc[j]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < N; ++j) acc[j] += vx[j];
+            }
+        }
+    }
+    // LDS layout [pl][C]: thread (cc, pl) writes its N channels
+    if (pl < ppi) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) red[pl * p.C + cc * N + j] = acc[j];
+    }
+    __syncthreads();
+    for (int c = t; c < p.C; c += 256) {
+        float v = 0.f;
+        for (int q = 0; q < ppi; ++q) v += red[q * p.C + c];
+        if (p.S == 1) {
+            p.out[(size_t)b * p.ld_out + c] = epilogue(v, p, b, c);
+        } else {
+            p.part[((size_t)b * p.S + s) * p.C + c] = v;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_reduce_partials(RedArgs a) {
+    // grid: (ceil(maxC/256), B, nprob)
+    const RedProb& p = a.p[blockIdx.z];
+    const int b = blockIdx.y;
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= p.C || p.S <= 1) return;
+    const float* src = p.part + (size_t)b * p.S * p.C + c;
+    float v = 0.f;
+    for (int s = 0; s < p.S; ++s) v += src[(size_t)s * p.C];
+    p.out[(size_t)b * p.ld_out + c] = epilogue(v, p, b, c);
+}
+
+// ---------------- channel scale (fwd) / apply (bwd) ----------------
+struct ScaleProb {
+    const void* x;
+    void* y;
+    const float* s;
+    const float* a;
+    int C, HW, ld_s, ld_a;
+    float alpha;
+    FastDiv div_hw;   // NCHW row = flat / HW
+    FastDiv div_c;    // NHWC: pixel = flat / C
+    FastDiv div_hwc;  // NHWC: b = flat / (HW*C)
+    long long vec_start;  // first global vector index of this problem
+    long long nvec;
+};
+struct ScaleArgs {
+    ScaleProb p[kMaxProb];
+    int nprob;
+    long long total_vec;
+};
+
+template <typename T, int N, int LAYOUT, bool ROWCONST>
+__global__ __launch_bounds__(256) void k_channel_scale(ScaleArgs a) {
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < a.total_vec; v += stride) {
+        int pi = 0;
+#pragma unroll
+        for (int q = 1; q < kMaxProb; ++q)
+            if (q < a.nprob && v >= a.p[q].vec_start) pi = q;
+        const ScaleProb& p = a.p[pi];
+        const uint32_t i0 = (uint32_t)((v - p.vec_start) * N);
+        const T* x = (const T*)p.x + i0;
+        T* y = (T*)p.y + i0;
+        float vx[N], sc[N], ad[N];
+        VecLd<T, N * (int)sizeof(T)>::ld(x, vx);
+        if (LAYOUT == GM_NCHW) {
+            if (ROWCONST) {
+                const uint32_t row = p.div_hw.div(i0);
+                const uint32_t b = row / (uint32_t)p.C, c = row - b * (uint32_t)p.C;
+                const float s0 = p.s[(size_t)b * p.ld_s + c];
+                const float a0 = p.a ? p.a[(size_t)b * p.ld_a + c] * p.alpha : 0.f;
+#pragma unroll
+                for (int j = 0; j < N; ++j) { sc[j] = s0; ad[j] = a0; }
+            } else {
+#pragma unroll
+                for (int j = 0; j < N; ++j) {
+                    const uint32_t row = p.div_hw.div(i0 + j);
+                    const uint32_t b = row / (uint32_t)p.C, c = row - b * (uint32_t)p.C;
+                    sc[j] = p.s[(size_t)b * p.ld_s + c];
+                    ad[j] = p.a ? p.a[(size_t)b * p.ld_a + c] * p.alpha : 0.f;
+                }
+            }
+        } else {
+            const uint32_t b = p.div_hwc.div(i0);
+            const uint32_t c0 = i0 - p.div_c.div(i0) * (uint32_t)p.C;
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+                sc[j] = p.s[(size_t)b * p.ld_s + c0 + j];
+                ad[j] = p.a ? p.a[(size_t)b * p.ld_a + c0 + j] * p.alpha : 0.f;
+            }
+        }
+        float o[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) o[j] = p.a ? fmaf(vx[j], sc[j], ad[j]) : vx[j] * sc[j];
+        if constexpr (sizeof(T) == 2) {
+            if constexpr (N == 8) {
+                uint4 w;
+                w.x = pack_bf2(o[0], o[1]); w.y = pack_bf2(o[2], o[3]);
+                w.z = pack_bf2(o[4], o[5]); w.w = pack_bf2(o[6], o[7]);
+                *(uint4*)y = w;
+            } else {
+#pragma unroll
+                for (int j = 0; j < N; ++j) Elem<uint16_t>::st((uint16_t*)y + j, o[j]);
+            }
+        } else {
+            if constexpr (N == 4) {
+                *(float4*)y = make_float4(o[0], o[1], o[2], o[3]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < N; ++j) ((float*)y)[j] = o[j];
+            }
+        }
+    }
+}
+
+// ---------------- running averages ----------------
+__global__ __launch_bounds__(256) void k_running_avg(const float* e, int ld, int B, int C,
+                                                     const float* rv, const float* rs,
+                                                     float* ov, float* os, int step) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= C) return;
+    float m = 0.f;
+    for (int b = 0; b < B; ++b) m += e[(size_t)b * ld + c];
+    m = m / (float)B;
+    const float k = (float)step, k1 = (float)(step + 1);
+    ov[c] = (m + rv[c] * k) / k1;
+    os[c] = (m + rs[c] * k) / k1;
+}
+
+static bool aligned(const void* p, int bytes) { return ((uintptr_t)p % bytes) == 0; }
+
+}  // namespace gm
+
+using namespace gm;
+
+// ======================= host entry points =======================
+
+static int red_setup(const gm_spatial_reduce* in, int nprob, int B, int dtype, int layout,
+                     RedArgs& a, size_t& scratch_need, int& nwg, int& vb) {
+    GM_REQUIRE(in && nprob >= 1 && nprob <= kMaxProb, "spatial_reduce: nprob must be 1..%d", kMaxProb);
+    GM_REQUIRE(B >= 1, "spatial_reduce: B must be >= 1");
+    GM_REQUIRE(dtype == GM_F32 || dtype == GM_BF16, "spatial_reduce: bad dtype %d", dtype);
+    GM_REQUIRE(layout == GM_NCHW || layout == GM_NHWC, "spatial_reduce: bad layout %d", layout);
+    const int es = dtype == GM_F32 ? 4 : 2;
+    memset(&a, 0, sizeof(a));
+    a.nprob = nprob;
+    a.B = B;
+    scratch_need = 0;
+    const bool bwd = in[0].dy != nullptr;
+    int rows = 0, wgs = 0;
+    vb = 16;
+    for (int i = 0; i < nprob; ++i) {
+        const gm_spatial_reduce& s = in[i];
+        GM_REQUIRE(s.x && s.out && s.C >= 1 && s.HW >= 1, "spatial_reduce[%d]: null pointer or empty shape", i);
+        GM_REQUIRE((s.dy != nullptr) == bwd, "spatial_reduce: all problems must agree on forward/backward");
+        GM_REQUIRE(s.ld_out >= s.C, "spatial_reduce[%d]: ld_out < C", i);
+        GM_REQUIRE(!s.e || s.ld_e >= 0, "spatial_reduce[%d]: bad ld_e", i);
+        RedProb& p = a.p[i];
+        p.x = s.x; p.dy = s.dy; p.out = s.out; p.e = s.e;
+        p.C = s.C; p.HW = s.HW; p.ld_out = s.ld_out; p.ld_e = s.ld_e; p.scale = s.scale;
+        if (layout == GM_NCHW) {
+            p.row_start = rows;
+            rows += B * s.C;
+            while (vb > es && (((size_t)s.HW * es) % vb != 0 || !aligned(s.x, vb) ||
+                               (s.dy && !aligned(s.dy, vb))))
+                vb >>= 1;
+        } else {
+            GM_REQUIRE((s.C * es) % 16 == 0 && s.C * es <= 4096,
+                       "spatial_reduce[%d]: NHWC needs C*elem %% 16 == 0 and <= 4096 B (C=%d)", i, s.C);
+            GM_REQUIRE(aligned(s.x, 16) && (!s.dy || aligned(s.dy, 16)),
+                       "spatial_reduce[%d]: NHWC tensors must be 16-byte aligned", i);
+            const int tpp = s.C * es / 16, ppi = 256 / tpp;
+            int S = (2048 + nprob * B - 1) / (nprob * B);
+            const int maxS = (s.HW + 2 * ppi - 1) / (2 * ppi);
+            S = S < 1 ? 1 : (S > maxS ? maxS : S);
+            if (S < 1) S = 1;
+            p.hw_per = (s.HW + S - 1) / S;
+            S = (s.HW + p.hw_per - 1) / p.hw_per;
+            p.S = S;
+            p.wg_start = wgs;
+            wgs += B * S;
+            if (S > 1) scratch_need += (size_t)B * S * s.C * sizeof(float);
+        }
+    }
+    nwg = layout == GM_NCHW ? rows : wgs;
+    return GM_OK;
+}
+
+extern "C" size_t gm_spatial_reduce_scratch(const gm_spatial_reduce* p, int nprob, int B, int dtype,
+                                            int layout) {
+    RedArgs a;
+    size_t need = 0;
+    int nwg = 0, vb = 0;
+    if (red_setup(p, nprob, B, dtype, layout, a, need, nwg, vb) != GM_OK) return 0;
+    return need;
+}
+
+template <typename T>
+static void launch_rows(RedArgs& a, int rows, int vb, bool bwd, hipStream_t st) {
+    const int waves_per_wg = 4;
+    int grid = (rows + waves_per_wg - 1) / waves_per_wg;
+    if (grid > 8192) grid = 8192;
+#define GM_ROWS(VB)                                                                   \
+    if (bwd) k_rowreduce_nchw<T, VB, true><<<grid, 256, 0, st>>>(a, rows);            \
+    else k_rowreduce_nchw<T, VB, false><<<grid, 256, 0, st>>>(a, rows);
+    if (vb == 16) { GM_ROWS(16) }
+    else if (vb == 8) { GM_ROWS(8) }
+    else if (vb == 4) { GM_ROWS(4) }
+    else if constexpr (sizeof(T) == 2) { GM_ROWS(2) }
+#undef GM_ROWS
+}
+
+extern "C" int gm_mmtm_spatial_reduce(const gm_spatial_reduce* in, int nprob, int B, int dtype,
+                                      int layout, void* scratch, size_t scratch_bytes, void* stream) {
+    RedArgs a;
+    size_t need = 0;
+    int nwg = 0, vb = 16;
+    int rc = red_setup(in, nprob, B, dtype, layout, a, need, nwg, vb);
+    if (rc) return rc;
+    hipStream_t st = as_stream(stream);
+    const bool bwd = in[0].dy != nullptr;
+    if (layout == GM_NCHW) {
+        if (dtype == GM_F32) launch_rows<float>(a, nwg, vb, bwd, st);
+        else launch_rows<uint16_t>(a, nwg, vb, bwd, st);
+        return check_launch("k_rowreduce_nchw");
+    }
+    GM_REQUIRE(scratch_bytes >= need && (need == 0 || scratch), "spatial_reduce: scratch %zu < %zu bytes",
+               scratch_bytes, need);
+    size_t off = 0;
+    int maxC = 0, anyS = 0;
+    for (int i = 0; i < nprob; ++i) {
+        RedProb& p = a.p[i];
+        if (p.S > 1) {
+            p.part = (float*)((char*)scratch + off);
+            off += (size_t)B * p.S * p.C * sizeof(float);
+            anyS = 1;
+        }
+        if (p.C > maxC) maxC = p.C;
+    }
+    if (dtype == GM_F32) {
+        if (bwd) k_colreduce_nhwc<float, true><<<nwg, 256, 0, st>>>(a);
+        else k_colreduce_nhwc<float, false><<<nwg, 256, 0, st>>>(a);
+    } else {
+        if (bwd) k_colreduce_nhwc<uint16_t, true><<<nwg, 256, 0, st>>>(a);
+        else k_colreduce_nhwc<uint16_t, false><<<nwg, 256, 0, st>>>(a);
+    }
+    rc = check_launch("k_colreduce_nhwc");
+    if (rc || !anyS) return rc;
+    dim3 g((maxC + 255) / 256, B, nprob);
+    k_reduce_partials<<<g, 256, 0, st>>>(a);
+    return check_launch("k_reduce_partials");
+}
+
+extern "C" int gm_mmtm_channel_scale(const gm_channel_scale* in, int nprob, int B, int dtype, int layout,
+                                     void* stream) {
+    GM_REQUIRE(in && nprob >= 1 && nprob <= kMaxProb, "channel_scale: nprob must be 1..%d", kMaxProb);
+    GM_REQUIRE(B >= 1, "channel_scale: B must be >= 1");
+    GM_REQUIRE(dtype == GM_F32 || dtype == GM_BF16, "channel_scale: bad dtype");
+    GM_REQUIRE(layout == GM_NCHW || layout == GM_NHWC, "channel_scale: bad layout");
+    const int es = dtype == GM_F32 ? 4 : 2;
+    int N = 16 / es;
+    bool rowconst = true;
+    for (int i = 0; i < nprob; ++i) {
+        const gm_channel_scale& s = in[i];
+        GM_REQUIRE(s.x && s.y && s.s && s.C >= 1 && s.HW >= 1, "channel_scale[%d]: null pointer or empty", i);
+        GM_REQUIRE(s.ld_s >= 0 && (!s.a || s.ld_a >= 0), "channel_scale[%d]: negative ld", i);
+        const size_t numel = (size_t)B * s.C * s.HW;
+        GM_REQUIRE(numel < (1ull << 32), "channel_scale[%d]: tensor too large for 32-bit indexing", i);
+        if (!aligned(s.x, 16) || !aligned(s.y, 16) || numel % N) N = 1;
+        if (layout == GM_NHWC && s.C % N) N = 1;
+        if (layout == GM_NCHW && s.HW % N) rowconst = false;
+    }
+    ScaleArgs a;
+    memset(&a, 0, sizeof(a));
+    a.nprob = nprob;
+    long long vs = 0;
+    for (int i = 0; i < nprob; ++i) {
+        const gm_channel_scale& s = in[i];
+        ScaleProb& p = a.p[i];
+        p.x = s.x; p.y = s.y; p.s = s.s; p.a = s.a;
+        p.C = s.C; p.HW = s.HW; p.ld_s = s.ld_s; p.ld_a = s.ld_a; p.alpha = s.alpha;
+        p.div_hw = FastDiv((uint32_t)s.HW);
+        p.div_c = FastDiv((uint32_t)s.C);
+        p.div_hwc = FastDiv((uint32_t)(s.HW * s.C));
+        p.vec_start = vs;
+        p.nvec = (long long)B * s.C * s.HW / N;
+        vs += p.nvec;
+    }
+    a.total_vec = vs;
+    hipStream_t st = as_stream(stream);
+    long long g = (vs + 255) / 256;
+    if (g > 16384) g = 16384;
+    const int grid = (int)g;
+#define GM_SC(T, NN, LAY, RC) k_channel_scale<T, NN, LAY, RC><<<grid, 256, 0, st>>>(a)
+    if (dtype == GM_F32) {
+        if (N == 4) {
+            if (layout == GM_NHWC) GM_SC(float, 4, GM_NHWC, true);
+            else if (rowconst) GM_SC(float, 4, GM_NCHW, true);
+            else GM_SC(float, 4, GM_NCHW, false);
+        } else {
+            if (layout == GM_NHWC) GM_SC(float, 1, GM_NHWC, true);
+            else GM_SC(float, 1, GM_NCHW, true);
+        }
+    } else {
+        if (N == 8) {
+            if (layout == GM_NHWC) GM_SC(uint16_t, 8, GM_NHWC, true);
+            else if (rowconst) GM_SC(uint16_t, 8, GM_NCHW, true);
+            else GM_SC(uint16_t, 8, GM_NCHW, false);
+        } else {
+            if (layout == GM_NHWC) GM_SC(uint16_t, 1, GM_NHWC, true);
+            else GM_SC(uint16_t, 1, GM_NCHW, true);
+        }
+    }
+#undef GM_SC
+    return check_launch("k_channel_scale");
+}
+
+extern "C" int gm_mmtm_running_avg(const float* e_v, int ld_e, int B, int C, const float* ra_v_old,
+                                   const float* ra_s_old, float* ra_v_new, float* ra_s_new, int step,
+                                   void* stream) {
+    GM_REQUIRE(e_v && ra_v_old && ra_s_old && ra_v_new && ra_s_new, "running_avg: null pointer");
+    GM_REQUIRE(B >= 1 && C >= 1 && ld_e >= C && step >= 0, "running_avg: bad shape");
+    k_running_avg<<<(C + 255) / 256, 256, 0, as_stream(stream)>>>(e_v, ld_e, B, C, ra_v_old, ra_s_old,
+                                                                  ra_v_new, ra_s_new, step);
+    return check_launch("k_running_avg");
+}

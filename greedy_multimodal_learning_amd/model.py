@@ -1,0 +1,72 @@
+"""MMTM_MVCNN on MI355X: drop-in for the reference's `src.model`.
+
+Same constructor signature, gin name, parameter names and forward contract as
+reference src/model.py:15-108: two unshared ResNet-18 trunks `net_view_0/1`
+(fc -> Linear(512, nclasses)) and MMTM fusion after layer2/3/4
+(`mmtm2/3/4`, C = 128/256/512, ratio 4).  forward(x[B,V,3,H,W],
+curation_mode, caring_modality) returns ((x0+x1)/2, [x0, x1], scales[3],
+squeezed[3]).  The MMTM sites run on libgreedymml_hip.so; `Model_`
+(src/framework.py:158-161) reads `saving_mmtm_scales` /
+`saving_mmtm_squeeze_array` from this object.
+"""
+import torch
+import torch.nn as nn
+
+from .balanced_mmtm import MMTM_mitigate as MMTM
+from .balanced_mmtm import get_rescale_weights
+from .gin_lite import configurable
+from .resnet import resnet18
+
+CLASSNAMES = ['airplane', 'bathtub', 'bed', 'bench', 'bookshelf', 'bottle', 'bowl', 'car', 'chair',
+              'cone', 'cup', 'curtain', 'desk', 'door', 'dresser', 'flower_pot', 'glass_box',
+              'guitar', 'keyboard', 'lamp', 'laptop', 'mantel', 'monitor', 'night_stand',
+              'person', 'piano', 'plant', 'radio', 'range_hood', 'sink', 'sofa', 'stairs',
+              'stool', 'table', 'tent', 'toilet', 'tv_stand', 'vase', 'wardrobe', 'xbox']
+
+
+@configurable
+class MMTM_MVCNN(nn.Module):
+    def __init__(self, nclasses=40, num_views=2, pretraining=False, mmtm_off=False,
+                 mmtm_rescale_eval_file_path=None, mmtm_rescale_training_file_path=None,
+                 device='cuda:0', saving_mmtm_scales=False, saving_mmtm_squeeze_array=False):
+        super().__init__()
+        self.classnames = list(CLASSNAMES)
+        self.nclasses = nclasses
+        self.num_views = num_views
+        self.mmtm_off = mmtm_off
+        if mmtm_off:
+            self.mmtm_rescale = get_rescale_weights(
+                mmtm_rescale_eval_file_path, mmtm_rescale_training_file_path, validation=False,
+                starting_mmtmindice=1, mmtmpositions=4, device=torch.device(device))
+        self.saving_mmtm_scales = saving_mmtm_scales
+        self.saving_mmtm_squeeze_array = saving_mmtm_squeeze_array
+        self.net_view_0 = resnet18(pretrained=pretraining)
+        self.net_view_0.fc = nn.Linear(512, nclasses)
+        self.net_view_1 = resnet18(pretrained=pretraining)
+        self.net_view_1.fc = nn.Linear(512, nclasses)
+        mdev = device if torch.cuda.is_available() else "cpu"
+        self.mmtm2 = MMTM(128, 128, 4, device=mdev)
+        self.mmtm3 = MMTM(256, 256, 4, device=mdev)
+        self.mmtm4 = MMTM(512, 512, 4, device=mdev)
+
+    @staticmethod
+    def _stem(net, x):
+        return net.layer1(net.maxpool(net.relu(net.bn1(net.conv1(x)))))
+
+    def forward(self, x, curation_mode=False, caring_modality=None):
+        f0 = self._stem(self.net_view_0, x[:, 0])
+        f1 = self._stem(self.net_view_1, x[:, 1])
+        scales, squeezed = [], []
+        for i in (2, 3, 4):
+            f0 = getattr(self.net_view_0, f"layer{i}")(f0)
+            f1 = getattr(self.net_view_1, f"layer{i}")(f1)
+            f0, f1, sc, sq = getattr(self, f"mmtm{i}")(
+                f0, f1, self.saving_mmtm_scales, self.saving_mmtm_squeeze_array,
+                turnoff_cross_modal_flow=bool(self.mmtm_off),
+                average_squeezemaps=self.mmtm_rescale[i - 1] if self.mmtm_off else None,
+                curation_mode=curation_mode, caring_modality=caring_modality)
+            scales.append(sc)
+            squeezed.append(sq)
+        x0 = self.net_view_0.fc(torch.flatten(self.net_view_0.avgpool(f0), 1))
+        x1 = self.net_view_1.fc(torch.flatten(self.net_view_1.avgpool(f1), 1))
+        return (x0 + x1) / 2, [x0, x1], scales, squeezed

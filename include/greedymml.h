@@ -1,0 +1,164 @@
+/*
+ * greedymml.h - C ABI of libgreedymml_hip.so, the MI355X (gfx950) kernels of the
+ * balanced multi-modal training step (MVCNN + MMTM fusion + conditional-learning-
+ * speed gating) of SebastianHafner/greedy_multimodal_learning.
+ *
+ * Conventions (every entry point):
+ *   - all pointers are caller-owned DEVICE pointers (the library never allocates,
+ *     frees or synchronises); descriptor structs themselves live in host memory;
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream);
+ *   - returns 0 on success, a negative GM_E* code on bad arguments, or a positive
+ *     hipError_t from the launch; gm_last_error() gives a thread-local message;
+ *   - no C++ exceptions cross the ABI; the entry points are reentrant (no mutable
+ *     globals besides the thread-local error text), so they may be called from the
+ *     autograd engine's worker thread and captured into hipGraphs.
+ *
+ * The reference is pure Python/PyTorch; each entry point below replaces the
+ * implicit PyTorch kernels of one reference call site (cited as file:line of the
+ * reference repository).
+ */
+#ifndef GREEDYMML_H
+#define GREEDYMML_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GM_ABI_VERSION 1
+
+/* activation element types */
+#define GM_F32  0
+#define GM_BF16 1
+/* activation layouts: NCHW = [B][C][H*W], NHWC = [B][H*W][C] (channels_last) */
+#define GM_NCHW 0
+#define GM_NHWC 1
+/* error codes */
+#define GM_OK          0
+#define GM_E_ARG      -1
+#define GM_E_SCRATCH  -2
+#define GM_E_UNSUP    -3
+
+int gm_abi_version(void);
+const char* gm_last_error(void);
+
+/* ---------------------------------------------------------------------------
+ * Spatial reduction per (batch, channel): the MMTM squeeze and its backward.
+ *   squeeze  (dy == NULL): out[b*ld_out + c] = scale * sum_hw x[b,c,hw]
+ *            replaces `torch.mean(tview, dim=-1)` (src/balanced_mmtm.py:62,67,75,84,96-97)
+ *   backward (dy != NULL): g = scale * sum_hw dy[b,c,hw] * x[b,c,hw]
+ *            out = e ? g*e*(1-e) : g     (sigmoid derivative fused; e[b*ld_e+c])
+ *            replaces autograd of `visual * vis_out` + `self.sigmoid` (:110-111,154)
+ * Up to 4 problems (e.g. both modalities) per launch; all share B, dtype, layout.
+ * scratch: NHWC uses fp32 partials, at least gm_spatial_reduce_scratch() bytes.
+ * ------------------------------------------------------------------------- */
+typedef struct gm_spatial_reduce {
+    const void* x;
+    const void* dy;
+    int C, HW;
+    float* out;
+    int ld_out;
+    const float* e;
+    int ld_e;
+    float scale;
+} gm_spatial_reduce;
+
+size_t gm_spatial_reduce_scratch(const gm_spatial_reduce* p, int nprob, int B, int dtype, int layout);
+int gm_mmtm_spatial_reduce(const gm_spatial_reduce* p, int nprob, int B, int dtype, int layout,
+                           void* scratch, size_t scratch_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Channel re-scale: y[b,c,hw] = x[b,c,hw] * s[b*ld_s + c] (+ alpha * a[b*ld_a + c])
+ *   forward  (a == NULL): `visual * vis_out` (src/balanced_mmtm.py:154), ld_s = 0
+ *            broadcasts one row (curation: the running average, :141-152);
+ *   backward (a = dsq):   dX = dY*e + dsq/HW (autograd of :154 and of the mean :96-97).
+ * Up to 4 problems per launch.
+ * ------------------------------------------------------------------------- */
+typedef struct gm_channel_scale {
+    const void* x;
+    void* y;
+    int C, HW;
+    const float* s;
+    int ld_s;
+    const float* a;
+    int ld_a;
+    float alpha;
+} gm_channel_scale;
+
+int gm_mmtm_channel_scale(const gm_channel_scale* p, int nprob, int B, int dtype, int layout,
+                          void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Small fp32 GEMM on MFMA (v_mfma_f32_16x16x4_f32, exact f32 fma chains):
+ *   C[m,n] (+)= act( sum_seg sum_k A_seg[m,k] * B_seg[k,n] + bias[n] ) * mask
+ * Element (i,j) of an operand X is X.ptr[i*ld0 + j*ld1]; ld0 = 0 broadcasts a row.
+ * A.ptr == NULL means A == 1 (column sums: bias gradients).
+ * act: 0 none, 1 relu, 2 sigmoid.  mask: if non-NULL, multiply by (mask[m,n] > 0)
+ * (relu backward).  Up to 2 K-segments (concatenated-input FCs), up to 6 problems
+ * per launch.  Replaces the MMTM nn.Linear layers and their autograd
+ * (src/balanced_mmtm.py:38,44-45,100,107-108; SE-only / shared / turn-off :60-91).
+ * ------------------------------------------------------------------------- */
+typedef struct gm_operand {
+    const float* ptr;
+    int ld0, ld1;
+} gm_operand;
+
+typedef struct gm_gemm {
+    int M, N;
+    int K[2];
+    gm_operand A[2];
+    gm_operand B[2];
+    const float* bias;
+    const float* mask;
+    int ld_mask;
+    float* C;
+    int ld_c;
+    int act;
+    int accumulate;
+} gm_gemm;
+
+int gm_gemm_f32(const gm_gemm* p, int nprob, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * MMTM running averages (src/balanced_mmtm.py:113-116), reference quirk kept:
+ * BOTH averages are updated with the VISUAL scale's batch mean:
+ *   m = mean_b e_v[b,:];  ra_X_new = (m + ra_X_old*step) / (step+1)
+ * ------------------------------------------------------------------------- */
+int gm_mmtm_running_avg(const float* e_v, int ld_e, int B, int C,
+                        const float* ra_v_old, const float* ra_s_old,
+                        float* ra_v_new, float* ra_s_new, int step, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Per-branch weight / gradient norms for the conditional-learning-speed gate
+ * (Bias_Mitigation_Strong.compute_BDR, src/callbacks.py:199-233), optionally fused
+ * with the SGD update of the same parameters (torch.optim.SGD momentum=0, wd=0;
+ * train.py:48-51, src/framework.py:315):
+ *   out[2*g]   = sum over tensors with bit g in group_mask of sum(param^2)
+ *   out[2*g+1] = same for sum((grad*grad_scale)^2)
+ *   if lr != 0: param -= lr * grad * grad_scale   (after reading param)
+ * `table` is a DEVICE array of ntensors gm_tensor entries (built once by the
+ * caller); `offset` = prefix sum of n (elements before this tensor).  grad may be
+ * NULL (a parameter without gradient: contributes 0 and is not updated).
+ * out: DEVICE double[2*ngroups]; scratch >= gm_group_sumsq_scratch(total) bytes.
+ * Deterministic (fixed reduction order).
+ * ------------------------------------------------------------------------- */
+typedef struct gm_tensor {
+    float* param;
+    const float* grad;
+    long long n;
+    long long offset;
+    unsigned int group_mask;
+    unsigned int pad;
+} gm_tensor;
+
+size_t gm_group_sumsq_scratch(long long total_elems);
+int gm_group_sumsq(const gm_tensor* table, int ntensors, long long total_elems, int ngroups,
+                   float grad_scale, float lr, double* out, void* scratch, size_t scratch_bytes,
+                   void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GREEDYMML_H */

@@ -1,0 +1,183 @@
+"""CPU-only checks: the C-ABI library loads and exports every declared symbol,
+and the host-side logic (gin subset, gating state machine, grouping, CUR
+averaging) matches the oracle.  No kernel is launched here."""
+import ctypes
+import os
+import pickle
+import random
+import re
+
+import numpy as np
+import pytest
+import torch
+
+import spec
+from oracle import cur_ref, gating_ref
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_symbols():
+    src = open(os.path.join(ROOT, "include", "greedymml.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(gm_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_builds_and_exports_every_declared_symbol():
+    from greedy_multimodal_learning_amd import build, _lib
+    build.build()
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    syms = _declared_symbols()
+    assert len(syms) >= 9
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(_lib.EXPORTS) == set(syms)
+    L = _lib.load()
+    assert L.gm_abi_version() == _lib.ABI_VERSION
+
+
+def test_abi_argument_errors_without_gpu():
+    """Argument validation runs before any launch, so it is testable on the CPU."""
+    from greedy_multimodal_learning_amd import _lib as L
+    lib = L.load()
+    rc = lib.gm_gemm_f32(None, 0, None)
+    assert rc == -1 and b"nprob" in lib.gm_last_error()
+    rc = lib.gm_group_sumsq(None, 0, 0, 4, 1.0, 0.0, None, None, 0, None)
+    assert rc == -1 and b"empty" in lib.gm_last_error()
+    rc = lib.gm_mmtm_spatial_reduce(None, 1, 1, 0, 0, None, 0, None)
+    assert rc == -1
+
+
+def test_struct_layouts_match_header():
+    from greedy_multimodal_learning_amd import _lib as L
+    assert ctypes.sizeof(L.Tensor) == 40
+    assert ctypes.sizeof(L.Operand) == 16
+    assert ctypes.sizeof(L.SpatialReduce) == 56
+    assert ctypes.sizeof(L.ChannelScale) == 56
+
+
+def test_product_ops_refuse_cpu_tensors():
+    from greedy_multimodal_learning_amd import ops
+    from greedy_multimodal_learning_amd._lib import GreedyMMLError
+    with pytest.raises(GreedyMMLError):
+        ops.linear(torch.randn(2, 3), torch.randn(4, 3))
+
+
+@pytest.mark.parametrize("cfg", ["training_guided", "training_random", "training", "recording", "eval"])
+def test_gin_lite_parses_reference_configs(cfg):
+    from greedy_multimodal_learning_amd import gin_lite as g
+    path = os.path.join(os.environ.get("GREEDYMML_REF", "/root/reference"), "configs", cfg + ".gin")
+    if not os.path.exists(path):
+        pytest.skip("reference configs not mounted")
+    g.clear_config()
+    g.parse_config_files_and_bindings([path], "train.lr=0.05#MMTM_MVCNN.num_views=2")
+    assert g.query("MMTM_MVCNN", "pretraining") is False
+    assert g.query("get_mvdcndata", "specific_views") == [0, 6]
+    if cfg in ("training_guided", "training"):
+        assert g.query("Bias_Mitigation_Strong", "epsilon") == 0.01
+        assert g.query("Bias_Mitigation_Strong", "branchnames") == ["net_view_0", "net_view_1"]
+        assert g.query("train", "lr") == 0.05
+    g.clear_config()
+
+
+def test_gin_lite_fills_configurable_defaults():
+    from greedy_multimodal_learning_amd import gin_lite as g
+    from greedy_multimodal_learning_amd.callbacks import Bias_Mitigation_Strong
+    g.clear_config()
+    g.parse_config("Bias_Mitigation_Strong.epsilon=0.02\nBias_Mitigation_Strong.curation_windowsize=3\n"
+                   "Bias_Mitigation_Strong.branchnames=['net_view_0', 'net_view_1']\n")
+    cb = Bias_Mitigation_Strong()
+    assert (cb.epsilon, cb.curation_windowsize, cb.starting_epoch) == (0.02, 3, 2)
+    cb = Bias_Mitigation_Strong(epsilon=0.5)
+    assert cb.epsilon == 0.5
+    g.clear_config()
+
+
+def test_group_masks_follow_reference_substring_rules():
+    from greedy_multimodal_learning_amd.callbacks import group_masks
+    from greedy_multimodal_learning_amd.model import MMTM_MVCNN
+    m = MMTM_MVCNN()
+    names = [n for n, _ in m.named_parameters()]
+    assert len(names) == 142
+    assert sum(p.numel() for p in m.parameters()) == 23773008
+    masks = group_masks(names, ["net_view_0", "net_view_1"], ["visual", "skeleton"])
+    for n, mk in zip(names, masks):
+        main, by = gating_ref.param_group(n)
+        want = sum(1 << i for i, f in enumerate(main) if f) + sum(1 << (2 + j) for j, f in enumerate(by) if f)
+        assert mk == want, n
+    assert sum(1 for mk in masks if mk == 1) == 62 and sum(1 for mk in masks if mk == 2) == 62
+    assert sum(1 for mk in masks if mk & 12) == 18
+
+
+class _MP:
+    curation_mode = False
+    caring_modality = None
+
+
+def test_gating_state_machine_matches_oracle():
+    """Drive product and oracle state machines with identical random group sums."""
+    from greedy_multimodal_learning_amd.callbacks import Bias_Mitigation_Strong
+    rng = np.random.default_rng(0)
+    cb = Bias_Mitigation_Strong(epsilon=0.01, curation_windowsize=3,
+                                branchnames=["net_view_0", "net_view_1"], starting_epoch=2)
+    mp = _MP()
+    cb.set_model_pytoune(mp)
+    cb.on_train_begin({})
+    ref = gating_ref.BDRState(0.01, 3, starting_epoch=2)
+    for epoch in range(1, 5):
+        cb.on_epoch_begin(epoch, {})
+        ref.on_epoch_begin(epoch)
+        for step in range(10):
+            s = np.exp(rng.normal(size=8))
+            cb.group_sums = lambda s=s: torch.from_numpy(s.copy())
+            d = dict(wn_main=[s[0], s[2]], gn_main=[s[1], s[3]], wn_bypass=[s[4], s[6]],
+                     gn_bypass=[s[5], s[7]])
+            cb.on_backward_end(step)
+            ref.on_backward_end(lambda d=d: d)
+            assert (mp.curation_mode, mp.caring_modality) == (ref.curation_mode, ref.caring_modality)
+            assert cb.d_BDR == pytest.approx(ref.d_BDR, abs=1e-12)
+            logs = {}
+            cb.on_batch_end(step, logs)
+            assert logs["d_BDR"] == cb.d_BDR
+
+
+def test_random_gate_matches_oracle():
+    from greedy_multimodal_learning_amd.callbacks import Bias_Mitigation_Random
+    cb = Bias_Mitigation_Random()
+    mp = _MP()
+    cb.set_model_pytoune(mp)
+    cb.on_train_begin({})
+    ref = gating_ref.RandomGate(rng=random.Random(5))
+    random.seed(5)
+    for epoch in range(1, 4):
+        cb.on_epoch_begin(epoch, {})
+        ref.on_epoch_begin(epoch)
+        for _ in range(20):
+            cb.on_backward_end(0)
+            ref.on_backward_end()
+            assert (mp.curation_mode, mp.caring_modality) == (ref.curation_mode, ref.caring_modality)
+
+
+def test_cur_rescale_weights_match_oracle(tmp_path):
+    from greedy_multimodal_learning_amd.cur import rescale_weights
+    ev, tr = spec.cur_histories()
+    for sub, h in (("eval", ev), ("train", tr)):
+        os.makedirs(tmp_path / sub)
+        with open(tmp_path / sub / "history.pickle", "wb") as f:
+            pickle.dump(h, f)
+    a = rescale_weights(str(tmp_path / "eval"), str(tmp_path / "train"))
+    b = cur_ref.rescale_weights(str(tmp_path / "eval"), str(tmp_path / "train"))
+    assert a[0] is None and b[0] is None
+    for i in range(1, 4):
+        for j in range(2):
+            np.testing.assert_array_equal(a[i][j], b[i][j])
+
+
+def test_losses_match_oracle():
+    from greedy_multimodal_learning_amd.losses import acc, blend_loss
+    g = torch.Generator().manual_seed(0)
+    outs = [torch.randn(6, 40, generator=g) for _ in range(2)]
+    y = torch.randint(0, 40, (6,), generator=g)
+    assert float(blend_loss(outs, y)) == pytest.approx(float(gating_ref.blend_loss(outs, y)), rel=1e-6)
+    assert float(acc(outs, y)) == float(gating_ref.acc(outs, y))
+    assert float(acc(outs[0], y[:2])) == float(gating_ref.acc(outs[0], y[:2]))
