@@ -1,0 +1,169 @@
+#!/usr/bin/env python3
+"""Benchmark of the balanced multi-modal training step on MI355X.
+
+Metric (BASELINE.json): multi-view images/sec + step ms, ModelNet40 2-view
+MVCNN+MMTM.  One step = forward + blend_loss + backward (+ RCCL gradient
+all-reduce when N > 1) + conditional-learning-speed gate (per-branch norm pass
+fused with the SGD update, one host sync for the decision) on one synthetic
+ModelNet40-shaped batch [B, 2, 3, 224, 224] resident in HBM.  Workload: config
+C2 (B = 64 per GPU, bf16 trunk, training_guided gating: eps 0.01, window 5,
+gate unlocked).  N > 1: weak scaling, 64 per GPU (config C3 = 512 at 8 GPUs).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+       torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+N_PARAMS = 23_773_008
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=64, help="per-GPU batch (multi-view objects)")
+    ap.add_argument("--size", type=int, default=224)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_group_sumsq.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(seconds, size):
+    """Oracle (port) of the reference step on the host cores, config C1 shape (B=4)."""
+    from oracle import model_ref, step_ref, gating_ref, weights
+    torch.manual_seed(0)
+    m = weights.apply_to_module(model_ref.MMTM_MVCNN_Ref(), seed=0)
+    gate = gating_ref.BDRState(0.01, 5, starting_epoch=1)
+    gate.on_epoch_begin(1)
+    step = step_ref.RefStep(m, lr=0.1, gate=gate)
+    B = 4
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(B, 2, 3, size, size, generator=g)
+    y = torch.randint(0, 40, (B,), generator=g)
+    step(x, y)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        step(x, y)
+        n += 1
+        dt = time.perf_counter() - t0
+        if dt >= seconds or n >= 200:
+            break
+    return {"value": round(n * B * 2 / dt, 3), "unit": "view-images/s", "cores": torch.get_num_threads(),
+            "kind": "port", "ms_per_step": round(1e3 * dt / n, 2),
+            "sample": f"{n} oracle steps (fp32 torch-CPU restatement of forward+blend_loss+backward+"
+                      f"compute_BDR+SGD), B=4 two-view {size}x{size} (config C1 shape), "
+                      f"{torch.get_num_threads()} threads, {os.cpu_count()} visible CPUs"}
+
+
+def main():
+    a = parse()
+    dist_on = "RANK" in os.environ and int(os.environ.get("WORLD_SIZE", "1")) > 1
+    if dist_on:
+        dist.init_process_group("nccl")
+        rank, world = dist.get_rank(), dist.get_world_size()
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+    else:
+        rank, world, local = 0, 1, 0
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    from greedy_multimodal_learning_amd import build
+    build.build()  # no-op when up to date
+    from greedy_multimodal_learning_amd.model import MMTM_MVCNN
+    from greedy_multimodal_learning_amd.callbacks import Bias_Mitigation_Strong
+    from greedy_multimodal_learning_amd.engine import BalancedStep
+
+    torch.manual_seed(0)
+    model = MMTM_MVCNN().to(dev)
+    gate = Bias_Mitigation_Strong(epsilon=0.01, curation_windowsize=5,
+                                  branchnames=["net_view_0", "net_view_1"], starting_epoch=1)
+    cdt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+    step = BalancedStep(model, lr=0.1, gate=gate, compute_dtype=cdt, channels_last=(a.dtype == "bf16"),
+                        process_group=dist.group.WORLD if dist_on else None)
+    step.on_epoch_begin(1)
+    B = a.batch
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    xdt = cdt
+    xs = [torch.randn(B, 2, 3, a.size, a.size, device=dev, generator=g).to(xdt) for _ in range(2)]
+    ys = [torch.randint(0, 40, (B,), device=dev, generator=g) for _ in range(2)]
+
+    for i in range(a.warmup):
+        step(xs[i % 2], ys[i % 2])
+    torch.cuda.synchronize()
+    step.timer = []
+    curation_steps = 0
+    if dist_on:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        curation_steps += int(step.flags.curation_mode)
+        step(xs[i % 2], ys[i % 2])
+    torch.cuda.synchronize()
+    if dist_on:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if dist_on:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    ms = 1e3 * elapsed / a.steps
+    kern_ms = [e0.elapsed_time(e1) for e0, e1 in step.timer]
+    kern_avg_s = sum(kern_ms) / len(kern_ms) / 1e3
+    step.timer = None
+    loss = float(step.last_loss)
+
+    if rank == 0:
+        views = 2
+        total_imgs = world * B * views * a.steps
+        bytes_alg = 12 * N_PARAMS  # read param + grad, write param (fp32)
+        achieved = bytes_alg / kern_avg_s / 1e9
+        traffic = None
+        if os.path.exists(a.traffic_file):
+            with open(a.traffic_file) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
+        line = {
+            "metric": "multi-view images/sec + step ms, ModelNet40 2-view MVCNN+MMTM @1/2/4/8 GPU",
+            "value": round(total_imgs / elapsed, 2),
+            "unit": "view-images/s",
+            "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": a.dtype,
+            "data": "synthetic N(0,1) [B,2,3,224,224] + uniform labels, resident in HBM; random-init weights",
+            "config": {"workload": "C2: 2-view MVCNN(ResNet-18 x2)+MMTM x3, guided gating "
+                                   "(training_guided.gin eps 0.01, window 5, unlocked)",
+                       "global_batch": B * world, "per_gpu_batch": B, "image": a.size,
+                       "parallelism": f"dp{world}", "samples_per_s": round(world * B * a.steps / elapsed, 2),
+                       "curation_steps_timed": curation_steps, "final_loss": round(loss, 4)},
+            "roofline": {"kernel": "k_group_sumsq<SGD> (fused per-branch norms + SGD, gm_group_sumsq)",
+                         "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "alg_bytes_per_launch": bytes_alg,
+                         "avg_launch_us": round(kern_avg_s * 1e6, 2)},
+        }
+        if not a.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(a.cpu_seconds, a.size)
+        print(json.dumps(line), flush=True)
+    if dist_on:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

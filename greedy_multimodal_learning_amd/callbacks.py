@@ -103,6 +103,10 @@ def group_masks(names, branchnames, MMTMnames):
     return out
 
 
+def _dense(t):
+    return t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last))
+
+
 class GroupNorms:
     """Device-side per-group sum(w^2), sum(g^2) over a fixed parameter list.
 
@@ -127,10 +131,11 @@ class GroupNorms:
         if key == self._key:
             return
         for p in self.params:
-            if p.dtype != torch.float32 or not p.is_contiguous():
-                raise L.GreedyMMLError("group norms need contiguous fp32 parameters")
-            if p.grad is not None and (p.grad.dtype != torch.float32 or not p.grad.is_contiguous()):
-                raise L.GreedyMMLError("group norms need contiguous fp32 gradients")
+            if p.dtype != torch.float32 or not _dense(p):
+                raise L.GreedyMMLError("group norms need dense fp32 parameters")
+            if p.grad is not None and (p.grad.dtype != torch.float32 or not _dense(p.grad)
+                                       or p.grad.stride() != p.stride()):
+                raise L.GreedyMMLError("group norms need dense fp32 gradients laid out like the parameter")
         n = len(self.params)
         tab = (L.Tensor * n)()
         off = 0

@@ -1,0 +1,180 @@
+"""Fused balanced training step for MI355X (single GPU or data parallel).
+
+Same sequence and semantics as one iteration of the reference's
+`Model_.train_loop` (src/framework.py:307-322) with the guided gate:
+
+    zero_grad -> forward(curation flags) -> blend_loss -> backward
+    -> [DP: gradient all-reduce] -> on_backward_end (gating) -> SGD.step
+
+re-organised for the hardware:
+
+* all parameters live in ONE flat fp32 buffer and all gradients in another
+  (parameters are views), laid out in reverse registration order so that
+  gradients become ready front-to-back during backward;
+* gradient all-reduce (RCCL over xGMI) runs per ~`bucket_mb` bucket from
+  post-accumulate-grad hooks, overlapping the rest of backward;
+* the per-branch norm pass of the gate and the SGD update are ONE HIP pass
+  (`gm_group_sumsq` with lr != 0): it reads every parameter before updating
+  it, so the sums equal those `compute_BDR` takes before `optimizer.step()`;
+  the only host sync per step is the 8-double copy the gate needs for its
+  decision (the decision applies to the NEXT forward, as in the reference);
+* the trunk runs in bf16 (autocast) on channels_last activations; master
+  weights, gradients, the MMTM FC chain and all reductions stay fp32.
+"""
+import torch
+import torch.distributed as dist
+
+from .callbacks import GroupNorms
+from .losses import blend_loss
+
+
+class _Flags:
+    """Holds the curation flags like the reference's Model_ (src/framework.py:137-138)."""
+
+    def __init__(self):
+        self.curation_mode = False
+        self.caring_modality = None
+
+
+class BalancedStep:
+    def __init__(self, model, lr=0.1, gate=None, compute_dtype=torch.bfloat16, channels_last=True,
+                 process_group=None, bucket_mb=25.0, branchnames=("net_view_0", "net_view_1"),
+                 MMTMnames=("visual", "skeleton")):
+        self.model = model
+        self.lr = float(lr)
+        self.gate = gate
+        self.compute_dtype = compute_dtype
+        self.channels_last = channels_last
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if process_group is not None else 1
+        self.flags = _Flags()
+        self.device = next(model.parameters()).device
+        if channels_last:
+            model.to(memory_format=torch.channels_last)
+        named = list(model.named_parameters())
+        self._flatten(named)
+        self.norms = GroupNorms(named, list(branchnames), list(MMTMnames))
+        if gate is not None:
+            gate.set_model(model, ignore=False)
+            gate.set_model_pytoune(self.flags)
+            gate.on_train_begin({})
+        if self.world > 1:
+            for m in model.modules():
+                if hasattr(m, "zero_grads_for_curated"):
+                    m.zero_grads_for_curated = True  # every bucket fills every step
+            self._setup_buckets(bucket_mb)
+        self.last_loss = None
+        self.step_count = 0
+        self.timer = None  # optional (start_event, end_event) list collector for the fused pass
+
+    # ---------------- flat storage ----------------
+    def _flatten(self, named):
+        params = [p for _, p in named][::-1]  # reverse: backward order
+        total = sum(p.numel() for p in params)
+        self.flat_param = torch.empty(total, device=self.device, dtype=torch.float32)
+        self.flat_grad = torch.zeros(total, device=self.device, dtype=torch.float32)
+        self.slices = {}
+        off = 0
+        for p in params:
+            n = p.numel()
+            view = self.flat_param[off:off + n]
+            if p.dim() == 4 and self.channels_last:
+                O, I, kh, kw = p.shape
+                nhwc = view.view(O, kh, kw, I)
+                nhwc.copy_(p.data.permute(0, 2, 3, 1))
+                p.data = nhwc.permute(0, 3, 1, 2)
+                p.grad = self.flat_grad[off:off + n].view(O, kh, kw, I).permute(0, 3, 1, 2)
+            else:
+                view.copy_(p.data.reshape(-1))
+                p.data = view.view(p.shape)
+                p.grad = self.flat_grad[off:off + n].view(p.shape)
+            self.slices[p] = (off, n)
+            off += n
+        self.total = total
+
+    # ---------------- data-parallel buckets ----------------
+    def _setup_buckets(self, bucket_mb):
+        cap = int(bucket_mb * 1024 * 1024 / 4)
+        order = sorted(self.slices.items(), key=lambda kv: kv[1][0])
+        self.buckets = []
+        cur, start, end = [], 0, 0
+        for p, (off, n) in order:
+            if cur and (off + n - start) > cap:
+                self.buckets.append((start, end, cur))
+                cur, start = [], off
+            if not cur:
+                start = off
+            cur.append(p)
+            end = off + n
+        if cur:
+            self.buckets.append((start, end, cur))
+        self.bucket_of = {}
+        for bi, (_, _, ps) in enumerate(self.buckets):
+            for p in ps:
+                self.bucket_of[p] = bi
+                p.register_post_accumulate_grad_hook(self._on_grad)
+        self._pending = [0] * len(self.buckets)
+        self._works = []
+
+    def _on_grad(self, p):
+        bi = self.bucket_of[p]
+        self._pending[bi] -= 1
+        if self._pending[bi] == 0:
+            self._launch(bi)
+
+    def _launch(self, bi):
+        s, e, _ = self.buckets[bi]
+        self._works.append(dist.all_reduce(self.flat_grad[s:e], group=self.pg, async_op=True))
+        self._pending[bi] = -1
+
+    def _reset_buckets(self):
+        self._pending = [len(ps) for (_, _, ps) in self.buckets]
+        self._works = []
+
+    def _finish_buckets(self):
+        for bi, c in enumerate(self._pending):
+            if c != -1:
+                self._launch(bi)  # a parameter without gradient this step: reduce anyway
+        for w in self._works:
+            w.wait()
+
+    # ---------------- the step ----------------
+    def forward(self, x):
+        fl = self.flags
+        with torch.autocast("cuda", dtype=self.compute_dtype, enabled=self.compute_dtype != torch.float32):
+            return self.model(x, curation_mode=fl.curation_mode, caring_modality=fl.caring_modality)
+
+    def __call__(self, x, y):
+        """One balanced step on batch (x [B,V,3,H,W], y [B]); returns the loss tensor."""
+        self.model.train(True)
+        self.flat_grad.zero_()
+        if self.world > 1:
+            self._reset_buckets()
+        _, outs, _, _ = self.forward(x)
+        loss = blend_loss([o.float() for o in outs], y)
+        loss.backward()
+        if self.world > 1:
+            self._finish_buckets()
+        gate = self.gate
+        want = gate is not None and hasattr(gate, "needs_bdr") and gate.needs_bdr()
+        t = self.timer
+        if t is not None:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
+        sums = self.norms.sums(grad_scale=1.0 / self.world, lr=self.lr)
+        if t is not None:
+            ev1.record()
+            t.append((ev0, ev1))
+        if gate is not None:
+            if want:
+                gate.pending_sums = sums
+            gate.on_backward_end(self.step_count)
+            gate.pending_sums = None
+        self.last_loss = loss
+        self.step_count += 1
+        return loss
+
+    def on_epoch_begin(self, epoch):
+        if self.gate is not None:
+            self.gate.on_epoch_begin(epoch, {})

@@ -180,15 +180,16 @@ def spec_blend_loss(outs, y):
     return T.blend_loss(outs, y)
 
 
-def trace_case(R):
+def trace_case(R, case=None, ev=None, tag="trace"):
     """F3: the reference's own Model_.train_loop, guided gating, per-step trace."""
     from src import callbacks as C
     from src.framework import Model_
     import train as T
-    case = spec.TRACE
+    case = spec.TRACE if case is None else case
+    ev = spec.TRACE_EVAL if ev is None else ev
     model = R.MMTM_MVCNN()
     weights.apply_to_module(model, seed=spec.SEED_MODEL)
-    train, valid, test = spec.trace_loaders()
+    train, valid, test = spec.trace_loaders(case)
     conv = lambda L: [(np.array(i), tt(x), tt(y)) for (i, x, y) in L]  # noqa: E731
     opt = torch.optim.SGD(model.parameters(), lr=case["lr"], momentum=0, weight_decay=0)
     gate = C.Bias_Mitigation_Strong(epsilon=case["epsilon"], curation_windowsize=case["window"],
@@ -218,7 +219,7 @@ def trace_case(R):
                      validation_steps=len(valid), test_steps=len(test), callbacks=cbs)
     out = {"trace/steps": np.array(rec, dtype=np.float64)}
     model.eval()
-    xe, _ = spec.model_inputs(spec.TRACE_EVAL)
+    xe, _ = spec.model_inputs(ev)
     with torch.no_grad():
         lm, lo, _, _ = model(tt(xe))
     out["trace/eval_logits"] = lm.numpy()
@@ -228,7 +229,7 @@ def trace_case(R):
     out["trace/mmtm4_ra_s"] = model.mmtm4.running_avg_weight_skeleton.numpy()
     for n in spec.TRACE_PARAMS:
         out["trace/param." + n] = dict(model.named_parameters())[n].detach().numpy()
-    return out
+    return {k.replace("trace/", tag + "/"): v for k, v in out.items()}
 
 
 def ddp_case(R):
@@ -293,7 +294,7 @@ def main():
     import src.model as RM
     import src.balanced_mmtm as BM
     R = types.SimpleNamespace(MMTM_MVCNN=RM.MMTM_MVCNN, MMTM_mitigate=BM.MMTM_mitigate)
-    blobs = {"mmtm": mmtm_cases(R), "model": model_cases(R), "trace": trace_case(R),
+    blobs = {"mmtm": mmtm_cases(R), "model": model_cases(R), "trace": {**trace_case(R), **trace_case(R, spec.TRACE_GPU, spec.TRACE_GPU_EVAL, "trace_gpu")},
              "ddp": ddp_case(R), "cur": cur_case(R)}
     for k, v in blobs.items():
         path = os.path.join(HERE, f"golden_{k}.npz")

@@ -28,17 +28,32 @@ MMTM_CASES = [
 ]
 
 # F2 - whole model, forward + backward
+# `gpu_tol`: cases whose train-mode BatchNorm normalises over <= 49 values per
+# channel (32x32 input -> 1x1 layer4 maps; B=1) amplify fp32 reduction-order
+# differences of ANY device (measured: 1e-3 on grad norms with PyTorch's own
+# GPU convs, identical with and without the HIP MMTM).  They pin the CPU oracle
+# at 1e-4 and the GPU at the relaxed tolerance; the well-conditioned cases pin
+# the GPU at 1e-4.
 MODEL_CASES = [
     dict(id="m64", B=2, H=64, W=64, seed=1),
-    dict(id="m32c0", B=3, H=32, W=32, seed=2, cur=True, caring=0),
-    dict(id="m32c1", B=3, H=32, W=32, seed=3, cur=True, caring=1),
-    dict(id="m224", B=1, H=224, W=224, seed=4),
+    dict(id="m64c0", B=3, H=64, W=64, seed=9, cur=True, caring=0),
+    dict(id="m64c1", B=3, H=64, W=64, seed=10, cur=True, caring=1),
+    dict(id="m224b2", B=2, H=224, W=224, seed=11),
+    dict(id="m32c0", B=3, H=32, W=32, seed=2, cur=True, caring=0, gpu_tol=5e-3),
+    dict(id="m32c1", B=3, H=32, W=32, seed=3, cur=True, caring=1, gpu_tol=5e-3),
+    dict(id="m224", B=1, H=224, W=224, seed=4, gpu_tol=1e-2),
 ]
 
 # F3 - gating trace through the reference's own Model_.train_loop
 TRACE = dict(B=4, H=32, W=32, steps=4, nval=1, ntest=1, epochs=3, lr=0.1,
              epsilon=0.01, window=2, starting_epoch=2, seed=5)
 TRACE_EVAL = dict(B=2, H=32, W=32, seed=6)
+# the same guided run, well conditioned for cross-device comparison (64x64 maps,
+# lr 0.01): the lr-0.1 / 32x32 run above diverges (loss 7 -> 11) and amplifies
+# 1e-6 differences to 1e-2 within two steps on any device.
+TRACE_GPU = dict(B=4, H=64, W=64, steps=4, nval=1, ntest=1, epochs=3, lr=0.01,
+                 epsilon=0.01, window=2, starting_epoch=2, seed=12)
+TRACE_GPU_EVAL = dict(B=2, H=64, W=64, seed=13)
 TRACE_PARAMS = ["mmtm3.fc_visual.bias", "mmtm2.fc_squeeze.bias", "net_view_0.fc.bias",
                 "net_view_1.layer1.0.bn1.weight"]
 
@@ -83,8 +98,8 @@ def model_inputs(c):
     return x, y
 
 
-def trace_loaders():
-    t = TRACE
+def trace_loaders(t=None):
+    t = TRACE if t is None else t
     r = _rng(SEED_MODEL, t["seed"])
     def batches(n, base):
         out = []

@@ -38,6 +38,7 @@ def test_model_vs_reference(golden, dev, case):
     from greedy_multimodal_learning_amd.losses import blend_loss
     fix = golden["model"]
     p = case["id"] + "/"
+    tol = case.get("gpu_tol", 1e-4)
     m = _model(dev)
     m.train(True)
     x, y = spec.model_inputs(case)
@@ -45,27 +46,27 @@ def test_model_vs_reference(golden, dev, case):
                                 caring_modality=case.get("caring", None))
     loss = blend_loss(outs, tt(y).to(dev))
     loss.backward()
-    close(fix, p + "logits", mean.detach().cpu(), rtol=1e-4, atol=1e-4)
-    close(fix, p + "logits0", outs[0].detach().cpu(), rtol=1e-4, atol=1e-4)
-    close(fix, p + "logits1", outs[1].detach().cpu(), rtol=1e-4, atol=1e-4)
-    assert abs(float(loss) - float(fix[p + "loss"])) < 1e-4 * abs(float(fix[p + "loss"]))
+    close(fix, p + "logits", mean.detach().cpu(), rtol=tol, atol=tol)
+    close(fix, p + "logits0", outs[0].detach().cpu(), rtol=tol, atol=tol)
+    close(fix, p + "logits1", outs[1].detach().cpu(), rtol=tol, atol=tol)
+    assert abs(float(loss.detach()) - float(fix[p + "loss"])) < tol * abs(float(fix[p + "loss"]))
     for i in range(3):
-        close(fix, p + f"scale{i}_v", scales[i][0], atol=1e-5)
-        close(fix, p + f"scale{i}_s", scales[i][1], atol=1e-5)
-        close(fix, p + f"sq{i}_v", sqs[i][0], atol=1e-5)
-        close(fix, p + f"sq{i}_s", sqs[i][1], atol=1e-5)
+        close(fix, p + f"scale{i}_v", scales[i][0], rtol=tol, atol=10 * tol)
+        close(fix, p + f"scale{i}_s", scales[i][1], rtol=tol, atol=10 * tol)
+        close(fix, p + f"sq{i}_v", sqs[i][0], rtol=tol, atol=10 * tol)
+        close(fix, p + f"sq{i}_s", sqs[i][1], rtol=tol, atol=10 * tol)
     names = [n for n, _ in m.named_parameters()]
     assert names == list(fix[p + "param_names"])
     gn = np.array([float((q.grad.double() ** 2).sum()) if q.grad is not None else 0.0
                    for _, q in m.named_parameters()])
-    np.testing.assert_allclose(gn, fix[p + "gn"], rtol=2e-3, atol=1e-9)
+    np.testing.assert_allclose(gn, fix[p + "gn"], rtol=max(tol, 1e-4), atol=1e-9)
     for n, q in m.named_parameters():
         key = p + "gsample." + n
         if key in fix.files:
             assert q.grad is not None, n
             idx = spec.sample_idx(n, q.numel())
             np.testing.assert_allclose(q.grad.reshape(-1)[idx].cpu().numpy(), fix[key],
-                                       rtol=2e-3, atol=1e-5, err_msg=n)
+                                       rtol=10 * tol, atol=1e-5, err_msg=n)
         else:
             assert q.grad is None, n  # curated branch: no gradient, like the reference
     if (p + "d_BDR") in fix.files:
@@ -73,7 +74,7 @@ def test_model_vs_reference(golden, dev, case):
                                     branchnames=["net_view_0", "net_view_1"])
         cb.set_model(m, ignore=False)
         cb.M_bypass_modal_0 = cb.M_bypass_modal_1 = cb.M_main_modal_0 = cb.M_main_modal_1 = 0
-        assert abs(cb.compute_BDR() - float(fix[p + "d_BDR"])) < 1e-5
+        assert abs(cb.compute_BDR() - float(fix[p + "d_BDR"])) < 10 * tol
 
 
 class _Engine:
@@ -88,7 +89,7 @@ def test_guided_trace_vs_reference(golden, dev):
     from greedy_multimodal_learning_amd.callbacks import Bias_Mitigation_Strong
     from greedy_multimodal_learning_amd.losses import acc, blend_loss
     fix = golden["trace"]
-    t = spec.TRACE
+    t = spec.TRACE_GPU
     m = _model(dev)
     m.saving_mmtm_scales = m.saving_mmtm_squeeze_array = False
     opt = torch.optim.SGD(m.parameters(), lr=t["lr"], momentum=0, weight_decay=0)
@@ -100,7 +101,7 @@ def test_guided_trace_vs_reference(golden, dev):
     gate.set_optimizer(opt)
     gate.set_model_pytoune(eng)
     gate.on_train_begin({})
-    train, valid, test = spec.trace_loaders()
+    train, valid, test = spec.trace_loaders(t)
     rows = []
     for epoch in range(1, t["epochs"] + 1):
         gate.on_epoch_begin(epoch, {})
@@ -125,21 +126,24 @@ def test_guided_trace_vs_reference(golden, dev):
                 for _, x, _ in L:
                     m(tt(x).to(dev), curation_mode=eng.curation_mode, caring_modality=eng.caring_modality)
     rows = np.array(rows, dtype=np.float64)
-    ref = fix["trace/steps"]
+    ref = fix["trace_gpu/steps"]
     assert rows.shape == ref.shape
-    np.testing.assert_allclose(rows[:, 0], ref[:, 0], rtol=1e-3)
-    np.testing.assert_allclose(rows[:, 1], ref[:, 1], atol=1e-4)
+    np.testing.assert_allclose(rows[:, 0], ref[:, 0], rtol=1e-4)
+    np.testing.assert_allclose(rows[:, 1], ref[:, 1], atol=1e-5)
     # decisions must match except where |d_BDR| sits within tolerance of epsilon
     band = np.abs(np.abs(ref[:, 1]) - t["epsilon"]) < 1e-4
     assert np.all((rows[:, 2:4] == ref[:, 2:4]).all(1) | band)
     m.eval()
-    xe, _ = spec.model_inputs(spec.TRACE_EVAL)
+    xe, _ = spec.model_inputs(spec.TRACE_GPU_EVAL)
     with torch.no_grad():
         lm, lo, _, _ = m(tt(xe).to(dev))
-    close(fix, "trace/eval_logits", lm.cpu(), rtol=1e-3, atol=1e-3)
-    assert int(fix["trace/mmtm2_step"]) == m.mmtm2.step
-    close(fix, "trace/mmtm4_ra_v", m.mmtm4.running_avg_weight_visual.cpu(), atol=1e-4)
-    close(fix, "trace/mmtm4_ra_s", m.mmtm4.running_avg_weight_skeleton.cpu(), atol=1e-4)
+    close(fix, "trace_gpu/eval_logits", lm.cpu(), rtol=1e-4, atol=1e-4)
+    assert int(fix["trace_gpu/mmtm2_step"]) == m.mmtm2.step
+    close(fix, "trace_gpu/mmtm4_ra_v", m.mmtm4.running_avg_weight_visual.cpu(), atol=1e-5)
+    close(fix, "trace_gpu/mmtm4_ra_s", m.mmtm4.running_avg_weight_skeleton.cpu(), atol=1e-5)
+    P = dict(m.named_parameters())
+    for n in spec.TRACE_PARAMS:
+        close(fix, "trace_gpu/param." + n, P[n].detach().cpu(), rtol=1e-4, atol=1e-5)
 
 
 def test_cur_turnoff_vs_reference(golden, dev, tmp_path):

@@ -113,34 +113,36 @@ def test_oracle_model(golden, case):
     close(fix, p + "bn_rv", m.net_view_1.layer4[1].bn2.running_var, atol=1e-5)
 
 
-def test_oracle_trace(golden):
+@pytest.mark.parametrize("tag", ["trace", "trace_gpu"])
+def test_oracle_trace(golden, tag):
     """Whole guided run (3 epochs x 4 steps) through the reference loop order."""
     fix = golden["trace"]
-    t = spec.TRACE
+    t = spec.TRACE if tag == "trace" else spec.TRACE_GPU
+    ev = spec.TRACE_EVAL if tag == "trace" else spec.TRACE_GPU_EVAL
     m = weights.apply_to_module(model_ref.MMTM_MVCNN_Ref(), seed=spec.SEED_MODEL)
     gate = gating_ref.BDRState(t["epsilon"], t["window"], t["starting_epoch"])
     step = step_ref.RefStep(m, lr=t["lr"], gate=gate)
-    train, valid, test = spec.trace_loaders()
+    train, valid, test = spec.trace_loaders(t)
     conv = lambda L: [(i, tt(x), tt(y)) for i, x, y in L]  # noqa: E731
     rows = np.array(loop_ref.run(m, step, gate, conv(train), conv(valid), conv(test), t["epochs"]),
                     dtype=np.float64)
-    ref = fix["trace/steps"]
+    ref = fix[tag + "/steps"]
     assert rows.shape == ref.shape
     np.testing.assert_allclose(rows[:, 0], ref[:, 0], rtol=1e-4)       # loss
     np.testing.assert_allclose(rows[:, 1], ref[:, 1], atol=1e-5)       # d_BDR
     np.testing.assert_array_equal(rows[:, 2:4], ref[:, 2:4])           # decisions
     np.testing.assert_allclose(rows[:, 4:], ref[:, 4:], atol=1e-9)     # accuracies
     m.eval()
-    xe, _ = spec.model_inputs(spec.TRACE_EVAL)
+    xe, _ = spec.model_inputs(ev)
     with torch.no_grad():
         lm, lo, _, _ = m(tt(xe))
-    close(fix, "trace/eval_logits", lm, rtol=1e-3, atol=1e-3)
-    assert int(fix["trace/mmtm2_step"]) == m.mmtm2.step
-    close(fix, "trace/mmtm4_ra_v", m.mmtm4.running_avg_weight_visual, atol=1e-5)
-    close(fix, "trace/mmtm4_ra_s", m.mmtm4.running_avg_weight_skeleton, atol=1e-5)
+    close(fix, tag + "/eval_logits", lm, rtol=1e-3, atol=1e-3)
+    assert int(fix[tag + "/mmtm2_step"]) == m.mmtm2.step
+    close(fix, tag + "/mmtm4_ra_v", m.mmtm4.running_avg_weight_visual, atol=1e-5)
+    close(fix, tag + "/mmtm4_ra_s", m.mmtm4.running_avg_weight_skeleton, atol=1e-5)
     P = dict(m.named_parameters())
     for n in spec.TRACE_PARAMS:
-        close(fix, "trace/param." + n, P[n].detach(), rtol=1e-3, atol=1e-4)
+        close(fix, tag + "/param." + n, P[n].detach(), rtol=1e-3, atol=1e-4)
 
 
 def test_oracle_ddp_mean_of_shards(golden):
