@@ -97,7 +97,14 @@ def main():
     B = a.batch
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
     xdt = cdt
-    xs = [torch.randn(B, 2, 3, a.size, a.size, device=dev, generator=g).to(xdt) for _ in range(2)]
+    # HBM layout of a batch: view-major, channels-last [V][B][H][W][3], exposed to the
+    # model as the reference's [B, V, 3, H, W] (a permuted view); each view's slice is
+    # then a dense channels_last image batch the first convolution reads directly.
+    def batch():
+        buf = torch.randn(2, B, a.size, a.size, 3, device=dev, generator=g).to(xdt)
+        x = buf.permute(1, 0, 4, 2, 3)
+        return x if a.dtype == "bf16" else x.contiguous()
+    xs = [batch() for _ in range(2)]
     ys = [torch.randint(0, 40, (B,), device=dev, generator=g) for _ in range(2)]
 
     for i in range(a.warmup):

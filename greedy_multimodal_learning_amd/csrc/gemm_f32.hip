@@ -28,8 +28,59 @@ struct GemmArgs {
     int nprob;
 };
 
-__device__ __forceinline__ float ld_op(const gm_operand& o, int i, int j) {
-    return o.ptr ? o.ptr[(size_t)i * o.ld0 + (size_t)j * o.ld1] : 1.0f;
+// One K-segment of a wave's 16x16 tile: k in [k0, k1) (segment-local), stepping 4.
+// Lane (li, lk) reads A[m0+li][k+lk] and B[k+lk][n0+li]; pointers advance by
+// 4*ld1 / 4*ld0 per step.  8 steps (32 k) per iteration with the next
+// iteration's 16 loads issued before this iteration's 8 MFMAs (register
+// double-buffer), so L2 latency hides behind MFMA issue.
+__device__ __forceinline__ void seg_mma(floatx4& acc, const gm_operand& A, const gm_operand& B,
+                                        int m, int n, bool mrow, bool ncol, int lk, int k0, int k1) {
+    if (k1 <= k0) return;
+    const bool aone = A.ptr == nullptr;
+    const float* pa = aone ? nullptr : A.ptr + (long)m * A.ld0 + (long)(k0 + lk) * A.ld1;
+    const float* pb = B.ptr + (long)(k0 + lk) * B.ld0 + (long)n * B.ld1;
+    const long sa = 4l * A.ld1, sb = 4l * B.ld0;
+    const bool va = mrow && !aone, vb = ncol;
+    const float one = mrow ? 1.0f : 0.0f;
+    int k = k0;
+    constexpr int U = 8;
+    if (k + 4 * U <= k1) {
+        float ac[U], bc[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            ac[u] = va ? pa[u * sa] : one;
+            bc[u] = vb ? pb[u * sb] : 0.f;
+        }
+        for (; k + 8 * U <= k1; k += 4 * U) {
+            float an[U], bn[U];
+            const float* qa = pa + U * sa;
+            const float* qb = pb + U * sb;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                an[u] = va ? qa[u * sa] : one;
+                bn[u] = vb ? qb[u * sb] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[u], bc[u], acc, 0, 0, 0);
+#pragma unroll
+            for (int u = 0; u < U; ++u) { ac[u] = an[u]; bc[u] = bn[u]; }
+            if (!aone) pa = qa;
+            pb = qb;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[u], bc[u], acc, 0, 0, 0);
+        k += 4 * U;
+        if (!aone) pa += U * sa;
+        pb += U * sb;
+    }
+    for (; k < k1; k += 4) {
+        const bool in = (k + lk) < k1;
+        const float av = (in && va) ? *pa : ((in && aone) ? one : 0.f);
+        const float bv = (in && vb) ? *pb : 0.f;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+        if (!aone) pa += sa;
+        pb += sb;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_gemm_f32(GemmArgs a) {
@@ -47,39 +98,17 @@ __global__ __launch_bounds__(256) void k_gemm_f32(GemmArgs a) {
     const int tm = tile / TN, tn = tile - tm * TN;
     const int m0 = (wm * TM + tm) * 16, n0 = (wn * TN + tn) * 16;
     const int li = lane & 15, lk = lane >> 4;
-    const int Ktot = p.K[0] + p.K[1];
-    // K range of this split, in units of 4
+    const int K0 = p.K[0], Ktot = p.K[0] + p.K[1];
+    // K range of this split (global k, multiple of 4 per split)
     const int k4 = (Ktot + 3) >> 2;
     const int per = (k4 + KS - 1) / KS;
-    const int kb = ks * per * 4, ke = min(Ktot, (ks + 1) * per * 4);
+    const int kb = min(Ktot, ks * per * 4), ke = min(Ktot, (ks + 1) * per * 4);
     const bool mrow = (m0 + li) < p.M, ncol = (n0 + li) < p.N;
+    const int mm = mrow ? m0 + li : 0, nn = ncol ? n0 + li : 0;
     floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-    int k = kb;
-    // unrolled main body: 4 MFMA steps (16 k) with all 8 loads issued first
-    for (; k + 16 <= ke; k += 16) {
-        float av[4], bv[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int kk = k + 4 * u + lk;
-            const int sg = kk >= p.K[0];
-            const int kl = kk - (sg ? p.K[0] : 0);
-            av[u] = mrow ? ld_op(p.A[sg], m0 + li, kl) : 0.f;
-            bv[u] = ncol ? ld_op(p.B[sg], kl, n0 + li) : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
-    }
-    for (; k < ke; k += 4) {
-        const int kk = k + lk;
-        float av = 0.f, bv = 0.f;
-        if (kk < ke) {
-            const int sg = kk >= p.K[0];
-            const int kl = kk - (sg ? p.K[0] : 0);
-            av = mrow ? ld_op(p.A[sg], m0 + li, kl) : 0.f;
-            bv = ncol ? ld_op(p.B[sg], kl, n0 + li) : 0.f;
-        }
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
-    }
+    seg_mma(acc, p.A[0], p.B[0], mm, nn, mrow, ncol, lk, kb, min(ke, K0));
+    if (p.K[1] > 0)
+        seg_mma(acc, p.A[1], p.B[1], mm, nn, mrow, ncol, lk, max(kb, K0) - K0, ke - K0);
     if (KS > 1) {
         red[wave][lane] = acc;
         __syncthreads();

@@ -64,7 +64,27 @@ __global__ __launch_bounds__(256) void k_group_sumsq(const gm_tensor* __restrict
         const long long nv = (te - head) >> 2;
         float4* pv = (float4*)(p + head);
         const float4* gv = (const float4*)(gr ? gr + head : nullptr);
-        for (long long i = threadIdx.x; i < nv; i += 256) {
+        long long i0 = threadIdx.x;
+        if (gr) {
+            // 4 independent 16-B loads of each stream in flight per thread
+            for (; i0 + 3 * 256 < nv; i0 += 4 * 256) {
+                float4 w[4], g[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) { w[u] = pv[i0 + u * 256]; g[u] = gv[i0 + u * 256]; }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    sw = fmaf(w[u].x, w[u].x, sw); sw = fmaf(w[u].y, w[u].y, sw);
+                    sw = fmaf(w[u].z, w[u].z, sw); sw = fmaf(w[u].w, w[u].w, sw);
+                    g[u].x *= gscale; g[u].y *= gscale; g[u].z *= gscale; g[u].w *= gscale;
+                    sg = fmaf(g[u].x, g[u].x, sg); sg = fmaf(g[u].y, g[u].y, sg);
+                    sg = fmaf(g[u].z, g[u].z, sg); sg = fmaf(g[u].w, g[u].w, sg);
+                    if (SGD)
+                        pv[i0 + u * 256] = make_float4(fmaf(-lr, g[u].x, w[u].x), fmaf(-lr, g[u].y, w[u].y),
+                                                       fmaf(-lr, g[u].z, w[u].z), fmaf(-lr, g[u].w, w[u].w));
+                }
+            }
+        }
+        for (long long i = i0; i < nv; i += 256) {
             const float4 w = pv[i];
             sw = fmaf(w.x, w.x, sw); sw = fmaf(w.y, w.y, sw);
             sw = fmaf(w.z, w.z, sw); sw = fmaf(w.w, w.w, sw);
@@ -109,19 +129,29 @@ __global__ __launch_bounds__(256) void k_group_sumsq(const gm_tensor* __restrict
 
 __global__ __launch_bounds__(256) void k_group_finalize(const double* __restrict__ rows, int nrows,
                                                         int ngroups, double* __restrict__ out) {
-    __shared__ double s[256];
+    // each thread accumulates whole rows (all 2*ngroups columns) in registers, then one
+    // wave-shuffle + LDS pass per column; fixed assignment => deterministic
+    __shared__ double s[4][2 * kMaxGroups];
     const int w = 2 * ngroups;
-    for (int j = 0; j < w; ++j) {
-        double acc = 0.0;
-        for (int r = threadIdx.x; r < nrows; r += 256) acc += rows[(size_t)r * w + j];
-        s[threadIdx.x] = acc;
-        __syncthreads();
-        for (int o = 128; o > 0; o >>= 1) {
-            if ((int)threadIdx.x < o) s[threadIdx.x] += s[threadIdx.x + o];
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) out[j] = s[0];
-        __syncthreads();
+    double acc[2 * kMaxGroups];
+#pragma unroll
+    for (int j = 0; j < 2 * kMaxGroups; ++j) acc[j] = 0.0;
+    for (int r = threadIdx.x; r < nrows; r += 256) {
+#pragma unroll
+        for (int j = 0; j < 2 * kMaxGroups; ++j)
+            if (j < w) acc[j] += rows[(size_t)r * w + j];
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int j = 0; j < 2 * kMaxGroups; ++j) {
+        if (j >= w) break;
+        const double v = wave_sum_d(acc[j]);
+        if (lane == 0) s[wave][j] = v;
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < w) {
+        const int j = threadIdx.x;
+        out[j] = ((s[0][j] + s[1][j]) + s[2][j]) + s[3][j];
     }
 }
 

@@ -236,10 +236,31 @@ __global__ __launch_bounds__(256) void k_channel_scale(ScaleArgs a) {
         } else {
             const uint32_t b = p.div_hwc.div(i0);
             const uint32_t c0 = i0 - p.div_c.div(i0) * (uint32_t)p.C;
+            const float* sp = p.s + (size_t)b * p.ld_s + c0;
+            if constexpr (N % 4 == 0) {
 #pragma unroll
-            for (int j = 0; j < N; ++j) {
-                sc[j] = p.s[(size_t)b * p.ld_s + c0 + j];
-                ad[j] = p.a ? p.a[(size_t)b * p.ld_a + c0 + j] * p.alpha : 0.f;
+                for (int j = 0; j < N; j += 4) {
+                    const float4 t = *(const float4*)(sp + j);
+                    sc[j] = t.x; sc[j + 1] = t.y; sc[j + 2] = t.z; sc[j + 3] = t.w;
+                }
+                if (p.a) {
+                    const float* ap = p.a + (size_t)b * p.ld_a + c0;
+#pragma unroll
+                    for (int j = 0; j < N; j += 4) {
+                        const float4 t = *(const float4*)(ap + j);
+                        ad[j] = t.x * p.alpha; ad[j + 1] = t.y * p.alpha;
+                        ad[j + 2] = t.z * p.alpha; ad[j + 3] = t.w * p.alpha;
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < N; ++j) ad[j] = 0.f;
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < N; ++j) {
+                    sc[j] = sp[j];
+                    ad[j] = p.a ? p.a[(size_t)b * p.ld_a + c0 + j] * p.alpha : 0.f;
+                }
             }
         }
         float o[N];
@@ -267,13 +288,23 @@ __global__ __launch_bounds__(256) void k_channel_scale(ScaleArgs a) {
 }
 
 // ---------------- running averages ----------------
+// grid: ceil(C/64) blocks of 256 threads; wave w sums rows b = w, w+4, ... of 64
+// consecutive channels (coalesced), the 4 partials are added in fixed order.
 __global__ __launch_bounds__(256) void k_running_avg(const float* e, int ld, int B, int C,
                                                      const float* rv, const float* rs,
                                                      float* ov, float* os, int step) {
-    const int c = blockIdx.x * 256 + threadIdx.x;
-    if (c >= C) return;
+    __shared__ float part[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + lane;
     float m = 0.f;
-    for (int b = 0; b < B; ++b) m += e[(size_t)b * ld + c];
+    if (c < C) {
+#pragma unroll 4
+        for (int b = w; b < B; b += 4) m += e[(size_t)b * ld + c];
+    }
+    part[w][lane] = m;
+    __syncthreads();
+    if (w != 0 || c >= C) return;
+    m = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
     m = m / (float)B;
     const float k = (float)step, k1 = (float)(step + 1);
     ov[c] = (m + rv[c] * k) / k1;
@@ -420,7 +451,9 @@ extern "C" int gm_mmtm_channel_scale(const gm_channel_scale* in, int nprob, int 
         const size_t numel = (size_t)B * s.C * s.HW;
         GM_REQUIRE(numel < (1ull << 32), "channel_scale[%d]: tensor too large for 32-bit indexing", i);
         if (!aligned(s.x, 16) || !aligned(s.y, 16) || numel % N) N = 1;
-        if (layout == GM_NHWC && s.C % N) N = 1;
+        if (layout == GM_NHWC && (s.C % N || !aligned(s.s, 16) || s.ld_s % 4 ||
+                                  (s.a && (!aligned(s.a, 16) || s.ld_a % 4))))
+            N = 1;
         if (layout == GM_NCHW && s.HW % N) rowconst = false;
     }
     ScaleArgs a;
@@ -473,7 +506,7 @@ extern "C" int gm_mmtm_running_avg(const float* e_v, int ld_e, int B, int C, con
                                    void* stream) {
     GM_REQUIRE(e_v && ra_v_old && ra_s_old && ra_v_new && ra_s_new, "running_avg: null pointer");
     GM_REQUIRE(B >= 1 && C >= 1 && ld_e >= C && step >= 0, "running_avg: bad shape");
-    k_running_avg<<<(C + 255) / 256, 256, 0, as_stream(stream)>>>(e_v, ld_e, B, C, ra_v_old, ra_s_old,
+    k_running_avg<<<(C + 63) / 64, 256, 0, as_stream(stream)>>>(e_v, ld_e, B, C, ra_v_old, ra_s_old,
                                                                   ra_v_new, ra_s_new, step);
     return check_launch("k_running_avg");
 }
