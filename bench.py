@@ -37,6 +37,7 @@ def parse():
     ap.add_argument("--size", type=int, default=224)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--miopen-find", action="store_true", help="torch.backends.cudnn.benchmark=True")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_group_sumsq.json"))
     return ap.parse_args()
@@ -79,6 +80,7 @@ def main():
     else:
         rank, world, local = 0, 1, 0
     torch.cuda.set_device(local)
+    torch.backends.cudnn.benchmark = a.miopen_find
     dev = torch.device("cuda", local)
     from greedy_multimodal_learning_amd import build
     build.build()  # no-op when up to date
