@@ -36,6 +36,97 @@ class _Flags:
         self.caring_modality = None
 
 
+class FlatParams:
+    """All parameters of `model` as views of ONE flat fp32 buffer and their
+    gradients as views of a second one (same offsets), in reverse registration
+    order (~ the order backward produces gradients).  Conv weights keep the
+    model's memory format (KRSC when channels_last)."""
+
+    def __init__(self, model, channels_last=False):
+        self.device = next(model.parameters()).device
+        named = list(model.named_parameters())
+        params = [p for _, p in named][::-1]
+        total = sum(p.numel() for p in params)
+        self.param = torch.empty(total, device=self.device, dtype=torch.float32)
+        self.grad = torch.zeros(total, device=self.device, dtype=torch.float32)
+        self.slices = {}
+        off = 0
+        for p in params:
+            n = p.numel()
+            view = self.param[off:off + n]
+            if p.dim() == 4 and channels_last:
+                O, I, kh, kw = p.shape
+                nhwc = view.view(O, kh, kw, I)
+                nhwc.copy_(p.data.permute(0, 2, 3, 1))
+                p.data = nhwc.permute(0, 3, 1, 2)
+                p.grad = self.grad[off:off + n].view(O, kh, kw, I).permute(0, 3, 1, 2)
+            else:
+                view.copy_(p.data.reshape(-1))
+                p.data = view.view(p.shape)
+                p.grad = self.grad[off:off + n].view(p.shape)
+            self.slices[p] = (off, n)
+            off += n
+        self.total = total
+
+
+class GradBuckets:
+    """Bucketed gradient all-reduce overlapped with backward.
+
+    The flat gradient buffer is cut into contiguous ~bucket_mb slices; a
+    post-accumulate-grad hook counts the parameters of each bucket and launches
+    an async all_reduce(SUM) on the slice the moment its last gradient lands,
+    while autograd keeps producing the next ones.  `finish()` launches any bucket
+    a parameter without gradient left incomplete and waits for all of them.
+    Backend-agnostic: RCCL ("nccl") on the GPU, gloo in the CPU tests."""
+
+    def __init__(self, flat, process_group=None, bucket_mb=25.0):
+        self.flat = flat
+        self.pg = process_group
+        cap = max(1, int(bucket_mb * 1024 * 1024 / 4))
+        order = sorted(flat.slices.items(), key=lambda kv: kv[1][0])
+        self.buckets = []
+        cur, start, end = [], 0, 0
+        for p, (off, n) in order:
+            if cur and (off + n - start) > cap:
+                self.buckets.append((start, end, cur))
+                cur = []
+            if not cur:
+                start = off
+            cur.append(p)
+            end = off + n
+        if cur:
+            self.buckets.append((start, end, cur))
+        self.bucket_of = {}
+        for bi, (_, _, ps) in enumerate(self.buckets):
+            for p in ps:
+                self.bucket_of[p] = bi
+                p.register_post_accumulate_grad_hook(self._on_grad)
+        self.reset()
+
+    def reset(self):
+        self._pending = [len(ps) for (_, _, ps) in self.buckets]
+        self._works = []
+
+    def _on_grad(self, p):
+        bi = self.bucket_of[p]
+        self._pending[bi] -= 1
+        if self._pending[bi] == 0:
+            self._launch(bi)
+
+    def _launch(self, bi):
+        s, e, _ = self.buckets[bi]
+        self._works.append(dist.all_reduce(self.flat.grad[s:e], group=self.pg, async_op=True))
+        self._pending[bi] = -1
+
+    def finish(self):
+        for bi, c in enumerate(self._pending):
+            if c != -1:
+                self._launch(bi)
+        for w in self._works:
+            w.wait()
+        self._works = []
+
+
 class BalancedStep:
     def __init__(self, model, lr=0.1, gate=None, compute_dtype=torch.bfloat16, channels_last=True,
                  process_group=None, bucket_mb=25.0, branchnames=("net_view_0", "net_view_1"),
@@ -52,91 +143,22 @@ class BalancedStep:
         if channels_last:
             model.to(memory_format=torch.channels_last)
         named = list(model.named_parameters())
-        self._flatten(named)
+        self.flat = FlatParams(model, channels_last)
+        self.flat_grad = self.flat.grad
         self.norms = GroupNorms(named, list(branchnames), list(MMTMnames))
         if gate is not None:
             gate.set_model(model, ignore=False)
             gate.set_model_pytoune(self.flags)
             gate.on_train_begin({})
+        self.buckets = None
         if self.world > 1:
             for m in model.modules():
                 if hasattr(m, "zero_grads_for_curated"):
                     m.zero_grads_for_curated = True  # every bucket fills every step
-            self._setup_buckets(bucket_mb)
+            self.buckets = GradBuckets(self.flat, process_group, bucket_mb)
         self.last_loss = None
         self.step_count = 0
         self.timer = None  # optional (start_event, end_event) list collector for the fused pass
-
-    # ---------------- flat storage ----------------
-    def _flatten(self, named):
-        params = [p for _, p in named][::-1]  # reverse: backward order
-        total = sum(p.numel() for p in params)
-        self.flat_param = torch.empty(total, device=self.device, dtype=torch.float32)
-        self.flat_grad = torch.zeros(total, device=self.device, dtype=torch.float32)
-        self.slices = {}
-        off = 0
-        for p in params:
-            n = p.numel()
-            view = self.flat_param[off:off + n]
-            if p.dim() == 4 and self.channels_last:
-                O, I, kh, kw = p.shape
-                nhwc = view.view(O, kh, kw, I)
-                nhwc.copy_(p.data.permute(0, 2, 3, 1))
-                p.data = nhwc.permute(0, 3, 1, 2)
-                p.grad = self.flat_grad[off:off + n].view(O, kh, kw, I).permute(0, 3, 1, 2)
-            else:
-                view.copy_(p.data.reshape(-1))
-                p.data = view.view(p.shape)
-                p.grad = self.flat_grad[off:off + n].view(p.shape)
-            self.slices[p] = (off, n)
-            off += n
-        self.total = total
-
-    # ---------------- data-parallel buckets ----------------
-    def _setup_buckets(self, bucket_mb):
-        cap = int(bucket_mb * 1024 * 1024 / 4)
-        order = sorted(self.slices.items(), key=lambda kv: kv[1][0])
-        self.buckets = []
-        cur, start, end = [], 0, 0
-        for p, (off, n) in order:
-            if cur and (off + n - start) > cap:
-                self.buckets.append((start, end, cur))
-                cur, start = [], off
-            if not cur:
-                start = off
-            cur.append(p)
-            end = off + n
-        if cur:
-            self.buckets.append((start, end, cur))
-        self.bucket_of = {}
-        for bi, (_, _, ps) in enumerate(self.buckets):
-            for p in ps:
-                self.bucket_of[p] = bi
-                p.register_post_accumulate_grad_hook(self._on_grad)
-        self._pending = [0] * len(self.buckets)
-        self._works = []
-
-    def _on_grad(self, p):
-        bi = self.bucket_of[p]
-        self._pending[bi] -= 1
-        if self._pending[bi] == 0:
-            self._launch(bi)
-
-    def _launch(self, bi):
-        s, e, _ = self.buckets[bi]
-        self._works.append(dist.all_reduce(self.flat_grad[s:e], group=self.pg, async_op=True))
-        self._pending[bi] = -1
-
-    def _reset_buckets(self):
-        self._pending = [len(ps) for (_, _, ps) in self.buckets]
-        self._works = []
-
-    def _finish_buckets(self):
-        for bi, c in enumerate(self._pending):
-            if c != -1:
-                self._launch(bi)  # a parameter without gradient this step: reduce anyway
-        for w in self._works:
-            w.wait()
 
     # ---------------- the step ----------------
     def forward(self, x):
@@ -148,13 +170,13 @@ class BalancedStep:
         """One balanced step on batch (x [B,V,3,H,W], y [B]); returns the loss tensor."""
         self.model.train(True)
         self.flat_grad.zero_()
-        if self.world > 1:
-            self._reset_buckets()
+        if self.buckets is not None:
+            self.buckets.reset()
         _, outs, _, _ = self.forward(x)
         loss = blend_loss([o.float() for o in outs], y)
         loss.backward()
-        if self.world > 1:
-            self._finish_buckets()
+        if self.buckets is not None:
+            self.buckets.finish()
         gate = self.gate
         want = gate is not None and hasattr(gate, "needs_bdr") and gate.needs_bdr()
         t = self.timer
