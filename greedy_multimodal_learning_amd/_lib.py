@@ -109,3 +109,18 @@ def stream_of(device=None):
 def arr(struct_type, items):
     a = (struct_type * len(items))(*items)
     return a
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [("N", c_int), ("H", c_int), ("W", c_int), ("C", c_int), ("K", c_int),
+                ("R", c_int), ("S", c_int), ("stride", c_int), ("pad", c_int)]
+
+
+EXPORTS.update({
+    "gm_conv2d_fwd_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "gm_conv2d_dgrad_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "gm_conv_weight_transpose_bf16": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "gm_conv2d_wgrad_scratch": (c_size_t, [c_void_p]),
+    "gm_conv2d_wgrad_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_size_t,
+                                     c_void_p]),
+})

@@ -1,0 +1,134 @@
+"""ResNet trunk convolutions on the bf16 MFMA implicit-GEMM kernels.
+
+`GMConv2d` is an `nn.Conv2d` (same parameters, names, init and state_dict) whose
+forward runs `gm_conv2d_fwd_bf16` and whose backward runs
+`gm_conv2d_dgrad_bf16` + `gm_conv2d_wgrad_bf16` whenever it sees a bf16 input on
+a HIP device (the engine's bf16 channels_last trunk, or autocast-bf16).  fp32
+inputs (the fp32 parity mode) go through PyTorch's convolution (MIOpen).
+Activations are channels_last (NHWC) bf16, weights are cast to bf16 KRSC per
+step, weight gradients come back in fp32 in the parameter's layout.
+"""
+import ctypes
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib as L
+
+CL = torch.channels_last
+
+
+def _desc(N, H, W, C, K, R, S, stride, pad):
+    return L.ConvDesc(N, H, W, C, K, R, S, stride, pad)
+
+
+def _nhwc(t):
+    return t if t.is_contiguous(memory_format=CL) else t.contiguous(memory_format=CL)
+
+
+def _pad_c(x, c):
+    """[N,C,H,W] channels_last -> channels padded with zeros to c (e.g. RGB -> 8)."""
+    N, C0, H, W = x.shape
+    out = torch.zeros(N, c, H, W, device=x.device, dtype=x.dtype, memory_format=CL)
+    out[:, :C0].copy_(x)
+    return out
+
+
+def _cpad(c):
+    p = 8
+    while p < c:
+        p *= 2
+    return p
+
+
+def conv_fwd(x, w, stride, pad):
+    """x [N,C,H,W] bf16 channels_last, w [K,C,R,S] bf16 channels_last -> y [N,K,P,Q]."""
+    lib = L.load()
+    N, C, H, W = x.shape
+    K, _, R, S = w.shape
+    P = (H + 2 * pad - R) // stride + 1
+    Q = (W + 2 * pad - S) // stride + 1
+    y = torch.empty(N, K, P, Q, device=x.device, dtype=torch.bfloat16, memory_format=CL)
+    d = _desc(N, H, W, C, K, R, S, stride, pad)
+    L.check(lib.gm_conv2d_fwd_bf16(ctypes.byref(d), x.data_ptr(), w.data_ptr(), y.data_ptr(),
+                                   L.stream_of(x.device)), "gm_conv2d_fwd_bf16")
+    return y
+
+
+def conv_dgrad(dy, w, H, W, stride, pad):
+    lib = L.load()
+    N, K, P, Q = dy.shape
+    _, C, R, S = w.shape
+    wt = torch.empty(C, K, R, S, device=w.device, dtype=torch.bfloat16, memory_format=CL)
+    L.check(lib.gm_conv_weight_transpose_bf16(w.data_ptr(), wt.data_ptr(), K, R * S, C,
+                                              L.stream_of(w.device)), "gm_conv_weight_transpose_bf16")
+    dx = torch.empty(N, C, H, W, device=dy.device, dtype=torch.bfloat16, memory_format=CL)
+    d = _desc(N, H, W, C, K, R, S, stride, pad)
+    L.check(lib.gm_conv2d_dgrad_bf16(ctypes.byref(d), dy.data_ptr(), wt.data_ptr(), dx.data_ptr(),
+                                     L.stream_of(dy.device)), "gm_conv2d_dgrad_bf16")
+    return dx
+
+
+def conv_wgrad(dy, x, R, S, stride, pad, c_real):
+    lib = L.load()
+    N, C, H, W = x.shape
+    K = dy.shape[1]
+    d = _desc(N, H, W, C, K, R, S, stride, pad)
+    need = lib.gm_conv2d_wgrad_scratch(ctypes.byref(d))
+    scratch = torch.empty(max(need, 16), device=x.device, dtype=torch.uint8)
+    dw = torch.empty(K, c_real, R, S, device=x.device, dtype=torch.float32, memory_format=CL)
+    L.check(lib.gm_conv2d_wgrad_bf16(ctypes.byref(d), dy.data_ptr(), x.data_ptr(), dw.data_ptr(), c_real,
+                                     scratch.data_ptr(), need, L.stream_of(x.device)), "gm_conv2d_wgrad_bf16")
+    return dw
+
+
+class _ConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, stride, pad):
+        C0 = x.shape[1]
+        Cp = _cpad(C0)
+        xb = _nhwc(x.to(torch.bfloat16))
+        wb = weight.detach().to(torch.bfloat16).contiguous(memory_format=CL)
+        if Cp != C0:
+            xb = _pad_c(xb, Cp)
+            wb = _pad_c(wb, Cp)
+        y = conv_fwd(xb, wb, stride, pad)
+        ctx.save_for_backward(xb, wb)
+        ctx.meta = (stride, pad, C0, x.shape[2], x.shape[3])
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        xb, wb = ctx.saved_tensors
+        stride, pad, C0, H, W = ctx.meta
+        gy = _nhwc(gy.to(torch.bfloat16))
+        R, S = wb.shape[2], wb.shape[3]
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = conv_dgrad(gy, wb, H, W, stride, pad)
+            if dx.shape[1] != C0:
+                dx = dx[:, :C0]
+        dw = conv_wgrad(gy, xb, R, S, stride, pad, C0) if ctx.needs_input_grad[1] else None
+        return dx, dw, None, None
+
+
+def _use_hip(x):
+    if not x.is_cuda:
+        return False
+    if x.dtype == torch.bfloat16:
+        return True
+    return torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+
+
+class GMConv2d(nn.Conv2d):
+    """nn.Conv2d whose bf16 path runs on libgreedymml_hip.so (groups=1, no bias,
+    square stride/padding, dilation 1 - the ResNet trunk's convolutions)."""
+
+    def forward(self, x):
+        if (_use_hip(x) and self.groups == 1 and self.bias is None and self.dilation == (1, 1)
+                and self.stride[0] == self.stride[1] and self.padding[0] == self.padding[1]
+                and self.padding_mode == "zeros"):
+            with torch.autocast("cuda", enabled=False):
+                return _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0])
+        return F.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation, self.groups)

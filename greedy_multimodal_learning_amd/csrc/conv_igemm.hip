@@ -1,0 +1,365 @@
+// bf16 implicit-GEMM convolution on MFMA (gfx950), NHWC activations, KRSC weights.
+//
+// One kernel serves the ResNet trunk's forward convolutions and their input
+// gradients (the trunk of reference src/model.py:53-106, torchvision ResNet):
+//
+//   out[b, p*oS+oH, q*oS+oW, n] = sum_{t < ntap} sum_c in[b, p*sA+dh_t, q*sA+dw_t, c] * wt[n, tap_t, c]
+//
+//   forward  : one class, taps (r,s) with dh = r - pad, dw = s - pad, sA = stride, oS = 1;
+//   dgrad    : input = dY, weights = transpose(W) [Ci][R][S][Co], sA = 1; the output
+//              pixels split into stride^2 parity classes (ph, pw), each with only the
+//              taps r where (ph + pad - r) % stride == 0 and dh = (ph + pad - r)/stride,
+//              so a strided convolution's input gradient wastes no MFMA work.
+//
+// GEMM view: M = B*P*Q output pixels, N = output channels, K = ntap*C (c fastest).
+// Tiles BM x BN x 64; 256 threads = 2x2 waves, each wave (BM/2)x(BN/2) built from
+// v_mfma_f32_32x32x16_bf16 tiles; operands staged global -> registers -> LDS
+// (double-buffered, next tile's loads issued before this tile's MFMAs), LDS rows of
+// 128 B XOR-swizzled by ((row>>1)&7) so the ds_read_b128 fragment reads are
+// conflict-free; fp32 accumulation; epilogue stages the bf16 tile through LDS and
+// writes whole 16-B chunks of NHWC rows.  Out-of-range taps read zeros.
+#include <cstring>
+
+#include "gm_common.h"
+
+namespace gm {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int kMaxTap = 49;
+constexpr int kMaxCls = 4;
+
+struct ConvCls {
+    uint16_t* out;
+    int P, Q;                 // GEMM output grid of this class
+    int oS, oH, oW;           // output pixel = (p*oS + oH, q*oS + oW)
+    int ntap;
+    int tile_start;           // first workgroup of this class
+    int tiles_m;
+    short tw[kMaxTap];        // weight tap index (r*S + s)
+    signed char dh[kMaxTap], dw[kMaxTap];
+};
+
+struct ConvArgs {
+    const uint16_t* in;       // [N][Hi][Wi][C]
+    const uint16_t* wt;       // [Nout][T][C]
+    int N, Hi, Wi, C, logC;
+    int Nout, T;              // output channels, taps per weight row
+    int Ho, Wo;               // full output spatial dims
+    int sA;
+    int ncls;
+    ConvCls cls[kMaxCls];
+};
+
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
+    constexpr int BK = 64;
+    constexpr int AR = BM / 32;       // A rows per thread
+    constexpr int BR = BN / 32;       // B rows per thread
+    constexpr int MT = BM / 64, NT = BN / 64;  // 32x32 MFMA tiles per wave
+    extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+    uint4* As = smem;                           // [2][BM][8] (16-B chunks)
+    uint4* Bs = smem + 2 * BM * 8;              // [2][BN][8]
+
+    int ci = 0;
+#pragma unroll
+    for (int q = 1; q < kMaxCls; ++q)
+        if (q < a.ncls && (int)blockIdx.x >= a.cls[q].tile_start) ci = q;
+    const ConvCls& cl = a.cls[ci];
+    const int wgid = blockIdx.x - cl.tile_start;
+    const int tm = wgid % cl.tiles_m, tn = wgid / cl.tiles_m;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int PQ = cl.P * cl.Q;
+    const int M = a.N * PQ;
+    const int Ktot = cl.ntap * a.C;
+    const int nk = (Ktot + BK - 1) / BK;
+
+    const int t = threadIdx.x;
+    const int lane = t & 63, wave = t >> 6;
+    // tap table -> LDS (static indices only into the kernel-argument struct)
+    int* tapt = (int*)(smem + 2 * (BM + BN) * 8);
+#pragma unroll
+    for (int i = 0; i < kMaxTap; ++i)
+        if (t == i && i < cl.ntap)
+            tapt[i] = (int)cl.tw[i] | ((int)(cl.dh[i] + 128) << 8) | ((int)(cl.dw[i] + 128) << 16);
+    __syncthreads();
+    const int wm = wave >> 1, wn = wave & 1;
+    const int lchunk = t & 7, lrow = t >> 3;   // loader: 8 threads per 128-B row
+
+    // per-thread A row geometry
+    int a_base[AR], a_h[AR], a_w[AR];
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+        const int m = m0 + lrow + 32 * i;
+        if (m < M) {
+            const int b = m / PQ, pq = m - b * PQ;
+            const int p = pq / cl.Q, q = pq - p * cl.Q;
+            a_base[i] = b * a.Hi * a.Wi;
+            a_h[i] = p * a.sA;
+            a_w[i] = q * a.sA;
+        } else {
+            a_base[i] = 0;
+            a_h[i] = -(1 << 28);  // never valid
+            a_w[i] = 0;
+        }
+    }
+
+    uint4 ra[AR], rb[BR];
+    auto load_tile = [&](int kt) {
+        const int k = kt * BK + lchunk * 8;
+        const bool kin = k < Ktot;
+        const int tap = kin ? (k >> a.logC) : 0;
+        const int c = k & (a.C - 1);
+        const int te = tapt[tap];
+        const int tw = te & 0xff, dh = ((te >> 8) & 0xff) - 128, dw = ((te >> 16) & 0xff) - 128;
+#pragma unroll
+        for (int i = 0; i < AR; ++i) {
+            const int hi = a_h[i] + dh, wi = a_w[i] + dw;
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (kin && (unsigned)hi < (unsigned)a.Hi && (unsigned)wi < (unsigned)a.Wi)
+                v = *(const uint4*)(a.in + ((size_t)(a_base[i] + hi * a.Wi + wi) << a.logC) + c);
+            ra[i] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < BR; ++i) {
+            const int n = n0 + lrow + 32 * i;
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (kin && n < a.Nout)
+                v = *(const uint4*)(a.wt + ((size_t)n * a.T + tw) * a.C + c);
+            rb[i] = v;
+        }
+    };
+    auto store_tile = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < AR; ++i) {
+            const int row = lrow + 32 * i;
+            As[(buf * BM + row) * 8 + swz(row, lchunk)] = ra[i];
+        }
+#pragma unroll
+        for (int i = 0; i < BR; ++i) {
+            const int row = lrow + 32 * i;
+            Bs[(buf * BN + row) * 8 + swz(row, lchunk)] = rb[i];
+        }
+    };
+
+    floatx16 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    if (nk > 0) {
+        load_tile(0);
+        store_tile(0);
+    }
+    __syncthreads();
+    const int fr = lane & 31, fh = lane >> 5;
+    for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+        if (kt + 1 < nk) load_tile(kt + 1);
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            const int chunk = ks * 2 + fh;
+            bf16x8 af[MT], bfr[NT];
+#pragma unroll
+            for (int i = 0; i < MT; ++i) {
+                const int row = wm * (BM / 2) + i * 32 + fr;
+                af[i] = __builtin_bit_cast(bf16x8, As[(buf * BM + row) * 8 + swz(row, chunk)]);
+            }
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+                const int row = wn * (BN / 2) + j * 32 + fr;
+                bfr[j] = __builtin_bit_cast(bf16x8, Bs[(buf * BN + row) * 8 + swz(row, chunk)]);
+            }
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+        if (kt + 1 < nk) store_tile(buf ^ 1);
+        __syncthreads();
+    }
+
+    // ---- epilogue: acc -> bf16 tile in LDS [BM][BN] -> 16-B NHWC stores ----
+    uint16_t* Cs = (uint16_t*)smem;
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+                const int col = wn * (BN / 2) + j * 32 + fr;
+                Cs[row * BN + col] = Elem<uint16_t>::f2bf(acc[i][j][r]);
+            }
+    __syncthreads();
+    constexpr int CPR = BN / 8;  // 16-B chunks per row
+    for (int idx = t; idx < BM * CPR; idx += 256) {
+        const int row = idx / CPR, ch = idx - row * CPR;
+        const int m = m0 + row, n = n0 + ch * 8;
+        if (m >= M || n >= a.Nout) continue;
+        const int b = m / PQ, pq = m - b * PQ;
+        const int p = pq / cl.Q, q = pq - p * cl.Q;
+        const int ho = p * cl.oS + cl.oH, wo = q * cl.oS + cl.oW;
+        uint16_t* dst = cl.out + ((size_t)(b * a.Ho + ho) * a.Wo + wo) * a.Nout + n;
+        *(uint4*)dst = *(const uint4*)(Cs + row * BN + ch * 8);
+    }
+}
+
+// zero the output pixels no dgrad class covers (e.g. odd pixels of a 1x1/s2 dgrad)
+__global__ void k_zero_bf16(uint16_t* p, size_t n) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i * 8 < n; i += (size_t)gridDim.x * blockDim.x) *(uint4*)(p + i * 8) = make_uint4(0, 0, 0, 0);
+}
+
+// W[Co][T][Ci] -> Wt[Ci][T][Co] (bf16), for the input-gradient convolution
+__global__ void k_transpose_w(const uint16_t* w, uint16_t* wt, int Co, int T, int Ci) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int n = Co * T * Ci;
+    if (i >= n) return;
+    const int c = i % Ci, tk = (i / Ci) % T, k = i / (Ci * T);
+    wt[((size_t)c * T + tk) * Co + k] = w[i];
+}
+
+static int ilog2(int v) {
+    int l = 0;
+    while ((1 << l) < v) ++l;
+    return (1 << l) == v ? l : -1;
+}
+
+}  // namespace gm
+
+using namespace gm;
+
+template <int BM, int BN>
+static int launch_igemm(ConvArgs& a, hipStream_t st) {
+    int tiles = 0;
+    for (int i = 0; i < a.ncls; ++i) {
+        ConvCls& c = a.cls[i];
+        const int M = a.N * c.P * c.Q;
+        c.tiles_m = (M + BM - 1) / BM;
+        c.tile_start = tiles;
+        tiles += c.tiles_m * ((a.Nout + BN - 1) / BN);
+    }
+    if (tiles == 0) return GM_OK;
+    const size_t lds = (size_t)2 * (BM + BN) * 128 + kMaxTap * 4 + 12;
+    static bool attr_set = false;  // idempotent, safe to race
+    if (!attr_set) {
+        hipFuncSetAttribute((const void*)k_conv_igemm<BM, BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+        attr_set = true;
+    }
+    k_conv_igemm<BM, BN><<<tiles, 256, lds, st>>>(a);
+    return check_launch("k_conv_igemm");
+}
+
+static int pick_and_launch(ConvArgs& a, hipStream_t st) {
+    long M = 0;
+    for (int i = 0; i < a.ncls; ++i) M += (long)a.N * a.cls[i].P * a.cls[i].Q;
+    // enough workgroups to fill 256 CUs, largest tile that does
+    if (a.Nout >= 128 && M / 128 * (a.Nout / 128) >= 512) return launch_igemm<128, 128>(a, st);
+    if (a.Nout <= 64 && M / 256 >= 512) return launch_igemm<256, 64>(a, st);
+    if (M / 128 * ((a.Nout + 63) / 64) >= 512) return launch_igemm<128, 64>(a, st);
+    return launch_igemm<64, 64>(a, st);
+}
+
+static int check_desc(const gm_conv_desc* d) {
+    GM_REQUIRE(d && d->N > 0 && d->H > 0 && d->W > 0 && d->C > 0 && d->K > 0 && d->R > 0 && d->S > 0,
+               "conv: empty shape");
+    GM_REQUIRE(d->stride >= 1 && d->pad >= 0, "conv: bad stride/pad");
+    GM_REQUIRE(d->R * d->S <= kMaxTap, "conv: at most %d taps", kMaxTap);
+    GM_REQUIRE(ilog2(d->C) >= 3, "conv: C must be a power of two >= 8 (got %d)", d->C);
+    GM_REQUIRE(d->K % 8 == 0, "conv: K must be a multiple of 8 (got %d)", d->K);
+    return GM_OK;
+}
+
+extern "C" int gm_conv2d_fwd_bf16(const gm_conv_desc* d, const void* x, const void* w, void* y, void* stream) {
+    int rc = check_desc(d);
+    if (rc) return rc;
+    GM_REQUIRE(x && w && y, "conv fwd: null pointer");
+    const int P = (d->H + 2 * d->pad - d->R) / d->stride + 1;
+    const int Q = (d->W + 2 * d->pad - d->S) / d->stride + 1;
+    ConvArgs a;
+    memset(&a, 0, sizeof(a));
+    a.in = (const uint16_t*)x;
+    a.wt = (const uint16_t*)w;
+    a.N = d->N; a.Hi = d->H; a.Wi = d->W; a.C = d->C; a.logC = ilog2(d->C);
+    a.Nout = d->K; a.T = d->R * d->S;
+    a.Ho = P; a.Wo = Q; a.sA = d->stride;
+    a.ncls = 1;
+    ConvCls& c = a.cls[0];
+    c.out = (uint16_t*)y;
+    c.P = P; c.Q = Q; c.oS = 1; c.oH = 0; c.oW = 0;
+    c.ntap = d->R * d->S;
+    for (int r = 0; r < d->R; ++r)
+        for (int s = 0; s < d->S; ++s) {
+            const int i = r * d->S + s;
+            c.tw[i] = (short)i;
+            c.dh[i] = (signed char)(r - d->pad);
+            c.dw[i] = (signed char)(s - d->pad);
+        }
+    return pick_and_launch(a, as_stream(stream));
+}
+
+extern "C" int gm_conv2d_dgrad_bf16(const gm_conv_desc* d, const void* dy, const void* wt, void* dx,
+                                    void* stream) {
+    int rc = check_desc(d);
+    if (rc) return rc;
+    GM_REQUIRE(dy && wt && dx, "conv dgrad: null pointer");
+    GM_REQUIRE(ilog2(d->K) >= 3, "conv dgrad: K must be a power of two >= 8 (got %d)", d->K);
+    const int st = d->stride;
+    GM_REQUIRE(st * st <= kMaxCls, "conv dgrad: stride %d unsupported", st);
+    const int P = (d->H + 2 * d->pad - d->R) / st + 1;
+    const int Q = (d->W + 2 * d->pad - d->S) / st + 1;
+    ConvArgs a;
+    memset(&a, 0, sizeof(a));
+    a.in = (const uint16_t*)dy;
+    a.wt = (const uint16_t*)wt;
+    a.N = d->N; a.Hi = P; a.Wi = Q; a.C = d->K; a.logC = ilog2(d->K);
+    a.Nout = d->C; a.T = d->R * d->S;
+    a.Ho = d->H; a.Wo = d->W; a.sA = 1;
+    bool full = true;
+    hipStream_t s = as_stream(stream);
+    for (int ph = 0; ph < st; ++ph)
+        for (int pw = 0; pw < st; ++pw) {
+            ConvCls& c = a.cls[a.ncls];
+            c.out = (uint16_t*)dx;
+            c.P = (d->H - ph + st - 1) / st;
+            c.Q = (d->W - pw + st - 1) / st;
+            c.oS = st; c.oH = ph; c.oW = pw;
+            int n = 0;
+            for (int r = 0; r < d->R; ++r) {
+                if (((ph + d->pad - r) % st + st) % st) continue;
+                for (int sx = 0; sx < d->S; ++sx) {
+                    if (((pw + d->pad - sx) % st + st) % st) continue;
+                    c.tw[n] = (short)(r * d->S + sx);
+                    c.dh[n] = (signed char)((ph + d->pad - r) / st);
+                    c.dw[n] = (signed char)((pw + d->pad - sx) / st);
+                    ++n;
+                }
+            }
+            c.ntap = n;
+            if (n == 0 || c.P <= 0 || c.Q <= 0) { full = false; continue; }
+            ++a.ncls;
+        }
+    if (!full) {
+        const size_t n = (size_t)d->N * d->H * d->W * d->C;
+        k_zero_bf16<<<(int)((n / 8 + 255) / 256 < 4096 ? (n / 8 + 255) / 256 : 4096), 256, 0, s>>>((uint16_t*)dx, n);
+        rc = check_launch("k_zero_bf16");
+        if (rc) return rc;
+    }
+    return pick_and_launch(a, s);
+}
+
+extern "C" int gm_conv_weight_transpose_bf16(const void* w, void* wt, int Co, int T, int Ci, void* stream) {
+    GM_REQUIRE(w && wt && Co > 0 && T > 0 && Ci > 0, "weight transpose: bad args");
+    const int n = Co * T * Ci;
+    k_transpose_w<<<(n + 255) / 256, 256, 0, as_stream(stream)>>>((const uint16_t*)w, (uint16_t*)wt, Co, T, Ci);
+    return check_launch("k_transpose_w");
+}

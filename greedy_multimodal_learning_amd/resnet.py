@@ -6,18 +6,20 @@ dependency here; this module provides the same architecture and the same
 parameter names (`conv1`, `bn1`, `layer{1..4}.{i}.{conv,bn}{1,2}`,
 `layer{2..4}.0.downsample.{0,1}`, `fc`), so checkpoints and the gating's
 name-based grouping carry over unchanged.  Bottleneck/ResNet-50 serves
-config C5.
+config C5.  Convolutions are `conv.GMConv2d` (bf16 MFMA kernels on HIP).
 """
 import torch
 import torch.nn as nn
 
+from .conv import GMConv2d
+
 
 def conv3x3(cin, cout, stride=1):
-    return nn.Conv2d(cin, cout, 3, stride=stride, padding=1, bias=False)
+    return GMConv2d(cin, cout, 3, stride=stride, padding=1, bias=False)
 
 
 def conv1x1(cin, cout, stride=1):
-    return nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
+    return GMConv2d(cin, cout, 1, stride=stride, bias=False)
 
 
 class BasicBlock(nn.Module):
@@ -67,7 +69,7 @@ class ResNet(nn.Module):
     def __init__(self, block, layers, num_classes=1000):
         super().__init__()
         self.inplanes = 64
-        self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
+        self.conv1 = GMConv2d(3, 64, 7, stride=2, padding=3, bias=False)
         self.bn1 = nn.BatchNorm2d(64)
         self.relu = nn.ReLU(inplace=True)
         self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)

@@ -158,6 +158,32 @@ int gm_group_sumsq(const gm_tensor* table, int ntensors, long long total_elems, 
                    float grad_scale, float lr, double* out, void* scratch, size_t scratch_bytes,
                    void* stream);
 
+/* ---------------------------------------------------------------------------
+ * ResNet trunk convolutions (torchvision resnet18/50 Conv2d, bias=False; called
+ * piecewise at reference src/model.py:65-106) as bf16 implicit GEMMs on MFMA.
+ * Activations NHWC [N][H][W][C] bf16, weights KRSC [K][R][S][C] bf16 (PyTorch
+ * channels_last weight order), fp32 accumulation.  Output P = (H+2pad-R)/stride+1.
+ *   fwd   : y[N][P][Q][K]   = conv(x, w)
+ *   dgrad : dx[N][H][W][C]  = conv_transpose(dy[N][P][Q][K], w); `wt` is the
+ *           channel-transposed weight [C][R][S][K] (gm_conv_weight_transpose_bf16)
+ *   wgrad : dw[K][R][S][C]  = sum over N,P,Q of dy x x-patch, fp32 output;
+ *           scratch >= gm_conv2d_wgrad_scratch() bytes (split-K partials)
+ * C must be a power of two >= 8 (pad 3-channel images to 8), K a multiple of 8.
+ * ------------------------------------------------------------------------- */
+typedef struct gm_conv_desc {
+    int N, H, W, C;
+    int K, R, S;
+    int stride, pad;
+} gm_conv_desc;
+
+int gm_conv2d_fwd_bf16(const gm_conv_desc* d, const void* x, const void* w, void* y, void* stream);
+int gm_conv2d_dgrad_bf16(const gm_conv_desc* d, const void* dy, const void* wt, void* dx, void* stream);
+int gm_conv_weight_transpose_bf16(const void* w, void* wt, int K, int RS, int C, void* stream);
+/* dw is fp32 [K][R][S][c_real]: the first c_real of the C (padded) input channels */
+size_t gm_conv2d_wgrad_scratch(const gm_conv_desc* d);
+int gm_conv2d_wgrad_bf16(const gm_conv_desc* d, const void* dy, const void* x, float* dw, int c_real,
+                         void* scratch, size_t scratch_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,76 @@
+"""bf16 MFMA implicit-GEMM convolutions (fwd / dgrad / wgrad) vs PyTorch fp32 on the CPU.
+
+Inputs and weights are rounded to bf16 first, so every product is exact in fp32 and
+the only differences are fp32 summation order and the bf16 rounding of the
+activation outputs (fwd, dgrad: 2^-8 relative) -> tolerance 1e-2 of the tensor's
+max; the fp32 weight gradient -> 2e-3 of its max.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [  # N, C, H, W, K, R, S, stride, pad
+    (2, 64, 56, 56, 64, 3, 3, 1, 1),
+    (2, 64, 56, 56, 128, 3, 3, 2, 1),
+    (2, 64, 56, 56, 128, 1, 1, 2, 0),
+    (2, 128, 28, 28, 128, 3, 3, 1, 1),
+    (2, 256, 14, 14, 512, 3, 3, 2, 1),
+    (2, 512, 7, 7, 512, 3, 3, 1, 1),
+    (2, 3, 64, 64, 64, 7, 7, 2, 3),
+    (3, 64, 9, 11, 64, 3, 3, 2, 1),
+    (1, 8, 5, 5, 16, 3, 3, 1, 1),
+    (5, 128, 7, 7, 256, 1, 1, 2, 0),
+]
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda:0")
+
+
+def _close(a, b, tol):
+    a, b = a.detach().float().cpu(), b.detach().float().cpu()
+    scale = float(b.abs().max()) + 1e-12
+    np.testing.assert_allclose(a.numpy(), b.numpy(), rtol=0, atol=tol * scale)
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_conv_fwd_dgrad_wgrad(dev, shape):
+    from greedy_multimodal_learning_amd.conv import GMConv2d
+    N, C, H, W, K, R, S, st, pad = shape
+    g = torch.Generator().manual_seed(sum(shape))
+    x = torch.randn(N, C, H, W, generator=g).bfloat16()
+    w = (torch.randn(K, C, R, S, generator=g) / (C * R * S) ** 0.5).bfloat16()
+    gy_shape = (N, K, (H + 2 * pad - R) // st + 1, (W + 2 * pad - S) // st + 1)
+    gy = torch.randn(*gy_shape, generator=g).bfloat16()
+    # reference: fp32 on the CPU from the bf16-rounded values
+    xr, wr = x.float().requires_grad_(True), w.float().requires_grad_(True)
+    yr = F.conv2d(xr, wr, stride=st, padding=pad)
+    yr.backward(gy.float())
+    # HIP
+    m = GMConv2d(C, K, (R, S), stride=st, padding=pad, bias=False).to(dev)
+    with torch.no_grad():
+        m.weight.copy_(w.float())
+    m = m.to(memory_format=torch.channels_last)
+    xd = x.to(dev).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    y = m(xd)
+    assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=torch.channels_last)
+    y.backward(gy.to(dev).contiguous(memory_format=torch.channels_last))
+    _close(y, yr, 1e-2)
+    _close(xd.grad, xr.grad, 1e-2)
+    assert m.weight.grad.dtype == torch.float32
+    _close(m.weight.grad, wr.grad, 2e-3)
+
+
+def test_conv_fp32_input_uses_vendor_path(dev):
+    from greedy_multimodal_learning_amd.conv import GMConv2d
+    m = GMConv2d(8, 8, 3, padding=1, bias=False).to(dev)
+    x = torch.randn(1, 8, 5, 5, device=dev)
+    y = m(x)
+    assert y.dtype == torch.float32
+    torch.testing.assert_close(y, F.conv2d(x, m.weight, padding=1))
