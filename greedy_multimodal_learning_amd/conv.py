@@ -30,7 +30,7 @@ def _nhwc(t):
 def _pad_c(x, c):
     """[N,C,H,W] channels_last -> channels padded with zeros to c (e.g. RGB -> 8)."""
     N, C0, H, W = x.shape
-    out = torch.zeros(N, c, H, W, device=x.device, dtype=x.dtype, memory_format=CL)
+    out = torch.empty(N, c, H, W, device=x.device, dtype=x.dtype, memory_format=CL).zero_()
     out[:, :C0].copy_(x)
     return out
 

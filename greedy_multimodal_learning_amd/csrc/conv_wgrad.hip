@@ -21,6 +21,7 @@ namespace gm {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short short4_t __attribute__((ext_vector_type(4)));
+typedef short short8_t __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int kWTap = 49;
@@ -40,13 +41,8 @@ typedef __attribute__((address_space(3))) short4_t lds_s4;
 __device__ __forceinline__ bf16x8 tr_frag(const uint16_t* base_row0, const uint16_t* base_row4) {
     const short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)base_row0);
     const short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)base_row4);
-    bf16x8 f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        f[j] = __builtin_bit_cast(__bf16, lo[j]);
-        f[j + 4] = __builtin_bit_cast(__bf16, hi[j]);
-    }
-    return f;
+    const short8_t s = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, s);
 }
 
 __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a) {
