@@ -83,30 +83,57 @@ def conv_wgrad(dy, x, R, S, stride, pad, c_real):
     return dw
 
 
+def weight_prep(weight, Cp, transposed):
+    """fp32 [K,C,R,S] parameter -> bf16 KRSC copy padded to Cp channels (+ optional
+    channel-transposed copy [Cp,K,R,S] for dgrad), one kernel."""
+    lib = L.load()
+    K, C, R, S = weight.shape
+    w32 = weight.detach()
+    if w32.dtype != torch.float32:
+        w32 = w32.float()
+    w32 = _nhwc(w32)
+    wb = torch.empty(K, Cp, R, S, device=w32.device, dtype=torch.bfloat16, memory_format=CL)
+    wt = torch.empty(Cp, K, R, S, device=w32.device, dtype=torch.bfloat16, memory_format=CL) if transposed else None
+    L.check(lib.gm_conv_weight_prep_bf16(w32.data_ptr(), K, R * S, C, Cp, wb.data_ptr(), L.ptr(wt),
+                                         L.stream_of(w32.device)), "gm_conv_weight_prep_bf16")
+    return wb, wt
+
+
+def conv_dgrad_t(dy, wt, H, W, stride, pad):
+    """dgrad from an already transposed bf16 weight wt [C,K,R,S] (channels_last)."""
+    lib = L.load()
+    N, K, P, Q = dy.shape
+    C, _, R, S = wt.shape
+    dx = torch.empty(N, C, H, W, device=dy.device, dtype=torch.bfloat16, memory_format=CL)
+    d = _desc(N, H, W, C, K, R, S, stride, pad)
+    L.check(lib.gm_conv2d_dgrad_bf16(ctypes.byref(d), dy.data_ptr(), wt.data_ptr(), dx.data_ptr(),
+                                     L.stream_of(dy.device)), "gm_conv2d_dgrad_bf16")
+    return dx
+
+
 class _ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, stride, pad):
         C0 = x.shape[1]
         Cp = _cpad(C0)
         xb = _nhwc(x.to(torch.bfloat16))
-        wb = weight.detach().to(torch.bfloat16).contiguous(memory_format=CL)
         if Cp != C0:
             xb = _pad_c(xb, Cp)
-            wb = _pad_c(wb, Cp)
+        need_dx = ctx.needs_input_grad[0]
+        wb, wt = weight_prep(weight, Cp, need_dx)
         y = conv_fwd(xb, wb, stride, pad)
-        ctx.save_for_backward(xb, wb)
-        ctx.meta = (stride, pad, C0, x.shape[2], x.shape[3])
+        ctx.save_for_backward(xb, wt)
+        ctx.meta = (stride, pad, C0, x.shape[2], x.shape[3], weight.shape[2], weight.shape[3])
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        xb, wb = ctx.saved_tensors
-        stride, pad, C0, H, W = ctx.meta
+        xb, wt = ctx.saved_tensors
+        stride, pad, C0, H, W, R, S = ctx.meta
         gy = _nhwc(gy.to(torch.bfloat16))
-        R, S = wb.shape[2], wb.shape[3]
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = conv_dgrad(gy, wb, H, W, stride, pad)
+            dx = conv_dgrad_t(gy, wt, H, W, stride, pad)
             if dx.shape[1] != C0:
                 dx = dx[:, :C0]
         dw = conv_wgrad(gy, xb, R, S, stride, pad, C0) if ctx.needs_input_grad[1] else None

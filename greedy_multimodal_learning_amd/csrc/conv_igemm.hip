@@ -180,35 +180,35 @@ __global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
             for (int i = 0; i < MT; ++i)
 #pragma unroll
                 for (int j = 0; j < NT; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                    // weights as the MFMA A operand, pixels as B: D[n][m], so each lane ends
+                    // up holding 4 consecutive output channels of ONE pixel per register group
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
         }
         if (kt + 1 < nk) store_tile(buf ^ 1);
         __syncthreads();
     }
 
-    // ---- epilogue: acc -> bf16 tile in LDS [BM][BN] -> 16-B NHWC stores ----
-    uint16_t* Cs = (uint16_t*)smem;
+    // ---- epilogue: D[n][m] layout: lane -> pixel m (col = lane&31), registers 4g..4g+3 ->
+    // channels 8g + 4h + 0..3 (row = (r&3) + 8(r>>2) + 4h): 8-byte NHWC stores, no LDS ----
 #pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
-                const int col = wn * (BN / 2) + j * 32 + fr;
-                Cs[row * BN + col] = Elem<uint16_t>::f2bf(acc[i][j][r]);
-            }
-    __syncthreads();
-    constexpr int CPR = BN / 8;  // 16-B chunks per row
-    for (int idx = t; idx < BM * CPR; idx += 256) {
-        const int row = idx / CPR, ch = idx - row * CPR;
-        const int m = m0 + row, n = n0 + ch * 8;
-        if (m >= M || n >= a.Nout) continue;
+    for (int i = 0; i < MT; ++i) {
+        const int m = m0 + wm * (BM / 2) + i * 32 + fr;
+        if (m >= M) continue;
         const int b = m / PQ, pq = m - b * PQ;
         const int p = pq / cl.Q, q = pq - p * cl.Q;
         const int ho = p * cl.oS + cl.oH, wo = q * cl.oS + cl.oW;
-        uint16_t* dst = cl.out + ((size_t)(b * a.Ho + ho) * a.Wo + wo) * a.Nout + n;
-        *(uint4*)dst = *(const uint4*)(Cs + row * BN + ch * 8);
+        uint16_t* dst = cl.out + ((size_t)(b * a.Ho + ho) * a.Wo + wo) * a.Nout;
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int gq = 0; gq < 4; ++gq) {
+                const int n = n0 + wn * (BN / 2) + j * 32 + 8 * gq + 4 * fh;
+                if (n >= a.Nout) continue;
+                uint2 v;
+                v.x = pack_bf2(acc[i][j][4 * gq], acc[i][j][4 * gq + 1]);
+                v.y = pack_bf2(acc[i][j][4 * gq + 2], acc[i][j][4 * gq + 3]);
+                *(uint2*)(dst + n) = v;
+            }
     }
 }
 
@@ -263,9 +263,8 @@ static int pick_and_launch(ConvArgs& a, hipStream_t st) {
     long M = 0;
     for (int i = 0; i < a.ncls; ++i) M += (long)a.N * a.cls[i].P * a.cls[i].Q;
     // enough workgroups to fill 256 CUs, largest tile that does
-    if (a.Nout >= 128 && M / 128 * (a.Nout / 128) >= 512) return launch_igemm<128, 128>(a, st);
-    if (a.Nout <= 64 && M / 256 >= 512) return launch_igemm<256, 64>(a, st);
-    if (M / 128 * ((a.Nout + 63) / 64) >= 512) return launch_igemm<128, 64>(a, st);
+    if (a.Nout >= 128 && M / 128 * (a.Nout / 128) >= 1024) return launch_igemm<128, 128>(a, st);
+    if (M / 128 * ((a.Nout + 63) / 64) >= 768) return launch_igemm<128, 64>(a, st);
     return launch_igemm<64, 64>(a, st);
 }
 
@@ -362,4 +361,28 @@ extern "C" int gm_conv_weight_transpose_bf16(const void* w, void* wt, int Co, in
     const int n = Co * T * Ci;
     k_transpose_w<<<(n + 255) / 256, 256, 0, as_stream(stream)>>>((const uint16_t*)w, (uint16_t*)wt, Co, T, Ci);
     return check_launch("k_transpose_w");
+}
+
+// fp32 master weight [K][RS][C] (KRSC) -> bf16 [K][RS][Cp] (channels zero-padded to Cp)
+// and, optionally, the channel-transposed bf16 copy [Cp][RS][K] used by dgrad: one pass
+// instead of a cast + a transpose per convolution.
+__global__ void k_weight_prep(const float* __restrict__ w, int K, int RS, int C, int Cp,
+                              uint16_t* __restrict__ wb, uint16_t* __restrict__ wt) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int n = K * RS * Cp;
+    if (i >= n) return;
+    const int c = i % Cp, t = (i / Cp) % RS, k = i / (Cp * RS);
+    const float v = c < C ? w[((size_t)k * RS + t) * C + c] : 0.f;
+    const uint16_t h = gm::Elem<uint16_t>::f2bf(v);
+    wb[i] = h;
+    if (wt) wt[((size_t)c * RS + t) * K + k] = h;
+}
+
+extern "C" int gm_conv_weight_prep_bf16(const float* w, int K, int RS, int C, int Cp, void* wb, void* wt,
+                                        void* stream) {
+    GM_REQUIRE(w && wb && K > 0 && RS > 0 && C > 0 && Cp >= C, "weight prep: bad args");
+    const int n = K * RS * Cp;
+    k_weight_prep<<<(n + 255) / 256, 256, 0, gm::as_stream(stream)>>>(w, K, RS, C, Cp, (uint16_t*)wb,
+                                                                       (uint16_t*)wt);
+    return gm::check_launch("k_weight_prep");
 }

@@ -140,6 +140,20 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a) {
     }
 }
 
+// stage 1 (many splits): part2[g][i] = sum of splits 8g..8g+7 (fixed order), float4 lanes,
+// grid (slab/1024, groups): parallel over splits so the reduce is bandwidth-, not latency-bound
+__global__ __launch_bounds__(256) void k_wgrad_sum8(const float* part, int splits, size_t slab, float* part2) {
+    const size_t i4 = ((size_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (i4 >= slab) return;
+    const int g = blockIdx.y, s0 = g * 8, s1 = min(splits, s0 + 8);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int s = s0; s < s1; ++s) {
+        const float4 v = *(const float4*)(part + (size_t)s * slab + i4);
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    *(float4*)(part2 + (size_t)g * slab + i4) = acc;
+}
+
 // dw = sum over splits (fixed order); also the [K][T][Cpad] -> [K][T][Creal] crop
 __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* part, int splits, int Kc, int T, int Cp,
                                                       int Cr, float* dw) {
@@ -183,7 +197,9 @@ extern "C" size_t gm_conv2d_wgrad_scratch(const gm_conv_desc* d) {
     if (!d) return 0;
     int P, Q, tk, tn, sp, sps;
     plan(d, P, Q, tk, tn, sp, sps);
-    return (size_t)sp * d->K * d->R * d->S * d->C * sizeof(float);
+    const size_t slab = (size_t)d->K * d->R * d->S * d->C;
+    const int groups = sp > 8 ? (sp + 7) / 8 : 0;
+    return (size_t)(sp + groups) * slab * sizeof(float);
 }
 
 extern "C" int gm_conv2d_wgrad_bf16(const gm_conv_desc* d, const void* dy, const void* x, float* dw, int c_real,
@@ -216,6 +232,19 @@ extern "C" int gm_conv2d_wgrad_bf16(const gm_conv_desc* d, const void* dy, const
     const size_t n = (size_t)d->K * a.T * c_real;
     int g = (int)((n + 255) / 256);
     if (g > 4096) g = 4096;
-    k_wgrad_reduce<<<g, 256, 0, st>>>(a.part, a.splits, d->K, a.T, d->C, c_real, dw);
+    const size_t slab = (size_t)d->K * a.T * d->C;
+    const float* src = a.part;
+    int nsrc = a.splits;
+    if (a.splits > 8) {
+        const int groups = (a.splits + 7) / 8;
+        float* part2 = a.part + (size_t)a.splits * slab;
+        dim3 g1((unsigned)((slab / 4 + 255) / 256), groups);
+        k_wgrad_sum8<<<g1, 256, 0, st>>>(a.part, a.splits, slab, part2);
+        rc = check_launch("k_wgrad_sum8");
+        if (rc) return rc;
+        src = part2;
+        nsrc = groups;
+    }
+    k_wgrad_reduce<<<g, 256, 0, st>>>(src, nsrc, d->K, a.T, d->C, c_real, dw);
     return check_launch("k_wgrad_reduce");
 }

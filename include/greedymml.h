@@ -179,6 +179,9 @@ typedef struct gm_conv_desc {
 int gm_conv2d_fwd_bf16(const gm_conv_desc* d, const void* x, const void* w, void* y, void* stream);
 int gm_conv2d_dgrad_bf16(const gm_conv_desc* d, const void* dy, const void* wt, void* dx, void* stream);
 int gm_conv_weight_transpose_bf16(const void* w, void* wt, int K, int RS, int C, void* stream);
+/* fp32 KRSC master weight -> bf16 [K][RS][Cp] (zero-padded channels) and, if wt != NULL,
+ * the transposed bf16 [Cp][RS][K] for dgrad, in one pass */
+int gm_conv_weight_prep_bf16(const float* w, int K, int RS, int C, int Cp, void* wb, void* wt, void* stream);
 /* dw is fp32 [K][R][S][c_real]: the first c_real of the C (padded) input channels */
 size_t gm_conv2d_wgrad_scratch(const gm_conv_desc* d);
 int gm_conv2d_wgrad_bf16(const gm_conv_desc* d, const void* dy, const void* x, float* dw, int c_real,
