@@ -54,7 +54,7 @@ struct ConvArgs {
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
-template <int BM, int BN>
+template <int BM, int BN, bool UT>
 __global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
     constexpr int BK = 64;
     constexpr int AR = BM / 32;       // A rows per thread
@@ -89,46 +89,67 @@ __global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
     const int wm = wave >> 1, wn = wave & 1;
     const int lchunk = t & 7, lrow = t >> 3;   // loader: 8 threads per 128-B row
 
-    // per-thread A row geometry
-    int a_base[AR], a_h[AR], a_w[AR];
+    // per-thread A row geometry: pixel pointer at tap offset (0,0) + the row's (h, w)
+    const uint16_t* a_ptr[AR];
+    int a_h[AR], a_w[AR];
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
         const int m = m0 + lrow + 32 * i;
         if (m < M) {
             const int b = m / PQ, pq = m - b * PQ;
             const int p = pq / cl.Q, q = pq - p * cl.Q;
-            a_base[i] = b * a.Hi * a.Wi;
             a_h[i] = p * a.sA;
             a_w[i] = q * a.sA;
+            a_ptr[i] = a.in + ((size_t)((b * a.Hi + a_h[i]) * a.Wi + a_w[i]) << a.logC);
         } else {
-            a_base[i] = 0;
             a_h[i] = -(1 << 28);  // never valid
             a_w[i] = 0;
+            a_ptr[i] = a.in;
         }
+    }
+    // per-thread B (weight) row pointers
+    const uint16_t* b_ptr[BR];
+    bool b_ok[BR];
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+        const int n = n0 + lrow + 32 * i;
+        b_ok[i] = n < a.Nout;
+        b_ptr[i] = a.wt + (size_t)(b_ok[i] ? n : 0) * a.T * a.C + lchunk * 8;
     }
 
     uint4 ra[AR], rb[BR];
+    // UT (C >= 64): a 64-wide K-tile lies inside one tap, so the tap decode and every
+    // offset below are wave-uniform (SALU); only the per-row bounds check is VALU.
     auto load_tile = [&](int kt) {
-        const int k = kt * BK + lchunk * 8;
-        const bool kin = k < Ktot;
-        const int tap = kin ? (k >> a.logC) : 0;
-        const int c = k & (a.C - 1);
-        const int te = tapt[tap];
+        int tap, c, kin;
+        if constexpr (UT) {
+            const int k = kt * BK;
+            tap = __builtin_amdgcn_readfirstlane(k >> a.logC);
+            c = k & (a.C - 1);
+            kin = 1;
+        } else {
+            const int k = kt * BK + lchunk * 8;
+            kin = k < Ktot;
+            tap = kin ? (k >> a.logC) : 0;
+            c = (k & (a.C - 1)) - lchunk * 8;
+        }
+        int te = tapt[tap];
+        if constexpr (UT) te = __builtin_amdgcn_readfirstlane(te);
         const int tw = te & 0xff, dh = ((te >> 8) & 0xff) - 128, dw = ((te >> 16) & 0xff) - 128;
+        const int toff = ((dh * a.Wi + dw) << a.logC) + c + lchunk * 8;
+        const int woff = tw * a.C + c;
 #pragma unroll
         for (int i = 0; i < AR; ++i) {
             const int hi = a_h[i] + dh, wi = a_w[i] + dw;
             uint4 v = make_uint4(0, 0, 0, 0);
             if (kin && (unsigned)hi < (unsigned)a.Hi && (unsigned)wi < (unsigned)a.Wi)
-                v = *(const uint4*)(a.in + ((size_t)(a_base[i] + hi * a.Wi + wi) << a.logC) + c);
+                v = *(const uint4*)(a_ptr[i] + toff);
             ra[i] = v;
         }
 #pragma unroll
         for (int i = 0; i < BR; ++i) {
-            const int n = n0 + lrow + 32 * i;
             uint4 v = make_uint4(0, 0, 0, 0);
-            if (kin && n < a.Nout)
-                v = *(const uint4*)(a.wt + ((size_t)n * a.T + tw) * a.C + c);
+            if (kin && b_ok[i]) v = *(const uint4*)(b_ptr[i] + woff);
             rb[i] = v;
         }
     };
@@ -251,11 +272,16 @@ static int launch_igemm(ConvArgs& a, hipStream_t st) {
     const size_t lds = (size_t)2 * (BM + BN) * 128 + kMaxTap * 4 + 12;
     static bool attr_set = false;  // idempotent, safe to race
     if (!attr_set) {
-        hipFuncSetAttribute((const void*)k_conv_igemm<BM, BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        hipFuncSetAttribute((const void*)k_conv_igemm<BM, BN, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+        hipFuncSetAttribute((const void*)k_conv_igemm<BM, BN, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
         attr_set = true;
     }
-    k_conv_igemm<BM, BN><<<tiles, 256, lds, st>>>(a);
+    if (a.C >= 64)
+        k_conv_igemm<BM, BN, true><<<tiles, 256, lds, st>>>(a);
+    else
+        k_conv_igemm<BM, BN, false><<<tiles, 256, lds, st>>>(a);
     return check_launch("k_conv_igemm");
 }
 

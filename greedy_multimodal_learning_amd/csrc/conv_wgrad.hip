@@ -33,6 +33,7 @@ struct WgradArgs {
     float* part;                // [splits][Kc][T*C]
     int N, H, W, C, logC, Kc, T, P, Q, st;
     int tiles_k, tiles_n, splits, steps_per_split;  // steps of 64 pixels
+    FastDiv fd_pq, fd_q;        // pixel -> (b, p, q) without integer division
     signed char dh[kWTap], dw[kWTap];
 };
 
@@ -81,8 +82,8 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a) {
             uint4 va = make_uint4(0, 0, 0, 0), vb = make_uint4(0, 0, 0, 0);
             if (m < M) {
                 if (acol_ok) va = *(const uint4*)(a.dy + (size_t)m * a.Kc + k0 + lchunk * 8);
-                const int b = m / PQ, pq = m - b * PQ;
-                const int p = pq / a.Q, q = pq - p * a.Q;
+                const int b = (int)a.fd_pq.div((uint32_t)m), pq = m - b * PQ;
+                const int p = (int)a.fd_q.div((uint32_t)pq), q = pq - p * a.Q;
                 const int hi = p * a.st + bdh, wi = q * a.st + bdw;
                 if (bcol_ok && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W)
                     vb = *(const uint4*)(a.x + ((size_t)((b * a.H + hi) * a.W + wi) << a.logC) + bc);
@@ -219,6 +220,8 @@ extern "C" int gm_conv2d_wgrad_bf16(const gm_conv_desc* d, const void* dy, const
     a.part = (float*)scratch;
     a.N = d->N; a.H = d->H; a.W = d->W; a.C = d->C; a.logC = ilog2w(d->C);
     a.Kc = d->K; a.T = d->R * d->S; a.st = d->stride;
+    a.fd_pq = FastDiv((uint32_t)(a.P * a.Q));
+    a.fd_q = FastDiv((uint32_t)a.Q);
     for (int r = 0; r < d->R; ++r)
         for (int s = 0; s < d->S; ++s) {
             a.dh[r * d->S + s] = (signed char)(r - d->pad);
