@@ -117,10 +117,9 @@ __global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
         b_ptr[i] = a.wt + (size_t)(b_ok[i] ? n : 0) * a.T * a.C + lchunk * 8;
     }
 
-    uint4 ra[AR], rb[BR];
     // UT (C >= 64): a 64-wide K-tile lies inside one tap, so the tap decode and every
     // offset below are wave-uniform (SALU); only the per-row bounds check is VALU.
-    auto load_tile = [&](int kt) {
+    auto load_tile = [&](int kt, uint4 (&ra)[AR], uint4 (&rb)[BR]) {
         int tap, c, kin;
         if constexpr (UT) {
             const int k = kt * BK;
@@ -153,7 +152,7 @@ __global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
             rb[i] = v;
         }
     };
-    auto store_tile = [&](int buf) {
+    auto store_tile = [&](int buf, const uint4 (&ra)[AR], const uint4 (&rb)[BR]) {
 #pragma unroll
         for (int i = 0; i < AR; ++i) {
             const int row = lrow + 32 * i;
@@ -174,15 +173,8 @@ __global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    if (nk > 0) {
-        load_tile(0);
-        store_tile(0);
-    }
-    __syncthreads();
     const int fr = lane & 31, fh = lane >> 5;
-    for (int kt = 0; kt < nk; ++kt) {
-        const int buf = kt & 1;
-        if (kt + 1 < nk) load_tile(kt + 1);
+    auto compute = [&](int buf) {
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
             const int chunk = ks * 2 + fh;
@@ -205,7 +197,25 @@ __global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
                     // up holding 4 consecutive output channels of ONE pixel per register group
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
         }
-        if (kt + 1 < nk) store_tile(buf ^ 1);
+    };
+    // 3-deep pipeline: two register sets (tiles kt+1, kt+2 in flight) + two LDS buffers;
+    // a tile's loads have a whole iteration of compute before they must land.
+    uint4 ra0[AR], rb0[BR], ra1[AR], rb1[BR];
+    if (nk > 0) {
+        load_tile(0, ra0, rb0);
+        store_tile(0, ra0, rb0);
+    }
+    if (nk > 1) load_tile(1, ra1, rb1);
+    __syncthreads();
+    for (int kt = 0; kt < nk; kt += 2) {
+        if (kt + 2 < nk) load_tile(kt + 2, ra0, rb0);
+        compute(0);
+        if (kt + 1 < nk) store_tile(1, ra1, rb1);
+        __syncthreads();
+        if (kt + 1 >= nk) break;
+        if (kt + 3 < nk) load_tile(kt + 3, ra1, rb1);
+        compute(1);
+        if (kt + 2 < nk) store_tile(0, ra0, rb0);
         __syncthreads();
     }
 
