@@ -13,11 +13,12 @@
 //
 // GEMM view: M = B*P*Q output pixels, N = output channels, K = ntap*C (c fastest).
 // Tiles BM x BN x 64; 256 threads = 2x2 waves, each wave (BM/2)x(BN/2) built from
-// v_mfma_f32_32x32x16_bf16 tiles; operands staged global -> registers -> LDS
-// (double-buffered, next tile's loads issued before this tile's MFMAs), LDS rows of
-// 128 B XOR-swizzled by ((row>>1)&7) so the ds_read_b128 fragment reads are
-// conflict-free; fp32 accumulation; epilogue stages the bf16 tile through LDS and
-// writes whole 16-B chunks of NHWC rows.  Out-of-range taps read zeros.
+// v_mfma_f32_32x32x16_bf16 tiles; operands staged global -> LDS by LDS-DMA
+// (global_load_lds_dwordx4; double-buffered, next tile's DMA under this tile's MFMAs),
+// LDS rows of 128 B XOR-swizzled by ((row>>1)&7) (applied on the DMA source address)
+// so the ds_read_b128 fragment reads are conflict-free; fp32 accumulation; weights are
+// the MFMA A operand so each lane holds 4 consecutive output channels of one pixel and
+// the epilogue writes 8-B NHWC chunks directly.  Out-of-range taps read zeros.
 #include <cstring>
 
 #include "gm_common.h"
@@ -54,6 +55,8 @@ struct ConvArgs {
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
+__device__ __attribute__((aligned(16))) const uint4 g_zero16[1] = {{0u, 0u, 0u, 0u}};
+
 template <int BM, int BN, bool UT>
 __global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
     constexpr int BK = 64;
@@ -87,81 +90,91 @@ __global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
             tapt[i] = (int)cl.tw[i] | ((int)(cl.dh[i] + 128) << 8) | ((int)(cl.dw[i] + 128) << 16);
     __syncthreads();
     const int wm = wave >> 1, wn = wave & 1;
-    const int lchunk = t & 7, lrow = t >> 3;   // loader: 8 threads per 128-B row
+    const int slot = lane & 7;                  // 16-B LDS slot this lane's DMA fills
 
-    // per-thread A row geometry: pixel pointer at tap offset (0,0) + the row's (h, w)
+    // Staging is LDS-DMA (global_load_lds_dwordx4): a wave instruction writes 64 x 16 B
+    // = 8 rows x 128 B linearly, so the XOR swizzle moves to the SOURCE: the lane that
+    // fills slot s of row r loads global chunk s ^ f(r).  Zero taps (padding) read a
+    // 16-B zero block of the code object.
     const uint16_t* a_ptr[AR];
-    int a_h[AR], a_w[AR];
+    int a_h[AR], a_w[AR], a_gc[AR];
 #pragma unroll
-    for (int i = 0; i < AR; ++i) {
-        const int m = m0 + lrow + 32 * i;
+    for (int j = 0; j < AR; ++j) {
+        const int row = (wave * AR + j) * 8 + (lane >> 3);
+        const int m = m0 + row;
+        a_gc[j] = slot ^ ((row >> 1) & 7);
         if (m < M) {
             const int b = m / PQ, pq = m - b * PQ;
             const int p = pq / cl.Q, q = pq - p * cl.Q;
-            a_h[i] = p * a.sA;
-            a_w[i] = q * a.sA;
-            a_ptr[i] = a.in + ((size_t)((b * a.Hi + a_h[i]) * a.Wi + a_w[i]) << a.logC);
+            a_h[j] = p * a.sA;
+            a_w[j] = q * a.sA;
+            a_ptr[j] = a.in + ((size_t)((b * a.Hi + a_h[j]) * a.Wi + a_w[j]) << a.logC);
         } else {
-            a_h[i] = -(1 << 28);  // never valid
-            a_w[i] = 0;
-            a_ptr[i] = a.in;
+            a_h[j] = -(1 << 28);  // never valid
+            a_w[j] = 0;
+            a_ptr[j] = a.in;
         }
     }
-    // per-thread B (weight) row pointers
     const uint16_t* b_ptr[BR];
     bool b_ok[BR];
+    int b_gc[BR];
 #pragma unroll
-    for (int i = 0; i < BR; ++i) {
-        const int n = n0 + lrow + 32 * i;
-        b_ok[i] = n < a.Nout;
-        b_ptr[i] = a.wt + (size_t)(b_ok[i] ? n : 0) * a.T * a.C + lchunk * 8;
+    for (int j = 0; j < BR; ++j) {
+        const int row = (wave * BR + j) * 8 + (lane >> 3);
+        const int n = n0 + row;
+        b_gc[j] = slot ^ ((row >> 1) & 7);
+        b_ok[j] = n < a.Nout;
+        b_ptr[j] = a.wt + (size_t)(b_ok[j] ? n : 0) * a.T * a.C;
     }
-
-    // UT (C >= 64): a 64-wide K-tile lies inside one tap, so the tap decode and every
-    // offset below are wave-uniform (SALU); only the per-row bounds check is VALU.
-    auto load_tile = [&](int kt, uint4 (&ra)[AR], uint4 (&rb)[BR]) {
-        int tap, c, kin;
-        if constexpr (UT) {
-            const int k = kt * BK;
-            tap = __builtin_amdgcn_readfirstlane(k >> a.logC);
-            c = k & (a.C - 1);
-            kin = 1;
-        } else {
-            const int k = kt * BK + lchunk * 8;
-            kin = k < Ktot;
-            tap = kin ? (k >> a.logC) : 0;
-            c = (k & (a.C - 1)) - lchunk * 8;
-        }
-        int te = tapt[tap];
-        if constexpr (UT) te = __builtin_amdgcn_readfirstlane(te);
-        const int tw = te & 0xff, dh = ((te >> 8) & 0xff) - 128, dw = ((te >> 16) & 0xff) - 128;
-        const int toff = ((dh * a.Wi + dw) << a.logC) + c + lchunk * 8;
-        const int woff = tw * a.C + c;
+    typedef __attribute__((address_space(1))) const void* gptr_t;
+    typedef __attribute__((address_space(3))) void* lptr_t;
+    auto issue = [&](int kt, int buf) {
 #pragma unroll
-        for (int i = 0; i < AR; ++i) {
-            const int hi = a_h[i] + dh, wi = a_w[i] + dw;
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (kin && (unsigned)hi < (unsigned)a.Hi && (unsigned)wi < (unsigned)a.Wi)
-                v = *(const uint4*)(a_ptr[i] + toff);
-            ra[i] = v;
-        }
-#pragma unroll
-        for (int i = 0; i < BR; ++i) {
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (kin && b_ok[i]) v = *(const uint4*)(b_ptr[i] + woff);
-            rb[i] = v;
-        }
-    };
-    auto store_tile = [&](int buf, const uint4 (&ra)[AR], const uint4 (&rb)[BR]) {
-#pragma unroll
-        for (int i = 0; i < AR; ++i) {
-            const int row = lrow + 32 * i;
-            As[(buf * BM + row) * 8 + swz(row, lchunk)] = ra[i];
+        for (int j = 0; j < AR; ++j) {
+            int tap, c;
+            bool kin;
+            if constexpr (UT) {
+                const int k = kt * BK;
+                tap = __builtin_amdgcn_readfirstlane(k >> a.logC);
+                c = (k & (a.C - 1)) + a_gc[j] * 8;
+                kin = true;
+            } else {
+                const int k = kt * BK + a_gc[j] * 8;
+                kin = k < Ktot;
+                tap = kin ? (k >> a.logC) : 0;
+                c = k & (a.C - 1);
+            }
+            int te = tapt[tap];
+            if constexpr (UT) te = __builtin_amdgcn_readfirstlane(te);
+            const int dh = ((te >> 8) & 0xff) - 128, dw = ((te >> 16) & 0xff) - 128;
+            const int hi = a_h[j] + dh, wi = a_w[j] + dw;
+            const bool ok = kin && (unsigned)hi < (unsigned)a.Hi && (unsigned)wi < (unsigned)a.Wi;
+            const void* src = ok ? (const void*)(a_ptr[j] + (((dh * a.Wi + dw) << a.logC) + c))
+                                 : (const void*)g_zero16;
+            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(As + (buf * BM + (wave * AR + j) * 8) * 8),
+                                             16, 0, 0);
         }
 #pragma unroll
-        for (int i = 0; i < BR; ++i) {
-            const int row = lrow + 32 * i;
-            Bs[(buf * BN + row) * 8 + swz(row, lchunk)] = rb[i];
+        for (int j = 0; j < BR; ++j) {
+            int tap, c;
+            bool kin;
+            if constexpr (UT) {
+                const int k = kt * BK;
+                tap = __builtin_amdgcn_readfirstlane(k >> a.logC);
+                c = (k & (a.C - 1)) + b_gc[j] * 8;
+                kin = true;
+            } else {
+                const int k = kt * BK + b_gc[j] * 8;
+                kin = k < Ktot;
+                tap = kin ? (k >> a.logC) : 0;
+                c = k & (a.C - 1);
+            }
+            int te = tapt[tap];
+            if constexpr (UT) te = __builtin_amdgcn_readfirstlane(te);
+            const int tw = te & 0xff;
+            const void* src = (kin && b_ok[j]) ? (const void*)(b_ptr[j] + tw * a.C + c) : (const void*)g_zero16;
+            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(Bs + (buf * BN + (wave * BR + j) * 8) * 8),
+                                             16, 0, 0);
         }
     };
 
@@ -198,24 +211,14 @@ __global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
         }
     };
-    // 3-deep pipeline: two register sets (tiles kt+1, kt+2 in flight) + two LDS buffers;
-    // a tile's loads have a whole iteration of compute before they must land.
-    uint4 ra0[AR], rb0[BR], ra1[AR], rb1[BR];
-    if (nk > 0) {
-        load_tile(0, ra0, rb0);
-        store_tile(0, ra0, rb0);
-    }
-    if (nk > 1) load_tile(1, ra1, rb1);
+    // 2 LDS buffers: the DMA of tile kt+1 runs under the MFMAs of tile kt; the barrier
+    // at the end of each step (vmcnt(0) + s_barrier) publishes it.
+    if (nk > 0) issue(0, 0);
     __syncthreads();
-    for (int kt = 0; kt < nk; kt += 2) {
-        if (kt + 2 < nk) load_tile(kt + 2, ra0, rb0);
-        compute(0);
-        if (kt + 1 < nk) store_tile(1, ra1, rb1);
-        __syncthreads();
-        if (kt + 1 >= nk) break;
-        if (kt + 3 < nk) load_tile(kt + 3, ra1, rb1);
-        compute(1);
-        if (kt + 2 < nk) store_tile(0, ra0, rb0);
+    for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+        if (kt + 1 < nk) issue(kt + 1, buf ^ 1);
+        compute(buf);
         __syncthreads();
     }
 
