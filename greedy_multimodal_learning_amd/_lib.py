@@ -125,3 +125,25 @@ EXPORTS.update({
     "gm_conv2d_wgrad_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_size_t,
                                      c_void_p]),
 })
+
+
+class BnFwd(ctypes.Structure):
+    _fields_ = [("M", ctypes.c_longlong), ("C", c_int), ("relu", c_int), ("x", c_void_p),
+                ("residual", c_void_p), ("y", c_void_p), ("gamma", c_void_p), ("beta", c_void_p),
+                ("running_mean", c_void_p), ("running_var", c_void_p), ("momentum", c_float),
+                ("eps", c_float), ("save_mean", c_void_p), ("save_invstd", c_void_p)]
+
+
+class BnBwd(ctypes.Structure):
+    _fields_ = [("M", ctypes.c_longlong), ("C", c_int), ("relu", c_int), ("dy", c_void_p),
+                ("y", c_void_p), ("x", c_void_p), ("gamma", c_void_p), ("save_mean", c_void_p),
+                ("save_invstd", c_void_p), ("dx", c_void_p), ("dres", c_void_p), ("dgamma", c_void_p),
+                ("dbeta", c_void_p), ("accumulate", c_int), ("pad", c_int)]
+
+
+EXPORTS.update({
+    "gm_bn_scratch": (c_size_t, [ctypes.c_longlong, c_int]),
+    "gm_bn_fwd_train_bf16": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
+    "gm_bn_fwd_infer_bf16": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
+    "gm_bn_bwd_bf16": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
+})

@@ -187,6 +187,59 @@ size_t gm_conv2d_wgrad_scratch(const gm_conv_desc* d);
 int gm_conv2d_wgrad_bf16(const gm_conv_desc* d, const void* dy, const void* x, float* dw, int c_real,
                          void* scratch, size_t scratch_bytes, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * BatchNorm2d (torchvision ResNet trunk, reference src/model.py:65-106 through
+ * torchvision.models.resnet18), NHWC bf16 activations x[M][C] (M = N*H*W), fp32
+ * affine parameters and statistics, fused with the residual add and ReLU that
+ * follow it in the blocks:
+ *   y = relu?( (x - mean) * invstd * gamma + beta  (+ residual) )
+ * train : batch statistics (biased variance for the normalisation; running_var
+ *         gets the unbiased one, momentum update - F.batch_norm semantics);
+ *         save_mean/save_invstd are written for the backward;
+ * infer : running statistics (module.eval()).
+ * backward: dz = dy * (y > 0) if relu else dy;  dres = dz (if non-NULL);
+ *         dx = BN backward(dz); dgamma/dbeta written (or added if accumulate).
+ * C must be a power of two in [8, 2048].  scratch >= gm_bn_scratch(M, C) bytes,
+ * ZEROED ONCE before first use; each call leaves its ticket word at zero again.
+ * Calls sharing one scratch buffer must be stream-ordered.
+ * ------------------------------------------------------------------------- */
+typedef struct gm_bn_fwd {
+    long long M;
+    int C, relu;
+    const void* x;
+    const void* residual;
+    void* y;
+    const float* gamma;
+    const float* beta;
+    float* running_mean;
+    float* running_var;
+    float momentum, eps;
+    float* save_mean;
+    float* save_invstd;
+} gm_bn_fwd;
+
+typedef struct gm_bn_bwd {
+    long long M;
+    int C, relu;
+    const void* dy;
+    const void* y;
+    const void* x;
+    const float* gamma;
+    const float* save_mean;
+    const float* save_invstd;
+    void* dx;
+    void* dres;
+    float* dgamma;
+    float* dbeta;
+    int accumulate;
+    int pad;
+} gm_bn_bwd;
+
+size_t gm_bn_scratch(long long M, int C);
+int gm_bn_fwd_train_bf16(const gm_bn_fwd* p, void* scratch, size_t scratch_bytes, void* stream);
+int gm_bn_fwd_infer_bf16(const gm_bn_fwd* p, void* scratch, size_t scratch_bytes, void* stream);
+int gm_bn_bwd_bf16(const gm_bn_bwd* p, void* scratch, size_t scratch_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
