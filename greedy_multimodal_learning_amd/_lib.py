@@ -122,8 +122,8 @@ EXPORTS.update({
     "gm_conv_weight_transpose_bf16": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "gm_conv2d_wgrad_scratch": (c_size_t, [c_void_p]),
     "gm_conv_weight_prep_bf16": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
-    "gm_conv2d_wgrad_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_size_t,
-                                     c_void_p]),
+    "gm_conv2d_wgrad_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
+                                     c_size_t, c_void_p]),
 })
 
 
@@ -131,7 +131,8 @@ class BnFwd(ctypes.Structure):
     _fields_ = [("M", ctypes.c_longlong), ("C", c_int), ("relu", c_int), ("x", c_void_p),
                 ("residual", c_void_p), ("y", c_void_p), ("gamma", c_void_p), ("beta", c_void_p),
                 ("running_mean", c_void_p), ("running_var", c_void_p), ("momentum", c_float),
-                ("eps", c_float), ("save_mean", c_void_p), ("save_invstd", c_void_p)]
+                ("eps", c_float), ("save_mean", c_void_p), ("save_invstd", c_void_p),
+                ("num_batches_tracked", c_void_p)]
 
 
 class BnBwd(ctypes.Structure):
@@ -146,4 +147,15 @@ EXPORTS.update({
     "gm_bn_fwd_train_bf16": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "gm_bn_fwd_infer_bf16": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "gm_bn_bwd_bf16": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
+})
+
+
+class PoolDesc(ctypes.Structure):
+    _fields_ = [("N", c_int), ("H", c_int), ("W", c_int), ("C", c_int), ("k", c_int), ("stride", c_int),
+                ("pad", c_int)]
+
+
+EXPORTS.update({
+    "gm_maxpool2d_fwd_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "gm_maxpool2d_bwd_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
 })

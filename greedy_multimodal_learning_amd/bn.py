@@ -1,0 +1,174 @@
+"""BatchNorm2d (+ residual add + ReLU) of the ResNet trunk on the HIP kernels.
+
+`GMBatchNorm2d` is an `nn.BatchNorm2d` (same parameters, buffers, names, init,
+state_dict) whose forward takes two optional fusions used by the ResNet blocks:
+
+    bn(x)                         == BatchNorm2d(x)
+    bn(x, relu=True)              == relu(BatchNorm2d(x))
+    bn(x, residual=r, relu=True)  == relu(BatchNorm2d(x) + r)
+
+For bf16 channels_last CUDA inputs in training mode it runs
+`gm_bn_fwd_train_bf16` / `gm_bn_bwd_bf16` (two kernels each way, batch
+statistics, running-stat and num_batches_tracked updates inside the kernel);
+in eval mode without autograd `gm_bn_fwd_infer_bf16`.  Other inputs (the fp32
+parity mode, CPU) use PyTorch's batch_norm.  Reference: torchvision ResNet
+BasicBlock/Bottleneck as used by src/model.py:53-56,65-106.
+"""
+import ctypes
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib as L
+from .gradsink import sink_done, sink_target
+
+CL = torch.channels_last
+
+_scratch = {}
+
+
+def _get_scratch(device, M, C):
+    """Per-device BN scratch (ticket word + coefficients + partials), zeroed once
+    at allocation; the kernels leave the ticket at zero."""
+    need = L.load().gm_bn_scratch(M, C)
+    key = device.index if device.index is not None else torch.cuda.current_device()
+    buf = _scratch.get(key)
+    if buf is None or buf.numel() < need:
+        size = max(need, 1 << 20) if buf is None else max(need, 2 * buf.numel())
+        buf = torch.zeros(size, device=device, dtype=torch.uint8)
+        _scratch[key] = buf
+    return buf
+
+
+def _nhwc(t):
+    return t if t.is_contiguous(memory_format=CL) else t.contiguous(memory_format=CL)
+
+
+def _check_shape(x, C):
+    if x.dim() != 4 or x.shape[1] != C:
+        raise ValueError(f"expected [N,{C},H,W], got {tuple(x.shape)}")
+    if C < 8 or C > 2048 or C & (C - 1):
+        raise ValueError(f"HIP batchnorm needs C a power of two in [8, 2048], got {C}")
+
+
+def bn_fwd_train(x, weight, bias, running_mean, running_var, nbt, momentum, eps, relu, residual):
+    lib = L.load()
+    N, C, H, W = x.shape
+    _check_shape(x, C)
+    M = N * H * W
+    x = _nhwc(x)
+    if residual is not None:
+        residual = _nhwc(residual.to(torch.bfloat16))
+    y = torch.empty_like(x, memory_format=CL)
+    sm = torch.empty(C, device=x.device, dtype=torch.float32)
+    si = torch.empty(C, device=x.device, dtype=torch.float32)
+    buf = _get_scratch(x.device, M, C)
+    p = L.BnFwd(M, C, int(relu), x.data_ptr(), L.ptr(residual), y.data_ptr(), weight.data_ptr(),
+                bias.data_ptr(), L.ptr(running_mean), L.ptr(running_var), float(momentum), float(eps),
+                sm.data_ptr(), si.data_ptr(), L.ptr(nbt))
+    L.check(lib.gm_bn_fwd_train_bf16(ctypes.byref(p), buf.data_ptr(), buf.numel(), L.stream_of(x.device)),
+            "gm_bn_fwd_train_bf16")
+    return y, sm, si
+
+
+def bn_fwd_infer(x, weight, bias, running_mean, running_var, eps, relu, residual):
+    lib = L.load()
+    N, C, H, W = x.shape
+    _check_shape(x, C)
+    M = N * H * W
+    x = _nhwc(x)
+    if residual is not None:
+        residual = _nhwc(residual.to(torch.bfloat16))
+    y = torch.empty_like(x, memory_format=CL)
+    buf = _get_scratch(x.device, M, C)
+    p = L.BnFwd(M, C, int(relu), x.data_ptr(), L.ptr(residual), y.data_ptr(), weight.data_ptr(),
+                bias.data_ptr(), running_mean.data_ptr(), running_var.data_ptr(), 0.0, float(eps), 0, 0, 0)
+    L.check(lib.gm_bn_fwd_infer_bf16(ctypes.byref(p), buf.data_ptr(), buf.numel(), L.stream_of(x.device)),
+            "gm_bn_fwd_infer_bf16")
+    return y
+
+
+def bn_bwd(dy, y, x, weight, sm, si, relu, want_dres, dgamma, dbeta, accumulate):
+    """Returns (dx, dres); dgamma/dbeta are written (or added) in place."""
+    lib = L.load()
+    N, C, H, W = x.shape
+    M = N * H * W
+    dy = _nhwc(dy.to(torch.bfloat16))
+    dx = torch.empty_like(x, memory_format=CL)
+    dres = torch.empty_like(x, memory_format=CL) if want_dres else None
+    buf = _get_scratch(x.device, M, C)
+    p = L.BnBwd(M, C, int(relu), dy.data_ptr(), L.ptr(y) if relu else 0, x.data_ptr(), weight.data_ptr(),
+                sm.data_ptr(), si.data_ptr(), dx.data_ptr(), L.ptr(dres), dgamma.data_ptr(), dbeta.data_ptr(),
+                int(accumulate), 0)
+    L.check(lib.gm_bn_bwd_bf16(ctypes.byref(p), buf.data_ptr(), buf.numel(), L.stream_of(x.device)),
+            "gm_bn_bwd_bf16")
+    return dx, dres
+
+
+class _BNFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, momentum, eps, relu):
+        xb = _nhwc(x.to(torch.bfloat16))
+        y, sm, si = bn_fwd_train(xb, weight.detach(), bias.detach(), running_mean, running_var, nbt, momentum,
+                                 eps, relu, residual)
+        ctx.save_for_backward(xb, y if relu else None, weight, bias, sm, si)
+        ctx.relu = relu
+        ctx.has_res = residual is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xb, y, weight, bias, sm, si = ctx.saved_tensors
+        C = xb.shape[1]
+        want_w, want_b = ctx.needs_input_grad[1], ctx.needs_input_grad[2]
+        tw = sink_target(weight) if want_w else None
+        tb = sink_target(bias) if want_b else None
+        if tw is not None and tb is not None and tw[1] == tb[1]:
+            dgamma, dbeta, acc = tw[0], tb[0], tw[1]
+            direct = True
+        else:
+            if tw is not None or tb is not None:  # mixed state: undo nothing, fall back to returned grads
+                raise RuntimeError("GMBatchNorm2d: weight and bias must share one gradient sink state")
+            dgamma = torch.empty(C, device=xb.device, dtype=torch.float32)
+            dbeta = torch.empty(C, device=xb.device, dtype=torch.float32)
+            acc, direct = False, False
+        want_dres = ctx.has_res and ctx.needs_input_grad[3]
+        dx, dres = bn_bwd(dy, y, xb, weight.detach(), sm, si, ctx.relu, want_dres, dgamma, dbeta, acc)
+        if direct:
+            sink_done(weight)
+            sink_done(bias)
+            gw = gb = None
+        else:
+            gw = dgamma if want_w else None
+            gb = dbeta if want_b else None
+        dx = dx if ctx.needs_input_grad[0] else None
+        return dx, gw, gb, dres, None, None, None, None, None, None
+
+
+def _use_hip(x):
+    if not x.is_cuda:
+        return False
+    if x.dtype == torch.bfloat16:
+        return True
+    return torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+
+
+class GMBatchNorm2d(nn.BatchNorm2d):
+    """nn.BatchNorm2d with optional fused residual add and ReLU (see module doc)."""
+
+    def forward(self, x, residual=None, relu=False):
+        C = self.num_features
+        hip = (_use_hip(x) and self.affine and x.dim() == 4 and C >= 8 and C <= 2048 and not (C & (C - 1)))
+        if hip and self.training and self.track_running_stats and self.momentum is not None:
+            with torch.autocast("cuda", enabled=False):
+                return _BNFn.apply(x, self.weight, self.bias, residual, self.running_mean, self.running_var,
+                                   self.num_batches_tracked, self.momentum, self.eps, bool(relu))
+        if (hip and not self.training and self.track_running_stats
+                and not (torch.is_grad_enabled() and (x.requires_grad or self.weight.requires_grad))):
+            return bn_fwd_infer(x.to(torch.bfloat16), self.weight, self.bias, self.running_mean, self.running_var,
+                                self.eps, bool(relu), residual)
+        y = super().forward(x)
+        if residual is not None:
+            y = y + residual
+        return F.relu(y) if relu else y

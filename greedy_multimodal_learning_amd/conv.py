@@ -15,6 +15,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib as L
+from .gradsink import sink_done, sink_target
 
 CL = torch.channels_last
 
@@ -70,16 +71,25 @@ def conv_dgrad(dy, w, H, W, stride, pad):
     return dx
 
 
-def conv_wgrad(dy, x, R, S, stride, pad, c_real):
+def conv_wgrad(dy, x, R, S, stride, pad, c_real, out=None, accumulate=False):
+    """fp32 weight gradient [K,c_real,R,S] (channels_last); written into `out`
+    (a KRSC-contiguous gradient buffer, added to if accumulate) when given."""
     lib = L.load()
     N, C, H, W = x.shape
     K = dy.shape[1]
     d = _desc(N, H, W, C, K, R, S, stride, pad)
     need = lib.gm_conv2d_wgrad_scratch(ctypes.byref(d))
     scratch = torch.empty(max(need, 16), device=x.device, dtype=torch.uint8)
-    dw = torch.empty(K, c_real, R, S, device=x.device, dtype=torch.float32, memory_format=CL)
+    if out is None:
+        dw = torch.empty(K, c_real, R, S, device=x.device, dtype=torch.float32, memory_format=CL)
+    else:
+        if (tuple(out.shape) != (K, c_real, R, S) or out.dtype != torch.float32
+                or not out.is_contiguous(memory_format=CL)):
+            raise ValueError("conv_wgrad: out must be fp32 [K,C,R,S] channels_last")
+        dw = out
     L.check(lib.gm_conv2d_wgrad_bf16(ctypes.byref(d), dy.data_ptr(), x.data_ptr(), dw.data_ptr(), c_real,
-                                     scratch.data_ptr(), need, L.stream_of(x.device)), "gm_conv2d_wgrad_bf16")
+                                     int(accumulate), scratch.data_ptr(), need, L.stream_of(x.device)),
+            "gm_conv2d_wgrad_bf16")
     return dw
 
 
@@ -122,13 +132,13 @@ class _ConvFn(torch.autograd.Function):
         need_dx = ctx.needs_input_grad[0]
         wb, wt = weight_prep(weight, Cp, need_dx)
         y = conv_fwd(xb, wb, stride, pad)
-        ctx.save_for_backward(xb, wt)
+        ctx.save_for_backward(xb, wt, weight)
         ctx.meta = (stride, pad, C0, x.shape[2], x.shape[3], weight.shape[2], weight.shape[3])
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        xb, wt = ctx.saved_tensors
+        xb, wt, weight = ctx.saved_tensors
         stride, pad, C0, H, W, R, S = ctx.meta
         gy = _nhwc(gy.to(torch.bfloat16))
         dx = None
@@ -136,7 +146,16 @@ class _ConvFn(torch.autograd.Function):
             dx = conv_dgrad_t(gy, wt, H, W, stride, pad)
             if dx.shape[1] != C0:
                 dx = dx[:, :C0]
-        dw = conv_wgrad(gy, xb, R, S, stride, pad, C0) if ctx.needs_input_grad[1] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            tgt = sink_target(weight)
+            if tgt is not None and tgt[0].is_contiguous(memory_format=CL):
+                conv_wgrad(gy, xb, R, S, stride, pad, C0, out=tgt[0], accumulate=tgt[1])
+                sink_done(weight)
+            else:
+                if tgt is not None:
+                    raise RuntimeError("GMConv2d: in-place gradient buffer must be channels_last")
+                dw = conv_wgrad(gy, xb, R, S, stride, pad, C0)
         return dx, dw, None, None
 
 

@@ -84,6 +84,7 @@ struct ReduceArgs {
     float* dgamma;
     float* dbeta;
     unsigned* counter;
+    long long* nbt;      // num_batches_tracked (fwd, may be null)
     float* coef;         // [4][C]
     float* part;         // [nblk][2C]
 };
@@ -220,6 +221,7 @@ __global__ __launch_bounds__(kT) void k_bn_reduce(ReduceArgs a) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         *a.counter = 0u;  // leave the ticket at zero for the next call
+        if (MODE == FWD && a.nbt) *a.nbt += 1;
     }
     __syncthreads();
 
@@ -401,6 +403,7 @@ extern "C" int gm_bn_fwd_train_bf16(const gm_bn_fwd* p, void* scratch, size_t by
     a.gamma = p->gamma; a.beta = p->beta; a.rmean = p->running_mean; a.rvar = p->running_var;
     a.momentum = p->momentum; a.eps = p->eps;
     a.save_mean = p->save_mean; a.save_invstd = p->save_invstd;
+    a.nbt = p->num_batches_tracked;
     a.counter = reinterpret_cast<unsigned*>(s);
     a.coef = reinterpret_cast<float*>(s + kHdr);
     a.part = a.coef + 4 * p->C;

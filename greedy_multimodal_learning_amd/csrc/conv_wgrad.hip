@@ -157,7 +157,7 @@ __global__ __launch_bounds__(256) void k_wgrad_sum8(const float* part, int split
 
 // dw = sum over splits (fixed order); also the [K][T][Cpad] -> [K][T][Creal] crop
 __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* part, int splits, int Kc, int T, int Cp,
-                                                      int Cr, float* dw) {
+                                                      int Cr, int accumulate, float* dw) {
     const size_t n = (size_t)Kc * T * Cr;
     const size_t slab = (size_t)Kc * T * Cp;
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
@@ -165,7 +165,7 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* part, int spl
         const size_t src = kt * Cp + c;
         float v = 0.f;
         for (int s = 0; s < splits; ++s) v += part[s * slab + src];
-        dw[i] = v;
+        dw[i] = accumulate ? dw[i] + v : v;
     }
 }
 
@@ -204,7 +204,7 @@ extern "C" size_t gm_conv2d_wgrad_scratch(const gm_conv_desc* d) {
 }
 
 extern "C" int gm_conv2d_wgrad_bf16(const gm_conv_desc* d, const void* dy, const void* x, float* dw, int c_real,
-                                    void* scratch, size_t scratch_bytes, void* stream) {
+                                    int accumulate, void* scratch, size_t scratch_bytes, void* stream) {
     GM_REQUIRE(d && dy && x && dw, "conv wgrad: null pointer");
     GM_REQUIRE(d->R * d->S <= kWTap, "conv wgrad: at most %d taps", kWTap);
     GM_REQUIRE(ilog2w(d->C) >= 3, "conv wgrad: C must be a power of two >= 8");
@@ -248,6 +248,6 @@ extern "C" int gm_conv2d_wgrad_bf16(const gm_conv_desc* d, const void* dy, const
         src = part2;
         nsrc = groups;
     }
-    k_wgrad_reduce<<<g, 256, 0, st>>>(src, nsrc, d->K, a.T, d->C, c_real, dw);
+    k_wgrad_reduce<<<g, 256, 0, st>>>(src, nsrc, d->K, a.T, d->C, c_real, accumulate, dw);
     return check_launch("k_wgrad_reduce");
 }

@@ -1,0 +1,167 @@
+// MaxPool2d of the ResNet stem (torchvision: kernel 3, stride 2, padding 1;
+// reference src/model.py:65-106 via torchvision.models.resnet18), NHWC bf16.
+//
+// Forward writes y and a 1-byte window-relative argmax per output element
+// (PyTorch stores an int64 flat index: 8x the bytes).  Tie/NaN rule follows
+// PyTorch's max_pool2d kernels: scan the window row-major and take a value when
+// `v > max || isnan(v)`, starting from -inf at the first in-bounds position.
+// Backward is a gather: each input pixel visits the <= ceil(k/s)^2 windows that
+// cover it and sums the dy of those whose argmax is that pixel (fp32, fixed
+// order), so no atomics and dx is written exactly once.
+#include "gm_common.h"
+
+namespace gm {
+namespace {
+
+struct PoolArgs {
+    int N, H, W, C8;  // C8 = C / 8 (16-byte channel groups)
+    int P, Q, k, s, pad;
+};
+
+__device__ __forceinline__ void unpack8(uint4 u, float* f) {
+    f[0] = bf_lo(u.x); f[1] = bf_hi(u.x); f[2] = bf_lo(u.y); f[3] = bf_hi(u.y);
+    f[4] = bf_lo(u.z); f[5] = bf_hi(u.z); f[6] = bf_lo(u.w); f[7] = bf_hi(u.w);
+}
+
+__global__ __launch_bounds__(256) void k_maxpool_fwd(PoolArgs a, const uint4* __restrict__ x, uint4* __restrict__ y,
+                                                     uint2* __restrict__ idx) {
+    const unsigned total = (unsigned)a.N * a.P * a.Q * a.C8;  // < 2^31 (checked on the host)
+    for (unsigned i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+        const int cg = (int)(i % a.C8);
+        unsigned t = i / a.C8;
+        const int q = (int)(t % a.Q);
+        t /= a.Q;
+        const int p = (int)(t % a.P);
+        const int n = (int)(t / a.P);
+        const int h0 = p * a.s - a.pad, w0 = q * a.s - a.pad;
+        float m[8];
+        uint32_t ix[8];
+        const int hs = h0 < 0 ? 0 : h0, ws = w0 < 0 ? 0 : w0;
+        const uint32_t first = (uint32_t)((hs - h0) * a.k + (ws - w0));
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            m[j] = -__builtin_huge_valf();
+            ix[j] = first;
+        }
+        for (int r = 0; r < a.k; ++r) {
+            const int h = h0 + r;
+            if (h < 0 || h >= a.H) continue;
+            for (int c = 0; c < a.k; ++c) {
+                const int w = w0 + c;
+                if (w < 0 || w >= a.W) continue;
+                float v[8];
+                unpack8(x[(((long long)n * a.H + h) * a.W + w) * a.C8 + cg], v);
+                const uint32_t pos = (uint32_t)(r * a.k + c);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    if (v[j] > m[j] || __builtin_isnan(v[j])) {
+                        m[j] = v[j];
+                        ix[j] = pos;
+                    }
+                }
+            }
+        }
+        // max of bf16 values is a bf16 value: the pack is exact
+        y[i] = make_uint4(pack_bf2(m[0], m[1]), pack_bf2(m[2], m[3]), pack_bf2(m[4], m[5]), pack_bf2(m[6], m[7]));
+        idx[i] = make_uint2(ix[0] | ix[1] << 8 | ix[2] << 16 | ix[3] << 24, ix[4] | ix[5] << 8 | ix[6] << 16 | ix[7] << 24);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_maxpool_bwd(PoolArgs a, const uint4* __restrict__ dy,
+                                                     const uint2* __restrict__ idx, uint4* __restrict__ dx) {
+    const unsigned total = (unsigned)a.N * a.H * a.W * a.C8;
+    for (unsigned i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+        const int cg = (int)(i % a.C8);
+        unsigned t = i / a.C8;
+        const int w = (int)(t % a.W);
+        t /= a.W;
+        const int h = (int)(t % a.H);
+        const int n = (int)(t / a.H);
+        // windows p with p*s - pad <= h <= p*s - pad + k - 1
+        int plo = h + a.pad - a.k + 1;
+        plo = plo <= 0 ? 0 : (plo + a.s - 1) / a.s;
+        int phi = (h + a.pad) / a.s;
+        if (phi > a.P - 1) phi = a.P - 1;
+        int qlo = w + a.pad - a.k + 1;
+        qlo = qlo <= 0 ? 0 : (qlo + a.s - 1) / a.s;
+        int qhi = (w + a.pad) / a.s;
+        if (qhi > a.Q - 1) qhi = a.Q - 1;
+        float g[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] = 0.f;
+        for (int p = plo; p <= phi; ++p) {
+            for (int q = qlo; q <= qhi; ++q) {
+                const long long o = (((long long)n * a.P + p) * a.Q + q) * a.C8 + cg;
+                const uint2 iv = idx[o];
+                const uint32_t pos = (uint32_t)((h - (p * a.s - a.pad)) * a.k + (w - (q * a.s - a.pad)));
+                float d[8];
+                unpack8(dy[o], d);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const uint32_t b = ((j < 4 ? iv.x : iv.y) >> (8 * (j & 3))) & 0xffu;
+                    if (b == pos) g[j] += d[j];
+                }
+            }
+        }
+        dx[i] = make_uint4(pack_bf2(g[0], g[1]), pack_bf2(g[2], g[3]), pack_bf2(g[4], g[5]), pack_bf2(g[6], g[7]));
+    }
+}
+
+int prep(const gm_pool_desc* d, PoolArgs& a, const char* fn) {
+    if (!d) {
+        set_error("%s: null descriptor", fn);
+        return GM_E_ARG;
+    }
+    if (d->N <= 0 || d->H <= 0 || d->W <= 0 || d->C <= 0 || d->C % 8 || d->k < 1 || d->k > 15 || d->stride < 1 ||
+        d->pad < 0 || 2 * d->pad > d->k) {
+        set_error("%s: unsupported N=%d H=%d W=%d C=%d k=%d s=%d pad=%d (C%%8==0, k<=15, pad<=k/2)", fn, d->N, d->H,
+                  d->W, d->C, d->k, d->stride, d->pad);
+        return GM_E_ARG;
+    }
+    a.N = d->N; a.H = d->H; a.W = d->W; a.C8 = d->C / 8;
+    a.k = d->k; a.s = d->stride; a.pad = d->pad;
+    a.P = (d->H + 2 * d->pad - d->k) / d->stride + 1;
+    a.Q = (d->W + 2 * d->pad - d->k) / d->stride + 1;
+    if (a.P <= 0 || a.Q <= 0) {
+        set_error("%s: empty output", fn);
+        return GM_E_ARG;
+    }
+    if ((long long)a.N * a.H * a.W * a.C8 >= (1ll << 31)) {
+        set_error("%s: tensor too large (N*H*W*C/8 >= 2^31)", fn);
+        return GM_E_ARG;
+    }
+    return GM_OK;
+}
+
+inline int grid_for(long long n) {
+    long long g = (n + 255) / 256;
+    if (g > 16384) g = 16384;
+    return (int)(g < 1 ? 1 : g);
+}
+
+}  // namespace
+}  // namespace gm
+
+using namespace gm;
+
+extern "C" int gm_maxpool2d_fwd_bf16(const gm_pool_desc* d, const void* x, void* y, void* idx, void* stream) {
+    PoolArgs a;
+    int rc = prep(d, a, "gm_maxpool2d_fwd_bf16");
+    if (rc) return rc;
+    GM_REQUIRE(x && y && idx, "gm_maxpool2d_fwd_bf16: null pointer");
+    const long long n = (long long)a.N * a.P * a.Q * a.C8;
+    hipLaunchKernelGGL(k_maxpool_fwd, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), a,
+                       static_cast<const uint4*>(x), static_cast<uint4*>(y), static_cast<uint2*>(idx));
+    return check_launch("k_maxpool_fwd");
+}
+
+extern "C" int gm_maxpool2d_bwd_bf16(const gm_pool_desc* d, const void* dy, const void* idx, void* dx, void* stream) {
+    PoolArgs a;
+    int rc = prep(d, a, "gm_maxpool2d_bwd_bf16");
+    if (rc) return rc;
+    GM_REQUIRE(dy && idx && dx, "gm_maxpool2d_bwd_bf16: null pointer");
+    const long long n = (long long)a.N * a.H * a.W * a.C8;
+    hipLaunchKernelGGL(k_maxpool_bwd, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), a,
+                       static_cast<const uint4*>(dy), static_cast<const uint2*>(idx), static_cast<uint4*>(dx));
+    return check_launch("k_maxpool_bwd");
+}

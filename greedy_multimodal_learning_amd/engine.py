@@ -25,6 +25,7 @@ import torch
 import torch.distributed as dist
 
 from .callbacks import GroupNorms
+from .gradsink import GradSink
 from .losses import blend_loss
 
 
@@ -109,6 +110,9 @@ class GradBuckets:
 
     def _on_grad(self, p):
         bi = self.bucket_of[p]
+        if self._pending[bi] == -1:
+            raise RuntimeError("gradient delivered after its bucket was all-reduced "
+                               "(a parameter used twice in one step under data parallelism)")
         self._pending[bi] -= 1
         if self._pending[bi] == 0:
             self._launch(bi)
@@ -156,6 +160,10 @@ class BalancedStep:
                 if hasattr(m, "zero_grads_for_curated"):
                     m.zero_grads_for_curated = True  # every bucket fills every step
             self.buckets = GradBuckets(self.flat, process_group, bucket_mb)
+        # HIP conv/BN backward kernels write their parameter gradients straight into
+        # the flat buffer (no AccumulateGrad add) and fire the bucket hook themselves
+        self.sink = GradSink(self.flat.slices.keys(),
+                             on_ready=self.buckets._on_grad if self.buckets is not None else None)
         self.last_loss = None
         self.step_count = 0
         self.timer = None  # optional (start_event, end_event) list collector for the fused pass
@@ -172,9 +180,13 @@ class BalancedStep:
         self.flat_grad.zero_()
         if self.buckets is not None:
             self.buckets.reset()
-        _, outs, _, _ = self.forward(x)
-        loss = blend_loss([o.float() for o in outs], y)
-        loss.backward()
+        self.sink.begin_step()
+        try:
+            _, outs, _, _ = self.forward(x)
+            loss = blend_loss([o.float() for o in outs], y)
+            loss.backward()
+        finally:
+            self.sink.end_step()
         if self.buckets is not None:
             self.buckets.finish()
         gate = self.gate

@@ -51,7 +51,7 @@ class MMTM_MVCNN(nn.Module):
 
     @staticmethod
     def _stem(net, x):
-        return net.layer1(net.maxpool(net.relu(net.bn1(net.conv1(x)))))
+        return net.layer1(net.maxpool(net.bn1(net.conv1(x), relu=True)))  # relu fused into bn1
 
     def forward(self, x, curation_mode=False, caring_modality=None):
         f0 = self._stem(self.net_view_0, x[:, 0])

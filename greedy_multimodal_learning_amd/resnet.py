@@ -6,12 +6,16 @@ dependency here; this module provides the same architecture and the same
 parameter names (`conv1`, `bn1`, `layer{1..4}.{i}.{conv,bn}{1,2}`,
 `layer{2..4}.0.downsample.{0,1}`, `fc`), so checkpoints and the gating's
 name-based grouping carry over unchanged.  Bottleneck/ResNet-50 serves
-config C5.  Convolutions are `conv.GMConv2d` (bf16 MFMA kernels on HIP).
+config C5.  Convolutions are `conv.GMConv2d` (bf16 MFMA kernels on HIP); batch
+norms are `bn.GMBatchNorm2d`, which take the block's residual add and ReLU as
+fused arguments (`relu` modules are kept for name/structure parity).
 """
 import torch
 import torch.nn as nn
 
+from .bn import GMBatchNorm2d
 from .conv import GMConv2d
+from .pool import GMMaxPool2d
 
 
 def conv3x3(cin, cout, stride=1):
@@ -28,18 +32,17 @@ class BasicBlock(nn.Module):
     def __init__(self, cin, cout, stride=1, downsample=None):
         super().__init__()
         self.conv1 = conv3x3(cin, cout, stride)
-        self.bn1 = nn.BatchNorm2d(cout)
+        self.bn1 = GMBatchNorm2d(cout)
         self.relu = nn.ReLU(inplace=True)
         self.conv2 = conv3x3(cout, cout)
-        self.bn2 = nn.BatchNorm2d(cout)
+        self.bn2 = GMBatchNorm2d(cout)
         self.downsample = downsample
         self.stride = stride
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.bn2(self.conv2(out))
-        return self.relu(out + idt)
+        out = self.bn1(self.conv1(x), relu=True)
+        return self.bn2(self.conv2(out), residual=idt, relu=True)
 
 
 class Bottleneck(nn.Module):
@@ -48,21 +51,20 @@ class Bottleneck(nn.Module):
     def __init__(self, cin, planes, stride=1, downsample=None):
         super().__init__()
         self.conv1 = conv1x1(cin, planes)
-        self.bn1 = nn.BatchNorm2d(planes)
+        self.bn1 = GMBatchNorm2d(planes)
         self.conv2 = conv3x3(planes, planes, stride)
-        self.bn2 = nn.BatchNorm2d(planes)
+        self.bn2 = GMBatchNorm2d(planes)
         self.conv3 = conv1x1(planes, planes * 4)
-        self.bn3 = nn.BatchNorm2d(planes * 4)
+        self.bn3 = GMBatchNorm2d(planes * 4)
         self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample
         self.stride = stride
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.relu(self.bn2(self.conv2(out)))
-        out = self.bn3(self.conv3(out))
-        return self.relu(out + idt)
+        out = self.bn1(self.conv1(x), relu=True)
+        out = self.bn2(self.conv2(out), relu=True)
+        return self.bn3(self.conv3(out), residual=idt, relu=True)
 
 
 class ResNet(nn.Module):
@@ -70,9 +72,9 @@ class ResNet(nn.Module):
         super().__init__()
         self.inplanes = 64
         self.conv1 = GMConv2d(3, 64, 7, stride=2, padding=3, bias=False)
-        self.bn1 = nn.BatchNorm2d(64)
+        self.bn1 = GMBatchNorm2d(64)
         self.relu = nn.ReLU(inplace=True)
-        self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+        self.maxpool = GMMaxPool2d(kernel_size=3, stride=2, padding=1)
         self.layer1 = self._make_layer(block, 64, layers[0])
         self.layer2 = self._make_layer(block, 128, layers[1], stride=2)
         self.layer3 = self._make_layer(block, 256, layers[2], stride=2)
@@ -90,14 +92,14 @@ class ResNet(nn.Module):
         down = None
         if stride != 1 or self.inplanes != planes * block.expansion:
             down = nn.Sequential(conv1x1(self.inplanes, planes * block.expansion, stride),
-                                 nn.BatchNorm2d(planes * block.expansion))
+                                 GMBatchNorm2d(planes * block.expansion))
         layers = [block(self.inplanes, planes, stride, down)]
         self.inplanes = planes * block.expansion
         layers += [block(self.inplanes, planes) for _ in range(1, blocks)]
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.maxpool(self.bn1(self.conv1(x), relu=True))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         return self.fc(torch.flatten(self.avgpool(x), 1))
 

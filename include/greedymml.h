@@ -182,10 +182,11 @@ int gm_conv_weight_transpose_bf16(const void* w, void* wt, int K, int RS, int C,
 /* fp32 KRSC master weight -> bf16 [K][RS][Cp] (zero-padded channels) and, if wt != NULL,
  * the transposed bf16 [Cp][RS][K] for dgrad, in one pass */
 int gm_conv_weight_prep_bf16(const float* w, int K, int RS, int C, int Cp, void* wb, void* wt, void* stream);
-/* dw is fp32 [K][R][S][c_real]: the first c_real of the C (padded) input channels */
+/* dw is fp32 [K][R][S][c_real]: the first c_real of the C (padded) input channels;
+ * accumulate != 0 adds into dw (a parameter's gradient buffer written in place) */
 size_t gm_conv2d_wgrad_scratch(const gm_conv_desc* d);
 int gm_conv2d_wgrad_bf16(const gm_conv_desc* d, const void* dy, const void* x, float* dw, int c_real,
-                         void* scratch, size_t scratch_bytes, void* stream);
+                         int accumulate, void* scratch, size_t scratch_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * BatchNorm2d (torchvision ResNet trunk, reference src/model.py:65-106 through
@@ -216,6 +217,7 @@ typedef struct gm_bn_fwd {
     float momentum, eps;
     float* save_mean;
     float* save_invstd;
+    long long* num_batches_tracked;  /* train: += 1 if non-NULL (nn.BatchNorm2d counter) */
 } gm_bn_fwd;
 
 typedef struct gm_bn_bwd {
@@ -239,6 +241,21 @@ size_t gm_bn_scratch(long long M, int C);
 int gm_bn_fwd_train_bf16(const gm_bn_fwd* p, void* scratch, size_t scratch_bytes, void* stream);
 int gm_bn_fwd_infer_bf16(const gm_bn_fwd* p, void* scratch, size_t scratch_bytes, void* stream);
 int gm_bn_bwd_bf16(const gm_bn_bwd* p, void* scratch, size_t scratch_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * MaxPool2d of the ResNet stem (kernel k, stride, padding; dilation 1, floor
+ * mode), NHWC bf16, C a multiple of 8.  Forward writes y[N][P][Q][C] and idx,
+ * one byte per output element = window-relative argmax (r*k + c), PyTorch's
+ * tie/NaN rule; backward scatters dy to the argmax positions as a gather (dx
+ * fully written, zero elsewhere).  Replaces `net.maxpool` (src/model.py:65-106).
+ * ------------------------------------------------------------------------- */
+typedef struct gm_pool_desc {
+    int N, H, W, C;
+    int k, stride, pad;
+} gm_pool_desc;
+
+int gm_maxpool2d_fwd_bf16(const gm_pool_desc* d, const void* x, void* y, void* idx, void* stream);
+int gm_maxpool2d_bwd_bf16(const gm_pool_desc* d, const void* dy, const void* idx, void* dx, void* stream);
 
 #ifdef __cplusplus
 }

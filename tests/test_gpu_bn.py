@@ -1,0 +1,125 @@
+"""HIP BatchNorm(+residual+ReLU) kernels vs a plain PyTorch fp32 reference of the
+same op (F.batch_norm on the bf16-rounded input), forward, backward, running
+statistics, eval mode, in-place gradient delivery and determinism."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+CL = torch.channels_last
+SHAPES = [(4, 64, 16, 16), (2, 128, 7, 7), (3, 8, 5, 5), (64, 512, 7, 7), (8, 256, 14, 14), (2, 2048, 4, 4),
+          (16, 64, 56, 56)]
+
+
+def _ref(x, w, b, rm, rv, res, relu, momentum=0.1, eps=1e-5):
+    """fp32 autograd reference; returns y, running stats after the update."""
+    rm, rv = rm.clone(), rv.clone()
+    y = F.batch_norm(x, rm, rv, w, b, training=True, momentum=momentum, eps=eps)
+    if res is not None:
+        y = y + res
+    if relu:
+        y = F.relu(y)
+    return y, rm, rv
+
+
+def _inputs(shape, seed, res):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    N, C, H, W = shape
+    x = (torch.randn(shape, device="cuda", generator=g) * 1.7 + 0.3).bfloat16().contiguous(memory_format=CL)
+    r = torch.randn(shape, device="cuda", generator=g).bfloat16().contiguous(memory_format=CL) if res else None
+    w = torch.rand(C, device="cuda", generator=g) + 0.5
+    b = torch.randn(C, device="cuda", generator=g) * 0.1
+    rm = torch.randn(C, device="cuda", generator=g) * 0.1
+    rv = torch.rand(C, device="cuda", generator=g) + 0.5
+    dy = torch.randn(shape, device="cuda", generator=g).bfloat16().contiguous(memory_format=CL)
+    return x, r, w, b, rm, rv, dy
+
+
+def _rel(a, b):
+    return (a.float() - b.float()).abs().max().item() / max(b.float().abs().max().item(), 1e-6)
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("res,relu", [(False, False), (False, True), (True, True)])
+def test_bn_train_fwd_bwd(shape, res, relu):
+    from greedy_multimodal_learning_amd.bn import GMBatchNorm2d
+    x, r, w, b, rm, rv, dy = _inputs(shape, 7 + shape[1], res)
+    C = shape[1]
+    m = GMBatchNorm2d(C).cuda().to(memory_format=CL)
+    with torch.no_grad():
+        m.weight.copy_(w)
+        m.bias.copy_(b)
+        m.running_mean.copy_(rm)
+        m.running_var.copy_(rv)
+    xg = x.clone().requires_grad_(True)
+    rg = r.clone().requires_grad_(True) if res else None
+    y = m(xg, residual=rg, relu=relu)
+    assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=CL)
+    y.backward(dy)
+
+    xr = x.float().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    rr = r.float().requires_grad_(True) if res else None
+    yr, rm_r, rv_r = _ref(xr, wr, br, rm, rv, rr, relu)
+    yr.backward(dy.float())
+
+    assert _rel(y, yr) < 1e-2
+    assert torch.allclose(m.running_mean, rm_r, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(m.running_var, rv_r, rtol=1e-4, atol=1e-5)
+    assert int(m.num_batches_tracked) == 1
+    assert _rel(xg.grad, xr.grad) < 1.5e-2
+    assert _rel(m.weight.grad, wr.grad) < 2e-3
+    assert _rel(m.bias.grad, br.grad) < 2e-3
+    if res:
+        assert _rel(rg.grad, rr.grad) < 1e-2
+
+
+def test_bn_deterministic_and_eval():
+    from greedy_multimodal_learning_amd.bn import GMBatchNorm2d
+    shape = (32, 64, 28, 28)
+    x, r, w, b, rm, rv, dy = _inputs(shape, 3, True)
+    outs = []
+    for _ in range(2):
+        m = GMBatchNorm2d(64).cuda()
+        xg = x.clone().requires_grad_(True)
+        y = m(xg, residual=r, relu=True)
+        y.backward(dy)
+        outs.append((y, xg.grad, m.weight.grad.clone(), m.running_var.clone()))
+    for a, b2 in zip(*outs):
+        assert torch.equal(a, b2)
+    # eval: running statistics
+    m.eval()
+    with torch.no_grad():
+        ye = m(x, residual=r, relu=True)
+        yr = F.relu(F.batch_norm(x.float(), m.running_mean, m.running_var, m.weight, m.bias, False) + r.float())
+    assert _rel(ye, yr) < 1e-2
+
+
+def test_bn_grad_sink_in_place():
+    """Engine mode: weight/bias gradients land in .grad in place (overwrite, then
+    accumulate on a second use within the step) and the hook fires."""
+    from greedy_multimodal_learning_amd.bn import GMBatchNorm2d
+    from greedy_multimodal_learning_amd.gradsink import GradSink
+    shape = (8, 128, 14, 14)
+    x, _, w, b, rm, rv, dy = _inputs(shape, 5, False)
+    m = GMBatchNorm2d(128).cuda()
+    fired = []
+    m.weight.grad = torch.full_like(m.weight, 7.0)  # stale content must be overwritten
+    m.bias.grad = torch.full_like(m.bias, 7.0)
+    sink = GradSink(m.parameters(), on_ready=fired.append)
+    sink.begin_step()
+    y = m(x.clone().requires_grad_(True), relu=True)
+    y.backward(dy)
+    g1 = m.weight.grad.clone()
+    y2 = m(x.clone().requires_grad_(True), relu=True)
+    y2.backward(dy)
+    sink.end_step()
+    assert len(fired) == 4
+    sink.detach()
+    m2 = GMBatchNorm2d(128).cuda()
+    y3 = m2(x.clone().requires_grad_(True), relu=True)
+    y3.backward(dy)
+    assert torch.allclose(g1, m2.weight.grad, rtol=0, atol=0)
+    assert torch.allclose(m.weight.grad, 2 * m2.weight.grad, rtol=1e-6, atol=1e-6)

@@ -74,3 +74,28 @@ def test_conv_fp32_input_uses_vendor_path(dev):
     y = m(x)
     assert y.dtype == torch.float32
     torch.testing.assert_close(y, F.conv2d(x, m.weight, padding=1))
+
+
+def test_conv_wgrad_in_place_sink(dev):
+    """Engine mode: the weight gradient is written into .grad in place (first use
+    overwrites stale content, second use in the same step accumulates)."""
+    from greedy_multimodal_learning_amd.conv import GMConv2d
+    from greedy_multimodal_learning_amd.gradsink import GradSink
+    CL = torch.channels_last
+    m = GMConv2d(64, 64, 3, padding=1, bias=False).to(dev).to(memory_format=CL)
+    x = torch.randn(2, 64, 14, 14, device=dev).bfloat16().contiguous(memory_format=CL)
+    gy = torch.randn(2, 64, 14, 14, device=dev).bfloat16().contiguous(memory_format=CL)
+    m(x).backward(gy)
+    ref = m.weight.grad.clone()
+    m.weight.grad = torch.full_like(ref, 3.0).contiguous(memory_format=CL)
+    fired = []
+    sink = GradSink([m.weight], on_ready=fired.append)
+    sink.begin_step()
+    m(x).backward(gy)
+    first = m.weight.grad.clone()
+    m(x).backward(gy)
+    sink.end_step()
+    sink.detach()
+    assert len(fired) == 2
+    assert torch.equal(first, ref)
+    torch.testing.assert_close(m.weight.grad, 2 * ref, rtol=1e-6, atol=1e-6)
