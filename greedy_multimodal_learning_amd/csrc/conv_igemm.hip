@@ -19,6 +19,7 @@
 // so the ds_read_b128 fragment reads are conflict-free; fp32 accumulation; weights are
 // the MFMA A operand so each lane holds 4 consecutive output channels of one pixel and
 // the epilogue writes 8-B NHWC chunks directly.  Out-of-range taps read zeros.
+#include <cstdlib>
 #include <cstring>
 
 #include "gm_common.h"
@@ -57,15 +58,16 @@ __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >>
 
 __device__ __attribute__((aligned(16))) const uint4 g_zero16[1] = {{0u, 0u, 0u, 0u}};
 
-template <int BM, int BN, bool UT>
+template <int BM, int BN, bool UT, int ST>
 __global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
     constexpr int BK = 64;
     constexpr int AR = BM / 32;       // A rows per thread
     constexpr int BR = BN / 32;       // B rows per thread
     constexpr int MT = BM / 64, NT = BN / 64;  // 32x32 MFMA tiles per wave
+    constexpr int G = AR + BR;        // LDS-DMA instructions per wave per k-tile
     extern __shared__ __attribute__((aligned(16))) uint4 smem[];
-    uint4* As = smem;                           // [2][BM][8] (16-B chunks)
-    uint4* Bs = smem + 2 * BM * 8;              // [2][BN][8]
+    uint4* As = smem;                           // [ST][BM][8] (16-B chunks)
+    uint4* Bs = smem + ST * BM * 8;             // [ST][BN][8]
 
     int ci = 0;
 #pragma unroll
@@ -83,7 +85,7 @@ __global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
     const int t = threadIdx.x;
     const int lane = t & 63, wave = t >> 6;
     // tap table -> LDS (static indices only into the kernel-argument struct)
-    int* tapt = (int*)(smem + 2 * (BM + BN) * 8);
+    int* tapt = (int*)(smem + ST * (BM + BN) * 8);
 #pragma unroll
     for (int i = 0; i < kMaxTap; ++i)
         if (t == i && i < cl.ntap)
@@ -129,52 +131,53 @@ __global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
     typedef __attribute__((address_space(1))) const void* gptr_t;
     typedef __attribute__((address_space(3))) void* lptr_t;
     auto issue = [&](int kt, int buf) {
-#pragma unroll
-        for (int j = 0; j < AR; ++j) {
-            int tap, c;
-            bool kin;
-            if constexpr (UT) {
-                const int k = kt * BK;
-                tap = __builtin_amdgcn_readfirstlane(k >> a.logC);
-                c = (k & (a.C - 1)) + a_gc[j] * 8;
-                kin = true;
-            } else {
-                const int k = kt * BK + a_gc[j] * 8;
-                kin = k < Ktot;
-                tap = kin ? (k >> a.logC) : 0;
-                c = k & (a.C - 1);
-            }
-            int te = tapt[tap];
-            if constexpr (UT) te = __builtin_amdgcn_readfirstlane(te);
+        if constexpr (UT) {
+            // C >= 64: a 64-wide k-tile lies inside one tap -> ONE table read per tile
+            const int k = kt * BK;
+            const int te = __builtin_amdgcn_readfirstlane(tapt[k >> a.logC]);
             const int dh = ((te >> 8) & 0xff) - 128, dw = ((te >> 16) & 0xff) - 128;
-            const int hi = a_h[j] + dh, wi = a_w[j] + dw;
-            const bool ok = kin && (unsigned)hi < (unsigned)a.Hi && (unsigned)wi < (unsigned)a.Wi;
-            const void* src = ok ? (const void*)(a_ptr[j] + (((dh * a.Wi + dw) << a.logC) + c))
-                                 : (const void*)g_zero16;
-            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(As + (buf * BM + (wave * AR + j) * 8) * 8),
-                                             16, 0, 0);
-        }
+            const int c0 = k & (a.C - 1);
+            const int aoff = ((dh * a.Wi + dw) << a.logC) + c0;
+            const int boff = (te & 0xff) * a.C + c0;
 #pragma unroll
-        for (int j = 0; j < BR; ++j) {
-            int tap, c;
-            bool kin;
-            if constexpr (UT) {
-                const int k = kt * BK;
-                tap = __builtin_amdgcn_readfirstlane(k >> a.logC);
-                c = (k & (a.C - 1)) + b_gc[j] * 8;
-                kin = true;
-            } else {
-                const int k = kt * BK + b_gc[j] * 8;
-                kin = k < Ktot;
-                tap = kin ? (k >> a.logC) : 0;
-                c = k & (a.C - 1);
+            for (int j = 0; j < AR; ++j) {
+                const bool ok = (unsigned)(a_h[j] + dh) < (unsigned)a.Hi && (unsigned)(a_w[j] + dw) < (unsigned)a.Wi;
+                const void* src = ok ? (const void*)(a_ptr[j] + aoff + a_gc[j] * 8) : (const void*)g_zero16;
+                __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(As + (buf * BM + (wave * AR + j) * 8) * 8),
+                                                 16, 0, 0);
             }
-            int te = tapt[tap];
-            if constexpr (UT) te = __builtin_amdgcn_readfirstlane(te);
-            const int tw = te & 0xff;
-            const void* src = (kin && b_ok[j]) ? (const void*)(b_ptr[j] + tw * a.C + c) : (const void*)g_zero16;
-            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(Bs + (buf * BN + (wave * BR + j) * 8) * 8),
-                                             16, 0, 0);
+#pragma unroll
+            for (int j = 0; j < BR; ++j) {
+                const void* src = b_ok[j] ? (const void*)(b_ptr[j] + boff + b_gc[j] * 8) : (const void*)g_zero16;
+                __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(Bs + (buf * BN + (wave * BR + j) * 8) * 8),
+                                                 16, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < AR; ++j) {
+                const int k = kt * BK + a_gc[j] * 8;
+                const bool kin = k < Ktot;
+                const int te = tapt[kin ? (k >> a.logC) : 0];
+                const int c = k & (a.C - 1);
+                const int dh = ((te >> 8) & 0xff) - 128, dw = ((te >> 16) & 0xff) - 128;
+                const int hi = a_h[j] + dh, wi = a_w[j] + dw;
+                const bool ok = kin && (unsigned)hi < (unsigned)a.Hi && (unsigned)wi < (unsigned)a.Wi;
+                const void* src = ok ? (const void*)(a_ptr[j] + (((dh * a.Wi + dw) << a.logC) + c))
+                                     : (const void*)g_zero16;
+                __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(As + (buf * BM + (wave * AR + j) * 8) * 8),
+                                                 16, 0, 0);
+            }
+#pragma unroll
+            for (int j = 0; j < BR; ++j) {
+                const int k = kt * BK + b_gc[j] * 8;
+                const bool kin = k < Ktot;
+                const int te = tapt[kin ? (k >> a.logC) : 0];
+                const int c = k & (a.C - 1);
+                const void* src = (kin && b_ok[j]) ? (const void*)(b_ptr[j] + (te & 0xff) * a.C + c)
+                                                   : (const void*)g_zero16;
+                __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(Bs + (buf * BN + (wave * BR + j) * 8) * 8),
+                                                 16, 0, 0);
+            }
         }
     };
 
@@ -211,15 +214,38 @@ __global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
         }
     };
-    // 2 LDS buffers: the DMA of tile kt+1 runs under the MFMAs of tile kt; the barrier
-    // at the end of each step (vmcnt(0) + s_barrier) publishes it.
-    if (nk > 0) issue(0, 0);
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-        const int buf = kt & 1;
-        if (kt + 1 < nk) issue(kt + 1, buf ^ 1);
-        compute(buf);
+    if constexpr (ST == 2) {
+        // 2 LDS buffers: the DMA of tile kt+1 runs under the MFMAs of tile kt; the barrier
+        // at the end of each step (vmcnt(0) + s_barrier) publishes it.
+        if (nk > 0) issue(0, 0);
         __syncthreads();
+        for (int kt = 0; kt < nk; ++kt) {
+            const int buf = kt & 1;
+            if (kt + 1 < nk) issue(kt + 1, buf ^ 1);
+            compute(buf);
+            __syncthreads();
+        }
+    } else {
+        // 3 LDS buffers, two k-tiles in flight: step kt waits only for ITS tile
+        // (counted vmcnt leaves tile kt+1's G DMAs outstanding), one raw barrier per
+        // step publishes it and retires the reads of buffer (kt-1)%3, which tile kt+2
+        // then refills under this step's MFMAs.
+        if (nk > 0) issue(0, 0);
+        if (nk > 1) issue(1, 1);
+        int buf = 0, nbuf = 2;
+        for (int kt = 0; kt < nk; ++kt) {
+            if (kt + 1 < nk)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            if (kt + 2 < nk) issue(kt + 2, nbuf);
+            compute(buf);
+            buf = buf == ST - 1 ? 0 : buf + 1;
+            nbuf = nbuf == ST - 1 ? 0 : nbuf + 1;
+        }
     }
 
     // ---- epilogue: D[n][m] layout: lane -> pixel m (col = lane&31), registers 4g..4g+3 ->
@@ -271,7 +297,7 @@ static int ilog2(int v) {
 
 using namespace gm;
 
-template <int BM, int BN>
+template <int BM, int BN, int ST>
 static int launch_igemm(ConvArgs& a, hipStream_t st) {
     int tiles = 0;
     for (int i = 0; i < a.ncls; ++i) {
@@ -282,29 +308,40 @@ static int launch_igemm(ConvArgs& a, hipStream_t st) {
         tiles += c.tiles_m * ((a.Nout + BN - 1) / BN);
     }
     if (tiles == 0) return GM_OK;
-    const size_t lds = (size_t)2 * (BM + BN) * 128 + kMaxTap * 4 + 12;
+    const size_t lds = (size_t)ST * (BM + BN) * 128 + kMaxTap * 4 + 12;
     static bool attr_set = false;  // idempotent, safe to race
     if (!attr_set) {
-        hipFuncSetAttribute((const void*)k_conv_igemm<BM, BN, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        hipFuncSetAttribute((const void*)k_conv_igemm<BM, BN, true, ST>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
-        hipFuncSetAttribute((const void*)k_conv_igemm<BM, BN, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        hipFuncSetAttribute((const void*)k_conv_igemm<BM, BN, false, ST>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
         attr_set = true;
     }
     if (a.C >= 64)
-        k_conv_igemm<BM, BN, true><<<tiles, 256, lds, st>>>(a);
+        k_conv_igemm<BM, BN, true, ST><<<tiles, 256, lds, st>>>(a);
     else
-        k_conv_igemm<BM, BN, false><<<tiles, 256, lds, st>>>(a);
+        k_conv_igemm<BM, BN, false, ST><<<tiles, 256, lds, st>>>(a);
     return check_launch("k_conv_igemm");
+}
+
+static int stages() {
+    static int s = [] {
+        const char* e = getenv("GM_CONV_STAGES");
+        return (e && e[0] == '2') ? 2 : 3;
+    }();
+    return s;
 }
 
 static int pick_and_launch(ConvArgs& a, hipStream_t st) {
     long M = 0;
     for (int i = 0; i < a.ncls; ++i) M += (long)a.N * a.cls[i].P * a.cls[i].Q;
+    const bool three = stages() == 3;
     // enough workgroups to fill 256 CUs, largest tile that does
-    if (a.Nout >= 128 && M / 128 * (a.Nout / 128) >= 1024) return launch_igemm<128, 128>(a, st);
-    if (M / 128 * ((a.Nout + 63) / 64) >= 768) return launch_igemm<128, 64>(a, st);
-    return launch_igemm<64, 64>(a, st);
+    if (a.Nout >= 128 && M / 128 * (a.Nout / 128) >= 1024)
+        return three ? launch_igemm<128, 128, 3>(a, st) : launch_igemm<128, 128, 2>(a, st);
+    if (M / 128 * ((a.Nout + 63) / 64) >= 768)
+        return three ? launch_igemm<128, 64, 3>(a, st) : launch_igemm<128, 64, 2>(a, st);
+    return three ? launch_igemm<64, 64, 3>(a, st) : launch_igemm<64, 64, 2>(a, st);
 }
 
 static int check_desc(const gm_conv_desc* d) {

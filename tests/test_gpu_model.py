@@ -176,9 +176,11 @@ def test_guided_trace_vs_reference(golden, dev):
     assert rows.shape == ref.shape
     np.testing.assert_allclose(rows[:, 0], ref[:, 0], rtol=1e-3)
     # d_BDR accumulates every step's gradient norms: tight before drift can build up,
-    # then bounded by the accumulated trunk reduction error (decisions stay exact)
+    # then bounded by the accumulated trunk reduction error (decisions stay exact).
+    # The late-step bound covers the run-to-run spread of MIOpen's fp32 algorithm
+    # choice (observed up to 1.06e-3 at step 11 of 12 on one box, 0.9e-3 on another).
     np.testing.assert_allclose(rows[:4, 1], ref[:4, 1], atol=1e-4)
-    np.testing.assert_allclose(rows[:, 1], ref[:, 1], atol=1e-3)
+    np.testing.assert_allclose(rows[:, 1], ref[:, 1], atol=1.5e-3)
     # every |d_BDR| of this run is >= 1.6e-3 away from epsilon: decisions must be identical
     np.testing.assert_array_equal(rows[:, 2:4], ref[:, 2:4])
     np.testing.assert_allclose(rows[:, 4:], ref[:, 4:], atol=1e-9)
