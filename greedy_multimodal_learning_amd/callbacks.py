@@ -86,7 +86,11 @@ class Callback(object):
 
 
 def group_masks(names, branchnames, MMTMnames):
-    """Bit i = main[i] (i < len(branchnames)); bit nb+j = bypass[j]."""
+    """Bit i = main[i] (i < len(branchnames)); bit nb+j = bypass[j].
+
+    Substring matching as in the reference (src/callbacks.py:207-223); when one
+    branch name contains another (net_view_1 / net_view_10 in the 12-view
+    config) the longest matching name wins."""
     nb = len(branchnames)
     out = []
     for name in names:
@@ -96,9 +100,12 @@ def group_masks(names, branchnames, MMTMnames):
             for j in (hit if hit else range(len(MMTMnames))):
                 m |= 1 << (nb + j)
         else:
-            for i, b in enumerate(branchnames):
-                if b in name:
-                    m |= 1 << i
+            hit = [i for i, b in enumerate(branchnames) if b in name]
+            if hit:
+                longest = max(len(branchnames[i]) for i in hit)
+                for i in hit:
+                    if len(branchnames[i]) == longest:
+                        m |= 1 << i
         out.append(m)
     return out
 
@@ -164,15 +171,29 @@ class GroupNorms:
         return out
 
 
-def bdr_update(M_bypass, M_main, s, nb):
-    """Accumulate the M's from one step's group sums (host float64) and return d_BDR.
-    s = [w_main0, g_main0, w_main1, g_main1, w_by0, g_by0, w_by1, g_by1]."""
+def bdr_values(M_bypass, M_main, s, nb):
+    """Accumulate the M's from one step's group sums (host float64) and return the
+    per-branch BDR_i = log10(M_bypass_i / M_main_i) (src/callbacks.py:225-232).
+    s = [w_main0, g_main0, ..., w_main{nb-1}, g_main{nb-1}, w_by0, g_by0, ...]."""
     for i in range(nb):
         M_main[i] += s[2 * i + 1] / s[2 * i]
         M_bypass[i] += s[2 * (nb + i) + 1] / s[2 * (nb + i)]
-    bdr0 = np.log10(M_bypass[0] / M_main[0])
-    bdr1 = np.log10(M_bypass[1] / M_main[1])
-    return bdr0 - bdr1
+    return [np.log10(M_bypass[i] / M_main[i]) for i in range(nb)]
+
+
+def bdr_update(M_bypass, M_main, s, nb):
+    """Two branches: d_BDR = BDR_0 - BDR_1 (src/callbacks.py:233)."""
+    b = bdr_values(M_bypass, M_main, s, nb)
+    return b[0] - b[1]
+
+
+def bdr_decision(bdr):
+    """N-branch generalisation (build decision): spread = max - min of
+    the BDRs and the branch to care for = argmax (first on ties).  At two branches
+    this is |BDR_0 - BDR_1| with caring = 1 iff d_BDR < 0, the reference's rule
+    (src/callbacks.py:244-252)."""
+    hi = int(np.argmax(bdr))
+    return float(np.max(bdr) - np.min(bdr)), hi
 
 
 @configurable
@@ -194,6 +215,10 @@ class Bias_Mitigation_Strong(Callback):
         self.M_bypass_modal_1 = 0
         self.M_main_modal_0 = 0
         self.M_main_modal_1 = 0
+        nb = len(self.branchnames)
+        self.M_bypass = [0.0] * nb  # N-branch accumulators (nb > 2)
+        self.M_main = [0.0] * nb
+        self.BDR = None
         self.model_pytoune.curation_mode = False
         self.model_pytoune.caring_modality = None
         self.unlock = False
@@ -210,6 +235,12 @@ class Bias_Mitigation_Strong(Callback):
 
     def compute_BDR(self):
         s = self.group_sums().cpu().numpy()  # the step's single host sync
+        nb = len(self.branchnames)
+        if nb != 2:
+            # N branches: d_BDR reports the BDR spread (max - min), decision = argmax
+            self.BDR = bdr_values(self.M_bypass, self.M_main, s, nb)
+            d, self._argmax = bdr_decision(self.BDR)
+            return d
         M_by = [self.M_bypass_modal_0, self.M_bypass_modal_1]
         M_main = [self.M_main_modal_0, self.M_main_modal_1]
         d = bdr_update(M_by, M_main, s, len(self.branchnames))
@@ -235,7 +266,9 @@ class Bias_Mitigation_Strong(Callback):
                     biased_direction = np.sign(self.d_BDR)
                     mp.curation_mode = True
                     self.curation_step = 0
-                    if biased_direction == -1:
+                    if len(self.branchnames) != 2:
+                        mp.caring_modality = self._argmax
+                    elif biased_direction == -1:
                         mp.caring_modality = 1
                     elif biased_direction == 1:
                         mp.caring_modality = 0

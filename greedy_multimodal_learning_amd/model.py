@@ -70,3 +70,52 @@ class MMTM_MVCNN(nn.Module):
         x0 = self.net_view_0.fc(torch.flatten(self.net_view_0.avgpool(f0), 1))
         x1 = self.net_view_1.fc(torch.flatten(self.net_view_1.avgpool(f1), 1))
         return (x0 + x1) / 2, [x0, x1], scales, squeezed
+
+
+@configurable
+class MMTM_MVCNN_N(nn.Module):
+    """N-branch generalisation: `num_views` unshared trunks
+    `net_view_{i}` (resnet18 for C4, resnet50 for C5) fused by `MMTM_N` after
+    layer2/3/4.  forward(x[B,V,3,H,W]) returns (mean of the branch logits,
+    [logits_i], scales[3], squeezed[3]) like MMTM_MVCNN; caring_modality may
+    be any branch index.  At num_views=2 / resnet18 it computes what
+    MMTM_MVCNN computes (parameter names differ only inside the MMTM sites:
+    fc_excite.{0,1} for fc_visual/fc_skeleton)."""
+
+    def __init__(self, nclasses=40, num_views=4, trunk="resnet18", ratio=4, ra_source="first",
+                 saving_mmtm_scales=False, saving_mmtm_squeeze_array=False):
+        super().__init__()
+        from .mmtm_n import MMTM_N
+        from .resnet import resnet50
+        make = {"resnet18": resnet18, "resnet50": resnet50}[trunk]
+        self.nclasses = nclasses
+        self.num_views = num_views
+        self.saving_mmtm_scales = saving_mmtm_scales
+        self.saving_mmtm_squeeze_array = saving_mmtm_squeeze_array
+        exp = 1 if trunk == "resnet18" else 4
+        for i in range(num_views):
+            net = make(pretrained=False)
+            net.fc = nn.Linear(512 * exp, nclasses)
+            setattr(self, f"net_view_{i}", net)
+        for i, c in ((2, 128), (3, 256), (4, 512)):
+            setattr(self, f"mmtm{i}", MMTM_N([c * exp] * num_views, ratio, ra_source=ra_source))
+
+    def branch_names(self):
+        return [f"net_view_{i}" for i in range(self.num_views)]
+
+    def mmtm_names(self):
+        return [f"fc_excite.{i}." for i in range(self.num_views)]
+
+    def forward(self, x, curation_mode=False, caring_modality=None):
+        nets = [getattr(self, f"net_view_{i}") for i in range(self.num_views)]
+        fs = [MMTM_MVCNN._stem(n, x[:, i]) for i, n in enumerate(nets)]
+        scales, squeezed = [], []
+        for li in (2, 3, 4):
+            fs = [getattr(n, f"layer{li}")(f) for n, f in zip(nets, fs)]
+            fs, sc, sq = getattr(self, f"mmtm{li}")(
+                fs, self.saving_mmtm_scales, self.saving_mmtm_squeeze_array, curation_mode=curation_mode,
+                caring_modality=caring_modality if caring_modality is not None else 0)
+            scales.append(sc)
+            squeezed.append(sq)
+        outs = [n.fc(torch.flatten(n.avgpool(f), 1)) for n, f in zip(nets, fs)]
+        return sum(outs) / len(outs), outs, scales, squeezed

@@ -34,8 +34,15 @@ def as_layout(x, layout):
     return x.contiguous()
 
 
+MAX_REDUCE, MAX_SCALE, MAX_GEMM = 4, 4, 6  # problems per launch (include/greedymml.h)
+
+
 def spatial_reduce(probs, B, dtype, layout, device):
     """probs: list of dict(x, dy, out, ld_out, e, ld_e, C, HW, scale, out_off) -> launches."""
+    if len(probs) > MAX_REDUCE:
+        for i in range(0, len(probs), MAX_REDUCE):
+            spatial_reduce(probs[i:i + MAX_REDUCE], B, dtype, layout, device)
+        return
     lib = L.load()
     items = []
     for p in probs:
@@ -54,6 +61,10 @@ def spatial_reduce(probs, B, dtype, layout, device):
 
 def channel_scale(probs, B, dtype, layout, device):
     """probs: list of dict(x, y, C, HW, s, s_off, ld_s, a, a_off, ld_a, alpha)."""
+    if len(probs) > MAX_SCALE:
+        for i in range(0, len(probs), MAX_SCALE):
+            channel_scale(probs[i:i + MAX_SCALE], B, dtype, layout, device)
+        return
     lib = L.load()
     items = []
     for p in probs:
@@ -84,7 +95,12 @@ ONES = Op(None, 0, 0)
 
 def gemm(problems, device):
     """problems: list of dict(M, N, segs=[(K, Op A, Op B)], C, c_off, ld_c, bias, act, mask,
-    ld_mask, accumulate). C[m,n] (+)= act(sum_seg A.B + bias) * (mask > 0)."""
+    ld_mask, accumulate). C[m,n] (+)= act(sum_seg A.B + bias) * (mask > 0).
+    Problems must be independent (no problem reads another's output)."""
+    if len(problems) > MAX_GEMM:
+        for i in range(0, len(problems), MAX_GEMM):
+            gemm(problems[i:i + MAX_GEMM], device)
+        return
     lib = L.load()
     items = []
     for p in problems:

@@ -48,12 +48,36 @@ def test_abi_argument_errors_without_gpu():
     assert rc == -1
 
 
-def test_struct_layouts_match_header():
+def test_struct_layouts_match_header(tmp_path):
+    """ctypes mirrors of every ABI struct have the C compiler's size and field offsets."""
+    import shutil
+    import subprocess
     from greedy_multimodal_learning_amd import _lib as L
     assert ctypes.sizeof(L.Tensor) == 40
     assert ctypes.sizeof(L.Operand) == 16
     assert ctypes.sizeof(L.SpatialReduce) == 56
     assert ctypes.sizeof(L.ChannelScale) == 56
+    pairs = [("gm_tensor", L.Tensor), ("gm_operand", L.Operand), ("gm_spatial_reduce", L.SpatialReduce),
+             ("gm_channel_scale", L.ChannelScale), ("gm_gemm", L.Gemm), ("gm_conv_desc", L.ConvDesc),
+             ("gm_bn_fwd", L.BnFwd), ("gm_bn_bwd", L.BnBwd), ("gm_pool_desc", L.PoolDesc)]
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no C compiler")
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "greedymml.h"', "int main(void){"]
+    for cname, py in pairs:
+        lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
+        for f, _ in py._fields_:
+            lines.append(f'printf("{cname}.{f} %zu\\n", offsetof({cname}, {f}));')
+    lines.append("return 0;}")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.check_call([cc, "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
+    got = dict(line.split() for line in subprocess.check_output([str(exe)]).decode().splitlines())
+    for cname, py in pairs:
+        assert int(got[cname]) == ctypes.sizeof(py), cname
+        for f, _ in py._fields_:
+            assert int(got[f"{cname}.{f}"]) == getattr(py, f).offset, f"{cname}.{f}"
 
 
 def test_product_ops_refuse_cpu_tensors():
@@ -139,6 +163,51 @@ def test_gating_state_machine_matches_oracle():
             logs = {}
             cb.on_batch_end(step, logs)
             assert logs["d_BDR"] == cb.d_BDR
+
+
+def test_group_masks_many_branches_longest_match():
+    from greedy_multimodal_learning_amd.callbacks import group_masks
+    branches = [f"net_view_{i}" for i in range(12)]
+    mods = [f"fc_excite.{i}." for i in range(12)]
+    names = ["net_view_1.conv1.weight", "net_view_10.conv1.weight", "net_view_11.fc.bias",
+             "mmtm2.fc_squeeze.weight", "mmtm3.fc_excite.1.weight", "mmtm4.fc_excite.11.bias"]
+    m = group_masks(names, branches, mods)
+    assert m[0] == 1 << 1 and m[1] == 1 << 10 and m[2] == 1 << 11
+    assert m[3] == sum(1 << (12 + j) for j in range(12))
+    assert m[4] == 1 << (12 + 1) and m[5] == 1 << (12 + 11)
+
+
+def test_n_branch_decision_reduces_to_reference_at_two():
+    """bdr_decision (N-branch rule) == the reference rule on two branches."""
+    from greedy_multimodal_learning_amd.callbacks import bdr_decision
+    rng = np.random.default_rng(3)
+    for _ in range(200):
+        b = rng.normal(size=2)
+        spread, care = bdr_decision(b)
+        d = b[0] - b[1]
+        assert spread == pytest.approx(abs(d))
+        assert care == (1 if d < 0 else 0)
+
+
+def test_n_branch_gate_cares_for_argmax():
+    from greedy_multimodal_learning_amd.callbacks import Bias_Mitigation_Strong
+    nb = 4
+    cb = Bias_Mitigation_Strong(epsilon=0.01, curation_windowsize=2,
+                                branchnames=[f"net_view_{i}" for i in range(nb)], starting_epoch=1,
+                                MMTMnames=[f"fc_excite.{i}." for i in range(nb)])
+    mp = _MP()
+    cb.set_model_pytoune(mp)
+    cb.on_train_begin({})
+    cb.on_epoch_begin(1, {})
+    s = np.ones(4 * nb)
+    s[2 * (nb + 2) + 1] = 5.0  # bypass_2 gradient ratio 5x: BDR_2 is the largest
+    cb.group_sums = lambda: torch.from_numpy(s.copy())
+    cb.on_backward_end(0)
+    assert mp.curation_mode and mp.caring_modality == 2
+    assert cb.d_BDR == pytest.approx(np.log10(5.0))
+    cb.on_backward_end(1)
+    cb.on_backward_end(2)  # window 2 ends
+    assert not mp.curation_mode
 
 
 def test_random_gate_matches_oracle():
