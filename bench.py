@@ -39,6 +39,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--miopen-find", action="store_true", help="torch.backends.cudnn.benchmark=True")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--eager", action="store_true", help="no hipGraph capture of the step")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_group_sumsq.json"))
     return ap.parse_args()
 
@@ -70,6 +71,19 @@ def cpu_baseline(seconds, size):
                       f"{torch.get_num_threads()} threads, {os.cpu_count()} visible CPUs"}
 
 
+def time_group_sumsq(step, n):
+    stream = torch.cuda.current_stream()
+    evs = []
+    for _ in range(n):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        step.norms.sums(grad_scale=1.0 / step.world, lr=step.lr)
+        e1.record(stream)
+        evs.append((e0, e1))
+    torch.cuda.synchronize()
+    return sum(a.elapsed_time(b) for a, b in evs) / n / 1e3
+
+
 def main():
     a = parse()
     dist_on = "RANK" in os.environ and int(os.environ.get("WORLD_SIZE", "1")) > 1
@@ -94,7 +108,7 @@ def main():
                                   branchnames=["net_view_0", "net_view_1"], starting_epoch=1)
     cdt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     step = BalancedStep(model, lr=0.1, gate=gate, compute_dtype=cdt, channels_last=(a.dtype == "bf16"),
-                        process_group=dist.group.WORLD if dist_on else None)
+                        process_group=dist.group.WORLD if dist_on else None, graphs=not a.eager)
     step.on_epoch_begin(1)
     B = a.batch
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
@@ -112,7 +126,6 @@ def main():
     for i in range(a.warmup):
         step(xs[i % 2], ys[i % 2])
     torch.cuda.synchronize()
-    step.timer = []
     curation_steps = 0
     if dist_on:
         dist.barrier()
@@ -131,10 +144,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
     ms = 1e3 * elapsed / a.steps
-    kern_ms = [e0.elapsed_time(e1) for e0, e1 in step.timer]
-    kern_avg_s = sum(kern_ms) / len(kern_ms) / 1e3
-    step.timer = None
     loss = float(step.last_loss)
+    # roofline kernel: the fused per-branch norms + SGD pass (k_group_sumsq<SGD>), the
+    # same launch the step runs (inside the graph), timed with HIP events on its stream
+    kern_avg_s = time_group_sumsq(step, 10)
 
     if rank == 0:
         views = 2
@@ -160,6 +173,7 @@ def main():
                                    "(training_guided.gin eps 0.01, window 5, unlocked)",
                        "global_batch": B * world, "per_gpu_batch": B, "image": a.size,
                        "parallelism": f"dp{world}", "samples_per_s": round(world * B * a.steps / elapsed, 2),
+                       "hipgraph": bool(step.graphs),
                        "curation_steps_timed": curation_steps, "final_loss": round(loss, 4)},
             "roofline": {"kernel": "k_group_sumsq<SGD> (fused per-branch norms + SGD, gm_group_sumsq)",
                          "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,

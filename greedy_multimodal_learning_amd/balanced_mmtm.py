@@ -36,6 +36,24 @@ def _as_f32(t, dev):
     return t.detach().to(device=dev, dtype=torch.float32).contiguous()
 
 
+def _state_f32(t, dev):
+    """Running-average state as a dense fp32 tensor on `dev` (updated in place)."""
+    if t.device != dev or t.dtype != torch.float32 or not t.is_contiguous():
+        t = t.to(device=dev, dtype=torch.float32).contiguous()
+    return t
+
+
+def _step_counter(mod, dev):
+    """Device copy of the module's `step` (int32 [1]); re-seeded from the host value
+    whenever the host attribute was changed from outside."""
+    sd = getattr(mod, "_step_dev", None)
+    if sd is None or sd.device != dev or getattr(mod, "_step_mirror", None) != mod.step:
+        sd = torch.full((1,), int(mod.step), dtype=torch.int32, device=dev)
+        mod._step_dev = sd
+        mod._step_mirror = mod.step
+    return sd
+
+
 class _MMTMFunction(torch.autograd.Function):
     """Y_v, Y_s = MMTM(X_v, X_s; fc weights).  Extra outputs e_v, e_s, sq are
     non-differentiable side results (scales / squeezed maps for recording)."""
@@ -89,9 +107,10 @@ class _MMTMFunction(torch.autograd.Function):
                        bias=bv_, act=2),
                   dict(M=B, N=Cs, segs=[(Cz, Op(z_s, Cz, 1), Op(ws_, 1, Cz))], C=e_s, ld_c=Cs,
                        bias=bs_, act=2)], dev)
-        # ---- running averages (both from e_v: reference quirk) + step
-        ra_v, ra_s = ops.running_avg(e_v, cfg["ra_v"], cfg["ra_s"], cfg["step"])
-        cfg["ra_v_new"], cfg["ra_s_new"] = ra_v, ra_s
+        # ---- running averages (both from e_v: reference quirk) + step, in place with
+        # the step counter in device memory (graph-capturable)
+        ra_v, ra_s = cfg["ra_v"], cfg["ra_s"]
+        ops.running_avg_dev(e_v, ra_v, ra_s, cfg["step_dev"])
         # ---- effective scales (curation substitutes the running average)
         cur, caring = cfg["curation"], cfg["caring"]
         sv, ld_sv, live_v = e_v, Cv, True
@@ -300,12 +319,14 @@ class MMTM_mitigate(nn.Module):
             lay = L.GM_NCHW
         visual = ops.as_layout(visual, lay)
         skeleton = ops.as_layout(skeleton, lay)
-        if self.running_avg_weight_visual.device != dev:
-            self.running_avg_weight_visual = self.running_avg_weight_visual.to(dev)
-            self.running_avg_weight_skeleton = self.running_avg_weight_skeleton.to(dev)
-        cfg = dict(layout=lay, mode=mode, share=self.shareweight, step=self.step,
-                   ra_v=self.running_avg_weight_visual.float().contiguous(),
-                   ra_s=self.running_avg_weight_skeleton.float().contiguous(),
+        self.running_avg_weight_visual = _state_f32(self.running_avg_weight_visual, dev)
+        self.running_avg_weight_skeleton = _state_f32(self.running_avg_weight_skeleton, dev)
+        if self.running_avg_weight_skeleton.data_ptr() == self.running_avg_weight_visual.data_ptr():
+            self.running_avg_weight_skeleton = self.running_avg_weight_skeleton.clone()
+        step_dev = _step_counter(self, dev)
+        cfg = dict(layout=lay, mode=mode, share=self.shareweight, step_dev=step_dev,
+                   ra_v=self.running_avg_weight_visual,
+                   ra_s=self.running_avg_weight_skeleton,
                    curation=bool(curation_mode), caring=caring_modality,
                    zero_curated=self.zero_grads_for_curated)
         if mode == TURNOFF:
@@ -322,9 +343,8 @@ class MMTM_mitigate(nn.Module):
             w_s, b_s = self._lin("fc_skeleton")
         yv, ys, e_v, e_s, sq = _MMTMFunction.apply(visual, skeleton, w_sq, b_sq, w_sq_v, b_sq_v,
                                                    w_sq_s, b_sq_s, w_v, b_v, w_s, b_s, cfg)
-        self.running_avg_weight_visual = cfg["ra_v_new"]
-        self.running_avg_weight_skeleton = cfg["ra_s_new"]
         self.step += 1
+        self._step_mirror = self.step
         scales = [e_v.cpu(), e_s.cpu()] if return_scale else None
         squeeze_array = None
         if return_squeezed_mps:

@@ -327,7 +327,7 @@ static int launch_igemm(ConvArgs& a, hipStream_t st) {
 static int stages() {
     static int s = [] {
         const char* e = getenv("GM_CONV_STAGES");
-        return (e && e[0] == '2') ? 2 : 3;
+        return (e && e[0] == '3') ? 3 : 2;
     }();
     return s;
 }

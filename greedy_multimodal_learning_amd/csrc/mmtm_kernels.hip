@@ -311,6 +311,34 @@ __global__ __launch_bounds__(256) void k_running_avg(const float* e, int ld, int
     os[c] = (m + rs[c] * k) / k1;
 }
 
+// graph-capturable form: one workgroup, step counter in device memory, averages
+// updated in place; the counter is advanced after every thread has read it
+__global__ __launch_bounds__(256) void k_running_avg_dev(const float* e, int ld, int B, int C, float* rv, float* rs,
+                                                         int* step, int increment) {
+    __shared__ float part[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int st = *step;
+    const float k = (float)st, k1 = (float)(st + 1);
+    for (int c0 = 0; c0 < C; c0 += 64) {
+        const int c = c0 + lane;
+        float m = 0.f;
+        if (c < C) {
+#pragma unroll 4
+            for (int b = w; b < B; b += 4) m += e[(size_t)b * ld + c];
+        }
+        part[w][lane] = m;
+        __syncthreads();
+        if (w == 0 && c < C) {
+            m = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+            m = m / (float)B;
+            rv[c] = (m + rv[c] * k) / k1;
+            if (rs != rv) rs[c] = (m + rs[c] * k) / k1;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && increment) *step = st + 1;
+}
+
 static bool aligned(const void* p, int bytes) { return ((uintptr_t)p % bytes) == 0; }
 
 }  // namespace gm
@@ -509,4 +537,12 @@ extern "C" int gm_mmtm_running_avg(const float* e_v, int ld_e, int B, int C, con
     k_running_avg<<<(C + 63) / 64, 256, 0, as_stream(stream)>>>(e_v, ld_e, B, C, ra_v_old, ra_s_old,
                                                                   ra_v_new, ra_s_new, step);
     return check_launch("k_running_avg");
+}
+
+extern "C" int gm_mmtm_running_avg_dev(const float* e_v, int ld_e, int B, int C, float* ra_v, float* ra_s,
+                                       int* step, int increment, void* stream) {
+    GM_REQUIRE(e_v && ra_v && ra_s && step, "running_avg_dev: null pointer");
+    GM_REQUIRE(B >= 1 && C >= 1 && ld_e >= C, "running_avg_dev: bad shape");
+    k_running_avg_dev<<<1, 256, 0, as_stream(stream)>>>(e_v, ld_e, B, C, ra_v, ra_s, step, increment);
+    return check_launch("k_running_avg_dev");
 }

@@ -19,7 +19,15 @@ re-organised for the hardware:
   the only host sync per step is the 8-double copy the gate needs for its
   decision (the decision applies to the NEXT forward, as in the reference);
 * the trunk runs in bf16 (autocast) on channels_last activations; master
-  weights, gradients, the MMTM FC chain and all reductions stay fp32.
+  weights, gradients, the MMTM FC chain and all reductions stay fp32;
+* `graphs=True` (single process): after one eager step, each curation setting
+  (none / caring 0 / caring 1 ...) is captured ONCE as a hipGraph of the whole
+  step - zero_grad, forward, loss, backward, fused norms+SGD - and replayed;
+  the host then only copies the 8 group sums and runs the gate's decision.
+  Everything the step mutates lives in device memory (parameters, BN running
+  statistics and counters, MMTM running averages and their step counter), so a
+  replay is exactly an eager step; the host-side `step` attributes of the MMTM
+  modules are advanced by the engine after each replay.
 """
 import torch
 import torch.distributed as dist
@@ -134,7 +142,7 @@ class GradBuckets:
 class BalancedStep:
     def __init__(self, model, lr=0.1, gate=None, compute_dtype=torch.bfloat16, channels_last=True,
                  process_group=None, bucket_mb=25.0, branchnames=("net_view_0", "net_view_1"),
-                 MMTMnames=("visual", "skeleton")):
+                 MMTMnames=("visual", "skeleton"), graphs=False):
         self.model = model
         self.lr = float(lr)
         self.gate = gate
@@ -167,6 +175,13 @@ class BalancedStep:
         self.last_loss = None
         self.step_count = 0
         self.timer = None  # optional (start_event, end_event) list collector for the fused pass
+        self.graphs = bool(graphs) and self.world == 1 and self.device.type == "cuda"
+        self._graphs = {}
+        self._gpool = None
+        self._static = None
+        from .balanced_mmtm import MMTM_mitigate
+        from .mmtm_n import MMTM_N
+        self._mmtms = [m for m in model.modules() if isinstance(m, (MMTM_mitigate, MMTM_N))]
 
     # ---------------- the step ----------------
     def forward(self, x):
@@ -174,9 +189,7 @@ class BalancedStep:
         with torch.autocast("cuda", dtype=self.compute_dtype, enabled=self.compute_dtype != torch.float32):
             return self.model(x, curation_mode=fl.curation_mode, caring_modality=fl.caring_modality)
 
-    def __call__(self, x, y):
-        """One balanced step on batch (x [B,V,3,H,W], y [B]); returns the loss tensor."""
-        self.model.train(True)
+    def _fwd_bwd(self, x, y):
         self.flat_grad.zero_()
         if self.buckets is not None:
             self.buckets.reset()
@@ -189,7 +202,52 @@ class BalancedStep:
             self.sink.end_step()
         if self.buckets is not None:
             self.buckets.finish()
+        return loss
+
+    def _graph_key(self):
+        fl = self.flags
+        return (bool(fl.curation_mode), fl.caring_modality if fl.curation_mode else None, self.lr)
+
+    def _capture(self, key):
+        """Record one whole step for the current curation flags (nothing executes)."""
+        steps = [(m, m.step) for m in self._mmtms]
+        g = torch.cuda.CUDAGraph()
+        if self._gpool is None:
+            self._gpool = torch.cuda.graph_pool_handle()
+        torch.cuda.synchronize(self.device)
+        with torch.cuda.graph(g, pool=self._gpool):
+            loss = self._fwd_bwd(*self._static)
+            sums = self.norms.sums(grad_scale=1.0 / self.world, lr=self.lr)
+        for m, st in steps:  # capture ran the Python forward but no kernel
+            m.step = st
+            m._step_mirror = st
+        self._graphs[key] = (g, loss, sums)
+        return self._graphs[key]
+
+    def __call__(self, x, y):
+        """One balanced step on batch (x [B,V,3,H,W], y [B]); returns the loss tensor
+        (with graphs=True: the captured step's static loss tensor)."""
+        self.model.train(True)
         gate = self.gate
+        if self.graphs and self.step_count > 0:
+            st = self._static
+            if st is None or st[0].shape != x.shape or st[1].shape != y.shape or st[0].dtype != x.dtype:
+                self._graphs = {}
+                self._static = st = (x.detach().clone(), y.detach().clone())
+            else:
+                if st[0].data_ptr() != x.data_ptr():
+                    st[0].copy_(x)
+                if st[1].data_ptr() != y.data_ptr():
+                    st[1].copy_(y)
+            key = self._graph_key()
+            g, loss, sums = self._graphs.get(key) or self._capture(key)
+            want = gate is not None and hasattr(gate, "needs_bdr") and gate.needs_bdr()
+            g.replay()
+            for m in self._mmtms:
+                m.step += 1
+                m._step_mirror = m.step
+            return self._after(loss, sums, want)
+        loss = self._fwd_bwd(x, y)
         want = gate is not None and hasattr(gate, "needs_bdr") and gate.needs_bdr()
         t = self.timer
         if t is not None:
@@ -200,6 +258,10 @@ class BalancedStep:
         if t is not None:
             ev1.record()
             t.append((ev0, ev1))
+        return self._after(loss, sums, want)
+
+    def _after(self, loss, sums, want):
+        gate = self.gate
         if gate is not None:
             if want:
                 gate.pending_sums = sums

@@ -76,18 +76,17 @@ class _MMTMNFunction(torch.autograd.Function):
         es = [torch.empty(B, Cs[i], **f32) for i in range(N)]
         ops.gemm([dict(M=B, N=Cs[i], segs=[(Cz, Op(zs[i], Cz, 1), Op(w_e[i], 1, Cz))], C=es[i], ld_c=Cs[i],
                        bias=b_e[i], act=2) for i in range(N)], dev)
-        # running averages + step (reference quirk at N=2: all from modality 0's scale)
-        ra_old = cfg["ra"]
-        ra_new = [None] * N
+        # running averages (in place) + device step counter; reference quirk at N=2:
+        # every average follows modality 0's scale
+        ra = cfg["ra"]
         if cfg["ra_source"] == "first":
-            for i in range(0, N, 2):
-                j = min(i + 1, N - 1)
-                ra_new[i], b = ops.running_avg(es[0], ra_old[i], ra_old[j], cfg["step"])
-                ra_new[j] = b if j != i else ra_new[i]
+            pairs = [(i, min(i + 1, N - 1)) for i in range(0, N, 2)]
+            for k, (i, j) in enumerate(pairs):
+                ops.running_avg_dev(es[0], ra[i], ra[j], cfg["step_dev"], increment=k == len(pairs) - 1)
         else:
             for i in range(N):
-                ra_new[i], _ = ops.running_avg(es[i], ra_old[i], ra_old[i], cfg["step"])
-        cfg["ra_new"] = ra_new
+                ops.running_avg_dev(es[i], ra[i], ra[i], cfg["step_dev"], increment=i == N - 1)
+        ra_new = ra
         caring = cfg["caring"] if cfg["curation"] else None
         scl = [(es[i], Cs[i]) if i != caring else (ra_new[i], 0) for i in range(N)]
         ys = [torch.empty_like(x) for x in xs]
@@ -216,12 +215,12 @@ class MMTM_N(nn.Module):
         if lay is None:
             lay = L.GM_NCHW
         xs = [ops.as_layout(x, lay) for x in xs]
-        if self.running_avg[0].device != dev:
-            self.running_avg = [r.to(dev) for r in self.running_avg]
+        from .balanced_mmtm import _state_f32, _step_counter
+        self.running_avg = [_state_f32(r, dev) for r in self.running_avg]
         if curation_mode and not (0 <= int(caring_modality) < self.N):
             raise ValueError(f"caring_modality must be in [0, {self.N})")
-        cfg = dict(N=self.N, layout=lay, turnoff=bool(turnoff_cross_modal_flow), step=self.step,
-                   ra=[r.float().contiguous() for r in self.running_avg], ra_source=self.ra_source,
+        cfg = dict(N=self.N, layout=lay, turnoff=bool(turnoff_cross_modal_flow), step_dev=_step_counter(self, dev),
+                   ra=self.running_avg, ra_source=self.ra_source,
                    curation=bool(curation_mode), caring=int(caring_modality) if curation_mode else None,
                    zero_curated=self.zero_grads_for_curated)
         if turnoff_cross_modal_flow:
@@ -233,8 +232,8 @@ class MMTM_N(nn.Module):
         b_e = [m.bias for m in self.fc_excite]
         outs = _MMTMNFunction.apply(cfg, self.fc_squeeze.weight, self.fc_squeeze.bias, *xs, *w_e, *b_e)
         ys, es, sq = list(outs[:self.N]), list(outs[self.N:2 * self.N]), outs[2 * self.N]
-        self.running_avg = cfg["ra_new"]
         self.step += 1
+        self._step_mirror = self.step
         scales = [e.cpu() for e in es] if return_scale else None
         squeeze = None
         if return_squeezed_mps:

@@ -127,6 +127,15 @@ def running_avg(e_v, ra_v, ra_s, step):
     return nv, ns
 
 
+def running_avg_dev(e_v, ra_v, ra_s, step_dev, increment=True):
+    """In-place running-average update with a device step counter (graph-capturable)."""
+    lib = L.load()
+    B, C = e_v.shape
+    L.check(lib.gm_mmtm_running_avg_dev(e_v.data_ptr(), e_v.stride(0), B, C, ra_v.data_ptr(), ra_s.data_ptr(),
+                                        step_dev.data_ptr(), int(increment), L.stream_of(e_v.device)),
+            "gm_mmtm_running_avg_dev")
+
+
 def linear(x, w, b=None, act=0):
     """y = act(x @ w.T + b) on the fp32 MFMA GEMM (x [M,K], w [N,K])."""
     _dev_check(x, w)

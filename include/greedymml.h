@@ -129,6 +129,11 @@ int gm_gemm_f32(const gm_gemm* p, int nprob, void* stream);
 int gm_mmtm_running_avg(const float* e_v, int ld_e, int B, int C,
                         const float* ra_v_old, const float* ra_s_old,
                         float* ra_v_new, float* ra_s_new, int step, void* stream);
+/* Graph-capturable form: the step counter lives in device memory (read, then
+ * advanced by one if `increment`), the averages are updated IN PLACE (ra_s may
+ * equal ra_v).  Same arithmetic as gm_mmtm_running_avg. */
+int gm_mmtm_running_avg_dev(const float* e_v, int ld_e, int B, int C, float* ra_v, float* ra_s,
+                            int* step, int increment, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Per-branch weight / gradient norms for the conditional-learning-speed gate

@@ -1,0 +1,50 @@
+"""Whole-step hipGraph capture (BalancedStep(graphs=True)) == eager steps: same
+losses, gate decisions, parameters and every piece of device state (BN running
+statistics and counters, MMTM running averages and step), across curation
+switches (one graph per curation setting)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(graphs, steps, dev):
+    from greedy_multimodal_learning_amd.callbacks import Bias_Mitigation_Strong
+    from greedy_multimodal_learning_amd.engine import BalancedStep
+    from greedy_multimodal_learning_amd.model import MMTM_MVCNN
+    torch.manual_seed(0)
+    m = MMTM_MVCNN().to(dev)
+    gate = Bias_Mitigation_Strong(epsilon=2e-3, curation_windowsize=2, branchnames=["net_view_0", "net_view_1"],
+                                  starting_epoch=1)
+    st = BalancedStep(m, lr=0.05, gate=gate, graphs=graphs)
+    st.on_epoch_begin(1)
+    g = torch.Generator(device=dev).manual_seed(5)
+    xs = [torch.randn(4, 2, 3, 64, 64, device=dev, generator=g) for _ in range(3)]
+    ys = [torch.randint(0, 40, (4,), device=dev, generator=g) for _ in range(3)]
+    trace = []
+    for i in range(steps):
+        loss = st(xs[i % 3], ys[i % 3])
+        trace.append((float(loss), gate.d_BDR, st.flags.curation_mode, st.flags.caring_modality))
+    return m, st, trace
+
+
+def test_graph_steps_equal_eager_steps():
+    dev = torch.device("cuda:0")
+    m_e, st_e, tr_e = _run(False, 9, dev)
+    m_g, st_g, tr_g = _run(True, 9, dev)
+    assert len(st_g._graphs) >= 2, "curation switches should have produced several graphs"
+    assert {t[2] for t in tr_e} == {True, False}
+    for a, b in zip(tr_e, tr_g):
+        assert a[2:] == b[2:]
+        assert a[0] == pytest.approx(b[0], rel=1e-6, abs=1e-6)
+        assert a[1] == pytest.approx(b[1], rel=1e-6, abs=1e-9)
+    se, sg = m_e.state_dict(), m_g.state_dict()
+    for k in se:
+        torch.testing.assert_close(sg[k], se[k], rtol=1e-6, atol=1e-6, msg=k)
+    for i in (2, 3, 4):
+        a, b = getattr(m_e, f"mmtm{i}"), getattr(m_g, f"mmtm{i}")
+        assert a.step == b.step == 9
+        torch.testing.assert_close(b.running_avg_weight_visual, a.running_avg_weight_visual, rtol=1e-6, atol=1e-7)
+        torch.testing.assert_close(b.running_avg_weight_skeleton, a.running_avg_weight_skeleton, rtol=1e-6,
+                                   atol=1e-7)
+        assert int(b._step_dev.item()) == 9

@@ -2,8 +2,8 @@
 # GPU iteration: tests (selected), conv/bn micro-benchmarks, full bench
 set -o pipefail
 mkdir -p gpurun_out
-T=${TESTS:-"tests/test_gpu_bn.py tests/test_gpu_pool.py tests/test_gpu_conv.py tests/test_gpu_model.py"}
-timeout -k 10 600 python -m pytest $T -q -p no:cacheprovider -x --timeout 300 > gpurun_out/iter_tests.log 2>&1
+T=${TESTS:-"tests/test_gpu_bn.py tests/test_gpu_pool.py tests/test_gpu_conv.py tests/test_gpu_mmtm_n.py tests/test_gpu_model.py"}
+timeout -k 10 600 python -m pytest $T -q -p no:cacheprovider --timeout 300 > gpurun_out/iter_tests.log 2>&1
 rc=$?
 tail -3 gpurun_out/iter_tests.log
 [ $rc -eq 0 ] || exit 1
