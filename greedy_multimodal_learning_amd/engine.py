@@ -216,7 +216,7 @@ class BalancedStep:
             self._gpool = torch.cuda.graph_pool_handle()
         torch.cuda.synchronize(self.device)
         with torch.cuda.graph(g, pool=self._gpool):
-            loss = self._fwd_bwd(*self._static)
+            loss = self._fwd_bwd(*self._static).detach()
             sums = self.norms.sums(grad_scale=1.0 / self.world, lr=self.lr)
         for m, st in steps:  # capture ran the Python forward but no kernel
             m.step = st
@@ -247,7 +247,9 @@ class BalancedStep:
                 m.step += 1
                 m._step_mirror = m.step
             return self._after(loss, sums, want)
-        loss = self._fwd_bwd(x, y)
+        # detached: a kept-alive autograd graph would pin AccumulateGrad nodes to this
+        # step's stream (breaks later graph capture, and holds memory)
+        loss = self._fwd_bwd(x, y).detach()
         want = gate is not None and hasattr(gate, "needs_bdr") and gate.needs_bdr()
         t = self.timer
         if t is not None:
