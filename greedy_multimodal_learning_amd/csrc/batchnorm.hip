@@ -24,10 +24,18 @@ constexpr int kMaxC = 2048;      // channels supported (ResNet-50 ends at 2048)
 constexpr size_t kHdr = 256;     // scratch header (ticket counter)
 constexpr int kFlag = 2 * kMaxC; // LDS slot of the last-arriver flag
 
+constexpr int kG1 = 32;          // level-1 ticket group: row chunks combined by one block
+
+// 2-D reduce grid: (row chunk, 64-channel slice).  Every block streams a
+// [rows x SW] strip (SW = min(C, 64) channels, 128-B row segments), unrolled x8
+// so ~32 KB per block is in flight; per-slice partials are combined in two
+// ticketed levels (groups of kG1 row chunks, then the groups), so no block ever
+// reads more than kG1 partial rows of 2*SW floats.
 struct Plan {
-    int nblk;        // reduce blocks
-    int tpr_log;     // log2(threads per row) = log2(C/8)
-    long long rpb;   // rows per block
+    int SW, tpr_log, rpp;  // slice width, log2(threads per row), rows per pass
+    int nslice, nrc, ng;   // slices, row chunks, level-1 groups per slice
+    long long rpb;         // rows per block
+    size_t off_coef, off_p1, off_p2, bytes;
 };
 
 inline int ilog2(int v) {
@@ -38,26 +46,28 @@ inline int ilog2(int v) {
 
 inline Plan make_plan(long long M, int C) {
     Plan p;
-    p.tpr_log = ilog2(C / 8);
-    const int rpp = kT / (C / 8);
-    // bound the partials the last block combines (nblk * 2C floats <= 128 KB) and
-    // give every block >= 64 KB of x
-    long long by_bytes = (M * C * 2 + 65535) / 65536;
-    long long cap = 16384 / C;
-    if (cap < 4) cap = 4;
-    long long nb = by_bytes < cap ? by_bytes : cap;
-    if (nb < 1) nb = 1;
-    long long rpb = (M + nb - 1) / nb;
-    rpb = (rpb + rpp - 1) / rpp * rpp;
+    p.SW = C < 64 ? C : 64;
+    p.tpr_log = ilog2(p.SW / 8);
+    p.rpp = kT >> p.tpr_log;
+    p.nslice = C / p.SW;
+    long long want = 1024 / p.nslice;
+    if (want < 1) want = 1;
+    if (want > (long long)kG1 * kG1) want = (long long)kG1 * kG1;
+    long long rpb = (M + want - 1) / want;
+    rpb = (rpb + p.rpp - 1) / p.rpp * p.rpp;
     p.rpb = rpb;
-    p.nblk = (int)((M + rpb - 1) / rpb);
+    p.nrc = (int)((M + rpb - 1) / rpb);
+    p.ng = (p.nrc + kG1 - 1) / kG1;
+    const size_t cnt = (size_t)p.nslice * (p.ng + 1) * sizeof(unsigned);
+    p.off_coef = (cnt + kHdr - 1) / kHdr * kHdr;
+    p.off_p1 = p.off_coef + (size_t)4 * C * sizeof(float);
+    p.off_p2 = p.off_p1 + (size_t)p.nslice * p.nrc * 2 * p.SW * sizeof(float);
+    p.off_p2 = (p.off_p2 + 7) / 8 * 8;
+    p.bytes = p.off_p2 + (size_t)p.nslice * p.ng * 2 * p.SW * sizeof(double);
     return p;
 }
 
-inline size_t scratch_bytes(long long M, int C) {
-    Plan p = make_plan(M, C);
-    return kHdr + (size_t)4 * C * sizeof(float) + (size_t)p.nblk * 2 * C * sizeof(float);
-}
+inline size_t scratch_bytes(long long M, int C) { return make_plan(M, C).bytes; }
 
 __device__ __forceinline__ void unpack8(uint4 u, float* f) {
     f[0] = bf_lo(u.x); f[1] = bf_hi(u.x); f[2] = bf_lo(u.y); f[3] = bf_hi(u.y);
@@ -70,6 +80,7 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
 struct ReduceArgs {
     long long M;
     int C, tpr_log, relu, accumulate;
+    int SW, nrc, ng;
     long long rpb;
     const uint4* x;      // fwd: x; bwd: x
     const uint4* dy;     // bwd
@@ -83,10 +94,11 @@ struct ReduceArgs {
     float* save_invstd;  // fwd: out; bwd: in
     float* dgamma;
     float* dbeta;
-    unsigned* counter;
+    unsigned* counter;   // [nslice][ng + 1] tickets (zero between calls)
     long long* nbt;      // num_batches_tracked (fwd, may be null)
     float* coef;         // [4][C]
-    float* part;         // [nblk][2C]
+    float* part;         // level 1: [nslice][nrc][SW][2] fp32
+    double* part2;       // level 2: [nslice][ng][SW][2] fp64
 };
 
 enum { FWD = 0, BWD = 1, BWD_RELU = 2 };  // relu as a template arg: no per-load branch
@@ -157,114 +169,119 @@ __device__ __forceinline__ void finalize(const ReduceArgs& a, int c, double S1, 
     }
 }
 
-// One launch: partial sums + last-arriver finalize.
+// Cross-workgroup hand-off without fences (cdna_hip_programming.md, in-launch
+// split-K recipe, sc1 form): partials are written with agent-scope atomic stores
+// (write-through sc1), every wave drains vmcnt, the block barriers, lane 0 takes a
+// relaxed agent-scope ticket; the block that draws the last ticket reads the
+// partials back with agent-scope atomic loads (sc1), so no L2 write-back or
+// invalidate is needed.  Returns true in that last block.
+template <typename T>
+__device__ __forceinline__ void st_sc1(T* p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// sc1 loads through a buffer resource: plain (non-atomic) loads, so the compiler
+// keeps many in flight, yet they bypass the stale-able caches like the stores
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ float ld_sc1_f32(__amdgpu_buffer_rsrc_t r, unsigned off_bytes) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off_bytes, 0, 16));
+}
+__device__ __forceinline__ double ld_sc1_f64(__amdgpu_buffer_rsrc_t r, unsigned off_bytes) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off_bytes, 0, 16));
+}
+
+__device__ __forceinline__ bool ticket(unsigned* ctr, unsigned n, float* flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned tk = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool last = tk == n - 1;
+        if (last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // reset
+        *flag = last ? 1.f : 0.f;
+    }
+    __syncthreads();
+    return *flag != 0.f;
+}
+
+// One launch: partial sums per (row chunk, channel slice) + two ticketed combine
+// levels + per-channel finalize.
 template <int MODE>
 __global__ __launch_bounds__(kT) void k_bn_reduce(ReduceArgs a) {
-    __shared__ float red[kFlag + 4];  // the one LDS object: row-group partials, flag, fp64 combine
+    __shared__ float red[kFlag + 4];  // the one LDS object: row-group partials, flag
     const int t = threadIdx.x;
-    const int C = a.C;
+    const int C = a.C, SW = a.SW;
+    const int rc = blockIdx.x, cs = blockIdx.y;
     const int tpr = 1 << a.tpr_log;
     const int cg = t & (tpr - 1);
     const int r0 = t >> a.tpr_log;
     const int rpp = kT >> a.tpr_log;
-    const long long vpr = C >> 3;  // vectors per row
+    const long long vpr = C >> 3;                     // 16-B vectors per row
+    const int c0 = cs * SW + cg * 8;                  // first channel of this thread
 
     float mu[8];
     if (MODE != FWD) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) mu[j] = a.save_mean[cg * 8 + j];
+        for (int j = 0; j < 8; ++j) mu[j] = a.save_mean[c0 + j];
     }
     float s1[8], s2[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
 
-    const long long rbeg = (long long)blockIdx.x * a.rpb;
+    const long long rbeg = (long long)rc * a.rpb;
     long long rend = rbeg + a.rpb;
     if (rend > a.M) rend = a.M;
     long long r = rbeg + r0;
-    for (; r + 3 * rpp < rend; r += 4 * rpp) {
-        const long long v = r * vpr + cg;
-        const long long st = (long long)rpp * vpr;
-        accum<MODE>(a, v, mu, s1, s2);
-        accum<MODE>(a, v + st, mu, s1, s2);
-        accum<MODE>(a, v + 2 * st, mu, s1, s2);
-        accum<MODE>(a, v + 3 * st, mu, s1, s2);
+    const long long cv = c0 >> 3;
+    const long long st = (long long)rpp * vpr;
+    for (; r + 7 * rpp < rend; r += 8 * rpp) {
+        const long long v = r * vpr + cv;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) accum<MODE>(a, v + u * st, mu, s1, s2);
     }
-    for (; r < rend; r += rpp) accum<MODE>(a, r * vpr + cg, mu, s1, s2);
+    for (; r < rend; r += rpp) accum<MODE>(a, r * vpr + cv, mu, s1, s2);
 
-    // row-group combine in LDS: red[r0][C][2]  (rpp * 2C == 4096 floats)
-    const int C2 = 2 * C;
+    // row-group combine in LDS: red[r0][SW][2]  (rpp * 2SW == 4096 floats)
+    const int S2w = 2 * SW;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        red[r0 * C2 + (cg * 8 + j) * 2] = s1[j];
-        red[r0 * C2 + (cg * 8 + j) * 2 + 1] = s2[j];
+        red[r0 * S2w + (cg * 8 + j) * 2] = s1[j];
+        red[r0 * S2w + (cg * 8 + j) * 2 + 1] = s2[j];
     }
     __syncthreads();
-    float* part = a.part + (size_t)blockIdx.x * C2;  // [nblk][C][2]
-    for (int col = t; col < C2; col += kT) {
+    float* p1 = a.part + ((size_t)cs * a.nrc + rc) * S2w;
+    if (t < S2w) {
         float acc = 0.f;
-        for (int i = 0; i < rpp; ++i) acc += red[i * C2 + col];
-        part[col] = acc;
+        for (int i = 0; i < rpp; ++i) acc += red[i * S2w + t];
+        st_sc1(&p1[t], acc);
     }
-    // hand-off: plain stores -> drain -> barrier -> agent release -> ticket
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        unsigned tk = __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        red[kFlag] = (tk == gridDim.x - 1) ? 1.f : 0.f;
+    // level 1: the last of a group of kG1 row chunks combines them (fp64)
+    const int g = rc / kG1;
+    const int g0 = g * kG1;
+    const int gs = min(kG1, a.nrc - g0);
+    unsigned* ctr = a.counter + (size_t)cs * (a.ng + 1);
+    if (!ticket(ctr + g, (unsigned)gs, &red[kFlag])) return;
+    double* p2 = a.part2 + ((size_t)cs * a.ng + g) * S2w;
+    if (t < S2w) {
+        const auto rq = rsrc_of(a.part + ((size_t)cs * a.nrc + g0) * S2w);
+        double acc = 0.0;
+#pragma unroll 8
+        for (int i = 0; i < gs; ++i) acc += (double)ld_sc1_f32(rq, (unsigned)(i * S2w + t) * 4u);
+        st_sc1(&p2[t], acc);
     }
-    __syncthreads();
-    if (red[kFlag] == 0.f) return;
-    if (t == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        *a.counter = 0u;  // leave the ticket at zero for the next call
-        if (MODE == FWD && a.nbt) *a.nbt += 1;
-    }
-    __syncthreads();
-
-    // last block: combine the nblk partial rows in fp64, in passes of <= kT float4
-    // columns (= 2*kT channels); thread = (float4 column, row group)
-    const int nb = gridDim.x;
-    const int ncol4 = C2 >> 2;
-    const int w4 = ncol4 < kT ? ncol4 : kT;
-    const int groups = kT / w4;
-    double* dred = reinterpret_cast<double*>(red);  // [groups][w4*4]
-    const float4* p4 = reinterpret_cast<const float4*>(a.part);
+    // level 2: the last group of the slice finalizes its SW channels
+    if (!ticket(ctr + a.ng, (unsigned)a.ng, &red[kFlag])) return;
+    if (MODE == FWD && a.nbt && cs == 0 && t == 0) *a.nbt += 1;
     const double invM = 1.0 / (double)a.M;
-    for (int base = 0; base < ncol4; base += w4) {
-        const int c4 = base + t % w4;
-        const int g = t / w4;
-        double acc[4] = {0.0, 0.0, 0.0, 0.0};
-        int b = g;
-        for (; b + 3 * groups < nb; b += 4 * groups) {
-            const float4 q0 = p4[(size_t)b * ncol4 + c4];
-            const float4 q1 = p4[(size_t)(b + groups) * ncol4 + c4];
-            const float4 q2 = p4[(size_t)(b + 2 * groups) * ncol4 + c4];
-            const float4 q3 = p4[(size_t)(b + 3 * groups) * ncol4 + c4];
-            acc[0] += ((double)q0.x + (double)q1.x) + ((double)q2.x + (double)q3.x);
-            acc[1] += ((double)q0.y + (double)q1.y) + ((double)q2.y + (double)q3.y);
-            acc[2] += ((double)q0.z + (double)q1.z) + ((double)q2.z + (double)q3.z);
-            acc[3] += ((double)q0.w + (double)q1.w) + ((double)q2.w + (double)q3.w);
+    if (t < SW) {
+        const auto rq = rsrc_of(a.part2 + (size_t)cs * a.ng * S2w);
+        double S1 = 0.0, S2 = 0.0;
+#pragma unroll 8
+        for (int i = 0; i < a.ng; ++i) {
+            S1 += ld_sc1_f64(rq, (unsigned)(i * S2w + 2 * t) * 8u);
+            S2 += ld_sc1_f64(rq, (unsigned)(i * S2w + 2 * t + 1) * 8u);
         }
-        for (; b < nb; b += groups) {
-            const float4 q = p4[(size_t)b * ncol4 + c4];
-            acc[0] += q.x; acc[1] += q.y; acc[2] += q.z; acc[3] += q.w;
-        }
-        __syncthreads();  // previous pass done with dred
-#pragma unroll
-        for (int j = 0; j < 4; ++j) dred[g * w4 * 4 + (t % w4) * 4 + j] = acc[j];
-        __syncthreads();
-        for (int cl = t; cl < w4 * 2; cl += kT) {  // channels of this pass
-            double S1 = 0.0, S2 = 0.0;
-            for (int i = 0; i < groups; ++i) {
-                S1 += dred[i * w4 * 4 + 2 * cl];
-                S2 += dred[i * w4 * 4 + 2 * cl + 1];
-            }
-            finalize<MODE>(a, base * 2 + cl, S1, S2, invM);
-        }
+        finalize<MODE>(a, cs * SW + t, S1, S2, invM);
     }
 }
 
@@ -399,19 +416,21 @@ extern "C" int gm_bn_fwd_train_bf16(const gm_bn_fwd* p, void* scratch, size_t by
     char* s = static_cast<char*>(scratch);
     ReduceArgs a{};
     a.M = p->M; a.C = p->C; a.tpr_log = pl.tpr_log; a.rpb = pl.rpb;
+    a.SW = pl.SW; a.nrc = pl.nrc; a.ng = pl.ng;
     a.x = static_cast<const uint4*>(p->x);
     a.gamma = p->gamma; a.beta = p->beta; a.rmean = p->running_mean; a.rvar = p->running_var;
     a.momentum = p->momentum; a.eps = p->eps;
     a.save_mean = p->save_mean; a.save_invstd = p->save_invstd;
     a.nbt = p->num_batches_tracked;
     a.counter = reinterpret_cast<unsigned*>(s);
-    a.coef = reinterpret_cast<float*>(s + kHdr);
-    a.part = a.coef + 4 * p->C;
+    a.coef = reinterpret_cast<float*>(s + pl.off_coef);
+    a.part = reinterpret_cast<float*>(s + pl.off_p1);
+    a.part2 = reinterpret_cast<double*>(s + pl.off_p2);
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(k_bn_reduce<FWD>, dim3(pl.nblk), dim3(kT), 0, st, a);
+    hipLaunchKernelGGL(k_bn_reduce<FWD>, dim3(pl.nrc, pl.nslice), dim3(kT), 0, st, a);
     if ((rc = check_launch("k_bn_reduce<fwd>"))) return rc;
     ApplyArgs b{};
-    b.nvec = p->M * (p->C / 8); b.tpr_log = pl.tpr_log; b.C = p->C; b.relu = p->relu;
+    b.nvec = p->M * (p->C / 8); b.tpr_log = ilog2(p->C / 8); b.C = p->C; b.relu = p->relu;
     b.x = a.x; b.res = static_cast<const uint4*>(p->residual); b.out = static_cast<uint4*>(p->y);
     b.coef = a.coef;
     const int g = apply_grid(b.nvec, p->C);
@@ -431,7 +450,7 @@ extern "C" int gm_bn_fwd_infer_bf16(const gm_bn_fwd* p, void* scratch, size_t by
     int rc = check_common(p->M, p->C, scratch, bytes, "gm_bn_fwd_infer_bf16");
     if (rc) return rc;
     char* s = static_cast<char*>(scratch);
-    float* coef = reinterpret_cast<float*>(s + kHdr);
+    float* coef = reinterpret_cast<float*>(s + make_plan(p->M, p->C).off_coef);
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(k_bn_infer_coef, dim3((p->C + 255) / 256), dim3(256), 0, st, p->C, p->gamma, p->beta,
                        p->running_mean, p->running_var, p->eps, coef);
@@ -461,6 +480,7 @@ extern "C" int gm_bn_bwd_bf16(const gm_bn_bwd* p, void* scratch, size_t bytes, v
     char* s = static_cast<char*>(scratch);
     ReduceArgs a{};
     a.M = p->M; a.C = p->C; a.tpr_log = pl.tpr_log; a.rpb = pl.rpb; a.relu = p->relu;
+    a.SW = pl.SW; a.nrc = pl.nrc; a.ng = pl.ng;
     a.accumulate = p->accumulate;
     a.x = static_cast<const uint4*>(p->x); a.dy = static_cast<const uint4*>(p->dy);
     a.y = static_cast<const uint4*>(p->y);
@@ -468,14 +488,15 @@ extern "C" int gm_bn_bwd_bf16(const gm_bn_bwd* p, void* scratch, size_t bytes, v
     a.save_mean = const_cast<float*>(p->save_mean); a.save_invstd = const_cast<float*>(p->save_invstd);
     a.dgamma = p->dgamma; a.dbeta = p->dbeta;
     a.counter = reinterpret_cast<unsigned*>(s);
-    a.coef = reinterpret_cast<float*>(s + kHdr);
-    a.part = a.coef + 4 * p->C;
+    a.coef = reinterpret_cast<float*>(s + pl.off_coef);
+    a.part = reinterpret_cast<float*>(s + pl.off_p1);
+    a.part2 = reinterpret_cast<double*>(s + pl.off_p2);
     hipStream_t st = as_stream(stream);
-    if (p->relu) hipLaunchKernelGGL(k_bn_reduce<BWD_RELU>, dim3(pl.nblk), dim3(kT), 0, st, a);
-    else hipLaunchKernelGGL(k_bn_reduce<BWD>, dim3(pl.nblk), dim3(kT), 0, st, a);
+    if (p->relu) hipLaunchKernelGGL(k_bn_reduce<BWD_RELU>, dim3(pl.nrc, pl.nslice), dim3(kT), 0, st, a);
+    else hipLaunchKernelGGL(k_bn_reduce<BWD>, dim3(pl.nrc, pl.nslice), dim3(kT), 0, st, a);
     if ((rc = check_launch("k_bn_reduce<bwd>"))) return rc;
     ApplyArgs b{};
-    b.nvec = p->M * (p->C / 8); b.tpr_log = pl.tpr_log; b.C = p->C; b.relu = p->relu;
+    b.nvec = p->M * (p->C / 8); b.tpr_log = ilog2(p->C / 8); b.C = p->C; b.relu = p->relu;
     b.x = a.x; b.res = a.y; b.dy = a.dy; b.out = static_cast<uint4*>(p->dx);
     b.out2 = static_cast<uint4*>(p->dres); b.coef = a.coef;
     const int g = apply_grid(b.nvec, p->C);

@@ -206,7 +206,7 @@ int gm_conv2d_wgrad_bf16(const gm_conv_desc* d, const void* dy, const void* x, f
  * backward: dz = dy * (y > 0) if relu else dy;  dres = dz (if non-NULL);
  *         dx = BN backward(dz); dgamma/dbeta written (or added if accumulate).
  * C must be a power of two in [8, 2048].  scratch >= gm_bn_scratch(M, C) bytes,
- * ZEROED ONCE before first use; each call leaves its ticket word at zero again.
+ * ZEROED ONCE before first use; each call leaves its ticket words at zero again.
  * Calls sharing one scratch buffer must be stream-ordered.
  * ------------------------------------------------------------------------- */
 typedef struct gm_bn_fwd {

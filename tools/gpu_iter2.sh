@@ -2,7 +2,7 @@
 # tests that touch the engine/MMTM + eager and graph bench + rocprof of the graph bench
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 > gpurun_out/iter_tests.log 2>&1
+timeout -k 10 900 python -m pytest tests -m gpu -q ${PYTEST_K:+-k "$PYTEST_K"} -p no:cacheprovider --timeout 300 > gpurun_out/iter_tests.log 2>&1
 rc=$?
 tail -5 gpurun_out/iter_tests.log
 [ $rc -eq 0 ] || exit 1
