@@ -272,6 +272,180 @@ __global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
     }
 }
 
+// Lean variant for C >= 64 (a 64-wide k-tile lies inside one tap) and <= 32 taps:
+//  * per-row tap validity precomputed as a bitmask (one bit test per DMA, no bounds math),
+//  * wave index in an SGPR, so every LDS-DMA destination (M0) is scalar arithmetic,
+//  * per-lane LDS fragment offsets precomputed and the k-loop unrolled by the two
+//    buffers, so every ds_read_b128 is base VGPR + immediate (no address VALU),
+//  * the tap-table entry of the next k-tile is read one step ahead.
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
+    constexpr int BK = 64;
+    constexpr int AR = BM / 32, BR = BN / 32;
+    constexpr int MT = BM / 64, NT = BN / 64;
+    constexpr int SA = BM * 128, SB = BN * 128;  // bytes per stage
+    extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+    char* lds = reinterpret_cast<char*>(smem);   // [A0][A1][B0][B1][taps]
+
+    int ci = 0;
+#pragma unroll
+    for (int q = 1; q < kMaxCls; ++q)
+        if (q < a.ncls && (int)blockIdx.x >= a.cls[q].tile_start) ci = q;
+    const ConvCls& cl = a.cls[ci];
+    const int wgid = blockIdx.x - cl.tile_start;
+    const int tm = wgid % cl.tiles_m, tn = wgid / cl.tiles_m;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int PQ = cl.P * cl.Q;
+    const int M = a.N * PQ;
+    const int nk = (cl.ntap * a.C) / BK;
+
+    const int t = threadIdx.x;
+    const int lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    int* tapt = reinterpret_cast<int*>(lds + 2 * (SA + SB));
+#pragma unroll
+    for (int i = 0; i < kMaxTap; ++i)
+        if (t == i && i < cl.ntap)
+            tapt[i] = (int)cl.tw[i] | ((int)(cl.dh[i] + 128) << 8) | ((int)(cl.dw[i] + 128) << 16);
+    __syncthreads();
+    const int wm = wave >> 1, wn = wave & 1;
+    const int slot = lane & 7;
+
+    const uint16_t* a_ptr[AR];
+    unsigned a_vm[AR];
+#pragma unroll
+    for (int j = 0; j < AR; ++j) {
+        const int row = (wave * AR + j) * 8 + (lane >> 3);
+        const int m = m0 + row;
+        const int gc = slot ^ ((row >> 1) & 7);
+        unsigned vm = 0;
+        a_ptr[j] = a.in + gc * 8;
+        if (m < M) {
+            const int b = m / PQ, pq = m - b * PQ;
+            const int p = pq / cl.Q, q = pq - p * cl.Q;
+            const int h = p * a.sA, w = q * a.sA;
+            a_ptr[j] = a.in + ((size_t)((b * a.Hi + h) * a.Wi + w) << a.logC) + gc * 8;
+            for (int tp = 0; tp < cl.ntap; ++tp) {
+                const int te = tapt[tp];
+                const int hi = h + ((te >> 8) & 0xff) - 128, wi = w + ((te >> 16) & 0xff) - 128;
+                if ((unsigned)hi < (unsigned)a.Hi && (unsigned)wi < (unsigned)a.Wi) vm |= 1u << tp;
+            }
+        }
+        a_vm[j] = vm;
+    }
+    const uint16_t* b_ptr[BR];
+    bool b_ok[BR];
+#pragma unroll
+    for (int j = 0; j < BR; ++j) {
+        const int row = (wave * BR + j) * 8 + (lane >> 3);
+        const int n = n0 + row;
+        const int gc = slot ^ ((row >> 1) & 7);
+        b_ok[j] = n < a.Nout;
+        b_ptr[j] = a.wt + (size_t)(b_ok[j] ? n : 0) * a.T * a.C + gc * 8;
+    }
+    // per-lane fragment byte offsets inside a stage: row*128 + swizzled 16-B chunk
+    const int fr = lane & 31, fh = lane >> 5;
+    int a_rd[MT][4], b_rd[NT][4];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+        const int row = wm * (BM / 2) + i * 32 + fr;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) a_rd[i][ks] = row * 128 + (swz(row, ks * 2 + fh) << 4);
+    }
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const int row = wn * (BN / 2) + j * 32 + fr;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) b_rd[j][ks] = 2 * SA + row * 128 + (swz(row, ks * 2 + fh) << 4);
+    }
+
+    typedef __attribute__((address_space(1))) const void* gptr_t;
+    typedef __attribute__((address_space(3))) void* lptr_t;
+    int te_next = tapt[0];
+    auto issue = [&](int kt, int buf) {
+        const int k = kt * BK;
+        const int tap = k >> a.logC;
+        const int te = __builtin_amdgcn_readfirstlane(te_next);
+        const int dh = ((te >> 8) & 0xff) - 128, dw = ((te >> 16) & 0xff) - 128;
+        const int c0 = k & (a.C - 1);
+        const long aoff = (long)(((dh * a.Wi + dw) << a.logC) + c0);
+        const long boff = (long)((te & 0xff) * a.C + c0);
+        const int knext = k + BK;
+        te_next = tapt[knext < cl.ntap * a.C ? (knext >> a.logC) : 0];
+#pragma unroll
+        for (int j = 0; j < AR; ++j) {
+            const bool ok = (a_vm[j] >> tap) & 1u;
+            const void* src = ok ? (const void*)(a_ptr[j] + aoff) : (const void*)g_zero16;
+            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + buf * SA + (wave * AR + j) * 1024), 16, 0,
+                                             0);
+        }
+#pragma unroll
+        for (int j = 0; j < BR; ++j) {
+            const void* src = b_ok[j] ? (const void*)(b_ptr[j] + boff) : (const void*)g_zero16;
+            __builtin_amdgcn_global_load_lds((gptr_t)src,
+                                             (lptr_t)(lds + 2 * SA + buf * SB + (wave * BR + j) * 1024), 16, 0, 0);
+        }
+    };
+
+    floatx16 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    auto compute = [&](int buf) {
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            bf16x8 af[MT], bfr[NT];
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+                af[i] = *reinterpret_cast<const bf16x8*>(lds + buf * SA + a_rd[i][ks]);
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+                bfr[j] = *reinterpret_cast<const bf16x8*>(lds + buf * SB + b_rd[j][ks]);
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+        }
+    };
+    issue(0, 0);
+    __syncthreads();
+    int kt = 0;
+    for (; kt + 1 < nk; kt += 2) {  // tiles kt (buffer 0) and kt+1 (buffer 1)
+        issue(kt + 1, 1);
+        compute(0);
+        __syncthreads();
+        if (kt + 2 < nk) issue(kt + 2, 0);
+        compute(1);
+        __syncthreads();
+    }
+    if (kt < nk) compute(0);  // odd tile count: the last tile sits in buffer 0
+
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+        const int m = m0 + wm * (BM / 2) + i * 32 + fr;
+        if (m >= M) continue;
+        const int b = m / PQ, pq = m - b * PQ;
+        const int p = pq / cl.Q, q = pq - p * cl.Q;
+        const int ho = p * cl.oS + cl.oH, wo = q * cl.oS + cl.oW;
+        uint16_t* dst = cl.out + ((size_t)(b * a.Ho + ho) * a.Wo + wo) * a.Nout;
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int gq = 0; gq < 4; ++gq) {
+                const int n = n0 + wn * (BN / 2) + j * 32 + 8 * gq + 4 * fh;
+                if (n >= a.Nout) continue;
+                uint2 v;
+                v.x = pack_bf2(acc[i][j][4 * gq], acc[i][j][4 * gq + 1]);
+                v.y = pack_bf2(acc[i][j][4 * gq + 2], acc[i][j][4 * gq + 3]);
+                *(uint2*)(dst + n) = v;
+            }
+    }
+}
+
 // zero the output pixels no dgrad class covers (e.g. odd pixels of a 1x1/s2 dgrad)
 __global__ void k_zero_bf16(uint16_t* p, size_t n) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -297,6 +471,14 @@ static int ilog2(int v) {
 
 using namespace gm;
 
+static bool lean_path() {
+    static bool on = [] {
+        const char* e = getenv("GM_CONV_LEAN");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 template <int BM, int BN, int ST>
 static int launch_igemm(ConvArgs& a, hipStream_t st) {
     int tiles = 0;
@@ -317,10 +499,22 @@ static int launch_igemm(ConvArgs& a, hipStream_t st) {
                             (int)lds);
         attr_set = true;
     }
-    if (a.C >= 64)
+    int maxtap = 0;
+    for (int i = 0; i < a.ncls; ++i) maxtap = a.cls[i].ntap > maxtap ? a.cls[i].ntap : maxtap;
+    if (a.C >= 64 && maxtap <= 32 && lean_path()) {
+        const size_t lds2 = (size_t)2 * (BM + BN) * 128 + kMaxTap * 4 + 12;
+        static bool attr2 = false;
+        if (!attr2) {
+            hipFuncSetAttribute((const void*)k_conv_igemm_ut<BM, BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds2);
+            attr2 = true;
+        }
+        k_conv_igemm_ut<BM, BN><<<tiles, 256, lds2, st>>>(a);
+    } else if (a.C >= 64) {
         k_conv_igemm<BM, BN, true, ST><<<tiles, 256, lds, st>>>(a);
-    else
+    } else {
         k_conv_igemm<BM, BN, false, ST><<<tiles, 256, lds, st>>>(a);
+    }
     return check_launch("k_conv_igemm");
 }
 
