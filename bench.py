@@ -26,6 +26,7 @@ sys.path.insert(0, ROOT)
 
 N_PARAMS = 23_773_008
 HBM_PEAK_GBS = 8000.0
+MFMA_PEAK_TFS = 2500.0  # dense bf16 (MI355X_MICROARCH.md)
 
 
 def parse():
@@ -71,8 +72,55 @@ def cpu_baseline(seconds, size):
                       f"{torch.get_num_threads()} threads, {os.cpu_count()} visible CPUs"}
 
 
+# trunk convolutions of one view at B (ResNet-18 at 224^2): (C, H, W, K, R, stride, pad, count)
+TRUNK = [(3, 224, 224, 64, 7, 2, 3, 1), (64, 56, 56, 64, 3, 1, 1, 4), (64, 56, 56, 128, 3, 2, 1, 1),
+         (64, 56, 56, 128, 1, 2, 0, 1), (128, 28, 28, 128, 3, 1, 1, 3), (128, 28, 28, 256, 3, 2, 1, 1),
+         (128, 28, 28, 256, 1, 2, 0, 1), (256, 14, 14, 256, 3, 1, 1, 3), (256, 14, 14, 512, 3, 2, 1, 1),
+         (256, 14, 14, 512, 1, 2, 0, 1), (512, 7, 7, 512, 3, 1, 1, 3)]
+
+
+def time_trunk_igemm(B, dev, reps=10):
+    """Roofline of the dominant kernel family, the implicit-GEMM convolution
+    (k_conv_igemm*: forward and input-gradient launches of every trunk shape of one
+    view): algorithmic FLOPs / summed average launch time, HIP events on the launch
+    stream behind a device sleep (kernel time, not host enqueue time)."""
+    from greedy_multimodal_learning_amd import conv as G
+    CL = torch.channels_last
+    flops = secs = 0.0
+    launches = 0
+    for (C, H, W, K, R, st, pad, cnt) in TRUNK:
+        Cp = G._cpad(C)
+        P, Q = (H + 2 * pad - R) // st + 1, (W + 2 * pad - R) // st + 1
+        x = torch.randn(B, Cp, H, W, device=dev).bfloat16().contiguous(memory_format=CL)
+        w = torch.randn(K, Cp, R, R, device=dev).bfloat16().contiguous(memory_format=CL)
+        dy = torch.randn(B, K, P, Q, device=dev).bfloat16().contiguous(memory_format=CL)
+        wt = w.permute(1, 0, 2, 3).contiguous(memory_format=CL)
+        ops = [lambda: G.conv_fwd(x, w, st, pad)]
+        if C != 3:  # the stem's input gradient is never computed
+            ops.append(lambda: G.conv_dgrad_t(dy, wt, H, W, st, pad))
+        for op in ops:
+            op()
+            torch.cuda.synchronize()
+            torch.cuda._sleep(20_000_000)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                op()
+            e1.record()
+            torch.cuda.synchronize()
+            secs += e0.elapsed_time(e1) / reps / 1e3 * cnt
+            flops += 2.0 * B * P * Q * K * C * R * R * cnt  # real (unpadded) channels
+            launches += cnt
+    return flops, secs, launches
+
+
 def time_group_sumsq(step, n):
+    """Average duration of the fused norms+SGD launch, HIP events on its stream; a
+    leading ~20 ms device sleep keeps the GPU busy while the host enqueues, so the
+    events bracket kernel time, not host launch latency."""
     stream = torch.cuda.current_stream()
+    torch.cuda.synchronize()
+    torch.cuda._sleep(50_000_000)
     evs = []
     for _ in range(n):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -148,6 +196,7 @@ def main():
     # roofline kernel: the fused per-branch norms + SGD pass (k_group_sumsq<SGD>), the
     # same launch the step runs (inside the graph), timed with HIP events on its stream
     kern_avg_s = time_group_sumsq(step, 10)
+    conv_flops, conv_s, conv_launches = time_trunk_igemm(B, dev)
 
     if rank == 0:
         views = 2
@@ -175,11 +224,18 @@ def main():
                        "parallelism": f"dp{world}", "samples_per_s": round(world * B * a.steps / elapsed, 2),
                        "hipgraph": bool(step.graphs),
                        "curation_steps_timed": curation_steps, "final_loss": round(loss, 4)},
-            "roofline": {"kernel": "k_group_sumsq<SGD> (fused per-branch norms + SGD, gm_group_sumsq)",
-                         "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "alg_bytes_per_launch": bytes_alg,
-                         "avg_launch_us": round(kern_avg_s * 1e6, 2)},
+            "roofline": {"kernel": "k_conv_igemm_ut / k_conv_igemm (bf16 implicit-GEMM conv, fwd + dgrad, "
+                                   "all trunk shapes of one view at the step's batch)",
+                         "bound": "mfma", "achieved": round(conv_flops / conv_s / 1e12, 1),
+                         "peak": MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                         "frac": round(conv_flops / conv_s / 1e12 / MFMA_PEAK_TFS, 4), "traffic": None,
+                         "alg_flops_per_launch": round(conv_flops / conv_launches),
+                         "avg_launch_us": round(conv_s / conv_launches * 1e6, 2)},
+            "roofline_hbm": {"kernel": "k_group_sumsq<SGD> (fused per-branch norms + SGD, gm_group_sumsq)",
+                             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                             "traffic": traffic, "alg_bytes_per_launch": bytes_alg,
+                             "avg_launch_us": round(kern_avg_s * 1e6, 2)},
         }
         if not a.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(a.cpu_seconds, a.size)
