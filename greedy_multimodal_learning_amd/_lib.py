@@ -126,7 +126,14 @@ EXPORTS.update({
     "gm_conv_weight_prep_bf16": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "gm_conv2d_wgrad_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
                                      c_size_t, c_void_p]),
+    "gm_wprep_tiles": (c_int, [c_int, c_int, c_int]),
+    "gm_conv_weight_prep_multi_bf16": (c_int, [c_void_p, c_int, c_int, c_void_p]),
 })
+
+
+class WPrep(ctypes.Structure):
+    _fields_ = [("w", c_void_p), ("wb", c_void_p), ("wt", c_void_p), ("K", c_int), ("RS", c_int),
+                ("C", c_int), ("Cp", c_int), ("tile_start", c_int), ("pad", c_int)]
 
 
 class BnFwd(ctypes.Structure):

@@ -127,6 +127,7 @@ class _MMTMFunction(torch.autograd.Function):
         ctx.meta = (B, Cv, Cs, Cz, HWv, HWs, lay, dt, mode, share, live_v, live_s,
                     ld_sv, ld_ss, cfg.get("avg_v"), cfg.get("avg_s"), cfg["zero_curated"])
         ctx.mark_non_differentiable(e_v, e_s, sq)
+        ctx.set_materialize_grads(False)  # no zero-filled grads for the side outputs
         return yv, ys, e_v, e_s, sq
 
     @staticmethod

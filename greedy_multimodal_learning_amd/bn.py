@@ -29,10 +29,13 @@ _scratch = {}
 
 
 def _get_scratch(device, M, C):
-    """Per-device BN scratch (ticket word + coefficients + partials), zeroed once
-    at allocation; the kernels leave the ticket at zero."""
+    """Per-(device, stream) BN scratch (ticket word + coefficients + partials),
+    zeroed once at allocation; the kernels leave the ticket at zero.  One buffer
+    per stream: the trunks run on separate streams concurrently (streams.py), and
+    two BN launches in flight must not share tickets."""
     need = L.load().gm_bn_scratch(M, C)
-    key = device.index if device.index is not None else torch.cuda.current_device()
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    key = (idx, torch.cuda.current_stream(idx).stream_id)
     buf = _scratch.get(key)
     if buf is None or buf.numel() < need:
         size = max(need, 1 << 20) if buf is None else max(need, 2 * buf.numel())

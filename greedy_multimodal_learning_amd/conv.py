@@ -109,6 +109,73 @@ def weight_prep(weight, Cp, transposed):
     return wb, wt
 
 
+_prepped = {}  # weight data_ptr -> (wb, wt): bf16 copies made by an active WeightPrep
+
+
+class WeightPrep:
+    """bf16 copies of every GMConv2d weight of a model, made by ONE launch per step
+    (gm_conv_weight_prep_multi_bf16) instead of one prep launch per convolution.
+    The engine runs it at the start of a step and activates the copies for that
+    step's forward only (a weight changed outside the step is never served stale)."""
+
+    def __init__(self, model):
+        lib = L.load()
+        convs = [m for m in model.modules() if isinstance(m, GMConv2d)]
+        dev = next(model.parameters()).device
+        specs, total = [], 0
+        for m in convs:
+            K, C, R, S = m.weight.shape
+            Cp = _cpad(C)
+            want_t = C >= 8  # the stem's input (RGB) never needs an input gradient
+            n = K * R * S * Cp
+            specs.append((m.weight, K, C, R, S, Cp, want_t, total))
+            total += n * (2 if want_t else 1)
+        self.buf = torch.empty(max(total, 1), device=dev, dtype=torch.bfloat16)
+        self.copies = []
+        items, tiles = [], 0
+        for (w, K, C, R, S, Cp, want_t, off) in specs:
+            n = K * R * S * Cp
+            wb = self.buf[off:off + n].view(K, R, S, Cp).permute(0, 3, 1, 2)
+            wt = self.buf[off + n:off + 2 * n].view(Cp, R, S, K).permute(0, 3, 1, 2) if want_t else None
+            self.copies.append((w, wb, wt))
+            items.append(L.WPrep(0, wb.data_ptr(), L.ptr(wt), K, R * S, C, Cp, tiles, 0))
+            tiles += lib.gm_wprep_tiles(K, R * S, Cp)
+        self.items = items
+        self.tiles = tiles
+        self.table = None
+        self._ptrs = None
+
+    def _refresh_table(self):
+        """(Re)build the device table when parameter storage moved (FlatParams)."""
+        ptrs = tuple(w.data_ptr() for (w, _, _) in self.copies)
+        if self.table is not None and ptrs == self._ptrs:
+            return
+        for it, (w, _, _), p in zip(self.items, self.copies, ptrs):
+            if w.dtype != torch.float32 or not w.is_contiguous(memory_format=CL):
+                raise RuntimeError("WeightPrep: conv weights must be fp32 channels_last (KRSC)")
+            it.w = p
+        raw = bytes(L.arr(L.WPrep, self.items))
+        host = torch.frombuffer(bytearray(raw), dtype=torch.uint8)
+        self.table = host.to(self.buf.device)
+        self._ptrs = ptrs
+
+    def run(self):
+        if not self.copies:
+            return
+        self._refresh_table()
+        L.check(L.load().gm_conv_weight_prep_multi_bf16(self.table.data_ptr(), len(self.items), self.tiles,
+                                                        L.stream_of(self.buf.device)),
+                "gm_conv_weight_prep_multi_bf16")
+
+    def activate(self):
+        for (w, wb, wt) in self.copies:
+            _prepped[w.data_ptr()] = (wb, wt)
+
+    @staticmethod
+    def deactivate():
+        _prepped.clear()
+
+
 def conv_dgrad_t(dy, wt, H, W, stride, pad):
     """dgrad from an already transposed bf16 weight wt [C,K,R,S] (channels_last)."""
     lib = L.load()
@@ -130,7 +197,11 @@ class _ConvFn(torch.autograd.Function):
         if Cp != C0:
             xb = _pad_c(xb, Cp)
         need_dx = ctx.needs_input_grad[0]
-        wb, wt = weight_prep(weight, Cp, need_dx)
+        pre = _prepped.get(weight.data_ptr()) if _prepped else None
+        if pre is not None and (pre[1] is not None or not need_dx):
+            wb, wt = pre
+        else:
+            wb, wt = weight_prep(weight, Cp, need_dx)
         y = conv_fwd(xb, wb, stride, pad)
         ctx.save_for_backward(xb, wt, weight)
         ctx.meta = (stride, pad, C0, x.shape[2], x.shape[3], weight.shape[2], weight.shape[3])

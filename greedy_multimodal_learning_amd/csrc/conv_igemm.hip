@@ -656,3 +656,53 @@ extern "C" int gm_conv_weight_prep_bf16(const float* w, int K, int RS, int C, in
                                                                        (uint16_t*)wt);
     return gm::check_launch("k_weight_prep");
 }
+
+// Multi-tensor weight prep: every trunk convolution of a step in ONE launch.  One
+// workgroup per 64(k) x 64(c) tile of one tap of one weight: fp32 loads coalesced
+// along c, the bf16 KRSC copy written along c, the tile transposed through LDS so the
+// [C][RS][K] dgrad copy is also written along k.
+__global__ __launch_bounds__(256) void k_wprep_multi(const gm_wprep* __restrict__ tab, int n) {
+    __shared__ uint16_t tile[64][66];
+    const int blk = blockIdx.x;
+    int lo = 0, hi = n - 1;  // last entry whose tile_start <= blk (uniform: scalar loads)
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (tab[mid].tile_start <= blk) lo = mid;
+        else hi = mid - 1;
+    }
+    const float* w = tab[lo].w;
+    uint16_t* wb = static_cast<uint16_t*>(tab[lo].wb);
+    uint16_t* wt = static_cast<uint16_t*>(tab[lo].wt);
+    const int K = tab[lo].K, RS = tab[lo].RS, C = tab[lo].C, Cp = tab[lo].Cp;
+    int r = blk - tab[lo].tile_start;
+    const int tc = (Cp + 63) >> 6;
+    const int ci = r % tc;
+    r /= tc;
+    const int tap = r % RS, k0 = (r / RS) * 64, c0 = ci * 64;
+    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+        const int kk = i >> 6, cc = i & 63;
+        const int k = k0 + kk, c = c0 + cc;
+        const float v = (k < K && c < C) ? w[((size_t)k * RS + tap) * C + c] : 0.f;
+        const uint16_t h = gm::Elem<uint16_t>::f2bf(v);
+        if (k < K && c < Cp) wb[((size_t)k * RS + tap) * Cp + c] = h;
+        tile[kk][cc] = h;
+    }
+    if (!wt) return;
+    __syncthreads();
+    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+        const int cc = i >> 6, kk = i & 63;
+        const int k = k0 + kk, c = c0 + cc;
+        if (k < K && c < Cp) wt[((size_t)c * RS + tap) * K + k] = tile[kk][cc];
+    }
+}
+
+extern "C" int gm_wprep_tiles(int K, int RS, int Cp) {
+    if (K <= 0 || RS <= 0 || Cp <= 0) return 0;
+    return ((K + 63) / 64) * RS * ((Cp + 63) / 64);
+}
+
+extern "C" int gm_conv_weight_prep_multi_bf16(const gm_wprep* table, int n, int total_tiles, void* stream) {
+    GM_REQUIRE(table && n > 0 && total_tiles > 0, "weight prep multi: bad args");
+    k_wprep_multi<<<total_tiles, 256, 0, gm::as_stream(stream)>>>(table, n);
+    return gm::check_launch("k_wprep_multi");
+}

@@ -35,6 +35,8 @@ import torch.distributed as dist
 from .callbacks import GroupNorms
 from .gradsink import GradSink
 from .losses import blend_loss
+from .streams import all_side_streams, side_stream
+from .streams import enabled as streams_enabled
 
 
 class _Flags:
@@ -115,6 +117,12 @@ class GradBuckets:
     def reset(self):
         self._pending = [len(ps) for (_, _, ps) in self.buckets]
         self._works = []
+        g = self.flat.grad
+        # the step's compute streams: main (current at step start) + the trunks' side
+        # streams; a bucket's gradients may come from any of them
+        self._streams = ([torch.cuda.current_stream(g.device)] + all_side_streams(g.device)) if g.is_cuda else []
+        if g.is_cuda and getattr(self, "_comm", None) is None:
+            self._comm = torch.cuda.Stream(device=g.device)
 
     def _on_grad(self, p):
         bi = self.bucket_of[p]
@@ -127,7 +135,17 @@ class GradBuckets:
 
     def _launch(self, bi):
         s, e, _ = self.buckets[bi]
-        self._works.append(dist.all_reduce(self.flat.grad[s:e], group=self.pg, async_op=True))
+        t = self.flat.grad[s:e]
+        if self._streams:
+            # issue from a comm stream that waits for every compute stream, so the
+            # collective sees gradients written on any of them
+            comm = self._comm
+            for st in self._streams:
+                comm.wait_stream(st)
+            with torch.cuda.stream(comm):
+                self._works.append(dist.all_reduce(t, group=self.pg, async_op=True))
+        else:
+            self._works.append(dist.all_reduce(t, group=self.pg, async_op=True))
         self._pending[bi] = -1
 
     def finish(self):
@@ -157,6 +175,9 @@ class BalancedStep:
         named = list(model.named_parameters())
         self.flat = FlatParams(model, channels_last)
         self.flat_grad = self.flat.grad
+        if self.device.type == "cuda" and streams_enabled():
+            for i in range(int(getattr(model, "num_views", 2)) - 1):
+                side_stream(self.device, i)  # created up front: the DP buckets wait on them
         self.norms = GroupNorms(named, list(branchnames), list(MMTMnames))
         if gate is not None:
             gate.set_model(model, ignore=False)
@@ -175,6 +196,10 @@ class BalancedStep:
         self.last_loss = None
         self.step_count = 0
         self.timer = None  # optional (start_event, end_event) list collector for the fused pass
+        self.wprep = None
+        if self.device.type == "cuda" and channels_last and compute_dtype == torch.bfloat16:
+            from .conv import WeightPrep
+            self.wprep = WeightPrep(model)
         self.graphs = bool(graphs) and self.world == 1 and self.device.type == "cuda"
         self._graphs = {}
         self._gpool = None
@@ -194,12 +219,26 @@ class BalancedStep:
         if self.buckets is not None:
             self.buckets.reset()
         self.sink.begin_step()
+        wp = self.wprep
         try:
+            if wp is not None:
+                wp.run()  # bf16 copies of every conv weight, one launch
+                wp.activate()
             _, outs, _, _ = self.forward(x)
+            if wp is not None:
+                wp.deactivate()
             loss = blend_loss([o.float() for o in outs], y)
             loss.backward()
+            if self.device.type == "cuda":
+                # backward nodes of the side-stream trunks ran on their streams (some of
+                # them write gradients in place, outside autograd's leaf-stream sync)
+                cur = torch.cuda.current_stream(self.device)
+                for s in all_side_streams(self.device):
+                    cur.wait_stream(s)
         finally:
             self.sink.end_step()
+            if wp is not None:
+                wp.deactivate()
         if self.buckets is not None:
             self.buckets.finish()
         return loss

@@ -16,6 +16,7 @@ from .balanced_mmtm import MMTM_mitigate as MMTM
 from .balanced_mmtm import get_rescale_weights
 from .gin_lite import configurable
 from .resnet import resnet18
+from .streams import ViewStreams
 
 CLASSNAMES = ['airplane', 'bathtub', 'bed', 'bench', 'bookshelf', 'bottle', 'bowl', 'car', 'chair',
               'cone', 'cup', 'curtain', 'desk', 'door', 'dresser', 'flower_pot', 'glass_box',
@@ -53,22 +54,38 @@ class MMTM_MVCNN(nn.Module):
     def _stem(net, x):
         return net.layer1(net.maxpool(net.bn1(net.conv1(x), relu=True)))  # relu fused into bn1
 
+    @staticmethod
+    def _head(net, f):
+        return net.fc(torch.flatten(net.avgpool(f), 1))
+
     def forward(self, x, curation_mode=False, caring_modality=None):
+        # view 1's trunk segments run on a side HIP stream (streams.py): the two
+        # trunks only meet at the MMTM sites, which run on the main stream
+        vs = ViewStreams.for_tensor(x, 2)
+        run = vs.run if vs is not None else (lambda i, fn, *a: fn(*a))
+        if vs is not None:
+            vs.fork()
+        f1 = run(1, self._stem, self.net_view_1, x[:, 1])
         f0 = self._stem(self.net_view_0, x[:, 0])
-        f1 = self._stem(self.net_view_1, x[:, 1])
         scales, squeezed = [], []
         for i in (2, 3, 4):
+            f1 = run(1, getattr(self.net_view_1, f"layer{i}"), f1)
             f0 = getattr(self.net_view_0, f"layer{i}")(f0)
-            f1 = getattr(self.net_view_1, f"layer{i}")(f1)
+            if vs is not None:
+                vs.join([f1])
             f0, f1, sc, sq = getattr(self, f"mmtm{i}")(
                 f0, f1, self.saving_mmtm_scales, self.saving_mmtm_squeeze_array,
                 turnoff_cross_modal_flow=bool(self.mmtm_off),
                 average_squeezemaps=self.mmtm_rescale[i - 1] if self.mmtm_off else None,
                 curation_mode=curation_mode, caring_modality=caring_modality)
+            if vs is not None:
+                vs.fork([(1, f1)])
             scales.append(sc)
             squeezed.append(sq)
-        x0 = self.net_view_0.fc(torch.flatten(self.net_view_0.avgpool(f0), 1))
-        x1 = self.net_view_1.fc(torch.flatten(self.net_view_1.avgpool(f1), 1))
+        x1 = run(1, self._head, self.net_view_1, f1)
+        x0 = self._head(self.net_view_0, f0)
+        if vs is not None:
+            vs.join([x1])
         return (x0 + x1) / 2, [x0, x1], scales, squeezed
 
 
@@ -108,14 +125,30 @@ class MMTM_MVCNN_N(nn.Module):
 
     def forward(self, x, curation_mode=False, caring_modality=None):
         nets = [getattr(self, f"net_view_{i}") for i in range(self.num_views)]
-        fs = [MMTM_MVCNN._stem(n, x[:, i]) for i, n in enumerate(nets)]
+        vs = ViewStreams.for_tensor(x, self.num_views)
+        run = vs.run if vs is not None else (lambda i, fn, *a: fn(*a))
+        order = list(range(self.num_views))[::-1]  # side streams first, main last
+        if vs is not None:
+            vs.fork()
+        fs = [None] * self.num_views
+        for i in order:
+            fs[i] = run(i, MMTM_MVCNN._stem, nets[i], x[:, i])
         scales, squeezed = [], []
         for li in (2, 3, 4):
-            fs = [getattr(n, f"layer{li}")(f) for n, f in zip(nets, fs)]
+            for i in order:
+                fs[i] = run(i, getattr(nets[i], f"layer{li}"), fs[i])
+            if vs is not None:
+                vs.join(fs[1:])
             fs, sc, sq = getattr(self, f"mmtm{li}")(
                 fs, self.saving_mmtm_scales, self.saving_mmtm_squeeze_array, curation_mode=curation_mode,
                 caring_modality=caring_modality if caring_modality is not None else 0)
+            if vs is not None:
+                vs.fork(list(enumerate(fs)))
             scales.append(sc)
             squeezed.append(sq)
-        outs = [n.fc(torch.flatten(n.avgpool(f), 1)) for n, f in zip(nets, fs)]
+        outs = [None] * self.num_views
+        for i in order:
+            outs[i] = run(i, MMTM_MVCNN._head, nets[i], fs[i])
+        if vs is not None:
+            vs.join(outs[1:])
         return sum(outs) / len(outs), outs, scales, squeezed

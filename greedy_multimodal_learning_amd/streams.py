@@ -1,0 +1,82 @@
+"""Per-view HIP streams for the unshared trunks.
+
+The reference runs its two ResNet trunks one after the other on one stream
+(src/model.py:65-106).  The trunks are independent between the MMTM sites, so
+here view i > 0 runs on its own HIP stream: small-map layers (layer3/4, their
+BatchNorms) of the two views then fill the 256 CUs together instead of leaving
+most of them idle.  PyTorch's autograd runs every backward node on the stream
+its forward ran on, so backward overlaps the same way; the engine's whole-step
+hipGraph capture records the fork/join edges as graph dependencies.
+
+    vs = ViewStreams.for_tensor(x, n_views)     # None on CPU / when disabled
+    vs.fork()                                   # side streams wait for main
+    f1 = vs.run(1, trunk_1, x1)                 # enqueued on side stream 0
+    ...
+    vs.join([f1])                               # main waits; f1 recorded on main
+
+Disable with GM_VIEW_STREAMS=0 (A/B measurements).
+"""
+import os
+
+import torch
+
+_side = {}
+
+
+def enabled():
+    return os.environ.get("GM_VIEW_STREAMS", "1") != "0"
+
+
+def side_stream(device, i):
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    key = (idx, i)
+    s = _side.get(key)
+    if s is None:
+        s = torch.cuda.Stream(device=idx)
+        _side[key] = s
+    return s
+
+
+def all_side_streams(device):
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    return [s for (d, _), s in sorted(_side.items(), key=lambda kv: kv[0]) if d == idx]
+
+
+class ViewStreams:
+    def __init__(self, device, n):
+        self.device = device
+        self.main = torch.cuda.current_stream(device)
+        self.side = [side_stream(device, i) for i in range(n - 1)]
+
+    @classmethod
+    def for_tensor(cls, x, n):
+        if n < 2 or not x.is_cuda or not enabled():
+            return None
+        return cls(x.device, n)
+
+    def stream(self, i):
+        return self.main if i == 0 else self.side[i - 1]
+
+    def fork(self, tensors=()):
+        """Side streams wait for everything enqueued on main so far; `tensors`
+        (main-stream outputs the side streams will read) are marked in use there."""
+        for s in self.side:
+            s.wait_stream(self.main)
+        for i, t in tensors:
+            if i > 0 and t is not None:
+                t.record_stream(self.side[i - 1])
+
+    def join(self, tensors=()):
+        """Main waits for every side stream; `tensors` produced on side streams
+        are marked in use on main."""
+        for s in self.side:
+            self.main.wait_stream(s)
+        for t in tensors:
+            if t is not None:
+                t.record_stream(self.main)
+
+    def run(self, i, fn, *args):
+        if i == 0:
+            return fn(*args)
+        with torch.cuda.stream(self.side[i - 1]):
+            return fn(*args)

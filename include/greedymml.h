@@ -187,6 +187,19 @@ int gm_conv_weight_transpose_bf16(const void* w, void* wt, int K, int RS, int C,
 /* fp32 KRSC master weight -> bf16 [K][RS][Cp] (zero-padded channels) and, if wt != NULL,
  * the transposed bf16 [Cp][RS][K] for dgrad, in one pass */
 int gm_conv_weight_prep_bf16(const float* w, int K, int RS, int C, int Cp, void* wb, void* wt, void* stream);
+/* Multi-tensor form: every weight of `table` (a DEVICE array of n entries, built once
+ * by the caller, tile_start = prefix sum of gm_wprep_tiles()) prepared in one launch
+ * of total_tiles workgroups.  Same outputs as gm_conv_weight_prep_bf16 per entry. */
+typedef struct gm_wprep {
+    const float* w;   /* fp32 [K][RS][C] */
+    void* wb;         /* bf16 [K][RS][Cp] */
+    void* wt;         /* bf16 [Cp][RS][K], or NULL */
+    int K, RS, C, Cp;
+    int tile_start;
+    int pad;
+} gm_wprep;
+int gm_wprep_tiles(int K, int RS, int Cp);
+int gm_conv_weight_prep_multi_bf16(const gm_wprep* table, int n, int total_tiles, void* stream);
 /* dw is fp32 [K][R][S][c_real]: the first c_real of the C (padded) input channels;
  * accumulate != 0 adds into dw (a parameter's gradient buffer written in place) */
 size_t gm_conv2d_wgrad_scratch(const gm_conv_desc* d);

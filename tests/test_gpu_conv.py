@@ -99,3 +99,24 @@ def test_conv_wgrad_in_place_sink(dev):
     assert len(fired) == 2
     assert torch.equal(first, ref)
     torch.testing.assert_close(m.weight.grad, 2 * ref, rtol=1e-6, atol=1e-6)
+
+
+def test_weight_prep_multi_matches_single(dev):
+    """One-launch multi-tensor weight prep == the per-convolution prep, bit for bit
+    (bf16 KRSC copy with zero-padded channels + transposed dgrad copy)."""
+    from greedy_multimodal_learning_amd.conv import GMConv2d, WeightPrep, _cpad, weight_prep
+    CL = torch.channels_last
+    torch.manual_seed(3)
+    net = torch.nn.Sequential(GMConv2d(3, 64, 7, stride=2, padding=3, bias=False),
+                              GMConv2d(64, 128, 3, padding=1, bias=False),
+                              GMConv2d(128, 256, 1, stride=2, bias=False),
+                              GMConv2d(256, 72, 3, padding=1, bias=False)).to(dev).to(memory_format=CL)
+    wp = WeightPrep(net)
+    wp.run()
+    torch.cuda.synchronize()
+    for (w, wb, wt), m in zip(wp.copies, net):
+        rb, rt = weight_prep(m.weight, _cpad(m.weight.shape[1]), wt is not None)
+        assert torch.equal(wb, rb)
+        if wt is not None:
+            assert torch.equal(wt, rt)
+    assert wp.copies[0][2] is None  # stem: no transposed copy

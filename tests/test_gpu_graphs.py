@@ -48,3 +48,17 @@ def test_graph_steps_equal_eager_steps():
         torch.testing.assert_close(b.running_avg_weight_skeleton, a.running_avg_weight_skeleton, rtol=1e-6,
                                    atol=1e-7)
         assert int(b._step_dev.item()) == 9
+
+
+def test_view_streams_equal_single_stream(monkeypatch):
+    """Trunks on two HIP streams (streams.py) == one stream, bit for bit: every
+    kernel is deterministic, so any cross-stream race would show up here."""
+    dev = torch.device("cuda:0")
+    monkeypatch.setenv("GM_VIEW_STREAMS", "0")
+    m_1, _, tr_1 = _run(False, 5, dev)
+    monkeypatch.setenv("GM_VIEW_STREAMS", "1")
+    m_2, _, tr_2 = _run(False, 5, dev)
+    assert tr_1 == tr_2
+    s1, s2 = m_1.state_dict(), m_2.state_dict()
+    for k in s1:
+        assert torch.equal(s1[k], s2[k]), k
