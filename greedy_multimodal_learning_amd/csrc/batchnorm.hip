@@ -14,6 +14,8 @@
 //      dgamma = S2*invstd, dx = a*dz + b*x + c per channel.
 //   2. k_bn_apply_bwd: dx (and dres = dz for the residual branch).
 // Bytes per element (bf16): fwd 2 (stats) + 4..6 (apply); bwd 4..6 + 6..8.
+#include <cstdlib>
+
 #include "gm_common.h"
 
 namespace gm {
@@ -21,21 +23,23 @@ namespace {
 
 constexpr int kT = 256;          // threads per block
 constexpr int kMaxC = 2048;      // channels supported (ResNet-50 ends at 2048)
-constexpr size_t kHdr = 256;     // scratch header (ticket counter)
-constexpr int kFlag = 2 * kMaxC; // LDS slot of the last-arriver flag
+constexpr size_t kHdr = 256;     // scratch header (ticket counters)
+constexpr int kMaxRC = 512;      // row chunks per channel slice (partials the last block combines)
+constexpr int kRedF = 4096;      // LDS floats of the row-group combine (rpp * 2 * SW == 4096)
 
-constexpr int kG1 = 32;          // level-1 ticket group: row chunks combined by one block
-
-// 2-D reduce grid: (row chunk, 64-channel slice).  Every block streams a
-// [rows x SW] strip (SW = min(C, 64) channels, 128-B row segments), unrolled x8
-// so ~32 KB per block is in flight; per-slice partials are combined in two
-// ticketed levels (groups of kG1 row chunks, then the groups), so no block ever
-// reads more than kG1 partial rows of 2*SW floats.
+// 2-D reduce grid: (row chunk, 64-channel slice), ~512 blocks (2x for large maps).  Every block
+// streams a [rows x SW] strip (SW = min(C, 64) channels, 128-B row segments),
+// unrolled x8 so ~32 KB per block is in flight, and writes one partial row of
+// 2*SW floats; ONE ticketed level per slice: the last-arriving block combines the
+// slice's <= kMaxRC partial rows with all 256 threads (16-B sc1 loads, all in
+// flight at once, fp64, fixed order) and finalizes.  One dependent memory round
+// trip after the ticket instead of two ticket levels: the small maps of layer3/4
+// are latency-, not bandwidth-bound.
 struct Plan {
     int SW, tpr_log, rpp;  // slice width, log2(threads per row), rows per pass
-    int nslice, nrc, ng;   // slices, row chunks, level-1 groups per slice
+    int nslice, nrc;       // slices, row chunks per slice
     long long rpb;         // rows per block
-    size_t off_coef, off_p1, off_p2, bytes;
+    size_t off_coef, off_p1, bytes;
 };
 
 inline int ilog2(int v) {
@@ -44,26 +48,32 @@ inline int ilog2(int v) {
     return l;
 }
 
+inline int bn_blocks() {
+    static int b = [] {
+        const char* e = getenv("GM_BN_BLOCKS");
+        return e ? atoi(e) : 512;
+    }();
+    return b;
+}
+
 inline Plan make_plan(long long M, int C) {
     Plan p;
     p.SW = C < 64 ? C : 64;
     p.tpr_log = ilog2(p.SW / 8);
     p.rpp = kT >> p.tpr_log;
     p.nslice = C / p.SW;
-    long long want = 1024 / p.nslice;
+    long long want = bn_blocks() / p.nslice;
+    if (M * C >= (16ll << 20)) want *= 2;  // large maps: bandwidth-bound, more blocks
     if (want < 1) want = 1;
-    if (want > (long long)kG1 * kG1) want = (long long)kG1 * kG1;
+    if (want > kMaxRC) want = kMaxRC;
     long long rpb = (M + want - 1) / want;
     rpb = (rpb + p.rpp - 1) / p.rpp * p.rpp;
     p.rpb = rpb;
     p.nrc = (int)((M + rpb - 1) / rpb);
-    p.ng = (p.nrc + kG1 - 1) / kG1;
-    const size_t cnt = (size_t)p.nslice * (p.ng + 1) * sizeof(unsigned);
+    const size_t cnt = (size_t)p.nslice * sizeof(unsigned);
     p.off_coef = (cnt + kHdr - 1) / kHdr * kHdr;
     p.off_p1 = p.off_coef + (size_t)4 * C * sizeof(float);
-    p.off_p2 = p.off_p1 + (size_t)p.nslice * p.nrc * 2 * p.SW * sizeof(float);
-    p.off_p2 = (p.off_p2 + 7) / 8 * 8;
-    p.bytes = p.off_p2 + (size_t)p.nslice * p.ng * 2 * p.SW * sizeof(double);
+    p.bytes = p.off_p1 + (size_t)p.nslice * p.nrc * 2 * p.SW * sizeof(float);
     return p;
 }
 
@@ -80,7 +90,7 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
 struct ReduceArgs {
     long long M;
     int C, tpr_log, relu, accumulate;
-    int SW, nrc, ng;
+    int SW, nrc;
     long long rpb;
     const uint4* x;      // fwd: x; bwd: x
     const uint4* dy;     // bwd
@@ -94,11 +104,10 @@ struct ReduceArgs {
     float* save_invstd;  // fwd: out; bwd: in
     float* dgamma;
     float* dbeta;
-    unsigned* counter;   // [nslice][ng + 1] tickets (zero between calls)
+    unsigned* counter;   // [nslice] tickets (zero between calls)
     long long* nbt;      // num_batches_tracked (fwd, may be null)
     float* coef;         // [4][C]
-    float* part;         // level 1: [nslice][nrc][SW][2] fp32
-    double* part2;       // level 2: [nslice][ng][SW][2] fp64
+    float* part;         // [nslice][nrc][SW][2] fp32 per-block partials
 };
 
 enum { FWD = 0, BWD = 1, BWD_RELU = 2 };  // relu as a template arg: no per-load branch
@@ -184,11 +193,8 @@ __device__ __forceinline__ void st_sc1(T* p, T v) {
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
 }
-__device__ __forceinline__ float ld_sc1_f32(__amdgpu_buffer_rsrc_t r, unsigned off_bytes) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off_bytes, 0, 16));
-}
-__device__ __forceinline__ double ld_sc1_f64(__amdgpu_buffer_rsrc_t r, unsigned off_bytes) {
-    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off_bytes, 0, 16));
+__device__ __forceinline__ float4 ld_sc1_f32x4(__amdgpu_buffer_rsrc_t r, unsigned off_bytes) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off_bytes, 0, 16));
 }
 
 __device__ __forceinline__ bool ticket(unsigned* ctr, unsigned n, float* flag) {
@@ -204,11 +210,11 @@ __device__ __forceinline__ bool ticket(unsigned* ctr, unsigned n, float* flag) {
     return *flag != 0.f;
 }
 
-// One launch: partial sums per (row chunk, channel slice) + two ticketed combine
-// levels + per-channel finalize.
+// One launch: partial sums per (row chunk, channel slice) + one ticketed combine
+// per slice + per-channel finalize.
 template <int MODE>
 __global__ __launch_bounds__(kT) void k_bn_reduce(ReduceArgs a) {
-    __shared__ float red[kFlag + 4];  // the one LDS object: row-group partials, flag
+    __shared__ float red[kRedF + 4];  // the one LDS object: row-group partials, flag
     const int t = threadIdx.x;
     const int C = a.C, SW = a.SW;
     const int rc = blockIdx.x, cs = blockIdx.y;
@@ -255,33 +261,40 @@ __global__ __launch_bounds__(kT) void k_bn_reduce(ReduceArgs a) {
         for (int i = 0; i < rpp; ++i) acc += red[i * S2w + t];
         st_sc1(&p1[t], acc);
     }
-    // level 1: the last of a group of kG1 row chunks combines them (fp64)
-    const int g = rc / kG1;
-    const int g0 = g * kG1;
-    const int gs = min(kG1, a.nrc - g0);
-    unsigned* ctr = a.counter + (size_t)cs * (a.ng + 1);
-    if (!ticket(ctr + g, (unsigned)gs, &red[kFlag])) return;
-    double* p2 = a.part2 + ((size_t)cs * a.ng + g) * S2w;
-    if (t < S2w) {
-        const auto rq = rsrc_of(a.part + ((size_t)cs * a.nrc + g0) * S2w);
-        double acc = 0.0;
-#pragma unroll 8
-        for (int i = 0; i < gs; ++i) acc += (double)ld_sc1_f32(rq, (unsigned)(i * S2w + t) * 4u);
-        st_sc1(&p2[t], acc);
-    }
-    // level 2: the last group of the slice finalizes its SW channels
-    if (!ticket(ctr + a.ng, (unsigned)a.ng, &red[kFlag])) return;
+    // the last block of the slice combines its nrc partial rows: lane group of L
+    // threads per row (one float4 each), G = 256/L row groups, rows g, g+G, ...
+    if (!ticket(a.counter + cs, (unsigned)a.nrc, &red[kRedF])) return;
     if (MODE == FWD && a.nbt && cs == 0 && t == 0) *a.nbt += 1;
-    const double invM = 1.0 / (double)a.M;
-    if (t < SW) {
-        const auto rq = rsrc_of(a.part2 + (size_t)cs * a.ng * S2w);
-        double S1 = 0.0, S2 = 0.0;
-#pragma unroll 8
-        for (int i = 0; i < a.ng; ++i) {
-            S1 += ld_sc1_f64(rq, (unsigned)(i * S2w + 2 * t) * 8u);
-            S2 += ld_sc1_f64(rq, (unsigned)(i * S2w + 2 * t + 1) * 8u);
+    const int L = S2w >> 2, G = kT / L;  // L in {4..32}, G in {8..64}
+    const int lv = t % L, g = t / L;
+    const auto rq = rsrc_of(a.part + (size_t)cs * a.nrc * S2w);
+    double d0 = 0.0, d1 = 0.0, d2 = 0.0, d3 = 0.0;
+    for (int i0 = g; i0 < a.nrc; i0 += 8 * G) {  // 8 independent 16-B loads in flight
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = i0 + u * G;
+            v[u] = i < a.nrc ? ld_sc1_f32x4(rq, (unsigned)(i * S2w + 4 * lv) * 4u) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        finalize<MODE>(a, cs * SW + t, S1, S2, invM);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            d0 += (double)v[u].x; d1 += (double)v[u].y; d2 += (double)v[u].z; d3 += (double)v[u].w;
+        }
+    }
+    __syncthreads();  // red[] is free again
+    double* rd = reinterpret_cast<double*>(red);  // [G][S2w] doubles: G * S2w == 2 * kT <= kRedF / 2
+    rd[g * S2w + 4 * lv + 0] = d0;
+    rd[g * S2w + 4 * lv + 1] = d1;
+    rd[g * S2w + 4 * lv + 2] = d2;
+    rd[g * S2w + 4 * lv + 3] = d3;
+    __syncthreads();
+    if (t < SW) {
+        double S1 = 0.0, S2 = 0.0;
+        for (int i = 0; i < G; ++i) {
+            S1 += rd[i * S2w + 2 * t];
+            S2 += rd[i * S2w + 2 * t + 1];
+        }
+        finalize<MODE>(a, cs * SW + t, S1, S2, 1.0 / (double)a.M);
     }
 }
 
@@ -416,7 +429,7 @@ extern "C" int gm_bn_fwd_train_bf16(const gm_bn_fwd* p, void* scratch, size_t by
     char* s = static_cast<char*>(scratch);
     ReduceArgs a{};
     a.M = p->M; a.C = p->C; a.tpr_log = pl.tpr_log; a.rpb = pl.rpb;
-    a.SW = pl.SW; a.nrc = pl.nrc; a.ng = pl.ng;
+    a.SW = pl.SW; a.nrc = pl.nrc;
     a.x = static_cast<const uint4*>(p->x);
     a.gamma = p->gamma; a.beta = p->beta; a.rmean = p->running_mean; a.rvar = p->running_var;
     a.momentum = p->momentum; a.eps = p->eps;
@@ -425,7 +438,6 @@ extern "C" int gm_bn_fwd_train_bf16(const gm_bn_fwd* p, void* scratch, size_t by
     a.counter = reinterpret_cast<unsigned*>(s);
     a.coef = reinterpret_cast<float*>(s + pl.off_coef);
     a.part = reinterpret_cast<float*>(s + pl.off_p1);
-    a.part2 = reinterpret_cast<double*>(s + pl.off_p2);
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(k_bn_reduce<FWD>, dim3(pl.nrc, pl.nslice), dim3(kT), 0, st, a);
     if ((rc = check_launch("k_bn_reduce<fwd>"))) return rc;
@@ -480,7 +492,7 @@ extern "C" int gm_bn_bwd_bf16(const gm_bn_bwd* p, void* scratch, size_t bytes, v
     char* s = static_cast<char*>(scratch);
     ReduceArgs a{};
     a.M = p->M; a.C = p->C; a.tpr_log = pl.tpr_log; a.rpb = pl.rpb; a.relu = p->relu;
-    a.SW = pl.SW; a.nrc = pl.nrc; a.ng = pl.ng;
+    a.SW = pl.SW; a.nrc = pl.nrc;
     a.accumulate = p->accumulate;
     a.x = static_cast<const uint4*>(p->x); a.dy = static_cast<const uint4*>(p->dy);
     a.y = static_cast<const uint4*>(p->y);
@@ -490,7 +502,6 @@ extern "C" int gm_bn_bwd_bf16(const gm_bn_bwd* p, void* scratch, size_t bytes, v
     a.counter = reinterpret_cast<unsigned*>(s);
     a.coef = reinterpret_cast<float*>(s + pl.off_coef);
     a.part = reinterpret_cast<float*>(s + pl.off_p1);
-    a.part2 = reinterpret_cast<double*>(s + pl.off_p2);
     hipStream_t st = as_stream(stream);
     if (p->relu) hipLaunchKernelGGL(k_bn_reduce<BWD_RELU>, dim3(pl.nrc, pl.nslice), dim3(kT), 0, st, a);
     else hipLaunchKernelGGL(k_bn_reduce<BWD>, dim3(pl.nrc, pl.nslice), dim3(kT), 0, st, a);

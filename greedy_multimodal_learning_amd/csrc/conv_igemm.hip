@@ -51,10 +51,21 @@ struct ConvArgs {
     int Ho, Wo;               // full output spatial dims
     int sA;
     int ncls;
+    int xcd;                  // remap block ids so consecutive tiles share an XCD (L2)
     ConvCls cls[kMaxCls];
 };
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+// Workgroups are dealt round-robin over the 8 XCDs (b and b+8 share one).  The
+// bijective remap gives each XCD a contiguous range of tile ids (tm fastest), so
+// the tiles of one output-channel column - one weight slice - stay in one L2.
+__device__ __forceinline__ int block_id(int xcd) {
+    const int b = blockIdx.x;
+    if (!xcd) return b;
+    const int n = gridDim.x, q = n >> 3, r = n & 7, x = b & 7;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
 
 __device__ __attribute__((aligned(16))) const uint4 g_zero16[1] = {{0u, 0u, 0u, 0u}};
 
@@ -69,12 +80,13 @@ __global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
     uint4* As = smem;                           // [ST][BM][8] (16-B chunks)
     uint4* Bs = smem + ST * BM * 8;             // [ST][BN][8]
 
+    const int bid = block_id(a.xcd);
     int ci = 0;
 #pragma unroll
     for (int q = 1; q < kMaxCls; ++q)
-        if (q < a.ncls && (int)blockIdx.x >= a.cls[q].tile_start) ci = q;
+        if (q < a.ncls && bid >= a.cls[q].tile_start) ci = q;
     const ConvCls& cl = a.cls[ci];
-    const int wgid = blockIdx.x - cl.tile_start;
+    const int wgid = bid - cl.tile_start;
     const int tm = wgid % cl.tiles_m, tn = wgid / cl.tiles_m;
     const int m0 = tm * BM, n0 = tn * BN;
     const int PQ = cl.P * cl.Q;
@@ -287,12 +299,13 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint4 smem[];
     char* lds = reinterpret_cast<char*>(smem);   // [A0][A1][B0][B1][taps]
 
+    const int bid = block_id(a.xcd);
     int ci = 0;
 #pragma unroll
     for (int q = 1; q < kMaxCls; ++q)
-        if (q < a.ncls && (int)blockIdx.x >= a.cls[q].tile_start) ci = q;
+        if (q < a.ncls && bid >= a.cls[q].tile_start) ci = q;
     const ConvCls& cl = a.cls[ci];
-    const int wgid = blockIdx.x - cl.tile_start;
+    const int wgid = bid - cl.tile_start;
     const int tm = wgid % cl.tiles_m, tn = wgid / cl.tiles_m;
     const int m0 = tm * BM, n0 = tn * BN;
     const int PQ = cl.P * cl.Q;
@@ -526,14 +539,32 @@ static int stages() {
     return s;
 }
 
+static int xcd_remap() {
+    static int on = [] {
+        const char* e = getenv("GM_CONV_XCD");  // off by default: measured no gain
+        return (e && e[0] == '1') ? 1 : 0;
+    }();
+    return on;
+}
+
+static int tile_bias() {
+    static int b = [] {
+        const char* e = getenv("GM_CONV_TILE_WGS");
+        return e ? atoi(e) : 1024;
+    }();
+    return b;
+}
+
 static int pick_and_launch(ConvArgs& a, hipStream_t st) {
     long M = 0;
     for (int i = 0; i < a.ncls; ++i) M += (long)a.N * a.cls[i].P * a.cls[i].Q;
     const bool three = stages() == 3;
+    const long wgs = tile_bias();  // workgroups wanted before a larger tile is taken
+    a.xcd = xcd_remap();
     // enough workgroups to fill 256 CUs, largest tile that does
-    if (a.Nout >= 128 && M / 128 * (a.Nout / 128) >= 1024)
+    if (a.Nout >= 128 && M / 128 * (a.Nout / 128) >= wgs)
         return three ? launch_igemm<128, 128, 3>(a, st) : launch_igemm<128, 128, 2>(a, st);
-    if (M / 128 * ((a.Nout + 63) / 64) >= 768)
+    if (M / 128 * ((a.Nout + 63) / 64) >= wgs * 3 / 4)
         return three ? launch_igemm<128, 64, 3>(a, st) : launch_igemm<128, 64, 2>(a, st);
     return three ? launch_igemm<64, 64, 3>(a, st) : launch_igemm<64, 64, 2>(a, st);
 }
