@@ -13,6 +13,7 @@
 // waves of 32x32, v_mfma_f32_32x32x16_bf16), double-buffered register-staged
 // loads, split-K over pixels into fp32 partial slabs, then a fixed-order reduce
 // (deterministic, no atomics).
+#include <cstdlib>
 #include <cstring>
 
 #include "gm_common.h"
@@ -34,6 +35,8 @@ struct WgradArgs {
     int N, H, W, C, logC, Kc, T, P, Q, st;
     int tiles_k, tiles_n, splits, steps_per_split;  // steps of 64 pixels
     FastDiv fd_pq, fd_q;        // pixel -> (b, p, q) without integer division
+    int accumulate;             // k_conv_wgrad4 with one split: add into part (= dw) instead of storing
+    int S, pad;                 // k_conv_wgrad4 decodes taps arithmetically
     signed char dh[kWTap], dw[kWTap];
 };
 
@@ -141,6 +144,196 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a) {
     }
 }
 
+__device__ __attribute__((aligned(16))) const uint4 g_wzero16[1] = {{0u, 0u, 0u, 0u}};
+
+// Workgroup tile (64*MT) x (64*NT) of dw, 2x2 waves each owning MT*NT independent 32x32
+// accumulators (the MFMAs of a k-slice do not wait on each other).  Operands are staged
+// by LDS-DMA (global_load_lds_dwordx4) into two buffers, the DMA of pixel step s+1
+// running under the MFMAs of step s, with the loop unrolled by the two buffers so every
+// LDS fragment read is a base VGPR + immediate offset.  A DMA instruction writes 64 x
+// 16 B linearly, so rows are unpadded (2*BM bytes) and a source-side XOR swizzle of the
+// 16-B chunk keeps the tr-read half-waves conflict-free (the four rows a half-wave
+// reads get their 64-B column window in four distinct bank quarters).  Padding taps
+// read a zero block of the code object.
+template <int RB>  // row bytes (128 or 256)
+__device__ __forceinline__ int wswz(int row) {
+    return RB == 256 ? 4 * (row & 3) : 4 * ((row >> 1) & 1);
+}
+
+template <int MT, int NT>
+__global__ __launch_bounds__(256) void k_conv_wgrad4(WgradArgs a) {
+    constexpr int BK = 64;
+    constexpr int BM = 64 * MT, BN = 64 * NT;
+    constexpr int RA = 2 * BM, RB = 2 * BN;          // row bytes
+    constexpr int SA = BK * RA, SB = BK * RB;        // bytes per buffer
+    constexpr int GA = SA / 1024 / 4, GB = SB / 1024 / 4;  // DMA instructions per wave per step
+    constexpr int LPA = RA / 16, LPB = RB / 16;      // lanes per row
+    extern __shared__ __attribute__((aligned(16))) uint4 wsm[];
+    char* lds = reinterpret_cast<char*>(wsm);        // [A0][B0][A1][B1]
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    int bid = blockIdx.x;
+    {   // XCD-major: the tiles of one pixel range share an XCD (and its L2 copy of the rows)
+        const int n = gridDim.x, q = n >> 3, r = n & 7, x = bid & 7;
+        bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+    }
+    const int tiles = a.tiles_k * a.tiles_n;
+    const int split = bid / tiles, tile = bid - split * tiles;
+    const int tk = tile % a.tiles_k, tn = tile / a.tiles_k;
+    const int k0 = tk * BM, n0 = tn * BN;
+    const int PQ = a.P * a.Q;
+    const int M = a.N * PQ;
+    const int TC = a.T * a.C;
+    const int step0 = split * a.steps_per_split;
+    const int step1 = min((M + BK - 1) / BK, step0 + a.steps_per_split);
+    const int nst = step1 - step0;
+
+    // A (dy) DMA lanes: row a_row[j] of the step, 16-B chunk (swizzled) of channels
+    const int a_rsub = lane / LPA, a_slot = lane % LPA;
+    const uint16_t* a_ptr[GA];
+    int a_row[GA];
+    bool a_cok[GA];
+#pragma unroll
+    for (int j = 0; j < GA; ++j) {
+        a_row[j] = (wave * GA + j) * (64 / LPA) + a_rsub;
+        const int col = k0 + ((a_slot ^ wswz<RA>(a_row[j])) << 3);
+        a_cok[j] = col < a.Kc;
+        a_ptr[j] = a.dy + ((size_t)step0 * BK + a_row[j]) * a.Kc + (a_cok[j] ? col : 0);
+    }
+    // B (x) DMA lanes: fixed (tap, channel chunk) per instruction
+    const int b_rsub = lane / LPB, b_slot = lane % LPB;
+    int b_row[GB], b_toff[GB], b_dh[GB], b_dw[GB];
+    bool b_cok[GB];
+#pragma unroll
+    for (int j = 0; j < GB; ++j) {
+        b_row[j] = (wave * GB + j) * (64 / LPB) + b_rsub;
+        const int col = n0 + ((b_slot ^ wswz<RB>(b_row[j])) << 3);
+        b_cok[j] = col < TC;
+        const int tap = b_cok[j] ? col >> a.logC : 0;
+        const int r = tap / a.S, s = tap - r * a.S;
+        b_dh[j] = r - a.pad;
+        b_dw[j] = s - a.pad;
+        b_toff[j] = ((b_dh[j] * a.W + b_dw[j]) << a.logC) + (col & (a.C - 1));
+    }
+    typedef __attribute__((address_space(1))) const void* gptr_t;
+    typedef __attribute__((address_space(3))) void* lptr_t;
+    auto issue = [&](int i, int bufoff) {  // step step0 + i
+        const bool full = (step0 + i + 1) * BK <= M;
+#pragma unroll
+        for (int j = 0; j < GA; ++j) {
+            const bool ok = a_cok[j] && (full || (step0 + i) * BK + a_row[j] < M);
+            const void* src = ok ? (const void*)(a_ptr[j] + (size_t)i * BK * a.Kc) : (const void*)g_wzero16;
+            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + bufoff + (wave * GA + j) * 1024), 16, 0,
+                                             0);
+        }
+#pragma unroll
+        for (int j = 0; j < GB; ++j) {
+            const int m = (step0 + i) * BK + b_row[j];
+            const int b = (int)a.fd_pq.div((uint32_t)m), pq = m - b * PQ;
+            const int p = (int)a.fd_q.div((uint32_t)pq), q = pq - p * a.Q;
+            const int hi = p * a.st + b_dh[j], wi = q * a.st + b_dw[j];
+            const bool ok = b_cok[j] && m < M && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+            const int pix = (b * a.H + p * a.st) * a.W + q * a.st;
+            const void* src =
+                ok ? (const void*)(a.x + (((long)pix << a.logC) + b_toff[j])) : (const void*)g_wzero16;
+            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + bufoff + SA + (wave * GB + j) * 1024), 16,
+                                             0, 0);
+        }
+    };
+
+    floatx16 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    // tr-read geometry: half-wave g>>1 reads rows 8*(g>>1)+q4 (+4) of a 16-row k-slice, 4-column
+    // block p4 of the 32-column fragment, 16-column half g&1.  The swizzle term depends on q4 only,
+    // so (k-slice, +4 row) offsets are immediates on one base per fragment.
+    const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+    const int rbase = 8 * (g >> 1) + q4;
+    int a_base[MT], b_base[NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+        const int c = wm * (32 * MT) + 32 * i + 16 * (g & 1) + 4 * p4;
+        a_base[i] = rbase * RA + (((c >> 3) ^ wswz<RA>(rbase)) << 4) + (c & 7) * 2;
+    }
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const int c = wn * (32 * NT) + 32 * j + 16 * (g & 1) + 4 * p4;
+        b_base[j] = SA + rbase * RB + (((c >> 3) ^ wswz<RB>(rbase)) << 4) + (c & 7) * 2;
+    }
+    auto compute = [&](const int bufoff) {
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            bf16x8 af[MT], bfr[NT];
+#pragma unroll
+            for (int i = 0; i < MT; ++i) {
+                const char* p = lds + bufoff + a_base[i] + ks * 16 * RA;
+                af[i] = tr_frag((const uint16_t*)p, (const uint16_t*)(p + 4 * RA));
+            }
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+                const char* p = lds + bufoff + b_base[j] + ks * 16 * RB;
+                bfr[j] = tr_frag((const uint16_t*)p, (const uint16_t*)(p + 4 * RB));
+            }
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+    };
+    constexpr int BUF1 = SA + SB;
+    if (nst > 0) issue(0, 0);
+    __syncthreads();
+    int i = 0;
+    for (; i + 1 < nst; i += 2) {  // steps i (buffer 0) and i+1 (buffer 1)
+        issue(i + 1, BUF1);
+        compute(0);
+        __syncthreads();
+        if (i + 2 < nst) issue(i + 2, 0);
+        compute(BUF1);
+        __syncthreads();
+    }
+    if (i < nst) compute(0);  // odd step count: the last step sits in buffer 0
+
+    float* out = a.part + (size_t)split * a.Kc * TC;
+    const bool inner = k0 + BM <= a.Kc && n0 + BN <= TC;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const int col = n0 + wn * (32 * NT) + 32 * j + (lane & 31);
+#pragma unroll
+        for (int ii = 0; ii < MT; ++ii) {
+            const int row0 = k0 + wm * (32 * MT) + 32 * ii + 4 * (lane >> 5);
+            float* o = out + (size_t)row0 * TC + col;
+            if (inner) {
+                if (a.accumulate) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        float* p = o + (size_t)((r & 3) + 8 * (r >> 2)) * TC;
+                        *p += acc[ii][j][r];
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) o[(size_t)((r & 3) + 8 * (r >> 2)) * TC] = acc[ii][j][r];
+                }
+            } else if (col < TC) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = row0 + (r & 3) + 8 * (r >> 2);
+                    if (row < a.Kc) {
+                        float* p = o + (size_t)((r & 3) + 8 * (r >> 2)) * TC;
+                        *p = a.accumulate ? *p + acc[ii][j][r] : acc[ii][j][r];
+                    }
+                }
+            }
+        }
+    }
+}
+
 // stage 1 (many splits): part2[g][i] = sum of splits 8g..8g+7 (fixed order), float4 lanes,
 // grid (slab/1024, groups): parallel over splits so the reduce is bandwidth-, not latency-bound
 __global__ __launch_bounds__(256) void k_wgrad_sum8(const float* part, int splits, size_t slab, float* part2) {
@@ -175,32 +368,76 @@ static int ilog2w(int v) {
     return (1 << l) == v ? l : -1;
 }
 
-static void plan(const gm_conv_desc* d, int& P, int& Q, int& tiles_k, int& tiles_n, int& splits, int& sps) {
-    P = (d->H + 2 * d->pad - d->R) / d->stride + 1;
-    Q = (d->W + 2 * d->pad - d->S) / d->stride + 1;
-    const int M = d->N * P * Q;
+static int wgrad_version() {
+    static int v = [] {
+        const char* e = getenv("GM_WGRAD_V");  // 1: 64x64 register-staged kernel, 2: k_conv_wgrad4
+        return (e && e[0] == '1') ? 1 : 2;
+    }();
+    return v;
+}
+
+static int wgrad_target_wgs() {
+    static int w = [] {
+        const char* e = getenv("GM_WGRAD_WGS");
+        return e ? atoi(e) : (wgrad_version() == 2 ? 512 : 1024);
+    }();
+    return w;
+}
+
+
+
+struct WPlan {
+    int P, Q, tiles_k, tiles_n, splits, sps, mt, nt;
+};
+
+static WPlan plan(const gm_conv_desc* d) {
+    WPlan w;
+    w.P = (d->H + 2 * d->pad - d->R) / d->stride + 1;
+    w.Q = (d->W + 2 * d->pad - d->S) / d->stride + 1;
+    const int M = d->N * w.P * w.Q;
     const int steps = (M + 63) / 64;
-    tiles_k = (d->K + 63) / 64;
-    tiles_n = (d->R * d->S * d->C + 63) / 64;
-    const int tiles = tiles_k * tiles_n;
-    int want = (1024 + tiles - 1) / tiles;           // ~1024 workgroups
-    if (want > steps / 4) want = steps / 4 > 0 ? steps / 4 : 1;  // >= 4 steps per split
+    const int TC = d->R * d->S * d->C;
+    w.mt = w.nt = 1;
+    if (wgrad_version() >= 2) {
+        w.mt = d->K >= 128 ? 2 : 1;
+        w.nt = TC >= 128 ? 2 : 1;
+    }
+    w.tiles_k = (d->K + 64 * w.mt - 1) / (64 * w.mt);
+    w.tiles_n = (TC + 64 * w.nt - 1) / (64 * w.nt);
+    const int tiles = w.tiles_k * w.tiles_n;
+    const int target = wgrad_version() >= 2 ? wgrad_target_wgs() : 1024;
+    const int min_steps = wgrad_version() == 2 ? 8 : 4;
+    int want = wgrad_version() == 2 ? (target > tiles ? target / tiles : 1) : (target + tiles - 1) / tiles;
+    if (wgrad_version() == 2 && tiles >= 256) want = 1;  // the chip is full: no partial slabs
+    if (want > steps / min_steps) want = steps / min_steps > 0 ? steps / min_steps : 1;
     if (want < 1) want = 1;
-    sps = (steps + want - 1) / want;
-    splits = (steps + sps - 1) / sps;
+    w.sps = (steps + want - 1) / want;
+    w.splits = (steps + w.sps - 1) / w.sps;
+    return w;
 }
 
 }  // namespace gm
 
 using namespace gm;
 
+template <int MT, int NT>
+static int launch_wgrad4(const WgradArgs& a, int grid, hipStream_t st) {
+    const size_t lds = (size_t)2 * 64 * 2 * (64 * MT + 64 * NT);
+    static bool attr = false;  // idempotent, safe to race
+    if (!attr) {
+        hipFuncSetAttribute((const void*)k_conv_wgrad4<MT, NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr = true;
+    }
+    k_conv_wgrad4<MT, NT><<<grid, 256, lds, st>>>(a);
+    return check_launch("k_conv_wgrad4");
+}
+
 extern "C" size_t gm_conv2d_wgrad_scratch(const gm_conv_desc* d) {
     if (!d) return 0;
-    int P, Q, tk, tn, sp, sps;
-    plan(d, P, Q, tk, tn, sp, sps);
+    const WPlan w = plan(d);
     const size_t slab = (size_t)d->K * d->R * d->S * d->C;
-    const int groups = sp > 8 ? (sp + 7) / 8 : 0;
-    return (size_t)(sp + groups) * slab * sizeof(float);
+    const int groups = w.splits > 8 ? (w.splits + 7) / 8 : 0;
+    return (size_t)(w.splits + groups) * slab * sizeof(float);
 }
 
 extern "C" int gm_conv2d_wgrad_bf16(const gm_conv_desc* d, const void* dy, const void* x, float* dw, int c_real,
@@ -214,7 +451,9 @@ extern "C" int gm_conv2d_wgrad_bf16(const gm_conv_desc* d, const void* dy, const
     GM_REQUIRE(scratch && scratch_bytes >= need, "conv wgrad: scratch %zu < %zu", scratch_bytes, need);
     WgradArgs a;
     memset(&a, 0, sizeof(a));
-    plan(d, a.P, a.Q, a.tiles_k, a.tiles_n, a.splits, a.steps_per_split);
+    const WPlan w = plan(d);
+    a.P = w.P; a.Q = w.Q; a.tiles_k = w.tiles_k; a.tiles_n = w.tiles_n;
+    a.splits = w.splits; a.steps_per_split = w.sps;
     a.dy = (const uint16_t*)dy;
     a.x = (const uint16_t*)x;
     a.part = (float*)scratch;
@@ -229,8 +468,24 @@ extern "C" int gm_conv2d_wgrad_bf16(const gm_conv_desc* d, const void* dy, const
         }
     hipStream_t st = as_stream(stream);
     const int grid = a.tiles_k * a.tiles_n * a.splits;
-    k_conv_wgrad<<<grid, 256, 0, st>>>(a);
-    int rc = check_launch("k_conv_wgrad");
+    int rc;
+    if (wgrad_version() >= 2) {
+        const bool direct = a.splits == 1 && c_real == d->C;
+        if (direct) {
+            a.part = dw;
+            a.accumulate = accumulate;
+        }
+        a.S = d->S;
+        a.pad = d->pad;
+        if (w.mt == 2 && w.nt == 2) rc = launch_wgrad4<2, 2>(a, grid, st);
+        else if (w.mt == 2) rc = launch_wgrad4<2, 1>(a, grid, st);
+        else if (w.nt == 2) rc = launch_wgrad4<1, 2>(a, grid, st);
+        else rc = launch_wgrad4<1, 1>(a, grid, st);
+        if (rc || direct) return rc;
+    } else {
+        k_conv_wgrad<<<grid, 256, 0, st>>>(a);
+        rc = check_launch("k_conv_wgrad");
+    }
     if (rc) return rc;
     const size_t n = (size_t)d->K * a.T * c_real;
     int g = (int)((n + 255) / 256);

@@ -65,8 +65,10 @@ def main():
         for op, (own, mio) in ops.items():
             if name == "conv1" and op == "dgrad":
                 continue
+            if os.environ.get("CB_OPS") and op not in os.environ["CB_OPS"].split(","):
+                continue
             t_own = timeit(own)
-            t_mio = timeit(mio)
+            t_mio = timeit(mio) if not os.environ.get("CB_NOMIO") else 1e9
             tot["own"] += t_own * cnt
             tot["miopen"] += t_mio * cnt
             print(f"{name:9s} {op:6s} {t_own:8.1f} {flops / t_own / 1e6:7.1f} {t_mio:9.1f} {flops / t_mio / 1e6:7.1f}",
