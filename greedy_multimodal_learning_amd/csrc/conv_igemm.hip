@@ -561,8 +561,9 @@ static int pick_and_launch(ConvArgs& a, hipStream_t st) {
     const bool three = stages() == 3;
     const long wgs = tile_bias();  // workgroups wanted before a larger tile is taken
     a.xcd = xcd_remap();
-    // enough workgroups to fill 256 CUs, largest tile that does
-    if (a.Nout >= 128 && M / 128 * (a.Nout / 128) >= wgs)
+    // enough workgroups to fill 256 CUs, largest tile that does (128x128: 4 independent
+    // accumulators per wave, so one workgroup per CU already keeps the MFMA pipe fed)
+    if (a.Nout >= 128 && M / 128 * (a.Nout / 128) >= wgs / 4)
         return three ? launch_igemm<128, 128, 3>(a, st) : launch_igemm<128, 128, 2>(a, st);
     if (M / 128 * ((a.Nout + 63) / 64) >= wgs * 3 / 4)
         return three ? launch_igemm<128, 64, 3>(a, st) : launch_igemm<128, 64, 2>(a, st);
