@@ -41,6 +41,15 @@ struct ConvCls {
     int tiles_m;
     short tw[kMaxTap];        // weight tap index (r*S + s)
     signed char dh[kMaxTap], dw[kMaxTap];
+    // the same taps as an Rc x Sc grid (tap = i*Sc + j): dh = cdh[i], dw = cdw[j],
+    // weight tap = crs[i] + cs[j]; i = (tap * smag) >> 8 (exact for tap < ntap).  The
+    // kernel reads them as 4-bit fields: pk_dh/pk_dw hold dh+8 / dw+8, pk_r/pk_s the
+    // weight row r_i / column s_j (weight tap = r_i * Sw + s_j).
+    int Rc, Sc, smag;
+    unsigned pk_dh, pk_dw, pk_r, pk_s;
+    FastDiv fd_pq, fd_q;      // output pixel -> (b, p, q)
+    signed char cdh[8], cdw[8];
+    unsigned char crs[8], cs[8];
 };
 
 struct ConvArgs {
@@ -48,6 +57,7 @@ struct ConvArgs {
     const uint16_t* wt;       // [Nout][T][C]
     int N, Hi, Wi, C, logC;
     int Nout, T;              // output channels, taps per weight row
+    int Sw;                   // weight columns (S)
     int Ho, Wo;               // full output spatial dims
     int sA;
     int ncls;
@@ -315,36 +325,34 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
     const int t = threadIdx.x;
     const int lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-    int* tapt = reinterpret_cast<int*>(lds + 2 * (SA + SB));
-#pragma unroll
-    for (int i = 0; i < kMaxTap; ++i)
-        if (t == i && i < cl.ntap)
-            tapt[i] = (int)cl.tw[i] | ((int)(cl.dh[i] + 128) << 8) | ((int)(cl.dw[i] + 128) << 16);
-    __syncthreads();
     const int wm = wave >> 1, wn = wave & 1;
     const int slot = lane & 7;
+    // the class's tap grid, unpacked in SGPRs from 4-bit fields
+    const unsigned pk_dh = cl.pk_dh, pk_dw = cl.pk_dw, pk_r = cl.pk_r, pk_s = cl.pk_s;
 
+    // per A row: pixel base pointer and the tap validity as two bitmasks over the
+    // grid's rows (bit i: h + cdh[i] in range) and columns (bit j: w + cdw[j] in range)
     const uint16_t* a_ptr[AR];
-    unsigned a_vm[AR];
+    unsigned a_vr[AR], a_vs[AR];
 #pragma unroll
     for (int j = 0; j < AR; ++j) {
         const int row = (wave * AR + j) * 8 + (lane >> 3);
         const int m = m0 + row;
         const int gc = slot ^ ((row >> 1) & 7);
-        unsigned vm = 0;
-        a_ptr[j] = a.in + gc * 8;
-        if (m < M) {
-            const int b = m / PQ, pq = m - b * PQ;
-            const int p = pq / cl.Q, q = pq - p * cl.Q;
-            const int h = p * a.sA, w = q * a.sA;
-            a_ptr[j] = a.in + ((size_t)((b * a.Hi + h) * a.Wi + w) << a.logC) + gc * 8;
-            for (int tp = 0; tp < cl.ntap; ++tp) {
-                const int te = tapt[tp];
-                const int hi = h + ((te >> 8) & 0xff) - 128, wi = w + ((te >> 16) & 0xff) - 128;
-                if ((unsigned)hi < (unsigned)a.Hi && (unsigned)wi < (unsigned)a.Wi) vm |= 1u << tp;
-            }
+        const int b = (int)cl.fd_pq.div((uint32_t)m), pq = m - b * PQ;
+        const int p = (int)cl.fd_q.div((uint32_t)pq), q = pq - p * cl.Q;
+        const int h = p * a.sA, w = q * a.sA;
+        unsigned vr = 0, vs = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int dh = (int)((pk_dh >> (4 * i)) & 15u) - 8, dw = (int)((pk_dw >> (4 * i)) & 15u) - 8;
+            vr |= (i < cl.Rc && (unsigned)(h + dh) < (unsigned)a.Hi) ? 1u << i : 0u;
+            vs |= (i < cl.Sc && (unsigned)(w + dw) < (unsigned)a.Wi) ? 1u << i : 0u;
         }
-        a_vm[j] = vm;
+        const bool in = m < M;
+        a_vr[j] = in ? vr : 0u;
+        a_vs[j] = vs;
+        a_ptr[j] = a.in + (in ? ((size_t)((b * a.Hi + h) * a.Wi + w) << a.logC) : 0) + gc * 8;
     }
     const uint16_t* b_ptr[BR];
     bool b_ok[BR];
@@ -374,20 +382,18 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
 
     typedef __attribute__((address_space(1))) const void* gptr_t;
     typedef __attribute__((address_space(3))) void* lptr_t;
-    int te_next = tapt[0];
     auto issue = [&](int kt, int buf) {
         const int k = kt * BK;
-        const int tap = k >> a.logC;
-        const int te = __builtin_amdgcn_readfirstlane(te_next);
-        const int dh = ((te >> 8) & 0xff) - 128, dw = ((te >> 16) & 0xff) - 128;
+        const int tap = __builtin_amdgcn_readfirstlane(k >> a.logC);
+        const int ti = (tap * cl.smag) >> 8, tj = tap - ti * cl.Sc;
+        const int dh = (int)((pk_dh >> (4 * ti)) & 15u) - 8, dw = (int)((pk_dw >> (4 * tj)) & 15u) - 8;
+        const int tw = (int)((pk_r >> (4 * ti)) & 15u) * a.Sw + (int)((pk_s >> (4 * tj)) & 15u);
         const int c0 = k & (a.C - 1);
         const long aoff = (long)(((dh * a.Wi + dw) << a.logC) + c0);
-        const long boff = (long)((te & 0xff) * a.C + c0);
-        const int knext = k + BK;
-        te_next = tapt[knext < cl.ntap * a.C ? (knext >> a.logC) : 0];
+        const long boff = (long)(tw * a.C + c0);
 #pragma unroll
         for (int j = 0; j < AR; ++j) {
-            const bool ok = (a_vm[j] >> tap) & 1u;
+            const bool ok = ((a_vr[j] >> ti) & (a_vs[j] >> tj)) & 1u;
             const void* src = ok ? (const void*)(a_ptr[j] + aoff) : (const void*)g_zero16;
             __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + buf * SA + (wave * AR + j) * 1024), 16, 0,
                                              0);
@@ -441,8 +447,8 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
     for (int i = 0; i < MT; ++i) {
         const int m = m0 + wm * (BM / 2) + i * 32 + fr;
         if (m >= M) continue;
-        const int b = m / PQ, pq = m - b * PQ;
-        const int p = pq / cl.Q, q = pq - p * cl.Q;
+        const int b = (int)cl.fd_pq.div((uint32_t)m), pq = m - b * PQ;
+        const int p = (int)cl.fd_q.div((uint32_t)pq), q = pq - p * cl.Q;
         const int ho = p * cl.oS + cl.oH, wo = q * cl.oS + cl.oW;
         uint16_t* dst = cl.out + ((size_t)(b * a.Ho + ho) * a.Wo + wo) * a.Nout;
 #pragma unroll
@@ -492,6 +498,9 @@ static bool lean_path() {
     return on;
 }
 
+static bool grid_ok(const ConvCls& c, int S);
+static void pack_grid(ConvCls& c, int S);
+
 template <int BM, int BN, int ST>
 static int launch_igemm(ConvArgs& a, hipStream_t st) {
     int tiles = 0;
@@ -512,9 +521,9 @@ static int launch_igemm(ConvArgs& a, hipStream_t st) {
                             (int)lds);
         attr_set = true;
     }
-    int maxtap = 0;
-    for (int i = 0; i < a.ncls; ++i) maxtap = a.cls[i].ntap > maxtap ? a.cls[i].ntap : maxtap;
-    if (a.C >= 64 && maxtap <= 32 && lean_path()) {
+    bool grid = true;
+    for (int i = 0; i < a.ncls; ++i) grid = grid && grid_ok(a.cls[i], a.Sw);
+    if (a.C >= 64 && grid && lean_path()) {
         const size_t lds2 = (size_t)2 * (BM + BN) * 128 + kMaxTap * 4 + 12;
         static bool attr2 = false;
         if (!attr2) {
@@ -570,6 +579,69 @@ static int pick_and_launch(ConvArgs& a, hipStream_t st) {
     return three ? launch_igemm<64, 64, 3>(a, st) : launch_igemm<64, 64, 2>(a, st);
 }
 
+// the class's taps as a grid: rows r (stride-compatible with the class parity ph) and
+// columns s (with pw); fwd is the st = 1 case with every (r, s) - same order as tw/dh/dw
+static void set_grid(ConvCls& c, const gm_conv_desc* d, int st, int ph, int pw) {
+    c.Rc = c.Sc = 0;
+    for (int r = 0; r < d->R && c.Rc < 8; ++r) {
+        if (((ph + d->pad - r) % st + st) % st) continue;
+        c.cdh[c.Rc] = (signed char)((ph + d->pad - r) / st);
+        c.crs[c.Rc++] = (unsigned char)(r * d->S);
+    }
+    for (int s = 0; s < d->S && c.Sc < 8; ++s) {
+        if (((pw + d->pad - s) % st + st) % st) continue;
+        c.cdw[c.Sc] = (signed char)((pw + d->pad - s) / st);
+        c.cs[c.Sc++] = (unsigned char)s;
+    }
+    c.smag = c.Sc > 0 ? (256 + c.Sc - 1) / c.Sc : 0;
+    c.fd_pq = FastDiv((uint32_t)(c.P * c.Q > 0 ? c.P * c.Q : 1));
+    c.fd_q = FastDiv((uint32_t)(c.Q > 0 ? c.Q : 1));
+    pack_grid(c, d->S);
+}
+
+// forward taps read dh = r - pad, i.e. the dgrad formula with st = 1 and a sign flip
+static void set_grid_fwd(ConvCls& c, const gm_conv_desc* d) {
+    c.Rc = d->R < 8 ? d->R : 8;
+    c.Sc = d->S < 8 ? d->S : 8;
+    for (int r = 0; r < c.Rc; ++r) {
+        c.cdh[r] = (signed char)(r - d->pad);
+        c.crs[r] = (unsigned char)(r * d->S);
+    }
+    for (int s = 0; s < c.Sc; ++s) {
+        c.cdw[s] = (signed char)(s - d->pad);
+        c.cs[s] = (unsigned char)s;
+    }
+    c.smag = (256 + c.Sc - 1) / c.Sc;
+    c.fd_pq = FastDiv((uint32_t)(c.P * c.Q));
+    c.fd_q = FastDiv((uint32_t)c.Q);
+    pack_grid(c, d->S);
+}
+
+static void pack_grid(ConvCls& c, int S) {
+    c.pk_dh = c.pk_dw = c.pk_r = c.pk_s = 0;
+    for (int i = 0; i < c.Rc; ++i) {
+        c.pk_dh |= (unsigned)((c.cdh[i] + 8) & 15) << (4 * i);
+        c.pk_r |= (unsigned)((c.crs[i] / S) & 15) << (4 * i);
+    }
+    for (int j = 0; j < c.Sc; ++j) {
+        c.pk_dw |= (unsigned)((c.cdw[j] + 8) & 15) << (4 * j);
+        c.pk_s |= (unsigned)(c.cs[j] & 15) << (4 * j);
+    }
+}
+
+// the lean kernel's tap grid must reproduce the tap list exactly (order, offsets, weights)
+static bool grid_ok(const ConvCls& c, int S) {
+    if (c.Rc * c.Sc != c.ntap || c.Rc > 8 || c.Sc > 8) return false;
+    for (int t = 0; t < c.ntap; ++t) {
+        const int i = (t * c.smag) >> 8, j = t - i * c.Sc;
+        if (i != t / c.Sc) return false;
+        const int dh = (int)((c.pk_dh >> (4 * i)) & 15u) - 8, dw = (int)((c.pk_dw >> (4 * j)) & 15u) - 8;
+        const int tw = (int)((c.pk_r >> (4 * i)) & 15u) * S + (int)((c.pk_s >> (4 * j)) & 15u);
+        if (dh != c.dh[t] || dw != c.dw[t] || tw != c.tw[t]) return false;
+    }
+    return true;
+}
+
 static int check_desc(const gm_conv_desc* d) {
     GM_REQUIRE(d && d->N > 0 && d->H > 0 && d->W > 0 && d->C > 0 && d->K > 0 && d->R > 0 && d->S > 0,
                "conv: empty shape");
@@ -591,7 +663,7 @@ extern "C" int gm_conv2d_fwd_bf16(const gm_conv_desc* d, const void* x, const vo
     a.in = (const uint16_t*)x;
     a.wt = (const uint16_t*)w;
     a.N = d->N; a.Hi = d->H; a.Wi = d->W; a.C = d->C; a.logC = ilog2(d->C);
-    a.Nout = d->K; a.T = d->R * d->S;
+    a.Nout = d->K; a.T = d->R * d->S; a.Sw = d->S;
     a.Ho = P; a.Wo = Q; a.sA = d->stride;
     a.ncls = 1;
     ConvCls& c = a.cls[0];
@@ -605,6 +677,7 @@ extern "C" int gm_conv2d_fwd_bf16(const gm_conv_desc* d, const void* x, const vo
             c.dh[i] = (signed char)(r - d->pad);
             c.dw[i] = (signed char)(s - d->pad);
         }
+    set_grid_fwd(c, d);
     return pick_and_launch(a, as_stream(stream));
 }
 
@@ -623,7 +696,7 @@ extern "C" int gm_conv2d_dgrad_bf16(const gm_conv_desc* d, const void* dy, const
     a.in = (const uint16_t*)dy;
     a.wt = (const uint16_t*)wt;
     a.N = d->N; a.Hi = P; a.Wi = Q; a.C = d->K; a.logC = ilog2(d->K);
-    a.Nout = d->C; a.T = d->R * d->S;
+    a.Nout = d->C; a.T = d->R * d->S; a.Sw = d->S;
     a.Ho = d->H; a.Wo = d->W; a.sA = 1;
     bool full = true;
     hipStream_t s = as_stream(stream);
@@ -647,6 +720,7 @@ extern "C" int gm_conv2d_dgrad_bf16(const gm_conv_desc* d, const void* dy, const
             }
             c.ntap = n;
             if (n == 0 || c.P <= 0 || c.Q <= 0) { full = false; continue; }
+            set_grid(c, d, st, ph, pw);
             ++a.ncls;
         }
     if (!full) {
