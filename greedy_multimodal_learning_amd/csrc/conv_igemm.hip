@@ -46,6 +46,7 @@ struct ConvCls {
     // kernel reads them as 4-bit fields: pk_dh/pk_dw hold dh+8 / dw+8, pk_r/pk_s the
     // weight row r_i / column s_j (weight tap = r_i * Sw + s_j).
     int Rc, Sc, smag;
+    int dh0, sh, dw0, sw;     // dh_i = dh0 + sh*i, dw_j = dw0 + sw*j (sh, sw = +-1)
     unsigned pk_dh, pk_dw, pk_r, pk_s;
     FastDiv fd_pq, fd_q;      // output pixel -> (b, p, q)
     signed char cdh[8], cdw[8];
@@ -78,6 +79,21 @@ __device__ __forceinline__ int block_id(int xcd) {
 }
 
 __device__ __attribute__((aligned(16))) const uint4 g_zero16[1] = {{0u, 0u, 0u, 0u}};
+
+// bits i in [0, n) with 0 <= x + d0 + s*i < lim (s = +-1): one contiguous range
+__device__ __forceinline__ unsigned span_mask(int x, int d0, int s, int n, int lim) {
+    int lo, hi;
+    if (s > 0) {
+        lo = -(x + d0);
+        hi = lim - 1 - (x + d0);
+    } else {
+        lo = x + d0 - (lim - 1);
+        hi = x + d0;
+    }
+    lo = lo < 0 ? 0 : lo;
+    hi = hi > n - 1 ? n - 1 : hi;
+    return lo > hi ? 0u : ((2u << hi) - (1u << lo));
+}
 
 template <int BM, int BN, bool UT, int ST>
 __global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
@@ -342,13 +358,10 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
         const int b = (int)cl.fd_pq.div((uint32_t)m), pq = m - b * PQ;
         const int p = (int)cl.fd_q.div((uint32_t)pq), q = pq - p * cl.Q;
         const int h = p * a.sA, w = q * a.sA;
-        unsigned vr = 0, vs = 0;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int dh = (int)((pk_dh >> (4 * i)) & 15u) - 8, dw = (int)((pk_dw >> (4 * i)) & 15u) - 8;
-            vr |= (i < cl.Rc && (unsigned)(h + dh) < (unsigned)a.Hi) ? 1u << i : 0u;
-            vs |= (i < cl.Sc && (unsigned)(w + dw) < (unsigned)a.Wi) ? 1u << i : 0u;
-        }
+        // dh_i = dh_0 + sh*i with sh = +-1 (fwd: r - pad; dgrad class: (ph+pad-r)/st), so
+        // the valid grid rows are one contiguous bit range [lo, hi]; same for columns
+        const unsigned vr = span_mask(h, cl.dh0, cl.sh, cl.Rc, a.Hi);
+        const unsigned vs = span_mask(w, cl.dw0, cl.sw, cl.Sc, a.Wi);
         const bool in = m < M;
         a_vr[j] = in ? vr : 0u;
         a_vs[j] = vs;
@@ -618,6 +631,10 @@ static void set_grid_fwd(ConvCls& c, const gm_conv_desc* d) {
 }
 
 static void pack_grid(ConvCls& c, int S) {
+    c.dh0 = c.cdh[0];
+    c.sh = c.Rc > 1 ? c.cdh[1] - c.cdh[0] : 1;
+    c.dw0 = c.cdw[0];
+    c.sw = c.Sc > 1 ? c.cdw[1] - c.cdw[0] : 1;
     c.pk_dh = c.pk_dw = c.pk_r = c.pk_s = 0;
     for (int i = 0; i < c.Rc; ++i) {
         c.pk_dh |= (unsigned)((c.cdh[i] + 8) & 15) << (4 * i);
@@ -632,6 +649,11 @@ static void pack_grid(ConvCls& c, int S) {
 // the lean kernel's tap grid must reproduce the tap list exactly (order, offsets, weights)
 static bool grid_ok(const ConvCls& c, int S) {
     if (c.Rc * c.Sc != c.ntap || c.Rc > 8 || c.Sc > 8) return false;
+    if ((c.sh != 1 && c.sh != -1) || (c.sw != 1 && c.sw != -1)) return false;
+    for (int i = 0; i < c.Rc; ++i)
+        if (c.cdh[i] != c.dh0 + c.sh * i) return false;
+    for (int j = 0; j < c.Sc; ++j)
+        if (c.cdw[j] != c.dw0 + c.sw * j) return false;
     for (int t = 0; t < c.ntap; ++t) {
         const int i = (t * c.smag) >> 8, j = t - i * c.Sc;
         if (i != t / c.Sc) return false;
