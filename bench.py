@@ -95,9 +95,12 @@ def time_trunk_igemm(B, dev, reps=10):
         w = torch.randn(K, Cp, R, R, device=dev).bfloat16().contiguous(memory_format=CL)
         dy = torch.randn(B, K, P, Q, device=dev).bfloat16().contiguous(memory_format=CL)
         wt = w.permute(1, 0, 2, 3).contiguous(memory_format=CL)
-        ops = [lambda: G.conv_fwd(x, w, st, pad)]
-        if C != 3:  # the stem's input gradient is never computed
-            ops.append(lambda: G.conv_dgrad_t(dy, wt, H, W, st, pad))
+        if C == 3:  # the stem runs on the pixel-pair view (conv.py); its input gradient is never computed
+            xp = G.stem_pack_input(x[:, :3], R, R, pad)
+            wp = G.stem_pack_weight(w[:, :3].float())
+            ops = [lambda: G.stem_fwd(xp, wp, P, Q)]
+        else:
+            ops = [lambda: G.conv_fwd(x, w, st, pad), lambda: G.conv_dgrad_t(dy, wt, H, W, st, pad)]
         for op in ops:
             op()
             torch.cuda.synchronize()

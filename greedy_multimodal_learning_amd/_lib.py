@@ -131,6 +131,19 @@ EXPORTS.update({
 })
 
 
+class ConvDescHW(ctypes.Structure):
+    _fields_ = [("N", c_int), ("H", c_int), ("W", c_int), ("C", c_int), ("K", c_int), ("R", c_int), ("S", c_int),
+                ("stride_h", c_int), ("stride_w", c_int), ("pad_h", c_int), ("pad_w", c_int)]
+
+
+EXPORTS.update({
+    "gm_conv2d_fwd_hw_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "gm_conv2d_wgrad_hw_scratch": (c_size_t, [c_void_p]),
+    "gm_conv2d_wgrad_hw_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
+                                        c_size_t, c_void_p]),
+})
+
+
 class WPrep(ctypes.Structure):
     _fields_ = [("w", c_void_p), ("wb", c_void_p), ("wt", c_void_p), ("K", c_int), ("RS", c_int),
                 ("C", c_int), ("Cp", c_int), ("tile_start", c_int), ("pad", c_int)]

@@ -9,6 +9,7 @@ Activations are channels_last (NHWC) bf16, weights are cast to bf16 KRSC per
 step, weight gradients come back in fp32 in the parameter's layout.
 """
 import ctypes
+import os
 
 import torch
 import torch.nn as nn
@@ -109,6 +110,106 @@ def weight_prep(weight, Cp, transposed):
     return wb, wt
 
 
+def _desc_hw(N, H, W, C, K, R, S, sh, sw, ph, pw):
+    return L.ConvDescHW(N, H, W, C, K, R, S, sh, sw, ph, pw)
+
+
+# ---- ResNet stem on a pixel-pair view -------------------------------------------
+# A 7x7/s2 convolution of an RGB image wastes most of an MFMA K-slice if every tap is
+# one 8-channel (3 real) chunk: K = 49 x 8 = 392 for 147 real products.  With the
+# input as zero-bordered 4-channel pixels, two horizontally adjacent pixels form ONE
+# 16-byte (8-channel) element, and the stride-2 filter becomes a 7 x 4 filter over
+# pairs with strides (2, 1) and no padding: K = 7 x 4 x 8 = 224, every tap in range
+# (the border is real zeros), half the input bytes.  The weights are re-packed to
+# [K][R][S/2][2 x 4] per step (a 25 KB tensor).
+
+def stem_pair_ok(C0, R, S, stride, pad):
+    return C0 <= 4 and stride == 2 and R <= 8 and S <= 8 and pad < R and pad < S
+
+
+def _stem_geom(H, W, R, S, pad):
+    P = (H + 2 * pad - R) // 2 + 1
+    Q = (W + 2 * pad - S) // 2 + 1
+    Sp = (S + 1) // 2
+    Hp = max(2 * (P - 1) + R, pad + H)
+    Wp = max(2 * (Q - 1) + 2 * Sp, pad + W)
+    Wp += Wp & 1
+    return P, Q, Sp, Hp, Wp
+
+
+def stem_pack_input(x, R, S, pad):
+    """x [N,C0<=4,H,W] -> zero-bordered pair view [N,8,Hp,Wp/2] (channels_last bf16)."""
+    N, C0, H, W = x.shape
+    P, Q, Sp, Hp, Wp = _stem_geom(H, W, R, S, pad)
+    xp = torch.zeros(N, Hp, Wp, 4, device=x.device, dtype=torch.bfloat16)
+    xp[:, pad:pad + H, pad:pad + W, :C0] = x.permute(0, 2, 3, 1)
+    return xp.view(N, Hp, Wp // 2, 8).permute(0, 3, 1, 2)
+
+
+def stem_pack_weight(weight):
+    """fp32 [K,C0,R,S] -> bf16 pair-packed [K,8,R,Sp] (channels_last: [K][R][Sp][2x4])."""
+    K, C0, R, S = weight.shape
+    Sp = (S + 1) // 2
+    wp = torch.zeros(K, R, 2 * Sp, 4, device=weight.device, dtype=torch.bfloat16)
+    wp[:, :, :S, :C0] = weight.detach().permute(0, 2, 3, 1)
+    return wp.view(K, R, Sp, 8).permute(0, 3, 1, 2)
+
+
+def stem_fwd(xp, wp, P, Q):
+    lib = L.load()
+    N, _, Hp, Wq = xp.shape
+    K, _, R, Sp = wp.shape
+    if (Hp - R) // 2 + 1 != P or Wq - Sp + 1 != Q:
+        raise ValueError(f"stem pair view {tuple(xp.shape)} does not give a {P}x{Q} output")
+    y = torch.empty(N, K, P, Q, device=xp.device, dtype=torch.bfloat16, memory_format=CL)
+    d = _desc_hw(N, Hp, Wq, 8, K, R, Sp, 2, 1, 0, 0)
+    L.check(lib.gm_conv2d_fwd_hw_bf16(ctypes.byref(d), xp.data_ptr(), wp.data_ptr(), y.data_ptr(),
+                                      L.stream_of(xp.device)), "gm_conv2d_fwd_hw_bf16")
+    return y
+
+
+class _StemFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, pad):
+        K, C0, R, S = weight.shape
+        N, _, H, W = x.shape
+        P, Q, Sp, Hp, Wp = _stem_geom(H, W, R, S, pad)
+        xp = stem_pack_input(x, R, S, pad)
+        wp = stem_pack_weight(weight)
+        y = stem_fwd(xp, wp, P, Q)
+        ctx.save_for_backward(xp, weight)
+        ctx.meta = (R, S, Sp)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        xp, weight = ctx.saved_tensors
+        R, S, Sp = ctx.meta
+        if not ctx.needs_input_grad[1]:
+            return None, None, None
+        lib = L.load()
+        gy = _nhwc(gy.to(torch.bfloat16))
+        N, _, Hp, Wq = xp.shape
+        K, C0 = weight.shape[0], weight.shape[1]
+        d = _desc_hw(N, Hp, Wq, 8, K, R, Sp, 2, 1, 0, 0)
+        need = lib.gm_conv2d_wgrad_hw_scratch(ctypes.byref(d))
+        scratch = torch.empty(max(need, 16), device=xp.device, dtype=torch.uint8)
+        dwp = torch.empty(K, R, Sp, 8, device=xp.device, dtype=torch.float32)
+        L.check(lib.gm_conv2d_wgrad_hw_bf16(ctypes.byref(d), gy.data_ptr(), xp.data_ptr(), dwp.data_ptr(), 8, 0,
+                                            scratch.data_ptr(), need, L.stream_of(xp.device)),
+                "gm_conv2d_wgrad_hw_bf16")
+        dw = dwp.view(K, R, 2 * Sp, 4)[:, :, :S, :C0].permute(0, 3, 1, 2)  # [K,C0,R,S] view of KRSC
+        tgt = sink_target(weight)
+        if tgt is not None:
+            if tgt[1]:
+                tgt[0].add_(dw)
+            else:
+                tgt[0].copy_(dw)
+            sink_done(weight)
+            return None, None, None
+        return None, dw.contiguous(memory_format=CL), None
+
+
 _prepped = {}  # weight data_ptr -> (wb, wt): bf16 copies made by an active WeightPrep
 
 
@@ -120,7 +221,7 @@ class WeightPrep:
 
     def __init__(self, model):
         lib = L.load()
-        convs = [m for m in model.modules() if isinstance(m, GMConv2d)]
+        convs = [m for m in model.modules() if isinstance(m, GMConv2d) and not m.uses_pair_stem()]
         dev = next(model.parameters()).device
         specs, total = [], 0
         for m in convs:
@@ -242,10 +343,22 @@ class GMConv2d(nn.Conv2d):
     """nn.Conv2d whose bf16 path runs on libgreedymml_hip.so (groups=1, no bias,
     square stride/padding, dilation 1 - the ResNet trunk's convolutions)."""
 
-    def forward(self, x):
-        if (_use_hip(x) and self.groups == 1 and self.bias is None and self.dilation == (1, 1)
+    pair_stem = os.environ.get("GM_STEM_PAIR", "1") != "0"
+
+    def _hip_ok(self):
+        return (self.groups == 1 and self.bias is None and self.dilation == (1, 1)
                 and self.stride[0] == self.stride[1] and self.padding[0] == self.padding[1]
-                and self.padding_mode == "zeros"):
+                and self.padding_mode == "zeros")
+
+    def uses_pair_stem(self):
+        """The RGB stem (<= 4 input channels, stride 2) runs on the pixel-pair view."""
+        K, C0, R, S = self.weight.shape
+        return self.pair_stem and self._hip_ok() and stem_pair_ok(C0, R, S, self.stride[0], self.padding[0])
+
+    def forward(self, x):
+        if _use_hip(x) and self._hip_ok():
             with torch.autocast("cuda", enabled=False):
+                if self.uses_pair_stem() and not x.requires_grad:
+                    return _StemFn.apply(x, self.weight, self.padding[0])
                 return _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0])
         return F.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation, self.groups)

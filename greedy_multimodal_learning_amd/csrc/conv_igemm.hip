@@ -60,7 +60,7 @@ struct ConvArgs {
     int Nout, T;              // output channels, taps per weight row
     int Sw;                   // weight columns (S)
     int Ho, Wo;               // full output spatial dims
-    int sA;
+    int sAh, sAw;             // input strides of the GEMM's A rows (H, W)
     int ncls;
     int xcd;                  // remap block ids so consecutive tiles share an XCD (L2)
     ConvCls cls[kMaxCls];
@@ -146,8 +146,8 @@ __global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
         if (m < M) {
             const int b = m / PQ, pq = m - b * PQ;
             const int p = pq / cl.Q, q = pq - p * cl.Q;
-            a_h[j] = p * a.sA;
-            a_w[j] = q * a.sA;
+            a_h[j] = p * a.sAh;
+            a_w[j] = q * a.sAw;
             a_ptr[j] = a.in + ((size_t)((b * a.Hi + a_h[j]) * a.Wi + a_w[j]) << a.logC);
         } else {
             a_h[j] = -(1 << 28);  // never valid
@@ -357,7 +357,7 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
         const int gc = slot ^ ((row >> 1) & 7);
         const int b = (int)cl.fd_pq.div((uint32_t)m), pq = m - b * PQ;
         const int p = (int)cl.fd_q.div((uint32_t)pq), q = pq - p * cl.Q;
-        const int h = p * a.sA, w = q * a.sA;
+        const int h = p * a.sAh, w = q * a.sAw;
         // dh_i = dh_0 + sh*i with sh = +-1 (fwd: r - pad; dgrad class: (ph+pad-r)/st), so
         // the valid grid rows are one contiguous bit range [lo, hi]; same for columns
         const unsigned vr = span_mask(h, cl.dh0, cl.sh, cl.Rc, a.Hi);
@@ -613,15 +613,15 @@ static void set_grid(ConvCls& c, const gm_conv_desc* d, int st, int ph, int pw) 
 }
 
 // forward taps read dh = r - pad, i.e. the dgrad formula with st = 1 and a sign flip
-static void set_grid_fwd(ConvCls& c, const gm_conv_desc* d) {
+static void set_grid_fwd(ConvCls& c, const gm_conv_desc_hw* d) {
     c.Rc = d->R < 8 ? d->R : 8;
     c.Sc = d->S < 8 ? d->S : 8;
     for (int r = 0; r < c.Rc; ++r) {
-        c.cdh[r] = (signed char)(r - d->pad);
+        c.cdh[r] = (signed char)(r - d->pad_h);
         c.crs[r] = (unsigned char)(r * d->S);
     }
     for (int s = 0; s < c.Sc; ++s) {
-        c.cdw[s] = (signed char)(s - d->pad);
+        c.cdw[s] = (signed char)(s - d->pad_w);
         c.cs[s] = (unsigned char)s;
     }
     c.smag = (256 + c.Sc - 1) / c.Sc;
@@ -674,19 +674,31 @@ static int check_desc(const gm_conv_desc* d) {
     return GM_OK;
 }
 
-extern "C" int gm_conv2d_fwd_bf16(const gm_conv_desc* d, const void* x, const void* w, void* y, void* stream) {
-    int rc = check_desc(d);
+static int check_desc_hw(const gm_conv_desc_hw* d) {
+    GM_REQUIRE(d && d->N > 0 && d->H > 0 && d->W > 0 && d->C > 0 && d->K > 0 && d->R > 0 && d->S > 0,
+               "conv: empty shape");
+    GM_REQUIRE(d->stride_h >= 1 && d->stride_w >= 1 && d->pad_h >= 0 && d->pad_w >= 0, "conv: bad stride/pad");
+    GM_REQUIRE(d->R * d->S <= kMaxTap, "conv: at most %d taps", kMaxTap);
+    GM_REQUIRE(ilog2(d->C) >= 3, "conv: C must be a power of two >= 8 (got %d)", d->C);
+    GM_REQUIRE(d->K % 8 == 0, "conv: K must be a multiple of 8 (got %d)", d->K);
+    GM_REQUIRE(d->H + 2 * d->pad_h >= d->R && d->W + 2 * d->pad_w >= d->S, "conv: filter larger than input");
+    return GM_OK;
+}
+
+extern "C" int gm_conv2d_fwd_hw_bf16(const gm_conv_desc_hw* d, const void* x, const void* w, void* y,
+                                     void* stream) {
+    int rc = check_desc_hw(d);
     if (rc) return rc;
     GM_REQUIRE(x && w && y, "conv fwd: null pointer");
-    const int P = (d->H + 2 * d->pad - d->R) / d->stride + 1;
-    const int Q = (d->W + 2 * d->pad - d->S) / d->stride + 1;
+    const int P = (d->H + 2 * d->pad_h - d->R) / d->stride_h + 1;
+    const int Q = (d->W + 2 * d->pad_w - d->S) / d->stride_w + 1;
     ConvArgs a;
     memset(&a, 0, sizeof(a));
     a.in = (const uint16_t*)x;
     a.wt = (const uint16_t*)w;
     a.N = d->N; a.Hi = d->H; a.Wi = d->W; a.C = d->C; a.logC = ilog2(d->C);
     a.Nout = d->K; a.T = d->R * d->S; a.Sw = d->S;
-    a.Ho = P; a.Wo = Q; a.sA = d->stride;
+    a.Ho = P; a.Wo = Q; a.sAh = d->stride_h; a.sAw = d->stride_w;
     a.ncls = 1;
     ConvCls& c = a.cls[0];
     c.out = (uint16_t*)y;
@@ -696,11 +708,18 @@ extern "C" int gm_conv2d_fwd_bf16(const gm_conv_desc* d, const void* x, const vo
         for (int s = 0; s < d->S; ++s) {
             const int i = r * d->S + s;
             c.tw[i] = (short)i;
-            c.dh[i] = (signed char)(r - d->pad);
-            c.dw[i] = (signed char)(s - d->pad);
+            c.dh[i] = (signed char)(r - d->pad_h);
+            c.dw[i] = (signed char)(s - d->pad_w);
         }
     set_grid_fwd(c, d);
     return pick_and_launch(a, as_stream(stream));
+}
+
+extern "C" int gm_conv2d_fwd_bf16(const gm_conv_desc* d, const void* x, const void* w, void* y, void* stream) {
+    int rc = check_desc(d);
+    if (rc) return rc;
+    const gm_conv_desc_hw h = {d->N, d->H, d->W, d->C, d->K, d->R, d->S, d->stride, d->stride, d->pad, d->pad};
+    return gm_conv2d_fwd_hw_bf16(&h, x, w, y, stream);
 }
 
 extern "C" int gm_conv2d_dgrad_bf16(const gm_conv_desc* d, const void* dy, const void* wt, void* dx,
@@ -719,7 +738,7 @@ extern "C" int gm_conv2d_dgrad_bf16(const gm_conv_desc* d, const void* dy, const
     a.wt = (const uint16_t*)wt;
     a.N = d->N; a.Hi = P; a.Wi = Q; a.C = d->K; a.logC = ilog2(d->K);
     a.Nout = d->C; a.T = d->R * d->S; a.Sw = d->S;
-    a.Ho = d->H; a.Wo = d->W; a.sA = 1;
+    a.Ho = d->H; a.Wo = d->W; a.sAh = a.sAw = 1;
     bool full = true;
     hipStream_t s = as_stream(stream);
     for (int ph = 0; ph < st; ++ph)

@@ -32,11 +32,11 @@ struct WgradArgs {
     const uint16_t* dy;         // [N][P][Q][Kc]
     const uint16_t* x;          // [N][H][W][C]
     float* part;                // [splits][Kc][T*C]
-    int N, H, W, C, logC, Kc, T, P, Q, st;
+    int N, H, W, C, logC, Kc, T, P, Q, sth, stw;
     int tiles_k, tiles_n, splits, steps_per_split;  // steps of 64 pixels
     FastDiv fd_pq, fd_q;        // pixel -> (b, p, q) without integer division
     int accumulate;             // k_conv_wgrad4 with one split: add into part (= dw) instead of storing
-    int S, pad;                 // k_conv_wgrad4 decodes taps arithmetically
+    int S, padh, padw;          // k_conv_wgrad4 decodes taps arithmetically
     signed char dh[kWTap], dw[kWTap];
 };
 
@@ -87,7 +87,7 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a) {
                 if (acol_ok) va = *(const uint4*)(a.dy + (size_t)m * a.Kc + k0 + lchunk * 8);
                 const int b = (int)a.fd_pq.div((uint32_t)m), pq = m - b * PQ;
                 const int p = (int)a.fd_q.div((uint32_t)pq), q = pq - p * a.Q;
-                const int hi = p * a.st + bdh, wi = q * a.st + bdw;
+                const int hi = p * a.sth + bdh, wi = q * a.stw + bdw;
                 if (bcol_ok && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W)
                     vb = *(const uint4*)(a.x + ((size_t)((b * a.H + hi) * a.W + wi) << a.logC) + bc);
             }
@@ -212,8 +212,8 @@ __global__ __launch_bounds__(256) void k_conv_wgrad4(WgradArgs a) {
         b_cok[j] = col < TC;
         const int tap = b_cok[j] ? col >> a.logC : 0;
         const int r = tap / a.S, s = tap - r * a.S;
-        b_dh[j] = r - a.pad;
-        b_dw[j] = s - a.pad;
+        b_dh[j] = r - a.padh;
+        b_dw[j] = s - a.padw;
         b_toff[j] = ((b_dh[j] * a.W + b_dw[j]) << a.logC) + (col & (a.C - 1));
     }
     typedef __attribute__((address_space(1))) const void* gptr_t;
@@ -232,9 +232,9 @@ __global__ __launch_bounds__(256) void k_conv_wgrad4(WgradArgs a) {
             const int m = (step0 + i) * BK + b_row[j];
             const int b = (int)a.fd_pq.div((uint32_t)m), pq = m - b * PQ;
             const int p = (int)a.fd_q.div((uint32_t)pq), q = pq - p * a.Q;
-            const int hi = p * a.st + b_dh[j], wi = q * a.st + b_dw[j];
+            const int hi = p * a.sth + b_dh[j], wi = q * a.stw + b_dw[j];
             const bool ok = b_cok[j] && m < M && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
-            const int pix = (b * a.H + p * a.st) * a.W + q * a.st;
+            const int pix = (b * a.H + p * a.sth) * a.W + q * a.stw;
             const void* src =
                 ok ? (const void*)(a.x + (((long)pix << a.logC) + b_toff[j])) : (const void*)g_wzero16;
             __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + bufoff + SA + (wave * GB + j) * 1024), 16,
@@ -390,10 +390,10 @@ struct WPlan {
     int P, Q, tiles_k, tiles_n, splits, sps, mt, nt;
 };
 
-static WPlan plan(const gm_conv_desc* d) {
+static WPlan plan(const gm_conv_desc_hw* d) {
     WPlan w;
-    w.P = (d->H + 2 * d->pad - d->R) / d->stride + 1;
-    w.Q = (d->W + 2 * d->pad - d->S) / d->stride + 1;
+    w.P = (d->H + 2 * d->pad_h - d->R) / d->stride_h + 1;
+    w.Q = (d->W + 2 * d->pad_w - d->S) / d->stride_w + 1;
     const int M = d->N * w.P * w.Q;
     const int steps = (M + 63) / 64;
     const int TC = d->R * d->S * d->C;
@@ -432,22 +432,34 @@ static int launch_wgrad4(const WgradArgs& a, int grid, hipStream_t st) {
     return check_launch("k_conv_wgrad4");
 }
 
-extern "C" size_t gm_conv2d_wgrad_scratch(const gm_conv_desc* d) {
-    if (!d) return 0;
+static gm_conv_desc_hw to_hw(const gm_conv_desc* d) {
+    return gm_conv_desc_hw{d->N, d->H, d->W, d->C, d->K, d->R, d->S, d->stride, d->stride, d->pad, d->pad};
+}
+
+extern "C" size_t gm_conv2d_wgrad_hw_scratch(const gm_conv_desc_hw* d) {
+    if (!d || d->stride_h < 1 || d->stride_w < 1) return 0;
     const WPlan w = plan(d);
     const size_t slab = (size_t)d->K * d->R * d->S * d->C;
     const int groups = w.splits > 8 ? (w.splits + 7) / 8 : 0;
     return (size_t)(w.splits + groups) * slab * sizeof(float);
 }
 
-extern "C" int gm_conv2d_wgrad_bf16(const gm_conv_desc* d, const void* dy, const void* x, float* dw, int c_real,
-                                    int accumulate, void* scratch, size_t scratch_bytes, void* stream) {
+extern "C" size_t gm_conv2d_wgrad_scratch(const gm_conv_desc* d) {
+    if (!d) return 0;
+    const gm_conv_desc_hw h = to_hw(d);
+    return gm_conv2d_wgrad_hw_scratch(&h);
+}
+
+extern "C" int gm_conv2d_wgrad_hw_bf16(const gm_conv_desc_hw* d, const void* dy, const void* x, float* dw,
+                                       int c_real, int accumulate, void* scratch, size_t scratch_bytes,
+                                       void* stream) {
     GM_REQUIRE(d && dy && x && dw, "conv wgrad: null pointer");
+    GM_REQUIRE(d->stride_h >= 1 && d->stride_w >= 1 && d->pad_h >= 0 && d->pad_w >= 0, "conv wgrad: bad stride/pad");
     GM_REQUIRE(d->R * d->S <= kWTap, "conv wgrad: at most %d taps", kWTap);
     GM_REQUIRE(ilog2w(d->C) >= 3, "conv wgrad: C must be a power of two >= 8");
     GM_REQUIRE(d->K % 8 == 0, "conv wgrad: K must be a multiple of 8");
     GM_REQUIRE(c_real >= 1 && c_real <= d->C, "conv wgrad: bad c_real");
-    const size_t need = gm_conv2d_wgrad_scratch(d);
+    const size_t need = gm_conv2d_wgrad_hw_scratch(d);
     GM_REQUIRE(scratch && scratch_bytes >= need, "conv wgrad: scratch %zu < %zu", scratch_bytes, need);
     WgradArgs a;
     memset(&a, 0, sizeof(a));
@@ -458,13 +470,13 @@ extern "C" int gm_conv2d_wgrad_bf16(const gm_conv_desc* d, const void* dy, const
     a.x = (const uint16_t*)x;
     a.part = (float*)scratch;
     a.N = d->N; a.H = d->H; a.W = d->W; a.C = d->C; a.logC = ilog2w(d->C);
-    a.Kc = d->K; a.T = d->R * d->S; a.st = d->stride;
+    a.Kc = d->K; a.T = d->R * d->S; a.sth = d->stride_h; a.stw = d->stride_w;
     a.fd_pq = FastDiv((uint32_t)(a.P * a.Q));
     a.fd_q = FastDiv((uint32_t)a.Q);
     for (int r = 0; r < d->R; ++r)
         for (int s = 0; s < d->S; ++s) {
-            a.dh[r * d->S + s] = (signed char)(r - d->pad);
-            a.dw[r * d->S + s] = (signed char)(s - d->pad);
+            a.dh[r * d->S + s] = (signed char)(r - d->pad_h);
+            a.dw[r * d->S + s] = (signed char)(s - d->pad_w);
         }
     hipStream_t st = as_stream(stream);
     const int grid = a.tiles_k * a.tiles_n * a.splits;
@@ -476,7 +488,8 @@ extern "C" int gm_conv2d_wgrad_bf16(const gm_conv_desc* d, const void* dy, const
             a.accumulate = accumulate;
         }
         a.S = d->S;
-        a.pad = d->pad;
+        a.padh = d->pad_h;
+        a.padw = d->pad_w;
         if (w.mt == 2 && w.nt == 2) rc = launch_wgrad4<2, 2>(a, grid, st);
         else if (w.mt == 2) rc = launch_wgrad4<2, 1>(a, grid, st);
         else if (w.nt == 2) rc = launch_wgrad4<1, 2>(a, grid, st);
@@ -505,4 +518,11 @@ extern "C" int gm_conv2d_wgrad_bf16(const gm_conv_desc* d, const void* dy, const
     }
     k_wgrad_reduce<<<g, 256, 0, st>>>(src, nsrc, d->K, a.T, d->C, c_real, accumulate, dw);
     return check_launch("k_wgrad_reduce");
+}
+
+extern "C" int gm_conv2d_wgrad_bf16(const gm_conv_desc* d, const void* dy, const void* x, float* dw, int c_real,
+                                    int accumulate, void* scratch, size_t scratch_bytes, void* stream) {
+    GM_REQUIRE(d, "conv wgrad: null pointer");
+    const gm_conv_desc_hw h = to_hw(d);
+    return gm_conv2d_wgrad_hw_bf16(&h, dy, x, dw, c_real, accumulate, scratch, scratch_bytes, stream);
 }

@@ -182,6 +182,16 @@ typedef struct gm_conv_desc {
 } gm_conv_desc;
 
 int gm_conv2d_fwd_bf16(const gm_conv_desc* d, const void* x, const void* w, void* y, void* stream);
+/* Per-axis stride and padding (same kernels).  The ResNet stem runs through these on a
+ * zero-bordered "pixel-pair" view of its RGB input: 4-channel pixels, two per 8-channel
+ * element, so the 7x7/s2 filter becomes a 7x4 (pair) filter with strides (2, 1), K = 224
+ * instead of 49 taps x 8 padded channels = 392 (conv.py, stem path). */
+typedef struct gm_conv_desc_hw {
+    int N, H, W, C;
+    int K, R, S;
+    int stride_h, stride_w, pad_h, pad_w;
+} gm_conv_desc_hw;
+int gm_conv2d_fwd_hw_bf16(const gm_conv_desc_hw* d, const void* x, const void* w, void* y, void* stream);
 int gm_conv2d_dgrad_bf16(const gm_conv_desc* d, const void* dy, const void* wt, void* dx, void* stream);
 int gm_conv_weight_transpose_bf16(const void* w, void* wt, int K, int RS, int C, void* stream);
 /* fp32 KRSC master weight -> bf16 [K][RS][Cp] (zero-padded channels) and, if wt != NULL,
@@ -205,6 +215,9 @@ int gm_conv_weight_prep_multi_bf16(const gm_wprep* table, int n, int total_tiles
 size_t gm_conv2d_wgrad_scratch(const gm_conv_desc* d);
 int gm_conv2d_wgrad_bf16(const gm_conv_desc* d, const void* dy, const void* x, float* dw, int c_real,
                          int accumulate, void* scratch, size_t scratch_bytes, void* stream);
+size_t gm_conv2d_wgrad_hw_scratch(const gm_conv_desc_hw* d);
+int gm_conv2d_wgrad_hw_bf16(const gm_conv_desc_hw* d, const void* dy, const void* x, float* dw, int c_real,
+                            int accumulate, void* scratch, size_t scratch_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * BatchNorm2d (torchvision ResNet trunk, reference src/model.py:65-106 through

@@ -111,6 +111,8 @@ def test_weight_prep_multi_matches_single(dev):
                               GMConv2d(64, 128, 3, padding=1, bias=False),
                               GMConv2d(128, 256, 1, stride=2, bias=False),
                               GMConv2d(256, 72, 3, padding=1, bias=False)).to(dev).to(memory_format=CL)
+    assert net[0].uses_pair_stem() and len(WeightPrep(net).copies) == 3  # the pair-view stem packs its own
+    net[0].pair_stem = False
     wp = WeightPrep(net)
     wp.run()
     torch.cuda.synchronize()
@@ -120,3 +122,33 @@ def test_weight_prep_multi_matches_single(dev):
         if wt is not None:
             assert torch.equal(wt, rt)
     assert wp.copies[0][2] is None  # stem: no transposed copy
+
+
+@pytest.mark.parametrize("shape", [(2, 3, 64, 64, 64, 7, 7, 2, 3), (1, 3, 224, 224, 64, 7, 7, 2, 3),
+                                   (3, 3, 37, 30, 64, 7, 7, 2, 3), (2, 4, 16, 18, 32, 5, 5, 2, 2)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_stem_pixel_pair_path(dev, shape):
+    """The RGB stem on the zero-bordered pixel-pair view (strides (2,1), K = R*ceil(S/2)*8)
+    == the fp32 convolution; weight gradient delivered in the parameter's layout."""
+    from greedy_multimodal_learning_amd.conv import GMConv2d
+    N, C, H, W, K, R, S, st, pad = shape
+    g = torch.Generator().manual_seed(sum(shape))
+    x = torch.randn(N, C, H, W, generator=g).bfloat16()
+    w = (torch.randn(K, C, R, S, generator=g) / (C * R * S) ** 0.5).bfloat16()
+    gy_shape = (N, K, (H + 2 * pad - R) // st + 1, (W + 2 * pad - S) // st + 1)
+    gy = torch.randn(*gy_shape, generator=g).bfloat16()
+    wr = w.float().requires_grad_(True)
+    yr = F.conv2d(x.float(), wr, stride=st, padding=pad)
+    yr.backward(gy.float())
+    m = GMConv2d(C, K, (R, S), stride=st, padding=pad, bias=False).to(dev)
+    with torch.no_grad():
+        m.weight.copy_(w.float())
+    m = m.to(memory_format=torch.channels_last)
+    assert m.uses_pair_stem()
+    xd = x.to(dev).contiguous(memory_format=torch.channels_last)
+    y = m(xd)
+    assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=torch.channels_last)
+    assert y.grad_fn is not None and "Stem" in type(y.grad_fn).__name__
+    y.backward(gy.to(dev).contiguous(memory_format=torch.channels_last))
+    _close(y, yr, 1e-2)
+    _close(m.weight.grad, wr.grad, 2e-3)
