@@ -44,6 +44,25 @@ def _cpad(c):
     return p
 
 
+_splitk_ws = {}
+
+
+def _splitk(device, d, dgrad):
+    """Split-K workspace of this (device, stream): (pointer, bytes), zeroed once at
+    allocation (the kernels leave their turnstile words at zero); per stream because
+    the two view trunks run concurrently (streams.py)."""
+    need = L.load().gm_conv2d_splitk_ws_bytes(ctypes.byref(d), int(dgrad))
+    if need == 0:
+        return 0, 0
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    key = (idx, torch.cuda.current_stream(idx).stream_id)
+    buf = _splitk_ws.get(key)
+    if buf is None or buf.numel() < need:
+        buf = torch.zeros((need + (1 << 20) - 1) >> 20 << 20, device=device, dtype=torch.uint8)
+        _splitk_ws[key] = buf
+    return buf.data_ptr(), buf.numel()
+
+
 def conv_fwd(x, w, stride, pad):
     """x [N,C,H,W] bf16 channels_last, w [K,C,R,S] bf16 channels_last -> y [N,K,P,Q]."""
     lib = L.load()
@@ -53,8 +72,9 @@ def conv_fwd(x, w, stride, pad):
     Q = (W + 2 * pad - S) // stride + 1
     y = torch.empty(N, K, P, Q, device=x.device, dtype=torch.bfloat16, memory_format=CL)
     d = _desc(N, H, W, C, K, R, S, stride, pad)
-    L.check(lib.gm_conv2d_fwd_bf16(ctypes.byref(d), x.data_ptr(), w.data_ptr(), y.data_ptr(),
-                                   L.stream_of(x.device)), "gm_conv2d_fwd_bf16")
+    ws, nb = _splitk(x.device, d, False)
+    L.check(lib.gm_conv2d_fwd_ex_bf16(ctypes.byref(d), x.data_ptr(), w.data_ptr(), y.data_ptr(), ws, nb,
+                                      L.stream_of(x.device)), "gm_conv2d_fwd_ex_bf16")
     return y
 
 
@@ -65,11 +85,7 @@ def conv_dgrad(dy, w, H, W, stride, pad):
     wt = torch.empty(C, K, R, S, device=w.device, dtype=torch.bfloat16, memory_format=CL)
     L.check(lib.gm_conv_weight_transpose_bf16(w.data_ptr(), wt.data_ptr(), K, R * S, C,
                                               L.stream_of(w.device)), "gm_conv_weight_transpose_bf16")
-    dx = torch.empty(N, C, H, W, device=dy.device, dtype=torch.bfloat16, memory_format=CL)
-    d = _desc(N, H, W, C, K, R, S, stride, pad)
-    L.check(lib.gm_conv2d_dgrad_bf16(ctypes.byref(d), dy.data_ptr(), wt.data_ptr(), dx.data_ptr(),
-                                     L.stream_of(dy.device)), "gm_conv2d_dgrad_bf16")
-    return dx
+    return conv_dgrad_t(dy, wt, H, W, stride, pad)
 
 
 def conv_wgrad(dy, x, R, S, stride, pad, c_real, out=None, accumulate=False):
@@ -284,8 +300,9 @@ def conv_dgrad_t(dy, wt, H, W, stride, pad):
     C, _, R, S = wt.shape
     dx = torch.empty(N, C, H, W, device=dy.device, dtype=torch.bfloat16, memory_format=CL)
     d = _desc(N, H, W, C, K, R, S, stride, pad)
-    L.check(lib.gm_conv2d_dgrad_bf16(ctypes.byref(d), dy.data_ptr(), wt.data_ptr(), dx.data_ptr(),
-                                     L.stream_of(dy.device)), "gm_conv2d_dgrad_bf16")
+    ws, nb = _splitk(dy.device, d, True)
+    L.check(lib.gm_conv2d_dgrad_ex_bf16(ctypes.byref(d), dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), ws, nb,
+                                        L.stream_of(dy.device)), "gm_conv2d_dgrad_ex_bf16")
     return dx
 
 

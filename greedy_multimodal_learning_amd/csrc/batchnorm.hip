@@ -184,18 +184,6 @@ __device__ __forceinline__ void finalize(const ReduceArgs& a, int c, double S1, 
 // relaxed agent-scope ticket; the block that draws the last ticket reads the
 // partials back with agent-scope atomic loads (sc1), so no L2 write-back or
 // invalidate is needed.  Returns true in that last block.
-template <typename T>
-__device__ __forceinline__ void st_sc1(T* p, T v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// sc1 loads through a buffer resource: plain (non-atomic) loads, so the compiler
-// keeps many in flight, yet they bypass the stale-able caches like the stores
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
-}
-__device__ __forceinline__ float4 ld_sc1_f32x4(__amdgpu_buffer_rsrc_t r, unsigned off_bytes) {
-    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off_bytes, 0, 16));
-}
 
 __device__ __forceinline__ bool ticket(unsigned* ctr, unsigned n, float* flag) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

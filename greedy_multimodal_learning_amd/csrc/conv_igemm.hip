@@ -63,6 +63,13 @@ struct ConvArgs {
     int sAh, sAw;             // input strides of the GEMM's A rows (H, W)
     int ncls;
     int xcd;                  // remap block ids so consecutive tiles share an XCD (L2)
+    // split-K (lean kernel): grid = splits x tiles, split-major; split s of a tile takes
+    // k-tiles [s*nk/S, (s+1)*nk/S) and the tile's splits hand their fp32 accumulators
+    // on in order 0 -> 1 -> ... -> S-1 through ws (turnstile flags[tile], zero between
+    // launches); the last split writes the output.  Deterministic (fixed order).
+    int splits, tiles_total;
+    float* ws;                // [tiles][MT*NT*16/4][256] float4
+    unsigned* flags;          // [tiles]
     ConvCls cls[kMaxCls];
 };
 
@@ -325,7 +332,12 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint4 smem[];
     char* lds = reinterpret_cast<char*>(smem);   // [A0][A1][B0][B1][taps]
 
-    const int bid = block_id(a.xcd);
+    int bid = block_id(a.xcd);
+    int split = 0;
+    if (a.splits > 1) {
+        split = bid / a.tiles_total;
+        bid -= split * a.tiles_total;
+    }
     int ci = 0;
 #pragma unroll
     for (int q = 1; q < kMaxCls; ++q)
@@ -336,7 +348,9 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
     const int m0 = tm * BM, n0 = tn * BN;
     const int PQ = cl.P * cl.Q;
     const int M = a.N * PQ;
-    const int nk = (cl.ntap * a.C) / BK;
+    const int nk_all = (cl.ntap * a.C) / BK;
+    const int kt0 = split * nk_all / a.splits;
+    const int nk = (split + 1) * nk_all / a.splits - kt0;
 
     const int t = threadIdx.x;
     const int lane = t & 63;
@@ -396,7 +410,7 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
     typedef __attribute__((address_space(1))) const void* gptr_t;
     typedef __attribute__((address_space(3))) void* lptr_t;
     auto issue = [&](int kt, int buf) {
-        const int k = kt * BK;
+        const int k = (kt0 + kt) * BK;
         const int tap = __builtin_amdgcn_readfirstlane(k >> a.logC);
         const int ti = (tap * cl.smag) >> 8, tj = tap - ti * cl.Sc;
         const int dh = (int)((pk_dh >> (4 * ti)) & 15u) - 8, dw = (int)((pk_dw >> (4 * tj)) & 15u) - 8;
@@ -455,6 +469,49 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
         __syncthreads();
     }
     if (kt < nk) compute(0);  // odd tile count: the last tile sits in buffer 0
+
+    if (a.splits > 1) {
+        constexpr int NQ = MT * NT * 4;  // float4 groups of accumulators per lane
+        const auto rs = rsrc_of(a.ws + (size_t)bid * NQ * 256 * 4);
+        if (split > 0) {  // wait for the previous split's running sum, then add it
+            if (t == 0) {
+                unsigned n = 0;  // bounded: a broken hand-off fails the parity tests, never hangs
+                while (__hip_atomic_load(a.flags + bid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
+                           (unsigned)split && ++n < (1u << 22))
+                    __builtin_amdgcn_s_sleep(2);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const float4 v = ld_sc1_f32x4(rs, (unsigned)((((i * NT + j) * 4 + g) * 256 + t) * 16));
+                        acc[i][j][4 * g] += v.x;
+                        acc[i][j][4 * g + 1] += v.y;
+                        acc[i][j][4 * g + 2] += v.z;
+                        acc[i][j][4 * g + 3] += v.w;
+                    }
+        }
+        if (split < a.splits - 1) {  // publish the running sum to the next split
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g)
+                        st_sc1_f32x4(rs, (unsigned)((((i * NT + j) * 4 + g) * 256 + t) * 16),
+                                     make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2],
+                                                 acc[i][j][4 * g + 3]));
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (t == 0) __hip_atomic_store(a.flags + bid, (unsigned)(split + 1), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        if (t == 0) __hip_atomic_store(a.flags + bid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
@@ -525,6 +582,8 @@ static int launch_igemm(ConvArgs& a, hipStream_t st) {
         tiles += c.tiles_m * ((a.Nout + BN - 1) / BN);
     }
     if (tiles == 0) return GM_OK;
+    a.tiles_total = tiles;
+    if (a.splits < 1) a.splits = 1;
     const size_t lds = (size_t)ST * (BM + BN) * 128 + kMaxTap * 4 + 12;
     static bool attr_set = false;  // idempotent, safe to race
     if (!attr_set) {
@@ -544,7 +603,10 @@ static int launch_igemm(ConvArgs& a, hipStream_t st) {
                                 (int)lds2);
             attr2 = true;
         }
-        k_conv_igemm_ut<BM, BN><<<tiles, 256, lds2, st>>>(a);
+        k_conv_igemm_ut<BM, BN><<<tiles * a.splits, 256, lds2, st>>>(a);
+    } else if (a.splits > 1) {
+        set_error("conv: split-K needs the lean kernel");
+        return GM_E_ARG;
     } else if (a.C >= 64) {
         k_conv_igemm<BM, BN, true, ST><<<tiles, 256, lds, st>>>(a);
     } else {
@@ -577,19 +639,87 @@ static int tile_bias() {
     return b;
 }
 
-static int pick_and_launch(ConvArgs& a, hipStream_t st) {
+static int splitk_target() {
+    static int t = [] {
+        const char* e = getenv("GM_CONV_SPLITK");  // workgroups wanted from split-K; 0 disables it
+        return e ? atoi(e) : 384;
+    }();
+    return t;
+}
+
+static int splitk_mink() {
+    static int t = [] {
+        const char* e = getenv("GM_CONV_SPLITK_MINK");  // minimum k-tiles per split
+        return e ? atoi(e) : 16;
+    }();
+    return t;
+}
+
+enum { T128x128 = 0, T128x64 = 1, T64x64 = 2 };
+struct TilePick {
+    int tile, splits, tiles;
+};
+
+static bool lean_ok(const ConvArgs& a) {
+    bool grid = a.C >= 64 && lean_path();
+    for (int i = 0; i < a.ncls; ++i) grid = grid && grid_ok(a.cls[i], a.Sw);
+    return grid;
+}
+
+// enough workgroups to fill 256 CUs with the largest tile that does (128x128: 4
+// independent accumulators per wave, so one workgroup per CU keeps the MFMA pipe fed);
+// when 128x128 tiles alone are too few (layers 3/4: small M, long K), split K over
+// 2-4 workgroups per tile (turnstile hand-off, lean kernel only) instead of shrinking
+// the tile, which halves the staged bytes per FLOP against 64x64.
+static TilePick pick_tile(const ConvArgs& a) {
     long M = 0;
-    for (int i = 0; i < a.ncls; ++i) M += (long)a.N * a.cls[i].P * a.cls[i].Q;
-    const bool three = stages() == 3;
+    int t128 = 0, nkmin = 1 << 30;
+    for (int i = 0; i < a.ncls; ++i) {
+        const long Mi = (long)a.N * a.cls[i].P * a.cls[i].Q;
+        M += Mi;
+        t128 += (int)((Mi + 127) / 128) * ((a.Nout + 127) / 128);
+        const int nk = a.cls[i].ntap * a.C / 64;
+        nkmin = nk < nkmin ? nk : nkmin;
+    }
     const long wgs = tile_bias();  // workgroups wanted before a larger tile is taken
-    a.xcd = xcd_remap();
-    // enough workgroups to fill 256 CUs, largest tile that does (128x128: 4 independent
-    // accumulators per wave, so one workgroup per CU already keeps the MFMA pipe fed)
-    if (a.Nout >= 128 && M / 128 * (a.Nout / 128) >= wgs / 4)
-        return three ? launch_igemm<128, 128, 3>(a, st) : launch_igemm<128, 128, 2>(a, st);
-    if (M / 128 * ((a.Nout + 63) / 64) >= wgs * 3 / 4)
-        return three ? launch_igemm<128, 64, 3>(a, st) : launch_igemm<128, 64, 2>(a, st);
-    return three ? launch_igemm<64, 64, 3>(a, st) : launch_igemm<64, 64, 2>(a, st);
+    if (a.Nout >= 128 && M / 128 * (a.Nout / 128) >= wgs / 4) return {T128x128, 1, t128};
+    const int want = splitk_target();
+    if (want > 0 && a.Nout >= 128 && a.C >= 64 && t128 > 0 && lean_ok(a)) {
+        int S = (want + t128 - 1) / t128;
+        if (S > 4) S = 4;
+        while (S > 1 && nkmin / S < splitk_mink()) --S;  // long enough splits to amortize the hand-off
+        if (S >= 2) return {T128x128, S, t128};
+    }
+    if (M / 128 * ((a.Nout + 63) / 64) >= wgs * 3 / 4) return {T128x64, 1, 0};
+    return {T64x64, 1, 0};
+}
+
+static size_t splitk_flag_bytes(int tiles) { return ((size_t)tiles * 4 + 255) / 256 * 256; }
+
+static size_t splitk_bytes(const TilePick& p) {
+    if (p.splits <= 1) return 0;
+    return splitk_flag_bytes(p.tiles) + (size_t)p.tiles * 16 * 256 * 16;  // 128x128: 16 float4 per lane
+}
+
+static int pick_and_launch(ConvArgs& a, hipStream_t st, void* ws, size_t ws_bytes) {
+    const bool three = stages() == 3;
+    TilePick p = pick_tile(a);
+    if (p.splits > 1 && (!ws || ws_bytes < splitk_bytes(p))) {  // no workspace: the unsplit choice
+        long M = 0;
+        for (int i = 0; i < a.ncls; ++i) M += (long)a.N * a.cls[i].P * a.cls[i].Q;
+        p = {M / 128 * ((a.Nout + 63) / 64) >= tile_bias() * 3 / 4 ? T128x64 : T64x64, 1, 0};
+    }
+    a.splits = p.splits;
+    a.xcd = p.splits > 1 ? 0 : xcd_remap();  // split-K relies on split-major dispatch order
+    if (p.splits > 1) {
+        a.flags = static_cast<unsigned*>(ws);
+        a.ws = reinterpret_cast<float*>(static_cast<char*>(ws) + splitk_flag_bytes(p.tiles));
+    }
+    switch (p.tile) {
+    case T128x128: return three ? launch_igemm<128, 128, 3>(a, st) : launch_igemm<128, 128, 2>(a, st);
+    case T128x64: return three ? launch_igemm<128, 64, 3>(a, st) : launch_igemm<128, 64, 2>(a, st);
+    default: return three ? launch_igemm<64, 64, 3>(a, st) : launch_igemm<64, 64, 2>(a, st);
+    }
 }
 
 // the class's taps as a grid: rows r (stride-compatible with the class parity ph) and
@@ -685,14 +815,9 @@ static int check_desc_hw(const gm_conv_desc_hw* d) {
     return GM_OK;
 }
 
-extern "C" int gm_conv2d_fwd_hw_bf16(const gm_conv_desc_hw* d, const void* x, const void* w, void* y,
-                                     void* stream) {
-    int rc = check_desc_hw(d);
-    if (rc) return rc;
-    GM_REQUIRE(x && w && y, "conv fwd: null pointer");
+static void fwd_setup(const gm_conv_desc_hw* d, const void* x, const void* w, void* y, ConvArgs& a) {
     const int P = (d->H + 2 * d->pad_h - d->R) / d->stride_h + 1;
     const int Q = (d->W + 2 * d->pad_w - d->S) / d->stride_w + 1;
-    ConvArgs a;
     memset(&a, 0, sizeof(a));
     a.in = (const uint16_t*)x;
     a.wt = (const uint16_t*)w;
@@ -712,27 +837,13 @@ extern "C" int gm_conv2d_fwd_hw_bf16(const gm_conv_desc_hw* d, const void* x, co
             c.dw[i] = (signed char)(s - d->pad_w);
         }
     set_grid_fwd(c, d);
-    return pick_and_launch(a, as_stream(stream));
 }
 
-extern "C" int gm_conv2d_fwd_bf16(const gm_conv_desc* d, const void* x, const void* w, void* y, void* stream) {
-    int rc = check_desc(d);
-    if (rc) return rc;
-    const gm_conv_desc_hw h = {d->N, d->H, d->W, d->C, d->K, d->R, d->S, d->stride, d->stride, d->pad, d->pad};
-    return gm_conv2d_fwd_hw_bf16(&h, x, w, y, stream);
-}
-
-extern "C" int gm_conv2d_dgrad_bf16(const gm_conv_desc* d, const void* dy, const void* wt, void* dx,
-                                    void* stream) {
-    int rc = check_desc(d);
-    if (rc) return rc;
-    GM_REQUIRE(dy && wt && dx, "conv dgrad: null pointer");
-    GM_REQUIRE(ilog2(d->K) >= 3, "conv dgrad: K must be a power of two >= 8 (got %d)", d->K);
+// returns false when some output pixels belong to no parity class (they must be zeroed)
+static bool dgrad_setup(const gm_conv_desc* d, const void* dy, const void* wt, void* dx, ConvArgs& a) {
     const int st = d->stride;
-    GM_REQUIRE(st * st <= kMaxCls, "conv dgrad: stride %d unsupported", st);
     const int P = (d->H + 2 * d->pad - d->R) / st + 1;
     const int Q = (d->W + 2 * d->pad - d->S) / st + 1;
-    ConvArgs a;
     memset(&a, 0, sizeof(a));
     a.in = (const uint16_t*)dy;
     a.wt = (const uint16_t*)wt;
@@ -740,7 +851,6 @@ extern "C" int gm_conv2d_dgrad_bf16(const gm_conv_desc* d, const void* dy, const
     a.Nout = d->C; a.T = d->R * d->S; a.Sw = d->S;
     a.Ho = d->H; a.Wo = d->W; a.sAh = a.sAw = 1;
     bool full = true;
-    hipStream_t s = as_stream(stream);
     for (int ph = 0; ph < st; ++ph)
         for (int pw = 0; pw < st; ++pw) {
             ConvCls& c = a.cls[a.ncls];
@@ -764,13 +874,79 @@ extern "C" int gm_conv2d_dgrad_bf16(const gm_conv_desc* d, const void* dy, const
             set_grid(c, d, st, ph, pw);
             ++a.ncls;
         }
+    return full;
+}
+
+static int check_dgrad(const gm_conv_desc* d) {
+    int rc = check_desc(d);
+    if (rc) return rc;
+    GM_REQUIRE(ilog2(d->K) >= 3, "conv dgrad: K must be a power of two >= 8 (got %d)", d->K);
+    GM_REQUIRE(d->stride * d->stride <= kMaxCls, "conv dgrad: stride %d unsupported", d->stride);
+    return GM_OK;
+}
+
+static gm_conv_desc_hw to_hw(const gm_conv_desc* d) {
+    return gm_conv_desc_hw{d->N, d->H, d->W, d->C, d->K, d->R, d->S, d->stride, d->stride, d->pad, d->pad};
+}
+
+extern "C" int gm_conv2d_fwd_hw_bf16(const gm_conv_desc_hw* d, const void* x, const void* w, void* y,
+                                     void* stream) {
+    int rc = check_desc_hw(d);
+    if (rc) return rc;
+    GM_REQUIRE(x && w && y, "conv fwd: null pointer");
+    ConvArgs a;
+    fwd_setup(d, x, w, y, a);
+    return pick_and_launch(a, as_stream(stream), nullptr, 0);
+}
+
+extern "C" int gm_conv2d_fwd_ex_bf16(const gm_conv_desc* d, const void* x, const void* w, void* y, void* ws,
+                                     size_t ws_bytes, void* stream) {
+    int rc = check_desc(d);
+    if (rc) return rc;
+    GM_REQUIRE(x && w && y, "conv fwd: null pointer");
+    const gm_conv_desc_hw h = to_hw(d);
+    ConvArgs a;
+    fwd_setup(&h, x, w, y, a);
+    return pick_and_launch(a, as_stream(stream), ws, ws_bytes);
+}
+
+extern "C" int gm_conv2d_fwd_bf16(const gm_conv_desc* d, const void* x, const void* w, void* y, void* stream) {
+    return gm_conv2d_fwd_ex_bf16(d, x, w, y, nullptr, 0, stream);
+}
+
+extern "C" int gm_conv2d_dgrad_ex_bf16(const gm_conv_desc* d, const void* dy, const void* wt, void* dx, void* ws,
+                                       size_t ws_bytes, void* stream) {
+    int rc = check_dgrad(d);
+    if (rc) return rc;
+    GM_REQUIRE(dy && wt && dx, "conv dgrad: null pointer");
+    ConvArgs a;
+    const bool full = dgrad_setup(d, dy, wt, dx, a);
+    hipStream_t s = as_stream(stream);
     if (!full) {
         const size_t n = (size_t)d->N * d->H * d->W * d->C;
         k_zero_bf16<<<(int)((n / 8 + 255) / 256 < 4096 ? (n / 8 + 255) / 256 : 4096), 256, 0, s>>>((uint16_t*)dx, n);
         rc = check_launch("k_zero_bf16");
         if (rc) return rc;
     }
-    return pick_and_launch(a, s);
+    return pick_and_launch(a, s, ws, ws_bytes);
+}
+
+extern "C" int gm_conv2d_dgrad_bf16(const gm_conv_desc* d, const void* dy, const void* wt, void* dx,
+                                    void* stream) {
+    return gm_conv2d_dgrad_ex_bf16(d, dy, wt, dx, nullptr, 0, stream);
+}
+
+extern "C" size_t gm_conv2d_splitk_ws_bytes(const gm_conv_desc* d, int dgrad) {
+    ConvArgs a;
+    if (dgrad) {
+        if (check_dgrad(d)) return 0;
+        dgrad_setup(d, nullptr, nullptr, nullptr, a);
+    } else {
+        if (check_desc(d)) return 0;
+        const gm_conv_desc_hw h = to_hw(d);
+        fwd_setup(&h, nullptr, nullptr, nullptr, a);
+    }
+    return splitk_bytes(pick_tile(a));
 }
 
 extern "C" int gm_conv_weight_transpose_bf16(const void* w, void* wt, int Co, int T, int Ci, void* stream) {

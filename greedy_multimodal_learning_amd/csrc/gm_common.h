@@ -75,4 +75,25 @@ struct FastDiv {
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// ---- cross-workgroup hand-off without fences (cdna_hip_programming.md, in-launch
+// split-K recipe, sc1 form): the producer writes with sc1 (write-through) stores,
+// drains vmcnt, barriers and publishes with a relaxed agent-scope atomic; the
+// consumer observes the atomic and reads with sc1 loads (L2-served, never stale) ----
+template <typename T>
+__device__ __forceinline__ void st_sc1(T* p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// sc1 accesses through a buffer resource: plain (non-atomic) instructions, so many
+// stay in flight; cache-policy bit 16 = sc1 on gfx950
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ float4 ld_sc1_f32x4(__amdgpu_buffer_rsrc_t r, unsigned off_bytes) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off_bytes, 0, 16));
+}
+__device__ __forceinline__ void st_sc1_f32x4(__amdgpu_buffer_rsrc_t r, unsigned off_bytes, float4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), r,
+                                           off_bytes, 0, 16);
+}
+
 }  // namespace gm

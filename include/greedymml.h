@@ -193,6 +193,17 @@ typedef struct gm_conv_desc_hw {
 } gm_conv_desc_hw;
 int gm_conv2d_fwd_hw_bf16(const gm_conv_desc_hw* d, const void* x, const void* w, void* y, void* stream);
 int gm_conv2d_dgrad_bf16(const gm_conv_desc* d, const void* dy, const void* wt, void* dx, void* stream);
+/* Same convolutions with a caller-owned split-K workspace: when 128x128 tiles alone
+ * would not fill the chip (small M, long K: ResNet layers 3/4) each tile's K range is
+ * split over 2-4 workgroups that hand their fp32 accumulators on in a fixed order
+ * (deterministic).  ws >= gm_conv2d_splitk_ws_bytes(d, dgrad) bytes (0 = no split for
+ * this shape; ws may then be NULL), ZEROED ONCE before first use (the kernel leaves
+ * its turnstile words at zero); calls sharing one ws must be stream-ordered. */
+size_t gm_conv2d_splitk_ws_bytes(const gm_conv_desc* d, int dgrad);
+int gm_conv2d_fwd_ex_bf16(const gm_conv_desc* d, const void* x, const void* w, void* y, void* ws,
+                          size_t ws_bytes, void* stream);
+int gm_conv2d_dgrad_ex_bf16(const gm_conv_desc* d, const void* dy, const void* wt, void* dx, void* ws,
+                            size_t ws_bytes, void* stream);
 int gm_conv_weight_transpose_bf16(const void* w, void* wt, int K, int RS, int C, void* stream);
 /* fp32 KRSC master weight -> bf16 [K][RS][Cp] (zero-padded channels) and, if wt != NULL,
  * the transposed bf16 [Cp][RS][K] for dgrad, in one pass */

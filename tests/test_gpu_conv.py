@@ -152,3 +152,32 @@ def test_stem_pixel_pair_path(dev, shape):
     y.backward(gy.to(dev).contiguous(memory_format=torch.channels_last))
     _close(y, yr, 1e-2)
     _close(m.weight.grad, wr.grad, 2e-3)
+
+
+@pytest.mark.parametrize("shape", [(64, 256, 14, 14, 256, 3, 3, 1, 1), (64, 512, 7, 7, 512, 3, 3, 1, 1),
+                                   (64, 256, 14, 14, 512, 3, 3, 2, 1), (8, 512, 7, 7, 512, 3, 3, 1, 1), (64, 256, 14, 14, 512, 3, 3, 2, 1)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_conv_splitk_turnstile(dev, shape):
+    """Layer-3/4 shapes take 128x128 tiles with K split over 2-4 workgroups that hand
+    their fp32 accumulators on in a fixed order: same result as the fp32 convolution,
+    bit-identical across runs (deterministic), workspace left reusable."""
+    import ctypes
+    from greedy_multimodal_learning_amd import _lib as L
+    from greedy_multimodal_learning_amd import conv as G
+    N, C, H, W, K, R, S, st, pad = shape
+    d = G._desc(N, H, W, C, K, R, S, st, pad)
+    assert L.load().gm_conv2d_splitk_ws_bytes(ctypes.byref(d), 0) > 0  # the split path is taken
+    g = torch.Generator(device="cuda").manual_seed(sum(shape))
+    CL = torch.channels_last
+    x = torch.randn(N, C, H, W, device=dev, generator=g).bfloat16().contiguous(memory_format=CL)
+    w = (torch.randn(K, C, R, S, device=dev, generator=g) / (C * R * S) ** 0.5).bfloat16().contiguous(memory_format=CL)
+    P, Q = (H + 2 * pad - R) // st + 1, (W + 2 * pad - S) // st + 1
+    dy = torch.randn(N, K, P, Q, device=dev, generator=g).bfloat16().contiguous(memory_format=CL)
+    y1, y2 = G.conv_fwd(x, w, st, pad), G.conv_fwd(x, w, st, pad)
+    dx1, dx2 = G.conv_dgrad(dy, w, H, W, st, pad), G.conv_dgrad(dy, w, H, W, st, pad)
+    assert torch.equal(y1, y2) and torch.equal(dx1, dx2)
+    yr = F.conv2d(x.float(), w.float(), stride=st, padding=pad)
+    dxr = torch.ops.aten.convolution_backward(dy.float(), x.float(), w.float(), None, [st, st], [pad, pad], [1, 1],
+                                              False, [0, 0], 1, [True, False, False])[0]
+    _close(y1, yr, 1e-2)
+    _close(dx1, dxr, 1e-2)
