@@ -139,10 +139,61 @@ __device__ __forceinline__ void accum(const ReduceArgs& a, long long v, const fl
     }
 }
 
+// accum() on already loaded vectors (zero vectors contribute nothing in every mode)
 template <int MODE>
-__device__ __forceinline__ void finalize(const ReduceArgs& a, int c, double S1, double S2, double invM) {
+__device__ __forceinline__ void accum_vals(uint4 ux, uint4 ud, uint4 uy, const float* mu, float* s1, float* s2) {
+    float xf[8];
+    unpack8(ux, xf);
+    if (MODE == FWD) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            s1[j] += xf[j];
+            s2[j] = fmaf(xf[j], xf[j], s2[j]);
+        }
+    } else {
+        float d[8];
+        unpack8(ud, d);
+        if (MODE == BWD_RELU) {
+            float yf[8];
+            unpack8(uy, yf);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) d[j] = yf[j] > 0.f ? d[j] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            s1[j] += d[j];
+            s2[j] = fmaf(d[j], xf[j] - mu[j], s2[j]);
+        }
+    }
+}
+
+// per-channel operands of finalize(), loaded by every block BEFORE its ticket so the
+// last block's dependent chain after the ticket has one memory round trip fewer
+struct FinOps {
+    float g, b, rm, rv;  // FWD: gamma, beta, running mean/var; BWD: gamma, -, save_mean, save_invstd
+};
+
+template <int MODE>
+__device__ __forceinline__ FinOps fin_load(const ReduceArgs& a, int c) {
+    FinOps f;
+    f.g = a.gamma[c];
+    if (MODE == FWD) {
+        f.b = a.beta[c];
+        f.rm = a.rmean ? a.rmean[c] : 0.f;
+        f.rv = a.rmean ? a.rvar[c] : 0.f;
+    } else {
+        f.b = 0.f;
+        f.rm = a.save_mean[c];
+        f.rv = a.save_invstd[c];
+    }
+    return f;
+}
+
+template <int MODE>
+__device__ __forceinline__ void finalize(const ReduceArgs& a, int c, double S1, double S2, double invM,
+                                         const FinOps& f) {
     const int C = a.C;
-    const double g = (double)a.gamma[c];
+    const double g = (double)f.g;
     if (MODE == FWD) {
         const double mean = S1 * invM;
         double var = S2 * invM - mean * mean;
@@ -150,18 +201,18 @@ __device__ __forceinline__ void finalize(const ReduceArgs& a, int c, double S1, 
         const double invstd = 1.0 / sqrt(var + (double)a.eps);
         const double sc = g * invstd;
         a.coef[c] = (float)sc;
-        a.coef[C + c] = (float)((double)a.beta[c] - mean * sc);
+        a.coef[C + c] = (float)((double)f.b - mean * sc);
         a.save_mean[c] = (float)mean;
         a.save_invstd[c] = (float)invstd;
         if (a.rmean) {
             const double m = (double)a.momentum;
             const double unb = a.M > 1 ? var * (double)a.M / (double)(a.M - 1) : var;
-            a.rmean[c] = (float)((1.0 - m) * (double)a.rmean[c] + m * mean);
-            a.rvar[c] = (float)((1.0 - m) * (double)a.rvar[c] + m * unb);
+            a.rmean[c] = (float)((1.0 - m) * (double)f.rm + m * mean);
+            a.rvar[c] = (float)((1.0 - m) * (double)f.rv + m * unb);
         }
     } else {
-        const double mean = (double)a.save_mean[c];
-        const double is = (double)a.save_invstd[c];
+        const double mean = (double)f.rm;
+        const double is = (double)f.rv;
         const double ca = g * is;
         const double cb = -g * is * is * is * S2 * invM;
         a.coef[c] = (float)ca;
@@ -233,7 +284,16 @@ __global__ __launch_bounds__(kT) void k_bn_reduce(ReduceArgs a) {
 #pragma unroll
         for (int u = 0; u < 8; ++u) accum<MODE>(a, v + u * st, mu, s1, s2);
     }
-    for (; r < rend; r += rpp) accum<MODE>(a, r * vpr + cv, mu, s1, s2);
+    if (MODE == FWD && r < rend) {  // the tail as ONE predicated batch: all its loads in flight
+        uint4 vx[8];
+        const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) vx[u] = a.x[(r + u * rpp < rend ? r + u * rpp : r) * vpr + cv];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) accum_vals<MODE>(r + u * rpp < rend ? vx[u] : z, z, z, mu, s1, s2);
+    } else {
+        for (; r < rend; r += rpp) accum<MODE>(a, r * vpr + cv, mu, s1, s2);
+    }
 
     // row-group combine in LDS: red[r0][SW][2]  (rpp * 2SW == 4096 floats)
     const int S2w = 2 * SW;
@@ -249,6 +309,8 @@ __global__ __launch_bounds__(kT) void k_bn_reduce(ReduceArgs a) {
         for (int i = 0; i < rpp; ++i) acc += red[i * S2w + t];
         st_sc1(&p1[t], acc);
     }
+    FinOps fo{};
+    if (t < SW) fo = fin_load<MODE>(a, cs * SW + t);  // in flight with the partial store
     // the last block of the slice combines its nrc partial rows: lane group of L
     // threads per row (one float4 each), G = 256/L row groups, rows g, g+G, ...
     if (!ticket(a.counter + cs, (unsigned)a.nrc, &red[kRedF])) return;
@@ -282,7 +344,7 @@ __global__ __launch_bounds__(kT) void k_bn_reduce(ReduceArgs a) {
             S1 += rd[i * S2w + 2 * t];
             S2 += rd[i * S2w + 2 * t + 1];
         }
-        finalize<MODE>(a, cs * SW + t, S1, S2, 1.0 / (double)a.M);
+        finalize<MODE>(a, cs * SW + t, S1, S2, 1.0 / (double)a.M, fo);
     }
 }
 

@@ -16,6 +16,7 @@ namespace {
 struct PoolArgs {
     int N, H, W, C8;  // C8 = C / 8 (16-byte channel groups)
     int P, Q, k, s, pad;
+    FastDiv fd_c8, fd_q, fd_p, fd_w, fd_h, fd_s;  // index decode without integer division
 };
 
 __device__ __forceinline__ void unpack8(uint4 u, float* f) {
@@ -27,12 +28,13 @@ __global__ __launch_bounds__(256) void k_maxpool_fwd(PoolArgs a, const uint4* __
                                                      uint2* __restrict__ idx) {
     const unsigned total = (unsigned)a.N * a.P * a.Q * a.C8;  // < 2^31 (checked on the host)
     for (unsigned i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
-        const int cg = (int)(i % a.C8);
-        unsigned t = i / a.C8;
-        const int q = (int)(t % a.Q);
-        t /= a.Q;
-        const int p = (int)(t % a.P);
-        const int n = (int)(t / a.P);
+        unsigned t = a.fd_c8.div(i);
+        const int cg = (int)(i - t * a.C8);
+        unsigned t2 = a.fd_q.div(t);
+        const int q = (int)(t - t2 * a.Q);
+        const unsigned n_ = a.fd_p.div(t2);
+        const int p = (int)(t2 - n_ * a.P);
+        const int n = (int)n_;
         const int h0 = p * a.s - a.pad, w0 = q * a.s - a.pad;
         float m[8];
         uint32_t ix[8];
@@ -71,20 +73,21 @@ __global__ __launch_bounds__(256) void k_maxpool_bwd(PoolArgs a, const uint4* __
                                                      const uint2* __restrict__ idx, uint4* __restrict__ dx) {
     const unsigned total = (unsigned)a.N * a.H * a.W * a.C8;
     for (unsigned i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
-        const int cg = (int)(i % a.C8);
-        unsigned t = i / a.C8;
-        const int w = (int)(t % a.W);
-        t /= a.W;
-        const int h = (int)(t % a.H);
-        const int n = (int)(t / a.H);
+        unsigned t = a.fd_c8.div(i);
+        const int cg = (int)(i - t * a.C8);
+        unsigned t2 = a.fd_w.div(t);
+        const int w = (int)(t - t2 * a.W);
+        const unsigned n_ = a.fd_h.div(t2);
+        const int h = (int)(t2 - n_ * a.H);
+        const int n = (int)n_;
         // windows p with p*s - pad <= h <= p*s - pad + k - 1
         int plo = h + a.pad - a.k + 1;
-        plo = plo <= 0 ? 0 : (plo + a.s - 1) / a.s;
-        int phi = (h + a.pad) / a.s;
+        plo = plo <= 0 ? 0 : (int)a.fd_s.div((unsigned)(plo + a.s - 1));
+        int phi = (int)a.fd_s.div((unsigned)(h + a.pad));
         if (phi > a.P - 1) phi = a.P - 1;
         int qlo = w + a.pad - a.k + 1;
-        qlo = qlo <= 0 ? 0 : (qlo + a.s - 1) / a.s;
-        int qhi = (w + a.pad) / a.s;
+        qlo = qlo <= 0 ? 0 : (int)a.fd_s.div((unsigned)(qlo + a.s - 1));
+        int qhi = (int)a.fd_s.div((unsigned)(w + a.pad));
         if (qhi > a.Q - 1) qhi = a.Q - 1;
         float g[8];
 #pragma unroll
@@ -130,6 +133,12 @@ int prep(const gm_pool_desc* d, PoolArgs& a, const char* fn) {
         set_error("%s: tensor too large (N*H*W*C/8 >= 2^31)", fn);
         return GM_E_ARG;
     }
+    a.fd_c8 = FastDiv((uint32_t)a.C8);
+    a.fd_q = FastDiv((uint32_t)a.Q);
+    a.fd_p = FastDiv((uint32_t)a.P);
+    a.fd_w = FastDiv((uint32_t)a.W);
+    a.fd_h = FastDiv((uint32_t)a.H);
+    a.fd_s = FastDiv((uint32_t)a.s);
     return GM_OK;
 }
 
