@@ -117,6 +117,38 @@ def time_trunk_igemm(B, dev, reps=10):
     return flops, secs, launches
 
 
+def time_mmtm_reduce(dev, B=256, reps=20):
+    """HBM roofline of the MMTM squeeze (global-average-pool of both views' activations,
+    k_colreduce_nhwc via gm_mmtm_spatial_reduce) at the north-star batch 256, on the
+    largest site (s2: 128 ch x 28x28 per view), the exact launch MMTM_mitigate.forward
+    issues (balanced_mmtm.py).  Algorithmic bytes = both views' bf16 activations read
+    once; time = HIP events on the launch stream behind a device sleep."""
+    from greedy_multimodal_learning_amd import ops
+    from greedy_multimodal_learning_amd import _lib as L
+    CL = torch.channels_last
+    C, H = 128, 28
+    xv = torch.randn(B, C, H, H, device=dev).bfloat16().contiguous(memory_format=CL)
+    xs = torch.randn(B, C, H, H, device=dev).bfloat16().contiguous(memory_format=CL)
+    sq = torch.empty(B, 2 * C, device=dev)
+    probs = [dict(x=xv, C=C, HW=H * H, out=sq, ld_out=2 * C, scale=1.0 / (H * H)),
+             dict(x=xs, C=C, HW=H * H, out=sq, out_off=C, ld_out=2 * C, scale=1.0 / (H * H))]
+
+    def op():
+        ops.spatial_reduce(probs, B, L.GM_BF16, L.GM_NHWC, dev)
+    op()
+    torch.cuda.synchronize()
+    torch.cuda._sleep(20_000_000)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        op()
+    e1.record()
+    torch.cuda.synchronize()
+    secs = e0.elapsed_time(e1) / reps / 1e3
+    nbytes = 2 * B * C * H * H * 2
+    return nbytes, secs
+
+
 def time_group_sumsq(step, n):
     """Average duration of the fused norms+SGD launch, HIP events on its stream; a
     leading ~20 ms device sleep keeps the GPU busy while the host enqueues, so the
@@ -200,6 +232,7 @@ def main():
     # same launch the step runs (inside the graph), timed with HIP events on its stream
     kern_avg_s = time_group_sumsq(step, 10)
     conv_flops, conv_s, conv_launches = time_trunk_igemm(B, dev)
+    mmtm_bytes, mmtm_s = time_mmtm_reduce(dev)
 
     if rank == 0:
         views = 2
@@ -239,6 +272,13 @@ def main():
                              "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                              "traffic": traffic, "alg_bytes_per_launch": bytes_alg,
                              "avg_launch_us": round(kern_avg_s * 1e6, 2)},
+            "roofline_mmtm": {"kernel": "k_colreduce_nhwc (MMTM squeeze: GAP of both views, site s2, "
+                                        "north-star batch 256, gm_mmtm_spatial_reduce)",
+                              "bound": "hbm", "batch": 256,
+                              "achieved": round(mmtm_bytes / mmtm_s / 1e9, 1), "peak": HBM_PEAK_GBS,
+                              "unit": "GB/s", "frac": round(mmtm_bytes / mmtm_s / 1e9 / HBM_PEAK_GBS, 4),
+                              "traffic": None, "alg_bytes_per_launch": mmtm_bytes,
+                              "avg_launch_us": round(mmtm_s * 1e6, 2)},
         }
         if not a.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(a.cpu_seconds, a.size)

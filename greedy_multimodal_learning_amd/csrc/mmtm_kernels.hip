@@ -13,6 +13,8 @@
 //         (deterministic, no float atomics).
 #include <cstring>
 
+#include <cstdlib>
+
 #include "gm_common.h"
 
 namespace gm {
@@ -138,7 +140,7 @@ __global__ __launch_bounds__(256) void k_colreduce_nhwc(RedArgs a) {
     for (int j = 0; j < N; ++j) acc[j] = 0.f;
     if (pl < ppi) {
         const size_t bbase = (size_t)b * p.HW * p.C + (size_t)cc * N;
-        for (int hw = hw0 + pl; hw < hw1; hw += ppi) {
+        auto one = [&](int hw) {
             const size_t off = bbase + (size_t)hw * p.C;
             float vx[N];
             VecLd<T, 16>::ld((const T*)p.x + off, vx);
@@ -151,7 +153,15 @@ __global__ __launch_bounds__(256) void k_colreduce_nhwc(RedArgs a) {
 #pragma unroll
                 for (int j = 0; j < N; ++j) acc[j] += vx[j];
             }
+        };
+        int hw = hw0 + pl;
+        // 4 pixels per thread per round: their loads are independent, so all four are in
+        // flight together (an HBM-latency-bound loop otherwise)
+        for (; hw + 3 * ppi < hw1; hw += 4 * ppi) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) one(hw + u * ppi);
         }
+        for (; hw < hw1; hw += ppi) one(hw);
     }
     // LDS layout [pl][C]: thread (cc, pl) writes its N channels
     if (pl < ppi) {
@@ -347,6 +357,14 @@ using namespace gm;
 
 // ======================= host entry points =======================
 
+static int red_wgs() {
+    static int w = [] {
+        const char* e = getenv("GM_MMTM_RED_WGS");  // workgroups wanted for the NHWC squeeze
+        return e ? atoi(e) : 512;  // B=256: one workgroup per (sample, view), no partials pass
+    }();
+    return w;
+}
+
 static int red_setup(const gm_spatial_reduce* in, int nprob, int B, int dtype, int layout,
                      RedArgs& a, size_t& scratch_need, int& nwg, int& vb) {
     GM_REQUIRE(in && nprob >= 1 && nprob <= kMaxProb, "spatial_reduce: nprob must be 1..%d", kMaxProb);
@@ -382,7 +400,7 @@ static int red_setup(const gm_spatial_reduce* in, int nprob, int B, int dtype, i
             GM_REQUIRE(aligned(s.x, 16) && (!s.dy || aligned(s.dy, 16)),
                        "spatial_reduce[%d]: NHWC tensors must be 16-byte aligned", i);
             const int tpp = s.C * es / 16, ppi = 256 / tpp;
-            int S = (2048 + nprob * B - 1) / (nprob * B);
+            int S = (red_wgs() + nprob * B - 1) / (nprob * B);
             const int maxS = (s.HW + 2 * ppi - 1) / (2 * ppi);
             S = S < 1 ? 1 : (S > maxS ? maxS : S);
             if (S < 1) S = 1;
