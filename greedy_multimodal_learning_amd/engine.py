@@ -20,7 +20,7 @@ re-organised for the hardware:
   decision (the decision applies to the NEXT forward, as in the reference);
 * the trunk runs in bf16 (autocast) on channels_last activations; master
   weights, gradients, the MMTM FC chain and all reductions stay fp32;
-* `graphs=True` (single process): after one eager step, each curation setting
+* `graphs=True`: after one eager step, each curation setting
   (none / caring 0 / caring 1 ...) is captured ONCE as a hipGraph of the whole
   step - zero_grad, forward, loss, backward, fused norms+SGD - and replayed;
   the host then only copies the 8 group sums and runs the gate's decision.
@@ -29,6 +29,8 @@ re-organised for the hardware:
   replay is exactly an eager step; the host-side `step` attributes of the MMTM
   modules are advanced by the engine after each replay.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -37,6 +39,9 @@ from .gradsink import GradSink
 from .losses import blend_loss
 from .streams import all_side_streams, side_stream
 from .streams import enabled as streams_enabled
+
+
+_DEBUG_BUCKETS = os.environ.get("GM_DEBUG_BUCKETS", "0") == "1"
 
 
 class _Flags:
@@ -107,6 +112,8 @@ class GradBuckets:
             end = off + n
         if cur:
             self.buckets.append((start, end, cur))
+        self.deferred = False
+        self.names = {}
         self.bucket_of = {}
         for bi, (_, _, ps) in enumerate(self.buckets):
             for p in ps:
@@ -116,6 +123,9 @@ class GradBuckets:
 
     def reset(self):
         self._pending = [len(ps) for (_, _, ps) in self.buckets]
+        self._seen = set()
+        self._via_sink = set()
+        self._first = {}
         self._works = []
         g = self.flat.grad
         # the step's compute streams: main (current at step start) + the trunks' side
@@ -125,10 +135,34 @@ class GradBuckets:
             self._comm = torch.cuda.Stream(device=g.device)
 
     def _on_grad(self, p):
+        """post-accumulate-grad hook.  torch fires it even when the backward returned
+        None for the parameter, i.e. also right after a HIP kernel delivered that
+        gradient in place through the sink (_on_sink): those calls are not a second
+        gradient and are skipped."""
+        if self.deferred or id(p) in self._via_sink:
+            return
+        self._count(p)
+
+    def _on_sink(self, p):
+        """a HIP backward wrote p's gradient straight into the flat buffer (gradsink)."""
+        if self.deferred:  # a hipGraph capture: the step reduces after the replay
+            return
+        self._count(p)
+        self._via_sink.add(id(p))
+
+    def _count(self, p):
         bi = self.bucket_of[p]
+        if id(p) in self._seen:
+            first = self._first.get(id(p), "")
+            raise RuntimeError(f"gradient of parameter {self.names.get(id(p), tuple(p.shape))} delivered twice "
+                               f"in one step (used twice under data parallelism){first}")
+        self._seen.add(id(p))
+        if _DEBUG_BUCKETS:
+            import traceback
+            self._first[id(p)] = "\nfirst delivery:\n" + "".join(traceback.format_stack(limit=12))
         if self._pending[bi] == -1:
             raise RuntimeError("gradient delivered after its bucket was all-reduced "
-                               "(a parameter used twice in one step under data parallelism)")
+                               f"(a parameter used twice in one step under data parallelism: {tuple(p.shape)})")
         self._pending[bi] -= 1
         if self._pending[bi] == 0:
             self._launch(bi)
@@ -155,6 +189,13 @@ class GradBuckets:
         for w in self._works:
             w.wait()
         self._works = []
+
+    def reduce_all(self):
+        """All buckets at once, after a replayed hipGraph step produced every gradient
+        (collectives stay outside the graph: RCCL work is issued eagerly on the comm
+        stream behind the replay)."""
+        self.reset()
+        self.finish()
 
 
 class BalancedStep:
@@ -189,10 +230,11 @@ class BalancedStep:
                 if hasattr(m, "zero_grads_for_curated"):
                     m.zero_grads_for_curated = True  # every bucket fills every step
             self.buckets = GradBuckets(self.flat, process_group, bucket_mb)
+            self.buckets.names = {id(p): n for n, p in named}
         # HIP conv/BN backward kernels write their parameter gradients straight into
         # the flat buffer (no AccumulateGrad add) and fire the bucket hook themselves
         self.sink = GradSink(self.flat.slices.keys(),
-                             on_ready=self.buckets._on_grad if self.buckets is not None else None)
+                             on_ready=self.buckets._on_sink if self.buckets is not None else None)
         self.last_loss = None
         self.step_count = 0
         self.timer = None  # optional (start_event, end_event) list collector for the fused pass
@@ -200,7 +242,10 @@ class BalancedStep:
         if self.device.type == "cuda" and channels_last and compute_dtype == torch.bfloat16:
             from .conv import WeightPrep
             self.wprep = WeightPrep(model)
-        self.graphs = bool(graphs) and self.world == 1 and self.device.type == "cuda"
+        # graphs under data parallelism: the per-rank compute (zero_grad, forward, loss,
+        # backward) is ONE hipGraph; the gradient all-reduce and the fused norms+SGD pass
+        # run eagerly behind each replay (no collective inside a graph)
+        self.graphs = bool(graphs) and self.device.type == "cuda"
         self._graphs = {}
         self._gpool = None
         self._static = None
@@ -239,7 +284,7 @@ class BalancedStep:
             self.sink.end_step()
             if wp is not None:
                 wp.deactivate()
-        if self.buckets is not None:
+        if self.buckets is not None and not self.buckets.deferred:
             self.buckets.finish()
         return loss
 
@@ -254,9 +299,16 @@ class BalancedStep:
         if self._gpool is None:
             self._gpool = torch.cuda.graph_pool_handle()
         torch.cuda.synchronize(self.device)
-        with torch.cuda.graph(g, pool=self._gpool):
-            loss = self._fwd_bwd(*self._static).detach()
-            sums = self.norms.sums(grad_scale=1.0 / self.world, lr=self.lr)
+        dp = self.buckets is not None
+        if dp:
+            self.buckets.deferred = True
+        try:
+            with torch.cuda.graph(g, pool=self._gpool):
+                loss = self._fwd_bwd(*self._static).detach()
+                sums = None if dp else self.norms.sums(grad_scale=1.0 / self.world, lr=self.lr)
+        finally:
+            if dp:
+                self.buckets.deferred = False
         for m, st in steps:  # capture ran the Python forward but no kernel
             m.step = st
             m._step_mirror = st
@@ -282,6 +334,9 @@ class BalancedStep:
             g, loss, sums = self._graphs.get(key) or self._capture(key)
             want = gate is not None and hasattr(gate, "needs_bdr") and gate.needs_bdr()
             g.replay()
+            if self.buckets is not None:
+                self.buckets.reduce_all()
+                sums = self.norms.sums(grad_scale=1.0 / self.world, lr=self.lr)
             for m in self._mmtms:
                 m.step += 1
                 m._step_mirror = m.step

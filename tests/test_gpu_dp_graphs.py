@@ -1,0 +1,70 @@
+"""Data parallelism with hipGraph steps: per-rank compute captured as one graph,
+the gradient all-reduce and the fused norms+SGD pass issued eagerly behind each
+replay.  Two ranks share cuda:0 over gloo (the collective path is the same code
+that runs RCCL on a multi-GPU node); graph steps must equal eager DP steps."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, graphs, out_dir):
+    import torch.distributed as dist
+    from greedy_multimodal_learning_amd.callbacks import Bias_Mitigation_Strong
+    from greedy_multimodal_learning_amd.engine import BalancedStep
+    from greedy_multimodal_learning_amd.model import MMTM_MVCNN
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    m = MMTM_MVCNN().to(dev)
+    gate = Bias_Mitigation_Strong(epsilon=2e-3, curation_windowsize=2, branchnames=["net_view_0", "net_view_1"],
+                                  starting_epoch=1)
+    st = BalancedStep(m, lr=0.05, gate=gate, process_group=dist.group.WORLD, bucket_mb=8.0, graphs=graphs)
+    st.on_epoch_begin(1)
+    g = torch.Generator(device=dev).manual_seed(100 + rank)
+    xs = [torch.randn(2, 2, 3, 64, 64, device=dev, generator=g) for _ in range(3)]
+    ys = [torch.randint(0, 40, (2,), device=dev, generator=g) for _ in range(3)]
+    trace = []
+    for i in range(6):
+        loss = st(xs[i % 3], ys[i % 3])
+        trace.append((float(loss), float(gate.d_BDR), bool(st.flags.curation_mode), st.flags.caring_modality))
+    torch.cuda.synchronize()
+    sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    torch.save({"trace": trace, "sd": sd, "graphs": bool(st.graphs), "ngraphs": len(st._graphs)},
+               os.path.join(out_dir, f"g{int(graphs)}_r{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_graph_steps_equal_eager_dp_steps(tmp_path):
+    world = 2
+    for graphs in (False, True):
+        mp.start_processes(_worker, args=(world, _free_port(), graphs, str(tmp_path)), nprocs=world, join=True,
+                           start_method="spawn")
+    for r in range(world):
+        e = torch.load(tmp_path / f"g0_r{r}.pt", weights_only=True)
+        g = torch.load(tmp_path / f"g1_r{r}.pt", weights_only=True)
+        assert g["graphs"] and g["ngraphs"] >= 1 and not e["graphs"] is None
+        for a, b in zip(e["trace"], g["trace"]):
+            assert a[2:] == b[2:]
+            assert a[0] == pytest.approx(b[0], rel=1e-6, abs=1e-6)
+            assert a[1] == pytest.approx(b[1], rel=1e-6, abs=1e-9)
+        for k in e["sd"]:
+            torch.testing.assert_close(g["sd"][k], e["sd"][k], rtol=1e-6, atol=1e-6, msg=k)
+    # both ranks hold identical parameters (the all-reduced SGD update)
+    g0 = torch.load(tmp_path / "g1_r0.pt", weights_only=True)["sd"]
+    g1 = torch.load(tmp_path / "g1_r1.pt", weights_only=True)["sd"]
+    for k in g0:
+        if "running" in k or "num_batches" in k:
+            continue  # BN statistics are per rank (no SyncBN, as the reference)
+        assert torch.equal(g0[k], g1[k]), k
