@@ -171,9 +171,11 @@ def main():
     a = parse()
     dist_on = "RANK" in os.environ and int(os.environ.get("WORLD_SIZE", "1")) > 1
     if dist_on:
-        dist.init_process_group("nccl")
+        # rehearsal knobs (not used by the driver): gloo, and every rank on cuda:0, run the
+        # N-rank code path on a one-GPU box
+        dist.init_process_group(os.environ.get("GM_BENCH_DIST_BACKEND", "nccl"))
         rank, world = dist.get_rank(), dist.get_world_size()
-        local = int(os.environ.get("LOCAL_RANK", "0"))
+        local = 0 if os.environ.get("GM_BENCH_SAME_DEVICE") == "1" else int(os.environ.get("LOCAL_RANK", "0"))
     else:
         rank, world, local = 0, 1, 0
     torch.cuda.set_device(local)
