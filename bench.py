@@ -212,14 +212,18 @@ def main():
         step(xs[i % 2], ys[i % 2])
     torch.cuda.synchronize()
     curation_steps = 0
+    n_cur0 = step.sync_gate()["n_curated"] if step.device_gate else 0
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(a.steps):
-        curation_steps += int(step.flags.curation_mode)
+        if not step.device_gate:  # host gate: the flags are current after every step
+            curation_steps += int(step.flags.curation_mode)
         step(xs[i % 2], ys[i % 2])
     torch.cuda.synchronize()
+    if step.device_gate:  # on-device gate: no per-step sync; read its counter once
+        curation_steps = step.sync_gate()["n_curated"] - n_cur0
     if dist_on:
         dist.barrier()
     t1 = time.perf_counter()
@@ -260,7 +264,7 @@ def main():
                                    "(training_guided.gin eps 0.01, window 5, unlocked)",
                        "global_batch": B * world, "per_gpu_batch": B, "image": a.size,
                        "parallelism": f"dp{world}", "samples_per_s": round(world * B * a.steps / elapsed, 2),
-                       "hipgraph": bool(step.graphs),
+                       "hipgraph": bool(step.graphs), "device_gate": bool(step.device_gate),
                        "curation_steps_timed": curation_steps, "final_loss": round(loss, 4)},
             "roofline": {"kernel": "k_conv_igemm_ut / k_conv_igemm (bf16 implicit-GEMM conv, fwd + dgrad, "
                                    "all trunk shapes of one view at the step's batch)",

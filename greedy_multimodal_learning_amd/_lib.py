@@ -152,6 +152,20 @@ class WPrep(ctypes.Structure):
                 ("C", c_int), ("Cp", c_int), ("tile_start", c_int), ("pad", c_int)]
 
 
+class GateState(ctypes.Structure):
+    _fields_ = [("curation_mode", c_int), ("caring", c_int), ("curation_step", c_int), ("unlock", c_int),
+                ("window", c_int), ("n_curated", c_int), ("pad0", c_int), ("pad1", c_int),
+                ("eps", ctypes.c_double), ("M", ctypes.c_double * 4), ("d_bdr", ctypes.c_double)]
+
+
+EXPORTS.update({
+    "gm_gate_strong_step": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "gm_mmtm_select_scale": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
+                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "gm_mmtm_mask_rows": (c_int, [c_void_p, ctypes.c_longlong, c_void_p, c_void_p]),
+})
+
+
 class BnFwd(ctypes.Structure):
     _fields_ = [("M", ctypes.c_longlong), ("C", c_int), ("relu", c_int), ("x", c_void_p),
                 ("residual", c_void_p), ("y", c_void_p), ("gamma", c_void_p), ("beta", c_void_p),

@@ -115,7 +115,19 @@ class _MMTMFunction(torch.autograd.Function):
         cur, caring = cfg["curation"], cfg["caring"]
         sv, ld_sv, live_v = e_v, Cv, True
         ss, ld_ss, live_s = e_s, Cs, True
-        if cur and caring == 0:
+        gmask = None
+        gate = cfg.get("gate")
+        if gate is not None:
+            # on-device gate (engine): the flags live in device memory, so one captured
+            # step serves every curation setting; the substituted modality's excitation
+            # gradient is masked to zero in backward instead of skipped
+            sv, ss = torch.empty(B, Cv, **f32), torch.empty(B, Cs, **f32)
+            gmask = torch.empty(2, **f32)
+            L.check(L.load().gm_mmtm_select_scale(e_v.data_ptr(), Cv, e_s.data_ptr(), Cs, ra_v.data_ptr(),
+                                                  ra_s.data_ptr(), B, Cv, Cs, gate.data_ptr(), sv.data_ptr(),
+                                                  ss.data_ptr(), gmask.data_ptr(), L.stream_of(dev)),
+                    "gm_mmtm_select_scale")
+        elif cur and caring == 0:
             sv, ld_sv, live_v = ra_v, 0, False
         elif cur and caring == 1:
             ss, ld_ss, live_s = ra_s, 0, False
@@ -125,7 +137,7 @@ class _MMTMFunction(torch.autograd.Function):
         ctx.save_for_backward(xv, xs, sq, z_v, z_s, e_v, e_s, sv, ss,
                               w_sq, w_sq_v, w_sq_s, wv_, ws_)
         ctx.meta = (B, Cv, Cs, Cz, HWv, HWs, lay, dt, mode, share, live_v, live_s,
-                    ld_sv, ld_ss, cfg.get("avg_v"), cfg.get("avg_s"), cfg["zero_curated"])
+                    ld_sv, ld_ss, cfg.get("avg_v"), cfg.get("avg_s"), cfg["zero_curated"], gmask)
         ctx.mark_non_differentiable(e_v, e_s, sq)
         ctx.set_materialize_grads(False)  # no zero-filled grads for the side outputs
         return yv, ys, e_v, e_s, sq
@@ -134,7 +146,7 @@ class _MMTMFunction(torch.autograd.Function):
     def backward(ctx, gyv, gys, _ge_v, _ge_s, _gsq):
         (xv, xs, sq, z_v, z_s, e_v, e_s, sv, ss, w_sq, w_sq_v, w_sq_s, wv_, ws_) = ctx.saved_tensors
         (B, Cv, Cs, Cz, HWv, HWs, lay, dt, mode, share, live_v, live_s,
-         ld_sv, ld_ss, avg_v, avg_s, zero_curated) = ctx.meta
+         ld_sv, ld_ss, avg_v, avg_s, zero_curated, gmask) = ctx.meta
         dev = xv.device
         f32 = dict(device=dev, dtype=torch.float32)
         C2 = Cv + Cs
@@ -154,6 +166,12 @@ class _MMTMFunction(torch.autograd.Function):
             probs.append(dict(x=xs, dy=gys, C=Cs, HW=HWs, out=da_s, ld_out=Cs, e=e_s, ld_e=Cs))
         if probs:
             ops.spatial_reduce(probs, B, dt, lay, dev)
+        if gmask is not None:  # on-device gate: zero the substituted modality's da
+            lib = L.load()
+            L.check(lib.gm_mmtm_mask_rows(da_v.data_ptr(), B * Cv, gmask.data_ptr(), L.stream_of(dev)),
+                    "gm_mmtm_mask_rows")
+            L.check(lib.gm_mmtm_mask_rows(da_s.data_ptr(), B * Cs, gmask.data_ptr() + 4, L.stream_of(dev)),
+                    "gm_mmtm_mask_rows")
         # ---- excite FC grads + dz
         g = {}
         probs = []
@@ -293,6 +311,20 @@ class MMTM_mitigate(nn.Module):
         # when set, a curated branch receives zeros instead of None (identical SGD
         # update with momentum = weight_decay = 0, the reference's configs)
         self.zero_grads_for_curated = False
+        # set by the engine's on-device gate: a device gm_gate_state whose flags replace
+        # the curation_mode / caring_modality arguments
+        self.device_gate = None
+        # True: host flags drive the same select/mask kernels as the device gate (the
+        # test that pins the device gate against the host gate bit for bit)
+        self.mask_curation = False
+
+    def _gate_for(self, curation_mode, caring_modality, dev):
+        if self.device_gate is not None or not self.mask_curation:
+            return self.device_gate
+        st = L.GateState()
+        st.curation_mode = int(bool(curation_mode))
+        st.caring = -1 if caring_modality is None else int(caring_modality)
+        return torch.frombuffer(bytearray(bytes(st)), dtype=torch.uint8).to(dev)
 
     def _lin(self, name):
         m = getattr(self, name, None)
@@ -329,7 +361,8 @@ class MMTM_mitigate(nn.Module):
                    ra_v=self.running_avg_weight_visual,
                    ra_s=self.running_avg_weight_skeleton,
                    curation=bool(curation_mode), caring=caring_modality,
-                   zero_curated=self.zero_grads_for_curated)
+                   zero_curated=self.zero_grads_for_curated,
+                   gate=self._gate_for(curation_mode, caring_modality, dev) if mode == NORMAL else None)
         if mode == TURNOFF:
             cfg["avg_v"] = _as_f32(average_squeezemaps[0], dev)
             cfg["avg_s"] = _as_f32(average_squeezemaps[1], dev)

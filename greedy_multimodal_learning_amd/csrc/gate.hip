@@ -1,0 +1,119 @@
+// On-device conditional-learning-speed gate: the curation decision of
+// Bias_Mitigation_Strong.on_backward_end (reference src/callbacks.py:199-267) made by a
+// one-thread kernel right after the fused norms+SGD pass, and the MMTM curation
+// substitution (src/balanced_mmtm.py:135-152) driven by the resulting device flags, so a
+// training step needs no host synchronisation: one hipGraph serves every curation
+// setting and steps are enqueued back to back.
+//
+// State (gm_gate_state, device memory, owned by the caller):
+//   curation_mode, caring (-1 = None), curation_step, unlock, window, n_curated (steps
+//   that ran curated, a statistic), eps, M = {bypass0, bypass1, main0, main1}, d_bdr.
+// Step rule, exactly the reference's (fp64, C log10 = numpy's IEEE behaviour):
+//   unlocked & not curating: M += g/w ratios; d = log10(Mb0/Mm0) - log10(Mb1/Mm1);
+//                            |d| > eps -> curate, caring = d < 0 ? 1 : 0; else caring 0
+//   unlocked & curating:     curation_step += 1; stop at the window
+//   locked:                  d as above, no curation, caring 0
+#include "gm_common.h"
+
+namespace gm {
+namespace {
+
+__global__ void k_gate_strong(const double* __restrict__ s, gm_gate_state* st) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    gm_gate_state g = *st;
+    if (g.curation_mode) ++g.n_curated;  // the step that just ran was curated
+    auto bdr = [&]() {
+        // s = [w_main0, g_main0, w_main1, g_main1, w_by0, g_by0, w_by1, g_by1]
+        g.M[2] += s[1] / s[0];
+        g.M[3] += s[3] / s[2];
+        g.M[0] += s[5] / s[4];
+        g.M[1] += s[7] / s[6];
+        g.d_bdr = log10(g.M[0] / g.M[2]) - log10(g.M[1] / g.M[3]);
+    };
+    if (g.unlock) {
+        if (!g.curation_mode) {
+            bdr();
+            if (fabs(g.d_bdr) > g.eps) {
+                g.curation_mode = 1;
+                g.curation_step = 0;
+                g.caring = g.d_bdr < 0.0 ? 1 : 0;
+            } else {
+                g.curation_mode = 0;
+                g.caring = 0;
+            }
+        } else {
+            g.curation_step += 1;
+            if (g.curation_step == g.window) g.curation_mode = 0;
+        }
+    } else {
+        bdr();
+        g.curation_mode = 0;
+        g.caring = 0;
+    }
+    *st = g;
+}
+
+// effective MMTM scales under the device flags: the cared-for modality's scale is the
+// (already updated) running average broadcast over the batch, the other stays live;
+// mask[m] = 0 for the substituted modality (its excitation path gets no gradient)
+__global__ __launch_bounds__(256) void k_select_scale(const float* __restrict__ e_v, int ld_v,
+                                                      const float* __restrict__ e_s, int ld_s,
+                                                      const float* __restrict__ ra_v,
+                                                      const float* __restrict__ ra_s, int B, int Cv, int Cs,
+                                                      const gm_gate_state* __restrict__ st, float* __restrict__ s_v,
+                                                      float* __restrict__ s_s, float* __restrict__ mask) {
+    const int cur = st->curation_mode, car = st->caring;
+    const bool sub_v = cur && car == 0, sub_s = cur && car == 1;
+    const long long nv = (long long)B * Cv, ns = (long long)B * Cs;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nv + ns; i += (long long)gridDim.x * 256) {
+        if (i < nv) {
+            const int b = (int)(i / Cv), c = (int)(i - (long long)b * Cv);
+            s_v[i] = sub_v ? ra_v[c] : e_v[(size_t)b * ld_v + c];
+        } else {
+            const long long j = i - nv;
+            const int b = (int)(j / Cs), c = (int)(j - (long long)b * Cs);
+            s_s[j] = sub_s ? ra_s[c] : e_s[(size_t)b * ld_s + c];
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        mask[0] = sub_v ? 0.f : 1.f;
+        mask[1] = sub_s ? 0.f : 1.f;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_mask_rows(float* __restrict__ a, long long n, const float* __restrict__ m) {
+    const float k = *m;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) a[i] *= k;
+}
+
+}  // namespace
+}  // namespace gm
+
+using namespace gm;
+
+extern "C" int gm_gate_strong_step(const double* sums, gm_gate_state* state, void* stream) {
+    GM_REQUIRE(sums && state, "gm_gate_strong_step: null pointer");
+    k_gate_strong<<<1, 64, 0, as_stream(stream)>>>(sums, state);
+    return check_launch("k_gate_strong");
+}
+
+extern "C" int gm_mmtm_select_scale(const float* e_v, int ld_v, const float* e_s, int ld_s, const float* ra_v,
+                                    const float* ra_s, int B, int Cv, int Cs, const gm_gate_state* state,
+                                    float* s_v, float* s_s, float* mask, void* stream) {
+    GM_REQUIRE(e_v && e_s && ra_v && ra_s && state && s_v && s_s && mask && B > 0 && Cv > 0 && Cs > 0,
+               "gm_mmtm_select_scale: bad arguments");
+    const long long n = (long long)B * (Cv + Cs);
+    int g = (int)((n + 255) / 256);
+    g = g > 1024 ? 1024 : g;
+    k_select_scale<<<g, 256, 0, as_stream(stream)>>>(e_v, ld_v, e_s, ld_s, ra_v, ra_s, B, Cv, Cs, state, s_v, s_s,
+                                                     mask);
+    return check_launch("k_select_scale");
+}
+
+extern "C" int gm_mmtm_mask_rows(float* a, long long n, const float* mask, void* stream) {
+    GM_REQUIRE(a && mask && n > 0, "gm_mmtm_mask_rows: bad arguments");
+    int g = (int)((n + 255) / 256);
+    g = g > 1024 ? 1024 : g;
+    k_mask_rows<<<g, 256, 0, as_stream(stream)>>>(a, n, mask);
+    return check_launch("k_mask_rows");
+}

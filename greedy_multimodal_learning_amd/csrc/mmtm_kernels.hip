@@ -400,7 +400,10 @@ static int red_setup(const gm_spatial_reduce* in, int nprob, int B, int dtype, i
             GM_REQUIRE(aligned(s.x, 16) && (!s.dy || aligned(s.dy, 16)),
                        "spatial_reduce[%d]: NHWC tensors must be 16-byte aligned", i);
             const int tpp = s.C * es / 16, ppi = 256 / tpp;
-            int S = (red_wgs() + nprob * B - 1) / (nprob * B);
+            // per-problem split independent of how many problems share the launch, so a
+            // modality's reduction order (and bits) never depends on its batch-mates
+            const int per = red_wgs() / 2;
+            int S = (per + B - 1) / B;
             const int maxS = (s.HW + 2 * ppi - 1) / (2 * ppi);
             S = S < 1 ? 1 : (S > maxS ? maxS : S);
             if (S < 1) S = 1;

@@ -201,7 +201,7 @@ class GradBuckets:
 class BalancedStep:
     def __init__(self, model, lr=0.1, gate=None, compute_dtype=torch.bfloat16, channels_last=True,
                  process_group=None, bucket_mb=25.0, branchnames=("net_view_0", "net_view_1"),
-                 MMTMnames=("visual", "skeleton"), graphs=False):
+                 MMTMnames=("visual", "skeleton"), graphs=False, device_gate=None):
         self.model = model
         self.lr = float(lr)
         self.gate = gate
@@ -252,6 +252,53 @@ class BalancedStep:
         from .balanced_mmtm import MMTM_mitigate
         from .mmtm_n import MMTM_N
         self._mmtms = [m for m in model.modules() if isinstance(m, (MMTM_mitigate, MMTM_N))]
+        # on-device gate: the Strong gate's decision made by a kernel behind
+        # the norms+SGD pass and consumed by the MMTM kernels from device memory, so no
+        # host sync per step and one graph for every curation setting
+        from .callbacks import Bias_Mitigation_Strong
+        eligible = (self.device.type == "cuda" and isinstance(gate, Bias_Mitigation_Strong)
+                    and len(gate.branchnames) == 2 and self._mmtms
+                    and all(isinstance(m, MMTM_mitigate) and not m.SEonly for m in self._mmtms))
+        if device_gate is None:
+            import os as _os
+            device_gate = _os.environ.get("GM_DEVICE_GATE", "1") != "0"
+        self.device_gate = bool(device_gate) and eligible
+        self.gate_state = None
+        if self.device_gate:
+            from . import _lib as L
+            st = L.GateState()
+            st.caring = -1
+            st.window = int(gate.curation_windowsize)
+            st.eps = float(gate.epsilon)
+            st.unlock = int(bool(getattr(gate, "unlock", False)))
+            self.gate_state = torch.frombuffer(bytearray(bytes(st)), dtype=torch.uint8).to(self.device)
+            for m in self._mmtms:
+                m.device_gate = self.gate_state
+
+    # ---------------- on-device gate ----------------
+    def _gate_step(self, sums):
+        from . import _lib as L
+        L.check(L.load().gm_gate_strong_step(sums.data_ptr(), self.gate_state.data_ptr(),
+                                             L.stream_of(self.device)), "gm_gate_strong_step")
+
+    def sync_gate(self):
+        """Copy the device gate state to the host mirrors (gate.d_BDR, its M
+        accumulators, curation_step, the flags object); returns it as a dict.  The
+        only host sync of the on-device gate, taken when someone asks."""
+        if not self.device_gate:
+            return None
+        from . import _lib as L
+        raw = self.gate_state.cpu().numpy().tobytes()
+        st = L.GateState.from_buffer_copy(raw)
+        g, fl = self.gate, self.flags
+        g.d_BDR = float(st.d_bdr)
+        g.M_bypass_modal_0, g.M_bypass_modal_1 = float(st.M[0]), float(st.M[1])
+        g.M_main_modal_0, g.M_main_modal_1 = float(st.M[2]), float(st.M[3])
+        g.curation_step = int(st.curation_step)
+        fl.curation_mode = bool(st.curation_mode)
+        fl.caring_modality = None if st.caring < 0 else int(st.caring)
+        return {"curation_mode": fl.curation_mode, "caring_modality": fl.caring_modality, "d_BDR": g.d_BDR,
+                "curation_step": g.curation_step, "n_curated": int(st.n_curated)}
 
     # ---------------- the step ----------------
     def forward(self, x):
@@ -289,6 +336,8 @@ class BalancedStep:
         return loss
 
     def _graph_key(self):
+        if self.device_gate:
+            return ("device-gate", self.lr)
         fl = self.flags
         return (bool(fl.curation_mode), fl.caring_modality if fl.curation_mode else None, self.lr)
 
@@ -309,6 +358,8 @@ class BalancedStep:
             with torch.cuda.graph(g, pool=self._gpool, capture_error_mode=mode):
                 loss = self._fwd_bwd(*self._static).detach()
                 sums = None if dp else self.norms.sums(grad_scale=1.0 / self.world, lr=self.lr)
+                if sums is not None and self.device_gate:
+                    self._gate_step(sums)
         finally:
             if dp:
                 self.buckets.deferred = False
@@ -349,6 +400,8 @@ class BalancedStep:
             if self.buckets is not None:
                 self.buckets.reduce_all()
                 sums = self.norms.sums(grad_scale=1.0 / self.world, lr=self.lr)
+                if self.device_gate:
+                    self._gate_step(sums)
             for m in self._mmtms:
                 m.step += 1
                 m._step_mirror = m.step
@@ -363,6 +416,8 @@ class BalancedStep:
             ev1 = torch.cuda.Event(enable_timing=True)
             ev0.record()
         sums = self.norms.sums(grad_scale=1.0 / self.world, lr=self.lr)
+        if self.device_gate:
+            self._gate_step(sums)
         if t is not None:
             ev1.record()
             t.append((ev0, ev1))
@@ -370,7 +425,7 @@ class BalancedStep:
 
     def _after(self, loss, sums, want):
         gate = self.gate
-        if gate is not None:
+        if gate is not None and not self.device_gate:
             if want:
                 gate.pending_sums = sums
             gate.on_backward_end(self.step_count)
@@ -382,3 +437,6 @@ class BalancedStep:
     def on_epoch_begin(self, epoch):
         if self.gate is not None:
             self.gate.on_epoch_begin(epoch, {})
+            if self.device_gate:  # push the unlock flag (int at byte offset 12)
+                flag = torch.tensor([int(bool(getattr(self.gate, "unlock", False)))], dtype=torch.int32)
+                self.gate_state[12:16].copy_(flag.view(torch.uint8))

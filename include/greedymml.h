@@ -159,6 +159,27 @@ typedef struct gm_tensor {
 } gm_tensor;
 
 size_t gm_group_sumsq_scratch(long long total_elems);
+/* ---------------------------------------------------------------------------
+ * On-device gate (Bias_Mitigation_Strong, reference src/callbacks.py:199-267) and the
+ * MMTM curation substitution it drives (src/balanced_mmtm.py:135-152): no host sync
+ * per training step.  gm_gate_state lives in device memory (caller-owned, 80 B).
+ * ------------------------------------------------------------------------- */
+typedef struct gm_gate_state {
+    int curation_mode, caring, curation_step, unlock;   /* caring: -1 = None */
+    int window, n_curated, pad0, pad1;
+    double eps;
+    double M[4];                                          /* bypass0, bypass1, main0, main1 */
+    double d_bdr;
+} gm_gate_state;
+/* sums: device fp64 [8] from gm_group_sumsq (main0, main1, bypass0, bypass1: w, g) */
+int gm_gate_strong_step(const double* sums, gm_gate_state* state, void* stream);
+/* s_m = running average (broadcast over B) for the cared-for modality when curating,
+ * else e_m; mask[2] = {0 or 1} per modality (0: substituted, no excitation gradient) */
+int gm_mmtm_select_scale(const float* e_v, int ld_v, const float* e_s, int ld_s, const float* ra_v,
+                         const float* ra_s, int B, int Cv, int Cs, const gm_gate_state* state,
+                         float* s_v, float* s_s, float* mask, void* stream);
+int gm_mmtm_mask_rows(float* a, long long n, const float* mask, void* stream);
+
 int gm_group_sumsq(const gm_tensor* table, int ntensors, long long total_elems, int ngroups,
                    float grad_scale, float lr, double* out, void* scratch, size_t scratch_bytes,
                    void* stream);

@@ -37,6 +37,8 @@ def _worker(rank, world, port, graphs, out_dir):
     trace = []
     for i in range(6):
         loss = st(xs[i % 3], ys[i % 3])
+        if st.device_gate:
+            st.sync_gate()
         trace.append((float(loss), float(gate.d_BDR), bool(st.flags.curation_mode), st.flags.caring_modality))
     torch.cuda.synchronize()
     sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}

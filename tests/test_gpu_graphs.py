@@ -16,7 +16,7 @@ def _run(graphs, steps, dev):
     m = MMTM_MVCNN().to(dev)
     gate = Bias_Mitigation_Strong(epsilon=2e-3, curation_windowsize=2, branchnames=["net_view_0", "net_view_1"],
                                   starting_epoch=1)
-    st = BalancedStep(m, lr=0.05, gate=gate, graphs=graphs)
+    st = BalancedStep(m, lr=0.05, gate=gate, graphs=graphs, device_gate=False)
     st.on_epoch_begin(1)
     g = torch.Generator(device=dev).manual_seed(5)
     xs = [torch.randn(4, 2, 3, 64, 64, device=dev, generator=g) for _ in range(3)]
@@ -62,3 +62,57 @@ def test_view_streams_equal_single_stream(monkeypatch):
     s1, s2 = m_1.state_dict(), m_2.state_dict()
     for k in s1:
         assert torch.equal(s1[k], s2[k]), k
+
+
+def _run_gate(device_gate, graphs, steps, dev):
+    from greedy_multimodal_learning_amd.callbacks import Bias_Mitigation_Strong
+    from greedy_multimodal_learning_amd.engine import BalancedStep
+    from greedy_multimodal_learning_amd.model import MMTM_MVCNN
+    torch.manual_seed(0)
+    m = MMTM_MVCNN().to(dev)
+    gate = Bias_Mitigation_Strong(epsilon=2e-3, curation_windowsize=2, branchnames=["net_view_0", "net_view_1"],
+                                  starting_epoch=1)
+    # The host-gate run routes its flags through the device gate's select/mask kernels
+    # (mask_curation): the host gate's own curated backward skips the substituted
+    # modality's excitation GEMMs, a different fp32 summation order whose 1e-8
+    # differences flip bf16 activation roundings and decorrelate two runs in a few steps.
+    st = BalancedStep(m, lr=0.05, gate=gate, graphs=graphs, device_gate=device_gate)
+    assert st.device_gate == device_gate
+    if not device_gate:  # host flags through the same select/mask kernels: bitwise comparable
+        for i in (2, 3, 4):
+            getattr(m, f"mmtm{i}").mask_curation = True
+    st.on_epoch_begin(1)
+    g = torch.Generator(device=dev).manual_seed(5)
+    xs = [torch.randn(4, 2, 3, 64, 64, device=dev, generator=g) for _ in range(3)]
+    ys = [torch.randint(0, 40, (4,), device=dev, generator=g) for _ in range(3)]
+    trace = []
+    for i in range(steps):
+        loss = st(xs[i % 3], ys[i % 3])
+        if device_gate:
+            st.sync_gate()
+        trace.append((float(loss), gate.d_BDR, st.flags.curation_mode, st.flags.caring_modality))
+    return m, st, trace
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_device_gate_equals_host_gate(graphs):
+    """The on-device gate (decision kernel behind the norms+SGD pass, MMTM curation from
+    device flags, one graph for every setting) reproduces the host gate step by step:
+    decisions, d_BDR, losses, parameters and MMTM running averages."""
+    dev = torch.device("cuda:0")
+    m_h, st_h, tr_h = _run_gate(False, False, 10, dev)
+    m_d, st_d, tr_d = _run_gate(True, graphs, 10, dev)
+    assert {t[2] for t in tr_h} == {True, False}, "the trace should contain curation steps"
+    if graphs:
+        assert len(st_d._graphs) == 1
+    diffs = [(a[0] - b[0], a[1] - b[1], a[2], b[2]) for a, b in zip(tr_h, tr_d)]
+    for a, b in zip(tr_h, tr_d):
+        assert a[2:] == b[2:], diffs
+        assert a[0] == pytest.approx(b[0], rel=1e-6, abs=1e-6), diffs
+        assert a[1] == pytest.approx(b[1], rel=1e-6, abs=1e-9), diffs
+    sh, sd = m_h.state_dict(), m_d.state_dict()
+    for k in sh:
+        torch.testing.assert_close(sd[k], sh[k], rtol=1e-6, atol=1e-6, msg=k)
+    for i in (2, 3, 4):
+        a, b = getattr(m_h, f"mmtm{i}"), getattr(m_d, f"mmtm{i}")
+        torch.testing.assert_close(b.running_avg_weight_visual, a.running_avg_weight_visual, rtol=1e-6, atol=1e-7)
