@@ -27,7 +27,12 @@ import torch.nn as nn
 
 from . import _lib as L
 from . import ops
+from .gradsink import sink_done, sink_target
 from .ops import ONES, Op
+
+# position of each parameter among _MMTMFunction.forward's inputs (ctx.needs_input_grad)
+_GRAD_INDEX = {"w_sq": 2, "b_sq": 3, "w_sq_v": 4, "b_sq_v": 5, "w_sq_s": 6, "b_sq_s": 7,
+               "w_v": 8, "b_v": 9, "w_s": 10, "b_s": 11}
 
 NORMAL, TURNOFF, SEONLY = 0, 1, 2
 
@@ -136,6 +141,9 @@ class _MMTMFunction(torch.autograd.Function):
                            dict(x=xs, y=ys, C=Cs, HW=HWs, s=ss, ld_s=ld_ss)], B, dt, lay, dev)
         ctx.save_for_backward(xv, xs, sq, z_v, z_s, e_v, e_s, sv, ss,
                               w_sq, w_sq_v, w_sq_s, wv_, ws_)
+        # the parameters themselves (leaves), for in-place gradient delivery (gradsink)
+        ctx.params = {"w_sq": w_sq, "b_sq": b_sq, "w_sq_v": w_sq_v, "b_sq_v": b_sq_v, "w_sq_s": w_sq_s,
+                      "b_sq_s": b_sq_s, "w_v": w_v, "b_v": b_v, "w_s": w_s, "b_s": b_s}
         ctx.meta = (B, Cv, Cs, Cz, HWv, HWs, lay, dt, mode, share, live_v, live_s,
                     ld_sv, ld_ss, cfg.get("avg_v"), cfg.get("avg_s"), cfg["zero_curated"], gmask)
         ctx.mark_non_differentiable(e_v, e_s, sq)
@@ -150,6 +158,27 @@ class _MMTMFunction(torch.autograd.Function):
         dev = xv.device
         f32 = dict(device=dev, dtype=torch.float32)
         C2 = Cv + Cs
+        # parameter gradients: written by the GEMMs straight into the engine's flat
+        # gradient buffer when the parameter is sink-managed (no AccumulateGrad add)
+        sunk, acc_of = {}, {}
+
+        def gbuf(key, *shape):
+            prm = ctx.params.get(key)
+            tgt = sink_target(prm) if prm is not None and ctx.needs_input_grad[_GRAD_INDEX[key]] else None
+            if tgt is not None:
+                t, acc = tgt
+                if t.is_contiguous() and tuple(t.shape) == shape:
+                    sunk[key] = prm
+                    acc_of[id(t)] = acc
+                    return t
+                raise RuntimeError(f"MMTM {key}: in-place gradient buffer must be a contiguous {shape}")
+            return torch.empty(*shape, **f32)
+
+        def gemm_acc(problems):
+            for q in problems:
+                if acc_of.get(id(q["C"])):
+                    q["accumulate"] = 1
+            ops.gemm(problems, dev)
         if gyv is None:
             gyv = torch.zeros_like(xv)
         if gys is None:
@@ -177,8 +206,8 @@ class _MMTMFunction(torch.autograd.Function):
         probs = []
         if share:
             if live_v or live_s:
-                g["w_v"] = torch.empty(Cv, Cz, **f32)
-                g["b_v"] = torch.empty(Cv, **f32)
+                g["w_v"] = gbuf("w_v", Cv, Cz)
+                g["b_v"] = gbuf("b_v", Cv)
                 segw = [(B, Op(da, 1, Cv), Op(z, Cz, 1)) for da, z in ((da_v, z_v), (da_s, z_s))
                         if da is not None]
                 segb = [(B, ONES, Op(da, Cv, 1)) for da in (da_v, da_s) if da is not None]
@@ -188,8 +217,8 @@ class _MMTMFunction(torch.autograd.Function):
             for key, da, z, C in (("v", da_v, z_v, Cv), ("s", da_s, z_s, Cs)):
                 if da is None:
                     continue
-                g["w_" + key] = torch.empty(C, Cz, **f32)
-                g["b_" + key] = torch.empty(C, **f32)
+                g["w_" + key] = gbuf("w_" + key, C, Cz)
+                g["b_" + key] = gbuf("b_" + key, C)
                 probs += [dict(M=C, N=Cz, segs=[(B, Op(da, 1, C), Op(z, Cz, 1))], C=g["w_" + key],
                                ld_c=Cz),
                           dict(M=1, N=C, segs=[(B, ONES, Op(da, C, 1))], C=g["b_" + key], ld_c=C)]
@@ -211,21 +240,21 @@ class _MMTMFunction(torch.autograd.Function):
                 probs.append(dict(M=B, N=Cz, segs=[(Cs, Op(da_s, Cs, 1), Op(ws_, Cz, 1))], C=dz_s,
                                   ld_c=Cz, mask=z_s, ld_mask=Cz))
         if probs:
-            ops.gemm(probs, dev)
+            gemm_acc(probs)
         # ---- squeeze FC grads + dsq
         probs = []
         dsq = None
         if mode == NORMAL and dz_v is not None:
             dsq = torch.empty(B, C2, **f32)
-            g["w_sq"] = torch.empty(Cz, C2, **f32)
-            g["b_sq"] = torch.empty(Cz, **f32)
+            g["w_sq"] = gbuf("w_sq", Cz, C2)
+            g["b_sq"] = gbuf("b_sq", Cz)
             probs += [dict(M=Cz, N=C2, segs=[(B, Op(dz_v, 1, Cz), Op(sq, C2, 1))], C=g["w_sq"], ld_c=C2),
                       dict(M=1, N=Cz, segs=[(B, ONES, Op(dz_v, Cz, 1))], C=g["b_sq"], ld_c=Cz),
                       dict(M=B, N=C2, segs=[(Cz, Op(dz_v, Cz, 1), Op(w_sq, C2, 1))], C=dsq, ld_c=C2)]
         elif mode == TURNOFF and (dz_v is not None or dz_s is not None):
             dsq = torch.zeros(B, C2, **f32) if (dz_v is None or dz_s is None) else torch.empty(B, C2, **f32)
-            g["w_sq"] = torch.empty(Cz, C2, **f32)
-            g["b_sq"] = torch.empty(Cz, **f32)
+            g["w_sq"] = gbuf("w_sq", Cz, C2)
+            g["b_sq"] = gbuf("b_sq", Cz)
             # fc_squeeze saw in_v = [sq_v | avg_s] and in_s = [avg_v | sq_s]
             left = [(B, Op(dz, 1, Cz), src) for dz, src in
                     ((dz_v, Op(sq, C2, 1)), (dz_s, Op(avg_v, 0, 1))) if dz is not None]
@@ -246,15 +275,15 @@ class _MMTMFunction(torch.autograd.Function):
             for key, dz, w, C, off in (("v", dz_v, w_sq_v, Cv, 0), ("s", dz_s, w_sq_s, Cs, Cv)):
                 if dz is None:
                     continue
-                g["w_sq_" + key] = torch.empty(Cz, C, **f32)
-                g["b_sq_" + key] = torch.empty(Cz, **f32)
+                g["w_sq_" + key] = gbuf("w_sq_" + key, Cz, C)
+                g["b_sq_" + key] = gbuf("b_sq_" + key, Cz)
                 probs += [dict(M=Cz, N=C, segs=[(B, Op(dz, 1, Cz), Op(sq, C2, 1, off=off))],
                                C=g["w_sq_" + key], ld_c=C),
                           dict(M=1, N=Cz, segs=[(B, ONES, Op(dz, Cz, 1))], C=g["b_sq_" + key], ld_c=Cz),
                           dict(M=B, N=C, segs=[(Cz, Op(dz, Cz, 1), Op(w, C, 1))], C=dsq, c_off=off,
                                ld_c=C2)]
         if probs:
-            ops.gemm(probs, dev)
+            gemm_acc(probs)
         # ---- dX_m = dY_m * s_m + dsq_m / HW
         dxv, dxs = torch.empty_like(xv), torch.empty_like(xs)
         pv = dict(x=gyv, y=dxv, C=Cv, HW=HWv, s=sv, ld_s=ld_sv)
@@ -264,7 +293,12 @@ class _MMTMFunction(torch.autograd.Function):
             ps.update(a=dsq, a_off=Cv, ld_a=C2, alpha=1.0 / HWs)
         ops.channel_scale([pv, ps], B, dt, lay, dev)
 
+        for prm in sunk.values():  # delivered in place: fire the engine's per-parameter hook
+            sink_done(prm)
+
         def out(key, shape_like):
+            if key in sunk:
+                return None
             t = g.get(key)
             if t is None and zero_curated and shape_like is not None:
                 return torch.zeros_like(shape_like)
