@@ -141,6 +141,8 @@ EXPORTS.update({
     "gm_conv2d_splitk_ws_bytes": (c_size_t, [c_void_p, c_int]),
     "gm_conv2d_fwd_ex_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "gm_conv2d_dgrad_ex_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "gm_conv2d_dgrad_add_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                         c_void_p]),
     "gm_conv2d_wgrad_hw_scratch": (c_size_t, [c_void_p]),
     "gm_conv2d_wgrad_hw_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
                                         c_size_t, c_void_p]),

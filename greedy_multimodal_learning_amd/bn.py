@@ -111,7 +111,8 @@ def bn_bwd(dy, y, x, weight, sm, si, relu, want_dres, dgamma, dbeta, accumulate)
 
 class _BNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, momentum, eps, relu):
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, momentum, eps, relu, join=None):
+        ctx.join = join
         xb = _nhwc(x.to(torch.bfloat16))
         y, sm, si = bn_fwd_train(xb, weight.detach(), bias.detach(), running_mean, running_var, nbt, momentum,
                                  eps, relu, residual)
@@ -146,7 +147,9 @@ class _BNFn(torch.autograd.Function):
             gw = dgamma if want_w else None
             gb = dbeta if want_b else None
         dx = dx if ctx.needs_input_grad[0] else None
-        return dx, gw, gb, dres, None, None, None, None, None, None
+        if dres is not None and ctx.join is not None:  # the residual's gradient joins the block input's
+            dres = ctx.join.contribute(lambda add: dres if add is None else dres + add)
+        return dx, gw, gb, dres, None, None, None, None, None, None, None
 
 
 def _use_hip(x):
@@ -160,13 +163,19 @@ def _use_hip(x):
 class GMBatchNorm2d(nn.BatchNorm2d):
     """nn.BatchNorm2d with optional fused residual add and ReLU (see module doc)."""
 
-    def forward(self, x, residual=None, relu=False):
+    def forward(self, x, residual=None, relu=False, residual_join=None):
+        """residual_join: gradsink.GradJoin of the residual tensor (see conv.GMConv2d)."""
         C = self.num_features
         hip = (_use_hip(x) and self.affine and x.dim() == 4 and C >= 8 and C <= 2048 and not (C & (C - 1)))
         if hip and self.training and self.track_running_stats and self.momentum is not None:
+            join = None
+            if (residual_join is not None and residual is not None and residual.requires_grad
+                    and torch.is_grad_enabled()):
+                residual_join.register()
+                join = residual_join
             with torch.autocast("cuda", enabled=False):
                 return _BNFn.apply(x, self.weight, self.bias, residual, self.running_mean, self.running_var,
-                                   self.num_batches_tracked, self.momentum, self.eps, bool(relu))
+                                   self.num_batches_tracked, self.momentum, self.eps, bool(relu), join)
         if (hip and not self.training and self.track_running_stats
                 and not (torch.is_grad_enabled() and (x.requires_grad or self.weight.requires_grad))):
             return bn_fwd_infer(x.to(torch.bfloat16), self.weight, self.bias, self.running_mean, self.running_var,

@@ -293,22 +293,28 @@ class WeightPrep:
         _prepped.clear()
 
 
-def conv_dgrad_t(dy, wt, H, W, stride, pad):
-    """dgrad from an already transposed bf16 weight wt [C,K,R,S] (channels_last)."""
+def conv_dgrad_t(dy, wt, H, W, stride, pad, addend=None):
+    """dgrad from an already transposed bf16 weight wt [C,K,R,S] (channels_last);
+    addend (bf16 [N,C,H,W] channels_last): dx = dgrad + addend in the epilogue."""
     lib = L.load()
     N, K, P, Q = dy.shape
     C, _, R, S = wt.shape
     dx = torch.empty(N, C, H, W, device=dy.device, dtype=torch.bfloat16, memory_format=CL)
     d = _desc(N, H, W, C, K, R, S, stride, pad)
     ws, nb = _splitk(dy.device, d, True)
-    L.check(lib.gm_conv2d_dgrad_ex_bf16(ctypes.byref(d), dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), ws, nb,
-                                        L.stream_of(dy.device)), "gm_conv2d_dgrad_ex_bf16")
+    if addend is not None:
+        if (tuple(addend.shape) != (N, C, H, W) or addend.dtype != torch.bfloat16
+                or not addend.is_contiguous(memory_format=CL)):
+            raise ValueError("conv dgrad addend must be a bf16 channels_last tensor shaped like dx")
+    L.check(lib.gm_conv2d_dgrad_add_bf16(ctypes.byref(d), dy.data_ptr(), wt.data_ptr(), dx.data_ptr(),
+                                         L.ptr(addend), ws, nb, L.stream_of(dy.device)), "gm_conv2d_dgrad_add_bf16")
     return dx
 
 
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, stride, pad):
+    def forward(ctx, x, weight, stride, pad, join=None):
+        ctx.join = join
         C0 = x.shape[1]
         Cp = _cpad(C0)
         xb = _nhwc(x.to(torch.bfloat16))
@@ -332,9 +338,12 @@ class _ConvFn(torch.autograd.Function):
         gy = _nhwc(gy.to(torch.bfloat16))
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = conv_dgrad_t(gy, wt, H, W, stride, pad)
-            if dx.shape[1] != C0:
-                dx = dx[:, :C0]
+            if ctx.join is not None and wt.shape[0] == C0:
+                dx = ctx.join.contribute(lambda add: conv_dgrad_t(gy, wt, H, W, stride, pad, addend=add))
+            else:
+                dx = conv_dgrad_t(gy, wt, H, W, stride, pad)
+                if dx.shape[1] != C0:
+                    dx = dx[:, :C0]
         dw = None
         if ctx.needs_input_grad[1]:
             tgt = sink_target(weight)
@@ -345,7 +354,7 @@ class _ConvFn(torch.autograd.Function):
                 if tgt is not None:
                     raise RuntimeError("GMConv2d: in-place gradient buffer must be channels_last")
                 dw = conv_wgrad(gy, xb, R, S, stride, pad, C0)
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
 def _use_hip(x):
@@ -372,10 +381,16 @@ class GMConv2d(nn.Conv2d):
         K, C0, R, S = self.weight.shape
         return self.pair_stem and self._hip_ok() and stem_pair_ok(C0, R, S, self.stride[0], self.padding[0])
 
-    def forward(self, x):
+    def forward(self, x, grad_join=None):
+        """grad_join: a gradsink.GradJoin shared with the other consumers of x (the
+        ResNet block input), so x's gradient is summed inside the dgrad epilogue."""
         if _use_hip(x) and self._hip_ok():
             with torch.autocast("cuda", enabled=False):
                 if self.uses_pair_stem() and not x.requires_grad:
                     return _StemFn.apply(x, self.weight, self.padding[0])
-                return _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0])
+                if grad_join is not None and x.requires_grad and torch.is_grad_enabled():
+                    grad_join.register()
+                else:
+                    grad_join = None
+                return _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0], grad_join)
         return F.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation, self.groups)

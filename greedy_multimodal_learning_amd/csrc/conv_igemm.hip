@@ -67,6 +67,7 @@ struct ConvArgs {
     // k-tiles [s*nk/S, (s+1)*nk/S) and the tile's splits hand their fp32 accumulators
     // on in order 0 -> 1 -> ... -> S-1 through ws (turnstile flags[tile], zero between
     // launches); the last split writes the output.  Deterministic (fixed order).
+    const uint16_t* addend;   // dgrad, optional: out = conv + addend (same layout as out)
     int splits, tiles_total;
     float* ws;                // [tiles][MT*NT*16/4][256] float4
     unsigned* flags;          // [tiles]
@@ -309,9 +310,15 @@ __global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
             for (int gq = 0; gq < 4; ++gq) {
                 const int n = n0 + wn * (BN / 2) + j * 32 + 8 * gq + 4 * fh;
                 if (n >= a.Nout) continue;
+                float o0 = acc[i][j][4 * gq], o1 = acc[i][j][4 * gq + 1];
+                float o2 = acc[i][j][4 * gq + 2], o3 = acc[i][j][4 * gq + 3];
+                if (a.addend) {  // fused gradient join (the residual branch's gradient)
+                    const uint2 av = *(const uint2*)(a.addend + (dst - cl.out) + n);
+                    o0 += bf_lo(av.x); o1 += bf_hi(av.x); o2 += bf_lo(av.y); o3 += bf_hi(av.y);
+                }
                 uint2 v;
-                v.x = pack_bf2(acc[i][j][4 * gq], acc[i][j][4 * gq + 1]);
-                v.y = pack_bf2(acc[i][j][4 * gq + 2], acc[i][j][4 * gq + 3]);
+                v.x = pack_bf2(o0, o1);
+                v.y = pack_bf2(o2, o3);
                 *(uint2*)(dst + n) = v;
             }
     }
@@ -527,18 +534,26 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
             for (int gq = 0; gq < 4; ++gq) {
                 const int n = n0 + wn * (BN / 2) + j * 32 + 8 * gq + 4 * fh;
                 if (n >= a.Nout) continue;
+                float o0 = acc[i][j][4 * gq], o1 = acc[i][j][4 * gq + 1];
+                float o2 = acc[i][j][4 * gq + 2], o3 = acc[i][j][4 * gq + 3];
+                if (a.addend) {  // fused gradient join (the residual branch's gradient)
+                    const uint2 av = *(const uint2*)(a.addend + (dst - cl.out) + n);
+                    o0 += bf_lo(av.x); o1 += bf_hi(av.x); o2 += bf_lo(av.y); o3 += bf_hi(av.y);
+                }
                 uint2 v;
-                v.x = pack_bf2(acc[i][j][4 * gq], acc[i][j][4 * gq + 1]);
-                v.y = pack_bf2(acc[i][j][4 * gq + 2], acc[i][j][4 * gq + 3]);
+                v.x = pack_bf2(o0, o1);
+                v.y = pack_bf2(o2, o3);
                 *(uint2*)(dst + n) = v;
             }
     }
 }
 
-// zero the output pixels no dgrad class covers (e.g. odd pixels of a 1x1/s2 dgrad)
-__global__ void k_zero_bf16(uint16_t* p, size_t n) {
+// zero the output pixels no dgrad class covers (e.g. odd pixels of a 1x1/s2 dgrad), or
+// copy the addend there when the dgrad is fused with a gradient join
+__global__ void k_zero_bf16(uint16_t* p, size_t n, const uint16_t* src) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; i * 8 < n; i += (size_t)gridDim.x * blockDim.x) *(uint4*)(p + i * 8) = make_uint4(0, 0, 0, 0);
+    for (; i * 8 < n; i += (size_t)gridDim.x * blockDim.x)
+        *(uint4*)(p + i * 8) = src ? *(const uint4*)(src + i * 8) : make_uint4(0, 0, 0, 0);
 }
 
 // W[Co][T][Ci] -> Wt[Ci][T][Co] (bf16), for the input-gradient convolution
@@ -914,21 +929,29 @@ extern "C" int gm_conv2d_fwd_bf16(const gm_conv_desc* d, const void* x, const vo
     return gm_conv2d_fwd_ex_bf16(d, x, w, y, nullptr, 0, stream);
 }
 
-extern "C" int gm_conv2d_dgrad_ex_bf16(const gm_conv_desc* d, const void* dy, const void* wt, void* dx, void* ws,
-                                       size_t ws_bytes, void* stream) {
+extern "C" int gm_conv2d_dgrad_add_bf16(const gm_conv_desc* d, const void* dy, const void* wt, void* dx,
+                                        const void* addend, void* ws, size_t ws_bytes, void* stream) {
     int rc = check_dgrad(d);
     if (rc) return rc;
     GM_REQUIRE(dy && wt && dx, "conv dgrad: null pointer");
+    GM_REQUIRE(addend != dx, "conv dgrad: addend must not alias dx");
     ConvArgs a;
     const bool full = dgrad_setup(d, dy, wt, dx, a);
+    a.addend = (const uint16_t*)addend;
     hipStream_t s = as_stream(stream);
     if (!full) {
         const size_t n = (size_t)d->N * d->H * d->W * d->C;
-        k_zero_bf16<<<(int)((n / 8 + 255) / 256 < 4096 ? (n / 8 + 255) / 256 : 4096), 256, 0, s>>>((uint16_t*)dx, n);
+        k_zero_bf16<<<(int)((n / 8 + 255) / 256 < 4096 ? (n / 8 + 255) / 256 : 4096), 256, 0, s>>>(
+            (uint16_t*)dx, n, (const uint16_t*)addend);
         rc = check_launch("k_zero_bf16");
         if (rc) return rc;
     }
     return pick_and_launch(a, s, ws, ws_bytes);
+}
+
+extern "C" int gm_conv2d_dgrad_ex_bf16(const gm_conv_desc* d, const void* dy, const void* wt, void* dx, void* ws,
+                                       size_t ws_bytes, void* stream) {
+    return gm_conv2d_dgrad_add_bf16(d, dy, wt, dx, nullptr, ws, ws_bytes, stream);
 }
 
 extern "C" int gm_conv2d_dgrad_bf16(const gm_conv_desc* d, const void* dy, const void* wt, void* dx,

@@ -61,3 +61,34 @@ def sink_done(p):
     s = p._gm_sink
     if s.on_ready is not None:
         s.on_ready(p)
+
+
+class GradJoin:
+    """Gradient of ONE activation consumed by several HIP backward functions (the
+    ResNet block input: the first convolution and the identity / downsample branch).
+
+    Autograd would materialise each consumer's gradient and add them with an extra
+    elementwise kernel.  Instead each consumer, in its backward, calls
+    `contribute(compute)`: every consumer but the last stores its gradient as the
+    pending addend and returns None to autograd; the last one computes its gradient
+    WITH the pending addend folded in (the conv dgrad epilogue adds it:
+    gm_conv2d_dgrad_add_bf16) and returns the total.  Order-independent; a consumer
+    that cannot fold gets `addend` and must add it itself."""
+
+    def __init__(self):
+        self.n = 0
+        self.done = 0
+        self.pending = None
+
+    def register(self):
+        self.n += 1
+
+    def contribute(self, compute):
+        self.done += 1
+        add, self.pending = self.pending, None
+        g = compute(add)
+        if self.done >= self.n:
+            self.done = 0
+            return g
+        self.pending = g
+        return None

@@ -10,11 +10,20 @@ config C5.  Convolutions are `conv.GMConv2d` (bf16 MFMA kernels on HIP); batch
 norms are `bn.GMBatchNorm2d`, which take the block's residual add and ReLU as
 fused arguments (`relu` modules are kept for name/structure parity).
 """
+import os
+
 import torch
 import torch.nn as nn
 
 from .bn import GMBatchNorm2d
 from .conv import GMConv2d
+from .gradsink import GradJoin
+
+_JOIN = os.environ.get("GM_GRAD_JOIN", "1") != "0"
+
+
+def _join():
+    return GradJoin() if _JOIN else None
 from .pool import GMMaxPool2d
 
 
@@ -40,9 +49,13 @@ class BasicBlock(nn.Module):
         self.stride = stride
 
     def forward(self, x):
-        idt = x if self.downsample is None else self.downsample(x)
-        out = self.bn1(self.conv1(x), relu=True)
-        return self.bn2(self.conv2(out), residual=idt, relu=True)
+        # x feeds conv1 and the identity / downsample branch: their gradients are summed
+        # inside the last consumer's backward kernel (gradsink.GradJoin), not by autograd
+        join = _join()
+        idt = x if self.downsample is None else self.downsample[1](self.downsample[0](x, grad_join=join))
+        out = self.bn1(self.conv1(x, grad_join=join), relu=True)
+        return self.bn2(self.conv2(out), residual=idt, relu=True,
+                        residual_join=join if self.downsample is None else None)
 
 
 class Bottleneck(nn.Module):
@@ -61,10 +74,12 @@ class Bottleneck(nn.Module):
         self.stride = stride
 
     def forward(self, x):
-        idt = x if self.downsample is None else self.downsample(x)
-        out = self.bn1(self.conv1(x), relu=True)
+        join = _join()
+        idt = x if self.downsample is None else self.downsample[1](self.downsample[0](x, grad_join=join))
+        out = self.bn1(self.conv1(x, grad_join=join), relu=True)
         out = self.bn2(self.conv2(out), relu=True)
-        return self.bn3(self.conv3(out), residual=idt, relu=True)
+        return self.bn3(self.conv3(out), residual=idt, relu=True,
+                        residual_join=join if self.downsample is None else None)
 
 
 class ResNet(nn.Module):

@@ -225,6 +225,12 @@ int gm_conv2d_fwd_ex_bf16(const gm_conv_desc* d, const void* x, const void* w, v
                           size_t ws_bytes, void* stream);
 int gm_conv2d_dgrad_ex_bf16(const gm_conv_desc* d, const void* dy, const void* wt, void* dx, void* ws,
                             size_t ws_bytes, void* stream);
+/* dgrad fused with a gradient join: dx = conv_transpose(dy, w) + addend (bf16, dx's
+ * layout, must not alias dx) - the other consumer's gradient of the same tensor, so
+ * the autograd add of the two is never materialised (ResNet blocks: the identity /
+ * downsample branch and the first convolution both consume the block input). */
+int gm_conv2d_dgrad_add_bf16(const gm_conv_desc* d, const void* dy, const void* wt, void* dx,
+                             const void* addend, void* ws, size_t ws_bytes, void* stream);
 int gm_conv_weight_transpose_bf16(const void* w, void* wt, int K, int RS, int C, void* stream);
 /* fp32 KRSC master weight -> bf16 [K][RS][Cp] (zero-padded channels) and, if wt != NULL,
  * the transposed bf16 [Cp][RS][K] for dgrad, in one pass */
