@@ -15,6 +15,7 @@ parity mode, CPU) use PyTorch's batch_norm.  Reference: torchvision ResNet
 BasicBlock/Bottleneck as used by src/model.py:53-56,65-106.
 """
 import ctypes
+import os
 
 import torch
 import torch.nn as nn
@@ -26,6 +27,12 @@ from .gradsink import sink_done, sink_target
 CL = torch.channels_last
 
 _scratch = {}
+
+# ReLU BNs without a residual keep the forward's fp32 affine coefficients (2C floats)
+# instead of y: the backward recomputes the mask x*sc + sh > 0 from x, which it reads
+# anyway, so y is never read back (one bf16 activation read fewer in each of the two
+# backward kernels).  GM_BN_MASKX=0 keeps the y mask.
+MASK_FROM_X = os.environ.get("GM_BN_MASKX", "1") != "0"
 
 
 def _get_scratch(device, M, C):
@@ -55,7 +62,8 @@ def _check_shape(x, C):
         raise ValueError(f"HIP batchnorm needs C a power of two in [8, 2048], got {C}")
 
 
-def bn_fwd_train(x, weight, bias, running_mean, running_var, nbt, momentum, eps, relu, residual):
+def bn_fwd_train(x, weight, bias, running_mean, running_var, nbt, momentum, eps, relu, residual, coef=None):
+    """coef: optional fp32 [2C] tensor receiving the affine coefficients (sc, sh)."""
     lib = L.load()
     N, C, H, W = x.shape
     _check_shape(x, C)
@@ -69,7 +77,7 @@ def bn_fwd_train(x, weight, bias, running_mean, running_var, nbt, momentum, eps,
     buf = _get_scratch(x.device, M, C)
     p = L.BnFwd(M, C, int(relu), x.data_ptr(), L.ptr(residual), y.data_ptr(), weight.data_ptr(),
                 bias.data_ptr(), L.ptr(running_mean), L.ptr(running_var), float(momentum), float(eps),
-                sm.data_ptr(), si.data_ptr(), L.ptr(nbt))
+                sm.data_ptr(), si.data_ptr(), L.ptr(nbt), L.ptr(coef))
     L.check(lib.gm_bn_fwd_train_bf16(ctypes.byref(p), buf.data_ptr(), buf.numel(), L.stream_of(x.device)),
             "gm_bn_fwd_train_bf16")
     return y, sm, si
@@ -92,8 +100,9 @@ def bn_fwd_infer(x, weight, bias, running_mean, running_var, eps, relu, residual
     return y
 
 
-def bn_bwd(dy, y, x, weight, sm, si, relu, want_dres, dgamma, dbeta, accumulate):
-    """Returns (dx, dres); dgamma/dbeta are written (or added) in place."""
+def bn_bwd(dy, y, x, weight, sm, si, relu, want_dres, dgamma, dbeta, accumulate, fwd_coef=None):
+    """Returns (dx, dres); dgamma/dbeta are written (or added) in place.  With relu,
+    the mask comes from y, or from x and the forward's coefficients when y is None."""
     lib = L.load()
     N, C, H, W = x.shape
     M = N * H * W
@@ -103,7 +112,7 @@ def bn_bwd(dy, y, x, weight, sm, si, relu, want_dres, dgamma, dbeta, accumulate)
     buf = _get_scratch(x.device, M, C)
     p = L.BnBwd(M, C, int(relu), dy.data_ptr(), L.ptr(y) if relu else 0, x.data_ptr(), weight.data_ptr(),
                 sm.data_ptr(), si.data_ptr(), dx.data_ptr(), L.ptr(dres), dgamma.data_ptr(), dbeta.data_ptr(),
-                int(accumulate), 0)
+                int(accumulate), 0, L.ptr(fwd_coef))
     L.check(lib.gm_bn_bwd_bf16(ctypes.byref(p), buf.data_ptr(), buf.numel(), L.stream_of(x.device)),
             "gm_bn_bwd_bf16")
     return dx, dres
@@ -114,9 +123,12 @@ class _BNFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, momentum, eps, relu, join=None):
         ctx.join = join
         xb = _nhwc(x.to(torch.bfloat16))
+        maskx = relu and residual is None and MASK_FROM_X
+        coef = torch.empty(2 * xb.shape[1], device=xb.device, dtype=torch.float32) if maskx else None
         y, sm, si = bn_fwd_train(xb, weight.detach(), bias.detach(), running_mean, running_var, nbt, momentum,
-                                 eps, relu, residual)
-        ctx.save_for_backward(xb, y if relu else None, weight, bias, sm, si)
+                                 eps, relu, residual, coef)
+        ctx.save_for_backward(xb, y if relu and not maskx else coef, weight, bias, sm, si)
+        ctx.maskx = maskx
         ctx.relu = relu
         ctx.has_res = residual is not None
         return y
@@ -124,6 +136,9 @@ class _BNFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         xb, y, weight, bias, sm, si = ctx.saved_tensors
+        coef = None
+        if ctx.maskx:
+            y, coef = None, y
         C = xb.shape[1]
         want_w, want_b = ctx.needs_input_grad[1], ctx.needs_input_grad[2]
         tw = sink_target(weight) if want_w else None
@@ -138,7 +153,7 @@ class _BNFn(torch.autograd.Function):
             dbeta = torch.empty(C, device=xb.device, dtype=torch.float32)
             acc, direct = False, False
         want_dres = ctx.has_res and ctx.needs_input_grad[3]
-        dx, dres = bn_bwd(dy, y, xb, weight.detach(), sm, si, ctx.relu, want_dres, dgamma, dbeta, acc)
+        dx, dres = bn_bwd(dy, y, xb, weight.detach(), sm, si, ctx.relu, want_dres, dgamma, dbeta, acc, coef)
         if direct:
             sink_done(weight)
             sink_done(bias)

@@ -108,12 +108,17 @@ struct ReduceArgs {
     long long* nbt;      // num_batches_tracked (fwd, may be null)
     float* coef;         // [4][C]
     float* part;         // [nslice][nrc][SW][2] fp32 per-block partials
+    float* coef_out;     // fwd, optional: the affine coefficients sc[C], sh[C] for the backward
+    const float* fcoef;  // BWD_RELUX: the forward's sc[C], sh[C]
 };
 
-enum { FWD = 0, BWD = 1, BWD_RELU = 2 };  // relu as a template arg: no per-load branch
+// BWD_RELUX: the relu mask recomputed from x and the forward's affine coefficients
+// (z = x*sc + sh > 0, the forward's own fp32 value) instead of read back from y
+enum { FWD = 0, BWD = 1, BWD_RELU = 2, BWD_RELUX = 3 };  // relu as a template arg: no per-load branch
 
 template <int MODE>
-__device__ __forceinline__ void accum(const ReduceArgs& a, long long v, const float* mu, float* s1, float* s2) {
+__device__ __forceinline__ void accum(const ReduceArgs& a, long long v, const float* mu, float* s1, float* s2,
+                                      const float* fsc, const float* fsh) {
     float xf[8];
     unpack8(a.x[v], xf);
     if (MODE == FWD) {
@@ -130,6 +135,10 @@ __device__ __forceinline__ void accum(const ReduceArgs& a, long long v, const fl
             unpack8(a.y[v], yf);
 #pragma unroll
             for (int j = 0; j < 8; ++j) d[j] = yf[j] > 0.f ? d[j] : 0.f;
+        }
+        if (MODE == BWD_RELUX) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) d[j] = fmaf(xf[j], fsc[j], fsh[j]) > 0.f ? d[j] : 0.f;
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -202,6 +211,10 @@ __device__ __forceinline__ void finalize(const ReduceArgs& a, int c, double S1, 
         const double sc = g * invstd;
         a.coef[c] = (float)sc;
         a.coef[C + c] = (float)((double)f.b - mean * sc);
+        if (a.coef_out) {
+            a.coef_out[c] = a.coef[c];
+            a.coef_out[C + c] = a.coef[C + c];
+        }
         a.save_mean[c] = (float)mean;
         a.save_invstd[c] = (float)invstd;
         if (a.rmean) {
@@ -264,6 +277,14 @@ __global__ __launch_bounds__(kT) void k_bn_reduce(ReduceArgs a) {
     const long long vpr = C >> 3;                     // 16-B vectors per row
     const int c0 = cs * SW + cg * 8;                  // first channel of this thread
 
+    float fsc[8], fsh[8];
+    if (MODE == BWD_RELUX) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            fsc[j] = a.fcoef[c0 + j];
+            fsh[j] = a.fcoef[C + c0 + j];
+        }
+    }
     float mu[8];
     if (MODE != FWD) {
 #pragma unroll
@@ -282,7 +303,7 @@ __global__ __launch_bounds__(kT) void k_bn_reduce(ReduceArgs a) {
     for (; r + 7 * rpp < rend; r += 8 * rpp) {
         const long long v = r * vpr + cv;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) accum<MODE>(a, v + u * st, mu, s1, s2);
+        for (int u = 0; u < 8; ++u) accum<MODE>(a, v + u * st, mu, s1, s2, fsc, fsh);
     }
     if (MODE == FWD && r < rend) {  // the tail as ONE predicated batch: all its loads in flight
         uint4 vx[8];
@@ -292,7 +313,7 @@ __global__ __launch_bounds__(kT) void k_bn_reduce(ReduceArgs a) {
 #pragma unroll
         for (int u = 0; u < 8; ++u) accum_vals<MODE>(r + u * rpp < rend ? vx[u] : z, z, z, mu, s1, s2);
     } else {
-        for (; r < rend; r += rpp) accum<MODE>(a, r * vpr + cv, mu, s1, s2);
+        for (; r < rend; r += rpp) accum<MODE>(a, r * vpr + cv, mu, s1, s2, fsc, fsh);
     }
 
     // row-group combine in LDS: red[r0][SW][2]  (rpp * 2SW == 4096 floats)
@@ -359,6 +380,7 @@ struct ApplyArgs {
     uint4* out2;         // bwd dres
     const float* coef;   // [4][C]
     int C;
+    const float* fcoef;  // bwd MASKX: the forward's sc[C], sh[C]
 };
 
 __device__ __forceinline__ void load_coef(const float* p, int cg, float* c) {
@@ -395,20 +417,27 @@ __global__ __launch_bounds__(kT) void k_bn_apply(ApplyArgs a) {
     if (v < a.nvec) one(v);
 }
 
-template <bool RELU, bool DRES>
+template <bool RELU, bool DRES, bool MASKX = false>
 __global__ __launch_bounds__(kT) void k_bn_apply_bwd(ApplyArgs a) {
     const long long stride = (long long)gridDim.x * kT;
     long long v = (long long)blockIdx.x * kT + threadIdx.x;
     const int cg = (int)(v & ((1 << a.tpr_log) - 1));
-    float ca[8], cb[8], cc[8];
+    float ca[8], cb[8], cc[8], fs[8], fh[8];
     load_coef(a.coef, cg, ca);
     load_coef(a.coef + a.C, cg, cb);
     load_coef(a.coef + 2 * a.C, cg, cc);
+    if (MASKX) {
+        load_coef(a.fcoef, cg, fs);
+        load_coef(a.fcoef + a.C, cg, fh);
+    }
     auto one = [&](long long i) {
         float d[8], xf[8];
         unpack8(a.dy[i], d);
         unpack8(a.x[i], xf);
-        if (RELU) {
+        if (RELU && MASKX) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) d[j] = fmaf(xf[j], fs[j], fh[j]) > 0.f ? d[j] : 0.f;
+        } else if (RELU) {
             float yf[8];
             unpack8(a.res[i], yf);
 #pragma unroll
@@ -485,6 +514,7 @@ extern "C" int gm_bn_fwd_train_bf16(const gm_bn_fwd* p, void* scratch, size_t by
     a.momentum = p->momentum; a.eps = p->eps;
     a.save_mean = p->save_mean; a.save_invstd = p->save_invstd;
     a.nbt = p->num_batches_tracked;
+    a.coef_out = p->coef_out;
     a.counter = reinterpret_cast<unsigned*>(s);
     a.coef = reinterpret_cast<float*>(s + pl.off_coef);
     a.part = reinterpret_cast<float*>(s + pl.off_p1);
@@ -535,7 +565,9 @@ extern "C" int gm_bn_fwd_infer_bf16(const gm_bn_fwd* p, void* scratch, size_t by
 extern "C" int gm_bn_bwd_bf16(const gm_bn_bwd* p, void* scratch, size_t bytes, void* stream) {
     GM_REQUIRE(p && p->dy && p->x && p->gamma && p->save_mean && p->save_invstd && p->dx && p->dgamma && p->dbeta,
                "gm_bn_bwd_bf16: null argument");
-    GM_REQUIRE(!p->relu || p->y, "gm_bn_bwd_bf16: relu needs the forward output y");
+    GM_REQUIRE(!p->relu || p->y || (p->fwd_coef && !p->dres),
+               "gm_bn_bwd_bf16: relu needs the forward output y (or fwd_coef, without a residual)");
+    const bool maskx = p->relu && !p->y;
     int rc = check_common(p->M, p->C, scratch, bytes, "gm_bn_bwd_bf16");
     if (rc) return rc;
     const Plan pl = make_plan(p->M, p->C);
@@ -549,19 +581,24 @@ extern "C" int gm_bn_bwd_bf16(const gm_bn_bwd* p, void* scratch, size_t bytes, v
     a.gamma = p->gamma;
     a.save_mean = const_cast<float*>(p->save_mean); a.save_invstd = const_cast<float*>(p->save_invstd);
     a.dgamma = p->dgamma; a.dbeta = p->dbeta;
+    a.fcoef = p->fwd_coef;
     a.counter = reinterpret_cast<unsigned*>(s);
     a.coef = reinterpret_cast<float*>(s + pl.off_coef);
     a.part = reinterpret_cast<float*>(s + pl.off_p1);
     hipStream_t st = as_stream(stream);
-    if (p->relu) hipLaunchKernelGGL(k_bn_reduce<BWD_RELU>, dim3(pl.nrc, pl.nslice), dim3(kT), 0, st, a);
+    if (maskx) hipLaunchKernelGGL(k_bn_reduce<BWD_RELUX>, dim3(pl.nrc, pl.nslice), dim3(kT), 0, st, a);
+    else if (p->relu) hipLaunchKernelGGL(k_bn_reduce<BWD_RELU>, dim3(pl.nrc, pl.nslice), dim3(kT), 0, st, a);
     else hipLaunchKernelGGL(k_bn_reduce<BWD>, dim3(pl.nrc, pl.nslice), dim3(kT), 0, st, a);
     if ((rc = check_launch("k_bn_reduce<bwd>"))) return rc;
     ApplyArgs b{};
     b.nvec = p->M * (p->C / 8); b.tpr_log = ilog2(p->C / 8); b.C = p->C; b.relu = p->relu;
     b.x = a.x; b.res = a.y; b.dy = a.dy; b.out = static_cast<uint4*>(p->dx);
     b.out2 = static_cast<uint4*>(p->dres); b.coef = a.coef;
+    b.fcoef = p->fwd_coef;
     const int g = apply_grid(b.nvec, p->C);
-    if (p->relu) {
+    if (maskx) {
+        hipLaunchKernelGGL((k_bn_apply_bwd<true, false, true>), dim3(g), dim3(kT), 0, st, b);
+    } else if (p->relu) {
         if (p->dres) hipLaunchKernelGGL((k_bn_apply_bwd<true, true>), dim3(g), dim3(kT), 0, st, b);
         else hipLaunchKernelGGL((k_bn_apply_bwd<true, false>), dim3(g), dim3(kT), 0, st, b);
     } else {

@@ -287,6 +287,7 @@ typedef struct gm_bn_fwd {
     float* save_mean;
     float* save_invstd;
     long long* num_batches_tracked;  /* train: += 1 if non-NULL (nn.BatchNorm2d counter) */
+    float* coef_out;                 /* train, optional: the affine coefficients sc[C], sh[C] (fp32) */
 } gm_bn_fwd;
 
 typedef struct gm_bn_bwd {
@@ -304,6 +305,8 @@ typedef struct gm_bn_bwd {
     float* dbeta;
     int accumulate;
     int pad;
+    const float* fwd_coef;  /* relu without residual: the forward's coef_out; y may then be NULL and
+                               the relu mask is recomputed from x (x*sc + sh > 0, the forward's value) */
 } gm_bn_bwd;
 
 size_t gm_bn_scratch(long long M, int C);

@@ -123,3 +123,25 @@ def test_bn_grad_sink_in_place():
     y3.backward(dy)
     assert torch.allclose(g1, m2.weight.grad, rtol=0, atol=0)
     assert torch.allclose(m.weight.grad, 2 * m2.weight.grad, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_bn_relu_mask_from_x_equals_y_mask(shape, monkeypatch):
+    """ReLU BN without a residual: the backward's mask recomputed from x and the
+    forward's coefficients (x*sc + sh > 0) == the mask read from y, bit for bit."""
+    from greedy_multimodal_learning_amd import bn as B
+    x, _, w, b, rm, rv, dy = _inputs(shape, 11 + shape[0], False)
+    C = shape[1]
+    outs = []
+    for maskx in (False, True):
+        monkeypatch.setattr(B, "MASK_FROM_X", maskx)
+        m = B.GMBatchNorm2d(C).cuda().to(memory_format=CL)
+        with torch.no_grad():
+            m.weight.copy_(w)
+            m.bias.copy_(b)
+        xg = x.clone().requires_grad_(True)
+        y = m(xg, relu=True)
+        y.backward(dy)
+        outs.append((y, xg.grad, m.weight.grad, m.bias.grad))
+    for a, b2 in zip(*outs):
+        assert torch.equal(a, b2)
