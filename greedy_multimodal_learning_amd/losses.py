@@ -5,7 +5,11 @@ import torch.nn.functional as F
 
 def blend_loss(y_hat, y):
     """Sum over branches of the mean cross-entropy of each branch's logits
-    (the loss never sees the averaged logits)."""
+    (the loss never sees the averaged logits).  HIP tensors: one fused launch each
+    way (head.branch_xent)."""
+    from .head import branch_xent, xent_ok
+    if len(y_hat) and xent_ok(y_hat, y):
+        return branch_xent(y_hat, y)
     return sum(F.cross_entropy(logits, y) for logits in y_hat)
 
 

@@ -15,6 +15,7 @@ import torch.nn as nn
 from .balanced_mmtm import MMTM_mitigate as MMTM
 from .balanced_mmtm import get_rescale_weights
 from .gin_lite import configurable
+from .head import head_ok, pooled_linear
 from .resnet import resnet18
 from .streams import ViewStreams
 
@@ -58,6 +59,15 @@ class MMTM_MVCNN(nn.Module):
     def _head(net, f):
         return net.fc(torch.flatten(net.avgpool(f), 1))
 
+    @staticmethod
+    def _fused_head(nets, fs):
+        """All branches' avgpool + fc in one launch each way (head.py), or None."""
+        fcs = [n.fc for n in nets]
+        if not (all(isinstance(n.avgpool, nn.AdaptiveAvgPool2d) and n.avgpool.output_size in ((1, 1), 1)
+                    and isinstance(n.fc, nn.Linear) for n in nets) and head_ok(fs, fcs)):
+            return None
+        return pooled_linear(fs, fcs)
+
     def forward(self, x, curation_mode=False, caring_modality=None):
         # view 1's trunk segments run on a side HIP stream (streams.py): the two
         # trunks only meet at the MMTM sites, which run on the main stream
@@ -82,10 +92,14 @@ class MMTM_MVCNN(nn.Module):
                 vs.fork([(1, f1)])
             scales.append(sc)
             squeezed.append(sq)
-        x1 = run(1, self._head, self.net_view_1, f1)
-        x0 = self._head(self.net_view_0, f0)
-        if vs is not None:
-            vs.join([x1])
+        fused = self._fused_head([self.net_view_0, self.net_view_1], [f0, f1])
+        if fused is not None:  # both heads on the main stream (f1 was joined at mmtm4)
+            x0, x1 = fused
+        else:
+            x1 = run(1, self._head, self.net_view_1, f1)
+            x0 = self._head(self.net_view_0, f0)
+            if vs is not None:
+                vs.join([x1])
         return (x0 + x1) / 2, [x0, x1], scales, squeezed
 
 
@@ -146,9 +160,11 @@ class MMTM_MVCNN_N(nn.Module):
                 vs.fork(list(enumerate(fs)))
             scales.append(sc)
             squeezed.append(sq)
-        outs = [None] * self.num_views
-        for i in order:
-            outs[i] = run(i, MMTM_MVCNN._head, nets[i], fs[i])
-        if vs is not None:
-            vs.join(outs[1:])
+        outs = MMTM_MVCNN._fused_head(nets, fs)
+        if outs is None:
+            outs = [None] * self.num_views
+            for i in order:
+                outs[i] = run(i, MMTM_MVCNN._head, nets[i], fs[i])
+            if vs is not None:
+                vs.join(outs[1:])
         return sum(outs) / len(outs), outs, scales, squeezed

@@ -180,6 +180,18 @@ int gm_mmtm_select_scale(const float* e_v, int ld_v, const float* e_s, int ld_s,
                          float* s_v, float* s_s, float* mask, void* stream);
 int gm_mmtm_mask_rows(float* a, long long n, const float* mask, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Branch-summed cross-entropy (reference train.py:22-29 blend_loss: sum over the
+ * branches of nn.CrossEntropyLoss()(logits, y), batch mean) and its gradient.
+ * logits: fp32 [nbranch][B][N] contiguous, labels int64 [B]; lse: fp32 [nbranch*B]
+ * (written by fwd, read by bwd); loss: fp32 scalar; gout: fp32 scalar (device).
+ * dlogits[r,n] = gout * (softmax(x_r)[n] - [n == y]) / B.  Deterministic.
+ * ------------------------------------------------------------------------- */
+int gm_xent_fwd(const float* logits, int nbranch, int B, int N, const long long* labels, float* lse,
+                float* loss, void* stream);
+int gm_xent_bwd(const float* logits, const float* lse, int nbranch, int B, int N, const long long* labels,
+                const float* gout, float* dlogits, void* stream);
+
 int gm_group_sumsq(const gm_tensor* table, int ntensors, long long total_elems, int ngroups,
                    float grad_scale, float lr, double* out, void* scratch, size_t scratch_bytes,
                    void* stream);
