@@ -160,11 +160,19 @@ class GateState(ctypes.Structure):
                 ("eps", ctypes.c_double), ("M", ctypes.c_double * 4), ("d_bdr", ctypes.c_double)]
 
 
+class StemPack(ctypes.Structure):
+    _fields_ = [("x", c_void_p), ("dtype", c_int), ("N", c_int), ("C0", c_int), ("H", c_int), ("W", c_int),
+                ("pad", c_int), ("sn", ctypes.c_longlong), ("sc", ctypes.c_longlong), ("sh", ctypes.c_longlong),
+                ("sw", ctypes.c_longlong), ("Hp", c_int), ("Wp", c_int), ("xp", c_void_p), ("w", c_void_p),
+                ("K", c_int), ("R", c_int), ("S", c_int), ("wp", c_void_p)]
+
+
 EXPORTS.update({
     "gm_gate_strong_step": (c_int, [c_void_p, c_void_p, c_void_p]),
     "gm_mmtm_select_scale": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "gm_mmtm_mask_rows": (c_int, [c_void_p, ctypes.c_longlong, c_void_p, c_void_p]),
+    "gm_stem_pack_bf16": (c_int, [c_void_p, c_void_p]),
     "gm_xent_fwd": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "gm_xent_bwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
 })

@@ -171,6 +171,24 @@ def stem_pack_weight(weight):
     return wp.view(K, R, Sp, 8).permute(0, 3, 1, 2)
 
 
+def stem_pack(x, weight, pad):
+    """(stem_pack_input(x), stem_pack_weight(weight)) in one launch (gm_stem_pack_bf16)."""
+    N, C0, H, W = x.shape
+    K, _, R, S = weight.shape
+    P, Q, Sp, Hp, Wp = _stem_geom(H, W, R, S, pad)
+    if x.dtype not in (torch.float32, torch.bfloat16):
+        x = x.float()
+    w = weight.detach()
+    if w.dtype != torch.float32 or not w.is_contiguous():
+        w = w.float().contiguous()
+    xp = torch.empty(N, Hp, Wp // 2, 8, device=x.device, dtype=torch.bfloat16)
+    wp = torch.empty(K, R, Sp, 8, device=x.device, dtype=torch.bfloat16)
+    p = L.StemPack(x.data_ptr(), L.GM_BF16 if x.dtype == torch.bfloat16 else L.GM_F32, N, C0, H, W, pad,
+                   *x.stride(), Hp, Wp, xp.data_ptr(), w.data_ptr(), K, R, S, wp.data_ptr())
+    L.check(L.load().gm_stem_pack_bf16(ctypes.byref(p), L.stream_of(x.device)), "gm_stem_pack_bf16")
+    return xp.permute(0, 3, 1, 2), wp.permute(0, 3, 1, 2)
+
+
 def stem_fwd(xp, wp, P, Q):
     lib = L.load()
     N, _, Hp, Wq = xp.shape
@@ -190,8 +208,7 @@ class _StemFn(torch.autograd.Function):
         K, C0, R, S = weight.shape
         N, _, H, W = x.shape
         P, Q, Sp, Hp, Wp = _stem_geom(H, W, R, S, pad)
-        xp = stem_pack_input(x, R, S, pad)
-        wp = stem_pack_weight(weight)
+        xp, wp = stem_pack(x, weight, pad)
         y = stem_fwd(xp, wp, P, Q)
         ctx.save_for_backward(xp, weight)
         ctx.meta = (R, S, Sp)

@@ -233,8 +233,10 @@ class BalancedStep:
             self.buckets.names = {id(p): n for n, p in named}
         # HIP conv/BN backward kernels write their parameter gradients straight into
         # the flat buffer (no AccumulateGrad add) and fire the bucket hook themselves
+        # lazy_zero: no zero-fill of the flat gradient buffer per step (gradsink.py)
         self.sink = GradSink(self.flat.slices.keys(),
-                             on_ready=self.buckets._on_sink if self.buckets is not None else None)
+                             on_ready=self.buckets._on_sink if self.buckets is not None else None,
+                             lazy_zero=os.environ.get("GM_LAZY_ZERO", "1") != "0")
         self.last_loss = None
         self.step_count = 0
         self.timer = None  # optional (start_event, end_event) list collector for the fused pass
@@ -307,7 +309,8 @@ class BalancedStep:
             return self.model(x, curation_mode=fl.curation_mode, caring_modality=fl.caring_modality)
 
     def _fwd_bwd(self, x, y):
-        self.flat_grad.zero_()
+        if not self.sink.lazy_zero:
+            self.flat_grad.zero_()
         if self.buckets is not None:
             self.buckets.reset()
         self.sink.begin_step()

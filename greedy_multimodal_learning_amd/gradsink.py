@@ -20,24 +20,49 @@ between branches stay correct.  Parameters outside a sink (or a sink that is
 not active) keep the ordinary autograd path.
 """
 
+import torch
+
 
 class GradSink:
-    def __init__(self, params, on_ready=None):
+    """lazy_zero: the caller does NOT zero the gradients before the step.  A gradient
+    that autograd is about to accumulate into is zeroed first (tensor pre-hook, only
+    for parameters not yet written this step), and end_step() zeroes the gradients
+    nothing wrote; sink writes overwrite anyway.  With every gradient sink-delivered
+    (the HIP training step) no zero-fill of the gradient buffer runs at all."""
+
+    def __init__(self, params, on_ready=None, lazy_zero=False):
         self.params = list(params)
         self.on_ready = on_ready
         self.active = False
+        self.lazy_zero = lazy_zero
         self._written = set()
+        self._hooks = []
         for p in self.params:
             p._gm_sink = self
+            if lazy_zero:
+                self._hooks.append(p.register_hook(lambda g, p=p: self._before_accumulate(p)))
+
+    def _before_accumulate(self, p):
+        if self.active and id(p) not in self._written:
+            self._written.add(id(p))
+            if p.grad is not None:
+                p.grad.zero_()
 
     def begin_step(self):
         self._written = set()
         self.active = True
 
     def end_step(self):
+        if self.active and self.lazy_zero:
+            rest = [p.grad for p in self.params if id(p) not in self._written and p.grad is not None]
+            if rest:
+                torch._foreach_zero_(rest)
         self.active = False
 
     def detach(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
         for p in self.params:
             if getattr(p, "_gm_sink", None) is self:
                 del p._gm_sink

@@ -181,6 +181,28 @@ int gm_mmtm_select_scale(const float* e_v, int ld_v, const float* e_s, int ld_s,
 int gm_mmtm_mask_rows(float* a, long long n, const float* mask, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Pixel-pair packing of the RGB stem (one launch, input and weight):
+ *   xp [N][Hp][Wp/2][8] bf16: xp[n][hp][wq][4j+c] = x[n, c, hp-pad, 2wq+j-pad], 0 outside
+ *                       the image or for c >= C0; x fp32/bf16 with element strides sn..sw
+ *   wp [K][R][(S+1)/2][8] bf16 (if w): wp[k][r][sq][4j+c] = w[k, c, r, 2sq+j], 0 past S/C0
+ * The stem convolution then runs as a C = 8, strides (2, 1) convolution on the pair
+ * view (conv.py).  Replaces the reference's plain Conv2d(3, 64, 7, 2, 3) input path.
+ * ------------------------------------------------------------------------- */
+typedef struct gm_stem_pack {
+    const void* x;
+    int dtype;                 /* GM_F32 or GM_BF16 */
+    int N, C0, H, W, pad;
+    long long sn, sc, sh, sw;  /* element strides of x */
+    int Hp, Wp;
+    void* xp;
+    const float* w;            /* optional fp32 [K, C0, R, S] contiguous */
+    int K, R, S;
+    void* wp;
+} gm_stem_pack;
+
+int gm_stem_pack_bf16(const gm_stem_pack* p, void* stream);
+
+/* ---------------------------------------------------------------------------
  * Branch-summed cross-entropy (reference train.py:22-29 blend_loss: sum over the
  * branches of nn.CrossEntropyLoss()(logits, y), batch mean) and its gradient.
  * logits: fp32 [nbranch][B][N] contiguous, labels int64 [B]; lse: fp32 [nbranch*B]

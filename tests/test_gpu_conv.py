@@ -181,3 +181,21 @@ def test_conv_splitk_turnstile(dev, shape):
                                               False, [0, 0], 1, [True, False, False])[0]
     _close(y1, yr, 1e-2)
     _close(dx1, dxr, 1e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(3, 2, 3, 37, 30, 64, 7, 7, 3), (2, 2, 3, 224, 224, 64, 7, 7, 3),
+                                   (2, 1, 4, 16, 18, 32, 5, 5, 2), (1, 3, 1, 9, 9, 8, 3, 3, 1)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_stem_pack_kernel_matches_torch_pack(dev, shape, dtype):
+    """gm_stem_pack_bf16 (input + weight pair views, one launch) == the PyTorch packing,
+    bit for bit, from a strided view of a [B, V, C, H, W] batch."""
+    from greedy_multimodal_learning_amd import conv as G
+    N, V, C, H, W, K, R, S, pad = shape
+    g = torch.Generator(device="cuda").manual_seed(sum(shape))
+    batch = torch.randn(N, V, C, H, W, device=dev, generator=g).to(dtype)
+    w = torch.randn(K, C, R, S, device=dev, generator=g)
+    x = batch[:, V - 1]
+    xp, wp = G.stem_pack(x, w, pad)
+    assert torch.equal(xp, G.stem_pack_input(x, R, S, pad))
+    assert torch.equal(wp, G.stem_pack_weight(w))
