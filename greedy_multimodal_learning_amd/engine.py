@@ -251,6 +251,7 @@ class BalancedStep:
         self._graphs = {}
         self._gpool = None
         self._static = None
+        self._slots = {}
         from .balanced_mmtm import MMTM_mitigate
         from .mmtm_n import MMTM_N
         self._mmtms = [m for m in model.modules() if isinstance(m, (MMTM_mitigate, MMTM_N))]
@@ -344,7 +345,21 @@ class BalancedStep:
         fl = self.flags
         return (bool(fl.curation_mode), fl.caring_modality if fl.curation_mode else None, self.lr)
 
-    def _capture(self, key):
+    def bind_batches(self, *pairs):
+        """Register device batches (x, y) as static graph inputs.  A step on a bound
+        batch replays that slot's own graph and copies nothing; a loader refills a slot
+        in place while another slot's step runs (double-buffered input).  Any other
+        batch is copied into the engine's own static buffers first, as before."""
+        self._slots = {(x.data_ptr(), y.data_ptr()): (x, y) for x, y in pairs}
+
+    def _slot_of(self, x, y):
+        slot = self._slots.get((x.data_ptr(), y.data_ptr())) if self._slots else None
+        if slot is None or slot[0].shape != x.shape or slot[0].stride() != x.stride() or slot[0].dtype != x.dtype \
+                or slot[1].shape != y.shape or slot[1].dtype != y.dtype:
+            return None
+        return slot
+
+    def _capture(self, key, inputs=None):
         """Record one whole step for the current curation flags (nothing executes)."""
         steps = [(m, m.step) for m in self._mmtms]
         g = torch.cuda.CUDAGraph()
@@ -359,7 +374,7 @@ class BalancedStep:
         mode = "thread_local" if dp else "global"
         try:
             with torch.cuda.graph(g, pool=self._gpool, capture_error_mode=mode):
-                loss = self._fwd_bwd(*self._static).detach()
+                loss = self._fwd_bwd(*(inputs or self._static)).detach()
                 sums = None if dp else self.norms.sums(grad_scale=1.0 / self.world, lr=self.lr)
                 if sums is not None and self.device_gate:
                     self._gate_step(sums)
@@ -378,18 +393,20 @@ class BalancedStep:
         self.model.train(True)
         gate = self.gate
         if self.graphs and self.step_count > 0:
-            st = self._static
-            if st is None or st[0].shape != x.shape or st[1].shape != y.shape or st[0].dtype != x.dtype:
-                self._graphs = {}
-                self._static = st = (x.detach().clone(), y.detach().clone())
-            else:
-                if st[0].data_ptr() != x.data_ptr():
-                    st[0].copy_(x)
-                if st[1].data_ptr() != y.data_ptr():
-                    st[1].copy_(y)
-            key = self._graph_key()
+            slot = self._slot_of(x, y)
+            if slot is None:
+                st = self._static
+                if st is None or st[0].shape != x.shape or st[1].shape != y.shape or st[0].dtype != x.dtype:
+                    self._graphs = {}
+                    self._static = st = (x.detach().clone(), y.detach().clone())
+                else:
+                    if st[0].data_ptr() != x.data_ptr():
+                        st[0].copy_(x)
+                    if st[1].data_ptr() != y.data_ptr():
+                        st[1].copy_(y)
+            key = (self._graph_key(), None if slot is None else (x.data_ptr(), y.data_ptr()))
             try:
-                g, loss, sums = self._graphs.get(key) or self._capture(key)
+                g, loss, sums = self._graphs.get(key) or self._capture(key, slot)
             except RuntimeError as e:  # capture refused on this system: keep stepping eagerly
                 import sys
                 print(f"[greedy_multimodal_learning_amd] hipGraph capture failed ({e}); eager steps from now on",
