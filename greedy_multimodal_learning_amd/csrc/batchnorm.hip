@@ -110,6 +110,9 @@ struct ReduceArgs {
     float* part;         // [nslice][nrc][SW][2] fp32 per-block partials
     float* coef_out;     // fwd, optional: the affine coefficients sc[C], sh[C] for the backward
     const float* fcoef;  // BWD_RELUX: the forward's sc[C], sh[C]
+    unsigned* gen;       // fused fwd: [nslice] generation words (coefficients published)
+    const uint4* res;    // fused fwd: residual
+    uint4* yout;         // fused fwd: output
 };
 
 // BWD_RELUX: the relu mask recomputed from x and the forward's affine coefficients
@@ -198,7 +201,9 @@ __device__ __forceinline__ FinOps fin_load(const ReduceArgs& a, int c) {
     return f;
 }
 
-template <int MODE>
+// SC1: the coefficients are published with write-through stores (read by the other
+// blocks of the same launch in the fused forward, k_bn_fwd_fused)
+template <int MODE, bool SC1 = false>
 __device__ __forceinline__ void finalize(const ReduceArgs& a, int c, double S1, double S2, double invM,
                                          const FinOps& f) {
     const int C = a.C;
@@ -211,6 +216,10 @@ __device__ __forceinline__ void finalize(const ReduceArgs& a, int c, double S1, 
         const double sc = g * invstd;
         a.coef[c] = (float)sc;
         a.coef[C + c] = (float)((double)f.b - mean * sc);
+        if (SC1) {
+            st_sc1(&a.coef[c], a.coef[c]);
+            st_sc1(&a.coef[C + c], a.coef[C + c]);
+        }
         if (a.coef_out) {
             a.coef_out[c] = a.coef[c];
             a.coef_out[C + c] = a.coef[C + c];
@@ -261,6 +270,9 @@ __device__ __forceinline__ bool ticket(unsigned* ctr, unsigned n, float* flag) {
     __syncthreads();
     return *flag != 0.f;
 }
+
+template <int MODE, bool SC1 = false>
+__device__ __forceinline__ void combine_finalize(const ReduceArgs& a, int cs, float* red, const FinOps& fo);
 
 // One launch: partial sums per (row chunk, channel slice) + one ticketed combine
 // per slice + per-channel finalize.
@@ -335,6 +347,16 @@ __global__ __launch_bounds__(kT) void k_bn_reduce(ReduceArgs a) {
     // the last block of the slice combines its nrc partial rows: lane group of L
     // threads per row (one float4 each), G = 256/L row groups, rows g, g+G, ...
     if (!ticket(a.counter + cs, (unsigned)a.nrc, &red[kRedF])) return;
+    combine_finalize<MODE>(a, cs, red, fo);
+}
+
+// The last block of a slice: combine the slice's nrc partial rows (lane group of L
+// threads per row, one float4 each, G = 256/L row groups, rows g, g+G, ...) in fp64
+// and finalize the slice's channels.
+template <int MODE, bool SC1>
+__device__ __forceinline__ void combine_finalize(const ReduceArgs& a, int cs, float* red, const FinOps& fo) {
+    const int t = threadIdx.x;
+    const int SW = a.SW, S2w = 2 * SW;
     if (MODE == FWD && a.nbt && cs == 0 && t == 0) *a.nbt += 1;
     const int L = S2w >> 2, G = kT / L;  // L in {4..32}, G in {8..64}
     const int lv = t % L, g = t / L;
@@ -365,7 +387,129 @@ __global__ __launch_bounds__(kT) void k_bn_reduce(ReduceArgs a) {
             S1 += rd[i * S2w + 2 * t];
             S2 += rd[i * S2w + 2 * t + 1];
         }
-        finalize<MODE>(a, cs * SW + t, S1, S2, 1.0 / (double)a.M, fo);
+        finalize<MODE, SC1>(a, cs * SW + t, S1, S2, 1.0 / (double)a.M, fo);
+    }
+}
+
+// Fused forward for maps whose grid is co-resident (fused_plan) and whose rows
+// fit NR 16-B vectors per thread: the block keeps its x strip in registers, takes
+// its ticket, the slice's last block finalizes and publishes the coefficients
+// (write-through stores, then a generation word), the other blocks spin on the
+// generation word (bounded) and every block applies y = relu?(x*sc + sh (+res)) from
+// its registers.  One launch and one read of x instead of two launches and two reads.
+constexpr unsigned kSpinLimit = 1u << 24;
+
+template <bool RES, bool RELU, int NR>
+__global__ __launch_bounds__(kT, NR == 16 ? 2 : NR == 8 ? 3 : 4) void k_bn_fwd_fused(ReduceArgs a) {  // NR 0: streaming
+    __shared__ float red[kRedF + 4];
+    const int t = threadIdx.x;
+    const int C = a.C, SW = a.SW;
+    const int rc = blockIdx.x, cs = blockIdx.y;
+    const int tpr = 1 << a.tpr_log;
+    const int cg = t & (tpr - 1);
+    const int r0 = t >> a.tpr_log;
+    const int rpp = kT >> a.tpr_log;
+    const long long vpr = C >> 3;
+    const int c0 = cs * SW + cg * 8;
+    const long long cv = c0 >> 3;
+    unsigned* gen = a.gen + cs;
+    unsigned g0 = 0;
+    if (t == 0) g0 = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+
+    const long long rbeg = (long long)rc * a.rpb;
+    long long rend = rbeg + a.rpb;
+    if (rend > a.M) rend = a.M;
+    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+    constexpr int NV = NR > 0 ? NR : 1;
+    uint4 v[NV];
+    float s1[8], s2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
+    if (NR > 0) {
+#pragma unroll
+        for (int u = 0; u < NV; ++u) {  // clamped loads (always valid), then a value select
+            const long long r = rbeg + r0 + (long long)u * rpp;
+            const uint4 w = a.x[(r < rend ? r : rend - 1) * vpr + cv];
+            v[u] = r < rend ? w : z;
+        }
+#pragma unroll
+        for (int u = 0; u < NV; ++u) accum_vals<FWD>(v[u], z, z, nullptr, s1, s2);
+    } else {  // streaming: 8 rows in flight per thread, x re-read (L2 / MALL) by the apply
+        long long r = rbeg + r0;
+        const long long st = (long long)rpp * vpr;
+        for (; r + 7 * rpp < rend; r += 8 * rpp) {
+            uint4 w[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) w[u] = a.x[r * vpr + cv + u * st];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) accum_vals<FWD>(w[u], z, z, nullptr, s1, s2);
+        }
+        for (; r < rend; r += rpp) accum_vals<FWD>(a.x[r * vpr + cv], z, z, nullptr, s1, s2);
+    }
+
+    const int S2w = 2 * SW;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        red[r0 * S2w + (cg * 8 + j) * 2] = s1[j];
+        red[r0 * S2w + (cg * 8 + j) * 2 + 1] = s2[j];
+    }
+    __syncthreads();
+    float* p1 = a.part + ((size_t)cs * a.nrc + rc) * S2w;
+    if (t < S2w) {
+        float acc = 0.f;
+        for (int i = 0; i < rpp; ++i) acc += red[i * S2w + t];
+        st_sc1(&p1[t], acc);
+    }
+    FinOps fo{};
+    if (t < SW) fo = fin_load<FWD>(a, cs * SW + t);
+    if (ticket(a.counter + cs, (unsigned)a.nrc, &red[kRedF])) {
+        combine_finalize<FWD, true>(a, cs, red, fo);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t == 0) __hip_atomic_store(gen, g0 + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        if (t == 0) {
+            unsigned it = 0;
+            while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g0 && ++it < kSpinLimit)
+                __builtin_amdgcn_s_sleep(2);
+        }
+        __syncthreads();
+    }
+    const auto rq = rsrc_of(a.coef);
+    const float4 sa = ld_sc1_f32x4(rq, (unsigned)c0 * 4u), sb = ld_sc1_f32x4(rq, (unsigned)(c0 + 4) * 4u);
+    const float4 ha = ld_sc1_f32x4(rq, (unsigned)(C + c0) * 4u), hb = ld_sc1_f32x4(rq, (unsigned)(C + c0 + 4) * 4u);
+    float sc[8], sh[8];
+    sc[0] = sa.x; sc[1] = sa.y; sc[2] = sa.z; sc[3] = sa.w; sc[4] = sb.x; sc[5] = sb.y; sc[6] = sb.z; sc[7] = sb.w;
+    sh[0] = ha.x; sh[1] = ha.y; sh[2] = ha.z; sh[3] = ha.w; sh[4] = hb.x; sh[5] = hb.y; sh[6] = hb.z; sh[7] = hb.w;
+    auto apply = [&](uint4 xv, long long i) {
+        float f[8], q[8];
+        unpack8(xv, f);
+        if (RES) unpack8(a.res[i], q);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float zz = fmaf(f[j], sc[j], sh[j]);
+            if (RES) zz += q[j];
+            f[j] = RELU ? fmaxf(zz, 0.f) : zz;
+        }
+        a.yout[i] = pack8(f);
+    };
+    if (NR > 0) {
+#pragma unroll
+        for (int u = 0; u < NV; ++u) {
+            const long long r = rbeg + r0 + (long long)u * rpp;
+            if (r < rend) apply(v[u], r * vpr + cv);
+        }
+    } else {
+        long long r = rbeg + r0;
+        const long long st = (long long)rpp * vpr;
+        for (; r + 3 * rpp < rend; r += 4 * rpp) {
+            uint4 w[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) w[u] = a.x[r * vpr + cv + u * st];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) apply(w[u], r * vpr + cv + u * st);
+        }
+        for (; r < rend; r += rpp) apply(a.x[r * vpr + cv], r * vpr + cv);
     }
 }
 
@@ -476,6 +620,61 @@ inline int apply_grid(long long nvec, int C) {
     return (int)g;
 }
 
+constexpr int kGenOff = 32;  // generation words: header words [32, 32 + nslice) (nslice <= 32)
+
+// Plan of the fused forward: rows per thread NR in {4, 8, 16} (the register-held
+// strip) and a grid that stays co-resident even when kFuseStreams such launches run
+// at once on different streams (the view trunks): grid <= CUs * occupancy(NR) /
+// kFuseStreams, occupancy being the kernel's launch bound (4, 3, 2 blocks per CU).
+// A grid that could exceed the resident capacity would let spinning blocks wait on
+// blocks that cannot be scheduled.  Returns NR (pl rewritten), -1 for the streaming
+// variant (x re-read by the apply phase; GM_BN_FUSED=1 disables it) or 0: use the two-kernel
+// path.  GM_BN_FUSED=0 disables it.
+constexpr int kFuseStreams = 4;
+
+inline int fused_plan(long long M, int C, Plan& pl) {
+    const char* e = getenv("GM_BN_FUSED");  // read per call: tests compare both paths
+    if (e && atoi(e) == 0) return 0;
+    static const int cus = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                     hipSuccess)
+            return 0;
+        return n;
+    }();
+    const Plan base = make_plan(M, C);
+    const int nrs[3] = {4, 8, 16}, occ[3] = {4, 3, 2};
+    for (int i = 0; i < 3; ++i) {
+        const long long budget = (long long)cus * occ[i] / kFuseStreams;
+        long long want = budget / base.nslice;
+        if (want < 1) continue;
+        long long rpb = (M + want - 1) / want;
+        rpb = (rpb + base.rpp - 1) / base.rpp * base.rpp;
+        if (rpb / base.rpp > nrs[i]) continue;
+        const long long nrc = (M + rpb - 1) / rpb;
+        if (nrc > base.nrc) continue;  // partials area sized by the base plan
+        pl = base;
+        pl.rpb = rpb;
+        pl.nrc = (int)nrc;
+        return nrs[i];
+    }
+    if (!e || atoi(e) >= 2) {  // streaming variant (occupancy 4): any map size
+        long long want = (long long)cus * 4 / kFuseStreams / base.nslice;
+        if (want >= 1) {
+            long long rpb = (M + want - 1) / want;
+            rpb = (rpb + base.rpp - 1) / base.rpp * base.rpp;
+            const long long nrc = (M + rpb - 1) / rpb;
+            if (nrc <= base.nrc) {
+                pl = base;
+                pl.rpb = rpb;
+                pl.nrc = (int)nrc;
+                return -1;
+            }
+        }
+    }
+    return 0;
+}
+
 int check_common(long long M, int C, const void* scratch, size_t bytes, const char* fn) {
     if (M <= 0 || C < 8 || C > kMaxC || (C & (C - 1)) != 0) {
         set_error("%s: need M > 0 and C a power of two in [8, %d] (M=%lld C=%d)", fn, kMaxC, M, C);
@@ -519,6 +718,28 @@ extern "C" int gm_bn_fwd_train_bf16(const gm_bn_fwd* p, void* scratch, size_t by
     a.coef = reinterpret_cast<float*>(s + pl.off_coef);
     a.part = reinterpret_cast<float*>(s + pl.off_p1);
     hipStream_t st = as_stream(stream);
+    Plan fp;
+    const int nr = fused_plan(p->M, p->C, fp);
+    if (nr) {
+        a.rpb = fp.rpb;
+        a.nrc = fp.nrc;
+        a.gen = reinterpret_cast<unsigned*>(s) + kGenOff;
+        a.res = static_cast<const uint4*>(p->residual);
+        a.yout = static_cast<uint4*>(p->y);
+        const dim3 g(fp.nrc, fp.nslice);
+        const bool res = p->residual != nullptr, relu = p->relu != 0;
+#define GM_BN_FUSED_LAUNCH(NR)                                                                        \
+    if (res && relu) hipLaunchKernelGGL((k_bn_fwd_fused<true, true, NR>), g, dim3(kT), 0, st, a);     \
+    else if (res) hipLaunchKernelGGL((k_bn_fwd_fused<true, false, NR>), g, dim3(kT), 0, st, a);       \
+    else if (relu) hipLaunchKernelGGL((k_bn_fwd_fused<false, true, NR>), g, dim3(kT), 0, st, a);      \
+    else hipLaunchKernelGGL((k_bn_fwd_fused<false, false, NR>), g, dim3(kT), 0, st, a);
+        if (nr < 0) { GM_BN_FUSED_LAUNCH(0) }
+        else if (nr == 4) { GM_BN_FUSED_LAUNCH(4) }
+        else if (nr == 8) { GM_BN_FUSED_LAUNCH(8) }
+        else { GM_BN_FUSED_LAUNCH(16) }
+#undef GM_BN_FUSED_LAUNCH
+        return check_launch("k_bn_fwd_fused");
+    }
     hipLaunchKernelGGL(k_bn_reduce<FWD>, dim3(pl.nrc, pl.nslice), dim3(kT), 0, st, a);
     if ((rc = check_launch("k_bn_reduce<fwd>"))) return rc;
     ApplyArgs b{};

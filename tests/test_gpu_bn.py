@@ -145,3 +145,31 @@ def test_bn_relu_mask_from_x_equals_y_mask(shape, monkeypatch):
         outs.append((y, xg.grad, m.weight.grad, m.bias.grad))
     for a, b2 in zip(*outs):
         assert torch.equal(a, b2)
+
+
+@pytest.mark.parametrize("mode", ["1", "2"])  # register-held strips only / + the streaming variant
+@pytest.mark.parametrize("shape", [(64, 64, 112, 112), (64, 64, 56, 56), (64, 128, 28, 28), (64, 256, 14, 14),
+                                   (64, 512, 7, 7), (3, 8, 5, 5), (7, 64, 9, 11)])
+@pytest.mark.parametrize("res,relu", [(False, False), (False, True), (True, True)])
+def test_bn_fused_forward_equals_two_kernel_forward(shape, res, relu, mode, monkeypatch):
+    """The single-launch forward (co-resident blocks, in-launch coefficient hand-off)
+    == the reduce + apply pair (its own row partition: fp32 partial sums in another
+    grouping, so y within one bf16 ulp, running stats to 1e-5), and bit-identical
+    to itself across launches."""
+    from greedy_multimodal_learning_amd.bn import GMBatchNorm2d
+    x, r, w, b, rm, rv, dy = _inputs(shape, 13 + shape[2], res)
+    outs = []
+    for fused in ("0", mode, mode):  # the fused path twice: its generation words advance
+        monkeypatch.setenv("GM_BN_FUSED", fused)
+        m = GMBatchNorm2d(shape[1]).cuda().to(memory_format=CL)
+        with torch.no_grad():
+            m.weight.copy_(w)
+            m.bias.copy_(b)
+        y = m(x.clone().requires_grad_(True), residual=r, relu=relu)
+        outs.append((y, m.running_mean.clone(), m.running_var.clone()))
+    for a, b2 in zip(outs[1], outs[2]):
+        assert torch.equal(a, b2)
+    y0, y1 = outs[0][0].float(), outs[1][0].float()
+    assert ((y0 - y1).abs() <= 2 ** -7 * y0.abs().clamp_min(1e-3)).all()
+    for a, b2 in zip(outs[0][1:], outs[1][1:]):
+        torch.testing.assert_close(b2, a, rtol=1e-5, atol=1e-6)
