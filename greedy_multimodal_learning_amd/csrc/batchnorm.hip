@@ -112,7 +112,8 @@ struct ReduceArgs {
     const float* fcoef;  // BWD_RELUX: the forward's sc[C], sh[C]
     unsigned* gen;       // fused fwd: [nslice] generation words (coefficients published)
     const uint4* res;    // fused fwd: residual
-    uint4* yout;         // fused fwd: output
+    uint4* yout;         // fused fwd: output / fused bwd: dx
+    uint4* dres_out;     // fused bwd: dres
 };
 
 // BWD_RELUX: the relu mask recomputed from x and the forward's affine coefficients
@@ -153,7 +154,8 @@ __device__ __forceinline__ void accum(const ReduceArgs& a, long long v, const fl
 
 // accum() on already loaded vectors (zero vectors contribute nothing in every mode)
 template <int MODE>
-__device__ __forceinline__ void accum_vals(uint4 ux, uint4 ud, uint4 uy, const float* mu, float* s1, float* s2) {
+__device__ __forceinline__ void accum_vals(uint4 ux, uint4 ud, uint4 uy, const float* mu, float* s1, float* s2,
+                                          const float* fsc = nullptr, const float* fsh = nullptr) {
     float xf[8];
     unpack8(ux, xf);
     if (MODE == FWD) {
@@ -170,6 +172,10 @@ __device__ __forceinline__ void accum_vals(uint4 ux, uint4 ud, uint4 uy, const f
             unpack8(uy, yf);
 #pragma unroll
             for (int j = 0; j < 8; ++j) d[j] = yf[j] > 0.f ? d[j] : 0.f;
+        }
+        if (MODE == BWD_RELUX) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) d[j] = fmaf(xf[j], fsc[j], fsh[j]) > 0.f ? d[j] : 0.f;
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -240,6 +246,11 @@ __device__ __forceinline__ void finalize(const ReduceArgs& a, int c, double S1, 
         a.coef[c] = (float)ca;
         a.coef[C + c] = (float)cb;
         a.coef[2 * C + c] = (float)(-ca * S1 * invM - cb * mean);
+        if (SC1) {
+            st_sc1(&a.coef[c], a.coef[c]);
+            st_sc1(&a.coef[C + c], a.coef[C + c]);
+            st_sc1(&a.coef[2 * C + c], a.coef[2 * C + c]);
+        }
         const float dg = (float)(S2 * is), db = (float)S1;
         if (a.accumulate) {
             a.dgamma[c] += dg;
@@ -513,6 +524,164 @@ __global__ __launch_bounds__(kT, NR == 16 ? 2 : NR == 8 ? 3 : 4) void k_bn_fwd_f
     }
 }
 
+// Fused backward, same scheme as k_bn_fwd_fused: the block holds its x / dy (/ y)
+// strip in registers (NR 4 or 8) or re-reads it (NR 0), the slice's last block
+// publishes (a, b, c) and every block writes dx = a*dz + b*x + c (and dres = dz).
+template <int MODE, bool DRES, int NR>
+__global__ __launch_bounds__(kT, NR == 8 ? 2 : 3) void k_bn_bwd_fused(ReduceArgs a) {
+    __shared__ float red[kRedF + 4];
+    const int t = threadIdx.x;
+    const int C = a.C, SW = a.SW;
+    const int rc = blockIdx.x, cs = blockIdx.y;
+    const int tpr = 1 << a.tpr_log;
+    const int cg = t & (tpr - 1);
+    const int r0 = t >> a.tpr_log;
+    const int rpp = kT >> a.tpr_log;
+    const long long vpr = C >> 3;
+    const int c0 = cs * SW + cg * 8;
+    const long long cv = c0 >> 3;
+    unsigned* gen = a.gen + cs;
+    unsigned g0 = 0;
+    if (t == 0) g0 = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    float mu[8], fsc[8], fsh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        mu[j] = a.save_mean[c0 + j];
+        if (MODE == BWD_RELUX) {
+            fsc[j] = a.fcoef[c0 + j];
+            fsh[j] = a.fcoef[C + c0 + j];
+        }
+    }
+    const long long rbeg = (long long)rc * a.rpb;
+    long long rend = rbeg + a.rpb;
+    if (rend > a.M) rend = a.M;
+    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+    constexpr int NV = NR > 0 ? NR : 1;
+    constexpr int NY = MODE == BWD_RELU ? NV : 1;
+    constexpr int US = MODE == BWD_RELU ? 2 : 4;  // streaming rows in flight (register budget)
+    uint4 vx[NV], vd[NV], vy[NY];
+    float s1[8], s2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
+    if (NR > 0) {
+#pragma unroll
+        for (int u = 0; u < NV; ++u) {  // clamped loads, then value selects (zero rows add nothing)
+            const long long r = rbeg + r0 + (long long)u * rpp;
+            const long long i = (r < rend ? r : rend - 1) * vpr + cv;
+            const uint4 wx = a.x[i], wd = a.dy[i];
+            vx[u] = r < rend ? wx : z;
+            vd[u] = r < rend ? wd : z;
+            if (MODE == BWD_RELU) vy[u] = a.y[i];
+        }
+#pragma unroll
+        for (int u = 0; u < NV; ++u)
+            accum_vals<MODE>(vx[u], vd[u], MODE == BWD_RELU ? vy[u < NY ? u : 0] : z, mu, s1, s2, fsc, fsh);
+    } else {
+        long long r = rbeg + r0;
+        const long long st = (long long)rpp * vpr;
+        for (; r + (US - 1) * rpp < rend; r += US * rpp) {
+            uint4 wx[US], wd[US], wy[US];
+#pragma unroll
+            for (int u = 0; u < US; ++u) {
+                const long long i = r * vpr + cv + u * st;
+                wx[u] = a.x[i];
+                wd[u] = a.dy[i];
+                if (MODE == BWD_RELU) wy[u] = a.y[i];
+            }
+#pragma unroll
+            for (int u = 0; u < US; ++u) accum_vals<MODE>(wx[u], wd[u], MODE == BWD_RELU ? wy[u] : z, mu, s1, s2, fsc, fsh);
+        }
+        for (; r < rend; r += rpp) {
+            const long long i = r * vpr + cv;
+            accum_vals<MODE>(a.x[i], a.dy[i], MODE == BWD_RELU ? a.y[i] : z, mu, s1, s2, fsc, fsh);
+        }
+    }
+
+    const int S2w = 2 * SW;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        red[r0 * S2w + (cg * 8 + j) * 2] = s1[j];
+        red[r0 * S2w + (cg * 8 + j) * 2 + 1] = s2[j];
+    }
+    __syncthreads();
+    float* p1 = a.part + ((size_t)cs * a.nrc + rc) * S2w;
+    if (t < S2w) {
+        float acc = 0.f;
+        for (int i = 0; i < rpp; ++i) acc += red[i * S2w + t];
+        st_sc1(&p1[t], acc);
+    }
+    FinOps fo{};
+    if (t < SW) fo = fin_load<MODE>(a, cs * SW + t);
+    if (ticket(a.counter + cs, (unsigned)a.nrc, &red[kRedF])) {
+        combine_finalize<MODE, true>(a, cs, red, fo);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t == 0) __hip_atomic_store(gen, g0 + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        if (t == 0) {
+            unsigned it = 0;
+            while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g0 && ++it < kSpinLimit)
+                __builtin_amdgcn_s_sleep(2);
+        }
+        __syncthreads();
+    }
+    const auto rq = rsrc_of(a.coef);
+    float ca[8], cb[8], cc[8];
+    auto ld8 = [&](int off, float* o) {
+        const float4 p = ld_sc1_f32x4(rq, (unsigned)(off + c0) * 4u), q = ld_sc1_f32x4(rq, (unsigned)(off + c0 + 4) * 4u);
+        o[0] = p.x; o[1] = p.y; o[2] = p.z; o[3] = p.w; o[4] = q.x; o[5] = q.y; o[6] = q.z; o[7] = q.w;
+    };
+    ld8(0, ca);
+    ld8(C, cb);
+    ld8(2 * C, cc);
+    auto out = [&](uint4 ux, uint4 ud, uint4 uy, long long i) {
+        float d[8], xf[8];
+        unpack8(ud, d);
+        unpack8(ux, xf);
+        if (MODE == BWD_RELU) {
+            float yf[8];
+            unpack8(uy, yf);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) d[j] = yf[j] > 0.f ? d[j] : 0.f;
+        }
+        if (MODE == BWD_RELUX) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) d[j] = fmaf(xf[j], fsc[j], fsh[j]) > 0.f ? d[j] : 0.f;
+        }
+        if (DRES) a.dres_out[i] = pack8(d);
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = fmaf(ca[j], d[j], fmaf(cb[j], xf[j], cc[j]));
+        a.yout[i] = pack8(o);
+    };
+    if (NR > 0) {
+#pragma unroll
+        for (int u = 0; u < NV; ++u) {
+            const long long r = rbeg + r0 + (long long)u * rpp;
+            if (r < rend) out(vx[u], vd[u], MODE == BWD_RELU ? vy[u < NY ? u : 0] : z, r * vpr + cv);
+        }
+    } else {
+        long long r = rbeg + r0;
+        const long long st = (long long)rpp * vpr;
+        for (; r + (US - 1) * rpp < rend; r += US * rpp) {
+            uint4 wx[US], wd[US], wy[US];
+#pragma unroll
+            for (int u = 0; u < US; ++u) {
+                const long long i = r * vpr + cv + u * st;
+                wx[u] = a.x[i];
+                wd[u] = a.dy[i];
+                if (MODE == BWD_RELU) wy[u] = a.y[i];
+            }
+#pragma unroll
+            for (int u = 0; u < US; ++u) out(wx[u], wd[u], MODE == BWD_RELU ? wy[u] : z, r * vpr + cv + u * st);
+        }
+        for (; r < rend; r += rpp) {
+            const long long i = r * vpr + cv;
+            out(a.x[i], a.dy[i], MODE == BWD_RELU ? a.y[i] : z, i);
+        }
+    }
+}
+
 struct ApplyArgs {
     long long nvec;      // M * C / 8
     int tpr_log;
@@ -632,7 +801,7 @@ constexpr int kGenOff = 32;  // generation words: header words [32, 32 + nslice)
 // path.  GM_BN_FUSED=0 disables it.
 constexpr int kFuseStreams = 4;
 
-inline int fused_plan(long long M, int C, Plan& pl) {
+inline int fused_plan(long long M, int C, Plan& pl, bool bwd = false) {
     const char* e = getenv("GM_BN_FUSED");  // read per call: tests compare both paths
     if (e && atoi(e) == 0) return 0;
     static const int cus = [] {
@@ -643,8 +812,11 @@ inline int fused_plan(long long M, int C, Plan& pl) {
         return n;
     }();
     const Plan base = make_plan(M, C);
-    const int nrs[3] = {4, 8, 16}, occ[3] = {4, 3, 2};
+    // launch bounds: fwd NR 4/8/16 -> 4/3/2 blocks per CU, streaming 4; bwd NR 4/8 -> 3/2, streaming 3
+    const int nrs[3] = {4, 8, 16}, occ_f[3] = {4, 3, 2}, occ_b[3] = {3, 2, 0};
+    const int* occ = bwd ? occ_b : occ_f;
     for (int i = 0; i < 3; ++i) {
+        if (!occ[i]) continue;
         const long long budget = (long long)cus * occ[i] / kFuseStreams;
         long long want = budget / base.nslice;
         if (want < 1) continue;
@@ -659,7 +831,7 @@ inline int fused_plan(long long M, int C, Plan& pl) {
         return nrs[i];
     }
     if (!e || atoi(e) >= 2) {  // streaming variant (occupancy 4): any map size
-        long long want = (long long)cus * 4 / kFuseStreams / base.nslice;
+        long long want = (long long)cus * (bwd ? 3 : 4) / kFuseStreams / base.nslice;
         if (want >= 1) {
             long long rpb = (M + want - 1) / want;
             rpb = (rpb + base.rpp - 1) / base.rpp * base.rpp;
@@ -807,6 +979,26 @@ extern "C" int gm_bn_bwd_bf16(const gm_bn_bwd* p, void* scratch, size_t bytes, v
     a.coef = reinterpret_cast<float*>(s + pl.off_coef);
     a.part = reinterpret_cast<float*>(s + pl.off_p1);
     hipStream_t st = as_stream(stream);
+    Plan fp;
+    const int nr = (!p->dres || p->relu) ? fused_plan(p->M, p->C, fp, true) : 0;
+    if (nr) {
+        a.rpb = fp.rpb;
+        a.nrc = fp.nrc;
+        a.gen = reinterpret_cast<unsigned*>(s) + kGenOff;
+        a.yout = static_cast<uint4*>(p->dx);
+        a.dres_out = static_cast<uint4*>(p->dres);
+        const dim3 g(fp.nrc, fp.nslice);
+#define GM_BN_BWD_FUSED_LAUNCH(NR)                                                                           \
+    if (maskx) hipLaunchKernelGGL((k_bn_bwd_fused<BWD_RELUX, false, NR>), g, dim3(kT), 0, st, a);            \
+    else if (p->relu && p->dres) hipLaunchKernelGGL((k_bn_bwd_fused<BWD_RELU, true, NR>), g, dim3(kT), 0, st, a); \
+    else if (p->relu) hipLaunchKernelGGL((k_bn_bwd_fused<BWD_RELU, false, NR>), g, dim3(kT), 0, st, a);    \
+    else hipLaunchKernelGGL((k_bn_bwd_fused<BWD, false, NR>), g, dim3(kT), 0, st, a);
+        if (nr < 0) { GM_BN_BWD_FUSED_LAUNCH(0) }
+        else if (nr == 4) { GM_BN_BWD_FUSED_LAUNCH(4) }
+        else { GM_BN_BWD_FUSED_LAUNCH(8) }
+#undef GM_BN_BWD_FUSED_LAUNCH
+        return check_launch("k_bn_bwd_fused");
+    }
     if (maskx) hipLaunchKernelGGL(k_bn_reduce<BWD_RELUX>, dim3(pl.nrc, pl.nslice), dim3(kT), 0, st, a);
     else if (p->relu) hipLaunchKernelGGL(k_bn_reduce<BWD_RELU>, dim3(pl.nrc, pl.nslice), dim3(kT), 0, st, a);
     else hipLaunchKernelGGL(k_bn_reduce<BWD>, dim3(pl.nrc, pl.nslice), dim3(kT), 0, st, a);

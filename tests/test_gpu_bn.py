@@ -173,3 +173,40 @@ def test_bn_fused_forward_equals_two_kernel_forward(shape, res, relu, mode, monk
     assert ((y0 - y1).abs() <= 2 ** -7 * y0.abs().clamp_min(1e-3)).all()
     for a, b2 in zip(outs[0][1:], outs[1][1:]):
         torch.testing.assert_close(b2, a, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("mode", ["1", "2"])
+@pytest.mark.parametrize("shape", [(64, 64, 112, 112), (64, 64, 56, 56), (64, 128, 28, 28), (64, 256, 14, 14),
+                                   (64, 512, 7, 7), (3, 8, 5, 5), (7, 64, 9, 11)])
+@pytest.mark.parametrize("res,relu,maskx", [(False, False, True), (False, True, True), (False, True, False),
+                                            (True, True, True)])
+def test_bn_fused_backward_equals_two_kernel_backward(shape, res, relu, maskx, mode, monkeypatch):
+    """The single-launch backward == the reduce + apply_bwd pair (own row partition:
+    dgamma/dbeta to 1e-5, dx/dres within one bf16 ulp of the larger magnitude) and
+    bit-identical to itself across launches."""
+    from greedy_multimodal_learning_amd import bn as B
+    monkeypatch.setattr(B, "MASK_FROM_X", maskx)
+    x, r, w, b, rm, rv, dy = _inputs(shape, 17 + shape[3], res)
+    outs = []
+    for fused in ("0", mode, mode):
+        monkeypatch.setenv("GM_BN_FUSED", "0")  # same forward for all three
+        m = B.GMBatchNorm2d(shape[1]).cuda().to(memory_format=CL)
+        with torch.no_grad():
+            m.weight.copy_(w)
+            m.bias.copy_(b)
+        xg = x.clone().requires_grad_(True)
+        rg = r.clone().requires_grad_(True) if res else None
+        y = m(xg, residual=rg, relu=relu)
+        monkeypatch.setenv("GM_BN_FUSED", fused)
+        y.backward(dy)
+        outs.append((xg.grad, rg.grad if res else None, m.weight.grad, m.bias.grad))
+    for a, b2 in zip(outs[1], outs[2]):
+        assert (a is None and b2 is None) or torch.equal(a, b2)
+    for k in (0, 1):
+        if outs[0][k] is None:
+            continue
+        a, b2 = outs[0][k].float(), outs[1][k].float()
+        tol = 2 ** -7 * torch.maximum(a.abs(), b2.abs()) + 1e-3 * a.abs().max()
+        assert ((a - b2).abs() <= tol).all()
+    for k in (2, 3):
+        torch.testing.assert_close(outs[1][k], outs[0][k], rtol=1e-4, atol=1e-4 * outs[0][k].abs().max().item())
