@@ -799,8 +799,6 @@ constexpr int kGenOff = 32;  // generation words: header words [32, 32 + nslice)
 // blocks that cannot be scheduled.  Returns NR (pl rewritten), -1 for the streaming
 // variant (x re-read by the apply phase; GM_BN_FUSED=1 disables it) or 0: use the two-kernel
 // path.  GM_BN_FUSED=0 disables it.
-constexpr int kFuseStreams = 4;
-
 inline int fused_plan(long long M, int C, Plan& pl, bool bwd = false) {
     const char* e = getenv("GM_BN_FUSED");  // read per call: tests compare both paths
     if (e && atoi(e) == 0) return 0;
@@ -811,6 +809,8 @@ inline int fused_plan(long long M, int C, Plan& pl, bool bwd = false) {
             return 0;
         return n;
     }();
+    const char* fs = getenv("GM_BN_FUSE_STREAMS");
+    const int kFuseStreams = fs ? atoi(fs) : 4;
     const Plan base = make_plan(M, C);
     // launch bounds: fwd NR 4/8/16 -> 4/3/2 blocks per CU, streaming 4; bwd NR 4/8 -> 3/2, streaming 3
     const int nrs[3] = {4, 8, 16}, occ_f[3] = {4, 3, 2}, occ_b[3] = {3, 2, 0};
