@@ -210,3 +210,59 @@ EXPORTS.update({
     "gm_maxpool2d_fwd_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "gm_maxpool2d_bwd_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
 })
+
+
+class ConvF32(ctypes.Structure):
+    _fields_ = [("mode", c_int), ("d", ConvDesc), ("x", c_void_p), ("w", c_void_p), ("dy", c_void_p),
+                ("out", c_void_p), ("addend", c_void_p), ("accumulate", c_int), ("pad0", c_int)]
+
+
+GM_CONV_FWD, GM_CONV_DGRAD, GM_CONV_WGRAD = 0, 1, 2
+
+EXPORTS.update({
+    "gm_conv2d_f32_scratch": (c_size_t, [c_void_p]),
+    "gm_conv2d_f32": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
+    "gm_bn_fwd_train_f32": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
+    "gm_bn_fwd_infer_f32": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
+    "gm_bn_bwd_f32": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
+    "gm_maxpool2d_fwd_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "gm_maxpool2d_bwd_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+})
+
+GM_FAULT_BN_SPIN, GM_FAULT_SPLITK_SPIN = 1, 2
+
+EXPORTS.update({
+    "gm_device_faults": (c_int, [ctypes.POINTER(ctypes.c_uint), c_int]),
+    "gm_set_spin_limit": (c_int, [ctypes.c_uint]),
+    "gm_bn_set_concurrency": (c_int, [c_int]),
+    "gm_bn_set_fused_mode": (c_int, [c_int]),
+})
+
+
+_fault_reset_hooks = []
+
+
+def on_fault_reset(fn):
+    """Register fn() to run when check_device_faults() finds a fault (state repair)."""
+    _fault_reset_hooks.append(fn)
+    return fn
+
+
+def device_faults(clear=False):
+    """OR of the library's sticky device fault words (synchronises the device)."""
+    v = ctypes.c_uint(0)
+    check(load().gm_device_faults(ctypes.byref(v), int(clear)), "gm_device_faults")
+    return v.value
+
+
+def check_device_faults(clear=True):
+    """Raise if an in-launch hand-off (fused BatchNorm, split-K turnstile) timed out
+    since the last check: its outputs were poisoned with NaN instead of stale data."""
+    v = device_faults(clear)
+    if v:
+        for hook in _fault_reset_hooks:  # e.g. re-zero split-K turnstile words left mid-hand-off
+            hook()
+        what = [n for b, n in ((GM_FAULT_BN_SPIN, "fused BatchNorm coefficient hand-off"),
+                               (GM_FAULT_SPLITK_SPIN, "split-K convolution turnstile")) if v & b]
+        raise GreedyMMLError(f"device fault 0x{v:x}: {', '.join(what) or 'unknown'} timed out "
+                             "(grid not co-resident?); the affected outputs are NaN")

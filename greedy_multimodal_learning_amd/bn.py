@@ -7,11 +7,13 @@ state_dict) whose forward takes two optional fusions used by the ResNet blocks:
     bn(x, relu=True)              == relu(BatchNorm2d(x))
     bn(x, residual=r, relu=True)  == relu(BatchNorm2d(x) + r)
 
-For bf16 channels_last CUDA inputs in training mode it runs
-`gm_bn_fwd_train_bf16` / `gm_bn_bwd_bf16` (two kernels each way, batch
-statistics, running-stat and num_batches_tracked updates inside the kernel);
-in eval mode without autograd `gm_bn_fwd_infer_bf16`.  Other inputs (the fp32
-parity mode, CPU) use PyTorch's batch_norm.  Reference: torchvision ResNet
+For CUDA inputs in training mode it runs `gm_bn_fwd_train_*` / `gm_bn_bwd_*`
+(batch statistics, running-stat and num_batches_tracked updates inside the
+kernel); in eval mode without autograd `gm_bn_fwd_infer_*`.  bf16 inputs (the
+engine's trunk, autocast-bf16) take the bf16 kernels (single launch each way
+where the grid can be co-resident); fp32 inputs - the reference's own
+arithmetic - take the fp32 kernels, activations channels_last.  There is no
+PyTorch batch_norm path: CPU tensors raise.  Reference: torchvision ResNet
 BasicBlock/Bottleneck as used by src/model.py:53-56,65-106.
 """
 import ctypes
@@ -19,7 +21,6 @@ import os
 
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 from . import _lib as L
 from .gradsink import sink_done, sink_target
@@ -62,15 +63,20 @@ def _check_shape(x, C):
         raise ValueError(f"HIP batchnorm needs C a power of two in [8, 2048], got {C}")
 
 
+def _fn(lib, name, dtype):
+    return getattr(lib, name + ("_f32" if dtype == torch.float32 else "_bf16"))
+
+
 def bn_fwd_train(x, weight, bias, running_mean, running_var, nbt, momentum, eps, relu, residual, coef=None):
-    """coef: optional fp32 [2C] tensor receiving the affine coefficients (sc, sh)."""
+    """coef: optional fp32 [2C] tensor receiving the affine coefficients (sc, sh).
+    x bf16 or fp32 (channels_last); the residual is cast to x's dtype."""
     lib = L.load()
     N, C, H, W = x.shape
     _check_shape(x, C)
     M = N * H * W
     x = _nhwc(x)
     if residual is not None:
-        residual = _nhwc(residual.to(torch.bfloat16))
+        residual = _nhwc(residual.to(x.dtype))
     y = torch.empty_like(x, memory_format=CL)
     sm = torch.empty(C, device=x.device, dtype=torch.float32)
     si = torch.empty(C, device=x.device, dtype=torch.float32)
@@ -78,8 +84,8 @@ def bn_fwd_train(x, weight, bias, running_mean, running_var, nbt, momentum, eps,
     p = L.BnFwd(M, C, int(relu), x.data_ptr(), L.ptr(residual), y.data_ptr(), weight.data_ptr(),
                 bias.data_ptr(), L.ptr(running_mean), L.ptr(running_var), float(momentum), float(eps),
                 sm.data_ptr(), si.data_ptr(), L.ptr(nbt), L.ptr(coef))
-    L.check(lib.gm_bn_fwd_train_bf16(ctypes.byref(p), buf.data_ptr(), buf.numel(), L.stream_of(x.device)),
-            "gm_bn_fwd_train_bf16")
+    L.check(_fn(lib, "gm_bn_fwd_train", x.dtype)(ctypes.byref(p), buf.data_ptr(), buf.numel(),
+                                                 L.stream_of(x.device)), "gm_bn_fwd_train")
     return y, sm, si
 
 
@@ -90,13 +96,13 @@ def bn_fwd_infer(x, weight, bias, running_mean, running_var, eps, relu, residual
     M = N * H * W
     x = _nhwc(x)
     if residual is not None:
-        residual = _nhwc(residual.to(torch.bfloat16))
+        residual = _nhwc(residual.to(x.dtype))
     y = torch.empty_like(x, memory_format=CL)
     buf = _get_scratch(x.device, M, C)
     p = L.BnFwd(M, C, int(relu), x.data_ptr(), L.ptr(residual), y.data_ptr(), weight.data_ptr(),
                 bias.data_ptr(), running_mean.data_ptr(), running_var.data_ptr(), 0.0, float(eps), 0, 0, 0)
-    L.check(lib.gm_bn_fwd_infer_bf16(ctypes.byref(p), buf.data_ptr(), buf.numel(), L.stream_of(x.device)),
-            "gm_bn_fwd_infer_bf16")
+    L.check(_fn(lib, "gm_bn_fwd_infer", x.dtype)(ctypes.byref(p), buf.data_ptr(), buf.numel(),
+                                                 L.stream_of(x.device)), "gm_bn_fwd_infer")
     return y
 
 
@@ -106,23 +112,24 @@ def bn_bwd(dy, y, x, weight, sm, si, relu, want_dres, dgamma, dbeta, accumulate,
     lib = L.load()
     N, C, H, W = x.shape
     M = N * H * W
-    dy = _nhwc(dy.to(torch.bfloat16))
+    dy = _nhwc(dy.to(x.dtype))
     dx = torch.empty_like(x, memory_format=CL)
     dres = torch.empty_like(x, memory_format=CL) if want_dres else None
     buf = _get_scratch(x.device, M, C)
     p = L.BnBwd(M, C, int(relu), dy.data_ptr(), L.ptr(y) if relu else 0, x.data_ptr(), weight.data_ptr(),
                 sm.data_ptr(), si.data_ptr(), dx.data_ptr(), L.ptr(dres), dgamma.data_ptr(), dbeta.data_ptr(),
                 int(accumulate), 0, L.ptr(fwd_coef))
-    L.check(lib.gm_bn_bwd_bf16(ctypes.byref(p), buf.data_ptr(), buf.numel(), L.stream_of(x.device)),
-            "gm_bn_bwd_bf16")
+    L.check(_fn(lib, "gm_bn_bwd", x.dtype)(ctypes.byref(p), buf.data_ptr(), buf.numel(), L.stream_of(x.device)),
+            "gm_bn_bwd")
     return dx, dres
 
 
 class _BNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, momentum, eps, relu, join=None):
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, momentum, eps, relu, join=None,
+                dtype=torch.bfloat16):
         ctx.join = join
-        xb = _nhwc(x.to(torch.bfloat16))
+        xb = _nhwc(x.to(dtype))
         maskx = relu and residual is None and MASK_FROM_X
         coef = torch.empty(2 * xb.shape[1], device=xb.device, dtype=torch.float32) if maskx else None
         y, sm, si = bn_fwd_train(xb, weight.detach(), bias.detach(), running_mean, running_var, nbt, momentum,
@@ -164,15 +171,12 @@ class _BNFn(torch.autograd.Function):
         dx = dx if ctx.needs_input_grad[0] else None
         if dres is not None and ctx.join is not None:  # the residual's gradient joins the block input's
             dres = ctx.join.contribute(lambda add: dres if add is None else dres + add)
-        return dx, gw, gb, dres, None, None, None, None, None, None, None
+        return dx, gw, gb, dres, None, None, None, None, None, None, None, None
 
 
-def _use_hip(x):
-    if not x.is_cuda:
-        return False
-    if x.dtype == torch.bfloat16:
-        return True
-    return torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+def _use_bf16(x):
+    return x.dtype == torch.bfloat16 or (
+        torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16)
 
 
 class GMBatchNorm2d(nn.BatchNorm2d):
@@ -181,8 +185,15 @@ class GMBatchNorm2d(nn.BatchNorm2d):
     def forward(self, x, residual=None, relu=False, residual_join=None):
         """residual_join: gradsink.GradJoin of the residual tensor (see conv.GMConv2d)."""
         C = self.num_features
-        hip = (_use_hip(x) and self.affine and x.dim() == 4 and C >= 8 and C <= 2048 and not (C & (C - 1)))
-        if hip and self.training and self.track_running_stats and self.momentum is not None:
+        if not x.is_cuda:
+            raise L.GreedyMMLError("GMBatchNorm2d: the trunk runs on libgreedymml_hip.so only (got a CPU tensor)")
+        if not (self.affine and self.track_running_stats and x.dim() == 4 and 8 <= C <= 2048 and not (C & (C - 1))):
+            raise L.GreedyMMLError("GMBatchNorm2d: needs affine, tracked running stats, [N,C,H,W] with C a power "
+                                   f"of two in [8, 2048] (got C={C})")
+        dt = torch.bfloat16 if _use_bf16(x) else torch.float32
+        if self.training:
+            if self.momentum is None:
+                raise L.GreedyMMLError("GMBatchNorm2d: cumulative averaging (momentum=None) is not supported")
             join = None
             if (residual_join is not None and residual is not None and residual.requires_grad
                     and torch.is_grad_enabled()):
@@ -190,12 +201,8 @@ class GMBatchNorm2d(nn.BatchNorm2d):
                 join = residual_join
             with torch.autocast("cuda", enabled=False):
                 return _BNFn.apply(x, self.weight, self.bias, residual, self.running_mean, self.running_var,
-                                   self.num_batches_tracked, self.momentum, self.eps, bool(relu), join)
-        if (hip and not self.training and self.track_running_stats
-                and not (torch.is_grad_enabled() and (x.requires_grad or self.weight.requires_grad))):
-            return bn_fwd_infer(x.to(torch.bfloat16), self.weight, self.bias, self.running_mean, self.running_var,
-                                self.eps, bool(relu), residual)
-        y = super().forward(x)
-        if residual is not None:
-            y = y + residual
-        return F.relu(y) if relu else y
+                                   self.num_batches_tracked, self.momentum, self.eps, bool(relu), join, dt)
+        if torch.is_grad_enabled() and (x.requires_grad or self.weight.requires_grad):
+            raise L.GreedyMMLError("GMBatchNorm2d: eval-mode forward with autograd is not supported")
+        return bn_fwd_infer(x.to(dt), self.weight, self.bias, self.running_mean, self.running_var,
+                            self.eps, bool(relu), residual)

@@ -1,19 +1,25 @@
-"""ResNet trunk convolutions on the bf16 MFMA implicit-GEMM kernels.
+"""ResNet trunk convolutions on the hand-written MFMA implicit-GEMM kernels.
 
 `GMConv2d` is an `nn.Conv2d` (same parameters, names, init and state_dict) whose
-forward runs `gm_conv2d_fwd_bf16` and whose backward runs
-`gm_conv2d_dgrad_bf16` + `gm_conv2d_wgrad_bf16` whenever it sees a bf16 input on
-a HIP device (the engine's bf16 channels_last trunk, or autocast-bf16).  fp32
-inputs (the fp32 parity mode) go through PyTorch's convolution (MIOpen).
-Activations are channels_last (NHWC) bf16, weights are cast to bf16 KRSC per
-step, weight gradients come back in fp32 in the parameter's layout.
+forward and backward run on libgreedymml_hip.so for every HIP input:
+
+  * bf16 (the engine's channels_last trunk, or autocast-bf16): `gm_conv2d_fwd_bf16`
+    + `gm_conv2d_dgrad_bf16` + `gm_conv2d_wgrad_bf16` (v_mfma_f32_32x32x16_bf16);
+    activations channels_last bf16, weights cast to bf16 KRSC per step;
+  * fp32 (the reference's own arithmetic: src/framework.py:146-148 feeds fp32
+    tensors with no autocast): `gm_conv2d_f32` fwd / dgrad / wgrad on the exact-f32
+    MFMA (v_mfma_f32_32x32x2_f32), activations channels_last fp32, any channel
+    count (the RGB stem unpadded).
+
+Weight gradients come back in fp32 in the parameter's layout (or are written in
+place through the gradient sink).  There is no vendor-library path: a CPU tensor
+or an unsupported configuration raises.
 """
 import ctypes
 import os
 
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 from . import _lib as L
 from .gradsink import sink_done, sink_target
@@ -27,6 +33,16 @@ def _desc(N, H, W, C, K, R, S, stride, pad):
 
 def _nhwc(t):
     return t if t.is_contiguous(memory_format=CL) else t.contiguous(memory_format=CL)
+
+
+def _like_param(g, p):
+    """A weight gradient in the parameter's own strides (what AccumulateGrad and the
+    gate's flat norm pass expect), copying only when the element order differs."""
+    if g.stride() == p.stride():
+        return g
+    out = torch.empty_strided(p.shape, p.stride(), device=g.device, dtype=g.dtype)
+    out.copy_(g)
+    return out
 
 
 def _pad_c(x, c):
@@ -61,6 +77,14 @@ def _splitk(device, d, dgrad):
         buf = torch.zeros((need + (1 << 20) - 1) >> 20 << 20, device=device, dtype=torch.uint8)
         _splitk_ws[key] = buf
     return buf.data_ptr(), buf.numel()
+
+
+@L.on_fault_reset
+def _reset_splitk_ws():
+    """A timed-out turnstile can leave a flag word mid-sequence: zero every workspace."""
+    for buf in _splitk_ws.values():
+        buf.zero_()
+    torch.cuda.synchronize()
 
 
 def conv_fwd(x, w, stride, pad):
@@ -240,7 +264,7 @@ class _StemFn(torch.autograd.Function):
                 tgt[0].copy_(dw)
             sink_done(weight)
             return None, None, None
-        return None, dw.contiguous(memory_format=CL), None
+        return None, _like_param(dw, weight), None
 
 
 _prepped = {}  # weight data_ptr -> (wb, wt): bf16 copies made by an active WeightPrep
@@ -371,6 +395,7 @@ class _ConvFn(torch.autograd.Function):
                 if tgt is not None:
                     raise RuntimeError("GMConv2d: in-place gradient buffer must be channels_last")
                 dw = conv_wgrad(gy, xb, R, S, stride, pad, C0)
+                dw = _like_param(dw, weight)
         return dx, dw, None, None, None
 
 
@@ -380,6 +405,70 @@ def _use_hip(x):
     if x.dtype == torch.bfloat16:
         return True
     return torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+
+
+# ---- reference-precision (fp32) path ------------------------------------------------
+
+def conv_f32(mode, d, x=None, w=None, dy=None, out=None, addend=None, accumulate=False):
+    """One gm_conv2d_f32 call (mode L.GM_CONV_FWD / _DGRAD / _WGRAD) on channels_last
+    fp32 tensors; `out` must be preallocated in its NHWC / KRSC layout."""
+    lib = L.load()
+    p = L.ConvF32(mode, d, L.ptr(x), L.ptr(w), L.ptr(dy), L.ptr(out), L.ptr(addend), int(accumulate), 0)
+    need = lib.gm_conv2d_f32_scratch(ctypes.byref(p))
+    dev = out.device
+    scratch = torch.empty(max(need, 16), device=dev, dtype=torch.uint8) if need else None
+    L.check(lib.gm_conv2d_f32(ctypes.byref(p), L.ptr(scratch), need, L.stream_of(dev)), "gm_conv2d_f32")
+    return out
+
+
+def _f32_cl(t):
+    t = t if t.dtype == torch.float32 else t.float()
+    return _nhwc(t)
+
+
+class _ConvF32Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, stride, pad, join=None):
+        ctx.join = join
+        xc = _f32_cl(x)
+        wk = _f32_cl(weight.detach())  # KRSC (a no-op for the engine's channels_last parameters)
+        N, C, H, W = xc.shape
+        K, _, R, S = wk.shape
+        P, Q = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
+        y = torch.empty(N, K, P, Q, device=xc.device, dtype=torch.float32, memory_format=CL)
+        conv_f32(L.GM_CONV_FWD, _desc(N, H, W, C, K, R, S, stride, pad), x=xc, w=wk, out=y)
+        ctx.save_for_backward(xc, wk, weight)
+        ctx.meta = (stride, pad)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        xc, wk, weight = ctx.saved_tensors
+        stride, pad = ctx.meta
+        gy = _f32_cl(gy)
+        N, C, H, W = xc.shape
+        K, _, R, S = wk.shape
+        d = _desc(N, H, W, C, K, R, S, stride, pad)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            def dgrad(add):
+                out = torch.empty(N, C, H, W, device=gy.device, dtype=torch.float32, memory_format=CL)
+                if add is not None:
+                    add = _f32_cl(add)
+                return conv_f32(L.GM_CONV_DGRAD, d, w=wk, dy=gy, out=out, addend=add)
+            dx = ctx.join.contribute(dgrad) if ctx.join is not None else dgrad(None)
+        if ctx.needs_input_grad[1]:
+            tgt = sink_target(weight)
+            if tgt is not None:
+                if not (tgt[0].is_contiguous(memory_format=CL) and tgt[0].dtype == torch.float32):
+                    raise RuntimeError("GMConv2d: in-place gradient buffer must be fp32 channels_last")
+                conv_f32(L.GM_CONV_WGRAD, d, x=xc, dy=gy, out=tgt[0], accumulate=tgt[1])
+                sink_done(weight)
+            else:
+                dw = torch.empty(K, C, R, S, device=gy.device, dtype=torch.float32, memory_format=CL)
+                conv_f32(L.GM_CONV_WGRAD, d, x=xc, dy=gy, out=dw)
+                dw = _like_param(dw, weight)
+        return dx, dw, None, None, None
 
 
 class GMConv2d(nn.Conv2d):
@@ -401,13 +490,21 @@ class GMConv2d(nn.Conv2d):
     def forward(self, x, grad_join=None):
         """grad_join: a gradsink.GradJoin shared with the other consumers of x (the
         ResNet block input), so x's gradient is summed inside the dgrad epilogue."""
-        if _use_hip(x) and self._hip_ok():
-            with torch.autocast("cuda", enabled=False):
-                if self.uses_pair_stem() and not x.requires_grad:
-                    return _StemFn.apply(x, self.weight, self.padding[0])
-                if grad_join is not None and x.requires_grad and torch.is_grad_enabled():
-                    grad_join.register()
-                else:
-                    grad_join = None
-                return _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0], grad_join)
-        return F.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation, self.groups)
+        if not x.is_cuda:
+            raise L.GreedyMMLError("GMConv2d: the trunk runs on libgreedymml_hip.so only (got a CPU tensor)")
+        if not self._hip_ok():
+            raise L.GreedyMMLError("GMConv2d: only groups=1, no bias, square stride/padding, dilation 1, "
+                                   "zero padding (the ResNet trunk's convolutions)")
+        bf16 = _use_hip(x)
+        with torch.autocast("cuda", enabled=False):
+            if grad_join is not None and x.requires_grad and torch.is_grad_enabled():
+                grad_join.register()
+            else:
+                grad_join = None
+            if not bf16:
+                return _ConvF32Fn.apply(x, self.weight, self.stride[0], self.padding[0], grad_join)
+            if self.uses_pair_stem() and not x.requires_grad:
+                if grad_join is not None:  # never: the stem input needs no gradient
+                    raise RuntimeError("GMConv2d: pair stem with a gradient join")
+                return _StemFn.apply(x, self.weight, self.padding[0])
+            return _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0], grad_join)

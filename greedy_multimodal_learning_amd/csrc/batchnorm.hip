@@ -14,7 +14,12 @@
 //      dgamma = S2*invstd, dx = a*dz + b*x + c per channel.
 //   2. k_bn_apply_bwd: dx (and dres = dz for the residual branch).
 // Bytes per element (bf16): fwd 2 (stats) + 4..6 (apply); bwd 4..6 + 6..8.
+// The reduce + apply kernels are templated on the element type E: bf16 (the
+// performance trunk) or fp32 (the reference-precision trunk, gm_bn_*_f32); the
+// single-launch fused kernels are bf16 only.
 #include <cstdlib>
+#include <initializer_list>
+#include <type_traits>
 
 #include "gm_common.h"
 
@@ -92,9 +97,9 @@ struct ReduceArgs {
     int C, tpr_log, relu, accumulate;
     int SW, nrc;
     long long rpb;
-    const uint4* x;      // fwd: x; bwd: x
-    const uint4* dy;     // bwd
-    const uint4* y;      // bwd relu mask
+    const void* x;       // fwd: x; bwd: x   (E elements)
+    const void* dy;      // bwd
+    const void* y;       // bwd relu mask
     const float* gamma;
     const float* beta;
     float* rmean;
@@ -114,17 +119,43 @@ struct ReduceArgs {
     const uint4* res;    // fused fwd: residual
     uint4* yout;         // fused fwd: output / fused bwd: dx
     uint4* dres_out;     // fused bwd: dres
+    unsigned spin_limit; // fused: poll budget of the coefficient hand-off
 };
+
+// sticky fault word of this translation unit (gm_device_faults): a fused launch whose
+// coefficient hand-off timed out
+__device__ unsigned g_bn_fault = 0;
+
+// Wait (thread 0, bounded) until the slice's generation word moves past g0; on
+// timeout raise the fault bit and return false in EVERY thread of the block (the
+// caller then applies NaN coefficients instead of stale ones).
+__device__ __forceinline__ bool wait_generation(const unsigned* gen, unsigned g0, unsigned limit, float* flag) {
+    if (threadIdx.x == 0) {
+        unsigned it = 0;
+        bool ok = true;
+        while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g0) {
+            if (++it >= limit) {
+                ok = false;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (!ok) atomicOr(&g_bn_fault, GM_FAULT_BN_SPIN);
+        *flag = ok ? 1.f : 0.f;
+    }
+    __syncthreads();
+    return *flag != 0.f;
+}
 
 // BWD_RELUX: the relu mask recomputed from x and the forward's affine coefficients
 // (z = x*sc + sh > 0, the forward's own fp32 value) instead of read back from y
 enum { FWD = 0, BWD = 1, BWD_RELU = 2, BWD_RELUX = 3 };  // relu as a template arg: no per-load branch
 
-template <int MODE>
+template <int MODE, typename E>
 __device__ __forceinline__ void accum(const ReduceArgs& a, long long v, const float* mu, float* s1, float* s2,
                                       const float* fsc, const float* fsh) {
     float xf[8];
-    unpack8(a.x[v], xf);
+    V8<E>::ld(a.x, v, xf);
     if (MODE == FWD) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -133,10 +164,10 @@ __device__ __forceinline__ void accum(const ReduceArgs& a, long long v, const fl
         }
     } else {
         float d[8];
-        unpack8(a.dy[v], d);
+        V8<E>::ld(a.dy, v, d);
         if (MODE == BWD_RELU) {
             float yf[8];
-            unpack8(a.y[v], yf);
+            V8<E>::ld(a.y, v, yf);
 #pragma unroll
             for (int j = 0; j < 8; ++j) d[j] = yf[j] > 0.f ? d[j] : 0.f;
         }
@@ -287,7 +318,7 @@ __device__ __forceinline__ void combine_finalize(const ReduceArgs& a, int cs, fl
 
 // One launch: partial sums per (row chunk, channel slice) + one ticketed combine
 // per slice + per-channel finalize.
-template <int MODE>
+template <int MODE, typename E>
 __global__ __launch_bounds__(kT) void k_bn_reduce(ReduceArgs a) {
     __shared__ float red[kRedF + 4];  // the one LDS object: row-group partials, flag
     const int t = threadIdx.x;
@@ -326,17 +357,18 @@ __global__ __launch_bounds__(kT) void k_bn_reduce(ReduceArgs a) {
     for (; r + 7 * rpp < rend; r += 8 * rpp) {
         const long long v = r * vpr + cv;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) accum<MODE>(a, v + u * st, mu, s1, s2, fsc, fsh);
+        for (int u = 0; u < 8; ++u) accum<MODE, E>(a, v + u * st, mu, s1, s2, fsc, fsh);
     }
-    if (MODE == FWD && r < rend) {  // the tail as ONE predicated batch: all its loads in flight
+    if (MODE == FWD && std::is_same<E, uint16_t>::value && r < rend) {  // the tail as ONE predicated batch
+        const uint4* X = static_cast<const uint4*>(a.x);
         uint4 vx[8];
         const uint4 z = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
-        for (int u = 0; u < 8; ++u) vx[u] = a.x[(r + u * rpp < rend ? r + u * rpp : r) * vpr + cv];
+        for (int u = 0; u < 8; ++u) vx[u] = X[(r + u * rpp < rend ? r + u * rpp : r) * vpr + cv];
 #pragma unroll
         for (int u = 0; u < 8; ++u) accum_vals<MODE>(r + u * rpp < rend ? vx[u] : z, z, z, mu, s1, s2);
     } else {
-        for (; r < rend; r += rpp) accum<MODE>(a, r * vpr + cv, mu, s1, s2, fsc, fsh);
+        for (; r < rend; r += rpp) accum<MODE, E>(a, r * vpr + cv, mu, s1, s2, fsc, fsh);
     }
 
     // row-group combine in LDS: red[r0][SW][2]  (rpp * 2SW == 4096 floats)
@@ -408,7 +440,6 @@ __device__ __forceinline__ void combine_finalize(const ReduceArgs& a, int cs, fl
 // (write-through stores, then a generation word), the other blocks spin on the
 // generation word (bounded) and every block applies y = relu?(x*sc + sh (+res)) from
 // its registers.  One launch and one read of x instead of two launches and two reads.
-constexpr unsigned kSpinLimit = 1u << 24;
 
 template <bool RES, bool RELU, int NR>
 __global__ __launch_bounds__(kT, NR == 16 ? 2 : NR == 8 ? 3 : 4) void k_bn_fwd_fused(ReduceArgs a) {  // NR 0: streaming
@@ -426,6 +457,7 @@ __global__ __launch_bounds__(kT, NR == 16 ? 2 : NR == 8 ? 3 : 4) void k_bn_fwd_f
     unsigned* gen = a.gen + cs;
     unsigned g0 = 0;
     if (t == 0) g0 = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint4* X = static_cast<const uint4*>(a.x);
 
     const long long rbeg = (long long)rc * a.rpb;
     long long rend = rbeg + a.rpb;
@@ -440,7 +472,7 @@ __global__ __launch_bounds__(kT, NR == 16 ? 2 : NR == 8 ? 3 : 4) void k_bn_fwd_f
 #pragma unroll
         for (int u = 0; u < NV; ++u) {  // clamped loads (always valid), then a value select
             const long long r = rbeg + r0 + (long long)u * rpp;
-            const uint4 w = a.x[(r < rend ? r : rend - 1) * vpr + cv];
+            const uint4 w = X[(r < rend ? r : rend - 1) * vpr + cv];
             v[u] = r < rend ? w : z;
         }
 #pragma unroll
@@ -451,11 +483,11 @@ __global__ __launch_bounds__(kT, NR == 16 ? 2 : NR == 8 ? 3 : 4) void k_bn_fwd_f
         for (; r + 7 * rpp < rend; r += 8 * rpp) {
             uint4 w[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) w[u] = a.x[r * vpr + cv + u * st];
+            for (int u = 0; u < 8; ++u) w[u] = X[r * vpr + cv + u * st];
 #pragma unroll
             for (int u = 0; u < 8; ++u) accum_vals<FWD>(w[u], z, z, nullptr, s1, s2);
         }
-        for (; r < rend; r += rpp) accum_vals<FWD>(a.x[r * vpr + cv], z, z, nullptr, s1, s2);
+        for (; r < rend; r += rpp) accum_vals<FWD>(X[r * vpr + cv], z, z, nullptr, s1, s2);
     }
 
     const int S2w = 2 * SW;
@@ -473,18 +505,14 @@ __global__ __launch_bounds__(kT, NR == 16 ? 2 : NR == 8 ? 3 : 4) void k_bn_fwd_f
     }
     FinOps fo{};
     if (t < SW) fo = fin_load<FWD>(a, cs * SW + t);
+    bool fresh = true;
     if (ticket(a.counter + cs, (unsigned)a.nrc, &red[kRedF])) {
         combine_finalize<FWD, true>(a, cs, red, fo);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (t == 0) __hip_atomic_store(gen, g0 + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
-        if (t == 0) {
-            unsigned it = 0;
-            while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g0 && ++it < kSpinLimit)
-                __builtin_amdgcn_s_sleep(2);
-        }
-        __syncthreads();
+        fresh = wait_generation(gen, g0, a.spin_limit, &red[kRedF + 1]);
     }
     const auto rq = rsrc_of(a.coef);
     const float4 sa = ld_sc1_f32x4(rq, (unsigned)c0 * 4u), sb = ld_sc1_f32x4(rq, (unsigned)(c0 + 4) * 4u);
@@ -492,6 +520,10 @@ __global__ __launch_bounds__(kT, NR == 16 ? 2 : NR == 8 ? 3 : 4) void k_bn_fwd_f
     float sc[8], sh[8];
     sc[0] = sa.x; sc[1] = sa.y; sc[2] = sa.z; sc[3] = sa.w; sc[4] = sb.x; sc[5] = sb.y; sc[6] = sb.z; sc[7] = sb.w;
     sh[0] = ha.x; sh[1] = ha.y; sh[2] = ha.z; sh[3] = ha.w; sh[4] = hb.x; sh[5] = hb.y; sh[6] = hb.z; sh[7] = hb.w;
+    if (!fresh) {  // timed out: never apply stale coefficients (the fault word is set)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sc[j] = sh[j] = __builtin_nanf("");
+    }
     auto apply = [&](uint4 xv, long long i) {
         float f[8], q[8];
         unpack8(xv, f);
@@ -501,6 +533,7 @@ __global__ __launch_bounds__(kT, NR == 16 ? 2 : NR == 8 ? 3 : 4) void k_bn_fwd_f
             float zz = fmaf(f[j], sc[j], sh[j]);
             if (RES) zz += q[j];
             f[j] = RELU ? fmaxf(zz, 0.f) : zz;
+            if (!fresh) f[j] = __builtin_nanf("");  // poisoned (fmaxf would turn NaN into 0)
         }
         a.yout[i] = pack8(f);
     };
@@ -516,11 +549,11 @@ __global__ __launch_bounds__(kT, NR == 16 ? 2 : NR == 8 ? 3 : 4) void k_bn_fwd_f
         for (; r + 3 * rpp < rend; r += 4 * rpp) {
             uint4 w[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) w[u] = a.x[r * vpr + cv + u * st];
+            for (int u = 0; u < 4; ++u) w[u] = X[r * vpr + cv + u * st];
 #pragma unroll
             for (int u = 0; u < 4; ++u) apply(w[u], r * vpr + cv + u * st);
         }
-        for (; r < rend; r += rpp) apply(a.x[r * vpr + cv], r * vpr + cv);
+        for (; r < rend; r += rpp) apply(X[r * vpr + cv], r * vpr + cv);
     }
 }
 
@@ -543,6 +576,9 @@ __global__ __launch_bounds__(kT, NR == 8 ? 2 : 3) void k_bn_bwd_fused(ReduceArgs
     unsigned* gen = a.gen + cs;
     unsigned g0 = 0;
     if (t == 0) g0 = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint4* X = static_cast<const uint4*>(a.x);
+    const uint4* DY = static_cast<const uint4*>(a.dy);
+    const uint4* Y = static_cast<const uint4*>(a.y);
     float mu[8], fsc[8], fsh[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -568,10 +604,10 @@ __global__ __launch_bounds__(kT, NR == 8 ? 2 : 3) void k_bn_bwd_fused(ReduceArgs
         for (int u = 0; u < NV; ++u) {  // clamped loads, then value selects (zero rows add nothing)
             const long long r = rbeg + r0 + (long long)u * rpp;
             const long long i = (r < rend ? r : rend - 1) * vpr + cv;
-            const uint4 wx = a.x[i], wd = a.dy[i];
+            const uint4 wx = X[i], wd = DY[i];
             vx[u] = r < rend ? wx : z;
             vd[u] = r < rend ? wd : z;
-            if (MODE == BWD_RELU) vy[u] = a.y[i];
+            if (MODE == BWD_RELU) vy[u] = Y[i];
         }
 #pragma unroll
         for (int u = 0; u < NV; ++u)
@@ -584,16 +620,16 @@ __global__ __launch_bounds__(kT, NR == 8 ? 2 : 3) void k_bn_bwd_fused(ReduceArgs
 #pragma unroll
             for (int u = 0; u < US; ++u) {
                 const long long i = r * vpr + cv + u * st;
-                wx[u] = a.x[i];
-                wd[u] = a.dy[i];
-                if (MODE == BWD_RELU) wy[u] = a.y[i];
+                wx[u] = X[i];
+                wd[u] = DY[i];
+                if (MODE == BWD_RELU) wy[u] = Y[i];
             }
 #pragma unroll
             for (int u = 0; u < US; ++u) accum_vals<MODE>(wx[u], wd[u], MODE == BWD_RELU ? wy[u] : z, mu, s1, s2, fsc, fsh);
         }
         for (; r < rend; r += rpp) {
             const long long i = r * vpr + cv;
-            accum_vals<MODE>(a.x[i], a.dy[i], MODE == BWD_RELU ? a.y[i] : z, mu, s1, s2, fsc, fsh);
+            accum_vals<MODE>(X[i], DY[i], MODE == BWD_RELU ? Y[i] : z, mu, s1, s2, fsc, fsh);
         }
     }
 
@@ -612,18 +648,14 @@ __global__ __launch_bounds__(kT, NR == 8 ? 2 : 3) void k_bn_bwd_fused(ReduceArgs
     }
     FinOps fo{};
     if (t < SW) fo = fin_load<MODE>(a, cs * SW + t);
+    bool fresh = true;
     if (ticket(a.counter + cs, (unsigned)a.nrc, &red[kRedF])) {
         combine_finalize<MODE, true>(a, cs, red, fo);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (t == 0) __hip_atomic_store(gen, g0 + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
-        if (t == 0) {
-            unsigned it = 0;
-            while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g0 && ++it < kSpinLimit)
-                __builtin_amdgcn_s_sleep(2);
-        }
-        __syncthreads();
+        fresh = wait_generation(gen, g0, a.spin_limit, &red[kRedF + 1]);
     }
     const auto rq = rsrc_of(a.coef);
     float ca[8], cb[8], cc[8];
@@ -634,6 +666,10 @@ __global__ __launch_bounds__(kT, NR == 8 ? 2 : 3) void k_bn_bwd_fused(ReduceArgs
     ld8(0, ca);
     ld8(C, cb);
     ld8(2 * C, cc);
+    if (!fresh) {  // timed out: never apply stale coefficients (the fault word is set)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ca[j] = cb[j] = cc[j] = __builtin_nanf("");
+    }
     auto out = [&](uint4 ux, uint4 ud, uint4 uy, long long i) {
         float d[8], xf[8];
         unpack8(ud, d);
@@ -668,16 +704,16 @@ __global__ __launch_bounds__(kT, NR == 8 ? 2 : 3) void k_bn_bwd_fused(ReduceArgs
 #pragma unroll
             for (int u = 0; u < US; ++u) {
                 const long long i = r * vpr + cv + u * st;
-                wx[u] = a.x[i];
-                wd[u] = a.dy[i];
-                if (MODE == BWD_RELU) wy[u] = a.y[i];
+                wx[u] = X[i];
+                wd[u] = DY[i];
+                if (MODE == BWD_RELU) wy[u] = Y[i];
             }
 #pragma unroll
             for (int u = 0; u < US; ++u) out(wx[u], wd[u], MODE == BWD_RELU ? wy[u] : z, r * vpr + cv + u * st);
         }
         for (; r < rend; r += rpp) {
             const long long i = r * vpr + cv;
-            out(a.x[i], a.dy[i], MODE == BWD_RELU ? a.y[i] : z, i);
+            out(X[i], DY[i], MODE == BWD_RELU ? Y[i] : z, i);
         }
     }
 }
@@ -686,11 +722,11 @@ struct ApplyArgs {
     long long nvec;      // M * C / 8
     int tpr_log;
     int relu;
-    const uint4* x;
-    const uint4* res;    // fwd residual / bwd: y (relu mask)
-    const uint4* dy;     // bwd
-    uint4* out;          // fwd y / bwd dx
-    uint4* out2;         // bwd dres
+    const void* x;       // E elements
+    const void* res;     // fwd residual / bwd: y (relu mask)
+    const void* dy;      // bwd
+    void* out;           // fwd y / bwd dx
+    void* out2;          // bwd dres
     const float* coef;   // [4][C]
     int C;
     const float* fcoef;  // bwd MASKX: the forward's sc[C], sh[C]
@@ -702,7 +738,7 @@ __device__ __forceinline__ void load_coef(const float* p, int cg, float* c) {
     c[0] = a.x; c[1] = a.y; c[2] = a.z; c[3] = a.w; c[4] = b.x; c[5] = b.y; c[6] = b.z; c[7] = b.w;
 }
 
-template <bool RES, bool RELU>
+template <bool RES, bool RELU, typename E>
 __global__ __launch_bounds__(kT) void k_bn_apply(ApplyArgs a) {
     const long long stride = (long long)gridDim.x * kT;  // multiple of C/8
     long long v = (long long)blockIdx.x * kT + threadIdx.x;
@@ -712,16 +748,16 @@ __global__ __launch_bounds__(kT) void k_bn_apply(ApplyArgs a) {
     load_coef(a.coef + a.C, cg, sh);
     auto one = [&](long long i) {
         float f[8];
-        unpack8(a.x[i], f);
+        V8<E>::ld(a.x, i, f);
         float r[8];
-        if (RES) unpack8(a.res[i], r);
+        if (RES) V8<E>::ld(a.res, i, r);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             float z = fmaf(f[j], sc[j], sh[j]);
             if (RES) z += r[j];
             f[j] = RELU ? fmaxf(z, 0.f) : z;
         }
-        a.out[i] = pack8(f);
+        V8<E>::st(a.out, i, f);
     };
     for (; v + stride < a.nvec; v += 2 * stride) {
         one(v);
@@ -730,7 +766,7 @@ __global__ __launch_bounds__(kT) void k_bn_apply(ApplyArgs a) {
     if (v < a.nvec) one(v);
 }
 
-template <bool RELU, bool DRES, bool MASKX = false>
+template <bool RELU, bool DRES, bool MASKX, typename E>
 __global__ __launch_bounds__(kT) void k_bn_apply_bwd(ApplyArgs a) {
     const long long stride = (long long)gridDim.x * kT;
     long long v = (long long)blockIdx.x * kT + threadIdx.x;
@@ -745,22 +781,22 @@ __global__ __launch_bounds__(kT) void k_bn_apply_bwd(ApplyArgs a) {
     }
     auto one = [&](long long i) {
         float d[8], xf[8];
-        unpack8(a.dy[i], d);
-        unpack8(a.x[i], xf);
+        V8<E>::ld(a.dy, i, d);
+        V8<E>::ld(a.x, i, xf);
         if (RELU && MASKX) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) d[j] = fmaf(xf[j], fs[j], fh[j]) > 0.f ? d[j] : 0.f;
         } else if (RELU) {
             float yf[8];
-            unpack8(a.res[i], yf);
+            V8<E>::ld(a.res, i, yf);
 #pragma unroll
             for (int j = 0; j < 8; ++j) d[j] = yf[j] > 0.f ? d[j] : 0.f;
         }
-        if (DRES) a.out2[i] = pack8(d);
+        if (DRES) V8<E>::st(a.out2, i, d);
         float o[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = fmaf(ca[j], d[j], fmaf(cb[j], xf[j], cc[j]));
-        a.out[i] = pack8(o);
+        V8<E>::st(a.out, i, o);
     };
     for (; v + stride < a.nvec; v += 2 * stride) {
         one(v);
@@ -792,16 +828,60 @@ inline int apply_grid(long long nvec, int C) {
 constexpr int kGenOff = 32;  // generation words: header words [32, 32 + nslice) (nslice <= 32)
 
 // Plan of the fused forward: rows per thread NR in {4, 8, 16} (the register-held
-// strip) and a grid that stays co-resident even when kFuseStreams such launches run
-// at once on different streams (the view trunks): grid <= CUs * occupancy(NR) /
-// kFuseStreams, occupancy being the kernel's launch bound (4, 3, 2 blocks per CU).
-// A grid that could exceed the resident capacity would let spinning blocks wait on
-// blocks that cannot be scheduled.  Returns NR (pl rewritten), -1 for the streaming
-// variant (x re-read by the apply phase; GM_BN_FUSED=1 disables it) or 0: use the two-kernel
-// path.  GM_BN_FUSED=0 disables it.
-inline int fused_plan(long long M, int C, Plan& pl, bool bwd = false) {
-    const char* e = getenv("GM_BN_FUSED");  // read per call: tests compare both paths
-    if (e && atoi(e) == 0) return 0;
+// strip) and a grid that stays co-resident even when `concurrency` such launches run
+// at once on different streams (the view trunks): grid <= CUs * occupancy / concurrency,
+// the occupancy MEASURED for the kernel instantiations that can be launched
+// (hipOccupancyMaxActiveBlocksPerMultiprocessor, the minimum over their variants) and
+// the concurrency set by the caller (gm_bn_set_concurrency: the number of trunk streams
+// that run concurrently plus headroom; default 4, GM_BN_FUSE_STREAMS at load).  A grid
+// that could exceed the resident capacity would let spinning blocks wait on blocks that
+// cannot be scheduled (the spin is bounded and then faults loudly, see wait_generation).
+// Returns NR (pl rewritten), -1 for the streaming variant (x re-read by the apply phase;
+// GM_BN_FUSED=1 disables it) or 0: use the two-kernel path.  GM_BN_FUSED=0 disables it.
+int g_concurrency = [] {
+    const char* e = getenv("GM_BN_FUSE_STREAMS");
+    const int v = e ? atoi(e) : 4;
+    return v >= 1 ? v : 4;  // 0 / garbage: the default (never a division by zero)
+}();
+int g_fused_env = [] {
+    const char* e = getenv("GM_BN_FUSED");  // read once; 0 = two-kernel path, 1 = no streaming variant
+    return e ? atoi(e) : 2;
+}();
+
+template <typename K>
+int occ_min(std::initializer_list<K> ks) {
+    int best = 1 << 30;
+    for (K k : ks) {
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(k), kT, 0) != hipSuccess)
+            n = 0;
+        best = n < best ? n : best;
+    }
+    return best == (1 << 30) ? 0 : best;
+}
+
+struct Occ {
+    int fwd[4];  // NR 4, 8, 16, streaming
+    int bwd[3];  // NR 4, 8, streaming
+};
+
+const Occ& occupancy() {
+    static const Occ o = [] {
+        Occ r{};
+#define GM_F(NR) occ_min({k_bn_fwd_fused<true, true, NR>, k_bn_fwd_fused<true, false, NR>, \
+                          k_bn_fwd_fused<false, true, NR>, k_bn_fwd_fused<false, false, NR>})
+#define GM_B(NR) occ_min({k_bn_bwd_fused<BWD_RELUX, false, NR>, k_bn_bwd_fused<BWD_RELU, true, NR>, \
+                          k_bn_bwd_fused<BWD_RELU, false, NR>, k_bn_bwd_fused<BWD, false, NR>})
+        r.fwd[0] = GM_F(4); r.fwd[1] = GM_F(8); r.fwd[2] = GM_F(16); r.fwd[3] = GM_F(0);
+        r.bwd[0] = GM_B(4); r.bwd[1] = GM_B(8); r.bwd[2] = GM_B(0);
+#undef GM_F
+#undef GM_B
+        return r;
+    }();
+    return o;
+}
+
+int device_cus() {
     static const int cus = [] {
         int dev = 0, n = 0;
         if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
@@ -809,15 +889,20 @@ inline int fused_plan(long long M, int C, Plan& pl, bool bwd = false) {
             return 0;
         return n;
     }();
-    const char* fs = getenv("GM_BN_FUSE_STREAMS");
-    const int kFuseStreams = fs ? atoi(fs) : 4;
+    return cus;
+}
+
+inline int fused_plan(long long M, int C, Plan& pl, bool bwd = false) {
+    if (g_fused_env == 0) return 0;
+    const int cus = device_cus();
+    const int conc = g_concurrency;
     const Plan base = make_plan(M, C);
-    // launch bounds: fwd NR 4/8/16 -> 4/3/2 blocks per CU, streaming 4; bwd NR 4/8 -> 3/2, streaming 3
-    const int nrs[3] = {4, 8, 16}, occ_f[3] = {4, 3, 2}, occ_b[3] = {3, 2, 0};
-    const int* occ = bwd ? occ_b : occ_f;
+    const Occ& oc = occupancy();
+    const int nrs[3] = {4, 8, 16};
+    const int occ_reg[3] = {bwd ? oc.bwd[0] : oc.fwd[0], bwd ? oc.bwd[1] : oc.fwd[1], bwd ? 0 : oc.fwd[2]};
     for (int i = 0; i < 3; ++i) {
-        if (!occ[i]) continue;
-        const long long budget = (long long)cus * occ[i] / kFuseStreams;
+        if (occ_reg[i] <= 0) continue;
+        const long long budget = (long long)cus * occ_reg[i] / conc;
         long long want = budget / base.nslice;
         if (want < 1) continue;
         long long rpb = (M + want - 1) / want;
@@ -830,8 +915,9 @@ inline int fused_plan(long long M, int C, Plan& pl, bool bwd = false) {
         pl.nrc = (int)nrc;
         return nrs[i];
     }
-    if (!e || atoi(e) >= 2) {  // streaming variant (occupancy 4): any map size
-        long long want = (long long)cus * (bwd ? 3 : 4) / kFuseStreams / base.nslice;
+    if (g_fused_env >= 2) {  // streaming variant: any map size
+        const int occ_s = bwd ? oc.bwd[2] : oc.fwd[3];
+        long long want = (long long)cus * occ_s / conc / base.nslice;
         if (want >= 1) {
             long long rpb = (M + want - 1) / want;
             rpb = (rpb + base.rpp - 1) / base.rpp * base.rpp;
@@ -869,18 +955,20 @@ extern "C" size_t gm_bn_scratch(long long M, int C) {
     return scratch_bytes(M, C);
 }
 
-extern "C" int gm_bn_fwd_train_bf16(const gm_bn_fwd* p, void* scratch, size_t bytes, void* stream) {
-    GM_REQUIRE(p && p->x && p->y && p->gamma && p->beta && p->save_mean && p->save_invstd,
-               "gm_bn_fwd_train_bf16: null argument");
-    GM_REQUIRE(!p->running_mean == !p->running_var, "gm_bn_fwd_train_bf16: running_mean/var both or neither");
-    int rc = check_common(p->M, p->C, scratch, bytes, "gm_bn_fwd_train_bf16");
+namespace {
+
+template <typename E>
+int bn_fwd_train(const gm_bn_fwd* p, void* scratch, size_t bytes, void* stream, const char* fn) {
+    GM_REQUIRE(p && p->x && p->y && p->gamma && p->beta && p->save_mean && p->save_invstd, "%s: null argument", fn);
+    GM_REQUIRE(!p->running_mean == !p->running_var, "%s: running_mean/var both or neither", fn);
+    int rc = check_common(p->M, p->C, scratch, bytes, fn);
     if (rc) return rc;
     const Plan pl = make_plan(p->M, p->C);
     char* s = static_cast<char*>(scratch);
     ReduceArgs a{};
     a.M = p->M; a.C = p->C; a.tpr_log = pl.tpr_log; a.rpb = pl.rpb;
     a.SW = pl.SW; a.nrc = pl.nrc;
-    a.x = static_cast<const uint4*>(p->x);
+    a.x = p->x;
     a.gamma = p->gamma; a.beta = p->beta; a.rmean = p->running_mean; a.rvar = p->running_var;
     a.momentum = p->momentum; a.eps = p->eps;
     a.save_mean = p->save_mean; a.save_invstd = p->save_invstd;
@@ -891,11 +979,12 @@ extern "C" int gm_bn_fwd_train_bf16(const gm_bn_fwd* p, void* scratch, size_t by
     a.part = reinterpret_cast<float*>(s + pl.off_p1);
     hipStream_t st = as_stream(stream);
     Plan fp;
-    const int nr = fused_plan(p->M, p->C, fp);
+    const int nr = std::is_same<E, uint16_t>::value ? fused_plan(p->M, p->C, fp) : 0;
     if (nr) {
         a.rpb = fp.rpb;
         a.nrc = fp.nrc;
         a.gen = reinterpret_cast<unsigned*>(s) + kGenOff;
+        a.spin_limit = spin_limit();
         a.res = static_cast<const uint4*>(p->residual);
         a.yout = static_cast<uint4*>(p->y);
         const dim3 g(fp.nrc, fp.nslice);
@@ -912,27 +1001,28 @@ extern "C" int gm_bn_fwd_train_bf16(const gm_bn_fwd* p, void* scratch, size_t by
 #undef GM_BN_FUSED_LAUNCH
         return check_launch("k_bn_fwd_fused");
     }
-    hipLaunchKernelGGL(k_bn_reduce<FWD>, dim3(pl.nrc, pl.nslice), dim3(kT), 0, st, a);
+    hipLaunchKernelGGL((k_bn_reduce<FWD, E>), dim3(pl.nrc, pl.nslice), dim3(kT), 0, st, a);
     if ((rc = check_launch("k_bn_reduce<fwd>"))) return rc;
     ApplyArgs b{};
     b.nvec = p->M * (p->C / 8); b.tpr_log = ilog2(p->C / 8); b.C = p->C; b.relu = p->relu;
-    b.x = a.x; b.res = static_cast<const uint4*>(p->residual); b.out = static_cast<uint4*>(p->y);
+    b.x = p->x; b.res = p->residual; b.out = p->y;
     b.coef = a.coef;
     const int g = apply_grid(b.nvec, p->C);
     if (p->residual) {
-        if (p->relu) hipLaunchKernelGGL((k_bn_apply<true, true>), dim3(g), dim3(kT), 0, st, b);
-        else hipLaunchKernelGGL((k_bn_apply<true, false>), dim3(g), dim3(kT), 0, st, b);
+        if (p->relu) hipLaunchKernelGGL((k_bn_apply<true, true, E>), dim3(g), dim3(kT), 0, st, b);
+        else hipLaunchKernelGGL((k_bn_apply<true, false, E>), dim3(g), dim3(kT), 0, st, b);
     } else {
-        if (p->relu) hipLaunchKernelGGL((k_bn_apply<false, true>), dim3(g), dim3(kT), 0, st, b);
-        else hipLaunchKernelGGL((k_bn_apply<false, false>), dim3(g), dim3(kT), 0, st, b);
+        if (p->relu) hipLaunchKernelGGL((k_bn_apply<false, true, E>), dim3(g), dim3(kT), 0, st, b);
+        else hipLaunchKernelGGL((k_bn_apply<false, false, E>), dim3(g), dim3(kT), 0, st, b);
     }
     return check_launch("k_bn_apply");
 }
 
-extern "C" int gm_bn_fwd_infer_bf16(const gm_bn_fwd* p, void* scratch, size_t bytes, void* stream) {
-    GM_REQUIRE(p && p->x && p->y && p->gamma && p->beta && p->running_mean && p->running_var,
-               "gm_bn_fwd_infer_bf16: null argument");
-    int rc = check_common(p->M, p->C, scratch, bytes, "gm_bn_fwd_infer_bf16");
+template <typename E>
+int bn_fwd_infer(const gm_bn_fwd* p, void* scratch, size_t bytes, void* stream, const char* fn) {
+    GM_REQUIRE(p && p->x && p->y && p->gamma && p->beta && p->running_mean && p->running_var, "%s: null argument",
+               fn);
+    int rc = check_common(p->M, p->C, scratch, bytes, fn);
     if (rc) return rc;
     char* s = static_cast<char*>(scratch);
     float* coef = reinterpret_cast<float*>(s + make_plan(p->M, p->C).off_coef);
@@ -942,26 +1032,26 @@ extern "C" int gm_bn_fwd_infer_bf16(const gm_bn_fwd* p, void* scratch, size_t by
     if ((rc = check_launch("k_bn_infer_coef"))) return rc;
     ApplyArgs b{};
     b.nvec = p->M * (p->C / 8); b.tpr_log = ilog2(p->C / 8); b.C = p->C; b.relu = p->relu;
-    b.x = static_cast<const uint4*>(p->x); b.res = static_cast<const uint4*>(p->residual);
-    b.out = static_cast<uint4*>(p->y); b.coef = coef;
+    b.x = p->x; b.res = p->residual; b.out = p->y; b.coef = coef;
     const int g = apply_grid(b.nvec, p->C);
     if (p->residual) {
-        if (p->relu) hipLaunchKernelGGL((k_bn_apply<true, true>), dim3(g), dim3(kT), 0, st, b);
-        else hipLaunchKernelGGL((k_bn_apply<true, false>), dim3(g), dim3(kT), 0, st, b);
+        if (p->relu) hipLaunchKernelGGL((k_bn_apply<true, true, E>), dim3(g), dim3(kT), 0, st, b);
+        else hipLaunchKernelGGL((k_bn_apply<true, false, E>), dim3(g), dim3(kT), 0, st, b);
     } else {
-        if (p->relu) hipLaunchKernelGGL((k_bn_apply<false, true>), dim3(g), dim3(kT), 0, st, b);
-        else hipLaunchKernelGGL((k_bn_apply<false, false>), dim3(g), dim3(kT), 0, st, b);
+        if (p->relu) hipLaunchKernelGGL((k_bn_apply<false, true, E>), dim3(g), dim3(kT), 0, st, b);
+        else hipLaunchKernelGGL((k_bn_apply<false, false, E>), dim3(g), dim3(kT), 0, st, b);
     }
     return check_launch("k_bn_apply");
 }
 
-extern "C" int gm_bn_bwd_bf16(const gm_bn_bwd* p, void* scratch, size_t bytes, void* stream) {
+template <typename E>
+int bn_bwd(const gm_bn_bwd* p, void* scratch, size_t bytes, void* stream, const char* fn) {
     GM_REQUIRE(p && p->dy && p->x && p->gamma && p->save_mean && p->save_invstd && p->dx && p->dgamma && p->dbeta,
-               "gm_bn_bwd_bf16: null argument");
+               "%s: null argument", fn);
     GM_REQUIRE(!p->relu || p->y || (p->fwd_coef && !p->dres),
-               "gm_bn_bwd_bf16: relu needs the forward output y (or fwd_coef, without a residual)");
+               "%s: relu needs the forward output y (or fwd_coef, without a residual)", fn);
     const bool maskx = p->relu && !p->y;
-    int rc = check_common(p->M, p->C, scratch, bytes, "gm_bn_bwd_bf16");
+    int rc = check_common(p->M, p->C, scratch, bytes, fn);
     if (rc) return rc;
     const Plan pl = make_plan(p->M, p->C);
     char* s = static_cast<char*>(scratch);
@@ -969,8 +1059,7 @@ extern "C" int gm_bn_bwd_bf16(const gm_bn_bwd* p, void* scratch, size_t bytes, v
     a.M = p->M; a.C = p->C; a.tpr_log = pl.tpr_log; a.rpb = pl.rpb; a.relu = p->relu;
     a.SW = pl.SW; a.nrc = pl.nrc;
     a.accumulate = p->accumulate;
-    a.x = static_cast<const uint4*>(p->x); a.dy = static_cast<const uint4*>(p->dy);
-    a.y = static_cast<const uint4*>(p->y);
+    a.x = p->x; a.dy = p->dy; a.y = p->y;
     a.gamma = p->gamma;
     a.save_mean = const_cast<float*>(p->save_mean); a.save_invstd = const_cast<float*>(p->save_invstd);
     a.dgamma = p->dgamma; a.dbeta = p->dbeta;
@@ -980,11 +1069,12 @@ extern "C" int gm_bn_bwd_bf16(const gm_bn_bwd* p, void* scratch, size_t bytes, v
     a.part = reinterpret_cast<float*>(s + pl.off_p1);
     hipStream_t st = as_stream(stream);
     Plan fp;
-    const int nr = (!p->dres || p->relu) ? fused_plan(p->M, p->C, fp, true) : 0;
+    const int nr = (std::is_same<E, uint16_t>::value && (!p->dres || p->relu)) ? fused_plan(p->M, p->C, fp, true) : 0;
     if (nr) {
         a.rpb = fp.rpb;
         a.nrc = fp.nrc;
         a.gen = reinterpret_cast<unsigned*>(s) + kGenOff;
+        a.spin_limit = spin_limit();
         a.yout = static_cast<uint4*>(p->dx);
         a.dres_out = static_cast<uint4*>(p->dres);
         const dim3 g(fp.nrc, fp.nslice);
@@ -999,24 +1089,70 @@ extern "C" int gm_bn_bwd_bf16(const gm_bn_bwd* p, void* scratch, size_t bytes, v
 #undef GM_BN_BWD_FUSED_LAUNCH
         return check_launch("k_bn_bwd_fused");
     }
-    if (maskx) hipLaunchKernelGGL(k_bn_reduce<BWD_RELUX>, dim3(pl.nrc, pl.nslice), dim3(kT), 0, st, a);
-    else if (p->relu) hipLaunchKernelGGL(k_bn_reduce<BWD_RELU>, dim3(pl.nrc, pl.nslice), dim3(kT), 0, st, a);
-    else hipLaunchKernelGGL(k_bn_reduce<BWD>, dim3(pl.nrc, pl.nslice), dim3(kT), 0, st, a);
+    const dim3 rg(pl.nrc, pl.nslice);
+    if (maskx) hipLaunchKernelGGL((k_bn_reduce<BWD_RELUX, E>), rg, dim3(kT), 0, st, a);
+    else if (p->relu) hipLaunchKernelGGL((k_bn_reduce<BWD_RELU, E>), rg, dim3(kT), 0, st, a);
+    else hipLaunchKernelGGL((k_bn_reduce<BWD, E>), rg, dim3(kT), 0, st, a);
     if ((rc = check_launch("k_bn_reduce<bwd>"))) return rc;
     ApplyArgs b{};
     b.nvec = p->M * (p->C / 8); b.tpr_log = ilog2(p->C / 8); b.C = p->C; b.relu = p->relu;
-    b.x = a.x; b.res = a.y; b.dy = a.dy; b.out = static_cast<uint4*>(p->dx);
-    b.out2 = static_cast<uint4*>(p->dres); b.coef = a.coef;
+    b.x = p->x; b.res = p->y; b.dy = p->dy; b.out = p->dx;
+    b.out2 = p->dres; b.coef = a.coef;
     b.fcoef = p->fwd_coef;
     const int g = apply_grid(b.nvec, p->C);
     if (maskx) {
-        hipLaunchKernelGGL((k_bn_apply_bwd<true, false, true>), dim3(g), dim3(kT), 0, st, b);
+        hipLaunchKernelGGL((k_bn_apply_bwd<true, false, true, E>), dim3(g), dim3(kT), 0, st, b);
     } else if (p->relu) {
-        if (p->dres) hipLaunchKernelGGL((k_bn_apply_bwd<true, true>), dim3(g), dim3(kT), 0, st, b);
-        else hipLaunchKernelGGL((k_bn_apply_bwd<true, false>), dim3(g), dim3(kT), 0, st, b);
+        if (p->dres) hipLaunchKernelGGL((k_bn_apply_bwd<true, true, false, E>), dim3(g), dim3(kT), 0, st, b);
+        else hipLaunchKernelGGL((k_bn_apply_bwd<true, false, false, E>), dim3(g), dim3(kT), 0, st, b);
     } else {
-        if (p->dres) hipLaunchKernelGGL((k_bn_apply_bwd<false, true>), dim3(g), dim3(kT), 0, st, b);
-        else hipLaunchKernelGGL((k_bn_apply_bwd<false, false>), dim3(g), dim3(kT), 0, st, b);
+        if (p->dres) hipLaunchKernelGGL((k_bn_apply_bwd<false, true, false, E>), dim3(g), dim3(kT), 0, st, b);
+        else hipLaunchKernelGGL((k_bn_apply_bwd<false, false, false, E>), dim3(g), dim3(kT), 0, st, b);
     }
     return check_launch("k_bn_apply_bwd");
+}
+
+}  // namespace
+
+namespace gm {
+unsigned bn_faults_read(bool clear) {
+    unsigned v = 0;
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_bn_fault), sizeof(v), 0, hipMemcpyDeviceToHost) != hipSuccess) return ~0u;
+    if (clear && v) {
+        const unsigned z = 0;
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_bn_fault), &z, sizeof(z), 0, hipMemcpyHostToDevice);
+    }
+    return v;
+}
+}  // namespace gm
+
+extern "C" int gm_bn_set_concurrency(int n) {
+    GM_REQUIRE(n >= 1 && n <= 1024, "gm_bn_set_concurrency: n must be in [1, 1024] (got %d)", n);
+    gm::g_concurrency = n;
+    return GM_OK;
+}
+
+extern "C" int gm_bn_set_fused_mode(int mode) {
+    GM_REQUIRE(mode >= 0 && mode <= 2, "gm_bn_set_fused_mode: mode must be 0, 1 or 2 (got %d)", mode);
+    gm::g_fused_env = mode;
+    return GM_OK;
+}
+
+extern "C" int gm_bn_fwd_train_bf16(const gm_bn_fwd* p, void* scratch, size_t bytes, void* stream) {
+    return bn_fwd_train<uint16_t>(p, scratch, bytes, stream, "gm_bn_fwd_train_bf16");
+}
+extern "C" int gm_bn_fwd_infer_bf16(const gm_bn_fwd* p, void* scratch, size_t bytes, void* stream) {
+    return bn_fwd_infer<uint16_t>(p, scratch, bytes, stream, "gm_bn_fwd_infer_bf16");
+}
+extern "C" int gm_bn_bwd_bf16(const gm_bn_bwd* p, void* scratch, size_t bytes, void* stream) {
+    return bn_bwd<uint16_t>(p, scratch, bytes, stream, "gm_bn_bwd_bf16");
+}
+extern "C" int gm_bn_fwd_train_f32(const gm_bn_fwd* p, void* scratch, size_t bytes, void* stream) {
+    return bn_fwd_train<float>(p, scratch, bytes, stream, "gm_bn_fwd_train_f32");
+}
+extern "C" int gm_bn_fwd_infer_f32(const gm_bn_fwd* p, void* scratch, size_t bytes, void* stream) {
+    return bn_fwd_infer<float>(p, scratch, bytes, stream, "gm_bn_fwd_infer_f32");
+}
+extern "C" int gm_bn_bwd_f32(const gm_bn_bwd* p, void* scratch, size_t bytes, void* stream) {
+    return bn_bwd<float>(p, scratch, bytes, stream, "gm_bn_bwd_f32");
 }

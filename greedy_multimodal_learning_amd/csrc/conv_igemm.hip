@@ -71,8 +71,13 @@ struct ConvArgs {
     int splits, tiles_total;
     float* ws;                // [tiles][MT*NT*16/4][256] float4
     unsigned* flags;          // [tiles]
+    unsigned spin_limit;      // poll budget of the turnstile wait
     ConvCls cls[kMaxCls];
 };
+
+// sticky fault word of this translation unit (gm_device_faults): a split whose
+// turnstile wait timed out
+__device__ unsigned g_conv_fault = 0;
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
@@ -481,13 +486,30 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
         constexpr int NQ = MT * NT * 4;  // float4 groups of accumulators per lane
         const auto rs = rsrc_of(a.ws + (size_t)bid * NQ * 256 * 4);
         if (split > 0) {  // wait for the previous split's running sum, then add it
-            if (t == 0) {
-                unsigned n = 0;  // bounded: a broken hand-off fails the parity tests, never hangs
+            __shared__ int late;
+            if (t == 0) {  // bounded: a broken hand-off never hangs, it faults loudly
+                unsigned n = 0;
+                bool ok = true;
                 while (__hip_atomic_load(a.flags + bid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
-                           (unsigned)split && ++n < (1u << 22))
+                       (unsigned)split) {
+                    if (++n >= a.spin_limit) {
+                        ok = false;
+                        break;
+                    }
                     __builtin_amdgcn_s_sleep(2);
+                }
+                if (!ok) atomicOr(&g_conv_fault, GM_FAULT_SPLITK_SPIN);
+                late = ok ? 0 : 1;
             }
             __syncthreads();
+            if (late) {  // poison: the running sum was not handed over (the fault word is set)
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+#pragma unroll
+                    for (int j = 0; j < NT; ++j)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) acc[i][j][r] = __builtin_nanf("");
+            }
 #pragma unroll
             for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -727,6 +749,7 @@ static int pick_and_launch(ConvArgs& a, hipStream_t st, void* ws, size_t ws_byte
     a.splits = p.splits;
     a.xcd = p.splits > 1 ? 0 : xcd_remap();  // split-K relies on split-major dispatch order
     if (p.splits > 1) {
+        a.spin_limit = spin_limit();
         a.flags = static_cast<unsigned*>(ws);
         a.ws = reinterpret_cast<float*>(static_cast<char*>(ws) + splitk_flag_bytes(p.tiles));
     }
@@ -903,6 +926,19 @@ static int check_dgrad(const gm_conv_desc* d) {
 static gm_conv_desc_hw to_hw(const gm_conv_desc* d) {
     return gm_conv_desc_hw{d->N, d->H, d->W, d->C, d->K, d->R, d->S, d->stride, d->stride, d->pad, d->pad};
 }
+
+namespace gm {
+unsigned conv_faults_read(bool clear) {
+    unsigned v = 0;
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_conv_fault), sizeof(v), 0, hipMemcpyDeviceToHost) != hipSuccess)
+        return ~0u;
+    if (clear && v) {
+        const unsigned z = 0;
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_conv_fault), &z, sizeof(z), 0, hipMemcpyHostToDevice);
+    }
+    return v;
+}
+}  // namespace gm
 
 extern "C" int gm_conv2d_fwd_hw_bf16(const gm_conv_desc_hw* d, const void* x, const void* w, void* y,
                                      void* stream) {

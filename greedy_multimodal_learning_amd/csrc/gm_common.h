@@ -46,6 +46,33 @@ __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
     return (uint32_t)Elem<uint16_t>::f2bf(lo) | ((uint32_t)Elem<uint16_t>::f2bf(hi) << 16);
 }
 
+// Group i of 8 consecutive channels of an NHWC activation: one 16-byte vector for
+// bf16, two for fp32 (the reference-precision trunk).  Values travel as fp32.
+template <typename E> struct V8;
+template <> struct V8<uint16_t> {
+    static __device__ __forceinline__ void ld(const void* base, long long i, float* f) {
+        const uint4 u = static_cast<const uint4*>(base)[i];
+        f[0] = bf_lo(u.x); f[1] = bf_hi(u.x); f[2] = bf_lo(u.y); f[3] = bf_hi(u.y);
+        f[4] = bf_lo(u.z); f[5] = bf_hi(u.z); f[6] = bf_lo(u.w); f[7] = bf_hi(u.w);
+    }
+    static __device__ __forceinline__ void st(void* base, long long i, const float* f) {
+        static_cast<uint4*>(base)[i] =
+            make_uint4(pack_bf2(f[0], f[1]), pack_bf2(f[2], f[3]), pack_bf2(f[4], f[5]), pack_bf2(f[6], f[7]));
+    }
+};
+template <> struct V8<float> {
+    static __device__ __forceinline__ void ld(const void* base, long long i, float* f) {
+        const float4* p = static_cast<const float4*>(base) + 2 * i;
+        const float4 a = p[0], b = p[1];
+        f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+    }
+    static __device__ __forceinline__ void st(void* base, long long i, const float* f) {
+        float4* p = static_cast<float4*>(base) + 2 * i;
+        p[0] = make_float4(f[0], f[1], f[2], f[3]);
+        p[1] = make_float4(f[4], f[5], f[6], f[7]);
+    }
+};
+
 // 64-lane wave sum (gfx950 wave64)
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -74,6 +101,14 @@ struct FastDiv {
 };
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---- in-launch hand-off health (fused BatchNorm, split-K turnstile) ----------------
+// A spin that runs out of its poll budget sets a bit in its translation unit's sticky
+// device fault word and poisons its result (NaN) instead of applying stale data;
+// gm_device_faults() (abi.hip) reports the OR of all fault words.
+unsigned spin_limit();                         // host: poll budget passed to the kernels
+unsigned bn_faults_read(bool clear);           // batchnorm.hip
+unsigned conv_faults_read(bool clear);         // conv_igemm.hip
 
 // ---- cross-workgroup hand-off without fences (cdna_hip_programming.md, in-launch
 // split-K recipe, sc1 form): the producer writes with sc1 (write-through) stores,

@@ -7,7 +7,8 @@
 // `v > max || isnan(v)`, starting from -inf at the first in-bounds position.
 // Backward is a gather: each input pixel visits the <= ceil(k/s)^2 windows that
 // cover it and sums the dy of those whose argmax is that pixel (fp32, fixed
-// order), so no atomics and dx is written exactly once.
+// order), so no atomics and dx is written exactly once.  Element type E: bf16 (the
+// performance trunk) or fp32 (the reference-precision trunk), 8 channels per access.
 #include "gm_common.h"
 
 namespace gm {
@@ -19,12 +20,8 @@ struct PoolArgs {
     FastDiv fd_c8, fd_q, fd_p, fd_w, fd_h, fd_s;  // index decode without integer division
 };
 
-__device__ __forceinline__ void unpack8(uint4 u, float* f) {
-    f[0] = bf_lo(u.x); f[1] = bf_hi(u.x); f[2] = bf_lo(u.y); f[3] = bf_hi(u.y);
-    f[4] = bf_lo(u.z); f[5] = bf_hi(u.z); f[6] = bf_lo(u.w); f[7] = bf_hi(u.w);
-}
-
-__global__ __launch_bounds__(256) void k_maxpool_fwd(PoolArgs a, const uint4* __restrict__ x, uint4* __restrict__ y,
+template <typename E>
+__global__ __launch_bounds__(256) void k_maxpool_fwd(PoolArgs a, const void* __restrict__ x, void* __restrict__ y,
                                                      uint2* __restrict__ idx) {
     const unsigned total = (unsigned)a.N * a.P * a.Q * a.C8;  // < 2^31 (checked on the host)
     for (unsigned i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
@@ -52,7 +49,7 @@ __global__ __launch_bounds__(256) void k_maxpool_fwd(PoolArgs a, const uint4* __
                 const int w = w0 + c;
                 if (w < 0 || w >= a.W) continue;
                 float v[8];
-                unpack8(x[(((long long)n * a.H + h) * a.W + w) * a.C8 + cg], v);
+                V8<E>::ld(x, (((long long)n * a.H + h) * a.W + w) * a.C8 + cg, v);
                 const uint32_t pos = (uint32_t)(r * a.k + c);
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
@@ -63,14 +60,14 @@ __global__ __launch_bounds__(256) void k_maxpool_fwd(PoolArgs a, const uint4* __
                 }
             }
         }
-        // max of bf16 values is a bf16 value: the pack is exact
-        y[i] = make_uint4(pack_bf2(m[0], m[1]), pack_bf2(m[2], m[3]), pack_bf2(m[4], m[5]), pack_bf2(m[6], m[7]));
+        V8<E>::st(y, i, m);  // the max of E values is an E value: the store is exact
         idx[i] = make_uint2(ix[0] | ix[1] << 8 | ix[2] << 16 | ix[3] << 24, ix[4] | ix[5] << 8 | ix[6] << 16 | ix[7] << 24);
     }
 }
 
-__global__ __launch_bounds__(256) void k_maxpool_bwd(PoolArgs a, const uint4* __restrict__ dy,
-                                                     const uint2* __restrict__ idx, uint4* __restrict__ dx) {
+template <typename E>
+__global__ __launch_bounds__(256) void k_maxpool_bwd(PoolArgs a, const void* __restrict__ dy,
+                                                     const uint2* __restrict__ idx, void* __restrict__ dx) {
     const unsigned total = (unsigned)a.N * a.H * a.W * a.C8;
     for (unsigned i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
         unsigned t = a.fd_c8.div(i);
@@ -98,7 +95,7 @@ __global__ __launch_bounds__(256) void k_maxpool_bwd(PoolArgs a, const uint4* __
                 const uint2 iv = idx[o];
                 const uint32_t pos = (uint32_t)((h - (p * a.s - a.pad)) * a.k + (w - (q * a.s - a.pad)));
                 float d[8];
-                unpack8(dy[o], d);
+                V8<E>::ld(dy, o, d);
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const uint32_t b = ((j < 4 ? iv.x : iv.y) >> (8 * (j & 3))) & 0xffu;
@@ -106,7 +103,7 @@ __global__ __launch_bounds__(256) void k_maxpool_bwd(PoolArgs a, const uint4* __
                 }
             }
         }
-        dx[i] = make_uint4(pack_bf2(g[0], g[1]), pack_bf2(g[2], g[3]), pack_bf2(g[4], g[5]), pack_bf2(g[6], g[7]));
+        V8<E>::st(dx, i, g);
     }
 }
 
@@ -153,24 +150,42 @@ inline int grid_for(long long n) {
 
 using namespace gm;
 
-extern "C" int gm_maxpool2d_fwd_bf16(const gm_pool_desc* d, const void* x, void* y, void* idx, void* stream) {
+template <typename E>
+int pool_fwd(const gm_pool_desc* d, const void* x, void* y, void* idx, void* stream, const char* fn) {
     PoolArgs a;
-    int rc = prep(d, a, "gm_maxpool2d_fwd_bf16");
+    int rc = prep(d, a, fn);
     if (rc) return rc;
-    GM_REQUIRE(x && y && idx, "gm_maxpool2d_fwd_bf16: null pointer");
+    GM_REQUIRE(x && y && idx, "%s: null pointer", fn);
     const long long n = (long long)a.N * a.P * a.Q * a.C8;
-    hipLaunchKernelGGL(k_maxpool_fwd, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), a,
-                       static_cast<const uint4*>(x), static_cast<uint4*>(y), static_cast<uint2*>(idx));
+    hipLaunchKernelGGL(k_maxpool_fwd<E>, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), a, x, y,
+                       static_cast<uint2*>(idx));
     return check_launch("k_maxpool_fwd");
 }
 
-extern "C" int gm_maxpool2d_bwd_bf16(const gm_pool_desc* d, const void* dy, const void* idx, void* dx, void* stream) {
+template <typename E>
+int pool_bwd(const gm_pool_desc* d, const void* dy, const void* idx, void* dx, void* stream, const char* fn) {
     PoolArgs a;
-    int rc = prep(d, a, "gm_maxpool2d_bwd_bf16");
+    int rc = prep(d, a, fn);
     if (rc) return rc;
-    GM_REQUIRE(dy && idx && dx, "gm_maxpool2d_bwd_bf16: null pointer");
+    GM_REQUIRE(dy && idx && dx, "%s: null pointer", fn);
     const long long n = (long long)a.N * a.H * a.W * a.C8;
-    hipLaunchKernelGGL(k_maxpool_bwd, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), a,
-                       static_cast<const uint4*>(dy), static_cast<const uint2*>(idx), static_cast<uint4*>(dx));
+    hipLaunchKernelGGL(k_maxpool_bwd<E>, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), a, dy,
+                       static_cast<const uint2*>(idx), dx);
     return check_launch("k_maxpool_bwd");
+}
+
+extern "C" int gm_maxpool2d_fwd_bf16(const gm_pool_desc* d, const void* x, void* y, void* idx, void* stream) {
+    return pool_fwd<uint16_t>(d, x, y, idx, stream, "gm_maxpool2d_fwd_bf16");
+}
+
+extern "C" int gm_maxpool2d_bwd_bf16(const gm_pool_desc* d, const void* dy, const void* idx, void* dx, void* stream) {
+    return pool_bwd<uint16_t>(d, dy, idx, dx, stream, "gm_maxpool2d_bwd_bf16");
+}
+
+extern "C" int gm_maxpool2d_fwd_f32(const gm_pool_desc* d, const void* x, void* y, void* idx, void* stream) {
+    return pool_fwd<float>(d, x, y, idx, stream, "gm_maxpool2d_fwd_f32");
+}
+
+extern "C" int gm_maxpool2d_bwd_f32(const gm_pool_desc* d, const void* dy, const void* idx, void* dx, void* stream) {
+    return pool_bwd<float>(d, dy, idx, dx, stream, "gm_maxpool2d_bwd_f32");
 }

@@ -287,10 +287,13 @@ class BalancedStep:
     def sync_gate(self):
         """Copy the device gate state to the host mirrors (gate.d_BDR, its M
         accumulators, curation_step, the flags object); returns it as a dict.  The
-        only host sync of the on-device gate, taken when someone asks."""
+        only host sync of the on-device gate, taken when someone asks.  Also raises
+        GreedyMMLError if a fused BatchNorm / split-K hand-off timed out since the
+        last call (gm_device_faults)."""
+        from . import _lib as L
+        L.check_device_faults()  # a timed-out in-launch hand-off since the last sync raises here
         if not self.device_gate:
             return None
-        from . import _lib as L
         raw = self.gate_state.cpu().numpy().tobytes()
         st = L.GateState.from_buffer_copy(raw)
         g, fl = self.gate, self.flags

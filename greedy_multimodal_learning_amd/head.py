@@ -27,9 +27,9 @@ CL = torch.channels_last
 
 
 def head_ok(fs, fcs):
-    """The fused head applies to bf16 channels_last CUDA maps of one shape with fp32 fc."""
+    """The fused head applies to bf16 or fp32 channels_last CUDA maps of one shape with fp32 fc."""
     f0 = fs[0]
-    if not (f0.is_cuda and f0.dim() == 4 and f0.dtype == torch.bfloat16):
+    if not (f0.is_cuda and f0.dim() == 4 and f0.dtype in (torch.bfloat16, torch.float32)):
         return False
     for f, fc in zip(fs, fcs):
         if (f.shape != f0.shape or f.dtype != f0.dtype or not f.is_contiguous(memory_format=CL)
@@ -61,13 +61,14 @@ class _PooledLinearFn(torch.autograd.Function):
         N = ws[0].shape[0]
         dev = fs[0].device
         lay = L.GM_NHWC if HW > 1 else L.GM_NCHW
+        dt = L.GM_F32 if fs[0].dtype == torch.float32 else L.GM_BF16
         pooled = torch.empty(nb, B, C, device=dev, dtype=torch.float32)
         ops.spatial_reduce([dict(x=f, C=C, HW=HW, out=pooled[i], ld_out=C, scale=1.0 / HW) for i, f in enumerate(fs)],
-                           B, L.GM_BF16, lay, dev)
+                           B, dt, lay, dev)
         logits = torch.empty(nb, B, N, device=dev, dtype=torch.float32)
         ops.gemm([dict(M=B, N=N, segs=[(C, ops.Op(pooled[i], C, 1), ops.Op(ws[i].detach(), 1, C))], C=logits[i],
                        ld_c=N, bias=bs[i].detach()) for i in range(nb)], dev)
-        ctx.nb, ctx.shape, ctx.lay = nb, (B, C, H, W), lay
+        ctx.nb, ctx.shape, ctx.lay, ctx.dt = nb, (B, C, H, W), lay, dt
         ctx.params = list(ws) + list(bs)
         ctx.save_for_backward(pooled, *ws, *fs)
         return tuple(logits[i] for i in range(nb))
@@ -117,7 +118,7 @@ class _PooledLinearFn(torch.autograd.Function):
                 gf[i] = torch.empty_like(fs[i], memory_format=CL if ctx.lay == L.GM_NHWC else torch.contiguous_format)
                 # df = 0 * f + d_pooled / HW (the mean's gradient broadcast over the map)
                 sc.append(dict(x=fs[i], y=gf[i], C=C, HW=HW, s=zero, ld_s=0, a=d, ld_a=C, alpha=1.0 / HW))
-            ops.channel_scale(sc, B, L.GM_BF16, ctx.lay, dev)
+            ops.channel_scale(sc, B, ctx.dt, ctx.lay, dev)
         for prm in sunk:
             sink_done(prm)
         return (None, *gw, *gb, *gf)

@@ -1,9 +1,10 @@
-"""Stem MaxPool2d on the HIP kernels (NHWC bf16, 1-byte argmax).
+"""Stem MaxPool2d on the HIP kernels (NHWC bf16 or fp32, 1-byte argmax).
 
-`GMMaxPool2d` is an `nn.MaxPool2d`; bf16 channels_last CUDA inputs (C % 8 == 0,
-dilation 1, floor mode, no return_indices) run `gm_maxpool2d_fwd_bf16` /
-`gm_maxpool2d_bwd_bf16`, everything else PyTorch's max_pool2d.  Reference:
-torchvision ResNet `maxpool` as called at src/model.py:65-106.
+`GMMaxPool2d` is an `nn.MaxPool2d`; CUDA inputs (C % 8 == 0, dilation 1, floor
+mode, no return_indices) run `gm_maxpool2d_{fwd,bwd}_{bf16,f32}` on channels_last
+activations (bf16: the engine's trunk; fp32: the reference's own arithmetic).
+There is no PyTorch max_pool2d path: CPU tensors and other configurations raise.
+Reference: torchvision ResNet `maxpool` as called at src/model.py:65-106.
 """
 import ctypes
 
@@ -33,31 +34,37 @@ class _PoolFn(torch.autograd.Function):
         y = torch.empty(N, C, P, Q, device=x.device, dtype=x.dtype, memory_format=CL)
         idx = torch.empty(N, P, Q, C, device=x.device, dtype=torch.uint8)
         d = L.PoolDesc(N, H, W, C, k, s, pad)
-        L.check(lib.gm_maxpool2d_fwd_bf16(ctypes.byref(d), x.data_ptr(), y.data_ptr(), idx.data_ptr(),
-                                          L.stream_of(x.device)), "gm_maxpool2d_fwd_bf16")
+        f32 = x.dtype == torch.float32
+        fn = lib.gm_maxpool2d_fwd_f32 if f32 else lib.gm_maxpool2d_fwd_bf16
+        L.check(fn(ctypes.byref(d), x.data_ptr(), y.data_ptr(), idx.data_ptr(), L.stream_of(x.device)),
+                "gm_maxpool2d_fwd")
         ctx.save_for_backward(idx)
-        ctx.meta = (N, C, H, W, k, s, pad)
+        ctx.meta = (N, C, H, W, k, s, pad, x.dtype)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         lib = L.load()
         (idx,) = ctx.saved_tensors
-        N, C, H, W, k, s, pad = ctx.meta
-        dy = dy.to(torch.bfloat16)
+        N, C, H, W, k, s, pad, dt = ctx.meta
+        dy = dy.to(dt)
         dy = dy if dy.is_contiguous(memory_format=CL) else dy.contiguous(memory_format=CL)
-        dx = torch.empty(N, C, H, W, device=dy.device, dtype=torch.bfloat16, memory_format=CL)
+        dx = torch.empty(N, C, H, W, device=dy.device, dtype=dt, memory_format=CL)
         d = L.PoolDesc(N, H, W, C, k, s, pad)
-        L.check(lib.gm_maxpool2d_bwd_bf16(ctypes.byref(d), dy.data_ptr(), idx.data_ptr(), dx.data_ptr(),
-                                          L.stream_of(dy.device)), "gm_maxpool2d_bwd_bf16")
+        fn = lib.gm_maxpool2d_bwd_f32 if dt == torch.float32 else lib.gm_maxpool2d_bwd_bf16
+        L.check(fn(ctypes.byref(d), dy.data_ptr(), idx.data_ptr(), dx.data_ptr(), L.stream_of(dy.device)),
+                "gm_maxpool2d_bwd")
         return dx, None, None, None
 
 
 class GMMaxPool2d(nn.MaxPool2d):
     def forward(self, x):
         k, s, p, dil = _pair1(self.kernel_size), _pair1(self.stride), _pair1(self.padding), _pair1(self.dilation)
-        if (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] % 8 == 0
+        if not x.is_cuda:
+            raise L.GreedyMMLError("GMMaxPool2d: runs on libgreedymml_hip.so only (got a CPU tensor)")
+        if not (x.dtype in (torch.bfloat16, torch.float32) and x.dim() == 4 and x.shape[1] % 8 == 0
                 and None not in (k, s, p) and dil == 1 and not self.ceil_mode and not self.return_indices
                 and k <= 15 and 2 * p <= k):
-            return _PoolFn.apply(x, k, s, p)
-        return super().forward(x)
+            raise L.GreedyMMLError("GMMaxPool2d: needs bf16/fp32 [N,C,H,W] with C % 8 == 0, square k <= 15, "
+                                   "pad <= k/2, dilation 1, floor mode")
+        return _PoolFn.apply(x, k, s, p)

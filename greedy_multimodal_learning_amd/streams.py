@@ -42,8 +42,30 @@ def all_side_streams(device):
     return [s for (d, _), s in sorted(_side.items(), key=lambda kv: kv[0]) if d == idx]
 
 
+def _env_int(name, default):
+    try:
+        v = int(os.environ.get(name, default))
+    except ValueError:
+        return default
+    return v if v >= 1 else default
+
+
+_bn_concurrency = [_env_int("GM_BN_FUSE_STREAMS", 4)]  # the library's value at load
+
+
+def reserve_concurrency(n):
+    """Tell the single-launch BatchNorm planner that up to n of its launches may run at
+    once (gm_bn_set_concurrency); only ever raised, so co-residency holds for every
+    model in the process."""
+    if n > _bn_concurrency[0]:
+        from . import _lib as L
+        L.check(L.load().gm_bn_set_concurrency(int(n)), "gm_bn_set_concurrency")
+        _bn_concurrency[0] = n
+
+
 class ViewStreams:
     def __init__(self, device, n):
+        reserve_concurrency(n + 2)  # one fused BN per view stream + headroom (RCCL, copies)
         self.device = device
         self.main = torch.cuda.current_stream(device)
         self.side = [side_stream(device, i) for i in range(n - 1)]

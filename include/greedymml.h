@@ -10,8 +10,10 @@
  *   - returns 0 on success, a negative GM_E* code on bad arguments, or a positive
  *     hipError_t from the launch; gm_last_error() gives a thread-local message;
  *   - no C++ exceptions cross the ABI; the entry points are reentrant (no mutable
- *     globals besides the thread-local error text), so they may be called from the
- *     autograd engine's worker thread and captured into hipGraphs.
+ *     globals besides the thread-local error text, the sticky device fault words and
+ *     two process-wide settings - spin limit, BatchNorm concurrency - see below), so
+ *     they may be called from the autograd engine's worker thread and captured into
+ *     hipGraphs.
  *
  * The reference is pure Python/PyTorch; each entry point below replaces the
  * implicit PyTorch kernels of one reference call site (cited as file:line of the
@@ -43,6 +45,27 @@ extern "C" {
 
 int gm_abi_version(void);
 const char* gm_last_error(void);
+
+/* In-launch hand-off health.  The single-launch BatchNorm kernels and the split-K
+ * convolution turnstile hand data between workgroups of one launch through a spin on
+ * a device word, bounded by a poll budget.  A spin that runs out (a grid that was not
+ * co-resident after all, or a broken hand-off) never hangs and never applies stale
+ * data: it sets a bit in a sticky device fault word and poisons its output with NaN.
+ * gm_device_faults() synchronises the device and returns the OR of the fault words
+ * (clear != 0 resets them).  gm_set_spin_limit() sets the poll budget (0 = default
+ * 1<<24; a test hook).  Not graph-capturable (gm_device_faults synchronises). */
+#define GM_FAULT_BN_SPIN     1u
+#define GM_FAULT_SPLITK_SPIN 2u
+int gm_device_faults(unsigned* out, int clear);
+int gm_set_spin_limit(unsigned polls);
+/* Co-residency of the single-launch BatchNorm: at most `n` such launches are assumed
+ * to run at once (one per concurrently running trunk stream, plus headroom for other
+ * kernels); the fused grid is capped at CUs x (measured blocks per CU) / n, else the
+ * two-launch path runs.  Default 4 (GM_BN_FUSE_STREAMS overrides at load). */
+int gm_bn_set_concurrency(int n);
+/* 0: always the two-launch path; 1: single launch with register-held strips only;
+ * 2 (default): also the streaming single-launch variant.  GM_BN_FUSED at load. */
+int gm_bn_set_fused_mode(int mode);
 
 /* ---------------------------------------------------------------------------
  * Spatial reduction per (batch, channel): the MMTM squeeze and its backward.
@@ -292,6 +315,37 @@ int gm_conv2d_wgrad_hw_bf16(const gm_conv_desc_hw* d, const void* dy, const void
                             int accumulate, void* scratch, size_t scratch_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Reference-precision (fp32) trunk convolutions: the same three passes on the exact
+ * f32 MFMA (v_mfma_f32_32x32x2_f32, one rounding per product, fp32 accumulate), the
+ * reference's own arithmetic type (src/model.py:65-106 through torchvision, fp32
+ * tensors, no autocast: src/framework.py:146-148).  NHWC activations, KRSC weights,
+ * any C >= 1 (the RGB stem runs unpadded), K any (16-byte loads when C % 4 == 0 and
+ * K % 4 == 0):
+ *   GM_CONV_FWD   : out = y [N][P][Q][K]            from x, w
+ *   GM_CONV_DGRAD : out = dx[N][H][W][C] (+ addend) from dy, w
+ *   GM_CONV_WGRAD : out = dw[K][R][S][C]            from dy, x
+ * accumulate != 0 adds into out.  scratch >= gm_conv2d_f32_scratch() bytes (split
+ * reductions: fp32 slabs summed in a fixed order; 0 = none needed).  Deterministic.
+ * ------------------------------------------------------------------------- */
+#define GM_CONV_FWD   0
+#define GM_CONV_DGRAD 1
+#define GM_CONV_WGRAD 2
+typedef struct gm_conv_f32 {
+    int mode;
+    gm_conv_desc d;
+    const float* x;
+    const float* w;
+    const float* dy;
+    float* out;
+    const float* addend;
+    int accumulate;
+    int pad0;
+} gm_conv_f32;
+
+size_t gm_conv2d_f32_scratch(const gm_conv_f32* p);
+int gm_conv2d_f32(const gm_conv_f32* p, void* scratch, size_t scratch_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
  * BatchNorm2d (torchvision ResNet trunk, reference src/model.py:65-106 through
  * torchvision.models.resnet18), NHWC bf16 activations x[M][C] (M = N*H*W), fp32
  * affine parameters and statistics, fused with the residual add and ReLU that
@@ -347,6 +401,11 @@ size_t gm_bn_scratch(long long M, int C);
 int gm_bn_fwd_train_bf16(const gm_bn_fwd* p, void* scratch, size_t scratch_bytes, void* stream);
 int gm_bn_fwd_infer_bf16(const gm_bn_fwd* p, void* scratch, size_t scratch_bytes, void* stream);
 int gm_bn_bwd_bf16(const gm_bn_bwd* p, void* scratch, size_t scratch_bytes, void* stream);
+/* the same three on fp32 activations (x, residual, y, dy, dx, dres fp32 NHWC): the
+ * reference-precision trunk; reduce + apply launches, same statistics arithmetic */
+int gm_bn_fwd_train_f32(const gm_bn_fwd* p, void* scratch, size_t scratch_bytes, void* stream);
+int gm_bn_fwd_infer_f32(const gm_bn_fwd* p, void* scratch, size_t scratch_bytes, void* stream);
+int gm_bn_bwd_f32(const gm_bn_bwd* p, void* scratch, size_t scratch_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * MaxPool2d of the ResNet stem (kernel k, stride, padding; dilation 1, floor
@@ -362,6 +421,9 @@ typedef struct gm_pool_desc {
 
 int gm_maxpool2d_fwd_bf16(const gm_pool_desc* d, const void* x, void* y, void* idx, void* stream);
 int gm_maxpool2d_bwd_bf16(const gm_pool_desc* d, const void* dy, const void* idx, void* dx, void* stream);
+/* fp32 activations (the reference-precision trunk), same index format */
+int gm_maxpool2d_fwd_f32(const gm_pool_desc* d, const void* x, void* y, void* idx, void* stream);
+int gm_maxpool2d_bwd_f32(const gm_pool_desc* d, const void* dy, const void* idx, void* dx, void* stream);
 
 #ifdef __cplusplus
 }

@@ -5,14 +5,16 @@ Follows `src/model.py:15-108`: two unshared torchvision ResNet-18 trunks
 after layer2/3/4 (`mmtm2/3/4`, C = 128/256/512, ratio 4; `:58-60`).  forward
 (`:63-108`) returns ((x0+x1)/2, [x0, x1], scales[3], squeezed[3]).
 
-`num_views > 2` / `arch="resnet50"` generalise to configs C4/C5 (N trunks, the
-N-way MMTM of `oracle.mmtm_nway_ref`); the reference itself is 2-way only.
+`MMTM_MVCNN_N_Ref(num_views, trunk="resnet18"|"resnet50")` generalises to configs
+C4/C5 (N trunks, the N-way MMTM of `oracle.mmtm_nway_ref`; same parameter names as
+the build's `MMTM_MVCNN_N`); the reference itself is 2-way ResNet-18 only.
 """
 import torch
 import torch.nn as nn
 
 from .resnet_ref import resnet18, resnet50
 from .mmtm_ref import MMTMRef
+from .mmtm_nway_ref import MMTMNRef
 
 
 class MMTM_MVCNN_Ref(nn.Module):
@@ -54,3 +56,33 @@ class MMTM_MVCNN_Ref(nn.Module):
         x0 = self.net_view_0.fc(torch.flatten(self.net_view_0.avgpool(f0), 1))
         x1 = self.net_view_1.fc(torch.flatten(self.net_view_1.avgpool(f1), 1))
         return (x0 + x1) / 2, [x0, x1], scales, squeezed
+
+
+class MMTM_MVCNN_N_Ref(nn.Module):
+    """N unshared trunks `net_view_{i}` (resnet18 / resnet50, fc -> Linear(512*exp,
+    nclasses)) fused by MMTMNRef after layer2/3/4 (C = 128/256/512 x expansion)."""
+
+    def __init__(self, nclasses=40, num_views=4, trunk="resnet18", ratio=4, ra_source="first"):
+        super().__init__()
+        make = {"resnet18": resnet18, "resnet50": resnet50}[trunk]
+        exp = 1 if trunk == "resnet18" else 4
+        self.num_views = num_views
+        for i in range(num_views):
+            net = make()
+            net.fc = nn.Linear(512 * exp, nclasses)
+            setattr(self, f"net_view_{i}", net)
+        for i, c in ((2, 128), (3, 256), (4, 512)):
+            setattr(self, f"mmtm{i}", MMTMNRef([c * exp] * num_views, ratio, ra_source=ra_source))
+
+    def forward(self, x, curation_mode=False, caring_modality=None):
+        nets = [getattr(self, f"net_view_{i}") for i in range(self.num_views)]
+        fs = [MMTM_MVCNN_Ref._stem(n, x[:, i]) for i, n in enumerate(nets)]
+        scales, squeezed = [], []
+        for li in (2, 3, 4):
+            fs = [getattr(n, f"layer{li}")(f) for n, f in zip(nets, fs)]
+            fs, sc, sq = getattr(self, f"mmtm{li}")(fs, curation_mode=curation_mode,
+                                                    caring_modality=caring_modality or 0)
+            scales.append(sc)
+            squeezed.append(sq)
+        outs = [n.fc(torch.flatten(n.avgpool(f), 1)) for n, f in zip(nets, fs)]
+        return sum(outs) / len(outs), outs, scales, squeezed

@@ -85,6 +85,15 @@ def test_product_ops_refuse_cpu_tensors():
     from greedy_multimodal_learning_amd._lib import GreedyMMLError
     with pytest.raises(GreedyMMLError):
         ops.linear(torch.randn(2, 3), torch.randn(4, 3))
+    # the trunk modules have no CPU / vendor-library path either
+    from greedy_multimodal_learning_amd.bn import GMBatchNorm2d
+    from greedy_multimodal_learning_amd.conv import GMConv2d
+    from greedy_multimodal_learning_amd.pool import GMMaxPool2d
+    for mod, x in ((GMConv2d(8, 8, 3, padding=1, bias=False), torch.randn(1, 8, 5, 5)),
+                   (GMBatchNorm2d(8), torch.randn(2, 8, 5, 5)),
+                   (GMMaxPool2d(3, 2, 1), torch.randn(1, 8, 5, 5))):
+        with pytest.raises(GreedyMMLError):
+            mod(x)
 
 
 @pytest.mark.parametrize("cfg", ["training_guided", "training_random", "training", "recording", "eval"])

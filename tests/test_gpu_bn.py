@@ -36,6 +36,14 @@ def _inputs(shape, seed, res):
     return x, r, w, b, rm, rv, dy
 
 
+@pytest.fixture
+def fused_mode():
+    """Switch the single-launch BatchNorm mode (gm_bn_set_fused_mode); restores 2."""
+    from greedy_multimodal_learning_amd import _lib as L
+    yield lambda m: L.check(L.load().gm_bn_set_fused_mode(int(m)), "gm_bn_set_fused_mode")
+    L.load().gm_bn_set_fused_mode(2)
+
+
 def _rel(a, b):
     return (a.float() - b.float()).abs().max().item() / max(b.float().abs().max().item(), 1e-6)
 
@@ -151,7 +159,7 @@ def test_bn_relu_mask_from_x_equals_y_mask(shape, monkeypatch):
 @pytest.mark.parametrize("shape", [(64, 64, 112, 112), (64, 64, 56, 56), (64, 128, 28, 28), (64, 256, 14, 14),
                                    (64, 512, 7, 7), (3, 8, 5, 5), (7, 64, 9, 11)])
 @pytest.mark.parametrize("res,relu", [(False, False), (False, True), (True, True)])
-def test_bn_fused_forward_equals_two_kernel_forward(shape, res, relu, mode, monkeypatch):
+def test_bn_fused_forward_equals_two_kernel_forward(shape, res, relu, mode, fused_mode):
     """The single-launch forward (co-resident blocks, in-launch coefficient hand-off)
     == the reduce + apply pair (its own row partition: fp32 partial sums in another
     grouping, so y within one bf16 ulp, running stats to 1e-5), and bit-identical
@@ -160,7 +168,7 @@ def test_bn_fused_forward_equals_two_kernel_forward(shape, res, relu, mode, monk
     x, r, w, b, rm, rv, dy = _inputs(shape, 13 + shape[2], res)
     outs = []
     for fused in ("0", mode, mode):  # the fused path twice: its generation words advance
-        monkeypatch.setenv("GM_BN_FUSED", fused)
+        fused_mode(fused)
         m = GMBatchNorm2d(shape[1]).cuda().to(memory_format=CL)
         with torch.no_grad():
             m.weight.copy_(w)
@@ -180,7 +188,7 @@ def test_bn_fused_forward_equals_two_kernel_forward(shape, res, relu, mode, monk
                                    (64, 512, 7, 7), (3, 8, 5, 5), (7, 64, 9, 11)])
 @pytest.mark.parametrize("res,relu,maskx", [(False, False, True), (False, True, True), (False, True, False),
                                             (True, True, True)])
-def test_bn_fused_backward_equals_two_kernel_backward(shape, res, relu, maskx, mode, monkeypatch):
+def test_bn_fused_backward_equals_two_kernel_backward(shape, res, relu, maskx, mode, monkeypatch, fused_mode):
     """The single-launch backward == the reduce + apply_bwd pair (own row partition:
     dgamma/dbeta to 1e-5, dx/dres within one bf16 ulp of the larger magnitude) and
     bit-identical to itself across launches."""
@@ -189,7 +197,7 @@ def test_bn_fused_backward_equals_two_kernel_backward(shape, res, relu, maskx, m
     x, r, w, b, rm, rv, dy = _inputs(shape, 17 + shape[3], res)
     outs = []
     for fused in ("0", mode, mode):
-        monkeypatch.setenv("GM_BN_FUSED", "0")  # same forward for all three
+        fused_mode(0)  # same forward for all three
         m = B.GMBatchNorm2d(shape[1]).cuda().to(memory_format=CL)
         with torch.no_grad():
             m.weight.copy_(w)
@@ -197,7 +205,7 @@ def test_bn_fused_backward_equals_two_kernel_backward(shape, res, relu, maskx, m
         xg = x.clone().requires_grad_(True)
         rg = r.clone().requires_grad_(True) if res else None
         y = m(xg, residual=rg, relu=relu)
-        monkeypatch.setenv("GM_BN_FUSED", fused)
+        fused_mode(fused)
         y.backward(dy)
         outs.append((xg.grad, rg.grad if res else None, m.weight.grad, m.bias.grad))
     for a, b2 in zip(outs[1], outs[2]):
@@ -210,3 +218,72 @@ def test_bn_fused_backward_equals_two_kernel_backward(shape, res, relu, maskx, m
         assert ((a - b2).abs() <= tol).all()
     for k in (2, 3):
         torch.testing.assert_close(outs[1][k], outs[0][k], rtol=1e-4, atol=1e-4 * outs[0][k].abs().max().item())
+
+
+def test_bn_fused_spin_timeout_faults_loudly(fused_mode):
+    """A coefficient hand-off that runs out of its poll budget (forced: budget 1 poll)
+    must never apply stale coefficients: the fault word is raised and the affected
+    outputs are NaN; the engine's sync point raises GreedyMMLError."""
+    from greedy_multimodal_learning_amd import _lib as L
+    from greedy_multimodal_learning_amd.bn import GMBatchNorm2d
+    lib = L.load()
+    L.device_faults(clear=True)
+    shape = (64, 64, 56, 56)  # hundreds of blocks: early arrivals poll before the last ticket
+    x, r, w, b, rm, rv, dy = _inputs(shape, 21, False)
+    fused_mode(2)
+    m = GMBatchNorm2d(64).cuda()
+    ref = m(x.clone(), relu=True).float()
+    m = GMBatchNorm2d(64).cuda()
+    try:
+        L.check(lib.gm_set_spin_limit(1), "gm_set_spin_limit")
+        y = m(x.clone(), relu=True).float()
+        torch.cuda.synchronize()
+    finally:
+        lib.gm_set_spin_limit(0)
+    faults = L.device_faults()
+    if faults & L.GM_FAULT_BN_SPIN:
+        assert torch.isnan(y).any()  # poisoned, never silently stale
+        with pytest.raises(L.GreedyMMLError, match="BatchNorm"):
+            L.check_device_faults()
+    else:  # every block happened to see the coefficients at its first poll: exact result
+        assert torch.equal(y, ref)
+    assert L.device_faults() == 0  # cleared by check_device_faults
+    assert torch.equal(m(x.clone(), relu=True).float(), ref)  # default budget: healthy again
+
+
+def test_bn_fused_concurrent_streams_match_serial(fused_mode):
+    """More concurrent single-launch BatchNorms than the default reservation (6 streams
+    x forward + backward, view trunks of a 6-view model) == the same launches one after
+    another, with no fault: the planner's co-residency cap holds (gm_bn_set_concurrency
+    raised by the N-view streams)."""
+    from greedy_multimodal_learning_amd import _lib as L
+    from greedy_multimodal_learning_amd.bn import GMBatchNorm2d
+    from greedy_multimodal_learning_amd.streams import reserve_concurrency
+    L.device_faults(clear=True)
+    fused_mode(2)
+    n = 6
+    reserve_concurrency(n + 2)
+    shapes = [(64, 64, 56, 56), (64, 128, 28, 28), (64, 256, 14, 14)]
+    ins = [_inputs(shapes[i % 3], 40 + i, i % 2 == 0) for i in range(n)]
+
+    def run(i):
+        x, r, w, b, rm, rv, dy = ins[i]
+        m = GMBatchNorm2d(x.shape[1]).cuda()
+        xg = x.clone().requires_grad_(True)
+        y = m(xg, residual=r, relu=True)
+        y.backward(dy)
+        return y, xg.grad, m.weight.grad
+
+    serial = [run(i) for i in range(n)]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream() for _ in range(n)]
+    outs = [None] * n
+    for i, s in enumerate(streams):
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            outs[i] = run(i)
+    torch.cuda.synchronize()
+    assert L.device_faults() == 0
+    for a, b2 in zip(serial, outs):
+        for u, v in zip(a, b2):
+            assert torch.equal(u, v)

@@ -67,13 +67,14 @@ def test_conv_fwd_dgrad_wgrad(dev, shape):
     _close(m.weight.grad, wr.grad, 2e-3)
 
 
-def test_conv_fp32_input_uses_vendor_path(dev):
+def test_conv_fp32_input_runs_hip_f32(dev):
+    """fp32 inputs take the exact-f32 MFMA kernels (gm_conv2d_f32), not a vendor library."""
     from greedy_multimodal_learning_amd.conv import GMConv2d
     m = GMConv2d(8, 8, 3, padding=1, bias=False).to(dev)
     x = torch.randn(1, 8, 5, 5, device=dev)
     y = m(x)
-    assert y.dtype == torch.float32
-    torch.testing.assert_close(y, F.conv2d(x, m.weight, padding=1))
+    assert y.dtype == torch.float32 and "ConvF32" in type(y.grad_fn).__name__ if y.grad_fn else True
+    torch.testing.assert_close(y, F.conv2d(x, m.weight, padding=1), rtol=1e-5, atol=1e-5)
 
 
 def test_conv_wgrad_in_place_sink(dev):
@@ -199,3 +200,35 @@ def test_stem_pack_kernel_matches_torch_pack(dev, shape, dtype):
     xp, wp = G.stem_pack(x, w, pad)
     assert torch.equal(xp, G.stem_pack_input(x, R, S, pad))
     assert torch.equal(wp, G.stem_pack_weight(w))
+
+
+def test_conv_splitk_spin_timeout_never_silent(dev):
+    """A split that runs out of its poll budget (forced: 1 poll) must not add a stale
+    running sum: either every split saw its predecessor in time (exact result, no
+    fault) or the fault word is raised and the affected outputs are NaN.  After the
+    fault check repairs the workspaces, the default budget gives exact results again."""
+    from greedy_multimodal_learning_amd import _lib as L
+    from greedy_multimodal_learning_amd import conv as G
+    lib = L.load()
+    L.device_faults(clear=True)
+    N, C, H, W, K, R, S, st, pad = 64, 512, 7, 7, 512, 3, 3, 1, 1
+    g = torch.Generator(device="cuda").manual_seed(9)
+    CL = torch.channels_last
+    x = torch.randn(N, C, H, W, device=dev, generator=g).bfloat16().contiguous(memory_format=CL)
+    w = (torch.randn(K, C, R, S, device=dev, generator=g) / (C * R * S) ** 0.5).bfloat16().contiguous(memory_format=CL)
+    ref = G.conv_fwd(x, w, st, pad)
+    try:
+        L.check(lib.gm_set_spin_limit(1), "gm_set_spin_limit")
+        ys = [G.conv_fwd(x, w, st, pad) for _ in range(4)]
+        torch.cuda.synchronize()
+    finally:
+        lib.gm_set_spin_limit(0)
+    faults = L.device_faults()
+    if faults & L.GM_FAULT_SPLITK_SPIN:
+        assert any(torch.isnan(y.float()).any() for y in ys)
+        with pytest.raises(L.GreedyMMLError, match="split-K"):
+            L.check_device_faults()
+    else:
+        assert all(torch.equal(y, ref) for y in ys)
+    assert L.device_faults() == 0
+    assert torch.equal(G.conv_fwd(x, w, st, pad), ref)

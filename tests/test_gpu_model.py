@@ -1,10 +1,11 @@
 """Whole-path parity on the GPU: MMTM_MVCNN forward/backward, the gating
 (compute_BDR on gm_group_sumsq) and a 3-epoch guided run, against the
-reference's golden fixtures.  fp32 path: the trunk convolutions run on
-MIOpen (supporting ops), every MMTM site and the gating pass on
-libgreedymml_hip.so.  Tolerances: logits rtol 1e-4 (north_star); gradients
-and d_BDR within the envelope of the reference's own fp32 error against a
-float64 oracle (see test_model_vs_reference).
+reference's golden fixtures.  fp32 path (the reference's own arithmetic):
+EVERY op runs on libgreedymml_hip.so - trunk convolutions on the exact-f32 MFMA
+(gm_conv2d_f32), BatchNorm / max-pool / heads / loss on the fp32 kernels, the
+MMTM sites and the gating pass.  Tolerances: logits rtol 1e-4 (north_star);
+gradients and d_BDR within the envelope of the reference's own fp32 error
+against a float64 oracle (see test_model_vs_reference).
 """
 import numpy as np
 import pytest
@@ -123,6 +124,20 @@ def test_model_vs_reference(golden, dev, case):
         assert abs(d_gpu - d64) <= max(4 * abs(d_ref - d64), 5e-4), (d_gpu, d_ref, d64)
 
 
+def _fp64_trace():
+    """The GPU trace run by the oracle in float64 on the CPU (the 'true' d_BDR sequence)."""
+    from oracle import gating_ref, loop_ref, model_ref, step_ref
+    t = spec.TRACE_GPU
+    m = weights.apply_to_module(model_ref.MMTM_MVCNN_Ref(), seed=spec.SEED_MODEL).double()
+    gate = gating_ref.BDRState(t["epsilon"], t["window"], t["starting_epoch"])
+    step = step_ref.RefStep(m, lr=t["lr"], gate=gate)
+    train, valid, test = spec.trace_loaders(t)
+    conv = lambda L: [(i, tt(x).double(), tt(y)) for i, x, y in L]  # noqa: E731
+    rows = np.array(loop_ref.run(m, step, gate, conv(train), conv(valid), conv(test), t["epochs"]),
+                    dtype=np.float64)
+    return rows, m
+
+
 class _Engine:
     """Holds the curation flags like the reference's Model_ (src/framework.py:137-138)."""
     curation_mode = False
@@ -174,27 +189,49 @@ def test_guided_trace_vs_reference(golden, dev):
     rows = np.array(rows, dtype=np.float64)
     ref = fix["trace_gpu/steps"]
     assert rows.shape == ref.shape
-    np.testing.assert_allclose(rows[:, 0], ref[:, 0], rtol=1e-3)
-    # d_BDR accumulates every step's gradient norms: tight before drift can build up,
-    # then bounded by the accumulated trunk reduction error (decisions stay exact).
-    # The late-step bound covers the run-to-run spread of MIOpen's fp32 algorithm
-    # choice (observed up to 1.06e-3 at step 11 of 12 on one box, 0.9e-3 on another).
-    np.testing.assert_allclose(rows[:4, 1], ref[:4, 1], atol=1e-4)
-    np.testing.assert_allclose(rows[:, 1], ref[:, 1], atol=1.5e-3)
-    # every |d_BDR| of this run is >= 1.6e-3 away from epsilon: decisions must be identical
+    tr64, m64 = _fp64_trace()
+    # Both fp32 runs (the reference's, in the fixture, and this HIP one) are judged
+    # against the same trace in float64.  A ReLU whose float64 input lies within fp32
+    # rounding of zero flips its mask in either run at random (step 1 of this trace
+    # has one: |pre-activation| = 1.3e-6 against a max of 6.8 at net_view_0.layer2.0,
+    # tools/diag_f32_blocks.py), and SGD carries the difference on.  So the bound is
+    # the envelope of the reference's own deviation so far (4x its running max) with
+    # floors sized for one such flip: loss 3e-4 relative, d_BDR 1.5e-3 absolute
+    # (15 % of epsilon; the decisions themselves must be identical - every |d_BDR|
+    # of this run is >= 1.6e-3 away from epsilon).
+    dev_ref = np.maximum.accumulate(np.abs(ref[:, :2] - tr64[:, :2]), axis=0)
+    dev_gpu = np.abs(rows[:, :2] - tr64[:, :2])
+    print("trace |loss-64|, |d_BDR-64|: gpu", dev_gpu.max(0), "reference", dev_ref.max(0))
+    assert np.all(dev_gpu[:, 0] <= np.maximum(4 * dev_ref[:, 0], 3e-4 * np.abs(tr64[:, 0]))), (dev_gpu, dev_ref)
+    assert np.all(dev_gpu[:, 1] <= np.maximum(4 * dev_ref[:, 1], 1.5e-3)), (dev_gpu, dev_ref)
     np.testing.assert_array_equal(rows[:, 2:4], ref[:, 2:4])
     np.testing.assert_allclose(rows[:, 4:], ref[:, 4:], atol=1e-9)
+    # the trained model after 12 steps: eval logits, MMTM running averages and sampled
+    # parameters, each within the envelope of the reference's own deviation from the
+    # float64 run (floors: 1e-3 of the logits' scale, 1e-5 absolute, rtol 1e-3)
     m.eval()
+    m64.eval()
     xe, _ = spec.model_inputs(spec.TRACE_GPU_EVAL)
     with torch.no_grad():
         lm, lo, _, _ = m(tt(xe).to(dev))
-    close(fix, "trace_gpu/eval_logits", lm.cpu(), rtol=1e-3, atol=1e-3)
+        lm64 = m64(tt(xe).double())[0].numpy()
+
+    def envelope(name, got, want64, floor):
+        e_ref = np.abs(fix[name] - want64).max()
+        e_gpu = np.abs(got - want64).max()
+        assert e_gpu <= max(4 * e_ref, floor), (name, e_gpu, e_ref)
+
+    envelope("trace_gpu/eval_logits", lm.cpu().double().numpy(), lm64, 1e-3 * np.abs(lm64).max())
     assert int(fix["trace_gpu/mmtm2_step"]) == m.mmtm2.step
-    close(fix, "trace_gpu/mmtm4_ra_v", m.mmtm4.running_avg_weight_visual.cpu(), atol=1e-5)
-    close(fix, "trace_gpu/mmtm4_ra_s", m.mmtm4.running_avg_weight_skeleton.cpu(), atol=1e-5)
-    P = dict(m.named_parameters())
+    envelope("trace_gpu/mmtm4_ra_v", m.mmtm4.running_avg_weight_visual.cpu().double().numpy(),
+             m64.mmtm4.running_avg_weight_visual.numpy(), 1e-5)
+    envelope("trace_gpu/mmtm4_ra_s", m.mmtm4.running_avg_weight_skeleton.cpu().double().numpy(),
+             m64.mmtm4.running_avg_weight_skeleton.numpy(), 1e-5)
+    P, P64 = dict(m.named_parameters()), dict(m64.named_parameters())
     for n in spec.TRACE_PARAMS:
-        close(fix, "trace_gpu/param." + n, P[n].detach().cpu(), rtol=1e-3, atol=1e-5)
+        w64 = P64[n].detach().numpy()
+        envelope("trace_gpu/param." + n, P[n].detach().cpu().double().numpy(), w64,
+                 1e-3 * np.abs(w64).max() + 1e-5)
 
 
 def test_cur_turnoff_vs_reference(golden, dev, tmp_path):

@@ -1,0 +1,69 @@
+#!/bin/bash
+# The one GPU-session driver (run on the box through gpurun from the repo root):
+#
+#   gpurun --timeout 1200 -- bash tools/gpu.sh STEP [STEP ...]
+#
+# Steps (run in order, each under its own time limit; the first failure ends the call):
+#   tests        pytest -m gpu (one process, per-test timeout)       -> gpurun_out/gpu_tests.log
+#   tests:EXPR   the same, restricted with -k EXPR
+#   smoke        __graft_entry__.smoke()                              -> gpurun_out/smoke.log
+#   bench        python bench.py (defaults, incl. cpu_baseline)       -> gpurun_out/bench.log
+#   benchq       python bench.py --no-cpu-baseline                    -> gpurun_out/benchq.log
+#   bench:ARGS   python bench.py ARGS (commas become spaces)          -> gpurun_out/bench_ARGS.log
+#   prof         rocprofv3 --kernel-trace --stats of a short bench    -> gpurun_out/prof/
+#   pmc:NAME     one rocprofv3 --pmc pass (counter sets below)        -> gpurun_out/pmc_NAME/
+#   py:FILE      python FILE (a tools/ script)                        -> gpurun_out/py_FILE.log
+set -o pipefail
+mkdir -p gpurun_out
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+PROFCMD="python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline"
+
+declare -A PMC
+PMC[mfma]="SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS"
+PMC[lds]="SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVE_CYCLES"
+PMC[fetch]="FETCH_SIZE"
+PMC[write]="WRITE_SIZE"
+
+for s in "$@"; do
+  echo "=== $s $(date +%T)"
+  case "$s" in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 \
+        --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { tail -30 gpurun_out/gpu_tests.log; exit 11; }
+      tail -3 gpurun_out/gpu_tests.log ;;
+    tests:*)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 \
+        --timeout-method thread -k "${s#tests:}" > gpurun_out/gpu_tests_k.log 2>&1 || { tail -40 gpurun_out/gpu_tests_k.log; exit 12; }
+      tail -3 gpurun_out/gpu_tests_k.log ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 \
+        || { tail -30 gpurun_out/smoke.log; exit 13; }
+      tail -2 gpurun_out/smoke.log ;;
+    bench)
+      timeout -k 10 600 python -u bench.py > gpurun_out/bench.log 2>&1 || { tail -30 gpurun_out/bench.log; exit 14; }
+      tail -1 gpurun_out/bench.log | cut -c1-400 ;;
+    benchq)
+      timeout -k 10 600 python -u bench.py --no-cpu-baseline > gpurun_out/benchq.log 2>&1 \
+        || { tail -30 gpurun_out/benchq.log; exit 15; }
+      tail -1 gpurun_out/benchq.log | cut -c1-400 ;;
+    bench:*)
+      a="${s#bench:}"; f="gpurun_out/bench_$(echo "$a" | tr -c 'A-Za-z0-9_=.\n-' '_').log"
+      timeout -k 10 600 python -u bench.py ${a//,/ } > "$f" 2>&1 || { tail -30 "$f"; exit 16; }
+      tail -1 "$f" | cut -c1-400 ;;
+    prof)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench \
+        -- $PROFCMD > gpurun_out/prof.log 2>&1 || { tail -30 gpurun_out/prof.log; exit 17; }
+      python3 tools/summarize_stats.py gpurun_out/prof/bench_kernel_stats.csv 13 | head -40 ;;
+    pmc:*)
+      n="${s#pmc:}"
+      timeout -s KILL 300 rocprofv3 --pmc ${PMC[$n]} --output-format csv -d "gpurun_out/pmc_$n" -o pmc \
+        -- $PROFCMD > "gpurun_out/pmc_$n.log" 2>&1 || { tail -30 "gpurun_out/pmc_$n.log"; exit 18; } ;;
+    py:*)
+      f="${s#py:}"; lg="gpurun_out/py_$(basename "$f" .py).log"
+      timeout -k 10 600 python -u "$f" > "$lg" 2>&1 || { tail -30 "$lg"; exit 19; }
+      tail -20 "$lg" ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "=== all done $(date +%T)"
