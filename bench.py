@@ -42,6 +42,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture of the step")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_group_sumsq.json"))
+    ap.add_argument("--conv-traffic-file", default=os.path.join(ROOT, "profiles", "r02_traffic_conv_family.json"))
+    ap.add_argument("--profile", action="store_true",
+                    help="steps only (no roofline / cpu_baseline measurements): for rocprofv3 runs")
     return ap.parse_args()
 
 
@@ -72,48 +75,13 @@ def cpu_baseline(seconds, size):
                       f"{torch.get_num_threads()} threads, {os.cpu_count()} visible CPUs"}
 
 
-# trunk convolutions of one view at B (ResNet-18 at 224^2): (C, H, W, K, R, stride, pad, count)
-TRUNK = [(3, 224, 224, 64, 7, 2, 3, 1), (64, 56, 56, 64, 3, 1, 1, 4), (64, 56, 56, 128, 3, 2, 1, 1),
-         (64, 56, 56, 128, 1, 2, 0, 1), (128, 28, 28, 128, 3, 1, 1, 3), (128, 28, 28, 256, 3, 2, 1, 1),
-         (128, 28, 28, 256, 1, 2, 0, 1), (256, 14, 14, 256, 3, 1, 1, 3), (256, 14, 14, 512, 3, 2, 1, 1),
-         (256, 14, 14, 512, 1, 2, 0, 1), (512, 7, 7, 512, 3, 1, 1, 3)]
-
-
-def time_trunk_igemm(B, dev, reps=10):
-    """Roofline of the dominant kernel family, the implicit-GEMM convolution
-    (k_conv_igemm*: forward and input-gradient launches of every trunk shape of one
-    view): algorithmic FLOPs / summed average launch time, HIP events on the launch
-    stream behind a device sleep (kernel time, not host enqueue time)."""
-    from greedy_multimodal_learning_amd import conv as G
-    CL = torch.channels_last
-    flops = secs = 0.0
-    launches = 0
-    for (C, H, W, K, R, st, pad, cnt) in TRUNK:
-        Cp = G._cpad(C)
-        P, Q = (H + 2 * pad - R) // st + 1, (W + 2 * pad - R) // st + 1
-        x = torch.randn(B, Cp, H, W, device=dev).bfloat16().contiguous(memory_format=CL)
-        w = torch.randn(K, Cp, R, R, device=dev).bfloat16().contiguous(memory_format=CL)
-        dy = torch.randn(B, K, P, Q, device=dev).bfloat16().contiguous(memory_format=CL)
-        wt = w.permute(1, 0, 2, 3).contiguous(memory_format=CL)
-        if C == 3:  # the stem runs on the pixel-pair view (conv.py); its input gradient is never computed
-            xp = G.stem_pack_input(x[:, :3], R, R, pad)
-            wp = G.stem_pack_weight(w[:, :3].float())
-            ops = [lambda: G.stem_fwd(xp, wp, P, Q)]
-        else:
-            ops = [lambda: G.conv_fwd(x, w, st, pad), lambda: G.conv_dgrad_t(dy, wt, H, W, st, pad)]
-        for op in ops:
-            op()
-            torch.cuda.synchronize()
-            torch.cuda._sleep(20_000_000)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(reps):
-                op()
-            e1.record()
-            torch.cuda.synchronize()
-            secs += e0.elapsed_time(e1) / reps / 1e3 * cnt
-            flops += 2.0 * B * P * Q * K * C * R * R * cnt  # real (unpadded) channels
-            launches += cnt
+def time_trunk_convs(B, dev):
+    """Roofline of the dominant kernel family, the trunk convolutions: forward, input-
+    and weight-gradient launches of every trunk shape of one view at the step's batch
+    (tools/trunk_table.py; HIP events on the launch stream behind a device sleep)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import trunk_table
+    flops, secs, launches, _ = trunk_table.measure_family(B, dev)
     return flops, secs, launches
 
 
@@ -240,16 +208,24 @@ def main():
     loss = float(step.last_loss)
     # roofline kernel: the fused per-branch norms + SGD pass (k_group_sumsq<SGD>), the
     # same launch the step runs (inside the graph), timed with HIP events on its stream
+    if a.profile:
+        if rank == 0:
+            print(json.dumps({"profile_run": True, "ms_per_step": round(ms, 3), "steps": a.steps}), flush=True)
+        if dist_on:
+            dist.destroy_process_group()
+        return
     kern_avg_s = time_group_sumsq(step, 10)
-    conv_flops, conv_s, conv_launches = time_trunk_igemm(B, dev)
+    conv_flops, conv_s, conv_launches = time_trunk_convs(B, dev)
     mmtm_bytes, mmtm_s = time_mmtm_reduce(dev)
-
     if rank == 0:
         views = 2
         total_imgs = world * B * views * a.steps
         bytes_alg = 12 * N_PARAMS  # read param + grad, write param (fp32)
         achieved = bytes_alg / kern_avg_s / 1e9
-        traffic = None
+        traffic = conv_traffic = None
+        if os.path.exists(a.conv_traffic_file):
+            with open(a.conv_traffic_file) as f:
+                conv_traffic = json.load(f).get("hbm_bytes_per_launch")
         if os.path.exists(a.traffic_file):
             with open(a.traffic_file) as f:
                 traffic = json.load(f).get("hbm_bytes_per_launch")
@@ -270,11 +246,12 @@ def main():
                        "parallelism": f"dp{world}", "samples_per_s": round(world * B * a.steps / elapsed, 2),
                        "hipgraph": bool(step.graphs), "device_gate": bool(step.device_gate),
                        "curation_steps_timed": curation_steps, "final_loss": round(loss, 4)},
-            "roofline": {"kernel": "k_conv_igemm_ut / k_conv_igemm (bf16 implicit-GEMM conv, fwd + dgrad, "
-                                   "all trunk shapes of one view at the step's batch)",
+            "roofline": {"kernel": "trunk convolutions (bf16 MFMA implicit GEMM k_conv_igemm_ut/k_conv_igemm fwd + "
+                                   "input grad, k_conv_wgrad4 weight grad; every trunk shape of one view at the "
+                                   "step's batch, tools/trunk_table.py)",
                          "bound": "mfma", "achieved": round(conv_flops / conv_s / 1e12, 1),
                          "peak": MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                         "frac": round(conv_flops / conv_s / 1e12 / MFMA_PEAK_TFS, 4), "traffic": None,
+                         "frac": round(conv_flops / conv_s / 1e12 / MFMA_PEAK_TFS, 4), "traffic": conv_traffic,
                          "alg_flops_per_launch": round(conv_flops / conv_launches),
                          "avg_launch_us": round(conv_s / conv_launches * 1e6, 2)},
             "roofline_hbm": {"kernel": "k_group_sumsq<SGD> (fused per-branch norms + SGD, gm_group_sumsq)",

@@ -11,13 +11,18 @@
 #   benchq       python bench.py --no-cpu-baseline                    -> gpurun_out/benchq.log
 #   bench:ARGS   python bench.py ARGS (commas become spaces)          -> gpurun_out/bench_ARGS.log
 #   prof         rocprofv3 --kernel-trace --stats of a short bench    -> gpurun_out/prof/
-#   pmc:NAME     one rocprofv3 --pmc pass (counter sets below)        -> gpurun_out/pmc_NAME/
+#   pmc:NAME     one rocprofv3 --pmc pass over a short bench (sets below) -> gpurun_out/pmc_NAME/
+#   table        tools/trunk_table.py: per-shape trunk launch table    -> gpurun_out/trunk_table.md
+#   pmct:NAME    one rocprofv3 --pmc pass over tools/trunk_table.py, summarised per (kernel, grid)
+#                                                                     -> gpurun_out/pmct_NAME.txt
+#   pmcg:NAME    one rocprofv3 --pmc pass over tools/traffic_probe.py (the fused norms+SGD pass)
+#                                                                     -> gpurun_out/pmcg_NAME.txt
 #   py:FILE      python FILE (a tools/ script)                        -> gpurun_out/py_FILE.log
 set -o pipefail
 mkdir -p gpurun_out
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-PROFCMD="python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline"
+PROFCMD="python3 bench.py --steps 10 --warmup 3 --profile"
 
 declare -A PMC
 PMC[mfma]="SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS"
@@ -59,6 +64,22 @@ for s in "$@"; do
       n="${s#pmc:}"
       timeout -s KILL 300 rocprofv3 --pmc ${PMC[$n]} --output-format csv -d "gpurun_out/pmc_$n" -o pmc \
         -- $PROFCMD > "gpurun_out/pmc_$n.log" 2>&1 || { tail -30 "gpurun_out/pmc_$n.log"; exit 18; } ;;
+    table)
+      timeout -k 10 600 python -u tools/trunk_table.py --md gpurun_out/trunk_table.md > gpurun_out/trunk_table.log 2>&1 \
+        || { tail -30 gpurun_out/trunk_table.log; exit 20; }
+      tail -4 gpurun_out/trunk_table.md ;;
+    pmct:*)
+      n="${s#pmct:}"
+      timeout -s KILL 300 rocprofv3 --pmc ${PMC[$n]} --output-format csv -d "gpurun_out/pmct_$n" -o pmc \
+        -- python3 tools/trunk_table.py --reps 4 > "gpurun_out/pmct_$n.log" 2>&1 || { tail -30 "gpurun_out/pmct_$n.log"; exit 21; }
+      python3 tools/pmc_table.py "gpurun_out/pmct_$n" > "gpurun_out/pmct_$n.txt" && rm -rf "gpurun_out/pmct_$n"
+      head -5 "gpurun_out/pmct_$n.txt" ;;
+    pmcg:*)
+      n="${s#pmcg:}"
+      timeout -s KILL 300 rocprofv3 --pmc ${PMC[$n]} --output-format csv -d "gpurun_out/pmcg_$n" -o pmc \
+        -- python3 tools/traffic_probe.py > "gpurun_out/pmcg_$n.log" 2>&1 || { tail -30 "gpurun_out/pmcg_$n.log"; exit 22; }
+      python3 tools/pmc_table.py "gpurun_out/pmcg_$n" > "gpurun_out/pmcg_$n.txt" && rm -rf "gpurun_out/pmcg_$n"
+      grep group_sumsq "gpurun_out/pmcg_$n.txt" ;;
     py:*)
       f="${s#py:}"; lg="gpurun_out/py_$(basename "$f" .py).log"
       timeout -k 10 600 python -u "$f" > "$lg" 2>&1 || { tail -30 "$lg"; exit 19; }

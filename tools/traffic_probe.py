@@ -1,5 +1,5 @@
 """Run the bench's fused norms+SGD pass (k_group_sumsq<SGD>) a few times on the C2
-model, for PMC collection (tools/gpu_traffic.sh)."""
+model, for PMC collection (tools/gpu.sh pmcg:fetch / pmcg:write)."""
 import os
 import sys
 

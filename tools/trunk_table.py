@@ -1,0 +1,205 @@
+"""Per-shape launch table of the bf16 ResNet-18 trunk of ONE view at the step's batch:
+every convolution pass (forward, input gradient, weight gradient; the stem on its
+pixel-pair view), every BatchNorm forward/backward (single-launch fused kernels) and
+the stem max-pool, each timed with HIP events on its launch stream behind a device
+sleep (kernel time, not host enqueue time).
+
+For each op: algorithmic FLOPs (real channels) and HBM bytes (each operand read once,
+each output written once), average microseconds, achieved TFLOP/s and GB/s, and the
+fraction of its own roofline bound = min(MFMA peak, arithmetic intensity x HBM peak)
+(peaks: MI355X_MICROARCH.md, 2.5 PFLOP/s dense bf16, 8 TB/s HBM3E).
+
+    python tools/trunk_table.py [--batch 64] [--md out.md] [--reps 10]
+
+Also imported by bench.py (`measure_family`) for the `roofline` object, and run under
+`rocprofv3 --pmc` by tools/gpu.sh (pmc_trunk:*) so counters can be attributed per
+(kernel, grid) to the same launches.
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+MFMA_PEAK_TFS = 2500.0
+HBM_PEAK_GBS = 8000.0
+CL = torch.channels_last
+
+# trunk convolutions of one view (ResNet-18 at 224^2): name, (C, H, W, K, R, stride, pad, count)
+TRUNK = [("conv1", (3, 224, 224, 64, 7, 2, 3, 1)), ("l1", (64, 56, 56, 64, 3, 1, 1, 4)),
+         ("l2.0.c1", (64, 56, 56, 128, 3, 2, 1, 1)), ("l2.ds", (64, 56, 56, 128, 1, 2, 0, 1)),
+         ("l2", (128, 28, 28, 128, 3, 1, 1, 3)), ("l3.0.c1", (128, 28, 28, 256, 3, 2, 1, 1)),
+         ("l3.ds", (128, 28, 28, 256, 1, 2, 0, 1)), ("l3", (256, 14, 14, 256, 3, 1, 1, 3)),
+         ("l4.0.c1", (256, 14, 14, 512, 3, 2, 1, 1)), ("l4.ds", (256, 14, 14, 512, 1, 2, 0, 1)),
+         ("l4", (512, 7, 7, 512, 3, 1, 1, 3))]
+# BatchNorms of one view: name, (C, H, W, residual, relu, count)
+BNS = [("bn1", (64, 112, 112, False, True, 1)), ("l1.bn1", (64, 56, 56, False, True, 2)),
+       ("l1.bn2", (64, 56, 56, True, True, 2)), ("l2.bn1", (128, 28, 28, False, True, 2)),
+       ("l2.bn2", (128, 28, 28, True, True, 2)), ("l2.ds", (128, 28, 28, False, False, 1)),
+       ("l3.bn1", (256, 14, 14, False, True, 2)), ("l3.bn2", (256, 14, 14, True, True, 2)),
+       ("l3.ds", (256, 14, 14, False, False, 1)), ("l4.bn1", (512, 7, 7, False, True, 2)),
+       ("l4.bn2", (512, 7, 7, True, True, 2)), ("l4.ds", (512, 7, 7, False, False, 1))]
+
+
+def _time(op, reps):
+    """Average seconds per call of op() (HIP events on the current stream)."""
+    op()
+    torch.cuda.synchronize()
+    torch.cuda._sleep(20_000_000)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        op()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps / 1e3
+
+
+def _row(name, op, cnt, flops, nbytes, secs, launches_per_call=1):
+    tf = flops / secs / 1e12 if flops else 0.0
+    gb = nbytes / secs / 1e9
+    bound = min(MFMA_PEAK_TFS, (flops / nbytes) * HBM_PEAK_GBS / 1e3) if flops else None
+    frac = (tf / bound) if bound else gb / HBM_PEAK_GBS
+    return dict(name=name, op=op, count=cnt, flops=flops, bytes=nbytes, us=secs * 1e6, tflops=tf, gbs=gb,
+                bound="mfma" if bound and bound >= MFMA_PEAK_TFS else "hbm", bound_tflops=bound, frac=frac,
+                launches=launches_per_call)
+
+
+def conv_rows(B, dev, reps=10):
+    from greedy_multimodal_learning_amd import conv as G
+    rows = []
+    for name, (C, H, W, K, R, st, pad, cnt) in TRUNK:
+        Cp = G._cpad(C)
+        P, Q = (H + 2 * pad - R) // st + 1, (W + 2 * pad - R) // st + 1
+        flops = 2.0 * B * P * Q * K * C * R * R
+        x = torch.randn(B, Cp, H, W, device=dev).bfloat16().contiguous(memory_format=CL)
+        w = torch.randn(K, Cp, R, R, device=dev).bfloat16().contiguous(memory_format=CL)
+        dy = torch.randn(B, K, P, Q, device=dev).bfloat16().contiguous(memory_format=CL)
+        wt = w.permute(1, 0, 2, 3).contiguous(memory_format=CL)
+        xb, yb, wb = B * H * W * C * 2, B * P * Q * K * 2, K * C * R * R * 2
+        if C == 3:  # the stem runs on the pixel-pair view; its input gradient is never computed
+            xp = G.stem_pack_input(x[:, :3], R, R, pad)
+            wp = G.stem_pack_weight(w[:, :3].float())
+            ops = [("fwd", lambda: G.stem_fwd(xp, wp, P, Q), xb + wb + yb)]
+            from greedy_multimodal_learning_amd import _lib as L
+            import ctypes
+            d = G._desc_hw(B, xp.shape[2], xp.shape[3], 8, K, R, wp.shape[3], 2, 1, 0, 0)
+            need = L.load().gm_conv2d_wgrad_hw_scratch(ctypes.byref(d))
+            scr = torch.empty(max(need, 16), device=dev, dtype=torch.uint8)
+            dwp = torch.empty(K, R, wp.shape[3], 8, device=dev, dtype=torch.float32)
+
+            def stem_wgrad():
+                L.check(L.load().gm_conv2d_wgrad_hw_bf16(ctypes.byref(d), dy.data_ptr(), xp.data_ptr(),
+                                                         dwp.data_ptr(), 8, 0, scr.data_ptr(), need,
+                                                         L.stream_of(dev)), "wgrad_hw")
+            ops.append(("wgrad", stem_wgrad, xb + yb + K * C * R * R * 4))
+        else:
+            dw = torch.empty(K, C, R, R, device=dev, dtype=torch.float32).contiguous(memory_format=CL)
+            ops = [("fwd", lambda: G.conv_fwd(x, w, st, pad), xb + wb + yb),
+                   ("dgrad", lambda: G.conv_dgrad_t(dy, wt, H, W, st, pad), yb + wb + xb),
+                   ("wgrad", lambda: G.conv_wgrad(dy, x, R, R, st, pad, C, out=dw), xb + yb + K * C * R * R * 4)]
+        for op, fn, nbytes in ops:
+            rows.append(_row(name, op, cnt, flops, nbytes, _time(fn, reps)))
+    return rows
+
+
+def bn_rows(B, dev, reps=10):
+    from greedy_multimodal_learning_amd import bn as BN
+    from greedy_multimodal_learning_amd import pool as PL
+    rows = []
+    for name, (C, H, W, res, relu, cnt) in BNS:
+        M = B * H * W
+        x = torch.randn(B, C, H, W, device=dev).bfloat16().contiguous(memory_format=CL)
+        r = torch.randn(B, C, H, W, device=dev).bfloat16().contiguous(memory_format=CL) if res else None
+        dy = torch.randn(B, C, H, W, device=dev).bfloat16().contiguous(memory_format=CL)
+        w = torch.ones(C, device=dev)
+        b = torch.zeros(C, device=dev)
+        rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        coef = torch.empty(2 * C, device=dev) if relu and not res else None
+        st = {}
+
+        def fwd():
+            st["y"], st["sm"], st["si"] = BN.bn_fwd_train(x, w, b, rm, rv, None, 0.1, 1e-5, relu, r, coef)
+        fwd()
+        dg, db = torch.empty(C, device=dev), torch.empty(C, device=dev)
+        maskx = coef is not None
+
+        def bwd():
+            BN.bn_bwd(dy, None if maskx else st["y"], x, w, st["sm"], st["si"], relu, res, dg, db, False,
+                      coef if maskx else None)
+        e = M * C * 2
+        rows.append(_row(name, "bn_fwd", cnt, 0, e * (2 + (1 if res else 0)), _time(fwd, reps)))
+        rows.append(_row(name, "bn_bwd", cnt, 0, e * (3 + (1 if relu and not maskx else 0) + (1 if res else 0)),
+                         _time(bwd, reps)))
+    # stem max-pool (3x3/2 on the 112^2 stem output): read x, write y + 1-byte argmax
+    x = torch.randn(B, 64, 112, 112, device=dev).bfloat16().contiguous(memory_format=CL).requires_grad_(True)
+    pool = PL.GMMaxPool2d(3, 2, 1)
+    y = pool(x)
+    gy = torch.randn_like(y)
+    e_in, e_out = B * 112 * 112 * 64, B * 56 * 56 * 64
+    rows.append(_row("maxpool", "fwd", 1, 0, e_in * 2 + e_out * 3, _time(lambda: pool(x.detach()), reps)))
+    rows.append(_row("maxpool", "bwd", 1, 0, e_out * 3 + e_in * 2,
+                     _time(lambda: torch.autograd.grad(y, x, gy, retain_graph=True), reps)))
+    return rows
+
+
+def measure_family(B, dev, reps=10):
+    """The conv family (fwd + dgrad + wgrad of every trunk shape of one view, weighted by
+    its count per view): (flops, secs, launches, rows)."""
+    rows = conv_rows(B, dev, reps)
+    flops = sum(r["flops"] * r["count"] for r in rows)
+    secs = sum(r["us"] * 1e-6 * r["count"] for r in rows)
+    launches = sum(r["count"] for r in rows)
+    return flops, secs, launches, rows
+
+
+def markdown(rows, B):
+    out = [f"| shape | pass | x/view | GFLOP | MB | avg us | TFLOP/s | GB/s | bound | frac of bound |",
+           "|---|---|---|---|---|---|---|---|---|---|"]
+    for r in rows:
+        bt = f"mfma {MFMA_PEAK_TFS:.0f}" if r["bound"] == "mfma" and r["flops"] else (
+            f"AIxHBM {r['bound_tflops']:.0f} TF" if r["flops"] else "hbm 8000 GB/s")
+        out.append(f"| {r['name']} | {r['op']} | {r['count']} | {r['flops'] / 1e9:.2f} | {r['bytes'] / 1e6:.1f} | "
+                   f"{r['us']:.1f} | {r['tflops']:.1f} | {r['gbs']:.0f} | {bt} | {r['frac']:.3f} |")
+    cf = [r for r in rows if r["flops"]]
+    fl = sum(r["flops"] * r["count"] for r in cf)
+    s = sum(r["us"] * r["count"] for r in cf) * 1e-6
+    out.append("")
+    out.append(f"conv family (one view, B={B}): {fl / 1e12:.3f} TFLOP in {s * 1e3:.3f} ms = "
+               f"{fl / s / 1e12:.1f} TFLOP/s = {fl / s / 1e12 / MFMA_PEAK_TFS:.3f} of {MFMA_PEAK_TFS:.0f} TF")
+    hb = [r for r in rows if not r["flops"]]
+    if hb:
+        by = sum(r["bytes"] * r["count"] for r in hb)
+        s2 = sum(r["us"] * r["count"] for r in hb) * 1e-6
+        out.append(f"BN + max-pool (one view): {by / 1e9:.3f} GB in {s2 * 1e3:.3f} ms = {by / s2 / 1e9:.0f} GB/s "
+                   f"= {by / s2 / 1e9 / HBM_PEAK_GBS:.3f} of {HBM_PEAK_GBS:.0f} GB/s")
+    return "\n".join(out)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--md", default=None)
+    ap.add_argument("--only", default="", help="conv | bn (default both)")
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    from greedy_multimodal_learning_amd import build
+    build.build()
+    rows = []
+    if a.only in ("", "conv"):
+        rows += conv_rows(a.batch, dev, a.reps)
+    if a.only in ("", "bn"):
+        rows += bn_rows(a.batch, dev, a.reps)
+    md = markdown(rows, a.batch)
+    print(md)
+    if a.md:
+        with open(a.md, "w") as f:
+            f.write(md + "\n")
+
+
+if __name__ == "__main__":
+    main()
