@@ -24,7 +24,12 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-N_PARAMS = 23_773_008
+N_PARAMS = 23_773_008  # C2 (MMTM_MVCNN)
+WORKLOADS = {
+    "C2": dict(views=2, trunk="resnet18", batch=64, desc="C2: 2-view MVCNN(ResNet-18 x2)+MMTM x3"),
+    "C4": dict(views=4, trunk="resnet18", batch=64, desc="C4: 4 synthetic modalities (ResNet-18 x4)+N-way MMTM x3"),
+    "C5": dict(views=12, trunk="resnet50", batch=32, desc="C5: 12-view MVCNN (ResNet-50 x12)+N-way MMTM x3"),
+}
 HBM_PEAK_GBS = 8000.0
 MFMA_PEAK_TFS = 2500.0  # dense bf16 (MI355X_MICROARCH.md)
 
@@ -34,7 +39,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=64, help="per-GPU batch (multi-view objects)")
+    ap.add_argument("--workload", default="C2", choices=["C2", "C4", "C5"],
+                    help="C2: 2-view ResNet-18 (BASELINE metric); C4: 4 ResNet-18 modalities; "
+                         "C5: 12 ResNet-50 views (BASELINE.json configs)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="per-GPU batch (multi-view objects); default 64 (C2, C4) / 32 (C5)")
     ap.add_argument("--size", type=int, default=224)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -49,30 +58,41 @@ def parse():
 
 
 def cpu_baseline(seconds, size):
-    """Oracle (port) of the reference step on the host cores, config C1 shape (B=4)."""
+    """Oracle (port) of the reference step on the host cores: config C1's
+    shape (B = 4) for ~`seconds`, then B = 64 (the GPU workload's batch) for a few steps.
+    Threads: torch's intra-op pool as the box configures it (OMP_NUM_THREADS = the CPU
+    share of the job); os.cpu_count() reports the whole machine and is stated beside it."""
     from oracle import model_ref, step_ref, gating_ref, weights
-    torch.manual_seed(0)
-    m = weights.apply_to_module(model_ref.MMTM_MVCNN_Ref(), seed=0)
-    gate = gating_ref.BDRState(0.01, 5, starting_epoch=1)
-    gate.on_epoch_begin(1)
-    step = step_ref.RefStep(m, lr=0.1, gate=gate)
-    B = 4
-    g = torch.Generator().manual_seed(0)
-    x = torch.randn(B, 2, 3, size, size, generator=g)
-    y = torch.randint(0, 40, (B,), generator=g)
-    step(x, y)  # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
-        step(x, y)
-        n += 1
-        dt = time.perf_counter() - t0
-        if dt >= seconds or n >= 200:
-            break
-    return {"value": round(n * B * 2 / dt, 3), "unit": "view-images/s", "cores": torch.get_num_threads(),
-            "kind": "port", "ms_per_step": round(1e3 * dt / n, 2),
-            "sample": f"{n} oracle steps (fp32 torch-CPU restatement of forward+blend_loss+backward+"
-                      f"compute_BDR+SGD), B=4 two-view {size}x{size} (config C1 shape), "
-                      f"{torch.get_num_threads()} threads, {os.cpu_count()} visible CPUs"}
+
+    def run(B, secs, max_steps):
+        torch.manual_seed(0)
+        m = weights.apply_to_module(model_ref.MMTM_MVCNN_Ref(), seed=0)
+        gate = gating_ref.BDRState(0.01, 5, starting_epoch=1)
+        gate.on_epoch_begin(1)
+        step = step_ref.RefStep(m, lr=0.1, gate=gate)
+        g = torch.Generator().manual_seed(0)
+        x = torch.randn(B, 2, 3, size, size, generator=g)
+        y = torch.randint(0, 40, (B,), generator=g)
+        step(x, y)  # warm-up
+        n, t0 = 0, time.perf_counter()
+        while True:
+            step(x, y)
+            n += 1
+            dt = time.perf_counter() - t0
+            if dt >= secs or n >= max_steps:
+                break
+        return n, dt
+
+    th = torch.get_num_threads()
+    n4, dt4 = run(4, seconds, 200)
+    n64, dt64 = run(64, 0.0, 2)
+    return {"value": round(n4 * 4 * 2 / dt4, 3), "unit": "view-images/s", "cores": th,
+            "kind": "port", "ms_per_step": round(1e3 * dt4 / n4, 2),
+            "b64": {"value": round(n64 * 64 * 2 / dt64, 3), "ms_per_step": round(1e3 * dt64 / n64, 1),
+                    "steps": n64},
+            "sample": f"{n4} oracle steps at B=4 (config C1 shape) + {n64} at B=64 (the bench batch); fp32 "
+                      f"torch-CPU restatement of forward+blend_loss+backward+compute_BDR+SGD, two-view "
+                      f"{size}x{size}; {th} threads (the job's CPU share; {os.cpu_count()} CPUs visible)"}
 
 
 def time_trunk_convs(B, dev):
@@ -83,6 +103,21 @@ def time_trunk_convs(B, dev):
     import trunk_table
     flops, secs, launches, _ = trunk_table.measure_family(B, dev)
     return flops, secs, launches
+
+
+def conv_roofline(conv, traffic):
+    """The `roofline` object of the dominant kernel family (the trunk convolutions)."""
+    if conv is None:
+        return {"kernel": "trunk convolutions", "bound": "mfma", "achieved": None, "peak": MFMA_PEAK_TFS,
+                "unit": "TFLOP/s", "frac": None, "traffic": None,
+                "note": "per-shape table covers the ResNet-18 trunk only (C2/C4); see the C2 line"}
+    flops, secs, launches = conv
+    return {"kernel": "trunk convolutions (bf16 MFMA implicit GEMM k_conv_igemm_ut/k_conv_igemm fwd + "
+                      "input grad, k_conv_wgrad4 weight grad; every trunk shape of one view at the "
+                      "step's batch, tools/trunk_table.py)",
+            "bound": "mfma", "achieved": round(flops / secs / 1e12, 1), "peak": MFMA_PEAK_TFS, "unit": "TFLOP/s",
+            "frac": round(flops / secs / 1e12 / MFMA_PEAK_TFS, 4), "traffic": traffic,
+            "alg_flops_per_launch": round(flops / launches), "avg_launch_us": round(secs / launches * 1e6, 2)}
 
 
 def time_mmtm_reduce(dev, B=256, reps=20):
@@ -156,21 +191,30 @@ def main():
     from greedy_multimodal_learning_amd.engine import BalancedStep
 
     torch.manual_seed(0)
-    model = MMTM_MVCNN().to(dev)
-    gate = Bias_Mitigation_Strong(epsilon=0.01, curation_windowsize=5,
-                                  branchnames=["net_view_0", "net_view_1"], starting_epoch=1)
+    WL = WORKLOADS[a.workload]
+    V = WL["views"]
+    if a.workload == "C2":
+        model = MMTM_MVCNN().to(dev)
+        bnames, mnames = ["net_view_0", "net_view_1"], ["visual", "skeleton"]
+    else:
+        from greedy_multimodal_learning_amd.model import MMTM_MVCNN_N
+        model = MMTM_MVCNN_N(num_views=V, trunk=WL["trunk"]).to(dev)
+        bnames, mnames = model.branch_names(), model.mmtm_names()
+    gate = Bias_Mitigation_Strong(epsilon=0.01, curation_windowsize=5, branchnames=bnames, starting_epoch=1,
+                                  MMTMnames=mnames)
     cdt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     step = BalancedStep(model, lr=0.1, gate=gate, compute_dtype=cdt, channels_last=True,
-                        process_group=dist.group.WORLD if dist_on else None, graphs=not a.eager)
+                        process_group=dist.group.WORLD if dist_on else None, graphs=not a.eager,
+                        branchnames=bnames, MMTMnames=mnames)
     step.on_epoch_begin(1)
-    B = a.batch
+    B = a.batch if a.batch is not None else WL["batch"]
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
     xdt = cdt
     # HBM layout of a batch: view-major, channels-last [V][B][H][W][3], exposed to the
     # model as the reference's [B, V, 3, H, W] (a permuted view); each view's slice is
     # then a dense channels_last image batch the first convolution reads directly.
     def batch():
-        buf = torch.randn(2, B, a.size, a.size, 3, device=dev, generator=g).to(xdt)
+        buf = torch.randn(V, B, a.size, a.size, 3, device=dev, generator=g).to(xdt)
         return buf.permute(1, 0, 4, 2, 3)
     xs = [batch() for _ in range(2)]
     ys = [torch.randint(0, 40, (B,), device=dev, generator=g) for _ in range(2)]
@@ -215,12 +259,12 @@ def main():
             dist.destroy_process_group()
         return
     kern_avg_s = time_group_sumsq(step, 10)
-    conv_flops, conv_s, conv_launches = time_trunk_convs(B, dev)
+    conv = time_trunk_convs(B, dev) if WL["trunk"] == "resnet18" else None
     mmtm_bytes, mmtm_s = time_mmtm_reduce(dev)
     if rank == 0:
-        views = 2
+        views = V
         total_imgs = world * B * views * a.steps
-        bytes_alg = 12 * N_PARAMS  # read param + grad, write param (fp32)
+        bytes_alg = 12 * step.flat.total  # read param + grad, write param (fp32)
         achieved = bytes_alg / kern_avg_s / 1e9
         traffic = conv_traffic = None
         if os.path.exists(a.conv_traffic_file):
@@ -239,21 +283,14 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": a.dtype,
-            "data": "synthetic N(0,1) [B,2,3,224,224] + uniform labels, resident in HBM; random-init weights",
-            "config": {"workload": "C2: 2-view MVCNN(ResNet-18 x2)+MMTM x3, guided gating "
-                                   "(training_guided.gin eps 0.01, window 5, unlocked)",
+            "data": f"synthetic N(0,1) [B,{V},3,224,224] + uniform labels, resident in HBM; random-init weights",
+            "config": {"workload": WL["desc"] + ", guided gating (training_guided.gin eps 0.01, window 5, unlocked)",
+                       "params": step.flat.total,
                        "global_batch": B * world, "per_gpu_batch": B, "image": a.size,
                        "parallelism": f"dp{world}", "samples_per_s": round(world * B * a.steps / elapsed, 2),
                        "hipgraph": bool(step.graphs), "device_gate": bool(step.device_gate),
                        "curation_steps_timed": curation_steps, "final_loss": round(loss, 4)},
-            "roofline": {"kernel": "trunk convolutions (bf16 MFMA implicit GEMM k_conv_igemm_ut/k_conv_igemm fwd + "
-                                   "input grad, k_conv_wgrad4 weight grad; every trunk shape of one view at the "
-                                   "step's batch, tools/trunk_table.py)",
-                         "bound": "mfma", "achieved": round(conv_flops / conv_s / 1e12, 1),
-                         "peak": MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                         "frac": round(conv_flops / conv_s / 1e12 / MFMA_PEAK_TFS, 4), "traffic": conv_traffic,
-                         "alg_flops_per_launch": round(conv_flops / conv_launches),
-                         "avg_launch_us": round(conv_s / conv_launches * 1e6, 2)},
+            "roofline": conv_roofline(conv, conv_traffic),
             "roofline_hbm": {"kernel": "k_group_sumsq<SGD> (fused per-branch norms + SGD, gm_group_sumsq)",
                              "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -266,3 +266,14 @@ def check_device_faults(clear=True):
                                (GM_FAULT_SPLITK_SPIN, "split-K convolution turnstile")) if v & b]
         raise GreedyMMLError(f"device fault 0x{v:x}: {', '.join(what) or 'unknown'} timed out "
                              "(grid not co-resident?); the affected outputs are NaN")
+
+
+class ViewsNorm(ctypes.Structure):
+    _fields_ = [("x", c_void_p), ("flip", c_void_p), ("B", c_int), ("V", c_int), ("H", c_int), ("W", c_int),
+                ("C", c_int), ("mean", c_float * 4), ("std", c_float * 4), ("out", c_void_p), ("dtype", c_int),
+                ("layout", c_int)]
+
+
+EXPORTS.update({
+    "gm_views_normalize": (c_int, [c_void_p, c_void_p]),
+})

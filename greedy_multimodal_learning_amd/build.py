@@ -44,7 +44,7 @@ def build(force=False, verbose=False):
     bdir = os.path.join(PKG, "csrc", "build")
     os.makedirs(bdir, exist_ok=True)
     cc = hipcc()
-    flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+    flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}",
              "-I", os.path.join(ROOT, "include"), "-I", os.path.join(PKG, "csrc")]
     procs = []
     for src in sources():

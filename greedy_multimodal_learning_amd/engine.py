@@ -248,6 +248,17 @@ class BalancedStep:
         # backward) is ONE hipGraph; the gradient all-reduce and the fused norms+SGD pass
         # run eagerly behind each replay (no collective inside a graph)
         self.graphs = bool(graphs) and self.device.type == "cuda"
+        # DP + graphs: with RCCL ("nccl") the bucketed all-reduces are captured INSIDE the
+        # step's graph on the comm stream, each bucket forked off backward the moment its
+        # last gradient is written, so the replay overlaps the collectives with the rest of
+        # backward (north_star: all-reduce overlapped with backward).  gloo collectives
+        # cannot be captured: there (and with GM_DP_GRAPH_COLLECTIVES=0) the per-rank
+        # compute is the graph and the all-reduce + norms/SGD run eagerly behind it.
+        self.graph_collectives = False
+        if self.buckets is not None and self.graphs:
+            backend = dist.get_backend(process_group)
+            self.graph_collectives = (backend == "nccl"
+                                      and os.environ.get("GM_DP_GRAPH_COLLECTIVES", "1") != "0")
         self._graphs = {}
         self._gpool = None
         self._static = None
@@ -370,7 +381,8 @@ class BalancedStep:
             self._gpool = torch.cuda.graph_pool_handle()
         torch.cuda.synchronize(self.device)
         dp = self.buckets is not None
-        if dp:
+        inline = dp and self.graph_collectives  # collectives captured in the graph
+        if dp and not inline:
             self.buckets.deferred = True
         # thread_local: the process group's watchdog thread keeps querying its events
         # while this thread captures (global mode would invalidate the capture)
@@ -378,7 +390,7 @@ class BalancedStep:
         try:
             with torch.cuda.graph(g, pool=self._gpool, capture_error_mode=mode):
                 loss = self._fwd_bwd(*(inputs or self._static)).detach()
-                sums = None if dp else self.norms.sums(grad_scale=1.0 / self.world, lr=self.lr)
+                sums = None if (dp and not inline) else self.norms.sums(grad_scale=1.0 / self.world, lr=self.lr)
                 if sums is not None and self.device_gate:
                     self._gate_step(sums)
         finally:
@@ -412,6 +424,13 @@ class BalancedStep:
                 g, loss, sums = self._graphs.get(key) or self._capture(key, slot)
             except RuntimeError as e:  # capture refused on this system: keep stepping eagerly
                 import sys
+                if self.graph_collectives:  # first fall back to the collectives-outside-the-graph form
+                    print(f"[greedy_multimodal_learning_amd] capturing the all-reduce failed ({e}); "
+                          "collectives run eagerly behind each replay", file=sys.stderr, flush=True)
+                    self.graph_collectives = False
+                    self._graphs = {}
+                    torch.cuda.synchronize(self.device)
+                    return self(x, y)
                 print(f"[greedy_multimodal_learning_amd] hipGraph capture failed ({e}); eager steps from now on",
                       file=sys.stderr, flush=True)
                 self.graphs = False
@@ -420,7 +439,7 @@ class BalancedStep:
                 return self(x, y)
             want = gate is not None and hasattr(gate, "needs_bdr") and gate.needs_bdr()
             g.replay()
-            if self.buckets is not None:
+            if self.buckets is not None and not self.graph_collectives:
                 self.buckets.reduce_all()
                 sums = self.norms.sums(grad_scale=1.0 / self.world, lr=self.lr)
                 if self.device_gate:

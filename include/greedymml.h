@@ -425,6 +425,29 @@ int gm_maxpool2d_bwd_bf16(const gm_pool_desc* d, const void* dy, const void* idx
 int gm_maxpool2d_fwd_f32(const gm_pool_desc* d, const void* x, void* y, void* idx, void* stream);
 int gm_maxpool2d_bwd_f32(const gm_pool_desc* d, const void* dy, const void* idx, void* dx, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Input pipeline (reference src/dataset.py:35-47,95-128): the multi-view batch of
+ * uint8 view stacks x[B][V][H][W][C=3] (each sample's `imgs[specific_view]`) becomes
+ * the network input in one launch:
+ *   value = (u / 255 - mean[c]) / std[c]   (ToTensor then Normalize, fp32, each
+ *                                           operation rounded as torchvision rounds it)
+ *   flip[b*V + v] != 0 mirrors that view horizontally (RandomHorizontalFlip; NULL = none,
+ *   the test transform)
+ *   out GM_NCHW: [B][V][C][H][W] (the reference's batch tensor), GM_NHWC: [V][B][H][W][C]
+ *   (view-major channels_last, the engine's layout); dtype GM_F32 or GM_BF16 (RNE).
+ * W must be a multiple of 4; x 4-byte aligned; out 8 (bf16) / 16 (fp32) byte aligned.
+ * ------------------------------------------------------------------------- */
+typedef struct gm_views_norm {
+    const uint8_t* x;
+    const uint8_t* flip;
+    int B, V, H, W, C;
+    float mean[4], std[4];
+    void* out;
+    int dtype, layout;
+} gm_views_norm;
+
+int gm_views_normalize(const gm_views_norm* p, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

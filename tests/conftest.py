@@ -17,7 +17,7 @@ def golden():
     import numpy as np
     d = os.path.join(ROOT, "tests", "golden")
     return {k: np.load(os.path.join(d, f"golden_{k}.npz")) for k in
-            ("mmtm", "model", "trace", "ddp", "cur")}
+            ("mmtm", "model", "trace", "ddp", "cur", "dataset")}
 
 
 # fp32 parity mode: keep MIOpen off its Winograd / FFT convolution algorithms,

@@ -154,3 +154,10 @@ def signature(key, arr):
         out[".sum_first"] = m.sum(0).sum(-1)
     out[".abs_total"] = np.array(np.abs(a.astype(np.float64)).sum())
     return out
+
+# F6 - input pipeline (src/dataset.py): a synthetic ModelNet40-shaped dataset of uint8
+# 12-view stacks (H, W small; W % 4 == 0 as gm_views_normalize needs), two loader cases
+DATASET = dict(seed=2024, views=12, H=8, W=12, n_train=11, n_test=5,
+               classnames=["airplane", "bathtub", "bed", "chair"],
+               cases=[dict(batch_size=3, valid_size=0.2, specific_views=[0, 6], epochs=2),
+                      dict(batch_size=4, valid_size=0.0, specific_views=[1, 2, 5], epochs=1)])

@@ -18,12 +18,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, graphs, out_dir):
+def _worker(rank, world, port, graphs, out_dir, backend="gloo"):
     import torch.distributed as dist
     from greedy_multimodal_learning_amd.callbacks import Bias_Mitigation_Strong
     from greedy_multimodal_learning_amd.engine import BalancedStep
     from greedy_multimodal_learning_amd.model import MMTM_MVCNN
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
     m = MMTM_MVCNN().to(dev)
@@ -42,8 +42,9 @@ def _worker(rank, world, port, graphs, out_dir):
         trace.append((float(loss), float(gate.d_BDR), bool(st.flags.curation_mode), st.flags.caring_modality))
     torch.cuda.synchronize()
     sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
-    torch.save({"trace": trace, "sd": sd, "graphs": bool(st.graphs), "ngraphs": len(st._graphs)},
-               os.path.join(out_dir, f"g{int(graphs)}_r{rank}.pt"))
+    torch.save({"trace": trace, "sd": sd, "graphs": bool(st.graphs), "ngraphs": len(st._graphs),
+                "inline": bool(st.graph_collectives)},
+               os.path.join(out_dir, f"{backend}_g{int(graphs)}_r{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -54,8 +55,8 @@ def test_dp_graph_steps_equal_eager_dp_steps(tmp_path):
         mp.start_processes(_worker, args=(world, _free_port(), graphs, str(tmp_path)), nprocs=world, join=True,
                            start_method="spawn")
     for r in range(world):
-        e = torch.load(tmp_path / f"g0_r{r}.pt", weights_only=True)
-        g = torch.load(tmp_path / f"g1_r{r}.pt", weights_only=True)
+        e = torch.load(tmp_path / f"gloo_g0_r{r}.pt", weights_only=True)
+        g = torch.load(tmp_path / f"gloo_g1_r{r}.pt", weights_only=True)
         assert g["graphs"] and g["ngraphs"] >= 1 and not e["graphs"] is None
         for a, b in zip(e["trace"], g["trace"]):
             assert a[2:] == b[2:]
@@ -64,9 +65,29 @@ def test_dp_graph_steps_equal_eager_dp_steps(tmp_path):
         for k in e["sd"]:
             torch.testing.assert_close(g["sd"][k], e["sd"][k], rtol=1e-6, atol=1e-6, msg=k)
     # both ranks hold identical parameters (the all-reduced SGD update)
-    g0 = torch.load(tmp_path / "g1_r0.pt", weights_only=True)["sd"]
-    g1 = torch.load(tmp_path / "g1_r1.pt", weights_only=True)["sd"]
+    g0 = torch.load(tmp_path / "gloo_g1_r0.pt", weights_only=True)["sd"]
+    g1 = torch.load(tmp_path / "gloo_g1_r1.pt", weights_only=True)["sd"]
     for k in g0:
         if "running" in k or "num_batches" in k:
             continue  # BN statistics are per rank (no SyncBN, as the reference)
         assert torch.equal(g0[k], g1[k]), k
+
+
+def test_rccl_collectives_captured_in_graph(tmp_path):
+    """RCCL ("nccl") process group of one rank on the box's one GPU: the graph step
+    captures the bucketed all-reduces INSIDE the graph (overlapped with backward on
+    replay) and must equal the eager DP step (same buckets, collectives issued from the
+    gradient hooks)."""
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    for graphs in (False, True):
+        mp.start_processes(_worker, args=(1, _free_port(), graphs, str(tmp_path), "nccl"), nprocs=1, join=True,
+                           start_method="spawn")
+    e = torch.load(tmp_path / "nccl_g0_r0.pt", weights_only=True)
+    g = torch.load(tmp_path / "nccl_g1_r0.pt", weights_only=True)
+    assert g["graphs"] and g["inline"], "collectives were not captured in the graph"
+    for a, b in zip(e["trace"], g["trace"]):
+        assert a[2:] == b[2:]
+        assert a[0] == pytest.approx(b[0], rel=1e-6, abs=1e-6)
+        assert a[1] == pytest.approx(b[1], rel=1e-6, abs=1e-9)
+    for k in e["sd"]:
+        torch.testing.assert_close(g["sd"][k], e["sd"][k], rtol=1e-6, atol=1e-6, msg=k)
