@@ -15,7 +15,7 @@
 namespace gm {
 
 constexpr int kChunk = 16384;     // elements per workgroup
-constexpr int kMaxGroups = 8;
+constexpr int kMaxGroups = 32;  // group_mask bits; 8-group instantiation for <= 4 branches
 
 __device__ __forceinline__ int find_tensor(const gm_tensor* t, int nt, long long e) {
     int lo = 0, hi = nt - 1;
@@ -26,16 +26,16 @@ __device__ __forceinline__ int find_tensor(const gm_tensor* t, int nt, long long
     return lo;
 }
 
-template <bool SGD>
+template <bool SGD, int MG>
 __global__ __launch_bounds__(256) void k_group_sumsq(const gm_tensor* __restrict__ tab, int nt,
                                                      long long total, int ngroups, float gscale,
                                                      float lr, double* __restrict__ rows) {
-    __shared__ double sred[4][2 * kMaxGroups];
+    __shared__ double sred[4][2 * MG];
     const long long e0 = (long long)blockIdx.x * kChunk;
     const long long e1 = min(total, e0 + kChunk);
-    double gw[kMaxGroups], gg[kMaxGroups];
+    double gw[MG], gg[MG];
 #pragma unroll
-    for (int g = 0; g < kMaxGroups; ++g) { gw[g] = 0.0; gg[g] = 0.0; }
+    for (int g = 0; g < MG; ++g) { gw[g] = 0.0; gg[g] = 0.0; }
     int ti = find_tensor(tab, nt, e0);
     long long e = e0;
     while (e < e1) {
@@ -107,14 +107,14 @@ __global__ __launch_bounds__(256) void k_group_sumsq(const gm_tensor* __restrict
         }
         const unsigned m = T.group_mask;
 #pragma unroll
-        for (int g = 0; g < kMaxGroups; ++g)
+        for (int g = 0; g < MG; ++g)
             if (g < ngroups && ((m >> g) & 1u)) { gw[g] += (double)sw; gg[g] += (double)sg; }
         e = T.offset + te;
         ++ti;
     }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
-    for (int g = 0; g < kMaxGroups; ++g) {
+    for (int g = 0; g < MG; ++g) {
         if (g >= ngroups) break;
         const double w = wave_sum_d(gw[g]);
         const double s = wave_sum_d(gg[g]);
@@ -176,10 +176,17 @@ extern "C" int gm_group_sumsq(const gm_tensor* table, int nt, long long total, i
                "group_sumsq: scratch %zu < %zu bytes", scratch_bytes, gm_group_sumsq_scratch(total));
     hipStream_t st = as_stream(stream);
     double* rows = (double*)scratch;
-    if (lr != 0.f)
-        k_group_sumsq<true><<<(int)nb, 256, 0, st>>>(table, nt, total, ngroups, gscale, lr, rows);
-    else
-        k_group_sumsq<false><<<(int)nb, 256, 0, st>>>(table, nt, total, ngroups, gscale, lr, rows);
+    if (ngroups <= 8) {
+        if (lr != 0.f)
+            k_group_sumsq<true, 8><<<(int)nb, 256, 0, st>>>(table, nt, total, ngroups, gscale, lr, rows);
+        else
+            k_group_sumsq<false, 8><<<(int)nb, 256, 0, st>>>(table, nt, total, ngroups, gscale, lr, rows);
+    } else {  // N-branch gates (C5: 12 branches -> 24 groups)
+        if (lr != 0.f)
+            k_group_sumsq<true, kMaxGroups><<<(int)nb, 256, 0, st>>>(table, nt, total, ngroups, gscale, lr, rows);
+        else
+            k_group_sumsq<false, kMaxGroups><<<(int)nb, 256, 0, st>>>(table, nt, total, ngroups, gscale, lr, rows);
+    }
     int rc = check_launch("k_group_sumsq");
     if (rc) return rc;
     k_group_finalize<<<1, 256, 0, st>>>(rows, (int)nb, ngroups, out);

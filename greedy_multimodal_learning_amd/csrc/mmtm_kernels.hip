@@ -32,6 +32,7 @@ struct RedProb {
     int wg_start;    // NHWC: first workgroup of this problem
     int S;           // NHWC: HW splits
     int hw_per;      // NHWC: pixels per split
+    int cw, ncs;     // NHWC: channels per slab (<= 4096 B of them), slabs (C = cw * ncs)
     float* part;     // NHWC partials [B][S][C] (S > 1)
 };
 struct RedArgs {
@@ -129,8 +130,12 @@ __global__ __launch_bounds__(256) void k_colreduce_nhwc(RedArgs a) {
         if (q < a.nprob && (int)blockIdx.x >= a.p[q].wg_start) pi = q;
     const RedProb& p = a.p[pi];
     const int w = blockIdx.x - p.wg_start;
-    const int b = w / p.S, s = w - b * p.S;
-    const int tpp = p.C / N;          // threads per pixel
+    // workgroup = (b, split s, channel slab cs); a slab is <= 4096 B of one pixel's channels
+    const int per_b = p.S * p.ncs;
+    const int b = w / per_b, rem = w - b * per_b;
+    const int s = rem / p.ncs, cs = rem - s * p.ncs;
+    const int CW = p.cw, c0 = cs * CW;
+    const int tpp = CW / N;           // threads per pixel
     const int ppi = 256 / tpp;        // pixels per iteration
     const int t = threadIdx.x;
     const int cc = t % tpp, pl = t / tpp;
@@ -139,7 +144,7 @@ __global__ __launch_bounds__(256) void k_colreduce_nhwc(RedArgs a) {
 #pragma unroll
     for (int j = 0; j < N; ++j) acc[j] = 0.f;
     if (pl < ppi) {
-        const size_t bbase = (size_t)b * p.HW * p.C + (size_t)cc * N;
+        const size_t bbase = (size_t)b * p.HW * p.C + c0 + (size_t)cc * N;
         auto one = [&](int hw) {
             const size_t off = bbase + (size_t)hw * p.C;
             float vx[N];
@@ -163,19 +168,19 @@ __global__ __launch_bounds__(256) void k_colreduce_nhwc(RedArgs a) {
         }
         for (; hw < hw1; hw += ppi) one(hw);
     }
-    // LDS layout [pl][C]: thread (cc, pl) writes its N channels
+    // LDS layout [pl][CW]: thread (cc, pl) writes its N channels
     if (pl < ppi) {
 #pragma unroll
-        for (int j = 0; j < N; ++j) red[pl * p.C + cc * N + j] = acc[j];
+        for (int j = 0; j < N; ++j) red[pl * CW + cc * N + j] = acc[j];
     }
     __syncthreads();
-    for (int c = t; c < p.C; c += 256) {
+    for (int c = t; c < CW; c += 256) {
         float v = 0.f;
-        for (int q = 0; q < ppi; ++q) v += red[q * p.C + c];
+        for (int q = 0; q < ppi; ++q) v += red[q * CW + c];
         if (p.S == 1) {
-            p.out[(size_t)b * p.ld_out + c] = epilogue(v, p, b, c);
+            p.out[(size_t)b * p.ld_out + c0 + c] = epilogue(v, p, b, c0 + c);
         } else {
-            p.part[((size_t)b * p.S + s) * p.C + c] = v;
+            p.part[((size_t)b * p.S + s) * p.C + c0 + c] = v;
         }
     }
 }
@@ -395,11 +400,14 @@ static int red_setup(const gm_spatial_reduce* in, int nprob, int B, int dtype, i
                                (s.dy && !aligned(s.dy, vb))))
                 vb >>= 1;
         } else {
-            GM_REQUIRE((s.C * es) % 16 == 0 && s.C * es <= 4096,
-                       "spatial_reduce[%d]: NHWC needs C*elem %% 16 == 0 and <= 4096 B (C=%d)", i, s.C);
+            GM_REQUIRE((s.C * es) % 16 == 0 && (s.C * es <= 4096 || (s.C * es) % 4096 == 0),
+                       "spatial_reduce[%d]: NHWC needs C*elem %% 16 == 0 and <= 4096 B or a multiple of it (C=%d)",
+                       i, s.C);
+            p.cw = s.C * es <= 4096 ? s.C : 4096 / es;
+            p.ncs = s.C / p.cw;
             GM_REQUIRE(aligned(s.x, 16) && (!s.dy || aligned(s.dy, 16)),
                        "spatial_reduce[%d]: NHWC tensors must be 16-byte aligned", i);
-            const int tpp = s.C * es / 16, ppi = 256 / tpp;
+            const int tpp = p.cw * es / 16, ppi = 256 / tpp;
             // per-problem split independent of how many problems share the launch, so a
             // modality's reduction order (and bits) never depends on its batch-mates
             const int per = red_wgs() / 2;
@@ -411,7 +419,7 @@ static int red_setup(const gm_spatial_reduce* in, int nprob, int B, int dtype, i
             S = (s.HW + p.hw_per - 1) / p.hw_per;
             p.S = S;
             p.wg_start = wgs;
-            wgs += B * S;
+            wgs += B * S * p.ncs;
             if (S > 1) scratch_need += (size_t)B * S * s.C * sizeof(float);
         }
     }

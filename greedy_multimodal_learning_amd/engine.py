@@ -201,7 +201,7 @@ class GradBuckets:
 class BalancedStep:
     def __init__(self, model, lr=0.1, gate=None, compute_dtype=torch.bfloat16, channels_last=True,
                  process_group=None, bucket_mb=25.0, branchnames=("net_view_0", "net_view_1"),
-                 MMTMnames=("visual", "skeleton"), graphs=False, device_gate=None):
+                 MMTMnames=("visual", "skeleton"), graphs=False, device_gate=None, dp_buckets=None):
         self.model = model
         self.lr = float(lr)
         self.gate = gate
@@ -225,7 +225,9 @@ class BalancedStep:
             gate.set_model_pytoune(self.flags)
             gate.on_train_begin({})
         self.buckets = None
-        if self.world > 1:
+        # dp_buckets (default: world > 1) - True also on a one-rank group, so the bucketed
+        # collective path (and its graph capture) runs on a single GPU (tests)
+        if (self.world > 1) if dp_buckets is None else (bool(dp_buckets) and process_group is not None):
             for m in model.modules():
                 if hasattr(m, "zero_grads_for_curated"):
                     m.zero_grads_for_curated = True  # every bucket fills every step

@@ -169,6 +169,7 @@ int gm_mmtm_running_avg_dev(const float* e_v, int ld_e, int B, int C, float* ra_
  * `table` is a DEVICE array of ntensors gm_tensor entries (built once by the
  * caller); `offset` = prefix sum of n (elements before this tensor).  grad may be
  * NULL (a parameter without gradient: contributes 0 and is not updated).
+ * ngroups <= 32 (one bit of group_mask each; the N-branch gate uses 2N groups).
  * out: DEVICE double[2*ngroups]; scratch >= gm_group_sumsq_scratch(total) bytes.
  * Deterministic (fixed reduction order).
  * ------------------------------------------------------------------------- */

@@ -29,7 +29,8 @@ def _worker(rank, world, port, graphs, out_dir, backend="gloo"):
     m = MMTM_MVCNN().to(dev)
     gate = Bias_Mitigation_Strong(epsilon=2e-3, curation_windowsize=2, branchnames=["net_view_0", "net_view_1"],
                                   starting_epoch=1)
-    st = BalancedStep(m, lr=0.05, gate=gate, process_group=dist.group.WORLD, bucket_mb=8.0, graphs=graphs)
+    st = BalancedStep(m, lr=0.05, gate=gate, process_group=dist.group.WORLD, bucket_mb=8.0, graphs=graphs,
+                      dp_buckets=True)
     st.on_epoch_begin(1)
     g = torch.Generator(device=dev).manual_seed(100 + rank)
     xs = [torch.randn(2, 2, 3, 64, 64, device=dev, generator=g) for _ in range(3)]

@@ -57,7 +57,8 @@ def test_gemm_segments_strides_ones_mask_accumulate(dev):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("layout", ["nchw", "nhwc"])
 @pytest.mark.parametrize("B,C,H,W", [(2, 128, 28, 28), (3, 256, 14, 14), (64, 512, 7, 7),
-                                     (1, 8, 1, 1), (5, 64, 3, 5), (7, 128, 1, 3)])
+                                     (1, 8, 1, 1), (5, 64, 3, 5), (7, 128, 1, 3),
+                                     (3, 2048, 7, 7), (2, 4096, 2, 3)])  # ResNet-50 widths: several channel slabs
 def test_spatial_reduce_and_scale(dev, dtype, layout, B, C, H, W):
     from greedy_multimodal_learning_amd import ops, _lib as L
     g = torch.Generator().manual_seed(B * C + H)
@@ -143,3 +144,31 @@ def test_group_sumsq_and_fused_sgd(dev, lr):
         w, gr = before[n]
         np.testing.assert_allclose(p.detach().cpu().double().numpy(), (w - lr * 0.5 * gr).numpy(),
                                    rtol=1e-6, atol=1e-7)
+
+
+def test_group_sumsq_twelve_branches(dev):
+    """The C5 gate: 12 branches x (main, bypass) = 24 groups (the 32-group kernel)."""
+    from greedy_multimodal_learning_amd.callbacks import GroupNorms, group_masks
+    g = torch.Generator().manual_seed(3)
+    V = 12
+    bn = [f"net_view_{i}" for i in range(V)]
+    mn = [f"fc_excite.{i}." for i in range(V)]
+    params = []
+    for i in range(V):
+        for n, s in ((f"net_view_{i}.conv.weight", (64, 3, 3, 3)), (f"net_view_{i}.bn.bias", (64,))):
+            params.append((n, torch.nn.Parameter(torch.randn(*s, generator=g).to(dev))))
+        params.append((f"mmtm4.fc_excite.{i}.weight", torch.nn.Parameter(torch.randn(32, 16, generator=g).to(dev))))
+    params.append(("mmtm4.fc_squeeze.weight", torch.nn.Parameter(torch.randn(16, 384, generator=g).to(dev))))
+    for _, p in params:
+        p.grad = torch.randn(p.shape, generator=g).to(dev)
+    gn = GroupNorms(params, bn, mn)
+    out = gn.sums().cpu().numpy()
+    masks = group_masks([n for n, _ in params], bn, mn)
+    ref = np.zeros(4 * V)
+    for (n, p), m in zip(params, masks):
+        for k in range(2 * V):
+            if (m >> k) & 1:
+                ref[2 * k] += float((p.detach().double() ** 2).sum())
+                ref[2 * k + 1] += float((p.grad.double() ** 2).sum())
+    assert masks[0] == 1 and masks[3 * 10] == 1 << 10  # net_view_10 is not net_view_1
+    np.testing.assert_allclose(out, ref, rtol=1e-6)
