@@ -277,3 +277,8 @@ class ViewsNorm(ctypes.Structure):
 EXPORTS.update({
     "gm_views_normalize": (c_int, [c_void_p, c_void_p]),
 })
+
+EXPORTS.update({
+    "gm_conv_set_pipe": (c_int, [c_int]),
+    "gm_conv_set_halo": (c_int, [c_int]),
+})

@@ -335,14 +335,24 @@ __global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
 //  * per-lane LDS fragment offsets precomputed and the k-loop unrolled by the two
 //    buffers, so every ds_read_b128 is base VGPR + immediate (no address VALU),
 //  * the tap-table entry of the next k-tile is read one step ahead.
-template <int BM, int BN>
+// PIPE 0: two LDS stages, issue(k+1) -> compute(k) -> __syncthreads (vmcnt(0) drain).
+// PIPE 2 / 3: an LDS ring of PIPE stages with ONE raw barrier per k-tile: wait with a
+// counted vmcnt for tile k only (PIPE 3 leaves tile k+1's DMA in flight across the
+// barrier), barrier, refill the stage compute(k-1) released, compute(k) with the next
+// k-step's fragments read from LDS under the current k-step's MFMAs.
+template <int BM, int BN, int PIPE>
 __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
     constexpr int BK = 64;
     constexpr int AR = BM / 32, BR = BN / 32;
     constexpr int MT = BM / 64, NT = BN / 64;
     constexpr int SA = BM * 128, SB = BN * 128;  // bytes per stage
+    constexpr int NST = PIPE == 3 ? 3 : 2;      // LDS stages
+    // diagnostics (timing only, outputs meaningless): PIPE 5 = the PIPE 2 loop without
+    // its LDS-DMA, PIPE 6 = without its MFMA/LDS reads
+    constexpr bool kDma = PIPE != 5, kMath = PIPE != 6;
+    constexpr int G = AR + BR;                   // LDS-DMA instructions per wave per k-tile
     extern __shared__ __attribute__((aligned(16))) uint4 smem[];
-    char* lds = reinterpret_cast<char*>(smem);   // [A0][A1][B0][B1][taps]
+    char* lds = reinterpret_cast<char*>(smem);   // [A0..A(NST-1)][B0..B(NST-1)]
 
     int bid = block_id(a.xcd);
     int split = 0;
@@ -416,7 +426,7 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
     for (int j = 0; j < NT; ++j) {
         const int row = wn * (BN / 2) + j * 32 + fr;
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) b_rd[j][ks] = 2 * SA + row * 128 + (swz(row, ks * 2 + fh) << 4);
+        for (int ks = 0; ks < 4; ++ks) b_rd[j][ks] = NST * SA + row * 128 + (swz(row, ks * 2 + fh) << 4);
     }
 
     typedef __attribute__((address_space(1))) const void* gptr_t;
@@ -441,7 +451,7 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
         for (int j = 0; j < BR; ++j) {
             const void* src = b_ok[j] ? (const void*)(b_ptr[j] + boff) : (const void*)g_zero16;
             __builtin_amdgcn_global_load_lds((gptr_t)src,
-                                             (lptr_t)(lds + 2 * SA + buf * SB + (wave * BR + j) * 1024), 16, 0, 0);
+                                             (lptr_t)(lds + NST * SA + buf * SB + (wave * BR + j) * 1024), 16, 0, 0);
         }
     };
 
@@ -469,18 +479,387 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
         }
     };
-    issue(0, 0);
-    __syncthreads();
-    int kt = 0;
-    for (; kt + 1 < nk; kt += 2) {  // tiles kt (buffer 0) and kt+1 (buffer 1)
-        issue(kt + 1, 1);
-        compute(0);
+    if constexpr (PIPE == 0) {
+        issue(0, 0);
         __syncthreads();
-        if (kt + 2 < nk) issue(kt + 2, 0);
-        compute(1);
-        __syncthreads();
+        int kt = 0;
+        for (; kt + 1 < nk; kt += 2) {  // tiles kt (buffer 0) and kt+1 (buffer 1)
+            issue(kt + 1, 1);
+            compute(0);
+            __syncthreads();
+            if (kt + 2 < nk) issue(kt + 2, 0);
+            compute(1);
+            __syncthreads();
+        }
+        if (kt < nk) compute(0);  // odd tile count: the last tile sits in buffer 0
+    } else {
+        // fragments of k-step ks+1 are read while k-step ks's MFMAs run
+        auto compute_pf = [&](int buf) {
+            bf16x8 af[2][MT], bfr[2][NT];
+#pragma unroll
+            for (int i = 0; i < MT; ++i) af[0][i] = *reinterpret_cast<const bf16x8*>(lds + buf * SA + a_rd[i][0]);
+#pragma unroll
+            for (int j = 0; j < NT; ++j) bfr[0][j] = *reinterpret_cast<const bf16x8*>(lds + buf * SB + b_rd[j][0]);
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) {
+                const int c = ks & 1;
+                if (ks < 3) {
+#pragma unroll
+                    for (int i = 0; i < MT; ++i)
+                        af[c ^ 1][i] = *reinterpret_cast<const bf16x8*>(lds + buf * SA + a_rd[i][ks + 1]);
+#pragma unroll
+                    for (int j = 0; j < NT; ++j)
+                        bfr[c ^ 1][j] = *reinterpret_cast<const bf16x8*>(lds + buf * SB + b_rd[j][ks + 1]);
+                }
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+#pragma unroll
+                    for (int j = 0; j < NT; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[c][j], af[c][i], acc[i][j], 0, 0, 0);
+            }
+            // emitted order: the first k-step's reads, then each k-step's MFMAs with the next
+            // k-step's reads threaded between them (one read per MFMA), so LDS latency hides
+            // under the matrix pipe instead of an lgkmcnt(0) before every group of MFMAs
+            constexpr int NR = MT + NT, NM = MT * NT;
+            __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+#pragma unroll
+            for (int ks = 0; ks < 3; ++ks) {
+#pragma unroll
+                for (int q = 0; q < (NM > NR ? NM : NR); ++q) {
+                    if (q < NM) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    if (q < NR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                }
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
+        };
+        // s_waitcnt immediates (gfx9 encoding: vmcnt[3:0] + [15:14], expcnt[6:4], lgkmcnt[11:8])
+        constexpr int kWaitTile = (G & 15) | (7 << 4) | (15 << 8) | (((G >> 4) & 3) << 14);  // vmcnt(G)
+        constexpr int kWaitAll = (7 << 4) | (15 << 8);                                       // vmcnt(0)
+        if (kDma) issue(0, 0);
+        if (kDma && NST == 3 && nk > 1) issue(1, 1);
+        int s = 0;  // stage of tile kt
+        for (int kt = 0; kt < nk; ++kt) {
+            if (NST == 3 && kt + 1 < nk) __builtin_amdgcn_s_waitcnt(kWaitTile);  // tile kt+1 stays in flight
+            else __builtin_amdgcn_s_waitcnt(kWaitAll);
+            __builtin_amdgcn_s_barrier();
+            if (kDma && kt + NST - 1 < nk) {
+                int sn = s + NST - 1;
+                if (sn >= NST) sn -= NST;
+                issue(kt + NST - 1, sn);
+            }
+            if (kMath) compute_pf(s);
+            if (++s == NST) s = 0;
+        }
     }
-    if (kt < nk) compute(0);  // odd tile count: the last tile sits in buffer 0
+
+    if (a.splits > 1) {
+        constexpr int NQ = MT * NT * 4;  // float4 groups of accumulators per lane
+        const auto rs = rsrc_of(a.ws + (size_t)bid * NQ * 256 * 4);
+        if (split > 0) {  // wait for the previous split's running sum, then add it
+            __shared__ int late;
+            if (t == 0) {  // bounded: a broken hand-off never hangs, it faults loudly
+                unsigned n = 0;
+                bool ok = true;
+                while (__hip_atomic_load(a.flags + bid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
+                       (unsigned)split) {
+                    if (++n >= a.spin_limit) {
+                        ok = false;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                if (!ok) atomicOr(&g_conv_fault, GM_FAULT_SPLITK_SPIN);
+                late = ok ? 0 : 1;
+            }
+            __syncthreads();
+            if (late) {  // poison: the running sum was not handed over (the fault word is set)
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+#pragma unroll
+                    for (int j = 0; j < NT; ++j)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) acc[i][j][r] = __builtin_nanf("");
+            }
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const float4 v = ld_sc1_f32x4(rs, (unsigned)((((i * NT + j) * 4 + g) * 256 + t) * 16));
+                        acc[i][j][4 * g] += v.x;
+                        acc[i][j][4 * g + 1] += v.y;
+                        acc[i][j][4 * g + 2] += v.z;
+                        acc[i][j][4 * g + 3] += v.w;
+                    }
+        }
+        if (split < a.splits - 1) {  // publish the running sum to the next split
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g)
+                        st_sc1_f32x4(rs, (unsigned)((((i * NT + j) * 4 + g) * 256 + t) * 16),
+                                     make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2],
+                                                 acc[i][j][4 * g + 3]));
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (t == 0) __hip_atomic_store(a.flags + bid, (unsigned)(split + 1), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        if (t == 0) __hip_atomic_store(a.flags + bid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+        const int m = m0 + wm * (BM / 2) + i * 32 + fr;
+        if (m >= M) continue;
+        const int b = (int)cl.fd_pq.div((uint32_t)m), pq = m - b * PQ;
+        const int p = (int)cl.fd_q.div((uint32_t)pq), q = pq - p * cl.Q;
+        const int ho = p * cl.oS + cl.oH, wo = q * cl.oS + cl.oW;
+        uint16_t* dst = cl.out + ((size_t)(b * a.Ho + ho) * a.Wo + wo) * a.Nout;
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int gq = 0; gq < 4; ++gq) {
+                const int n = n0 + wn * (BN / 2) + j * 32 + 8 * gq + 4 * fh;
+                if (n >= a.Nout) continue;
+                float o0 = acc[i][j][4 * gq], o1 = acc[i][j][4 * gq + 1];
+                float o2 = acc[i][j][4 * gq + 2], o3 = acc[i][j][4 * gq + 3];
+                if (a.addend) {  // fused gradient join (the residual branch's gradient)
+                    const uint2 av = *(const uint2*)(a.addend + (dst - cl.out) + n);
+                    o0 += bf_lo(av.x); o1 += bf_hi(av.x); o2 += bf_lo(av.y); o3 += bf_hi(av.y);
+                }
+                uint2 v;
+                v.x = pack_bf2(o0, o1);
+                v.y = pack_bf2(o2, o3);
+                *(uint2*)(dst + n) = v;
+            }
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// 3x3 / stride-1 / pad-1 convolutions (the ResNet trunk's 13 main convolutions per view
+// and their stride-1 input gradients) with the A operand staged ONCE per 64-channel
+// chunk as a halo instead of once per tap (implicit-GEMM im2col re-stages every input
+// pixel 9 times).  The lean kernel above is bound by the per-CU LDS-DMA rate
+// (~26 B/clk/CU measured: tools/conv_ab.py diagnostics), so bytes staged per FLOP is
+// the lever: per 64-deep k-tile the A stage shrinks from 16 KB to (halo / 9) ~3-6 KB.
+//
+// Geometry.  An M tile is 128 consecutive output pixels (b, p, q) of the flat
+// N*H*W order (it may span rows and images).  Input rows live in a "padded row" space:
+// image b's row h is padded row b*(H+1) + 1 + h, and padded rows b*(H+1) are zero rows
+// (one between consecutive images, one after the last), columns are padded by one zero
+// column each side.  Output (b, p, q) with tap offset (dh, dw) in [-1, 1]^2 reads halo
+// pixel ((b*(H+1) + 1 + p + dh) - pr0) * (W+2) + (1 + q + dw), pr0 the tile's first
+// padded row - so every tap reads in-range LDS and padding is real zeros (DMA'd from a
+// zero vector), with no per-lane predicates.  Halo pixels are 128-B LDS rows (64
+// channels) with the 16-B chunk XOR-swizzled by ((pixel >> 1) & 7), applied on the DMA
+// source as everywhere in this file.
+//
+// Schedule: k-tiles run chunk-major, tap-minor (k = chunk * 9 + tap); the halo of a
+// chunk is loaded at the chunk's first k-tile (one buffer; the other co-resident
+// workgroup of the CU hides that stall), the B operand (weights) through the usual
+// 2-stage ring with one barrier per k-tile.  Epilogue and split-K turnstile as in the
+// lean kernel.
+struct HaloArgs {
+    int halo_bytes;           // LDS bytes of the halo region (multiple of 1 KB)
+    FastDiv fd_w2, fd_h1;     // W + 2, H + 1
+};
+
+template <int BN, int DIAG, int NB>
+__global__ __launch_bounds__(256) void k_conv_halo(ConvArgs a, HaloArgs h) {
+    constexpr int BM = 128, BK = 64;  // NB: stages of the weight (B) ring, 2 or 3
+    // DIAG (timing diagnostics, outputs meaningless): 5 = no DMA, 6 = no MFMA/LDS reads
+    constexpr bool kDma = DIAG != 5, kMath = DIAG != 6;
+    constexpr int BR = BN / 32;
+    constexpr int MT = BM / 64, NT = BN / 64;
+    constexpr int SB = BN * 128;
+    extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+    char* lds = reinterpret_cast<char*>(smem);  // [halo][B0][B1]
+    const int HB = h.halo_bytes;
+
+    int bid = blockIdx.x;
+    int split = 0;
+    if (a.splits > 1) {
+        split = bid / a.tiles_total;
+        bid -= split * a.tiles_total;
+    }
+    const ConvCls& cl = a.cls[0];
+    const int tm = bid % cl.tiles_m, tn = bid / cl.tiles_m;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int H = a.Hi, W = a.Wi, W2 = W + 2, H1 = H + 1;
+    const int PQ = cl.P * cl.Q;  // == H * W (stride 1, same size)
+    const int M = a.N * PQ;
+    const int nk_all = 9 * (a.C >> 6);
+    const int kt0 = split * nk_all / a.splits;
+    const int nk = (split + 1) * nk_all / a.splits - kt0;
+
+    const int t = threadIdx.x;
+    const int lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int slot = lane & 7;
+    const unsigned pk_dh = cl.pk_dh, pk_dw = cl.pk_dw, pk_r = cl.pk_r, pk_s = cl.pk_s;
+
+    // tile's padded row range
+    int pr0, npix;
+    {
+        const int b0 = (int)cl.fd_pq.div((uint32_t)m0), q0 = m0 - b0 * PQ;
+        const int p0 = (int)cl.fd_q.div((uint32_t)q0);
+        const int m1 = min(m0 + BM, M) - 1;
+        const int b1 = (int)cl.fd_pq.div((uint32_t)m1), q1 = m1 - b1 * PQ;
+        const int p1 = (int)cl.fd_q.div((uint32_t)q1);
+        pr0 = b0 * H1 + p0;
+        npix = (b1 * H1 + p1 + 2 - pr0 + 1) * W2;
+    }
+    pr0 = __builtin_amdgcn_readfirstlane(pr0);
+    npix = __builtin_amdgcn_readfirstlane(npix);
+    const int nI = (npix + 7) >> 3;  // halo DMA instructions of the workgroup
+
+    // A fragments: per MFMA row block i the lane's output pixel's halo index (tap 0,0)
+    const int fr = lane & 31, fh = lane >> 5;
+    int hbase[MT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+        int m = m0 + wm * (BM / 2) + i * 32 + fr;
+        m = m < M ? m : m0;  // rows past M read a valid pixel; their outputs are not stored
+        const int b = (int)cl.fd_pq.div((uint32_t)m), pq = m - b * PQ;
+        const int p = (int)cl.fd_q.div((uint32_t)pq), q = pq - p * cl.Q;
+        hbase[i] = (b * H1 + 1 + p - pr0) * W2 + 1 + q;
+    }
+    // B rows (weights [Nout][9][C])
+    const uint16_t* b_ptr[BR];
+    bool b_ok[BR];
+#pragma unroll
+    for (int j = 0; j < BR; ++j) {
+        const int row = (wave * BR + j) * 8 + (lane >> 3);
+        const int n = n0 + row;
+        const int gc = slot ^ ((row >> 1) & 7);
+        b_ok[j] = n < a.Nout;
+        b_ptr[j] = a.wt + (size_t)(b_ok[j] ? n : 0) * a.T * a.C + gc * 8;
+    }
+    int b_rd[NT][4];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const int row = wn * (BN / 2) + j * 32 + fr;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) b_rd[j][ks] = HB + row * 128 + (swz(row, ks * 2 + fh) << 4);
+    }
+
+    typedef __attribute__((address_space(1))) const void* gptr_t;
+    typedef __attribute__((address_space(3))) void* lptr_t;
+    // the halo of channel chunk cc: instructions I = wave, wave+4, ... of nI, 8 pixels each
+    auto issue_halo = [&](int cc) {
+        const int cbase = cc << 6;
+        for (int I = wave; I < nI; I += 4) {
+            const int hp = I * 8 + (lane >> 3);
+            const void* src = (const void*)g_zero16;
+            if (hp < npix) {
+                const int r = (int)h.fd_w2.div((uint32_t)hp), c = hp - r * W2;
+                const int pr = pr0 + r;
+                const int b = (int)h.fd_h1.div((uint32_t)pr), rr = pr - b * H1;
+                if (rr != 0 && c != 0 && c != W + 1 && b < a.N) {
+                    const int gc = slot ^ ((hp >> 1) & 7);
+                    src = (const void*)(a.in + ((size_t)((b * H + rr - 1) * W + c - 1) << a.logC) + cbase + gc * 8);
+                }
+            }
+            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + I * 1024), 16, 0, 0);
+        }
+    };
+    auto issue_b = [&](int kt, int buf) {
+        const int k = kt0 + kt;
+        const int cc = k / 9, tp = k - cc * 9;
+        const int ti = tp / 3, tj = tp - ti * 3;
+        const int tw = (int)((pk_r >> (4 * ti)) & 15u) * a.Sw + (int)((pk_s >> (4 * tj)) & 15u);
+        const long boff = (long)(tw * a.C + (cc << 6));
+#pragma unroll
+        for (int j = 0; j < BR; ++j) {
+            const void* src = b_ok[j] ? (const void*)(b_ptr[j] + boff) : (const void*)g_zero16;
+            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + HB + buf * SB + (wave * BR + j) * 1024), 16,
+                                             0, 0);
+        }
+    };
+
+    floatx16 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    auto compute = [&](int buf, int toff) {
+        int abase[MT];
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+            const int hp = hbase[i] + toff;
+            abase[i] = (hp << 7) | ((((hp >> 1) & 7) ^ fh) << 4);  // chunk (2ks+fh)^swz = this ^ (ks<<5)
+        }
+        bf16x8 af[2][MT], bfr[2][NT];
+#pragma unroll
+        for (int i = 0; i < MT; ++i) af[0][i] = *reinterpret_cast<const bf16x8*>(lds + abase[i]);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) bfr[0][j] = *reinterpret_cast<const bf16x8*>(lds + buf * SB + b_rd[j][0]);
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            const int c = ks & 1;
+            if (ks < 3) {
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+                    af[c ^ 1][i] = *reinterpret_cast<const bf16x8*>(lds + (abase[i] ^ ((ks + 1) << 5)));
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+                    bfr[c ^ 1][j] = *reinterpret_cast<const bf16x8*>(lds + buf * SB + b_rd[j][ks + 1]);
+            }
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[c][j], af[c][i], acc[i][j], 0, 0, 0);
+        }
+        constexpr int NR = MT + NT, NM = MT * NT;
+        __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+#pragma unroll
+        for (int ks = 0; ks < 3; ++ks) {
+#pragma unroll
+            for (int q = 0; q < (NM > NR ? NM : NR); ++q) {
+                if (q < NM) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                if (q < NR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
+    };
+
+    constexpr int kWaitAll = (7 << 4) | (15 << 8);  // s_waitcnt vmcnt(0)
+    if (kDma) issue_halo(kt0 / 9);
+    if (kDma) issue_b(0, 0);
+    if (kDma && NB == 3 && nk > 1) issue_b(1, 1);
+    constexpr int kWaitB = (BR & 15) | (7 << 4) | (15 << 8);  // vmcnt(BR): the newest B stage stays in flight
+    int sb = 0;  // B stage of k-tile kt
+    for (int kt = 0; kt < nk; ++kt) {
+        const int k = kt0 + kt;
+        const int tp = k % 9;
+        if (NB == 3 && kt + 1 < nk) __builtin_amdgcn_s_waitcnt(kWaitB);
+        else __builtin_amdgcn_s_waitcnt(kWaitAll);
+        __builtin_amdgcn_s_barrier();
+        if (kDma && kt > 0 && tp == 0) {  // next channel chunk: every wave is done with the old halo
+            issue_halo(k / 9);
+            __builtin_amdgcn_s_waitcnt(kWaitAll);
+            __builtin_amdgcn_s_barrier();
+        }
+        if (kDma && kt + NB - 1 < nk) {
+            int sn = sb + NB - 1;
+            if (sn >= NB) sn -= NB;
+            issue_b(kt + NB - 1, sn);
+        }
+        const int ti = tp / 3, tj = tp - ti * 3;
+        const int dh = (int)((pk_dh >> (4 * ti)) & 15u) - 8, dw = (int)((pk_dw >> (4 * tj)) & 15u) - 8;
+        if (kMath) compute(sb, dh * W2 + dw);
+        if (++sb == NB) sb = 0;
+    }
 
     if (a.splits > 1) {
         constexpr int NQ = MT * NT * 4;  // float4 groups of accumulators per lane
@@ -608,6 +987,27 @@ static bool lean_path() {
 static bool grid_ok(const ConvCls& c, int S);
 static void pack_grid(ConvCls& c, int S);
 
+// main-loop form of the lean kernel (k_conv_igemm_ut PIPE); GM_CONV_PIPE at load,
+// gm_conv_set_pipe() at run time (A/B in one process)
+static int g_conv_pipe = [] {
+    const char* e = getenv("GM_CONV_PIPE");
+    return e ? atoi(e) : 0;
+}();
+static int conv_pipe() { return g_conv_pipe; }
+
+template <int BM, int BN, int PIPE>
+static void launch_ut(const ConvArgs& a, int grid, hipStream_t st) {
+    constexpr int NST = PIPE == 3 ? 3 : 2;
+    const size_t lds = (size_t)NST * (BM + BN) * 128;
+    static bool attr = false;  // idempotent, safe to race
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_conv_igemm_ut<BM, BN, PIPE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+        attr = true;
+    }
+    k_conv_igemm_ut<BM, BN, PIPE><<<grid, 256, lds, st>>>(a);
+}
+
 template <int BM, int BN, int ST>
 static int launch_igemm(ConvArgs& a, hipStream_t st) {
     int tiles = 0;
@@ -624,23 +1024,21 @@ static int launch_igemm(ConvArgs& a, hipStream_t st) {
     const size_t lds = (size_t)ST * (BM + BN) * 128 + kMaxTap * 4 + 12;
     static bool attr_set = false;  // idempotent, safe to race
     if (!attr_set) {
-        hipFuncSetAttribute((const void*)k_conv_igemm<BM, BN, true, ST>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)k_conv_igemm<BM, BN, true, ST>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
-        hipFuncSetAttribute((const void*)k_conv_igemm<BM, BN, false, ST>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)k_conv_igemm<BM, BN, false, ST>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
         attr_set = true;
     }
     bool grid = true;
     for (int i = 0; i < a.ncls; ++i) grid = grid && grid_ok(a.cls[i], a.Sw);
     if (a.C >= 64 && grid && lean_path()) {
-        const size_t lds2 = (size_t)2 * (BM + BN) * 128 + kMaxTap * 4 + 12;
-        static bool attr2 = false;
-        if (!attr2) {
-            hipFuncSetAttribute((const void*)k_conv_igemm_ut<BM, BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)lds2);
-            attr2 = true;
-        }
-        k_conv_igemm_ut<BM, BN><<<tiles * a.splits, 256, lds2, st>>>(a);
+        const int pipe = conv_pipe();
+        if (pipe == 3) launch_ut<BM, BN, 3>(a, tiles * a.splits, st);
+        else if (pipe == 5) launch_ut<BM, BN, 5>(a, tiles * a.splits, st);
+        else if (pipe == 6) launch_ut<BM, BN, 6>(a, tiles * a.splits, st);
+        else if (pipe == 2) launch_ut<BM, BN, 2>(a, tiles * a.splits, st);
+        else launch_ut<BM, BN, 0>(a, tiles * a.splits, st);
     } else if (a.splits > 1) {
         set_error("conv: split-K needs the lean kernel");
         return GM_E_ARG;
@@ -731,17 +1129,88 @@ static TilePick pick_tile(const ConvArgs& a) {
     return {T64x64, 1, 0};
 }
 
-static size_t splitk_flag_bytes(int tiles) { return ((size_t)tiles * 4 + 255) / 256 * 256; }
+// turnstile words live in a FIXED region at the start of the workspace (never overlapped
+// by any call's slabs, whatever its tile count), so they stay zero between calls that
+// share the workspace
+constexpr int kMaxSplitTiles = 16384;
+static size_t splitk_flag_bytes(int /*tiles*/) { return (size_t)kMaxSplitTiles * 4; }
 
 static size_t splitk_bytes(const TilePick& p) {
     if (p.splits <= 1) return 0;
     return splitk_flag_bytes(p.tiles) + (size_t)p.tiles * 16 * 256 * 16;  // 128x128: 16 float4 per lane
 }
 
+static int g_conv_halo = [] {
+    const char* e = getenv("GM_CONV_HALO");
+    return e ? atoi(e) : 1;
+}();
+
+// the halo kernel serves one-class, 3x3 tap grids with offsets in [-1, 1] at stride 1
+// and same-size output (forward 3x3/s1/p1 and its input gradient), C a multiple of 64;
+// returns the halo LDS bytes (0 = not eligible)
+static int halo_bytes(const ConvArgs& a) {
+    // C >= 128 (two or more chunks): with one chunk (ResNet layer 1) the whole halo must
+    // land before the first k-tile and the im2col kernel measured faster (tools/conv_ab.py)
+    if (!g_conv_halo || a.ncls != 1 || a.C < 128 || (a.C & 63) || a.sAh != 1 || a.sAw != 1) return 0;
+    const ConvCls& c = a.cls[0];
+    if (c.ntap != 9 || c.Rc != 3 || c.Sc != 3 || c.oS != 1 || c.P != a.Hi || c.Q != a.Wi || a.Ho != a.Hi ||
+        a.Wo != a.Wi || !grid_ok(c, a.Sw))
+        return 0;
+    for (int i = 0; i < 3; ++i)
+        if (c.cdh[i] < -1 || c.cdh[i] > 1 || c.cdw[i] < -1 || c.cdw[i] > 1) return 0;
+    const int H1 = a.Hi + 1, W2 = a.Wi + 2, PQ = c.P * c.Q, M = a.N * PQ;
+    int maxpix = 0;
+    for (int m0 = 0; m0 < M; m0 += 128) {
+        const int m1 = (m0 + 128 < M ? m0 + 128 : M) - 1;
+        const int b0 = m0 / PQ, p0 = (m0 - b0 * PQ) / c.Q;
+        const int b1 = m1 / PQ, p1 = (m1 - b1 * PQ) / c.Q;
+        const int npix = (b1 * H1 + p1 + 2 - (b0 * H1 + p0) + 1) * W2;
+        maxpix = npix > maxpix ? npix : maxpix;
+    }
+    return (maxpix + 7) / 8 * 1024;
+}
+
+template <int BN, int DIAG, int NB>
+static int launch_halo_v(ConvArgs& a, int hb, hipStream_t st) {
+    ConvCls& c = a.cls[0];
+    const int M = a.N * c.P * c.Q;
+    c.tiles_m = (M + 127) / 128;
+    c.tile_start = 0;
+    a.tiles_total = c.tiles_m * ((a.Nout + BN - 1) / BN);
+    if (a.splits < 1) a.splits = 1;
+    HaloArgs h;
+    h.halo_bytes = hb;
+    h.fd_w2 = FastDiv((uint32_t)(a.Wi + 2));
+    h.fd_h1 = FastDiv((uint32_t)(a.Hi + 1));
+    const size_t lds = (size_t)hb + NB * (size_t)BN * 128;
+    static size_t attr = 0;  // largest dynamic LDS granted so far (idempotent, safe to race)
+    if (lds > attr) {
+        const hipError_t e = hipFuncSetAttribute((const void*)k_conv_halo<BN, DIAG, NB>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) {
+            set_error("k_conv_halo: %zu B of LDS refused (%s)", lds, hipGetErrorString(e));
+            return GM_E_UNSUP;
+        }
+        attr = lds;
+    }
+    k_conv_halo<BN, DIAG, NB><<<a.tiles_total * a.splits, 256, lds, st>>>(a, h);
+    return check_launch("k_conv_halo");
+}
+
+template <int BN>
+static int launch_halo(ConvArgs& a, int hb, hipStream_t st) {
+    const int p = conv_pipe();
+    if (p == 5) return launch_halo_v<BN, 5, 2>(a, hb, st);
+    if (p == 6) return launch_halo_v<BN, 6, 2>(a, hb, st);
+    // a third weight stage when two workgroups per CU still fit (or when asked: pipe 3)
+    if (p == 3 || hb + 3 * BN * 128 <= 80 * 1024 - 256) return launch_halo_v<BN, 0, 3>(a, hb, st);
+    return launch_halo_v<BN, 0, 2>(a, hb, st);
+}
+
 static int pick_and_launch(ConvArgs& a, hipStream_t st, void* ws, size_t ws_bytes) {
     const bool three = stages() == 3;
     TilePick p = pick_tile(a);
-    if (p.splits > 1 && (!ws || ws_bytes < splitk_bytes(p))) {  // no workspace: the unsplit choice
+    if (p.splits > 1 && (!ws || ws_bytes < splitk_bytes(p) || p.tiles > kMaxSplitTiles)) {  // the unsplit choice
         long M = 0;
         for (int i = 0; i < a.ncls; ++i) M += (long)a.N * a.cls[i].P * a.cls[i].Q;
         p = {M / 128 * ((a.Nout + 63) / 64) >= tile_bias() * 3 / 4 ? T128x64 : T64x64, 1, 0};
@@ -752,6 +1221,13 @@ static int pick_and_launch(ConvArgs& a, hipStream_t st, void* ws, size_t ws_byte
         a.spin_limit = spin_limit();
         a.flags = static_cast<unsigned*>(ws);
         a.ws = reinterpret_cast<float*>(static_cast<char*>(ws) + splitk_flag_bytes(p.tiles));
+    }
+    const int hb = halo_bytes(a);
+    if (hb > 0 && hb + 2 * 128 * 128 <= 160 * 1024) {
+        if (p.tile == T128x128) return launch_halo<128>(a, hb, st);
+        a.splits = 1;  // (split-K is only chosen with 128x128 tiles)
+        if (a.Nout >= 128) return launch_halo<128>(a, hb, st);
+        return launch_halo<64>(a, hb, st);
     }
     switch (p.tile) {
     case T128x128: return three ? launch_igemm<128, 128, 3>(a, st) : launch_igemm<128, 128, 2>(a, st);
@@ -939,6 +1415,18 @@ unsigned conv_faults_read(bool clear) {
     return v;
 }
 }  // namespace gm
+
+extern "C" int gm_conv_set_halo(int on) {
+    g_conv_halo = on ? 1 : 0;
+    return GM_OK;
+}
+
+extern "C" int gm_conv_set_pipe(int pipe) {
+    GM_REQUIRE(pipe == 0 || pipe == 2 || pipe == 3 || pipe == 5 || pipe == 6,
+               "gm_conv_set_pipe: 0, 2, 3 (5, 6: timing diagnostics)");
+    g_conv_pipe = pipe;
+    return GM_OK;
+}
 
 extern "C" int gm_conv2d_fwd_hw_bf16(const gm_conv_desc_hw* d, const void* x, const void* w, void* y,
                                      void* stream) {

@@ -279,6 +279,16 @@ int gm_conv2d_dgrad_bf16(const gm_conv_desc* d, const void* dy, const void* wt, 
  * this shape; ws may then be NULL), ZEROED ONCE before first use (the kernel leaves
  * its turnstile words at zero); calls sharing one ws must be stream-ordered. */
 size_t gm_conv2d_splitk_ws_bytes(const gm_conv_desc* d, int dgrad);
+/* Main-loop form of the implicit-GEMM kernel (process-wide; default GM_CONV_PIPE or 0):
+ * 0 = two LDS stages drained at every barrier; 2 / 3 = a 2- / 3-stage LDS ring with one
+ * barrier per k-tile and counted DMA waits (3: the next tile's DMA stays in flight);
+ * 5 / 6 = timing diagnostics only (the 2-stage loop without its DMA / without its math;
+ * outputs meaningless). */
+int gm_conv_set_pipe(int pipe);
+/* 3x3 / stride-1 / pad-1 convolutions (forward and input gradient, C % 64 == 0) stage
+ * the input once per 64-channel chunk as a halo instead of once per tap (default on;
+ * GM_CONV_HALO=0 or gm_conv_set_halo(0) selects the im2col kernel for them). */
+int gm_conv_set_halo(int on);
 int gm_conv2d_fwd_ex_bf16(const gm_conv_desc* d, const void* x, const void* w, void* y, void* ws,
                           size_t ws_bytes, void* stream);
 int gm_conv2d_dgrad_ex_bf16(const gm_conv_desc* d, const void* dy, const void* wt, void* dx, void* ws,

@@ -1,0 +1,45 @@
+"""Run ONE trunk convolution shape repeatedly (for rocprofv3 --pmc passes):
+
+    python tools/conv_one.py --shape l2 --op fwd --pipe 0 --reps 50
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+CL = torch.channels_last
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shape", default="l2")
+    ap.add_argument("--op", default="fwd", choices=["fwd", "dgrad"])
+    ap.add_argument("--pipe", type=int, default=0)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--reps", type=int, default=50)
+    a = ap.parse_args()
+    from greedy_multimodal_learning_amd import _lib as L
+    from greedy_multimodal_learning_amd import conv as G
+    import trunk_table as T
+    dev = torch.device("cuda:0")
+    C, H, W, K, R, st, pad, _ = dict(T.TRUNK)[a.shape]
+    B = a.batch
+    P, Q = (H + 2 * pad - R) // st + 1, (W + 2 * pad - R) // st + 1
+    x = torch.randn(B, C, H, W, device=dev).bfloat16().contiguous(memory_format=CL)
+    w = torch.randn(K, C, R, R, device=dev).bfloat16().contiguous(memory_format=CL)
+    dy = torch.randn(B, K, P, Q, device=dev).bfloat16().contiguous(memory_format=CL)
+    wt = w.permute(1, 0, 2, 3).contiguous(memory_format=CL)
+    L.check(L.load().gm_conv_set_pipe(a.pipe), "set_pipe")
+    fn = (lambda: G.conv_fwd(x, w, st, pad)) if a.op == "fwd" else (lambda: G.conv_dgrad_t(dy, wt, H, W, st, pad))
+    t = T._time(fn, a.reps)
+    flops = 2.0 * B * P * Q * K * C * R * R
+    print(f"{a.shape} {a.op} pipe {a.pipe}: {t * 1e6:.2f} us, {flops / t / 1e12:.1f} TFLOP/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()
