@@ -17,6 +17,8 @@
 #                                                                     -> gpurun_out/pmct_NAME.txt
 #   pmcg:NAME    one rocprofv3 --pmc pass over tools/traffic_probe.py (the fused norms+SGD pass)
 #                                                                     -> gpurun_out/pmcg_NAME.txt
+#   trunkpmc     three rocprofv3 --pmc passes over tools/trunk_pmc.py (FETCH, WRITE, MFMA/LDS set),
+#                per-op table + conv-family traffic json         -> gpurun_out/trunk_pmc.md, trunk_pmc.json
 #   py:FILE      python FILE (a tools/ script)                        -> gpurun_out/py_FILE.log
 set -o pipefail
 mkdir -p gpurun_out
@@ -29,6 +31,7 @@ PMC[mfma]="SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_INS
 PMC[lds]="SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVE_CYCLES"
 PMC[fetch]="FETCH_SIZE"
 PMC[write]="WRITE_SIZE"
+PMC[opmfma]="SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVES"
 
 for s in "$@"; do
   echo "=== $s $(date +%T)"
@@ -80,6 +83,14 @@ for s in "$@"; do
         -- python3 tools/traffic_probe.py > "gpurun_out/pmcg_$n.log" 2>&1 || { tail -30 "gpurun_out/pmcg_$n.log"; exit 22; }
       python3 tools/pmc_table.py "gpurun_out/pmcg_$n" > "gpurun_out/pmcg_$n.txt" && rm -rf "gpurun_out/pmcg_$n"
       grep group_sumsq "gpurun_out/pmcg_$n.txt" ;;
+    trunkpmc)
+      for n in fetch write opmfma; do
+        timeout -s KILL 300 rocprofv3 --pmc ${PMC[$n]} --output-format csv -d "gpurun_out/tp_$n" -o pmc \
+          -- python3 tools/trunk_pmc.py run > "gpurun_out/tp_$n.log" 2>&1 || { tail -30 "gpurun_out/tp_$n.log"; exit 23; }
+      done
+      python3 tools/trunk_pmc.py report gpurun_out/tp_fetch gpurun_out/tp_write gpurun_out/tp_opmfma \
+        --json gpurun_out/trunk_pmc.json > gpurun_out/trunk_pmc.md && rm -rf gpurun_out/tp_fetch gpurun_out/tp_write gpurun_out/tp_opmfma
+      tail -3 gpurun_out/trunk_pmc.md ;;
     py:*)
       f="${s#py:}"; lg="gpurun_out/py_$(basename "$f" .py).log"
       timeout -k 10 600 python -u "$f" > "$lg" 2>&1 || { tail -30 "$lg"; exit 19; }

@@ -69,8 +69,14 @@ def _row(name, op, cnt, flops, nbytes, secs, launches_per_call=1):
 
 
 def conv_rows(B, dev, reps=10):
+    return [_row(name, op, cnt, flops, nbytes, _time(fn, reps)) for name, op, cnt, flops, nbytes, fn in conv_ops(B, dev)]
+
+
+def conv_ops(B, dev):
+    """(name, pass, count per view, FLOPs, algorithmic bytes, callable) of every trunk
+    convolution pass of one view at batch B."""
     from greedy_multimodal_learning_amd import conv as G
-    rows = []
+    out = []
     for name, (C, H, W, K, R, st, pad, cnt) in TRUNK:
         Cp = G._cpad(C)
         P, Q = (H + 2 * pad - R) // st + 1, (W + 2 * pad - R) // st + 1
@@ -83,7 +89,7 @@ def conv_rows(B, dev, reps=10):
         if C == 3:  # the stem runs on the pixel-pair view; its input gradient is never computed
             xp = G.stem_pack_input(x[:, :3], R, R, pad)
             wp = G.stem_pack_weight(w[:, :3].float())
-            ops = [("fwd", lambda: G.stem_fwd(xp, wp, P, Q), xb + wb + yb)]
+            ops = [("fwd", lambda xp=xp, wp=wp, P=P, Q=Q: G.stem_fwd(xp, wp, P, Q), xb + wb + yb)]
             from greedy_multimodal_learning_amd import _lib as L
             import ctypes
             d = G._desc_hw(B, xp.shape[2], xp.shape[3], 8, K, R, wp.shape[3], 2, 1, 0, 0)
@@ -91,25 +97,33 @@ def conv_rows(B, dev, reps=10):
             scr = torch.empty(max(need, 16), device=dev, dtype=torch.uint8)
             dwp = torch.empty(K, R, wp.shape[3], 8, device=dev, dtype=torch.float32)
 
-            def stem_wgrad():
+            def stem_wgrad(d=d, dy=dy, xp=xp, dwp=dwp, scr=scr, need=need):
                 L.check(L.load().gm_conv2d_wgrad_hw_bf16(ctypes.byref(d), dy.data_ptr(), xp.data_ptr(),
                                                          dwp.data_ptr(), 8, 0, scr.data_ptr(), need,
                                                          L.stream_of(dev)), "wgrad_hw")
             ops.append(("wgrad", stem_wgrad, xb + yb + K * C * R * R * 4))
         else:
             dw = torch.empty(K, C, R, R, device=dev, dtype=torch.float32).contiguous(memory_format=CL)
-            ops = [("fwd", lambda: G.conv_fwd(x, w, st, pad), xb + wb + yb),
-                   ("dgrad", lambda: G.conv_dgrad_t(dy, wt, H, W, st, pad), yb + wb + xb),
-                   ("wgrad", lambda: G.conv_wgrad(dy, x, R, R, st, pad, C, out=dw), xb + yb + K * C * R * R * 4)]
+            ops = [("fwd", lambda x=x, w=w, st=st, pad=pad: G.conv_fwd(x, w, st, pad), xb + wb + yb),
+                   ("dgrad", lambda dy=dy, wt=wt, H=H, W=W, st=st, pad=pad: G.conv_dgrad_t(dy, wt, H, W, st, pad),
+                    yb + wb + xb),
+                   ("wgrad", lambda dy=dy, x=x, R=R, st=st, pad=pad, C=C, dw=dw: G.conv_wgrad(dy, x, R, R, st, pad, C,
+                                                                                             out=dw),
+                    xb + yb + K * C * R * R * 4)]
         for op, fn, nbytes in ops:
-            rows.append(_row(name, op, cnt, flops, nbytes, _time(fn, reps)))
-    return rows
+            out.append((name, op, cnt, flops, nbytes, fn))
+    return out
 
 
 def bn_rows(B, dev, reps=10):
+    return [_row(name, op, cnt, flops, nbytes, _time(fn, reps)) for name, op, cnt, flops, nbytes, fn in bn_ops(B, dev)]
+
+
+def bn_ops(B, dev):
+    """The same for every BatchNorm forward/backward of one view and the stem max-pool."""
     from greedy_multimodal_learning_amd import bn as BN
     from greedy_multimodal_learning_amd import pool as PL
-    rows = []
+    out = []
     for name, (C, H, W, res, relu, cnt) in BNS:
         M = B * H * W
         x = torch.randn(B, C, H, W, device=dev).bfloat16().contiguous(memory_format=CL)
@@ -121,29 +135,28 @@ def bn_rows(B, dev, reps=10):
         coef = torch.empty(2 * C, device=dev) if relu and not res else None
         st = {}
 
-        def fwd():
+        def fwd(x=x, w=w, b=b, rm=rm, rv=rv, relu=relu, r=r, coef=coef, st=st):
             st["y"], st["sm"], st["si"] = BN.bn_fwd_train(x, w, b, rm, rv, None, 0.1, 1e-5, relu, r, coef)
         fwd()
         dg, db = torch.empty(C, device=dev), torch.empty(C, device=dev)
         maskx = coef is not None
 
-        def bwd():
+        def bwd(dy=dy, x=x, w=w, relu=relu, res=res, dg=dg, db=db, coef=coef, maskx=maskx, st=st):
             BN.bn_bwd(dy, None if maskx else st["y"], x, w, st["sm"], st["si"], relu, res, dg, db, False,
                       coef if maskx else None)
         e = M * C * 2
-        rows.append(_row(name, "bn_fwd", cnt, 0, e * (2 + (1 if res else 0)), _time(fwd, reps)))
-        rows.append(_row(name, "bn_bwd", cnt, 0, e * (3 + (1 if relu and not maskx else 0) + (1 if res else 0)),
-                         _time(bwd, reps)))
+        out.append((name, "bn_fwd", cnt, 0, e * (2 + (1 if res else 0)), fwd))
+        out.append((name, "bn_bwd", cnt, 0, e * (3 + (1 if relu and not maskx else 0) + (1 if res else 0)), bwd))
     # stem max-pool (3x3/2 on the 112^2 stem output): read x, write y + 1-byte argmax
     x = torch.randn(B, 64, 112, 112, device=dev).bfloat16().contiguous(memory_format=CL).requires_grad_(True)
     pool = PL.GMMaxPool2d(3, 2, 1)
     y = pool(x)
     gy = torch.randn_like(y)
     e_in, e_out = B * 112 * 112 * 64, B * 56 * 56 * 64
-    rows.append(_row("maxpool", "fwd", 1, 0, e_in * 2 + e_out * 3, _time(lambda: pool(x.detach()), reps)))
-    rows.append(_row("maxpool", "bwd", 1, 0, e_out * 3 + e_in * 2,
-                     _time(lambda: torch.autograd.grad(y, x, gy, retain_graph=True), reps)))
-    return rows
+    out.append(("maxpool", "fwd", 1, 0, e_in * 2 + e_out * 3, lambda: pool(x.detach())))
+    out.append(("maxpool", "bwd", 1, 0, e_out * 3 + e_in * 2,
+                lambda: torch.autograd.grad(y, x, gy, retain_graph=True)))
+    return out
 
 
 def measure_family(B, dev, reps=10):
