@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--pipes", default="0,h", help="comma list of pipe numbers; 'h' = halo kernel on")
+    ap.add_argument("--wgrad", action="store_true", help="also time the weight-gradient passes")
     a = ap.parse_args()
     from greedy_multimodal_learning_amd import _lib as L
     from greedy_multimodal_learning_amd import conv as G
@@ -53,6 +54,11 @@ def main():
         ops.append((name, "fwd", cnt, flops, (lambda x=x, w=w, st=st, pad=pad: G.conv_fwd(x, w, st, pad))))
         ops.append((name, "dgrad", cnt, flops,
                     (lambda dy=dy, wt=wt, H=H, W=W, st=st, pad=pad: G.conv_dgrad_t(dy, wt, H, W, st, pad))))
+        if a.wgrad:
+            dw = torch.empty(K, C, R, R, device=dev, dtype=torch.float32).contiguous(memory_format=CL)
+            ops.append((name, "wgrad", cnt, flops,
+                        (lambda dy=dy, x=x, R=R, st=st, pad=pad, C=C, dw=dw: G.conv_wgrad(dy, x, R, R, st, pad, C,
+                                                                                          out=dw))))
     # correctness: pipe variants == variant 0 bitwise; the halo kernel (another
     # summation order) within bf16 output rounding of it
     ref = {}
@@ -92,7 +98,7 @@ def main():
             cells.append(f"{t * 1e6:.1f} ({flops / t / 1e12:.0f})")
         print(f"| {name} | {op} | " + " | ".join(cells) + " |")
     for p in pipes:
-        print(f"{p}: fwd+dgrad family {tot[p][0] / tot[p][1] / 1e12:.1f} TFLOP/s "
+        print(f"{p}: family {tot[p][0] / tot[p][1] / 1e12:.1f} TFLOP/s "
               f"({tot[p][1] * 1e3:.3f} ms per view)")
     select("h")
 
