@@ -334,18 +334,54 @@ __global__ __launch_bounds__(256) void k_conv_wgrad4(WgradArgs a) {
     }
 }
 
-// stage 1 (many splits): part2[g][i] = sum of splits 8g..8g+7 (fixed order), float4 lanes,
-// grid (slab/1024, groups): parallel over splits so the reduce is bandwidth-, not latency-bound
-__global__ __launch_bounds__(256) void k_wgrad_sum8(const float* part, int splits, size_t slab, float* part2) {
-    const size_t i4 = ((size_t)blockIdx.x * 256 + threadIdx.x) * 4;
-    if (i4 >= slab) return;
-    const int g = blockIdx.y, s0 = g * 8, s1 = min(splits, s0 + 8);
+// dw[i] (+)= sum over splits of part[s][i] in ONE launch, for the uncropped case (Cp == Cr,
+// every layer but the RGB stem).  A block covers 256/R float4 columns with R split lanes
+// per column: lane r sums splits r, r+R, ... (four loads in flight), the R lane sums are
+// then combined in lane order through LDS - a fixed summation order for a given shape,
+// so the result is deterministic.  R is picked on the host so that small slabs (layer 1:
+// 9k float4 columns x 100 splits) still spread over hundreds of blocks.
+template <int R>
+__global__ __launch_bounds__(256) void k_wgrad_sum(const float* __restrict__ part, int splits, size_t slab,
+                                                   int accumulate, float* __restrict__ dw) {
+    constexpr int CPB = 256 / R;
+    const int t = threadIdx.x, col = t % CPB, r = t / CPB;
+    const size_t i4 = ((size_t)blockIdx.x * CPB + col) * 4;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int s = s0; s < s1; ++s) {
-        const float4 v = *(const float4*)(part + (size_t)s * slab + i4);
+    if (i4 < slab) {
+        const float* p = part + i4;
+        int s = r;
+        for (; s + 3 * R < splits; s += 4 * R) {
+            float4 v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = *(const float4*)(p + (size_t)(s + j * R) * slab);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                acc.x += v[j].x; acc.y += v[j].y; acc.z += v[j].z; acc.w += v[j].w;
+            }
+        }
+        for (; s < splits; s += R) {
+            const float4 v = *(const float4*)(p + (size_t)s * slab);
+            acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        }
+    }
+    if constexpr (R > 1) {
+        __shared__ float4 red[256];
+        red[t] = acc;
+        __syncthreads();
+        if (r != 0) return;
+#pragma unroll
+        for (int q = 1; q < R; ++q) {
+            const float4 v = red[q * CPB + col];
+            acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        }
+    }
+    if (i4 >= slab) return;
+    float4* o = (float4*)(dw + i4);
+    if (accumulate) {
+        const float4 v = *o;
         acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
-    *(float4*)(part2 + (size_t)g * slab + i4) = acc;
+    *o = acc;
 }
 
 // dw = sum over splits (fixed order); also the [K][T][Cpad] -> [K][T][Creal] crop
@@ -440,8 +476,7 @@ extern "C" size_t gm_conv2d_wgrad_hw_scratch(const gm_conv_desc_hw* d) {
     if (!d || d->stride_h < 1 || d->stride_w < 1) return 0;
     const WPlan w = plan(d);
     const size_t slab = (size_t)d->K * d->R * d->S * d->C;
-    const int groups = w.splits > 8 ? (w.splits + 7) / 8 : 0;
-    return (size_t)(w.splits + groups) * slab * sizeof(float);
+    return (size_t)w.splits * slab * sizeof(float);
 }
 
 extern "C" size_t gm_conv2d_wgrad_scratch(const gm_conv_desc* d) {
@@ -500,23 +535,26 @@ extern "C" int gm_conv2d_wgrad_hw_bf16(const gm_conv_desc_hw* d, const void* dy,
         rc = check_launch("k_conv_wgrad");
     }
     if (rc) return rc;
+    const size_t slab = (size_t)d->K * a.T * d->C;
+    if (c_real == d->C) {  // one-launch split reduction (slab is a multiple of 4: K % 8 == 0)
+        const size_t ncol = slab / 4;
+        int R = 1;  // split lanes per column: aim for >= 512 blocks without idle lanes
+        while (R < 32 && R * 2 <= a.splits && (ncol * R + 255) / 256 < 512) R *= 2;
+        const unsigned g = (unsigned)((ncol + 256 / R - 1) / (256 / R));
+        switch (R) {
+            case 1: k_wgrad_sum<1><<<g, 256, 0, st>>>(a.part, a.splits, slab, accumulate, dw); break;
+            case 2: k_wgrad_sum<2><<<g, 256, 0, st>>>(a.part, a.splits, slab, accumulate, dw); break;
+            case 4: k_wgrad_sum<4><<<g, 256, 0, st>>>(a.part, a.splits, slab, accumulate, dw); break;
+            case 8: k_wgrad_sum<8><<<g, 256, 0, st>>>(a.part, a.splits, slab, accumulate, dw); break;
+            case 16: k_wgrad_sum<16><<<g, 256, 0, st>>>(a.part, a.splits, slab, accumulate, dw); break;
+            default: k_wgrad_sum<32><<<g, 256, 0, st>>>(a.part, a.splits, slab, accumulate, dw); break;
+        }
+        return check_launch("k_wgrad_sum");
+    }
     const size_t n = (size_t)d->K * a.T * c_real;
     int g = (int)((n + 255) / 256);
     if (g > 4096) g = 4096;
-    const size_t slab = (size_t)d->K * a.T * d->C;
-    const float* src = a.part;
-    int nsrc = a.splits;
-    if (a.splits > 8) {
-        const int groups = (a.splits + 7) / 8;
-        float* part2 = a.part + (size_t)a.splits * slab;
-        dim3 g1((unsigned)((slab / 4 + 255) / 256), groups);
-        k_wgrad_sum8<<<g1, 256, 0, st>>>(a.part, a.splits, slab, part2);
-        rc = check_launch("k_wgrad_sum8");
-        if (rc) return rc;
-        src = part2;
-        nsrc = groups;
-    }
-    k_wgrad_reduce<<<g, 256, 0, st>>>(src, nsrc, d->K, a.T, d->C, c_real, accumulate, dw);
+    k_wgrad_reduce<<<g, 256, 0, st>>>(a.part, a.splits, d->K, a.T, d->C, c_real, accumulate, dw);
     return check_launch("k_wgrad_reduce");
 }
 
