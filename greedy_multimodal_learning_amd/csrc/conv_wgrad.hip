@@ -13,8 +13,10 @@
 // waves of 32x32, v_mfma_f32_32x32x16_bf16), double-buffered register-staged
 // loads, split-K over pixels into fp32 partial slabs, then a fixed-order reduce
 // (deterministic, no atomics).
+#include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "gm_common.h"
 
@@ -37,6 +39,7 @@ struct WgradArgs {
     FastDiv fd_pq, fd_q;        // pixel -> (b, p, q) without integer division
     int accumulate;             // k_conv_wgrad4 with one split: add into part (= dw) instead of storing
     int S, padh, padw;          // k_conv_wgrad4 decodes taps arithmetically
+    int adv_b, adv_p, adv_q;    // one 64-pixel step in (b, p, q): 64 = adv_b*P*Q + adv_p*Q + adv_q
     signed char dh[kWTap], dw[kWTap];
 };
 
@@ -47,6 +50,45 @@ __device__ __forceinline__ bf16x8 tr_frag(const uint16_t* base_row0, const uint1
     const short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)base_row4);
     const short8_t s = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     return __builtin_bit_cast(bf16x8, s);
+}
+
+// ds_read_b64_tr_b16 as inline asm for k_conv_wgrad4: the builtin form makes hipcc wait
+// vmcnt(0) for every LDS-DMA in flight before each transposed read (it cannot tell the
+// DMA's LDS destination from the read's buffer), which serialised the next step's DMA with
+// this step's MFMAs.  The asm reads are invisible to the compiler's lgkmcnt tracking, so
+// the caller waits for them explicitly (wait_lgkm0 on the fragments it is about to use).
+template <int OFF>
+__device__ __forceinline__ short4_t tr_rd(unsigned a) {
+    short4_t d;
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(d) : "v"(a), "i"(OFF));
+    return d;
+}
+
+// fragment of k-slice ks (rows 16ks + {q, q+4}) at immediate offsets BASE + ks*16*R (+4R)
+template <int BASE, int R>
+__device__ __forceinline__ bf16x8 tr_frag_asm(int ks, unsigned a) {
+    short4_t lo, hi;
+    switch (ks) {
+        case 0: lo = tr_rd<BASE>(a); hi = tr_rd<BASE + 4 * R>(a); break;
+        case 1: lo = tr_rd<BASE + 16 * R>(a); hi = tr_rd<BASE + 20 * R>(a); break;
+        case 2: lo = tr_rd<BASE + 32 * R>(a); hi = tr_rd<BASE + 36 * R>(a); break;
+        default: lo = tr_rd<BASE + 48 * R>(a); hi = tr_rd<BASE + 52 * R>(a); break;
+    }
+    const short8_t s = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, s);
+}
+
+// lgkmcnt(0), tied to the fragments (MT + NT of them) the next MFMAs read
+template <int MT, int NT>
+__device__ __forceinline__ void wait_lgkm0(bf16x8 (&a)[MT], bf16x8 (&b)[NT]) {
+    if constexpr (MT == 2 && NT == 2)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(a[1]), "+v"(b[0]), "+v"(b[1]));
+    else if constexpr (MT == 2)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(a[1]), "+v"(b[0]));
+    else if constexpr (NT == 2)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]), "+v"(b[1]));
+    else
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]));
 }
 
 __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a) {
@@ -201,9 +243,12 @@ __global__ __launch_bounds__(256) void k_conv_wgrad4(WgradArgs a) {
         a_cok[j] = col < a.Kc;
         a_ptr[j] = a.dy + ((size_t)step0 * BK + a_row[j]) * a.Kc + (a_cok[j] ? col : 0);
     }
-    // B (x) DMA lanes: fixed (tap, channel chunk) per instruction
+    // B (x) DMA lanes: fixed (tap, channel chunk) per instruction; the lane's pixel
+    // (b, p, q) is decoded once and then advanced by one 64-pixel step per issue
+    // (adv_*: no per-step division in the issue path)
     const int b_rsub = lane / LPB, b_slot = lane % LPB;
     int b_row[GB], b_toff[GB], b_dh[GB], b_dw[GB];
+    int b_b[GB], b_p[GB], b_q[GB];
     bool b_cok[GB];
 #pragma unroll
     for (int j = 0; j < GB; ++j) {
@@ -215,6 +260,11 @@ __global__ __launch_bounds__(256) void k_conv_wgrad4(WgradArgs a) {
         b_dh[j] = r - a.padh;
         b_dw[j] = s - a.padw;
         b_toff[j] = ((b_dh[j] * a.W + b_dw[j]) << a.logC) + (col & (a.C - 1));
+        const int m = step0 * BK + b_row[j];
+        b_b[j] = (int)a.fd_pq.div((uint32_t)m);
+        const int pq = m - b_b[j] * PQ;
+        b_p[j] = (int)a.fd_q.div((uint32_t)pq);
+        b_q[j] = pq - b_p[j] * a.Q;
     }
     typedef __attribute__((address_space(1))) const void* gptr_t;
     typedef __attribute__((address_space(3))) void* lptr_t;
@@ -229,16 +279,20 @@ __global__ __launch_bounds__(256) void k_conv_wgrad4(WgradArgs a) {
         }
 #pragma unroll
         for (int j = 0; j < GB; ++j) {
-            const int m = (step0 + i) * BK + b_row[j];
-            const int b = (int)a.fd_pq.div((uint32_t)m), pq = m - b * PQ;
-            const int p = (int)a.fd_q.div((uint32_t)pq), q = pq - p * a.Q;
-            const int hi = p * a.sth + b_dh[j], wi = q * a.stw + b_dw[j];
-            const bool ok = b_cok[j] && m < M && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
-            const int pix = (b * a.H + p * a.sth) * a.W + q * a.stw;
+            const int b = b_b[j], p = b_p[j], q = b_q[j];
+            const int h0 = p * a.sth, w0 = q * a.stw;
+            const int hi = h0 + b_dh[j], wi = w0 + b_dw[j];
+            const bool ok = b_cok[j] && b < a.N && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+            const int pix = (b * a.H + h0) * a.W + w0;
             const void* src =
                 ok ? (const void*)(a.x + (((long)pix << a.logC) + b_toff[j])) : (const void*)g_wzero16;
             __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + bufoff + SA + (wave * GB + j) * 1024), 16,
                                              0, 0);
+            // next step's pixel: + 64 = (adv_b, adv_p, adv_q), one carry per component at most
+            int nq = q + a.adv_q, np = p + a.adv_p, nb = b + a.adv_b;
+            if (nq >= a.Q) { nq -= a.Q; ++np; }
+            if (np >= a.P) { np -= a.P; ++nb; }
+            b_b[j] = nb; b_p[j] = np; b_q[j] = nq;
         }
     };
 
@@ -265,40 +319,52 @@ __global__ __launch_bounds__(256) void k_conv_wgrad4(WgradArgs a) {
         const int c = wn * (32 * NT) + 32 * j + 16 * (g & 1) + 4 * p4;
         b_base[j] = SA + rbase * RB + (((c >> 3) ^ wswz<RB>(rbase)) << 4) + (c & 7) * 2;
     }
-    auto compute = [&](const int bufoff) {
+    unsigned a_lds[MT], b_lds[NT];  // LDS byte addresses of the fragment bases
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+        a_lds[i] = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)(lds + a_base[i]);
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+        b_lds[j] = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)(lds + b_base[j]);
+    // one k-slice's fragments (asm reads; the caller waits), then its MFMAs; the next
+    // slice's reads are issued before this slice's MFMAs
+    auto compute = [&](auto bufc) {
+        constexpr int BO = decltype(bufc)::value;
+        bf16x8 af[2][MT], bfr[2][NT];
+        auto load = [&](int ks, int c) {
+#pragma unroll
+            for (int i = 0; i < MT; ++i) af[c][i] = tr_frag_asm<BO, RA>(ks, a_lds[i]);
+#pragma unroll
+            for (int j = 0; j < NT; ++j) bfr[c][j] = tr_frag_asm<BO, RB>(ks, b_lds[j]);
+        };
+        load(0, 0);
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
-            bf16x8 af[MT], bfr[NT];
-#pragma unroll
-            for (int i = 0; i < MT; ++i) {
-                const char* p = lds + bufoff + a_base[i] + ks * 16 * RA;
-                af[i] = tr_frag((const uint16_t*)p, (const uint16_t*)(p + 4 * RA));
-            }
-#pragma unroll
-            for (int j = 0; j < NT; ++j) {
-                const char* p = lds + bufoff + b_base[j] + ks * 16 * RB;
-                bfr[j] = tr_frag((const uint16_t*)p, (const uint16_t*)(p + 4 * RB));
-            }
+            const int c = ks & 1;
+            wait_lgkm0<MT, NT>(af[c], bfr[c]);
+            if (ks < 3) load(ks + 1, c ^ 1);
 #pragma unroll
             for (int i = 0; i < MT; ++i)
 #pragma unroll
                 for (int j = 0; j < NT; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[c][i], bfr[c][j], acc[i][j], 0, 0, 0);
         }
     };
     constexpr int BUF1 = SA + SB;
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, BUF1>;
     if (nst > 0) issue(0, 0);
     __syncthreads();
     int i = 0;
     for (; i + 1 < nst; i += 2) {  // steps i (buffer 0) and i+1 (buffer 1)
         issue(i + 1, BUF1);
-        compute(0);
+        compute(B0{});
         __syncthreads();
         if (i + 2 < nst) issue(i + 2, 0);
-        compute(BUF1);
+        compute(B1{});
         __syncthreads();
     }
-    if (i < nst) compute(0);  // odd step count: the last step sits in buffer 0
+    if (i < nst) compute(B0{});  // odd step count: the last step sits in buffer 0
 
     float* out = a.part + (size_t)split * a.Kc * TC;
     const bool inner = k0 + BM <= a.Kc && n0 + BN <= TC;
@@ -461,7 +527,7 @@ static int launch_wgrad4(const WgradArgs& a, int grid, hipStream_t st) {
     const size_t lds = (size_t)2 * 64 * 2 * (64 * MT + 64 * NT);
     static bool attr = false;  // idempotent, safe to race
     if (!attr) {
-        hipFuncSetAttribute((const void*)k_conv_wgrad4<MT, NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute((const void*)k_conv_wgrad4<MT, NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr = true;
     }
     k_conv_wgrad4<MT, NT><<<grid, 256, lds, st>>>(a);
@@ -508,6 +574,9 @@ extern "C" int gm_conv2d_wgrad_hw_bf16(const gm_conv_desc_hw* d, const void* dy,
     a.Kc = d->K; a.T = d->R * d->S; a.sth = d->stride_h; a.stw = d->stride_w;
     a.fd_pq = FastDiv((uint32_t)(a.P * a.Q));
     a.fd_q = FastDiv((uint32_t)a.Q);
+    a.adv_b = 64 / (a.P * a.Q);
+    a.adv_p = (64 % (a.P * a.Q)) / a.Q;
+    a.adv_q = (64 % (a.P * a.Q)) % a.Q;
     for (int r = 0; r < d->R; ++r)
         for (int s = 0; s < d->S; ++s) {
             a.dh[r * d->S + s] = (signed char)(r - d->pad_h);
