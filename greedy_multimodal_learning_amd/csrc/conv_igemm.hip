@@ -19,8 +19,10 @@
 // so the ds_read_b128 fragment reads are conflict-free; fp32 accumulation; weights are
 // the MFMA A operand so each lane holds 4 consecutive output channels of one pixel and
 // the epilogue writes 8-B NHWC chunks directly.  Out-of-range taps read zeros.
+#include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "gm_common.h"
 
@@ -949,6 +951,242 @@ __global__ __launch_bounds__(256) void k_conv_halo(ConvArgs a, HaloArgs h) {
     }
 }
 
+// ---------------------------------------------------------------------------------
+// 3x3 / stride-1 convolutions with 64 input and 64 output channels (ResNet layer 1:
+// forward and input gradient).  The whole weight tensor (9 taps x 64 x 64 bf16 = 72 KB)
+// stays resident in LDS for the life of a persistent workgroup, which walks output tiles
+// of RT whole image rows (RT*W <= 128 pixels; MFMA rows past RT*W are padding whose
+// outputs are not stored).  A tile's input is its (RT+2) x (W+2) zero-bordered halo
+// (29 KB at 56x56), DMA'd into the second of two halo buffers while the MFMAs of the
+// current tile run, so the only bytes staged per tile are the halo - instead of nine
+// 16 KB im2col A tiles plus 72 KB of weights in the im2col kernel - and the k-loop is
+// LDS reads + MFMAs only.  Halo pixels are 128-B rows XOR-swizzled as in k_conv_halo;
+// weights are [tap][n][128 B] with the same swizzle on n.
+// LDS fragment read as inline asm (k_conv_rw): hipcc cannot count these, so the kernel
+// waits for them itself with counted lgkmcnt waits tied to the fragments; that keeps two
+// k-steps of reads in flight, where the compiler's own waits drained all of them
+template <int OFF>
+__device__ __forceinline__ bf16x8 lds_rd128(unsigned addr) {
+    bf16x8 d;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "i"(OFF));
+    return d;
+}
+
+struct RwArgs {
+    int RT;        // image rows per tile
+    int tpi;       // tiles per image (H / RT)
+    int tiles;     // N * tpi
+    int hbytes;    // one halo buffer (multiple of 1 KB)
+    int nI;        // halo DMA instructions per tile
+    int npix;      // (RT + 2) * (W + 2)
+    FastDiv fd_w2, fd_tpi;
+};
+
+constexpr int kRwWeightBytes = 9 * 64 * 128;
+
+template <int DIAG>  // DIAG (timing diagnostics, outputs meaningless): 1 = no halo wait, 2 = no MFMA
+__global__ __launch_bounds__(256) void k_conv_rw(ConvArgs a, RwArgs r) {
+    extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+    char* lds = reinterpret_cast<char*>(smem);  // [weights][halo 0][halo 1]
+    constexpr int WB = kRwWeightBytes;
+    const ConvCls& cl = a.cls[0];
+    const int H = a.Hi, W = a.Wi, W2 = W + 2;
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int slot = lane & 7, fr = lane & 31, fh = lane >> 5;
+    const unsigned pk_dh = cl.pk_dh, pk_dw = cl.pk_dw, pk_r = cl.pk_r, pk_s = cl.pk_s;
+    typedef __attribute__((address_space(1))) const void* gptr_t;
+    typedef __attribute__((address_space(3))) void* lptr_t;
+    int tl = blockIdx.x;
+    if (tl >= r.tiles) return;
+
+    // weights, once: instruction I = tap (I >> 3), rows n = 8 (I & 7) .. + 7
+    for (int I = wave; I < 72; I += 4) {
+        const int tp = I >> 3, n = (I & 7) * 8 + (lane >> 3);
+        const int ti = tp / 3, tj = tp - ti * 3;
+        const int tw = (int)((pk_r >> (4 * ti)) & 15u) * a.Sw + (int)((pk_s >> (4 * tj)) & 15u);
+        const int gc = slot ^ ((n >> 1) & 7);
+        __builtin_amdgcn_global_load_lds((gptr_t)(a.wt + ((size_t)n * a.T + tw) * 64 + gc * 8),
+                                         (lptr_t)(lds + I * 1024), 16, 0, 0);
+    }
+    // the halo of tile tl (image b, output rows p0 .. p0+RT-1) into buffer bb.  The halo's
+    // geometry relative to the tile origin is the same for every tile, so each lane's
+    // source offsets (kMaxHI instructions per wave at most) are decoded once: per tile only
+    // the origin and the image-border rows (top row valid iff p0 > 0, bottom iff p0+RT < H).
+    constexpr int kMaxHI = 12;
+    int h_rel[kMaxHI];
+    unsigned h_cls = 0;  // 2 bits per instruction: 0 always, 1 top row, 2 bottom row, 3 never
+#pragma unroll
+    for (int j = 0; j < kMaxHI; ++j) {
+        const int I = wave + 4 * j;
+        const int hp = I * 8 + (lane >> 3);
+        const int rr = (int)r.fd_w2.div((uint32_t)hp), c = hp - rr * W2;
+        const int gc = slot ^ ((hp >> 1) & 7);
+        h_rel[j] = ((rr - 1) * W + c - 1) * 64 + gc * 8;
+        unsigned k = rr == 0 ? 1u : rr == r.RT + 1 ? 2u : 0u;
+        if (I >= r.nI || hp >= r.npix || c == 0 || c == W + 1) k = 3u;
+        h_cls |= k << (2 * j);
+    }
+    auto issue_halo = [&](int tile, int bb) {
+        const int b = (int)r.fd_tpi.div((uint32_t)tile);
+        const int p0 = (tile - b * r.tpi) * r.RT;
+        const uint16_t* origin = a.in + ((size_t)(b * H + p0) * W << 6);
+        const unsigned okmask = 1u | (p0 > 0 ? 2u : 0u) | (p0 + r.RT < H ? 4u : 0u);  // bit k: class k valid
+        char* base = lds + WB + bb * r.hbytes;
+#pragma unroll
+        for (int j = 0; j < kMaxHI; ++j) {
+            const int I = wave + 4 * j;
+            if (I >= r.nI) break;
+            const bool ok = (okmask >> ((h_cls >> (2 * j)) & 3u)) & 1u;
+            const void* src = ok ? (const void*)(origin + h_rel[j]) : (const void*)g_zero16;
+            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(base + I * 1024), 16, 0, 0);
+        }
+    };
+    issue_halo(tl, 0);
+
+    // tile-invariant fragment geometry: MFMA row block i of this wave -> tile pixel
+    const int valid = r.RT * W;
+    int hbase[2], prow[2], pcol[2];
+    bool pok[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        int m = wm * 64 + i * 32 + fr;
+        pok[i] = m < valid;
+        m = pok[i] ? m : 0;
+        prow[i] = m / W;
+        pcol[i] = m - prow[i] * W;
+        hbase[i] = (prow[i] + 1) * W2 + pcol[i] + 1;
+    }
+    const int nb = wn * 32 + fr;
+    const int b0 = nb * 128 + ((fh ^ ((nb >> 1) & 7)) << 4);  // B fragment, tap 0, k-step 0
+    int b_ks[4];  // per k-step (the tap adds an immediate tap * 8192)
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) b_ks[ks] = b0 ^ (ks << 5);
+
+    constexpr int kWaitAll = (7 << 4) | (15 << 8);  // s_waitcnt vmcnt(0)
+    constexpr int kStores = 8;                      // epilogue stores per wave per tile
+    constexpr int kWaitStores = kStores | (7 << 4) | (15 << 8);  // vmcnt(kStores)
+    __builtin_amdgcn_s_waitcnt(kWaitAll);
+    __builtin_amdgcn_s_barrier();
+    const size_t out_bytes = (size_t)a.N * a.Ho * a.Wo * a.Nout * 2;
+    const __amdgpu_buffer_rsrc_t orsrc =
+        __builtin_amdgcn_make_buffer_rsrc(cl.out, 0, (int)(out_bytes < 0x7fffffffu ? out_bytes : 0x7fffffffu),
+                                          0x00020000);
+
+    int bb = 0;
+    for (; tl < r.tiles; tl += gridDim.x) {
+        const int nx = tl + gridDim.x;
+        if (nx < r.tiles) issue_halo(nx, bb ^ 1);  // buffer bb^1 was released by the last barrier
+        const int hoff = WB + bb * r.hbytes;
+
+        floatx16 acc[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+        bf16x8 af[3][2], bfr[3];
+        unsigned abase[2];
+        const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
+        auto tap_base = [&](int tp) {
+            const int ti = tp / 3, tj = tp - ti * 3;
+            const int dh = (int)((pk_dh >> (4 * ti)) & 15u) - 8, dw = (int)((pk_dw >> (4 * tj)) & 15u) - 8;
+            const int toff = dh * W2 + dw;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int hp = hbase[i] + toff;
+                abase[i] = lds0 + ((unsigned)(hoff + (hp << 7)) | (unsigned)((((hp >> 1) & 7) ^ fh) << 4));
+            }
+        };
+        auto load_b = [&](auto tpc, int ks, int c) {
+            constexpr int TP = decltype(tpc)::value;  // ds offsets are 16-bit: tap 8 moves the base
+            if constexpr (TP < 8) bfr[c] = lds_rd128<TP * 8192>(lds0 + (unsigned)b_ks[ks]);
+            else bfr[c] = lds_rd128<0>(lds0 + (unsigned)b_ks[ks] + TP * 8192u);
+        };
+        auto load = [&](int k, int c) {  // k-step k = 4 * tap + ks
+            const int tp = k >> 2, ks = k & 3;
+            if (ks == 0) tap_base(tp);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) af[c][i] = lds_rd128<0>(abase[i] ^ (unsigned)(ks << 5));
+            switch (tp) {
+                case 0: load_b(std::integral_constant<int, 0>{}, ks, c); break;
+                case 1: load_b(std::integral_constant<int, 1>{}, ks, c); break;
+                case 2: load_b(std::integral_constant<int, 2>{}, ks, c); break;
+                case 3: load_b(std::integral_constant<int, 3>{}, ks, c); break;
+                case 4: load_b(std::integral_constant<int, 4>{}, ks, c); break;
+                case 5: load_b(std::integral_constant<int, 5>{}, ks, c); break;
+                case 6: load_b(std::integral_constant<int, 6>{}, ks, c); break;
+                case 7: load_b(std::integral_constant<int, 7>{}, ks, c); break;
+                default: load_b(std::integral_constant<int, 8>{}, ks, c); break;
+            }
+        };
+        // fragments two k-steps ahead (one wave per SIMD: 64 MFMA cycles per k-step do not
+        // cover an LDS round trip): before k-step k's MFMAs only its own three reads are
+        // waited for, k+1's and k+2's stay in flight
+        load(0, 0);
+        load(1, 1);
+#pragma unroll
+        for (int k = 0; k < 36; ++k) {
+            const int c = k % 3;
+            if (k + 2 < 36) load(k + 2, (k + 2) % 3);
+            if (k + 2 < 36)
+                asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(af[c][0]), "+v"(af[c][1]), "+v"(bfr[c]));
+            else if (k + 1 < 36)
+                asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(af[c][0]), "+v"(af[c][1]), "+v"(bfr[c]));
+            else
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[c][0]), "+v"(af[c][1]), "+v"(bfr[c]));
+            if (DIAG != 2) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+                    acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[c], af[c][i], acc[i], 0, 0, 0);
+            }
+        }
+
+        // epilogue: rows p0 + prow, columns pcol; 4 consecutive output channels per store.
+        // The addend (fused gradient join) is loaded for the whole tile first, so its loads
+        // are in flight together instead of one dependent round trip per store.
+        const int b = (int)r.fd_tpi.div((uint32_t)tl);
+        const int p0 = (tl - b * r.tpi) * r.RT;
+        size_t off[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int ho = (p0 + prow[i]) * cl.oS + cl.oH, wo = pcol[i] * cl.oS + cl.oW;
+            off[i] = ((size_t)(b * a.Ho + ho) * a.Wo + wo) * a.Nout + wn * 32 + 4 * fh;
+        }
+        uint2 av[2][4];
+        if (a.addend) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int gq = 0; gq < 4; ++gq)
+                    av[i][gq] = *(const uint2*)(a.addend + off[i] + 8 * gq);  // rows past RT*W read row 0
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+#pragma unroll
+            for (int gq = 0; gq < 4; ++gq) {
+                float o0 = acc[i][4 * gq], o1 = acc[i][4 * gq + 1];
+                float o2 = acc[i][4 * gq + 2], o3 = acc[i][4 * gq + 3];
+                if (a.addend) {
+                    o0 += bf_lo(av[i][gq].x); o1 += bf_hi(av[i][gq].x);
+                    o2 += bf_lo(av[i][gq].y); o3 += bf_hi(av[i][gq].y);
+                }
+                typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+                const u32x2 v = {pack_bf2(o0, o1), pack_bf2(o2, o3)};
+                // every wave issues exactly kStores stores (padding rows get an offset past
+                // the buffer's range, which the hardware drops), so the wait below can count them
+                __builtin_amdgcn_raw_buffer_store_b64(v, orsrc, pok[i] ? (unsigned)((off[i] + 8 * gq) * 2) : 0xfffffff0u,
+                                                      0, 0);
+            }
+        }
+        // the next tile's halo (issued before these stores) has landed; the stores may
+        // still be in flight.  Then every wave is done with buffer bb.
+        if (DIAG != 1) __builtin_amdgcn_s_waitcnt(kWaitStores);
+        __builtin_amdgcn_s_barrier();
+        bb ^= 1;
+    }
+}
+
 // zero the output pixels no dgrad class covers (e.g. odd pixels of a 1x1/s2 dgrad), or
 // copy the addend there when the dgrad is fused with a gradient join
 __global__ void k_zero_bf16(uint16_t* p, size_t n, const uint16_t* src) {
@@ -1197,6 +1435,60 @@ static int launch_halo_v(ConvArgs& a, int hb, hipStream_t st) {
     return check_launch("k_conv_halo");
 }
 
+static int g_conv_rw = [] {
+    const char* e = getenv("GM_CONV_RW");  // 0: layer-1 shapes take the im2col kernel
+    return e ? atoi(e) : 1;
+}();
+
+// the resident-weight kernel serves one-class 3x3 / stride-1 / same-size convolutions with
+// C = Nout = 64 and tap offsets in [-1, 1]; returns its LDS bytes (0 = not eligible)
+static size_t rw_plan(const ConvArgs& a, RwArgs& r) {
+    if (!g_conv_rw || a.ncls != 1 || a.C != 64 || a.Nout != 64 || a.T != 9 || a.sAh != 1 || a.sAw != 1) return 0;
+    const ConvCls& c = a.cls[0];
+    if (c.ntap != 9 || c.Rc != 3 || c.Sc != 3 || c.oS != 1 || c.P != a.Hi || c.Q != a.Wi || a.Ho != a.Hi ||
+        a.Wo != a.Wi || !grid_ok(c, a.Sw) || a.Wi > 128)
+        return 0;
+    if ((size_t)a.N * a.Ho * a.Wo * a.Nout * 2 >= 0x7ffff000u) return 0;  // 32-bit buffer offsets
+    for (int i = 0; i < 3; ++i)
+        if (c.cdh[i] < -1 || c.cdh[i] > 1 || c.cdw[i] < -1 || c.cdw[i] > 1) return 0;
+    int RT = 128 / a.Wi;
+    if (RT > a.Hi) RT = a.Hi;
+    while (RT > 1 && a.Hi % RT) --RT;
+    r.RT = RT;
+    r.tpi = a.Hi / RT;
+    r.tiles = a.N * r.tpi;
+    r.npix = (RT + 2) * (a.Wi + 2);
+    r.nI = (r.npix + 7) / 8;
+    if (r.nI > 48) return 0;  // k_conv_rw decodes at most 12 halo instructions per wave
+    r.hbytes = r.nI * 1024;
+    r.fd_w2 = FastDiv((uint32_t)(a.Wi + 2));
+    r.fd_tpi = FastDiv((uint32_t)r.tpi);
+    const size_t lds = (size_t)kRwWeightBytes + 2 * (size_t)r.hbytes;
+    return lds <= 160 * 1024 ? lds : 0;
+}
+
+static int launch_rw(const ConvArgs& a, const RwArgs& r, size_t lds, hipStream_t st) {
+    static size_t granted = 0;  // largest dynamic LDS granted so far (idempotent, safe to race)
+    if (lds > granted) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_conv_rw<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)lds);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void*)k_conv_rw<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void*)k_conv_rw<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) {
+            set_error("k_conv_rw: %zu B of LDS refused (%s)", lds, hipGetErrorString(e));
+            return GM_E_UNSUP;
+        }
+        granted = lds;
+    }
+    const int grid = r.tiles < 256 ? r.tiles : 256;  // persistent: one workgroup per CU
+    if (g_conv_rw == 2) k_conv_rw<1><<<grid, 256, lds, st>>>(a, r);       // timing diagnostics
+    else if (g_conv_rw == 3) k_conv_rw<2><<<grid, 256, lds, st>>>(a, r);
+    else k_conv_rw<0><<<grid, 256, lds, st>>>(a, r);
+    return check_launch("k_conv_rw");
+}
+
 template <int BN>
 static int launch_halo(ConvArgs& a, int hb, hipStream_t st) {
     const int p = conv_pipe();
@@ -1209,6 +1501,11 @@ static int launch_halo(ConvArgs& a, int hb, hipStream_t st) {
 
 static int pick_and_launch(ConvArgs& a, hipStream_t st, void* ws, size_t ws_bytes) {
     const bool three = stages() == 3;
+    {
+        RwArgs r;
+        const size_t lds = rw_plan(a, r);
+        if (lds > 0) return launch_rw(a, r, lds, st);
+    }
     TilePick p = pick_tile(a);
     if (p.splits > 1 && (!ws || ws_bytes < splitk_bytes(p) || p.tiles > kMaxSplitTiles)) {  // the unsplit choice
         long M = 0;
@@ -1418,6 +1715,11 @@ unsigned conv_faults_read(bool clear) {
 
 extern "C" int gm_conv_set_halo(int on) {
     g_conv_halo = on ? 1 : 0;
+    return GM_OK;
+}
+
+extern "C" int gm_conv_set_rw(int on) {
+    g_conv_rw = on;  // 0 off, 1 on (2, 3: timing diagnostics without halo wait / MFMA)
     return GM_OK;
 }
 

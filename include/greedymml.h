@@ -289,6 +289,10 @@ int gm_conv_set_pipe(int pipe);
  * the input once per 64-channel chunk as a halo instead of once per tap (default on;
  * GM_CONV_HALO=0 or gm_conv_set_halo(0) selects the im2col kernel for them). */
 int gm_conv_set_halo(int on);
+/* Resident-weight kernel for 3x3 / stride-1 convolutions with 64 -> 64 channels (ResNet
+ * layer 1, forward and input gradient; default on, GM_CONV_RW=0 at load or
+ * gm_conv_set_rw(0) selects the im2col kernel for them). */
+int gm_conv_set_rw(int on);
 int gm_conv2d_fwd_ex_bf16(const gm_conv_desc* d, const void* x, const void* w, void* y, void* ws,
                           size_t ws_bytes, void* stream);
 int gm_conv2d_dgrad_ex_bf16(const gm_conv_desc* d, const void* dy, const void* wt, void* dx, void* ws,

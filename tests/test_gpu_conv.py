@@ -232,3 +232,41 @@ def test_conv_splitk_spin_timeout_never_silent(dev):
         assert all(torch.equal(y, ref) for y in ys)
     assert L.device_faults() == 0
     assert torch.equal(G.conv_fwd(x, w, st, pad), ref)
+
+
+@pytest.mark.parametrize("shape", [(64, 64, 56, 56), (2, 64, 28, 28), (3, 64, 9, 11), (1, 64, 7, 7), (2, 64, 5, 40)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_conv_resident_weight_layer1(dev, shape):
+    """3x3/s1 64->64 convolutions (ResNet layer 1) run the resident-weight kernel: weights
+    held in LDS by a persistent workgroup, whole-row tiles with a double-buffered input
+    halo.  Forward, input gradient and the fused gradient join (addend) equal the fp32
+    reference and the im2col kernel within bf16 output rounding."""
+    from greedy_multimodal_learning_amd import _lib as L
+    from greedy_multimodal_learning_amd import conv as G
+    lib = L.load()
+    N, C, H, W = shape
+    g = torch.Generator(device="cuda").manual_seed(sum(shape))
+    CL = torch.channels_last
+    x = torch.randn(N, C, H, W, device=dev, generator=g).bfloat16().contiguous(memory_format=CL)
+    w = (torch.randn(C, C, 3, 3, device=dev, generator=g) / (C * 9) ** 0.5).bfloat16().contiguous(memory_format=CL)
+    dy = torch.randn(N, C, H, W, device=dev, generator=g).bfloat16().contiguous(memory_format=CL)
+    add = torch.randn(N, C, H, W, device=dev, generator=g).bfloat16().contiguous(memory_format=CL)
+    wt = w.permute(1, 0, 2, 3).contiguous(memory_format=CL)
+    outs = {}
+    try:
+        for rw in (0, 1):
+            L.check(lib.gm_conv_set_rw(rw), "gm_conv_set_rw")
+            outs[rw] = (G.conv_fwd(x, w, 1, 1), G.conv_dgrad_t(dy, wt, H, W, 1, 1),
+                        G.conv_dgrad_t(dy, wt, H, W, 1, 1, addend=add))
+        torch.cuda.synchronize()
+    finally:
+        lib.gm_conv_set_rw(1)
+    yr = F.conv2d(x.float(), w.float(), padding=1)
+    dxr = torch.ops.aten.convolution_backward(dy.float(), x.float(), w.float(), None, [1, 1], [1, 1], [1, 1],
+                                              False, [0, 0], 1, [True, False, False])[0]
+    y, dx, dxa = outs[1]
+    _close(y, yr, 1e-2)
+    _close(dx, dxr, 1e-2)
+    _close(dxa, dxr + add.float(), 1e-2)
+    for a_, b_ in zip(outs[1], outs[0]):
+        _close(a_, b_, 1e-2)
