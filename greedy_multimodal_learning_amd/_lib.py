@@ -196,6 +196,7 @@ class BnBwd(ctypes.Structure):
 EXPORTS.update({
     "gm_bn_scratch": (c_size_t, [ctypes.c_longlong, c_int]),
     "gm_bn_fwd_train_bf16": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
+    "gm_bn_fwd_stats_bf16": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "gm_bn_fwd_infer_bf16": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "gm_bn_bwd_bf16": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
 })
@@ -208,6 +209,7 @@ class PoolDesc(ctypes.Structure):
 
 EXPORTS.update({
     "gm_maxpool2d_fwd_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "gm_bn_relu_maxpool2d_fwd_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "gm_maxpool2d_bwd_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
 })
 

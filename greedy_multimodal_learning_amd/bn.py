@@ -35,6 +35,10 @@ _scratch = {}
 # backward kernels).  GM_BN_MASKX=0 keeps the y mask.
 MASK_FROM_X = os.environ.get("GM_BN_MASKX", "1") != "0"
 
+# The stem's BN + ReLU + max-pool in one statistics launch and one pool launch
+# (GMBatchNorm2d.relu_maxpool); GM_BN_FUSE_POOL=0 composes the two modules.
+FUSE_POOL = os.environ.get("GM_BN_FUSE_POOL", "1") != "0"
+
 
 def _get_scratch(device, M, C):
     """Per-(device, stream) BN scratch (ticket word + coefficients + partials),
@@ -146,32 +150,88 @@ class _BNFn(torch.autograd.Function):
         coef = None
         if ctx.maskx:
             y, coef = None, y
-        C = xb.shape[1]
-        want_w, want_b = ctx.needs_input_grad[1], ctx.needs_input_grad[2]
-        tw = sink_target(weight) if want_w else None
-        tb = sink_target(bias) if want_b else None
-        if tw is not None and tb is not None and tw[1] == tb[1]:
-            dgamma, dbeta, acc = tw[0], tb[0], tw[1]
-            direct = True
-        else:
-            if tw is not None or tb is not None:  # mixed state: undo nothing, fall back to returned grads
-                raise RuntimeError("GMBatchNorm2d: weight and bias must share one gradient sink state")
-            dgamma = torch.empty(C, device=xb.device, dtype=torch.float32)
-            dbeta = torch.empty(C, device=xb.device, dtype=torch.float32)
-            acc, direct = False, False
         want_dres = ctx.has_res and ctx.needs_input_grad[3]
-        dx, dres = bn_bwd(dy, y, xb, weight.detach(), sm, si, ctx.relu, want_dres, dgamma, dbeta, acc, coef)
-        if direct:
-            sink_done(weight)
-            sink_done(bias)
-            gw = gb = None
-        else:
-            gw = dgamma if want_w else None
-            gb = dbeta if want_b else None
+        dx, gw, gb, dres = _bn_backward(dy, y, xb, weight, bias, sm, si, ctx.relu, want_dres, coef,
+                                        ctx.needs_input_grad[1], ctx.needs_input_grad[2])
         dx = dx if ctx.needs_input_grad[0] else None
         if dres is not None and ctx.join is not None:  # the residual's gradient joins the block input's
             dres = ctx.join.contribute(lambda add: dres if add is None else dres + add)
         return dx, gw, gb, dres, None, None, None, None, None, None, None, None
+
+
+def _bn_backward(dy, y, xb, weight, bias, sm, si, relu, want_dres, coef, want_w, want_b):
+    """BN backward with the parameter gradients written straight into the gradient sink
+    when the engine armed one (weight and bias share its state), else returned.
+    Returns (dx, grad_weight, grad_bias, dres)."""
+    C = xb.shape[1]
+    tw = sink_target(weight) if want_w else None
+    tb = sink_target(bias) if want_b else None
+    if tw is not None and tb is not None and tw[1] == tb[1]:
+        dgamma, dbeta, acc = tw[0], tb[0], tw[1]
+        direct = True
+    else:
+        if tw is not None or tb is not None:  # mixed state: undo nothing, fall back to returned grads
+            raise RuntimeError("GMBatchNorm2d: weight and bias must share one gradient sink state")
+        dgamma = torch.empty(C, device=xb.device, dtype=torch.float32)
+        dbeta = torch.empty(C, device=xb.device, dtype=torch.float32)
+        acc, direct = False, False
+    dx, dres = bn_bwd(dy, y, xb, weight.detach(), sm, si, relu, want_dres, dgamma, dbeta, acc, coef)
+    if direct:
+        sink_done(weight)
+        sink_done(bias)
+        return dx, None, None, dres
+    return dx, (dgamma if want_w else None), (dbeta if want_b else None), dres
+
+
+class _BNReluPoolFn(torch.autograd.Function):
+    """relu(BatchNorm2d(x)) followed by MaxPool2d(k, s, pad) - the ResNet stem - with the
+    normalised activation never materialised: one statistics launch
+    (gm_bn_fwd_stats_bf16), then the pool applies the affine + ReLU on the fly
+    (gm_bn_relu_maxpool2d_fwd_bf16); bit-identical to bn(x, relu=True) on the two-launch
+    path followed by the max-pool.  Backward: the pool's gather (dz), then the BN
+    backward with the ReLU mask recomputed from x and the forward's coefficients."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, nbt, momentum, eps, k, s, pad):
+        lib = L.load()
+        xb = _nhwc(x.to(torch.bfloat16))
+        N, C, H, W = xb.shape
+        _check_shape(xb, C)
+        M = N * H * W
+        sm = torch.empty(C, device=xb.device, dtype=torch.float32)
+        si = torch.empty(C, device=xb.device, dtype=torch.float32)
+        coef = torch.empty(2 * C, device=xb.device, dtype=torch.float32)
+        buf = _get_scratch(xb.device, M, C)
+        st = L.stream_of(xb.device)
+        p = L.BnFwd(M, C, 1, xb.data_ptr(), 0, 0, weight.data_ptr(), bias.data_ptr(), L.ptr(running_mean),
+                    L.ptr(running_var), float(momentum), float(eps), sm.data_ptr(), si.data_ptr(), L.ptr(nbt),
+                    coef.data_ptr())
+        L.check(lib.gm_bn_fwd_stats_bf16(ctypes.byref(p), buf.data_ptr(), buf.numel(), st), "gm_bn_fwd_stats_bf16")
+        P, Q = (H + 2 * pad - k) // s + 1, (W + 2 * pad - k) // s + 1
+        y = torch.empty(N, C, P, Q, device=xb.device, dtype=torch.bfloat16, memory_format=CL)
+        idx = torch.empty(N, P, Q, C, device=xb.device, dtype=torch.uint8)
+        d = L.PoolDesc(N, H, W, C, k, s, pad)
+        L.check(lib.gm_bn_relu_maxpool2d_fwd_bf16(ctypes.byref(d), xb.data_ptr(), coef.data_ptr(), y.data_ptr(),
+                                                  idx.data_ptr(), st), "gm_bn_relu_maxpool2d_fwd_bf16")
+        ctx.save_for_backward(xb, coef, weight, bias, sm, si, idx)
+        ctx.pool = (k, s, pad)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = L.load()
+        xb, coef, weight, bias, sm, si, idx = ctx.saved_tensors
+        k, s, pad = ctx.pool
+        N, C, H, W = xb.shape
+        dy = _nhwc(dy.to(torch.bfloat16))
+        dz = torch.empty_like(xb, memory_format=CL)
+        d = L.PoolDesc(N, H, W, C, k, s, pad)
+        L.check(lib.gm_maxpool2d_bwd_bf16(ctypes.byref(d), dy.data_ptr(), idx.data_ptr(), dz.data_ptr(),
+                                          L.stream_of(xb.device)), "gm_maxpool2d_bwd_bf16")
+        dx, gw, gb, _ = _bn_backward(dz, None, xb, weight, bias, sm, si, True, False, coef,
+                                     ctx.needs_input_grad[1], ctx.needs_input_grad[2])
+        dx = dx if ctx.needs_input_grad[0] else None
+        return dx, gw, gb, None, None, None, None, None, None, None, None
 
 
 def _use_bf16(x):
@@ -206,3 +266,21 @@ class GMBatchNorm2d(nn.BatchNorm2d):
             raise L.GreedyMMLError("GMBatchNorm2d: eval-mode forward with autograd is not supported")
         return bn_fwd_infer(x.to(dt), self.weight, self.bias, self.running_mean, self.running_var,
                             self.eps, bool(relu), residual)
+
+    def relu_maxpool(self, x, pool):
+        """pool(relu(self(x))) - the ResNet stem.  Training on the bf16 trunk with the
+        engine's max-pool takes the fused path (_BNReluPoolFn: the normalised activation
+        is never written); anything else composes the two modules."""
+        from .pool import GMMaxPool2d, _pair1
+        C = self.num_features
+        k, s, p = (_pair1(getattr(pool, a)) for a in ("kernel_size", "stride", "padding"))
+        fused = (FUSE_POOL and self.training and x.is_cuda and _use_bf16(x) and isinstance(pool, GMMaxPool2d)
+                 and None not in (k, s, p) and _pair1(pool.dilation) == 1 and not pool.ceil_mode
+                 and not pool.return_indices and k <= 15 and 2 * p <= k and C % 8 == 0 and 8 <= C <= 2048
+                 and not (C & (C - 1)) and self.affine and self.track_running_stats and self.momentum is not None
+                 and x.dim() == 4 and x.shape[1] == C)
+        if not fused:
+            return pool(self(x, relu=True))
+        with torch.autocast("cuda", enabled=False):
+            return _BNReluPoolFn.apply(x, self.weight, self.bias, self.running_mean, self.running_var,
+                                       self.num_batches_tracked, self.momentum, self.eps, k, s, p)

@@ -1138,6 +1138,34 @@ extern "C" int gm_bn_set_fused_mode(int mode) {
     return GM_OK;
 }
 
+// Statistics half of the training forward only (one reduce launch): save_mean/invstd,
+// running statistics, num_batches_tracked and the affine coefficients in coef_out
+// (required); no y.  The apply is fused into the consumer (gm_bn_relu_maxpool2d_fwd_bf16).
+extern "C" int gm_bn_fwd_stats_bf16(const gm_bn_fwd* p, void* scratch, size_t bytes, void* stream) {
+    const char* fn = "gm_bn_fwd_stats_bf16";
+    GM_REQUIRE(p && p->x && p->gamma && p->beta && p->save_mean && p->save_invstd && p->coef_out,
+               "%s: null argument (coef_out required)", fn);
+    GM_REQUIRE(!p->running_mean == !p->running_var, "%s: running_mean/var both or neither", fn);
+    int rc = check_common(p->M, p->C, scratch, bytes, fn);
+    if (rc) return rc;
+    const Plan pl = make_plan(p->M, p->C);
+    char* s = static_cast<char*>(scratch);
+    ReduceArgs a{};
+    a.M = p->M; a.C = p->C; a.tpr_log = pl.tpr_log; a.rpb = pl.rpb;
+    a.SW = pl.SW; a.nrc = pl.nrc;
+    a.x = p->x;
+    a.gamma = p->gamma; a.beta = p->beta; a.rmean = p->running_mean; a.rvar = p->running_var;
+    a.momentum = p->momentum; a.eps = p->eps;
+    a.save_mean = p->save_mean; a.save_invstd = p->save_invstd;
+    a.nbt = p->num_batches_tracked;
+    a.coef_out = p->coef_out;
+    a.counter = reinterpret_cast<unsigned*>(s);
+    a.coef = reinterpret_cast<float*>(s + pl.off_coef);
+    a.part = reinterpret_cast<float*>(s + pl.off_p1);
+    hipLaunchKernelGGL((k_bn_reduce<FWD, uint16_t>), dim3(pl.nrc, pl.nslice), dim3(kT), 0, as_stream(stream), a);
+    return check_launch("k_bn_reduce<fwd>");
+}
+
 extern "C" int gm_bn_fwd_train_bf16(const gm_bn_fwd* p, void* scratch, size_t bytes, void* stream) {
     return bn_fwd_train<uint16_t>(p, scratch, bytes, stream, "gm_bn_fwd_train_bf16");
 }

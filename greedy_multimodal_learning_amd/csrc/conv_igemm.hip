@@ -110,6 +110,93 @@ __device__ __forceinline__ unsigned span_mask(int x, int d0, int s, int n, int l
     return lo > hi ? 0u : ((2u << hi) - (1u << lo));
 }
 
+// ---- shared epilogue: D[n][m] layout: lane -> pixel m (col = lane&31), registers
+// 4g..4g+3 -> channels 8g + 4h + 0..3: 8-byte NHWC stores, no LDS.  Through buffer
+// resources, the stores and the addend loads (fused gradient join) are issued for the
+// whole tile with no per-element branch: out-of-tile positions get an offset past the
+// buffer's range, which the hardware drops (stores) or reads as zero (loads), so the
+// addend loads are all in flight together instead of one dependent round trip per store.
+template <int MT, int NT, int BM, int BN>
+__device__ __forceinline__ void store_tile(const ConvArgs& a, const ConvCls& cl, int m0, int n0, int wm, int wn,
+                                           int fr, int fh, int M, floatx16 (&acc)[MT][NT]) {
+    const int PQ = cl.P * cl.Q;
+    const size_t out_bytes = (size_t)a.N * a.Ho * a.Wo * a.Nout * 2;
+    if (out_bytes < 0x7ffff000u) {
+        const auto orsrc = __builtin_amdgcn_make_buffer_rsrc(cl.out, 0, (int)out_bytes, 0x00020000);
+        unsigned off[MT];
+        bool mok[MT];
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+            int m = m0 + wm * (BM / 2) + i * 32 + fr;
+            mok[i] = m < M;
+            m = mok[i] ? m : m0;
+            const int b = (int)cl.fd_pq.div((uint32_t)m), pq = m - b * PQ;
+            const int p = (int)cl.fd_q.div((uint32_t)pq), q = pq - p * cl.Q;
+            const int ho = p * cl.oS + cl.oH, wo = q * cl.oS + cl.oW;
+            off[i] = (unsigned)(((b * a.Ho + ho) * a.Wo + wo) * a.Nout) * 2u;
+        }
+        auto boff = [&](int i, int j, int gq) {
+            const int n = n0 + wn * (BN / 2) + j * 32 + 8 * gq + 4 * fh;
+            return (mok[i] && n < a.Nout) ? off[i] + (unsigned)n * 2u : 0xfffffff0u;
+        };
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+        u32x2 av[MT][NT][4];
+        if (a.addend) {
+            const auto arsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.addend), 0, (int)out_bytes,
+                                                                 0x00020000);
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+#pragma unroll
+                    for (int gq = 0; gq < 4; ++gq)
+                        av[i][j][gq] = __builtin_amdgcn_raw_buffer_load_b64(arsrc, boff(i, j, gq), 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+#pragma unroll
+                for (int gq = 0; gq < 4; ++gq) {
+                    float o0 = acc[i][j][4 * gq], o1 = acc[i][j][4 * gq + 1];
+                    float o2 = acc[i][j][4 * gq + 2], o3 = acc[i][j][4 * gq + 3];
+                    if (a.addend) {
+                        o0 += bf_lo(av[i][j][gq].x); o1 += bf_hi(av[i][j][gq].x);
+                        o2 += bf_lo(av[i][j][gq].y); o3 += bf_hi(av[i][j][gq].y);
+                    }
+                    const u32x2 v = {pack_bf2(o0, o1), pack_bf2(o2, o3)};
+                    __builtin_amdgcn_raw_buffer_store_b64(v, orsrc, boff(i, j, gq), 0, 0);
+                }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {  // outputs of 2 GB or more: 64-bit addressing
+        const int m = m0 + wm * (BM / 2) + i * 32 + fr;
+        if (m >= M) continue;
+        const int b = (int)cl.fd_pq.div((uint32_t)m), pq = m - b * PQ;
+        const int p = (int)cl.fd_q.div((uint32_t)pq), q = pq - p * cl.Q;
+        const int ho = p * cl.oS + cl.oH, wo = q * cl.oS + cl.oW;
+        uint16_t* dst = cl.out + ((size_t)(b * a.Ho + ho) * a.Wo + wo) * a.Nout;
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int gq = 0; gq < 4; ++gq) {
+                const int n = n0 + wn * (BN / 2) + j * 32 + 8 * gq + 4 * fh;
+                if (n >= a.Nout) continue;
+                float o0 = acc[i][j][4 * gq], o1 = acc[i][j][4 * gq + 1];
+                float o2 = acc[i][j][4 * gq + 2], o3 = acc[i][j][4 * gq + 3];
+                if (a.addend) {
+                    const uint2 av = *(const uint2*)(a.addend + (dst - cl.out) + n);
+                    o0 += bf_lo(av.x); o1 += bf_hi(av.x); o2 += bf_lo(av.y); o3 += bf_hi(av.y);
+                }
+                uint2 v;
+                v.x = pack_bf2(o0, o1);
+                v.y = pack_bf2(o2, o3);
+                *(uint2*)(dst + n) = v;
+            }
+    }
+}
+
 template <int BM, int BN, bool UT, int ST>
 __global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
     constexpr int BK = 64;
@@ -301,34 +388,7 @@ __global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
         }
     }
 
-    // ---- epilogue: D[n][m] layout: lane -> pixel m (col = lane&31), registers 4g..4g+3 ->
-    // channels 8g + 4h + 0..3 (row = (r&3) + 8(r>>2) + 4h): 8-byte NHWC stores, no LDS ----
-#pragma unroll
-    for (int i = 0; i < MT; ++i) {
-        const int m = m0 + wm * (BM / 2) + i * 32 + fr;
-        if (m >= M) continue;
-        const int b = m / PQ, pq = m - b * PQ;
-        const int p = pq / cl.Q, q = pq - p * cl.Q;
-        const int ho = p * cl.oS + cl.oH, wo = q * cl.oS + cl.oW;
-        uint16_t* dst = cl.out + ((size_t)(b * a.Ho + ho) * a.Wo + wo) * a.Nout;
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-#pragma unroll
-            for (int gq = 0; gq < 4; ++gq) {
-                const int n = n0 + wn * (BN / 2) + j * 32 + 8 * gq + 4 * fh;
-                if (n >= a.Nout) continue;
-                float o0 = acc[i][j][4 * gq], o1 = acc[i][j][4 * gq + 1];
-                float o2 = acc[i][j][4 * gq + 2], o3 = acc[i][j][4 * gq + 3];
-                if (a.addend) {  // fused gradient join (the residual branch's gradient)
-                    const uint2 av = *(const uint2*)(a.addend + (dst - cl.out) + n);
-                    o0 += bf_lo(av.x); o1 += bf_hi(av.x); o2 += bf_lo(av.y); o3 += bf_hi(av.y);
-                }
-                uint2 v;
-                v.x = pack_bf2(o0, o1);
-                v.y = pack_bf2(o2, o3);
-                *(uint2*)(dst + n) = v;
-            }
-    }
+    store_tile<MT, NT, BM, BN>(a, cl, m0, n0, wm, wn, fr, fh, M, acc);
 }
 
 // Lean variant for C >= 64 (a 64-wide k-tile lies inside one tap) and <= 32 taps:
@@ -614,32 +674,7 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
         if (t == 0) __hip_atomic_store(a.flags + bid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 
-#pragma unroll
-    for (int i = 0; i < MT; ++i) {
-        const int m = m0 + wm * (BM / 2) + i * 32 + fr;
-        if (m >= M) continue;
-        const int b = (int)cl.fd_pq.div((uint32_t)m), pq = m - b * PQ;
-        const int p = (int)cl.fd_q.div((uint32_t)pq), q = pq - p * cl.Q;
-        const int ho = p * cl.oS + cl.oH, wo = q * cl.oS + cl.oW;
-        uint16_t* dst = cl.out + ((size_t)(b * a.Ho + ho) * a.Wo + wo) * a.Nout;
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-#pragma unroll
-            for (int gq = 0; gq < 4; ++gq) {
-                const int n = n0 + wn * (BN / 2) + j * 32 + 8 * gq + 4 * fh;
-                if (n >= a.Nout) continue;
-                float o0 = acc[i][j][4 * gq], o1 = acc[i][j][4 * gq + 1];
-                float o2 = acc[i][j][4 * gq + 2], o3 = acc[i][j][4 * gq + 3];
-                if (a.addend) {  // fused gradient join (the residual branch's gradient)
-                    const uint2 av = *(const uint2*)(a.addend + (dst - cl.out) + n);
-                    o0 += bf_lo(av.x); o1 += bf_hi(av.x); o2 += bf_lo(av.y); o3 += bf_hi(av.y);
-                }
-                uint2 v;
-                v.x = pack_bf2(o0, o1);
-                v.y = pack_bf2(o2, o3);
-                *(uint2*)(dst + n) = v;
-            }
-    }
+    store_tile<MT, NT, BM, BN>(a, cl, m0, n0, wm, wn, fr, fh, M, acc);
 }
 
 // ---------------------------------------------------------------------------------
@@ -666,6 +701,16 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
 // workgroup of the CU hides that stall), the B operand (weights) through the usual
 // 2-stage ring with one barrier per k-tile.  Epilogue and split-K turnstile as in the
 // lean kernel.
+// LDS fragment read as inline asm (k_conv_rw): hipcc cannot count these, so the kernel
+// waits for them itself with counted lgkmcnt waits tied to the fragments; that keeps two
+// k-steps of reads in flight, where the compiler's own waits drained all of them
+template <int OFF>
+__device__ __forceinline__ bf16x8 lds_rd128(unsigned addr) {
+    bf16x8 d;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "i"(OFF));
+    return d;
+}
+
 struct HaloArgs {
     int halo_bytes;           // LDS bytes of the halo region (multiple of 1 KB)
     FastDiv fd_w2, fd_h1;     // W + 2, H + 1
@@ -923,32 +968,7 @@ __global__ __launch_bounds__(256) void k_conv_halo(ConvArgs a, HaloArgs h) {
         if (t == 0) __hip_atomic_store(a.flags + bid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 
-#pragma unroll
-    for (int i = 0; i < MT; ++i) {
-        const int m = m0 + wm * (BM / 2) + i * 32 + fr;
-        if (m >= M) continue;
-        const int b = (int)cl.fd_pq.div((uint32_t)m), pq = m - b * PQ;
-        const int p = (int)cl.fd_q.div((uint32_t)pq), q = pq - p * cl.Q;
-        const int ho = p * cl.oS + cl.oH, wo = q * cl.oS + cl.oW;
-        uint16_t* dst = cl.out + ((size_t)(b * a.Ho + ho) * a.Wo + wo) * a.Nout;
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-#pragma unroll
-            for (int gq = 0; gq < 4; ++gq) {
-                const int n = n0 + wn * (BN / 2) + j * 32 + 8 * gq + 4 * fh;
-                if (n >= a.Nout) continue;
-                float o0 = acc[i][j][4 * gq], o1 = acc[i][j][4 * gq + 1];
-                float o2 = acc[i][j][4 * gq + 2], o3 = acc[i][j][4 * gq + 3];
-                if (a.addend) {  // fused gradient join (the residual branch's gradient)
-                    const uint2 av = *(const uint2*)(a.addend + (dst - cl.out) + n);
-                    o0 += bf_lo(av.x); o1 += bf_hi(av.x); o2 += bf_lo(av.y); o3 += bf_hi(av.y);
-                }
-                uint2 v;
-                v.x = pack_bf2(o0, o1);
-                v.y = pack_bf2(o2, o3);
-                *(uint2*)(dst + n) = v;
-            }
-    }
+    store_tile<MT, NT, BM, BN>(a, cl, m0, n0, wm, wn, fr, fh, M, acc);
 }
 
 // ---------------------------------------------------------------------------------
@@ -962,16 +982,6 @@ __global__ __launch_bounds__(256) void k_conv_halo(ConvArgs a, HaloArgs h) {
 // 16 KB im2col A tiles plus 72 KB of weights in the im2col kernel - and the k-loop is
 // LDS reads + MFMAs only.  Halo pixels are 128-B rows XOR-swizzled as in k_conv_halo;
 // weights are [tap][n][128 B] with the same swizzle on n.
-// LDS fragment read as inline asm (k_conv_rw): hipcc cannot count these, so the kernel
-// waits for them itself with counted lgkmcnt waits tied to the fragments; that keeps two
-// k-steps of reads in flight, where the compiler's own waits drained all of them
-template <int OFF>
-__device__ __forceinline__ bf16x8 lds_rd128(unsigned addr) {
-    bf16x8 d;
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "i"(OFF));
-    return d;
-}
-
 struct RwArgs {
     int RT;        // image rows per tile
     int tpi;       // tiles per image (H / RT)

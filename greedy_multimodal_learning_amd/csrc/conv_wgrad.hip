@@ -268,12 +268,13 @@ __global__ __launch_bounds__(256) void k_conv_wgrad4(WgradArgs a) {
     }
     typedef __attribute__((address_space(1))) const void* gptr_t;
     typedef __attribute__((address_space(3))) void* lptr_t;
+    const void* zero = (const void*)g_wzero16;
     auto issue = [&](int i, int bufoff) {  // step step0 + i
         const bool full = (step0 + i + 1) * BK <= M;
 #pragma unroll
         for (int j = 0; j < GA; ++j) {
-            const bool ok = a_cok[j] && (full || (step0 + i) * BK + a_row[j] < M);
-            const void* src = ok ? (const void*)(a_ptr[j] + (size_t)i * BK * a.Kc) : (const void*)g_wzero16;
+            const bool ok = a_cok[j] & (full | ((step0 + i) * BK + a_row[j] < M));  // no short-circuit branch
+            const void* src = ok ? (const void*)(a_ptr[j] + (size_t)i * BK * a.Kc) : zero;
             __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + bufoff + (wave * GA + j) * 1024), 16, 0,
                                              0);
         }
@@ -282,10 +283,9 @@ __global__ __launch_bounds__(256) void k_conv_wgrad4(WgradArgs a) {
             const int b = b_b[j], p = b_p[j], q = b_q[j];
             const int h0 = p * a.sth, w0 = q * a.stw;
             const int hi = h0 + b_dh[j], wi = w0 + b_dw[j];
-            const bool ok = b_cok[j] && b < a.N && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+            const bool ok = b_cok[j] & (b < a.N) & ((unsigned)hi < (unsigned)a.H) & ((unsigned)wi < (unsigned)a.W);
             const int pix = (b * a.H + h0) * a.W + w0;
-            const void* src =
-                ok ? (const void*)(a.x + (((long)pix << a.logC) + b_toff[j])) : (const void*)g_wzero16;
+            const void* src = ok ? (const void*)(a.x + (((long)pix << a.logC) + b_toff[j])) : zero;
             __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + bufoff + SA + (wave * GB + j) * 1024), 16,
                                              0, 0);
             // next step's pixel: + 64 = (adv_b, adv_p, adv_q), one carry per component at most

@@ -9,10 +9,18 @@
 // cover it and sums the dy of those whose argmax is that pixel (fp32, fixed
 // order), so no atomics and dx is written exactly once.  Element type E: bf16 (the
 // performance trunk) or fp32 (the reference-precision trunk), 8 channels per access.
+#include <type_traits>
+
 #include "gm_common.h"
 
 namespace gm {
 namespace {
+
+template <typename E>
+__device__ __forceinline__ float round_to(float v) {
+    if constexpr (std::is_same<E, uint16_t>::value) return __uint_as_float((uint32_t)Elem<uint16_t>::f2bf(v) << 16);
+    else return v;
+}
 
 struct PoolArgs {
     int N, H, W, C8;  // C8 = C / 8 (16-byte channel groups)
@@ -20,9 +28,12 @@ struct PoolArgs {
     FastDiv fd_c8, fd_q, fd_p, fd_w, fd_h, fd_s;  // index decode without integer division
 };
 
-template <typename E>
+// BNRELU: the pooled values are relu(x*sc + sh) rounded to E, i.e. the stem's BatchNorm +
+// ReLU applied on the fly (coef = sc[C], sh[C]): the normalised activation is never
+// written, bit-identical to BN-apply (fmaf, fmaxf, RNE store) followed by the plain pool
+template <typename E, bool BNRELU = false>
 __global__ __launch_bounds__(256) void k_maxpool_fwd(PoolArgs a, const void* __restrict__ x, void* __restrict__ y,
-                                                     uint2* __restrict__ idx) {
+                                                     uint2* __restrict__ idx, const float* __restrict__ coef = nullptr) {
     const unsigned total = (unsigned)a.N * a.P * a.Q * a.C8;  // < 2^31 (checked on the host)
     for (unsigned i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
         unsigned t = a.fd_c8.div(i);
@@ -35,6 +46,14 @@ __global__ __launch_bounds__(256) void k_maxpool_fwd(PoolArgs a, const void* __r
         const int h0 = p * a.s - a.pad, w0 = q * a.s - a.pad;
         float m[8];
         uint32_t ix[8];
+        float sc[8], sh[8];
+        if (BNRELU) {
+            const float4* c4 = reinterpret_cast<const float4*>(coef + cg * 8);
+            const float4* s4 = reinterpret_cast<const float4*>(coef + a.C8 * 8 + cg * 8);
+            const float4 c0 = c4[0], c1 = c4[1], s0 = s4[0], s1 = s4[1];
+            sc[0] = c0.x; sc[1] = c0.y; sc[2] = c0.z; sc[3] = c0.w; sc[4] = c1.x; sc[5] = c1.y; sc[6] = c1.z; sc[7] = c1.w;
+            sh[0] = s0.x; sh[1] = s0.y; sh[2] = s0.z; sh[3] = s0.w; sh[4] = s1.x; sh[5] = s1.y; sh[6] = s1.z; sh[7] = s1.w;
+        }
         const int hs = h0 < 0 ? 0 : h0, ws = w0 < 0 ? 0 : w0;
         const uint32_t first = (uint32_t)((hs - h0) * a.k + (ws - w0));
 #pragma unroll
@@ -50,6 +69,10 @@ __global__ __launch_bounds__(256) void k_maxpool_fwd(PoolArgs a, const void* __r
                 if (w < 0 || w >= a.W) continue;
                 float v[8];
                 V8<E>::ld(x, (((long long)n * a.H + h) * a.W + w) * a.C8 + cg, v);
+                if (BNRELU) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) v[j] = round_to<E>(fmaxf(fmaf(v[j], sc[j], sh[j]), 0.f));
+                }
                 const uint32_t pos = (uint32_t)(r * a.k + c);
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
@@ -176,6 +199,19 @@ int pool_bwd(const gm_pool_desc* d, const void* dy, const void* idx, void* dx, v
 
 extern "C" int gm_maxpool2d_fwd_bf16(const gm_pool_desc* d, const void* x, void* y, void* idx, void* stream) {
     return pool_fwd<uint16_t>(d, x, y, idx, stream, "gm_maxpool2d_fwd_bf16");
+}
+
+extern "C" int gm_bn_relu_maxpool2d_fwd_bf16(const gm_pool_desc* d, const void* x, const float* coef, void* y,
+                                             void* idx, void* stream) {
+    const char* fn = "gm_bn_relu_maxpool2d_fwd_bf16";
+    PoolArgs a;
+    int rc = prep(d, a, fn);
+    if (rc) return rc;
+    GM_REQUIRE(x && coef && y && idx, "%s: null pointer", fn);
+    const long long n = (long long)a.N * a.P * a.Q * a.C8;
+    hipLaunchKernelGGL((k_maxpool_fwd<uint16_t, true>), dim3(grid_for(n)), dim3(256), 0, as_stream(stream), a, x, y,
+                       static_cast<uint2*>(idx), coef);
+    return check_launch("k_maxpool_fwd<bnrelu>");
 }
 
 extern "C" int gm_maxpool2d_bwd_bf16(const gm_pool_desc* d, const void* dy, const void* idx, void* dx, void* stream) {

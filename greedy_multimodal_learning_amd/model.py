@@ -53,7 +53,10 @@ class MMTM_MVCNN(nn.Module):
 
     @staticmethod
     def _stem(net, x):
-        return net.layer1(net.maxpool(net.bn1(net.conv1(x), relu=True)))  # relu fused into bn1
+        y = net.conv1(x)
+        if hasattr(net.bn1, "relu_maxpool"):  # bn1 + relu + maxpool fused (bn.py)
+            return net.layer1(net.bn1.relu_maxpool(y, net.maxpool))
+        return net.layer1(net.maxpool(net.relu(net.bn1(y))))
 
     @staticmethod
     def _head(net, f):

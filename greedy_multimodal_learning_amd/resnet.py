@@ -114,7 +114,7 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(self.bn1(self.conv1(x), relu=True))
+        x = self.bn1.relu_maxpool(self.conv1(x), self.maxpool)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         return self.fc(torch.flatten(self.avgpool(x), 1))
 

@@ -416,6 +416,9 @@ size_t gm_bn_scratch(long long M, int C);
 int gm_bn_fwd_train_bf16(const gm_bn_fwd* p, void* scratch, size_t scratch_bytes, void* stream);
 int gm_bn_fwd_infer_bf16(const gm_bn_fwd* p, void* scratch, size_t scratch_bytes, void* stream);
 int gm_bn_bwd_bf16(const gm_bn_bwd* p, void* scratch, size_t scratch_bytes, void* stream);
+/* the statistics half of gm_bn_fwd_train_bf16 alone (y is not written; coef_out required):
+ * the stem's BN + ReLU is applied inside its max-pool (gm_bn_relu_maxpool2d_fwd_bf16) */
+int gm_bn_fwd_stats_bf16(const gm_bn_fwd* p, void* scratch, size_t scratch_bytes, void* stream);
 /* the same three on fp32 activations (x, residual, y, dy, dx, dres fp32 NHWC): the
  * reference-precision trunk; reduce + apply launches, same statistics arithmetic */
 int gm_bn_fwd_train_f32(const gm_bn_fwd* p, void* scratch, size_t scratch_bytes, void* stream);
@@ -436,6 +439,11 @@ typedef struct gm_pool_desc {
 
 int gm_maxpool2d_fwd_bf16(const gm_pool_desc* d, const void* x, void* y, void* idx, void* stream);
 int gm_maxpool2d_bwd_bf16(const gm_pool_desc* d, const void* dy, const void* idx, void* dx, void* stream);
+/* the stem's BatchNorm + ReLU + MaxPool forward: pools relu(x*sc + sh) rounded to bf16
+ * (coef = sc[C], sh[C] from gm_bn_fwd_stats_bf16), bit-identical to gm_bn_fwd_train's
+ * apply followed by gm_maxpool2d_fwd_bf16, without writing the normalised activation */
+int gm_bn_relu_maxpool2d_fwd_bf16(const gm_pool_desc* d, const void* x, const float* coef, void* y, void* idx,
+                                  void* stream);
 /* fp32 activations (the reference-precision trunk), same index format */
 int gm_maxpool2d_fwd_f32(const gm_pool_desc* d, const void* x, void* y, void* idx, void* stream);
 int gm_maxpool2d_bwd_f32(const gm_pool_desc* d, const void* dy, const void* idx, void* dx, void* stream);

@@ -270,3 +270,28 @@ def test_conv_resident_weight_layer1(dev, shape):
     _close(dxa, dxr + add.float(), 1e-2)
     for a_, b_ in zip(outs[1], outs[0]):
         _close(a_, b_, 1e-2)
+
+
+@pytest.mark.parametrize("shape", [(4, 128, 28, 28, 128, 3, 3, 1, 1), (4, 64, 56, 56, 128, 3, 3, 2, 1),
+                                   (64, 256, 14, 14, 256, 3, 3, 1, 1), (5, 128, 7, 7, 256, 1, 1, 2, 0)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_conv_dgrad_fused_addend(dev, shape):
+    """The input-gradient epilogue's fused gradient join (dx = dgrad + addend, the
+    residual branch's gradient) on the halo, im2col and split-K kernels: equal to the
+    fp32 reference plus the addend, and to the unfused dgrad plus the addend."""
+    from greedy_multimodal_learning_amd import conv as G
+    N, C, H, W, K, R, S, st, pad = shape
+    g = torch.Generator(device="cuda").manual_seed(sum(shape) + 1)
+    CL = torch.channels_last
+    x = torch.randn(N, C, H, W, device=dev, generator=g).bfloat16().contiguous(memory_format=CL)
+    w = (torch.randn(K, C, R, S, device=dev, generator=g) / (C * R * S) ** 0.5).bfloat16().contiguous(memory_format=CL)
+    P, Q = (H + 2 * pad - R) // st + 1, (W + 2 * pad - S) // st + 1
+    dy = torch.randn(N, K, P, Q, device=dev, generator=g).bfloat16().contiguous(memory_format=CL)
+    add = torch.randn(N, C, H, W, device=dev, generator=g).bfloat16().contiguous(memory_format=CL)
+    wt = w.permute(1, 0, 2, 3).contiguous(memory_format=CL)
+    dx = G.conv_dgrad_t(dy, wt, H, W, st, pad)
+    dxa = G.conv_dgrad_t(dy, wt, H, W, st, pad, addend=add)
+    dxr = torch.ops.aten.convolution_backward(dy.float(), x.float(), w.float(), None, [st, st], [pad, pad], [1, 1],
+                                              False, [0, 0], 1, [True, False, False])[0]
+    _close(dxa, dxr + add.float(), 1e-2)
+    _close(dxa, dx.float() + add.float(), 1e-2)
