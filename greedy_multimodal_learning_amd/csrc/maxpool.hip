@@ -61,6 +61,30 @@ __global__ __launch_bounds__(256) void k_maxpool_fwd(PoolArgs a, const void* __r
             m[j] = -__builtin_huge_valf();
             ix[j] = first;
         }
+        if (a.k == 3) {
+            // 3 x 3 windows (the ResNet stem): the nine loads in flight at once, out-of-image
+            // positions clamped to (hs, ws) and skipped in the row-major scan below
+            float v[9][8];
+#pragma unroll
+            for (int u = 0; u < 9; ++u) {
+                const int h = h0 + u / 3, w = w0 + u % 3;
+                const bool in = h >= 0 && h < a.H && w >= 0 && w < a.W;
+                V8<E>::ld(x, (((long long)n * a.H + (in ? h : hs)) * a.W + (in ? w : ws)) * a.C8 + cg, v[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < 9; ++u) {
+                const int h = h0 + u / 3, w = w0 + u % 3;
+                if (h < 0 || h >= a.H || w < 0 || w >= a.W) continue;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float z = BNRELU ? round_to<E>(fmaxf(fmaf(v[u][j], sc[j], sh[j]), 0.f)) : v[u][j];
+                    if (z > m[j] || __builtin_isnan(z)) {
+                        m[j] = z;
+                        ix[j] = (uint32_t)u;
+                    }
+                }
+            }
+        } else
         for (int r = 0; r < a.k; ++r) {
             const int h = h0 + r;
             if (h < 0 || h >= a.H) continue;
@@ -112,6 +136,34 @@ __global__ __launch_bounds__(256) void k_maxpool_bwd(PoolArgs a, const void* __r
         float g[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) g[j] = 0.f;
+        if (a.k == 3 && a.s == 2) {
+            // the ResNet stem's pool: at most 2 x 2 windows; all eight loads in flight at
+            // once (addresses clamped to a valid window, contributions predicated), summed
+            // in the generic loop's order (p, then q, ascending)
+            uint2 iv[4];
+            float dv[4][8];
+            bool ok[4];
+            uint32_t pos[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int p = phi - 1 + (u >> 1), q = qhi - 1 + (u & 1);
+                ok[u] = p >= plo && q >= qlo;
+                const int pc = ok[u] ? p : phi, qc = ok[u] ? q : qhi;
+                const long long o = (((long long)n * a.P + pc) * a.Q + qc) * a.C8 + cg;
+                iv[u] = idx[o];
+                V8<E>::ld(dy, o, dv[u]);
+                pos[u] = (uint32_t)((h - (p * a.s - a.pad)) * a.k + (w - (q * a.s - a.pad)));
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const uint32_t b = ((j < 4 ? iv[u].x : iv[u].y) >> (8 * (j & 3))) & 0xffu;
+                    if (ok[u] && b == pos[u]) g[j] += dv[u][j];
+                }
+            V8<E>::st(dx, i, g);
+            continue;
+        }
         for (int p = plo; p <= phi; ++p) {
             for (int q = qlo; q <= qhi; ++q) {
                 const long long o = (((long long)n * a.P + p) * a.Q + q) * a.C8 + cg;
