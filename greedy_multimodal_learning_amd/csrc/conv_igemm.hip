@@ -701,9 +701,17 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
 // workgroup of the CU hides that stall), the B operand (weights) through the usual
 // 2-stage ring with one barrier per k-tile.  Epilogue and split-K turnstile as in the
 // lean kernel.
-// LDS fragment read as inline asm (k_conv_rw): hipcc cannot count these, so the kernel
-// waits for them itself with counted lgkmcnt waits tied to the fragments; that keeps two
-// k-steps of reads in flight, where the compiler's own waits drained all of them
+// s_barrier that is also a compiler memory barrier: without the fences the scheduler may
+// move an LDS access of the next tile above the raw barrier (it is not a memory fence)
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// LDS fragment read as inline asm (k_conv_rw, k_conv_stem): hipcc does not see these as
+// LDS accesses, so it neither drains the LDS-DMA in flight before them nor counts them;
+// the kernels wait for them explicitly (lgkmcnt(0) tied to the fragments about to be used)
 template <int OFF>
 __device__ __forceinline__ bf16x8 lds_rd128(unsigned addr) {
     bf16x8 d;
@@ -1078,7 +1086,7 @@ __global__ __launch_bounds__(256) void k_conv_rw(ConvArgs a, RwArgs r) {
     constexpr int kStores = 8;                      // epilogue stores per wave per tile
     constexpr int kWaitStores = kStores | (7 << 4) | (15 << 8);  // vmcnt(kStores)
     __builtin_amdgcn_s_waitcnt(kWaitAll);
-    __builtin_amdgcn_s_barrier();
+    lds_barrier();
     const size_t out_bytes = (size_t)a.N * a.Ho * a.Wo * a.Nout * 2;
     const __amdgpu_buffer_rsrc_t orsrc =
         __builtin_amdgcn_make_buffer_rsrc(cl.out, 0, (int)(out_bytes < 0x7fffffffu ? out_bytes : 0x7fffffffu),
@@ -1095,7 +1103,7 @@ __global__ __launch_bounds__(256) void k_conv_rw(ConvArgs a, RwArgs r) {
         for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
-        bf16x8 af[3][2], bfr[3];
+        bf16x8 af[2][2], bfr[2];
         unsigned abase[2];
         const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
         auto tap_base = [&](int tp) {
@@ -1130,26 +1138,18 @@ __global__ __launch_bounds__(256) void k_conv_rw(ConvArgs a, RwArgs r) {
                 default: load_b(std::integral_constant<int, 8>{}, ks, c); break;
             }
         };
-        // fragments two k-steps ahead (one wave per SIMD: 64 MFMA cycles per k-step do not
-        // cover an LDS round trip): before k-step k's MFMAs only its own three reads are
-        // waited for, k+1's and k+2's stay in flight
+        // one k-step of fragments in flight under the MFMAs: wait for everything, issue the
+        // next k-step's reads, then this k-step's MFMAs (counted waits that keep two
+        // k-steps in flight are not used: k_conv_stem showed sporadic wrong tiles with them)
         load(0, 0);
-        load(1, 1);
 #pragma unroll
         for (int k = 0; k < 36; ++k) {
-            const int c = k % 3;
-            if (k + 2 < 36) load(k + 2, (k + 2) % 3);
-            if (k + 2 < 36)
-                asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(af[c][0]), "+v"(af[c][1]), "+v"(bfr[c]));
-            else if (k + 1 < 36)
-                asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(af[c][0]), "+v"(af[c][1]), "+v"(bfr[c]));
-            else
-                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[c][0]), "+v"(af[c][1]), "+v"(bfr[c]));
-            if (DIAG != 2) {
+            const int c = k & 1;
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[c][0]), "+v"(af[c][1]), "+v"(bfr[c]));
+            if (k + 1 < 36) load(k + 1, c ^ 1);
 #pragma unroll
-                for (int i = 0; i < 2; ++i)
-                    acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[c], af[c][i], acc[i], 0, 0, 0);
-            }
+            for (int i = 0; i < 2; ++i)
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[c], af[c][i], acc[i], 0, 0, 0);
         }
 
         // epilogue: rows p0 + prow, columns pcol; 4 consecutive output channels per store.
@@ -1193,6 +1193,157 @@ __global__ __launch_bounds__(256) void k_conv_rw(ConvArgs a, RwArgs r) {
         // still be in flight.  Then every wave is done with buffer bb.
         if (DIAG != 1) __builtin_amdgcn_s_waitcnt(kWaitStores);
         __builtin_amdgcn_s_barrier();
+        bb ^= 1;
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// Convolutions over 8-channel (16-byte) input elements with 64 output channels and
+// no padding - the ResNet stem on its pixel-pair view (conv.py: a 7 x 4 filter over
+// pairs, strides (2, 1), K = 224).  The im2col kernel re-stages every input element
+// R*S times through LDS-DMA for a 64-wide N tile; here a persistent workgroup keeps
+// the whole weight tensor in LDS (64 x T x 16 B, row pitch padded by 16 B) and walks
+// output rows: one output row's input is R consecutive input rows (contiguous in
+// NHWC), DMA'd as one block into the second of two buffers while the current row's
+// MFMAs run.  A k-step covers two taps (16 channels); output columns past Q are MFMA
+// padding.  LDS reads as asm one k-step ahead of the MFMAs; the output row leaves
+// through an LDS tile as whole 128-B pixel rows, with a counted store wait.
+struct StemArgs {
+    int T, ksteps;      // taps (R * S, even), k-steps (T / 2)
+    int rows;           // output rows N * P (one tile each)
+    int hbytes, nI;     // one input block: R * Wi * 16 B rounded up to 1 KB, its DMA instructions
+    int blk;            // bytes of one input block (R * Wi * 16)
+    int wpitch;         // LDS bytes per output channel's weights (T * 16 + 16)
+    FastDiv fd_p;       // P
+    FastDiv fd_s;       // S
+};
+
+__global__ __launch_bounds__(256) void k_conv_stem(ConvArgs a, StemArgs r) {
+    extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+    char* lds = reinterpret_cast<char*>(smem);  // [weights 64 x wpitch][block 0][block 1]
+    const ConvCls& cl = a.cls[0];
+    const int Wi = a.Wi, Q = cl.Q, P = cl.P;
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int fr = lane & 31, fh = lane >> 5;
+    const int WB = 64 * r.wpitch;
+    typedef __attribute__((address_space(1))) const void* gptr_t;
+    typedef __attribute__((address_space(3))) void* lptr_t;
+    int tl = blockIdx.x;
+    if (tl >= r.rows) return;
+
+    // weights [64][T][8] -> LDS rows of wpitch bytes (register path: the padded pitch
+    // is not lane-linear)
+    const uint4* wsrc = reinterpret_cast<const uint4*>(a.wt);
+    for (int e = t; e < 64 * r.T; e += 256) {
+        const int n = e / r.T, tp = e - n * r.T;
+        *reinterpret_cast<uint4*>(lds + n * r.wpitch + tp * 16) = wsrc[e];
+    }
+    // the R input rows of output row `row` (= image b, output row p): one contiguous block
+    auto issue_block = [&](int row, int bb) {
+        const int b = (int)r.fd_p.div((uint32_t)row), p = row - b * P;
+        const char* src = reinterpret_cast<const char*>(a.in) + ((size_t)(b * a.Hi + p * a.sAh) * Wi) * 16;
+        char* base = lds + WB + bb * r.hbytes;
+        for (int I = wave; I < r.nI; I += 4) {
+            const int off = I * 1024 + lane * 16;
+            const void* s = off < r.blk ? (const void*)(src + off) : (const void*)g_zero16;
+            __builtin_amdgcn_global_load_lds((gptr_t)s, (lptr_t)(base + I * 1024), 16, 0, 0);
+        }
+    };
+    issue_block(tl, 0);
+
+    // tile-invariant geometry: MFMA row block i of this wave -> output column q
+    int qv[2];
+    bool qok[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int q = wm * 64 + i * 32 + fr;
+        qok[i] = q < Q;
+        qv[i] = qok[i] ? q : 0;
+    }
+    const int nb = wn * 32 + fr;
+    const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
+    const unsigned bbase = lds0 + (unsigned)(nb * r.wpitch + fh * 16);  // + 32 per k-step
+
+    constexpr int kWaitAll = (7 << 4) | (15 << 8);
+    constexpr int kStores = 4;  // 16-B output stores per thread per row (Q * 8 <= 1024 chunks)
+    constexpr int kWaitStores = kStores | (7 << 4) | (15 << 8);
+    __builtin_amdgcn_s_waitcnt(kWaitAll);
+    __syncthreads();  // weights (ds_write) and the first block (DMA) are in LDS
+    const size_t out_bytes = (size_t)a.N * a.Ho * a.Wo * a.Nout * 2;
+    const __amdgpu_buffer_rsrc_t orsrc =
+        __builtin_amdgcn_make_buffer_rsrc(cl.out, 0, (int)(out_bytes < 0x7fffffffu ? out_bytes : 0x7fffffffu),
+                                          0x00020000);
+
+    int bb = 0;
+    for (; tl < r.rows; tl += gridDim.x) {
+        const int nx = tl + gridDim.x;
+        if (nx < r.rows) issue_block(nx, bb ^ 1);
+        const unsigned hoff = lds0 + (unsigned)(WB + bb * r.hbytes);
+
+        floatx16 acc[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+        bf16x8 af[2][2], bfr[2];
+        // k-step k: taps 2k (fh = 0) and 2k + 1 (fh = 1); tap (rr, ss) reads input row rr,
+        // column q + ss of the block
+        auto load = [&](int k, int c) {
+            const int tp = 2 * k + fh;
+            const int rr = (int)r.fd_s.div((uint32_t)tp), ss = tp - rr * a.Sw;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) af[c][i] = lds_rd128<0>(hoff + (unsigned)((rr * Wi + qv[i] + ss) * 16));
+            bfr[c] = lds_rd128<0>(bbase + (unsigned)(k * 32));
+        };
+        // one k-step of fragments in flight under the MFMAs: wait for everything (lgkmcnt(0)),
+        // then issue the next k-step's reads, then this k-step's MFMAs.  (Counted waits that
+        // keep two k-steps in flight produced sporadic wrong tiles with two workgroups per CU:
+        // LDS returns are not relied on to be in order.)
+        load(0, 0);
+        for (int k0 = 0; k0 < r.ksteps; k0 += 2) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int k = k0 + u;
+                if (k >= r.ksteps) break;
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[u][0]), "+v"(af[u][1]), "+v"(bfr[u]));
+                if (k + 1 < r.ksteps) load(k + 1, u ^ 1);
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+                    acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[u], af[u][i], acc[i], 0, 0, 0);
+            }
+        }
+
+        // epilogue through LDS: the row's [Q][64] bf16 tile is assembled in LDS (16-B chunks
+        // XOR-swizzled by pixel) and written as whole 128-B pixel rows with 16-B stores -
+        // the MFMA layout would store 8 B per lane at a 128-B stride
+        char* ot = lds + WB + 2 * r.hbytes;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int q = wm * 64 + i * 32 + fr;
+#pragma unroll
+            for (int gq = 0; gq < 4; ++gq) {
+                const int chunk = (wn * 4 + gq) ^ (q & 7);
+                *reinterpret_cast<uint2*>(ot + q * 128 + chunk * 16 + 8 * fh) =
+                    make_uint2(pack_bf2(acc[i][4 * gq], acc[i][4 * gq + 1]),
+                               pack_bf2(acc[i][4 * gq + 2], acc[i][4 * gq + 3]));
+            }
+        }
+        __syncthreads();
+        const int b = (int)r.fd_p.div((uint32_t)tl), p = tl - b * P;
+        const unsigned rowoff = (unsigned)(((size_t)(b * a.Ho + p) * a.Wo) * a.Nout * 2);
+#pragma unroll
+        for (int u = 0; u < kStores; ++u) {
+            const int e = t + 256 * u;  // 16-B chunk e of the row: pixel e / 8, chunk e % 8
+            const int q = e >> 3, j = e & 7;
+            const bool ok = q < Q;
+            const uint4 v = *reinterpret_cast<const uint4*>(ot + (ok ? q : 0) * 128 + ((j ^ (q & 7)) << 4));
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
+                                                   orsrc, ok ? rowoff + (unsigned)e * 16u : 0xfffffff0u, 0, 0);
+        }
+        __builtin_amdgcn_s_waitcnt(kWaitStores);  // the next block has landed; stores may fly
+        lds_barrier();                            // and the LDS tile / block bb are free again
         bb ^= 1;
     }
 }
@@ -1445,6 +1596,54 @@ static int launch_halo_v(ConvArgs& a, int hb, hipStream_t st) {
     return check_launch("k_conv_halo");
 }
 
+static int g_conv_stem = [] {
+    const char* e = getenv("GM_CONV_STEM");  // 0: the pixel-pair stem takes the im2col kernel
+    return e ? atoi(e) : 1;
+}();
+
+// k_conv_stem serves one-class forward convolutions over 8-channel elements with 64
+// output channels, no padding, unit column stride, output columns <= 128 and an even
+// tap count; returns its LDS bytes (0 = not eligible)
+static size_t stem_plan(const ConvArgs& a, StemArgs& r) {
+    if (!g_conv_stem || a.ncls != 1 || a.C != 8 || a.Nout != 64 || a.sAw != 1 || a.sAh < 1) return 0;
+    const ConvCls& c = a.cls[0];
+    if (c.oS != 1 || c.oH != 0 || c.oW != 0 || c.Q > 128 || c.ntap != a.T || (a.T & 1) || a.T > 64) return 0;
+    for (int tp = 0; tp < c.ntap; ++tp) {  // forward taps without padding: (r, s) = (dh, dw), weight tap tp
+        const int rr = tp / a.Sw, ss = tp - rr * a.Sw;
+        if (c.tw[tp] != tp || c.dh[tp] != rr || c.dw[tp] != ss) return 0;
+    }
+    const int R = a.T / a.Sw;
+    if ((c.P - 1) * a.sAh + R > a.Hi || c.Q - 1 + a.Sw > a.Wi) return 0;
+    if ((size_t)a.N * a.Ho * a.Wo * a.Nout * 2 >= 0x7ffff000u) return 0;
+    r.T = a.T;
+    r.ksteps = a.T / 2;
+    r.rows = a.N * c.P;
+    r.blk = R * a.Wi * 16;
+    r.nI = (r.blk + 1023) / 1024;
+    r.hbytes = r.nI * 1024;
+    r.wpitch = a.T * 16 + 16;
+    r.fd_p = FastDiv((uint32_t)c.P);
+    r.fd_s = FastDiv((uint32_t)a.Sw);
+    const size_t lds = (size_t)64 * r.wpitch + 2 * (size_t)r.hbytes + 128 * 128;  // + the output tile
+    return lds <= 80 * 1024 ? lds : 0;  // two workgroups per CU
+}
+
+static int launch_stem(const ConvArgs& a, const StemArgs& r, size_t lds, hipStream_t st) {
+    static size_t granted = 0;
+    if (lds > granted) {
+        const hipError_t e =
+            hipFuncSetAttribute((const void*)k_conv_stem, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) {
+            set_error("k_conv_stem: %zu B of LDS refused (%s)", lds, hipGetErrorString(e));
+            return GM_E_UNSUP;
+        }
+        granted = lds;
+    }
+    const int grid = r.rows < 512 ? r.rows : 512;  // persistent: two workgroups per CU
+    k_conv_stem<<<grid, 256, lds, st>>>(a, r);
+    return check_launch("k_conv_stem");
+}
+
 static int g_conv_rw = [] {
     const char* e = getenv("GM_CONV_RW");  // 0: layer-1 shapes take the im2col kernel
     return e ? atoi(e) : 1;
@@ -1515,6 +1714,11 @@ static int pick_and_launch(ConvArgs& a, hipStream_t st, void* ws, size_t ws_byte
         RwArgs r;
         const size_t lds = rw_plan(a, r);
         if (lds > 0) return launch_rw(a, r, lds, st);
+    }
+    {
+        StemArgs r;
+        const size_t lds = stem_plan(a, r);
+        if (lds > 0) return launch_stem(a, r, lds, st);
     }
     TilePick p = pick_tile(a);
     if (p.splits > 1 && (!ws || ws_bytes < splitk_bytes(p) || p.tiles > kMaxSplitTiles)) {  // the unsplit choice
@@ -1725,6 +1929,11 @@ unsigned conv_faults_read(bool clear) {
 
 extern "C" int gm_conv_set_halo(int on) {
     g_conv_halo = on ? 1 : 0;
+    return GM_OK;
+}
+
+extern "C" int gm_conv_set_stem(int on) {
+    g_conv_stem = on ? 1 : 0;
     return GM_OK;
 }
 

@@ -295,3 +295,31 @@ def test_conv_dgrad_fused_addend(dev, shape):
                                               False, [0, 0], 1, [True, False, False])[0]
     _close(dxa, dxr + add.float(), 1e-2)
     _close(dxa, dx.float() + add.float(), 1e-2)
+
+
+@pytest.mark.parametrize("shape", [(64, 3, 224, 224), (3, 3, 37, 30), (2, 3, 64, 64), (5, 3, 250, 200)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_stem_resident_weight_kernel(dev, shape):
+    """The pixel-pair stem (7x7/s2, 3 -> 64 channels) on the resident-weight kernel
+    (weights in LDS, one output row per step, double-buffered input rows) equals the
+    im2col kernel and the fp32 convolution."""
+    from greedy_multimodal_learning_amd import _lib as L
+    from greedy_multimodal_learning_amd import conv as G
+    lib = L.load()
+    N, C, H, W = shape
+    g = torch.Generator(device="cuda").manual_seed(sum(shape))
+    x = torch.randn(N, C, H, W, device=dev, generator=g)
+    w = torch.randn(64, C, 7, 7, device=dev, generator=g) / (C * 49) ** 0.5
+    P, Q, Sp, Hp, Wp = G._stem_geom(H, W, 7, 7, 3)
+    xp, wp = G.stem_pack(x, w, 3)
+    try:
+        L.check(lib.gm_conv_set_stem(0), "gm_conv_set_stem")
+        y0 = G.stem_fwd(xp, wp, P, Q)
+        L.check(lib.gm_conv_set_stem(1), "gm_conv_set_stem")
+        y1 = G.stem_fwd(xp, wp, P, Q)
+        torch.cuda.synchronize()
+    finally:
+        lib.gm_conv_set_stem(1)
+    yr = F.conv2d(x.bfloat16().float(), w.bfloat16().float(), stride=2, padding=3)
+    _close(y1, yr, 1e-2)
+    _close(y1, y0, 1e-2)
