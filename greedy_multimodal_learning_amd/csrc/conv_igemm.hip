@@ -1083,8 +1083,9 @@ __global__ __launch_bounds__(256) void k_conv_rw(ConvArgs a, RwArgs r) {
     for (int ks = 0; ks < 4; ++ks) b_ks[ks] = b0 ^ (ks << 5);
 
     constexpr int kWaitAll = (7 << 4) | (15 << 8);  // s_waitcnt vmcnt(0)
-    constexpr int kStores = 8;                      // epilogue stores per wave per tile
+    constexpr int kStores = 8;                      // epilogue stores per wave per tile (addend path)
     constexpr int kWaitStores = kStores | (7 << 4) | (15 << 8);  // vmcnt(kStores)
+    constexpr int kWaitStores4 = 4 | (7 << 4) | (15 << 8);       // LDS-tile path: 4 16-B stores
     __builtin_amdgcn_s_waitcnt(kWaitAll);
     lds_barrier();
     const size_t out_bytes = (size_t)a.N * a.Ho * a.Wo * a.Nout * 2;
@@ -1152,11 +1153,46 @@ __global__ __launch_bounds__(256) void k_conv_rw(ConvArgs a, RwArgs r) {
                 acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[c], af[c][i], acc[i], 0, 0, 0);
         }
 
-        // epilogue: rows p0 + prow, columns pcol; 4 consecutive output channels per store.
-        // The addend (fused gradient join) is loaded for the whole tile first, so its loads
-        // are in flight together instead of one dependent round trip per store.
         const int b = (int)r.fd_tpi.div((uint32_t)tl);
         const int p0 = (tl - b * r.tpi) * r.RT;
+        if (!a.addend) {
+            // epilogue through LDS: the tile's RT whole image rows are one contiguous NHWC
+            // block, assembled in LDS (16-B chunks XOR-swizzled by pixel) and written with
+            // 16-B stores instead of 8 B per lane at a 128-B stride
+            char* ot = lds + WB + 2 * r.hbytes;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int m = wm * 64 + i * 32 + fr;
+#pragma unroll
+                for (int gq = 0; gq < 4; ++gq) {
+                    const int chunk = (wn * 4 + gq) ^ (m & 7);
+                    *reinterpret_cast<uint2*>(ot + m * 128 + chunk * 16 + 8 * fh) =
+                        make_uint2(pack_bf2(acc[i][4 * gq], acc[i][4 * gq + 1]),
+                                   pack_bf2(acc[i][4 * gq + 2], acc[i][4 * gq + 3]));
+                }
+            }
+            __syncthreads();
+            const unsigned tbase = (unsigned)(((size_t)(b * a.Ho + p0) * a.Wo) * a.Nout * 2);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int e = t + 256 * u;  // 16-B chunk e of the tile: pixel e / 8, chunk e % 8
+                const int m = e >> 3, j = e & 7;
+                const bool ok = m < valid;
+                const uint4 v = *reinterpret_cast<const uint4*>(ot + (ok ? m : 0) * 128 + ((j ^ (m & 7)) << 4));
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), orsrc,
+                    ok ? tbase + (unsigned)e * 16u : 0xfffffff0u, 0, 0);
+            }
+            // the next tile's halo (issued before these stores) has landed; the stores may
+            // still be in flight.  Then every wave is done with buffer bb and the LDS tile.
+            if (DIAG != 1) __builtin_amdgcn_s_waitcnt(kWaitStores4);
+            lds_barrier();
+            bb ^= 1;
+            continue;
+        }
+        // epilogue with the fused gradient join: rows p0 + prow, columns pcol; 4 consecutive
+        // output channels per store, the addend loaded for the whole tile first (its loads in
+        // flight together), added in fp32 before the one rounding to bf16
         size_t off[2];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
@@ -1192,7 +1228,7 @@ __global__ __launch_bounds__(256) void k_conv_rw(ConvArgs a, RwArgs r) {
         // the next tile's halo (issued before these stores) has landed; the stores may
         // still be in flight.  Then every wave is done with buffer bb.
         if (DIAG != 1) __builtin_amdgcn_s_waitcnt(kWaitStores);
-        __builtin_amdgcn_s_barrier();
+        lds_barrier();
         bb ^= 1;
     }
 }
@@ -1672,7 +1708,7 @@ static size_t rw_plan(const ConvArgs& a, RwArgs& r) {
     r.hbytes = r.nI * 1024;
     r.fd_w2 = FastDiv((uint32_t)(a.Wi + 2));
     r.fd_tpi = FastDiv((uint32_t)r.tpi);
-    const size_t lds = (size_t)kRwWeightBytes + 2 * (size_t)r.hbytes;
+    const size_t lds = (size_t)kRwWeightBytes + 2 * (size_t)r.hbytes + 128 * 128;  // + the output tile
     return lds <= 160 * 1024 ? lds : 0;
 }
 
