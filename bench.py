@@ -112,8 +112,9 @@ def conv_roofline(conv, traffic):
                 "unit": "TFLOP/s", "frac": None, "traffic": None,
                 "note": "per-shape table covers the ResNet-18 trunk only (C2/C4); see the C2 line"}
     flops, secs, launches = conv
-    return {"kernel": "trunk convolutions (bf16 MFMA implicit GEMM k_conv_igemm_ut/k_conv_igemm fwd + "
-                      "input grad, k_conv_wgrad4 weight grad; every trunk shape of one view at the "
+    return {"kernel": "trunk convolutions (bf16 MFMA: k_conv_stem pixel-pair stem, k_conv_rw layer-1 "
+                      "resident-weight, k_conv_halo layer 2-4 3x3, k_conv_igemm_ut strided/1x1 fwd + input "
+                      "grad, k_conv_wgrad4 + k_wgrad_sum weight grad; every trunk shape of one view at the "
                       "step's batch, tools/trunk_table.py)",
             "bound": "mfma", "achieved": round(flops / secs / 1e12, 1), "peak": MFMA_PEAK_TFS, "unit": "TFLOP/s",
             "frac": round(flops / secs / 1e12 / MFMA_PEAK_TFS, 4), "traffic": traffic,
