@@ -428,7 +428,13 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
         if (q < a.ncls && bid >= a.cls[q].tile_start) ci = q;
     const ConvCls& cl = a.cls[ci];
     const int wgid = bid - cl.tile_start;
-    const int tm = wgid % cl.tiles_m, tn = wgid / cl.tiles_m;
+    // tile order: with the XCD remap, tm fastest (an XCD's contiguous tile range shares a
+    // weight slice); without it (split-K needs the dispatch order), tn fastest, so that
+    // with a power-of-two column count the round-robin XCD dealing (block b on XCD b % 8)
+    // keeps each weight slice on the same XCD(s) - L2-resident instead of re-fetched
+    const int tiles_n = (a.Nout + BN - 1) / BN;
+    const int tm = a.xcd ? wgid % cl.tiles_m : wgid / tiles_n;
+    const int tn = a.xcd ? wgid / cl.tiles_m : wgid - tm * tiles_n;
     const int m0 = tm * BM, n0 = tn * BN;
     const int PQ = cl.P * cl.Q;
     const int M = a.N * PQ;
@@ -743,7 +749,10 @@ __global__ __launch_bounds__(256) void k_conv_halo(ConvArgs a, HaloArgs h) {
         bid -= split * a.tiles_total;
     }
     const ConvCls& cl = a.cls[0];
-    const int tm = bid % cl.tiles_m, tn = bid / cl.tiles_m;
+    // tn fastest: blocks are dealt round-robin over the 8 XCDs (b on XCD b % 8), so with a
+    // power-of-two column count each XCD's blocks share one weight slice (L2-resident)
+    const int tiles_n = (a.Nout + BN - 1) / BN;
+    const int tm = bid / tiles_n, tn = bid - tm * tiles_n;
     const int m0 = tm * BM, n0 = tn * BN;
     const int H = a.Hi, W = a.Wi, W2 = W + 2, H1 = H + 1;
     const int PQ = cl.P * cl.Q;  // == H * W (stride 1, same size)
