@@ -283,6 +283,7 @@ EXPORTS.update({
 EXPORTS.update({
     "gm_conv_set_pipe": (c_int, [c_int]),
     "gm_conv_set_halo": (c_int, [c_int]),
+    "gm_conv_set_wgrad_wide": (c_int, [c_int]),
     "gm_conv_set_rw": (c_int, [c_int]),
     "gm_conv_set_stem": (c_int, [c_int]),
 })

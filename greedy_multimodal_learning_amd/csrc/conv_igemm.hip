@@ -730,17 +730,23 @@ struct HaloArgs {
     FastDiv fd_w2, fd_h1;     // W + 2, H + 1
 };
 
-template <int BN, int DIAG, int NB>
+// BM = 256 (one workgroup per CU): the weight bytes staged per FLOP - the binding
+// LDS-DMA traffic of the BM = 128 form - halve; the halo is double-buffered and the
+// next chunk's halo is DMA'd in pieces under the current chunk's first eight k-tiles
+// (the BM = 128 form relies on its co-resident second workgroup to hide that load).
+template <int BM, int BN, int DIAG, int NB>
 __global__ __launch_bounds__(256) void k_conv_halo(ConvArgs a, HaloArgs h) {
-    constexpr int BM = 128, BK = 64;  // NB: stages of the weight (B) ring, 2 or 3
+    constexpr int BK = 64;  // NB: stages of the weight (B) ring, 2 or 3
     // DIAG (timing diagnostics, outputs meaningless): 5 = no DMA, 6 = no MFMA/LDS reads
     constexpr bool kDma = DIAG != 5, kMath = DIAG != 6;
+    constexpr bool kHB2 = BM == 256;  // double-buffered halo, prefetched in pieces
     constexpr int BR = BN / 32;
     constexpr int MT = BM / 64, NT = BN / 64;
     constexpr int SB = BN * 128;
     extern __shared__ __attribute__((aligned(16))) uint4 smem[];
-    char* lds = reinterpret_cast<char*>(smem);  // [halo][B0][B1]
+    char* lds = reinterpret_cast<char*>(smem);  // [halo (x2 when kHB2)][B0][B1]([B2])
     const int HB = h.halo_bytes;
+    const int BOFF = kHB2 ? 2 * HB : HB;  // start of the B ring
 
     int bid = blockIdx.x;
     int split = 0;
@@ -810,15 +816,17 @@ __global__ __launch_bounds__(256) void k_conv_halo(ConvArgs a, HaloArgs h) {
     for (int j = 0; j < NT; ++j) {
         const int row = wn * (BN / 2) + j * 32 + fr;
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) b_rd[j][ks] = HB + row * 128 + (swz(row, ks * 2 + fh) << 4);
+        for (int ks = 0; ks < 4; ++ks) b_rd[j][ks] = BOFF + row * 128 + (swz(row, ks * 2 + fh) << 4);
     }
 
     typedef __attribute__((address_space(1))) const void* gptr_t;
     typedef __attribute__((address_space(3))) void* lptr_t;
     // the halo of channel chunk cc: instructions I = wave, wave+4, ... of nI, 8 pixels each
-    auto issue_halo = [&](int cc) {
+    // (instructions [I0, I1) only, into halo buffer hb)
+    auto issue_halo_part = [&](int cc, int hb, int I0, int I1) {
         const int cbase = cc << 6;
-        for (int I = wave; I < nI; I += 4) {
+        char* dst = lds + hb * HB;
+        for (int I = I0 + wave; I < I1; I += 4) {
             const int hp = I * 8 + (lane >> 3);
             const void* src = (const void*)g_zero16;
             if (hp < npix) {
@@ -830,9 +838,13 @@ __global__ __launch_bounds__(256) void k_conv_halo(ConvArgs a, HaloArgs h) {
                     src = (const void*)(a.in + ((size_t)((b * H + rr - 1) * W + c - 1) << a.logC) + cbase + gc * 8);
                 }
             }
-            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + I * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + I * 1024), 16, 0, 0);
         }
     };
+    auto issue_halo = [&](int cc) { issue_halo_part(cc, kHB2 ? (cc & 1) : 0, 0, nI); };
+    // the kHB2 prefetch: piece tp (0..7) of the next chunk's halo, 4 instructions a
+    // multiple so every wave issues whole rounds
+    const int nIp = ((nI + 31) >> 5) << 2;  // instructions per piece
     auto issue_b = [&](int kt, int buf) {
         const int k = kt0 + kt;
         const int cc = k / 9, tp = k - cc * 9;
@@ -842,7 +854,7 @@ __global__ __launch_bounds__(256) void k_conv_halo(ConvArgs a, HaloArgs h) {
 #pragma unroll
         for (int j = 0; j < BR; ++j) {
             const void* src = b_ok[j] ? (const void*)(b_ptr[j] + boff) : (const void*)g_zero16;
-            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + HB + buf * SB + (wave * BR + j) * 1024), 16,
+            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + BOFF + buf * SB + (wave * BR + j) * 1024), 16,
                                              0, 0);
         }
     };
@@ -855,12 +867,12 @@ __global__ __launch_bounds__(256) void k_conv_halo(ConvArgs a, HaloArgs h) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    auto compute = [&](int buf, int toff) {
+    auto compute = [&](int buf, int toff, int hoff) {
         int abase[MT];
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
             const int hp = hbase[i] + toff;
-            abase[i] = (hp << 7) | ((((hp >> 1) & 7) ^ fh) << 4);  // chunk (2ks+fh)^swz = this ^ (ks<<5)
+            abase[i] = hoff + ((hp << 7) | ((((hp >> 1) & 7) ^ fh) << 4));  // chunk (2ks+fh)^swz = this ^ (ks<<5)
         }
         bf16x8 af[2][MT], bfr[2][NT];
 #pragma unroll
@@ -909,10 +921,19 @@ __global__ __launch_bounds__(256) void k_conv_halo(ConvArgs a, HaloArgs h) {
         if (NB == 3 && kt + 1 < nk) __builtin_amdgcn_s_waitcnt(kWaitB);
         else __builtin_amdgcn_s_waitcnt(kWaitAll);
         __builtin_amdgcn_s_barrier();
-        if (kDma && kt > 0 && tp == 0) {  // next channel chunk: every wave is done with the old halo
+        if (!kHB2 && kDma && kt > 0 && tp == 0) {  // next channel chunk: every wave is done with the old halo
             issue_halo(k / 9);
             __builtin_amdgcn_s_waitcnt(kWaitAll);
             __builtin_amdgcn_s_barrier();
+        }
+        // kHB2: the next chunk's halo goes to the other buffer (last read by the previous
+        // chunk, whose k-tiles every wave has passed at this barrier), issued before this
+        // k-tile's B stage so the counted B waits stay valid, landed by the chunk's first wait
+        if (kHB2 && kDma && kt - tp + 9 < nk) {
+            // pieces [lo, hi): a split that starts mid-chunk issues the pieces it skipped
+            const int lo = kt == 0 ? 0 : tp, hi = tp < 8 ? tp + 1 : 8;
+            const int cn = k / 9 + 1;
+            if (lo < hi) issue_halo_part(cn, cn & 1, lo * nIp, min(hi * nIp, nI));
         }
         if (kDma && kt + NB - 1 < nk) {
             int sn = sb + NB - 1;
@@ -921,7 +942,7 @@ __global__ __launch_bounds__(256) void k_conv_halo(ConvArgs a, HaloArgs h) {
         }
         const int ti = tp / 3, tj = tp - ti * 3;
         const int dh = (int)((pk_dh >> (4 * ti)) & 15u) - 8, dw = (int)((pk_dw >> (4 * tj)) & 15u) - 8;
-        if (kMath) compute(sb, dh * W2 + dw);
+        if (kMath) compute(sb, dh * W2 + dw, kHB2 ? ((k / 9) & 1) * HB : 0);
         if (++sb == NB) sb = 0;
     }
 
@@ -1592,7 +1613,7 @@ static int g_conv_halo = [] {
 // the halo kernel serves one-class, 3x3 tap grids with offsets in [-1, 1] at stride 1
 // and same-size output (forward 3x3/s1/p1 and its input gradient), C a multiple of 64;
 // returns the halo LDS bytes (0 = not eligible)
-static int halo_bytes(const ConvArgs& a) {
+static int halo_bytes(const ConvArgs& a, int BM = 128) {
     // C >= 128 (two or more chunks): with one chunk (ResNet layer 1) the whole halo must
     // land before the first k-tile and the im2col kernel measured faster (tools/conv_ab.py)
     if (!g_conv_halo || a.ncls != 1 || a.C < 128 || (a.C & 63) || a.sAh != 1 || a.sAw != 1) return 0;
@@ -1604,8 +1625,8 @@ static int halo_bytes(const ConvArgs& a) {
         if (c.cdh[i] < -1 || c.cdh[i] > 1 || c.cdw[i] < -1 || c.cdw[i] > 1) return 0;
     const int H1 = a.Hi + 1, W2 = a.Wi + 2, PQ = c.P * c.Q, M = a.N * PQ;
     int maxpix = 0;
-    for (int m0 = 0; m0 < M; m0 += 128) {
-        const int m1 = (m0 + 128 < M ? m0 + 128 : M) - 1;
+    for (int m0 = 0; m0 < M; m0 += BM) {
+        const int m1 = (m0 + BM < M ? m0 + BM : M) - 1;
         const int b0 = m0 / PQ, p0 = (m0 - b0 * PQ) / c.Q;
         const int b1 = m1 / PQ, p1 = (m1 - b1 * PQ) / c.Q;
         const int npix = (b1 * H1 + p1 + 2 - (b0 * H1 + p0) + 1) * W2;
@@ -1614,11 +1635,11 @@ static int halo_bytes(const ConvArgs& a) {
     return (maxpix + 7) / 8 * 1024;
 }
 
-template <int BN, int DIAG, int NB>
+template <int BN, int DIAG, int NB, int BM = 128>
 static int launch_halo_v(ConvArgs& a, int hb, hipStream_t st) {
     ConvCls& c = a.cls[0];
     const int M = a.N * c.P * c.Q;
-    c.tiles_m = (M + 127) / 128;
+    c.tiles_m = (M + BM - 1) / BM;
     c.tile_start = 0;
     a.tiles_total = c.tiles_m * ((a.Nout + BN - 1) / BN);
     if (a.splits < 1) a.splits = 1;
@@ -1626,10 +1647,10 @@ static int launch_halo_v(ConvArgs& a, int hb, hipStream_t st) {
     h.halo_bytes = hb;
     h.fd_w2 = FastDiv((uint32_t)(a.Wi + 2));
     h.fd_h1 = FastDiv((uint32_t)(a.Hi + 1));
-    const size_t lds = (size_t)hb + NB * (size_t)BN * 128;
+    const size_t lds = (size_t)hb * (BM == 256 ? 2 : 1) + NB * (size_t)BN * 128;
     static size_t attr = 0;  // largest dynamic LDS granted so far (idempotent, safe to race)
     if (lds > attr) {
-        const hipError_t e = hipFuncSetAttribute((const void*)k_conv_halo<BN, DIAG, NB>,
+        const hipError_t e = hipFuncSetAttribute((const void*)k_conv_halo<BM, BN, DIAG, NB>,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) {
             set_error("k_conv_halo: %zu B of LDS refused (%s)", lds, hipGetErrorString(e));
@@ -1637,7 +1658,7 @@ static int launch_halo_v(ConvArgs& a, int hb, hipStream_t st) {
         }
         attr = lds;
     }
-    k_conv_halo<BN, DIAG, NB><<<a.tiles_total * a.splits, 256, lds, st>>>(a, h);
+    k_conv_halo<BM, BN, DIAG, NB><<<a.tiles_total * a.splits, 256, lds, st>>>(a, h);
     return check_launch("k_conv_halo");
 }
 
@@ -1753,8 +1774,62 @@ static int launch_halo(ConvArgs& a, int hb, hipStream_t st) {
     return launch_halo_v<BN, 0, 2>(a, hb, st);
 }
 
+// 256-pixel halo tiles (one workgroup per CU, BN = 128): eligible when the double
+// halo plus a 3-stage weight ring fits the CU's LDS.  Tiles too few to fill the chip
+// split K (2-4 ways, >= 16 k-tiles each) through the turnstile when the workspace holds
+// the 256x128 slabs.  Returns 0 when not taken.
+struct Halo256Plan {
+    int hb = 0;        // one halo buffer's LDS bytes (0: not taken)
+    int tiles = 0, splits = 1;
+    size_t ws = 0;     // split-K workspace bytes (turnstile words + 256x128 fp32 slabs)
+};
+
+static Halo256Plan halo256_plan(const ConvArgs& a) {
+    Halo256Plan p;
+    if (g_conv_halo != 2 || a.Nout % 128) return p;
+    const int hb = halo_bytes(a, 256);
+    if (hb <= 0 || 2 * hb + 3 * 128 * 128 > 160 * 1024) return p;
+    const int M = a.N * a.cls[0].P * a.cls[0].Q;
+    p.hb = hb;
+    p.tiles = (M + 255) / 256 * (a.Nout / 128);
+    const int nk = 9 * (a.C >> 6);
+    int S = p.tiles >= 192 ? 1 : 256 / p.tiles;
+    S = S > 4 ? 4 : S;
+    while (S > 1 && nk / S < 16) --S;
+    if (p.tiles > kMaxSplitTiles) S = 1;
+    p.splits = S;
+    if (S > 1) p.ws = splitk_flag_bytes(p.tiles) + (size_t)p.tiles * 32 * 256 * 16;
+    return p;
+}
+
+static int try_halo256(ConvArgs& a, hipStream_t st, void* ws, size_t ws_bytes) {
+    const Halo256Plan pl = halo256_plan(a);
+    if (pl.hb <= 0) return 0;
+    const int hb = pl.hb, tiles = pl.tiles;
+    int S = pl.splits;
+    if (S > 1 && (!ws || ws_bytes < pl.ws)) S = 1;
+    a.splits = S;
+    a.xcd = 0;
+    if (S > 1) {
+        a.spin_limit = spin_limit();
+        a.flags = static_cast<unsigned*>(ws);
+        a.ws = reinterpret_cast<float*>(static_cast<char*>(ws) + splitk_flag_bytes(tiles));
+    }
+    const int p = conv_pipe();
+    int rc;
+    if (p == 5) rc = launch_halo_v<128, 5, 3, 256>(a, hb, st);
+    else if (p == 6) rc = launch_halo_v<128, 6, 3, 256>(a, hb, st);
+    else rc = launch_halo_v<128, 0, 3, 256>(a, hb, st);
+    return rc == GM_OK ? 1 : rc;
+}
+
 static int pick_and_launch(ConvArgs& a, hipStream_t st, void* ws, size_t ws_bytes) {
     const bool three = stages() == 3;
+    {
+        const int r = try_halo256(a, st, ws, ws_bytes);
+        if (r == 1) return GM_OK;
+        if (r != 0) return r;
+    }
     {
         RwArgs r;
         const size_t lds = rw_plan(a, r);
@@ -1973,7 +2048,7 @@ unsigned conv_faults_read(bool clear) {
 }  // namespace gm
 
 extern "C" int gm_conv_set_halo(int on) {
-    g_conv_halo = on ? 1 : 0;
+    g_conv_halo = on < 0 ? 0 : on > 2 ? 2 : on;
     return GM_OK;
 }
 
@@ -2059,7 +2134,8 @@ extern "C" size_t gm_conv2d_splitk_ws_bytes(const gm_conv_desc* d, int dgrad) {
         const gm_conv_desc_hw h = to_hw(d);
         fwd_setup(&h, nullptr, nullptr, nullptr, a);
     }
-    return splitk_bytes(pick_tile(a));
+    const size_t b128 = splitk_bytes(pick_tile(a)), b256 = halo256_plan(a).ws;
+    return b128 > b256 ? b128 : b256;
 }
 
 extern "C" int gm_conv_weight_transpose_bf16(const void* w, void* wt, int Co, int T, int Ci, void* stream) {

@@ -81,7 +81,13 @@ __device__ __forceinline__ bf16x8 tr_frag_asm(int ks, unsigned a) {
 // lgkmcnt(0), tied to the fragments (MT + NT of them) the next MFMAs read
 template <int MT, int NT>
 __device__ __forceinline__ void wait_lgkm0(bf16x8 (&a)[MT], bf16x8 (&b)[NT]) {
-    if constexpr (MT == 2 && NT == 2)
+    if constexpr (MT > 2 || NT > 2) {  // the wait, then every fragment re-defined after it
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int i = 0; i < MT; ++i) asm volatile("" : "+v"(a[i]));
+#pragma unroll
+        for (int j = 0; j < NT; ++j) asm volatile("" : "+v"(b[j]));
+    } else if constexpr (MT == 2 && NT == 2)
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(a[1]), "+v"(b[0]), "+v"(b[1]));
     else if constexpr (MT == 2)
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(a[1]), "+v"(b[0]));
@@ -199,7 +205,7 @@ __device__ __attribute__((aligned(16))) const uint4 g_wzero16[1] = {{0u, 0u, 0u,
 // read a zero block of the code object.
 template <int RB>  // row bytes (128 or 256)
 __device__ __forceinline__ int wswz(int row) {
-    return RB == 256 ? 4 * (row & 3) : 4 * ((row >> 1) & 1);
+    return RB >= 256 ? 4 * (row & 3) : 4 * ((row >> 1) & 1);
 }
 
 template <int MT, int NT>
@@ -328,14 +334,25 @@ __global__ __launch_bounds__(256) void k_conv_wgrad4(WgradArgs a) {
         b_lds[j] = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)(lds + b_base[j]);
     // one k-slice's fragments (asm reads; the caller waits), then its MFMAs; the next
     // slice's reads are issued before this slice's MFMAs
+    // buffer 1 at an immediate offset while that fits the 16-bit field, else from its own
+    // base registers (wide tiles: 64 KB buffers)
+    constexpr bool kFarBuf = 2 * (SA + SB) > 65536;
+    unsigned a_lds1[MT], b_lds1[NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) a_lds1[i] = a_lds[i] + (SA + SB);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) b_lds1[j] = b_lds[j] + (SA + SB);
     auto compute = [&](auto bufc) {
-        constexpr int BO = decltype(bufc)::value;
+        constexpr int BO0 = decltype(bufc)::value;
+        constexpr int BO = kFarBuf ? 0 : BO0;
+        const unsigned* ab = (kFarBuf && BO0) ? a_lds1 : a_lds;
+        const unsigned* bb = (kFarBuf && BO0) ? b_lds1 : b_lds;
         bf16x8 af[2][MT], bfr[2][NT];
         auto load = [&](int ks, int c) {
 #pragma unroll
-            for (int i = 0; i < MT; ++i) af[c][i] = tr_frag_asm<BO, RA>(ks, a_lds[i]);
+            for (int i = 0; i < MT; ++i) af[c][i] = tr_frag_asm<BO, RA>(ks, ab[i]);
 #pragma unroll
-            for (int j = 0; j < NT; ++j) bfr[c][j] = tr_frag_asm<BO, RB>(ks, b_lds[j]);
+            for (int j = 0; j < NT; ++j) bfr[c][j] = tr_frag_asm<BO, RB>(ks, bb[j]);
         };
         load(0, 0);
 #pragma unroll
@@ -488,6 +505,12 @@ static int wgrad_target_wgs() {
 
 
 
+static int g_wgrad_wide = [] {
+    const char* e = getenv("GM_WGRAD_WIDE");
+    return e ? atoi(e) : 0;
+}();
+static int wgrad_wide() { return g_wgrad_wide; }
+
 struct WPlan {
     int P, Q, tiles_k, tiles_n, splits, sps, mt, nt;
 };
@@ -503,6 +526,11 @@ static WPlan plan(const gm_conv_desc_hw* d) {
     if (wgrad_version() >= 2) {
         w.mt = d->K >= 128 ? 2 : 1;
         w.nt = TC >= 128 ? 2 : 1;
+        // wide tiles (one workgroup per CU): 256-row / 256-column tiles halve the
+        // staged bytes per MFMA of the dimension they widen (g_wgrad_wide bit 0: rows,
+        // bit 1: columns)
+        if ((wgrad_wide() & 1) && d->K >= 256 && w.mt == 2) w.mt = 4;
+        if ((wgrad_wide() & 2) && TC >= 256 && w.nt == 2) w.nt = 4;
     }
     w.tiles_k = (d->K + 64 * w.mt - 1) / (64 * w.mt);
     w.tiles_n = (TC + 64 * w.nt - 1) / (64 * w.nt);
@@ -594,7 +622,11 @@ extern "C" int gm_conv2d_wgrad_hw_bf16(const gm_conv_desc_hw* d, const void* dy,
         a.S = d->S;
         a.padh = d->pad_h;
         a.padw = d->pad_w;
-        if (w.mt == 2 && w.nt == 2) rc = launch_wgrad4<2, 2>(a, grid, st);
+        if (w.mt == 4 && w.nt == 4) rc = launch_wgrad4<4, 4>(a, grid, st);
+        else if (w.mt == 4) rc = launch_wgrad4<4, 2>(a, grid, st);
+        else if (w.nt == 4 && w.mt == 2) rc = launch_wgrad4<2, 4>(a, grid, st);
+        else if (w.nt == 4) rc = launch_wgrad4<1, 4>(a, grid, st);
+        else if (w.mt == 2 && w.nt == 2) rc = launch_wgrad4<2, 2>(a, grid, st);
         else if (w.mt == 2) rc = launch_wgrad4<2, 1>(a, grid, st);
         else if (w.nt == 2) rc = launch_wgrad4<1, 2>(a, grid, st);
         else rc = launch_wgrad4<1, 1>(a, grid, st);
@@ -625,6 +657,12 @@ extern "C" int gm_conv2d_wgrad_hw_bf16(const gm_conv_desc_hw* d, const void* dy,
     if (g > 4096) g = 4096;
     k_wgrad_reduce<<<g, 256, 0, st>>>(a.part, a.splits, d->K, a.T, d->C, c_real, accumulate, dw);
     return check_launch("k_wgrad_reduce");
+}
+
+extern "C" int gm_conv_set_wgrad_wide(int mode) {
+    GM_REQUIRE(mode >= 0 && mode <= 3, "gm_conv_set_wgrad_wide: 0..3 (bit 0: 256-row tiles, bit 1: 256-column tiles)");
+    g_wgrad_wide = mode;
+    return GM_OK;
 }
 
 extern "C" int gm_conv2d_wgrad_bf16(const gm_conv_desc* d, const void* dy, const void* x, float* dw, int c_real,

@@ -31,6 +31,8 @@ re-organised for the hardware:
 """
 import os
 
+import time
+
 import torch
 import torch.distributed as dist
 
@@ -384,6 +386,12 @@ class BalancedStep:
         torch.cuda.synchronize(self.device)
         dp = self.buckets is not None
         inline = dp and self.graph_collectives  # collectives captured in the graph
+        if inline:
+            # the process group's watchdog (polling every 100 ms) must have dropped the
+            # completed eager works first: HIP refuses a query of an event recorded on the
+            # RCCL stream while that stream is being captured, and the watchdog thread
+            # aborts the process on that error
+            time.sleep(0.5)
         if dp and not inline:
             self.buckets.deferred = True
         # thread_local: the process group's watchdog thread keeps querying its events

@@ -289,6 +289,9 @@ int gm_conv_set_pipe(int pipe);
  * the input once per 64-channel chunk as a halo instead of once per tap (default on;
  * GM_CONV_HALO=0 or gm_conv_set_halo(0) selects the im2col kernel for them). */
 int gm_conv_set_halo(int on);
+/* Weight-gradient tile form (process-wide; GM_WGRAD_WIDE at load): bit 0 takes
+ * 256-row tiles for K >= 256, bit 1 256-column (tap, channel) tiles; 0 = 128 x 128. */
+int gm_conv_set_wgrad_wide(int mode);
 /* Resident-weight kernel for 3x3 / stride-1 convolutions with 64 -> 64 channels (ResNet
  * layer 1, forward and input gradient; default on, GM_CONV_RW=0 at load or
  * gm_conv_set_rw(0) selects the im2col kernel for them). */

@@ -323,3 +323,42 @@ def test_stem_resident_weight_kernel(dev, shape):
     yr = F.conv2d(x.bfloat16().float(), w.bfloat16().float(), stride=2, padding=3)
     _close(y1, yr, 1e-2)
     _close(y1, y0, 1e-2)
+
+
+HALO_SHAPES = [  # N, C, H, W, K: 3x3 / stride 1 / pad 1 (ResNet layers 2-4 and a ragged batch)
+    (8, 128, 28, 28, 128),   # 256-pixel tiles unsplit
+    (8, 256, 14, 14, 256),   # split-K 2 through the turnstile
+    (8, 512, 7, 7, 512),     # split-K 4
+    (3, 128, 9, 11, 256),    # tiles spanning images, a partial last tile
+]
+
+
+@pytest.mark.parametrize("mode", [1, 2], ids=["halo128", "halo256"])
+@pytest.mark.parametrize("shape", HALO_SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_conv_halo_tiles(dev, shape, mode):
+    """The halo-staged kernel in its 128- and 256-pixel tile forms (gm_conv_set_halo 1 / 2)
+    vs fp32 PyTorch: forward and the stride-1 input gradient."""
+    from greedy_multimodal_learning_amd import _lib as L
+    from greedy_multimodal_learning_amd import conv as G
+    N, C, H, W, K = shape
+    g = torch.Generator().manual_seed(sum(shape) + mode)
+    x = torch.randn(N, C, H, W, generator=g).bfloat16()
+    w = (torch.randn(K, C, 3, 3, generator=g) / (C * 9) ** 0.5).bfloat16()
+    gy = torch.randn(N, K, H, W, generator=g).bfloat16()
+    xr, wr = x.float().requires_grad_(True), w.float()
+    yr = F.conv2d(xr, wr, padding=1)
+    yr.backward(gy.float())
+    cl = torch.channels_last
+    lib = L.load()
+    L.check(lib.gm_conv_set_halo(mode), "gm_conv_set_halo")
+    try:
+        xd, wd = x.to(dev).contiguous(memory_format=cl), w.to(dev).contiguous(memory_format=cl)
+        y = G.conv_fwd(xd, wd, 1, 1)
+        wt = wd.permute(1, 0, 2, 3).contiguous(memory_format=cl)
+        dx = G.conv_dgrad_t(gy.to(dev).contiguous(memory_format=cl), wt, H, W, 1, 1)
+        torch.cuda.synchronize()
+        assert L.device_faults(clear=True) == 0
+    finally:
+        lib.gm_conv_set_halo(1)
+    _close(y, yr, 1e-2)
+    _close(dx, xr.grad, 1e-2)

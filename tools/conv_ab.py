@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--pipes", default="0,h", help="comma list of pipe numbers; 'h' = halo kernel on")
+    ap.add_argument("--pipes", default="0,h", help="comma list of pipe numbers; 'h' = halo kernel on, 'H' = 256-pixel halo tiles")
     ap.add_argument("--wgrad", action="store_true", help="also time the weight-gradient passes")
     a = ap.parse_args()
     from greedy_multimodal_learning_amd import _lib as L
@@ -34,11 +34,16 @@ def main():
     import trunk_table as T
     dev = torch.device("cuda:0")
     B = a.batch
-    pipes = a.pipes.split(",")
+    pipes = a.pipes.replace("+", ",").split(",")
 
-    def select(p):  # "h", "h5", "h6": the halo kernel (+ diagnostics)
-        L.check(lib.gm_conv_set_halo(1 if p.startswith("h") else 0), "set_halo")
-        L.check(lib.gm_conv_set_pipe(int(p[1:] or 0) if p.startswith("h") else int(p)), "set_pipe")
+    def select(p):  # "h", "h5", "h6": the halo kernel (+ diagnostics); "H...": 256-pixel halo tiles;
+        # "W<n>": halo kernel + weight-gradient tile form n (gm_conv_set_wgrad_wide)
+        L.check(lib.gm_conv_set_wgrad_wide(int(p[1:]) if p[0] == "W" else 0), "set_wgrad_wide")
+        if p[0] == "W":
+            p = "h"
+        hl = p[:1] in ("h", "H")
+        L.check(lib.gm_conv_set_halo((2 if p[0] == "H" else 1) if hl else 0), "set_halo")
+        L.check(lib.gm_conv_set_pipe(int(p[1:] or 0) if hl else int(p)), "set_pipe")
     lib = L.load()
     ops = []
     g = torch.Generator(device=dev).manual_seed(0)
@@ -63,7 +68,7 @@ def main():
     # summation order) within bf16 output rounding of it
     ref = {}
     for p in pipes:
-        if p in ("5", "6", "h5", "h6"):
+        if p in ("5", "6", "h5", "h6", "H5", "H6"):
             continue  # timing diagnostics: outputs meaningless
         select(p)
         for name, op, _, _, fn in ops:
@@ -75,7 +80,7 @@ def main():
                 continue
             d = (out.float() - ref[k].float()).abs().max().item()
             sc = ref[k].float().abs().max().item()
-            if (not p.startswith("h") and not torch.equal(out, ref[k])) or d > 2e-2 * sc:
+            if (p[:1] not in ("h", "H", "W") and not torch.equal(out, ref[k])) or d > 2e-2 * sc:
                 print(f"MISMATCH {p} {name} {op}: max |diff| {d} (scale {sc})", flush=True)
                 sys.exit(3)
     print("all variants agree", flush=True)

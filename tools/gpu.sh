@@ -19,7 +19,7 @@
 #                                                                     -> gpurun_out/pmcg_NAME.txt
 #   trunkpmc     three rocprofv3 --pmc passes over tools/trunk_pmc.py (FETCH, WRITE, MFMA/LDS set),
 #                per-op table + conv-family traffic json         -> gpurun_out/trunk_pmc.md, trunk_pmc.json
-#   py:FILE      python FILE (a tools/ script)                        -> gpurun_out/py_FILE.log
+#   py:FILE[,ARGS] python FILE ARGS (a tools/ script; commas become spaces) -> gpurun_out/py_FILE.log
 set -o pipefail
 mkdir -p gpurun_out
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -92,8 +92,9 @@ for s in "$@"; do
         --json gpurun_out/trunk_pmc.json > gpurun_out/trunk_pmc.md && rm -rf gpurun_out/tp_fetch gpurun_out/tp_write gpurun_out/tp_opmfma
       tail -3 gpurun_out/trunk_pmc.md ;;
     py:*)
-      f="${s#py:}"; lg="gpurun_out/py_$(basename "$f" .py).log"
-      timeout -k 10 600 python -u "$f" > "$lg" 2>&1 || { tail -30 "$lg"; exit 19; }
+      a="${s#py:}"; f="${a%%,*}"; args=""; [ "$f" != "$a" ] && args="${a#*,}"
+      lg="gpurun_out/py_$(basename "$f" .py).log"
+      timeout -k 10 600 python -u "$f" ${args//,/ } > "$lg" 2>&1 || { tail -30 "$lg"; exit 19; }
       tail -20 "$lg" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

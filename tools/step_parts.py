@@ -41,6 +41,17 @@ def main():
     torch.cuda.synchronize()
     rep = (time.perf_counter() - t0) / n * 1e3
     print(f"full step {full:.3f} ms, bare graph replay {rep:.3f} ms, host/tail {full - rep:.3f} ms", flush=True)
+    # CPU cost of the launch call itself: one replay enqueued on an idle GPU, timed to return
+    cpu = []
+    for _ in range(10):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        gr.replay()
+        cpu.append(time.perf_counter() - t0)
+        torch.cuda.synchronize()
+    cpu.sort()
+    print(f"graph launch call (CPU, returns before the GPU finishes): median {cpu[5] * 1e3:.3f} ms, "
+          f"min {cpu[0] * 1e3:.3f} ms", flush=True)
 
 
 if __name__ == "__main__":
