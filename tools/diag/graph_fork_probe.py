@@ -53,6 +53,25 @@ def build(order, n, cyc, main, side):
     return g
 
 
+def build_segments(segs, n, cyc, side):
+    """segs fork/join segments of two n-kernel branches, like the step's MMTM sites"""
+    g = torch.cuda.CUDAGraph()
+    x = torch.zeros(1, device="cuda")
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g):
+        for _ in range(segs):
+            x.add_(1)
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                for _ in range(n):
+                    work(cyc)
+            for _ in range(n):
+                work(cyc)
+            torch.cuda.current_stream().wait_stream(side)
+        x.add_(1)
+    return g
+
+
 def timeit(fn, reps=20):
     fn()
     torch.cuda.synchronize()
@@ -76,6 +95,9 @@ def main():
         g = build(order, n, cyc, main_s, side)
         t = timeit(g.replay)
         print(f"{order:7s} n={n}: {t:8.1f} us per replay = {t / (n * one):.2f} x one chain", flush=True)
+    g = build_segments(8, n, cyc, side)
+    t = timeit(g.replay)
+    print(f"8 segments n={n}: {t:8.1f} us per replay = {t / (8 * n * one):.2f} x one chain per segment", flush=True)
 
 
 if __name__ == "__main__":

@@ -21,7 +21,9 @@ for v in "$@"; do
     base) run base GM_X=0 || exit 1 ;;
     hwq8) run hwq8 GPU_MAX_HW_QUEUES=8 || exit 1 ;;
     eager) BENCHX=--eager run eager GM_X=0 || exit 1 ;;
+    il0) run il0 GM_VIEW_INTERLEAVE=0 || exit 1 ;;
     nopkt) run nopkt DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 || exit 1 ;;
+    env:*) kv="${v#env:}"; run "$(echo "$kv" | tr -c 'A-Za-z0-9_\n' '_')" "${kv//+/ }" || exit 1 ;;
     *) echo "unknown $v"; exit 2 ;;
   esac
 done

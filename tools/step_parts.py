@@ -50,6 +50,16 @@ def main():
         cpu.append(time.perf_counter() - t0)
         torch.cuda.synchronize()
     cpu.sort()
+    # back-to-back: does a launch call wait for the previous replay of the same graph?
+    torch.cuda.synchronize()
+    ts = [time.perf_counter()]
+    for _ in range(8):
+        gr.replay()
+        ts.append(time.perf_counter())
+    torch.cuda.synchronize()
+    te = time.perf_counter()
+    print("back-to-back launch calls (ms): " + " ".join(f"{(b - a) * 1e3:.2f}" for a, b in zip(ts, ts[1:]))
+          + f"; then sync {(te - ts[-1]) * 1e3:.2f}", flush=True)
     print(f"graph launch call (CPU, returns before the GPU finishes): median {cpu[5] * 1e3:.3f} ms, "
           f"min {cpu[0] * 1e3:.3f} ms", flush=True)
 
