@@ -330,27 +330,28 @@ __global__ __launch_bounds__(256) void k_running_avg(const float* e, int ld, int
 // updated in place; the counter is advanced after every thread has read it
 __global__ __launch_bounds__(256) void k_running_avg_dev(const float* e, int ld, int B, int C, float* rv, float* rs,
                                                          int* step, int increment) {
-    __shared__ float part[4][64];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    // one thread per channel (all 256 of them busy, no serial 64-channel passes), the
+    // batch mean in the same order as before: four partial sums over b = w, w+4, ...
+    // combined ((p0 + p1) + p2) + p3
     const int st = *step;
     const float k = (float)st, k1 = (float)(st + 1);
-    for (int c0 = 0; c0 < C; c0 += 64) {
-        const int c = c0 + lane;
-        float m = 0.f;
-        if (c < C) {
-#pragma unroll 4
-            for (int b = w; b < B; b += 4) m += e[(size_t)b * ld + c];
+    for (int c = threadIdx.x; c < C; c += 256) {
+        float p[4] = {0.f, 0.f, 0.f, 0.f};
+        int b = 0;
+        for (; b + 16 <= B; b += 16) {
+            float v[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) v[u] = e[(size_t)(b + u) * ld + c];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) p[u & 3] += v[u];
         }
-        part[w][lane] = m;
-        __syncthreads();
-        if (w == 0 && c < C) {
-            m = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
-            m = m / (float)B;
-            rv[c] = (m + rv[c] * k) / k1;
-            if (rs != rv) rs[c] = (m + rs[c] * k) / k1;
-        }
-        __syncthreads();
+        for (; b < B; ++b) p[b & 3] += e[(size_t)b * ld + c];
+        float m = ((p[0] + p[1]) + p[2]) + p[3];
+        m = m / (float)B;
+        rv[c] = (m + rv[c] * k) / k1;
+        if (rs != rv) rs[c] = (m + rs[c] * k) / k1;
     }
+    __syncthreads();  // every thread has read *step
     if (threadIdx.x == 0 && increment) *step = st + 1;
 }
 
