@@ -735,13 +735,15 @@ struct HaloArgs {
 // next chunk's halo is DMA'd in pieces under the current chunk's first eight k-tiles
 // (the BM = 128 form relies on its co-resident second workgroup to hide that load).
 template <int BM, int BN, int DIAG, int NB>
-__global__ __launch_bounds__(256) void k_conv_halo(ConvArgs a, HaloArgs h) {
+__global__ __launch_bounds__(BM == 256 ? 512 : 256) void k_conv_halo(ConvArgs a, HaloArgs h) {
     constexpr int BK = 64;  // NB: stages of the weight (B) ring, 2 or 3
     // DIAG (timing diagnostics, outputs meaningless): 5 = no DMA, 6 = no MFMA/LDS reads
     constexpr bool kDma = DIAG != 5, kMath = DIAG != 6;
     constexpr bool kHB2 = BM == 256;  // double-buffered halo, prefetched in pieces
-    constexpr int BR = BN / 32;
-    constexpr int MT = BM / 64, NT = BN / 64;
+    constexpr int NW = BM == 256 ? 8 : 4;  // waves: (NW/2) x 2, each a 64x64 sub-tile
+    constexpr int NT_ = NW * 64;           // threads
+    constexpr int BR = BN / (8 * NW);      // B-stage DMA instructions per wave
+    constexpr int MT = 2, NT = BN / 64;
     constexpr int SB = BN * 128;
     extern __shared__ __attribute__((aligned(16))) uint4 smem[];
     char* lds = reinterpret_cast<char*>(smem);  // [halo (x2 when kHB2)][B0][B1]([B2])
@@ -794,7 +796,7 @@ __global__ __launch_bounds__(256) void k_conv_halo(ConvArgs a, HaloArgs h) {
     int hbase[MT];
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
-        int m = m0 + wm * (BM / 2) + i * 32 + fr;
+        int m = m0 + wm * (MT * 32) + i * 32 + fr;
         m = m < M ? m : m0;  // rows past M read a valid pixel; their outputs are not stored
         const int b = (int)cl.fd_pq.div((uint32_t)m), pq = m - b * PQ;
         const int p = (int)cl.fd_q.div((uint32_t)pq), q = pq - p * cl.Q;
@@ -826,7 +828,7 @@ __global__ __launch_bounds__(256) void k_conv_halo(ConvArgs a, HaloArgs h) {
     auto issue_halo_part = [&](int cc, int hb, int I0, int I1) {
         const int cbase = cc << 6;
         char* dst = lds + hb * HB;
-        for (int I = I0 + wave; I < I1; I += 4) {
+        for (int I = I0 + wave; I < I1; I += NW) {
             const int hp = I * 8 + (lane >> 3);
             const void* src = (const void*)g_zero16;
             if (hp < npix) {
@@ -842,9 +844,9 @@ __global__ __launch_bounds__(256) void k_conv_halo(ConvArgs a, HaloArgs h) {
         }
     };
     auto issue_halo = [&](int cc) { issue_halo_part(cc, kHB2 ? (cc & 1) : 0, 0, nI); };
-    // the kHB2 prefetch: piece tp (0..7) of the next chunk's halo, 4 instructions a
+    // the kHB2 prefetch: piece tp (0..7) of the next chunk's halo, NW instructions a
     // multiple so every wave issues whole rounds
-    const int nIp = ((nI + 31) >> 5) << 2;  // instructions per piece
+    const int nIp = (nI + 8 * NW - 1) / (8 * NW) * NW;  // instructions per piece
     auto issue_b = [&](int kt, int buf) {
         const int k = kt0 + kt;
         const int cc = k / 9, tp = k - cc * 9;
@@ -948,7 +950,7 @@ __global__ __launch_bounds__(256) void k_conv_halo(ConvArgs a, HaloArgs h) {
 
     if (a.splits > 1) {
         constexpr int NQ = MT * NT * 4;  // float4 groups of accumulators per lane
-        const auto rs = rsrc_of(a.ws + (size_t)bid * NQ * 256 * 4);
+        const auto rs = rsrc_of(a.ws + (size_t)bid * NQ * NT_ * 4);
         if (split > 0) {  // wait for the previous split's running sum, then add it
             __shared__ int late;
             if (t == 0) {  // bounded: a broken hand-off never hangs, it faults loudly
@@ -980,7 +982,7 @@ __global__ __launch_bounds__(256) void k_conv_halo(ConvArgs a, HaloArgs h) {
                 for (int j = 0; j < NT; ++j)
 #pragma unroll
                     for (int g = 0; g < 4; ++g) {
-                        const float4 v = ld_sc1_f32x4(rs, (unsigned)((((i * NT + j) * 4 + g) * 256 + t) * 16));
+                        const float4 v = ld_sc1_f32x4(rs, (unsigned)((((i * NT + j) * 4 + g) * NT_ + t) * 16));
                         acc[i][j][4 * g] += v.x;
                         acc[i][j][4 * g + 1] += v.y;
                         acc[i][j][4 * g + 2] += v.z;
@@ -994,7 +996,7 @@ __global__ __launch_bounds__(256) void k_conv_halo(ConvArgs a, HaloArgs h) {
                 for (int j = 0; j < NT; ++j)
 #pragma unroll
                     for (int g = 0; g < 4; ++g)
-                        st_sc1_f32x4(rs, (unsigned)((((i * NT + j) * 4 + g) * 256 + t) * 16),
+                        st_sc1_f32x4(rs, (unsigned)((((i * NT + j) * 4 + g) * NT_ + t) * 16),
                                      make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2],
                                                  acc[i][j][4 * g + 3]));
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1006,7 +1008,8 @@ __global__ __launch_bounds__(256) void k_conv_halo(ConvArgs a, HaloArgs h) {
         if (t == 0) __hip_atomic_store(a.flags + bid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 
-    store_tile<MT, NT, BM, BN>(a, cl, m0, n0, wm, wn, fr, fh, M, acc);
+    // (BM = 256: two 128-row halves of wave rows 0-1 and 2-3)
+    store_tile<MT, NT, 128, BN>(a, cl, m0 + (wm >> 1) * 128, n0, wm & 1, wn, fr, fh, M, acc);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1658,7 +1661,7 @@ static int launch_halo_v(ConvArgs& a, int hb, hipStream_t st) {
         }
         attr = lds;
     }
-    k_conv_halo<BM, BN, DIAG, NB><<<a.tiles_total * a.splits, 256, lds, st>>>(a, h);
+    k_conv_halo<BM, BN, DIAG, NB><<<a.tiles_total * a.splits, BM == 256 ? 512 : 256, lds, st>>>(a, h);
     return check_launch("k_conv_halo");
 }
 
@@ -1784,16 +1787,26 @@ struct Halo256Plan {
     size_t ws = 0;     // split-K workspace bytes (turnstile words + 256x128 fp32 slabs)
 };
 
+static int halo256_env(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+// GM_HALO256_MINTILES: shapes with fewer 256x128 tiles keep the 128-pixel form;
+// GM_HALO256_SPLIT=0: never split K
+static const int g_h256_mintiles = halo256_env("GM_HALO256_MINTILES", 192);
+static const int g_h256_split = halo256_env("GM_HALO256_SPLIT", 1);
+
 static Halo256Plan halo256_plan(const ConvArgs& a) {
     Halo256Plan p;
     if (g_conv_halo != 2 || a.Nout % 128) return p;
     const int hb = halo_bytes(a, 256);
     if (hb <= 0 || 2 * hb + 3 * 128 * 128 > 160 * 1024) return p;
     const int M = a.N * a.cls[0].P * a.cls[0].Q;
-    p.hb = hb;
     p.tiles = (M + 255) / 256 * (a.Nout / 128);
+    if (p.tiles < g_h256_mintiles) return p;
+    p.hb = hb;
     const int nk = 9 * (a.C >> 6);
-    int S = p.tiles >= 192 ? 1 : 256 / p.tiles;
+    int S = (p.tiles >= 192 || !g_h256_split) ? 1 : 256 / p.tiles;
     S = S > 4 ? 4 : S;
     while (S > 1 && nk / S < 16) --S;
     if (p.tiles > kMaxSplitTiles) S = 1;
