@@ -180,6 +180,8 @@ def main():
         dist.init_process_group(os.environ.get("GM_BENCH_DIST_BACKEND", "nccl"))
         rank, world = dist.get_rank(), dist.get_world_size()
         local = 0 if os.environ.get("GM_BENCH_SAME_DEVICE") == "1" else int(os.environ.get("LOCAL_RANK", "0"))
+        if os.environ.get("GM_BENCH_SAME_DEVICE") == "1":  # split-K waiters sized for `world` sharers
+            os.environ.setdefault("GM_CONV_DEVICE_SHARE", str(world))
     else:
         rank, world, local = 0, 1, 0
     torch.cuda.set_device(local)
