@@ -127,31 +127,48 @@ __global__ __launch_bounds__(256) void k_group_sumsq(const gm_tensor* __restrict
     }
 }
 
-__global__ __launch_bounds__(256) void k_group_finalize(const double* __restrict__ rows, int nrows,
-                                                        int ngroups, double* __restrict__ out) {
-    // each thread accumulates whole rows (all 2*ngroups columns) in registers, then one
-    // wave-shuffle + LDS pass per column; fixed assignment => deterministic
-    __shared__ double s[4][2 * kMaxGroups];
+// 1024 threads, each owning rows tid, tid + 1024, ... of ONE 16-column chunk per pass,
+// all of its loads in flight (the former 256-thread form walked ~6 rows per thread one
+// round trip at a time: 22 us on the serial end-of-step path); then a wave shuffle and
+// a fixed-order LDS combine per column => deterministic
+constexpr int kFinT = 1024;
+__global__ __launch_bounds__(kFinT) void k_group_finalize(const double* __restrict__ rows, int nrows,
+                                                          int ngroups, double* __restrict__ out) {
+    __shared__ double s[kFinT / 64][16];
     const int w = 2 * ngroups;
-    double acc[2 * kMaxGroups];
-#pragma unroll
-    for (int j = 0; j < 2 * kMaxGroups; ++j) acc[j] = 0.0;
-    for (int r = threadIdx.x; r < nrows; r += 256) {
-#pragma unroll
-        for (int j = 0; j < 2 * kMaxGroups; ++j)
-            if (j < w) acc[j] += rows[(size_t)r * w + j];
-    }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int c0 = 0; c0 < w; c0 += 16) {
+        double acc[16];
 #pragma unroll
-    for (int j = 0; j < 2 * kMaxGroups; ++j) {
-        if (j >= w) break;
-        const double v = wave_sum_d(acc[j]);
-        if (lane == 0) s[wave][j] = v;
-    }
-    __syncthreads();
-    if ((int)threadIdx.x < w) {
-        const int j = threadIdx.x;
-        out[j] = ((s[0][j] + s[1][j]) + s[2][j]) + s[3][j];
+        for (int j = 0; j < 16; ++j) acc[j] = 0.0;
+        int r = threadIdx.x;
+        for (; r + kFinT < nrows; r += 2 * kFinT) {  // two rows per round trip
+            double a0[16], a1[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                a0[j] = c0 + j < w ? rows[(size_t)r * w + c0 + j] : 0.0;
+                a1[j] = c0 + j < w ? rows[(size_t)(r + kFinT) * w + c0 + j] : 0.0;
+            }
+#pragma unroll
+            for (int j = 0; j < 16; ++j) acc[j] += a0[j] + a1[j];
+        }
+        if (r < nrows) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                if (c0 + j < w) acc[j] += rows[(size_t)r * w + c0 + j];
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const double v = wave_sum_d(acc[j]);
+            if (lane == 0) s[wave][j] = v;
+        }
+        __syncthreads();
+        if ((int)threadIdx.x < 16 && c0 + (int)threadIdx.x < w) {
+            double t = 0.0;
+            for (int q = 0; q < kFinT / 64; ++q) t += s[q][threadIdx.x];
+            out[c0 + threadIdx.x] = t;
+        }
+        __syncthreads();
     }
 }
 
@@ -189,6 +206,6 @@ extern "C" int gm_group_sumsq(const gm_tensor* table, int nt, long long total, i
     }
     int rc = check_launch("k_group_sumsq");
     if (rc) return rc;
-    k_group_finalize<<<1, 256, 0, st>>>(rows, (int)nb, ngroups, out);
+    k_group_finalize<<<1, kFinT, 0, st>>>(rows, (int)nb, ngroups, out);
     return check_launch("k_group_finalize");
 }
