@@ -322,10 +322,14 @@ class BalancedStep:
                 "curation_step": g.curation_step, "n_curated": int(st.n_curated)}
 
     # ---------------- the step ----------------
-    def forward(self, x):
+    def forward(self, x, mean=True):
         fl = self.flags
-        with torch.autocast("cuda", dtype=self.compute_dtype, enabled=self.compute_dtype != torch.float32):
-            return self.model(x, curation_mode=fl.curation_mode, caring_modality=fl.caring_modality)
+        self.model._no_mean = not mean
+        try:
+            with torch.autocast("cuda", dtype=self.compute_dtype, enabled=self.compute_dtype != torch.float32):
+                return self.model(x, curation_mode=fl.curation_mode, caring_modality=fl.caring_modality)
+        finally:
+            self.model._no_mean = False
 
     def _fwd_bwd(self, x, y):
         if not self.sink.lazy_zero:
@@ -338,11 +342,15 @@ class BalancedStep:
             if wp is not None:
                 wp.run()  # bf16 copies of every conv weight, one launch
                 wp.activate()
-            _, outs, _, _ = self.forward(x)
+            _, outs, _, _ = self.forward(x, mean=False)
             if wp is not None:
                 wp.deactivate()
             loss = blend_loss([o.float() for o in outs], y)
-            loss.backward()
+            # the backward seed from a persistent ones tensor (no fill launch per step)
+            if getattr(self, "_seed", None) is None or self._seed.shape != loss.shape \
+                    or self._seed.device != loss.device:
+                self._seed = torch.ones_like(loss)
+            loss.backward(self._seed)
             if self.device.type == "cuda":
                 # backward nodes of the side-stream trunks ran on their streams (some of
                 # them write gradients in place, outside autograd's leaf-stream sync)

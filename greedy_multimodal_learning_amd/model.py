@@ -103,7 +103,9 @@ class MMTM_MVCNN(nn.Module):
             x0 = self._head(self.net_view_0, f0)
             if vs is not None:
                 vs.join([x1])
-        return (x0 + x1) / 2, [x0, x1], scales, squeezed
+        # (the engine's step reads only the branch logits: no averaging launches there)
+        mean = None if getattr(self, "_no_mean", False) else (x0 + x1) / 2
+        return mean, [x0, x1], scales, squeezed
 
 
 @configurable
@@ -170,4 +172,5 @@ class MMTM_MVCNN_N(nn.Module):
                 outs[i] = run(i, MMTM_MVCNN._head, nets[i], fs[i])
             if vs is not None:
                 vs.join(outs[1:])
-        return sum(outs) / len(outs), outs, scales, squeezed
+        mean = None if getattr(self, "_no_mean", False) else sum(outs) / len(outs)
+        return mean, outs, scales, squeezed
