@@ -172,6 +172,7 @@ EXPORTS.update({
     "gm_mmtm_select_scale": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "gm_mmtm_mask_rows": (c_int, [c_void_p, ctypes.c_longlong, c_void_p, c_void_p]),
+    "gm_mmtm_mask_rows2": (c_int, [c_void_p, ctypes.c_longlong, c_void_p, ctypes.c_longlong, c_void_p, c_void_p]),
     "gm_stem_pack_bf16": (c_int, [c_void_p, c_void_p]),
     "gm_xent_fwd": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "gm_xent_bwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),

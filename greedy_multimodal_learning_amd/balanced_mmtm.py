@@ -197,10 +197,8 @@ class _MMTMFunction(torch.autograd.Function):
             ops.spatial_reduce(probs, B, dt, lay, dev)
         if gmask is not None:  # on-device gate: zero the substituted modality's da
             lib = L.load()
-            L.check(lib.gm_mmtm_mask_rows(da_v.data_ptr(), B * Cv, gmask.data_ptr(), L.stream_of(dev)),
-                    "gm_mmtm_mask_rows")
-            L.check(lib.gm_mmtm_mask_rows(da_s.data_ptr(), B * Cs, gmask.data_ptr() + 4, L.stream_of(dev)),
-                    "gm_mmtm_mask_rows")
+            L.check(lib.gm_mmtm_mask_rows2(da_v.data_ptr(), B * Cv, da_s.data_ptr(), B * Cs, gmask.data_ptr(),
+                                           L.stream_of(dev)), "gm_mmtm_mask_rows2")
         # ---- excite FC grads + dz
         g = {}
         probs = []

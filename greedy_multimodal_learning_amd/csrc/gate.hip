@@ -86,6 +86,17 @@ __global__ __launch_bounds__(256) void k_mask_rows(float* __restrict__ a, long l
     for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) a[i] *= k;
 }
 
+// both modalities' rows in one launch: a[i] *= m[0], b[i] *= m[1]
+__global__ __launch_bounds__(256) void k_mask_rows2(float* __restrict__ a, long long na, float* __restrict__ b,
+                                                    long long nb, const float* __restrict__ m) {
+    const float ka = m[0], kb = m[1];
+    const long long st = (long long)gridDim.x * 256;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < na + nb; i += st) {
+        if (i < na) a[i] *= ka;
+        else b[i - na] *= kb;
+    }
+}
+
 }  // namespace
 }  // namespace gm
 
@@ -116,4 +127,12 @@ extern "C" int gm_mmtm_mask_rows(float* a, long long n, const float* mask, void*
     g = g > 1024 ? 1024 : g;
     k_mask_rows<<<g, 256, 0, as_stream(stream)>>>(a, n, mask);
     return check_launch("k_mask_rows");
+}
+
+extern "C" int gm_mmtm_mask_rows2(float* a, long long na, float* b, long long nb, const float* mask, void* stream) {
+    GM_REQUIRE(a && b && mask && na > 0 && nb > 0, "gm_mmtm_mask_rows2: bad arguments");
+    long long g = (na + nb + 255) / 256;
+    g = g > 1024 ? 1024 : g;
+    k_mask_rows2<<<(int)g, 256, 0, as_stream(stream)>>>(a, na, b, nb, mask);
+    return check_launch("k_mask_rows2");
 }

@@ -203,6 +203,8 @@ int gm_mmtm_select_scale(const float* e_v, int ld_v, const float* e_s, int ld_s,
                          const float* ra_s, int B, int Cv, int Cs, const gm_gate_state* state,
                          float* s_v, float* s_s, float* mask, void* stream);
 int gm_mmtm_mask_rows(float* a, long long n, const float* mask, void* stream);
+/* Both modalities in one launch: a[0..na) *= mask[0], b[0..nb) *= mask[1]. */
+int gm_mmtm_mask_rows2(float* a, long long na, float* b, long long nb, const float* mask, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Pixel-pair packing of the RGB stem (one launch, input and weight):
