@@ -217,6 +217,12 @@ class BalancedStep:
             model.to(memory_format=torch.channels_last)
         named = list(model.named_parameters())
         self.flat = FlatParams(model, channels_last)
+        self._seed = torch.ones((), device=self.device, dtype=torch.float32)  # backward seed
+        if self.device.type == "cuda":  # the fused head backward's zero rows, outside any capture
+            from .head import zero_row
+            for name, mod in model.named_modules():
+                if name.endswith("fc") and isinstance(mod, torch.nn.Linear):
+                    zero_row(self.device, mod.in_features)
         self.flat_grad = self.flat.grad
         if self.device.type == "cuda" and streams_enabled():
             for i in range(int(getattr(model, "num_views", 2)) - 1):
@@ -346,9 +352,10 @@ class BalancedStep:
             if wp is not None:
                 wp.deactivate()
             loss = blend_loss([o.float() for o in outs], y)
-            # the backward seed from a persistent ones tensor (no fill launch per step)
+            # the backward seed from a persistent ones tensor made before any capture (no
+            # fill launch per step; blend_loss returns a 0-d fp32 loss)
             if getattr(self, "_seed", None) is None or self._seed.shape != loss.shape \
-                    or self._seed.device != loss.device:
+                    or self._seed.device != loss.device or self._seed.dtype != loss.dtype:
                 self._seed = torch.ones_like(loss)
             loss.backward(self._seed)
             if self.device.type == "cuda":

@@ -26,6 +26,20 @@ from .gradsink import sink_done, sink_target
 CL = torch.channels_last
 
 
+
+_ZERO = {}
+
+
+def zero_row(dev, C):
+    """A persistent [1, C] fp32 zero row (the head backward's zero scale operand): made once,
+    ideally before any graph capture (BalancedStep does), so no fill launch per step."""
+    key = (str(dev), C)
+    z = _ZERO.get(key)
+    if z is None:
+        z = torch.zeros(1, C, device=dev, dtype=torch.float32)
+        _ZERO[key] = z
+    return z
+
 def head_ok(fs, fcs):
     """The fused head applies to bf16 or fp32 channels_last CUDA maps of one shape with fp32 fc."""
     f0 = fs[0]
@@ -112,7 +126,7 @@ class _PooledLinearFn(torch.autograd.Function):
             ops.gemm(probs, dev)
         gf = [None] * nb
         if dp:
-            zero = torch.zeros(1, C, device=dev, dtype=torch.float32)
+            zero = zero_row(dev, C)
             sc = []
             for i, d in dp.items():
                 gf[i] = torch.empty_like(fs[i], memory_format=CL if ctx.lay == L.GM_NHWC else torch.contiguous_format)
