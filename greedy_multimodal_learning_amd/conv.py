@@ -334,19 +334,24 @@ class WeightPrep:
         _prepped.clear()
 
 
-def conv_dgrad_t(dy, wt, H, W, stride, pad, addend=None):
+def conv_dgrad_t(dy, wt, H, W, stride, pad, addend=None, inplace=False):
     """dgrad from an already transposed bf16 weight wt [C,K,R,S] (channels_last);
-    addend (bf16 [N,C,H,W] channels_last): dx = dgrad + addend in the epilogue."""
+    addend (bf16 [N,C,H,W] channels_last): dx = dgrad + addend in the epilogue, written
+    over the addend itself when inplace (a strided dgrad then needs no pass that copies
+    the addend to the pixels its parity classes do not cover)."""
     lib = L.load()
     N, K, P, Q = dy.shape
     C, _, R, S = wt.shape
-    dx = torch.empty(N, C, H, W, device=dy.device, dtype=torch.bfloat16, memory_format=CL)
     d = _desc(N, H, W, C, K, R, S, stride, pad)
     ws, nb = _splitk(dy.device, d, True)
     if addend is not None:
         if (tuple(addend.shape) != (N, C, H, W) or addend.dtype != torch.bfloat16
                 or not addend.is_contiguous(memory_format=CL)):
             raise ValueError("conv dgrad addend must be a bf16 channels_last tensor shaped like dx")
+    if inplace and addend is not None:
+        dx = addend
+    else:
+        dx = torch.empty(N, C, H, W, device=dy.device, dtype=torch.bfloat16, memory_format=CL)
     L.check(lib.gm_conv2d_dgrad_add_bf16(ctypes.byref(d), dy.data_ptr(), wt.data_ptr(), dx.data_ptr(),
                                          L.ptr(addend), ws, nb, L.stream_of(dy.device)), "gm_conv2d_dgrad_add_bf16")
     return dx
@@ -380,7 +385,8 @@ class _ConvFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             if ctx.join is not None and wt.shape[0] == C0:
-                dx = ctx.join.contribute(lambda add: conv_dgrad_t(gy, wt, H, W, stride, pad, addend=add))
+                # the pending addend is this join's own tensor: summed in place
+                dx = ctx.join.contribute(lambda add: conv_dgrad_t(gy, wt, H, W, stride, pad, addend=add, inplace=True))
             else:
                 dx = conv_dgrad_t(gy, wt, H, W, stride, pad)
                 if dx.shape[1] != C0:

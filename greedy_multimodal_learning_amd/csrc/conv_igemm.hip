@@ -2142,12 +2142,14 @@ extern "C" int gm_conv2d_dgrad_add_bf16(const gm_conv_desc* d, const void* dy, c
     int rc = check_dgrad(d);
     if (rc) return rc;
     GM_REQUIRE(dy && wt && dx, "conv dgrad: null pointer");
-    GM_REQUIRE(addend != dx, "conv dgrad: addend must not alias dx");
+    // addend == dx (in place) is allowed: every epilogue loads an output element's addend
+    // and stores that element from the same thread, and pixels no parity class covers
+    // then simply keep the addend (no zero / copy pass)
     ConvArgs a;
     const bool full = dgrad_setup(d, dy, wt, dx, a);
     a.addend = (const uint16_t*)addend;
     hipStream_t s = as_stream(stream);
-    if (!full) {
+    if (!full && addend != dx) {
         const size_t n = (size_t)d->N * d->H * d->W * d->C;
         k_zero_bf16<<<(int)((n / 8 + 255) / 256 < 4096 ? (n / 8 + 255) / 256 : 4096), 256, 0, s>>>(
             (uint16_t*)dx, n, (const uint16_t*)addend);

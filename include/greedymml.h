@@ -307,7 +307,8 @@ int gm_conv2d_fwd_ex_bf16(const gm_conv_desc* d, const void* x, const void* w, v
 int gm_conv2d_dgrad_ex_bf16(const gm_conv_desc* d, const void* dy, const void* wt, void* dx, void* ws,
                             size_t ws_bytes, void* stream);
 /* dgrad fused with a gradient join: dx = conv_transpose(dy, w) + addend (bf16, dx's
- * layout, must not alias dx) - the other consumer's gradient of the same tensor, so
+ * layout; may BE dx: summed in place, pixels no parity class covers keep it) - the
+ * other consumer's gradient of the same tensor, so
  * the autograd add of the two is never materialised (ResNet blocks: the identity /
  * downsample branch and the first convolution both consume the block input). */
 int gm_conv2d_dgrad_add_bf16(const gm_conv_desc* d, const void* dy, const void* wt, void* dx,

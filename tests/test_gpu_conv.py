@@ -295,6 +295,11 @@ def test_conv_dgrad_fused_addend(dev, shape):
                                               False, [0, 0], 1, [True, False, False])[0]
     _close(dxa, dxr + add.float(), 1e-2)
     _close(dxa, dx.float() + add.float(), 1e-2)
+    # in place over the addend (the gradient join's pending tensor): bit-identical
+    buf = add.clone()
+    dxi = G.conv_dgrad_t(dy, wt, H, W, st, pad, addend=buf, inplace=True)
+    assert dxi.data_ptr() == buf.data_ptr()
+    assert torch.equal(dxi, dxa)
 
 
 @pytest.mark.parametrize("shape", [(64, 3, 224, 224), (3, 3, 37, 30), (2, 3, 64, 64), (5, 3, 250, 200)],
