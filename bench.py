@@ -32,6 +32,7 @@ WORKLOADS = {
 }
 HBM_PEAK_GBS = 8000.0
 MFMA_PEAK_TFS = 2500.0  # dense bf16 (MI355X_MICROARCH.md)
+MFMA_F32_PEAK_TFS = 157.3  # f32-input MFMA = the f32 vector rate (MI355X_MICROARCH.md)
 
 
 def parse():
@@ -52,6 +53,7 @@ def parse():
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture of the step")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_group_sumsq.json"))
     ap.add_argument("--conv-traffic-file", default=os.path.join(ROOT, "profiles", "r02_traffic_conv_family.json"))
+    ap.add_argument("--mmtm-traffic-file", default=os.path.join(ROOT, "profiles", "r03_traffic_mmtm.json"))
     ap.add_argument("--profile", action="store_true",
                     help="steps only (no roofline / cpu_baseline measurements): for rocprofv3 runs")
     return ap.parse_args()
@@ -95,18 +97,29 @@ def cpu_baseline(seconds, size):
                       f"{size}x{size}; {th} threads (the job's CPU share; {os.cpu_count()} CPUs visible)"}
 
 
-def time_trunk_convs(B, dev):
+def time_trunk_convs(B, dev, dtype="bf16"):
     """Roofline of the dominant kernel family, the trunk convolutions: forward, input-
     and weight-gradient launches of every trunk shape of one view at the step's batch
-    (tools/trunk_table.py; HIP events on the launch stream behind a device sleep)."""
+    (tools/trunk_table.py; HIP events on the launch stream behind a device sleep; the
+    launches rotate over more operand bytes than the 256 MiB Infinity Cache holds)."""
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import trunk_table
-    flops, secs, launches, _ = trunk_table.measure_family(B, dev)
+    flops, secs, launches, _ = trunk_table.measure_family(B, dev, dtype=dtype)
     return flops, secs, launches
 
 
-def conv_roofline(conv, traffic):
+def conv_roofline(conv, traffic, dtype="bf16"):
     """The `roofline` object of the dominant kernel family (the trunk convolutions)."""
+    if dtype == "fp32":
+        if conv is None:
+            return None
+        flops, secs, launches = conv
+        return {"kernel": "trunk convolutions, reference precision (k_conv_f32: exact-f32 MFMA "
+                          "v_mfma_f32_32x32x2_f32 implicit GEMM fwd / input grad / weight grad; every trunk "
+                          "shape of one view at the step's batch, tools/trunk_table.py)",
+                "bound": "mfma", "achieved": round(flops / secs / 1e12, 2), "peak": MFMA_F32_PEAK_TFS,
+                "unit": "TFLOP/s", "frac": round(flops / secs / 1e12 / MFMA_F32_PEAK_TFS, 4), "traffic": None,
+                "alg_flops_per_launch": round(flops / launches), "avg_launch_us": round(secs / launches * 1e6, 2)}
     if conv is None:
         return {"kernel": "trunk convolutions", "bound": "mfma", "achieved": None, "peak": MFMA_PEAK_TFS,
                 "unit": "TFLOP/s", "frac": None, "traffic": None,
@@ -122,34 +135,13 @@ def conv_roofline(conv, traffic):
 
 
 def time_mmtm_reduce(dev, B=256, reps=20):
-    """HBM roofline of the MMTM squeeze (global-average-pool of both views' activations,
-    k_colreduce_nhwc via gm_mmtm_spatial_reduce) at the north-star batch 256, on the
-    largest site (s2: 128 ch x 28x28 per view), the exact launch MMTM_mitigate.forward
-    issues (balanced_mmtm.py).  Algorithmic bytes = both views' bf16 activations read
-    once; time = HIP events on the launch stream behind a device sleep."""
-    from greedy_multimodal_learning_amd import ops
-    from greedy_multimodal_learning_amd import _lib as L
-    CL = torch.channels_last
-    C, H = 128, 28
-    xv = torch.randn(B, C, H, H, device=dev).bfloat16().contiguous(memory_format=CL)
-    xs = torch.randn(B, C, H, H, device=dev).bfloat16().contiguous(memory_format=CL)
-    sq = torch.empty(B, 2 * C, device=dev)
-    probs = [dict(x=xv, C=C, HW=H * H, out=sq, ld_out=2 * C, scale=1.0 / (H * H)),
-             dict(x=xs, C=C, HW=H * H, out=sq, out_off=C, ld_out=2 * C, scale=1.0 / (H * H))]
-
-    def op():
-        ops.spatial_reduce(probs, B, L.GM_BF16, L.GM_NHWC, dev)
-    op()
-    torch.cuda.synchronize()
-    torch.cuda._sleep(20_000_000)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        op()
-    e1.record()
-    torch.cuda.synchronize()
-    secs = e0.elapsed_time(e1) / reps / 1e3
-    nbytes = 2 * B * C * H * H * 2
+    """HBM roofline of the MMTM squeeze (k_colreduce_nhwc via gm_mmtm_spatial_reduce) at the
+    north-star batch 256, site s2, the launch MMTM_mitigate.forward issues; launches rotate
+    over 4 distinct activation pairs (411 MB, more than the 256 MiB Infinity Cache) so each
+    reads HBM (tools/mmtm_probe.py).  Returns (algorithmic bytes, seconds) per launch."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import mmtm_probe
+    nbytes, secs, _ = mmtm_probe.measure(dev, B, pairs=4, reps=reps)
     return nbytes, secs
 
 
@@ -179,9 +171,8 @@ def main():
         # N-rank code path on a one-GPU box
         dist.init_process_group(os.environ.get("GM_BENCH_DIST_BACKEND", "nccl"))
         rank, world = dist.get_rank(), dist.get_world_size()
+        # (ranks sharing one GPU are found by the engine: gm_set_residency's `sharers`)
         local = 0 if os.environ.get("GM_BENCH_SAME_DEVICE") == "1" else int(os.environ.get("LOCAL_RANK", "0"))
-        if os.environ.get("GM_BENCH_SAME_DEVICE") == "1":  # split-K waiters sized for `world` sharers
-            os.environ.setdefault("GM_CONV_DEVICE_SHARE", str(world))
     else:
         rank, world, local = 0, 1, 0
     torch.cuda.set_device(local)
@@ -262,14 +253,17 @@ def main():
             dist.destroy_process_group()
         return
     kern_avg_s = time_group_sumsq(step, 10)
-    conv = time_trunk_convs(B, dev) if WL["trunk"] == "resnet18" else None
+    conv = time_trunk_convs(B, dev, a.dtype) if WL["trunk"] == "resnet18" else None
     mmtm_bytes, mmtm_s = time_mmtm_reduce(dev)
     if rank == 0:
         views = V
         total_imgs = world * B * views * a.steps
         bytes_alg = 12 * step.flat.total  # read param + grad, write param (fp32)
         achieved = bytes_alg / kern_avg_s / 1e9
-        traffic = conv_traffic = None
+        traffic = conv_traffic = mmtm_traffic = None
+        if os.path.exists(a.mmtm_traffic_file):
+            with open(a.mmtm_traffic_file) as f:
+                mmtm_traffic = json.load(f).get("hbm_bytes_per_launch")
         if os.path.exists(a.conv_traffic_file):
             with open(a.conv_traffic_file) as f:
                 conv_traffic = json.load(f).get("hbm_bytes_per_launch")
@@ -293,18 +287,19 @@ def main():
                        "parallelism": f"dp{world}", "samples_per_s": round(world * B * a.steps / elapsed, 2),
                        "hipgraph": bool(step.graphs), "device_gate": bool(step.device_gate),
                        "curation_steps_timed": curation_steps, "final_loss": round(loss, 4)},
-            "roofline": conv_roofline(conv, conv_traffic),
+            "roofline": conv_roofline(conv, conv_traffic if a.dtype == "bf16" else None, a.dtype),
             "roofline_hbm": {"kernel": "k_group_sumsq<SGD> (fused per-branch norms + SGD, gm_group_sumsq)",
                              "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                              "traffic": traffic, "alg_bytes_per_launch": bytes_alg,
                              "avg_launch_us": round(kern_avg_s * 1e6, 2)},
             "roofline_mmtm": {"kernel": "k_colreduce_nhwc (MMTM squeeze: GAP of both views, site s2, "
-                                        "north-star batch 256, gm_mmtm_spatial_reduce)",
+                                        "north-star batch 256, gm_mmtm_spatial_reduce; launches rotate over 4 "
+                                        "distinct pairs = 411 MB > 256 MiB Infinity Cache)",
                               "bound": "hbm", "batch": 256,
                               "achieved": round(mmtm_bytes / mmtm_s / 1e9, 1), "peak": HBM_PEAK_GBS,
                               "unit": "GB/s", "frac": round(mmtm_bytes / mmtm_s / 1e9 / HBM_PEAK_GBS, 4),
-                              "traffic": None, "alg_bytes_per_launch": mmtm_bytes,
+                              "traffic": mmtm_traffic, "alg_bytes_per_launch": mmtm_bytes,
                               "avg_launch_us": round(mmtm_s * 1e6, 2)},
         }
         if not a.no_cpu_baseline:

@@ -14,7 +14,7 @@ LIB_PATH = os.path.join(_PKG, "libgreedymml_hip.so")
 
 GM_F32, GM_BF16 = 0, 1
 GM_NCHW, GM_NHWC = 0, 1
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 c_int, c_float, c_void_p, c_size_t = ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
 c_float_p = ctypes.c_void_p  # device pointers are opaque
@@ -239,7 +239,25 @@ EXPORTS.update({
     "gm_set_spin_limit": (c_int, [ctypes.c_uint]),
     "gm_bn_set_concurrency": (c_int, [c_int]),
     "gm_bn_set_fused_mode": (c_int, [c_int]),
+    "gm_set_residency": (c_int, [c_int, c_int, c_int]),
+    "gm_get_residency": (c_int, [ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
+    "gm_test_hold_cus": (c_int, [c_int, c_int, c_int, ctypes.c_uint, c_void_p]),
 })
+
+
+def set_residency(streams=None, sharers=None, reserved_cus=None):
+    """Update the library's device residency plan (gm_set_residency); None keeps a field."""
+    cur = get_residency()
+    new = (cur[0] if streams is None else int(streams), cur[1] if sharers is None else int(sharers),
+           cur[2] if reserved_cus is None else int(reserved_cus))
+    check(load().gm_set_residency(*new), "gm_set_residency")
+    return new
+
+
+def get_residency():
+    a, b, c = c_int(0), c_int(0), c_int(0)
+    check(load().gm_get_residency(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), "gm_get_residency")
+    return a.value, b.value, c.value
 
 
 _fault_reset_hooks = []

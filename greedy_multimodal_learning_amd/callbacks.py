@@ -323,3 +323,55 @@ class Bias_Mitigation_Random(Callback):
     def on_epoch_begin(self, epoch, logs):
         if epoch >= self.starting_epoch:
             self.unlock = True
+
+
+@configurable
+class CompletedStopping(Callback):
+    """Reference src/callbacks.py:305-331: stop training once the monitored epoch metric
+    (training accuracy by default) has been exactly 100 in `patience` epochs.  The count
+    is cumulative (never reset when the metric drops), as in the reference."""
+
+    def __init__(self, *, monitor='acc', patience=5, verbose=True):
+        super().__init__()
+        self.monitor = monitor
+        self.patience = patience
+        self.verbose = verbose
+        self.stopped_epoch = 0
+
+    def on_train_begin(self, logs):
+        self.stopped_epoch = 0
+        self.counter = 0
+
+    def on_epoch_end(self, epoch, logs):
+        if logs[self.monitor] == 100:
+            self.counter += 1
+        if self.counter >= self.patience:
+            self.stopped_epoch = epoch
+            self.model_pytoune.stop_training = True
+
+    def on_train_end(self, logs):
+        if self.stopped_epoch > 0 and self.verbose:
+            print('Epoch %05d: completed stopping' % (self.stopped_epoch + 1))
+
+
+@configurable
+class ReduceLROnPlateau_PyTorch(Callback):
+    """Reference src/callbacks.py:334-348: torch's ReduceLROnPlateau on an epoch metric
+    (`loss` in training_guided.gin), mode 'min', threshold 1e-3 relative, min_lr 1e-6.
+    It drives the optimizer the loop hands over (set_optimizer); the fused engine reads
+    that optimizer's learning rate before every step (a new rate is a new captured graph).
+    The reference's verbose=True is dropped: a TypeError on torch >= 2.7."""
+
+    def __init__(self, metric, factor=0.3, patience=10):
+        super().__init__()
+        self.metric = metric
+        self.factor = factor
+        self.patience = patience
+
+    def on_train_begin(self, logs):
+        self.scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(
+            self.optimizer, mode='min', factor=self.factor, patience=self.patience, threshold=0.001,
+            threshold_mode='rel', cooldown=0, min_lr=1e-6, eps=1e-08)
+
+    def on_epoch_end(self, epoch, logs):
+        self.scheduler.step(logs[self.metric])

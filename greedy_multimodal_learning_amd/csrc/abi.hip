@@ -1,4 +1,5 @@
 // ABI housekeeping: version and thread-local error text.
+#include <cstdlib>
 #include <cstring>
 
 #include "gm_common.h"
@@ -27,6 +28,24 @@ static unsigned g_spin_limit = 0;  // 0: default
 
 unsigned spin_limit() { return g_spin_limit ? g_spin_limit : (1u << 24); }
 
+static Residency g_res = {2, 1, 0};  // two trunk streams, one process, nothing reserved
+
+const Residency& residency() { return g_res; }
+
+int usable_cus(int cus) {
+    const int u = cus - g_res.reserved_cus;
+    return u > cus / 4 ? u : cus / 4;
+}
+
+// one workgroup per CU when lds_bytes is the whole LDS: spins on the 100 MHz real-time
+// counter, sleeping between polls, until `usec` have passed
+__global__ void k_hold_cus(unsigned long long ticks) {
+    extern __shared__ int lds[];
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+    if (threadIdx.x == 0) lds[0] = 0;
+}
+
 }  // namespace gm
 
 extern "C" int gm_abi_version(void) { return GM_ABI_VERSION; }
@@ -47,3 +66,32 @@ extern "C" int gm_set_spin_limit(unsigned polls) {
     return GM_OK;
 }
 extern "C" const char* gm_last_error(void) { return gm::g_err; }
+
+extern "C" int gm_set_residency(int streams, int sharers, int reserved_cus) {
+    GM_REQUIRE(streams >= 1 && streams <= 64, "gm_set_residency: streams must be in [1, 64] (got %d)", streams);
+    GM_REQUIRE(sharers >= 1 && sharers <= 64, "gm_set_residency: sharers must be in [1, 64] (got %d)", sharers);
+    GM_REQUIRE(reserved_cus >= 0 && reserved_cus <= 4096, "gm_set_residency: reserved_cus out of range (%d)",
+               reserved_cus);
+    gm::g_res = gm::Residency{streams, sharers, reserved_cus};
+    return GM_OK;
+}
+
+extern "C" int gm_get_residency(int* streams, int* sharers, int* reserved_cus) {
+    GM_REQUIRE(streams && sharers && reserved_cus, "gm_get_residency: null output");
+    *streams = gm::g_res.streams;
+    *sharers = gm::g_res.sharers;
+    *reserved_cus = gm::g_res.reserved_cus;
+    return GM_OK;
+}
+
+extern "C" int gm_test_hold_cus(int blocks, int threads, int lds_bytes, unsigned usec, void* stream) {
+    GM_REQUIRE(blocks >= 1 && blocks <= 4096 && threads >= 64 && threads <= 1024 && lds_bytes >= 4 &&
+                   lds_bytes <= 160 * 1024 && usec <= 10000000u,
+               "gm_test_hold_cus: bad arguments");
+    if (lds_bytes > 64 * 1024)
+        hipFuncSetAttribute(reinterpret_cast<const void*>(gm::k_hold_cus), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            lds_bytes);
+    hipLaunchKernelGGL(gm::k_hold_cus, dim3(blocks), dim3(threads), lds_bytes, gm::as_stream(stream),
+                       (unsigned long long)usec * 100ull);
+    return gm::check_launch("gm_test_hold_cus");
+}

@@ -894,8 +894,12 @@ int device_cus() {
 
 inline int fused_plan(long long M, int C, Plan& pl, bool bwd = false) {
     if (g_fused_env == 0) return 0;
-    const int cus = device_cus();
-    const int conc = g_concurrency;
+    // co-residency under the device residency plan (gm_set_residency): CUs held by
+    // never-yielding kernels (RCCL) are not counted, and every process sharing the GPU
+    // may run its own launches at once
+    const Residency& rs = residency();
+    const int cus = usable_cus(device_cus());
+    const int conc = (g_concurrency > rs.streams ? g_concurrency : rs.streams) * rs.sharers;
     const Plan base = make_plan(M, C);
     const Occ& oc = occupancy();
     const int nrs[3] = {4, 8, 16};

@@ -1569,15 +1569,6 @@ static bool lean_ok(const ConvArgs& a) {
     return grid;
 }
 
-static int device_share() {
-    static int n = [] {
-        const char* e = getenv("GM_CONV_DEVICE_SHARE");  // processes sharing this GPU (rehearsals)
-        const int v = e ? atoi(e) : 1;
-        return v >= 1 ? v : 1;
-    }();
-    return n;
-}
-
 static int conv_cus() {
     static int n = [] {
         int dev = 0, c = 0;
@@ -1613,12 +1604,14 @@ static TilePick pick_tile(const ConvArgs& a) {
         while (S > 1 && nkmin / S < splitk_mink()) --S;  // long enough splits to amortize the hand-off
         // deadlock freedom of the turnstile: a waiting split holds its CU slot while the
         // split it waits on may still be queued behind OTHER launches' waiting splits (the
-        // other trunk's stream; another process when ranks share the device).  Keep the
-        // waiting workgroups of one launch (tiles x (S-1)) within the device's two slots
-        // per CU divided by the launches that can wait at once - two trunk streams per
-        // process, times GM_CONV_DEVICE_SHARE processes (S = 4 at layer 4 timed out with
-        // two ranks sharing one GPU)
-        while (S > 1 && (long)t128 * (S - 1) > (long)conv_cus() * 2 / (2 * device_share())) --S;
+        // other trunk's stream; another process when ranks share the device) or behind
+        // kernels that never yield (RCCL collectives overlapping backward).  Keep the
+        // waiting workgroups of one launch (tiles x (S-1)) within two slots per usable CU
+        // (CUs minus the reserved ones) divided by the launches that can wait at once -
+        // the residency plan's streams x sharers (gm_set_residency; S = 4 at layer 4 timed
+        // out with two ranks sharing one GPU before the plan counted them)
+        const Residency& rs = residency();
+        while (S > 1 && (long)t128 * (S - 1) > (long)usable_cus(conv_cus()) * 2 / (rs.streams * rs.sharers)) --S;
         if (S >= 2) return {T128x128, S, t128};
     }
     if (M / 128 * ((a.Nout + 63) / 64) >= wgs * 3 / 4) return {T128x64, 1, 0};
@@ -1838,7 +1831,8 @@ static Halo256Plan halo256_plan(const ConvArgs& a) {
     S = S > 4 ? 4 : S;
     while (S > 1 && nk / S < 16) --S;
     // waiters within the device's slots (one workgroup per CU here) per concurrent launch: see pick_tile
-    while (S > 1 && (long)p.tiles * (S - 1) > (long)conv_cus() / (2 * device_share())) --S;
+    const Residency& rs = residency();
+    while (S > 1 && (long)p.tiles * (S - 1) > (long)usable_cus(conv_cus()) / (rs.streams * rs.sharers)) --S;
     if (p.tiles > kMaxSplitTiles) S = 1;
     p.splits = S;
     if (S > 1) p.ws = splitk_flag_bytes(p.tiles) + (size_t)p.tiles * 32 * 256 * 16;

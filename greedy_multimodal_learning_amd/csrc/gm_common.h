@@ -107,6 +107,13 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 // device fault word and poisons its result (NaN) instead of applying stale data;
 // gm_device_faults() (abi.hip) reports the OR of all fault words.
 unsigned spin_limit();                         // host: poll budget passed to the kernels
+// the device residency plan (gm_set_residency): who else can hold CU slots while a
+// launch whose workgroups wait on each other runs
+struct Residency {
+    int streams, sharers, reserved_cus;
+};
+const Residency& residency();
+int usable_cus(int cus);                       // cus - reserved (at least cus / 4)
 unsigned bn_faults_read(bool clear);           // batchnorm.hip
 unsigned conv_faults_read(bool clear);         // conv_igemm.hip
 

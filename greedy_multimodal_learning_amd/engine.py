@@ -31,8 +31,6 @@ re-organised for the hardware:
 """
 import os
 
-import time
-
 import torch
 import torch.distributed as dist
 
@@ -52,6 +50,7 @@ class _Flags:
     def __init__(self):
         self.curation_mode = False
         self.caring_modality = None
+        self.stop_training = False  # set by CompletedStopping / a NaN loss (src/framework.py:321-322)
 
 
 class FlatParams:
@@ -248,6 +247,7 @@ class BalancedStep:
                              on_ready=self.buckets._on_sink if self.buckets is not None else None,
                              lazy_zero=os.environ.get("GM_LAZY_ZERO", "1") != "0")
         self.last_loss = None
+        self.last_outs = None  # the last step's branch logits (fp32), e.g. for training accuracy
         self.step_count = 0
         self.timer = None  # optional (start_event, end_event) list collector for the fused pass
         self.wprep = None
@@ -265,10 +265,22 @@ class BalancedStep:
         # cannot be captured: there (and with GM_DP_GRAPH_COLLECTIVES=0) the per-rank
         # compute is the graph and the all-reduce + norms/SGD run eagerly behind it.
         self.graph_collectives = False
+        self._capture_pg = None
         if self.buckets is not None and self.graphs:
             backend = dist.get_backend(process_group)
             self.graph_collectives = (backend == "nccl"
                                       and os.environ.get("GM_DP_GRAPH_COLLECTIVES", "1") != "0")
+            if self.graph_collectives:
+                # the captured all-reduces run on a process group of their own that never
+                # issues an eager collective: its communicator is initialised here (device_id:
+                # eager connect, no work item), so the group's watchdog never holds an event
+                # recorded on the stream being captured (HIP refuses that query and the
+                # watchdog aborts the process).  The eager steps keep using `process_group`.
+                # new_group is collective over the default group: every rank builds the engine.
+                self._capture_pg = dist.new_group(ranks=dist.get_process_group_ranks(process_group),
+                                                  backend="nccl", device_id=self.device)
+        if self.device.type == "cuda":
+            self._plan_residency(model)
         self._graphs = {}
         self._gpool = None
         self._static = None
@@ -298,6 +310,28 @@ class BalancedStep:
             self.gate_state = torch.frombuffer(bytearray(bytes(st)), dtype=torch.uint8).to(self.device)
             for m in self._mmtms:
                 m.device_gate = self.gate_state
+
+    def _plan_residency(self, model):
+        """The library's device residency plan (gm_set_residency): launches whose
+        workgroups wait on each other (single-launch BatchNorm, split-K turnstile) size
+        their grids for the trunk streams that run at once, the ranks sharing this GPU
+        (found by exchanging (host, device) over the step's group) and, under RCCL data
+        parallelism, the CUs the all-reduce kernels hold while they overlap backward
+        (GM_RCCL_RESERVED_CUS, default 64: RCCL's channel blocks, one CU each at most)."""
+        from . import _lib as L
+        views = int(getattr(model, "num_views", 2))
+        streams = views if streams_enabled() else 1
+        sharers, reserved = 1, 0
+        if self.pg is not None and self.world > 1:
+            import socket
+            me = (socket.gethostname(), torch.cuda.get_device_properties(self.device).uuid
+                  if hasattr(torch.cuda.get_device_properties(self.device), "uuid") else self.device.index)
+            who = [None] * self.world
+            dist.all_gather_object(who, (me[0], str(me[1])), group=self.pg)
+            sharers = sum(1 for w in who if w == (me[0], str(me[1])))
+        if self.buckets is not None and dist.get_backend(self.pg) == "nccl":
+            reserved = int(os.environ.get("GM_RCCL_RESERVED_CUS", "64"))
+        self.residency = L.set_residency(streams=max(1, streams), sharers=max(1, sharers), reserved_cus=reserved)
 
     # ---------------- on-device gate ----------------
     def _gate_step(self, sums):
@@ -351,7 +385,8 @@ class BalancedStep:
             _, outs, _, _ = self.forward(x, mean=False)
             if wp is not None:
                 wp.deactivate()
-            loss = blend_loss([o.float() for o in outs], y)
+            outs = [o.float() for o in outs]
+            loss = blend_loss(outs, y)
             # the backward seed from a persistent ones tensor made before any capture (no
             # fill launch per step; blend_loss returns a 0-d fp32 loss)
             if getattr(self, "_seed", None) is None or self._seed.shape != loss.shape \
@@ -370,7 +405,7 @@ class BalancedStep:
                 wp.deactivate()
         if self.buckets is not None and not self.buckets.deferred:
             self.buckets.finish()
-        return loss
+        return loss, [o.detach() for o in outs]
 
     def _graph_key(self):
         if self.device_gate:
@@ -402,11 +437,7 @@ class BalancedStep:
         dp = self.buckets is not None
         inline = dp and self.graph_collectives  # collectives captured in the graph
         if inline:
-            # the process group's watchdog (polling every 100 ms) must have dropped the
-            # completed eager works first: HIP refuses a query of an event recorded on the
-            # RCCL stream while that stream is being captured, and the watchdog thread
-            # aborts the process on that error
-            time.sleep(0.5)
+            self.buckets.pg = self._capture_pg  # (see __init__: no eager work on this group)
         if dp and not inline:
             self.buckets.deferred = True
         # thread_local: the process group's watchdog thread keeps querying its events
@@ -414,17 +445,19 @@ class BalancedStep:
         mode = "thread_local" if dp else "global"
         try:
             with torch.cuda.graph(g, pool=self._gpool, capture_error_mode=mode):
-                loss = self._fwd_bwd(*(inputs or self._static)).detach()
+                loss, outs = self._fwd_bwd(*(inputs or self._static))
+                loss = loss.detach()
                 sums = None if (dp and not inline) else self.norms.sums(grad_scale=1.0 / self.world, lr=self.lr)
                 if sums is not None and self.device_gate:
                     self._gate_step(sums)
         finally:
             if dp:
                 self.buckets.deferred = False
+                self.buckets.pg = self.pg
             for m, st in steps:  # capture ran the Python forward but no kernel
                 m.step = st
                 m._step_mirror = st
-        self._graphs[key] = (g, loss, sums)
+        self._graphs[key] = (g, loss, sums, outs)
         return self._graphs[key]
 
     def __call__(self, x, y):
@@ -445,23 +478,35 @@ class BalancedStep:
                     if st[1].data_ptr() != y.data_ptr():
                         st[1].copy_(y)
             key = (self._graph_key(), None if slot is None else (x.data_ptr(), y.data_ptr()))
-            try:
-                g, loss, sums = self._graphs.get(key) or self._capture(key, slot)
-            except RuntimeError as e:  # capture refused on this system: keep stepping eagerly
+            entry, err = self._graphs.get(key), None
+            if entry is None:
+                try:
+                    entry = self._capture(key, slot)
+                except RuntimeError as e:  # capture refused on this system
+                    entry, err = None, e
+                if self.buckets is not None and self.world > 1 and not self._agree(entry is not None):
+                    # every rank takes the same fallback, so the ranks' collective sequences
+                    # stay identical (a rank replaying in-graph collectives beside one that
+                    # reduces eagerly would hang or sum the wrong buffers)
+                    self._graphs.pop(key, None)
+                    entry = None
+                    err = err or RuntimeError("graph capture failed on another rank")
+            if entry is None:
                 import sys
                 if self.graph_collectives:  # first fall back to the collectives-outside-the-graph form
-                    print(f"[greedy_multimodal_learning_amd] capturing the all-reduce failed ({e}); "
+                    print(f"[greedy_multimodal_learning_amd] capturing the all-reduce failed ({err}); "
                           "collectives run eagerly behind each replay", file=sys.stderr, flush=True)
                     self.graph_collectives = False
                     self._graphs = {}
                     torch.cuda.synchronize(self.device)
                     return self(x, y)
-                print(f"[greedy_multimodal_learning_amd] hipGraph capture failed ({e}); eager steps from now on",
+                print(f"[greedy_multimodal_learning_amd] hipGraph capture failed ({err}); eager steps from now on",
                       file=sys.stderr, flush=True)
                 self.graphs = False
                 self._graphs = {}
                 torch.cuda.synchronize(self.device)
                 return self(x, y)
+            g, loss, sums, outs = entry
             want = gate is not None and hasattr(gate, "needs_bdr") and gate.needs_bdr()
             g.replay()
             if self.buckets is not None and not self.graph_collectives:
@@ -472,10 +517,12 @@ class BalancedStep:
             for m in self._mmtms:
                 m.step += 1
                 m._step_mirror = m.step
+            self.last_outs = outs  # the graph's static branch logits, current after the replay
             return self._after(loss, sums, want)
         # detached: a kept-alive autograd graph would pin AccumulateGrad nodes to this
         # step's stream (breaks later graph capture, and holds memory)
-        loss = self._fwd_bwd(x, y).detach()
+        loss, self.last_outs = self._fwd_bwd(x, y)
+        loss = loss.detach()
         want = gate is not None and hasattr(gate, "needs_bdr") and gate.needs_bdr()
         t = self.timer
         if t is not None:
@@ -489,6 +536,13 @@ class BalancedStep:
             ev1.record()
             t.append((ev0, ev1))
         return self._after(loss, sums, want)
+
+    def _agree(self, ok):
+        """True iff `ok` on every rank (an eager MIN all-reduce on the step's group)."""
+        on_dev = dist.get_backend(self.pg) == "nccl"
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.device if on_dev else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.pg)
+        return bool(int(t.item()))
 
     def _after(self, loss, sums, want):
         gate = self.gate

@@ -10,13 +10,15 @@ Here the same gin names and parameters (`train.*`, `training_loop.*`, `MMTM_MVCN
 `get_mvdcndata.*`, `Bias_Mitigation_Strong.*`) build the MI355X path: the device input
 pipeline (dataset.py) delivers view-major channels_last batches, and every training
 step is one `engine.BalancedStep` (forward, blend_loss, backward, gate, SGD fused; a
-hipGraph replay).  Callback names that this package does not provide
-(`CompletedStopping`, `ReduceLROnPlateau_PyTorch`: host bookkeeping, out of scope) are
-skipped exactly as the reference skips names missing from `src.callbacks`.
+hipGraph replay).  The callbacks of training_guided.gin - `CompletedStopping`,
+`ReduceLROnPlateau_PyTorch` (which lowers the engine's learning rate through the
+optimizer object) and the gate - run on their reference hooks; names missing from
+`src.callbacks` are skipped exactly as the reference skips them.
 The loop keeps the reference's per-epoch history keys (`loss`, `acc`,
-`acc_modal_{i}`, `train_indices`, `val_*`, `test_*`, `d_BDR`, `curation_mode`,
-`caring_modality`) in `history.pickle` / `history.csv`, and `model_best_val.pt`
-holds `{'model': state_dict}` (the format `eval_` loads, src/training_loop.py:78-83).
+`acc_modal_{i}`, `train_indices`, `val_*`, `test_*`, plus the gate's `d_BDR`,
+`curation_mode`, `caring_modality` lists) in `history.pickle` / `history.csv`, and
+`model_best_val.pt` / `model_last_epoch.pt` hold `{'model', 'optimizer'}` state dicts
+(src/training_loop.py:26-48, 78-83).
 
 CLI (reference: `train.py save_path configs/x.gin [bindings]`, src/utils.py:58-68):
     python -m greedy_multimodal_learning_amd.train SAVE_PATH CONFIG[#CONFIG...] [BINDINGS]
@@ -38,7 +40,9 @@ _DTYPES = {"bf16": torch.bfloat16, "fp32": torch.float32}
 
 def construct_callbacks(names):
     """Reference train.py:53-57: instantiate (gin-bound) every named callback that the
-    callbacks module provides; silently skip the others."""
+    callbacks module provides (Bias_Mitigation_Strong / _Random, CompletedStopping,
+    ReduceLROnPlateau_PyTorch); names the reference's src.callbacks does not export are
+    skipped as the reference skips them."""
     out = []
     for name in names:
         cls = avail_callbacks.__dict__.get(name)
@@ -51,10 +55,12 @@ def _metrics(lm, outs, y):
     return float(acc(lm, y)), [float(acc(o, y)) for o in outs]
 
 
-def evaluate(model, loader, phase, compute_dtype, steps=None, record_squeezed=False):
+def evaluate(model, loader, phase, compute_dtype, steps=None, record_squeezed=False, curation=(False, None)):
     """Reference Model_._eval_generator (src/framework.py:216-248): eval mode, no grad,
     size-weighted loss and accuracies, the batches' indices, and (recording runs) the
-    squeezed maps per batch (`{phase}_squeezedmaps_array_list`, :160-161)."""
+    squeezed maps per batch (`{phase}_squeezedmaps_array_list`, :160-161).  `curation`:
+    the (curation_mode, caring_modality) the model is called with, as Model_ passes its
+    own flags in evaluation too (src/framework.py:146-148)."""
     model.eval()
     n, loss_sum, acc_sum, accm_sum, idxs, squeezed = 0, 0.0, 0.0, None, [], []
     with torch.no_grad():
@@ -62,7 +68,7 @@ def evaluate(model, loader, phase, compute_dtype, steps=None, record_squeezed=Fa
             if steps is not None and bi >= steps:
                 break
             with torch.autocast("cuda", dtype=compute_dtype, enabled=compute_dtype != torch.float32):
-                lm, outs, _, sq = model(x)
+                lm, outs, _, sq = model(x, curation_mode=curation[0], caring_modality=curation[1])
             outs = [o.float() for o in outs]
             b = len(y)
             loss_sum += float(blend_loss(outs, y)) * b
@@ -105,9 +111,18 @@ def training_loop(model, loss_function, metrics, optimizer, config, save_path, s
                   compute_dtype="bf16", graphs=True):
     """Reference src/training_loop.py:86-143 + Model_.train_loop (src/framework.py:
     250-330) on the fused engine.  `optimizer` is the (lr, momentum, wd) triple of the
-    reference's SGD (only momentum = wd = 0, as every config uses, is fused); `metrics`
-    and `loss_function` are the reference's acc / blend_loss (fixed in the engine).
-    Epochs 1 .. n_epochs-1 as the reference (`epochs=n_epochs - 1`)."""
+    reference's SGD (only momentum = wd = 0, as every config uses, is fused; a torch SGD
+    over the model's parameters holds the learning rate and the state_dict the
+    checkpoints carry, and ReduceLROnPlateau_PyTorch drives it); `metrics` and
+    `loss_function` are the reference's acc / blend_loss (fixed in the engine).
+    Epochs 1 .. n_epochs-1 as the reference (`epochs=n_epochs - 1`).  Per epoch the
+    history gets the reference's train_dict keys (`loss`, `acc`, `acc_modal_{i}`,
+    `train_indices`), the validation / test dicts, and the gate's per-step lists; a NaN
+    step loss or CompletedStopping ends training after that epoch (:321-322, :343);
+    `model_best_val.pt` (best `checkpoint_monitor`) and `model_last_epoch.pt` (every
+    epoch) hold {'model', 'optimizer'} (src/training_loop.py:26-48, src/utils.py:107-115)."""
+    import math
+
     from .engine import BalancedStep
     lr, momentum, wd = optimizer
     if momentum != 0 or wd != 0:
@@ -122,54 +137,89 @@ def training_loop(model, loss_function, metrics, optimizer, config, save_path, s
     gate = gates[0] if gates else None
     cdt = _DTYPES[compute_dtype]
     step = BalancedStep(model, lr=lr, gate=gate, compute_dtype=cdt, channels_last=True, graphs=graphs)
+    # the reference's optimizer object (never stepped: the engine's fused pass applies the
+    # update with the learning rate read from it)
+    opt = torch.optim.SGD(model.parameters(), lr=lr, momentum=momentum, weight_decay=wd)
+    flags = step.flags  # the gate's model_pytoune; every other callback shares it
+    flags.stop_training = False
+    others = [c for c in custom_callbacks if c is not gate]
     for c in custom_callbacks:
         c.set_save_path(save_path)
         c.set_config(config)
+        c.set_optimizer(opt)
         if c is not gate:
             c.set_model(model, ignore=False)
+            c.set_model_pytoune(flags)
+    for c in others:
+        c.on_train_begin({})
     H = {}
     best = None
     for epoch in range(1, n_epochs):
         step.on_epoch_begin(epoch)
-        for c in custom_callbacks:
-            if c is not gate:
-                c.on_epoch_begin(epoch, {})
-        loss_sum = torch.zeros((), device=dev)
-        n, idxs, d_bdr, cur, caring = 0, [], [], [], []
+        for c in others:
+            c.on_epoch_begin(epoch, {})
+        n, loss_sum, acc_sum, accm_sum = 0, 0.0, 0.0, np.zeros(nummodalities)
+        idxs, d_bdr, cur, caring = [], [], [], []
         for bi, (idx, x, y) in enumerate(train):
             if steps_per_epoch is not None and bi >= steps_per_epoch:
                 break
-            loss = step(x, y)
-            loss_sum += loss * len(y)
-            n += len(y)
+            for c in others:
+                c.on_batch_begin(bi + 1, {})
+            step.lr = float(opt.param_groups[0]["lr"])
+            loss = float(step(x, y))
+            outs = step.last_outs
+            with torch.no_grad():  # Model_._compute_loss_and_metrics (src/framework.py:152-156)
+                a = float(acc(list(outs), y))
+                am = [float(acc(o, y)) for o in outs]
+            b = len(y)
+            loss_sum += loss * b
+            acc_sum += a * b
+            accm_sum += np.array(am) * b
+            n += b
             idxs.append(idx.numpy())
             if gate is not None:
                 st = step.sync_gate() if step.device_gate else None
                 d_bdr.append(float(st["d_BDR"] if st else getattr(gate, "d_BDR", 0.0) or 0.0))
                 cur.append(bool(step.flags.curation_mode))
                 caring.append(step.flags.caring_modality)
-        logs = {"epoch": epoch, "loss": float(loss_sum) / max(n, 1),
+            batch_logs = {"batch": bi + 1, "size": b, "loss": loss, "acc": a,
+                          **{f"acc_modal_{i}": v for i, v in enumerate(am)}}
+            for c in others:
+                c.on_batch_end(bi + 1, batch_logs)
+            if math.isnan(loss):
+                flags.stop_training = True
+        logs = {"epoch": epoch, "loss": loss_sum / max(n, 1), "acc": acc_sum / max(n, 1),
+                **{f"acc_modal_{i}": v / max(n, 1) for i, v in enumerate(accm_sum)},
                 "train_indices": np.concatenate(idxs) if idxs else np.zeros(0, np.int64)}
         if gate is not None:
             logs.update({"d_BDR": d_bdr, "curation_mode": cur, "caring_modality": caring})
+        # validation / test with the model's current curation flags (src/framework.py:146-148)
+        if step.device_gate:
+            step.sync_gate()
+        fl = (bool(step.flags.curation_mode), step.flags.caring_modality)
         if valid is not None:
-            logs.update(evaluate(model, valid, "val", cdt, validation_steps))
+            logs.update(evaluate(model, valid, "val", cdt, validation_steps, curation=fl))
         if test is not None:
-            logs.update(evaluate(model, test, "test", cdt, test_steps))
+            logs.update(evaluate(model, test, "test", cdt, test_steps, curation=fl))
         for k, v in logs.items():
             H.setdefault(k, []).append(v)
-        mon = logs.get(checkpoint_monitor)
-        if save_path and mon is not None and (best is None or mon > best):
-            best = mon
-            torch.save({"model": model.state_dict()}, os.path.join(save_path, "model_best_val.pt"))
         if save_path:
             save_history(H, save_path)
+            ck = {"model": model.state_dict(), "optimizer": opt.state_dict()}
+            mon = logs.get(checkpoint_monitor)
+            if mon is not None and (best is None or mon > best):
+                best = mon
+                torch.save(ck, os.path.join(save_path, "model_best_val.pt"))
+            torch.save(ck, os.path.join(save_path, "model_last_epoch.pt"))
         if verbose:
-            print(f"epoch {epoch}: loss {logs['loss']:.4f}" +
+            print(f"epoch {epoch}: loss {logs['loss']:.4f} acc {logs['acc']:.2f} lr {step.lr:g}" +
                   (f" val_acc {logs['val_acc']:.2f}" if "val_acc" in logs else ""), flush=True)
-        for c in custom_callbacks:
-            if c is not gate:
-                c.on_epoch_end(epoch, logs)
+        for c in others:
+            c.on_epoch_end(epoch, logs)
+        if flags.stop_training:
+            break
+    for c in others:
+        c.on_train_end({})
     return H
 
 

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define GM_ABI_VERSION 1
+#define GM_ABI_VERSION 2
 
 /* activation element types */
 #define GM_F32  0
@@ -63,6 +63,24 @@ int gm_set_spin_limit(unsigned polls);
  * kernels); the fused grid is capped at CUs x (measured blocks per CU) / n, else the
  * two-launch path runs.  Default 4 (GM_BN_FUSE_STREAMS overrides at load). */
 int gm_bn_set_concurrency(int n);
+/* Device residency plan for every kernel whose workgroups wait on other workgroups of
+ * the same launch (single-launch BatchNorm, split-K turnstile).  Such a launch is only
+ * safe while all the workgroups it waits on can be resident; what else holds CU slots
+ * at the same time is declared here:
+ *   streams      launches of this process that can wait at once (trunk streams; >= 1)
+ *   sharers      processes sharing this GPU (ranks on one device in rehearsals; >= 1)
+ *   reserved_cus CUs held by concurrently resident kernels that never yield, e.g. the
+ *                RCCL all-reduce kernels that overlap backward under data parallelism
+ * The BatchNorm grid is capped at (CUs - reserved) x (blocks per CU) /
+ * (max(concurrency, streams) x sharers) and the waiting split-K workgroups of one launch at
+ * (CUs - reserved) x 2 / (streams x sharers).  Defaults: 2, 1, 0.
+ * The engine sets it per process (engine.BalancedStep).  gm_get_residency reads it. */
+int gm_set_residency(int streams, int sharers, int reserved_cus);
+int gm_get_residency(int* streams, int* sharers, int* reserved_cus);
+/* Test hook: `blocks` workgroups of `threads` threads, each holding `lds_bytes` of LDS
+ * (up to 160 KiB: one workgroup per CU), spinning for `usec` microseconds (s_sleep +
+ * the 100 MHz real-time counter) - a stand-in for a resident collective kernel. */
+int gm_test_hold_cus(int blocks, int threads, int lds_bytes, unsigned usec, void* stream);
 /* 0: always the two-launch path; 1: single launch with register-held strips only;
  * 2 (default): also the streaming single-launch variant.  GM_BN_FUSED at load. */
 int gm_bn_set_fused_mode(int mode);

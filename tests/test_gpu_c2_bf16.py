@@ -111,4 +111,6 @@ def test_c2_group_sums_and_d_bdr_vs_oracle(c2_run):
     # (main0, main1, bypass0, bypass1); d_BDR -0.01283 vs -0.01673 (3.9e-3)
     assert e_w.max() < 1e-6
     assert e_g.max() < 3e-2
-    assert e_d < 1.2e-2
+    # below epsilon (0.01) with a 2x margin over the measured gap; decision-level parity of
+    # the same gate over a 20-step trace: test_gpu_gate_decisions.py
+    assert e_d < 8e-3

@@ -273,12 +273,14 @@ def test_conv_resident_weight_layer1(dev, shape):
 
 
 @pytest.mark.parametrize("shape", [(4, 128, 28, 28, 128, 3, 3, 1, 1), (4, 64, 56, 56, 128, 3, 3, 2, 1),
-                                   (64, 256, 14, 14, 256, 3, 3, 1, 1), (5, 128, 7, 7, 256, 1, 1, 2, 0)],
+                                   (64, 256, 14, 14, 256, 3, 3, 1, 1), (5, 128, 7, 7, 256, 1, 1, 2, 0),
+                                   (4, 64, 56, 56, 64, 3, 3, 1, 1)],
                          ids=lambda s: "x".join(map(str, s)))
 def test_conv_dgrad_fused_addend(dev, shape):
     """The input-gradient epilogue's fused gradient join (dx = dgrad + addend, the
-    residual branch's gradient) on the halo, im2col and split-K kernels: equal to the
-    fp32 reference plus the addend, and to the unfused dgrad plus the addend."""
+    residual branch's gradient) on the halo, im2col, split-K and layer-1 resident-weight
+    kernels (every identity block joins in place, layer 1 included): equal to the fp32
+    reference plus the addend, and to the unfused dgrad plus the addend."""
     from greedy_multimodal_learning_amd import conv as G
     N, C, H, W, K, R, S, st, pad = shape
     g = torch.Generator(device="cuda").manual_seed(sum(shape) + 1)

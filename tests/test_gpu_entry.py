@@ -24,6 +24,9 @@ train.lr=0.1
 train.wd=0.0
 train.momentum=0
 train.callbacks=['CompletedStopping', 'ReduceLROnPlateau_PyTorch', 'Bias_Mitigation_Strong']
+ReduceLROnPlateau_PyTorch.metric='loss'
+CompletedStopping.patience=5
+CompletedStopping.monitor='acc'
 Bias_Mitigation_Strong.epsilon=0.01
 Bias_Mitigation_Strong.curation_windowsize=5
 Bias_Mitigation_Strong.starting_epoch=1
@@ -75,7 +78,11 @@ def test_train_record_cur_eval(tmp_path):
     assert len(H["loss"]) == 2 and all(np.isfinite(H["loss"]))
     assert all(len(d) == 3 for d in H["d_BDR"])  # 12 training samples (80 % of 14) at batch 4 -> 3 steps
     assert sorted(np.concatenate([H["train_indices"][0], H["val_indices"][0]]).tolist()) == list(range(14))
-    assert os.path.exists(os.path.join(tsave, "model_best_val.pt"))
+    for f in ("model_best_val.pt", "model_last_epoch.pt"):  # src/training_loop.py:39-48, src/utils.py:107-115
+        ck = torch.load(os.path.join(tsave, f), weights_only=True)
+        assert set(ck) == {"model", "optimizer"} and ck["optimizer"]["param_groups"][0]["lr"] == 0.1
+    # the reference's train_dict metrics (src/framework.py:324-327)
+    assert all(0 <= a <= 100 for k in ("acc", "acc_modal_0", "acc_modal_1") for a in H[k])
     with open(os.path.join(tsave, "history.pickle"), "rb") as f:
         assert "train_indices" in pickle.load(f)
 

@@ -1,0 +1,93 @@
+"""Decision-level parity of the BENCHMARKED gate: BalancedStep in bf16 at config C2
+(B = 64 two-view 224x224 objects, hipGraph replay, on-device gate) trained with
+training_guided.gin's gate (lr 0.1, epsilon 0.01, window 5, unlocked) for 20 steps,
+checked step by step against the fp32 oracle of the reference step
+(/root/reference/src/callbacks.py:199-263, src/model.py:63-108, train.py:23-29).
+
+Teacher-forced: before every step whose gate computes d_BDR (unlocked, not inside a
+curation window) the oracle takes the HIP run's current fp32 master weights and M
+accumulators, runs the reference's forward/backward on the same bf16-rounded batch
+and makes the reference's decision.  So each step compares ONE step's arithmetic
+(bf16 trunk vs fp32) and the decision it leads to, not two diverging trajectories.
+
+The bf16 trunk moves d_BDR by rounding noise (test_gpu_c2_bf16.py); a decision can only
+differ where the oracle's |d_BDR| lies within that noise of epsilon.  BAND is that
+noise bound: every step whose oracle |d_BDR| is more than BAND away from epsilon must
+make the identical decision (curate or not, and which modality).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+B, H, STEPS, EPS, WINDOW, LR = 64, 224, 20, 0.01, 5, 0.1
+BAND = 4e-3  # bf16-vs-fp32 d_BDR noise bound (see test_bf16_gate_decisions_vs_oracle)
+
+
+@pytest.fixture(scope="module")
+def trace():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from greedy_multimodal_learning_amd.callbacks import Bias_Mitigation_Strong
+    from greedy_multimodal_learning_amd.engine import BalancedStep
+    from greedy_multimodal_learning_amd.model import MMTM_MVCNN
+    from oracle import gating_ref, model_ref, weights
+    dev = torch.device("cuda:0")
+    torch.set_num_threads(max(1, min(32, torch.get_num_threads())))
+    model = weights.apply_to_module(MMTM_MVCNN(), seed=5).to(dev)
+    gate = Bias_Mitigation_Strong(epsilon=EPS, curation_windowsize=WINDOW, branchnames=["net_view_0", "net_view_1"],
+                                  starting_epoch=1)
+    step = BalancedStep(model, lr=LR, gate=gate, graphs=True)
+    step.on_epoch_begin(1)
+    assert step.device_gate and step.graphs
+    g = torch.Generator().manual_seed(77)
+    batches = []
+    for _ in range(4):
+        buf = torch.randn(2, B, H, H, 3, generator=g).bfloat16()
+        batches.append((buf, torch.randint(0, 40, (B,), generator=g)))
+    dbat = [(b.to(dev).permute(1, 0, 4, 2, 3), y.to(dev)) for b, y in batches]
+    oracle = model_ref.MMTM_MVCNN_Ref()
+    rows = []
+    for t in range(STEPS):
+        st = step.sync_gate()
+        deciding = not st["curation_mode"]  # unlocked: d_BDR is computed unless inside a window
+        if deciding:
+            sd = {n: p.detach().float().contiguous().cpu() for n, p in model.named_parameters()}
+            M = [gate.M_bypass_modal_0, gate.M_bypass_modal_1, gate.M_main_modal_0, gate.M_main_modal_1]
+        x, y = dbat[t % 4]
+        step(x, y)
+        after = step.sync_gate()
+        if not deciding:
+            continue
+        # the oracle's step from the same state
+        oracle.load_state_dict(sd, strict=False)
+        oracle.zero_grad(set_to_none=True)
+        oracle.train(True)
+        buf, yc = batches[t % 4]
+        _, outs, _, _ = oracle(buf.float().permute(1, 0, 4, 2, 3).contiguous())
+        gating_ref.blend_loss(outs, yc).backward()
+        s = gating_ref.group_sums([(n, p, p.grad) for n, p in oracle.named_parameters()])
+        bdr = gating_ref.BDRState(EPS, WINDOW)
+        bdr.M_bypass, bdr.M_main = [M[0], M[1]], [M[2], M[3]]
+        d_o = float(bdr.update(s))
+        dec_o = (abs(d_o) > EPS, (1 if d_o < 0 else 0) if abs(d_o) > EPS else 0)
+        dec_h = (bool(after["curation_mode"]), after["caring_modality"] if after["curation_mode"] else 0)
+        rows.append((t, after["d_BDR"], d_o, dec_h, dec_o))
+        print(f"step {t:2d}: d_BDR hip {after['d_BDR']:+.5f} oracle {d_o:+.5f} |diff| "
+              f"{abs(after['d_BDR'] - d_o):.2e} decision hip {dec_h} oracle {dec_o}", flush=True)
+    return rows
+
+
+def test_bf16_gate_decisions_vs_oracle(trace):
+    rows = trace
+    assert len(rows) >= 4, "too few deciding steps"
+    diff = np.array([abs(r[1] - r[2]) for r in rows])
+    print(f"d_BDR |hip - oracle| over {len(rows)} deciding steps: median {np.median(diff):.2e} "
+          f"p90 {np.percentile(diff, 90):.2e} max {diff.max():.2e}")
+    assert diff.max() < BAND, "bf16 d_BDR noise above the band the decisions are judged with"
+    clear = [r for r in rows if abs(abs(r[2]) - EPS) > BAND]
+    for t, dh, do, dec_h, dec_o in clear:
+        assert dec_h == dec_o, (t, dh, do, dec_h, dec_o)
+    agree = sum(r[3] == r[4] for r in rows)
+    print(f"decisions identical on {agree}/{len(rows)} deciding steps ({len(clear)} outside the band)")

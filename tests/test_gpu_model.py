@@ -92,6 +92,8 @@ def test_model_vs_reference(golden, dev, case):
                    for _, q in m.named_parameters()])
     live = gn64 > 0
     e_ref, e_gpu = _rel(fix[p + "gn"][live], gn64[live]), _rel(gn[live], gn64[live])
+    print(f"{case['id']}: grad-norm rel vs fp64 rms {np.sqrt((e_gpu ** 2).mean()):.2e} max {e_gpu.max():.2e} "
+          f"(reference rms {np.sqrt((e_ref ** 2).mean()):.2e} max {e_ref.max():.2e})")
     # Floors: the trunk's vendor BatchNorm/convolution kernels reduce in fp32 (the
     # reference's CPU run accumulates BN in double); measured on 224x224 maps across
     # MIOpen's fp32 algorithms: 3e-4 .. 1.4e-3 rms, <= 7e-3 max.  A wrong gradient
@@ -111,6 +113,7 @@ def test_model_vs_reference(golden, dev, case):
         else:
             assert q.grad is None, n  # curated branch: no gradient, like the reference
     es_ref, es_gpu = np.concatenate(es_ref), np.concatenate(es_gpu)
+    print(f"{case['id']}: grad samples rel vs fp64 max {es_gpu.max():.2e} (reference {es_ref.max():.2e})")
     assert es_gpu.max() <= max(10 * es_ref.max(), 2e-2), "grad samples"  # vendor fp32 BN floor (see above)
     if (p + "d_BDR") in fix.files:
         cb = Bias_Mitigation_Strong(epsilon=0.01, curation_windowsize=5,

@@ -19,6 +19,8 @@
 #                                                                     -> gpurun_out/pmcg_NAME.txt
 #   trunkpmc     three rocprofv3 --pmc passes over tools/trunk_pmc.py (FETCH, WRITE, MFMA/LDS set),
 #                per-op table + conv-family traffic json         -> gpurun_out/trunk_pmc.md, trunk_pmc.json
+#   mmtmpmc      two rocprofv3 --pmc passes (FETCH, WRITE) over tools/mmtm_probe.py (the MMTM squeeze
+#                at B=256 rotating over 411 MB)                   -> gpurun_out/traffic_mmtm.json
 #   py:FILE[,ARGS] python FILE ARGS (a tools/ script; commas become spaces) -> gpurun_out/py_FILE.log
 set -o pipefail
 mkdir -p gpurun_out
@@ -37,11 +39,11 @@ for s in "$@"; do
   echo "=== $s $(date +%T)"
   case "$s" in
     tests)
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 \
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 -rA \
         --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { tail -30 gpurun_out/gpu_tests.log; exit 11; }
       tail -3 gpurun_out/gpu_tests.log ;;
     tests:*)
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 \
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 -rA \
         --timeout-method thread -k "${s#tests:}" > gpurun_out/gpu_tests_k.log 2>&1 || { tail -40 gpurun_out/gpu_tests_k.log; exit 12; }
       tail -3 gpurun_out/gpu_tests_k.log ;;
     smoke)
@@ -91,6 +93,14 @@ for s in "$@"; do
       python3 tools/trunk_pmc.py report gpurun_out/tp_fetch gpurun_out/tp_write gpurun_out/tp_opmfma \
         --json gpurun_out/trunk_pmc.json > gpurun_out/trunk_pmc.md && rm -rf gpurun_out/tp_fetch gpurun_out/tp_write gpurun_out/tp_opmfma
       tail -3 gpurun_out/trunk_pmc.md ;;
+    mmtmpmc)
+      for n in fetch write; do
+        timeout -s KILL 120 rocprofv3 --pmc ${PMC[$n]} --output-format csv -d "gpurun_out/mp_$n" -o pmc \
+          -- python3 tools/mmtm_probe.py run > "gpurun_out/mp_$n.log" 2>&1 || { tail -30 "gpurun_out/mp_$n.log"; exit 24; }
+      done
+      python3 tools/mmtm_probe.py report gpurun_out/mp_fetch gpurun_out/mp_write --json gpurun_out/traffic_mmtm.json \
+        > gpurun_out/mmtm_pmc.log && rm -rf gpurun_out/mp_fetch gpurun_out/mp_write
+      tail -4 gpurun_out/traffic_mmtm.json ;;
     py:*)
       a="${s#py:}"; f="${a%%,*}"; args=""; [ "$f" != "$a" ] && args="${a#*,}"
       lg="gpurun_out/py_$(basename "$f" .py).log"

@@ -25,6 +25,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 MFMA_PEAK_TFS = 2500.0
+MFMA_F32_PEAK_TFS = 157.3  # v_mfma_f32_32x32x2_f32 = the f32 vector rate (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
 CL = torch.channels_last
 
@@ -68,49 +69,109 @@ def _row(name, op, cnt, flops, nbytes, secs, launches_per_call=1):
                 launches=launches_per_call)
 
 
-def conv_rows(B, dev, reps=10):
-    return [_row(name, op, cnt, flops, nbytes, _time(fn, reps)) for name, op, cnt, flops, nbytes, fn in conv_ops(B, dev)]
+def conv_rows(B, dev, reps=10, rotate_bytes=0, dtype="bf16"):
+    ops = conv_ops(B, dev, rotate_bytes) if dtype == "bf16" else conv_ops_f32(B, dev, rotate_bytes)
+    return [_row(name, op, cnt, flops, nbytes, _time(fn, reps)) for name, op, cnt, flops, nbytes, fn in ops]
 
 
-def conv_ops(B, dev):
-    """(name, pass, count per view, FLOPs, algorithmic bytes, callable) of every trunk
-    convolution pass of one view at batch B."""
+def conv_ops_f32(B, dev, rotate_bytes=0):
+    """The same passes on the reference-precision path: gm_conv2d_f32 (exact-f32 MFMA),
+    fp32 channels_last activations, the stem unpadded (what the fp32 drop-in runs)."""
     from greedy_multimodal_learning_amd import conv as G
+    from greedy_multimodal_learning_amd import _lib as L
+    out = []
+    for name, (C, H, W, K, R, st, pad, cnt) in TRUNK:
+        P, Q = (H + 2 * pad - R) // st + 1, (W + 2 * pad - R) // st + 1
+        flops = 2.0 * B * P * Q * K * C * R * R
+        xb, yb, wb = B * H * W * C * 4, B * P * Q * K * 4, K * C * R * R * 4
+        d = G._desc(B, H, W, C, K, R, R, st, pad)
+
+        def make(op, d=d, C=C, H=H, W=W, K=K, R=R, P=P, Q=Q):
+            x = torch.randn(B, C, H, W, device=dev).contiguous(memory_format=CL)
+            w = torch.randn(K, C, R, R, device=dev).contiguous(memory_format=CL)
+            dy = torch.randn(B, K, P, Q, device=dev).contiguous(memory_format=CL)
+            if op == "fwd":
+                y = torch.empty(B, K, P, Q, device=dev).contiguous(memory_format=CL)
+                return lambda: G.conv_f32(L.GM_CONV_FWD, d, x=x, w=w, out=y)
+            if op == "dgrad":
+                dx = torch.empty(B, C, H, W, device=dev).contiguous(memory_format=CL)
+                return lambda: G.conv_f32(L.GM_CONV_DGRAD, d, w=w, dy=dy, out=dx)
+            dw = torch.empty(K, C, R, R, device=dev).contiguous(memory_format=CL)
+            return lambda: G.conv_f32(L.GM_CONV_WGRAD, d, x=x, dy=dy, out=dw)
+        passes = [("fwd", xb + wb + yb), ("wgrad", xb + yb + wb)]
+        if C != 3:
+            passes.insert(1, ("dgrad", yb + wb + xb))
+        for op, nbytes in passes:
+            sets = max(1, -(-int(rotate_bytes) // nbytes)) if rotate_bytes else 1
+            fn = make(op) if sets == 1 else _cycle([make(op) for _ in range(sets)])
+            out.append((name, op, cnt, flops, nbytes, fn))
+    return out
+
+
+def _cycle(fns):
+    """One callable that calls fns[0], fns[1], ... in turn (distinct buffer sets)."""
+    state = [0]
+
+    def fn():
+        f = fns[state[0] % len(fns)]
+        state[0] += 1
+        return f()
+    return fn
+
+
+def conv_ops(B, dev, rotate_bytes=0):
+    """(name, pass, count per view, FLOPs, algorithmic bytes, callable) of every trunk
+    convolution pass of one view at batch B.  rotate_bytes > 0: each callable cycles over
+    enough distinct operand sets that consecutive launches touch more than rotate_bytes
+    (beyond the 256 MiB Infinity Cache: every launch reads HBM, not the last one's lines)."""
+    from greedy_multimodal_learning_amd import conv as G
+    from greedy_multimodal_learning_amd import _lib as L
+    import ctypes
     out = []
     for name, (C, H, W, K, R, st, pad, cnt) in TRUNK:
         Cp = G._cpad(C)
         P, Q = (H + 2 * pad - R) // st + 1, (W + 2 * pad - R) // st + 1
         flops = 2.0 * B * P * Q * K * C * R * R
-        x = torch.randn(B, Cp, H, W, device=dev).bfloat16().contiguous(memory_format=CL)
-        w = torch.randn(K, Cp, R, R, device=dev).bfloat16().contiguous(memory_format=CL)
-        dy = torch.randn(B, K, P, Q, device=dev).bfloat16().contiguous(memory_format=CL)
-        wt = w.permute(1, 0, 2, 3).contiguous(memory_format=CL)
         xb, yb, wb = B * H * W * C * 2, B * P * Q * K * 2, K * C * R * R * 2
-        if C == 3:  # the stem runs on the pixel-pair view; its input gradient is never computed
-            xp = G.stem_pack_input(x[:, :3], R, R, pad)
-            wp = G.stem_pack_weight(w[:, :3].float())
-            ops = [("fwd", lambda xp=xp, wp=wp, P=P, Q=Q: G.stem_fwd(xp, wp, P, Q), xb + wb + yb)]
-            from greedy_multimodal_learning_amd import _lib as L
-            import ctypes
-            d = G._desc_hw(B, xp.shape[2], xp.shape[3], 8, K, R, wp.shape[3], 2, 1, 0, 0)
-            need = L.load().gm_conv2d_wgrad_hw_scratch(ctypes.byref(d))
-            scr = torch.empty(max(need, 16), device=dev, dtype=torch.uint8)
-            dwp = torch.empty(K, R, wp.shape[3], 8, device=dev, dtype=torch.float32)
 
-            def stem_wgrad(d=d, dy=dy, xp=xp, dwp=dwp, scr=scr, need=need):
-                L.check(L.load().gm_conv2d_wgrad_hw_bf16(ctypes.byref(d), dy.data_ptr(), xp.data_ptr(),
-                                                         dwp.data_ptr(), 8, 0, scr.data_ptr(), need,
-                                                         L.stream_of(dev)), "wgrad_hw")
-            ops.append(("wgrad", stem_wgrad, xb + yb + K * C * R * R * 4))
+        def operands():
+            x = torch.randn(B, Cp, H, W, device=dev).bfloat16().contiguous(memory_format=CL)
+            w = torch.randn(K, Cp, R, R, device=dev).bfloat16().contiguous(memory_format=CL)
+            dy = torch.randn(B, K, P, Q, device=dev).bfloat16().contiguous(memory_format=CL)
+            return x, w, dy
+
+        if C == 3:  # the stem runs on the pixel-pair view; its input gradient is never computed
+            def make(op):
+                x, w, dy = operands()
+                xp = G.stem_pack_input(x[:, :3], R, R, pad)
+                wp = G.stem_pack_weight(w[:, :3].float())
+                if op == "fwd":
+                    return lambda: G.stem_fwd(xp, wp, P, Q)
+                d = G._desc_hw(B, xp.shape[2], xp.shape[3], 8, K, R, wp.shape[3], 2, 1, 0, 0)
+                need = L.load().gm_conv2d_wgrad_hw_scratch(ctypes.byref(d))
+                scr = torch.empty(max(need, 16), device=dev, dtype=torch.uint8)
+                dwp = torch.empty(K, R, wp.shape[3], 8, device=dev, dtype=torch.float32)
+
+                def stem_wgrad():
+                    L.check(L.load().gm_conv2d_wgrad_hw_bf16(ctypes.byref(d), dy.data_ptr(), xp.data_ptr(),
+                                                             dwp.data_ptr(), 8, 0, scr.data_ptr(), need,
+                                                             L.stream_of(dev)), "wgrad_hw")
+                return stem_wgrad
+            passes = [("fwd", xb + wb + yb), ("wgrad", xb + yb + K * C * R * R * 4)]
         else:
-            dw = torch.empty(K, C, R, R, device=dev, dtype=torch.float32).contiguous(memory_format=CL)
-            ops = [("fwd", lambda x=x, w=w, st=st, pad=pad: G.conv_fwd(x, w, st, pad), xb + wb + yb),
-                   ("dgrad", lambda dy=dy, wt=wt, H=H, W=W, st=st, pad=pad: G.conv_dgrad_t(dy, wt, H, W, st, pad),
-                    yb + wb + xb),
-                   ("wgrad", lambda dy=dy, x=x, R=R, st=st, pad=pad, C=C, dw=dw: G.conv_wgrad(dy, x, R, R, st, pad, C,
-                                                                                             out=dw),
-                    xb + yb + K * C * R * R * 4)]
-        for op, fn, nbytes in ops:
+            def make(op, st=st, pad=pad):
+                x, w, dy = operands()
+                if op == "fwd":
+                    return lambda: G.conv_fwd(x, w, st, pad)
+                if op == "dgrad":
+                    wt = w.permute(1, 0, 2, 3).contiguous(memory_format=CL)
+                    return lambda: G.conv_dgrad_t(dy, wt, H, W, st, pad)
+                dw = torch.empty(K, C, R, R, device=dev, dtype=torch.float32).contiguous(memory_format=CL)
+                return lambda: G.conv_wgrad(dy, x, R, R, st, pad, C, out=dw)
+            passes = [("fwd", xb + wb + yb), ("dgrad", yb + wb + xb), ("wgrad", xb + yb + K * C * R * R * 4)]
+        for op, nbytes in passes:
+            sets = max(1, -(-int(rotate_bytes) // nbytes)) if rotate_bytes else 1
+            fn = make(op) if sets == 1 else _cycle([make(op) for _ in range(sets)])
             out.append((name, op, cnt, flops, nbytes, fn))
     return out
 
@@ -159,10 +220,11 @@ def bn_ops(B, dev):
     return out
 
 
-def measure_family(B, dev, reps=10):
+def measure_family(B, dev, reps=10, rotate_bytes=320e6, dtype="bf16"):
     """The conv family (fwd + dgrad + wgrad of every trunk shape of one view, weighted by
-    its count per view): (flops, secs, launches, rows)."""
-    rows = conv_rows(B, dev, reps)
+    its count per view): (flops, secs, launches, rows).  Launches rotate over operand sets
+    of more than the 256 MiB Infinity Cache (rotate_bytes), so none reads warm lines."""
+    rows = conv_rows(B, dev, reps, rotate_bytes, dtype)
     flops = sum(r["flops"] * r["count"] for r in rows)
     secs = sum(r["us"] * 1e-6 * r["count"] for r in rows)
     launches = sum(r["count"] for r in rows)
@@ -198,13 +260,15 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--md", default=None)
     ap.add_argument("--only", default="", help="conv | bn (default both)")
+    ap.add_argument("--rotate-mb", type=float, default=320.0,
+                    help="conv launches rotate over operand sets of this many MB (0: one warm set)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     from greedy_multimodal_learning_amd import build
     build.build()
     rows = []
     if a.only in ("", "conv"):
-        rows += conv_rows(a.batch, dev, a.reps)
+        rows += conv_rows(a.batch, dev, a.reps, a.rotate_mb * 1e6)
     if a.only in ("", "bn"):
         rows += bn_rows(a.batch, dev, a.reps)
     md = markdown(rows, a.batch)
