@@ -78,7 +78,7 @@ inline Plan make_plan(long long M, int C) {
     const size_t cnt = (size_t)p.nslice * sizeof(unsigned);
     p.off_coef = (cnt + kHdr - 1) / kHdr * kHdr;
     p.off_p1 = p.off_coef + (size_t)4 * C * sizeof(float);
-    p.bytes = p.off_p1 + (size_t)p.nslice * p.nrc * 2 * p.SW * sizeof(float);
+    p.bytes = p.off_p1 + (size_t)p.nslice * p.nrc * 2 * p.SW * sizeof(double);  // fp64 partials (fp32 path)
     return p;
 }
 
@@ -240,7 +240,7 @@ __device__ __forceinline__ FinOps fin_load(const ReduceArgs& a, int c) {
 
 // SC1: the coefficients are published with write-through stores (read by the other
 // blocks of the same launch in the fused forward, k_bn_fwd_fused)
-template <int MODE, bool SC1 = false>
+template <int MODE, bool SC1 = false, bool CENTER = false>
 __device__ __forceinline__ void finalize(const ReduceArgs& a, int c, double S1, double S2, double invM,
                                          const FinOps& f) {
     const int C = a.C;
@@ -276,7 +276,12 @@ __device__ __forceinline__ void finalize(const ReduceArgs& a, int c, double S1, 
         const double cb = -g * is * is * is * S2 * invM;
         a.coef[c] = (float)ca;
         a.coef[C + c] = (float)cb;
-        a.coef[2 * C + c] = (float)(-ca * S1 * invM - cb * mean);
+        if (CENTER) {  // dx = ca*dz + cb*(x - mean) + cc (fp32 path: no cb*x - cb*mean cancellation)
+            a.coef[2 * C + c] = (float)(-ca * S1 * invM);
+            a.coef[3 * C + c] = (float)mean;
+        } else {
+            a.coef[2 * C + c] = (float)(-ca * S1 * invM - cb * mean);
+        }
         if (SC1) {
             st_sc1(&a.coef[c], a.coef[c]);
             st_sc1(&a.coef[C + c], a.coef[C + c]);
@@ -432,6 +437,90 @@ __device__ __forceinline__ void combine_finalize(const ReduceArgs& a, int cs, fl
         }
         finalize<MODE, SC1>(a, cs * SW + t, S1, S2, 1.0 / (double)a.M, fo);
     }
+}
+
+// The reference-precision (fp32) reduce: the reference's CPU BatchNorm accumulates its
+// sums in double (ATen acc_type<float> on the CPU), and long fp32 sums of gradients with
+// mixed signs lose the digits the parameter gradients are made of (1e-3 relative at
+// 224x224 maps, measured).  So every level accumulates in fp64: per-thread sums, the
+// row-group combine, the per-block partials (sc1 stores, 8 B) and the last block's
+// combine; the centred backward coefficients (finalize<CENTER>).
+template <int MODE>
+__global__ __launch_bounds__(kT) void k_bn_reduce_f64(ReduceArgs a) {
+    __shared__ double red[kRedF];  // rpp * 2 * SW == 4096 doubles
+    __shared__ float flag;
+    const int t = threadIdx.x;
+    const int C = a.C, SW = a.SW;
+    const int rc = blockIdx.x, cs = blockIdx.y;
+    const int tpr = 1 << a.tpr_log;
+    const int cg = t & (tpr - 1);
+    const int r0 = t >> a.tpr_log;
+    const int rpp = kT >> a.tpr_log;
+    const long long vpr = C >> 3;
+    const int c0 = cs * SW + cg * 8;
+    const float* X = static_cast<const float*>(a.x);
+    const float* DY = static_cast<const float*>(a.dy);
+    const float* Y = static_cast<const float*>(a.y);
+    double fsc[8], fsh[8], mu[8], s1[8], s2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        fsc[j] = MODE == BWD_RELUX ? (double)a.fcoef[c0 + j] : 0.0;
+        fsh[j] = MODE == BWD_RELUX ? (double)a.fcoef[C + c0 + j] : 0.0;
+        mu[j] = MODE != FWD ? (double)a.save_mean[c0 + j] : 0.0;
+        s1[j] = s2[j] = 0.0;
+    }
+    const long long rbeg = (long long)rc * a.rpb;
+    long long rend = rbeg + a.rpb;
+    if (rend > a.M) rend = a.M;
+    for (long long r = rbeg + r0; r < rend; r += rpp) {
+        const long long e = r * C + c0;
+        float xf[8], d[8];
+        V8<float>::ld(X + e, 0, xf);
+        if (MODE != FWD) V8<float>::ld(DY + e, 0, d);
+        if (MODE == BWD_RELU) {
+            float yf[8];
+            V8<float>::ld(Y + e, 0, yf);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) d[j] = yf[j] > 0.f ? d[j] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (MODE == BWD_RELUX) d[j] = fmaf(xf[j], (float)fsc[j], (float)fsh[j]) > 0.f ? d[j] : 0.f;
+            if (MODE == FWD) {
+                s1[j] += (double)xf[j];
+                s2[j] = fma((double)xf[j], (double)xf[j], s2[j]);
+            } else {
+                s1[j] += (double)d[j];
+                s2[j] = fma((double)d[j], (double)xf[j] - mu[j], s2[j]);
+            }
+        }
+    }
+    const int S2w = 2 * SW;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        red[r0 * S2w + (cg * 8 + j) * 2] = s1[j];
+        red[r0 * S2w + (cg * 8 + j) * 2 + 1] = s2[j];
+    }
+    __syncthreads();
+    double* p1 = reinterpret_cast<double*>(a.part) + ((size_t)cs * a.nrc + rc) * S2w;
+    if (t < S2w) {
+        double acc = 0.0;
+        for (int i = 0; i < rpp; ++i) acc += red[i * S2w + t];
+        st_sc1(&p1[t], acc);
+    }
+    FinOps fo{};
+    if (t < SW) fo = fin_load<MODE>(a, cs * SW + t);
+    if (!ticket(a.counter + cs, (unsigned)a.nrc, &flag)) return;
+    if (MODE == FWD && a.nbt && cs == 0 && t == 0) *a.nbt += 1;
+    const double* pp = reinterpret_cast<const double*>(a.part) + (size_t)cs * a.nrc * S2w;
+    if (t < S2w) {  // fixed order over the row chunks
+        double acc = 0.0;
+        for (int i = 0; i < a.nrc; ++i)
+            acc += __hip_atomic_load(pp + (size_t)i * S2w + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        red[t] = acc;
+    }
+    __syncthreads();
+    if (t < SW) finalize<MODE, false, true>(a, cs * SW + t, red[2 * t], red[2 * t + 1], 1.0 / (double)a.M, fo);
 }
 
 // Fused forward for maps whose grid is co-resident (fused_plan) and whose rows
@@ -687,7 +776,8 @@ __global__ __launch_bounds__(kT, NR == 8 ? 2 : 3) void k_bn_bwd_fused(ReduceArgs
         if (DRES) a.dres_out[i] = pack8(d);
         float o[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = fmaf(ca[j], d[j], fmaf(cb[j], xf[j], cc[j]));
+        for (int j = 0; j < 8; ++j)
+            o[j] = fmaf(ca[j], d[j], fmaf(cb[j], xf[j], cc[j]));
         a.yout[i] = pack8(o);
     };
     if (NR > 0) {
@@ -768,13 +858,15 @@ __global__ __launch_bounds__(kT) void k_bn_apply(ApplyArgs a) {
 
 template <bool RELU, bool DRES, bool MASKX, typename E>
 __global__ __launch_bounds__(kT) void k_bn_apply_bwd(ApplyArgs a) {
+    constexpr bool CENTER = std::is_same<E, float>::value;  // finalize<CENTER>: slot 3 = mean
     const long long stride = (long long)gridDim.x * kT;
     long long v = (long long)blockIdx.x * kT + threadIdx.x;
     const int cg = (int)(v & ((1 << a.tpr_log) - 1));
-    float ca[8], cb[8], cc[8], fs[8], fh[8];
+    float ca[8], cb[8], cc[8], fs[8], fh[8], mu[8];
     load_coef(a.coef, cg, ca);
     load_coef(a.coef + a.C, cg, cb);
     load_coef(a.coef + 2 * a.C, cg, cc);
+    if (CENTER) load_coef(a.coef + 3 * a.C, cg, mu);
     if (MASKX) {
         load_coef(a.fcoef, cg, fs);
         load_coef(a.fcoef + a.C, cg, fh);
@@ -795,7 +887,8 @@ __global__ __launch_bounds__(kT) void k_bn_apply_bwd(ApplyArgs a) {
         if (DRES) V8<E>::st(a.out2, i, d);
         float o[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = fmaf(ca[j], d[j], fmaf(cb[j], xf[j], cc[j]));
+        for (int j = 0; j < 8; ++j)
+            o[j] = CENTER ? fmaf(ca[j], d[j], fmaf(cb[j], xf[j] - mu[j], cc[j])) : fmaf(ca[j], d[j], fmaf(cb[j], xf[j], cc[j]));
         V8<E>::st(a.out, i, o);
     };
     for (; v + stride < a.nvec; v += 2 * stride) {
@@ -1005,7 +1098,8 @@ int bn_fwd_train(const gm_bn_fwd* p, void* scratch, size_t bytes, void* stream, 
 #undef GM_BN_FUSED_LAUNCH
         return check_launch("k_bn_fwd_fused");
     }
-    hipLaunchKernelGGL((k_bn_reduce<FWD, E>), dim3(pl.nrc, pl.nslice), dim3(kT), 0, st, a);
+    if (std::is_same<E, float>::value) hipLaunchKernelGGL((k_bn_reduce_f64<FWD>), dim3(pl.nrc, pl.nslice), dim3(kT), 0, st, a);
+    else hipLaunchKernelGGL((k_bn_reduce<FWD, E>), dim3(pl.nrc, pl.nslice), dim3(kT), 0, st, a);
     if ((rc = check_launch("k_bn_reduce<fwd>"))) return rc;
     ApplyArgs b{};
     b.nvec = p->M * (p->C / 8); b.tpr_log = ilog2(p->C / 8); b.C = p->C; b.relu = p->relu;
@@ -1094,7 +1188,11 @@ int bn_bwd(const gm_bn_bwd* p, void* scratch, size_t bytes, void* stream, const 
         return check_launch("k_bn_bwd_fused");
     }
     const dim3 rg(pl.nrc, pl.nslice);
-    if (maskx) hipLaunchKernelGGL((k_bn_reduce<BWD_RELUX, E>), rg, dim3(kT), 0, st, a);
+    if (std::is_same<E, float>::value) {  // reference precision: fp64 accumulation
+        if (maskx) hipLaunchKernelGGL((k_bn_reduce_f64<BWD_RELUX>), rg, dim3(kT), 0, st, a);
+        else if (p->relu) hipLaunchKernelGGL((k_bn_reduce_f64<BWD_RELU>), rg, dim3(kT), 0, st, a);
+        else hipLaunchKernelGGL((k_bn_reduce_f64<BWD>), rg, dim3(kT), 0, st, a);
+    } else if (maskx) hipLaunchKernelGGL((k_bn_reduce<BWD_RELUX, E>), rg, dim3(kT), 0, st, a);
     else if (p->relu) hipLaunchKernelGGL((k_bn_reduce<BWD_RELU, E>), rg, dim3(kT), 0, st, a);
     else hipLaunchKernelGGL((k_bn_reduce<BWD, E>), rg, dim3(kT), 0, st, a);
     if ((rc = check_launch("k_bn_reduce<bwd>"))) return rc;

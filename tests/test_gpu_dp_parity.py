@@ -42,7 +42,7 @@ def _gn_of(step, model, world):
     return np.array(out)
 
 
-def _worker_f32(rank, world, port, out_dir):
+def _worker_f32(rank, world, port, out_dir, case=None):
     import torch.distributed as dist
     from greedy_multimodal_learning_amd.engine import BalancedStep
     from greedy_multimodal_learning_amd.model import MMTM_MVCNN
@@ -54,8 +54,9 @@ def _worker_f32(rank, world, port, out_dir):
     # lr 0: every step sees the fixture's weights; graphs: step 1 eager, 2 captured + replayed, 3 replayed
     st = BalancedStep(m, lr=0.0, gate=None, compute_dtype=torch.float32, process_group=dist.group.WORLD,
                       bucket_mb=2.0, graphs=True, dp_buckets=True)
-    x, y = spec.model_inputs(spec.DDP)
-    lo = spec.DDP["B"] // world
+    case = case or spec.DDP
+    x, y = spec.model_inputs(case)
+    lo = case["B"] // world
     xs = torch.from_numpy(np.ascontiguousarray(x[rank * lo:(rank + 1) * lo])).to(dev)
     ys = torch.from_numpy(np.ascontiguousarray(y[rank * lo:(rank + 1) * lo])).to(dev)
     gns = []
@@ -70,19 +71,20 @@ def _worker_f32(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def _fp64_mean_of_shards():
+def _fp64_mean_of_shards(case=None):
     from oracle import gating_ref, model_ref, weights
-    x, y = spec.model_inputs(spec.DDP)
-    lo = spec.DDP["B"] // spec.DDP["world"]
+    case = case or spec.DDP
+    x, y = spec.model_inputs(case)
+    lo = case["B"] // case["world"]
     acc = None
-    for r in range(spec.DDP["world"]):
+    for r in range(case["world"]):
         o = weights.apply_to_module(model_ref.MMTM_MVCNN_Ref(), seed=spec.SEED_MODEL).double()
         o.train(True)
         _, outs, _, _ = o(torch.from_numpy(x[r * lo:(r + 1) * lo]).double())
         gating_ref.blend_loss(outs, torch.from_numpy(y[r * lo:(r + 1) * lo])).backward()
         g = {n: p.grad.clone() for n, p in o.named_parameters()}
         acc = g if acc is None else {n: acc[n] + g[n] for n in acc}
-    return {n: v / spec.DDP["world"] for n, v in acc.items()}
+    return {n: v / case["world"] for n, v in acc.items()}
 
 
 def test_dp_f32_hip_gradients_match_mean_of_shards(golden, tmp_path):
@@ -105,9 +107,36 @@ def test_dp_f32_hip_gradients_match_mean_of_shards(golden, tmp_path):
         e_gpu = np.abs(g0[i] - gn64) / gn64
         print(f"F4 fp32 DP ({label}): vs fixture max {e_fix.max():.2e} rms {np.sqrt((e_fix ** 2).mean()):.2e}; "
               f"vs fp64 max {e_gpu.max():.2e} (reference vs fp64 max {e_ref.max():.2e})")
-        # the reference's own fp32 run (the fixture) and this one both carry fp32 rounding
-        # of a BatchNorm over 2 values per channel at layer 4 (1x1 maps, B = 2 per shard)
-        assert e_fix.max() <= 2e-4 or e_gpu.max() <= max(4 * e_ref.max(), 2e-4), (label, e_fix.max(), e_gpu.max())
+        # F4 is ill-conditioned by construction: B = 2 per shard at 32x32 puts a BatchNorm
+        # over 2 values per channel at layer 4 (1x1 maps), whose gradient is mostly rounding
+        # - the reference's OWN fp32 run is 9.3e-2 off the fp64 mean of shards (measured).
+        # So this fixture pins the plumbing (shards, per-rank statistics, mean) within the
+        # envelope of the reference's own error; the well-conditioned case below pins the
+        # numbers.  Measured: 1.04e-1 vs fp64 (reference 9.32e-2).
+        assert e_gpu.max() <= max(2 * e_ref.max(), 2e-4), (label, e_fix.max(), e_gpu.max())
+
+
+DDP_WELL = dict(B=8, H=64, W=64, world=2, seed=21)  # 4 per shard, 64x64: layer-4 BN over 16 values
+
+
+def test_dp_f32_hip_gradients_well_conditioned(tmp_path):
+    """The same all-reduced fp32 HIP gradients on a well-conditioned shard size, against
+    the oracle's fp64 mean of per-shard gradients (the oracle is pinned to the
+    reference's fixtures at 1e-4: test_oracle_golden.py)."""
+    c = DDP_WELL
+    mp.start_processes(_worker_f32, args=(c["world"], _free_port(), str(tmp_path), c), nprocs=c["world"],
+                       join=True, start_method="spawn")
+    names = list(np.load(tmp_path / "names.npy"))
+    g0, g1 = np.load(tmp_path / "f32_gn_0.npy"), np.load(tmp_path / "f32_gn_1.npy")
+    np.testing.assert_array_equal(g0, g1)
+    g64 = _fp64_mean_of_shards(c)
+    gn64 = np.array([float((g64[n] ** 2).sum()) for n in names])
+    e = np.abs(g0 - gn64[None]) / gn64[None]
+    worst = names[int(np.argmax(e.max(0)))]
+    print(f"DP fp32 2x4 @64x64 vs fp64 mean of shards: max {e.max():.2e} rms {np.sqrt((e ** 2).mean()):.2e} "
+          f"(worst {worst})")
+    # measured m64 single-device: max 4e-6 vs fp64 (test_gpu_model.py)
+    assert e.max() < 1e-4
 
 
 def _worker_bf16(rank, world, port, out_dir, B, H):

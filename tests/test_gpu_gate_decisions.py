@@ -1,7 +1,8 @@
 """Decision-level parity of the BENCHMARKED gate: BalancedStep in bf16 at config C2
 (B = 64 two-view 224x224 objects, hipGraph replay, on-device gate) trained with
-training_guided.gin's gate (lr 0.1, epsilon 0.01, window 5, unlocked) for 20 steps,
-checked step by step against the fp32 oracle of the reference step
+training_guided.gin's gate (lr 0.1, epsilon 0.01, window 5, unlocked) for 36 steps
+(36 steps: with every decision opening a 5-step window, 6 deciding steps) checked step
+by step against the fp32 oracle of the reference step
 (/root/reference/src/callbacks.py:199-263, src/model.py:63-108, train.py:23-29).
 
 Teacher-forced: before every step whose gate computes d_BDR (unlocked, not inside a
@@ -21,8 +22,12 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-B, H, STEPS, EPS, WINDOW, LR = 64, 224, 20, 0.01, 5, 0.1
-BAND = 4e-3  # bf16-vs-fp32 d_BDR noise bound (see test_bf16_gate_decisions_vs_oracle)
+B, H, STEPS, EPS, WINDOW, LR = 64, 224, 36, 0.01, 5, 0.1
+# bf16-vs-fp32 d_BDR noise bound: d_BDR = sum of four log10(M) terms, so its error is at
+# most (1/ln 10) x the sum of the four gradient-sum relative errors; with the C2 test's
+# measured gradient-sum errors (9.8e-3, 6.0e-4, 1.7e-3, 2.0e-3; test_gpu_c2_bf16.py):
+# 0.434 x 1.41e-2 = 6.1e-3.  (Measured on MI355X: max 3.4e-3 over the deciding steps.)
+BAND = 6e-3
 
 
 @pytest.fixture(scope="module")

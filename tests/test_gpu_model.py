@@ -83,8 +83,12 @@ def test_model_vs_reference(golden, dev, case):
     names = [n for n, _ in m.named_parameters()]
     assert names == list(fix[p + "param_names"])
     o, mean64 = _fp64_oracle(case)
-    e_ref = _rel(fix[p + "logits"], mean64.numpy()).max()
-    e_gpu = _rel(mean.detach().cpu().double().numpy(), mean64.numpy()).max()
+    # logit errors relative to the logits' scale (an element-wise ratio is set by whichever
+    # logit happens to lie near zero)
+    sc64 = np.abs(mean64.numpy()).max()
+    e_ref = (np.abs(fix[p + "logits"] - mean64.numpy()) / sc64).max()
+    e_gpu = (np.abs(mean.detach().cpu().double().numpy() - mean64.numpy()) / sc64).max()
+    print(f"{case['id']}: logits vs fp64 (scale-relative) gpu {e_gpu:.2e} reference {e_ref:.2e}")
     assert e_gpu <= max(4 * e_ref, tol), (e_gpu, e_ref)
     g64 = {n: q.grad for n, q in o.named_parameters()}
     gn64 = np.array([float((g64[n] ** 2).sum()) if g64[n] is not None else 0.0 for n in names])
@@ -94,10 +98,19 @@ def test_model_vs_reference(golden, dev, case):
     e_ref, e_gpu = _rel(fix[p + "gn"][live], gn64[live]), _rel(gn[live], gn64[live])
     print(f"{case['id']}: grad-norm rel vs fp64 rms {np.sqrt((e_gpu ** 2).mean()):.2e} max {e_gpu.max():.2e} "
           f"(reference rms {np.sqrt((e_ref ** 2).mean()):.2e} max {e_ref.max():.2e})")
-    # Floors: the trunk's vendor BatchNorm/convolution kernels reduce in fp32 (the
-    # reference's CPU run accumulates BN in double); measured on 224x224 maps across
-    # MIOpen's fp32 algorithms: 3e-4 .. 1.4e-3 rms, <= 7e-3 max.  A wrong gradient
-    # formula shows up as O(1).
+    lnames = [n for n, f in zip(names, live) if f]
+    for i in np.argsort(-e_gpu)[:6]:
+        print(f"   {lnames[i]}: gpu {e_gpu[i]:.2e} reference {e_ref[i]:.2e}")
+    # Floors, measured on the HIP path (profiles/r03a_f32_precision_probe.txt,
+    # tools/f32_precision_probe.py): at 224x224 ONE ReLU output whose float64 value lies
+    # within fp32 rounding of zero flips its mask (m224: view 0, layer4.0's output, 1 of
+    # 25,088 elements; a BatchNorm over 49 values per channel spreads it over the
+    # channel), which moves every upstream gradient of that view by ~1.5e-3 relative L2
+    # while the forward stays at 3e-6.  The reference's own fp32 run has no flip on these
+    # inputs; any fp32 implementation flips or not by rounding luck.  Measured HIP maxima:
+    # m224b2 rms 1.4e-3, max 6.2e-3, samples 1.0e-2 (floors 2e-3 / 1e-2 / 2e-2); 64x64
+    # cases ~1e-6 like the reference.  BatchNorm reductions of this path accumulate in
+    # float64 as the reference's CPU BatchNorm does.  A wrong formula shows up as O(1).
     assert np.sqrt((e_gpu ** 2).mean()) <= max(3 * np.sqrt((e_ref ** 2).mean()), 2e-3), "grad-norm rms"
     assert e_gpu.max() <= max(10 * e_ref.max(), 1e-2), "grad-norm max"
     es_ref, es_gpu = [], []
@@ -114,7 +127,7 @@ def test_model_vs_reference(golden, dev, case):
             assert q.grad is None, n  # curated branch: no gradient, like the reference
     es_ref, es_gpu = np.concatenate(es_ref), np.concatenate(es_gpu)
     print(f"{case['id']}: grad samples rel vs fp64 max {es_gpu.max():.2e} (reference {es_ref.max():.2e})")
-    assert es_gpu.max() <= max(10 * es_ref.max(), 2e-2), "grad samples"  # vendor fp32 BN floor (see above)
+    assert es_gpu.max() <= max(10 * es_ref.max(), 2e-2), "grad samples"  # one-ReLU-flip floor (see above)
     if (p + "d_BDR") in fix.files:
         cb = Bias_Mitigation_Strong(epsilon=0.01, curation_windowsize=5,
                                     branchnames=["net_view_0", "net_view_1"])
@@ -208,7 +221,14 @@ def test_guided_trace_vs_reference(golden, dev):
     assert np.all(dev_gpu[:, 0] <= np.maximum(4 * dev_ref[:, 0], 3e-4 * np.abs(tr64[:, 0]))), (dev_gpu, dev_ref)
     assert np.all(dev_gpu[:, 1] <= np.maximum(4 * dev_ref[:, 1], 1.5e-3)), (dev_gpu, dev_ref)
     np.testing.assert_array_equal(rows[:, 2:4], ref[:, 2:4])
-    np.testing.assert_allclose(rows[:, 4:], ref[:, 4:], atol=1e-9)
+    # accuracies (argmax of the logits, B = 8): a sample whose top two logits lie within
+    # fp32 rounding of each other may flip in either fp32 run; judged against the float64
+    # trace: at most one sample (100 / B points) off per entry, and only where the
+    # reference's own fp32 run is off too or in at most 2 of the 36 entries
+    d_acc = np.abs(rows[:, 4:] - tr64[:, 4:])
+    d_ref = np.abs(ref[:, 4:] - tr64[:, 4:])
+    assert d_acc.max() <= 100.0 / t["B"] + 1e-9, d_acc
+    assert int(((d_acc > 1e-9) & (d_ref <= 1e-9)).sum()) <= 2, (rows[:, 4:], ref[:, 4:], tr64[:, 4:])
     # the trained model after 12 steps: eval logits, MMTM running averages and sampled
     # parameters, each within the envelope of the reference's own deviation from the
     # float64 run (floors: 1e-3 of the logits' scale, 1e-5 absolute, rtol 1e-3)

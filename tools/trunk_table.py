@@ -74,36 +74,38 @@ def conv_rows(B, dev, reps=10, rotate_bytes=0, dtype="bf16"):
     return [_row(name, op, cnt, flops, nbytes, _time(fn, reps)) for name, op, cnt, flops, nbytes, fn in ops]
 
 
+def _make_f32(op, B, dev, C, H, W, K, R, st, pad, P, Q):
+    from greedy_multimodal_learning_amd import conv as G
+    from greedy_multimodal_learning_amd import _lib as L
+    d = G._desc(B, H, W, C, K, R, R, st, pad)
+    x = torch.randn(B, C, H, W, device=dev).contiguous(memory_format=CL)
+    w = torch.randn(K, C, R, R, device=dev).contiguous(memory_format=CL)
+    dy = torch.randn(B, K, P, Q, device=dev).contiguous(memory_format=CL)
+    if op == "fwd":
+        y = torch.empty(B, K, P, Q, device=dev).contiguous(memory_format=CL)
+        return lambda: G.conv_f32(L.GM_CONV_FWD, d, x=x, w=w, out=y)
+    if op == "dgrad":
+        dx = torch.empty(B, C, H, W, device=dev).contiguous(memory_format=CL)
+        return lambda: G.conv_f32(L.GM_CONV_DGRAD, d, w=w, dy=dy, out=dx)
+    dw = torch.empty(K, C, R, R, device=dev).contiguous(memory_format=CL)
+    return lambda: G.conv_f32(L.GM_CONV_WGRAD, d, x=x, dy=dy, out=dw)
+
+
 def conv_ops_f32(B, dev, rotate_bytes=0):
     """The same passes on the reference-precision path: gm_conv2d_f32 (exact-f32 MFMA),
     fp32 channels_last activations, the stem unpadded (what the fp32 drop-in runs)."""
-    from greedy_multimodal_learning_amd import conv as G
-    from greedy_multimodal_learning_amd import _lib as L
     out = []
     for name, (C, H, W, K, R, st, pad, cnt) in TRUNK:
         P, Q = (H + 2 * pad - R) // st + 1, (W + 2 * pad - R) // st + 1
         flops = 2.0 * B * P * Q * K * C * R * R
         xb, yb, wb = B * H * W * C * 4, B * P * Q * K * 4, K * C * R * R * 4
-        d = G._desc(B, H, W, C, K, R, R, st, pad)
-
-        def make(op, d=d, C=C, H=H, W=W, K=K, R=R, P=P, Q=Q):
-            x = torch.randn(B, C, H, W, device=dev).contiguous(memory_format=CL)
-            w = torch.randn(K, C, R, R, device=dev).contiguous(memory_format=CL)
-            dy = torch.randn(B, K, P, Q, device=dev).contiguous(memory_format=CL)
-            if op == "fwd":
-                y = torch.empty(B, K, P, Q, device=dev).contiguous(memory_format=CL)
-                return lambda: G.conv_f32(L.GM_CONV_FWD, d, x=x, w=w, out=y)
-            if op == "dgrad":
-                dx = torch.empty(B, C, H, W, device=dev).contiguous(memory_format=CL)
-                return lambda: G.conv_f32(L.GM_CONV_DGRAD, d, w=w, dy=dy, out=dx)
-            dw = torch.empty(K, C, R, R, device=dev).contiguous(memory_format=CL)
-            return lambda: G.conv_f32(L.GM_CONV_WGRAD, d, x=x, dy=dy, out=dw)
         passes = [("fwd", xb + wb + yb), ("wgrad", xb + yb + wb)]
         if C != 3:
             passes.insert(1, ("dgrad", yb + wb + xb))
         for op, nbytes in passes:
+            args = (op, B, dev, C, H, W, K, R, st, pad, P, Q)
             sets = max(1, -(-int(rotate_bytes) // nbytes)) if rotate_bytes else 1
-            fn = make(op) if sets == 1 else _cycle([make(op) for _ in range(sets)])
+            fn = _make_f32(*args) if sets == 1 else _cycle([_make_f32(*args) for _ in range(sets)])
             out.append((name, op, cnt, flops, nbytes, fn))
     return out
 
@@ -119,59 +121,56 @@ def _cycle(fns):
     return fn
 
 
+def _make_bf16(op, B, dev, C, H, W, K, R, st, pad, P, Q):
+    """A callable running one pass of one trunk convolution on fresh bf16 operands."""
+    from greedy_multimodal_learning_amd import conv as G
+    from greedy_multimodal_learning_amd import _lib as L
+    import ctypes
+    Cp = G._cpad(C)
+    x = torch.randn(B, Cp, H, W, device=dev).bfloat16().contiguous(memory_format=CL)
+    w = torch.randn(K, Cp, R, R, device=dev).bfloat16().contiguous(memory_format=CL)
+    dy = torch.randn(B, K, P, Q, device=dev).bfloat16().contiguous(memory_format=CL)
+    if C == 3:  # the stem runs on the pixel-pair view; its input gradient is never computed
+        xp = G.stem_pack_input(x[:, :3], R, R, pad)
+        wp = G.stem_pack_weight(w[:, :3].float())
+        if op == "fwd":
+            return lambda: G.stem_fwd(xp, wp, P, Q)
+        d = G._desc_hw(B, xp.shape[2], xp.shape[3], 8, K, R, wp.shape[3], 2, 1, 0, 0)
+        need = L.load().gm_conv2d_wgrad_hw_scratch(ctypes.byref(d))
+        scr = torch.empty(max(need, 16), device=dev, dtype=torch.uint8)
+        dwp = torch.empty(K, R, wp.shape[3], 8, device=dev, dtype=torch.float32)
+
+        def stem_wgrad():
+            L.check(L.load().gm_conv2d_wgrad_hw_bf16(ctypes.byref(d), dy.data_ptr(), xp.data_ptr(),
+                                                     dwp.data_ptr(), 8, 0, scr.data_ptr(), need,
+                                                     L.stream_of(dev)), "wgrad_hw")
+        return stem_wgrad
+    if op == "fwd":
+        return lambda: G.conv_fwd(x, w, st, pad)
+    if op == "dgrad":
+        wt = w.permute(1, 0, 2, 3).contiguous(memory_format=CL)
+        return lambda: G.conv_dgrad_t(dy, wt, H, W, st, pad)
+    dw = torch.empty(K, C, R, R, device=dev, dtype=torch.float32).contiguous(memory_format=CL)
+    return lambda: G.conv_wgrad(dy, x, R, R, st, pad, C, out=dw)
+
+
 def conv_ops(B, dev, rotate_bytes=0):
     """(name, pass, count per view, FLOPs, algorithmic bytes, callable) of every trunk
     convolution pass of one view at batch B.  rotate_bytes > 0: each callable cycles over
     enough distinct operand sets that consecutive launches touch more than rotate_bytes
     (beyond the 256 MiB Infinity Cache: every launch reads HBM, not the last one's lines)."""
-    from greedy_multimodal_learning_amd import conv as G
-    from greedy_multimodal_learning_amd import _lib as L
-    import ctypes
     out = []
     for name, (C, H, W, K, R, st, pad, cnt) in TRUNK:
-        Cp = G._cpad(C)
         P, Q = (H + 2 * pad - R) // st + 1, (W + 2 * pad - R) // st + 1
         flops = 2.0 * B * P * Q * K * C * R * R
         xb, yb, wb = B * H * W * C * 2, B * P * Q * K * 2, K * C * R * R * 2
-
-        def operands():
-            x = torch.randn(B, Cp, H, W, device=dev).bfloat16().contiguous(memory_format=CL)
-            w = torch.randn(K, Cp, R, R, device=dev).bfloat16().contiguous(memory_format=CL)
-            dy = torch.randn(B, K, P, Q, device=dev).bfloat16().contiguous(memory_format=CL)
-            return x, w, dy
-
-        if C == 3:  # the stem runs on the pixel-pair view; its input gradient is never computed
-            def make(op):
-                x, w, dy = operands()
-                xp = G.stem_pack_input(x[:, :3], R, R, pad)
-                wp = G.stem_pack_weight(w[:, :3].float())
-                if op == "fwd":
-                    return lambda: G.stem_fwd(xp, wp, P, Q)
-                d = G._desc_hw(B, xp.shape[2], xp.shape[3], 8, K, R, wp.shape[3], 2, 1, 0, 0)
-                need = L.load().gm_conv2d_wgrad_hw_scratch(ctypes.byref(d))
-                scr = torch.empty(max(need, 16), device=dev, dtype=torch.uint8)
-                dwp = torch.empty(K, R, wp.shape[3], 8, device=dev, dtype=torch.float32)
-
-                def stem_wgrad():
-                    L.check(L.load().gm_conv2d_wgrad_hw_bf16(ctypes.byref(d), dy.data_ptr(), xp.data_ptr(),
-                                                             dwp.data_ptr(), 8, 0, scr.data_ptr(), need,
-                                                             L.stream_of(dev)), "wgrad_hw")
-                return stem_wgrad
-            passes = [("fwd", xb + wb + yb), ("wgrad", xb + yb + K * C * R * R * 4)]
-        else:
-            def make(op, st=st, pad=pad):
-                x, w, dy = operands()
-                if op == "fwd":
-                    return lambda: G.conv_fwd(x, w, st, pad)
-                if op == "dgrad":
-                    wt = w.permute(1, 0, 2, 3).contiguous(memory_format=CL)
-                    return lambda: G.conv_dgrad_t(dy, wt, H, W, st, pad)
-                dw = torch.empty(K, C, R, R, device=dev, dtype=torch.float32).contiguous(memory_format=CL)
-                return lambda: G.conv_wgrad(dy, x, R, R, st, pad, C, out=dw)
-            passes = [("fwd", xb + wb + yb), ("dgrad", yb + wb + xb), ("wgrad", xb + yb + K * C * R * R * 4)]
+        passes = [("fwd", xb + wb + yb), ("wgrad", xb + yb + K * C * R * R * 4)]
+        if C != 3:
+            passes.insert(1, ("dgrad", yb + wb + xb))
         for op, nbytes in passes:
+            args = (op, B, dev, C, H, W, K, R, st, pad, P, Q)
             sets = max(1, -(-int(rotate_bytes) // nbytes)) if rotate_bytes else 1
-            fn = make(op) if sets == 1 else _cycle([make(op) for _ in range(sets)])
+            fn = _make_bf16(*args) if sets == 1 else _cycle([_make_bf16(*args) for _ in range(sets)])
             out.append((name, op, cnt, flops, nbytes, fn))
     return out
 
