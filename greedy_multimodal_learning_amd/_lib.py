@@ -144,6 +144,15 @@ EXPORTS.update({
     "gm_conv2d_dgrad_add_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                                          c_void_p]),
     "gm_conv2d_wgrad_hw_scratch": (c_size_t, [c_void_p]),
+    # view groups: G views stacked along the batch, one weight per view
+    "gm_conv2d_fwd_grouped_bf16": (c_int, [c_void_p, c_int, c_void_p, c_void_p, ctypes.c_longlong, c_void_p,
+                                           c_void_p, c_size_t, c_void_p]),
+    "gm_conv2d_dgrad_grouped_bf16": (c_int, [c_void_p, c_int, c_void_p, c_void_p, ctypes.c_longlong, c_void_p,
+                                             c_void_p, c_void_p, c_size_t, c_void_p]),
+    "gm_conv2d_splitk_ws_bytes_grouped": (c_size_t, [c_void_p, c_int, c_int]),
+    "gm_conv2d_wgrad_grouped_scratch": (c_size_t, [c_void_p, c_int]),
+    "gm_conv2d_wgrad_grouped_bf16": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, ctypes.c_longlong,
+                                             c_int, c_int, c_void_p, c_size_t, c_void_p]),
     "gm_conv2d_wgrad_hw_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
                                         c_size_t, c_void_p]),
 })
@@ -198,6 +207,10 @@ EXPORTS.update({
     "gm_bn_scratch": (c_size_t, [ctypes.c_longlong, c_int]),
     "gm_bn_fwd_train_bf16": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "gm_bn_fwd_stats_bf16": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
+    "gm_bn_scratch_grouped": (c_size_t, [ctypes.c_longlong, c_int, c_int]),
+    "gm_bn_fwd_train_grouped_bf16": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_void_p]),
+    "gm_bn_bwd_grouped_bf16": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_void_p]),
+    "gm_bn_fwd_stats_grouped_bf16": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_void_p]),
     "gm_bn_fwd_infer_bf16": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "gm_bn_bwd_bf16": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
 })
@@ -211,6 +224,8 @@ class PoolDesc(ctypes.Structure):
 EXPORTS.update({
     "gm_maxpool2d_fwd_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "gm_bn_relu_maxpool2d_fwd_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "gm_bn_relu_maxpool2d_fwd_grouped_bf16": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                                      c_void_p]),
     "gm_maxpool2d_bwd_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
 })
 
@@ -302,6 +317,8 @@ EXPORTS.update({
 EXPORTS.update({
     "gm_conv_set_pipe": (c_int, [c_int]),
     "gm_conv_set_halo": (c_int, [c_int]),
+    "gm_conv_set_h9": (c_int, [c_int]),
+    "gm_conv_set_splitk": (c_int, [c_int]),
     "gm_conv_set_wgrad_wide": (c_int, [c_int]),
     "gm_conv_set_rw": (c_int, [c_int]),
     "gm_conv_set_stem": (c_int, [c_int]),

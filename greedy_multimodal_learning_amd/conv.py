@@ -195,8 +195,10 @@ def stem_pack_weight(weight):
     return wp.view(K, R, Sp, 8).permute(0, 3, 1, 2)
 
 
-def stem_pack(x, weight, pad):
-    """(stem_pack_input(x), stem_pack_weight(weight)) in one launch (gm_stem_pack_bf16)."""
+def stem_pack(x, weight, pad, xp=None, wp=None):
+    """(stem_pack_input(x), stem_pack_weight(weight)) in one launch (gm_stem_pack_bf16);
+    xp [N,Hp,Wp/2,8] / wp [K,R,Sp,8] bf16 dense outputs may be given (a view group's
+    slice of the stacked trunk's buffers)."""
     N, C0, H, W = x.shape
     K, _, R, S = weight.shape
     P, Q, Sp, Hp, Wp = _stem_geom(H, W, R, S, pad)
@@ -205,8 +207,13 @@ def stem_pack(x, weight, pad):
     w = weight.detach()
     if w.dtype != torch.float32 or not w.is_contiguous():
         w = w.float().contiguous()
-    xp = torch.empty(N, Hp, Wp // 2, 8, device=x.device, dtype=torch.bfloat16)
-    wp = torch.empty(K, R, Sp, 8, device=x.device, dtype=torch.bfloat16)
+    if xp is None:
+        xp = torch.empty(N, Hp, Wp // 2, 8, device=x.device, dtype=torch.bfloat16)
+    if wp is None:
+        wp = torch.empty(K, R, Sp, 8, device=x.device, dtype=torch.bfloat16)
+    if (tuple(xp.shape) != (N, Hp, Wp // 2, 8) or tuple(wp.shape) != (K, R, Sp, 8) or not xp.is_contiguous()
+            or not wp.is_contiguous()):
+        raise ValueError("stem_pack: output buffers must be dense [N,Hp,Wp/2,8] / [K,R,Sp,8]")
     p = L.StemPack(x.data_ptr(), L.GM_BF16 if x.dtype == torch.bfloat16 else L.GM_F32, N, C0, H, W, pad,
                    *x.stride(), Hp, Wp, xp.data_ptr(), w.data_ptr(), K, R, S, wp.data_ptr())
     L.check(L.load().gm_stem_pack_bf16(ctypes.byref(p), L.stream_of(x.device)), "gm_stem_pack_bf16")

@@ -92,6 +92,30 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
     return make_uint4(pack_bf2(f[0], f[1]), pack_bf2(f[2], f[3]), pack_bf2(f[4], f[5]), pack_bf2(f[6], f[7]));
 }
 
+// Per-view-group operands: a grouped launch (gm_bn_*_grouped_bf16) normalises G views
+// stacked along the batch, each with its own parameters, statistics and scratch, in one
+// grid (blockIdx.z = group); every kernel starts from group_args().
+constexpr int kMaxBnG = 4;
+struct BnGroup {
+    const void* x;
+    const void* dy;
+    const void* y;
+    const float* gamma;
+    const float* beta;
+    float* rmean;
+    float* rvar;
+    float* save_mean;
+    float* save_invstd;
+    float* dgamma;
+    float* dbeta;
+    long long* nbt;
+    float* coef_out;
+    const float* fcoef;
+    const uint4* res;
+    uint4* yout;
+    uint4* dres_out;
+};
+
 struct ReduceArgs {
     long long M;
     int C, tpr_log, relu, accumulate;
@@ -120,7 +144,30 @@ struct ReduceArgs {
     uint4* yout;         // fused fwd: output / fused bwd: dx
     uint4* dres_out;     // fused bwd: dres
     unsigned spin_limit; // fused: poll budget of the coefficient hand-off
+    unsigned long long scr_stride;  // bytes between the groups' coefficient + partial areas
+    unsigned hdr_words;             // words between the groups' ticket / generation headers
+    BnGroup grp[kMaxBnG];           // grp[blockIdx.z] replaces the per-group pointers above
 };
+
+// this block's group: its pointers and its slice of the scratch (tickets, coefficients,
+// partials, generation words)
+__device__ __forceinline__ ReduceArgs group_args(const ReduceArgs& a0) {
+    ReduceArgs a = a0;
+    const int g = blockIdx.z;
+    const BnGroup& q = a0.grp[g];
+    a.x = q.x; a.dy = q.dy; a.y = q.y;
+    a.gamma = q.gamma; a.beta = q.beta; a.rmean = q.rmean; a.rvar = q.rvar;
+    a.save_mean = q.save_mean; a.save_invstd = q.save_invstd;
+    a.dgamma = q.dgamma; a.dbeta = q.dbeta; a.nbt = q.nbt;
+    a.coef_out = q.coef_out; a.fcoef = q.fcoef;
+    a.res = q.res; a.yout = q.yout; a.dres_out = q.dres_out;
+    const unsigned long long off = (unsigned long long)g * a0.scr_stride;
+    a.counter = a0.counter + g * a0.hdr_words;
+    a.coef = reinterpret_cast<float*>(reinterpret_cast<char*>(a0.coef) + off);
+    a.part = reinterpret_cast<float*>(reinterpret_cast<char*>(a0.part) + off);
+    if (a0.gen) a.gen = a0.gen + g * a0.hdr_words;
+    return a;
+}
 
 // sticky fault word of this translation unit (gm_device_faults): a fused launch whose
 // coefficient hand-off timed out
@@ -324,7 +371,8 @@ __device__ __forceinline__ void combine_finalize(const ReduceArgs& a, int cs, fl
 // One launch: partial sums per (row chunk, channel slice) + one ticketed combine
 // per slice + per-channel finalize.
 template <int MODE, typename E>
-__global__ __launch_bounds__(kT) void k_bn_reduce(ReduceArgs a) {
+__global__ __launch_bounds__(kT) void k_bn_reduce(ReduceArgs a0) {
+    const ReduceArgs a = group_args(a0);
     __shared__ float red[kRedF + 4];  // the one LDS object: row-group partials, flag
     const int t = threadIdx.x;
     const int C = a.C, SW = a.SW;
@@ -446,7 +494,8 @@ __device__ __forceinline__ void combine_finalize(const ReduceArgs& a, int cs, fl
 // row-group combine, the per-block partials (sc1 stores, 8 B) and the last block's
 // combine; the centred backward coefficients (finalize<CENTER>).
 template <int MODE>
-__global__ __launch_bounds__(kT) void k_bn_reduce_f64(ReduceArgs a) {
+__global__ __launch_bounds__(kT) void k_bn_reduce_f64(ReduceArgs a0) {
+    const ReduceArgs a = group_args(a0);
     __shared__ double red[kRedF];  // rpp * 2 * SW == 4096 doubles
     __shared__ float flag;
     const int t = threadIdx.x;
@@ -531,7 +580,8 @@ __global__ __launch_bounds__(kT) void k_bn_reduce_f64(ReduceArgs a) {
 // its registers.  One launch and one read of x instead of two launches and two reads.
 
 template <bool RES, bool RELU, int NR>
-__global__ __launch_bounds__(kT, NR == 16 ? 2 : NR == 8 ? 3 : 4) void k_bn_fwd_fused(ReduceArgs a) {  // NR 0: streaming
+__global__ __launch_bounds__(kT, NR == 16 ? 2 : NR == 8 ? 3 : 4) void k_bn_fwd_fused(ReduceArgs a0) {  // NR 0: streaming
+    const ReduceArgs a = group_args(a0);
     __shared__ float red[kRedF + 4];
     const int t = threadIdx.x;
     const int C = a.C, SW = a.SW;
@@ -650,7 +700,8 @@ __global__ __launch_bounds__(kT, NR == 16 ? 2 : NR == 8 ? 3 : 4) void k_bn_fwd_f
 // strip in registers (NR 4 or 8) or re-reads it (NR 0), the slice's last block
 // publishes (a, b, c) and every block writes dx = a*dz + b*x + c (and dres = dz).
 template <int MODE, bool DRES, int NR>
-__global__ __launch_bounds__(kT, NR == 8 ? 2 : 3) void k_bn_bwd_fused(ReduceArgs a) {
+__global__ __launch_bounds__(kT, NR == 8 ? 2 : 3) void k_bn_bwd_fused(ReduceArgs a0) {
+    const ReduceArgs a = group_args(a0);
     __shared__ float red[kRedF + 4];
     const int t = threadIdx.x;
     const int C = a.C, SW = a.SW;
@@ -985,14 +1036,15 @@ int device_cus() {
     return cus;
 }
 
-inline int fused_plan(long long M, int C, Plan& pl, bool bwd = false) {
+inline int fused_plan(long long M, int C, Plan& pl, bool bwd = false, int G = 1) {
     if (g_fused_env == 0) return 0;
     // co-residency under the device residency plan (gm_set_residency): CUs held by
     // never-yielding kernels (RCCL) are not counted, and every process sharing the GPU
     // may run its own launches at once
     const Residency& rs = residency();
     const int cus = usable_cus(device_cus());
-    const int conc = (g_concurrency > rs.streams ? g_concurrency : rs.streams) * rs.sharers;
+    // a grouped launch (G views in one grid) holds G plans' worth of workgroups at once
+    const int conc = (g_concurrency > rs.streams ? g_concurrency : rs.streams) * rs.sharers * G;
     const Plan base = make_plan(M, C);
     const Occ& oc = occupancy();
     const int nrs[3] = {4, 8, 16};
@@ -1054,37 +1106,120 @@ extern "C" size_t gm_bn_scratch(long long M, int C) {
 
 namespace {
 
-template <typename E>
-int bn_fwd_train(const gm_bn_fwd* p, void* scratch, size_t bytes, void* stream, const char* fn) {
-    GM_REQUIRE(p && p->x && p->y && p->gamma && p->beta && p->save_mean && p->save_invstd, "%s: null argument", fn);
-    GM_REQUIRE(!p->running_mean == !p->running_var, "%s: running_mean/var both or neither", fn);
-    int rc = check_common(p->M, p->C, scratch, bytes, fn);
+// Grouped scratch layout (the gm_bn_*_grouped_bf16 calls; never mixed with ungrouped calls
+// on one buffer): kMaxBnG fixed 256-byte headers (each group's tickets and generation
+// words: they stay at the same place whatever the shape, so a ticket word is only ever
+// a ticket word and stays zero between calls), then per group its coefficients and
+// partials (no zero invariant) at a shape-dependent stride.
+constexpr size_t kGrpHdr = kMaxBnG * kHdr;
+inline size_t group_stride(long long M, int C) {
+    const Plan p = make_plan(M, C);
+    return (p.bytes - p.off_coef + 255) / 256 * 256;
+}
+inline size_t grouped_bytes(long long M, int C, int G) { return kGrpHdr + G * group_stride(M, C); }
+
+// the scratch pointers of a call: ungrouped layout (header, coefficients, partials) or
+// the grouped one above
+void set_scratch(ReduceArgs& a, const Plan& pl, char* s, bool grouped) {
+    a.counter = reinterpret_cast<unsigned*>(s);
+    if (grouped) {
+        a.coef = reinterpret_cast<float*>(s + kGrpHdr);
+        a.part = reinterpret_cast<float*>(s + kGrpHdr + (pl.off_p1 - pl.off_coef));
+        a.scr_stride = group_stride(a.M, a.C);
+        a.hdr_words = kHdr / sizeof(unsigned);
+    } else {
+        a.coef = reinterpret_cast<float*>(s + pl.off_coef);
+        a.part = reinterpret_cast<float*>(s + pl.off_p1);
+        a.scr_stride = 0;
+        a.hdr_words = 0;
+    }
+}
+
+// the G descriptors of a grouped call must agree on everything but their pointers
+int check_groups_fwd(const gm_bn_fwd* ps, int G, const char* fn) {
+    GM_REQUIRE(ps && G >= 1 && G <= kMaxBnG, "%s: 1..%d groups (got %d)", fn, kMaxBnG, G);
+    for (int g = 0; g < G; ++g) {
+        const gm_bn_fwd& p = ps[g], &q = ps[0];
+        GM_REQUIRE(p.x && p.gamma && p.beta && p.save_mean && p.save_invstd, "%s: null argument (group %d)", fn, g);
+        GM_REQUIRE(!p.running_mean == !p.running_var, "%s: running_mean/var both or neither", fn);
+        GM_REQUIRE(p.M == q.M && p.C == q.C && p.relu == q.relu && !p.residual == !q.residual &&
+                       !p.running_mean == !q.running_mean && !p.num_batches_tracked == !q.num_batches_tracked &&
+                       !p.coef_out == !q.coef_out && !p.y == !q.y && p.momentum == q.momentum && p.eps == q.eps,
+                   "%s: group %d differs from group 0 in shape or options", fn, g);
+    }
+    return GM_OK;
+}
+
+int check_groups_bwd(const gm_bn_bwd* ps, int G, const char* fn) {
+    GM_REQUIRE(ps && G >= 1 && G <= kMaxBnG, "%s: 1..%d groups (got %d)", fn, kMaxBnG, G);
+    for (int g = 0; g < G; ++g) {
+        const gm_bn_bwd& p = ps[g], &q = ps[0];
+        GM_REQUIRE(p.dy && p.x && p.gamma && p.save_mean && p.save_invstd && p.dx && p.dgamma && p.dbeta,
+                   "%s: null argument (group %d)", fn, g);
+        GM_REQUIRE(!p.relu || p.y || (p.fwd_coef && !p.dres),
+                   "%s: relu needs the forward output y (or fwd_coef, without a residual)", fn);
+        GM_REQUIRE(p.M == q.M && p.C == q.C && p.relu == q.relu && !p.y == !q.y && !p.dres == !q.dres &&
+                       !p.fwd_coef == !q.fwd_coef && p.accumulate == q.accumulate,
+                   "%s: group %d differs from group 0 in shape or options", fn, g);
+    }
+    return GM_OK;
+}
+
+int check_scratch(long long M, int C, int G, bool grouped, const void* scratch, size_t bytes, const char* fn) {
+    int rc = check_common(M, C, scratch, bytes, fn);
     if (rc) return rc;
+    const size_t need = grouped ? grouped_bytes(M, C, G) : scratch_bytes(M, C);
+    if (bytes < need) {
+        set_error("%s: scratch %zu bytes < required %zu for %d groups", fn, bytes, need, G);
+        return GM_E_SCRATCH;
+    }
+    return GM_OK;
+}
+
+// shared fields from group 0, per-group pointers into grp[], scratch split per group
+void fill_fwd(ReduceArgs& a, const gm_bn_fwd* ps, int G, bool grouped, const Plan& pl, char* s) {
+    const gm_bn_fwd* p = ps;
+    a.M = p->M; a.C = p->C; a.tpr_log = pl.tpr_log; a.rpb = pl.rpb;
+    a.SW = pl.SW; a.nrc = pl.nrc;
+    a.momentum = p->momentum; a.eps = p->eps;
+    set_scratch(a, pl, s, grouped);
+    for (int g = 0; g < G; ++g) {
+        BnGroup& q = a.grp[g];
+        q.x = ps[g].x;
+        q.gamma = ps[g].gamma; q.beta = ps[g].beta;
+        q.rmean = ps[g].running_mean; q.rvar = ps[g].running_var;
+        q.save_mean = ps[g].save_mean; q.save_invstd = ps[g].save_invstd;
+        q.nbt = ps[g].num_batches_tracked;
+        q.coef_out = ps[g].coef_out;
+        q.res = static_cast<const uint4*>(ps[g].residual);
+        q.yout = static_cast<uint4*>(ps[g].y);
+    }
+    BnGroup& q = a.grp[0];  // the single-group fields (host bookkeeping only: kernels read grp[])
+    a.x = q.x; a.gamma = q.gamma; a.beta = q.beta; a.rmean = q.rmean; a.rvar = q.rvar;
+    a.save_mean = q.save_mean; a.save_invstd = q.save_invstd; a.nbt = q.nbt; a.coef_out = q.coef_out;
+}
+
+template <typename E>
+int bn_fwd_train(const gm_bn_fwd* ps, int G, bool grouped, void* scratch, size_t bytes, void* stream,
+                 const char* fn) {
+    int rc = check_groups_fwd(ps, G, fn);
+    if (rc) return rc;
+    const gm_bn_fwd* p = ps;
+    GM_REQUIRE(p->y, "%s: null argument (y)", fn);
+    if ((rc = check_scratch(p->M, p->C, G, grouped, scratch, bytes, fn))) return rc;
     const Plan pl = make_plan(p->M, p->C);
     char* s = static_cast<char*>(scratch);
     ReduceArgs a{};
-    a.M = p->M; a.C = p->C; a.tpr_log = pl.tpr_log; a.rpb = pl.rpb;
-    a.SW = pl.SW; a.nrc = pl.nrc;
-    a.x = p->x;
-    a.gamma = p->gamma; a.beta = p->beta; a.rmean = p->running_mean; a.rvar = p->running_var;
-    a.momentum = p->momentum; a.eps = p->eps;
-    a.save_mean = p->save_mean; a.save_invstd = p->save_invstd;
-    a.nbt = p->num_batches_tracked;
-    a.coef_out = p->coef_out;
-    a.counter = reinterpret_cast<unsigned*>(s);
-    a.coef = reinterpret_cast<float*>(s + pl.off_coef);
-    a.part = reinterpret_cast<float*>(s + pl.off_p1);
+    fill_fwd(a, ps, G, grouped, pl, s);
     hipStream_t st = as_stream(stream);
     Plan fp;
-    const int nr = std::is_same<E, uint16_t>::value ? fused_plan(p->M, p->C, fp) : 0;
+    const int nr = std::is_same<E, uint16_t>::value ? fused_plan(p->M, p->C, fp, false, G) : 0;
     if (nr) {
         a.rpb = fp.rpb;
         a.nrc = fp.nrc;
         a.gen = reinterpret_cast<unsigned*>(s) + kGenOff;
         a.spin_limit = spin_limit();
-        a.res = static_cast<const uint4*>(p->residual);
-        a.yout = static_cast<uint4*>(p->y);
-        const dim3 g(fp.nrc, fp.nslice);
+        const dim3 g(fp.nrc, fp.nslice, G);
         const bool res = p->residual != nullptr, relu = p->relu != 0;
 #define GM_BN_FUSED_LAUNCH(NR)                                                                        \
     if (res && relu) hipLaunchKernelGGL((k_bn_fwd_fused<true, true, NR>), g, dim3(kT), 0, st, a);     \
@@ -1098,22 +1233,26 @@ int bn_fwd_train(const gm_bn_fwd* p, void* scratch, size_t bytes, void* stream, 
 #undef GM_BN_FUSED_LAUNCH
         return check_launch("k_bn_fwd_fused");
     }
-    if (std::is_same<E, float>::value) hipLaunchKernelGGL((k_bn_reduce_f64<FWD>), dim3(pl.nrc, pl.nslice), dim3(kT), 0, st, a);
-    else hipLaunchKernelGGL((k_bn_reduce<FWD, E>), dim3(pl.nrc, pl.nslice), dim3(kT), 0, st, a);
+    const dim3 rg(pl.nrc, pl.nslice, G);
+    if (std::is_same<E, float>::value) hipLaunchKernelGGL((k_bn_reduce_f64<FWD>), rg, dim3(kT), 0, st, a);
+    else hipLaunchKernelGGL((k_bn_reduce<FWD, E>), rg, dim3(kT), 0, st, a);
     if ((rc = check_launch("k_bn_reduce<fwd>"))) return rc;
-    ApplyArgs b{};
-    b.nvec = p->M * (p->C / 8); b.tpr_log = ilog2(p->C / 8); b.C = p->C; b.relu = p->relu;
-    b.x = p->x; b.res = p->residual; b.out = p->y;
-    b.coef = a.coef;
-    const int g = apply_grid(b.nvec, p->C);
-    if (p->residual) {
-        if (p->relu) hipLaunchKernelGGL((k_bn_apply<true, true, E>), dim3(g), dim3(kT), 0, st, b);
-        else hipLaunchKernelGGL((k_bn_apply<true, false, E>), dim3(g), dim3(kT), 0, st, b);
-    } else {
-        if (p->relu) hipLaunchKernelGGL((k_bn_apply<false, true, E>), dim3(g), dim3(kT), 0, st, b);
-        else hipLaunchKernelGGL((k_bn_apply<false, false, E>), dim3(g), dim3(kT), 0, st, b);
+    for (int gi = 0; gi < G; ++gi) {  // the apply: one launch per group
+        ApplyArgs b{};
+        b.nvec = p->M * (p->C / 8); b.tpr_log = ilog2(p->C / 8); b.C = p->C; b.relu = p->relu;
+        b.x = ps[gi].x; b.res = ps[gi].residual; b.out = ps[gi].y;
+        b.coef = reinterpret_cast<float*>(reinterpret_cast<char*>(a.coef) + gi * a.scr_stride);
+        const int g = apply_grid(b.nvec, p->C);
+        if (p->residual) {
+            if (p->relu) hipLaunchKernelGGL((k_bn_apply<true, true, E>), dim3(g), dim3(kT), 0, st, b);
+            else hipLaunchKernelGGL((k_bn_apply<true, false, E>), dim3(g), dim3(kT), 0, st, b);
+        } else {
+            if (p->relu) hipLaunchKernelGGL((k_bn_apply<false, true, E>), dim3(g), dim3(kT), 0, st, b);
+            else hipLaunchKernelGGL((k_bn_apply<false, false, E>), dim3(g), dim3(kT), 0, st, b);
+        }
+        if ((rc = check_launch("k_bn_apply"))) return rc;
     }
-    return check_launch("k_bn_apply");
+    return GM_OK;
 }
 
 template <typename E>
@@ -1143,39 +1282,40 @@ int bn_fwd_infer(const gm_bn_fwd* p, void* scratch, size_t bytes, void* stream, 
 }
 
 template <typename E>
-int bn_bwd(const gm_bn_bwd* p, void* scratch, size_t bytes, void* stream, const char* fn) {
-    GM_REQUIRE(p && p->dy && p->x && p->gamma && p->save_mean && p->save_invstd && p->dx && p->dgamma && p->dbeta,
-               "%s: null argument", fn);
-    GM_REQUIRE(!p->relu || p->y || (p->fwd_coef && !p->dres),
-               "%s: relu needs the forward output y (or fwd_coef, without a residual)", fn);
-    const bool maskx = p->relu && !p->y;
-    int rc = check_common(p->M, p->C, scratch, bytes, fn);
+int bn_bwd(const gm_bn_bwd* ps, int G, bool grouped, void* scratch, size_t bytes, void* stream, const char* fn) {
+    int rc = check_groups_bwd(ps, G, fn);
     if (rc) return rc;
+    const gm_bn_bwd* p = ps;
+    const bool maskx = p->relu && !p->y;
+    if ((rc = check_scratch(p->M, p->C, G, grouped, scratch, bytes, fn))) return rc;
     const Plan pl = make_plan(p->M, p->C);
     char* s = static_cast<char*>(scratch);
     ReduceArgs a{};
     a.M = p->M; a.C = p->C; a.tpr_log = pl.tpr_log; a.rpb = pl.rpb; a.relu = p->relu;
     a.SW = pl.SW; a.nrc = pl.nrc;
     a.accumulate = p->accumulate;
-    a.x = p->x; a.dy = p->dy; a.y = p->y;
-    a.gamma = p->gamma;
-    a.save_mean = const_cast<float*>(p->save_mean); a.save_invstd = const_cast<float*>(p->save_invstd);
-    a.dgamma = p->dgamma; a.dbeta = p->dbeta;
-    a.fcoef = p->fwd_coef;
-    a.counter = reinterpret_cast<unsigned*>(s);
-    a.coef = reinterpret_cast<float*>(s + pl.off_coef);
-    a.part = reinterpret_cast<float*>(s + pl.off_p1);
+    set_scratch(a, pl, s, grouped);
+    for (int g = 0; g < G; ++g) {
+        BnGroup& q = a.grp[g];
+        q.x = ps[g].x; q.dy = ps[g].dy; q.y = ps[g].y;
+        q.gamma = ps[g].gamma;
+        q.save_mean = const_cast<float*>(ps[g].save_mean);
+        q.save_invstd = const_cast<float*>(ps[g].save_invstd);
+        q.dgamma = ps[g].dgamma; q.dbeta = ps[g].dbeta;
+        q.fcoef = ps[g].fwd_coef;
+        q.yout = static_cast<uint4*>(ps[g].dx);
+        q.dres_out = static_cast<uint4*>(ps[g].dres);
+    }
     hipStream_t st = as_stream(stream);
     Plan fp;
-    const int nr = (std::is_same<E, uint16_t>::value && (!p->dres || p->relu)) ? fused_plan(p->M, p->C, fp, true) : 0;
+    const int nr = (std::is_same<E, uint16_t>::value && (!p->dres || p->relu)) ? fused_plan(p->M, p->C, fp, true, G)
+                                                                               : 0;
     if (nr) {
         a.rpb = fp.rpb;
         a.nrc = fp.nrc;
         a.gen = reinterpret_cast<unsigned*>(s) + kGenOff;
         a.spin_limit = spin_limit();
-        a.yout = static_cast<uint4*>(p->dx);
-        a.dres_out = static_cast<uint4*>(p->dres);
-        const dim3 g(fp.nrc, fp.nslice);
+        const dim3 g(fp.nrc, fp.nslice, G);
 #define GM_BN_BWD_FUSED_LAUNCH(NR)                                                                           \
     if (maskx) hipLaunchKernelGGL((k_bn_bwd_fused<BWD_RELUX, false, NR>), g, dim3(kT), 0, st, a);            \
     else if (p->relu && p->dres) hipLaunchKernelGGL((k_bn_bwd_fused<BWD_RELU, true, NR>), g, dim3(kT), 0, st, a); \
@@ -1187,7 +1327,7 @@ int bn_bwd(const gm_bn_bwd* p, void* scratch, size_t bytes, void* stream, const 
 #undef GM_BN_BWD_FUSED_LAUNCH
         return check_launch("k_bn_bwd_fused");
     }
-    const dim3 rg(pl.nrc, pl.nslice);
+    const dim3 rg(pl.nrc, pl.nslice, G);
     if (std::is_same<E, float>::value) {  // reference precision: fp64 accumulation
         if (maskx) hipLaunchKernelGGL((k_bn_reduce_f64<BWD_RELUX>), rg, dim3(kT), 0, st, a);
         else if (p->relu) hipLaunchKernelGGL((k_bn_reduce_f64<BWD_RELU>), rg, dim3(kT), 0, st, a);
@@ -1196,22 +1336,41 @@ int bn_bwd(const gm_bn_bwd* p, void* scratch, size_t bytes, void* stream, const 
     else if (p->relu) hipLaunchKernelGGL((k_bn_reduce<BWD_RELU, E>), rg, dim3(kT), 0, st, a);
     else hipLaunchKernelGGL((k_bn_reduce<BWD, E>), rg, dim3(kT), 0, st, a);
     if ((rc = check_launch("k_bn_reduce<bwd>"))) return rc;
-    ApplyArgs b{};
-    b.nvec = p->M * (p->C / 8); b.tpr_log = ilog2(p->C / 8); b.C = p->C; b.relu = p->relu;
-    b.x = p->x; b.res = p->y; b.dy = p->dy; b.out = p->dx;
-    b.out2 = p->dres; b.coef = a.coef;
-    b.fcoef = p->fwd_coef;
-    const int g = apply_grid(b.nvec, p->C);
-    if (maskx) {
-        hipLaunchKernelGGL((k_bn_apply_bwd<true, false, true, E>), dim3(g), dim3(kT), 0, st, b);
-    } else if (p->relu) {
-        if (p->dres) hipLaunchKernelGGL((k_bn_apply_bwd<true, true, false, E>), dim3(g), dim3(kT), 0, st, b);
-        else hipLaunchKernelGGL((k_bn_apply_bwd<true, false, false, E>), dim3(g), dim3(kT), 0, st, b);
-    } else {
-        if (p->dres) hipLaunchKernelGGL((k_bn_apply_bwd<false, true, false, E>), dim3(g), dim3(kT), 0, st, b);
-        else hipLaunchKernelGGL((k_bn_apply_bwd<false, false, false, E>), dim3(g), dim3(kT), 0, st, b);
+    for (int gi = 0; gi < G; ++gi) {  // the apply: one launch per group
+        const gm_bn_bwd* q = ps + gi;
+        ApplyArgs b{};
+        b.nvec = p->M * (p->C / 8); b.tpr_log = ilog2(p->C / 8); b.C = p->C; b.relu = p->relu;
+        b.x = q->x; b.res = q->y; b.dy = q->dy; b.out = q->dx;
+        b.out2 = q->dres;
+        b.coef = reinterpret_cast<float*>(reinterpret_cast<char*>(a.coef) + gi * a.scr_stride);
+        b.fcoef = q->fwd_coef;
+        const int g = apply_grid(b.nvec, p->C);
+        if (maskx) {
+            hipLaunchKernelGGL((k_bn_apply_bwd<true, false, true, E>), dim3(g), dim3(kT), 0, st, b);
+        } else if (p->relu) {
+            if (p->dres) hipLaunchKernelGGL((k_bn_apply_bwd<true, true, false, E>), dim3(g), dim3(kT), 0, st, b);
+            else hipLaunchKernelGGL((k_bn_apply_bwd<true, false, false, E>), dim3(g), dim3(kT), 0, st, b);
+        } else {
+            if (p->dres) hipLaunchKernelGGL((k_bn_apply_bwd<false, true, false, E>), dim3(g), dim3(kT), 0, st, b);
+            else hipLaunchKernelGGL((k_bn_apply_bwd<false, false, false, E>), dim3(g), dim3(kT), 0, st, b);
+        }
+        if ((rc = check_launch("k_bn_apply_bwd"))) return rc;
     }
-    return check_launch("k_bn_apply_bwd");
+    return GM_OK;
+}
+
+int bn_fwd_stats(const gm_bn_fwd* ps, int G, bool grouped, void* scratch, size_t bytes, void* stream,
+                 const char* fn) {
+    int rc = check_groups_fwd(ps, G, fn);
+    if (rc) return rc;
+    const gm_bn_fwd* p = ps;
+    GM_REQUIRE(p->coef_out, "%s: coef_out required", fn);
+    if ((rc = check_scratch(p->M, p->C, G, grouped, scratch, bytes, fn))) return rc;
+    const Plan pl = make_plan(p->M, p->C);
+    ReduceArgs a{};
+    fill_fwd(a, ps, G, grouped, pl, static_cast<char*>(scratch));
+    hipLaunchKernelGGL((k_bn_reduce<FWD, uint16_t>), dim3(pl.nrc, pl.nslice, G), dim3(kT), 0, as_stream(stream), a);
+    return check_launch("k_bn_reduce<fwd>");
 }
 
 }  // namespace
@@ -1244,45 +1403,39 @@ extern "C" int gm_bn_set_fused_mode(int mode) {
 // running statistics, num_batches_tracked and the affine coefficients in coef_out
 // (required); no y.  The apply is fused into the consumer (gm_bn_relu_maxpool2d_fwd_bf16).
 extern "C" int gm_bn_fwd_stats_bf16(const gm_bn_fwd* p, void* scratch, size_t bytes, void* stream) {
-    const char* fn = "gm_bn_fwd_stats_bf16";
-    GM_REQUIRE(p && p->x && p->gamma && p->beta && p->save_mean && p->save_invstd && p->coef_out,
-               "%s: null argument (coef_out required)", fn);
-    GM_REQUIRE(!p->running_mean == !p->running_var, "%s: running_mean/var both or neither", fn);
-    int rc = check_common(p->M, p->C, scratch, bytes, fn);
-    if (rc) return rc;
-    const Plan pl = make_plan(p->M, p->C);
-    char* s = static_cast<char*>(scratch);
-    ReduceArgs a{};
-    a.M = p->M; a.C = p->C; a.tpr_log = pl.tpr_log; a.rpb = pl.rpb;
-    a.SW = pl.SW; a.nrc = pl.nrc;
-    a.x = p->x;
-    a.gamma = p->gamma; a.beta = p->beta; a.rmean = p->running_mean; a.rvar = p->running_var;
-    a.momentum = p->momentum; a.eps = p->eps;
-    a.save_mean = p->save_mean; a.save_invstd = p->save_invstd;
-    a.nbt = p->num_batches_tracked;
-    a.coef_out = p->coef_out;
-    a.counter = reinterpret_cast<unsigned*>(s);
-    a.coef = reinterpret_cast<float*>(s + pl.off_coef);
-    a.part = reinterpret_cast<float*>(s + pl.off_p1);
-    hipLaunchKernelGGL((k_bn_reduce<FWD, uint16_t>), dim3(pl.nrc, pl.nslice), dim3(kT), 0, as_stream(stream), a);
-    return check_launch("k_bn_reduce<fwd>");
+    return bn_fwd_stats(p, 1, false, scratch, bytes, stream, "gm_bn_fwd_stats_bf16");
+}
+
+extern "C" size_t gm_bn_scratch_grouped(long long M, int C, int G) {
+    if (M <= 0 || C < 8 || C > kMaxC || G < 1 || G > kMaxBnG) return 0;
+    return grouped_bytes(M, C, G);
+}
+
+extern "C" int gm_bn_fwd_train_grouped_bf16(const gm_bn_fwd* ps, int G, void* scratch, size_t bytes, void* stream) {
+    return bn_fwd_train<uint16_t>(ps, G, true, scratch, bytes, stream, "gm_bn_fwd_train_grouped_bf16");
+}
+extern "C" int gm_bn_bwd_grouped_bf16(const gm_bn_bwd* ps, int G, void* scratch, size_t bytes, void* stream) {
+    return bn_bwd<uint16_t>(ps, G, true, scratch, bytes, stream, "gm_bn_bwd_grouped_bf16");
+}
+extern "C" int gm_bn_fwd_stats_grouped_bf16(const gm_bn_fwd* ps, int G, void* scratch, size_t bytes, void* stream) {
+    return bn_fwd_stats(ps, G, true, scratch, bytes, stream, "gm_bn_fwd_stats_grouped_bf16");
 }
 
 extern "C" int gm_bn_fwd_train_bf16(const gm_bn_fwd* p, void* scratch, size_t bytes, void* stream) {
-    return bn_fwd_train<uint16_t>(p, scratch, bytes, stream, "gm_bn_fwd_train_bf16");
+    return bn_fwd_train<uint16_t>(p, 1, false, scratch, bytes, stream, "gm_bn_fwd_train_bf16");
 }
 extern "C" int gm_bn_fwd_infer_bf16(const gm_bn_fwd* p, void* scratch, size_t bytes, void* stream) {
     return bn_fwd_infer<uint16_t>(p, scratch, bytes, stream, "gm_bn_fwd_infer_bf16");
 }
 extern "C" int gm_bn_bwd_bf16(const gm_bn_bwd* p, void* scratch, size_t bytes, void* stream) {
-    return bn_bwd<uint16_t>(p, scratch, bytes, stream, "gm_bn_bwd_bf16");
+    return bn_bwd<uint16_t>(p, 1, false, scratch, bytes, stream, "gm_bn_bwd_bf16");
 }
 extern "C" int gm_bn_fwd_train_f32(const gm_bn_fwd* p, void* scratch, size_t bytes, void* stream) {
-    return bn_fwd_train<float>(p, scratch, bytes, stream, "gm_bn_fwd_train_f32");
+    return bn_fwd_train<float>(p, 1, false, scratch, bytes, stream, "gm_bn_fwd_train_f32");
 }
 extern "C" int gm_bn_fwd_infer_f32(const gm_bn_fwd* p, void* scratch, size_t bytes, void* stream) {
     return bn_fwd_infer<float>(p, scratch, bytes, stream, "gm_bn_fwd_infer_f32");
 }
 extern "C" int gm_bn_bwd_f32(const gm_bn_bwd* p, void* scratch, size_t bytes, void* stream) {
-    return bn_bwd<float>(p, scratch, bytes, stream, "gm_bn_bwd_f32");
+    return bn_bwd<float>(p, 1, false, scratch, bytes, stream, "gm_bn_bwd_f32");
 }

@@ -74,6 +74,11 @@ struct ConvArgs {
     float* ws;                // [tiles][MT*NT*16/4][256] float4
     unsigned* flags;          // [tiles]
     unsigned spin_limit;      // poll budget of the turnstile wait
+    // view groups in one launch (the view-batched trunk): group g's input, weights and output
+    // (and addend) sit gs_in / gs_wt / gs_out elements after group 0's; tiled kernels give
+    // group g the tiles [g * tiles_g, (g + 1) * tiles_g), persistent ones gridDim / G workgroups
+    int G, tiles_g;
+    long long gs_in, gs_wt, gs_out;
     ConvCls cls[kMaxCls];
 };
 
@@ -118,11 +123,13 @@ __device__ __forceinline__ unsigned span_mask(int x, int d0, int s, int n, int l
 // addend loads are all in flight together instead of one dependent round trip per store.
 template <int MT, int NT, int BM, int BN>
 __device__ __forceinline__ void store_tile(const ConvArgs& a, const ConvCls& cl, int m0, int n0, int wm, int wn,
-                                           int fr, int fh, int M, floatx16 (&acc)[MT][NT]) {
+                                           int fr, int fh, int M, floatx16 (&acc)[MT][NT], long long goff = 0) {
     const int PQ = cl.P * cl.Q;
+    uint16_t* const outp = cl.out + goff;  // this group's output (and addend)
+    const uint16_t* const addp = a.addend ? a.addend + goff : nullptr;
     const size_t out_bytes = (size_t)a.N * a.Ho * a.Wo * a.Nout * 2;
     if (out_bytes < 0x7ffff000u) {
-        const auto orsrc = __builtin_amdgcn_make_buffer_rsrc(cl.out, 0, (int)out_bytes, 0x00020000);
+        const auto orsrc = __builtin_amdgcn_make_buffer_rsrc(outp, 0, (int)out_bytes, 0x00020000);
         unsigned off[MT];
         bool mok[MT];
 #pragma unroll
@@ -142,7 +149,7 @@ __device__ __forceinline__ void store_tile(const ConvArgs& a, const ConvCls& cl,
         typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
         u32x2 av[MT][NT][4];
         if (a.addend) {
-            const auto arsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.addend), 0, (int)out_bytes,
+            const auto arsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(addp), 0, (int)out_bytes,
                                                                  0x00020000);
 #pragma unroll
             for (int i = 0; i < MT; ++i)
@@ -176,7 +183,7 @@ __device__ __forceinline__ void store_tile(const ConvArgs& a, const ConvCls& cl,
         const int b = (int)cl.fd_pq.div((uint32_t)m), pq = m - b * PQ;
         const int p = (int)cl.fd_q.div((uint32_t)pq), q = pq - p * cl.Q;
         const int ho = p * cl.oS + cl.oH, wo = q * cl.oS + cl.oW;
-        uint16_t* dst = cl.out + ((size_t)(b * a.Ho + ho) * a.Wo + wo) * a.Nout;
+        uint16_t* dst = outp + ((size_t)(b * a.Ho + ho) * a.Wo + wo) * a.Nout;
 #pragma unroll
         for (int j = 0; j < NT; ++j)
 #pragma unroll
@@ -186,7 +193,7 @@ __device__ __forceinline__ void store_tile(const ConvArgs& a, const ConvCls& cl,
                 float o0 = acc[i][j][4 * gq], o1 = acc[i][j][4 * gq + 1];
                 float o2 = acc[i][j][4 * gq + 2], o3 = acc[i][j][4 * gq + 3];
                 if (a.addend) {
-                    const uint2 av = *(const uint2*)(a.addend + (dst - cl.out) + n);
+                    const uint2 av = *(const uint2*)(addp + (dst - outp) + n);
                     o0 += bf_lo(av.x); o1 += bf_hi(av.x); o2 += bf_lo(av.y); o3 += bf_hi(av.y);
                 }
                 uint2 v;
@@ -422,6 +429,14 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
         split = bid / a.tiles_total;
         bid -= split * a.tiles_total;
     }
+    const int tid = bid;  // launch-wide tile index: split-K slab and turnstile word
+    int g = 0;            // view group
+    if (a.G > 1) {
+        g = bid / a.tiles_g;
+        bid -= g * a.tiles_g;
+    }
+    const uint16_t* const gin = a.in + g * a.gs_in;
+    const uint16_t* const gwt = a.wt + g * a.gs_wt;
     int ci = 0;
 #pragma unroll
     for (int q = 1; q < kMaxCls; ++q)
@@ -469,7 +484,7 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
         const bool in = m < M;
         a_vr[j] = in ? vr : 0u;
         a_vs[j] = vs;
-        a_ptr[j] = a.in + (in ? ((size_t)((b * a.Hi + h) * a.Wi + w) << a.logC) : 0) + gc * 8;
+        a_ptr[j] = gin + (in ? ((size_t)((b * a.Hi + h) * a.Wi + w) << a.logC) : 0) + gc * 8;
     }
     const uint16_t* b_ptr[BR];
     bool b_ok[BR];
@@ -479,7 +494,7 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
         const int n = n0 + row;
         const int gc = slot ^ ((row >> 1) & 7);
         b_ok[j] = n < a.Nout;
-        b_ptr[j] = a.wt + (size_t)(b_ok[j] ? n : 0) * a.T * a.C + gc * 8;
+        b_ptr[j] = gwt + (size_t)(b_ok[j] ? n : 0) * a.T * a.C + gc * 8;
     }
     // per-lane fragment byte offsets inside a stage: row*128 + swizzled 16-B chunk
     const int fr = lane & 31, fh = lane >> 5;
@@ -622,13 +637,13 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
 
     if (a.splits > 1) {
         constexpr int NQ = MT * NT * 4;  // float4 groups of accumulators per lane
-        const auto rs = rsrc_of(a.ws + (size_t)bid * NQ * 256 * 4);
+        const auto rs = rsrc_of(a.ws + (size_t)tid * NQ * 256 * 4);
         if (split > 0) {  // wait for the previous split's running sum, then add it
             __shared__ int late;
             if (t == 0) {  // bounded: a broken hand-off never hangs, it faults loudly
                 unsigned n = 0;
                 bool ok = true;
-                while (__hip_atomic_load(a.flags + bid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
+                while (__hip_atomic_load(a.flags + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
                        (unsigned)split) {
                     if (++n >= a.spin_limit) {
                         ok = false;
@@ -673,14 +688,14 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
                                                  acc[i][j][4 * g + 3]));
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-            if (t == 0) __hip_atomic_store(a.flags + bid, (unsigned)(split + 1), __ATOMIC_RELAXED,
+            if (t == 0) __hip_atomic_store(a.flags + tid, (unsigned)(split + 1), __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
             return;
         }
-        if (t == 0) __hip_atomic_store(a.flags + bid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == 0) __hip_atomic_store(a.flags + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 
-    store_tile<MT, NT, BM, BN>(a, cl, m0, n0, wm, wn, fr, fh, M, acc);
+    store_tile<MT, NT, BM, BN>(a, cl, m0, n0, wm, wn, fr, fh, M, acc, g * a.gs_out);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1013,6 +1028,316 @@ __global__ __launch_bounds__(BM == 256 ? 512 : 256) void k_conv_halo(ConvArgs a,
 }
 
 // ---------------------------------------------------------------------------------
+// k_conv_h9: the halo-staged 3x3 / stride-1 convolution (forward and stride-1 input
+// gradient, C a multiple of 64) with its nine taps UNROLLED.  k_conv_halo decodes the
+// tap of every k-tile at run time (k / 9, tap / 3, packed-field shifts, the ring stage
+// modulo, per-DMA pointer selects): ~45 scalar and ~40 vector instructions per 16 MFMAs
+// per wave, which at two waves per SIMD issue-bind the loop (ISA census, round 3).  Here
+// the k-loop runs over 64-channel chunks with the nine taps as compile-time steps, so
+//   * the weight-ring stage of a tap is tap % 3 (nine is a multiple of the ring depth):
+//     the B fragment addresses are precomputed lane offsets + an immediate;
+//   * each tap's halo offset and weight tap index are decoded ONCE per workgroup (the A
+//     fragment address of tap t / fragment i is a precomputed VGPR);
+//   * the halo pixel decode (two fast divides per DMA instruction) is done once per tile,
+//     not once per channel chunk; chunks only add their channel base;
+//   * weights are DMA'd without per-lane bounds selects (Nout % BN == 0 is required).
+// Split-K splits whole channel chunks (splits <= C / 64) and hands the fp32 running sum
+// on through the same turnstile as k_conv_halo.  One workgroup = 128 output pixels x BN
+// channels, 4 waves of 64x64 (v_mfma_f32_32x32x16_bf16), two workgroups per CU.
+constexpr int kH9MaxQ = 12;  // halo DMA instructions per wave (nI <= 48)
+
+// NB: weight-ring stages (NB - 2 stay in flight across a k-tile); DIAG (timing
+// diagnostics, outputs meaningless): 1 = no weight DMA in the k-loop, 2 = no MFMAs /
+// fragment reads, 3 = no barrier in the k-loop, 4 = no halo reload
+template <int BN, int NB, int DIAG = 0>
+__global__ __launch_bounds__(256, 2) void k_conv_h9(ConvArgs a, HaloArgs h) {
+    constexpr int BM = 128, MT = 2, NT = BN / 64, NW = 4;
+    static_assert(NB >= 2 && NB <= 8, "ring depth");
+    constexpr int BR = BN / (8 * NW);  // weight DMA instructions per wave per k-tile
+    constexpr int SB = BN * 128;       // bytes of one ring stage
+    extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+    char* lds = reinterpret_cast<char*>(smem);  // [halo][B0]..[B(NB-1)]
+    const int HB = h.halo_bytes;
+
+    int bid = blockIdx.x;
+    int split = 0;
+    if (a.splits > 1) {
+        split = bid / a.tiles_total;
+        bid -= split * a.tiles_total;
+    }
+    const int tid = bid;  // launch-wide tile index: split-K slab and turnstile word
+    int g = 0;            // view group
+    if (a.G > 1) {
+        g = bid / a.tiles_g;
+        bid -= g * a.tiles_g;
+    }
+    const uint16_t* const gin = a.in + g * a.gs_in;
+    const uint16_t* const gwt = a.wt + g * a.gs_wt;
+    const ConvCls& cl = a.cls[0];
+    const int tiles_n = a.Nout / BN;
+    const int tm = bid / tiles_n, tn = bid - tm * tiles_n;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int H = a.Hi, W = a.Wi, W2 = W + 2, H1 = H + 1;
+    const int PQ = cl.P * cl.Q;
+    const int M = a.N * PQ;
+    const int nch = a.C >> 6;
+    const int c0 = split * nch / a.splits, c1 = (split + 1) * nch / a.splits;
+
+    const int t = threadIdx.x;
+    const int lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int slot = lane & 7;
+    const int fr = lane & 31, fh = lane >> 5;
+
+    // the tile's padded halo rows
+    int pr0, npix;
+    {
+        const int b0 = (int)cl.fd_pq.div((uint32_t)m0), q0 = m0 - b0 * PQ;
+        const int p0 = (int)cl.fd_q.div((uint32_t)q0);
+        const int m1 = min(m0 + BM, M) - 1;
+        const int b1 = (int)cl.fd_pq.div((uint32_t)m1), q1 = m1 - b1 * PQ;
+        const int p1 = (int)cl.fd_q.div((uint32_t)q1);
+        pr0 = b0 * H1 + p0;
+        npix = (b1 * H1 + p1 + 2 - pr0 + 1) * W2;
+    }
+    pr0 = __builtin_amdgcn_readfirstlane(pr0);
+    npix = __builtin_amdgcn_readfirstlane(npix);
+    const int nI = (npix + 7) >> 3;
+    const int nq = (nI - wave + NW - 1) / NW;  // this wave's halo instructions
+
+    // per-tap halo offset and weight tap (uniform), decoded once
+    int toff[9], twc[9];
+#pragma unroll
+    for (int tp = 0; tp < 9; ++tp) {
+        const int ti = tp / 3, tj = tp % 3;
+        const int dh = (int)((cl.pk_dh >> (4 * ti)) & 15u) - 8, dw = (int)((cl.pk_dw >> (4 * tj)) & 15u) - 8;
+        toff[tp] = __builtin_amdgcn_readfirstlane(dh * W2 + dw);
+        const int tw = (int)((cl.pk_r >> (4 * ti)) & 15u) * a.Sw + (int)((cl.pk_s >> (4 * tj)) & 15u);
+        twc[tp] = __builtin_amdgcn_readfirstlane(tw * a.C);
+    }
+    // A fragment addresses (ks = 0) per tap and row block: chunk (2ks+fh) ^ swz(pixel)
+    int aad[9][MT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+        int m = m0 + wm * (MT * 32) + i * 32 + fr;
+        m = m < M ? m : m0;  // rows past M read a valid pixel; their outputs are not stored
+        const int b = (int)cl.fd_pq.div((uint32_t)m), pq = m - b * PQ;
+        const int p = (int)cl.fd_q.div((uint32_t)pq), q = pq - p * cl.Q;
+        const int hb = (b * H1 + 1 + p - pr0) * W2 + 1 + q;
+#pragma unroll
+        for (int tp = 0; tp < 9; ++tp) {
+            const int hp = hb + toff[tp];
+            aad[tp][i] = (hp << 7) | ((((hp >> 1) & 7) ^ fh) << 4);
+        }
+    }
+    // B: weight rows of this wave's DMA instructions ([Nout][9][C]), source-swizzled
+    const uint16_t* b_src[BR];
+#pragma unroll
+    for (int j = 0; j < BR; ++j) {
+        const int row = (wave * BR + j) * 8 + (lane >> 3);
+        b_src[j] = gwt + (size_t)(n0 + row) * a.T * a.C + ((slot ^ ((row >> 1) & 7)) << 3);
+    }
+    int b_rd[NT][4];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const int row = wn * (BN / 2) + j * 32 + fr;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) b_rd[j][ks] = HB + row * 128 + (swz(row, ks * 2 + fh) << 4);
+    }
+    // halo sources of this wave's DMA instructions: channel-0 element offset or -1 (zero)
+    int hsrc[kH9MaxQ];
+#pragma unroll
+    for (int q = 0; q < kH9MaxQ; ++q) {
+        hsrc[q] = -1;
+        const int hp = (wave + NW * q) * 8 + (lane >> 3);
+        if (q < nq && hp < npix) {
+            const int r = (int)h.fd_w2.div((uint32_t)hp), c = hp - r * W2;
+            const int pr = pr0 + r;
+            const int b = (int)h.fd_h1.div((uint32_t)pr), rr = pr - b * H1;
+            if (rr != 0 && c != 0 && c != W + 1 && b < a.N)
+                hsrc[q] = (((b * H + rr - 1) * W + c - 1) << a.logC) + ((slot ^ ((hp >> 1) & 7)) << 3);
+        }
+    }
+
+    typedef __attribute__((address_space(1))) const void* gptr_t;
+    typedef __attribute__((address_space(3))) void* lptr_t;
+    auto issue_halo = [&](int cc) {
+        const int cbase = cc << 6;
+#pragma unroll
+        for (int q = 0; q < kH9MaxQ; ++q) {
+            if (q < nq) {
+                const void* src = hsrc[q] >= 0 ? (const void*)(gin + hsrc[q] + cbase) : (const void*)g_zero16;
+                __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + (wave + NW * q) * 1024), 16, 0, 0);
+            }
+        }
+    };
+    // k-tile (chunk cc, tap tp) -> ring stage st
+    auto issue_b = [&](int cc, int tp, int st) {
+        const int off = twc[tp] + (cc << 6);
+#pragma unroll
+        for (int j = 0; j < BR; ++j)
+            __builtin_amdgcn_global_load_lds((gptr_t)(b_src[j] + off),
+                                             (lptr_t)(lds + HB + st * SB + (wave * BR + j) * 1024), 16, 0, 0);
+    };
+
+    floatx16 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    auto compute = [&](int tp, int st) {
+        bf16x8 af[2][MT], bfr[2][NT];
+#pragma unroll
+        for (int i = 0; i < MT; ++i) af[0][i] = *reinterpret_cast<const bf16x8*>(lds + aad[tp][i]);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) bfr[0][j] = *reinterpret_cast<const bf16x8*>(lds + st * SB + b_rd[j][0]);
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            const int c = ks & 1;
+            if (ks < 3) {
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+                    af[c ^ 1][i] = *reinterpret_cast<const bf16x8*>(lds + (aad[tp][i] ^ ((ks + 1) << 5)));
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+                    bfr[c ^ 1][j] = *reinterpret_cast<const bf16x8*>(lds + st * SB + b_rd[j][ks + 1]);
+            }
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[c][j], af[c][i], acc[i][j], 0, 0, 0);
+        }
+        constexpr int NR = MT + NT, NM = MT * NT;
+        __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+#pragma unroll
+        for (int ks = 0; ks < 3; ++ks) {
+#pragma unroll
+            for (int q = 0; q < (NM > NR ? NM : NR); ++q) {
+                if (q < NM) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                if (q < NR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
+    };
+
+    // vmcnt(n): all but the wave's n newest vector-memory operations done
+    auto wait_vm = [](int n) {
+        switch (n) {
+        case 0: __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8)); break;
+        case 1: __builtin_amdgcn_s_waitcnt(1 | (7 << 4) | (15 << 8)); break;
+        case 2: __builtin_amdgcn_s_waitcnt(2 | (7 << 4) | (15 << 8)); break;
+        case 3: __builtin_amdgcn_s_waitcnt(3 | (7 << 4) | (15 << 8)); break;
+        case 4: __builtin_amdgcn_s_waitcnt(4 | (7 << 4) | (15 << 8)); break;
+        case 5: __builtin_amdgcn_s_waitcnt(5 | (7 << 4) | (15 << 8)); break;
+        case 6: __builtin_amdgcn_s_waitcnt(6 | (7 << 4) | (15 << 8)); break;
+        case 7: __builtin_amdgcn_s_waitcnt(7 | (7 << 4) | (15 << 8)); break;
+        case 8: __builtin_amdgcn_s_waitcnt(8 | (7 << 4) | (15 << 8)); break;
+        case 9: __builtin_amdgcn_s_waitcnt(9 | (7 << 4) | (15 << 8)); break;
+        case 10: __builtin_amdgcn_s_waitcnt(10 | (7 << 4) | (15 << 8)); break;
+        case 11: __builtin_amdgcn_s_waitcnt(11 | (7 << 4) | (15 << 8)); break;
+        default: __builtin_amdgcn_s_waitcnt(12 | (7 << 4) | (15 << 8)); break;
+        }
+    };
+    static_assert((NB - 2) * BR <= 12, "counted wait range");
+    const int nkt = (c1 - c0) * 9;
+    issue_halo(c0);
+#pragma unroll
+    for (int k = 0; k < NB - 1; ++k)
+        if (k < nkt) issue_b(c0 + k / 9, k % 9, k);
+    int sb = 0;  // ring slot of k-tile kt
+    int kt = 0;
+    for (int cc = c0; cc < c1; ++cc) {
+#pragma unroll
+        for (int tp = 0; tp < 9; ++tp, ++kt) {
+            // stages issued after k-tile kt: min(NB - 2, nkt - 1 - kt), left in flight
+            const int ahead = min(NB - 2, nkt - 1 - kt);
+            if (DIAG == 1) wait_vm(0);
+            else wait_vm(ahead * BR);
+            if (DIAG != 3) __builtin_amdgcn_s_barrier();
+            if (DIAG != 4 && tp == 0 && cc > c0) {  // every wave is done with the previous chunk's halo
+                issue_halo(cc);
+                wait_vm(0);
+                __builtin_amdgcn_s_barrier();
+            }
+            if (DIAG != 1 && kt + NB - 1 < nkt) {
+                int sn = sb + NB - 1;
+                if (sn >= NB) sn -= NB;
+                if (tp + NB - 1 < 9) issue_b(cc, tp + NB - 1, sn);
+                else issue_b(cc + 1, tp + NB - 1 - 9, sn);
+            }
+            if (DIAG != 2) compute(tp, sb);
+            if (++sb == NB) sb = 0;
+        }
+    }
+
+    if (a.splits > 1) {
+        constexpr int NQ = MT * NT * 4;  // float4 groups of accumulators per lane
+        const auto rs = rsrc_of(a.ws + (size_t)tid * NQ * 256 * 4);
+        if (split > 0) {  // wait for the previous split's running sum, then add it
+            __shared__ int late;
+            if (t == 0) {  // bounded: a broken hand-off never hangs, it faults loudly
+                unsigned n = 0;
+                bool ok = true;
+                while (__hip_atomic_load(a.flags + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
+                       (unsigned)split) {
+                    if (++n >= a.spin_limit) {
+                        ok = false;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                if (!ok) atomicOr(&g_conv_fault, GM_FAULT_SPLITK_SPIN);
+                late = ok ? 0 : 1;
+            }
+            __syncthreads();
+            if (late) {
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+#pragma unroll
+                    for (int j = 0; j < NT; ++j)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) acc[i][j][r] = __builtin_nanf("");
+            }
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const float4 v = ld_sc1_f32x4(rs, (unsigned)((((i * NT + j) * 4 + g) * 256 + t) * 16));
+                        acc[i][j][4 * g] += v.x;
+                        acc[i][j][4 * g + 1] += v.y;
+                        acc[i][j][4 * g + 2] += v.z;
+                        acc[i][j][4 * g + 3] += v.w;
+                    }
+        }
+        if (split < a.splits - 1) {  // publish the running sum to the next split
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g)
+                        st_sc1_f32x4(rs, (unsigned)((((i * NT + j) * 4 + g) * 256 + t) * 16),
+                                     make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2],
+                                                 acc[i][j][4 * g + 3]));
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (t == 0) __hip_atomic_store(a.flags + tid, (unsigned)(split + 1), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        if (t == 0) __hip_atomic_store(a.flags + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    store_tile<MT, NT, 128, BN>(a, cl, m0, n0, wm, wn, fr, fh, M, acc, g * a.gs_out);
+}
+
+// ---------------------------------------------------------------------------------
 // 3x3 / stride-1 convolutions with 64 input and 64 output channels (ResNet layer 1:
 // forward and input gradient).  The whole weight tensor (9 taps x 64 x 64 bf16 = 72 KB)
 // stays resident in LDS for the life of a persistent workgroup, which walks output tiles
@@ -1049,8 +1374,17 @@ __global__ __launch_bounds__(256) void k_conv_rw(ConvArgs a, RwArgs r) {
     const unsigned pk_dh = cl.pk_dh, pk_dw = cl.pk_dw, pk_r = cl.pk_r, pk_s = cl.pk_s;
     typedef __attribute__((address_space(1))) const void* gptr_t;
     typedef __attribute__((address_space(3))) void* lptr_t;
-    int tl = blockIdx.x;
-    if (tl >= r.tiles) return;
+    // view groups: gridDim / G workgroups per group, each walking that group's tiles
+    int g = 0, tl = blockIdx.x, nwg = gridDim.x;
+    if (a.G > 1) {
+        nwg = gridDim.x / a.G;
+        g = tl / nwg;
+        tl -= g * nwg;
+    }
+    if (tl >= r.tiles || g >= a.G) return;
+    const uint16_t* const gin = a.in + g * a.gs_in;
+    const uint16_t* const gwt = a.wt + g * a.gs_wt;
+    const uint16_t* const gadd = a.addend ? a.addend + g * a.gs_out : nullptr;
 
     // weights, once: instruction I = tap (I >> 3), rows n = 8 (I & 7) .. + 7
     for (int I = wave; I < 72; I += 4) {
@@ -1058,7 +1392,7 @@ __global__ __launch_bounds__(256) void k_conv_rw(ConvArgs a, RwArgs r) {
         const int ti = tp / 3, tj = tp - ti * 3;
         const int tw = (int)((pk_r >> (4 * ti)) & 15u) * a.Sw + (int)((pk_s >> (4 * tj)) & 15u);
         const int gc = slot ^ ((n >> 1) & 7);
-        __builtin_amdgcn_global_load_lds((gptr_t)(a.wt + ((size_t)n * a.T + tw) * 64 + gc * 8),
+        __builtin_amdgcn_global_load_lds((gptr_t)(gwt + ((size_t)n * a.T + tw) * 64 + gc * 8),
                                          (lptr_t)(lds + I * 1024), 16, 0, 0);
     }
     // the halo of tile tl (image b, output rows p0 .. p0+RT-1) into buffer bb.  The halo's
@@ -1082,7 +1416,7 @@ __global__ __launch_bounds__(256) void k_conv_rw(ConvArgs a, RwArgs r) {
     auto issue_halo = [&](int tile, int bb) {
         const int b = (int)r.fd_tpi.div((uint32_t)tile);
         const int p0 = (tile - b * r.tpi) * r.RT;
-        const uint16_t* origin = a.in + ((size_t)(b * H + p0) * W << 6);
+        const uint16_t* origin = gin + ((size_t)(b * H + p0) * W << 6);
         const unsigned okmask = 1u | (p0 > 0 ? 2u : 0u) | (p0 + r.RT < H ? 4u : 0u);  // bit k: class k valid
         char* base = lds + WB + bb * r.hbytes;
 #pragma unroll
@@ -1123,12 +1457,12 @@ __global__ __launch_bounds__(256) void k_conv_rw(ConvArgs a, RwArgs r) {
     lds_barrier();
     const size_t out_bytes = (size_t)a.N * a.Ho * a.Wo * a.Nout * 2;
     const __amdgpu_buffer_rsrc_t orsrc =
-        __builtin_amdgcn_make_buffer_rsrc(cl.out, 0, (int)(out_bytes < 0x7fffffffu ? out_bytes : 0x7fffffffu),
+        __builtin_amdgcn_make_buffer_rsrc(cl.out + g * a.gs_out, 0, (int)(out_bytes < 0x7fffffffu ? out_bytes : 0x7fffffffu),
                                           0x00020000);
 
     int bb = 0;
-    for (; tl < r.tiles; tl += gridDim.x) {
-        const int nx = tl + gridDim.x;
+    for (; tl < r.tiles; tl += nwg) {
+        const int nx = tl + nwg;
         if (nx < r.tiles) issue_halo(nx, bb ^ 1);  // buffer bb^1 was released by the last barrier
         const int hoff = WB + bb * r.hbytes;
 
@@ -1238,7 +1572,7 @@ __global__ __launch_bounds__(256) void k_conv_rw(ConvArgs a, RwArgs r) {
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int gq = 0; gq < 4; ++gq)
-                    av[i][gq] = *(const uint2*)(a.addend + off[i] + 8 * gq);  // rows past RT*W read row 0
+                    av[i][gq] = *(const uint2*)(gadd + off[i] + 8 * gq);  // rows past RT*W read row 0
         }
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
@@ -1299,12 +1633,19 @@ __global__ __launch_bounds__(256) void k_conv_stem(ConvArgs a, StemArgs r) {
     const int WB = 64 * r.wpitch;
     typedef __attribute__((address_space(1))) const void* gptr_t;
     typedef __attribute__((address_space(3))) void* lptr_t;
-    int tl = blockIdx.x;
-    if (tl >= r.rows) return;
+    // view groups: gridDim / G workgroups per group, each walking that group's output rows
+    int g = 0, tl = blockIdx.x, nwg = gridDim.x;
+    if (a.G > 1) {
+        nwg = gridDim.x / a.G;
+        g = tl / nwg;
+        tl -= g * nwg;
+    }
+    if (tl >= r.rows || g >= a.G) return;
+    const uint16_t* const gin = a.in + g * a.gs_in;
 
     // weights [64][T][8] -> LDS rows of wpitch bytes (register path: the padded pitch
     // is not lane-linear)
-    const uint4* wsrc = reinterpret_cast<const uint4*>(a.wt);
+    const uint4* wsrc = reinterpret_cast<const uint4*>(a.wt + g * a.gs_wt);
     for (int e = t; e < 64 * r.T; e += 256) {
         const int n = e / r.T, tp = e - n * r.T;
         *reinterpret_cast<uint4*>(lds + n * r.wpitch + tp * 16) = wsrc[e];
@@ -1312,7 +1653,7 @@ __global__ __launch_bounds__(256) void k_conv_stem(ConvArgs a, StemArgs r) {
     // the R input rows of output row `row` (= image b, output row p): one contiguous block
     auto issue_block = [&](int row, int bb) {
         const int b = (int)r.fd_p.div((uint32_t)row), p = row - b * P;
-        const char* src = reinterpret_cast<const char*>(a.in) + ((size_t)(b * a.Hi + p * a.sAh) * Wi) * 16;
+        const char* src = reinterpret_cast<const char*>(gin) + ((size_t)(b * a.Hi + p * a.sAh) * Wi) * 16;
         char* base = lds + WB + bb * r.hbytes;
         for (int I = wave; I < r.nI; I += 4) {
             const int off = I * 1024 + lane * 16;
@@ -1342,12 +1683,12 @@ __global__ __launch_bounds__(256) void k_conv_stem(ConvArgs a, StemArgs r) {
     __syncthreads();  // weights (ds_write) and the first block (DMA) are in LDS
     const size_t out_bytes = (size_t)a.N * a.Ho * a.Wo * a.Nout * 2;
     const __amdgpu_buffer_rsrc_t orsrc =
-        __builtin_amdgcn_make_buffer_rsrc(cl.out, 0, (int)(out_bytes < 0x7fffffffu ? out_bytes : 0x7fffffffu),
+        __builtin_amdgcn_make_buffer_rsrc(cl.out + g * a.gs_out, 0, (int)(out_bytes < 0x7fffffffu ? out_bytes : 0x7fffffffu),
                                           0x00020000);
 
     int bb = 0;
-    for (; tl < r.rows; tl += gridDim.x) {
-        const int nx = tl + gridDim.x;
+    for (; tl < r.rows; tl += nwg) {
+        const int nx = tl + nwg;
         if (nx < r.rows) issue_block(nx, bb ^ 1);
         const unsigned hoff = lds0 + (unsigned)(WB + bb * r.hbytes);
 
@@ -1487,6 +1828,8 @@ static int launch_igemm(ConvArgs& a, hipStream_t st) {
         tiles += c.tiles_m * ((a.Nout + BN - 1) / BN);
     }
     if (tiles == 0) return GM_OK;
+    a.tiles_g = tiles;
+    tiles *= a.G;  // view groups: G x the tiles of one group
     a.tiles_total = tiles;
     if (a.splits < 1) a.splits = 1;
     const size_t lds = (size_t)ST * (BM + BN) * 128 + kMaxTap * 4 + 12;
@@ -1510,6 +1853,9 @@ static int launch_igemm(ConvArgs& a, hipStream_t st) {
     } else if (a.splits > 1) {
         set_error("conv: split-K needs the lean kernel");
         return GM_E_ARG;
+    } else if (a.G > 1) {
+        set_error("conv: view groups need the lean, halo or resident-weight kernels (C >= 64)");
+        return GM_E_UNSUP;
     } else if (a.C >= 64) {
         k_conv_igemm<BM, BN, true, ST><<<tiles, 256, lds, st>>>(a);
     } else {
@@ -1542,13 +1888,11 @@ static int tile_bias() {
     return b;
 }
 
-static int splitk_target() {
-    static int t = [] {
-        const char* e = getenv("GM_CONV_SPLITK");  // workgroups wanted from split-K; 0 disables it
-        return e ? atoi(e) : 384;
-    }();
-    return t;
-}
+static int g_splitk_target = [] {
+    const char* e = getenv("GM_CONV_SPLITK");  // workgroups wanted from split-K; 0 disables it
+    return e ? atoi(e) : 384;
+}();
+static int splitk_target() { return g_splitk_target; }
 
 static int splitk_mink() {
     static int t = [] {
@@ -1590,8 +1934,8 @@ static TilePick pick_tile(const ConvArgs& a) {
     int t128 = 0, nkmin = 1 << 30;
     for (int i = 0; i < a.ncls; ++i) {
         const long Mi = (long)a.N * a.cls[i].P * a.cls[i].Q;
-        M += Mi;
-        t128 += (int)((Mi + 127) / 128) * ((a.Nout + 127) / 128);
+        M += Mi * a.G;
+        t128 += a.G * (int)((Mi + 127) / 128) * ((a.Nout + 127) / 128);
         const int nk = a.cls[i].ntap * a.C / 64;
         nkmin = nk < nkmin ? nk : nkmin;
     }
@@ -1729,7 +2073,9 @@ static int launch_stem(const ConvArgs& a, const StemArgs& r, size_t lds, hipStre
         }
         granted = lds;
     }
-    const int grid = r.rows < 512 ? r.rows : 512;  // persistent: two workgroups per CU
+    // persistent: two workgroups per CU, split evenly over the view groups
+    const int per = r.rows < 512 / a.G ? r.rows : (512 / a.G > 0 ? 512 / a.G : 1);
+    const int grid = per * a.G;
     k_conv_stem<<<grid, 256, lds, st>>>(a, r);
     return check_launch("k_conv_stem");
 }
@@ -1781,16 +2127,103 @@ static int launch_rw(const ConvArgs& a, const RwArgs& r, size_t lds, hipStream_t
         }
         granted = lds;
     }
-    const int grid = r.tiles < 256 ? r.tiles : 256;  // persistent: one workgroup per CU
+    // persistent: one workgroup per CU, split evenly over the view groups
+    const int per = r.tiles < 256 / a.G ? r.tiles : (256 / a.G > 0 ? 256 / a.G : 1);
+    const int grid = per * a.G;
     if (g_conv_rw == 2) k_conv_rw<1><<<grid, 256, lds, st>>>(a, r);       // timing diagnostics
     else if (g_conv_rw == 3) k_conv_rw<2><<<grid, 256, lds, st>>>(a, r);
     else k_conv_rw<0><<<grid, 256, lds, st>>>(a, r);
     return check_launch("k_conv_rw");
 }
 
+static int g_conv_h9 = [] {
+    const char* e = getenv("GM_CONV_H9");  // 0: the halo shapes take k_conv_halo (A/B)
+    return e ? atoi(e) : 1;
+}();
+
+// k_conv_h9 when eligible: Nout a multiple of BN, at most 48 halo DMA instructions, the
+// halo + 3 weight stages within half the CU's LDS (two workgroups per CU), splits over
+// whole channel chunks.  Returns 0 when not taken.
+template <int BN, int NB>
+static int launch_h9(ConvArgs& a, int hb, hipStream_t st) {
+    ConvCls& c = a.cls[0];
+    const int M = a.N * c.P * c.Q;
+    c.tiles_m = (M + 127) / 128;
+    c.tile_start = 0;
+    a.tiles_g = c.tiles_m * (a.Nout / BN);
+    a.tiles_total = a.tiles_g * a.G;
+    if (a.splits < 1) a.splits = 1;
+    HaloArgs h;
+    h.halo_bytes = hb;
+    h.fd_w2 = FastDiv((uint32_t)(a.Wi + 2));
+    h.fd_h1 = FastDiv((uint32_t)(a.Hi + 1));
+    const size_t lds = (size_t)hb + NB * (size_t)BN * 128;
+    static size_t attr = 0;
+    if (lds > attr) {
+        hipError_t e = hipSuccess;
+        for (const void* k : {(const void*)k_conv_h9<BN, NB, 0>, (const void*)k_conv_h9<BN, NB, 1>,
+                              (const void*)k_conv_h9<BN, NB, 2>, (const void*)k_conv_h9<BN, NB, 3>,
+                              (const void*)k_conv_h9<BN, NB, 4>})
+            if (e == hipSuccess) e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) {
+            set_error("k_conv_h9: %zu B of LDS refused (%s)", lds, hipGetErrorString(e));
+            return GM_E_UNSUP;
+        }
+        attr = lds;
+    }
+    const dim3 grid(a.tiles_total * a.splits);
+    switch (conv_pipe()) {  // 5..8: timing diagnostics (outputs meaningless)
+    case 5: k_conv_h9<BN, NB, 1><<<grid, 256, lds, st>>>(a, h); break;
+    case 6: k_conv_h9<BN, NB, 2><<<grid, 256, lds, st>>>(a, h); break;
+    case 7: k_conv_h9<BN, NB, 3><<<grid, 256, lds, st>>>(a, h); break;
+    case 8: k_conv_h9<BN, NB, 4><<<grid, 256, lds, st>>>(a, h); break;
+    default: k_conv_h9<BN, NB, 0><<<grid, 256, lds, st>>>(a, h);
+    }
+    const int rc = check_launch("k_conv_h9");
+    return rc == GM_OK ? 1 : rc;
+}
+
+// (BN, NB) of k_conv_h9 for a shape: gm_conv_set_h9(1) = automatic - the deepest weight
+// ring (<= 3 stages) of 128-channel tiles that keeps two workgroups per CU; a forced
+// form (BN << 8 | NB, A/B runs) when it fits.  0 when not eligible.
+static int h9_form(const ConvArgs& a, int hb, int BNmax) {
+    if (!g_conv_h9 || hb / 1024 > 4 * kH9MaxQ || a.N * a.cls[0].P * a.cls[0].Q >= (1 << 30) / 8) return 0;
+    const int budget = 80 * 1024 - 256;
+    auto fits = [&](int bn, int nb) { return bn <= BNmax && a.Nout % bn == 0 && hb + nb * bn * 128 <= budget; };
+    if (g_conv_h9 > 1) {
+        const int bn = g_conv_h9 >> 8, nb = g_conv_h9 & 255;
+        return fits(bn, nb) ? g_conv_h9 : 0;
+    }
+    for (int nb = 3; nb >= 2; --nb)
+        if (fits(128, nb)) return 128 << 8 | nb;
+    return fits(64, 4) ? 64 << 8 | 4 : 0;
+}
+
+// k_conv_h9 when eligible (Nout a multiple of BN, at most 48 halo DMA instructions, splits
+// over whole channel chunks).  Returns 1 when launched, 0 when not taken.
+template <int BN>
+static int try_h9(ConvArgs& a, int hb, hipStream_t st) {
+    if (a.splits > (a.C >> 6)) return 0;
+    const int f = h9_form(a, hb, BN);
+    if (!f) return 0;
+    switch (f) {
+    case 128 << 8 | 2: return launch_h9<128, 2>(a, hb, st);
+    case 128 << 8 | 3: return launch_h9<128, 3>(a, hb, st);
+    case 64 << 8 | 3: return launch_h9<64, 3>(a, hb, st);
+    case 64 << 8 | 4: return launch_h9<64, 4>(a, hb, st);
+    case 64 << 8 | 5: return launch_h9<64, 5>(a, hb, st);
+    default: return 0;
+    }
+}
+
 template <int BN>
 static int launch_halo(ConvArgs& a, int hb, hipStream_t st) {
     const int p = conv_pipe();
+    if (p == 0 || p == 3 || p >= 5) {
+        const int r = try_h9<BN>(a, hb, st);
+        if (r == 1) return GM_OK;
+        if (r != 0) return r;
+    }
     if (p == 5) return launch_halo_v<BN, 5, 2>(a, hb, st);
     if (p == 6) return launch_halo_v<BN, 6, 2>(a, hb, st);
     // a third weight stage when two workgroups per CU still fit (or when asked: pipe 3)
@@ -1862,7 +2295,8 @@ static int try_halo256(ConvArgs& a, hipStream_t st, void* ws, size_t ws_bytes) {
 
 static int pick_and_launch(ConvArgs& a, hipStream_t st, void* ws, size_t ws_bytes) {
     const bool three = stages() == 3;
-    {
+    if (a.G < 1) a.G = 1;
+    if (a.G == 1) {
         const int r = try_halo256(a, st, ws, ws_bytes);
         if (r == 1) return GM_OK;
         if (r != 0) return r;
@@ -1880,7 +2314,7 @@ static int pick_and_launch(ConvArgs& a, hipStream_t st, void* ws, size_t ws_byte
     TilePick p = pick_tile(a);
     if (p.splits > 1 && (!ws || ws_bytes < splitk_bytes(p) || p.tiles > kMaxSplitTiles)) {  // the unsplit choice
         long M = 0;
-        for (int i = 0; i < a.ncls; ++i) M += (long)a.N * a.cls[i].P * a.cls[i].Q;
+        for (int i = 0; i < a.ncls; ++i) M += (long)a.N * a.cls[i].P * a.cls[i].Q * a.G;
         p = {M / 128 * ((a.Nout + 63) / 64) >= tile_bias() * 3 / 4 ? T128x64 : T64x64, 1, 0};
     }
     a.splits = p.splits;
@@ -1891,7 +2325,14 @@ static int pick_and_launch(ConvArgs& a, hipStream_t st, void* ws, size_t ws_byte
         a.ws = reinterpret_cast<float*>(static_cast<char*>(ws) + splitk_flag_bytes(p.tiles));
     }
     const int hb = halo_bytes(a);
-    if (hb > 0 && hb + 2 * 128 * 128 <= 160 * 1024) {
+    if (hb > 0 && hb + 2 * 128 * 128 <= 160 * 1024 && a.G > 1) {
+        // view groups: k_conv_h9 when it takes the shape, else the lean kernel below
+        if (p.tile != T128x128) a.splits = 1;
+        const int r = (p.tile == T128x128 || a.Nout >= 128) ? try_h9<128>(a, hb, st) : try_h9<64>(a, hb, st);
+        if (r == 1) return GM_OK;
+        if (r != 0) return r;
+        if (a.splits != p.splits) p.tile = a.Nout >= 128 ? T128x64 : T64x64;
+    } else if (hb > 0 && hb + 2 * 128 * 128 <= 160 * 1024) {
         if (p.tile == T128x128) return launch_halo<128>(a, hb, st);
         a.splits = 1;  // (split-K is only chosen with 128x128 tiles)
         if (a.Nout >= 128) return launch_halo<128>(a, hb, st);
@@ -2007,6 +2448,7 @@ static void fwd_setup(const gm_conv_desc_hw* d, const void* x, const void* w, vo
     a.Nout = d->K; a.T = d->R * d->S; a.Sw = d->S;
     a.Ho = P; a.Wo = Q; a.sAh = d->stride_h; a.sAw = d->stride_w;
     a.ncls = 1;
+    a.G = 1;
     ConvCls& c = a.cls[0];
     c.out = (uint16_t*)y;
     c.P = P; c.Q = Q; c.oS = 1; c.oH = 0; c.oW = 0;
@@ -2032,6 +2474,7 @@ static bool dgrad_setup(const gm_conv_desc* d, const void* dy, const void* wt, v
     a.N = d->N; a.Hi = P; a.Wi = Q; a.C = d->K; a.logC = ilog2(d->K);
     a.Nout = d->C; a.T = d->R * d->S; a.Sw = d->S;
     a.Ho = d->H; a.Wo = d->W; a.sAh = a.sAw = 1;
+    a.G = 1;
     bool full = true;
     for (int ph = 0; ph < st; ++ph)
         for (int pw = 0; pw < st; ++pw) {
@@ -2084,6 +2527,17 @@ unsigned conv_faults_read(bool clear) {
 }
 }  // namespace gm
 
+extern "C" int gm_conv_set_splitk(int target) {
+    GM_REQUIRE(target >= 0, "gm_conv_set_splitk: target must be >= 0");
+    g_splitk_target = target;
+    return GM_OK;
+}
+
+extern "C" int gm_conv_set_h9(int on) {
+    g_conv_h9 = on;
+    return GM_OK;
+}
+
 extern "C" int gm_conv_set_halo(int on) {
     g_conv_halo = on < 0 ? 0 : on > 2 ? 2 : on;
     return GM_OK;
@@ -2100,8 +2554,8 @@ extern "C" int gm_conv_set_rw(int on) {
 }
 
 extern "C" int gm_conv_set_pipe(int pipe) {
-    GM_REQUIRE(pipe == 0 || pipe == 2 || pipe == 3 || pipe == 5 || pipe == 6,
-               "gm_conv_set_pipe: 0, 2, 3 (5, 6: timing diagnostics)");
+    GM_REQUIRE(pipe == 0 || pipe == 2 || pipe == 3 || (pipe >= 5 && pipe <= 8),
+               "gm_conv_set_pipe: 0, 2, 3 (5..8: timing diagnostics)");
     g_conv_pipe = pipe;
     return GM_OK;
 }
@@ -2129,6 +2583,56 @@ extern "C" int gm_conv2d_fwd_ex_bf16(const gm_conv_desc* d, const void* x, const
 
 extern "C" int gm_conv2d_fwd_bf16(const gm_conv_desc* d, const void* x, const void* w, void* y, void* stream) {
     return gm_conv2d_fwd_ex_bf16(d, x, w, y, nullptr, 0, stream);
+}
+
+// G view groups in one launch: group g reads x + g*N*H*W*C with the weight w + g*w_stride
+// and writes y + g*N*P*Q*K (the views stacked along the batch, one weight per view)
+extern "C" int gm_conv2d_fwd_grouped_bf16(const gm_conv_desc_hw* d, int G, const void* x, const void* w,
+                                          long long w_stride, void* y, void* ws, size_t ws_bytes, void* stream) {
+    int rc = check_desc_hw(d);
+    if (rc) return rc;
+    GM_REQUIRE(x && w && y, "conv fwd: null pointer");
+    GM_REQUIRE(G >= 1 && G <= 64, "conv fwd: view groups must be 1..64 (got %d)", G);
+    GM_REQUIRE(G == 1 || w_stride >= (long long)d->K * d->R * d->S * d->C ||
+                   -w_stride >= (long long)d->K * d->R * d->S * d->C,
+               "conv fwd: group weight stride %lld shorter than one weight", w_stride);
+    ConvArgs a;
+    fwd_setup(d, x, w, y, a);
+    a.G = G;
+    a.gs_in = (long long)d->N * d->H * d->W * d->C;
+    a.gs_wt = w_stride;
+    a.gs_out = (long long)d->N * a.cls[0].P * a.cls[0].Q * d->K;
+    return pick_and_launch(a, as_stream(stream), ws, ws_bytes);
+}
+
+extern "C" int gm_conv2d_dgrad_grouped_bf16(const gm_conv_desc* d, int G, const void* dy, const void* wt,
+                                            long long wt_stride, void* dx, const void* addend, void* ws,
+                                            size_t ws_bytes, void* stream) {
+    int rc = check_dgrad(d);
+    if (rc) return rc;
+    GM_REQUIRE(dy && wt && dx, "conv dgrad: null pointer");
+    GM_REQUIRE(G >= 1 && G <= 64, "conv dgrad: view groups must be 1..64 (got %d)", G);
+    GM_REQUIRE(G == 1 || wt_stride >= (long long)d->K * d->R * d->S * d->C ||
+                   -wt_stride >= (long long)d->K * d->R * d->S * d->C,
+               "conv dgrad: group weight stride %lld shorter than one weight", wt_stride);
+    const int P = (d->H + 2 * d->pad - d->R) / d->stride + 1;
+    const int Q = (d->W + 2 * d->pad - d->S) / d->stride + 1;
+    ConvArgs a;
+    const bool full = dgrad_setup(d, dy, wt, dx, a);
+    a.G = G;
+    a.gs_in = (long long)d->N * P * Q * d->K;
+    a.gs_wt = wt_stride;
+    a.gs_out = (long long)d->N * d->H * d->W * d->C;
+    a.addend = (const uint16_t*)addend;
+    hipStream_t s = as_stream(stream);
+    if (!full && addend != dx) {  // the groups are contiguous: one pass zeroes (or copies) them all
+        const size_t n = (size_t)G * d->N * d->H * d->W * d->C;
+        k_zero_bf16<<<(int)((n / 8 + 255) / 256 < 4096 ? (n / 8 + 255) / 256 : 4096), 256, 0, s>>>(
+            (uint16_t*)dx, n, (const uint16_t*)addend);
+        rc = check_launch("k_zero_bf16");
+        if (rc) return rc;
+    }
+    return pick_and_launch(a, s, ws, ws_bytes);
 }
 
 extern "C" int gm_conv2d_dgrad_add_bf16(const gm_conv_desc* d, const void* dy, const void* wt, void* dx,
@@ -2163,8 +2667,9 @@ extern "C" int gm_conv2d_dgrad_bf16(const gm_conv_desc* d, const void* dy, const
     return gm_conv2d_dgrad_ex_bf16(d, dy, wt, dx, nullptr, 0, stream);
 }
 
-extern "C" size_t gm_conv2d_splitk_ws_bytes(const gm_conv_desc* d, int dgrad) {
+extern "C" size_t gm_conv2d_splitk_ws_bytes_grouped(const gm_conv_desc* d, int G, int dgrad) {
     ConvArgs a;
+    if (G < 1) return 0;
     if (dgrad) {
         if (check_dgrad(d)) return 0;
         dgrad_setup(d, nullptr, nullptr, nullptr, a);
@@ -2173,8 +2678,13 @@ extern "C" size_t gm_conv2d_splitk_ws_bytes(const gm_conv_desc* d, int dgrad) {
         const gm_conv_desc_hw h = to_hw(d);
         fwd_setup(&h, nullptr, nullptr, nullptr, a);
     }
-    const size_t b128 = splitk_bytes(pick_tile(a)), b256 = halo256_plan(a).ws;
+    a.G = G;
+    const size_t b128 = splitk_bytes(pick_tile(a)), b256 = G == 1 ? halo256_plan(a).ws : 0;
     return b128 > b256 ? b128 : b256;
+}
+
+extern "C" size_t gm_conv2d_splitk_ws_bytes(const gm_conv_desc* d, int dgrad) {
+    return gm_conv2d_splitk_ws_bytes_grouped(d, 1, dgrad);
 }
 
 extern "C" int gm_conv_weight_transpose_bf16(const void* w, void* wt, int Co, int T, int Ci, void* stream) {

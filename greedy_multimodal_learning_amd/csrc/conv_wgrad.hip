@@ -41,6 +41,8 @@ struct WgradArgs {
     int S, padh, padw;          // k_conv_wgrad4 decodes taps arithmetically
     int adv_b, adv_p, adv_q;    // one 64-pixel step in (b, p, q): 64 = adv_b*P*Q + adv_p*Q + adv_q
     signed char dh[kWTap], dw[kWTap];
+    int G;                      // view groups (k_conv_wgrad4): group g reads dy + g*gs_dy, x + g*gs_x
+    long long gs_dy, gs_x, gs_part;  // and writes part + g*gs_part (elements)
 };
 
 typedef __attribute__((address_space(3))) short4_t lds_s4;
@@ -227,6 +229,10 @@ __global__ __launch_bounds__(256) void k_conv_wgrad4(WgradArgs a) {
         bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
     }
     const int tiles = a.tiles_k * a.tiles_n;
+    const int grp = bid / (tiles * a.splits);  // group-major: a group's tiles share XCDs
+    bid -= grp * tiles * a.splits;
+    const uint16_t* __restrict__ gdy = a.dy + grp * a.gs_dy;
+    const uint16_t* __restrict__ gx = a.x + grp * a.gs_x;
     const int split = bid / tiles, tile = bid - split * tiles;
     const int tk = tile % a.tiles_k, tn = tile / a.tiles_k;
     const int k0 = tk * BM, n0 = tn * BN;
@@ -247,7 +253,7 @@ __global__ __launch_bounds__(256) void k_conv_wgrad4(WgradArgs a) {
         a_row[j] = (wave * GA + j) * (64 / LPA) + a_rsub;
         const int col = k0 + ((a_slot ^ wswz<RA>(a_row[j])) << 3);
         a_cok[j] = col < a.Kc;
-        a_ptr[j] = a.dy + ((size_t)step0 * BK + a_row[j]) * a.Kc + (a_cok[j] ? col : 0);
+        a_ptr[j] = gdy + ((size_t)step0 * BK + a_row[j]) * a.Kc + (a_cok[j] ? col : 0);
     }
     // B (x) DMA lanes: fixed (tap, channel chunk) per instruction; the lane's pixel
     // (b, p, q) is decoded once and then advanced by one 64-pixel step per issue
@@ -291,7 +297,7 @@ __global__ __launch_bounds__(256) void k_conv_wgrad4(WgradArgs a) {
             const int hi = h0 + b_dh[j], wi = w0 + b_dw[j];
             const bool ok = b_cok[j] & (b < a.N) & ((unsigned)hi < (unsigned)a.H) & ((unsigned)wi < (unsigned)a.W);
             const int pix = (b * a.H + h0) * a.W + w0;
-            const void* src = ok ? (const void*)(a.x + (((long)pix << a.logC) + b_toff[j])) : zero;
+            const void* src = ok ? (const void*)(gx + (((long)pix << a.logC) + b_toff[j])) : zero;
             __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + bufoff + SA + (wave * GB + j) * 1024), 16,
                                              0, 0);
             // next step's pixel: + 64 = (adv_b, adv_p, adv_q), one carry per component at most
@@ -383,7 +389,7 @@ __global__ __launch_bounds__(256) void k_conv_wgrad4(WgradArgs a) {
     }
     if (i < nst) compute(B0{});  // odd step count: the last step sits in buffer 0
 
-    float* out = a.part + (size_t)split * a.Kc * TC;
+    float* out = a.part + grp * a.gs_part + (size_t)split * a.Kc * TC;
     const bool inner = k0 + BM <= a.Kc && n0 + BN <= TC;
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
@@ -425,8 +431,10 @@ __global__ __launch_bounds__(256) void k_conv_wgrad4(WgradArgs a) {
 // 9k float4 columns x 100 splits) still spread over hundreds of blocks.
 template <int R>
 __global__ __launch_bounds__(256) void k_wgrad_sum(const float* __restrict__ part, int splits, size_t slab,
-                                                   int accumulate, float* __restrict__ dw) {
+                                                   int accumulate, float* __restrict__ dw, long long gs_dw) {
     constexpr int CPB = 256 / R;
+    part += (size_t)blockIdx.y * splits * slab;  // view group blockIdx.y
+    dw += blockIdx.y * gs_dw;
     const int t = threadIdx.x, col = t % CPB, r = t / CPB;
     const size_t i4 = ((size_t)blockIdx.x * CPB + col) * 4;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -469,9 +477,11 @@ __global__ __launch_bounds__(256) void k_wgrad_sum(const float* __restrict__ par
 
 // dw = sum over splits (fixed order); also the [K][T][Cpad] -> [K][T][Creal] crop
 __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* part, int splits, int Kc, int T, int Cp,
-                                                      int Cr, int accumulate, float* dw) {
+                                                      int Cr, int accumulate, float* dw, long long gs_dw) {
     const size_t n = (size_t)Kc * T * Cr;
     const size_t slab = (size_t)Kc * T * Cp;
+    part += (size_t)blockIdx.y * splits * slab;  // view group blockIdx.y
+    dw += blockIdx.y * gs_dw;
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
         const size_t c = i % Cr, kt = i / Cr;
         const size_t src = kt * Cp + c;
@@ -515,7 +525,7 @@ struct WPlan {
     int P, Q, tiles_k, tiles_n, splits, sps, mt, nt;
 };
 
-static WPlan plan(const gm_conv_desc_hw* d) {
+static WPlan plan(const gm_conv_desc_hw* d, int G = 1) {
     WPlan w;
     w.P = (d->H + 2 * d->pad_h - d->R) / d->stride_h + 1;
     w.Q = (d->W + 2 * d->pad_w - d->S) / d->stride_w + 1;
@@ -534,7 +544,7 @@ static WPlan plan(const gm_conv_desc_hw* d) {
     }
     w.tiles_k = (d->K + 64 * w.mt - 1) / (64 * w.mt);
     w.tiles_n = (TC + 64 * w.nt - 1) / (64 * w.nt);
-    const int tiles = w.tiles_k * w.tiles_n;
+    const int tiles = w.tiles_k * w.tiles_n * G;  // the groups' tiles share the chip
     const int target = wgrad_version() >= 2 ? wgrad_target_wgs() : 1024;
     const int min_steps = wgrad_version() == 2 ? 8 : 4;
     int want = wgrad_version() == 2 ? (target > tiles ? target / tiles : 1) : (target + tiles - 1) / tiles;
@@ -566,11 +576,15 @@ static gm_conv_desc_hw to_hw(const gm_conv_desc* d) {
     return gm_conv_desc_hw{d->N, d->H, d->W, d->C, d->K, d->R, d->S, d->stride, d->stride, d->pad, d->pad};
 }
 
-extern "C" size_t gm_conv2d_wgrad_hw_scratch(const gm_conv_desc_hw* d) {
-    if (!d || d->stride_h < 1 || d->stride_w < 1) return 0;
-    const WPlan w = plan(d);
+extern "C" size_t gm_conv2d_wgrad_grouped_scratch(const gm_conv_desc_hw* d, int G) {
+    if (!d || d->stride_h < 1 || d->stride_w < 1 || G < 1) return 0;
+    const WPlan w = plan(d, G);
     const size_t slab = (size_t)d->K * d->R * d->S * d->C;
-    return (size_t)w.splits * slab * sizeof(float);
+    return (size_t)G * w.splits * slab * sizeof(float);
+}
+
+extern "C" size_t gm_conv2d_wgrad_hw_scratch(const gm_conv_desc_hw* d) {
+    return gm_conv2d_wgrad_grouped_scratch(d, 1);
 }
 
 extern "C" size_t gm_conv2d_wgrad_scratch(const gm_conv_desc* d) {
@@ -579,20 +593,27 @@ extern "C" size_t gm_conv2d_wgrad_scratch(const gm_conv_desc* d) {
     return gm_conv2d_wgrad_hw_scratch(&h);
 }
 
-extern "C" int gm_conv2d_wgrad_hw_bf16(const gm_conv_desc_hw* d, const void* dy, const void* x, float* dw,
-                                       int c_real, int accumulate, void* scratch, size_t scratch_bytes,
-                                       void* stream) {
+// G view groups in one launch: group g reads dy + g*N*P*Q*K and x + g*N*H*W*C (the views
+// stacked along the batch) and writes its weight gradient to dw + g*dw_stride (floats)
+extern "C" int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, const void* dy, const void* x,
+                                            float* dw, long long dw_stride, int c_real, int accumulate,
+                                            void* scratch, size_t scratch_bytes, void* stream) {
     GM_REQUIRE(d && dy && x && dw, "conv wgrad: null pointer");
+    GM_REQUIRE(G >= 1 && G <= 64, "conv wgrad: view groups must be 1..64 (got %d)", G);
+    GM_REQUIRE(wgrad_version() >= 2 || G == 1, "conv wgrad: view groups need k_conv_wgrad4");
     GM_REQUIRE(d->stride_h >= 1 && d->stride_w >= 1 && d->pad_h >= 0 && d->pad_w >= 0, "conv wgrad: bad stride/pad");
     GM_REQUIRE(d->R * d->S <= kWTap, "conv wgrad: at most %d taps", kWTap);
     GM_REQUIRE(ilog2w(d->C) >= 3, "conv wgrad: C must be a power of two >= 8");
     GM_REQUIRE(d->K % 8 == 0, "conv wgrad: K must be a multiple of 8");
     GM_REQUIRE(c_real >= 1 && c_real <= d->C, "conv wgrad: bad c_real");
-    const size_t need = gm_conv2d_wgrad_hw_scratch(d);
+    const size_t slab_c = (size_t)d->K * d->R * d->S * (size_t)c_real;
+    GM_REQUIRE(G == 1 || (dw_stride >= (long long)slab_c || dw_stride <= -(long long)slab_c),
+               "conv wgrad: group gradient stride %lld overlaps one gradient", dw_stride);
+    const size_t need = gm_conv2d_wgrad_grouped_scratch(d, G);
     GM_REQUIRE(scratch && scratch_bytes >= need, "conv wgrad: scratch %zu < %zu", scratch_bytes, need);
     WgradArgs a;
     memset(&a, 0, sizeof(a));
-    const WPlan w = plan(d);
+    const WPlan w = plan(d, G);
     a.P = w.P; a.Q = w.Q; a.tiles_k = w.tiles_k; a.tiles_n = w.tiles_n;
     a.splits = w.splits; a.steps_per_split = w.sps;
     a.dy = (const uint16_t*)dy;
@@ -602,6 +623,10 @@ extern "C" int gm_conv2d_wgrad_hw_bf16(const gm_conv_desc_hw* d, const void* dy,
     a.Kc = d->K; a.T = d->R * d->S; a.sth = d->stride_h; a.stw = d->stride_w;
     a.fd_pq = FastDiv((uint32_t)(a.P * a.Q));
     a.fd_q = FastDiv((uint32_t)a.Q);
+    a.G = G;
+    a.gs_dy = (long long)d->N * w.P * w.Q * d->K;
+    a.gs_x = (long long)d->N * d->H * d->W * d->C;
+    a.gs_part = (long long)w.splits * d->K * a.T * d->C;
     a.adv_b = 64 / (a.P * a.Q);
     a.adv_p = (64 % (a.P * a.Q)) / a.Q;
     a.adv_q = (64 % (a.P * a.Q)) % a.Q;
@@ -611,12 +636,13 @@ extern "C" int gm_conv2d_wgrad_hw_bf16(const gm_conv_desc_hw* d, const void* dy,
             a.dw[r * d->S + s] = (signed char)(s - d->pad_w);
         }
     hipStream_t st = as_stream(stream);
-    const int grid = a.tiles_k * a.tiles_n * a.splits;
+    const int grid = a.tiles_k * a.tiles_n * a.splits * G;
     int rc;
     if (wgrad_version() >= 2) {
         const bool direct = a.splits == 1 && c_real == d->C;
         if (direct) {
             a.part = dw;
+            a.gs_part = dw_stride;
             a.accumulate = accumulate;
         }
         a.S = d->S;
@@ -641,22 +667,30 @@ extern "C" int gm_conv2d_wgrad_hw_bf16(const gm_conv_desc_hw* d, const void* dy,
         const size_t ncol = slab / 4;
         int R = 1;  // split lanes per column: aim for >= 512 blocks without idle lanes
         while (R < 32 && R * 2 <= a.splits && (ncol * R + 255) / 256 < 512) R *= 2;
-        const unsigned g = (unsigned)((ncol + 256 / R - 1) / (256 / R));
+        const dim3 g((unsigned)((ncol + 256 / R - 1) / (256 / R)), (unsigned)G);
+        const long long gs = dw_stride;
         switch (R) {
-            case 1: k_wgrad_sum<1><<<g, 256, 0, st>>>(a.part, a.splits, slab, accumulate, dw); break;
-            case 2: k_wgrad_sum<2><<<g, 256, 0, st>>>(a.part, a.splits, slab, accumulate, dw); break;
-            case 4: k_wgrad_sum<4><<<g, 256, 0, st>>>(a.part, a.splits, slab, accumulate, dw); break;
-            case 8: k_wgrad_sum<8><<<g, 256, 0, st>>>(a.part, a.splits, slab, accumulate, dw); break;
-            case 16: k_wgrad_sum<16><<<g, 256, 0, st>>>(a.part, a.splits, slab, accumulate, dw); break;
-            default: k_wgrad_sum<32><<<g, 256, 0, st>>>(a.part, a.splits, slab, accumulate, dw); break;
+            case 1: k_wgrad_sum<1><<<g, 256, 0, st>>>(a.part, a.splits, slab, accumulate, dw, gs); break;
+            case 2: k_wgrad_sum<2><<<g, 256, 0, st>>>(a.part, a.splits, slab, accumulate, dw, gs); break;
+            case 4: k_wgrad_sum<4><<<g, 256, 0, st>>>(a.part, a.splits, slab, accumulate, dw, gs); break;
+            case 8: k_wgrad_sum<8><<<g, 256, 0, st>>>(a.part, a.splits, slab, accumulate, dw, gs); break;
+            case 16: k_wgrad_sum<16><<<g, 256, 0, st>>>(a.part, a.splits, slab, accumulate, dw, gs); break;
+            default: k_wgrad_sum<32><<<g, 256, 0, st>>>(a.part, a.splits, slab, accumulate, dw, gs); break;
         }
         return check_launch("k_wgrad_sum");
     }
     const size_t n = (size_t)d->K * a.T * c_real;
     int g = (int)((n + 255) / 256);
     if (g > 4096) g = 4096;
-    k_wgrad_reduce<<<g, 256, 0, st>>>(a.part, a.splits, d->K, a.T, d->C, c_real, accumulate, dw);
+    k_wgrad_reduce<<<dim3(g, G), 256, 0, st>>>(a.part, a.splits, d->K, a.T, d->C, c_real, accumulate, dw,
+                                               dw_stride);
     return check_launch("k_wgrad_reduce");
+}
+
+extern "C" int gm_conv2d_wgrad_hw_bf16(const gm_conv_desc_hw* d, const void* dy, const void* x, float* dw,
+                                       int c_real, int accumulate, void* scratch, size_t scratch_bytes,
+                                       void* stream) {
+    return gm_conv2d_wgrad_grouped_bf16(d, 1, dy, x, dw, 0, c_real, accumulate, scratch, scratch_bytes, stream);
 }
 
 extern "C" int gm_conv_set_wgrad_wide(int mode) {

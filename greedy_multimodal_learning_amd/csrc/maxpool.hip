@@ -26,6 +26,7 @@ struct PoolArgs {
     int N, H, W, C8;  // C8 = C / 8 (16-byte channel groups)
     int P, Q, k, s, pad;
     FastDiv fd_c8, fd_q, fd_p, fd_w, fd_h, fd_s;  // index decode without integer division
+    FastDiv fd_ng;  // images per view group (BNRELU: group g = n / Ng reads coef + g*2C)
 };
 
 // BNRELU: the pooled values are relu(x*sc + sh) rounded to E, i.e. the stem's BatchNorm +
@@ -48,8 +49,9 @@ __global__ __launch_bounds__(256) void k_maxpool_fwd(PoolArgs a, const void* __r
         uint32_t ix[8];
         float sc[8], sh[8];
         if (BNRELU) {
-            const float4* c4 = reinterpret_cast<const float4*>(coef + cg * 8);
-            const float4* s4 = reinterpret_cast<const float4*>(coef + a.C8 * 8 + cg * 8);
+            const float* cf = coef + (size_t)a.fd_ng.div((unsigned)n) * (a.C8 * 16);
+            const float4* c4 = reinterpret_cast<const float4*>(cf + cg * 8);
+            const float4* s4 = reinterpret_cast<const float4*>(cf + a.C8 * 8 + cg * 8);
             const float4 c0 = c4[0], c1 = c4[1], s0 = s4[0], s1 = s4[1];
             sc[0] = c0.x; sc[1] = c0.y; sc[2] = c0.z; sc[3] = c0.w; sc[4] = c1.x; sc[5] = c1.y; sc[6] = c1.z; sc[7] = c1.w;
             sh[0] = s0.x; sh[1] = s0.y; sh[2] = s0.z; sh[3] = s0.w; sh[4] = s1.x; sh[5] = s1.y; sh[6] = s1.z; sh[7] = s1.w;
@@ -211,6 +213,7 @@ int prep(const gm_pool_desc* d, PoolArgs& a, const char* fn) {
     a.fd_w = FastDiv((uint32_t)a.W);
     a.fd_h = FastDiv((uint32_t)a.H);
     a.fd_s = FastDiv((uint32_t)a.s);
+    a.fd_ng = FastDiv((uint32_t)a.N);
     return GM_OK;
 }
 
@@ -253,17 +256,28 @@ extern "C" int gm_maxpool2d_fwd_bf16(const gm_pool_desc* d, const void* x, void*
     return pool_fwd<uint16_t>(d, x, y, idx, stream, "gm_maxpool2d_fwd_bf16");
 }
 
-extern "C" int gm_bn_relu_maxpool2d_fwd_bf16(const gm_pool_desc* d, const void* x, const float* coef, void* y,
-                                             void* idx, void* stream) {
-    const char* fn = "gm_bn_relu_maxpool2d_fwd_bf16";
+// G view groups of d->N images each, stacked along the batch; group g applies the
+// coefficients coef + g*2C
+extern "C" int gm_bn_relu_maxpool2d_fwd_grouped_bf16(const gm_pool_desc* d, int G, const void* x, const float* coef,
+                                                     void* y, void* idx, void* stream) {
+    const char* fn = "gm_bn_relu_maxpool2d_fwd_grouped_bf16";
+    GM_REQUIRE(d && G >= 1 && G <= 64, "%s: 1..64 groups", fn);
+    gm_pool_desc dg = *d;
+    dg.N = d->N * G;
     PoolArgs a;
-    int rc = prep(d, a, fn);
+    int rc = prep(&dg, a, fn);
     if (rc) return rc;
+    a.fd_ng = FastDiv((uint32_t)d->N);
     GM_REQUIRE(x && coef && y && idx, "%s: null pointer", fn);
     const long long n = (long long)a.N * a.P * a.Q * a.C8;
     hipLaunchKernelGGL((k_maxpool_fwd<uint16_t, true>), dim3(grid_for(n)), dim3(256), 0, as_stream(stream), a, x, y,
                        static_cast<uint2*>(idx), coef);
     return check_launch("k_maxpool_fwd<bnrelu>");
+}
+
+extern "C" int gm_bn_relu_maxpool2d_fwd_bf16(const gm_pool_desc* d, const void* x, const float* coef, void* y,
+                                             void* idx, void* stream) {
+    return gm_bn_relu_maxpool2d_fwd_grouped_bf16(d, 1, x, coef, y, idx, stream);
 }
 
 extern "C" int gm_maxpool2d_bwd_bf16(const gm_pool_desc* d, const void* dy, const void* idx, void* dx, void* stream) {

@@ -226,6 +226,9 @@ class BalancedStep:
         if self.device.type == "cuda" and streams_enabled():
             for i in range(int(getattr(model, "num_views", 2)) - 1):
                 side_stream(self.device, i)  # created up front: the DP buckets wait on them
+        if self.device.type == "cuda":
+            from . import vtrunk
+            vtrunk._wgrad_stream(self.device)  # (the stacked trunk's weight-gradient stream, likewise)
         self.norms = GroupNorms(named, list(branchnames), list(MMTMnames))
         if gate is not None:
             gate.set_model(model, ignore=False)
@@ -321,6 +324,10 @@ class BalancedStep:
         from . import _lib as L
         views = int(getattr(model, "num_views", 2))
         streams = views if streams_enabled() else 1
+        from . import vtrunk
+        if vtrunk.ENABLED and hasattr(model, "_forward_stacked") and self.compute_dtype == torch.bfloat16:
+            # the view-batched trunk: grouped launches on one stream (+ its weight gradients)
+            streams = 2 if vtrunk.WGRAD_STREAM else 1
         sharers, reserved = 1, 0
         if self.pg is not None and self.world > 1:
             import socket

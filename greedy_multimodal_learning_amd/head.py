@@ -68,8 +68,15 @@ def _grad_buf(prm, shape, want):
 
 class _PooledLinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, nb, *args):
+    def forward(ctx, nb, stacked, *args):
+        """stacked: args end with ONE [nb*B, C, H, W] tensor (the view-batched trunk's,
+        branch i = rows i*B..), whose gradient then comes back as one tensor."""
         ws, bs, fs = args[:nb], args[nb:2 * nb], args[2 * nb:]
+        ctx.stacked = stacked
+        if stacked:
+            X = fs[0]
+            Bs = X.shape[0] // nb
+            fs = [X[i * Bs:(i + 1) * Bs] for i in range(nb)]
         B, C, H, W = fs[0].shape
         HW = H * W
         N = ws[0].shape[0]
@@ -84,7 +91,7 @@ class _PooledLinearFn(torch.autograd.Function):
                        ld_c=N, bias=bs[i].detach()) for i in range(nb)], dev)
         ctx.nb, ctx.shape, ctx.lay, ctx.dt = nb, (B, C, H, W), lay, dt
         ctx.params = list(ws) + list(bs)
-        ctx.save_for_backward(pooled, *ws, *fs)
+        ctx.save_for_backward(pooled, *ws, *(args[2 * nb:] if stacked else fs))
         return tuple(logits[i] for i in range(nb))
 
     @staticmethod
@@ -93,6 +100,10 @@ class _PooledLinearFn(torch.autograd.Function):
         pooled, rest = ctx.saved_tensors[0], ctx.saved_tensors[1:]
         ws, fs = rest[:nb], rest[nb:]
         B, C, H, W = ctx.shape
+        gX = None
+        if ctx.stacked:
+            X = fs[0]
+            fs = [X[i * B:(i + 1) * B] for i in range(nb)]
         HW = H * W
         N = ws[0].shape[0]
         dev = pooled.device
@@ -102,8 +113,8 @@ class _PooledLinearFn(torch.autograd.Function):
         probs, sunk = [], []
         gw, gb, dp = [None] * nb, [None] * nb, {}
         for i in live:
-            w_t, w_acc, w_s = _grad_buf(ctx.params[i], (N, C), need[1 + i])
-            b_t, b_acc, b_s = _grad_buf(ctx.params[nb + i], (N,), need[1 + nb + i])
+            w_t, w_acc, w_s = _grad_buf(ctx.params[i], (N, C), need[2 + i])
+            b_t, b_acc, b_s = _grad_buf(ctx.params[nb + i], (N,), need[2 + nb + i])
             if w_t is not None:  # dW[n,c] = sum_b dl[b,n] pooled[b,c]
                 probs.append(dict(M=N, N=C, segs=[(B, ops.Op(dl[i], 1, N), ops.Op(pooled[i], C, 1))], C=w_t,
                                   ld_c=C, accumulate=int(w_acc)))
@@ -118,31 +129,48 @@ class _PooledLinearFn(torch.autograd.Function):
                     sunk.append(ctx.params[nb + i])
                 else:
                     gb[i] = b_t
-            if need[1 + 2 * nb + i]:  # d_pooled[b,c] = sum_n dl[b,n] W[n,c]
+            if need[2 + 2 * nb + (0 if ctx.stacked else i)]:  # d_pooled[b,c] = sum_n dl[b,n] W[n,c]
                 dp[i] = torch.empty(B, C, device=dev, dtype=torch.float32)
                 probs.append(dict(M=B, N=C, segs=[(N, ops.Op(dl[i], N, 1), ops.Op(ws[i].detach(), C, 1))],
                                   C=dp[i], ld_c=C))
         if probs:
             ops.gemm(probs, dev)
         gf = [None] * nb
+        if ctx.stacked and dp:
+            gX = torch.empty_like(ctx.saved_tensors[-1],
+                                  memory_format=CL if ctx.lay == L.GM_NHWC else torch.contiguous_format)
+            for i in range(nb):
+                if i not in dp:  # a branch without a logits gradient: its rows get zeros
+                    gX[i * B:(i + 1) * B].zero_()
         if dp:
             zero = zero_row(dev, C)
             sc = []
             for i, d in dp.items():
-                gf[i] = torch.empty_like(fs[i], memory_format=CL if ctx.lay == L.GM_NHWC else torch.contiguous_format)
+                gf[i] = gX[i * B:(i + 1) * B] if gX is not None else torch.empty_like(
+                    fs[i], memory_format=CL if ctx.lay == L.GM_NHWC else torch.contiguous_format)
                 # df = 0 * f + d_pooled / HW (the mean's gradient broadcast over the map)
                 sc.append(dict(x=fs[i], y=gf[i], C=C, HW=HW, s=zero, ld_s=0, a=d, ld_a=C, alpha=1.0 / HW))
             ops.channel_scale(sc, B, ctx.dt, ctx.lay, dev)
         for prm in sunk:
             sink_done(prm)
-        return (None, *gw, *gb, *gf)
+        if ctx.stacked:
+            return (None, None, *gw, *gb, gX)
+        return (None, None, *gw, *gb, *gf)
 
 
 def pooled_linear(fs, fcs):
     """Logits (fp32 [B, N]) of every branch: fc_i(flatten(avgpool(f_i)))."""
     nb = len(fs)
     with torch.autocast("cuda", enabled=False):
-        return list(_PooledLinearFn.apply(nb, *[fc.weight for fc in fcs], *[fc.bias for fc in fcs], *fs))
+        return list(_PooledLinearFn.apply(nb, False, *[fc.weight for fc in fcs], *[fc.bias for fc in fcs], *fs))
+
+
+def pooled_linear_stacked(X, fcs):
+    """pooled_linear over the view-batched trunk's stacked map X ([nb*B, C, H, W]): same
+    logits, one stacked input gradient."""
+    nb = len(fcs)
+    with torch.autocast("cuda", enabled=False):
+        return list(_PooledLinearFn.apply(nb, True, *[fc.weight for fc in fcs], *[fc.bias for fc in fcs], X))
 
 
 class _XentFn(torch.autograd.Function):

@@ -15,7 +15,8 @@ import torch.nn as nn
 from .balanced_mmtm import MMTM_mitigate as MMTM
 from .balanced_mmtm import get_rescale_weights
 from .gin_lite import configurable
-from .head import head_ok, pooled_linear
+from . import vtrunk
+from .head import head_ok, pooled_linear, pooled_linear_stacked
 from .resnet import resnet18
 from .streams import ViewStreams
 
@@ -71,7 +72,35 @@ class MMTM_MVCNN(nn.Module):
             return None
         return pooled_linear(fs, fcs)
 
+    def _forward_stacked(self, x, curation_mode, caring_modality):
+        """The two trunks as ONE view-batched trunk (vtrunk.py): every convolution /
+        BatchNorm position is one grouped launch over [x0; x1], the MMTM sites and the
+        heads read and write the stacked activation."""
+        nets = [self.net_view_0, self.net_view_1]
+        X = vtrunk.vstem(x, nets)
+        X = vtrunk.vlayer(nets, 1, X)
+        scales, squeezed = [], []
+        for i in (2, 3, 4):
+            X = vtrunk.vlayer(nets, i, X)
+            X, sc, sq = getattr(self, f"mmtm{i}").forward_stacked(
+                X, self.saving_mmtm_scales, self.saving_mmtm_squeeze_array,
+                turnoff_cross_modal_flow=bool(self.mmtm_off),
+                average_squeezemaps=self.mmtm_rescale[i - 1] if self.mmtm_off else None,
+                curation_mode=curation_mode, caring_modality=caring_modality)
+            scales.append(sc)
+            squeezed.append(sq)
+        B = X.shape[0] // 2
+        if head_ok([X[:B], X[B:]], [n.fc for n in nets]) and all(
+                isinstance(n.avgpool, nn.AdaptiveAvgPool2d) and n.avgpool.output_size in ((1, 1), 1) for n in nets):
+            x0, x1 = pooled_linear_stacked(X, [n.fc for n in nets])
+        else:
+            x0, x1 = self._head(nets[0], X[:B]), self._head(nets[1], X[B:])
+        mean = None if getattr(self, "_no_mean", False) else (x0 + x1) / 2
+        return mean, [x0, x1], scales, squeezed
+
     def forward(self, x, curation_mode=False, caring_modality=None):
+        if vtrunk.usable(self, [self.net_view_0, self.net_view_1], x):
+            return self._forward_stacked(x, curation_mode, caring_modality)
         # view 1's trunk segments run on a side HIP stream (streams.py): the two
         # trunks only meet at the MMTM sites, which run on the main stream
         vs = ViewStreams.for_tensor(x, 2)

@@ -1,0 +1,537 @@
+"""View-batched trunk: the G unshared ResNet trunks of the multi-view model as ONE stacked trunk.
+
+The reference runs its two view trunks one after the other (src/model.py:65-106: `net_view_0`
+then `net_view_1`, torchvision resnet18 pieces, MMTM after layer2/3/4).  The trunks have
+identical shapes and different weights, so on MI355X every convolution / BatchNorm of a
+block position is ONE launch over both views: the activations are stacked along the batch
+([G*B, C, H, W] channels_last bf16, view g = rows g*B .. (g+1)*B-1) and each kernel takes
+the G weights (or the G parameter / statistic sets) of that position:
+
+    conv fwd / dgrad : gm_conv2d_{fwd,dgrad}_grouped_bf16 (weight g at wb + g*stride)
+    conv wgrad       : gm_conv2d_wgrad_grouped_bf16 (dW g at grad + g*stride: the engine's
+                       flat gradient buffer lays the views' parameters out at one stride)
+    BatchNorm        : gm_bn_{fwd_train,bwd,fwd_stats}_grouped_bf16 (per-view statistics,
+                       running stats, num_batches_tracked: exactly the per-view modules')
+    stem pool        : gm_bn_relu_maxpool2d_fwd_grouped_bf16
+
+Layer 3/4 grids of one view (B = 64: 49-196 output tiles) leave most of the 256 CUs idle;
+stacked, the launch count halves and each grid doubles.  The arithmetic per view is the
+per-view trunk's (same kernels, same tile order within a view): the stacked trunk is
+checked against the per-view trunk in tests/test_gpu_vtrunk.py.
+
+The modules stay what they are (`net_view_i.layer*.conv*` / `bn*` parameters, buffers,
+state_dict); this executor only reads them.  Training-mode bf16 only; everything else
+takes the per-view path (model.MMTM_MVCNN.forward decides).
+"""
+import contextlib
+import ctypes
+import os
+
+import torch
+
+from . import _lib as L
+from .bn import MASK_FROM_X
+from .conv import CL, _cpad, _desc, _desc_hw, _like_param, _prepped, _splitk_ws, _stem_geom, stem_pack
+from .gradsink import GradJoin, sink_done, sink_target
+
+BF = torch.bfloat16
+ENABLED = os.environ.get("GM_VTRUNK", "1") != "0"
+
+
+def _nhwc(t):
+    return t if t.is_contiguous(memory_format=CL) else t.contiguous(memory_format=CL)
+
+
+def _stride(ts, elem_bytes):
+    """Element stride between consecutive tensors' storage if it is one constant (0 for a
+    single tensor; negative when the later views sit lower, as in the engine's flat buffer,
+    which is laid out in reverse registration order), else None."""
+    if len(ts) < 2:
+        return 0
+    d = ts[1].data_ptr() - ts[0].data_ptr()
+    if d == 0 or d % elem_bytes:
+        return None
+    for a, b in zip(ts[1:], ts[2:]):
+        if b.data_ptr() - a.data_ptr() != d:
+            return None
+    return d // elem_bytes
+
+
+def _splitk_g(device, d, G, dgrad):
+    """Split-K workspace (shared with the per-view convolutions: its turnstile words sit in
+    a fixed region, so one zeroed buffer per stream serves both)."""
+    need = L.load().gm_conv2d_splitk_ws_bytes_grouped(ctypes.byref(d), G, int(dgrad))
+    if need == 0:
+        return 0, 0
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    key = (idx, torch.cuda.current_stream(idx).stream_id)
+    buf = _splitk_ws.get(key)
+    if buf is None or buf.numel() < need:
+        buf = torch.zeros((need + (1 << 20) - 1) >> 20 << 20, device=device, dtype=torch.uint8)
+        _splitk_ws[key] = buf
+    return buf.data_ptr(), buf.numel()
+
+
+_bn_scratch = {}
+
+
+def _bn_scratch_g(device, M, C, G):
+    """Grouped-layout BatchNorm scratch per (device, stream), zeroed once (its ticket words
+    sit in fixed per-group headers: never shared with the ungrouped calls' buffers)."""
+    need = L.load().gm_bn_scratch_grouped(M, C, G)
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    key = (idx, torch.cuda.current_stream(idx).stream_id)
+    buf = _bn_scratch.get(key)
+    if buf is None or buf.numel() < need:
+        size = max(need, 1 << 20) if buf is None else max(need, 2 * buf.numel())
+        buf = torch.zeros(size, device=device, dtype=torch.uint8)
+        _bn_scratch[key] = buf
+    return buf
+
+
+@L.on_fault_reset
+def _reset_bn_scratch():
+    for buf in _bn_scratch.values():
+        buf.zero_()
+    torch.cuda.synchronize()
+
+
+# ---- convolution -------------------------------------------------------------------
+
+WGRAD_STREAM = os.environ.get("GM_WGRAD_STREAM", "1") != "0"
+_WGRAD_SIDE = 64  # streams.side_stream index of the weight-gradient stream
+
+
+def _wgrad_stream(dev):
+    if not WGRAD_STREAM or dev.type != "cuda":
+        return None
+    from .streams import side_stream
+    return side_stream(dev, _WGRAD_SIDE)
+
+
+def _group_weights(weights, Cp, need_t):
+    """bf16 KRSC copies of the G weights at one stride: the step's WeightPrep copies when
+    they are laid out that way (the engine's), else a fresh stacked prep.  Returns
+    (wb, wb_stride, wt, wt_stride) with wb / wt the group-0 tensors."""
+    pre = [_prepped.get(w.data_ptr()) for w in weights] if _prepped else [None]
+    if all(p is not None and (p[1] is not None or not need_t) for p in pre):
+        wbs, wts = [p[0] for p in pre], [p[1] for p in pre]
+        sb = _stride(wbs, 2)
+        st = _stride(wts, 2) if need_t else 0
+        n = wbs[0].numel()
+        if sb is not None and st is not None and (len(wbs) == 1 or (abs(sb) >= n and (not need_t or abs(st) >= n))):
+            return wbs[0], sb, wts[0], st
+    lib = L.load()
+    G = len(weights)
+    K, C, R, S = weights[0].shape
+    dev = weights[0].device
+    wb = torch.empty(G, K, R, S, Cp, device=dev, dtype=BF)
+    wt = torch.empty(G, Cp, R, S, K, device=dev, dtype=BF) if need_t else None
+    for g, w in enumerate(weights):
+        w32 = _nhwc(w.detach().float())
+        L.check(lib.gm_conv_weight_prep_bf16(w32.data_ptr(), K, R * S, C, Cp, wb[g].data_ptr(),
+                                             wt[g].data_ptr() if need_t else 0, L.stream_of(dev)),
+                "gm_conv_weight_prep_bf16")
+    n = K * R * S * Cp
+    return wb[0], n, (wt[0] if need_t else None), n
+
+
+class _VConvFn(torch.autograd.Function):
+    """y = conv(X_g, W_g) for every view group g of the stacked X, one launch per pass."""
+
+    @staticmethod
+    def forward(ctx, X, G, stride, pad, join, *weights):
+        lib = L.load()
+        ctx.join = join
+        GN, C, H, W = X.shape
+        N = GN // G
+        K, C0, R, S = weights[0].shape
+        if C != C0 or _cpad(C) != C or GN != N * G:
+            raise L.GreedyMMLError(f"vtrunk conv: stacked input {tuple(X.shape)} does not fit {G} x {C0} channels")
+        xb = _nhwc(X.to(BF))
+        need_dx = ctx.needs_input_grad[0]
+        wb, sb, wt, st = _group_weights(weights, C, need_dx)
+        P = (H + 2 * pad - R) // stride + 1
+        Q = (W + 2 * pad - S) // stride + 1
+        y = torch.empty(GN, K, P, Q, device=X.device, dtype=BF, memory_format=CL)
+        d = _desc_hw(N, H, W, C, K, R, S, stride, stride, pad, pad)
+        ws, nb = _splitk_g(X.device, _desc(N, H, W, C, K, R, S, stride, pad), G, False)
+        L.check(lib.gm_conv2d_fwd_grouped_bf16(ctypes.byref(d), G, xb.data_ptr(), wb.data_ptr(), sb, y.data_ptr(),
+                                               ws, nb, L.stream_of(X.device)), "gm_conv2d_fwd_grouped_bf16")
+        ctx.save_for_backward(xb, wt, *weights)
+        ctx.meta = (G, N, stride, pad, st)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        lib = L.load()
+        xb, wt, *weights = ctx.saved_tensors
+        G, N, stride, pad, st = ctx.meta
+        GN, C, H, W = xb.shape
+        K, _, R, S = weights[0].shape
+        gy = _nhwc(gy.to(BF))
+        dev = gy.device
+        dx = None
+        if ctx.needs_input_grad[0]:
+            d = _desc(N, H, W, C, K, R, S, stride, pad)
+
+            def dgrad(add):
+                if add is not None and (tuple(add.shape) != (GN, C, H, W) or add.dtype != BF
+                                        or not add.is_contiguous(memory_format=CL)):
+                    raise ValueError("vtrunk conv dgrad: addend must be bf16 channels_last shaped like dx")
+                out = add if add is not None else torch.empty(GN, C, H, W, device=dev, dtype=BF, memory_format=CL)
+                ws, nb = _splitk_g(dev, d, G, True)
+                L.check(lib.gm_conv2d_dgrad_grouped_bf16(ctypes.byref(d), G, gy.data_ptr(), wt.data_ptr(), st,
+                                                         out.data_ptr(), L.ptr(add), ws, nb, L.stream_of(dev)),
+                        "gm_conv2d_dgrad_grouped_bf16")
+                return out
+            dx = ctx.join.contribute(dgrad) if ctx.join is not None else dgrad(None)
+        grads = [None] * G
+        want = [ctx.needs_input_grad[5 + g] for g in range(G)]
+        if any(want):
+            dh = _desc_hw(N, H, W, C, K, R, S, stride, stride, pad, pad)
+            tg = [sink_target(w) if wn else None for w, wn in zip(weights, want)]
+            need = lib.gm_conv2d_wgrad_grouped_scratch(ctypes.byref(dh), G)
+            scratch = torch.empty(max(need, 16), device=dev, dtype=torch.uint8)
+            sunk = all(t is not None for t in tg)
+            if sunk:
+                bufs = [t[0] for t in tg]
+                sd = _stride(bufs, 4)
+                if (sd is None or len({t[1] for t in tg}) != 1 or (G > 1 and abs(sd) < bufs[0].numel())
+                        or not all(b.is_contiguous(memory_format=CL) for b in bufs)):
+                    raise RuntimeError("vtrunk conv: the views' gradient buffers must be channels_last, one "
+                                       "accumulate state, at one stride (the engine's flat layout)")
+                # the weight gradient is off the critical path (only the step's end reads it):
+                # it runs on the wgrad stream, overlapping the next input-gradient launches;
+                # the engine joins the side streams before the gradients are read
+                side = _wgrad_stream(dev)
+                if side is not None:
+                    side.wait_stream(torch.cuda.current_stream(dev))
+                    gy.record_stream(side)
+                    xb.record_stream(side)
+                    scratch.record_stream(side)
+                with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+                    L.check(lib.gm_conv2d_wgrad_grouped_bf16(ctypes.byref(dh), G, gy.data_ptr(), xb.data_ptr(),
+                                                             bufs[0].data_ptr(), sd, C, int(tg[0][1]),
+                                                             scratch.data_ptr(), need, L.stream_of(dev)),
+                            "gm_conv2d_wgrad_grouped_bf16")
+                for w in weights:
+                    sink_done(w)
+            else:
+                if any(t is not None for t in tg):
+                    raise RuntimeError("vtrunk conv: all or none of the views' weights must be sink-managed")
+                dw = torch.empty(G, K, R, S, C, device=dev, dtype=torch.float32)
+                L.check(lib.gm_conv2d_wgrad_grouped_bf16(ctypes.byref(dh), G, gy.data_ptr(), xb.data_ptr(),
+                                                         dw.data_ptr(), K * R * S * C, C, 0, scratch.data_ptr(),
+                                                         need, L.stream_of(dev)), "gm_conv2d_wgrad_grouped_bf16")
+                grads = [_like_param(dw[g].permute(0, 3, 1, 2), w) if wn else None
+                         for g, (w, wn) in enumerate(zip(weights, want))]
+        return (dx, None, None, None, None, *grads)
+
+
+def vconv(X, convs, join=None):
+    """The G GMConv2d modules `convs` (one per view, same shape) over the stacked X."""
+    c0 = convs[0]
+    if not c0._hip_ok():
+        raise L.GreedyMMLError("vtrunk conv: only the ResNet trunk's convolutions")
+    if join is not None and X.requires_grad and torch.is_grad_enabled():
+        join.register()
+    else:
+        join = None
+    with torch.autocast("cuda", enabled=False):
+        return _VConvFn.apply(X, len(convs), c0.stride[0], c0.padding[0], join, *[c.weight for c in convs])
+
+
+# ---- BatchNorm ---------------------------------------------------------------------
+
+def _bn_param_grads(gammas, betas, want_w, want_b):
+    """Per-view (dgamma, dbeta) buffers: the sink targets when the engine armed them (one
+    accumulate state for all views), else fresh.  Returns (dgs, dbs, acc, sunk)."""
+    G = len(gammas)
+    tw = [sink_target(w) for w in gammas] if want_w and want_b else []
+    tb = [sink_target(b) for b in betas] if want_w and want_b else []
+    if tw and all(t is not None for t in tw + tb):
+        accs = {t[1] for t in tw + tb}
+        if len(accs) != 1:
+            raise RuntimeError("vtrunk BatchNorm: the views' parameters must share one gradient sink state")
+        return [t[0] for t in tw], [t[0] for t in tb], accs.pop(), True
+    if any(t is not None for t in tw + tb):
+        raise RuntimeError("vtrunk BatchNorm: all or none of the views' parameters must be sink-managed")
+    C = gammas[0].shape[0]
+    dev = gammas[0].device
+    return ([torch.empty(C, device=dev, dtype=torch.float32) for _ in range(G)],
+            [torch.empty(C, device=dev, dtype=torch.float32) for _ in range(G)], False, False)
+
+
+def _bn_backward(dz, y, xb, G, gammas, betas, sm, si, relu, want_dres, coef, want_w, want_b):
+    """Grouped BN backward; returns (dx, dres, grads_w[G], grads_b[G])."""
+    lib = L.load()
+    GN, C, H, W = xb.shape
+    M = (GN // G) * H * W
+    dz = _nhwc(dz.to(BF))
+    dx = torch.empty_like(xb, memory_format=CL)
+    dres = torch.empty_like(xb, memory_format=CL) if want_dres else None
+    dgs, dbs, acc, sunk = _bn_param_grads(gammas, betas, want_w, want_b)
+    descs = []
+    for g in range(G):
+        r = slice(g * (GN // G), (g + 1) * (GN // G))
+        descs.append(L.BnBwd(M, C, int(relu), dz[r].data_ptr(), y[r].data_ptr() if (relu and y is not None) else 0,
+                             xb[r].data_ptr(), gammas[g].data_ptr(), sm[g].data_ptr(), si[g].data_ptr(),
+                             dx[r].data_ptr(), dres[r].data_ptr() if dres is not None else 0, dgs[g].data_ptr(),
+                             dbs[g].data_ptr(), int(acc), 0, coef[g].data_ptr() if coef is not None else 0))
+    buf = _bn_scratch_g(xb.device, M, C, G)
+    L.check(lib.gm_bn_bwd_grouped_bf16(L.arr(L.BnBwd, descs), G, buf.data_ptr(), buf.numel(),
+                                       L.stream_of(xb.device)), "gm_bn_bwd_grouped_bf16")
+    if sunk:
+        for p in list(gammas) + list(betas):
+            sink_done(p)
+        return dx, dres, [None] * G, [None] * G
+    return dx, dres, [d if want_w else None for d in dgs], [d if want_b else None for d in dbs]
+
+
+class _VBNFn(torch.autograd.Function):
+    """relu?(BatchNorm_g(X_g) (+ residual_g)) per view group g of the stacked X."""
+
+    @staticmethod
+    def forward(ctx, X, residual, G, bns, relu, join, *params):
+        lib = L.load()
+        ctx.join = join
+        gammas, betas = params[:G], params[G:]
+        xb = _nhwc(X.to(BF))
+        GN, C, H, W = xb.shape
+        N = GN // G
+        M = N * H * W
+        if residual is not None:
+            residual = _nhwc(residual.to(BF))
+        maskx = relu and residual is None and MASK_FROM_X
+        y = torch.empty_like(xb, memory_format=CL)
+        dev = xb.device
+        sm = torch.empty(G, C, device=dev, dtype=torch.float32)
+        si = torch.empty(G, C, device=dev, dtype=torch.float32)
+        coef = torch.empty(G, 2 * C, device=dev, dtype=torch.float32) if maskx else None
+        descs = []
+        for g, bn in enumerate(bns):
+            r = slice(g * N, (g + 1) * N)
+            descs.append(L.BnFwd(M, C, int(relu), xb[r].data_ptr(),
+                                 residual[r].data_ptr() if residual is not None else 0, y[r].data_ptr(),
+                                 gammas[g].data_ptr(), betas[g].data_ptr(), L.ptr(bn.running_mean),
+                                 L.ptr(bn.running_var), float(bn.momentum), float(bn.eps), sm[g].data_ptr(),
+                                 si[g].data_ptr(), L.ptr(bn.num_batches_tracked),
+                                 coef[g].data_ptr() if maskx else 0))
+        buf = _bn_scratch_g(dev, M, C, G)
+        L.check(lib.gm_bn_fwd_train_grouped_bf16(L.arr(L.BnFwd, descs), G, buf.data_ptr(), buf.numel(),
+                                                 L.stream_of(dev)), "gm_bn_fwd_train_grouped_bf16")
+        ctx.save_for_backward(xb, y if relu and not maskx else coef, sm, si, *gammas, *betas)
+        ctx.meta = (G, maskx, relu, residual is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xb, yc, sm, si, *prm = ctx.saved_tensors
+        G, maskx, relu, has_res = ctx.meta
+        gammas, betas = prm[:G], prm[G:]
+        y, coef = (None, yc) if maskx else (yc, None)
+        want_dres = has_res and ctx.needs_input_grad[1]
+        dx, dres, gw, gb = _bn_backward(dy, y, xb, G, gammas, betas, sm, si, relu, want_dres, coef,
+                                        any(ctx.needs_input_grad[6:6 + G]), any(ctx.needs_input_grad[6 + G:]))
+        if dres is not None and ctx.join is not None:
+            dres = ctx.join.contribute(lambda add: dres if add is None else dres + add)
+        return (dx if ctx.needs_input_grad[0] else None, dres, None, None, None, None, *gw, *gb)
+
+
+def vbn(X, bns, residual=None, relu=False, residual_join=None):
+    """The G GMBatchNorm2d modules `bns` (training mode) over the stacked X."""
+    b0 = bns[0]
+    if any(b.momentum is None or b.momentum != b0.momentum or b.eps != b0.eps for b in bns):
+        raise L.GreedyMMLError("vtrunk BatchNorm: the views must share momentum and eps")
+    join = None
+    if residual_join is not None and residual is not None and residual.requires_grad and torch.is_grad_enabled():
+        residual_join.register()
+        join = residual_join
+    with torch.autocast("cuda", enabled=False):
+        return _VBNFn.apply(X, residual, len(bns), bns, bool(relu), join,
+                            *[b.weight for b in bns], *[b.bias for b in bns])
+
+
+# ---- stem: 7x7/s2 convolution on the pixel-pair view, BN + ReLU + max-pool --------------
+
+class _VStemFn(torch.autograd.Function):
+    """The G views' RGB stems: view g = x[:, g] (the model input [B, G, C0, H, W]),
+    packed into one stacked pair view and convolved in one launch."""
+
+    @staticmethod
+    def forward(ctx, x, G, pad, *weights):
+        lib = L.load()
+        B, _, C0, H, W = x.shape
+        K, _, R, S = weights[0].shape
+        P, Q, Sp, Hp, Wp = _stem_geom(H, W, R, S, pad)
+        dev = x.device
+        xp = torch.empty(G * B, Hp, Wp // 2, 8, device=dev, dtype=BF)
+        wp = torch.empty(G, K, R, Sp, 8, device=dev, dtype=BF)
+        for g in range(G):
+            stem_pack(x[:, g], weights[g], pad, xp=xp[g * B:(g + 1) * B], wp=wp[g])
+        y = torch.empty(G * B, K, P, Q, device=dev, dtype=BF, memory_format=CL)
+        d = _desc_hw(B, Hp, Wp // 2, 8, K, R, Sp, 2, 1, 0, 0)
+        L.check(lib.gm_conv2d_fwd_grouped_bf16(ctypes.byref(d), G, xp.data_ptr(), wp.data_ptr(), K * R * Sp * 8,
+                                               y.data_ptr(), 0, 0, L.stream_of(dev)), "gm_conv2d_fwd_grouped_bf16")
+        ctx.save_for_backward(xp, *weights)
+        ctx.meta = (G, B, R, S, Sp)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        xp, *weights = ctx.saved_tensors
+        G, B, R, S, Sp = ctx.meta
+        want = [ctx.needs_input_grad[3 + g] for g in range(G)]
+        if not any(want):
+            return (None, None, None, *[None] * G)
+        lib = L.load()
+        gy = _nhwc(gy.to(BF))
+        dev = gy.device
+        _, Hp, Wq, _ = xp.shape
+        K, C0 = weights[0].shape[0], weights[0].shape[1]
+        d = _desc_hw(B, Hp, Wq, 8, K, R, Sp, 2, 1, 0, 0)
+        need = lib.gm_conv2d_wgrad_grouped_scratch(ctypes.byref(d), G)
+        scratch = torch.empty(max(need, 16), device=dev, dtype=torch.uint8)
+        dwp = torch.empty(G, K, R, Sp, 8, device=dev, dtype=torch.float32)
+        L.check(lib.gm_conv2d_wgrad_grouped_bf16(ctypes.byref(d), G, gy.data_ptr(), xp.data_ptr(), dwp.data_ptr(),
+                                                 K * R * Sp * 8, 8, 0, scratch.data_ptr(), need, L.stream_of(dev)),
+                "gm_conv2d_wgrad_grouped_bf16")
+        grads = []
+        for g, w in enumerate(weights):
+            if not want[g]:
+                grads.append(None)
+                continue
+            dw = dwp[g].view(K, R, 2 * Sp, 4)[:, :, :S, :C0].permute(0, 3, 1, 2)  # [K,C0,R,S]
+            tgt = sink_target(w)
+            if tgt is not None:
+                if tgt[1]:
+                    tgt[0].add_(dw)
+                else:
+                    tgt[0].copy_(dw)
+                sink_done(w)
+                grads.append(None)
+            else:
+                grads.append(_like_param(dw, w))
+        return (None, None, None, *grads)
+
+
+class _VBNReluPoolFn(torch.autograd.Function):
+    """pool(relu(BatchNorm_g(X_g))) per view group: one grouped statistics launch, one pool
+    launch applying each group's coefficients (bn._BNReluPoolFn, stacked)."""
+
+    @staticmethod
+    def forward(ctx, X, G, bns, k, s, pad, *params):
+        lib = L.load()
+        gammas, betas = params[:G], params[G:]
+        xb = _nhwc(X.to(BF))
+        GN, C, H, W = xb.shape
+        N = GN // G
+        M = N * H * W
+        dev = xb.device
+        sm = torch.empty(G, C, device=dev, dtype=torch.float32)
+        si = torch.empty(G, C, device=dev, dtype=torch.float32)
+        coef = torch.empty(G, 2 * C, device=dev, dtype=torch.float32)
+        descs = [L.BnFwd(M, C, 1, xb[g * N:(g + 1) * N].data_ptr(), 0, 0, gammas[g].data_ptr(), betas[g].data_ptr(),
+                         L.ptr(bn.running_mean), L.ptr(bn.running_var), float(bn.momentum), float(bn.eps),
+                         sm[g].data_ptr(), si[g].data_ptr(), L.ptr(bn.num_batches_tracked), coef[g].data_ptr())
+                 for g, bn in enumerate(bns)]
+        buf = _bn_scratch_g(dev, M, C, G)
+        st = L.stream_of(dev)
+        L.check(lib.gm_bn_fwd_stats_grouped_bf16(L.arr(L.BnFwd, descs), G, buf.data_ptr(), buf.numel(), st),
+                "gm_bn_fwd_stats_grouped_bf16")
+        P, Q = (H + 2 * pad - k) // s + 1, (W + 2 * pad - k) // s + 1
+        y = torch.empty(GN, C, P, Q, device=dev, dtype=BF, memory_format=CL)
+        idx = torch.empty(GN, P, Q, C, device=dev, dtype=torch.uint8)
+        d = L.PoolDesc(N, H, W, C, k, s, pad)
+        L.check(lib.gm_bn_relu_maxpool2d_fwd_grouped_bf16(ctypes.byref(d), G, xb.data_ptr(), coef.data_ptr(),
+                                                          y.data_ptr(), idx.data_ptr(), st),
+                "gm_bn_relu_maxpool2d_fwd_grouped_bf16")
+        ctx.save_for_backward(xb, coef, sm, si, idx, *gammas, *betas)
+        ctx.meta = (G, k, s, pad)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = L.load()
+        xb, coef, sm, si, idx, *prm = ctx.saved_tensors
+        G, k, s, pad = ctx.meta
+        gammas, betas = prm[:G], prm[G:]
+        GN, C, H, W = xb.shape
+        dy = _nhwc(dy.to(BF))
+        dz = torch.empty_like(xb, memory_format=CL)
+        d = L.PoolDesc(GN, H, W, C, k, s, pad)
+        L.check(lib.gm_maxpool2d_bwd_bf16(ctypes.byref(d), dy.data_ptr(), idx.data_ptr(), dz.data_ptr(),
+                                          L.stream_of(xb.device)), "gm_maxpool2d_bwd_bf16")
+        dx, _, gw, gb = _bn_backward(dz, None, xb, G, gammas, betas, sm, si, True, False, coef,
+                                     any(ctx.needs_input_grad[6:6 + G]), any(ctx.needs_input_grad[6 + G:]))
+        return (dx if ctx.needs_input_grad[0] else None, None, None, None, None, None, *gw, *gb)
+
+
+def vstem(x, nets):
+    """layer-1 input of every view, stacked: maxpool(relu(bn1(conv1(x[:, g])))) per net g."""
+    G = len(nets)
+    c0 = nets[0].conv1
+    pool = nets[0].maxpool
+    from .pool import _pair1
+    k, s, p = (_pair1(getattr(pool, a)) for a in ("kernel_size", "stride", "padding"))
+    with torch.autocast("cuda", enabled=False):
+        y = _VStemFn.apply(x, G, c0.padding[0], *[n.conv1.weight for n in nets])
+        bns = [n.bn1 for n in nets]
+        return _VBNReluPoolFn.apply(y, G, bns, k, s, p, *[b.weight for b in bns], *[b.bias for b in bns])
+
+
+# ---- blocks and eligibility ---------------------------------------------------------
+
+def vblock(blocks, X):
+    """One ResNet block position of every view (BasicBlock.forward / Bottleneck.forward,
+    resnet.py, stacked)."""
+    b0 = blocks[0]
+    join = GradJoin()
+    ds = b0.downsample is not None
+    if ds:
+        idt = vbn(vconv(X, [b.downsample[0] for b in blocks], join), [b.downsample[1] for b in blocks])
+    else:
+        idt = X
+    out = vbn(vconv(X, [b.conv1 for b in blocks], join), [b.bn1 for b in blocks], relu=True)
+    if hasattr(b0, "conv3"):  # Bottleneck
+        out = vbn(vconv(out, [b.conv2 for b in blocks]), [b.bn2 for b in blocks], relu=True)
+        return vbn(vconv(out, [b.conv3 for b in blocks]), [b.bn3 for b in blocks], residual=idt, relu=True,
+                   residual_join=None if ds else join)
+    return vbn(vconv(out, [b.conv2 for b in blocks]), [b.bn2 for b in blocks], residual=idt, relu=True,
+               residual_join=None if ds else join)
+
+
+def vlayer(nets, i, X):
+    """layer{i} of every view over the stacked X."""
+    layers = [getattr(n, f"layer{i}") for n in nets]
+    for j in range(len(layers[0])):
+        X = vblock([lay[j] for lay in layers], X)
+    return X
+
+
+def usable(model, nets, x):
+    """The stacked trunk applies: training-mode bf16 (input or autocast) on HIP, 2..4 views of
+    one architecture with the pixel-pair stem, every BN tracking statistics with momentum."""
+    from .bn import GMBatchNorm2d
+    from .conv import GMConv2d
+    if not (ENABLED and model.training and x.is_cuda and x.dim() == 5 and 2 <= len(nets) <= 4):
+        return False
+    if not (x.dtype == BF or (torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == BF)):
+        return False
+    if not torch.is_grad_enabled():
+        return False
+    sig = None
+    for n in nets:
+        if not n.training or not n.conv1.uses_pair_stem():
+            return False
+        mods = [m for m in n.modules() if isinstance(m, (GMConv2d, GMBatchNorm2d))]
+        s = [(type(m).__name__, tuple(m.weight.shape)) for m in mods]
+        if sig is None:
+            sig = s
+        elif s != sig:
+            return False
+        if any(isinstance(m, GMBatchNorm2d) and (m.momentum is None or not m.track_running_stats or not m.affine)
+               for m in mods):
+            return False
+    return True

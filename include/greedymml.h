@@ -309,6 +309,12 @@ int gm_conv_set_pipe(int pipe);
  * the input once per 64-channel chunk as a halo instead of once per tap (default on;
  * GM_CONV_HALO=0 or gm_conv_set_halo(0) selects the im2col kernel for them). */
 int gm_conv_set_halo(int on);
+/* The halo kernel with its nine taps unrolled (k_conv_h9; default on, GM_CONV_H9=0 at
+ * load or gm_conv_set_h9(0) selects the run-time-decoded k_conv_halo, an A/B switch). */
+int gm_conv_set_h9(int on);
+/* Split-K target: workgroups wanted from splitting K of 128x128-tile convolutions whose
+ * tiles alone do not fill the device (default 384, GM_CONV_SPLITK at load; 0 = never). */
+int gm_conv_set_splitk(int target);
 /* Weight-gradient tile form (process-wide; GM_WGRAD_WIDE at load): bit 0 takes
  * 256-row tiles for K >= 256, bit 1 256-column (tap, channel) tiles; 0 = 128 x 128. */
 int gm_conv_set_wgrad_wide(int mode);
@@ -356,6 +362,22 @@ int gm_conv2d_wgrad_bf16(const gm_conv_desc* d, const void* dy, const void* x, f
 size_t gm_conv2d_wgrad_hw_scratch(const gm_conv_desc_hw* d);
 int gm_conv2d_wgrad_hw_bf16(const gm_conv_desc_hw* d, const void* dy, const void* x, float* dw, int c_real,
                             int accumulate, void* scratch, size_t scratch_bytes, void* stream);
+/* View groups: G views of the multi-view trunk stacked along the batch (activations
+ * [G*N][H][W][C], d->N = images per view), each with its own weight, in ONE launch per
+ * pass (the views' tiles fill the chip together instead of one stream each).  Group g
+ * reads x + g*N*H*W*C and the weight w + g*w_stride (bf16 elements, >= one weight),
+ * writes y + g*N*P*Q*K; dgrad's addend/dx and wgrad's dy/x follow the same stacking,
+ * wgrad writes dw + g*dw_stride (fp32 elements).  G = 1 is the ungrouped call.  The
+ * workspaces are sized for the whole grouped launch. */
+int gm_conv2d_fwd_grouped_bf16(const gm_conv_desc_hw* d, int G, const void* x, const void* w, long long w_stride,
+                               void* y, void* ws, size_t ws_bytes, void* stream);
+int gm_conv2d_dgrad_grouped_bf16(const gm_conv_desc* d, int G, const void* dy, const void* wt, long long wt_stride,
+                                 void* dx, const void* addend, void* ws, size_t ws_bytes, void* stream);
+size_t gm_conv2d_splitk_ws_bytes_grouped(const gm_conv_desc* d, int G, int dgrad);
+size_t gm_conv2d_wgrad_grouped_scratch(const gm_conv_desc_hw* d, int G);
+int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, const void* dy, const void* x, float* dw,
+                                 long long dw_stride, int c_real, int accumulate, void* scratch,
+                                 size_t scratch_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Reference-precision (fp32) trunk convolutions: the same three passes on the exact
@@ -447,6 +469,15 @@ int gm_bn_bwd_bf16(const gm_bn_bwd* p, void* scratch, size_t scratch_bytes, void
 /* the statistics half of gm_bn_fwd_train_bf16 alone (y is not written; coef_out required):
  * the stem's BN + ReLU is applied inside its max-pool (gm_bn_relu_maxpool2d_fwd_bf16) */
 int gm_bn_fwd_stats_bf16(const gm_bn_fwd* p, void* scratch, size_t scratch_bytes, void* stream);
+/* View groups: G (<= 4) descriptors that agree on M, C and every option, differing only
+ * in their pointers (the views of the multi-view trunk, each with its own parameters
+ * and statistics), normalised in ONE launch.  scratch >= gm_bn_scratch_grouped(M, C, G)
+ * (each group its own ticket / partial area), zeroed once like gm_bn_scratch's.  The
+ * grouped forms of gm_bn_fwd_train_bf16 / gm_bn_bwd_bf16 / gm_bn_fwd_stats_bf16. */
+size_t gm_bn_scratch_grouped(long long M, int C, int G);
+int gm_bn_fwd_train_grouped_bf16(const gm_bn_fwd* ps, int G, void* scratch, size_t scratch_bytes, void* stream);
+int gm_bn_bwd_grouped_bf16(const gm_bn_bwd* ps, int G, void* scratch, size_t scratch_bytes, void* stream);
+int gm_bn_fwd_stats_grouped_bf16(const gm_bn_fwd* ps, int G, void* scratch, size_t scratch_bytes, void* stream);
 /* the same three on fp32 activations (x, residual, y, dy, dx, dres fp32 NHWC): the
  * reference-precision trunk; reduce + apply launches, same statistics arithmetic */
 int gm_bn_fwd_train_f32(const gm_bn_fwd* p, void* scratch, size_t scratch_bytes, void* stream);
@@ -472,6 +503,10 @@ int gm_maxpool2d_bwd_bf16(const gm_pool_desc* d, const void* dy, const void* idx
  * apply followed by gm_maxpool2d_fwd_bf16, without writing the normalised activation */
 int gm_bn_relu_maxpool2d_fwd_bf16(const gm_pool_desc* d, const void* x, const float* coef, void* y, void* idx,
                                   void* stream);
+/* G view groups of d->N images each stacked along the batch (x [G*N][H][W][C]); group g
+ * applies coef + g*2C (gm_bn_fwd_stats_grouped_bf16's coef_out of group g) */
+int gm_bn_relu_maxpool2d_fwd_grouped_bf16(const gm_pool_desc* d, int G, const void* x, const float* coef, void* y,
+                                          void* idx, void* stream);
 /* fp32 activations (the reference-precision trunk), same index format */
 int gm_maxpool2d_fwd_f32(const gm_pool_desc* d, const void* x, void* y, void* idx, void* stream);
 int gm_maxpool2d_bwd_f32(const gm_pool_desc* d, const void* dy, const void* idx, void* dx, void* stream);

@@ -1,0 +1,207 @@
+"""View-batched trunk (vtrunk.py): the two view trunks as grouped launches.
+
+* grouped convolution (fwd / dgrad with and without the gradient-join addend / wgrad),
+  every kernel family (resident-weight layer 1, halo h9, lean im2col, strided, 1x1,
+  pixel-pair stem): each view group against PyTorch fp32 on the CPU from the same
+  bf16-rounded operands (test_gpu_conv.py's tolerances), and against the per-view HIP
+  convolution;
+* grouped BatchNorm (+ residual + ReLU, ReLU with the mask from x, plain): each group
+  against the per-view GMBatchNorm2d (outputs, parameter gradients, running statistics,
+  num_batches_tracked);
+* the whole MMTM_MVCNN training forward + backward, stacked vs per-view trunks: logits,
+  every parameter gradient, every BatchNorm buffer.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+CL = torch.channels_last
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda:0")
+
+
+def _close(a, b, tol, what=""):
+    a, b = a.detach().float().cpu(), b.detach().float().cpu()
+    scale = float(b.abs().max()) + 1e-12
+    err = float((a - b).abs().max()) / scale
+    assert err <= tol, f"{what}: max |diff| / max |ref| = {err:.3e} > {tol}"
+    return err
+
+
+CONV_SHAPES = [  # N per view, C, H, W, K, R, S, stride, pad
+    (4, 64, 56, 56, 64, 3, 3, 1, 1),     # layer 1: resident-weight kernel
+    (8, 128, 28, 28, 128, 3, 3, 1, 1),   # layer 2: halo (h9)
+    (8, 256, 14, 14, 256, 3, 3, 1, 1),   # layer 3: halo (h9), split-K candidates
+    (8, 512, 7, 7, 512, 3, 3, 1, 1),     # layer 4
+    (4, 64, 56, 56, 128, 3, 3, 2, 1),    # strided 3x3 (lean)
+    (4, 128, 28, 28, 256, 1, 1, 2, 0),   # downsample 1x1
+    (3, 64, 9, 11, 64, 3, 3, 1, 1),      # ragged map
+]
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES, ids=lambda s: "x".join(map(str, s)))
+@pytest.mark.parametrize("join", [False, True], ids=["plain", "join"])
+def test_grouped_conv_matches_reference(dev, shape, join):
+    from greedy_multimodal_learning_amd.conv import GMConv2d
+    from greedy_multimodal_learning_amd.gradsink import GradJoin
+    from greedy_multimodal_learning_amd.vtrunk import vconv
+    N, C, H, W, K, R, S, st, pad = shape
+    G = 2
+    g = torch.Generator().manual_seed(sum(shape) + join)
+    x = torch.randn(G * N, C, H, W, generator=g).bfloat16()
+    ws = [(torch.randn(K, C, R, S, generator=g) / (C * R * S) ** 0.5).bfloat16() for _ in range(G)]
+    P, Q = (H + 2 * pad - R) // st + 1, (W + 2 * pad - S) // st + 1
+    gy = torch.randn(G * N, K, P, Q, generator=g).bfloat16()
+    addend = torch.randn(G * N, C, H, W, generator=g).bfloat16() if join else None
+    mods = []
+    for w in ws:
+        m = GMConv2d(C, K, (R, S), stride=st, padding=pad, bias=False).to(dev)
+        with torch.no_grad():
+            m.weight.copy_(w.float())
+        mods.append(m.to(memory_format=CL))
+    xd = x.to(dev).contiguous(memory_format=CL).requires_grad_(True)
+    jn = GradJoin() if join else None
+    y = vconv(xd, mods, jn)
+    if join:  # a second consumer of x: its gradient (the addend) joins the dgrad in place
+        jn.register()
+        add_d = addend.to(dev).contiguous(memory_format=CL)
+        assert jn.contribute(lambda a: add_d.clone()) is None
+    y.backward(gy.to(dev).contiguous(memory_format=CL))
+    for i in range(G):
+        r = slice(i * N, (i + 1) * N)
+        xr = x[r].float().requires_grad_(True)
+        wr = ws[i].float().requires_grad_(True)
+        yr = F.conv2d(xr, wr, stride=st, padding=pad)
+        yr.backward(gy[r].float())
+        _close(y[r], yr, 1e-2, f"y[{i}]")
+        ref_dx = xr.grad + (addend[r].float() if join else 0)
+        _close(xd.grad[r], ref_dx, 1e-2, f"dx[{i}]")
+        _close(mods[i].weight.grad, wr.grad, 2e-3, f"dw[{i}]")
+    # and against the per-view HIP convolution (same kernels, at most another split-K order)
+    for i in range(G):
+        r = slice(i * N, (i + 1) * N)
+        xi = x[r].to(dev).contiguous(memory_format=CL)
+        yi = mods[i](xi)
+        _close(y[r], yi, 8e-3, f"y[{i}] vs per-view")
+
+
+def test_grouped_stem_and_pool(dev):
+    """vstem (pixel-pair stem conv + grouped BN statistics + grouped BN-ReLU-maxpool) vs
+    the per-view stem path, forward and backward."""
+    from greedy_multimodal_learning_amd.resnet import resnet18
+    from greedy_multimodal_learning_amd.vtrunk import vstem
+    torch.manual_seed(3)
+    B, H = 4, 64
+    nets = [resnet18().to(dev).to(memory_format=CL) for _ in range(2)]
+    ref = [resnet18().to(dev).to(memory_format=CL) for _ in range(2)]
+    for a, b in zip(nets, ref):
+        b.load_state_dict(a.state_dict())
+        a.train(), b.train()
+    x = torch.randn(B, 2, 3, H, H, device=dev).bfloat16()
+    Y = vstem(x, nets)
+    gY = torch.randn_like(Y)
+    Y.backward(gY)
+    for i in range(2):
+        n = ref[i]
+        y = n.bn1.relu_maxpool(n.conv1(x[:, i]), n.maxpool)
+        y.backward(gY[i * B:(i + 1) * B])
+        _close(Y[i * B:(i + 1) * B], y, 1e-2, f"stem y[{i}]")
+        _close(nets[i].conv1.weight.grad, n.conv1.weight.grad, 2e-2, f"stem dw[{i}]")
+        _close(nets[i].bn1.weight.grad, n.bn1.weight.grad, 2e-2, f"bn1 dgamma[{i}]")
+        _close(nets[i].bn1.bias.grad, n.bn1.bias.grad, 2e-2, f"bn1 dbeta[{i}]")
+        _close(nets[i].bn1.running_mean, n.bn1.running_mean, 1e-5, f"bn1 running_mean[{i}]")
+        _close(nets[i].bn1.running_var, n.bn1.running_var, 1e-5, f"bn1 running_var[{i}]")
+        assert int(nets[i].bn1.num_batches_tracked) == int(n.bn1.num_batches_tracked) == 1
+
+
+@pytest.mark.parametrize("mode", ["res_relu", "relu", "plain"])
+@pytest.mark.parametrize("shape", [(8, 64, 56, 56), (8, 256, 14, 14), (8, 512, 7, 7)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_grouped_bn_matches_per_view(dev, mode, shape):
+    from greedy_multimodal_learning_amd.bn import GMBatchNorm2d
+    from greedy_multimodal_learning_amd.vtrunk import vbn
+    N, C, H, W = shape
+    G = 2
+    g = torch.Generator().manual_seed(C + len(mode))
+    x = torch.randn(G * N, C, H, W, generator=g).bfloat16().to(dev).contiguous(memory_format=CL)
+    res = torch.randn(G * N, C, H, W, generator=g).bfloat16().to(dev).contiguous(memory_format=CL)
+    gy = torch.randn(G * N, C, H, W, generator=g).bfloat16().to(dev).contiguous(memory_format=CL)
+    bns, ref = [], []
+    for i in range(G):
+        b = GMBatchNorm2d(C).to(dev)
+        with torch.no_grad():
+            b.weight.uniform_(0.5, 1.5, generator=None)
+            b.bias.uniform_(-0.5, 0.5)
+            b.running_mean.uniform_(-0.1, 0.1)
+        r = GMBatchNorm2d(C).to(dev)
+        r.load_state_dict(b.state_dict())
+        bns.append(b.train())
+        ref.append(r.train())
+    xs = x.clone().requires_grad_(True)
+    rs = res.clone().requires_grad_(True) if mode == "res_relu" else None
+    y = vbn(xs, bns, residual=rs, relu=mode != "plain")
+    y.backward(gy)
+    for i in range(G):
+        r = slice(i * N, (i + 1) * N)
+        xi = x[r].clone().requires_grad_(True)
+        ri = res[r].clone().requires_grad_(True) if mode == "res_relu" else None
+        yi = ref[i](xi, residual=ri, relu=mode != "plain")
+        yi.backward(gy[r])
+        _close(y[r], yi, 8e-3, f"y[{i}]")
+        _close(xs.grad[r], xi.grad, 8e-3, f"dx[{i}]")
+        if ri is not None:
+            _close(rs.grad[r], ri.grad, 1e-2, f"dres[{i}]")
+        _close(bns[i].weight.grad, ref[i].weight.grad, 2e-3, f"dgamma[{i}]")
+        _close(bns[i].bias.grad, ref[i].bias.grad, 2e-3, f"dbeta[{i}]")
+        _close(bns[i].running_mean, ref[i].running_mean, 1e-6, f"running_mean[{i}]")
+        _close(bns[i].running_var, ref[i].running_var, 1e-6, f"running_var[{i}]")
+        assert int(bns[i].num_batches_tracked) == int(ref[i].num_batches_tracked) == 1
+
+
+def test_model_stacked_vs_per_view(dev):
+    """MMTM_MVCNN training forward + backward: the view-batched trunk against the per-view
+    trunks (GM_VTRUNK off), same weights and input."""
+    from greedy_multimodal_learning_amd import vtrunk
+    from greedy_multimodal_learning_amd.losses import blend_loss
+    from greedy_multimodal_learning_amd.model import MMTM_MVCNN
+    torch.manual_seed(11)
+    B, H = 8, 64
+    a = MMTM_MVCNN().to(dev).to(memory_format=CL).train()
+    b = MMTM_MVCNN().to(dev).to(memory_format=CL).train()
+    b.load_state_dict(a.state_dict())
+    x = torch.randn(B, 2, 3, H, H, device=dev).bfloat16()
+    y = torch.randint(0, 40, (B,), device=dev)
+    assert vtrunk.usable(a, [a.net_view_0, a.net_view_1], x)
+    outs = {}
+    for m, on in ((a, True), (b, False)):
+        old = vtrunk.ENABLED
+        vtrunk.ENABLED = on
+        try:
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                _, o, _, _ = m(x)
+            blend_loss([t.float() for t in o], y).backward()
+        finally:
+            vtrunk.ENABLED = old
+        outs[on] = [t.detach().float() for t in o]
+    for i in range(2):
+        _close(outs[True][i], outs[False][i], 2e-2, f"logits[{i}]")
+    worst = 0.0
+    for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+        ga, gb = pa.grad.double(), pb.grad.double()
+        e = float((ga - gb).norm() / (gb.norm() + 1e-30))
+        worst = max(worst, e)
+        assert e < 5e-2, f"{n}: relative gradient difference {e:.3e}"
+    print(f"stacked vs per-view: worst parameter-gradient relative L2 difference {worst:.2e}")
+    for (n, ba), (_, bb) in zip(a.named_buffers(), b.named_buffers()):
+        if ba.dtype == torch.long:
+            assert int(ba) == int(bb), n
+        else:
+            _close(ba, bb, 1e-2, n)

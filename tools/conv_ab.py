@@ -26,8 +26,10 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--pipes", default="0,h", help="comma list of pipe numbers; 'h' = halo kernel on, 'H' = 256-pixel halo tiles")
+    ap.add_argument("--pipes", default="0,h", help="comma list of pipe numbers; 'h' = halo kernel on (k_conv_h9), "
+                                                 "'o' = halo kernel with run-time tap decode, 'H' = 256-pixel halo tiles")
     ap.add_argument("--wgrad", action="store_true", help="also time the weight-gradient passes")
+    ap.add_argument("--shapes", default="", help="'+'-separated trunk shape names (default: all)")
     a = ap.parse_args()
     from greedy_multimodal_learning_amd import _lib as L
     from greedy_multimodal_learning_amd import conv as G
@@ -39,7 +41,18 @@ def main():
     def select(p):  # "h", "h5", "h6": the halo kernel (+ diagnostics); "H...": 256-pixel halo tiles;
         # "W<n>": halo kernel + weight-gradient tile form n (gm_conv_set_wgrad_wide)
         L.check(lib.gm_conv_set_wgrad_wide(int(p[1:]) if p[0] == "W" else 0), "set_wgrad_wide")
-        if p[0] == "W":
+        # "o": the halo kernel with run-time tap decode (k_conv_halo) instead of k_conv_h9;
+        # "fBN.NB": k_conv_h9 forced to BN-channel tiles and an NB-stage weight ring
+        # "s<n>": split-K target n (0: never split), auto form otherwise
+        L.check(lib.gm_conv_set_splitk(int(p[1:]) if p[0] == "s" else 384), "set_splitk")
+        if p[0] == "s":
+            p = "h"
+        if p[0] == "f":
+            bn, nb = p[1:].split(".")
+            L.check(lib.gm_conv_set_h9((int(bn) << 8) | int(nb)), "set_h9")
+        else:
+            L.check(lib.gm_conv_set_h9(0 if p == "o" else 1), "set_h9")
+        if p[0] in ("W", "o", "f"):
             p = "h"
         hl = p[:1] in ("h", "H")
         L.check(lib.gm_conv_set_halo((2 if p[0] == "H" else 1) if hl else 0), "set_halo")
@@ -47,8 +60,9 @@ def main():
     lib = L.load()
     ops = []
     g = torch.Generator(device=dev).manual_seed(0)
+    only = set(a.shapes.split("+")) if a.shapes else None
     for name, (C, H, W, K, R, st, pad, cnt) in T.TRUNK:
-        if C == 3:
+        if C == 3 or (only and name not in only):
             continue
         P, Q = (H + 2 * pad - R) // st + 1, (W + 2 * pad - R) // st + 1
         flops = 2.0 * B * P * Q * K * C * R * R
@@ -68,7 +82,7 @@ def main():
     # summation order) within bf16 output rounding of it
     ref = {}
     for p in pipes:
-        if p in ("5", "6", "h5", "h6", "H5", "H6"):
+        if p in ("5", "6", "h5", "h6", "H5", "H6", "h7", "h8"):
             continue  # timing diagnostics: outputs meaningless
         select(p)
         for name, op, _, _, fn in ops:
@@ -80,7 +94,7 @@ def main():
                 continue
             d = (out.float() - ref[k].float()).abs().max().item()
             sc = ref[k].float().abs().max().item()
-            if (p[:1] not in ("h", "H", "W") and not torch.equal(out, ref[k])) or d > 2e-2 * sc:
+            if (p[:1] not in ("h", "H", "W", "o", "f", "s") and not torch.equal(out, ref[k])) or d > 2e-2 * sc:
                 print(f"MISMATCH {p} {name} {op}: max |diff| {d} (scale {sc})", flush=True)
                 sys.exit(3)
     print("all variants agree", flush=True)

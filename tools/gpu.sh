@@ -11,6 +11,7 @@
 #   benchq       python bench.py --no-cpu-baseline                    -> gpurun_out/benchq.log
 #   bench:ARGS   python bench.py ARGS (commas become spaces)          -> gpurun_out/bench_ARGS.log
 #   prof         rocprofv3 --kernel-trace --stats of a short bench    -> gpurun_out/prof/
+#   prof:V=X,..  the same with environment variables set               -> gpurun_out/prof_V_X/
 #   pmc:NAME     one rocprofv3 --pmc pass over a short bench (sets below) -> gpurun_out/pmc_NAME/
 #   table        tools/trunk_table.py: per-shape trunk launch table    -> gpurun_out/trunk_table.md
 #   pmct:NAME    one rocprofv3 --pmc pass over tools/trunk_table.py, summarised per (kernel, grid)
@@ -21,6 +22,8 @@
 #                per-op table + conv-family traffic json         -> gpurun_out/trunk_pmc.md, trunk_pmc.json
 #   mmtmpmc      two rocprofv3 --pmc passes (FETCH, WRITE) over tools/mmtm_probe.py (the MMTM squeeze
 #                at B=256 rotating over 411 MB)                   -> gpurun_out/traffic_mmtm.json
+#   pmcone:SET:ARGS one rocprofv3 --pmc pass (counter set SET above) over tools/conv_one.py ARGS
+#                (commas become spaces), summarised per kernel  -> gpurun_out/pmcone_SET.txt
 #   py:FILE[,ARGS] python FILE ARGS (a tools/ script; commas become spaces) -> gpurun_out/py_FILE.log
 set -o pipefail
 mkdir -p gpurun_out
@@ -34,6 +37,9 @@ PMC[lds]="SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVE_CYCLES"
 PMC[fetch]="FETCH_SIZE"
 PMC[write]="WRITE_SIZE"
 PMC[opmfma]="SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVES"
+PMC[stall]="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU"
+PMC[l2]="TCC_HIT_sum TCC_MISS_sum"
+PMC[lds2]="SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_WAVES"
 
 for s in "$@"; do
   echo "=== $s $(date +%T)"
@@ -65,6 +71,13 @@ for s in "$@"; do
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench \
         -- $PROFCMD > gpurun_out/prof.log 2>&1 || { tail -30 gpurun_out/prof.log; exit 17; }
       python3 tools/summarize_stats.py gpurun_out/prof/bench_kernel_stats.csv 13 | head -40 ;;
+    prof:*)
+      e="${s#prof:}"; d="gpurun_out/prof_$(echo "$e" | tr -c 'A-Za-z0-9\n' '_')"
+      export ${e//,/ }
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$d" -o bench \
+        -- $PROFCMD > "$d.log" 2>&1 || { tail -30 "$d.log"; exit 17; }
+      for v in ${e//,/ }; do unset "${v%%=*}"; done
+      python3 tools/summarize_stats.py "$d/bench_kernel_stats.csv" 13 | head -40 ;;
     pmc:*)
       n="${s#pmc:}"
       timeout -s KILL 300 rocprofv3 --pmc ${PMC[$n]} --output-format csv -d "gpurun_out/pmc_$n" -o pmc \
@@ -101,6 +114,12 @@ for s in "$@"; do
       python3 tools/mmtm_probe.py report gpurun_out/mp_fetch gpurun_out/mp_write --json gpurun_out/traffic_mmtm.json \
         > gpurun_out/mmtm_pmc.log && rm -rf gpurun_out/mp_fetch gpurun_out/mp_write
       tail -4 gpurun_out/traffic_mmtm.json ;;
+    pmcone:*)
+      r="${s#pmcone:}"; n="${r%%:*}"; args="${r#*:}"; d="gpurun_out/pmcone_${n}_$(echo "$args" | tr -c 'A-Za-z0-9\n' '_')"
+      timeout -s KILL 120 rocprofv3 --pmc ${PMC[$n]} --output-format csv -d "$d" -o pmc \
+        -- python3 tools/conv_one.py ${args//,/ } > "$d.log" 2>&1 || { tail -30 "$d.log"; exit 25; }
+      python3 tools/pmc_table.py "$d" | grep -v spin_kernel > "$d.txt" && rm -rf "$d"
+      cat "$d.txt" ;;
     py:*)
       a="${s#py:}"; f="${a%%,*}"; args=""; [ "$f" != "$a" ] && args="${a#*,}"
       lg="gpurun_out/py_$(basename "$f" .py).log"

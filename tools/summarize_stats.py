@@ -7,5 +7,5 @@ rows = list(csv.DictReader(open(path)))
 tot = sum(float(r['TotalDurationNs']) for r in rows)
 print(f"kernel time per step: {tot / nsteps / 1e6:.3f} ms")
 for r in rows[:30]:
-    print(f"{r['Name'][:80]:80s} calls/step={int(r['Calls']) / nsteps:6.1f} avg_us={float(r['AverageNs']) / 1e3:8.2f} "
+    print(f"{r['Name'][:100]:100s} calls/step={int(r['Calls']) / nsteps:6.1f} avg_us={float(r['AverageNs']) / 1e3:8.2f} "
           f"ms/step={float(r['TotalDurationNs']) / nsteps / 1e6:.3f}")
