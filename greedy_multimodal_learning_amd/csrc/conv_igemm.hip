@@ -1048,8 +1048,17 @@ constexpr int kH9MaxQ = 12;  // halo DMA instructions per wave (nI <= 48)
 
 // NB: weight-ring stages (NB - 2 stay in flight across a k-tile); DIAG (timing
 // diagnostics, outputs meaningless): 1 = no weight DMA in the k-loop, 2 = no MFMAs /
-// fragment reads, 3 = no barrier in the k-loop, 4 = no halo reload
-template <int BN, int NB, int DIAG = 0>
+// fragment reads, 3 = no barrier in the k-loop, 4 = no halo reload.
+// WR: how the operands reach LDS.  0: LDS-DMA (global_load_lds) for the weights and the
+// halo.  1: the weights register-staged - global_load_dwordx4 one k-tile ahead into VGPRs,
+// ds_write_b128 into the ring stage the previous k-tile freed - because an LDS-DMA piece
+// costs its wave ~60-185 issue cycles among MFMAs (MI355X_MICROARCH.md price table) where a
+// load + ds_write_b128 costs ~20; the halo stays LDS-DMA, reloaded at each chunk start.
+// 2: as 1, and the next chunk's halo is prefetched into VGPRs at the chunk start and
+// written to LDS at the next one, so no chunk start waits for a halo load.
+// 3: LDS-DMA as 0, with the next k-tile's weight pieces issued one after each k-slice's
+// MFMAs instead of back to back before them.
+template <int BN, int NB, int DIAG = 0, int WR = 0>
 __global__ __launch_bounds__(256, 2) void k_conv_h9(ConvArgs a, HaloArgs h) {
     constexpr int BM = 128, MT = 2, NT = BN / 64, NW = 4;
     static_assert(NB >= 2 && NB <= 8, "ring depth");
@@ -1189,7 +1198,9 @@ __global__ __launch_bounds__(256, 2) void k_conv_h9(ConvArgs a, HaloArgs h) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    auto compute = [&](int tp, int st) {
+    // piece(ks) runs after k-slice ks's MFMAs (WR 3: the next k-tile's weight DMA pieces
+    // spread between the MFMAs instead of issued back to back before them)
+    auto compute = [&](int tp, int st, auto&& piece) {
         bf16x8 af[2][MT], bfr[2][NT];
 #pragma unroll
         for (int i = 0; i < MT; ++i) af[0][i] = *reinterpret_cast<const bf16x8*>(lds + aad[tp][i]);
@@ -1211,19 +1222,23 @@ __global__ __launch_bounds__(256, 2) void k_conv_h9(ConvArgs a, HaloArgs h) {
 #pragma unroll
                 for (int j = 0; j < NT; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[c][j], af[c][i], acc[i][j], 0, 0, 0);
+            piece(ks);
         }
         constexpr int NR = MT + NT, NM = MT * NT;
-        __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+        if constexpr (WR != 3) {
+            __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
 #pragma unroll
-        for (int ks = 0; ks < 3; ++ks) {
+            for (int ks = 0; ks < 3; ++ks) {
 #pragma unroll
-            for (int q = 0; q < (NM > NR ? NM : NR); ++q) {
-                if (q < NM) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                if (q < NR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                for (int q = 0; q < (NM > NR ? NM : NR); ++q) {
+                    if (q < NM) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    if (q < NR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                }
             }
+            __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
         }
-        __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
     };
+    auto none = [](int) {};
 
     // vmcnt(n): all but the wave's n newest vector-memory operations done
     auto wait_vm = [](int n) {
@@ -1245,6 +1260,90 @@ __global__ __launch_bounds__(256, 2) void k_conv_h9(ConvArgs a, HaloArgs h) {
     };
     static_assert((NB - 2) * BR <= 12, "counted wait range");
     const int nkt = (c1 - c0) * 9;
+    if constexpr (WR == 1 || WR == 2) {
+        // register-staged weights (and, WR 2, halo): see the template comment
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));  // (a native vector: SROA-able)
+        u32x4 wreg[BR];
+        auto gload_b = [&](int cc, int tp) __attribute__((always_inline)) {
+            const int off = twc[tp] + (cc << 6);
+#pragma unroll
+            for (int j = 0; j < BR; ++j) wreg[j] = *reinterpret_cast<const u32x4*>(b_src[j] + off);
+        };
+        auto swrite_b = [&](int st) __attribute__((always_inline)) {
+#pragma unroll
+            for (int j = 0; j < BR; ++j)
+                *reinterpret_cast<u32x4*>(lds + HB + st * SB + (wave * BR + j) * 1024 + lane * 16) = wreg[j];
+        };
+        constexpr int HQ = WR == 2 ? kH9MaxQ : 1;
+        u32x4 hreg[HQ];
+        auto gload_halo = [&](int cc) __attribute__((always_inline)) {
+            const int cbase = cc << 6;
+#pragma unroll
+            for (int q = 0; q < HQ; ++q)
+                if (q < nq)
+                    hreg[q] = hsrc[q] >= 0 ? *reinterpret_cast<const u32x4*>(gin + hsrc[q] + cbase)
+                                           : u32x4{0u, 0u, 0u, 0u};
+        };
+        auto swrite_halo = [&]() __attribute__((always_inline)) {
+#pragma unroll
+            for (int q = 0; q < HQ; ++q)
+                if (q < nq) *reinterpret_cast<u32x4*>(lds + (wave + NW * q) * 1024 + lane * 16) = hreg[q];
+        };
+        // LDS stores drained, then the barrier; the memory clobber keeps the compiler from
+        // moving LDS accesses across it (the loads in flight into VGPRs stay in flight: the
+        // compiler waits for them where their registers are used)
+        auto bar = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+        // prologue: the first chunk's halo and k-tiles 0 .. NB-2 in LDS, k-tile NB-1 in flight
+        if constexpr (WR == 2) {
+            gload_halo(c0);
+            swrite_halo();
+        } else {
+            issue_halo(c0);
+        }
+#pragma unroll
+        for (int k = 0; k < NB - 1; ++k) {
+            if (k < nkt) {
+                gload_b(c0 + k / 9, k % 9);
+                swrite_b(k);
+            }
+        }
+        if (NB - 1 < nkt) gload_b(c0 + (NB - 1) / 9, (NB - 1) % 9);
+        // a chunk-start iteration issues its next-k-tile loads, then (WR 2) the next chunk's
+        // halo loads; the compiler's counted waits let the halo loads stay in flight until
+        // the k-tile loads issued after them are consumed (two iterations later)
+        int sb = 0;
+        int kt = 0;
+        for (int cc = c0; cc < c1; ++cc) {
+            const bool pre = WR == 2 && cc + 1 < c1;  // this chunk prefetches the next one's halo
+#pragma clang loop unroll(full)
+            for (int tp = 0; tp < 9; ++tp, ++kt) {
+                if (WR == 1 && kt == 0) wait_vm(0);  // the prologue's halo DMA
+                bar();  // every wave's ds_writes of k-tile kt (and of the halo) are in LDS
+                if (tp == 0 && cc > c0) {  // every wave is done with the previous chunk's halo
+                    if constexpr (WR == 2) {
+                        swrite_halo();  // (the prefetch landed by tp 2 of the previous chunk)
+                    } else {
+                        issue_halo(cc);
+                        wait_vm(0);
+                    }
+                    bar();
+                }
+                compute(tp, sb, none);
+                if (kt + NB - 1 < nkt) {  // k-tile kt+NB-1 into the stage k-tile kt-1 freed
+                    int sn = sb + NB - 1;
+                    if (sn >= NB) sn -= NB;
+                    swrite_b(sn);
+                }
+                if (kt + NB < nkt) {
+                    if (tp + NB < 9) gload_b(cc, tp + NB);
+                    else gload_b(cc + 1, tp + NB - 9);
+                }
+                if constexpr (WR == 2)
+                    if (tp == 0 && pre) gload_halo(cc + 1);
+                if (++sb == NB) sb = 0;
+            }
+        }
+    } else {
     issue_halo(c0);
 #pragma unroll
     for (int k = 0; k < NB - 1; ++k)
@@ -1264,16 +1363,34 @@ __global__ __launch_bounds__(256, 2) void k_conv_h9(ConvArgs a, HaloArgs h) {
                 wait_vm(0);
                 __builtin_amdgcn_s_barrier();
             }
-            if (DIAG != 1 && kt + NB - 1 < nkt) {
-                int sn = sb + NB - 1;
-                if (sn >= NB) sn -= NB;
+            int sn = sb + NB - 1;
+            if (sn >= NB) sn -= NB;
+            const bool refill = DIAG != 1 && kt + NB - 1 < nkt;
+            if (WR != 3 && refill) {
                 if (tp + NB - 1 < 9) issue_b(cc, tp + NB - 1, sn);
                 else issue_b(cc + 1, tp + NB - 1 - 9, sn);
             }
-            if (DIAG != 2) compute(tp, sb);
+            // WR 3: piece j of the refill after k-slice j * 4 / BR's MFMAs
+            auto piece = [&](int ks) __attribute__((always_inline)) {
+                if constexpr (WR == 3) {
+                    if (refill && (ks * BR) % 4 == 0) {
+                        const int j = ks * BR / 4;
+                        const int ccn = tp + NB - 1 < 9 ? cc : cc + 1;
+                        const int tpn = tp + NB - 1 < 9 ? tp + NB - 1 : tp + NB - 1 - 9;
+                        const int off = twc[tpn] + (ccn << 6);
+#pragma unroll
+                        for (int r = 0; r < (BR >= 4 ? BR / 4 : 1); ++r)
+                            __builtin_amdgcn_global_load_lds(
+                                (gptr_t)(b_src[j + r] + off),
+                                (lptr_t)(lds + HB + sn * SB + (wave * BR + j + r) * 1024), 16, 0, 0);
+                    }
+                }
+            };
+            if (DIAG != 2) compute(tp, sb, piece);
             if (++sb == NB) sb = 0;
         }
     }
+    }  // WR
 
     if (a.splits > 1) {
         constexpr int NQ = MT * NT * 4;  // float4 groups of accumulators per lane
@@ -2140,6 +2257,12 @@ static int g_conv_h9 = [] {
     const char* e = getenv("GM_CONV_H9");  // 0: the halo shapes take k_conv_halo (A/B)
     return e ? atoi(e) : 1;
 }();
+// k_conv_h9's operand staging (its WR template argument): 0 LDS-DMA, 1 register-staged
+// weights, 2 register-staged weights + halo prefetch (GM_CONV_H9_WR at load)
+static int g_conv_h9_wr = [] {
+    const char* e = getenv("GM_CONV_H9_WR");
+    return e ? atoi(e) : 0;
+}();
 
 // k_conv_h9 when eligible: Nout a multiple of BN, at most 48 halo DMA instructions, the
 // halo + 3 weight stages within half the CU's LDS (two workgroups per CU), splits over
@@ -2163,7 +2286,8 @@ static int launch_h9(ConvArgs& a, int hb, hipStream_t st) {
         hipError_t e = hipSuccess;
         for (const void* k : {(const void*)k_conv_h9<BN, NB, 0>, (const void*)k_conv_h9<BN, NB, 1>,
                               (const void*)k_conv_h9<BN, NB, 2>, (const void*)k_conv_h9<BN, NB, 3>,
-                              (const void*)k_conv_h9<BN, NB, 4>})
+                              (const void*)k_conv_h9<BN, NB, 4>, (const void*)k_conv_h9<BN, NB, 0, 1>,
+                              (const void*)k_conv_h9<BN, NB, 0, 2>, (const void*)k_conv_h9<BN, NB, 0, 3>})
             if (e == hipSuccess) e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) {
             set_error("k_conv_h9: %zu B of LDS refused (%s)", lds, hipGetErrorString(e));
@@ -2172,6 +2296,21 @@ static int launch_h9(ConvArgs& a, int hb, hipStream_t st) {
         attr = lds;
     }
     const dim3 grid(a.tiles_total * a.splits);
+    if (g_conv_h9_wr == 1) {
+        k_conv_h9<BN, NB, 0, 1><<<grid, 256, lds, st>>>(a, h);
+        const int rc = check_launch("k_conv_h9<wr1>");
+        return rc == GM_OK ? 1 : rc;
+    }
+    if (g_conv_h9_wr == 2) {
+        k_conv_h9<BN, NB, 0, 2><<<grid, 256, lds, st>>>(a, h);
+        const int rc = check_launch("k_conv_h9<wr2>");
+        return rc == GM_OK ? 1 : rc;
+    }
+    if (g_conv_h9_wr == 3) {
+        k_conv_h9<BN, NB, 0, 3><<<grid, 256, lds, st>>>(a, h);
+        const int rc = check_launch("k_conv_h9<wr3>");
+        return rc == GM_OK ? 1 : rc;
+    }
     switch (conv_pipe()) {  // 5..8: timing diagnostics (outputs meaningless)
     case 5: k_conv_h9<BN, NB, 1><<<grid, 256, lds, st>>>(a, h); break;
     case 6: k_conv_h9<BN, NB, 2><<<grid, 256, lds, st>>>(a, h); break;
@@ -2535,6 +2674,13 @@ extern "C" int gm_conv_set_splitk(int target) {
 
 extern "C" int gm_conv_set_h9(int on) {
     g_conv_h9 = on;
+    return GM_OK;
+}
+
+extern "C" int gm_conv_set_h9_staging(int wr) {
+    GM_REQUIRE(wr >= 0 && wr <= 3, "gm_conv_set_h9_staging: 0 (LDS-DMA), 1 (register weights), 2 (+ halo "
+                                   "prefetch), 3 (LDS-DMA weight pieces between the MFMAs)");
+    g_conv_h9_wr = wr;
     return GM_OK;
 }
 

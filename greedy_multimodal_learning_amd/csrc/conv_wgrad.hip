@@ -210,7 +210,12 @@ __device__ __forceinline__ int wswz(int row) {
     return RB >= 256 ? 4 * (row & 3) : 4 * ((row >> 1) & 1);
 }
 
-template <int MT, int NT>
+// WR = 1: the operands register-staged instead of LDS-DMA'd: global_load_dwordx4 of step
+// s+2 into VGPRs while step s computes, ds_write_b128 of step s+1 into the buffer step s-1
+// freed - an LDS-DMA piece costs its wave ~60-185 issue cycles among MFMAs (MI355X_MICROARCH.md
+// price table), eight of them per 16-MFMA step at 128 x 128 tiles; a load + ds_write_b128
+// costs ~20.  Same LDS image, same arithmetic (bit-identical results).
+template <int MT, int NT, int WR = 0>
 __global__ __launch_bounds__(256) void k_conv_wgrad4(WgradArgs a) {
     constexpr int BK = 64;
     constexpr int BM = 64 * MT, BN = 64 * NT;
@@ -281,14 +286,14 @@ __global__ __launch_bounds__(256) void k_conv_wgrad4(WgradArgs a) {
     typedef __attribute__((address_space(1))) const void* gptr_t;
     typedef __attribute__((address_space(3))) void* lptr_t;
     const void* zero = (const void*)g_wzero16;
-    auto issue = [&](int i, int bufoff) {  // step step0 + i
+    // the sources of step step0 + i's pieces (A: dy rows, B: gathered x rows), in call order
+    // (B's pixel walk advances one step per call)
+    auto sources = [&](int i, const void* (&sa)[GA], const void* (&sb)[GB]) __attribute__((always_inline)) {
         const bool full = (step0 + i + 1) * BK <= M;
 #pragma unroll
         for (int j = 0; j < GA; ++j) {
             const bool ok = a_cok[j] & (full | ((step0 + i) * BK + a_row[j] < M));  // no short-circuit branch
-            const void* src = ok ? (const void*)(a_ptr[j] + (size_t)i * BK * a.Kc) : zero;
-            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + bufoff + (wave * GA + j) * 1024), 16, 0,
-                                             0);
+            sa[j] = ok ? (const void*)(a_ptr[j] + (size_t)i * BK * a.Kc) : zero;
         }
 #pragma unroll
         for (int j = 0; j < GB; ++j) {
@@ -297,15 +302,44 @@ __global__ __launch_bounds__(256) void k_conv_wgrad4(WgradArgs a) {
             const int hi = h0 + b_dh[j], wi = w0 + b_dw[j];
             const bool ok = b_cok[j] & (b < a.N) & ((unsigned)hi < (unsigned)a.H) & ((unsigned)wi < (unsigned)a.W);
             const int pix = (b * a.H + h0) * a.W + w0;
-            const void* src = ok ? (const void*)(gx + (((long)pix << a.logC) + b_toff[j])) : zero;
-            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + bufoff + SA + (wave * GB + j) * 1024), 16,
-                                             0, 0);
+            sb[j] = ok ? (const void*)(gx + (((long)pix << a.logC) + b_toff[j])) : zero;
             // next step's pixel: + 64 = (adv_b, adv_p, adv_q), one carry per component at most
             int nq = q + a.adv_q, np = p + a.adv_p, nb = b + a.adv_b;
             if (nq >= a.Q) { nq -= a.Q; ++np; }
             if (np >= a.P) { np -= a.P; ++nb; }
             b_b[j] = nb; b_p[j] = np; b_q[j] = nq;
         }
+    };
+    auto issue = [&](int i, int bufoff) __attribute__((always_inline)) {  // step step0 + i
+        const void* sa[GA];
+        const void* sb[GB];
+        sources(i, sa, sb);
+#pragma unroll
+        for (int j = 0; j < GA; ++j)
+            __builtin_amdgcn_global_load_lds((gptr_t)sa[j], (lptr_t)(lds + bufoff + (wave * GA + j) * 1024), 16, 0, 0);
+#pragma unroll
+        for (int j = 0; j < GB; ++j)
+            __builtin_amdgcn_global_load_lds((gptr_t)sb[j], (lptr_t)(lds + bufoff + SA + (wave * GB + j) * 1024), 16, 0,
+                                             0);
+    };
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 ra[WR ? GA : 1], rb[WR ? GB : 1];
+    auto gload = [&](int i) __attribute__((always_inline)) {  // step step0 + i into registers
+        const void* sa[GA];
+        const void* sb[GB];
+        sources(i, sa, sb);
+#pragma unroll
+        for (int j = 0; j < GA; ++j) ra[WR ? j : 0] = *reinterpret_cast<const u32x4*>(sa[j]);
+#pragma unroll
+        for (int j = 0; j < GB; ++j) rb[WR ? j : 0] = *reinterpret_cast<const u32x4*>(sb[j]);
+    };
+    auto swrite = [&](int bufoff) __attribute__((always_inline)) {  // the same LDS image as issue()
+#pragma unroll
+        for (int j = 0; j < GA; ++j)
+            *reinterpret_cast<u32x4*>(lds + bufoff + (wave * GA + j) * 1024 + lane * 16) = ra[WR ? j : 0];
+#pragma unroll
+        for (int j = 0; j < GB; ++j)
+            *reinterpret_cast<u32x4*>(lds + bufoff + SA + (wave * GB + j) * 1024 + lane * 16) = rb[WR ? j : 0];
     };
 
     floatx16 acc[MT][NT];
@@ -376,16 +410,37 @@ __global__ __launch_bounds__(256) void k_conv_wgrad4(WgradArgs a) {
     constexpr int BUF1 = SA + SB;
     using B0 = std::integral_constant<int, 0>;
     using B1 = std::integral_constant<int, BUF1>;
-    if (nst > 0) issue(0, 0);
-    __syncthreads();
     int i = 0;
-    for (; i + 1 < nst; i += 2) {  // steps i (buffer 0) and i+1 (buffer 1)
-        issue(i + 1, BUF1);
-        compute(B0{});
+    if constexpr (WR) {
+        // LDS stores drained, then the barrier; the clobber keeps LDS accesses on their side
+        auto bar = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+        if (nst > 0) {
+            gload(0);
+            swrite(0);
+        }
+        if (nst > 1) gload(1);
+        bar();
+        for (; i + 1 < nst; i += 2) {  // steps i (buffer 0) and i+1 (buffer 1)
+            compute(B0{});
+            swrite(BUF1);  // step i+1 (buffer 1 was freed by step i-1, before the last barrier)
+            if (i + 2 < nst) gload(i + 2);
+            bar();
+            compute(B1{});
+            if (i + 2 < nst) swrite(0);
+            if (i + 3 < nst) gload(i + 3);
+            bar();
+        }
+    } else {
+        if (nst > 0) issue(0, 0);
         __syncthreads();
-        if (i + 2 < nst) issue(i + 2, 0);
-        compute(B1{});
-        __syncthreads();
+        for (; i + 1 < nst; i += 2) {  // steps i (buffer 0) and i+1 (buffer 1)
+            issue(i + 1, BUF1);
+            compute(B0{});
+            __syncthreads();
+            if (i + 2 < nst) issue(i + 2, 0);
+            compute(B1{});
+            __syncthreads();
+        }
     }
     if (i < nst) compute(B0{});  // odd step count: the last step sits in buffer 0
 
@@ -560,15 +615,24 @@ static WPlan plan(const gm_conv_desc_hw* d, int G = 1) {
 
 using namespace gm;
 
+// operand staging of k_conv_wgrad4 (its WR argument; GM_WGRAD_WR at load, default 0)
+static int g_wgrad_wr = [] {
+    const char* e = getenv("GM_WGRAD_WR");
+    return e ? atoi(e) : 0;
+}();
+
 template <int MT, int NT>
 static int launch_wgrad4(const WgradArgs& a, int grid, hipStream_t st) {
     const size_t lds = (size_t)2 * 64 * 2 * (64 * MT + 64 * NT);
     static bool attr = false;  // idempotent, safe to race
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)k_conv_wgrad4<MT, NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute((const void*)k_conv_wgrad4<MT, NT, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
         attr = true;
     }
-    k_conv_wgrad4<MT, NT><<<grid, 256, lds, st>>>(a);
+    if (g_wgrad_wr) k_conv_wgrad4<MT, NT, 1><<<grid, 256, lds, st>>>(a);
+    else k_conv_wgrad4<MT, NT><<<grid, 256, lds, st>>>(a);
     return check_launch("k_conv_wgrad4");
 }
 
@@ -691,6 +755,12 @@ extern "C" int gm_conv2d_wgrad_hw_bf16(const gm_conv_desc_hw* d, const void* dy,
                                        int c_real, int accumulate, void* scratch, size_t scratch_bytes,
                                        void* stream) {
     return gm_conv2d_wgrad_grouped_bf16(d, 1, dy, x, dw, 0, c_real, accumulate, scratch, scratch_bytes, stream);
+}
+
+extern "C" int gm_conv_set_wgrad_staging(int wr) {
+    GM_REQUIRE(wr == 0 || wr == 1, "gm_conv_set_wgrad_staging: 0 (LDS-DMA) or 1 (register-staged)");
+    g_wgrad_wr = wr;
+    return GM_OK;
 }
 
 extern "C" int gm_conv_set_wgrad_wide(int mode) {

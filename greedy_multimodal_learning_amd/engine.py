@@ -326,8 +326,13 @@ class BalancedStep:
         streams = views if streams_enabled() else 1
         from . import vtrunk
         if vtrunk.ENABLED and hasattr(model, "_forward_stacked") and self.compute_dtype == torch.bfloat16:
-            # the view-batched trunk: grouped launches on one stream (+ its weight gradients)
+            # the view-batched trunk: grouped launches on one stream (+ its weight gradients);
+            # no view streams, so the single-launch BatchNorm may size its grid for that
+            # (GM_BN_FUSE_STREAMS, when set, keeps the operator's value)
             streams = 2 if vtrunk.WGRAD_STREAM else 1
+            if "GM_BN_FUSE_STREAMS" not in os.environ:
+                from .streams import set_concurrency
+                set_concurrency(streams)
         sharers, reserved = 1, 0
         if self.pg is not None and self.world > 1:
             import socket

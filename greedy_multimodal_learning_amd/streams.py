@@ -63,6 +63,14 @@ def reserve_concurrency(n):
         _bn_concurrency[0] = n
 
 
+def set_concurrency(n):
+    """Set the single-launch BatchNorm concurrency outright (the engine's view-batched
+    trunk: one trunk stream); a later ViewStreams still raises it for its streams."""
+    from . import _lib as L
+    L.check(L.load().gm_bn_set_concurrency(int(n)), "gm_bn_set_concurrency")
+    _bn_concurrency[0] = int(n)
+
+
 class ViewStreams:
     def __init__(self, device, n):
         reserve_concurrency(n + 2)  # one fused BN per view stream + headroom (RCCL, copies)

@@ -312,12 +312,19 @@ int gm_conv_set_halo(int on);
 /* The halo kernel with its nine taps unrolled (k_conv_h9; default on, GM_CONV_H9=0 at
  * load or gm_conv_set_h9(0) selects the run-time-decoded k_conv_halo, an A/B switch). */
 int gm_conv_set_h9(int on);
+/* k_conv_h9's operand staging: 0 = LDS-DMA (global_load_lds) weights and halo; 1 = weights
+ * register-staged (global_load_dwordx4 one k-tile ahead + ds_write_b128); 2 = as 1, and the
+ * next channel chunk's halo prefetched into registers (GM_CONV_H9_WR at load; A/B switch) */
+int gm_conv_set_h9_staging(int wr);
 /* Split-K target: workgroups wanted from splitting K of 128x128-tile convolutions whose
  * tiles alone do not fill the device (default 384, GM_CONV_SPLITK at load; 0 = never). */
 int gm_conv_set_splitk(int target);
 /* Weight-gradient tile form (process-wide; GM_WGRAD_WIDE at load): bit 0 takes
  * 256-row tiles for K >= 256, bit 1 256-column (tap, channel) tiles; 0 = 128 x 128. */
 int gm_conv_set_wgrad_wide(int mode);
+/* Weight-gradient operand staging: 0 = LDS-DMA pieces, 1 = register-staged (global_load_dwordx4
+ * two steps ahead + ds_write_b128; same LDS image and arithmetic).  GM_WGRAD_WR at load. */
+int gm_conv_set_wgrad_staging(int wr);
 /* Resident-weight kernel for 3x3 / stride-1 convolutions with 64 -> 64 channels (ResNet
  * layer 1, forward and input gradient; default on, GM_CONV_RW=0 at load or
  * gm_conv_set_rw(0) selects the im2col kernel for them). */

@@ -25,9 +25,10 @@ pytestmark = pytest.mark.gpu
 B, H, STEPS, EPS, WINDOW, LR = 64, 224, 36, 0.01, 5, 0.1
 # bf16-vs-fp32 d_BDR noise bound: d_BDR = sum of four log10(M) terms, so its error is at
 # most (1/ln 10) x the sum of the four gradient-sum relative errors; with the C2 test's
-# measured gradient-sum errors (9.8e-3, 6.0e-4, 1.7e-3, 2.0e-3; test_gpu_c2_bf16.py):
-# 0.434 x 1.41e-2 = 6.1e-3.  (Measured on MI355X: max 3.4e-3 over the deciding steps.)
-BAND = 6e-3
+# measured gradient-sum errors on the view-batched trunk (1.11e-2, 4.2e-4, 4.2e-3, 4.3e-3;
+# test_gpu_c2_bf16.py, round 3): 0.434 x 2.0e-2 = 8.7e-3 -> 9e-3.  (Measured on MI355X:
+# max 4.3e-3 and 6.6e-3 over the deciding steps of two runs; per-view trunks: 3.4e-3.)
+BAND = 9e-3
 
 
 @pytest.fixture(scope="module")

@@ -45,6 +45,12 @@ def main():
         # "fBN.NB": k_conv_h9 forced to BN-channel tiles and an NB-stage weight ring
         # "s<n>": split-K target n (0: never split), auto form otherwise
         L.check(lib.gm_conv_set_splitk(int(p[1:]) if p[0] == "s" else 384), "set_splitk")
+        # "r<n>": k_conv_h9 with operand staging n (gm_conv_set_h9_staging)
+        L.check(lib.gm_conv_set_h9_staging(int(p[1:]) if p[0] == "r" else 0), "set_h9_staging")
+        # "g<n>": weight-gradient operand staging n (gm_conv_set_wgrad_staging)
+        L.check(lib.gm_conv_set_wgrad_staging(int(p[1:]) if p[0] == "g" else 0), "set_wgrad_staging")
+        if p[0] in ("r", "g"):
+            p = "h"
         if p[0] == "s":
             p = "h"
         if p[0] == "f":
@@ -94,7 +100,7 @@ def main():
                 continue
             d = (out.float() - ref[k].float()).abs().max().item()
             sc = ref[k].float().abs().max().item()
-            if (p[:1] not in ("h", "H", "W", "o", "f", "s") and not torch.equal(out, ref[k])) or d > 2e-2 * sc:
+            if (p[:1] not in ("h", "H", "W", "o", "f", "s", "r", "g") and not torch.equal(out, ref[k])) or d > 2e-2 * sc:
                 print(f"MISMATCH {p} {name} {op}: max |diff| {d} (scale {sc})", flush=True)
                 sys.exit(3)
     print("all variants agree", flush=True)

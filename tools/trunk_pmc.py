@@ -104,8 +104,9 @@ def report(dirs, json_out=None):
     conv = [r for r in rows if r["flops"]]
     w = sum(r["count"] for r in conv)
     fam = {
-        "what": "trunk convolution family of one view at B=64 (fwd + dgrad + wgrad of every shape, count-weighted "
-                "as bench.py's roofline), HBM bytes from rocprofv3 PMC (2 x FETCH_SIZE + WRITE_SIZE per call)",
+        "what": "trunk convolution family as the step launches it: both views per launch (view-batched trunk), "
+                "B=64 per view (fwd + dgrad + wgrad of every position, count-weighted as bench.py's roofline), "
+                "HBM bytes from rocprofv3 PMC (2 x FETCH_SIZE + WRITE_SIZE per call)",
         "launches": w,
         "hbm_bytes_per_launch": sum((r["hbm_read"] + r["hbm_write"]) * r["count"] for r in conv) / w,
         "algorithmic_bytes_per_launch": sum(r["bytes"] * r["count"] for r in conv) / w,

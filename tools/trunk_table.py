@@ -1,8 +1,9 @@
-"""Per-shape launch table of the bf16 ResNet-18 trunk of ONE view at the step's batch:
-every convolution pass (forward, input gradient, weight gradient; the stem on its
-pixel-pair view), every BatchNorm forward/backward (single-launch fused kernels) and
-the stem max-pool, each timed with HIP events on its launch stream behind a device
-sleep (kernel time, not host enqueue time).
+"""Per-shape launch table of the bf16 ResNet-18 trunk at the step's batch, as the step
+launches it: the two views' trunks batched into grouped launches (vtrunk.py; --groups 1
+for one view alone): every convolution pass (forward, input gradient, weight gradient;
+the stem on its pixel-pair view), every BatchNorm forward/backward (single-launch fused
+kernels) and the stem's BN-ReLU-max-pool, each timed with HIP events on its launch
+stream behind a device sleep (kernel time, not host enqueue time).
 
 For each op: algorithmic FLOPs (real channels) and HBM bytes (each operand read once,
 each output written once), average microseconds, achieved TFLOP/s and GB/s, and the
@@ -69,8 +70,8 @@ def _row(name, op, cnt, flops, nbytes, secs, launches_per_call=1):
                 launches=launches_per_call)
 
 
-def conv_rows(B, dev, reps=10, rotate_bytes=0, dtype="bf16"):
-    ops = conv_ops(B, dev, rotate_bytes) if dtype == "bf16" else conv_ops_f32(B, dev, rotate_bytes)
+def conv_rows(B, dev, reps=10, rotate_bytes=0, dtype="bf16", G=2):
+    ops = conv_ops(B, dev, rotate_bytes, G) if dtype == "bf16" else conv_ops_f32(B, dev, rotate_bytes)
     return [_row(name, op, cnt, flops, nbytes, _time(fn, reps)) for name, op, cnt, flops, nbytes, fn in ops]
 
 
@@ -121,117 +122,171 @@ def _cycle(fns):
     return fn
 
 
-def _make_bf16(op, B, dev, C, H, W, K, R, st, pad, P, Q):
-    """A callable running one pass of one trunk convolution on fresh bf16 operands."""
-    from greedy_multimodal_learning_amd import conv as G
+def _make_bf16(op, B, dev, C, H, W, K, R, st, pad, P, Q, G=2):
+    """A callable running one pass of one trunk convolution position on fresh bf16 operands:
+    the G views' launch of the view-batched trunk (vtrunk.py: activations stacked along the
+    batch, one weight per view, gm_conv2d_*_grouped_bf16); G = 1 is one view alone."""
+    from greedy_multimodal_learning_amd import conv as CV
+    from greedy_multimodal_learning_amd import vtrunk as VT
     from greedy_multimodal_learning_amd import _lib as L
     import ctypes
-    Cp = G._cpad(C)
-    x = torch.randn(B, Cp, H, W, device=dev).bfloat16().contiguous(memory_format=CL)
-    w = torch.randn(K, Cp, R, R, device=dev).bfloat16().contiguous(memory_format=CL)
-    dy = torch.randn(B, K, P, Q, device=dev).bfloat16().contiguous(memory_format=CL)
+    lib = L.load()
+    Cp = CV._cpad(C)
+    x = torch.randn(G * B, Cp, H, W, device=dev).bfloat16().contiguous(memory_format=CL)
+    dy = torch.randn(G * B, K, P, Q, device=dev).bfloat16().contiguous(memory_format=CL)
     if C == 3:  # the stem runs on the pixel-pair view; its input gradient is never computed
-        xp = G.stem_pack_input(x[:, :3], R, R, pad)
-        wp = G.stem_pack_weight(w[:, :3].float())
+        P_, Q_, Sp, Hp, Wp = CV._stem_geom(H, W, R, R, pad)
+        xp = torch.empty(G * B, Hp, Wp // 2, 8, device=dev, dtype=torch.bfloat16)
+        wp = torch.empty(G, K, R, Sp, 8, device=dev, dtype=torch.bfloat16)
+        for g in range(G):
+            CV.stem_pack(x[g * B:(g + 1) * B, :3], torch.randn(K, 3, R, R, device=dev), pad,
+                         xp=xp[g * B:(g + 1) * B], wp=wp[g])
+        d = CV._desc_hw(B, Hp, Wp // 2, 8, K, R, Sp, 2, 1, 0, 0)
         if op == "fwd":
-            return lambda: G.stem_fwd(xp, wp, P, Q)
-        d = G._desc_hw(B, xp.shape[2], xp.shape[3], 8, K, R, wp.shape[3], 2, 1, 0, 0)
-        need = L.load().gm_conv2d_wgrad_hw_scratch(ctypes.byref(d))
+            y = torch.empty(G * B, K, P, Q, device=dev, dtype=torch.bfloat16)
+            return lambda: L.check(lib.gm_conv2d_fwd_grouped_bf16(ctypes.byref(d), G, xp.data_ptr(), wp.data_ptr(),
+                                                                  K * R * Sp * 8, y.data_ptr(), 0, 0,
+                                                                  L.stream_of(dev)), "stem fwd")
+        need = lib.gm_conv2d_wgrad_grouped_scratch(ctypes.byref(d), G)
         scr = torch.empty(max(need, 16), device=dev, dtype=torch.uint8)
-        dwp = torch.empty(K, R, wp.shape[3], 8, device=dev, dtype=torch.float32)
-
-        def stem_wgrad():
-            L.check(L.load().gm_conv2d_wgrad_hw_bf16(ctypes.byref(d), dy.data_ptr(), xp.data_ptr(),
-                                                     dwp.data_ptr(), 8, 0, scr.data_ptr(), need,
-                                                     L.stream_of(dev)), "wgrad_hw")
-        return stem_wgrad
+        dwp = torch.empty(G, K, R, Sp, 8, device=dev, dtype=torch.float32)
+        return lambda: L.check(lib.gm_conv2d_wgrad_grouped_bf16(ctypes.byref(d), G, dy.data_ptr(), xp.data_ptr(),
+                                                                dwp.data_ptr(), K * R * Sp * 8, 8, 0, scr.data_ptr(),
+                                                                need, L.stream_of(dev)), "stem wgrad")
+    n = K * R * R * Cp
     if op == "fwd":
-        return lambda: G.conv_fwd(x, w, st, pad)
+        w = torch.randn(G, K, R, R, Cp, device=dev).bfloat16()
+        y = torch.empty(G * B, K, P, Q, device=dev, dtype=torch.bfloat16).contiguous(memory_format=CL)
+        d = CV._desc_hw(B, H, W, Cp, K, R, R, st, st, pad, pad)
+        ws, nb = VT._splitk_g(dev, CV._desc(B, H, W, Cp, K, R, R, st, pad), G, False)
+        return lambda: L.check(lib.gm_conv2d_fwd_grouped_bf16(ctypes.byref(d), G, x.data_ptr(), w.data_ptr(), n,
+                                                              y.data_ptr(), ws, nb, L.stream_of(dev)), "fwd")
     if op == "dgrad":
-        wt = w.permute(1, 0, 2, 3).contiguous(memory_format=CL)
-        return lambda: G.conv_dgrad_t(dy, wt, H, W, st, pad)
-    dw = torch.empty(K, C, R, R, device=dev, dtype=torch.float32).contiguous(memory_format=CL)
-    return lambda: G.conv_wgrad(dy, x, R, R, st, pad, C, out=dw)
+        wt = torch.randn(G, Cp, R, R, K, device=dev).bfloat16()
+        dx = torch.empty(G * B, Cp, H, W, device=dev, dtype=torch.bfloat16).contiguous(memory_format=CL)
+        d = CV._desc(B, H, W, Cp, K, R, R, st, pad)
+        ws, nb = VT._splitk_g(dev, d, G, True)
+        return lambda: L.check(lib.gm_conv2d_dgrad_grouped_bf16(ctypes.byref(d), G, dy.data_ptr(), wt.data_ptr(),
+                                                                n, dx.data_ptr(), 0, ws, nb, L.stream_of(dev)),
+                               "dgrad")
+    d = CV._desc_hw(B, H, W, Cp, K, R, R, st, st, pad, pad)
+    need = lib.gm_conv2d_wgrad_grouped_scratch(ctypes.byref(d), G)
+    scr = torch.empty(max(need, 16), device=dev, dtype=torch.uint8)
+    dw = torch.empty(G, K, R, R, C, device=dev, dtype=torch.float32)
+    return lambda: L.check(lib.gm_conv2d_wgrad_grouped_bf16(ctypes.byref(d), G, dy.data_ptr(), x.data_ptr(),
+                                                            dw.data_ptr(), K * R * R * C, C, 0, scr.data_ptr(), need,
+                                                            L.stream_of(dev)), "wgrad")
 
 
-def conv_ops(B, dev, rotate_bytes=0):
-    """(name, pass, count per view, FLOPs, algorithmic bytes, callable) of every trunk
-    convolution pass of one view at batch B.  rotate_bytes > 0: each callable cycles over
-    enough distinct operand sets that consecutive launches touch more than rotate_bytes
-    (beyond the 256 MiB Infinity Cache: every launch reads HBM, not the last one's lines)."""
+def conv_ops(B, dev, rotate_bytes=0, G=2):
+    """(name, pass, count per step, FLOPs, algorithmic bytes, callable) of every trunk
+    convolution position at batch B per view, G views per launch (the view-batched trunk).
+    rotate_bytes > 0: each callable cycles over enough distinct operand sets that
+    consecutive launches touch more than rotate_bytes (beyond the 256 MiB Infinity Cache:
+    every launch reads HBM, not the last one's lines)."""
     out = []
     for name, (C, H, W, K, R, st, pad, cnt) in TRUNK:
         P, Q = (H + 2 * pad - R) // st + 1, (W + 2 * pad - R) // st + 1
-        flops = 2.0 * B * P * Q * K * C * R * R
-        xb, yb, wb = B * H * W * C * 2, B * P * Q * K * 2, K * C * R * R * 2
-        passes = [("fwd", xb + wb + yb), ("wgrad", xb + yb + K * C * R * R * 4)]
+        flops = 2.0 * G * B * P * Q * K * C * R * R
+        xb, yb, wb = G * B * H * W * C * 2, G * B * P * Q * K * 2, G * K * C * R * R * 2
+        passes = [("fwd", xb + wb + yb), ("wgrad", xb + yb + G * K * C * R * R * 4)]
         if C != 3:
             passes.insert(1, ("dgrad", yb + wb + xb))
         for op, nbytes in passes:
-            args = (op, B, dev, C, H, W, K, R, st, pad, P, Q)
+            args = (op, B, dev, C, H, W, K, R, st, pad, P, Q, G)
             sets = max(1, -(-int(rotate_bytes) // nbytes)) if rotate_bytes else 1
             fn = _make_bf16(*args) if sets == 1 else _cycle([_make_bf16(*args) for _ in range(sets)])
             out.append((name, op, cnt, flops, nbytes, fn))
     return out
 
 
-def bn_rows(B, dev, reps=10):
-    return [_row(name, op, cnt, flops, nbytes, _time(fn, reps)) for name, op, cnt, flops, nbytes, fn in bn_ops(B, dev)]
+def bn_rows(B, dev, reps=10, G=2):
+    return [_row(name, op, cnt, flops, nbytes, _time(fn, reps))
+            for name, op, cnt, flops, nbytes, fn in bn_ops(B, dev, G)]
 
 
-def bn_ops(B, dev):
-    """The same for every BatchNorm forward/backward of one view and the stem max-pool."""
-    from greedy_multimodal_learning_amd import bn as BN
-    from greedy_multimodal_learning_amd import pool as PL
+def bn_ops(B, dev, G=2):
+    """The same for every BatchNorm forward/backward position (the G views' grouped launch,
+    gm_bn_*_grouped_bf16) and the stem's statistics + BN-ReLU-max-pool / max-pool backward."""
+    import ctypes
+    from greedy_multimodal_learning_amd import _lib as L
+    from greedy_multimodal_learning_amd import vtrunk as VT
+    lib = L.load()
     out = []
     for name, (C, H, W, res, relu, cnt) in BNS:
         M = B * H * W
-        x = torch.randn(B, C, H, W, device=dev).bfloat16().contiguous(memory_format=CL)
-        r = torch.randn(B, C, H, W, device=dev).bfloat16().contiguous(memory_format=CL) if res else None
-        dy = torch.randn(B, C, H, W, device=dev).bfloat16().contiguous(memory_format=CL)
-        w = torch.ones(C, device=dev)
-        b = torch.zeros(C, device=dev)
-        rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
-        coef = torch.empty(2 * C, device=dev) if relu and not res else None
-        st = {}
+        stem = name == "bn1"
+        x = torch.randn(G * B, C, H, W, device=dev).bfloat16().contiguous(memory_format=CL)
+        r = torch.randn(G * B, C, H, W, device=dev).bfloat16().contiguous(memory_format=CL) if res else None
+        dy = torch.randn(G * B, C, H, W, device=dev).bfloat16().contiguous(memory_format=CL)
+        y = torch.empty_like(x)
+        dx = torch.empty_like(x)
+        dres = torch.empty_like(x) if res else None
+        prm = torch.ones(G, 8, C, device=dev)  # gamma, beta, rm, rv, sm, si, dg, db per view
+        prm[:, 1].zero_()
+        prm[:, 2].zero_()
+        maskx = relu and not res
+        coef = torch.empty(G, 2 * C, device=dev)
+        buf = VT._bn_scratch_g(dev, M, C, G)
+        rows = lambda g: slice(g * B, (g + 1) * B)  # noqa: E731
+        fd = [L.BnFwd(M, C, int(relu), x[rows(g)].data_ptr(), r[rows(g)].data_ptr() if res else 0,
+                      0 if stem else y[rows(g)].data_ptr(), prm[g, 0].data_ptr(), prm[g, 1].data_ptr(),
+                      prm[g, 2].data_ptr(), prm[g, 3].data_ptr(), 0.1, 1e-5, prm[g, 4].data_ptr(), prm[g, 5].data_ptr(),
+                      0, coef[g].data_ptr() if maskx else 0) for g in range(G)]
+        bd = [L.BnBwd(M, C, int(relu), dy[rows(g)].data_ptr(), 0 if maskx or not relu else y[rows(g)].data_ptr(),
+                      x[rows(g)].data_ptr(), prm[g, 0].data_ptr(), prm[g, 4].data_ptr(), prm[g, 5].data_ptr(),
+                      dx[rows(g)].data_ptr(), dres[rows(g)].data_ptr() if res else 0, prm[g, 6].data_ptr(),
+                      prm[g, 7].data_ptr(), 0, 0, coef[g].data_ptr() if maskx else 0) for g in range(G)]
+        fa, ba = L.arr(L.BnFwd, fd), L.arr(L.BnBwd, bd)
+        st = L.stream_of(dev)
+        fwd_fn = lib.gm_bn_fwd_stats_grouped_bf16 if stem else lib.gm_bn_fwd_train_grouped_bf16
 
-        def fwd(x=x, w=w, b=b, rm=rm, rv=rv, relu=relu, r=r, coef=coef, st=st):
-            st["y"], st["sm"], st["si"] = BN.bn_fwd_train(x, w, b, rm, rv, None, 0.1, 1e-5, relu, r, coef)
+        def fwd(fa=fa, buf=buf, fwd_fn=fwd_fn):
+            L.check(fwd_fn(fa, G, buf.data_ptr(), buf.numel(), st), "bn fwd")
+
+        def bwd(ba=ba, buf=buf):
+            L.check(lib.gm_bn_bwd_grouped_bf16(ba, G, buf.data_ptr(), buf.numel(), st), "bn bwd")
         fwd()
-        dg, db = torch.empty(C, device=dev), torch.empty(C, device=dev)
-        maskx = coef is not None
-
-        def bwd(dy=dy, x=x, w=w, relu=relu, res=res, dg=dg, db=db, coef=coef, maskx=maskx, st=st):
-            BN.bn_bwd(dy, None if maskx else st["y"], x, w, st["sm"], st["si"], relu, res, dg, db, False,
-                      coef if maskx else None)
-        e = M * C * 2
-        out.append((name, "bn_fwd", cnt, 0, e * (2 + (1 if res else 0)), fwd))
+        e = G * M * C * 2
+        out.append((name, "bn_stats" if stem else "bn_fwd", cnt, 0, e * (1 if stem else 2 + (1 if res else 0)), fwd))
         out.append((name, "bn_bwd", cnt, 0, e * (3 + (1 if relu and not maskx else 0) + (1 if res else 0)), bwd))
-    # stem max-pool (3x3/2 on the 112^2 stem output): read x, write y + 1-byte argmax
-    x = torch.randn(B, 64, 112, 112, device=dev).bfloat16().contiguous(memory_format=CL).requires_grad_(True)
-    pool = PL.GMMaxPool2d(3, 2, 1)
-    y = pool(x)
-    gy = torch.randn_like(y)
-    e_in, e_out = B * 112 * 112 * 64, B * 56 * 56 * 64
-    out.append(("maxpool", "fwd", 1, 0, e_in * 2 + e_out * 3, lambda: pool(x.detach())))
-    out.append(("maxpool", "bwd", 1, 0, e_out * 3 + e_in * 2,
-                lambda: torch.autograd.grad(y, x, gy, retain_graph=True)))
+        if stem:  # the stem's BN + ReLU applied inside the max-pool, and the pool's backward
+            P, Q = H // 2, W // 2
+            yp = torch.empty(G * B, C, P, Q, device=dev, dtype=torch.bfloat16).contiguous(memory_format=CL)
+            idx = torch.empty(G * B, P, Q, C, device=dev, dtype=torch.uint8)
+            gyp = torch.randn(G * B, C, P, Q, device=dev).bfloat16().contiguous(memory_format=CL)
+            d1 = L.PoolDesc(B, H, W, C, 3, 2, 1)
+            dG = L.PoolDesc(G * B, H, W, C, 3, 2, 1)
+
+            def pool_fwd(d1=d1, x=x, coef=coef, yp=yp, idx=idx):
+                L.check(lib.gm_bn_relu_maxpool2d_fwd_grouped_bf16(ctypes.byref(d1), G, x.data_ptr(), coef.data_ptr(),
+                                                                  yp.data_ptr(), idx.data_ptr(), st), "pool fwd")
+
+            def pool_bwd(dG=dG, gyp=gyp, idx=idx, dx=dx):
+                L.check(lib.gm_maxpool2d_bwd_bf16(ctypes.byref(dG), gyp.data_ptr(), idx.data_ptr(), dx.data_ptr(),
+                                                  st), "pool bwd")
+            e_in, e_out = G * M * C, G * B * P * Q * C
+            out.append(("maxpool", "bn_relu_fwd", 1, 0, e_in * 2 + e_out * 3, pool_fwd))
+            out.append(("maxpool", "bwd", 1, 0, e_out * 3 + e_in * 2, pool_bwd))
     return out
 
 
-def measure_family(B, dev, reps=10, rotate_bytes=320e6, dtype="bf16"):
-    """The conv family (fwd + dgrad + wgrad of every trunk shape of one view, weighted by
-    its count per view): (flops, secs, launches, rows).  Launches rotate over operand sets
-    of more than the 256 MiB Infinity Cache (rotate_bytes), so none reads warm lines."""
-    rows = conv_rows(B, dev, reps, rotate_bytes, dtype)
+def measure_family(B, dev, reps=10, rotate_bytes=320e6, dtype="bf16", G=2):
+    """The conv family (fwd + dgrad + wgrad of every trunk position, weighted by its count
+    per step; bf16: the G views' grouped launches the step runs, fp32: one view's launches,
+    the reference-precision path runs the views one by one): (flops, secs, launches, rows).
+    Launches rotate over operand sets of more than the 256 MiB Infinity Cache
+    (rotate_bytes), so none reads warm lines."""
+    rows = conv_rows(B, dev, reps, rotate_bytes, dtype, G)
     flops = sum(r["flops"] * r["count"] for r in rows)
     secs = sum(r["us"] * 1e-6 * r["count"] for r in rows)
     launches = sum(r["count"] for r in rows)
     return flops, secs, launches, rows
 
 
-def markdown(rows, B):
-    out = [f"| shape | pass | x/view | GFLOP | MB | avg us | TFLOP/s | GB/s | bound | frac of bound |",
+def markdown(rows, B, G=2):
+    out = [f"{G} view(s) per launch (view-batched trunk), batch {B} per view", "",
+           f"| shape | pass | x/step | GFLOP | MB | avg us | TFLOP/s | GB/s | bound | frac of bound |",
            "|---|---|---|---|---|---|---|---|---|---|"]
     for r in rows:
         bt = f"mfma {MFMA_PEAK_TFS:.0f}" if r["bound"] == "mfma" and r["flops"] else (
@@ -242,13 +297,13 @@ def markdown(rows, B):
     fl = sum(r["flops"] * r["count"] for r in cf)
     s = sum(r["us"] * r["count"] for r in cf) * 1e-6
     out.append("")
-    out.append(f"conv family (one view, B={B}): {fl / 1e12:.3f} TFLOP in {s * 1e3:.3f} ms = "
+    out.append(f"conv family ({G} view(s) per launch, B={B} per view): {fl / 1e12:.3f} TFLOP in {s * 1e3:.3f} ms = "
                f"{fl / s / 1e12:.1f} TFLOP/s = {fl / s / 1e12 / MFMA_PEAK_TFS:.3f} of {MFMA_PEAK_TFS:.0f} TF")
     hb = [r for r in rows if not r["flops"]]
     if hb:
         by = sum(r["bytes"] * r["count"] for r in hb)
         s2 = sum(r["us"] * r["count"] for r in hb) * 1e-6
-        out.append(f"BN + max-pool (one view): {by / 1e9:.3f} GB in {s2 * 1e3:.3f} ms = {by / s2 / 1e9:.0f} GB/s "
+        out.append(f"BN + max-pool ({G} view(s) per launch): {by / 1e9:.3f} GB in {s2 * 1e3:.3f} ms = {by / s2 / 1e9:.0f} GB/s "
                    f"= {by / s2 / 1e9 / HBM_PEAK_GBS:.3f} of {HBM_PEAK_GBS:.0f} GB/s")
     return "\n".join(out)
 
@@ -256,6 +311,7 @@ def markdown(rows, B):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--groups", type=int, default=2, help="views per launch (2: the step's view-batched trunk)")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--md", default=None)
     ap.add_argument("--only", default="", help="conv | bn (default both)")
@@ -267,10 +323,10 @@ def main():
     build.build()
     rows = []
     if a.only in ("", "conv"):
-        rows += conv_rows(a.batch, dev, a.reps, a.rotate_mb * 1e6)
+        rows += conv_rows(a.batch, dev, a.reps, a.rotate_mb * 1e6, G=a.groups)
     if a.only in ("", "bn"):
-        rows += bn_rows(a.batch, dev, a.reps)
-    md = markdown(rows, a.batch)
+        rows += bn_rows(a.batch, dev, a.reps, a.groups)
+    md = markdown(rows, a.batch, a.groups)
     print(md)
     if a.md:
         with open(a.md, "w") as f:
