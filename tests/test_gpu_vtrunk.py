@@ -168,7 +168,12 @@ def test_grouped_bn_matches_per_view(dev, mode, shape):
 
 def test_model_stacked_vs_per_view(dev):
     """MMTM_MVCNN training forward + backward: the view-batched trunk against the per-view
-    trunks (GM_VTRUNK off), same weights and input."""
+    trunks (GM_VTRUNK off), same weights and input, both measured against the fp32 path of
+    the same model (every op on HIP in fp32).  The two bf16 paths round differently (split-K
+    and BatchNorm partitions differ), and at B = 8, 64^2 a flipped ReLU mask moves the
+    small, heavily cancelling stem gradient by tens of percent in EITHER path, so the bound
+    is relative: the stacked path's gradient error against fp32 stays within twice the
+    per-view path's (or 3e-2), parameter by parameter."""
     from greedy_multimodal_learning_amd import vtrunk
     from greedy_multimodal_learning_amd.losses import blend_loss
     from greedy_multimodal_learning_amd.model import MMTM_MVCNN
@@ -176,7 +181,9 @@ def test_model_stacked_vs_per_view(dev):
     B, H = 8, 64
     a = MMTM_MVCNN().to(dev).to(memory_format=CL).train()
     b = MMTM_MVCNN().to(dev).to(memory_format=CL).train()
+    c = MMTM_MVCNN().to(dev).to(memory_format=CL).train()
     b.load_state_dict(a.state_dict())
+    c.load_state_dict(a.state_dict())
     x = torch.randn(B, 2, 3, H, H, device=dev).bfloat16()
     y = torch.randint(0, 40, (B,), device=dev)
     assert vtrunk.usable(a, [a.net_view_0, a.net_view_1], x)
@@ -191,15 +198,21 @@ def test_model_stacked_vs_per_view(dev):
         finally:
             vtrunk.ENABLED = old
         outs[on] = [t.detach().float() for t in o]
+    _, o, _, _ = c(x.float())
+    blend_loss(o, y).backward()
     for i in range(2):
         _close(outs[True][i], outs[False][i], 2e-2, f"logits[{i}]")
-    worst = 0.0
-    for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
-        ga, gb = pa.grad.double(), pb.grad.double()
-        e = float((ga - gb).norm() / (gb.norm() + 1e-30))
-        worst = max(worst, e)
-        assert e < 5e-2, f"{n}: relative gradient difference {e:.3e}"
-    print(f"stacked vs per-view: worst parameter-gradient relative L2 difference {worst:.2e}")
+        _close(outs[True][i], o[i].detach(), 3e-2, f"logits[{i}] vs fp32")
+    worst = []
+    for (n, pa), (_, pb), (_, pc) in zip(a.named_parameters(), b.named_parameters(), c.named_parameters()):
+        ga, gb, gc = pa.grad.double(), pb.grad.double(), pc.grad.double()
+        den = gc.norm() + 1e-30
+        ea, eb = float((ga - gc).norm() / den), float((gb - gc).norm() / den)
+        worst.append((ea, eb, n))
+        assert ea < max(2 * eb, 3e-2), f"{n}: stacked {ea:.3e} vs per-view {eb:.3e} (relative to fp32)"
+    worst.sort(reverse=True)
+    print("stacked vs per-view gradient error vs fp32 (worst 5):",
+          ", ".join(f"{n} {ea:.2e}/{eb:.2e}" for ea, eb, n in worst[:5]))
     for (n, ba), (_, bb) in zip(a.named_buffers(), b.named_buffers()):
         if ba.dtype == torch.long:
             assert int(ba) == int(bb), n
