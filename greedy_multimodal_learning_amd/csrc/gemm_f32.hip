@@ -5,8 +5,10 @@
 // kernel is latency/parallelism-bound, not HBM- or MFMA-bound.  Design:
 //   * each wave computes one 16x16 output tile over a K range with the exact-f32
 //     MFMA (an fmaf chain: same numerics as the fp32 reference's FMA GEMMs);
-//   * a 256-thread workgroup holds TM x TN tiles x KS K-splits (TM*TN*KS = 4);
-//     split-K partial tiles are summed through LDS in fixed order (deterministic);
+//   * a 1024-thread workgroup holds TM x TN tiles x KS K-splits (TM*TN*KS = 16 waves),
+//     KS up to 16 so a wave's dependent chain is at most ~64 k (two rounds of loads in
+//     flight) - the MMTM GEMMs are L2-latency chains, not MFMA work; split-K partial
+//     tiles are summed through LDS in fixed order (deterministic);
 //   * operands are generic strided views (ld0 = 0 broadcasts a row, ptr = NULL
 //     means an all-ones operand) so transposes, concatenated inputs and bias
 //     gradients need no copies; up to 6 problems run in one launch;
@@ -20,36 +22,43 @@ namespace gm {
 constexpr int kMaxGemm = 6;
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
+
 struct GemmArgs {
     gm_gemm p[kMaxGemm];
     int tile_start[kMaxGemm + 1];
     int tiles_n[kMaxGemm];  // workgroup tiles along N
-    int cfg[kMaxGemm];      // TM | TN<<4 | KS<<8
+    int cfg[kMaxGemm];      // TM | TN<<5 | KS<<10
     int nprob;
+    int vec;  // 1: the float4 K-segment form where the operands allow it (A/B knob)
 };
 
 // One K-segment of a wave's 16x16 tile: k in [k0, k1) (segment-local), stepping 4.
 // Lane (li, lk) reads A[m0+li][k+lk] and B[k+lk][n0+li]; pointers advance by
 // 4*ld1 / 4*ld0 per step.  8 steps (32 k) per iteration with the next
 // iteration's 16 loads issued before this iteration's 8 MFMAs (register
-// double-buffer), so L2 latency hides behind MFMA issue.
+// double-buffer), so L2 latency hides behind MFMA issue.  Every load is
+// unconditional from a clamped, in-range address and the validity select comes
+// after it: a "load or constant" select on a per-lane condition makes hipcc branch
+// around each load with a vmcnt(0) inside (cdna_hip_programming.md §5 trap 4c),
+// i.e. one dependent L2 round trip per k-step.
+template <int U>
 __device__ __forceinline__ void seg_mma(floatx4& acc, const gm_operand& A, const gm_operand& B,
                                         int m, int n, bool mrow, bool ncol, int lk, int k0, int k1) {
     if (k1 <= k0) return;
     const bool aone = A.ptr == nullptr;
-    const float* pa = aone ? nullptr : A.ptr + (long)m * A.ld0 + (long)(k0 + lk) * A.ld1;
+    // an all-ones A operand loads (and ignores) B's in-range elements
+    const float* pa = aone ? B.ptr : A.ptr + (long)m * A.ld0 + (long)(k0 + lk) * A.ld1;
     const float* pb = B.ptr + (long)(k0 + lk) * B.ld0 + (long)n * B.ld1;
-    const long sa = 4l * A.ld1, sb = 4l * B.ld0;
+    const long sa = aone ? 0 : 4l * A.ld1, sb = 4l * B.ld0;
     const bool va = mrow && !aone, vb = ncol;
     const float one = mrow ? 1.0f : 0.0f;
     int k = k0;
-    constexpr int U = 8;
     if (k + 4 * U <= k1) {
         float ac[U], bc[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            ac[u] = va ? pa[u * sa] : one;
-            bc[u] = vb ? pb[u * sb] : 0.f;
+            ac[u] = pa[u * sa];
+            bc[u] = pb[u * sb];
         }
         for (; k + 8 * U <= k1; k += 4 * U) {
             float an[U], bn[U];
@@ -57,41 +66,142 @@ __device__ __forceinline__ void seg_mma(floatx4& acc, const gm_operand& A, const
             const float* qb = pb + U * sb;
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                an[u] = va ? qa[u * sa] : one;
-                bn[u] = vb ? qb[u * sb] : 0.f;
+                an[u] = qa[u * sa];
+                bn[u] = qb[u * sb];
             }
 #pragma unroll
-            for (int u = 0; u < U; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[u], bc[u], acc, 0, 0, 0);
+            for (int u = 0; u < U; ++u)
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(va ? ac[u] : one, vb ? bc[u] : 0.f, acc, 0, 0, 0);
 #pragma unroll
             for (int u = 0; u < U; ++u) { ac[u] = an[u]; bc[u] = bn[u]; }
-            if (!aone) pa = qa;
+            pa = qa;
             pb = qb;
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[u], bc[u], acc, 0, 0, 0);
+        for (int u = 0; u < U; ++u)
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(va ? ac[u] : one, vb ? bc[u] : 0.f, acc, 0, 0, 0);
         k += 4 * U;
-        if (!aone) pa += U * sa;
+        pa += U * sa;
         pb += U * sb;
     }
+    // tail (< 4U k): lanes past k1 re-read the segment's last k and contribute zero
     for (; k < k1; k += 4) {
         const bool in = (k + lk) < k1;
-        const float av = (in && va) ? *pa : ((in && aone) ? one : 0.f);
-        const float bv = (in && vb) ? *pb : 0.f;
+        const long back = in ? 0 : (long)(k + lk - (k1 - 1));
+        const float al = pa[-back * (aone ? 0 : A.ld1)];
+        const float bl = pb[-back * B.ld0];
+        const float av = in ? (va ? al : (aone ? one : 0.f)) : 0.f;
+        const float bv = (in && vb) ? bl : 0.f;
         acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
-        if (!aone) pa += sa;
+        pa += sa;
         pb += sb;
     }
 }
 
-__global__ __launch_bounds__(256) void k_gemm_f32(GemmArgs a) {
-    __shared__ floatx4 red[4][64];
-    int pi = 0;
+// The same K-segment on 16-k groups with 16-byte loads along k where an operand is
+// k-contiguous (A.ld1 == 1 / B.ld0 == 1, 16-B aligned rows): the four MFMAs of a group
+// take k = kg + 4*lk + q in MFMA q (any k -> (lane, instruction) assignment is valid
+// when A and B agree), so lane lk's float4 at kg + 4*lk feeds all four; a k-strided
+// operand loads its four scalars at those same k.  A strided fp32 load touches one
+// cache line per lane row for 4 B of it: the float4 form asks the TA for 4x fewer lines.
+// UG groups (16*UG k) per load round, the next round in flight under this one's MFMAs.
+template <bool VA, bool VB, int UG>
+__device__ __forceinline__ void seg_mma_v(floatx4& acc, const gm_operand& A, const gm_operand& B, int m, int n,
+                                          bool mrow, bool ncol, int lk, int k0, int k1) {
+    const bool aone = A.ptr == nullptr;
+    const bool va = mrow && !aone, vb = ncol;
+    const float one = mrow ? 1.0f : 0.0f;
+    const float* pa = aone ? B.ptr : A.ptr + (long)m * A.ld0;
+    const float* pb = B.ptr + (long)n * B.ld1;
+    const long sa = aone ? 0 : A.ld1, sb = B.ld0;
+    auto load = [&](int kg, float (&a)[4], float (&b)[4]) {
+        const int k = kg + 4 * lk;
+        if constexpr (VA) {
+            const float4 t = *reinterpret_cast<const float4*>(pa + k);
+            a[0] = t.x; a[1] = t.y; a[2] = t.z; a[3] = t.w;
+        } else {
 #pragma unroll
-    for (int q = 1; q < kMaxGemm; ++q)
-        if (q < a.nprob && (int)blockIdx.x >= a.tile_start[q]) pi = q;
+            for (int q = 0; q < 4; ++q) a[q] = pa[(long)(k + q) * sa];
+        }
+        if constexpr (VB) {
+            const float4 t = *reinterpret_cast<const float4*>(pb + k);
+            b[0] = t.x; b[1] = t.y; b[2] = t.z; b[3] = t.w;
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) b[q] = pb[(long)(k + q) * sb];
+        }
+    };
+    auto mma = [&](const float (&a)[4], const float (&b)[4]) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(va ? a[q] : one, vb ? b[q] : 0.f, acc, 0, 0, 0);
+    };
+    int kg = k0;
+    if (kg + 16 * UG <= k1) {
+        float ac[UG][4], bc[UG][4];
+#pragma unroll
+        for (int g = 0; g < UG; ++g) load(kg + 16 * g, ac[g], bc[g]);
+        for (; kg + 32 * UG <= k1; kg += 16 * UG) {
+            float an[UG][4], bn[UG][4];
+#pragma unroll
+            for (int g = 0; g < UG; ++g) load(kg + 16 * (UG + g), an[g], bn[g]);
+#pragma unroll
+            for (int g = 0; g < UG; ++g) mma(ac[g], bc[g]);
+#pragma unroll
+            for (int g = 0; g < UG; ++g)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) { ac[g][q] = an[g][q]; bc[g][q] = bn[g][q]; }
+        }
+#pragma unroll
+        for (int g = 0; g < UG; ++g) mma(ac[g], bc[g]);
+        kg += 16 * UG;
+    }
+    for (; kg + 16 <= k1; kg += 16) {
+        float a[4], b[4];
+        load(kg, a, b);
+        mma(a, b);
+    }
+    if (kg < k1) seg_mma<4>(acc, A, B, m, n, mrow, ncol, lk, kg, k1);  // < 16 k left
+}
+
+// one K-segment: the float4 form where the operands allow it (uniform per problem)
+template <int U>
+__device__ __forceinline__ void seg_any(int vec, floatx4& acc, const gm_operand& A, const gm_operand& B, int m,
+                                        int n, bool mrow, bool ncol, int lk, int k0, int k1) {
+    if (k1 <= k0) return;
+    const bool va4 = A.ptr != nullptr && A.ld1 == 1 && (A.ld0 & 3) == 0 && ((uintptr_t)A.ptr & 15) == 0;
+    const bool vb4 = B.ld0 == 1 && (B.ld1 & 3) == 0 && ((uintptr_t)B.ptr & 15) == 0;
+    if (vec == 0 || (!va4 && !vb4)) seg_mma<U>(acc, A, B, m, n, mrow, ncol, lk, k0, k1);
+    else if (va4 && vb4) seg_mma_v<true, true, U / 4>(acc, A, B, m, n, mrow, ncol, lk, k0, k1);
+    else if (va4) seg_mma_v<true, false, U / 4>(acc, A, B, m, n, mrow, ncol, lk, k0, k1);
+    else seg_mma_v<false, true, U / 4>(acc, A, B, m, n, mrow, ncol, lk, k0, k1);
+}
+
+// GEMM forms (gm_gemm_set_waves A/B knob): waves per workgroup x k-steps per load round
+struct GemmForm { int nw, u; };
+// forms 4 / 5: timing diagnostics of form 1 (outputs meaningless): arguments and one
+// store only / everything but the operand loads and MFMAs
+constexpr GemmForm kForms[] = {{4, 8}, {4, 16}, {8, 16}, {16, 8}, {4, 16}, {4, 16}};
+static int g_gemm_form = 1, g_gemm_vec = 1;
+
+// The MMTM GEMMs are dependent-latency chains (kernel arguments -> operand loads ->
+// MFMAs -> epilogue loads -> store), not MFMA work: every round trip costs ~1-2 us.  So
+// the problem index is the grid's y (no tile-table lookup before the argument loads),
+// the epilogue's operands (bias, relu mask, accumulated C) are loaded together with the
+// first operand round, and a wave's K range is at most two load rounds.
+template <int NW, int U, int DIAG = 0>
+__global__ __launch_bounds__(NW * 64) void k_gemm_f32(GemmArgs a) {
+    __shared__ floatx4 red[NW][64];
+    const int pi = blockIdx.y;
     const gm_gemm& p = a.p[pi];
-    const int TM = a.cfg[pi] & 15, TN = (a.cfg[pi] >> 4) & 15, KS = (a.cfg[pi] >> 8) & 15;
-    const int wg = blockIdx.x - a.tile_start[pi];
+    const int cfg = a.cfg[pi];
+    const int TM = cfg & 31, TN = (cfg >> 5) & 31, KS = (cfg >> 10) & 31;
+    const int wg = blockIdx.x;
+    if (wg >= a.tile_start[pi + 1] - a.tile_start[pi]) return;
+    if (DIAG == 1) {  // timing diagnostic: arguments only, one store
+        if (threadIdx.x == 0 && wg == 0) p.C[0] = (float)cfg;
+        return;
+    }
     const int wm = wg / a.tiles_n[pi], wn = wg - wm * a.tiles_n[pi];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tile = wave / KS, ks = wave - tile * KS;
@@ -99,16 +209,29 @@ __global__ __launch_bounds__(256) void k_gemm_f32(GemmArgs a) {
     const int m0 = (wm * TM + tm) * 16, n0 = (wn * TN + tn) * 16;
     const int li = lane & 15, lk = lane >> 4;
     const int K0 = p.K[0], Ktot = p.K[0] + p.K[1];
-    // K range of this split (global k, multiple of 4 per split)
-    const int k4 = (Ktot + 3) >> 2;
-    const int per = (k4 + KS - 1) / KS;
-    const int kb = min(Ktot, ks * per * 4), ke = min(Ktot, (ks + 1) * per * 4);
+    // K range of this split (global k, a multiple of 16 per split)
+    const int k16 = (Ktot + 15) >> 4;
+    const int per = (k16 + KS - 1) / KS;
+    const int kb = min(Ktot, ks * per * 16), ke = min(Ktot, (ks + 1) * per * 16);
     const bool mrow = (m0 + li) < p.M, ncol = (n0 + li) < p.N;
     const int mm = mrow ? m0 + li : 0, nn = ncol ? n0 + li : 0;
+    // epilogue operands, in flight with the first operand round (clamped addresses)
+    float bias = 0.f, mk[4] = {1.f, 1.f, 1.f, 1.f}, co[4] = {0.f, 0.f, 0.f, 0.f};
+    if (ks == 0) {
+        if (p.bias) bias = p.bias[nn];
+        if (p.mask) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) mk[r] = p.mask[(size_t)min(m0 + lk * 4 + r, p.M - 1) * p.ld_mask + nn];
+        }
+        if (p.accumulate) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) co[r] = p.C[(size_t)min(m0 + lk * 4 + r, p.M - 1) * p.ld_c + nn];
+        }
+    }
     floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-    seg_mma(acc, p.A[0], p.B[0], mm, nn, mrow, ncol, lk, kb, min(ke, K0));
-    if (p.K[1] > 0)
-        seg_mma(acc, p.A[1], p.B[1], mm, nn, mrow, ncol, lk, max(kb, K0) - K0, ke - K0);
+    if (DIAG != 2) seg_any<U>(a.vec, acc, p.A[0], p.B[0], mm, nn, mrow, ncol, lk, kb, min(ke, K0));
+    if (DIAG != 2 && p.K[1] > 0)
+        seg_any<U>(a.vec, acc, p.A[1], p.B[1], mm, nn, mrow, ncol, lk, max(kb, K0) - K0, ke - K0);
     if (KS > 1) {
         red[wave][lane] = acc;
         __syncthreads();
@@ -121,17 +244,14 @@ __global__ __launch_bounds__(256) void k_gemm_f32(GemmArgs a) {
     // C/D map of 16x16x4: col = lane&15, row = (lane>>4)*4 + r
     const int n = n0 + li;
     if (n >= p.N) return;
-    const float bias = p.bias ? p.bias[n] : 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int m = m0 + lk * 4 + r;
-        if (m >= p.M) continue;
         float v = acc[r] + bias;
         if (p.act == 1) v = v > 0.f ? v : 0.f;
         else if (p.act == 2) v = 1.0f / (1.0f + expf(-v));
-        if (p.mask) v = p.mask[(size_t)m * p.ld_mask + n] > 0.f ? v : 0.f;
-        float* c = p.C + (size_t)m * p.ld_c + n;
-        *c = p.accumulate ? *c + v : v;
+        v = mk[r] > 0.f ? v : 0.f;
+        if (m < p.M) p.C[(size_t)m * p.ld_c + n] = co[r] + v;
     }
 }
 
@@ -144,7 +264,7 @@ extern "C" int gm_gemm_f32(const gm_gemm* in, int nprob, void* stream) {
     GemmArgs a;
     memset(&a, 0, sizeof(a));
     a.nprob = nprob;
-    int tiles = 0;
+    int tiles = 0, maxt = 0;
     for (int i = 0; i < nprob; ++i) {
         const gm_gemm& p = in[i];
         GM_REQUIRE(p.M >= 1 && p.N >= 1 && p.K[0] >= 0 && p.K[1] >= 0 && p.K[0] + p.K[1] >= 1,
@@ -157,23 +277,45 @@ extern "C" int gm_gemm_f32(const gm_gemm* in, int nprob, void* stream) {
                 GM_REQUIRE(p.B[s].ptr, "gemm_f32[%d]: segment %d has no B operand", i, s);
         a.p[i] = p;
         const int Kt = p.K[0] + p.K[1];
-        int KS = Kt >= 512 ? 4 : (Kt >= 128 ? 2 : 1);
-        int TM, TN;
-        const int rest = 4 / KS;
-        if (rest == 1) { TM = TN = 1; }
-        else if (rest == 2) { if (p.M >= p.N) { TM = 2; TN = 1; } else { TM = 1; TN = 2; } }
-        else {
-            if (p.M <= 16) { TM = 1; TN = 4; }
-            else if (p.N <= 16) { TM = 4; TN = 1; }
-            else { TM = 2; TN = 2; }
+        // K splits: about two load rounds (8U k) per wave, at most the workgroup's waves
+        const GemmForm f = kForms[g_gemm_form];
+        const int NW = f.nw;
+        int KS = 1;
+        while (KS < NW && KS * 8 * f.u < Kt) KS *= 2;
+        const int mt16 = (p.M + 15) / 16, nt16 = (p.N + 15) / 16;
+        int TM = 1, TN = 1;
+        while (TM * TN * KS < NW) {
+            if (TN < nt16 && (TN <= TM || TM >= mt16)) TN *= 2;
+            else if (TM < mt16) TM *= 2;
+            else TN *= 2;
         }
         const int tm = (p.M + 16 * TM - 1) / (16 * TM), tn = (p.N + 16 * TN - 1) / (16 * TN);
-        a.cfg[i] = TM | (TN << 4) | (KS << 8);
+        a.cfg[i] = TM | (TN << 5) | (KS << 10);
         a.tiles_n[i] = tn;
         a.tile_start[i] = tiles;
         tiles += tm * tn;
+        if (tm * tn > maxt) maxt = tm * tn;
     }
     a.tile_start[nprob] = tiles;
-    k_gemm_f32<<<tiles, 256, 0, as_stream(stream)>>>(a);
+    a.vec = g_gemm_vec;
+    const dim3 grid(maxt, nprob);
+    hipStream_t st = as_stream(stream);
+    switch (g_gemm_form) {
+        case 0: k_gemm_f32<4, 8><<<grid, 256, 0, st>>>(a); break;
+        case 1: k_gemm_f32<4, 16><<<grid, 256, 0, st>>>(a); break;
+        case 2: k_gemm_f32<8, 16><<<grid, 512, 0, st>>>(a); break;
+        case 3: k_gemm_f32<16, 8><<<grid, 1024, 0, st>>>(a); break;
+        case 4: k_gemm_f32<4, 16, 1><<<grid, 256, 0, st>>>(a); break;  // diagnostics
+        default: k_gemm_f32<4, 16, 2><<<grid, 256, 0, st>>>(a); break;
+    }
     return check_launch("k_gemm_f32");
+}
+
+extern "C" int gm_gemm_set_form(int form) {
+    g_gemm_vec = !(form & 256);  // bit 8: scalar k-steps only
+    form &= 255;
+    GM_REQUIRE(form >= 0 && form < (int)(sizeof(kForms) / sizeof(kForms[0])), "gemm form must be 0..5 (got %d)",
+               form);
+    g_gemm_form = form;
+    return GM_OK;
 }

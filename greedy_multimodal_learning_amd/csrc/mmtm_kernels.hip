@@ -120,10 +120,14 @@ __global__ __launch_bounds__(256) void k_rowreduce_nchw(RedArgs a, int total_row
 }
 
 // ---------------- NHWC: workgroup per (b, split) ----------------
-template <typename T, bool BWD>
-__global__ __launch_bounds__(256) void k_colreduce_nhwc(RedArgs a) {
+// U: pixels per thread whose 16-B loads are issued together (the loop is HBM-latency-bound:
+// bytes in flight per CU, not instructions, set its rate)
+// NTH: threads per workgroup (256 or 1024: the waves per CU at B x slabs workgroups)
+// NT: nontemporal (streaming) loads - the activations are read once
+template <typename T, bool BWD, int U, int NTH, bool NT = false>
+__global__ __launch_bounds__(NTH) void k_colreduce_nhwc(RedArgs a) {
     constexpr int N = 16 / (int)sizeof(T);  // channels per thread (16 B)
-    __shared__ float red[256 * N];
+    __shared__ float red[NTH * N];
     int pi = 0;
 #pragma unroll
     for (int q = 1; q < kMaxProb; ++q)
@@ -136,7 +140,7 @@ __global__ __launch_bounds__(256) void k_colreduce_nhwc(RedArgs a) {
     const int s = rem / p.ncs, cs = rem - s * p.ncs;
     const int CW = p.cw, c0 = cs * CW;
     const int tpp = CW / N;           // threads per pixel
-    const int ppi = 256 / tpp;        // pixels per iteration
+    const int ppi = NTH / tpp;        // pixels per iteration
     const int t = threadIdx.x;
     const int cc = t % tpp, pl = t / tpp;
     const int hw0 = s * p.hw_per, hw1 = min(p.HW, hw0 + p.hw_per);
@@ -148,7 +152,14 @@ __global__ __launch_bounds__(256) void k_colreduce_nhwc(RedArgs a) {
         auto one = [&](int hw) {
             const size_t off = bbase + (size_t)hw * p.C;
             float vx[N];
-            VecLd<T, 16>::ld((const T*)p.x + off, vx);
+            if constexpr (NT && sizeof(T) == 2) {
+                typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+                const u32x4 t4 = __builtin_nontemporal_load((const u32x4*)((const T*)p.x + off));
+                vx[0] = bf_lo(t4.x); vx[1] = bf_hi(t4.x); vx[2] = bf_lo(t4.y); vx[3] = bf_hi(t4.y);
+                vx[4] = bf_lo(t4.z); vx[5] = bf_hi(t4.z); vx[6] = bf_lo(t4.w); vx[7] = bf_hi(t4.w);
+            } else {
+                VecLd<T, 16>::ld((const T*)p.x + off, vx);
+            }
             if constexpr (BWD) {
                 float vd[N];
                 VecLd<T, 16>::ld((const T*)p.dy + off, vd);
@@ -160,11 +171,17 @@ __global__ __launch_bounds__(256) void k_colreduce_nhwc(RedArgs a) {
             }
         };
         int hw = hw0 + pl;
-        // 4 pixels per thread per round: their loads are independent, so all four are in
+        // U pixels per thread per round: their loads are independent, so all U are in
         // flight together (an HBM-latency-bound loop otherwise)
-        for (; hw + 3 * ppi < hw1; hw += 4 * ppi) {
+        for (; hw + (U - 1) * ppi < hw1; hw += U * ppi) {
 #pragma unroll
-            for (int u = 0; u < 4; ++u) one(hw + u * ppi);
+            for (int u = 0; u < U; ++u) one(hw + u * ppi);
+        }
+        if constexpr (U > 4) {
+            for (; hw + 3 * ppi < hw1; hw += 4 * ppi) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) one(hw + u * ppi);
+            }
         }
         for (; hw < hw1; hw += ppi) one(hw);
     }
@@ -174,9 +191,26 @@ __global__ __launch_bounds__(256) void k_colreduce_nhwc(RedArgs a) {
         for (int j = 0; j < N; ++j) red[pl * CW + cc * N + j] = acc[j];
     }
     __syncthreads();
-    for (int c = t; c < CW; c += 256) {
+    // two-level fixed-order sum over the ppi pixel lanes: R = NTH / CW threads per channel
+    // each sum a strided share, then one thread per channel sums the R shares
+    const int R = CW <= NTH ? NTH / CW : 1;
+    __shared__ float red2[NTH];
+    if (R > 1) {
+        if (t < R * CW) {
+            const int c = t % CW, r = t / CW;
+            float v = 0.f;
+            for (int q = r; q < ppi; q += R) v += red[q * CW + c];
+            red2[r * CW + c] = v;
+        }
+        __syncthreads();
+    }
+    for (int c = t; c < CW; c += NTH) {
         float v = 0.f;
-        for (int q = 0; q < ppi; ++q) v += red[q * CW + c];
+        if (R > 1) {
+            for (int r = 0; r < R; ++r) v += red2[r * CW + c];
+        } else {
+            for (int q = 0; q < ppi; ++q) v += red[q * CW + c];
+        }
         if (p.S == 1) {
             p.out[(size_t)b * p.ld_out + c0 + c] = epilogue(v, p, b, c0 + c);
         } else {
@@ -363,6 +397,37 @@ using namespace gm;
 
 // ======================= host entry points =======================
 
+// k_colreduce_nhwc form: pixels in flight per thread (4, 8, 16) and threads per workgroup
+// (256, 1024); GM_RED_UNROLL / GM_RED_THREADS / gm_mmtm_set_reduce_form, an A/B knob
+static int g_red_unroll = -1, g_red_threads = -1;
+static int red_unroll() {
+    if (g_red_unroll < 0) {
+        const char* e = getenv("GM_RED_UNROLL");
+        g_red_unroll = e ? atoi(e) : 4;
+    }
+    return g_red_unroll;
+}
+static int red_threads() {
+    if (g_red_threads < 0) {
+        const char* e = getenv("GM_RED_THREADS");
+        g_red_threads = e ? atoi(e) : 256;
+    }
+    return g_red_threads;
+}
+static int g_red_nt = [] {
+    const char* e = getenv("GM_RED_NT");
+    return e ? atoi(e) : 1;
+}();
+extern "C" int gm_mmtm_set_reduce_form(int threads, int unroll) {
+    g_red_nt = threads < 0;  // negative threads: nontemporal loads (forward, bf16; the default)
+    if (threads < 0) threads = -threads;
+    GM_REQUIRE(unroll == 4 || unroll == 8 || unroll == 16, "reduce unroll must be 4, 8 or 16 (got %d)", unroll);
+    GM_REQUIRE(threads == 256 || threads == 1024, "reduce threads must be 256 or 1024 (got %d)", threads);
+    g_red_unroll = unroll;
+    g_red_threads = threads;
+    return GM_OK;
+}
+
 static int red_wgs() {
     static int w = [] {
         const char* e = getenv("GM_MMTM_RED_WGS");  // workgroups wanted for the NHWC squeeze
@@ -410,7 +475,7 @@ static int red_setup(const gm_spatial_reduce* in, int nprob, int B, int dtype, i
             p.ncs = s.C / p.cw;
             GM_REQUIRE(aligned(s.x, 16) && (!s.dy || aligned(s.dy, 16)),
                        "spatial_reduce[%d]: NHWC tensors must be 16-byte aligned", i);
-            const int tpp = p.cw * es / 16, ppi = 256 / tpp;
+            const int tpp = p.cw * es / 16, ppi = red_threads() / tpp;
             // per-problem split independent of how many problems share the launch, so a
             // modality's reduction order (and bits) never depends on its batch-mates
             const int per = red_wgs() / 2;
@@ -481,13 +546,22 @@ extern "C" int gm_mmtm_spatial_reduce(const gm_spatial_reduce* in, int nprob, in
         }
         if (p.C > maxC) maxC = p.C;
     }
-    if (dtype == GM_F32) {
-        if (bwd) k_colreduce_nhwc<float, true><<<nwg, 256, 0, st>>>(a);
-        else k_colreduce_nhwc<float, false><<<nwg, 256, 0, st>>>(a);
+#define GM_COLRED(T, U, NTH)                                                  \
+    if (bwd) k_colreduce_nhwc<T, true, U, NTH><<<nwg, NTH, 0, st>>>(a);      \
+    else k_colreduce_nhwc<T, false, U, NTH><<<nwg, NTH, 0, st>>>(a);
+    const int u = red_unroll(), wide = red_threads() == 1024;
+    if (dtype == GM_BF16 && !bwd && g_red_nt) {
+        if (wide) k_colreduce_nhwc<uint16_t, false, 4, 1024, true><<<nwg, 1024, 0, st>>>(a);
+        else if (u >= 8) k_colreduce_nhwc<uint16_t, false, 8, 256, true><<<nwg, 256, 0, st>>>(a);
+        else k_colreduce_nhwc<uint16_t, false, 4, 256, true><<<nwg, 256, 0, st>>>(a);
+    } else if (dtype == GM_F32) {
+        if (wide) { GM_COLRED(float, 4, 1024) } else if (u >= 8) { GM_COLRED(float, 8, 256) } else { GM_COLRED(float, 4, 256) }
+    } else if (wide) {
+        if (u >= 8) { GM_COLRED(uint16_t, 8, 1024) } else { GM_COLRED(uint16_t, 4, 1024) }
     } else {
-        if (bwd) k_colreduce_nhwc<uint16_t, true><<<nwg, 256, 0, st>>>(a);
-        else k_colreduce_nhwc<uint16_t, false><<<nwg, 256, 0, st>>>(a);
+        if (u >= 16) { GM_COLRED(uint16_t, 16, 256) } else if (u >= 8) { GM_COLRED(uint16_t, 8, 256) } else { GM_COLRED(uint16_t, 4, 256) }
     }
+#undef GM_COLRED
     rc = check_launch("k_colreduce_nhwc");
     if (rc || !anyS) return rc;
     dim3 g((maxC + 255) / 256, B, nprob);

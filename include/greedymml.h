@@ -109,6 +109,11 @@ typedef struct gm_spatial_reduce {
 size_t gm_spatial_reduce_scratch(const gm_spatial_reduce* p, int nprob, int B, int dtype, int layout);
 int gm_mmtm_spatial_reduce(const gm_spatial_reduce* p, int nprob, int B, int dtype, int layout,
                            void* scratch, size_t scratch_bytes, void* stream);
+/* A/B knob of the NHWC squeeze: threads per workgroup (256 or 1024; GM_RED_THREADS; negative:
+ * nontemporal loads in the bf16 forward, GM_RED_NT) and
+ * pixels whose 16-B loads one thread keeps in flight (4, 8 or 16; GM_RED_UNROLL).
+ * Process-wide, not thread-safe. */
+int gm_mmtm_set_reduce_form(int threads, int unroll);
 
 /* ---------------------------------------------------------------------------
  * Channel re-scale: y[b,c,hw] = x[b,c,hw] * s[b*ld_s + c] (+ alpha * a[b*ld_a + c])
@@ -161,6 +166,10 @@ typedef struct gm_gemm {
 } gm_gemm;
 
 int gm_gemm_f32(const gm_gemm* p, int nprob, void* stream);
+/* A/B knob: fp32 GEMM form, waves per workgroup x k-steps per load round:
+ * 0 = 4 x 8, 1 = 4 x 16 (default), 2 = 8 x 16, 3 = 16 x 8; + 256: no float4 k-segments
+ * (4, 5: timing diagnostics).  Process-wide. */
+int gm_gemm_set_form(int form);
 
 /* ---------------------------------------------------------------------------
  * MMTM running averages (src/balanced_mmtm.py:113-116), reference quirk kept:

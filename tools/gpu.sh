@@ -24,6 +24,7 @@
 #                at B=256 rotating over 411 MB)                   -> gpurun_out/traffic_mmtm.json
 #   pmcone:SET:ARGS one rocprofv3 --pmc pass (counter set SET above) over tools/conv_one.py ARGS
 #                (commas become spaces), summarised per kernel  -> gpurun_out/pmcone_SET.txt
+#   rp:FILE[,ARGS] rocprofv3 --kernel-trace --stats of python FILE ARGS -> gpurun_out/rp_FILE/
 #   py:FILE[,ARGS] python FILE ARGS (a tools/ script; commas become spaces) -> gpurun_out/py_FILE.log
 set -o pipefail
 mkdir -p gpurun_out
@@ -120,6 +121,12 @@ for s in "$@"; do
         -- python3 tools/conv_one.py ${args//,/ } > "$d.log" 2>&1 || { tail -30 "$d.log"; exit 25; }
       python3 tools/pmc_table.py "$d" | grep -v spin_kernel > "$d.txt" && rm -rf "$d"
       cat "$d.txt" ;;
+    rp:*)
+      a="${s#rp:}"; f="${a%%,*}"; args=""; [ "$f" != "$a" ] && args="${a#*,}"
+      d="gpurun_out/rp_$(basename "$f" .py)"
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$d" -o rp \
+        -- python3 "$f" ${args//,/ } > "$d.log" 2>&1 || { tail -30 "$d.log"; exit 26; }
+      tail -5 "$d.log"; python3 tools/summarize_stats.py "$d/rp_kernel_stats.csv" 1 | head -12 ;;
     py:*)
       a="${s#py:}"; f="${a%%,*}"; args=""; [ "$f" != "$a" ] && args="${a#*,}"
       lg="gpurun_out/py_$(basename "$f" .py).log"

@@ -74,11 +74,25 @@ def _counter_means(d, counter):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["run", "report"])
+    ap.add_argument("mode", choices=["run", "report", "ab"])
     ap.add_argument("dirs", nargs="*")
     ap.add_argument("--json", default=None)
     ap.add_argument("--batch", type=int, default=256)
     a = ap.parse_args()
+    if a.mode == "ab":  # interleaved rounds of the unroll forms in one process
+        from greedy_multimodal_learning_amd import _lib as L
+        lib = L.load()
+        res = {u: [] for u in ((256, 4), (1024, 4), (-256, 4), (-256, 8), (-1024, 4))}
+        for _ in range(5):
+            for u in res:
+                L.check(lib.gm_mmtm_set_reduce_form(*u), "set_reduce_form")
+                nb, secs, _ = measure(torch.device("cuda:0"), a.batch)
+                res[u].append(secs * 1e6)
+        for u, ts in res.items():
+            ts.sort()
+            print(f"threads, unroll {u}: median {ts[len(ts) // 2]:.2f} us  min {ts[0]:.2f} us  "
+                  f"-> {nb / ts[len(ts) // 2] / 1e3:.0f} GB/s ({nb / ts[len(ts) // 2] / 1e3 / 8000:.3f} of 8 TB/s)")
+        return
     if a.mode == "run":
         nb, secs, rot = measure(torch.device("cuda:0"), a.batch)
         print(f"{nb / 1e6:.1f} MB per launch, {secs * 1e6:.2f} us, {nb / secs / 1e9:.0f} GB/s "
