@@ -97,18 +97,18 @@ def cpu_baseline(seconds, size):
                       f"{size}x{size}; {th} threads (the job's CPU share; {os.cpu_count()} CPUs visible)"}
 
 
-def time_trunk_convs(B, dev, dtype="bf16"):
+def time_trunk_convs(B, dev, dtype="bf16", G=2, arch="resnet18"):
     """Roofline of the dominant kernel family, the trunk convolutions: forward, input-
     and weight-gradient launches of every trunk shape of one view at the step's batch
     (tools/trunk_table.py; HIP events on the launch stream behind a device sleep; the
     launches rotate over more operand bytes than the 256 MiB Infinity Cache holds)."""
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import trunk_table
-    flops, secs, launches, _ = trunk_table.measure_family(B, dev, dtype=dtype)
+    flops, secs, launches, _ = trunk_table.measure_family(B, dev, dtype=dtype, G=G, arch=arch)
     return flops, secs, launches
 
 
-def conv_roofline(conv, traffic, dtype="bf16"):
+def conv_roofline(conv, traffic, dtype="bf16", workload="C2"):
     """The `roofline` object of the dominant kernel family (the trunk convolutions)."""
     if dtype == "fp32":
         if conv is None:
@@ -120,15 +120,13 @@ def conv_roofline(conv, traffic, dtype="bf16"):
                 "bound": "mfma", "achieved": round(flops / secs / 1e12, 2), "peak": MFMA_F32_PEAK_TFS,
                 "unit": "TFLOP/s", "frac": round(flops / secs / 1e12 / MFMA_F32_PEAK_TFS, 4), "traffic": None,
                 "alg_flops_per_launch": round(flops / launches), "avg_launch_us": round(secs / launches * 1e6, 2)}
-    if conv is None:
-        return {"kernel": "trunk convolutions", "bound": "mfma", "achieved": None, "peak": MFMA_PEAK_TFS,
-                "unit": "TFLOP/s", "frac": None, "traffic": None,
-                "note": "per-shape table covers the ResNet-18 trunk only (C2/C4); see the C2 line"}
     flops, secs, launches = conv
+    what = {"C2": "every ResNet-18 trunk shape, both views per launch (the view-batched trunk)",
+            "C4": "every ResNet-18 trunk shape of one view", "C5": "every ResNet-50 trunk shape of one view"}[workload]
     return {"kernel": "trunk convolutions (bf16 MFMA: k_conv_stem pixel-pair stem, k_conv_rw layer-1 "
-                      "resident-weight, k_conv_halo layer 2-4 3x3, k_conv_igemm_ut strided/1x1 fwd + input "
-                      "grad, k_conv_wgrad4 + k_wgrad_sum weight grad; every trunk shape of one view at the "
-                      "step's batch, tools/trunk_table.py)",
+                      "resident-weight, k_conv_h9 3x3 halo, k_conv_igemm_ut strided/1x1 fwd + input "
+                      "grad, k_conv_wgrad4 + k_wgrad_sum weight grad; " + what + " at the step's batch, "
+                      "tools/trunk_table.py)",
             "bound": "mfma", "achieved": round(flops / secs / 1e12, 1), "peak": MFMA_PEAK_TFS, "unit": "TFLOP/s",
             "frac": round(flops / secs / 1e12 / MFMA_PEAK_TFS, 4), "traffic": traffic,
             "alg_flops_per_launch": round(flops / launches), "avg_launch_us": round(secs / launches * 1e6, 2)}
@@ -253,7 +251,9 @@ def main():
             dist.destroy_process_group()
         return
     kern_avg_s = time_group_sumsq(step, 10)
-    conv = time_trunk_convs(B, dev, a.dtype) if WL["trunk"] == "resnet18" else None
+    # the step's own launches: C2's view-batched trunk (vtrunk.py, 2 views per launch); the
+    # N-view models (C4 ResNet-18 x4, C5 ResNet-50 x12) launch view by view
+    conv = time_trunk_convs(B, dev, a.dtype, G=2 if a.workload == "C2" else 1, arch=WL["trunk"])
     mmtm_bytes, mmtm_s = time_mmtm_reduce(dev)
     if rank == 0:
         views = V
@@ -287,7 +287,8 @@ def main():
                        "parallelism": f"dp{world}", "samples_per_s": round(world * B * a.steps / elapsed, 2),
                        "hipgraph": bool(step.graphs), "device_gate": bool(step.device_gate),
                        "curation_steps_timed": curation_steps, "final_loss": round(loss, 4)},
-            "roofline": conv_roofline(conv, conv_traffic if a.dtype == "bf16" else None, a.dtype),
+            "roofline": conv_roofline(conv, conv_traffic if a.dtype == "bf16" and a.workload == "C2" else None,
+                                      a.dtype, a.workload),
             "roofline_hbm": {"kernel": "k_group_sumsq<SGD> (fused per-branch norms + SGD, gm_group_sumsq)",
                              "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

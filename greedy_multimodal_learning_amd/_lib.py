@@ -184,6 +184,10 @@ EXPORTS.update({
                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "gm_mmtm_mask_rows": (c_int, [c_void_p, ctypes.c_longlong, c_void_p, c_void_p]),
     "gm_mmtm_mask_rows2": (c_int, [c_void_p, ctypes.c_longlong, c_void_p, ctypes.c_longlong, c_void_p, c_void_p]),
+    "gm_mmtm_channel_scale_gated": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                            c_void_p]),
+    "gm_mmtm_spatial_reduce_gated": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_size_t,
+                                             c_void_p]),
     "gm_stem_pack_bf16": (c_int, [c_void_p, c_void_p]),
     "gm_xent_fwd": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "gm_xent_bwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -156,32 +156,27 @@ def _mmtm_forward(ctx, xv, xs, w_sq, b_sq, w_sq_v, b_sq_v, w_sq_s, b_sq_s, w_v, 
     cur, caring = cfg["curation"], cfg["caring"]
     sv, ld_sv, live_v = e_v, Cv, True
     ss, ld_ss, live_s = e_s, Cs, True
-    gmask = None
     gate = cfg.get("gate")
-    if gate is not None:
-        # on-device gate (engine): the flags live in device memory, so one captured
-        # step serves every curation setting; the substituted modality's excitation
-        # gradient is masked to zero in backward instead of skipped
-        sv, ss = torch.empty(B, Cv, **f32), torch.empty(B, Cs, **f32)
-        gmask = torch.empty(2, **f32)
-        L.check(L.load().gm_mmtm_select_scale(e_v.data_ptr(), Cv, e_s.data_ptr(), Cs, ra_v.data_ptr(),
-                                              ra_s.data_ptr(), B, Cv, Cs, gate.data_ptr(), sv.data_ptr(),
-                                              ss.data_ptr(), gmask.data_ptr(), L.stream_of(dev)),
-                "gm_mmtm_select_scale")
-    elif cur and caring == 0:
-        sv, ld_sv, live_v = ra_v, 0, False
-    elif cur and caring == 1:
-        ss, ld_ss, live_s = ra_s, 0, False
+    if gate is None:
+        if cur and caring == 0:
+            sv, ld_sv, live_v = ra_v, 0, False
+        elif cur and caring == 1:
+            ss, ld_ss, live_s = ra_s, 0, False
+    # on-device gate (engine): the flags live in device memory, so one captured step serves
+    # every curation setting; the channel scale reads the substituted modality's running
+    # average in place of its scale rows, and backward zeroes that modality's excitation
+    # gradient inside the squeeze-backward launch (gm_mmtm_*_gated)
     yv, ys = (torch.empty_like(xv), torch.empty_like(xs)) if outs is None else outs
     ops.channel_scale([dict(x=xv, y=yv, C=Cv, HW=HWv, s=sv, ld_s=ld_sv),
-                       dict(x=xs, y=ys, C=Cs, HW=HWs, s=ss, ld_s=ld_ss)], B, dt, lay, dev)
+                       dict(x=xs, y=ys, C=Cs, HW=HWs, s=ss, ld_s=ld_ss)], B, dt, lay, dev,
+                      gate=gate, alt=(ra_v, ra_s))
     ctx.save_for_backward(xv, xs, sq, z_v, z_s, e_v, e_s, sv, ss,
                           w_sq, w_sq_v, w_sq_s, wv_, ws_)
     # the parameters themselves (leaves), for in-place gradient delivery (gradsink)
     ctx.params = {"w_sq": w_sq, "b_sq": b_sq, "w_sq_v": w_sq_v, "b_sq_v": b_sq_v, "w_sq_s": w_sq_s,
                   "b_sq_s": b_sq_s, "w_v": w_v, "b_v": b_v, "w_s": w_s, "b_s": b_s}
     ctx.meta = (B, Cv, Cs, Cz, HWv, HWs, lay, dt, mode, share, live_v, live_s,
-                ld_sv, ld_ss, cfg.get("avg_v"), cfg.get("avg_s"), cfg["zero_curated"], gmask)
+                ld_sv, ld_ss, cfg.get("avg_v"), cfg.get("avg_s"), cfg["zero_curated"], gate, ra_v, ra_s)
     ctx.mark_non_differentiable(e_v, e_s, sq)
     ctx.set_materialize_grads(False)  # no zero-filled grads for the side outputs
     return yv, ys, e_v, e_s, sq
@@ -190,7 +185,7 @@ def _mmtm_forward(ctx, xv, xs, w_sq, b_sq, w_sq_v, b_sq_v, w_sq_s, b_sq_s, w_v, 
 def _mmtm_backward(ctx, gyv, gys, outs=None):
     (xv, xs, sq, z_v, z_s, e_v, e_s, sv, ss, w_sq, w_sq_v, w_sq_s, wv_, ws_) = ctx.saved_tensors
     (B, Cv, Cs, Cz, HWv, HWs, lay, dt, mode, share, live_v, live_s,
-     ld_sv, ld_ss, avg_v, avg_s, zero_curated, gmask) = ctx.meta
+     ld_sv, ld_ss, avg_v, avg_s, zero_curated, gate, ra_v, ra_s) = ctx.meta
     dev = xv.device
     f32 = dict(device=dev, dtype=torch.float32)
     C2 = Cv + Cs
@@ -230,12 +225,8 @@ def _mmtm_backward(ctx, gyv, gys, outs=None):
         probs.append(dict(x=xv, dy=gyv, C=Cv, HW=HWv, out=da_v, ld_out=Cv, e=e_v, ld_e=Cv))
     if live_s:
         probs.append(dict(x=xs, dy=gys, C=Cs, HW=HWs, out=da_s, ld_out=Cs, e=e_s, ld_e=Cs))
-    if probs:
-        ops.spatial_reduce(probs, B, dt, lay, dev)
-    if gmask is not None:  # on-device gate: zero the substituted modality's da
-        lib = L.load()
-        L.check(lib.gm_mmtm_mask_rows2(da_v.data_ptr(), B * Cv, da_s.data_ptr(), B * Cs, gmask.data_ptr(),
-                                       L.stream_of(dev)), "gm_mmtm_mask_rows2")
+    if probs:  # on-device gate: the substituted modality's da is zeroed in the same launch
+        ops.spatial_reduce(probs, B, dt, lay, dev, gate=gate)
     # ---- excite FC grads + dz
     g = {}
     probs = []
@@ -326,7 +317,7 @@ def _mmtm_backward(ctx, gyv, gys, outs=None):
     if dsq is not None:
         pv.update(a=dsq, ld_a=C2, alpha=1.0 / HWv)
         ps.update(a=dsq, a_off=Cv, ld_a=C2, alpha=1.0 / HWs)
-    ops.channel_scale([pv, ps], B, dt, lay, dev)
+    ops.channel_scale([pv, ps], B, dt, lay, dev, gate=gate, alt=(ra_v, ra_s))
 
     for prm in sunk.values():  # delivered in place: fire the engine's per-parameter hook
         sink_done(prm)

@@ -596,6 +596,9 @@ static WPlan plan(const gm_conv_desc_hw* d, int G = 1) {
         // bit 1: columns)
         if ((wgrad_wide() & 1) && d->K >= 256 && w.mt == 2) w.mt = 4;
         if ((wgrad_wide() & 2) && TC >= 256 && w.nt == 2) w.nt = 4;
+        // bit 2: 256-column tiles for the 64-row (K = 64) shapes only - layer 1, where a
+        // 64 x 128 tile gives each wave 8 MFMAs per 64-pixel step between barriers
+        if ((wgrad_wide() & 4) && d->K <= 64 && TC >= 256 && w.nt == 2) w.nt = 4;
     }
     w.tiles_k = (d->K + 64 * w.mt - 1) / (64 * w.mt);
     w.tiles_n = (TC + 64 * w.nt - 1) / (64 * w.nt);

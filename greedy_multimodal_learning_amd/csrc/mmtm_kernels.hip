@@ -38,15 +38,22 @@ struct RedProb {
 struct RedArgs {
     RedProb p[kMaxProb];
     int nprob, B;
+    const gm_gate_state* gate;  // gated form: the substituted modality's outputs x 0
 };
 
-__device__ __forceinline__ float epilogue(float g, const RedProb& p, int b, int c) {
+// the modality (problem 0 / 1) whose scale the on-device gate substitutes, or -1
+__device__ __forceinline__ int gate_sub(const gm_gate_state* g) {
+    if (!g) return -1;
+    return g->curation_mode ? g->caring : -1;
+}
+
+__device__ __forceinline__ float epilogue(float g, const RedProb& p, int b, int c, float k = 1.f) {
     g *= p.scale;
     if (p.e) {
         float e = p.e[(size_t)b * p.ld_e + c];
         g = g * ((1.0f - e) * e);
     }
-    return g;
+    return g * k;  // gm_mmtm_mask_rows2's factor, applied in place of that launch
 }
 
 // ---- vector loaders: VB bytes per lane -> N floats ----
@@ -114,7 +121,7 @@ __global__ __launch_bounds__(256) void k_rowreduce_nchw(RedArgs a, int total_row
         acc = wave_sum(acc);
         if (lane == 0) {
             const int b = r / p.C, c = r - b * p.C;
-            p.out[(size_t)b * p.ld_out + c] = epilogue(acc, p, b, c);
+            p.out[(size_t)b * p.ld_out + c] = epilogue(acc, p, b, c, pi == gate_sub(a.gate) ? 0.f : 1.f);
         }
     }
 }
@@ -212,7 +219,7 @@ __global__ __launch_bounds__(NTH) void k_colreduce_nhwc(RedArgs a) {
             for (int q = 0; q < ppi; ++q) v += red[q * CW + c];
         }
         if (p.S == 1) {
-            p.out[(size_t)b * p.ld_out + c0 + c] = epilogue(v, p, b, c0 + c);
+            p.out[(size_t)b * p.ld_out + c0 + c] = epilogue(v, p, b, c0 + c, pi == gate_sub(a.gate) ? 0.f : 1.f);
         } else {
             p.part[((size_t)b * p.S + s) * p.C + c0 + c] = v;
         }
@@ -228,7 +235,7 @@ __global__ __launch_bounds__(256) void k_reduce_partials(RedArgs a) {
     const float* src = p.part + (size_t)b * p.S * p.C + c;
     float v = 0.f;
     for (int s = 0; s < p.S; ++s) v += src[(size_t)s * p.C];
-    p.out[(size_t)b * p.ld_out + c] = epilogue(v, p, b, c);
+    p.out[(size_t)b * p.ld_out + c] = epilogue(v, p, b, c, (int)blockIdx.z == gate_sub(a.gate) ? 0.f : 1.f);
 }
 
 // ---------------- channel scale (fwd) / apply (bwd) ----------------
@@ -249,17 +256,22 @@ struct ScaleArgs {
     ScaleProb p[kMaxProb];
     int nprob;
     long long total_vec;
+    const gm_gate_state* gate;  // gated form: problem gate_sub() reads alt[it] broadcast
+    const float* alt[2];
 };
 
 template <typename T, int N, int LAYOUT, bool ROWCONST>
 __global__ __launch_bounds__(256) void k_channel_scale(ScaleArgs a) {
     const long long stride = (long long)gridDim.x * blockDim.x;
+    const int sub = gate_sub(a.gate);
     for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < a.total_vec; v += stride) {
         int pi = 0;
 #pragma unroll
         for (int q = 1; q < kMaxProb; ++q)
             if (q < a.nprob && v >= a.p[q].vec_start) pi = q;
         const ScaleProb& p = a.p[pi];
+        const float* ps = pi == sub ? a.alt[pi] : p.s;  // substituted: the running average row
+        const int ld_s = pi == sub ? 0 : p.ld_s;
         const uint32_t i0 = (uint32_t)((v - p.vec_start) * N);
         const T* x = (const T*)p.x + i0;
         T* y = (T*)p.y + i0;
@@ -269,7 +281,7 @@ __global__ __launch_bounds__(256) void k_channel_scale(ScaleArgs a) {
             if (ROWCONST) {
                 const uint32_t row = p.div_hw.div(i0);
                 const uint32_t b = row / (uint32_t)p.C, c = row - b * (uint32_t)p.C;
-                const float s0 = p.s[(size_t)b * p.ld_s + c];
+                const float s0 = ps[(size_t)b * ld_s + c];
                 const float a0 = p.a ? p.a[(size_t)b * p.ld_a + c] * p.alpha : 0.f;
 #pragma unroll
                 for (int j = 0; j < N; ++j) { sc[j] = s0; ad[j] = a0; }
@@ -278,14 +290,14 @@ __global__ __launch_bounds__(256) void k_channel_scale(ScaleArgs a) {
                 for (int j = 0; j < N; ++j) {
                     const uint32_t row = p.div_hw.div(i0 + j);
                     const uint32_t b = row / (uint32_t)p.C, c = row - b * (uint32_t)p.C;
-                    sc[j] = p.s[(size_t)b * p.ld_s + c];
+                    sc[j] = ps[(size_t)b * ld_s + c];
                     ad[j] = p.a ? p.a[(size_t)b * p.ld_a + c] * p.alpha : 0.f;
                 }
             }
         } else {
             const uint32_t b = p.div_hwc.div(i0);
             const uint32_t c0 = i0 - p.div_c.div(i0) * (uint32_t)p.C;
-            const float* sp = p.s + (size_t)b * p.ld_s + c0;
+            const float* sp = ps + (size_t)b * ld_s + c0;
             if constexpr (N % 4 == 0) {
 #pragma unroll
                 for (int j = 0; j < N; j += 4) {
@@ -519,13 +531,14 @@ static void launch_rows(RedArgs& a, int rows, int vb, bool bwd, hipStream_t st) 
 #undef GM_ROWS
 }
 
-extern "C" int gm_mmtm_spatial_reduce(const gm_spatial_reduce* in, int nprob, int B, int dtype,
-                                      int layout, void* scratch, size_t scratch_bytes, void* stream) {
+static int spatial_reduce_impl(const gm_spatial_reduce* in, int nprob, int B, int dtype, int layout,
+                               const gm_gate_state* gate, void* scratch, size_t scratch_bytes, void* stream) {
     RedArgs a;
     size_t need = 0;
     int nwg = 0, vb = 16;
     int rc = red_setup(in, nprob, B, dtype, layout, a, need, nwg, vb);
     if (rc) return rc;
+    a.gate = gate;
     hipStream_t st = as_stream(stream);
     const bool bwd = in[0].dy != nullptr;
     if (layout == GM_NCHW) {
@@ -569,8 +582,20 @@ extern "C" int gm_mmtm_spatial_reduce(const gm_spatial_reduce* in, int nprob, in
     return check_launch("k_reduce_partials");
 }
 
-extern "C" int gm_mmtm_channel_scale(const gm_channel_scale* in, int nprob, int B, int dtype, int layout,
-                                     void* stream) {
+extern "C" int gm_mmtm_spatial_reduce(const gm_spatial_reduce* in, int nprob, int B, int dtype, int layout,
+                                      void* scratch, size_t scratch_bytes, void* stream) {
+    return spatial_reduce_impl(in, nprob, B, dtype, layout, nullptr, scratch, scratch_bytes, stream);
+}
+
+extern "C" int gm_mmtm_spatial_reduce_gated(const gm_spatial_reduce* in, int nprob, int B, int dtype, int layout,
+                                            const gm_gate_state* gate, void* scratch, size_t scratch_bytes,
+                                            void* stream) {
+    GM_REQUIRE(gate && nprob >= 2, "spatial_reduce_gated: gate and the two modalities' problems (0, 1) required");
+    return spatial_reduce_impl(in, nprob, B, dtype, layout, gate, scratch, scratch_bytes, stream);
+}
+
+static int channel_scale_impl(const gm_channel_scale* in, int nprob, int B, int dtype, int layout,
+                              const gm_gate_state* gate, const float* alt0, const float* alt1, void* stream) {
     GM_REQUIRE(in && nprob >= 1 && nprob <= kMaxProb, "channel_scale: nprob must be 1..%d", kMaxProb);
     GM_REQUIRE(B >= 1, "channel_scale: B must be >= 1");
     GM_REQUIRE(dtype == GM_F32 || dtype == GM_BF16, "channel_scale: bad dtype");
@@ -607,6 +632,9 @@ extern "C" int gm_mmtm_channel_scale(const gm_channel_scale* in, int nprob, int 
         vs += p.nvec;
     }
     a.total_vec = vs;
+    a.gate = gate;
+    a.alt[0] = alt0;
+    a.alt[1] = alt1;
     hipStream_t st = as_stream(stream);
     long long g = (vs + 255) / 256;
     if (g > 16384) g = 16384;
@@ -633,6 +661,20 @@ extern "C" int gm_mmtm_channel_scale(const gm_channel_scale* in, int nprob, int 
     }
 #undef GM_SC
     return check_launch("k_channel_scale");
+}
+
+extern "C" int gm_mmtm_channel_scale(const gm_channel_scale* in, int nprob, int B, int dtype, int layout,
+                                     void* stream) {
+    return channel_scale_impl(in, nprob, B, dtype, layout, nullptr, nullptr, nullptr, stream);
+}
+
+extern "C" int gm_mmtm_channel_scale_gated(const gm_channel_scale* in, int nprob, int B, int dtype, int layout,
+                                           const gm_gate_state* gate, const float* alt0, const float* alt1,
+                                           void* stream) {
+    GM_REQUIRE(gate && alt0 && alt1 && nprob >= 2, "channel_scale_gated: gate, two alternative rows and the two "
+               "modalities' problems (0, 1) are required");
+    GM_REQUIRE(aligned(alt0, 16) && aligned(alt1, 16), "channel_scale_gated: alternative rows must be 16-B aligned");
+    return channel_scale_impl(in, nprob, B, dtype, layout, gate, alt0, alt1, stream);
 }
 
 extern "C" int gm_mmtm_running_avg(const float* e_v, int ld_e, int B, int C, const float* ra_v_old,

@@ -37,8 +37,12 @@ def as_layout(x, layout):
 MAX_REDUCE, MAX_SCALE, MAX_GEMM = 4, 4, 6  # problems per launch (include/greedymml.h)
 
 
-def spatial_reduce(probs, B, dtype, layout, device):
-    """probs: list of dict(x, dy, out, ld_out, e, ld_e, C, HW, scale, out_off) -> launches."""
+def spatial_reduce(probs, B, dtype, layout, device, gate=None):
+    """probs: list of dict(x, dy, out, ld_out, e, ld_e, C, HW, scale, out_off) -> launches.
+    gate (device gm_gate_state): problems 0 / 1 are the two modalities and the substituted
+    one's outputs are zeroed in the same launch (gm_mmtm_spatial_reduce_gated)."""
+    if gate is not None:
+        assert 2 <= len(probs) <= MAX_REDUCE
     if len(probs) > MAX_REDUCE:
         for i in range(0, len(probs), MAX_REDUCE):
             spatial_reduce(probs[i:i + MAX_REDUCE], B, dtype, layout, device)
@@ -55,12 +59,20 @@ def spatial_reduce(probs, B, dtype, layout, device):
     a = L.arr(L.SpatialReduce, items)
     need = lib.gm_spatial_reduce_scratch(a, len(items), B, dtype, layout)
     scratch = torch.empty(max(need, 16), dtype=torch.uint8, device=device) if need else None
+    if gate is not None:
+        L.check(lib.gm_mmtm_spatial_reduce_gated(a, len(items), B, dtype, layout, gate.data_ptr(), L.ptr(scratch),
+                                                 need, L.stream_of(device)), "gm_mmtm_spatial_reduce_gated")
+        return
     L.check(lib.gm_mmtm_spatial_reduce(a, len(items), B, dtype, layout, L.ptr(scratch), need,
                                        L.stream_of(device)), "gm_mmtm_spatial_reduce")
 
 
-def channel_scale(probs, B, dtype, layout, device):
-    """probs: list of dict(x, y, C, HW, s, s_off, ld_s, a, a_off, ld_a, alpha)."""
+def channel_scale(probs, B, dtype, layout, device, gate=None, alt=None):
+    """probs: list of dict(x, y, C, HW, s, s_off, ld_s, a, a_off, ld_a, alpha).
+    gate (device gm_gate_state) + alt (two fp32 rows): problems 0 / 1 are the two
+    modalities and the substituted one scales by its alt row (gm_mmtm_channel_scale_gated)."""
+    if gate is not None:
+        assert 2 <= len(probs) <= MAX_SCALE and alt is not None
     if len(probs) > MAX_SCALE:
         for i in range(0, len(probs), MAX_SCALE):
             channel_scale(probs[i:i + MAX_SCALE], B, dtype, layout, device)
@@ -75,6 +87,11 @@ def channel_scale(probs, B, dtype, layout, device):
             (a.data_ptr() + 4 * p.get("a_off", 0)) if a is not None else 0, p.get("ld_a", 0),
             p.get("alpha", 0.0)))
     arr = L.arr(L.ChannelScale, items)
+    if gate is not None:
+        L.check(lib.gm_mmtm_channel_scale_gated(arr, len(items), B, dtype, layout, gate.data_ptr(), alt[0].data_ptr(),
+                                                alt[1].data_ptr(), L.stream_of(device)),
+                "gm_mmtm_channel_scale_gated")
+        return
     L.check(lib.gm_mmtm_channel_scale(arr, len(items), B, dtype, layout, L.stream_of(device)),
             "gm_mmtm_channel_scale")
 

@@ -232,6 +232,20 @@ int gm_mmtm_select_scale(const float* e_v, int ld_v, const float* e_s, int ld_s,
 int gm_mmtm_mask_rows(float* a, long long n, const float* mask, void* stream);
 /* Both modalities in one launch: a[0..na) *= mask[0], b[0..nb) *= mask[1]. */
 int gm_mmtm_mask_rows2(float* a, long long na, float* b, long long nb, const float* mask, void* stream);
+/* The gate folded into the MMTM launches themselves (no select / mask launch): problem 0
+ * (visual) and 1 (skeleton) are the two modalities; when state says modality i is
+ * substituted (curation_mode && caring == i):
+ *   channel_scale_gated  - problem i scales by alt_i broadcast over the batch (its running
+ *                          average; ld 0) instead of its s rows, as gm_mmtm_select_scale's
+ *                          s_i would hold;
+ *   spatial_reduce_gated - problem i's outputs are multiplied by 0 (gm_mmtm_mask_rows2's
+ *                          factor: the substituted excitation receives no gradient).
+ * Both are otherwise gm_mmtm_channel_scale / gm_mmtm_spatial_reduce. */
+int gm_mmtm_channel_scale_gated(const gm_channel_scale* p, int nprob, int B, int dtype, int layout,
+                                const gm_gate_state* state, const float* alt_s0, const float* alt_s1,
+                                void* stream);
+int gm_mmtm_spatial_reduce_gated(const gm_spatial_reduce* p, int nprob, int B, int dtype, int layout,
+                                 const gm_gate_state* state, void* scratch, size_t scratch_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Pixel-pair packing of the RGB stem (one launch, input and weight):

@@ -70,26 +70,46 @@ def test_n_view_model_vs_oracle(trunk, V, B, H, caring):
     assert e_gpu.max() <= max(10 * e_ref.max(), 1e-2), ("grad-norm max", names[int(e_gpu.argmax())])
 
 
-def test_c4_engine_bf16_step_vs_oracle():
-    """The benchmarked C4 step (4 ResNet-18 branches, bf16 trunk, hipGraphs, N-branch
-    host gate) at 224x224: loss and per-branch logits against the fp32 oracle on the
-    same bf16-rounded inputs and weights (bf16 tolerance: 3e-2 of the logit scale)."""
+@pytest.mark.parametrize("trunk,V,B", [("resnet18", 4, 8), ("resnet50", 12, 2)], ids=["c4", "c5"])
+def test_engine_bf16_step_vs_oracle(trunk, V, B):
+    """The benchmarked C4 / C5 steps (4 ResNet-18 / 12 ResNet-50 branches, bf16 trunk,
+    hipGraphs, N-branch host gate) at 224x224: the step's loss, and the per-branch logits
+    of the same model's bf16 forward, against the fp32 oracle on the same bf16-rounded
+    inputs and weights (bf16 tolerance: 3e-2 of the loss / of the logit scale)."""
     from greedy_multimodal_learning_amd.callbacks import Bias_Mitigation_Strong
     from greedy_multimodal_learning_amd.engine import BalancedStep
     from greedy_multimodal_learning_amd.model import MMTM_MVCNN_N
     from oracle import gating_ref, model_ref
     dev = torch.device("cuda:0")
-    V, B = 4, 8
     g = torch.Generator().manual_seed(11)
     x = torch.randn(B, V, 3, 224, 224, generator=g).bfloat16()
     y = torch.randint(0, 40, (B,), generator=g)
-    m = weights.apply_to_module(MMTM_MVCNN_N(num_views=V), seed=5)
+    m = weights.apply_to_module(MMTM_MVCNN_N(num_views=V, trunk=trunk), seed=5)
     for p in m.parameters():  # the trunk computes on bf16 weights: start from bf16-exact ones
         p.data = p.data.bfloat16().float()
-    o = model_ref.MMTM_MVCNN_N_Ref(num_views=V)
+    o = model_ref.MMTM_MVCNN_N_Ref(num_views=V, trunk=trunk)
     missing, _ = o.load_state_dict(m.state_dict(), strict=False)
     assert not missing, missing
+    o.train(True)
+    _, outs_ref, _, _ = o(x.float())
+    ref = float(gating_ref.blend_loss(outs_ref, y))
     m = m.to(dev)
+    xd, yd = x.to(dev), y.to(dev)
+    m.train(True)
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        _, outs, _, _ = m(xd)
+    # the bf16 noise floor of this model and batch: the same oracle forward with its
+    # convolutions in bf16 (CPU autocast), against the fp32 oracle
+    o16 = model_ref.MMTM_MVCNN_N_Ref(num_views=V, trunk=trunk)
+    o16.load_state_dict(m.state_dict(), strict=False)
+    o16.train(True)
+    with torch.no_grad(), torch.autocast("cpu", dtype=torch.bfloat16):
+        _, outs16, _, _ = o16(x.float())
+    for i, (u, u16, v) in enumerate(zip(outs, outs16, outs_ref)):
+        u, u16, v = u.float().cpu(), u16.float(), v.detach()
+        scale = float(v.abs().max()) + 1e-12
+        err, floor = float((u - v).abs().max()) / scale, float((u16 - v).abs().max()) / scale
+        assert err <= max(3e-2, 2 * floor), (f"branch {i} logits", err, "bf16 floor", floor)
     # epsilon 1e9: the gate computes every branch's BDR but never curates, so with lr 0
     # every step sees the same weights and the same MMTM path
     gate = Bias_Mitigation_Strong(epsilon=1e9, curation_windowsize=5, branchnames=m.branch_names(),
@@ -97,11 +117,7 @@ def test_c4_engine_bf16_step_vs_oracle():
     step = BalancedStep(m, lr=0.0, gate=gate, branchnames=m.branch_names(), MMTMnames=m.mmtm_names(),
                         graphs=True)
     step.on_epoch_begin(1)
-    xd, yd = x.to(dev), y.to(dev)
     losses = [float(step(xd, yd)) for _ in range(3)]  # lr 0: every step sees the same weights
-    o.train(True)
-    _, outs, _, _ = o(x.float())
-    ref = float(gating_ref.blend_loss(outs, y))
     assert losses[0] == losses[1] == losses[2] or max(losses) - min(losses) < 1e-3 * abs(ref)
     assert abs(losses[-1] - ref) <= 3e-2 * abs(ref), (losses, ref)
     assert np.isfinite(gate.BDR).all() and len(gate.BDR) == V

@@ -37,6 +37,22 @@ TRUNK = [("conv1", (3, 224, 224, 64, 7, 2, 3, 1)), ("l1", (64, 56, 56, 64, 3, 1,
          ("l3.ds", (128, 28, 28, 256, 1, 2, 0, 1)), ("l3", (256, 14, 14, 256, 3, 1, 1, 3)),
          ("l4.0.c1", (256, 14, 14, 512, 3, 2, 1, 1)), ("l4.ds", (256, 14, 14, 512, 1, 2, 0, 1)),
          ("l4", (512, 7, 7, 512, 3, 1, 1, 3))]
+# ResNet-50 (Bottleneck, stride on the 3x3 as torchvision v1.5 / resnet.py) of one view at 224^2,
+# the C5 workload's trunk: positions with the same shape merged (count per step)
+TRUNK50 = [("conv1", (3, 224, 224, 64, 7, 2, 3, 1)),
+           ("l1.0.c1", (64, 56, 56, 64, 1, 1, 0, 1)), ("l1.c1", (256, 56, 56, 64, 1, 1, 0, 2)),
+           ("l1.c2", (64, 56, 56, 64, 3, 1, 1, 3)), ("l1.c3", (64, 56, 56, 256, 1, 1, 0, 3)),
+           ("l1.ds", (64, 56, 56, 256, 1, 1, 0, 1)),
+           ("l2.0.c1", (256, 56, 56, 128, 1, 1, 0, 1)), ("l2.0.c2", (128, 56, 56, 128, 3, 2, 1, 1)),
+           ("l2.ds", (256, 56, 56, 512, 1, 2, 0, 1)), ("l2.c1", (512, 28, 28, 128, 1, 1, 0, 3)),
+           ("l2.c2", (128, 28, 28, 128, 3, 1, 1, 3)), ("l2.c3", (128, 28, 28, 512, 1, 1, 0, 4)),
+           ("l3.0.c1", (512, 28, 28, 256, 1, 1, 0, 1)), ("l3.0.c2", (256, 28, 28, 256, 3, 2, 1, 1)),
+           ("l3.ds", (512, 28, 28, 1024, 1, 2, 0, 1)), ("l3.c1", (1024, 14, 14, 256, 1, 1, 0, 5)),
+           ("l3.c2", (256, 14, 14, 256, 3, 1, 1, 5)), ("l3.c3", (256, 14, 14, 1024, 1, 1, 0, 6)),
+           ("l4.0.c1", (1024, 14, 14, 512, 1, 1, 0, 1)), ("l4.0.c2", (512, 14, 14, 512, 3, 2, 1, 1)),
+           ("l4.ds", (1024, 14, 14, 2048, 1, 2, 0, 1)), ("l4.c1", (2048, 7, 7, 512, 1, 1, 0, 2)),
+           ("l4.c2", (512, 7, 7, 512, 3, 1, 1, 2)), ("l4.c3", (512, 7, 7, 2048, 1, 1, 0, 3))]
+TRUNKS = {"resnet18": TRUNK, "resnet50": TRUNK50}
 # BatchNorms of one view: name, (C, H, W, residual, relu, count)
 BNS = [("bn1", (64, 112, 112, False, True, 1)), ("l1.bn1", (64, 56, 56, False, True, 2)),
        ("l1.bn2", (64, 56, 56, True, True, 2)), ("l2.bn1", (128, 28, 28, False, True, 2)),
@@ -70,8 +86,8 @@ def _row(name, op, cnt, flops, nbytes, secs, launches_per_call=1):
                 launches=launches_per_call)
 
 
-def conv_rows(B, dev, reps=10, rotate_bytes=0, dtype="bf16", G=2):
-    ops = conv_ops(B, dev, rotate_bytes, G) if dtype == "bf16" else conv_ops_f32(B, dev, rotate_bytes)
+def conv_rows(B, dev, reps=10, rotate_bytes=0, dtype="bf16", G=2, arch="resnet18"):
+    ops = conv_ops(B, dev, rotate_bytes, G, arch) if dtype == "bf16" else conv_ops_f32(B, dev, rotate_bytes)
     return [_row(name, op, cnt, flops, nbytes, _time(fn, reps)) for name, op, cnt, flops, nbytes, fn in ops]
 
 
@@ -178,14 +194,14 @@ def _make_bf16(op, B, dev, C, H, W, K, R, st, pad, P, Q, G=2):
                                                             L.stream_of(dev)), "wgrad")
 
 
-def conv_ops(B, dev, rotate_bytes=0, G=2):
+def conv_ops(B, dev, rotate_bytes=0, G=2, arch="resnet18"):
     """(name, pass, count per step, FLOPs, algorithmic bytes, callable) of every trunk
     convolution position at batch B per view, G views per launch (the view-batched trunk).
     rotate_bytes > 0: each callable cycles over enough distinct operand sets that
     consecutive launches touch more than rotate_bytes (beyond the 256 MiB Infinity Cache:
     every launch reads HBM, not the last one's lines)."""
     out = []
-    for name, (C, H, W, K, R, st, pad, cnt) in TRUNK:
+    for name, (C, H, W, K, R, st, pad, cnt) in TRUNKS[arch]:
         P, Q = (H + 2 * pad - R) // st + 1, (W + 2 * pad - R) // st + 1
         flops = 2.0 * G * B * P * Q * K * C * R * R
         xb, yb, wb = G * B * H * W * C * 2, G * B * P * Q * K * 2, G * K * C * R * R * 2
@@ -271,21 +287,22 @@ def bn_ops(B, dev, G=2):
     return out
 
 
-def measure_family(B, dev, reps=10, rotate_bytes=320e6, dtype="bf16", G=2):
+def measure_family(B, dev, reps=10, rotate_bytes=320e6, dtype="bf16", G=2, arch="resnet18"):
     """The conv family (fwd + dgrad + wgrad of every trunk position, weighted by its count
     per step; bf16: the G views' grouped launches the step runs, fp32: one view's launches,
     the reference-precision path runs the views one by one): (flops, secs, launches, rows).
     Launches rotate over operand sets of more than the 256 MiB Infinity Cache
     (rotate_bytes), so none reads warm lines."""
-    rows = conv_rows(B, dev, reps, rotate_bytes, dtype, G)
+    rows = conv_rows(B, dev, reps, rotate_bytes, dtype, G, arch)
     flops = sum(r["flops"] * r["count"] for r in rows)
     secs = sum(r["us"] * 1e-6 * r["count"] for r in rows)
     launches = sum(r["count"] for r in rows)
     return flops, secs, launches, rows
 
 
-def markdown(rows, B, G=2):
-    out = [f"{G} view(s) per launch (view-batched trunk), batch {B} per view", "",
+def markdown(rows, B, G=2, arch="resnet18"):
+    out = [f"{arch}: {G} view(s) per launch ({'view-batched trunk' if G > 1 else 'per-view launches'}), "
+           f"batch {B} per view", "",
            f"| shape | pass | x/step | GFLOP | MB | avg us | TFLOP/s | GB/s | bound | frac of bound |",
            "|---|---|---|---|---|---|---|---|---|---|"]
     for r in rows:
@@ -315,6 +332,8 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--md", default=None)
     ap.add_argument("--only", default="", help="conv | bn (default both)")
+    ap.add_argument("--arch", default="resnet18", choices=sorted(TRUNKS),
+                    help="trunk (resnet50: the C5 workload's, convolutions only; use --groups 1 --batch 32)")
     ap.add_argument("--rotate-mb", type=float, default=320.0,
                     help="conv launches rotate over operand sets of this many MB (0: one warm set)")
     a = ap.parse_args()
@@ -323,10 +342,10 @@ def main():
     build.build()
     rows = []
     if a.only in ("", "conv"):
-        rows += conv_rows(a.batch, dev, a.reps, a.rotate_mb * 1e6, G=a.groups)
-    if a.only in ("", "bn"):
+        rows += conv_rows(a.batch, dev, a.reps, a.rotate_mb * 1e6, G=a.groups, arch=a.arch)
+    if a.only in ("", "bn") and a.arch == "resnet18":
         rows += bn_rows(a.batch, dev, a.reps, a.groups)
-    md = markdown(rows, a.batch, a.groups)
+    md = markdown(rows, a.batch, a.groups, a.arch)
     print(md)
     if a.md:
         with open(a.md, "w") as f:
