@@ -55,6 +55,7 @@ EXPORTS = {
     "gm_mmtm_spatial_reduce": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_size_t,
                                        c_void_p]),
     "gm_mmtm_set_reduce_form": (c_int, [c_int, c_int]),
+    "gm_mmtm_set_reduce_dma": (c_int, [c_int]),
     "gm_mmtm_channel_scale": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "gm_gemm_f32": (c_int, [c_void_p, c_int, c_void_p]),
     "gm_gemm_set_form": (c_int, [c_int]),

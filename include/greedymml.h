@@ -114,6 +114,9 @@ int gm_mmtm_spatial_reduce(const gm_spatial_reduce* p, int nprob, int B, int dty
  * pixels whose 16-B loads one thread keeps in flight (4, 8 or 16; GM_RED_UNROLL).
  * Process-wide, not thread-safe. */
 int gm_mmtm_set_reduce_form(int threads, int unroll);
+/* A/B knob: the bf16 forward squeeze streamed by LDS-DMA through a 3- or 4-stage ring
+ * (0 = off; GM_RED_DMA).  Process-wide. */
+int gm_mmtm_set_reduce_dma(int stages);
 
 /* ---------------------------------------------------------------------------
  * Channel re-scale: y[b,c,hw] = x[b,c,hw] * s[b*ld_s + c] (+ alpha * a[b*ld_a + c])
