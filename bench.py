@@ -122,7 +122,8 @@ def conv_roofline(conv, traffic, dtype="bf16", workload="C2"):
                 "alg_flops_per_launch": round(flops / launches), "avg_launch_us": round(secs / launches * 1e6, 2)}
     flops, secs, launches = conv
     what = {"C2": "every ResNet-18 trunk shape, both views per launch (the view-batched trunk)",
-            "C4": "every ResNet-18 trunk shape of one view", "C5": "every ResNet-50 trunk shape of one view"}[workload]
+            "C4": "every ResNet-18 trunk shape, the 4 views per launch (the view-batched trunk)",
+            "C5": "every ResNet-50 trunk shape, the 12 views per launch (the view-batched trunk)"}[workload]
     return {"kernel": "trunk convolutions (bf16 MFMA: k_conv_stem pixel-pair stem, k_conv_rw layer-1 "
                       "resident-weight, k_conv_h9 3x3 halo, k_conv_igemm_ut strided/1x1 fwd + input "
                       "grad, k_conv_wgrad4 + k_wgrad_sum weight grad; " + what + " at the step's batch, "
@@ -251,9 +252,9 @@ def main():
             dist.destroy_process_group()
         return
     kern_avg_s = time_group_sumsq(step, 10)
-    # the step's own launches: C2's view-batched trunk (vtrunk.py, 2 views per launch); the
-    # N-view models (C4 ResNet-18 x4, C5 ResNet-50 x12) launch view by view
-    conv = time_trunk_convs(B, dev, a.dtype, G=2 if a.workload == "C2" else 1, arch=WL["trunk"])
+    # the step's own launches: the view-batched trunk (vtrunk.py), all V views per launch
+    # (C2: 2 x ResNet-18, C4: 4 x ResNet-18, C5: 12 x ResNet-50); the fp32 line's one view
+    conv = time_trunk_convs(B, dev, a.dtype, G=V, arch=WL["trunk"])
     mmtm_bytes, mmtm_s = time_mmtm_reduce(dev)
     if rank == 0:
         views = V

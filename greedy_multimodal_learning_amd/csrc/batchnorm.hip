@@ -95,7 +95,7 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
 // Per-view-group operands: a grouped launch (gm_bn_*_grouped_bf16) normalises G views
 // stacked along the batch, each with its own parameters, statistics and scratch, in one
 // grid (blockIdx.z = group); every kernel starts from group_args().
-constexpr int kMaxBnG = 4;
+constexpr int kMaxBnG = 16;  // view groups per grouped launch (C5: 12 views)
 struct BnGroup {
     const void* x;
     const void* dy;

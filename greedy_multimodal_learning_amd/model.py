@@ -171,8 +171,35 @@ class MMTM_MVCNN_N(nn.Module):
     def mmtm_names(self):
         return [f"fc_excite.{i}." for i in range(self.num_views)]
 
+    def _forward_stacked(self, nets, x, curation_mode, caring_modality):
+        """All views' trunks as ONE view-batched trunk (vtrunk.py: every convolution /
+        BatchNorm position one grouped launch over the V views stacked along the batch),
+        the MMTM sites and the heads on the stacked activation (MMTM_N.forward_stacked,
+        head.pooled_linear_stacked)."""
+        X = vtrunk.vstem(x, nets)
+        X = vtrunk.vlayer(nets, 1, X)
+        scales, squeezed = [], []
+        for li in (2, 3, 4):
+            X = vtrunk.vlayer(nets, li, X)
+            X, sc, sq = getattr(self, f"mmtm{li}").forward_stacked(
+                X, self.saving_mmtm_scales, self.saving_mmtm_squeeze_array, curation_mode=curation_mode,
+                caring_modality=caring_modality if caring_modality is not None else 0)
+            scales.append(sc)
+            squeezed.append(sq)
+        B = X.shape[0] // self.num_views
+        fcs = [n.fc for n in nets]
+        if head_ok([X[i * B:(i + 1) * B] for i in range(self.num_views)], fcs) and all(
+                isinstance(n.avgpool, nn.AdaptiveAvgPool2d) and n.avgpool.output_size in ((1, 1), 1) for n in nets):
+            outs = pooled_linear_stacked(X, fcs)
+        else:
+            outs = [MMTM_MVCNN._head(n, X[i * B:(i + 1) * B]) for i, n in enumerate(nets)]
+        mean = None if getattr(self, "_no_mean", False) else sum(outs) / len(outs)
+        return mean, outs, scales, squeezed
+
     def forward(self, x, curation_mode=False, caring_modality=None):
         nets = [getattr(self, f"net_view_{i}") for i in range(self.num_views)]
+        if vtrunk.usable(self, nets, x):
+            return self._forward_stacked(nets, x, curation_mode, caring_modality)
         vs = ViewStreams.for_tensor(x, self.num_views)
         run = vs.run if vs is not None else (lambda i, fn, *a: fn(*a))
         order = list(range(self.num_views))[::-1]  # side streams first, main last

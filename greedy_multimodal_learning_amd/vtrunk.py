@@ -511,11 +511,11 @@ def vlayer(nets, i, X):
 
 
 def usable(model, nets, x):
-    """The stacked trunk applies: training-mode bf16 (input or autocast) on HIP, 2..4 views of
+    """The stacked trunk applies: training-mode bf16 (input or autocast) on HIP, 2..16 views of
     one architecture with the pixel-pair stem, every BN tracking statistics with momentum."""
     from .bn import GMBatchNorm2d
     from .conv import GMConv2d
-    if not (ENABLED and model.training and x.is_cuda and x.dim() == 5 and 2 <= len(nets) <= 4):
+    if not (ENABLED and model.training and x.is_cuda and x.dim() == 5 and 2 <= len(nets) <= 16):
         return False
     if not (x.dtype == BF or (torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == BF)):
         return False

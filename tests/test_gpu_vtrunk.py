@@ -166,7 +166,8 @@ def test_grouped_bn_matches_per_view(dev, mode, shape):
         assert int(bns[i].num_batches_tracked) == int(ref[i].num_batches_tracked) == 1
 
 
-def test_model_stacked_vs_per_view(dev):
+@pytest.mark.parametrize("kind", ["mvcnn2", "n4-r18", "n3-r50"])
+def test_model_stacked_vs_per_view(dev, kind):
     """MMTM_MVCNN training forward + backward: the view-batched trunk against the per-view
     trunks (GM_VTRUNK off), same weights and input, both measured against the fp32 path of
     the same model (every op on HIP in fp32).  The two bf16 paths round differently (split-K
@@ -177,16 +178,22 @@ def test_model_stacked_vs_per_view(dev):
     from greedy_multimodal_learning_amd import vtrunk
     from greedy_multimodal_learning_amd.losses import blend_loss
     from greedy_multimodal_learning_amd.model import MMTM_MVCNN
+    from greedy_multimodal_learning_amd.model import MMTM_MVCNN_N
     torch.manual_seed(11)
     B, H = 8, 64
-    a = MMTM_MVCNN().to(dev).to(memory_format=CL).train()
-    b = MMTM_MVCNN().to(dev).to(memory_format=CL).train()
-    c = MMTM_MVCNN().to(dev).to(memory_format=CL).train()
+    if kind == "mvcnn2":
+        V, make = 2, MMTM_MVCNN
+    else:
+        V = int(kind[1])
+        make = lambda: MMTM_MVCNN_N(num_views=V, trunk="resnet50" if kind.endswith("r50") else "resnet18")  # noqa
+    a = make().to(dev).to(memory_format=CL).train()
+    b = make().to(dev).to(memory_format=CL).train()
+    c = make().to(dev).to(memory_format=CL).train()
     b.load_state_dict(a.state_dict())
     c.load_state_dict(a.state_dict())
-    x = torch.randn(B, 2, 3, H, H, device=dev).bfloat16()
+    x = torch.randn(B, V, 3, H, H, device=dev).bfloat16()
     y = torch.randint(0, 40, (B,), device=dev)
-    assert vtrunk.usable(a, [a.net_view_0, a.net_view_1], x)
+    assert vtrunk.usable(a, [getattr(a, f"net_view_{i}") for i in range(V)], x)
     outs = {}
     for m, on in ((a, True), (b, False)):
         old = vtrunk.ENABLED
@@ -200,9 +207,12 @@ def test_model_stacked_vs_per_view(dev):
         outs[on] = [t.detach().float() for t in o]
     _, o, _, _ = c(x.float())
     blend_loss(o, y).backward()
-    for i in range(2):
-        _close(outs[True][i], outs[False][i], 2e-2, f"logits[{i}]")
-        _close(outs[True][i], o[i].detach(), 3e-2, f"logits[{i}] vs fp32")
+    for i in range(V):  # logits: the stacked path's error vs fp32 within twice the per-view path's
+        ref = o[i].detach().float().cpu()
+        scale = float(ref.abs().max()) + 1e-12
+        e_st = float((outs[True][i].cpu() - ref).abs().max()) / scale
+        e_pv = float((outs[False][i].cpu() - ref).abs().max()) / scale
+        assert e_st <= max(3e-2, 2 * e_pv), (f"logits[{i}]", e_st, e_pv)
     worst = []
     for (n, pa), (_, pb), (_, pc) in zip(a.named_parameters(), b.named_parameters(), c.named_parameters()):
         ga, gb, gc = pa.grad.double(), pb.grad.double(), pc.grad.double()
@@ -213,8 +223,12 @@ def test_model_stacked_vs_per_view(dev):
     worst.sort(reverse=True)
     print("stacked vs per-view gradient error vs fp32 (worst 5):",
           ", ".join(f"{n} {ea:.2e}/{eb:.2e}" for ea, eb, n in worst[:5]))
-    for (n, ba), (_, bb) in zip(a.named_buffers(), b.named_buffers()):
+    for (n, ba), (_, bb), (_, bc) in zip(a.named_buffers(), b.named_buffers(), c.named_buffers()):
         if ba.dtype == torch.long:
-            assert int(ba) == int(bb), n
-        else:
-            _close(ba, bb, 1e-2, n)
+            assert int(ba) == int(bb) == int(bc), n
+        else:  # running statistics: the stacked path's error vs fp32 within twice the per-view's
+            ref = bc.detach().float().cpu()
+            scale = float(ref.abs().max()) + 1e-12
+            e_st = float((ba.detach().float().cpu() - ref).abs().max()) / scale
+            e_pv = float((bb.detach().float().cpu() - ref).abs().max()) / scale
+            assert e_st <= max(1e-2, 2 * e_pv), (n, e_st, e_pv)
