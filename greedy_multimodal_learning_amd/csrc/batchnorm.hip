@@ -487,6 +487,188 @@ __device__ __forceinline__ void combine_finalize(const ReduceArgs& a, int cs, fl
     }
 }
 
+// ---------------------------------------------------------------------------------
+// The stem's max-pool backward gathered straight into its BatchNorm + ReLU backward
+// (torchvision stem: relu(bn1(x)) -> MaxPool2d(3, 2, 1); reference src/model.py:65-106).
+// The pool gradient dz (input resolution, 205 MB at C2) is never written: each thread owns
+// a 2 x 2 block of input pixels (rows 2k, 2k+1, columns 2l, 2l+1) x 8 channels and gathers
+// their pool gradient from the (at most) 2 x 2 windows (k..k+1, l..l+1) that can select
+// them - one window read serves four pixels instead of the per-pixel gather's one (four
+// times fewer L2 reads than k_maxpool_bwd) - summed in k_maxpool_bwd's order (window row,
+// then column, ascending) and rounded to bf16 as k_maxpool_bwd stores it, then masked by
+// the forward's ReLU (x*sc + sh > 0).  Pass 1 (APPLY = false) reduces S1 = sum dz,
+// S2 = sum dz*(x - mean) per channel into partial rows + the ticketed fp64 combine and
+// finalize of k_bn_reduce; pass 2 applies dx = ca*dz + cb*x + cc.  HBM: pass 1 reads x and
+// the pooled gradient + argmax, pass 2 the same and writes dx - against k_maxpool_bwd
+// (read pooled, write dz) + the BN backward (read dz and x twice, write dx).
+struct StemPoolGeo {
+    int Ng, H, W, P, Q;      // images per view group, input and pooled sizes
+    long long items;         // owner blocks x channel groups per view group
+    long long ipb;           // items per block (pass 1; a multiple of kT)
+    const uint2* idx;        // [G*Ng][P][Q][C] window-relative argmax bytes
+    const uint4* gp;         // [G*Ng][P][Q][C] bf16 pool gradient
+};
+
+template <bool APPLY>
+__global__ __launch_bounds__(kT) void k_stem_pool_bn_bwd(ReduceArgs a0, StemPoolGeo pg) {
+    const ReduceArgs a = group_args(a0);
+    __shared__ float red[kRedF + 4];
+    const int t = threadIdx.x;
+    const int C = a.C, C8 = C >> 3;
+    const int g = blockIdx.z;
+    const long long goff = (long long)g * pg.Ng * pg.P * pg.Q * C8;  // this group's pooled vectors
+    const uint2* __restrict__ IDX = pg.idx + goff;
+    const uint4* __restrict__ GP = pg.gp + goff;
+    const uint4* __restrict__ X = static_cast<const uint4*>(a.x);
+    float fsc[8], fsh[8], mu[8], ca[8], cb[8], cc[8];
+    const int cg0 = t % C8;  // fixed per thread in pass 1 (kT and the block base are multiples of C8)
+    auto ld_coef = [&](const float* p, int cg, float* v) {
+        const float4 u0 = *reinterpret_cast<const float4*>(p + cg * 8);
+        const float4 u1 = *reinterpret_cast<const float4*>(p + cg * 8 + 4);
+        v[0] = u0.x; v[1] = u0.y; v[2] = u0.z; v[3] = u0.w; v[4] = u1.x; v[5] = u1.y; v[6] = u1.z; v[7] = u1.w;
+    };
+    ld_coef(a.fcoef, cg0, fsc);
+    ld_coef(a.fcoef + C, cg0, fsh);
+    if (!APPLY) ld_coef(a.save_mean, cg0, mu);
+    else {
+        ld_coef(a.coef, cg0, ca);
+        ld_coef(a.coef + C, cg0, cb);
+        ld_coef(a.coef + 2 * C, cg0, cc);
+    }
+    float s1[8], s2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
+    // one owner block x channel group, in two phases (loads, then arithmetic) so that a
+    // thread keeps UI items' loads in flight together
+    struct Item {
+        uint2 iv[4];
+        uint4 gq[4], xv[4];
+        int n, k, l, cg;
+        unsigned okw;  // bit u: window u exists (a select on the loaded value instead would
+                       // make hipcc branch around the load and drain vmcnt per window)
+    };
+    auto load = [&](long long i, Item& it) {
+        it.cg = (int)(i % C8);
+        const long long ob = i / C8;
+        it.l = (int)(ob % pg.Q);
+        const long long r1 = ob / pg.Q;
+        it.k = (int)(r1 % pg.P);
+        it.n = (int)(r1 / pg.P);
+        const int n = it.n, k = it.k, l = it.l, cg = it.cg;
+        // windows (k + wr, l + wc); pixel (dh, dw) of the block is covered by window
+        // (k + wr, l + wc) iff wr <= dh and wc <= dw (and the window exists)
+        it.okw = 0u;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int wr = u >> 1, wc = u & 1;
+            const bool ok = k + wr < pg.P && l + wc < pg.Q;
+            const long long o = (((long long)n * pg.P + (ok ? k + wr : k)) * pg.Q + (ok ? l + wc : l)) * C8 + cg;
+            it.iv[u] = IDX[o];
+            it.gq[u] = GP[o];
+            it.okw |= ok ? (1u << u) : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int h = 2 * k + (q >> 1), w = 2 * l + (q & 1);
+            const bool in = h < pg.H && w < pg.W;
+            it.xv[q] = X[(((long long)n * pg.H + (in ? h : 2 * k)) * pg.W + (in ? w : 2 * l)) * C8 + cg];
+        }
+    };
+    auto compute = [&](const Item& it) {
+        const int n = it.n, k = it.k, l = it.l, cg = it.cg;
+        float gv[4][8];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) unpack8(it.gq[u], gv[u]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int dh = q >> 1, dw = q & 1;
+            const int h = 2 * k + dh, w = 2 * l + dw;
+            if (h >= pg.H || w >= pg.W) continue;
+            float d[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) d[j] = 0.f;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int wr = u >> 1, wc = u & 1;
+                if (wr > dh || wc > dw) continue;
+                const bool okw = (it.okw >> u) & 1u;
+                // position of pixel (h, w) in window (k + wr, l + wc): rows 2(k+wr)-1 .., cols 2(l+wc)-1 ..
+                const uint32_t pos = (uint32_t)((h - (2 * (k + wr) - 1)) * 3 + (w - (2 * (l + wc) - 1)));
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const uint32_t b = ((j < 4 ? it.iv[u].x : it.iv[u].y) >> (8 * (j & 3))) & 0xffu;
+                    if (okw && b == pos) d[j] += gv[u][j];
+                }
+            }
+            float xf[8];
+            unpack8(it.xv[q], xf);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float dr = __uint_as_float((uint32_t)Elem<uint16_t>::f2bf(d[j]) << 16);  // k_maxpool_bwd's bf16 dz
+                d[j] = fmaf(xf[j], fsc[j], fsh[j]) > 0.f ? dr : 0.f;
+            }
+            if (APPLY) {
+                float o[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) o[j] = fmaf(ca[j], d[j], fmaf(cb[j], xf[j], cc[j]));
+                reinterpret_cast<uint4*>(a.yout)[(((long long)n * pg.H + h) * pg.W + w) * C8 + cg] = pack8(o);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    s1[j] += d[j];
+                    s2[j] = fmaf(d[j], xf[j] - mu[j], s2[j]);
+                }
+            }
+        }
+    };
+    auto item = [&](long long i) {
+        Item it;
+        load(i, it);
+        compute(it);
+    };
+    if (APPLY) {
+        // (the coefficient registers hold channel group cg0: a grid-stride step is a multiple of C8)
+        const long long stride = (long long)gridDim.x * kT;
+        for (long long i = (long long)blockIdx.x * kT + t; i < pg.items; i += stride) item(i);
+        return;
+    }
+    const int rc = blockIdx.x;
+    const long long i0 = (long long)rc * pg.ipb;
+    const long long i1 = i0 + pg.ipb < pg.items ? i0 + pg.ipb : pg.items;
+    for (long long i = i0 + t; i < i1; i += kT) item(i);  // (two items in flight per thread: slower)
+    // row-group combine in LDS as k_bn_reduce: red[r0][SW][2], r0 = t / C8 (C8 threads per row)
+    const int S2w = 2 * C, r0 = t / C8, rpp = kT / C8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        red[r0 * S2w + (cg0 * 8 + j) * 2] = s1[j];
+        red[r0 * S2w + (cg0 * 8 + j) * 2 + 1] = s2[j];
+    }
+    __syncthreads();
+    float* p1 = a.part + (size_t)rc * S2w;
+    if (t < S2w) {
+        float acc = 0.f;
+        for (int i = 0; i < rpp; ++i) acc += red[i * S2w + t];
+        st_sc1(&p1[t], acc);
+    }
+    FinOps fo{};
+    if (t < C) fo = fin_load<BWD_RELUX>(a, t);
+    if (!ticket(a.counter, (unsigned)a.nrc, &red[kRedF])) return;
+    combine_finalize<BWD_RELUX>(a, 0, red, fo);
+}
+
+// Finalize of BatchNorm forward statistics whose per-workgroup partial rows were written by
+// the producer (k_conv_stem's epilogue): one block per view group combines the rows in fp64
+// (fixed order) and finalizes as k_bn_reduce's last block does.  a0.part / a0.coef: group 0's
+// rows and coefficient area, the groups scr_stride bytes apart.
+__global__ __launch_bounds__(kT) void k_bn_stats_finalize(ReduceArgs a0) {
+    const ReduceArgs a = group_args(a0);
+    __shared__ float red[kRedF + 4];
+    const int t = threadIdx.x;
+    FinOps fo{};
+    if (t < a.SW) fo = fin_load<FWD>(a, t);
+    combine_finalize<FWD>(a, 0, red, fo);
+}
+
 // The reference-precision (fp32) reduce: the reference's CPU BatchNorm accumulates its
 // sums in double (ATen acc_type<float> on the CPU), and long fp32 sums of gradients with
 // mixed signs lose the digits the parameter gradients are made of (1e-3 relative at
@@ -1438,4 +1620,89 @@ extern "C" int gm_bn_fwd_infer_f32(const gm_bn_fwd* p, void* scratch, size_t byt
 }
 extern "C" int gm_bn_bwd_f32(const gm_bn_bwd* p, void* scratch, size_t bytes, void* stream) {
     return bn_bwd<float>(p, 1, false, scratch, bytes, stream, "gm_bn_bwd_f32");
+}
+
+// The stem's BatchNorm + ReLU + max-pool backward in two launches (k_stem_pool_bn_bwd):
+// d describes one view group's pool (N images, k 3, stride 2, pad 1, C 64); ps[g] the BN
+// backward of group g with relu, fwd_coef (the mask from x) and no y / dres; ps[g].dy unused.
+extern "C" int gm_bn_relu_maxpool2d_bwd_grouped_bf16(const gm_pool_desc* d, int G, const void* dy_pool,
+                                                     const void* idx, const gm_bn_bwd* ps, void* scratch,
+                                                     size_t bytes, void* stream) {
+    const char* fn = "gm_bn_relu_maxpool2d_bwd_grouped_bf16";
+    GM_REQUIRE(d && dy_pool && idx && ps && G >= 1 && G <= kMaxBnG, "%s: bad arguments", fn);
+    GM_REQUIRE(d->k == 3 && d->stride == 2 && d->pad == 1 && d->C == 64 && d->N >= 1 && d->H >= 2 && d->W >= 2,
+               "%s: the stem's pool only (k 3, stride 2, pad 1, C 64)", fn);
+    const int P = (d->H + 2 - 3) / 2 + 1, Q = (d->W + 2 - 3) / 2 + 1;
+    GM_REQUIRE((d->H + 1) / 2 == P && (d->W + 1) / 2 == Q, "%s: pool geometry", fn);
+    for (int g = 0; g < G; ++g) {
+        const gm_bn_bwd& p = ps[g];
+        GM_REQUIRE(p.M == (long long)d->N * d->H * d->W && p.C == d->C && p.relu && p.fwd_coef && !p.y && !p.dres &&
+                       p.x && p.dx && p.gamma && p.save_mean && p.save_invstd && p.dgamma && p.dbeta &&
+                       p.accumulate == ps[0].accumulate,
+                   "%s: group %d: BN backward must be M = N*H*W, C, relu with fwd_coef, no y / dres", fn, g);
+    }
+    int rc;
+    if ((rc = check_scratch(ps[0].M, ps[0].C, G, true, scratch, bytes, fn))) return rc;
+    const Plan pl = make_plan(ps[0].M, ps[0].C);
+    ReduceArgs a{};
+    a.M = ps[0].M; a.C = ps[0].C; a.relu = 1; a.SW = ps[0].C; a.tpr_log = 3;
+    a.accumulate = ps[0].accumulate;
+    set_scratch(a, pl, static_cast<char*>(scratch), true);
+    for (int g = 0; g < G; ++g) {
+        BnGroup& q = a.grp[g];
+        q.x = ps[g].x;
+        q.gamma = ps[g].gamma;
+        q.save_mean = const_cast<float*>(ps[g].save_mean);
+        q.save_invstd = const_cast<float*>(ps[g].save_invstd);
+        q.dgamma = ps[g].dgamma; q.dbeta = ps[g].dbeta;
+        q.fcoef = ps[g].fwd_coef;
+        q.yout = static_cast<uint4*>(ps[g].dx);
+    }
+    StemPoolGeo pg;
+    pg.Ng = d->N; pg.H = d->H; pg.W = d->W; pg.P = P; pg.Q = Q;
+    pg.items = (long long)d->N * P * Q * (d->C / 8);
+    // pass-1 partial rows: at most the plan's (the grouped scratch holds pl.nrc rows per group)
+    int nrc = pl.nrc < kMaxRC ? pl.nrc : kMaxRC;
+    pg.ipb = (pg.items + nrc - 1) / nrc;
+    pg.ipb = (pg.ipb + kT - 1) / kT * kT;
+    nrc = (int)((pg.items + pg.ipb - 1) / pg.ipb);
+    a.nrc = nrc;
+    pg.idx = static_cast<const uint2*>(idx);
+    pg.gp = static_cast<const uint4*>(dy_pool);
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL((k_stem_pool_bn_bwd<false>), dim3(nrc, 1, G), dim3(kT), 0, st, a, pg);
+    if ((rc = check_launch("k_stem_pool_bn_bwd<reduce>"))) return rc;
+    long long grid = (pg.items + kT - 1) / kT;
+    if (grid > 4096) grid = 4096;
+    hipLaunchKernelGGL((k_stem_pool_bn_bwd<true>), dim3((unsigned)grid, 1, G), dim3(kT), 0, st, a, pg);
+    return check_launch("k_stem_pool_bn_bwd<apply>");
+}
+
+// BatchNorm forward statistics from producer partial rows (gm_conv2d_fwd_grouped_stats_bf16):
+// stats = [G][rows + 1][128] floats (rows partial rows of 64 x (sum, sum of squares), then
+// 128 floats of coefficient scratch); ps[g] as for gm_bn_fwd_stats_grouped_bf16 (C = 64).
+extern "C" int gm_bn_fwd_stats_finalize_grouped(const gm_bn_fwd* ps, int G, float* stats, int rows, void* stream) {
+    const char* fn = "gm_bn_fwd_stats_finalize_grouped";
+    int rc = check_groups_fwd(ps, G, fn);
+    if (rc) return rc;
+    GM_REQUIRE(stats && rows >= 1 && ps[0].C == 64 && !ps[0].residual && ps[0].M >= 1,
+               "%s: C 64, no residual, rows >= 1", fn);
+    ReduceArgs a{};
+    a.M = ps[0].M; a.C = 64; a.SW = 64; a.tpr_log = 3; a.nrc = rows;
+    a.momentum = ps[0].momentum; a.eps = ps[0].eps;
+    a.part = stats;
+    a.coef = stats + (size_t)rows * 128;
+    a.scr_stride = (unsigned long long)(rows + 1) * 128 * sizeof(float);
+    a.hdr_words = 0;
+    for (int g = 0; g < G; ++g) {
+        BnGroup& q = a.grp[g];
+        q.x = ps[g].x;
+        q.gamma = ps[g].gamma; q.beta = ps[g].beta;
+        q.rmean = ps[g].running_mean; q.rvar = ps[g].running_var;
+        q.save_mean = ps[g].save_mean; q.save_invstd = ps[g].save_invstd;
+        q.nbt = ps[g].num_batches_tracked;
+        q.coef_out = ps[g].coef_out;
+    }
+    hipLaunchKernelGGL(k_bn_stats_finalize, dim3(1, 1, G), dim3(kT), 0, as_stream(stream), a);
+    return check_launch("k_bn_stats_finalize");
 }

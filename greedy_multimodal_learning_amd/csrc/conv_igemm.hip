@@ -1736,6 +1736,9 @@ struct StemArgs {
     int wpitch;         // LDS bytes per output channel's weights (T * 16 + 16)
     FastDiv fd_p;       // P
     FastDiv fd_s;       // S
+    float* stats;       // optional: per-workgroup BatchNorm partial rows of the stored output
+                        // ([G][stats_rows][64 x (sum, sum of squares)] + 128 floats per group)
+    int stats_rows;     // workgroups per group (the rows of each group's partials)
 };
 
 __global__ __launch_bounds__(256) void k_conv_stem(ConvArgs a, StemArgs r) {
@@ -1757,8 +1760,14 @@ __global__ __launch_bounds__(256) void k_conv_stem(ConvArgs a, StemArgs r) {
         g = tl / nwg;
         tl -= g * nwg;
     }
+    const int wg = tl;  // this workgroup's index within its group (its BN partial row)
     if (tl >= r.rows || g >= a.G) return;
     const uint16_t* const gin = a.in + g * a.gs_in;
+    // BatchNorm statistics of the stored (bf16) output, per thread over its stores: every
+    // store of thread t is channel group t & 7 (k_bn_reduce's FWD accumulation)
+    float bs1[8], bs2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bs1[j] = bs2[j] = 0.f;
 
     // weights [64][T][8] -> LDS rows of wpitch bytes (register path: the padded pitch
     // is not lane-linear)
@@ -1868,10 +1877,35 @@ __global__ __launch_bounds__(256) void k_conv_stem(ConvArgs a, StemArgs r) {
             const uint4 v = *reinterpret_cast<const uint4*>(ot + (ok ? q : 0) * 128 + ((j ^ (q & 7)) << 4));
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
                                                    orsrc, ok ? rowoff + (unsigned)e * 16u : 0xfffffff0u, 0, 0);
+            if (r.stats) {
+                const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int jj = 0; jj < 8; ++jj) {
+                    const float f = ok ? __uint_as_float((jj & 1) ? (w4[jj >> 1] & 0xffff0000u) : (w4[jj >> 1] << 16))
+                                       : 0.f;
+                    bs1[jj] += f;
+                    bs2[jj] = fmaf(f, f, bs2[jj]);
+                }
+            }
         }
         __builtin_amdgcn_s_waitcnt(kWaitStores);  // the next block has landed; stores may fly
         lds_barrier();                            // and the LDS tile / block bb are free again
         bb ^= 1;
+    }
+    if (r.stats) {  // the workgroup's partial row: [32 thread rows][64 channels][2] combined in LDS
+        float* red = reinterpret_cast<float*>(lds + WB + 2 * r.hbytes);  // the output tile (16 KB)
+        const int r0 = t >> 3, cg = t & 7;
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+            red[r0 * 128 + (cg * 8 + jj) * 2] = bs1[jj];
+            red[r0 * 128 + (cg * 8 + jj) * 2 + 1] = bs2[jj];
+        }
+        __syncthreads();
+        if (t < 128) {
+            float acc = 0.f;
+            for (int i = 0; i < 32; ++i) acc += red[i * 128 + t];
+            r.stats[((size_t)g * (r.stats_rows + 1) + wg) * 128 + t] = acc;
+        }
     }
 }
 
@@ -2179,6 +2213,8 @@ static size_t stem_plan(const ConvArgs& a, StemArgs& r) {
     return lds <= 80 * 1024 ? lds : 0;  // two workgroups per CU
 }
 
+static int stem_wgs(int rows, int G) { return rows < 512 / G ? rows : (512 / G > 0 ? 512 / G : 1); }
+
 static int launch_stem(const ConvArgs& a, const StemArgs& r, size_t lds, hipStream_t st) {
     static size_t granted = 0;
     if (lds > granted) {
@@ -2191,7 +2227,7 @@ static int launch_stem(const ConvArgs& a, const StemArgs& r, size_t lds, hipStre
         granted = lds;
     }
     // persistent: two workgroups per CU, split evenly over the view groups
-    const int per = r.rows < 512 / a.G ? r.rows : (512 / a.G > 0 ? 512 / a.G : 1);
+    const int per = stem_wgs(r.rows, a.G);
     const int grid = per * a.G;
     k_conv_stem<<<grid, 256, lds, st>>>(a, r);
     return check_launch("k_conv_stem");
@@ -2448,6 +2484,8 @@ static int pick_and_launch(ConvArgs& a, hipStream_t st, void* ws, size_t ws_byte
     {
         StemArgs r;
         const size_t lds = stem_plan(a, r);
+        r.stats = nullptr;
+        r.stats_rows = 0;
         if (lds > 0) return launch_stem(a, r, lds, st);
     }
     TilePick p = pick_tile(a);
@@ -2749,6 +2787,45 @@ extern "C" int gm_conv2d_fwd_grouped_bf16(const gm_conv_desc_hw* d, int G, const
     a.gs_wt = w_stride;
     a.gs_out = (long long)d->N * a.cls[0].P * a.cls[0].Q * d->K;
     return pick_and_launch(a, as_stream(stream), ws, ws_bytes);
+}
+
+// The stem convolution (k_conv_stem's shapes) with the BatchNorm statistics of its output
+// accumulated in its epilogue: partial rows per workgroup, finalized by
+// gm_bn_fwd_stats_finalize_grouped (no statistics pass over the 205 MB output).
+extern "C" int gm_conv_stem_stats_rows(const gm_conv_desc_hw* d, int G) {
+    if (check_desc_hw(d) || G < 1 || G > 64) return 0;
+    ConvArgs a;
+    fwd_setup(d, reinterpret_cast<const void*>(16), reinterpret_cast<const void*>(16), reinterpret_cast<void*>(16), a);
+    a.G = G;
+    StemArgs r;
+    if (stem_plan(a, r) == 0 || a.Nout != 64) return 0;
+    return stem_wgs(r.rows, G);
+}
+
+extern "C" int gm_conv2d_fwd_grouped_stats_bf16(const gm_conv_desc_hw* d, int G, const void* x, const void* w,
+                                                long long w_stride, void* y, float* stats, int stats_rows,
+                                                void* stream) {
+    int rc = check_desc_hw(d);
+    if (rc) return rc;
+    GM_REQUIRE(x && w && y && stats, "conv fwd stats: null pointer");
+    GM_REQUIRE(G >= 1 && G <= 64, "conv fwd stats: view groups must be 1..64 (got %d)", G);
+    GM_REQUIRE(G == 1 || w_stride >= (long long)d->K * d->R * d->S * d->C ||
+                   -w_stride >= (long long)d->K * d->R * d->S * d->C,
+               "conv fwd stats: group weight stride %lld shorter than one weight", w_stride);
+    ConvArgs a;
+    fwd_setup(d, x, w, y, a);
+    a.G = G;
+    a.gs_in = (long long)d->N * d->H * d->W * d->C;
+    a.gs_wt = w_stride;
+    a.gs_out = (long long)d->N * a.cls[0].P * a.cls[0].Q * d->K;
+    StemArgs r;
+    const size_t lds = stem_plan(a, r);
+    GM_REQUIRE(lds > 0 && a.Nout == 64, "conv fwd stats: only the stem kernel's shapes (64 output channels)");
+    GM_REQUIRE(stats_rows == stem_wgs(r.rows, G), "conv fwd stats: stats_rows %d != gm_conv_stem_stats_rows %d",
+               stats_rows, stem_wgs(r.rows, G));
+    r.stats = stats;
+    r.stats_rows = stats_rows;
+    return launch_stem(a, r, lds, as_stream(stream));
 }
 
 extern "C" int gm_conv2d_dgrad_grouped_bf16(const gm_conv_desc* d, int G, const void* dy, const void* wt,

@@ -38,6 +38,14 @@ BF = torch.bfloat16
 ENABLED = os.environ.get("GM_VTRUNK", "1") != "0"
 
 
+# the stem's pool + BN backward in the gathered two-pass form (GM_FUSED_STEM_BWD=0: the
+# max-pool backward + BatchNorm backward pair, an A/B switch)
+FUSED_STEM_BWD = os.environ.get("GM_FUSED_STEM_BWD", "1") != "0"
+# the stem BN's statistics from the stem convolution's epilogue (GM_FUSED_STEM_STATS=0: the
+# statistics pass over the convolution's output, an A/B switch)
+FUSED_STEM_STATS = os.environ.get("GM_FUSED_STEM_STATS", "1") != "0"
+
+
 def _nhwc(t):
     return t if t.is_contiguous(memory_format=CL) else t.contiguous(memory_format=CL)
 
@@ -360,7 +368,9 @@ class _VStemFn(torch.autograd.Function):
     packed into one stacked pair view and convolved in one launch."""
 
     @staticmethod
-    def forward(ctx, x, G, pad, *weights):
+    def forward(ctx, x, G, pad, stats, *weights):
+        """stats (optional dict): receives the BN statistics partial rows of the output
+        (gm_conv2d_fwd_grouped_stats_bf16), for the stem BN's finalize."""
         lib = L.load()
         B, _, C0, H, W = x.shape
         K, _, R, S = weights[0].shape
@@ -372,8 +382,16 @@ class _VStemFn(torch.autograd.Function):
             stem_pack(x[:, g], weights[g], pad, xp=xp[g * B:(g + 1) * B], wp=wp[g])
         y = torch.empty(G * B, K, P, Q, device=dev, dtype=BF, memory_format=CL)
         d = _desc_hw(B, Hp, Wp // 2, 8, K, R, Sp, 2, 1, 0, 0)
-        L.check(lib.gm_conv2d_fwd_grouped_bf16(ctypes.byref(d), G, xp.data_ptr(), wp.data_ptr(), K * R * Sp * 8,
-                                               y.data_ptr(), 0, 0, L.stream_of(dev)), "gm_conv2d_fwd_grouped_bf16")
+        rows = lib.gm_conv_stem_stats_rows(ctypes.byref(d), G) if (stats is not None and FUSED_STEM_STATS) else 0
+        if rows > 0:
+            part = torch.empty(G, rows + 1, 128, device=dev, dtype=torch.float32)
+            L.check(lib.gm_conv2d_fwd_grouped_stats_bf16(ctypes.byref(d), G, xp.data_ptr(), wp.data_ptr(),
+                                                         K * R * Sp * 8, y.data_ptr(), part.data_ptr(), rows,
+                                                         L.stream_of(dev)), "gm_conv2d_fwd_grouped_stats_bf16")
+            stats["part"], stats["rows"] = part, rows
+        else:
+            L.check(lib.gm_conv2d_fwd_grouped_bf16(ctypes.byref(d), G, xp.data_ptr(), wp.data_ptr(), K * R * Sp * 8,
+                                                   y.data_ptr(), 0, 0, L.stream_of(dev)), "gm_conv2d_fwd_grouped_bf16")
         ctx.save_for_backward(xp, *weights)
         ctx.meta = (G, B, R, S, Sp)
         return y
@@ -382,9 +400,9 @@ class _VStemFn(torch.autograd.Function):
     def backward(ctx, gy):
         xp, *weights = ctx.saved_tensors
         G, B, R, S, Sp = ctx.meta
-        want = [ctx.needs_input_grad[3 + g] for g in range(G)]
+        want = [ctx.needs_input_grad[4 + g] for g in range(G)]
         if not any(want):
-            return (None, None, None, *[None] * G)
+            return (None, None, None, None, *[None] * G)
         lib = L.load()
         gy = _nhwc(gy.to(BF))
         dev = gy.device
@@ -413,7 +431,7 @@ class _VStemFn(torch.autograd.Function):
                 grads.append(None)
             else:
                 grads.append(_like_param(dw, w))
-        return (None, None, None, *grads)
+        return (None, None, None, None, *grads)
 
 
 class _VBNReluPoolFn(torch.autograd.Function):
@@ -421,7 +439,7 @@ class _VBNReluPoolFn(torch.autograd.Function):
     launch applying each group's coefficients (bn._BNReluPoolFn, stacked)."""
 
     @staticmethod
-    def forward(ctx, X, G, bns, k, s, pad, *params):
+    def forward(ctx, X, G, bns, k, s, pad, stats, *params):
         lib = L.load()
         gammas, betas = params[:G], params[G:]
         xb = _nhwc(X.to(BF))
@@ -436,10 +454,14 @@ class _VBNReluPoolFn(torch.autograd.Function):
                          L.ptr(bn.running_mean), L.ptr(bn.running_var), float(bn.momentum), float(bn.eps),
                          sm[g].data_ptr(), si[g].data_ptr(), L.ptr(bn.num_batches_tracked), coef[g].data_ptr())
                  for g, bn in enumerate(bns)]
-        buf = _bn_scratch_g(dev, M, C, G)
         st = L.stream_of(dev)
-        L.check(lib.gm_bn_fwd_stats_grouped_bf16(L.arr(L.BnFwd, descs), G, buf.data_ptr(), buf.numel(), st),
-                "gm_bn_fwd_stats_grouped_bf16")
+        if stats is not None and "part" in stats:  # partial rows from the stem convolution's epilogue
+            L.check(lib.gm_bn_fwd_stats_finalize_grouped(L.arr(L.BnFwd, descs), G, stats["part"].data_ptr(),
+                                                         stats["rows"], st), "gm_bn_fwd_stats_finalize_grouped")
+        else:
+            buf = _bn_scratch_g(dev, M, C, G)
+            L.check(lib.gm_bn_fwd_stats_grouped_bf16(L.arr(L.BnFwd, descs), G, buf.data_ptr(), buf.numel(), st),
+                    "gm_bn_fwd_stats_grouped_bf16")
         P, Q = (H + 2 * pad - k) // s + 1, (W + 2 * pad - k) // s + 1
         y = torch.empty(GN, C, P, Q, device=dev, dtype=BF, memory_format=CL)
         idx = torch.empty(GN, P, Q, C, device=dev, dtype=torch.uint8)
@@ -459,13 +481,37 @@ class _VBNReluPoolFn(torch.autograd.Function):
         gammas, betas = prm[:G], prm[G:]
         GN, C, H, W = xb.shape
         dy = _nhwc(dy.to(BF))
+        want_w, want_b = any(ctx.needs_input_grad[7:7 + G]), any(ctx.needs_input_grad[7 + G:])
+        if FUSED_STEM_BWD and (k, s, pad, C) == (3, 2, 1, 64) and (want_w or want_b):
+            # the pool's input gradient is gathered inside the BN backward's two passes
+            # (gm_bn_relu_maxpool2d_bwd_grouped_bf16): never written
+            N = GN // G
+            M = N * H * W
+            dx = torch.empty_like(xb, memory_format=CL)
+            dgs, dbs, acc, sunk = _bn_param_grads(gammas, betas, want_w, want_b)
+            descs = [L.BnBwd(M, C, 1, 0, 0, xb[g * N:(g + 1) * N].data_ptr(), gammas[g].data_ptr(), sm[g].data_ptr(),
+                             si[g].data_ptr(), dx[g * N:(g + 1) * N].data_ptr(), 0, dgs[g].data_ptr(),
+                             dbs[g].data_ptr(), int(acc), 0, coef[g].data_ptr()) for g in range(G)]
+            buf = _bn_scratch_g(xb.device, M, C, G)
+            d = L.PoolDesc(N, H, W, C, k, s, pad)
+            L.check(lib.gm_bn_relu_maxpool2d_bwd_grouped_bf16(ctypes.byref(d), G, dy.data_ptr(), idx.data_ptr(),
+                                                              L.arr(L.BnBwd, descs), buf.data_ptr(), buf.numel(),
+                                                              L.stream_of(xb.device)),
+                    "gm_bn_relu_maxpool2d_bwd_grouped_bf16")
+            if sunk:
+                for p in list(gammas) + list(betas):
+                    sink_done(p)
+                gw, gb = [None] * G, [None] * G
+            else:
+                gw = [t if want_w else None for t in dgs]
+                gb = [t if want_b else None for t in dbs]
+            return (dx if ctx.needs_input_grad[0] else None, None, None, None, None, None, None, *gw, *gb)
         dz = torch.empty_like(xb, memory_format=CL)
         d = L.PoolDesc(GN, H, W, C, k, s, pad)
         L.check(lib.gm_maxpool2d_bwd_bf16(ctypes.byref(d), dy.data_ptr(), idx.data_ptr(), dz.data_ptr(),
                                           L.stream_of(xb.device)), "gm_maxpool2d_bwd_bf16")
-        dx, _, gw, gb = _bn_backward(dz, None, xb, G, gammas, betas, sm, si, True, False, coef,
-                                     any(ctx.needs_input_grad[6:6 + G]), any(ctx.needs_input_grad[6 + G:]))
-        return (dx if ctx.needs_input_grad[0] else None, None, None, None, None, None, *gw, *gb)
+        dx, _, gw, gb = _bn_backward(dz, None, xb, G, gammas, betas, sm, si, True, False, coef, want_w, want_b)
+        return (dx if ctx.needs_input_grad[0] else None, None, None, None, None, None, None, *gw, *gb)
 
 
 def vstem(x, nets):
@@ -475,10 +521,11 @@ def vstem(x, nets):
     pool = nets[0].maxpool
     from .pool import _pair1
     k, s, p = (_pair1(getattr(pool, a)) for a in ("kernel_size", "stride", "padding"))
+    stats = {}  # the stem convolution's BN partial rows, handed to the BN's finalize
     with torch.autocast("cuda", enabled=False):
-        y = _VStemFn.apply(x, G, c0.padding[0], *[n.conv1.weight for n in nets])
+        y = _VStemFn.apply(x, G, c0.padding[0], stats, *[n.conv1.weight for n in nets])
         bns = [n.bn1 for n in nets]
-        return _VBNReluPoolFn.apply(y, G, bns, k, s, p, *[b.weight for b in bns], *[b.bias for b in bns])
+        return _VBNReluPoolFn.apply(y, G, bns, k, s, p, stats, *[b.weight for b in bns], *[b.bias for b in bns])
 
 
 # ---- blocks and eligibility ---------------------------------------------------------

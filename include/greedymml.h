@@ -531,6 +531,29 @@ typedef struct gm_pool_desc {
 
 int gm_maxpool2d_fwd_bf16(const gm_pool_desc* d, const void* x, void* y, void* idx, void* stream);
 int gm_maxpool2d_bwd_bf16(const gm_pool_desc* d, const void* dy, const void* idx, void* dx, void* stream);
+/* The stem's BatchNorm + ReLU + max-pool backward (torchvision stem: maxpool(relu(bn1(x))),
+ * reference src/model.py:65-106) in two launches without materialising the pool's input
+ * gradient: every thread owns a 2 x 2 pixel block and gathers its pool gradient from the
+ * <= 2 x 2 windows that can select it (k_maxpool_bwd's arithmetic: fp32 sums in window
+ * order, rounded to bf16), masks it with the forward's ReLU (x*sc + sh > 0); pass 1 reduces
+ * and finalizes the BN backward (dgamma, dbeta, dx coefficients), pass 2 writes dx.
+ * d: ONE view group's pool (N images; k 3, stride 2, pad 1, C 64); dy_pool / idx: the G
+ * groups' pooled gradient and argmax stacked ([G*N][P][Q][C], gm_bn_relu_maxpool2d_fwd_*);
+ * ps[g]: group g's BN backward with relu, fwd_coef, y = dres = NULL (dy unused); scratch:
+ * gm_bn_scratch_grouped(N*H*W, C, G) bytes of the grouped layout. */
+/* The stem's BatchNorm statistics without a pass over its output: the stem convolution
+ * (gm_conv2d_fwd_grouped_stats_bf16, k_conv_stem's shapes, 64 output channels) adds every
+ * workgroup's (sum, sum of squares) of its stored bf16 outputs into a partial row, and
+ * gm_bn_fwd_stats_finalize_grouped combines them in fp64 and finalizes like
+ * gm_bn_fwd_stats_grouped_bf16 (save_mean / save_invstd, running statistics, counter,
+ * coef_out).  stats: float [G][rows + 1][128], rows = gm_conv_stem_stats_rows(d, G)
+ * (0: the stem kernel does not apply). */
+int gm_conv_stem_stats_rows(const gm_conv_desc_hw* d, int G);
+int gm_conv2d_fwd_grouped_stats_bf16(const gm_conv_desc_hw* d, int G, const void* x, const void* w,
+                                     long long w_stride, void* y, float* stats, int rows, void* stream);
+int gm_bn_fwd_stats_finalize_grouped(const gm_bn_fwd* ps, int G, float* stats, int rows, void* stream);
+int gm_bn_relu_maxpool2d_bwd_grouped_bf16(const gm_pool_desc* d, int G, const void* dy_pool, const void* idx,
+                                          const gm_bn_bwd* ps, void* scratch, size_t scratch_bytes, void* stream);
 /* the stem's BatchNorm + ReLU + MaxPool forward: pools relu(x*sc + sh) rounded to bf16
  * (coef = sc[C], sh[C] from gm_bn_fwd_stats_bf16), bit-identical to gm_bn_fwd_train's
  * apply followed by gm_maxpool2d_fwd_bf16, without writing the normalised activation */

@@ -232,3 +232,64 @@ def test_model_stacked_vs_per_view(dev, kind):
             e_st = float((ba.detach().float().cpu() - ref).abs().max()) / scale
             e_pv = float((bb.detach().float().cpu() - ref).abs().max()) / scale
             assert e_st <= max(1e-2, 2 * e_pv), (n, e_st, e_pv)
+
+
+@pytest.mark.parametrize("G,B,H", [(2, 4, 64), (3, 2, 38), (1, 2, 224)])
+def test_fused_stem_backward_matches_pool_then_bn(dev, G, B, H):
+    """gm_bn_relu_maxpool2d_bwd_grouped_bf16 (pool gradient gathered inside the BN backward,
+    never written) against k_maxpool_bwd + the grouped BN backward: the same dz arithmetic
+    (bf16-rounded gathered sums), so dx agrees to the BN reductions' summation order
+    (<= 1 bf16 ulp) and dgamma / dbeta to fp32 rounding; ragged maps (38 -> 19x19 pool)."""
+    from greedy_multimodal_learning_amd import vtrunk
+    from greedy_multimodal_learning_amd.resnet import resnet18
+    torch.manual_seed(5 + G)
+    nets = [resnet18().to(dev).to(memory_format=CL).train() for _ in range(G)]
+    x = torch.randn(B, G, 3, H, H, device=dev).bfloat16()
+    res = {}
+    for fused in (True, False):
+        for n in nets:
+            for p in n.parameters():
+                p.grad = None
+        old = vtrunk.FUSED_STEM_BWD
+        vtrunk.FUSED_STEM_BWD = fused
+        try:
+            Y = vtrunk.vstem(x, nets)
+            gY = torch.randn(Y.shape, generator=torch.Generator(device=dev).manual_seed(9), device=dev).bfloat16()
+            Y.backward(gY.contiguous(memory_format=CL))
+        finally:
+            vtrunk.FUSED_STEM_BWD = old
+        res[fused] = [(n.conv1.weight.grad.clone(), n.bn1.weight.grad.clone(), n.bn1.bias.grad.clone()) for n in nets]
+    for g in range(G):
+        (wf, gf, bf), (wu, gu, bu) = res[True][g], res[False][g]
+        _close(gf, gu, 1e-4, f"dgamma[{g}]")
+        _close(bf, bu, 1e-4, f"dbeta[{g}]")
+        _close(wf, wu, 1e-2, f"stem dw[{g}]")
+
+
+@pytest.mark.parametrize("G,B,H", [(2, 4, 64), (3, 2, 224)])
+def test_fused_stem_statistics_match_stats_pass(dev, G, B, H):
+    """BN statistics of the stem from the convolution's epilogue partial rows
+    (gm_conv2d_fwd_grouped_stats_bf16 + gm_bn_fwd_stats_finalize_grouped) against the
+    statistics pass over the stored output: running statistics to fp32 summation order,
+    the counter, and the pooled output to 1 bf16 ulp (coefficients differ in the last bits)."""
+    from greedy_multimodal_learning_amd import vtrunk
+    from greedy_multimodal_learning_amd.resnet import resnet18
+    torch.manual_seed(7 + G)
+    nets = [resnet18().to(dev).to(memory_format=CL).train() for _ in range(G)]
+    ref = [resnet18().to(dev).to(memory_format=CL).train() for _ in range(G)]
+    for a, b in zip(nets, ref):
+        b.load_state_dict(a.state_dict())
+    x = torch.randn(B, G, 3, H, H, device=dev).bfloat16()
+    old = vtrunk.FUSED_STEM_STATS
+    try:
+        vtrunk.FUSED_STEM_STATS = True
+        Y1 = vtrunk.vstem(x, nets)
+        vtrunk.FUSED_STEM_STATS = False
+        Y0 = vtrunk.vstem(x, ref)
+    finally:
+        vtrunk.FUSED_STEM_STATS = old
+    _close(Y1, Y0, 1e-2, "pooled output")
+    for g in range(G):
+        _close(nets[g].bn1.running_mean, ref[g].bn1.running_mean, 1e-5, f"running_mean[{g}]")
+        _close(nets[g].bn1.running_var, ref[g].bn1.running_var, 1e-5, f"running_var[{g}]")
+        assert int(nets[g].bn1.num_batches_tracked) == int(ref[g].bn1.num_batches_tracked) == 1

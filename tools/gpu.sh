@@ -11,6 +11,7 @@
 #   benchq       python bench.py --no-cpu-baseline                    -> gpurun_out/benchq.log
 #   bench:ARGS   python bench.py ARGS (commas become spaces)          -> gpurun_out/bench_ARGS.log
 #   prof         rocprofv3 --kernel-trace --stats of a short bench    -> gpurun_out/prof/
+#   profw:W      the same for bench.py --workload W (C4, C5)           -> gpurun_out/prof_W/
 #   prof:V=X,..  the same with environment variables set               -> gpurun_out/prof_V_X/
 #   pmc:NAME     one rocprofv3 --pmc pass over a short bench (sets below) -> gpurun_out/pmc_NAME/
 #   table        tools/trunk_table.py: per-shape trunk launch table    -> gpurun_out/trunk_table.md
@@ -78,6 +79,11 @@ for s in "$@"; do
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$d" -o bench \
         -- $PROFCMD > "$d.log" 2>&1 || { tail -30 "$d.log"; exit 17; }
       for v in ${e//,/ }; do unset "${v%%=*}"; done
+      python3 tools/summarize_stats.py "$d/bench_kernel_stats.csv" 13 | head -40 ;;
+    profw:*)
+      w="${s#profw:}"; d="gpurun_out/prof_$w"
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$d" -o bench \
+        -- python3 bench.py --workload "$w" --steps 10 --warmup 3 --profile > "$d.log" 2>&1 || { tail -30 "$d.log"; exit 27; }
       python3 tools/summarize_stats.py "$d/bench_kernel_stats.csv" 13 | head -40 ;;
     pmc:*)
       n="${s#pmc:}"
