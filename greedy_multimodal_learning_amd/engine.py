@@ -144,6 +144,11 @@ class GradBuckets:
             return
         self._count(p)
 
+    def _on_pending(self, p):
+        """p's in-place delivery is deferred (gradsink.sink_pending): skip its hook."""
+        if not self.deferred:
+            self._via_sink.add(id(p))
+
     def _on_sink(self, p):
         """a HIP backward wrote p's gradient straight into the flat buffer (gradsink)."""
         if self.deferred:  # a hipGraph capture: the step reduces after the replay
@@ -249,6 +254,8 @@ class BalancedStep:
         self.sink = GradSink(self.flat.slices.keys(),
                              on_ready=self.buckets._on_sink if self.buckets is not None else None,
                              lazy_zero=os.environ.get("GM_LAZY_ZERO", "1") != "0")
+        if self.buckets is not None:
+            self.sink.on_pending = self.buckets._on_pending
         self.last_loss = None
         self.last_outs = None  # the last step's branch logits (fp32), e.g. for training accuracy
         self.step_count = 0

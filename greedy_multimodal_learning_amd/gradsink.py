@@ -33,6 +33,7 @@ class GradSink:
     def __init__(self, params, on_ready=None, lazy_zero=False):
         self.params = list(params)
         self.on_ready = on_ready
+        self.on_pending = None  # a delivery that will be reported later (sink_pending)
         self.active = False
         self.lazy_zero = lazy_zero
         self._written = set()
@@ -86,6 +87,15 @@ def sink_done(p):
     s = p._gm_sink
     if s.on_ready is not None:
         s.on_ready(p)
+
+
+def sink_pending(p):
+    """p's gradient will be written in place by a launch issued later in this backward
+    (vtrunk's batched weight gradients): its autograd hook is not a delivery, sink_done
+    follows once the launch is issued."""
+    s = p._gm_sink
+    if s.on_pending is not None:
+        s.on_pending(p)
 
 
 class GradJoin:

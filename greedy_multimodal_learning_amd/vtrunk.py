@@ -32,7 +32,7 @@ import torch
 from . import _lib as L
 from .bn import MASK_FROM_X
 from .conv import CL, _cpad, _desc, _desc_hw, _like_param, _prepped, _splitk_ws, _stem_geom, stem_pack
-from .gradsink import GradJoin, sink_done, sink_target
+from .gradsink import GradJoin, sink_done, sink_pending, sink_target
 
 BF = torch.bfloat16
 ENABLED = os.environ.get("GM_VTRUNK", "1") != "0"
@@ -108,6 +108,46 @@ def _reset_bn_scratch():
 
 WGRAD_STREAM = os.environ.get("GM_WGRAD_STREAM", "1") != "0"
 _WGRAD_SIDE = 64  # streams.side_stream index of the weight-gradient stream
+# Weight-gradient launches are handed to the wgrad stream in batches of WGRAD_BATCH (one
+# stream fork per batch, GM_WGRAD_BATCH; 1 = a fork per convolution).  In a replayed
+# hipGraph every fork makes the main chain's next node start on another hardware queue,
+# ~15-25 us of idle GPU per hop (profiles/r03e_step_listing.txt, tools/trace_gaps.py).
+# A batch is flushed when full, by the stem's backward (the trunk's last), and at the end
+# of the backward pass (autograd queue_callback), so no launch is ever left pending.
+WGRAD_BATCH = max(1, int(os.environ.get("GM_WGRAD_BATCH", "4")))
+_PENDING = []  # (launch, weights, tensors to keep alive, device)
+
+
+def flush_wgrads():
+    """Launch the pending weight gradients on the wgrad stream (one fork) and report their
+    parameters' gradients delivered (gradsink)."""
+    if not _PENDING:
+        return
+    items = list(_PENDING)
+    _PENDING.clear()
+    dev = items[0][3]
+    side = _wgrad_stream(dev)
+    if side is not None:
+        side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+        for launch, _, keep, _ in items:
+            if side is not None:
+                for t in keep:
+                    t.record_stream(side)
+            launch()
+    for _, weights, _, _ in items:
+        for w in weights:
+            sink_done(w)
+
+
+def _defer_wgrad(launch, weights, keep, dev):
+    for w in weights:
+        sink_pending(w)
+    if not _PENDING:
+        torch.autograd.Variable._execution_engine.queue_callback(flush_wgrads)
+    _PENDING.append((launch, weights, keep, dev))
+    if len(_PENDING) >= WGRAD_BATCH:
+        flush_wgrads()
 
 
 def _wgrad_stream(dev):
@@ -212,19 +252,16 @@ class _VConvFn(torch.autograd.Function):
                 # the weight gradient is off the critical path (only the step's end reads it):
                 # it runs on the wgrad stream, overlapping the next input-gradient launches;
                 # the engine joins the side streams before the gradients are read
-                side = _wgrad_stream(dev)
-                if side is not None:
-                    side.wait_stream(torch.cuda.current_stream(dev))
-                    gy.record_stream(side)
-                    xb.record_stream(side)
-                    scratch.record_stream(side)
-                with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+                def launch(dh=dh, gy=gy, xb=xb, buf=bufs[0], sd=sd, acc=int(tg[0][1]), scratch=scratch, need=need):
                     L.check(lib.gm_conv2d_wgrad_grouped_bf16(ctypes.byref(dh), G, gy.data_ptr(), xb.data_ptr(),
-                                                             bufs[0].data_ptr(), sd, C, int(tg[0][1]),
-                                                             scratch.data_ptr(), need, L.stream_of(dev)),
-                            "gm_conv2d_wgrad_grouped_bf16")
-                for w in weights:
-                    sink_done(w)
+                                                             buf.data_ptr(), sd, C, acc, scratch.data_ptr(), need,
+                                                             L.stream_of(dev)), "gm_conv2d_wgrad_grouped_bf16")
+                if _wgrad_stream(dev) is not None:
+                    _defer_wgrad(launch, list(weights), (gy, xb, scratch), dev)
+                else:
+                    launch()
+                    for w in weights:
+                        sink_done(w)
             else:
                 if any(t is not None for t in tg):
                     raise RuntimeError("vtrunk conv: all or none of the views' weights must be sink-managed")
@@ -475,6 +512,7 @@ class _VBNReluPoolFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        flush_wgrads()  # the trunk's remaining weight gradients overlap the stem's backward
         lib = L.load()
         xb, coef, sm, si, idx, *prm = ctx.saved_tensors
         G, k, s, pad = ctx.meta
