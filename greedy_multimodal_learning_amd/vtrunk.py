@@ -114,7 +114,7 @@ _WGRAD_SIDE = 64  # streams.side_stream index of the weight-gradient stream
 # ~15-25 us of idle GPU per hop (profiles/r03e_step_listing.txt, tools/trace_gaps.py).
 # A batch is flushed when full, by the stem's backward (the trunk's last), and at the end
 # of the backward pass (autograd queue_callback), so no launch is ever left pending.
-WGRAD_BATCH = max(1, int(os.environ.get("GM_WGRAD_BATCH", "4")))
+WGRAD_BATCH = max(1, int(os.environ.get("GM_WGRAD_BATCH", "8")))
 _PENDING = []  # (launch, weights, tensors to keep alive, device)
 
 
