@@ -144,6 +144,7 @@ struct ReduceArgs {
     uint4* yout;         // fused fwd: output / fused bwd: dx
     uint4* dres_out;     // fused bwd: dres
     unsigned spin_limit; // fused: poll budget of the coefficient hand-off
+    int redundant;       // fused, small maps: every block combines the partial rows itself
     unsigned long long scr_stride;  // bytes between the groups' coefficient + partial areas
     unsigned hdr_words;             // words between the groups' ticket / generation headers
     BnGroup grp[kMaxBnG];           // grp[blockIdx.z] replaces the per-group pointers above
@@ -669,6 +670,116 @@ __global__ __launch_bounds__(kT) void k_bn_stats_finalize(ReduceArgs a0) {
     combine_finalize<FWD>(a, 0, red, fo);
 }
 
+// ---------------------------------------------------------------------------------
+// Redundant-finalize hand-off of the single-launch kernels for small maps (a.redundant):
+// the last-arriving block no longer combines, finalizes, publishes the coefficients and a
+// generation word that the other blocks poll and then read the coefficients from - four
+// dependent memory round trips after the last partial row lands.  Every block polls the
+// slice's ticket counter itself (the partial rows' writers add to it after their sc1
+// stores: cdna_hip_programming.md Guideline 16, the sc1 poll row), combines the <= nrc
+// partial rows (sc1 loads, fp64, the fixed order of combine_finalize: every block computes
+// the same coefficients) and keeps the coefficients in LDS; the block whose ticket came
+// last also writes the side outputs (statistics, running averages, counter, coef_out /
+// dgamma, dbeta) through finalize().  The counter then counts a second round (each block
+// once it has seen nrc arrivals), and the block completing that round re-zeroes it, so
+// no poller can miss the value nrc and the ticket words are zero between calls again.
+__device__ __forceinline__ bool arrive(unsigned* ctr, unsigned n, float* flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned tk = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *flag = tk == n - 1 ? 1.f : 0.f;
+    }
+    __syncthreads();
+    return *flag != 0.f;
+}
+
+__device__ __forceinline__ bool wait_count(unsigned* ctr, unsigned n, unsigned limit, float* flag) {
+    if (threadIdx.x == 0) {
+        unsigned it = 0;
+        bool ok = true;
+        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n) {
+            if (++it >= limit) {
+                ok = false;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (!ok) atomicOr(&g_bn_fault, GM_FAULT_BN_SPIN);
+        *flag = ok ? 1.f : 0.f;
+    }
+    __syncthreads();
+    return *flag != 0.f;
+}
+
+__device__ __forceinline__ void depart(unsigned* ctr, unsigned n) {
+    if (threadIdx.x == 0) {
+        const unsigned tk = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tk == 2 * n - 1) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// the slice's coefficients into cf[3][SW] (LDS): FWD sc, sh; BWD ca, cb, cc (bf16 form)
+template <int MODE>
+__device__ __forceinline__ void combine_coefs(const ReduceArgs& a, int cs, float* red, const FinOps& fo, bool last,
+                                              float* cf) {
+    const int t = threadIdx.x;
+    const int SW = a.SW, S2w = 2 * SW;
+    const int L = S2w >> 2, G = kT / L;
+    const int lv = t % L, g = t / L;
+    const auto rq = rsrc_of(a.part + (size_t)cs * a.nrc * S2w);
+    double d0 = 0.0, d1 = 0.0, d2 = 0.0, d3 = 0.0;
+    for (int i0 = g; i0 < a.nrc; i0 += 8 * G) {
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = i0 + u * G;
+            v[u] = i < a.nrc ? ld_sc1_f32x4(rq, (unsigned)(i * S2w + 4 * lv) * 4u) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            d0 += (double)v[u].x; d1 += (double)v[u].y; d2 += (double)v[u].z; d3 += (double)v[u].w;
+        }
+    }
+    __syncthreads();
+    double* rd = reinterpret_cast<double*>(red);
+    rd[g * S2w + 4 * lv + 0] = d0;
+    rd[g * S2w + 4 * lv + 1] = d1;
+    rd[g * S2w + 4 * lv + 2] = d2;
+    rd[g * S2w + 4 * lv + 3] = d3;
+    __syncthreads();
+    if (t < SW) {
+        double S1 = 0.0, S2 = 0.0;
+        for (int i = 0; i < G; ++i) {
+            S1 += rd[i * S2w + 2 * t];
+            S2 += rd[i * S2w + 2 * t + 1];
+        }
+        const double invM = 1.0 / (double)a.M;
+        const int c = cs * SW + t;
+        if (last) {
+            if (MODE == FWD && a.nbt && cs == 0 && t == 0) *a.nbt += 1;
+            finalize<MODE, false>(a, c, S1, S2, invM, fo);
+        }
+        const double gg = (double)fo.g;
+        if (MODE == FWD) {
+            const double mean = S1 * invM;
+            double var = S2 * invM - mean * mean;
+            if (var < 0.0) var = 0.0;
+            const double invstd = 1.0 / sqrt(var + (double)a.eps);
+            const double sc = gg * invstd;
+            cf[t] = (float)sc;
+            cf[SW + t] = (float)((double)fo.b - mean * sc);
+        } else {
+            const double mean = (double)fo.rm, is = (double)fo.rv;
+            const double ca = gg * is, cb = -gg * is * is * is * S2 * invM;
+            cf[t] = (float)ca;
+            cf[SW + t] = (float)cb;
+            cf[2 * SW + t] = (float)(-ca * S1 * invM - cb * mean);
+        }
+    }
+    __syncthreads();
+}
+
 // The reference-precision (fp32) reduce: the reference's CPU BatchNorm accumulates its
 // sums in double (ATen acc_type<float> on the CPU), and long fp32 sums of gradients with
 // mixed signs lose the digits the parameter gradients are made of (1e-3 relative at
@@ -827,20 +938,33 @@ __global__ __launch_bounds__(kT, NR == 16 ? 2 : NR == 8 ? 3 : 4) void k_bn_fwd_f
     FinOps fo{};
     if (t < SW) fo = fin_load<FWD>(a, cs * SW + t);
     bool fresh = true;
-    if (ticket(a.counter + cs, (unsigned)a.nrc, &red[kRedF])) {
-        combine_finalize<FWD, true>(a, cs, red, fo);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (t == 0) __hip_atomic_store(gen, g0 + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-        fresh = wait_generation(gen, g0, a.spin_limit, &red[kRedF + 1]);
-    }
-    const auto rq = rsrc_of(a.coef);
-    const float4 sa = ld_sc1_f32x4(rq, (unsigned)c0 * 4u), sb = ld_sc1_f32x4(rq, (unsigned)(c0 + 4) * 4u);
-    const float4 ha = ld_sc1_f32x4(rq, (unsigned)(C + c0) * 4u), hb = ld_sc1_f32x4(rq, (unsigned)(C + c0 + 4) * 4u);
     float sc[8], sh[8];
-    sc[0] = sa.x; sc[1] = sa.y; sc[2] = sa.z; sc[3] = sa.w; sc[4] = sb.x; sc[5] = sb.y; sc[6] = sb.z; sc[7] = sb.w;
-    sh[0] = ha.x; sh[1] = ha.y; sh[2] = ha.z; sh[3] = ha.w; sh[4] = hb.x; sh[5] = hb.y; sh[6] = hb.z; sh[7] = hb.w;
+    if (a.redundant) {
+        __shared__ float cf[3 * 64];
+        const bool last = arrive(a.counter + cs, (unsigned)a.nrc, &red[kRedF]);
+        fresh = wait_count(a.counter + cs, (unsigned)a.nrc, a.spin_limit, &red[kRedF + 1]);
+        combine_coefs<FWD>(a, cs, red, fo, last, cf);
+        depart(a.counter + cs, (unsigned)a.nrc);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            sc[j] = cf[cg * 8 + j];
+            sh[j] = cf[SW + cg * 8 + j];
+        }
+    } else {
+        if (ticket(a.counter + cs, (unsigned)a.nrc, &red[kRedF])) {
+            combine_finalize<FWD, true>(a, cs, red, fo);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (t == 0) __hip_atomic_store(gen, g0 + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            fresh = wait_generation(gen, g0, a.spin_limit, &red[kRedF + 1]);
+        }
+        const auto rq = rsrc_of(a.coef);
+        const float4 sa = ld_sc1_f32x4(rq, (unsigned)c0 * 4u), sb = ld_sc1_f32x4(rq, (unsigned)(c0 + 4) * 4u);
+        const float4 ha = ld_sc1_f32x4(rq, (unsigned)(C + c0) * 4u), hb = ld_sc1_f32x4(rq, (unsigned)(C + c0 + 4) * 4u);
+        sc[0] = sa.x; sc[1] = sa.y; sc[2] = sa.z; sc[3] = sa.w; sc[4] = sb.x; sc[5] = sb.y; sc[6] = sb.z; sc[7] = sb.w;
+        sh[0] = ha.x; sh[1] = ha.y; sh[2] = ha.z; sh[3] = ha.w; sh[4] = hb.x; sh[5] = hb.y; sh[6] = hb.z; sh[7] = hb.w;
+    }
     if (!fresh) {  // timed out: never apply stale coefficients (the fault word is set)
 #pragma unroll
         for (int j = 0; j < 8; ++j) sc[j] = sh[j] = __builtin_nanf("");
@@ -971,23 +1095,37 @@ __global__ __launch_bounds__(kT, NR == 8 ? 2 : 3) void k_bn_bwd_fused(ReduceArgs
     FinOps fo{};
     if (t < SW) fo = fin_load<MODE>(a, cs * SW + t);
     bool fresh = true;
-    if (ticket(a.counter + cs, (unsigned)a.nrc, &red[kRedF])) {
-        combine_finalize<MODE, true>(a, cs, red, fo);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (t == 0) __hip_atomic_store(gen, g0 + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-        fresh = wait_generation(gen, g0, a.spin_limit, &red[kRedF + 1]);
-    }
-    const auto rq = rsrc_of(a.coef);
     float ca[8], cb[8], cc[8];
-    auto ld8 = [&](int off, float* o) {
-        const float4 p = ld_sc1_f32x4(rq, (unsigned)(off + c0) * 4u), q = ld_sc1_f32x4(rq, (unsigned)(off + c0 + 4) * 4u);
-        o[0] = p.x; o[1] = p.y; o[2] = p.z; o[3] = p.w; o[4] = q.x; o[5] = q.y; o[6] = q.z; o[7] = q.w;
-    };
-    ld8(0, ca);
-    ld8(C, cb);
-    ld8(2 * C, cc);
+    if (a.redundant) {
+        __shared__ float cf[3 * 64];
+        const bool last = arrive(a.counter + cs, (unsigned)a.nrc, &red[kRedF]);
+        fresh = wait_count(a.counter + cs, (unsigned)a.nrc, a.spin_limit, &red[kRedF + 1]);
+        combine_coefs<MODE>(a, cs, red, fo, last, cf);
+        depart(a.counter + cs, (unsigned)a.nrc);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            ca[j] = cf[cg * 8 + j];
+            cb[j] = cf[SW + cg * 8 + j];
+            cc[j] = cf[2 * SW + cg * 8 + j];
+        }
+    } else {
+        if (ticket(a.counter + cs, (unsigned)a.nrc, &red[kRedF])) {
+            combine_finalize<MODE, true>(a, cs, red, fo);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (t == 0) __hip_atomic_store(gen, g0 + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            fresh = wait_generation(gen, g0, a.spin_limit, &red[kRedF + 1]);
+        }
+        const auto rq = rsrc_of(a.coef);
+        auto ld8 = [&](int off, float* o) {
+            const float4 p = ld_sc1_f32x4(rq, (unsigned)(off + c0) * 4u), q = ld_sc1_f32x4(rq, (unsigned)(off + c0 + 4) * 4u);
+            o[0] = p.x; o[1] = p.y; o[2] = p.z; o[3] = p.w; o[4] = q.x; o[5] = q.y; o[6] = q.z; o[7] = q.w;
+        };
+        ld8(0, ca);
+        ld8(C, cb);
+        ld8(2 * C, cc);
+    }
     if (!fresh) {  // timed out: never apply stale coefficients (the fault word is set)
 #pragma unroll
         for (int j = 0; j < 8; ++j) ca[j] = cb[j] = cc[j] = __builtin_nanf("");
@@ -1218,6 +1356,14 @@ int device_cus() {
     return cus;
 }
 
+// the redundant-finalize hand-off (every block combines the partial rows): small maps only,
+// where a block's extra partial-row reads are a few KB (GM_BN_REDUNDANT=0: the publish form)
+static int g_bn_redundant_max = [] {
+    const char* e = getenv("GM_BN_REDUNDANT");
+    return e ? atoi(e) : 16;  // measured: 8 / 16 help layer 4 (~1-1.3 us a launch), 32+ slow layer 3
+}();
+inline int redundant_ok(int nrc) { return nrc <= g_bn_redundant_max ? 1 : 0; }
+
 inline int fused_plan(long long M, int C, Plan& pl, bool bwd = false, int G = 1) {
     if (g_fused_env == 0) return 0;
     // co-residency under the device residency plan (gm_set_residency): CUs held by
@@ -1401,6 +1547,7 @@ int bn_fwd_train(const gm_bn_fwd* ps, int G, bool grouped, void* scratch, size_t
         a.nrc = fp.nrc;
         a.gen = reinterpret_cast<unsigned*>(s) + kGenOff;
         a.spin_limit = spin_limit();
+        a.redundant = redundant_ok(a.nrc);
         const dim3 g(fp.nrc, fp.nslice, G);
         const bool res = p->residual != nullptr, relu = p->relu != 0;
 #define GM_BN_FUSED_LAUNCH(NR)                                                                        \
@@ -1497,6 +1644,7 @@ int bn_bwd(const gm_bn_bwd* ps, int G, bool grouped, void* scratch, size_t bytes
         a.nrc = fp.nrc;
         a.gen = reinterpret_cast<unsigned*>(s) + kGenOff;
         a.spin_limit = spin_limit();
+        a.redundant = redundant_ok(a.nrc);
         const dim3 g(fp.nrc, fp.nslice, G);
 #define GM_BN_BWD_FUSED_LAUNCH(NR)                                                                           \
     if (maskx) hipLaunchKernelGGL((k_bn_bwd_fused<BWD_RELUX, false, NR>), g, dim3(kT), 0, st, a);            \

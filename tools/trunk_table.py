@@ -314,8 +314,9 @@ def markdown(rows, B, G=2, arch="resnet18"):
     fl = sum(r["flops"] * r["count"] for r in cf)
     s = sum(r["us"] * r["count"] for r in cf) * 1e-6
     out.append("")
-    out.append(f"conv family ({G} view(s) per launch, B={B} per view): {fl / 1e12:.3f} TFLOP in {s * 1e3:.3f} ms = "
-               f"{fl / s / 1e12:.1f} TFLOP/s = {fl / s / 1e12 / MFMA_PEAK_TFS:.3f} of {MFMA_PEAK_TFS:.0f} TF")
+    if cf:
+        out.append(f"conv family ({G} view(s) per launch, B={B} per view): {fl / 1e12:.3f} TFLOP in {s * 1e3:.3f} ms = "
+                   f"{fl / s / 1e12:.1f} TFLOP/s = {fl / s / 1e12 / MFMA_PEAK_TFS:.3f} of {MFMA_PEAK_TFS:.0f} TF")
     hb = [r for r in rows if not r["flops"]]
     if hb:
         by = sum(r["bytes"] * r["count"] for r in hb)
