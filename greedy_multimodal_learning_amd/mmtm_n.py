@@ -30,6 +30,7 @@ import torch.nn as nn
 
 from . import _lib as L
 from . import ops
+from .gradsink import sink_done, sink_target
 from .ops import ONES, Op
 
 
@@ -41,6 +42,7 @@ class _MMTMNFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, cfg, w_sq, b_sq, *rest):
         N = cfg["N"]
+        ctx.gidx = (1, 2, 3 + N, 3 + 2 * N)  # needs_input_grad index of w_sq, b_sq, w_e[0], b_e[0]
         return _mmtmn_forward(ctx, cfg, w_sq, b_sq, list(rest[:N]), list(rest[N:2 * N]), list(rest[2 * N:3 * N]))
 
     @staticmethod
@@ -59,6 +61,7 @@ class _MMTMNStackedFn(torch.autograd.Function):
         N = cfg["N"]
         B = X.shape[0] // N
         Y = torch.empty_like(X)
+        ctx.gidx = (1, 2, 4, 4 + N)
         outs = _mmtmn_forward(ctx, cfg, w_sq, b_sq, [X[i * B:(i + 1) * B] for i in range(N)], list(rest[:N]),
                               list(rest[N:2 * N]), ys=[Y[i * B:(i + 1) * B] for i in range(N)])
         ctx.stacked_shape = (B, X.shape, X.dtype)
@@ -132,6 +135,7 @@ def _mmtmn_forward(ctx, cfg, w_sq, b_sq, xs, w_e, b_e, ys=None):
     ctx.meta = (N, B, Cs, HWs, offs, CT, Cz, lay, dt, turnoff, caring, [ld for _, ld in scl],
                 cfg["zero_curated"])
     ctx.mark_non_differentiable(*es, sq)
+    ctx.prm = (w_sq, b_sq, list(w_e), list(b_e))  # the leaves, for in-place delivery (gradsink)
     return (*ys, *es, sq)
 
 
@@ -156,14 +160,32 @@ def _mmtmn_backward(ctx, grads, dxs=None):
     da = {i: torch.empty(B, Cs[i], **f32) for i in live}
     ops.spatial_reduce([dict(x=xs[i], dy=gy[i], C=Cs[i], HW=HWs[i], out=da[i], ld_out=Cs[i], e=es[i],
                              ld_e=Cs[i]) for i in live], B, dt, lay, dev)
+    # parameter gradients: written by the GEMMs straight into the engine's flat gradient
+    # buffer when the parameter is sink-managed (no AccumulateGrad fill + add per tensor)
+    p_wsq, p_bsq, p_we, p_be = ctx.prm
+    i_wsq, i_bsq, i_we, i_be = ctx.gidx
+    sunk = []
+
+    def gbuf(prm, idx, *shape):
+        tgt = sink_target(prm) if ctx.needs_input_grad[idx] else None
+        if tgt is None:
+            return torch.empty(*shape, **f32), 0
+        t, acc = tgt
+        if not t.is_contiguous() or tuple(t.shape) != shape:
+            raise RuntimeError(f"MMTM_N: in-place gradient buffer must be a contiguous {shape}")
+        sunk.append((prm, t))
+        return t, int(acc)
+
     gw = {}
     gb = {}
     probs = []
     for i in live:
-        gw[i] = torch.empty(Cs[i], Cz, **f32)
-        gb[i] = torch.empty(Cs[i], **f32)
-        probs += [dict(M=Cs[i], N=Cz, segs=[(B, Op(da[i], 1, Cs[i]), Op(zs[i], Cz, 1))], C=gw[i], ld_c=Cz),
-                  dict(M=1, N=Cs[i], segs=[(B, ONES, Op(da[i], Cs[i], 1))], C=gb[i], ld_c=Cs[i])]
+        gw[i], acc_w = gbuf(p_we[i], i_we + i, Cs[i], Cz)
+        gb[i], acc_b = gbuf(p_be[i], i_be + i, Cs[i])
+        probs += [dict(M=Cs[i], N=Cz, segs=[(B, Op(da[i], 1, Cs[i]), Op(zs[i], Cz, 1))], C=gw[i], ld_c=Cz,
+                       accumulate=acc_w),
+                  dict(M=1, N=Cs[i], segs=[(B, ONES, Op(da[i], Cs[i], 1))], C=gb[i], ld_c=Cs[i],
+                       accumulate=acc_b)]
     ops.gemm(probs, dev)
     # dz: NORMAL sums every live modality's contribution (2 K-segments per launch,
     # later launches accumulate; the relu mask is linear so it applies per launch)
@@ -177,23 +199,24 @@ def _mmtmn_backward(ctx, grads, dxs=None):
                 ops.gemm([dict(M=B, N=Cz, segs=segs, C=dz, ld_c=Cz, mask=zs[0], ld_mask=Cz,
                                accumulate=int(n > 0))], dev)
             dsq = torch.empty(B, CT, **f32)
-            g_sq_w = torch.empty(Cz, CT, **f32)
-            g_sq_b = torch.empty(Cz, **f32)
-            ops.gemm([dict(M=Cz, N=CT, segs=[(B, Op(dz, 1, Cz), Op(sq, CT, 1))], C=g_sq_w, ld_c=CT),
-                      dict(M=1, N=Cz, segs=[(B, ONES, Op(dz, Cz, 1))], C=g_sq_b, ld_c=Cz),
+            g_sq_w, acc_w = gbuf(p_wsq, i_wsq, Cz, CT)
+            g_sq_b, acc_b = gbuf(p_bsq, i_bsq, Cz)
+            ops.gemm([dict(M=Cz, N=CT, segs=[(B, Op(dz, 1, Cz), Op(sq, CT, 1))], C=g_sq_w, ld_c=CT,
+                           accumulate=acc_w),
+                      dict(M=1, N=Cz, segs=[(B, ONES, Op(dz, Cz, 1))], C=g_sq_b, ld_c=Cz, accumulate=acc_b),
                       dict(M=B, N=CT, segs=[(Cz, Op(dz, Cz, 1), Op(w_sq, CT, 1))], C=dsq, ld_c=CT)], dev)
         else:
             dzs = {i: torch.empty(B, Cz, **f32) for i in live}
             ops.gemm([dict(M=B, N=Cz, segs=[(Cs[i], Op(da[i], Cs[i], 1), Op(w_e[i], Cz, 1))], C=dzs[i],
                            ld_c=Cz, mask=zs[i], ld_mask=Cz) for i in live], dev)
-            g_sq_w = torch.empty(Cz, CT, **f32)
-            g_sq_b = torch.empty(Cz, **f32)
+            g_sq_w, acc_w = gbuf(p_wsq, i_wsq, Cz, CT)
+            g_sq_b, acc_b = gbuf(p_bsq, i_bsq, Cz)
             for n, k in enumerate(range(0, len(live), 2)):
                 grp = live[k:k + 2]
                 ops.gemm([dict(M=Cz, N=CT, segs=[(B, Op(dzs[i], 1, Cz), Op(ins[i], CT, 1)) for i in grp],
-                               C=g_sq_w, ld_c=CT, accumulate=int(n > 0)),
+                               C=g_sq_w, ld_c=CT, accumulate=int(n > 0) | acc_w),
                           dict(M=1, N=Cz, segs=[(B, ONES, Op(dzs[i], Cz, 1)) for i in grp], C=g_sq_b,
-                               ld_c=Cz, accumulate=int(n > 0))], dev)
+                               ld_c=Cz, accumulate=int(n > 0) | acc_b)], dev)
             dsq = torch.zeros(B, CT, **f32)
             ops.gemm([dict(M=B, N=Cs[i], segs=[(Cz, Op(dzs[i], Cz, 1), Op(w_sq, CT, 1, off=offs[i]))],
                            C=dsq, c_off=offs[i], ld_c=CT) for i in live], dev)
@@ -206,10 +229,13 @@ def _mmtmn_backward(ctx, grads, dxs=None):
             p.update(a=dsq, a_off=offs[i], ld_a=CT, alpha=1.0 / HWs[i])
         probs.append(p)
     ops.channel_scale(probs, B, dt, lay, dev)
+    for prm, _ in sunk:  # delivered in place: fire the engine's per-parameter hook
+        sink_done(prm)
+    sunk_ids = {id(t) for _, t in sunk}
 
     def z_or_none(t, like):
         if t is not None:
-            return t
+            return None if id(t) in sunk_ids else t
         return torch.zeros_like(like) if zero_curated else None
     out_we = [z_or_none(gw.get(i), w_e[i]) for i in range(N)]
     out_be = [z_or_none(gb.get(i), w_e[i][:, 0]) for i in range(N)]

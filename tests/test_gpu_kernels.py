@@ -172,3 +172,39 @@ def test_group_sumsq_twelve_branches(dev):
                 ref[2 * k + 1] += float((p.grad.double() ** 2).sum())
     assert masks[0] == 1 and masks[3 * 10] == 1 << 10  # net_view_10 is not net_view_1
     np.testing.assert_allclose(out, ref, rtol=1e-6)
+
+
+@pytest.mark.parametrize("V", [12, 2])
+def test_group_sumsq_long_chunks(dev, V):
+    """Totals above 16384 x 4096 elements take longer chunks (fewer finalize rows); the
+    many-group form (V=12) flushes per mask run.  Odd tensor sizes exercise the scalar
+    heads/tails at every chunk boundary; reference = fp64 sums on the device."""
+    from greedy_multimodal_learning_amd.callbacks import GroupNorms, group_masks
+    g = torch.Generator(device=dev).manual_seed(5)
+    bn = [f"net_view_{i}" for i in range(V)]
+    mn = [f"fc_excite.{i}." for i in range(V)]
+    per = 72_000_000 // V
+    params = []
+    for i in range(V):
+        for n, s in ((f"net_view_{i}.conv.weight", (per - 1001,)), (f"net_view_{i}.bn.bias", (1001,)),
+                     (f"net_view_{i}.bn.weight", (3,))):
+            params.append((n, torch.nn.Parameter(torch.randn(*s, generator=g, device=dev))))
+        params.append((f"mmtm4.fc_excite.{i}.weight", torch.nn.Parameter(torch.randn(333, 17, generator=g, device=dev))))
+    params.append(("mmtm4.fc_squeeze.weight", torch.nn.Parameter(torch.randn(1000, 77, generator=g, device=dev))))
+    for _, p in params:
+        p.grad = torch.randn(p.shape, generator=g, device=dev)
+    masks = group_masks([n for n, _ in params], bn, mn)
+    ref = torch.zeros(4 * V, dtype=torch.float64, device=dev)
+    for (n, p), m in zip(params, masks):
+        sw = (p.detach().double() ** 2).sum()
+        sg = ((p.grad.double() * 0.5) ** 2).sum()
+        for k in range(2 * V):
+            if (m >> k) & 1:
+                ref[2 * k] += sw
+                ref[2 * k + 1] += sg
+    want = [(p.detach() - 0.01 * 0.5 * p.grad).clone() for _, p in params]
+    gn = GroupNorms(params, bn, mn)
+    out = gn.sums(grad_scale=0.5, lr=0.01)
+    np.testing.assert_allclose(out.cpu().numpy(), ref.cpu().numpy(), rtol=1e-6)
+    for (_, p), w in zip(params, want):
+        torch.testing.assert_close(p.detach(), w, rtol=1e-6, atol=1e-7)
