@@ -618,10 +618,13 @@ static WPlan plan(const gm_conv_desc_hw* d, int G = 1) {
 
 using namespace gm;
 
-// operand staging of k_conv_wgrad4 (its WR argument; GM_WGRAD_WR at load, default 0)
+// operand staging of k_conv_wgrad4 (its WR argument; GM_WGRAD_WR at load).  Default 1
+// (register-staged): 4.085 -> 4.062 ms per C2 step over six interleaved bench pairs on one
+// box, every pair in its favour (the weight gradients run beside the input-gradient chain,
+// where an LDS-DMA piece's issue cost is paid by a wave that shares its CU)
 static int g_wgrad_wr = [] {
     const char* e = getenv("GM_WGRAD_WR");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 1;
 }();
 
 template <int MT, int NT>

@@ -369,3 +369,30 @@ def test_conv_halo_tiles(dev, shape, mode):
         lib.gm_conv_set_halo(1)
     _close(y, yr, 1e-2)
     _close(dx, xr.grad, 1e-2)
+
+
+@pytest.mark.parametrize("shape", [SHAPES[0], SHAPES[1], SHAPES[4], SHAPES[6], SHAPES[8]],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_wgrad_staging_forms_bit_identical(dev, shape):
+    """k_conv_wgrad4's register-staged operands (default) and LDS-DMA staging build the
+    same LDS image and run the same MFMAs: bit-identical weight gradients."""
+    from greedy_multimodal_learning_amd import _lib as L
+    from greedy_multimodal_learning_amd.conv import GMConv2d
+    N, C, H, W, K, R, S, st, pad = shape
+    CL = torch.channels_last
+    torch.manual_seed(sum(shape))
+    m = GMConv2d(C, K, (R, S), stride=st, padding=pad, bias=False).to(dev).to(memory_format=CL)
+    x = torch.randn(N, C, H, W, device=dev).bfloat16().contiguous(memory_format=CL)
+    gy_shape = (N, K, (H + 2 * pad - R) // st + 1, (W + 2 * pad - S) // st + 1)
+    gy = torch.randn(*gy_shape, device=dev).bfloat16().contiguous(memory_format=CL)
+    lib = L.load()
+    grads = []
+    try:
+        for wr in (1, 0):
+            L.check(lib.gm_conv_set_wgrad_staging(wr), "wgrad staging")
+            m.weight.grad = None
+            m(x).backward(gy)
+            grads.append(m.weight.grad.clone())
+    finally:
+        L.check(lib.gm_conv_set_wgrad_staging(1), "wgrad staging")
+    assert torch.equal(grads[0], grads[1])
