@@ -17,7 +17,7 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("nb,B,C,H,N", [(2, 64, 512, 7, 40), (2, 5, 64, 3, 10), (3, 16, 128, 1, 7),
-                                        (4, 33, 256, 4, 40)])
+                                        (4, 33, 256, 4, 40), (2, 9, 64, 2, 130)])
 def test_pooled_linear_and_xent_match_torch(nb, B, C, H, N):
     from greedy_multimodal_learning_amd.head import branch_xent, pooled_linear
     g = torch.Generator(device="cuda").manual_seed(B * C + H)
