@@ -199,48 +199,47 @@ __global__ __launch_bounds__(256) void k_group_sumsq_runs(const gm_tensor* __res
     if (threadIdx.x < 2 * ngroups) rows[(size_t)blockIdx.x * 2 * ngroups + threadIdx.x] = acc[threadIdx.x];
 }
 
-// 1024 threads, each owning rows tid, tid + 1024, ... of ONE 16-column chunk per pass,
-// all of its loads in flight (the former 256-thread form walked ~6 rows per thread one
-// round trip at a time: 22 us on the serial end-of-step path); then a wave shuffle and
-// a fixed-order LDS combine per column => deterministic
+// 1024 threads stream the [nrows][w] row block as one flat array with fully coalesced
+// 8-byte loads: thread t < S (S = the largest multiple of w <= 1024) owns column t % w and
+// reads elements t, t + S, ... (8 in flight).  The former form gave each thread whole
+// 128-B rows (every load instruction touched 64 cache lines; 13 us on the serial end of
+// the C2 step for 1451 rows).  Then per column 32 fixed partial sums of its slots and
+// their fixed-order total => deterministic.  (Threads t >= S hold 0 and take no part.)
 constexpr int kFinT = 1024;
 __global__ __launch_bounds__(kFinT) void k_group_finalize(const double* __restrict__ rows, int nrows,
                                                           int ngroups, double* __restrict__ out) {
-    __shared__ double s[kFinT / 64][16];
+    __shared__ double s[kFinT];
+    __shared__ double part[32 * 2 * kMaxGroups];
     const int w = 2 * ngroups;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (int c0 = 0; c0 < w; c0 += 16) {
-        double acc[16];
+    const int S = (kFinT / w) * w, R = S / w;  // R row slots per column
+    const int t = threadIdx.x;
+    const long long n = (long long)nrows * w;
+    double acc = 0.0;
+    if (t < S) {
+        long long e = t;
+        for (; e + 7ll * S < n; e += 8ll * S) {
+            double v[8];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) acc[j] = 0.0;
-        int r = threadIdx.x;
-        for (; r + kFinT < nrows; r += 2 * kFinT) {  // two rows per round trip
-            double a0[16], a1[16];
+            for (int u = 0; u < 8; ++u) v[u] = rows[e + u * (long long)S];
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                a0[j] = c0 + j < w ? rows[(size_t)r * w + c0 + j] : 0.0;
-                a1[j] = c0 + j < w ? rows[(size_t)(r + kFinT) * w + c0 + j] : 0.0;
-            }
-#pragma unroll
-            for (int j = 0; j < 16; ++j) acc[j] += a0[j] + a1[j];
+            for (int u = 0; u < 8; ++u) acc += v[u];
         }
-        if (r < nrows) {
-#pragma unroll
-            for (int j = 0; j < 16; ++j)
-                if (c0 + j < w) acc[j] += rows[(size_t)r * w + c0 + j];
-        }
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const double v = wave_sum_d(acc[j]);
-            if (lane == 0) s[wave][j] = v;
-        }
-        __syncthreads();
-        if ((int)threadIdx.x < 16 && c0 + (int)threadIdx.x < w) {
-            double t = 0.0;
-            for (int q = 0; q < kFinT / 64; ++q) t += s[q][threadIdx.x];
-            out[c0 + threadIdx.x] = t;
-        }
-        __syncthreads();
+        for (; e < n; e += S) acc += rows[e];
+    }
+    s[t] = acc;
+    __syncthreads();
+    const int P = min(32, R);  // partial sums per column (R = kFinT / w >= 16)
+    if (t < P * w) {  // column c = t % w, partial q = t / w over slots q, q + P, ...
+        const int c = t % w, q = t / w;
+        double p = 0.0;
+        for (int j = q; j < R; j += P) p += s[j * w + c];
+        part[q * w + c] = p;
+    }
+    __syncthreads();
+    if (t < w) {
+        double tot = 0.0;
+        for (int q = 0; q < P; ++q) tot += part[q * w + t];
+        out[t] = tot;
     }
 }
 
