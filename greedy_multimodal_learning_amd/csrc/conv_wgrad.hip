@@ -618,13 +618,16 @@ static WPlan plan(const gm_conv_desc_hw* d, int G = 1) {
 
 using namespace gm;
 
-// operand staging of k_conv_wgrad4 (its WR argument; GM_WGRAD_WR at load).  Default 1
-// (register-staged): 4.085 -> 4.062 ms per C2 step over six interleaved bench pairs on one
-// box, every pair in its favour (the weight gradients run beside the input-gradient chain,
-// where an LDS-DMA piece's issue cost is paid by a wave that shares its CU)
+// operand staging of k_conv_wgrad4 (its WR argument; GM_WGRAD_WR at load): 0 LDS-DMA,
+// 1 register-staged, 2 (default) register-staged for 1x1 filters only.  Isolated
+// (tools/trunk_table.py) the register-staged form is faster on the 1x1/s2 downsample
+// gradients (16.6-18.7 vs 18.0-19.6 us) and slower on every 3x3 shape (layer 4 64.6 ->
+// 73.6 us, conv family 0.195 -> 0.191); in the step, where the weight gradients run beside
+// the input-gradient chain, the all-register form measured 0.4 % faster on average over
+// nine interleaved pairs, within the box-to-box noise.
 static int g_wgrad_wr = [] {
     const char* e = getenv("GM_WGRAD_WR");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 2;
 }();
 
 template <int MT, int NT>
@@ -637,7 +640,7 @@ static int launch_wgrad4(const WgradArgs& a, int grid, hipStream_t st) {
                                   (int)lds);
         attr = true;
     }
-    if (g_wgrad_wr) k_conv_wgrad4<MT, NT, 1><<<grid, 256, lds, st>>>(a);
+    if (g_wgrad_wr == 1 || (g_wgrad_wr == 2 && a.T == 1)) k_conv_wgrad4<MT, NT, 1><<<grid, 256, lds, st>>>(a);
     else k_conv_wgrad4<MT, NT><<<grid, 256, lds, st>>>(a);
     return check_launch("k_conv_wgrad4");
 }
@@ -764,7 +767,8 @@ extern "C" int gm_conv2d_wgrad_hw_bf16(const gm_conv_desc_hw* d, const void* dy,
 }
 
 extern "C" int gm_conv_set_wgrad_staging(int wr) {
-    GM_REQUIRE(wr == 0 || wr == 1, "gm_conv_set_wgrad_staging: 0 (LDS-DMA) or 1 (register-staged)");
+    GM_REQUIRE(wr >= 0 && wr <= 2,
+               "gm_conv_set_wgrad_staging: 0 (LDS-DMA), 1 (register-staged), 2 (register-staged for 1x1 filters)");
     g_wgrad_wr = wr;
     return GM_OK;
 }

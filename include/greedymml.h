@@ -349,7 +349,8 @@ int gm_conv_set_splitk(int target);
  * 256-row tiles for K >= 256, bit 1 256-column (tap, channel) tiles; 0 = 128 x 128. */
 int gm_conv_set_wgrad_wide(int mode);
 /* Weight-gradient operand staging: 0 = LDS-DMA pieces, 1 = register-staged (global_load_dwordx4
- * two steps ahead + ds_write_b128; same LDS image and arithmetic).  GM_WGRAD_WR at load. */
+ * two steps ahead + ds_write_b128; same LDS image and arithmetic), 2 (default) = register-staged
+ * for 1x1 filters, LDS-DMA otherwise.  GM_WGRAD_WR at load. */
 int gm_conv_set_wgrad_staging(int wr);
 /* Resident-weight kernel for 3x3 / stride-1 convolutions with 64 -> 64 channels (ResNet
  * layer 1, forward and input gradient; default on, GM_CONV_RW=0 at load or

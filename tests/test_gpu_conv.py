@@ -371,11 +371,11 @@ def test_conv_halo_tiles(dev, shape, mode):
     _close(dx, xr.grad, 1e-2)
 
 
-@pytest.mark.parametrize("shape", [SHAPES[0], SHAPES[1], SHAPES[4], SHAPES[6], SHAPES[8]],
+@pytest.mark.parametrize("shape", [SHAPES[0], SHAPES[1], SHAPES[2], SHAPES[4], SHAPES[6], SHAPES[8]],
                          ids=lambda s: "x".join(map(str, s)))
 def test_wgrad_staging_forms_bit_identical(dev, shape):
-    """k_conv_wgrad4's register-staged operands (default) and LDS-DMA staging build the
-    same LDS image and run the same MFMAs: bit-identical weight gradients."""
+    """k_conv_wgrad4's register-staged operands and LDS-DMA staging build the same LDS
+    image and run the same MFMAs: bit-identical weight gradients."""
     from greedy_multimodal_learning_amd import _lib as L
     from greedy_multimodal_learning_amd.conv import GMConv2d
     N, C, H, W, K, R, S, st, pad = shape
@@ -394,5 +394,5 @@ def test_wgrad_staging_forms_bit_identical(dev, shape):
             m(x).backward(gy)
             grads.append(m.weight.grad.clone())
     finally:
-        L.check(lib.gm_conv_set_wgrad_staging(1), "wgrad staging")
+        L.check(lib.gm_conv_set_wgrad_staging(2), "wgrad staging")  # the default
     assert torch.equal(grads[0], grads[1])

@@ -13,6 +13,6 @@ for r in $(seq 1 "$rounds"); do
     envs=()
     [ "$s" != "-" ] && IFS=, read -ra envs <<< "$s"
     out=$(env "${envs[@]}" timeout -k 10 300 python bench.py --no-cpu-baseline --steps 40 2>gpurun_out/ab_env_err.log) || { echo "FAILED: $s"; exit 1; }
-    echo "round $r  $s  $(grep -o '"ms_per_step": [0-9.]*' <<< "$out")" | tee -a gpurun_out/ab_env.txt
+    echo "round $r  $s  $(grep -o '"ms_per_step": [0-9.]*' <<< "$out") $(grep -o '"frac": [0-9.]*' <<< "$out" | head -1)" | tee -a gpurun_out/ab_env.txt
   done
 done
