@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--size", type=int, default=224)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--curate-all", action="store_true",
+                    help="A/B: open a curation window longer than the run on the on-device gate before "
+                         "the timed steps, so every timed step is a curated one")
     ap.add_argument("--miopen-find", action="store_true", help="torch.backends.cudnn.benchmark=True")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture of the step")
@@ -221,6 +224,13 @@ def main():
         step(xs[i % 2], ys[i % 2])
     torch.cuda.synchronize()
     curation_steps = 0
+    if a.curate_all and step.device_gate:
+        from greedy_multimodal_learning_amd import _lib as L
+        st = L.GateState.from_buffer_copy(step.gate_state.cpu().numpy().tobytes())
+        st.curation_mode, st.curation_step, st.window, st.unlock = 1, 0, 1 << 30, 1
+        st.caring = st.caring if st.caring >= 0 else 0
+        step.gate_state.copy_(torch.frombuffer(bytearray(bytes(st)), dtype=torch.uint8))
+        torch.cuda.synchronize()
     n_cur0 = step.sync_gate()["n_curated"] if step.device_gate else 0
     if dist_on:
         dist.barrier()
