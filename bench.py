@@ -165,9 +165,46 @@ def time_group_sumsq(step, n):
     return sum(a.elapsed_time(b) for a, b in evs) / n / 1e3
 
 
+def spawn_ranks(n, script, argv, poll_s=0.2):
+    """`--gpus N` without a launcher: start N rank processes of `script` (one per GPU,
+    RANK = LOCAL_RANK = i, rendezvous on 127.0.0.1) and return the job's exit code.
+    Runs BEFORE anything touches the GPU (this process never initialises HIP: the
+    ranks are children, not an exec).  If one rank fails the others are terminated,
+    so a rank stuck in a collective cannot hang the job.  Only rank 0 prints the line."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in live:
+                    q.terminate()
+        time.sleep(poll_s)
+    return rc
+
+
 def main():
     a = parse()
+    if "RANK" not in os.environ and a.gpus > 1:
+        sys.exit(spawn_ranks(a.gpus, os.path.abspath(__file__), sys.argv[1:]))
     dist_on = "RANK" in os.environ and int(os.environ.get("WORLD_SIZE", "1")) > 1
+    if int(os.environ.get("WORLD_SIZE", "1")) != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={os.environ.get('WORLD_SIZE', '1')}", file=sys.stderr)
+        sys.exit(2)
     if dist_on:
         # rehearsal knobs (not used by the driver): gloo, and every rank on cuda:0, run the
         # N-rank code path on a one-GPU box
@@ -225,11 +262,10 @@ def main():
     torch.cuda.synchronize()
     curation_steps = 0
     if a.curate_all and step.device_gate:
-        from greedy_multimodal_learning_amd import _lib as L
-        st = L.GateState.from_buffer_copy(step.gate_state.cpu().numpy().tobytes())
+        st = step.gate_struct()
         st.curation_mode, st.curation_step, st.window, st.unlock = 1, 0, 1 << 30, 1
         st.caring = st.caring if st.caring >= 0 else 0
-        step.gate_state.copy_(torch.frombuffer(bytearray(bytes(st)), dtype=torch.uint8))
+        step.set_gate_struct(st)
         torch.cuda.synchronize()
     n_cur0 = step.sync_gate()["n_curated"] if step.device_gate else 0
     if dist_on:

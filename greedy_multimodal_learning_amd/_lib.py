@@ -172,6 +172,18 @@ class GateState(ctypes.Structure):
                 ("eps", ctypes.c_double), ("M", ctypes.c_double * 4), ("d_bdr", ctypes.c_double)]
 
 
+GATE_MAX_BRANCHES = 16
+
+
+class GateStateN(ctypes.Structure):
+    """gm_gate_state_n: the N-branch on-device gate (same 32-byte prefix as GateState)."""
+    _fields_ = [("curation_mode", c_int), ("caring", c_int), ("curation_step", c_int), ("unlock", c_int),
+                ("window", c_int), ("n_curated", c_int), ("nb", c_int), ("pad0", c_int),
+                ("eps", ctypes.c_double), ("M_bypass", ctypes.c_double * GATE_MAX_BRANCHES),
+                ("M_main", ctypes.c_double * GATE_MAX_BRANCHES), ("bdr", ctypes.c_double * GATE_MAX_BRANCHES),
+                ("d_bdr", ctypes.c_double)]
+
+
 class StemPack(ctypes.Structure):
     _fields_ = [("x", c_void_p), ("dtype", c_int), ("N", c_int), ("C0", c_int), ("H", c_int), ("W", c_int),
                 ("pad", c_int), ("sn", ctypes.c_longlong), ("sc", ctypes.c_longlong), ("sh", ctypes.c_longlong),
@@ -181,6 +193,11 @@ class StemPack(ctypes.Structure):
 
 EXPORTS.update({
     "gm_gate_strong_step": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "gm_gate_strong_step_n": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "gm_mmtm_channel_scale_gated_n": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                              c_void_p]),
+    "gm_mmtm_spatial_reduce_gated_n": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                               ctypes.c_size_t, c_void_p]),
     "gm_mmtm_select_scale": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "gm_mmtm_mask_rows": (c_int, [c_void_p, ctypes.c_longlong, c_void_p, c_void_p]),

@@ -13,10 +13,18 @@
 //                            |d| > eps -> curate, caring = d < 0 ? 1 : 0; else caring 0
 //   unlocked & curating:     curation_step += 1; stop at the window
 //   locked:                  d as above, no curation, caring 0
+#include <cstddef>
+
 #include "gm_common.h"
 
 namespace gm {
 namespace {
+
+// the gated MMTM kernels read curation_mode / caring through a gm_gate_state pointer
+static_assert(offsetof(gm_gate_state_n, curation_mode) == offsetof(gm_gate_state, curation_mode) &&
+                  offsetof(gm_gate_state_n, caring) == offsetof(gm_gate_state, caring) &&
+                  offsetof(gm_gate_state_n, unlock) == offsetof(gm_gate_state, unlock),
+              "gm_gate_state_n must share gm_gate_state's prefix");
 
 __global__ void k_gate_strong(const double* __restrict__ s, gm_gate_state* st) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
@@ -37,6 +45,50 @@ __global__ void k_gate_strong(const double* __restrict__ s, gm_gate_state* st) {
                 g.curation_mode = 1;
                 g.curation_step = 0;
                 g.caring = g.d_bdr < 0.0 ? 1 : 0;
+            } else {
+                g.curation_mode = 0;
+                g.caring = 0;
+            }
+        } else {
+            g.curation_step += 1;
+            if (g.curation_step == g.window) g.curation_mode = 0;
+        }
+    } else {
+        bdr();
+        g.curation_mode = 0;
+        g.caring = 0;
+    }
+    *st = g;
+}
+
+// N branches (C4 / C5): the host gate's N-branch rule (callbacks.bdr_values /
+// bdr_decision) in fp64 - M_main_i += g/w of group i, M_bypass_i += g/w of group nb+i,
+// BDR_i = log10(M_bypass_i / M_main_i), d = max - min, caring = argmax (first on ties)
+__global__ void k_gate_strong_n(const double* __restrict__ s, gm_gate_state_n* st) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    gm_gate_state_n g = *st;
+    const int nb = g.nb < 0 ? 0 : (g.nb > GM_GATE_MAX_BRANCHES ? GM_GATE_MAX_BRANCHES : g.nb);
+    if (g.curation_mode) ++g.n_curated;
+    int hi = 0;
+    auto bdr = [&]() {
+        double mx = 0.0, mn = 0.0;
+        for (int i = 0; i < nb; ++i) {
+            g.M_main[i] += s[2 * i + 1] / s[2 * i];
+            g.M_bypass[i] += s[2 * (nb + i) + 1] / s[2 * (nb + i)];
+            const double b = log10(g.M_bypass[i] / g.M_main[i]);
+            g.bdr[i] = b;
+            if (i == 0 || b > mx) { mx = b; hi = i; }  // numpy argmax: first maximum
+            if (i == 0 || b < mn) mn = b;
+        }
+        g.d_bdr = mx - mn;
+    };
+    if (g.unlock) {
+        if (!g.curation_mode) {
+            bdr();
+            if (fabs(g.d_bdr) > g.eps) {
+                g.curation_mode = 1;
+                g.curation_step = 0;
+                g.caring = hi;
             } else {
                 g.curation_mode = 0;
                 g.caring = 0;
@@ -106,6 +158,12 @@ extern "C" int gm_gate_strong_step(const double* sums, gm_gate_state* state, voi
     GM_REQUIRE(sums && state, "gm_gate_strong_step: null pointer");
     k_gate_strong<<<1, 64, 0, as_stream(stream)>>>(sums, state);
     return check_launch("k_gate_strong");
+}
+
+extern "C" int gm_gate_strong_step_n(const double* sums, gm_gate_state_n* state, void* stream) {
+    GM_REQUIRE(sums && state, "gm_gate_strong_step_n: null pointer");
+    k_gate_strong_n<<<1, 64, 0, as_stream(stream)>>>(sums, state);
+    return check_launch("k_gate_strong_n");
 }
 
 extern "C" int gm_mmtm_select_scale(const float* e_v, int ld_v, const float* e_s, int ld_s, const float* ra_v,

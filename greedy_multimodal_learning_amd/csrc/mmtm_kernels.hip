@@ -39,12 +39,20 @@ struct RedArgs {
     RedProb p[kMaxProb];
     int nprob, B;
     const gm_gate_state* gate;  // gated form: the substituted modality's outputs x 0
+    int mod[kMaxProb];          // gated form: modality of each problem (-2: never substituted)
 };
 
-// the modality (problem 0 / 1) whose scale the on-device gate substitutes, or -1
+// the modality whose scale the on-device gate substitutes, or -1 (reads only the
+// curation_mode / caring prefix shared by gm_gate_state and gm_gate_state_n)
 __device__ __forceinline__ int gate_sub(const gm_gate_state* g) {
     if (!g) return -1;
     return g->curation_mode ? g->caring : -1;
+}
+
+// gm_mmtm_mask_rows2's factor of problem pi under the gate (0 for the substituted one)
+__device__ __forceinline__ float gate_factor(const RedArgs& a, int pi) {
+    const int sub = gate_sub(a.gate);
+    return (sub >= 0 && a.mod[pi] == sub) ? 0.f : 1.f;
 }
 
 __device__ __forceinline__ float epilogue(float g, const RedProb& p, int b, int c, float k = 1.f) {
@@ -121,7 +129,7 @@ __global__ __launch_bounds__(256) void k_rowreduce_nchw(RedArgs a, int total_row
         acc = wave_sum(acc);
         if (lane == 0) {
             const int b = r / p.C, c = r - b * p.C;
-            p.out[(size_t)b * p.ld_out + c] = epilogue(acc, p, b, c, pi == gate_sub(a.gate) ? 0.f : 1.f);
+            p.out[(size_t)b * p.ld_out + c] = epilogue(acc, p, b, c, gate_factor(a, pi));
         }
     }
 }
@@ -219,7 +227,7 @@ __global__ __launch_bounds__(NTH) void k_colreduce_nhwc(RedArgs a) {
             for (int q = 0; q < ppi; ++q) v += red[q * CW + c];
         }
         if (p.S == 1) {
-            p.out[(size_t)b * p.ld_out + c0 + c] = epilogue(v, p, b, c0 + c, pi == gate_sub(a.gate) ? 0.f : 1.f);
+            p.out[(size_t)b * p.ld_out + c0 + c] = epilogue(v, p, b, c0 + c, gate_factor(a, pi));
         } else {
             p.part[((size_t)b * p.S + s) * p.C + c0 + c] = v;
         }
@@ -338,7 +346,7 @@ __global__ __launch_bounds__(256) void k_reduce_partials(RedArgs a) {
     const float* src = p.part + (size_t)b * p.S * p.C + c;
     float v = 0.f;
     for (int s = 0; s < p.S; ++s) v += src[(size_t)s * p.C];
-    p.out[(size_t)b * p.ld_out + c] = epilogue(v, p, b, c, (int)blockIdx.z == gate_sub(a.gate) ? 0.f : 1.f);
+    p.out[(size_t)b * p.ld_out + c] = epilogue(v, p, b, c, gate_factor(a, (int)blockIdx.z));
 }
 
 // ---------------- channel scale (fwd) / apply (bwd) ----------------
@@ -359,8 +367,9 @@ struct ScaleArgs {
     ScaleProb p[kMaxProb];
     int nprob;
     long long total_vec;
-    const gm_gate_state* gate;  // gated form: problem gate_sub() reads alt[it] broadcast
-    const float* alt[2];
+    const gm_gate_state* gate;  // gated form: the problem whose modality is gate_sub() reads
+    const float* alt[kMaxProb];   // its alt row broadcast (ld 0)
+    int mod[kMaxProb];            // modality of each problem (-2: never substituted)
 };
 
 template <typename T, int N, int LAYOUT, bool ROWCONST>
@@ -373,8 +382,9 @@ __global__ __launch_bounds__(256) void k_channel_scale(ScaleArgs a) {
         for (int q = 1; q < kMaxProb; ++q)
             if (q < a.nprob && v >= a.p[q].vec_start) pi = q;
         const ScaleProb& p = a.p[pi];
-        const float* ps = pi == sub ? a.alt[pi] : p.s;  // substituted: the running average row
-        const int ld_s = pi == sub ? 0 : p.ld_s;
+        const bool subst = sub >= 0 && a.mod[pi] == sub;
+        const float* ps = subst ? a.alt[pi] : p.s;  // substituted: the running average row
+        const int ld_s = subst ? 0 : p.ld_s;
         const uint32_t i0 = (uint32_t)((v - p.vec_start) * N);
         const T* x = (const T*)p.x + i0;
         T* y = (T*)p.y + i0;
@@ -645,13 +655,15 @@ static void launch_rows(RedArgs& a, int rows, int vb, bool bwd, hipStream_t st) 
 }
 
 static int spatial_reduce_impl(const gm_spatial_reduce* in, int nprob, int B, int dtype, int layout,
-                               const gm_gate_state* gate, void* scratch, size_t scratch_bytes, void* stream) {
+                               const gm_gate_state* gate, const int* mods, void* scratch, size_t scratch_bytes,
+                               void* stream) {
     RedArgs a;
     size_t need = 0;
     int nwg = 0, vb = 16;
     int rc = red_setup(in, nprob, B, dtype, layout, a, need, nwg, vb);
     if (rc) return rc;
     a.gate = gate;
+    for (int i = 0; i < kMaxProb; ++i) a.mod[i] = (mods && i < nprob) ? mods[i] : -2;
     hipStream_t st = as_stream(stream);
     const bool bwd = in[0].dy != nullptr;
     if (layout == GM_NCHW) {
@@ -712,18 +724,29 @@ static int spatial_reduce_impl(const gm_spatial_reduce* in, int nprob, int B, in
 
 extern "C" int gm_mmtm_spatial_reduce(const gm_spatial_reduce* in, int nprob, int B, int dtype, int layout,
                                       void* scratch, size_t scratch_bytes, void* stream) {
-    return spatial_reduce_impl(in, nprob, B, dtype, layout, nullptr, scratch, scratch_bytes, stream);
+    return spatial_reduce_impl(in, nprob, B, dtype, layout, nullptr, nullptr, scratch, scratch_bytes, stream);
 }
 
 extern "C" int gm_mmtm_spatial_reduce_gated(const gm_spatial_reduce* in, int nprob, int B, int dtype, int layout,
                                             const gm_gate_state* gate, void* scratch, size_t scratch_bytes,
                                             void* stream) {
     GM_REQUIRE(gate && nprob >= 2, "spatial_reduce_gated: gate and the two modalities' problems (0, 1) required");
-    return spatial_reduce_impl(in, nprob, B, dtype, layout, gate, scratch, scratch_bytes, stream);
+    const int mods[kMaxProb] = {0, 1, -2, -2};
+    return spatial_reduce_impl(in, nprob, B, dtype, layout, gate, mods, scratch, scratch_bytes, stream);
+}
+
+extern "C" int gm_mmtm_spatial_reduce_gated_n(const gm_spatial_reduce* in, int nprob, int B, int dtype, int layout,
+                                              const gm_gate_state* gate, const int* mods, void* scratch,
+                                              size_t scratch_bytes, void* stream) {
+    GM_REQUIRE(gate && mods && nprob >= 1 && nprob <= kMaxProb,
+               "spatial_reduce_gated_n: gate, 1..%d problems and their modality ids required", kMaxProb);
+    for (int i = 0; i < nprob; ++i)
+        GM_REQUIRE(mods[i] >= -2 && mods[i] < 64, "spatial_reduce_gated_n: bad modality id %d", mods[i]);
+    return spatial_reduce_impl(in, nprob, B, dtype, layout, gate, mods, scratch, scratch_bytes, stream);
 }
 
 static int channel_scale_impl(const gm_channel_scale* in, int nprob, int B, int dtype, int layout,
-                              const gm_gate_state* gate, const float* alt0, const float* alt1, void* stream) {
+                              const gm_gate_state* gate, const int* mods, const float* const* alts, void* stream) {
     GM_REQUIRE(in && nprob >= 1 && nprob <= kMaxProb, "channel_scale: nprob must be 1..%d", kMaxProb);
     GM_REQUIRE(B >= 1, "channel_scale: B must be >= 1");
     GM_REQUIRE(dtype == GM_F32 || dtype == GM_BF16, "channel_scale: bad dtype");
@@ -761,8 +784,10 @@ static int channel_scale_impl(const gm_channel_scale* in, int nprob, int B, int 
     }
     a.total_vec = vs;
     a.gate = gate;
-    a.alt[0] = alt0;
-    a.alt[1] = alt1;
+    for (int i = 0; i < kMaxProb; ++i) {
+        a.mod[i] = (mods && i < nprob) ? mods[i] : -2;
+        a.alt[i] = (alts && i < nprob) ? alts[i] : nullptr;
+    }
     hipStream_t st = as_stream(stream);
     long long g = (vs + 255) / 256;
     if (g > 16384) g = 16384;
@@ -802,7 +827,23 @@ extern "C" int gm_mmtm_channel_scale_gated(const gm_channel_scale* in, int nprob
     GM_REQUIRE(gate && alt0 && alt1 && nprob >= 2, "channel_scale_gated: gate, two alternative rows and the two "
                "modalities' problems (0, 1) are required");
     GM_REQUIRE(aligned(alt0, 16) && aligned(alt1, 16), "channel_scale_gated: alternative rows must be 16-B aligned");
-    return channel_scale_impl(in, nprob, B, dtype, layout, gate, alt0, alt1, stream);
+    const int mods[kMaxProb] = {0, 1, -2, -2};
+    const float* alts[kMaxProb] = {alt0, alt1, nullptr, nullptr};
+    return channel_scale_impl(in, nprob, B, dtype, layout, gate, mods, alts, stream);
+}
+
+extern "C" int gm_mmtm_channel_scale_gated_n(const gm_channel_scale* in, int nprob, int B, int dtype, int layout,
+                                             const gm_gate_state* gate, const int* mods, const float* const* alts,
+                                             void* stream) {
+    GM_REQUIRE(gate && mods && alts && nprob >= 1 && nprob <= kMaxProb,
+               "channel_scale_gated_n: gate, 1..%d problems, their modality ids and alternative rows required",
+               kMaxProb);
+    for (int i = 0; i < nprob; ++i) {
+        GM_REQUIRE(mods[i] >= -2 && mods[i] < 64, "channel_scale_gated_n: bad modality id %d", mods[i]);
+        GM_REQUIRE(mods[i] < 0 || (alts[i] && aligned(alts[i], 16)),
+                   "channel_scale_gated_n: problem %d needs a 16-B aligned alternative row", i);
+    }
+    return channel_scale_impl(in, nprob, B, dtype, layout, gate, mods, alts, stream);
 }
 
 extern "C" int gm_mmtm_running_avg(const float* e_v, int ld_e, int B, int C, const float* ra_v_old,

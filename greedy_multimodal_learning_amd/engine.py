@@ -39,6 +39,7 @@ from .gradsink import GradSink
 from .losses import blend_loss
 from .streams import all_side_streams, side_stream
 from .streams import enabled as streams_enabled
+from .vtrunk import drop_pending_wgrads
 
 
 _DEBUG_BUCKETS = os.environ.get("GM_DEBUG_BUCKETS", "0") == "1"
@@ -301,18 +302,27 @@ class BalancedStep:
         # on-device gate: the Strong gate's decision made by a kernel behind
         # the norms+SGD pass and consumed by the MMTM kernels from device memory, so no
         # host sync per step and one graph for every curation setting
+        # Two branches over MMTM_mitigate: gm_gate_state (the reference's d = BDR_0 - BDR_1);
+        # N branches over MMTM_N (C4 / C5): gm_gate_state_n (the host gate's N-branch rule,
+        # callbacks.bdr_decision), up to GATE_MAX_BRANCHES branches.
+        from . import _lib as L
         from .callbacks import Bias_Mitigation_Strong
-        eligible = (self.device.type == "cuda" and isinstance(gate, Bias_Mitigation_Strong)
-                    and len(gate.branchnames) == 2 and self._mmtms
-                    and all(isinstance(m, MMTM_mitigate) and not m.SEonly for m in self._mmtms))
+        nb = len(gate.branchnames) if isinstance(gate, Bias_Mitigation_Strong) else 0
+        two = (nb == 2 and bool(self._mmtms)
+               and all(isinstance(m, MMTM_mitigate) and not m.SEonly for m in self._mmtms))
+        many = (2 <= nb <= L.GATE_MAX_BRANCHES and bool(self._mmtms)
+                and all(isinstance(m, MMTM_N) and m.N == nb for m in self._mmtms))
+        eligible = self.device.type == "cuda" and (two or many)
         if device_gate is None:
             import os as _os
             device_gate = _os.environ.get("GM_DEVICE_GATE", "1") != "0"
         self.device_gate = bool(device_gate) and eligible
+        self.gate_n = self.device_gate and not two
         self.gate_state = None
         if self.device_gate:
-            from . import _lib as L
-            st = L.GateState()
+            st = L.GateStateN() if self.gate_n else L.GateState()
+            if self.gate_n:
+                st.nb = nb
             st.caring = -1
             st.window = int(gate.curation_windowsize)
             st.eps = float(gate.epsilon)
@@ -355,8 +365,22 @@ class BalancedStep:
     # ---------------- on-device gate ----------------
     def _gate_step(self, sums):
         from . import _lib as L
+        if self.gate_n:
+            L.check(L.load().gm_gate_strong_step_n(sums.data_ptr(), self.gate_state.data_ptr(),
+                                                   L.stream_of(self.device)), "gm_gate_strong_step_n")
+            return
         L.check(L.load().gm_gate_strong_step(sums.data_ptr(), self.gate_state.data_ptr(),
                                              L.stream_of(self.device)), "gm_gate_strong_step")
+
+    def gate_struct(self):
+        """The device gate state as its ctypes mirror (GateState / GateStateN); a host sync."""
+        from . import _lib as L
+        cls = L.GateStateN if self.gate_n else L.GateState
+        return cls.from_buffer_copy(self.gate_state.cpu().numpy().tobytes())
+
+    def set_gate_struct(self, st):
+        """Write a (modified) gate_struct() back to the device."""
+        self.gate_state.copy_(torch.frombuffer(bytearray(bytes(st)), dtype=torch.uint8))
 
     def sync_gate(self):
         """Copy the device gate state to the host mirrors (gate.d_BDR, its M
@@ -368,12 +392,17 @@ class BalancedStep:
         L.check_device_faults()  # a timed-out in-launch hand-off since the last sync raises here
         if not self.device_gate:
             return None
-        raw = self.gate_state.cpu().numpy().tobytes()
-        st = L.GateState.from_buffer_copy(raw)
+        st = self.gate_struct()
         g, fl = self.gate, self.flags
         g.d_BDR = float(st.d_bdr)
-        g.M_bypass_modal_0, g.M_bypass_modal_1 = float(st.M[0]), float(st.M[1])
-        g.M_main_modal_0, g.M_main_modal_1 = float(st.M[2]), float(st.M[3])
+        if self.gate_n:
+            nb = int(st.nb)
+            g.M_bypass = [float(v) for v in st.M_bypass[:nb]]
+            g.M_main = [float(v) for v in st.M_main[:nb]]
+            g.BDR = [float(v) for v in st.bdr[:nb]]
+        else:
+            g.M_bypass_modal_0, g.M_bypass_modal_1 = float(st.M[0]), float(st.M[1])
+            g.M_main_modal_0, g.M_main_modal_1 = float(st.M[2]), float(st.M[3])
         g.curation_step = int(st.curation_step)
         fl.curation_mode = bool(st.curation_mode)
         fl.caring_modality = None if st.caring < 0 else int(st.caring)
@@ -395,6 +424,7 @@ class BalancedStep:
             self.flat_grad.zero_()
         if self.buckets is not None:
             self.buckets.reset()
+        drop_pending_wgrads()
         self.sink.begin_step()
         wp = self.wprep
         try:
@@ -418,6 +448,9 @@ class BalancedStep:
                 cur = torch.cuda.current_stream(self.device)
                 for s in all_side_streams(self.device):
                     cur.wait_stream(s)
+        except BaseException:
+            drop_pending_wgrads()
+            raise
         finally:
             self.sink.end_step()
             if wp is not None:

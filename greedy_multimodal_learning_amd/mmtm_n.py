@@ -125,22 +125,27 @@ def _mmtmn_forward(ctx, cfg, w_sq, b_sq, xs, w_e, b_e, ys=None):
         for i in range(N):
             ops.running_avg_dev(es[i], ra[i], ra[i], cfg["step_dev"], increment=i == N - 1)
     ra_new = ra
-    caring = cfg["caring"] if cfg["curation"] else None
+    # on-device gate (engine, N branches): the flags live in device memory; the channel scale
+    # reads the substituted modality's running average in place of its rows and backward
+    # zeroes its excitation gradient inside the squeeze-backward launch (gm_mmtm_*_gated_n)
+    gate = cfg.get("gate")
+    caring = cfg["caring"] if (cfg["curation"] and gate is None) else None
     scl = [(es[i], Cs[i]) if i != caring else (ra_new[i], 0) for i in range(N)]
     if ys is None:
         ys = [torch.empty_like(x) for x in xs]
     ops.channel_scale([dict(x=xs[i], y=ys[i], C=Cs[i], HW=HWs[i], s=scl[i][0], ld_s=scl[i][1])
-                       for i in range(N)], B, dt, lay, dev)
+                       for i in range(N)], B, dt, lay, dev, gate=gate,
+                      alt=None if gate is None else list(ra_new), mods=None if gate is None else list(range(N)))
     ctx.save_for_backward(sq, w_sq, *xs, *zs, *es, *w_e, *[s for s, _ in scl], *(ins or []))
     ctx.meta = (N, B, Cs, HWs, offs, CT, Cz, lay, dt, turnoff, caring, [ld for _, ld in scl],
-                cfg["zero_curated"])
+                cfg["zero_curated"], gate, list(ra_new))
     ctx.mark_non_differentiable(*es, sq)
     ctx.prm = (w_sq, b_sq, list(w_e), list(b_e))  # the leaves, for in-place delivery (gradsink)
     return (*ys, *es, sq)
 
 
 def _mmtmn_backward(ctx, grads, dxs=None):
-    N, B, Cs, HWs, offs, CT, Cz, lay, dt, turnoff, caring, lds, zero_curated = ctx.meta
+    N, B, Cs, HWs, offs, CT, Cz, lay, dt, turnoff, caring, lds, zero_curated, gate, ra = ctx.meta
     sv = ctx.saved_tensors
     sq, w_sq = sv[0], sv[1]
     xs = list(sv[2:2 + N])
@@ -159,7 +164,8 @@ def _mmtmn_backward(ctx, grads, dxs=None):
     live = [i for i in range(N) if i != caring]
     da = {i: torch.empty(B, Cs[i], **f32) for i in live}
     ops.spatial_reduce([dict(x=xs[i], dy=gy[i], C=Cs[i], HW=HWs[i], out=da[i], ld_out=Cs[i], e=es[i],
-                             ld_e=Cs[i]) for i in live], B, dt, lay, dev)
+                             ld_e=Cs[i]) for i in live], B, dt, lay, dev, gate=gate,
+                       mods=None if gate is None else live)
     # parameter gradients: written by the GEMMs straight into the engine's flat gradient
     # buffer when the parameter is sink-managed (no AccumulateGrad fill + add per tensor)
     p_wsq, p_bsq, p_we, p_be = ctx.prm
@@ -228,7 +234,8 @@ def _mmtmn_backward(ctx, grads, dxs=None):
         if dsq is not None:
             p.update(a=dsq, a_off=offs[i], ld_a=CT, alpha=1.0 / HWs[i])
         probs.append(p)
-    ops.channel_scale(probs, B, dt, lay, dev)
+    ops.channel_scale(probs, B, dt, lay, dev, gate=gate, alt=None if gate is None else ra,
+                      mods=None if gate is None else list(range(N)))
     for prm, _ in sunk:  # delivered in place: fire the engine's per-parameter hook
         sink_done(prm)
     sunk_ids = {id(t) for _, t in sunk}
@@ -263,6 +270,21 @@ class MMTM_N(nn.Module):
         self.running_avg = [torch.zeros(d) for d in dims]
         self.step = 0
         self.zero_grads_for_curated = False
+        # set by the engine's on-device gate: a device gm_gate_state_n whose flags replace
+        # the curation_mode / caring_modality arguments
+        self.device_gate = None
+        # True: host flags drive the same gated kernels as the device gate (the test that
+        # pins the N-branch device gate against the host gate bit for bit)
+        self.mask_curation = False
+
+    def _gate_for(self, curation_mode, caring_modality, dev):
+        if self.device_gate is not None or not self.mask_curation:
+            return self.device_gate
+        st = L.GateStateN()
+        st.curation_mode = int(bool(curation_mode))
+        st.caring = int(caring_modality) if curation_mode else -1
+        st.nb = self.N
+        return torch.frombuffer(bytearray(bytes(st)), dtype=torch.uint8).to(dev)
 
     def forward_stacked(self, X, return_scale=False, return_squeezed_mps=False, turnoff_cross_modal_flow=False,
                         average_squeezemaps=None, curation_mode=False, caring_modality=0):
@@ -289,7 +311,8 @@ class MMTM_N(nn.Module):
         cfg = dict(N=self.N, layout=lay, turnoff=bool(turnoff_cross_modal_flow), step_dev=_step_counter(self, dev),
                    ra=self.running_avg, ra_source=self.ra_source,
                    curation=bool(curation_mode), caring=int(caring_modality) if curation_mode else None,
-                   zero_curated=self.zero_grads_for_curated)
+                   zero_curated=self.zero_grads_for_curated,
+                   gate=None if turnoff_cross_modal_flow else self._gate_for(curation_mode, caring_modality, dev))
         if turnoff_cross_modal_flow:
             if return_squeezed_mps:
                 raise UnboundLocalError("local variable 'squeeze_array' referenced before assignment")

@@ -4,6 +4,8 @@ Every function takes device tensors, launches on the current HIP stream of
 their device and raises GreedyMMLError on failure.  No CPU path exists: a
 non-HIP tensor is an error.
 """
+import ctypes
+
 import torch
 
 from . import _lib as L
@@ -37,15 +39,18 @@ def as_layout(x, layout):
 MAX_REDUCE, MAX_SCALE, MAX_GEMM = 4, 4, 6  # problems per launch (include/greedymml.h)
 
 
-def spatial_reduce(probs, B, dtype, layout, device, gate=None):
+def spatial_reduce(probs, B, dtype, layout, device, gate=None, mods=None):
     """probs: list of dict(x, dy, out, ld_out, e, ld_e, C, HW, scale, out_off) -> launches.
     gate (device gm_gate_state): problems 0 / 1 are the two modalities and the substituted
-    one's outputs are zeroed in the same launch (gm_mmtm_spatial_reduce_gated)."""
-    if gate is not None:
+    one's outputs are zeroed in the same launch (gm_mmtm_spatial_reduce_gated); with
+    mods (modality id per problem, N-modality form) any number of problems
+    (gm_mmtm_spatial_reduce_gated_n, MAX_REDUCE per launch)."""
+    if gate is not None and mods is None:
         assert 2 <= len(probs) <= MAX_REDUCE
     if len(probs) > MAX_REDUCE:
         for i in range(0, len(probs), MAX_REDUCE):
-            spatial_reduce(probs[i:i + MAX_REDUCE], B, dtype, layout, device)
+            spatial_reduce(probs[i:i + MAX_REDUCE], B, dtype, layout, device, gate=gate,
+                           mods=None if mods is None else mods[i:i + MAX_REDUCE])
         return
     lib = L.load()
     items = []
@@ -59,6 +64,12 @@ def spatial_reduce(probs, B, dtype, layout, device, gate=None):
     a = L.arr(L.SpatialReduce, items)
     need = lib.gm_spatial_reduce_scratch(a, len(items), B, dtype, layout)
     scratch = torch.empty(max(need, 16), dtype=torch.uint8, device=device) if need else None
+    if gate is not None and mods is not None:
+        m = (ctypes.c_int * len(items))(*[int(v) for v in mods])
+        L.check(lib.gm_mmtm_spatial_reduce_gated_n(a, len(items), B, dtype, layout, gate.data_ptr(), m,
+                                                   L.ptr(scratch), need, L.stream_of(device)),
+                "gm_mmtm_spatial_reduce_gated_n")
+        return
     if gate is not None:
         L.check(lib.gm_mmtm_spatial_reduce_gated(a, len(items), B, dtype, layout, gate.data_ptr(), L.ptr(scratch),
                                                  need, L.stream_of(device)), "gm_mmtm_spatial_reduce_gated")
@@ -67,15 +78,23 @@ def spatial_reduce(probs, B, dtype, layout, device, gate=None):
                                        L.stream_of(device)), "gm_mmtm_spatial_reduce")
 
 
-def channel_scale(probs, B, dtype, layout, device, gate=None, alt=None):
+def channel_scale(probs, B, dtype, layout, device, gate=None, alt=None, mods=None):
     """probs: list of dict(x, y, C, HW, s, s_off, ld_s, a, a_off, ld_a, alpha).
     gate (device gm_gate_state) + alt (two fp32 rows): problems 0 / 1 are the two
-    modalities and the substituted one scales by its alt row (gm_mmtm_channel_scale_gated)."""
+    modalities and the substituted one scales by its alt row (gm_mmtm_channel_scale_gated);
+    with mods (modality id per problem) alt holds one row per problem and any number of
+    problems is allowed (gm_mmtm_channel_scale_gated_n, MAX_SCALE per launch)."""
     if gate is not None:
-        assert 2 <= len(probs) <= MAX_SCALE and alt is not None
+        assert alt is not None
+        if mods is None:
+            assert 2 <= len(probs) <= MAX_SCALE
+        else:
+            assert len(mods) == len(alt) == len(probs)
     if len(probs) > MAX_SCALE:
         for i in range(0, len(probs), MAX_SCALE):
-            channel_scale(probs[i:i + MAX_SCALE], B, dtype, layout, device)
+            sl = slice(i, i + MAX_SCALE)
+            channel_scale(probs[sl], B, dtype, layout, device, gate=gate,
+                          alt=None if mods is None else alt[sl], mods=None if mods is None else mods[sl])
         return
     lib = L.load()
     items = []
@@ -87,6 +106,12 @@ def channel_scale(probs, B, dtype, layout, device, gate=None, alt=None):
             (a.data_ptr() + 4 * p.get("a_off", 0)) if a is not None else 0, p.get("ld_a", 0),
             p.get("alpha", 0.0)))
     arr = L.arr(L.ChannelScale, items)
+    if gate is not None and mods is not None:
+        m = (ctypes.c_int * len(items))(*[int(v) for v in mods])
+        rows = (ctypes.c_void_p * len(items))(*[r.data_ptr() for r in alt])
+        L.check(lib.gm_mmtm_channel_scale_gated_n(arr, len(items), B, dtype, layout, gate.data_ptr(), m, rows,
+                                                  L.stream_of(device)), "gm_mmtm_channel_scale_gated_n")
+        return
     if gate is not None:
         L.check(lib.gm_mmtm_channel_scale_gated(arr, len(items), B, dtype, layout, gate.data_ptr(), alt[0].data_ptr(),
                                                 alt[1].data_ptr(), L.stream_of(device)),

@@ -140,6 +140,16 @@ def flush_wgrads():
             sink_done(w)
 
 
+def drop_pending_wgrads():
+    """Forget weight-gradient launches a failed backward left queued (the autograd
+    end-of-backward callback does not run when backward raises).  Called by the engine
+    at the start of every step and on its error path, so a stale closure (old gy / x,
+    possibly capture-pool memory) is never launched into the next step's gradients."""
+    n = len(_PENDING)
+    _PENDING.clear()
+    return n
+
+
 def _defer_wgrad(launch, weights, keep, dev):
     for w in weights:
         sink_pending(w)

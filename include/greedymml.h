@@ -227,6 +227,23 @@ typedef struct gm_gate_state {
 } gm_gate_state;
 /* sums: device fp64 [8] from gm_group_sumsq (main0, main1, bypass0, bypass1: w, g) */
 int gm_gate_strong_step(const double* sums, gm_gate_state* state, void* stream);
+/* N-branch form (configs C4 / C5: 2 <= nb <= GM_GATE_MAX_BRANCHES).  Same 32-byte prefix as
+ * gm_gate_state, so the gated MMTM kernels read either.  The host gate's N-branch rule
+ * (callbacks.bdr_decision): BDR_i = log10(M_bypass_i / M_main_i), d_bdr = max - min,
+ * caring = argmax (first on ties); at nb = 2 this is the reference's rule
+ * (src/callbacks.py:244-252).  sums: device fp64 [4*nb] from gm_group_sumsq over the 2*nb
+ * groups main0..main{nb-1}, bypass0..bypass{nb-1} (w, g per group). */
+#define GM_GATE_MAX_BRANCHES 16
+typedef struct gm_gate_state_n {
+    int curation_mode, caring, curation_step, unlock;   /* caring: -1 = None */
+    int window, n_curated, nb, pad0;
+    double eps;
+    double M_bypass[GM_GATE_MAX_BRANCHES];
+    double M_main[GM_GATE_MAX_BRANCHES];
+    double bdr[GM_GATE_MAX_BRANCHES];
+    double d_bdr;
+} gm_gate_state_n;
+int gm_gate_strong_step_n(const double* sums, gm_gate_state_n* state, void* stream);
 /* s_m = running average (broadcast over B) for the cared-for modality when curating,
  * else e_m; mask[2] = {0 or 1} per modality (0: substituted, no excitation gradient) */
 int gm_mmtm_select_scale(const float* e_v, int ld_v, const float* e_s, int ld_s, const float* ra_v,
@@ -249,6 +266,16 @@ int gm_mmtm_channel_scale_gated(const gm_channel_scale* p, int nprob, int B, int
                                 void* stream);
 int gm_mmtm_spatial_reduce_gated(const gm_spatial_reduce* p, int nprob, int B, int dtype, int layout,
                                  const gm_gate_state* state, void* scratch, size_t scratch_bytes, void* stream);
+/* N-modality forms (MMTM_N under the on-device gate): problem i belongs to modality
+ * mods[i] (-2: never substituted) and, when that modality is substituted, scales by
+ * alts[i] broadcast (channel_scale) / has its outputs multiplied by 0 (spatial_reduce).
+ * `state` may point at a gm_gate_state or a gm_gate_state_n (shared prefix). */
+int gm_mmtm_channel_scale_gated_n(const gm_channel_scale* p, int nprob, int B, int dtype, int layout,
+                                  const gm_gate_state* state, const int* mods, const float* const* alts,
+                                  void* stream);
+int gm_mmtm_spatial_reduce_gated_n(const gm_spatial_reduce* p, int nprob, int B, int dtype, int layout,
+                                   const gm_gate_state* state, const int* mods, void* scratch,
+                                   size_t scratch_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Pixel-pair packing of the RGB stem (one launch, input and weight):
