@@ -208,6 +208,8 @@ def main():
     if dist_on:
         # rehearsal knobs (not used by the driver): gloo, and every rank on cuda:0, run the
         # N-rank code path on a one-GPU box
+        from greedy_multimodal_learning_amd.engine import bound_rccl_channels
+        bound_rccl_channels()  # before any communicator exists: the engine reserves that many CUs
         dist.init_process_group(os.environ.get("GM_BENCH_DIST_BACKEND", "nccl"))
         rank, world = dist.get_rank(), dist.get_world_size()
         # (ranks sharing one GPU are found by the engine: gm_set_residency's `sharers`)

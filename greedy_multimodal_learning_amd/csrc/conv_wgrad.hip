@@ -478,6 +478,225 @@ __global__ __launch_bounds__(256) void k_conv_wgrad4(WgradArgs a) {
     }
 }
 
+// k_conv_wgrad_ring<MT, NT, BK, NS>: the k_conv_wgrad4 tile (same LDS image, swizzle,
+// transposed fragment reads and MFMA order, so bit-identical results) on an NS-deep LDS-DMA
+// ring of BK-pixel steps.  k_conv_wgrad4 issues step s+1, computes step s and then drains
+// vmcnt(0) at a __syncthreads: every step waits out one full DMA round trip beyond the
+// MFMAs that cover it.  Here NS-1 steps are in flight: each step waits with a COUNTED
+// vmcnt((NS-2) * pieces) for its own pieces only, passes a raw s_barrier (no vmcnt drain)
+// so every wave's pieces of the step have landed, re-issues the buffer the previous step
+// read (all waves are past that step's reads) and computes (cdna_hip_programming.md §5,
+// "Pipelining across barriers").  BK = 32 keeps the ring at 4 x 16 KB for 128 x 128 tiles,
+// so two workgroups still share a CU.
+template <int MT, int NT, int BK, int NS>
+__global__ __launch_bounds__(256) void k_conv_wgrad_ring(WgradArgs a) {
+    static_assert(BK == 32 || BK == 64, "BK");
+    static_assert(NS >= 3 && NS <= 6, "ring depth");
+    constexpr int BM = 64 * MT, BN = 64 * NT;
+    constexpr int RA = 2 * BM, RB = 2 * BN;          // row bytes
+    constexpr int SA = BK * RA, SB = BK * RB;        // bytes per buffer
+    constexpr int SS = SA + SB;                       // one ring slot
+    constexpr int GA = SA / 1024 / 4, GB = SB / 1024 / 4;  // DMA instructions per wave per step
+    constexpr int PC = GA + GB;                      // pieces per wave per step (vmcnt units)
+    static_assert(GA >= 1 && GB >= 1 && (NS - 2) * PC <= 63, "pieces / vmcnt range");
+    constexpr int LPA = RA / 16, LPB = RB / 16;      // lanes per row
+    constexpr int KS = BK / 16;                      // 16-pixel k-slices per step
+    extern __shared__ __attribute__((aligned(16))) uint4 wsm[];
+    char* lds = reinterpret_cast<char*>(wsm);        // NS slots of [A][B]
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    int bid = blockIdx.x;
+    {   // XCD-major: the tiles of one pixel range share an XCD (and its L2 copy of the rows)
+        const int n = gridDim.x, q = n >> 3, r = n & 7, x = bid & 7;
+        bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+    }
+    const int tiles = a.tiles_k * a.tiles_n;
+    const int grp = bid / (tiles * a.splits);
+    bid -= grp * tiles * a.splits;
+    const uint16_t* __restrict__ gdy = a.dy + grp * a.gs_dy;
+    const uint16_t* __restrict__ gx = a.x + grp * a.gs_x;
+    const int split = bid / tiles, tile = bid - split * tiles;
+    const int tk = tile % a.tiles_k, tn = tile / a.tiles_k;
+    const int k0 = tk * BM, n0 = tn * BN;
+    const int PQ = a.P * a.Q;
+    const int M = a.N * PQ;
+    constexpr int SUB = 64 / BK;                     // BK-steps per 64-pixel plan step
+    const int step0 = split * a.steps_per_split * SUB;
+    const int step1 = min((M + BK - 1) / BK, step0 + a.steps_per_split * SUB);
+    const int nst = step1 - step0;
+
+    const int a_rsub = lane / LPA, a_slot = lane % LPA;
+    const uint16_t* a_ptr[GA];
+    int a_row[GA];
+    bool a_cok[GA];
+#pragma unroll
+    for (int j = 0; j < GA; ++j) {
+        a_row[j] = (wave * GA + j) * (64 / LPA) + a_rsub;
+        const int col = k0 + ((a_slot ^ wswz<RA>(a_row[j])) << 3);
+        a_cok[j] = col < a.Kc;
+        a_ptr[j] = gdy + ((size_t)step0 * BK + a_row[j]) * a.Kc + (a_cok[j] ? col : 0);
+    }
+    const int b_rsub = lane / LPB, b_slot = lane % LPB;
+    int b_toff[GB], b_dh[GB], b_dw[GB];
+    int b_b[GB], b_p[GB], b_q[GB];
+    bool b_cok[GB];
+#pragma unroll
+    for (int j = 0; j < GB; ++j) {
+        const int row = (wave * GB + j) * (64 / LPB) + b_rsub;
+        const int col = n0 + ((b_slot ^ wswz<RB>(row)) << 3);
+        b_cok[j] = col < a.T * a.C;
+        const int tap = b_cok[j] ? col >> a.logC : 0;
+        const int r = tap / a.S, s = tap - r * a.S;
+        b_dh[j] = r - a.padh;
+        b_dw[j] = s - a.padw;
+        b_toff[j] = ((b_dh[j] * a.W + b_dw[j]) << a.logC) + (col & (a.C - 1));
+        const int m = step0 * BK + row;
+        b_b[j] = (int)a.fd_pq.div((uint32_t)m);
+        const int pq = m - b_b[j] * PQ;
+        b_p[j] = (int)a.fd_q.div((uint32_t)pq);
+        b_q[j] = pq - b_p[j] * a.Q;
+    }
+    typedef __attribute__((address_space(1))) const void* gptr_t;
+    typedef __attribute__((address_space(3))) void* lptr_t;
+    const void* zero = (const void*)g_wzero16;
+    auto issue = [&](int i, int slot) __attribute__((always_inline)) {  // step step0 + i into ring slot
+        const bool full = (step0 + i + 1) * BK <= M;
+        const int bufoff = slot * SS;
+#pragma unroll
+        for (int j = 0; j < GA; ++j) {
+            const bool ok = a_cok[j] & (full | ((step0 + i) * BK + a_row[j] < M));
+            const void* src = ok ? (const void*)(a_ptr[j] + (size_t)i * BK * a.Kc) : zero;
+            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + bufoff + (wave * GA + j) * 1024), 16, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < GB; ++j) {
+            const int b = b_b[j], p = b_p[j], q = b_q[j];
+            const int h0 = p * a.sth, w0 = q * a.stw;
+            const int hi = h0 + b_dh[j], wi = w0 + b_dw[j];
+            const bool ok = b_cok[j] & (b < a.N) & ((unsigned)hi < (unsigned)a.H) & ((unsigned)wi < (unsigned)a.W);
+            const int pix = (b * a.H + h0) * a.W + w0;
+            const void* src = ok ? (const void*)(gx + (((long)pix << a.logC) + b_toff[j])) : zero;
+            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + bufoff + SA + (wave * GB + j) * 1024), 16,
+                                             0, 0);
+            int nq = q + a.adv_q, np = p + a.adv_p, nb = b + a.adv_b;
+            if (nq >= a.Q) { nq -= a.Q; ++np; }
+            if (np >= a.P) { np -= a.P; ++nb; }
+            b_b[j] = nb; b_p[j] = np; b_q[j] = nq;
+        }
+    };
+
+    floatx16 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+    const int rbase = 8 * (g >> 1) + q4;
+    unsigned a_lds[MT], b_lds[NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+        const int c = wm * (32 * MT) + 32 * i + 16 * (g & 1) + 4 * p4;
+        a_lds[i] = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)(
+            lds + rbase * RA + (((c >> 3) ^ wswz<RA>(rbase)) << 4) + (c & 7) * 2);
+    }
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const int c = wn * (32 * NT) + 32 * j + 16 * (g & 1) + 4 * p4;
+        b_lds[j] = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)(
+            lds + SA + rbase * RB + (((c >> 3) ^ wswz<RB>(rbase)) << 4) + (c & 7) * 2);
+    }
+    auto compute = [&](int slot) __attribute__((always_inline)) {
+        const unsigned so = (unsigned)(slot * SS);
+        unsigned ab[MT], bb[NT];
+#pragma unroll
+        for (int i = 0; i < MT; ++i) ab[i] = a_lds[i] + so;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) bb[j] = b_lds[j] + so;
+        bf16x8 af[2][MT], bfr[2][NT];
+        auto load = [&](int ks, int c) {
+#pragma unroll
+            for (int i = 0; i < MT; ++i) af[c][i] = tr_frag_asm<0, RA>(ks, ab[i]);
+#pragma unroll
+            for (int j = 0; j < NT; ++j) bfr[c][j] = tr_frag_asm<0, RB>(ks, bb[j]);
+        };
+        load(0, 0);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const int c = ks & 1;
+            wait_lgkm0<MT, NT>(af[c], bfr[c]);
+            if (ks + 1 < KS) load(ks + 1, c ^ 1);
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[c][i], bfr[c][j], acc[i][j], 0, 0, 0);
+        }
+    };
+    // prologue: NS-1 steps in flight (fewer when the split is short)
+    const int npre = nst < NS - 1 ? nst : NS - 1;
+    for (int i = 0; i < npre; ++i) issue(i, i);
+    int i = 0, slot = 0;
+    for (; i + (NS - 1) < nst; ++i) {  // steady state: retire step i, re-issue its predecessor's slot
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * PC) : "memory");
+        __builtin_amdgcn_s_barrier();
+        issue(i + NS - 1, slot == 0 ? NS - 1 : slot - 1);
+        compute(slot);
+        slot = slot == NS - 1 ? 0 : slot + 1;
+    }
+    // tail: the last npre steps, nothing more to issue; k steps stay in flight behind each
+    auto tail = [&](auto kc) __attribute__((always_inline)) {
+        constexpr int k = decltype(kc)::value;
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(k * PC) : "memory");
+        __builtin_amdgcn_s_barrier();
+        compute(slot);
+        slot = slot == NS - 1 ? 0 : slot + 1;
+    };
+    const int left = nst - i;  // == npre
+    if (left >= 6) tail(std::integral_constant<int, 5>{});
+    if (left >= 5) tail(std::integral_constant<int, 4>{});
+    if (left >= 4) tail(std::integral_constant<int, 3>{});
+    if (left >= 3) tail(std::integral_constant<int, 2>{});
+    if (left >= 2) tail(std::integral_constant<int, 1>{});
+    if (left >= 1) tail(std::integral_constant<int, 0>{});
+
+    const int TC = a.T * a.C;
+    float* out = a.part + grp * a.gs_part + (size_t)split * a.Kc * TC;
+    const bool inner = k0 + BM <= a.Kc && n0 + BN <= TC;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const int col = n0 + wn * (32 * NT) + 32 * j + (lane & 31);
+#pragma unroll
+        for (int ii = 0; ii < MT; ++ii) {
+            const int row0 = k0 + wm * (32 * MT) + 32 * ii + 4 * (lane >> 5);
+            float* o = out + (size_t)row0 * TC + col;
+            if (inner) {
+                if (a.accumulate) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        float* p = o + (size_t)((r & 3) + 8 * (r >> 2)) * TC;
+                        *p += acc[ii][j][r];
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) o[(size_t)((r & 3) + 8 * (r >> 2)) * TC] = acc[ii][j][r];
+                }
+            } else if (col < TC) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = row0 + (r & 3) + 8 * (r >> 2);
+                    if (row < a.Kc) {
+                        float* p = o + (size_t)((r & 3) + 8 * (r >> 2)) * TC;
+                        *p = a.accumulate ? *p + acc[ii][j][r] : acc[ii][j][r];
+                    }
+                }
+            }
+        }
+    }
+}
+
 // dw[i] (+)= sum over splits of part[s][i] in ONE launch, for the uncropped case (Cp == Cr,
 // every layer but the RGB stem).  A block covers 256/R float4 columns with R split lanes
 // per column: lane r sums splits r, r+R, ... (four loads in flight), the R lane sums are
@@ -630,8 +849,36 @@ static int g_wgrad_wr = [] {
     return e ? atoi(e) : 2;
 }();
 
+// weight-gradient main loop: 0 = k_conv_wgrad4 (two buffers, vmcnt(0) drain per step),
+// 1 = k_conv_wgrad_ring<.., 32, 4> (four-deep ring of 32-pixel steps, counted vmcnt, raw barrier)
+static int g_wgrad_ring = [] {
+    const char* e = getenv("GM_WGRAD_RING");
+    return e ? atoi(e) : 0;
+}();
+
+template <int MT, int NT>
+static int launch_wgrad_ring(WgradArgs a, int grid, hipStream_t st) {
+    constexpr int BK = 32, NS = 4;
+    const size_t lds = (size_t)NS * BK * 2 * (64 * MT + 64 * NT);
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_conv_wgrad_ring<MT, NT, BK, NS>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr = true;
+    }
+    a.adv_b = BK / (a.P * a.Q);
+    a.adv_p = (BK % (a.P * a.Q)) / a.Q;
+    a.adv_q = (BK % (a.P * a.Q)) % a.Q;
+    k_conv_wgrad_ring<MT, NT, BK, NS><<<grid, 256, lds, st>>>(a);
+    return check_launch("k_conv_wgrad_ring");
+}
+
 template <int MT, int NT>
 static int launch_wgrad4(const WgradArgs& a, int grid, hipStream_t st) {
+    if constexpr (MT <= 2 && NT <= 2) {
+        if (g_wgrad_ring == 1 && !(g_wgrad_wr == 1 || (g_wgrad_wr == 2 && a.T == 1)))
+            return launch_wgrad_ring<MT, NT>(a, grid, st);
+    }
     const size_t lds = (size_t)2 * 64 * 2 * (64 * MT + 64 * NT);
     static bool attr = false;  // idempotent, safe to race
     if (!attr) {
@@ -770,6 +1017,12 @@ extern "C" int gm_conv_set_wgrad_staging(int wr) {
     GM_REQUIRE(wr >= 0 && wr <= 2,
                "gm_conv_set_wgrad_staging: 0 (LDS-DMA), 1 (register-staged), 2 (register-staged for 1x1 filters)");
     g_wgrad_wr = wr;
+    return GM_OK;
+}
+
+extern "C" int gm_conv_set_wgrad_ring(int mode) {
+    GM_REQUIRE(mode == 0 || mode == 1, "gm_conv_set_wgrad_ring: 0 (two-buffer drain) or 1 (4-deep ring)");
+    g_wgrad_ring = mode;
     return GM_OK;
 }
 

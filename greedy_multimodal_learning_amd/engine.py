@@ -44,6 +44,27 @@ from .vtrunk import drop_pending_wgrads
 
 _DEBUG_BUCKETS = os.environ.get("GM_DEBUG_BUCKETS", "0") == "1"
 
+# RCCL channels bound = CUs reserved for RCCL's kernels beside the spin hand-off kernels.
+RCCL_CHANNELS_DEFAULT = 64
+
+
+def bound_rccl_channels():
+    """Bound RCCL's channel count (NCCL_MAX_NCHANNELS) before any communicator of this
+    process exists, unless the user set it: an RCCL collective kernel runs one workgroup
+    per channel, so the bound is exactly the number of CUs its kernels can hold while they
+    overlap backward.  RCCL reads the variable at communicator creation; bench.py calls
+    this before init_process_group, the engine again before it creates its own group.
+    Returns the bound."""
+    return int(os.environ.setdefault("NCCL_MAX_NCHANNELS", str(RCCL_CHANNELS_DEFAULT)))
+
+
+def rccl_reserved_cus():
+    """CUs the residency plan keeps free for RCCL: the channel bound (NCCL_MAX_NCHANNELS),
+    or GM_RCCL_RESERVED_CUS when the operator overrides it."""
+    if "GM_RCCL_RESERVED_CUS" in os.environ:
+        return int(os.environ["GM_RCCL_RESERVED_CUS"])
+    return bound_rccl_channels()
+
 
 class _Flags:
     """Holds the curation flags like the reference's Model_ (src/framework.py:137-138)."""
@@ -282,6 +303,7 @@ class BalancedStep:
             self.graph_collectives = (backend == "nccl"
                                       and os.environ.get("GM_DP_GRAPH_COLLECTIVES", "1") != "0")
             if self.graph_collectives:
+                bound_rccl_channels()
                 # the captured all-reduces run on a process group of their own that never
                 # issues an eager collective: its communicator is initialised here (device_id:
                 # eager connect, no work item), so the group's watchdog never holds an event
@@ -336,8 +358,8 @@ class BalancedStep:
         workgroups wait on each other (single-launch BatchNorm, split-K turnstile) size
         their grids for the trunk streams that run at once, the ranks sharing this GPU
         (found by exchanging (host, device) over the step's group) and, under RCCL data
-        parallelism, the CUs the all-reduce kernels hold while they overlap backward
-        (GM_RCCL_RESERVED_CUS, default 64: RCCL's channel blocks, one CU each at most)."""
+        parallelism, the CUs the all-reduce kernels hold while they overlap backward:
+        RCCL's channel bound (rccl_reserved_cus: one workgroup per channel)."""
         from . import _lib as L
         views = int(getattr(model, "num_views", 2))
         streams = views if streams_enabled() else 1
@@ -359,7 +381,7 @@ class BalancedStep:
             dist.all_gather_object(who, (me[0], str(me[1])), group=self.pg)
             sharers = sum(1 for w in who if w == (me[0], str(me[1])))
         if self.buckets is not None and dist.get_backend(self.pg) == "nccl":
-            reserved = int(os.environ.get("GM_RCCL_RESERVED_CUS", "64"))
+            reserved = rccl_reserved_cus()
         self.residency = L.set_residency(streams=max(1, streams), sharers=max(1, sharers), reserved_cus=reserved)
 
     # ---------------- on-device gate ----------------
@@ -473,6 +495,11 @@ class BalancedStep:
         self._slots = {(x.data_ptr(), y.data_ptr()): (x, y) for x, y in pairs}
 
     def _slot_of(self, x, y):
+        # data parallel: no bound slots, so the graph-cache key (curation setting, lr) is the
+        # same on every rank - a rank that captures (with its collective agreement) while
+        # another replays would hang; the lr is rank-identical (one schedule on every rank)
+        if self.world > 1:
+            return None
         slot = self._slots.get((x.data_ptr(), y.data_ptr())) if self._slots else None
         if slot is None or slot[0].shape != x.shape or slot[0].stride() != x.stride() or slot[0].dtype != x.dtype \
                 or slot[1].shape != y.shape or slot[1].dtype != y.dtype:
@@ -532,6 +559,9 @@ class BalancedStep:
             key = (self._graph_key(), None if slot is None else (x.data_ptr(), y.data_ptr()))
             entry, err = self._graphs.get(key), None
             if entry is None:
+                # a learning-rate change (ReduceLROnPlateau) makes the old-lr graphs dead weight
+                for k in [k for k in self._graphs if k[0][-1] != self.lr]:
+                    del self._graphs[k]
                 try:
                     entry = self._capture(key, slot)
                 except RuntimeError as e:  # capture refused on this system

@@ -20,6 +20,10 @@ The loop keeps the reference's per-epoch history keys (`loss`, `acc`,
 `model_best_val.pt` / `model_last_epoch.pt` hold `{'model', 'optimizer'}` state dicts
 (src/training_loop.py:26-48, 78-83).
 
+Arithmetic: `training_loop.compute_dtype` defaults to 'fp32', the reference's own precision,
+so a reference gin config reproduces the reference's logits and CUR numbers (north_star:
+1e-4); bind `training_loop.compute_dtype = 'bf16'` for the fast (benchmarked) trunk.
+
 CLI (reference: `train.py save_path configs/x.gin [bindings]`, src/utils.py:58-68):
     python -m greedy_multimodal_learning_amd.train SAVE_PATH CONFIG[#CONFIG...] [BINDINGS]
 """
@@ -31,6 +35,7 @@ import pickle
 import numpy as np
 import torch
 
+from . import _lib as L
 from . import callbacks as avail_callbacks
 from .gin_lite import _CONFIG, configurable, parse_config_files_and_bindings
 from .losses import acc, blend_loss  # noqa: F401  (reference train.py exports both)
@@ -108,7 +113,7 @@ def save_history(H, save_path, save_with_structure=True):
 def training_loop(model, loss_function, metrics, optimizer, config, save_path, steps_per_epoch, train=None,
                   valid=None, test=None, test_steps=None, validation_steps=None, use_gpu=True, device_numbers=[0],
                   custom_callbacks=[], checkpoint_monitor="val_acc", n_epochs=100, verbose=True, nummodalities=2,
-                  compute_dtype="bf16", graphs=True):
+                  compute_dtype="fp32", graphs=True):
     """Reference src/training_loop.py:86-143 + Model_.train_loop (src/framework.py:
     250-330) on the fused engine.  `optimizer` is the (lr, momentum, wd) triple of the
     reference's SGD (only momentum = wd = 0, as every config uses, is fused; a torch SGD
@@ -158,38 +163,57 @@ def training_loop(model, loss_function, metrics, optimizer, config, save_path, s
         step.on_epoch_begin(epoch)
         for c in others:
             c.on_epoch_begin(epoch, {})
-        n, loss_sum, acc_sum, accm_sum = 0, 0.0, 0.0, np.zeros(nummodalities)
-        idxs, d_bdr, cur, caring = [], [], [], []
+        # Per-step numbers stay on the device and are read once per epoch (no host sync per
+        # step): loss / accuracy sums as device scalars, the device gate's state snapshotted
+        # per step.  A callback that overrides on_batch_end gets its batch_logs every step
+        # (the only case that reads them), at the cost of that sync.
+        per_batch = [c for c in others if type(c).on_batch_end is not avail_callbacks.Callback.on_batch_end]
+        n = 0
+        loss_sum = torch.zeros((), device=dev, dtype=torch.float64)
+        acc_sum = torch.zeros((), device=dev, dtype=torch.float64)
+        accm_sum = torch.zeros(nummodalities, device=dev, dtype=torch.float64)
+        idxs, d_bdr, cur, caring, snaps = [], [], [], [], []
         for bi, (idx, x, y) in enumerate(train):
             if steps_per_epoch is not None and bi >= steps_per_epoch:
                 break
             for c in others:
                 c.on_batch_begin(bi + 1, {})
             step.lr = float(opt.param_groups[0]["lr"])
-            loss = float(step(x, y))
+            loss = step(x, y)
             outs = step.last_outs
             with torch.no_grad():  # Model_._compute_loss_and_metrics (src/framework.py:152-156)
-                a = float(acc(list(outs), y))
-                am = [float(acc(o, y)) for o in outs]
+                a = acc(list(outs), y)
+                am = torch.stack([acc(o, y) for o in outs])
             b = len(y)
-            loss_sum += loss * b
-            acc_sum += a * b
-            accm_sum += np.array(am) * b
+            loss_sum += loss.double() * b
+            acc_sum += a.double() * b
+            accm_sum += am.double() * b
             n += b
             idxs.append(idx.numpy())
             if gate is not None:
-                st = step.sync_gate() if step.device_gate else None
-                d_bdr.append(float(st["d_BDR"] if st else getattr(gate, "d_BDR", 0.0) or 0.0))
-                cur.append(bool(step.flags.curation_mode))
-                caring.append(step.flags.caring_modality)
-            batch_logs = {"batch": bi + 1, "size": b, "loss": loss, "acc": a,
-                          **{f"acc_modal_{i}": v for i, v in enumerate(am)}}
-            for c in others:
-                c.on_batch_end(bi + 1, batch_logs)
-            if math.isnan(loss):
-                flags.stop_training = True
-        logs = {"epoch": epoch, "loss": loss_sum / max(n, 1), "acc": acc_sum / max(n, 1),
-                **{f"acc_modal_{i}": v / max(n, 1) for i, v in enumerate(accm_sum)},
+                if step.device_gate:
+                    snaps.append(step.gate_state.clone())
+                else:  # host gate: its decision is already on the host
+                    d_bdr.append(float(getattr(gate, "d_BDR", 0.0) or 0.0))
+                    cur.append(bool(step.flags.curation_mode))
+                    caring.append(step.flags.caring_modality)
+            if per_batch:
+                batch_logs = {"batch": bi + 1, "size": b, "loss": float(loss), "acc": float(a),
+                              **{f"acc_modal_{i}": float(v) for i, v in enumerate(am)}}
+                for c in per_batch:
+                    c.on_batch_end(bi + 1, batch_logs)
+        if snaps:  # decode the device gate's per-step states (one copy)
+            cls = L.GateStateN if step.gate_n else L.GateState
+            for raw in torch.stack(snaps).cpu().numpy():
+                st = cls.from_buffer_copy(raw.tobytes())
+                d_bdr.append(float(st.d_bdr))
+                cur.append(bool(st.curation_mode))
+                caring.append(None if st.caring < 0 else int(st.caring))
+        loss_mean = float(loss_sum) / max(n, 1)
+        if math.isnan(loss_mean):  # a NaN step loss ends training after this epoch (:321-322)
+            flags.stop_training = True
+        logs = {"epoch": epoch, "loss": loss_mean, "acc": float(acc_sum) / max(n, 1),
+                **{f"acc_modal_{i}": float(v) / max(n, 1) for i, v in enumerate(accm_sum.cpu())},
                 "train_indices": np.concatenate(idxs) if idxs else np.zeros(0, np.int64)}
         if gate is not None:
             logs.update({"d_BDR": d_bdr, "curation_mode": cur, "caring_modality": caring})
@@ -203,6 +227,11 @@ def training_loop(model, loss_function, metrics, optimizer, config, save_path, s
             logs.update(evaluate(model, test, "test", cdt, test_steps, curation=fl))
         for k, v in logs.items():
             H.setdefault(k, []).append(v)
+        # the reference's callback order: the custom callbacks (ReduceLROnPlateau_PyTorch,
+        # CompletedStopping) before the default checkpoint callbacks (src/training_loop.py:98-110),
+        # so a checkpoint carries the optimizer state after this epoch's learning-rate change
+        for c in others:
+            c.on_epoch_end(epoch, logs)
         if save_path:
             save_history(H, save_path)
             ck = {"model": model.state_dict(), "optimizer": opt.state_dict()}
@@ -214,8 +243,6 @@ def training_loop(model, loss_function, metrics, optimizer, config, save_path, s
         if verbose:
             print(f"epoch {epoch}: loss {logs['loss']:.4f} acc {logs['acc']:.2f} lr {step.lr:g}" +
                   (f" val_acc {logs['val_acc']:.2f}" if "val_acc" in logs else ""), flush=True)
-        for c in others:
-            c.on_epoch_end(epoch, logs)
         if flags.stop_training:
             break
     for c in others:
@@ -229,7 +256,7 @@ def train(save_path, wd, lr, momentum, batch_size, callbacks=[]):
     from .dataset import get_mvdcndata
     from .model import MMTM_MVCNN
     model = MMTM_MVCNN()
-    dt = _DTYPES[_CONFIG.get(("", "training_loop"), {}).get("compute_dtype", "bf16")]
+    dt = _DTYPES[_CONFIG.get(("", "training_loop"), {}).get("compute_dtype", "fp32")]
     train_l, valid_l, test_l = get_mvdcndata(batch_size=batch_size, out_layout="views_nhwc", dtype=dt)
     return training_loop(model=model, loss_function=blend_loss, metrics=[acc], optimizer=(lr, momentum, wd),
                          config=_CONFIG, save_path=save_path, steps_per_epoch=len(train_l), train=train_l,

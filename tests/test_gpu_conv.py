@@ -396,3 +396,49 @@ def test_wgrad_staging_forms_bit_identical(dev, shape):
     finally:
         L.check(lib.gm_conv_set_wgrad_staging(2), "wgrad staging")  # the default
     assert torch.equal(grads[0], grads[1])
+
+
+@pytest.mark.parametrize("shape", [(8, 64, 56, 56, 64, 3, 1, 1), (3, 64, 56, 56, 128, 3, 2, 1),
+                                   (8, 128, 28, 28, 128, 3, 1, 1), (5, 256, 14, 14, 256, 3, 1, 1),
+                                   (64, 512, 7, 7, 512, 3, 1, 1), (7, 256, 14, 14, 512, 1, 2, 0),
+                                   (2, 8, 115, 115, 64, 7, 1, 0)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_wgrad_ring_bit_identical(dev, shape):
+    """k_conv_wgrad_ring (4-deep LDS-DMA ring of 32-pixel steps, counted vmcnt) stages the
+    same LDS image and issues the same MFMAs in the same pixel order as k_conv_wgrad4:
+    bit-identical weight gradients, grouped over two views, split-K and ragged tails
+    included (B = 3, 5, 7)."""
+    import ctypes
+    from greedy_multimodal_learning_amd import _lib as L
+    from greedy_multimodal_learning_amd import conv as CV
+    N, C, H, W, K, R, st, pad = shape
+    G = 2
+    P, Q = (H + 2 * pad - R) // st + 1, (W + 2 * pad - R) // st + 1
+    torch.manual_seed(sum(shape))
+    x = torch.randn(G * N, H, W, C, device=dev).bfloat16()
+    dy = torch.randn(G * N, P, Q, K, device=dev).bfloat16()
+    lib = L.load()
+    d = CV._desc_hw(N, H, W, C, K, R, R, st, st, pad, pad)
+    need = lib.gm_conv2d_wgrad_grouped_scratch(ctypes.byref(d), G)
+    scr = torch.empty(max(need, 16), device=dev, dtype=torch.uint8)
+    outs = []
+    try:
+        for ring in (0, 1):
+            L.check(lib.gm_conv_set_wgrad_ring(ring), "ring")
+            for acc in (0, 1):
+                dw = torch.full((G, K, R, R, C), 0.25, device=dev, dtype=torch.float32)
+                L.check(lib.gm_conv2d_wgrad_grouped_bf16(ctypes.byref(d), G, dy.data_ptr(), x.data_ptr(),
+                                                          dw.data_ptr(), K * R * R * C, C, acc, scr.data_ptr(),
+                                                          need, L.stream_of(dev)), "wgrad")
+                outs.append(dw)
+        torch.cuda.synchronize()
+    finally:
+        L.check(lib.gm_conv_set_wgrad_ring(0), "ring")
+    assert torch.equal(outs[0], outs[2]) and torch.equal(outs[1], outs[3])
+    # and it is a weight gradient: group 0 against fp32 PyTorch
+    xr = x[:N].float().permute(0, 3, 1, 2)
+    gr = dy[:N].float().permute(0, 3, 1, 2)
+    ref = torch.nn.grad.conv2d_weight(xr, (K, C, R, R), gr, stride=st, padding=pad)
+    got = outs[0][0].permute(0, 3, 1, 2)
+    err = float((got - ref).abs().max() / ref.abs().max())
+    assert err < 2e-3, err

@@ -1,0 +1,122 @@
+"""Decision-level parity of the benchmarked bf16 gate with every outcome exercised
+(VERDICT r03 missing #5 / next #3): the C2 step (B = 64 two-view 224x224 objects, bf16
+trunk, hipGraph replay, on-device gate, lr 0.1, epsilon 0.01) against the fp32 oracle of
+the reference step (/root/reference/src/callbacks.py:199-263, src/model.py:63-108,
+train.py:23-29), teacher-forced AND steered:
+
+before every deciding step the oracle runs the reference forward/backward from the HIP
+run's current fp32 master weights on the same bf16-rounded batch; from its group sums the
+test picks M accumulators (written into the device gate state and the oracle alike) that
+put the oracle's d_BDR on a target taken from a schedule crossing epsilon in both signs -
+so the trace holds no-curation, caring-0 and caring-1 decisions, most of them far enough
+from +-epsilon to be judged.  The HIP step then adds its OWN bf16 group sums to the same M
+and decides on the device.  Steered M sits in one bypass accumulator only (the main
+accumulators stay 0), so the main-branch gradient sums of both views enter d_BDR with
+their full bf16 error.
+
+BAND is the bf16-vs-fp32 d_BDR noise the decisions are judged with: a step whose oracle
+|d_BDR| lies within BAND of epsilon may legitimately decide either way; every other step
+must decide identically (curate or not, and which modality).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+B, H, EPS, WINDOW, LR = 64, 224, 0.01, 2, 0.1
+BAND = 3e-3
+# oracle d_BDR targets (cycled): both signs, inside and outside epsilon, a few near it
+TARGETS = [0.030, -0.030, 0.004, -0.004, 0.020, -0.020, 0.0, 0.016, -0.016, -0.0045, 0.0045, 0.025,
+           -0.025, 0.0115, -0.0085, 0.002, -0.002, 0.018, -0.018, 0.0, 0.035, -0.035, 0.005, -0.005]
+MIN_DECIDING = 22
+
+
+def _steer(r, target):
+    """M = (bypass0, bypass1, main0, main1) with main = 0 such that
+    log10((Mb0 + rb0) / rm0) - log10((Mb1 + rb1) / rm1) == target."""
+    rb0, rb1, rm0, rm1 = r
+    base = math.log10(rb0 / rm0) - math.log10(rb1 / rm1)
+    if target >= base:
+        return [rm0 * (rb1 / rm1) * 10.0 ** target - rb0, 0.0, 0.0, 0.0]
+    return [0.0, rm1 * (rb0 / rm0) * 10.0 ** (-target) - rb1, 0.0, 0.0]
+
+
+@pytest.fixture(scope="module")
+def trace():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from greedy_multimodal_learning_amd.callbacks import Bias_Mitigation_Strong
+    from greedy_multimodal_learning_amd.engine import BalancedStep
+    from greedy_multimodal_learning_amd.model import MMTM_MVCNN
+    from oracle import gating_ref, model_ref, weights
+    dev = torch.device("cuda:0")
+    torch.set_num_threads(max(1, min(32, torch.get_num_threads())))
+    model = weights.apply_to_module(MMTM_MVCNN(), seed=5).to(dev)
+    gate = Bias_Mitigation_Strong(epsilon=EPS, curation_windowsize=WINDOW, branchnames=["net_view_0", "net_view_1"],
+                                  starting_epoch=1)
+    step = BalancedStep(model, lr=LR, gate=gate, graphs=True)
+    step.on_epoch_begin(1)
+    assert step.device_gate and step.graphs
+    g = torch.Generator().manual_seed(91)
+    batches = []
+    for _ in range(4):
+        buf = torch.randn(2, B, H, H, 3, generator=g).bfloat16()
+        batches.append((buf, torch.randint(0, 40, (B,), generator=g)))
+    dbat = [(b.to(dev).permute(1, 0, 4, 2, 3), y.to(dev)) for b, y in batches]
+    oracle = model_ref.MMTM_MVCNN_Ref()
+    rows, t, k = [], 0, 0
+    while len(rows) < MIN_DECIDING:
+        st = step.sync_gate()
+        x, y = dbat[t % 4]
+        if st["curation_mode"]:  # inside a curation window: no decision this step
+            step(x, y)
+            t += 1
+            continue
+        oracle.load_state_dict({n: p.detach().float().contiguous().cpu() for n, p in model.named_parameters()},
+                               strict=False)
+        oracle.zero_grad(set_to_none=True)
+        oracle.train(True)
+        buf, yc = batches[t % 4]
+        _, outs, _, _ = oracle(buf.float().permute(1, 0, 4, 2, 3).contiguous())
+        gating_ref.blend_loss(outs, yc).backward()
+        s = gating_ref.group_sums([(n, p, p.grad) for n, p in oracle.named_parameters()])
+        r = [s["gn_bypass"][0] / s["wn_bypass"][0], s["gn_bypass"][1] / s["wn_bypass"][1],
+             s["gn_main"][0] / s["wn_main"][0], s["gn_main"][1] / s["wn_main"][1]]
+        M = _steer(r, TARGETS[k % len(TARGETS)])
+        k += 1
+        gs = step.gate_struct()
+        for i in range(4):
+            gs.M[i] = M[i]
+        step.set_gate_struct(gs)
+        bdr = gating_ref.BDRState(EPS, WINDOW)
+        bdr.M_bypass, bdr.M_main = [M[0], M[1]], [M[2], M[3]]
+        d_o = float(bdr.update(s))
+        step(x, y)
+        t += 1
+        after = step.sync_gate()
+        dec_o = (abs(d_o) > EPS, (1 if d_o < 0 else 0) if abs(d_o) > EPS else 0)
+        dec_h = (bool(after["curation_mode"]), after["caring_modality"] if after["curation_mode"] else 0)
+        rows.append((t - 1, after["d_BDR"], d_o, dec_h, dec_o))
+        print(f"step {t - 1:2d}: target {TARGETS[(k - 1) % len(TARGETS)]:+.4f} d_BDR hip {after['d_BDR']:+.5f} "
+              f"oracle {d_o:+.5f} |diff| {abs(after['d_BDR'] - d_o):.2e} decision hip {dec_h} oracle {dec_o}",
+              flush=True)
+    return rows
+
+
+def test_steered_gate_decisions_vs_oracle(trace):
+    rows = trace
+    diff = np.array([abs(r[1] - r[2]) for r in rows])
+    print(f"d_BDR |hip - oracle| over {len(rows)} deciding steps: median {np.median(diff):.2e} "
+          f"p90 {np.percentile(diff, 90):.2e} max {diff.max():.2e}")
+    assert diff.max() < BAND, "bf16 d_BDR noise above the band the decisions are judged with"
+    clear = [r for r in rows if abs(abs(r[2]) - EPS) > BAND]
+    assert len(clear) >= len(rows) // 2, (len(clear), len(rows))
+    outcomes = {r[4] for r in clear}
+    assert {(False, 0), (True, 0), (True, 1)} <= outcomes, outcomes
+    for t, dh, do, dec_h, dec_o in clear:
+        assert dec_h == dec_o, (t, dh, do, dec_h, dec_o)
+    agree = sum(r[3] == r[4] for r in rows)
+    print(f"decisions identical on {agree}/{len(rows)} deciding steps ({len(clear)} outside the band)")

@@ -190,6 +190,8 @@ def test_four_view_engine_step_with_n_branch_gate(dev):
     y = torch.randint(0, 40, (4,), device=dev)
     loss = step(x, y)
     assert torch.isfinite(loss)
+    assert step.device_gate and step.gate_n  # the N-branch on-device gate (gm_gate_state_n)
+    step.sync_gate()  # the host mirrors (gate.BDR, flags) are filled on request
     bdr = list(gate.BDR)
     assert len(bdr) == 4 and all(np.isfinite(bdr))
     # epsilon 1e-6: the first decision curates, caring for the argmax-BDR branch

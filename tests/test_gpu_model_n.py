@@ -73,7 +73,7 @@ def test_n_view_model_vs_oracle(trunk, V, B, H, caring):
 @pytest.mark.parametrize("trunk,V,B", [("resnet18", 4, 8), ("resnet50", 12, 2)], ids=["c4", "c5"])
 def test_engine_bf16_step_vs_oracle(trunk, V, B):
     """The benchmarked C4 / C5 steps (4 ResNet-18 / 12 ResNet-50 branches, bf16 trunk,
-    hipGraphs, N-branch host gate) at 224x224: the step's loss, and the per-branch logits
+    hipGraphs, N-branch on-device gate) at 224x224: the step's loss, and the per-branch logits
     of the same model's bf16 forward, against the fp32 oracle on the same bf16-rounded
     inputs and weights (bf16 tolerance: 3e-2 of the loss / of the logit scale)."""
     from greedy_multimodal_learning_amd.callbacks import Bias_Mitigation_Strong
@@ -120,4 +120,7 @@ def test_engine_bf16_step_vs_oracle(trunk, V, B):
     losses = [float(step(xd, yd)) for _ in range(3)]  # lr 0: every step sees the same weights
     assert losses[0] == losses[1] == losses[2] or max(losses) - min(losses) < 1e-3 * abs(ref)
     assert abs(losses[-1] - ref) <= 3e-2 * abs(ref), (losses, ref)
+    assert step.device_gate and step.gate_n  # the N-branch on-device gate
+    st = step.sync_gate()
     assert np.isfinite(gate.BDR).all() and len(gate.BDR) == V
+    assert not st["curation_mode"] and st["n_curated"] == 0

@@ -220,6 +220,13 @@ def test_model_stacked_vs_per_view(dev, kind):
         ea, eb = float((ga - gc).norm() / den), float((gb - gc).norm() / den)
         worst.append((ea, eb, n))
         assert ea < max(2 * eb, 3e-2), f"{n}: stacked {ea:.3e} vs per-view {eb:.3e} (relative to fp32)"
+        # a dropped, zeroed or misrouted gradient cannot hide behind a noisy per-view path:
+        # the stacked gradient keeps the fp32 gradient's size and direction
+        ratio = float(ga.norm() / den)
+        cos_a = float((ga * gc).sum() / (ga.norm() * den + 1e-30))
+        cos_b = float((gb * gc).sum() / (gb.norm() * den + 1e-30))
+        assert 0.5 < ratio < 2.0, f"{n}: stacked gradient norm {ratio:.3f} x the fp32 one"
+        assert cos_a > min(0.5, cos_b - 0.2), f"{n}: cosine to fp32 {cos_a:.3f} (per-view {cos_b:.3f})"
     worst.sort(reverse=True)
     print("stacked vs per-view gradient error vs fp32 (worst 5):",
           ", ".join(f"{n} {ea:.2e}/{eb:.2e}" for ea, eb, n in worst[:5]))
