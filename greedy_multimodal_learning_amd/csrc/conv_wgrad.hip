@@ -697,6 +697,167 @@ __global__ __launch_bounds__(256) void k_conv_wgrad_ring(WgradArgs a) {
     }
 }
 
+// k_wgrad_halo64: weight gradient of the ResNet layer-1 convolution (3x3, stride 1, pad 1,
+// C = K = 64, W <= 62), the whole 64 x (9 taps x 64) gradient of a view group held in the
+// accumulators of one workgroup (wave (kh, ch): output channels 32 kh .., input channels
+// 32 ch .., all nine taps = 9 x 32x32 accumulators) while it walks a contiguous range of
+// output rows.  Per output row only that row's dy (64 pixel rows of 128 B, pixels >= W zero)
+// and ONE new input row (the x ring holds rows r-1, r, r+1 of the current output row r plus
+// the prefetched ones) are staged: 16 KB per 36 MFMAs per wave, against 24 KB per 8 MFMAs
+// per wave of k_conv_wgrad4's 64 x 128 tiles, whose B operand re-stages every input pixel
+// once per tap.  The nine taps read the same ring row at a pixel shift s (and ring rows
+// r-1 .. r+1 for the kernel rows): x halo pixel j = input column j - 1, so output pixel q,
+// tap (rr, s) reads halo pixel q + s of input row p + rr - 1 (a zero row outside the image).
+// Both operands go through the ds_read_b64_tr_b16 transposed reads of k_conv_wgrad4 (rows
+// of 128 B, chunk XOR 4 * ((row >> 1) & 1): conflict-free for any 4 consecutive rows, so a
+// tap shift keeps the reads conflict-free).  Rows stream D = 2 ahead through LDS-DMA with
+// counted vmcnt waits and raw barriers.  Each workgroup writes its fp32 partial slab
+// [64][9 x 64] (split-K over rows; k_wgrad_sum reduces them in a fixed order).
+struct WHaloArgs {
+    const uint16_t* dy;  // [G][N*P][Q][64]  (P = H, Q = W)
+    const uint16_t* x;   // [G][N*H][W][64]
+    float* part;         // [G][splits][64][9*64]
+    int N, H, W, rows, splits, rpw;  // rows = N*H per group, rpw = rows per workgroup
+    long long gs;        // group stride of dy / x (elements): N*H*W*64
+};
+
+template <int D>
+__global__ __launch_bounds__(256) void k_wgrad_halo64(WHaloArgs a) {
+    constexpr int XS = D + 3, DS = D + 1;  // x ring (rows r-1 .. r+1 + D ahead), dy ring
+    constexpr int SL = 8192;               // one staged row: 64 pixels x 128 B
+    constexpr int OX = 0, OZ = XS * SL, OD = OZ + SL + 1024;  // x ring | zero row (+ pad) | dy ring
+    extern __shared__ __attribute__((aligned(16))) uint4 wsm[];
+    char* lds = reinterpret_cast<char*>(wsm);
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int kh = wave & 1, ch = wave >> 1;
+    const int grp = blockIdx.x / a.splits, split = blockIdx.x - grp * a.splits;
+    const uint16_t* __restrict__ gdy = a.dy + grp * a.gs;
+    const uint16_t* __restrict__ gx = a.x + grp * a.gs;
+    const int r0 = split * a.rpw;
+    const int r1 = min(a.rows, r0 + a.rpw);
+    // the zero row (+ 1 KB pad: tap reads run two pixels past a row)
+    for (int i = t; i < (SL + 1024) / 16; i += 256) *reinterpret_cast<uint4*>(lds + OZ + i * 16) = make_uint4(0, 0, 0, 0);
+
+    typedef __attribute__((address_space(1))) const void* gptr_t;
+    typedef __attribute__((address_space(3))) void* lptr_t;
+    const void* zero = (const void*)g_wzero16;
+    // DMA lanes: piece I = 2 wave + j (j = 0, 1) covers pixel rows 8 I .. 8 I + 7; lane -> pixel
+    // 8 I + lane / 8, source chunk (lane % 8) ^ swizzle(pixel)
+    int px[2], soff[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        px[j] = (2 * wave + j) * 8 + (lane >> 3);
+        soff[j] = (((lane & 7) ^ wswz<128>(px[j])) << 3);
+    }
+    auto issue = [&](int r) __attribute__((always_inline)) {  // dy row r and x row r + 1 (ring slots)
+        const int ds = r % DS, xs = (r + 1) % XS;
+        const bool dok = r < r1, xok = r + 1 < a.rows;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const void* src = (dok && px[j] < a.W) ? (const void*)(gdy + ((size_t)r * a.W + px[j]) * 64 + soff[j]) : zero;
+            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + OD + ds * SL + (2 * wave + j) * 1024), 16, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int col = px[j] - 1;
+            const bool ok = xok && col >= 0 && col < a.W;
+            const void* src = ok ? (const void*)(gx + ((size_t)(r + 1) * a.W + col) * 64 + soff[j]) : zero;
+            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + OX + xs * SL + (2 * wave + j) * 1024), 16, 0, 0);
+        }
+    };
+    auto issue_x = [&](int f) __attribute__((always_inline)) {  // x row f alone (prologue)
+        const int xs = ((f % XS) + XS) % XS;
+        const bool fok = f >= 0 && f < a.rows;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int col = px[j] - 1;
+            const bool ok = fok && col >= 0 && col < a.W;
+            const void* src = ok ? (const void*)(gx + ((size_t)f * a.W + col) * 64 + soff[j]) : zero;
+            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + OX + xs * SL + (2 * wave + j) * 1024), 16, 0, 0);
+        }
+    };
+
+    floatx16 acc[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+    // tr-read lane geometry (k_conv_wgrad4's): half-wave g >> 1 reads rows 8 (g >> 1) + q4 (+4) of
+    // a 16-row slice, 4-column block p4 of the 32-column fragment, 16-column half g & 1
+    const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+    const int rbase = 8 * (g >> 1) + q4;
+    const int acol = kh * 32 + 16 * (g & 1) + 4 * p4;
+    const int bcol = ch * 32 + 16 * (g & 1) + 4 * p4;
+    const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
+    auto rowoff = [](int row, int col) { return (unsigned)(row * 128 + ((((col >> 3) ^ wswz<128>(row))) << 4) + (col & 7) * 2); };
+    const unsigned a_lane = rowoff(rbase, acol);
+    unsigned b_lane[3];
+#pragma unroll
+    for (int s = 0; s < 3; ++s) b_lane[s] = rowoff(rbase + s, bcol);
+    const int nks = (a.W + 15) >> 4;  // 16-pixel k-slices of a row
+
+    // prologue: x rows r0 - 1, r0, then D steps of (dy r, x r + 1)
+    if (r0 < r1) {
+        issue_x(r0 - 1);
+        issue_x(r0);
+        for (int i = 0; i < D; ++i) issue(r0 + i);
+    }
+    for (int r = r0; r < r1; ++r) {
+        // row r's pieces landed (the D - 1 later steps' 4 pieces per wave may stay in flight),
+        // and after the barrier every wave's have, and every wave is done with row r - 1 -
+        // whose dy slot and oldest x slot the next issue refills
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (D - 1)) : "memory");
+        __builtin_amdgcn_s_barrier();
+        issue(r + D);  // uniform count: past the range it loads zeros
+        const int p = r % a.H;
+        const unsigned abase = lds0 + OD + (r % DS) * SL + a_lane;
+        unsigned xb[3];  // kernel row rr: input row p + rr - 1 (zero row outside the image)
+#pragma unroll
+        for (int rr = 0; rr < 3; ++rr) {
+            const int h = p + rr - 1;
+            xb[rr] = lds0 + ((h < 0 || h >= a.H) ? (unsigned)OZ : (unsigned)(OX + ((r + rr - 1 + XS) % XS) * SL));
+        }
+        unsigned bb[9];
+#pragma unroll
+        for (int tp = 0; tp < 9; ++tp) bb[tp] = xb[tp / 3] + b_lane[tp % 3];
+        for (int ks = 0; ks < nks; ++ks) {
+            const unsigned ko = (unsigned)(ks * 16 * 128);
+            bf16x8 af, bfr[9];
+            {
+                short4_t lo, hi;
+                asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(abase + ko));
+                asm volatile("ds_read_b64_tr_b16 %0, %1 offset:512" : "=v"(hi) : "v"(abase + ko));
+                af = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+            }
+#pragma unroll
+            for (int tp = 0; tp < 9; ++tp) {
+                short4_t lo, hi;
+                asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(bb[tp] + ko));
+                asm volatile("ds_read_b64_tr_b16 %0, %1 offset:512" : "=v"(hi) : "v"(bb[tp] + ko));
+                bfr[tp] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af), "+v"(bfr[0]), "+v"(bfr[1]), "+v"(bfr[2]), "+v"(bfr[3]),
+                         "+v"(bfr[4]), "+v"(bfr[5]), "+v"(bfr[6]), "+v"(bfr[7]), "+v"(bfr[8]));
+#pragma unroll
+            for (int tp = 0; tp < 9; ++tp)
+                acc[tp] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr[tp], acc[tp], 0, 0, 0);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // D[k][c]: col = lane & 31 (c), row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5) (k)
+    float* out = a.part + ((size_t)grp * a.splits + split) * (64 * 576);
+#pragma unroll
+    for (int tp = 0; tp < 9; ++tp) {
+        const int col = tp * 64 + ch * 32 + (lane & 31);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int row = kh * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+            out[(size_t)row * 576 + col] = acc[tp][e];
+        }
+    }
+}
+
 // dw[i] (+)= sum over splits of part[s][i] in ONE launch, for the uncropped case (Cp == Cr,
 // every layer but the RGB stem).  A block covers 256/R float4 columns with R split lanes
 // per column: lane r sums splits r, r+R, ... (four loads in flight), the R lane sums are
@@ -849,10 +1010,12 @@ static int g_wgrad_wr = [] {
     return e ? atoi(e) : 2;
 }();
 
-// weight-gradient main loop: 0 = k_conv_wgrad4 (two buffers, vmcnt(0) drain per step),
-// 1 = k_conv_wgrad_ring<.., 32, 4> (four-deep ring of 32-pixel steps, counted vmcnt, raw barrier)
-static int g_wgrad_ring = [] {
-    const char* e = getenv("GM_WGRAD_RING");
+// weight-gradient main loops (GM_WGRAD_LOOP at load, gm_conv_set_wgrad_loop): bit 0 =
+// k_conv_wgrad_ring<.., 32, 4> (four-deep ring of 32-pixel steps, counted vmcnt, raw barrier)
+// instead of k_conv_wgrad4 (two buffers, vmcnt(0) drain per step); bit 1 = k_wgrad_halo64 for
+// the layer-1 shape (3x3 / s1 / p1, C = K = 64, W <= 62)
+static int g_wgrad_loop = [] {
+    const char* e = getenv("GM_WGRAD_LOOP");
     return e ? atoi(e) : 0;
 }();
 
@@ -876,7 +1039,7 @@ static int launch_wgrad_ring(WgradArgs a, int grid, hipStream_t st) {
 template <int MT, int NT>
 static int launch_wgrad4(const WgradArgs& a, int grid, hipStream_t st) {
     if constexpr (MT <= 2 && NT <= 2) {
-        if (g_wgrad_ring == 1 && !(g_wgrad_wr == 1 || (g_wgrad_wr == 2 && a.T == 1)))
+        if ((g_wgrad_loop & 1) && !(g_wgrad_wr == 1 || (g_wgrad_wr == 2 && a.T == 1)))
             return launch_wgrad_ring<MT, NT>(a, grid, st);
     }
     const size_t lds = (size_t)2 * 64 * 2 * (64 * MT + 64 * NT);
@@ -896,8 +1059,22 @@ static gm_conv_desc_hw to_hw(const gm_conv_desc* d) {
     return gm_conv_desc_hw{d->N, d->H, d->W, d->C, d->K, d->R, d->S, d->stride, d->stride, d->pad, d->pad};
 }
 
+// k_wgrad_halo64 serves the layer-1 shape: splits = workgroups per view group
+static bool halo64_ok(const gm_conv_desc_hw* d) {
+    return (g_wgrad_loop & 2) && d->R == 3 && d->S == 3 && d->stride_h == 1 && d->stride_w == 1 && d->pad_h == 1 &&
+           d->pad_w == 1 && d->C == 64 && d->K == 64 && d->W <= 62 && d->W >= 1 && d->H >= 1 &&
+           (long long)d->N * d->H * d->W * 64 < (1ll << 31);
+}
+static int halo64_splits(const gm_conv_desc_hw* d, int G) {
+    const int rows = d->N * d->H;
+    int sp = 256 / G;
+    if (sp < 1) sp = 1;
+    return sp < rows ? sp : rows;
+}
+
 extern "C" size_t gm_conv2d_wgrad_grouped_scratch(const gm_conv_desc_hw* d, int G) {
     if (!d || d->stride_h < 1 || d->stride_w < 1 || G < 1) return 0;
+    if (halo64_ok(d)) return (size_t)G * halo64_splits(d, G) * 64 * 576 * sizeof(float);
     const WPlan w = plan(d, G);
     const size_t slab = (size_t)d->K * d->R * d->S * d->C;
     return (size_t)G * w.splits * slab * sizeof(float);
@@ -931,6 +1108,43 @@ extern "C" int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, con
                "conv wgrad: group gradient stride %lld overlaps one gradient", dw_stride);
     const size_t need = gm_conv2d_wgrad_grouped_scratch(d, G);
     GM_REQUIRE(scratch && scratch_bytes >= need, "conv wgrad: scratch %zu < %zu", scratch_bytes, need);
+    hipStream_t st0 = as_stream(stream);
+    if (halo64_ok(d) && c_real == 64) {
+        WHaloArgs h;
+        h.dy = (const uint16_t*)dy;
+        h.x = (const uint16_t*)x;
+        h.part = (float*)scratch;
+        h.N = d->N; h.H = d->H; h.W = d->W;
+        h.rows = d->N * d->H;
+        h.splits = halo64_splits(d, G);
+        h.rpw = (h.rows + h.splits - 1) / h.splits;
+        h.gs = (long long)d->N * d->H * d->W * 64;
+        constexpr int D = 2;
+        const size_t lds = (size_t)(D + 3) * 8192 + 8192 + 1024 + (size_t)(D + 1) * 8192;
+        static bool attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute((const void*)k_wgrad_halo64<D>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            attr = true;
+        }
+        k_wgrad_halo64<D><<<h.splits * G, 256, lds, st0>>>(h);
+        int rc = check_launch("k_wgrad_halo64");
+        if (rc) return rc;
+        const size_t slab = (size_t)64 * 576;
+        const size_t ncol = slab / 4;
+        int R = 1;
+        while (R < 32 && R * 2 <= h.splits && (ncol * R + 255) / 256 < 512) R *= 2;
+        const dim3 gg((unsigned)((ncol + 256 / R - 1) / (256 / R)), (unsigned)G);
+        float* part = h.part;
+        switch (R) {
+            case 1: k_wgrad_sum<1><<<gg, 256, 0, st0>>>(part, h.splits, slab, accumulate, dw, dw_stride); break;
+            case 2: k_wgrad_sum<2><<<gg, 256, 0, st0>>>(part, h.splits, slab, accumulate, dw, dw_stride); break;
+            case 4: k_wgrad_sum<4><<<gg, 256, 0, st0>>>(part, h.splits, slab, accumulate, dw, dw_stride); break;
+            case 8: k_wgrad_sum<8><<<gg, 256, 0, st0>>>(part, h.splits, slab, accumulate, dw, dw_stride); break;
+            case 16: k_wgrad_sum<16><<<gg, 256, 0, st0>>>(part, h.splits, slab, accumulate, dw, dw_stride); break;
+            default: k_wgrad_sum<32><<<gg, 256, 0, st0>>>(part, h.splits, slab, accumulate, dw, dw_stride); break;
+        }
+        return check_launch("k_wgrad_sum");
+    }
     WgradArgs a;
     memset(&a, 0, sizeof(a));
     const WPlan w = plan(d, G);
@@ -1020,9 +1234,9 @@ extern "C" int gm_conv_set_wgrad_staging(int wr) {
     return GM_OK;
 }
 
-extern "C" int gm_conv_set_wgrad_ring(int mode) {
-    GM_REQUIRE(mode == 0 || mode == 1, "gm_conv_set_wgrad_ring: 0 (two-buffer drain) or 1 (4-deep ring)");
-    g_wgrad_ring = mode;
+extern "C" int gm_conv_set_wgrad_loop(int mode) {
+    GM_REQUIRE(mode >= 0 && mode <= 3, "gm_conv_set_wgrad_loop: bit 0 ring main loop, bit 1 layer-1 halo kernel");
+    g_wgrad_loop = mode;
     return GM_OK;
 }
 

@@ -375,9 +375,11 @@ int gm_conv_set_splitk(int target);
 /* Weight-gradient tile form (process-wide; GM_WGRAD_WIDE at load): bit 0 takes
  * 256-row tiles for K >= 256, bit 1 256-column (tap, channel) tiles; 0 = 128 x 128. */
 int gm_conv_set_wgrad_wide(int mode);
-/* Weight-gradient main loop (A/B): 0 = two buffers drained per step, 1 = 4-deep LDS-DMA ring of
- * 32-pixel steps with counted vmcnt waits (k_conv_wgrad_ring; bit-identical results). */
-int gm_conv_set_wgrad_ring(int mode);
+/* Weight-gradient main loops (A/B; GM_WGRAD_LOOP at load): bit 0 = 4-deep LDS-DMA ring of
+ * 32-pixel steps with counted vmcnt waits (k_conv_wgrad_ring; bit-identical to the two-buffer
+ * k_conv_wgrad4), bit 1 = k_wgrad_halo64 for the layer-1 shape (3x3 / s1 / p1, 64 -> 64:
+ * whole-gradient accumulators, one new input row staged per output row). */
+int gm_conv_set_wgrad_loop(int mode);
 /* Weight-gradient operand staging: 0 = LDS-DMA pieces, 1 = register-staged (global_load_dwordx4
  * two steps ahead + ds_write_b128; same LDS image and arithmetic), 2 (default) = register-staged
  * for 1x1 filters, LDS-DMA otherwise.  GM_WGRAD_WR at load. */

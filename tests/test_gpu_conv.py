@@ -424,7 +424,7 @@ def test_wgrad_ring_bit_identical(dev, shape):
     outs = []
     try:
         for ring in (0, 1):
-            L.check(lib.gm_conv_set_wgrad_ring(ring), "ring")
+            L.check(lib.gm_conv_set_wgrad_loop(ring), "ring")
             for acc in (0, 1):
                 dw = torch.full((G, K, R, R, C), 0.25, device=dev, dtype=torch.float32)
                 L.check(lib.gm_conv2d_wgrad_grouped_bf16(ctypes.byref(d), G, dy.data_ptr(), x.data_ptr(),
@@ -433,7 +433,7 @@ def test_wgrad_ring_bit_identical(dev, shape):
                 outs.append(dw)
         torch.cuda.synchronize()
     finally:
-        L.check(lib.gm_conv_set_wgrad_ring(0), "ring")
+        L.check(lib.gm_conv_set_wgrad_loop(0), "ring")
     assert torch.equal(outs[0], outs[2]) and torch.equal(outs[1], outs[3])
     # and it is a weight gradient: group 0 against fp32 PyTorch
     xr = x[:N].float().permute(0, 3, 1, 2)
@@ -442,3 +442,88 @@ def test_wgrad_ring_bit_identical(dev, shape):
     got = outs[0][0].permute(0, 3, 1, 2)
     err = float((got - ref).abs().max() / ref.abs().max())
     assert err < 2e-3, err
+
+
+@pytest.mark.parametrize("shape", [(64, 64, 56, 56), (2, 64, 28, 28), (3, 64, 9, 11), (1, 64, 7, 7), (2, 64, 5, 40)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_conv_rw2_bit_identical(dev, shape):
+    """k_conv_rw2 (weights resident in VGPRs, 256-row tiles, four accumulators per wave)
+    issues the same MFMAs in the same k order per output as k_conv_rw: forward, input
+    gradient and the fused gradient join (addend) are bit-identical; also as the two-view
+    grouped launch the view-batched trunk issues."""
+    import ctypes
+    from greedy_multimodal_learning_amd import _lib as L
+    from greedy_multimodal_learning_amd import conv as G
+    lib = L.load()
+    N, C, H, W = shape
+    g = torch.Generator(device="cuda").manual_seed(sum(shape) + 7)
+    CL = torch.channels_last
+    x = torch.randn(2 * N, C, H, W, device=dev, generator=g).bfloat16().contiguous(memory_format=CL)
+    w = (torch.randn(2, C, C, 3, 3, device=dev, generator=g) / (C * 9) ** 0.5).bfloat16()
+    dy = torch.randn(N, C, H, W, device=dev, generator=g).bfloat16().contiguous(memory_format=CL)
+    add = torch.randn(N, C, H, W, device=dev, generator=g).bfloat16().contiguous(memory_format=CL)
+    w0 = w[0].contiguous(memory_format=CL)
+    wt = w0.permute(1, 0, 2, 3).contiguous(memory_format=CL)
+    wg = w.permute(0, 1, 3, 4, 2).contiguous()  # [G][K][R][S][C]
+    d = G._desc_hw(N, H, W, C, C, 3, 3, 1, 1, 1, 1)
+    outs = {}
+    try:
+        for rw in (1, 4):
+            L.check(lib.gm_conv_set_rw(rw), "gm_conv_set_rw")
+            yg = torch.empty(2 * N, C, H, W, device=dev, dtype=torch.bfloat16).contiguous(memory_format=CL)
+            L.check(lib.gm_conv2d_fwd_grouped_bf16(ctypes.byref(d), 2, x.data_ptr(), wg.data_ptr(), C * 9 * C,
+                                                   yg.data_ptr(), 0, 0, L.stream_of(dev)), "grouped fwd")
+            outs[rw] = (G.conv_fwd(x[:N], w0, 1, 1), G.conv_dgrad_t(dy, wt, H, W, 1, 1),
+                        G.conv_dgrad_t(dy, wt, H, W, 1, 1, addend=add), yg)
+        torch.cuda.synchronize()
+    finally:
+        lib.gm_conv_set_rw(1)
+    for name, a_, b_ in zip(("fwd", "dgrad", "dgrad+addend", "grouped fwd"), outs[4], outs[1]):
+        assert torch.equal(a_, b_), name
+
+
+@pytest.mark.parametrize("shape", [(64, 56, 56), (3, 56, 56), (5, 20, 20), (2, 9, 7), (1, 3, 62)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_wgrad_halo64_vs_fp32(dev, shape):
+    """k_wgrad_halo64 (layer-1 weight gradient: the whole 64 x 9 x 64 gradient in one
+    workgroup's accumulators, one input row staged per output row, rows split over the
+    workgroups, slabs summed in a fixed order) against fp32 PyTorch, grouped over two views,
+    plain and accumulating; and against k_conv_wgrad4 within fp32 summation-order noise."""
+    import ctypes
+    from greedy_multimodal_learning_amd import _lib as L
+    from greedy_multimodal_learning_amd import conv as CV
+    N, H, W = shape
+    C = K = 64
+    G = 2
+    torch.manual_seed(N * 1000 + H * 10 + W)
+    x = torch.randn(G * N, H, W, C, device=dev).bfloat16()
+    dy = torch.randn(G * N, H, W, K, device=dev).bfloat16()
+    lib = L.load()
+    d = CV._desc_hw(N, H, W, C, K, 3, 3, 1, 1, 1, 1)
+    outs = {}
+    try:
+        for mode in (0, 2):
+            L.check(lib.gm_conv_set_wgrad_loop(mode), "loop")
+            need = lib.gm_conv2d_wgrad_grouped_scratch(ctypes.byref(d), G)
+            scr = torch.empty(max(need, 16), device=dev, dtype=torch.uint8)
+            res = []
+            for acc in (0, 1):
+                dw = torch.full((G, K, 3, 3, C), 0.5, device=dev, dtype=torch.float32)
+                L.check(lib.gm_conv2d_wgrad_grouped_bf16(ctypes.byref(d), G, dy.data_ptr(), x.data_ptr(),
+                                                          dw.data_ptr(), K * 9 * C, C, acc, scr.data_ptr(),
+                                                          need, L.stream_of(dev)), "wgrad")
+                res.append(dw)
+            outs[mode] = res
+        torch.cuda.synchronize()
+    finally:
+        L.check(lib.gm_conv_set_wgrad_loop(0), "loop")
+    for gi in range(G):
+        xr = x[gi * N:(gi + 1) * N].float().permute(0, 3, 1, 2)
+        gr = dy[gi * N:(gi + 1) * N].float().permute(0, 3, 1, 2)
+        ref = torch.nn.grad.conv2d_weight(xr, (K, C, 3, 3), gr, stride=1, padding=1)
+        for acc, base in ((0, 0.0), (1, 0.5)):
+            got = outs[2][acc][gi].permute(0, 3, 1, 2) - base
+            err = float((got - ref).abs().max() / ref.abs().max())
+            assert err < 2e-3, (gi, acc, err)
+            old = outs[0][acc][gi].permute(0, 3, 1, 2) - base
+            assert float((got - old).abs().max() / ref.abs().max()) < 1e-4
