@@ -295,7 +295,9 @@ def main():
     # same launch the step runs (inside the graph), timed with HIP events on its stream
     if a.profile:
         if rank == 0:
-            print(json.dumps({"profile_run": True, "ms_per_step": round(ms, 3), "steps": a.steps}), flush=True)
+            print(json.dumps({"profile_run": True, "ms_per_step": round(ms, 3), "steps": a.steps, "n_gpus": world,
+                              "value": round(world * B * V * a.steps / elapsed, 2), "unit": "view-images/s"}),
+                  flush=True)
         if dist_on:
             dist.destroy_process_group()
         return

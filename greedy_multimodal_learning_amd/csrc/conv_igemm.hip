@@ -1632,9 +1632,11 @@ __global__ __launch_bounds__(256) void k_conv_rw(ConvArgs a, RwArgs r) {
             const int c = k & 1;
             asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[c][0]), "+v"(af[c][1]), "+v"(bfr[c]));
             if (k + 1 < 36) load(k + 1, c ^ 1);
+            __builtin_amdgcn_sched_barrier(0);  // the next k-step's reads go out before these MFMAs
 #pragma unroll
             for (int i = 0; i < 2; ++i)
                 acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[c], af[c][i], acc[i], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
         }
 
         const int b = (int)r.fd_tpi.div((uint32_t)tl);
@@ -1845,9 +1847,11 @@ __global__ __launch_bounds__(256) void k_conv_stem(ConvArgs a, StemArgs r) {
                 if (k >= r.ksteps) break;
                 asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[u][0]), "+v"(af[u][1]), "+v"(bfr[u]));
                 if (k + 1 < r.ksteps) load(k + 1, u ^ 1);
+                __builtin_amdgcn_sched_barrier(0);  // the next k-step's reads go out before these MFMAs
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
                     acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[u], af[u][i], acc[i], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
 
@@ -2368,9 +2372,15 @@ __global__ __launch_bounds__(256) void k_conv_rw2(ConvArgs a, RwArgs r) {
             const int c = k & 1;
             asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[c][0]), "+v"(af[c][1]), "+v"(af[c][2]), "+v"(af[c][3]));
             if (k + 1 < 36) load(k + 1, c ^ 1);
+            // the next k-step's reads go out BEFORE this k-step's MFMAs: without the fence
+            // hipcc hoists the (register-only) MFMAs above the asm reads, reuses their
+            // registers as the read targets and leaves each read's latency exposed at the
+            // next wait (measured: a quarter of the MFMA rate)
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int i = 0; i < 4; ++i)
                 acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k >> 2][k & 3], af[c][i], acc[i], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
         }
 
         const int b = (int)r.fd_tpi.div((uint32_t)tl);

@@ -400,11 +400,13 @@ __global__ __launch_bounds__(256) void k_conv_wgrad4(WgradArgs a) {
             const int c = ks & 1;
             wait_lgkm0<MT, NT>(af[c], bfr[c]);
             if (ks < 3) load(ks + 1, c ^ 1);
+            __builtin_amdgcn_sched_barrier(0);  // the next slice's reads go out before these MFMAs
 #pragma unroll
             for (int i = 0; i < MT; ++i)
 #pragma unroll
                 for (int j = 0; j < NT; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[c][i], bfr[c][j], acc[i][j], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
         }
     };
     constexpr int BUF1 = SA + SB;
@@ -628,6 +630,7 @@ __global__ __launch_bounds__(256) void k_conv_wgrad_ring(WgradArgs a) {
             const int c = ks & 1;
             wait_lgkm0<MT, NT>(af[c], bfr[c]);
             if (ks + 1 < KS) load(ks + 1, c ^ 1);
+            __builtin_amdgcn_sched_barrier(0);  // the next slice's reads before these MFMAs
 #pragma unroll
             for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -697,9 +700,9 @@ __global__ __launch_bounds__(256) void k_conv_wgrad_ring(WgradArgs a) {
     }
 }
 
-// k_wgrad_halo64: weight gradient of the ResNet layer-1 convolution (3x3, stride 1, pad 1,
-// C = K = 64, W <= 62), the whole 64 x (9 taps x 64) gradient of a view group held in the
-// accumulators of one workgroup (wave (kh, ch): output channels 32 kh .., input channels
+// k_wgrad_halo64: weight gradient of a 3x3 / stride-1 / pad-1 convolution with 64-channel
+// multiples and W <= 62 (ResNet layers 1 and 2), a 64 x (9 taps x 64) block of a view group's
+// gradient (the whole layer-1 gradient) held in the accumulators of one workgroup (wave (kh, ch): output channels 32 kh .., input channels
 // 32 ch .., all nine taps = 9 x 32x32 accumulators) while it walks a contiguous range of
 // output rows.  Per output row only that row's dy (64 pixel rows of 128 B, pixels >= W zero)
 // and ONE new input row (the x ring holds rows r-1, r, r+1 of the current output row r plus
@@ -714,11 +717,12 @@ __global__ __launch_bounds__(256) void k_conv_wgrad_ring(WgradArgs a) {
 // counted vmcnt waits and raw barriers.  Each workgroup writes its fp32 partial slab
 // [64][9 x 64] (split-K over rows; k_wgrad_sum reduces them in a fixed order).
 struct WHaloArgs {
-    const uint16_t* dy;  // [G][N*P][Q][64]  (P = H, Q = W)
-    const uint16_t* x;   // [G][N*H][W][64]
-    float* part;         // [G][splits][64][9*64]
+    const uint16_t* dy;  // [G][N*P][Q][K]  (P = H, Q = W)
+    const uint16_t* x;   // [G][N*H][W][C]
+    float* part;         // [G][kt*ct tiles][splits][K][9*C] (tile (kb, cb) writes its 64 x 9 x 64 block)
     int N, H, W, rows, splits, rpw;  // rows = N*H per group, rpw = rows per workgroup
-    long long gs;        // group stride of dy / x (elements): N*H*W*64
+    int K, C, kt, ct;    // channels; 64-channel tiles of dy (kt) and x (ct)
+    long long gs_dy, gs_x;  // group strides (elements)
 };
 
 template <int D>
@@ -731,9 +735,14 @@ __global__ __launch_bounds__(256) void k_wgrad_halo64(WHaloArgs a) {
     const int t = threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const int kh = wave & 1, ch = wave >> 1;
-    const int grp = blockIdx.x / a.splits, split = blockIdx.x - grp * a.splits;
-    const uint16_t* __restrict__ gdy = a.dy + grp * a.gs;
-    const uint16_t* __restrict__ gx = a.x + grp * a.gs;
+    // block -> (group, 64 x 64 channel tile, split): splits innermost
+    int bid = blockIdx.x;
+    const int split = bid % a.splits;
+    bid /= a.splits;
+    const int tile = bid % (a.kt * a.ct), grp = bid / (a.kt * a.ct);
+    const int kb = tile % a.kt, cb = tile / a.kt;
+    const uint16_t* __restrict__ gdy = a.dy + grp * a.gs_dy + kb * 64;
+    const uint16_t* __restrict__ gx = a.x + grp * a.gs_x + cb * 64;
     const int r0 = split * a.rpw;
     const int r1 = min(a.rows, r0 + a.rpw);
     // the zero row (+ 1 KB pad: tap reads run two pixels past a row)
@@ -755,14 +764,14 @@ __global__ __launch_bounds__(256) void k_wgrad_halo64(WHaloArgs a) {
         const bool dok = r < r1, xok = r + 1 < a.rows;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            const void* src = (dok && px[j] < a.W) ? (const void*)(gdy + ((size_t)r * a.W + px[j]) * 64 + soff[j]) : zero;
+            const void* src = (dok && px[j] < a.W) ? (const void*)(gdy + ((size_t)r * a.W + px[j]) * a.K + soff[j]) : zero;
             __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + OD + ds * SL + (2 * wave + j) * 1024), 16, 0, 0);
         }
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int col = px[j] - 1;
             const bool ok = xok && col >= 0 && col < a.W;
-            const void* src = ok ? (const void*)(gx + ((size_t)(r + 1) * a.W + col) * 64 + soff[j]) : zero;
+            const void* src = ok ? (const void*)(gx + ((size_t)(r + 1) * a.W + col) * a.C + soff[j]) : zero;
             __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + OX + xs * SL + (2 * wave + j) * 1024), 16, 0, 0);
         }
     };
@@ -773,7 +782,7 @@ __global__ __launch_bounds__(256) void k_wgrad_halo64(WHaloArgs a) {
         for (int j = 0; j < 2; ++j) {
             const int col = px[j] - 1;
             const bool ok = fok && col >= 0 && col < a.W;
-            const void* src = ok ? (const void*)(gx + ((size_t)f * a.W + col) * 64 + soff[j]) : zero;
+            const void* src = ok ? (const void*)(gx + ((size_t)f * a.W + col) * a.C + soff[j]) : zero;
             __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + OX + xs * SL + (2 * wave + j) * 1024), 16, 0, 0);
         }
     };
@@ -821,39 +830,51 @@ __global__ __launch_bounds__(256) void k_wgrad_halo64(WHaloArgs a) {
         unsigned bb[9];
 #pragma unroll
         for (int tp = 0; tp < 9; ++tp) bb[tp] = xb[tp / 3] + b_lane[tp % 3];
-        for (int ks = 0; ks < nks; ++ks) {
+        // k-slice fragments double-buffered: slice ks + 1's reads go out before slice ks's
+        // MFMAs (sched_barrier: hipcc would otherwise hoist the MFMAs above the asm reads)
+        bf16x8 af[2], bfr[2][9];
+        auto rd = [&](int ks, int c) __attribute__((always_inline)) {
             const unsigned ko = (unsigned)(ks * 16 * 128);
-            bf16x8 af, bfr[9];
-            {
-                short4_t lo, hi;
-                asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(abase + ko));
-                asm volatile("ds_read_b64_tr_b16 %0, %1 offset:512" : "=v"(hi) : "v"(abase + ko));
-                af = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-            }
+            short4_t lo, hi;
+            asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(abase + ko));
+            asm volatile("ds_read_b64_tr_b16 %0, %1 offset:512" : "=v"(hi) : "v"(abase + ko));
+            af[c] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
             for (int tp = 0; tp < 9; ++tp) {
-                short4_t lo, hi;
                 asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(bb[tp] + ko));
                 asm volatile("ds_read_b64_tr_b16 %0, %1 offset:512" : "=v"(hi) : "v"(bb[tp] + ko));
-                bfr[tp] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+                bfr[c][tp] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
             }
-            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af), "+v"(bfr[0]), "+v"(bfr[1]), "+v"(bfr[2]), "+v"(bfr[3]),
-                         "+v"(bfr[4]), "+v"(bfr[5]), "+v"(bfr[6]), "+v"(bfr[7]), "+v"(bfr[8]));
+        };
+        rd(0, 0);
+        for (int ks = 0; ks < nks; ks += 2) {
 #pragma unroll
-            for (int tp = 0; tp < 9; ++tp)
-                acc[tp] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr[tp], acc[tp], 0, 0, 0);
+            for (int h = 0; h < 2; ++h) {
+                if (ks + h >= nks) break;
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[h]), "+v"(bfr[h][0]), "+v"(bfr[h][1]), "+v"(bfr[h][2]),
+                             "+v"(bfr[h][3]), "+v"(bfr[h][4]), "+v"(bfr[h][5]), "+v"(bfr[h][6]), "+v"(bfr[h][7]),
+                             "+v"(bfr[h][8]));
+                if (ks + h + 1 < nks) rd(ks + h + 1, h ^ 1);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int tp = 0; tp < 9; ++tp)
+                    acc[tp] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[h], bfr[h][tp], acc[tp], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+            }
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // D[k][c]: col = lane & 31 (c), row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5) (k)
-    float* out = a.part + ((size_t)grp * a.splits + split) * (64 * 576);
+    // the split's slab [K][9*C]; this tile fills rows kb*64 .., columns tap*C + cb*64 ..
+    const int TC = 9 * a.C;
+    float* out = a.part + ((size_t)grp * a.splits + split) * ((size_t)a.K * TC);
 #pragma unroll
     for (int tp = 0; tp < 9; ++tp) {
-        const int col = tp * 64 + ch * 32 + (lane & 31);
+        const int col = tp * a.C + cb * 64 + ch * 32 + (lane & 31);
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-            const int row = kh * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-            out[(size_t)row * 576 + col] = acc[tp][e];
+            const int row = kb * 64 + kh * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+            out[(size_t)row * TC + col] = acc[tp][e];
         }
     }
 }
@@ -1014,9 +1035,9 @@ static int g_wgrad_wr = [] {
 // k_conv_wgrad_ring<.., 32, 4> (four-deep ring of 32-pixel steps, counted vmcnt, raw barrier)
 // instead of k_conv_wgrad4 (two buffers, vmcnt(0) drain per step); bit 1 = k_wgrad_halo64 for
 // the layer-1 shape (3x3 / s1 / p1, C = K = 64, W <= 62)
-static int g_wgrad_loop = [] {
+static int g_wgrad_loop = [] {  // default 2: k_wgrad_halo64 for layer 1 (62 vs 77 us per launch)
     const char* e = getenv("GM_WGRAD_LOOP");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 2;
 }();
 
 template <int MT, int NT>
@@ -1061,20 +1082,23 @@ static gm_conv_desc_hw to_hw(const gm_conv_desc* d) {
 
 // k_wgrad_halo64 serves the layer-1 shape: splits = workgroups per view group
 static bool halo64_ok(const gm_conv_desc_hw* d) {
+    const int maxc = (g_wgrad_loop & 4) ? 128 : 64;  // bit 2: also the 128-channel (layer-2) shape
     return (g_wgrad_loop & 2) && d->R == 3 && d->S == 3 && d->stride_h == 1 && d->stride_w == 1 && d->pad_h == 1 &&
-           d->pad_w == 1 && d->C == 64 && d->K == 64 && d->W <= 62 && d->W >= 1 && d->H >= 1 &&
-           (long long)d->N * d->H * d->W * 64 < (1ll << 31);
+           d->pad_w == 1 && d->C % 64 == 0 && d->K % 64 == 0 && d->C <= maxc && d->K <= maxc && d->W <= 62 &&
+           d->W >= 1 && d->H >= 1 && (long long)d->N * d->H * d->W * (d->C > d->K ? d->C : d->K) < (1ll << 31);
 }
+// workgroups per (view group, channel tile): about one per CU in all
 static int halo64_splits(const gm_conv_desc_hw* d, int G) {
     const int rows = d->N * d->H;
-    int sp = 256 / G;
+    const int tiles = (d->K / 64) * (d->C / 64) * G;
+    int sp = 256 / tiles;
     if (sp < 1) sp = 1;
     return sp < rows ? sp : rows;
 }
 
 extern "C" size_t gm_conv2d_wgrad_grouped_scratch(const gm_conv_desc_hw* d, int G) {
     if (!d || d->stride_h < 1 || d->stride_w < 1 || G < 1) return 0;
-    if (halo64_ok(d)) return (size_t)G * halo64_splits(d, G) * 64 * 576 * sizeof(float);
+    if (halo64_ok(d)) return (size_t)G * halo64_splits(d, G) * d->K * 9 * d->C * sizeof(float);
     const WPlan w = plan(d, G);
     const size_t slab = (size_t)d->K * d->R * d->S * d->C;
     return (size_t)G * w.splits * slab * sizeof(float);
@@ -1109,7 +1133,7 @@ extern "C" int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, con
     const size_t need = gm_conv2d_wgrad_grouped_scratch(d, G);
     GM_REQUIRE(scratch && scratch_bytes >= need, "conv wgrad: scratch %zu < %zu", scratch_bytes, need);
     hipStream_t st0 = as_stream(stream);
-    if (halo64_ok(d) && c_real == 64) {
+    if (halo64_ok(d) && c_real == d->C) {
         WHaloArgs h;
         h.dy = (const uint16_t*)dy;
         h.x = (const uint16_t*)x;
@@ -1118,7 +1142,9 @@ extern "C" int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, con
         h.rows = d->N * d->H;
         h.splits = halo64_splits(d, G);
         h.rpw = (h.rows + h.splits - 1) / h.splits;
-        h.gs = (long long)d->N * d->H * d->W * 64;
+        h.K = d->K; h.C = d->C; h.kt = d->K / 64; h.ct = d->C / 64;
+        h.gs_dy = (long long)d->N * d->H * d->W * d->K;
+        h.gs_x = (long long)d->N * d->H * d->W * d->C;
         constexpr int D = 2;
         const size_t lds = (size_t)(D + 3) * 8192 + 8192 + 1024 + (size_t)(D + 1) * 8192;
         static bool attr = false;
@@ -1126,10 +1152,10 @@ extern "C" int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, con
             (void)hipFuncSetAttribute((const void*)k_wgrad_halo64<D>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             attr = true;
         }
-        k_wgrad_halo64<D><<<h.splits * G, 256, lds, st0>>>(h);
+        k_wgrad_halo64<D><<<h.splits * h.kt * h.ct * G, 256, lds, st0>>>(h);
         int rc = check_launch("k_wgrad_halo64");
         if (rc) return rc;
-        const size_t slab = (size_t)64 * 576;
+        const size_t slab = (size_t)d->K * 9 * d->C;
         const size_t ncol = slab / 4;
         int R = 1;
         while (R < 32 && R * 2 <= h.splits && (ncol * R + 255) / 256 < 512) R *= 2;
@@ -1235,7 +1261,8 @@ extern "C" int gm_conv_set_wgrad_staging(int wr) {
 }
 
 extern "C" int gm_conv_set_wgrad_loop(int mode) {
-    GM_REQUIRE(mode >= 0 && mode <= 3, "gm_conv_set_wgrad_loop: bit 0 ring main loop, bit 1 layer-1 halo kernel");
+    GM_REQUIRE(mode >= 0 && mode <= 7,
+               "gm_conv_set_wgrad_loop: bit 0 ring main loop, bit 1 layer-1 halo kernel, bit 2 also layer 2");
     g_wgrad_loop = mode;
     return GM_OK;
 }

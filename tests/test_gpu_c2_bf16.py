@@ -70,6 +70,18 @@ def c2_run(dev):
            [v for i in range(2) for v in (osums["wn_bypass"][i], osums["gn_bypass"][i])]
     ref = dict(loss=float(oloss), d_BDR=od, sums=np.asarray(flat, np.float64), mean=om.detach().numpy(),
                outs=[t.detach().numpy() for t in oo])
+    # the bf16 floor: the same oracle under PyTorch's own CPU bf16 autocast (its convolutions
+    # and matmuls in bf16, as the HIP trunk computes) against the fp32 oracle
+    o16 = weights.apply_to_module(model_ref.MMTM_MVCNN_Ref(), seed=5)
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        _, oo16, _, _ = o16(xo)
+    gating_ref.blend_loss([t.float() for t in oo16], y).backward()
+    s16 = gating_ref.group_sums([(n, p, p.grad) for n, p in o16.named_parameters()])
+    od16 = gating_ref.BDRState(0.01, 5).update(s16)
+    flat16 = [v for i in range(2) for v in (s16["wn_main"][i], s16["gn_main"][i])] + \
+             [v for i in range(2) for v in (s16["wn_bypass"][i], s16["gn_bypass"][i])]
+    ref["sums16"] = np.asarray(flat16, np.float64)
+    ref["d_BDR16"] = od16
     return hip, ref
 
 
@@ -105,12 +117,20 @@ def test_c2_group_sums_and_d_bdr_vs_oracle(c2_run):
     e_w = np.abs(w_h - w_r) / w_r
     e_g = np.abs(g_h - g_r) / g_r
     e_d = abs(hip["d_BDR"] - ref["d_BDR"])
+    f_g = np.abs(ref["sums16"][1::2] - g_r) / g_r  # PyTorch's own bf16 (CPU autocast) vs fp32
+    f_d = abs(ref["d_BDR16"] - ref["d_BDR"])
     print(f"C2 bf16 vs oracle: weight sums rel {e_w.max():.3e}, grad sums rel {e_g}, "
-          f"d_BDR {hip['d_BDR']:.6f} vs {ref['d_BDR']:.6f} (|diff| {e_d:.3e})")
-    # measured: weight sums 3.6e-8; gradient sums 9.8e-3 / 6.0e-4 / 1.7e-3 / 2.0e-3
-    # (main0, main1, bypass0, bypass1); d_BDR -0.01283 vs -0.01673 (3.9e-3)
+          f"d_BDR {hip['d_BDR']:.6f} vs {ref['d_BDR']:.6f} (|diff| {e_d:.3e}); PyTorch CPU bf16 floor: "
+          f"grad sums rel {f_g}, d_BDR |diff| {f_d:.3e}")
+    # measured (round 3/4): weight sums 3.6e-8; gradient sums 7.9e-3 / 2.0e-4 / 8.0e-4 / 6.9e-4
+    # (main0, main1, bypass0, bypass1) against a CPU bf16 floor of 7.8e-3 / 6.1e-3 / 6.5e-3 /
+    # 6.0e-3 (B = 16, /tmp probe); which branch lands high follows the weights
+    # (test_gpu_view_symmetry.py)
     assert e_w.max() < 1e-6
-    assert e_g.max() < 3e-2
-    # below epsilon (0.01) with a 2x margin over the measured gap; decision-level parity of
-    # the same gate over a 20-step trace: test_gpu_gate_decisions.py
-    assert e_d < 8e-3
+    # per branch within twice PyTorch's own bf16 error (a lucky small floor on one branch is
+    # not held against it: half the largest floor is the least a branch is allowed)
+    assert (e_g <= 2 * np.maximum(f_g, 0.5 * f_g.max()) + 1e-4).all(), (e_g, f_g)
+    # d_BDR = sum of four log10 terms: no further from fp32 than the floor's worst case
+    # (0.434 x the four gradient-sum errors of the bf16 floor); decision-level parity of the
+    # same gate: test_gpu_gate_decisions.py, test_gpu_gate_steered.py
+    assert e_d <= max(2 * f_d, 0.434 * f_g.sum()), (e_d, f_d, f_g)

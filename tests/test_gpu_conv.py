@@ -433,7 +433,7 @@ def test_wgrad_ring_bit_identical(dev, shape):
                 outs.append(dw)
         torch.cuda.synchronize()
     finally:
-        L.check(lib.gm_conv_set_wgrad_loop(0), "ring")
+        L.check(lib.gm_conv_set_wgrad_loop(2), "ring")  # the default
     assert torch.equal(outs[0], outs[2]) and torch.equal(outs[1], outs[3])
     # and it is a weight gradient: group 0 against fp32 PyTorch
     xr = x[:N].float().permute(0, 3, 1, 2)
@@ -482,7 +482,8 @@ def test_conv_rw2_bit_identical(dev, shape):
         assert torch.equal(a_, b_), name
 
 
-@pytest.mark.parametrize("shape", [(64, 56, 56), (3, 56, 56), (5, 20, 20), (2, 9, 7), (1, 3, 62)],
+@pytest.mark.parametrize("shape", [(64, 56, 56, 64), (3, 56, 56, 64), (5, 20, 20, 64), (2, 9, 7, 64), (1, 3, 62, 64),
+                                   (64, 28, 28, 128), (3, 28, 28, 128), (2, 5, 9, 128)],
                          ids=lambda s: "x".join(map(str, s)))
 def test_wgrad_halo64_vs_fp32(dev, shape):
     """k_wgrad_halo64 (layer-1 weight gradient: the whole 64 x 9 x 64 gradient in one
@@ -492,9 +493,10 @@ def test_wgrad_halo64_vs_fp32(dev, shape):
     import ctypes
     from greedy_multimodal_learning_amd import _lib as L
     from greedy_multimodal_learning_amd import conv as CV
-    N, H, W = shape
-    C = K = 64
+    N, H, W, C = shape
+    K = C
     G = 2
+    mode = 2 if C == 64 else 6
     torch.manual_seed(N * 1000 + H * 10 + W)
     x = torch.randn(G * N, H, W, C, device=dev).bfloat16()
     dy = torch.randn(G * N, H, W, K, device=dev).bfloat16()
@@ -502,8 +504,8 @@ def test_wgrad_halo64_vs_fp32(dev, shape):
     d = CV._desc_hw(N, H, W, C, K, 3, 3, 1, 1, 1, 1)
     outs = {}
     try:
-        for mode in (0, 2):
-            L.check(lib.gm_conv_set_wgrad_loop(mode), "loop")
+        for m in (0, mode):
+            L.check(lib.gm_conv_set_wgrad_loop(m), "loop")
             need = lib.gm_conv2d_wgrad_grouped_scratch(ctypes.byref(d), G)
             scr = torch.empty(max(need, 16), device=dev, dtype=torch.uint8)
             res = []
@@ -513,16 +515,16 @@ def test_wgrad_halo64_vs_fp32(dev, shape):
                                                           dw.data_ptr(), K * 9 * C, C, acc, scr.data_ptr(),
                                                           need, L.stream_of(dev)), "wgrad")
                 res.append(dw)
-            outs[mode] = res
+            outs[m] = res
         torch.cuda.synchronize()
     finally:
-        L.check(lib.gm_conv_set_wgrad_loop(0), "loop")
+        L.check(lib.gm_conv_set_wgrad_loop(2), "loop")  # the default
     for gi in range(G):
         xr = x[gi * N:(gi + 1) * N].float().permute(0, 3, 1, 2)
         gr = dy[gi * N:(gi + 1) * N].float().permute(0, 3, 1, 2)
         ref = torch.nn.grad.conv2d_weight(xr, (K, C, 3, 3), gr, stride=1, padding=1)
         for acc, base in ((0, 0.0), (1, 0.5)):
-            got = outs[2][acc][gi].permute(0, 3, 1, 2) - base
+            got = outs[mode][acc][gi].permute(0, 3, 1, 2) - base
             err = float((got - ref).abs().max() / ref.abs().max())
             assert err < 2e-3, (gi, acc, err)
             old = outs[0][acc][gi].permute(0, 3, 1, 2) - base

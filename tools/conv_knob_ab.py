@@ -38,9 +38,9 @@ def main():
     build.build()
     dev = torch.device("cuda:0")
     lib = L.load()
-    modes = [int(m) for m in a.modes.split(",")]
-    want_ops = set(a.ops.split(","))
-    want_shapes = set(a.shapes.split(",")) if a.shapes else None
+    modes = [int(m) for m in a.modes.replace("/", ",").split(",")]
+    want_ops = set(a.ops.replace("/", ",").split(","))
+    want_shapes = set(a.shapes.replace("/", ",").split(",")) if a.shapes else None
     ops = [o for o in T.conv_ops(a.batch, dev, 320e6, a.groups, a.arch)
            if o[1] in want_ops and (want_shapes is None or o[0] in want_shapes)]
     setter = getattr(lib, a.setter)

@@ -52,8 +52,9 @@ for s in "$@"; do
       tail -3 gpurun_out/gpu_tests.log ;;
     tests:*)
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 -rA \
-        --timeout-method thread -k "${s#tests:}" > gpurun_out/gpu_tests_k.log 2>&1 || { tail -40 gpurun_out/gpu_tests_k.log; exit 12; }
-      tail -3 gpurun_out/gpu_tests_k.log ;;
+        --timeout-method thread -k "${s#tests:}" > "gpurun_out/gpu_tests_k_$(echo "${s#tests:}" | tr -c 'A-Za-z0-9\n' '_' | cut -c1-40).log" 2>&1 \
+        || { tail -40 "gpurun_out/gpu_tests_k_$(echo "${s#tests:}" | tr -c 'A-Za-z0-9\n' '_' | cut -c1-40).log"; exit 12; }
+      tail -3 "gpurun_out/gpu_tests_k_$(echo "${s#tests:}" | tr -c 'A-Za-z0-9\n' '_' | cut -c1-40).log" ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 \
         || { tail -30 gpurun_out/smoke.log; exit 13; }
@@ -135,7 +136,7 @@ for s in "$@"; do
       tail -5 "$d.log"; python3 tools/summarize_stats.py "$d/rp_kernel_stats.csv" 1 | head -12 ;;
     py:*)
       a="${s#py:}"; f="${a%%,*}"; args=""; [ "$f" != "$a" ] && args="${a#*,}"
-      lg="gpurun_out/py_$(basename "$f" .py).log"
+      lg="gpurun_out/py_$(basename "$f" .py)$(echo "$args" | tr -c 'A-Za-z0-9\n' '_' | cut -c1-60).log"
       timeout -k 10 600 python -u "$f" ${args//,/ } > "$lg" 2>&1 || { tail -30 "$lg"; exit 19; }
       tail -20 "$lg" ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -186,12 +186,17 @@ def _make_bf16(op, B, dev, C, H, W, K, R, st, pad, P, Q, G=2):
                                                                 n, dx.data_ptr(), 0, ws, nb, L.stream_of(dev)),
                                "dgrad")
     d = CV._desc_hw(B, H, W, Cp, K, R, R, st, st, pad, pad)
-    need = lib.gm_conv2d_wgrad_grouped_scratch(ctypes.byref(d), G)
-    scr = torch.empty(max(need, 16), device=dev, dtype=torch.uint8)
     dw = torch.empty(G, K, R, R, C, device=dev, dtype=torch.float32)
-    return lambda: L.check(lib.gm_conv2d_wgrad_grouped_bf16(ctypes.byref(d), G, dy.data_ptr(), x.data_ptr(),
-                                                            dw.data_ptr(), K * R * R * C, C, 0, scr.data_ptr(), need,
-                                                            L.stream_of(dev)), "wgrad")
+    scr = [torch.empty(16, device=dev, dtype=torch.uint8)]
+
+    def wgrad():  # the scratch the current kernel plan needs (A/B switches change it)
+        need = lib.gm_conv2d_wgrad_grouped_scratch(ctypes.byref(d), G)
+        if scr[0].numel() < need:
+            scr[0] = torch.empty(need, device=dev, dtype=torch.uint8)
+        L.check(lib.gm_conv2d_wgrad_grouped_bf16(ctypes.byref(d), G, dy.data_ptr(), x.data_ptr(), dw.data_ptr(),
+                                                 K * R * R * C, C, 0, scr[0].data_ptr(), scr[0].numel(),
+                                                 L.stream_of(dev)), "wgrad")
+    return wgrad
 
 
 def conv_ops(B, dev, rotate_bytes=0, G=2, arch="resnet18"):
@@ -284,6 +289,14 @@ def bn_ops(B, dev, G=2):
             e_in, e_out = G * M * C, G * B * P * Q * C
             out.append(("maxpool", "bn_relu_fwd", 1, 0, e_in * 2 + e_out * 3, pool_fwd))
             out.append(("maxpool", "bwd", 1, 0, e_out * 3 + e_in * 2, pool_bwd))
+            pool_fwd()  # valid argmax bytes for the fused backward
+
+            def pool_bn_bwd(d1=d1, gyp=gyp, idx=idx, ba=ba, buf=buf):  # what the step runs (vtrunk)
+                L.check(lib.gm_bn_relu_maxpool2d_bwd_grouped_bf16(ctypes.byref(d1), G, gyp.data_ptr(), idx.data_ptr(),
+                                                                  ba, buf.data_ptr(), buf.numel(), st),
+                        "pool+bn bwd")
+            # two passes: (x, pooled gradient, argmax) each, + the dx write
+            out.append(("bn1+maxpool", "pool_bn_bwd", 1, 0, 2 * (e_in * 2 + e_out * 3) + e_in * 2, pool_bn_bwd))
     return out
 
 
