@@ -600,18 +600,17 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
                     for (int j = 0; j < NT; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[c][j], af[c][i], acc[i][j], 0, 0, 0);
             }
-            // emitted order: the first k-step's reads, then each k-step's MFMAs with the next
-            // k-step's reads threaded between them (one read per MFMA), so LDS latency hides
-            // under the matrix pipe instead of an lgkmcnt(0) before every group of MFMAs
+            // emitted order: k-step ks + 1's reads BEFORE k-step ks's MFMAs, so they stay in
+            // flight under the matrix pipe.  (Threading them between the MFMAs, one read per
+            // MFMA, issued each k-step's last read after its MFMAs into a register an MFMA had
+            // just released, and the lgkmcnt(0) the compiler put before the next MFMAs then
+            // exposed that read's whole LDS latency once per k-step.)
             constexpr int NR = MT + NT, NM = MT * NT;
             __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
 #pragma unroll
             for (int ks = 0; ks < 3; ++ks) {
-#pragma unroll
-                for (int q = 0; q < (NM > NR ? NM : NR); ++q) {
-                    if (q < NM) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                    if (q < NR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                }
+                __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
             }
             __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
         };
@@ -913,15 +912,12 @@ __global__ __launch_bounds__(BM == 256 ? 512 : 256) void k_conv_halo(ConvArgs a,
                 for (int j = 0; j < NT; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[c][j], af[c][i], acc[i][j], 0, 0, 0);
         }
-        constexpr int NR = MT + NT, NM = MT * NT;
+        constexpr int NR = MT + NT, NM = MT * NT;  // next k-step's reads before these MFMAs
         __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
 #pragma unroll
         for (int ks = 0; ks < 3; ++ks) {
-#pragma unroll
-            for (int q = 0; q < (NM > NR ? NM : NR); ++q) {
-                if (q < NM) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                if (q < NR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-            }
+            __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
         }
         __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
     };
@@ -1226,14 +1222,16 @@ __global__ __launch_bounds__(256, 2) void k_conv_h9(ConvArgs a, HaloArgs h) {
         }
         constexpr int NR = MT + NT, NM = MT * NT;
         if constexpr (WR != 3) {
+            // slice ks + 1's fragment reads are issued BEFORE slice ks's MFMAs (the compiler's
+            // counted lgkmcnt then waits for slice ks's reads only, slice ks + 1's stay in
+            // flight under the MFMAs).  The read/MFMA interleave this replaces issued each
+            // slice's last read after its MFMAs, into a register an MFMA had just released,
+            // and waited lgkmcnt(0) on it: one exposed LDS round trip per k-slice.
             __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
 #pragma unroll
             for (int ks = 0; ks < 3; ++ks) {
-#pragma unroll
-                for (int q = 0; q < (NM > NR ? NM : NR); ++q) {
-                    if (q < NM) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                    if (q < NR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                }
+                __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
             }
             __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
         }

@@ -714,7 +714,11 @@ __global__ __launch_bounds__(256) void k_conv_wgrad_ring(WgradArgs a) {
 // Both operands go through the ds_read_b64_tr_b16 transposed reads of k_conv_wgrad4 (rows
 // of 128 B, chunk XOR 4 * ((row >> 1) & 1): conflict-free for any 4 consecutive rows, so a
 // tap shift keeps the reads conflict-free).  Rows stream D = 2 ahead through LDS-DMA with
-// counted vmcnt waits and raw barriers.  Each workgroup writes its fp32 partial slab
+// counted vmcnt waits and raw barriers.  Taps s = 1, 2 of the last k-slice read halo pixels
+// 64 and 65 (they meet dy pixels >= W, which are zero - but 0 x NaN is NaN): every x slot is
+// followed by two zeroed pad rows that no DMA writes, so those reads never land in the next
+// slot, which may still be in flight or hold a previous kernel's LDS contents.
+// Each workgroup writes its fp32 partial slab
 // [64][9 x 64] (split-K over rows; k_wgrad_sum reduces them in a fixed order).
 struct WHaloArgs {
     const uint16_t* dy;  // [G][N*P][Q][K]  (P = H, Q = W)
@@ -729,7 +733,8 @@ template <int D>
 __global__ __launch_bounds__(256) void k_wgrad_halo64(WHaloArgs a) {
     constexpr int XS = D + 3, DS = D + 1;  // x ring (rows r-1 .. r+1 + D ahead), dy ring
     constexpr int SL = 8192;               // one staged row: 64 pixels x 128 B
-    constexpr int OX = 0, OZ = XS * SL, OD = OZ + SL + 1024;  // x ring | zero row (+ pad) | dy ring
+    constexpr int XSL = SL + 256;          // x slot: the row + two zeroed pad pixel rows
+    constexpr int OX = 0, OZ = XS * XSL, OD = OZ + SL + 1024;  // x ring | zero row (+ pad) | dy ring
     extern __shared__ __attribute__((aligned(16))) uint4 wsm[];
     char* lds = reinterpret_cast<char*>(wsm);
     const int t = threadIdx.x, lane = t & 63;
@@ -745,8 +750,10 @@ __global__ __launch_bounds__(256) void k_wgrad_halo64(WHaloArgs a) {
     const uint16_t* __restrict__ gx = a.x + grp * a.gs_x + cb * 64;
     const int r0 = split * a.rpw;
     const int r1 = min(a.rows, r0 + a.rpw);
-    // the zero row (+ 1 KB pad: tap reads run two pixels past a row)
+    // the zero row (+ 1 KB pad: tap reads run two pixels past a row) and each x slot's pad rows
     for (int i = t; i < (SL + 1024) / 16; i += 256) *reinterpret_cast<uint4*>(lds + OZ + i * 16) = make_uint4(0, 0, 0, 0);
+    if (t < XS * 16) *reinterpret_cast<uint4*>(lds + OX + (t >> 4) * XSL + SL + (t & 15) * 16) = make_uint4(0, 0, 0, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // visible to every wave at the loop's first barrier
 
     typedef __attribute__((address_space(1))) const void* gptr_t;
     typedef __attribute__((address_space(3))) void* lptr_t;
@@ -772,7 +779,7 @@ __global__ __launch_bounds__(256) void k_wgrad_halo64(WHaloArgs a) {
             const int col = px[j] - 1;
             const bool ok = xok && col >= 0 && col < a.W;
             const void* src = ok ? (const void*)(gx + ((size_t)(r + 1) * a.W + col) * a.C + soff[j]) : zero;
-            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + OX + xs * SL + (2 * wave + j) * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + OX + xs * XSL + (2 * wave + j) * 1024), 16, 0, 0);
         }
     };
     auto issue_x = [&](int f) __attribute__((always_inline)) {  // x row f alone (prologue)
@@ -783,7 +790,7 @@ __global__ __launch_bounds__(256) void k_wgrad_halo64(WHaloArgs a) {
             const int col = px[j] - 1;
             const bool ok = fok && col >= 0 && col < a.W;
             const void* src = ok ? (const void*)(gx + ((size_t)f * a.W + col) * a.C + soff[j]) : zero;
-            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + OX + xs * SL + (2 * wave + j) * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + OX + xs * XSL + (2 * wave + j) * 1024), 16, 0, 0);
         }
     };
 
@@ -825,7 +832,7 @@ __global__ __launch_bounds__(256) void k_wgrad_halo64(WHaloArgs a) {
 #pragma unroll
         for (int rr = 0; rr < 3; ++rr) {
             const int h = p + rr - 1;
-            xb[rr] = lds0 + ((h < 0 || h >= a.H) ? (unsigned)OZ : (unsigned)(OX + ((r + rr - 1 + XS) % XS) * SL));
+            xb[rr] = lds0 + ((h < 0 || h >= a.H) ? (unsigned)OZ : (unsigned)(OX + ((r + rr - 1 + XS) % XS) * XSL));
         }
         unsigned bb[9];
 #pragma unroll
@@ -1146,7 +1153,7 @@ extern "C" int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, con
         h.gs_dy = (long long)d->N * d->H * d->W * d->K;
         h.gs_x = (long long)d->N * d->H * d->W * d->C;
         constexpr int D = 2;
-        const size_t lds = (size_t)(D + 3) * 8192 + 8192 + 1024 + (size_t)(D + 1) * 8192;
+        const size_t lds = (size_t)(D + 3) * (8192 + 256) + 8192 + 1024 + (size_t)(D + 1) * 8192;
         static bool attr = false;
         if (!attr) {
             (void)hipFuncSetAttribute((const void*)k_wgrad_halo64<D>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -529,3 +529,38 @@ def test_wgrad_halo64_vs_fp32(dev, shape):
             assert err < 2e-3, (gi, acc, err)
             old = outs[0][acc][gi].permute(0, 3, 1, 2) - base
             assert float((got - old).abs().max() / ref.abs().max()) < 1e-4
+
+
+def test_wgrad_halo64_beside_a_busy_neighbour(dev):
+    """The layer-1 weight gradient repeated beside a large matmul on another stream (its
+    waves share the CUs and leave their LDS contents behind): every repetition bit-identical
+    and finite.  Regression: taps s = 1, 2 read halo pixels 64 / 65, which once spilled into
+    the next ring slot - possibly still in flight or holding a neighbour's stale LDS data -
+    and 0 x NaN turned whole gradient columns non-finite about every other repetition."""
+    import ctypes
+    from greedy_multimodal_learning_amd import _lib as L
+    from greedy_multimodal_learning_amd import conv as CV
+    N, H, W, C, G = 64, 56, 56, 64, 2
+    torch.manual_seed(0)
+    x = torch.randn(G * N, H, W, C, device=dev).bfloat16()
+    dy = torch.randn(G * N, H, W, C, device=dev).bfloat16()
+    lib = L.load()
+    d = CV._desc_hw(N, H, W, C, C, 3, 3, 1, 1, 1, 1)
+    L.check(lib.gm_conv_set_wgrad_loop(2), "loop")
+    need = lib.gm_conv2d_wgrad_grouped_scratch(ctypes.byref(d), G)
+    scr = torch.empty(need, device=dev, dtype=torch.uint8)
+    side = torch.cuda.Stream()
+    big = torch.randn(8192, 8192, device=dev)
+    outs = []
+    for i in range(12):
+        dw = torch.empty(G, C, 3, 3, C, device=dev)
+        if i:
+            with torch.cuda.stream(side):
+                big @ big
+        L.check(lib.gm_conv2d_wgrad_grouped_bf16(ctypes.byref(d), G, dy.data_ptr(), x.data_ptr(), dw.data_ptr(),
+                                                  C * 9 * C, C, 0, scr.data_ptr(), need, L.stream_of(dev)), "wgrad")
+        torch.cuda.synchronize()
+        outs.append(dw)
+    assert torch.isfinite(outs[0]).all()
+    for i, dw in enumerate(outs[1:], 1):
+        assert torch.equal(dw, outs[0]), (i, int((~torch.isfinite(dw)).sum()))

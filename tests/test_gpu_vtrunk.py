@@ -214,6 +214,7 @@ def test_model_stacked_vs_per_view(dev, kind):
         e_pv = float((outs[False][i].cpu() - ref).abs().max()) / scale
         assert e_st <= max(3e-2, 2 * e_pv), (f"logits[{i}]", e_st, e_pv)
     worst = []
+    tot = [0.0, 0.0, 0.0]  # all parameters as one vector: stacked / per-view error^2, fp32 norm^2
     for (n, pa), (_, pb), (_, pc) in zip(a.named_parameters(), b.named_parameters(), c.named_parameters()):
         ga, gb, gc = pa.grad.double(), pb.grad.double(), pc.grad.double()
         den = gc.norm() + 1e-30
@@ -221,13 +222,20 @@ def test_model_stacked_vs_per_view(dev, kind):
         worst.append((ea, eb, n))
         assert ea < max(2 * eb, 3e-2), f"{n}: stacked {ea:.3e} vs per-view {eb:.3e} (relative to fp32)"
         # a dropped, zeroed or misrouted gradient cannot hide behind a noisy per-view path:
-        # the stacked gradient keeps the fp32 gradient's size and direction
-        ratio = float(ga.norm() / den)
-        cos_a = float((ga * gc).sum() / (ga.norm() * den + 1e-30))
-        cos_b = float((gb * gc).sum() / (gb.norm() * den + 1e-30))
-        assert 0.5 < ratio < 2.0, f"{n}: stacked gradient norm {ratio:.3f} x the fp32 one"
-        assert cos_a > min(0.5, cos_b - 0.2), f"{n}: cosine to fp32 {cos_a:.3f} (per-view {cos_b:.3f})"
+        # wherever the per-view bf16 gradient is itself meaningful (within 50 % of fp32), the
+        # stacked one keeps the fp32 gradient's size and direction
+        if eb < 0.5:
+            ratio = float(ga.norm() / den)
+            cos_a = float((ga * gc).sum() / (ga.norm() * den + 1e-30))
+            assert 0.5 < ratio < 2.0, f"{n}: stacked gradient norm {ratio:.3f} x the fp32 one"
+            assert cos_a > 0.5, f"{n}: cosine to fp32 {cos_a:.3f} (per-view error {eb:.3f})"
+        tot[0] += float((ga - gc).pow(2).sum())
+        tot[1] += float((gb - gc).pow(2).sum())
+        tot[2] += float(gc.pow(2).sum())
+    e_all, e_all_pv = (tot[0] / tot[2]) ** 0.5, (tot[1] / tot[2]) ** 0.5
+    assert e_all < max(2 * e_all_pv, 1e-2), ("all parameters", e_all, e_all_pv)
     worst.sort(reverse=True)
+    print(f"whole gradient vs fp32: stacked {e_all:.3e}, per-view {e_all_pv:.3e}")
     print("stacked vs per-view gradient error vs fp32 (worst 5):",
           ", ".join(f"{n} {ea:.2e}/{eb:.2e}" for ea, eb, n in worst[:5]))
     for (n, ba), (_, bb), (_, bc) in zip(a.named_buffers(), b.named_buffers(), c.named_buffers()):
