@@ -249,9 +249,9 @@ EXPORTS.update({
     "gm_maxpool2d_fwd_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "gm_bn_relu_maxpool2d_fwd_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "gm_bn_relu_maxpool2d_fwd_grouped_bf16": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
-                                                      c_void_p]),
+                                                      c_void_p, c_void_p]),
     "gm_bn_relu_maxpool2d_bwd_grouped_bf16": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
-                                                      c_size_t, c_void_p]),
+                                                      c_void_p, c_size_t, c_void_p]),
     "gm_conv_stem_stats_rows": (c_int, [c_void_p, c_int]),
     "gm_conv2d_fwd_grouped_stats_bf16": (c_int, [c_void_p, c_int, c_void_p, c_void_p, ctypes.c_longlong, c_void_p,
                                                  c_void_p, c_int, c_void_p]),

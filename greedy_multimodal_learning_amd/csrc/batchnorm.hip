@@ -502,12 +502,19 @@ __device__ __forceinline__ void combine_finalize(const ReduceArgs& a, int cs, fl
 // finalize of k_bn_reduce; pass 2 applies dx = ca*dz + cb*x + cc.  HBM: pass 1 reads x and
 // the pooled gradient + argmax, pass 2 the same and writes dx - against k_maxpool_bwd
 // (read pooled, write dz) + the BN backward (read dz and x twice, write dx).
+// With xs (the forward's selected raw x per pooled output) pass 1 needs no pixel gather:
+// S1 and S2 are linear in the per-pixel gradient, so they sum over the pooled outputs -
+// dy_pool * mask(xs) and dy_pool * mask(xs) * (xs - mean) - reading the pooled gradient and
+// xs (a quarter of the pixels, 2 x 51 MB at C2) instead of x, the gradient and the argmax.
+// (The per-pixel bf16 rounding of the gathered gradient, which pass 2 applies to dx, is not
+// applied to these sums: they are the fp32 sums of the same terms.)
 struct StemPoolGeo {
     int Ng, H, W, P, Q;      // images per view group, input and pooled sizes
     long long items;         // owner blocks x channel groups per view group
     long long ipb;           // items per block (pass 1; a multiple of kT)
     const uint2* idx;        // [G*Ng][P][Q][C] window-relative argmax bytes
     const uint4* gp;         // [G*Ng][P][Q][C] bf16 pool gradient
+    const uint4* xs;         // [G*Ng][P][Q][C] bf16 selected x (optional)
 };
 
 template <bool APPLY>
@@ -636,7 +643,34 @@ __global__ __launch_bounds__(kT) void k_stem_pool_bn_bwd(ReduceArgs a0, StemPool
     const int rc = blockIdx.x;
     const long long i0 = (long long)rc * pg.ipb;
     const long long i1 = i0 + pg.ipb < pg.items ? i0 + pg.ipb : pg.items;
-    for (long long i = i0 + t; i < i1; i += kT) item(i);  // (two items in flight per thread: slower)
+    if (pg.xs) {
+        // pooled outputs i (an item index is a pooled (n, k, l, cg) vector: the same decode)
+        const uint4* __restrict__ XS = pg.xs + goff;
+        for (long long i = i0 + t; i < i1; i += 4 * kT) {
+            uint4 gq[4], xq[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {  // four vectors' loads in flight
+                const long long iu = i + u * kT < i1 ? i + u * kT : i;
+                gq[u] = GP[iu];
+                xq[u] = XS[iu];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (i + u * kT >= i1) break;
+                float gv[8], xf[8];
+                unpack8(gq[u], gv);
+                unpack8(xq[u], xf);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float d = fmaf(xf[j], fsc[j], fsh[j]) > 0.f ? gv[j] : 0.f;
+                    s1[j] += d;
+                    s2[j] = fmaf(d, xf[j] - mu[j], s2[j]);
+                }
+            }
+        }
+    } else {
+        for (long long i = i0 + t; i < i1; i += kT) item(i);  // (two items in flight per thread: slower)
+    }
     // row-group combine in LDS as k_bn_reduce: red[r0][SW][2], r0 = t / C8 (C8 threads per row)
     const int S2w = 2 * C, r0 = t / C8, rpp = kT / C8;
 #pragma unroll
@@ -1774,8 +1808,8 @@ extern "C" int gm_bn_bwd_f32(const gm_bn_bwd* p, void* scratch, size_t bytes, vo
 // d describes one view group's pool (N images, k 3, stride 2, pad 1, C 64); ps[g] the BN
 // backward of group g with relu, fwd_coef (the mask from x) and no y / dres; ps[g].dy unused.
 extern "C" int gm_bn_relu_maxpool2d_bwd_grouped_bf16(const gm_pool_desc* d, int G, const void* dy_pool,
-                                                     const void* idx, const gm_bn_bwd* ps, void* scratch,
-                                                     size_t bytes, void* stream) {
+                                                     const void* idx, const void* xsel, const gm_bn_bwd* ps,
+                                                     void* scratch, size_t bytes, void* stream) {
     const char* fn = "gm_bn_relu_maxpool2d_bwd_grouped_bf16";
     GM_REQUIRE(d && dy_pool && idx && ps && G >= 1 && G <= kMaxBnG, "%s: bad arguments", fn);
     GM_REQUIRE(d->k == 3 && d->stride == 2 && d->pad == 1 && d->C == 64 && d->N >= 1 && d->H >= 2 && d->W >= 2,
@@ -1817,6 +1851,7 @@ extern "C" int gm_bn_relu_maxpool2d_bwd_grouped_bf16(const gm_pool_desc* d, int 
     a.nrc = nrc;
     pg.idx = static_cast<const uint2*>(idx);
     pg.gp = static_cast<const uint4*>(dy_pool);
+    pg.xs = static_cast<const uint4*>(xsel);
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL((k_stem_pool_bn_bwd<false>), dim3(nrc, 1, G), dim3(kT), 0, st, a, pg);
     if ((rc = check_launch("k_stem_pool_bn_bwd<reduce>"))) return rc;

@@ -2235,217 +2235,6 @@ static int launch_stem(const ConvArgs& a, const StemArgs& r, size_t lds, hipStre
     return check_launch("k_conv_stem");
 }
 
-// k_conv_rw2: the layer-1 3x3 / stride-1 / 64 -> 64 convolution (forward and input
-// gradient) with the weights resident in VGPRs instead of LDS.  k_conv_rw keeps the 72 KB
-// weight tensor in LDS, so a 128-pixel tile (two halo buffers + weights + output tile fill
-// the LDS) gives each wave two 32x32 accumulators: two MFMAs per k-step cover each LDS
-// read round trip and the per-tap address work, and the kernel ran at a quarter of the MFMA
-// rate (instruction-issue and LDS-latency bound).  Here each wave holds its 32 output
-// channels x 576 (tap, channel) weight fragments in 144 VGPRs for the life of the persistent
-// workgroup, the LDS holds only the two halo buffers and the output tile, and the tile is
-// 256 MFMA rows (RT = 256 / W whole image rows, 224 pixels at 56 x 56): each wave computes
-// 128 pixels x 32 channels = four accumulators, four MFMAs per k-step, and reads only its
-// four pixel fragments per k-step.  Same halo image, swizzle, tap order and k order as
-// k_conv_rw (same fp32 accumulation order per output: bit-identical results).
-template <int DIAG>  // DIAG (timing diagnostics, outputs meaningless): 1 = no halo wait
-__global__ __launch_bounds__(256) void k_conv_rw2(ConvArgs a, RwArgs r) {
-    extern __shared__ __attribute__((aligned(16))) uint4 smem[];
-    char* lds = reinterpret_cast<char*>(smem);  // [halo 0][halo 1][output tile]
-    const ConvCls& cl = a.cls[0];
-    const int H = a.Hi, W = a.Wi, W2 = W + 2;
-    const int t = threadIdx.x, lane = t & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-    const int wm = wave >> 1, wn = wave & 1;
-    const int slot = lane & 7, fr = lane & 31, fh = lane >> 5;
-    const unsigned pk_dh = cl.pk_dh, pk_dw = cl.pk_dw, pk_r = cl.pk_r, pk_s = cl.pk_s;
-    typedef __attribute__((address_space(1))) const void* gptr_t;
-    typedef __attribute__((address_space(3))) void* lptr_t;
-    int g = 0, tl = blockIdx.x, nwg = gridDim.x;
-    if (a.G > 1) {
-        nwg = gridDim.x / a.G;
-        g = tl / nwg;
-        tl -= g * nwg;
-    }
-    if (tl >= r.tiles || g >= a.G) return;
-    const uint16_t* const gin = a.in + g * a.gs_in;
-    const uint16_t* const gwt = a.wt + g * a.gs_wt;
-    const uint16_t* const gadd = a.addend ? a.addend + g * a.gs_out : nullptr;
-
-    constexpr int kMaxHI = 12;
-    int h_rel[kMaxHI];
-    unsigned h_cls = 0;
-#pragma unroll
-    for (int j = 0; j < kMaxHI; ++j) {
-        const int I = wave + 4 * j;
-        const int hp = I * 8 + (lane >> 3);
-        const int rr = (int)r.fd_w2.div((uint32_t)hp), c = hp - rr * W2;
-        const int gc = slot ^ ((hp >> 1) & 7);
-        h_rel[j] = ((rr - 1) * W + c - 1) * 64 + gc * 8;
-        unsigned k = rr == 0 ? 1u : rr == r.RT + 1 ? 2u : 0u;
-        if (I >= r.nI || hp >= r.npix || c == 0 || c == W + 1) k = 3u;
-        h_cls |= k << (2 * j);
-    }
-    auto issue_halo = [&](int tile, int bb) {
-        const int b = (int)r.fd_tpi.div((uint32_t)tile);
-        const int p0 = (tile - b * r.tpi) * r.RT;
-        const uint16_t* origin = gin + ((size_t)(b * H + p0) * W << 6);
-        const unsigned okmask = 1u | (p0 > 0 ? 2u : 0u) | (p0 + r.RT < H ? 4u : 0u);
-        char* base = lds + bb * r.hbytes;
-#pragma unroll
-        for (int j = 0; j < kMaxHI; ++j) {
-            const int I = wave + 4 * j;
-            if (I >= r.nI) break;
-            const bool ok = (okmask >> ((h_cls >> (2 * j)) & 3u)) & 1u;
-            const void* src = ok ? (const void*)(origin + h_rel[j]) : (const void*)g_zero16;
-            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(base + I * 1024), 16, 0, 0);
-        }
-    };
-    issue_halo(tl, 0);
-    // the wave's weight fragments: output channel n = 32 wn + fr, input channels
-    // 16 ks + 8 fh .. + 7 of tap tp (the MFMA's A operand, as k_conv_rw's B fragment)
-    bf16x8 wf[9][4];
-    {
-        const int n = wn * 32 + fr;
-#pragma unroll
-        for (int tp = 0; tp < 9; ++tp) {
-            const int ti = tp / 3, tj = tp - ti * 3;
-            const int tw = (int)((pk_r >> (4 * ti)) & 15u) * a.Sw + (int)((pk_s >> (4 * tj)) & 15u);
-            const uint16_t* src = gwt + ((size_t)n * a.T + tw) * 64 + 8 * fh;
-#pragma unroll
-            for (int ks = 0; ks < 4; ++ks) wf[tp][ks] = *reinterpret_cast<const bf16x8*>(src + 16 * ks);
-        }
-    }
-    const int valid = r.RT * W;
-    int hbase[4];
-    bool pok[4];
-    int prow[4], pcol[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        int m = wm * 128 + i * 32 + fr;
-        pok[i] = m < valid;
-        m = pok[i] ? m : 0;
-        prow[i] = m / W;
-        pcol[i] = m - prow[i] * W;
-        hbase[i] = (prow[i] + 1) * W2 + pcol[i] + 1;
-    }
-    constexpr int kWaitAll = (7 << 4) | (15 << 8);
-    __builtin_amdgcn_s_waitcnt(kWaitAll);  // the halo and the weight loads
-    lds_barrier();
-    const size_t out_bytes = (size_t)a.N * a.Ho * a.Wo * a.Nout * 2;
-    const __amdgpu_buffer_rsrc_t orsrc =
-        __builtin_amdgcn_make_buffer_rsrc(cl.out + g * a.gs_out, 0, (int)(out_bytes < 0x7fffffffu ? out_bytes : 0x7fffffffu),
-                                          0x00020000);
-    const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
-    int bb = 0;
-    for (; tl < r.tiles; tl += nwg) {
-        const int nx = tl + nwg;
-        if (nx < r.tiles) issue_halo(nx, bb ^ 1);
-        const int hoff = bb * r.hbytes;
-        floatx16 acc[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
-        bf16x8 af[2][4];
-        unsigned abase[4];
-        auto tap_base = [&](int tp) {
-            const int ti = tp / 3, tj = tp - ti * 3;
-            const int dh = (int)((pk_dh >> (4 * ti)) & 15u) - 8, dw = (int)((pk_dw >> (4 * tj)) & 15u) - 8;
-            const int toff = dh * W2 + dw;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int hp = hbase[i] + toff;
-                abase[i] = lds0 + ((unsigned)(hoff + (hp << 7)) | (unsigned)((((hp >> 1) & 7) ^ fh) << 4));
-            }
-        };
-        auto load = [&](int k, int c) {
-            const int tp = k >> 2, ks = k & 3;
-            if (ks == 0) tap_base(tp);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) af[c][i] = lds_rd128<0>(abase[i] ^ (unsigned)(ks << 5));
-        };
-        load(0, 0);
-#pragma unroll
-        for (int k = 0; k < 36; ++k) {
-            const int c = k & 1;
-            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[c][0]), "+v"(af[c][1]), "+v"(af[c][2]), "+v"(af[c][3]));
-            if (k + 1 < 36) load(k + 1, c ^ 1);
-            // the next k-step's reads go out BEFORE this k-step's MFMAs: without the fence
-            // hipcc hoists the (register-only) MFMAs above the asm reads, reuses their
-            // registers as the read targets and leaves each read's latency exposed at the
-            // next wait (measured: a quarter of the MFMA rate)
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k >> 2][k & 3], af[c][i], acc[i], 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-
-        const int b = (int)r.fd_tpi.div((uint32_t)tl);
-        const int p0 = (tl - b * r.tpi) * r.RT;
-        if (!a.addend) {
-            char* ot = lds + 2 * r.hbytes;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int m = wm * 128 + i * 32 + fr;
-#pragma unroll
-                for (int gq = 0; gq < 4; ++gq) {
-                    const int chunk = (wn * 4 + gq) ^ (m & 7);
-                    *reinterpret_cast<uint2*>(ot + m * 128 + chunk * 16 + 8 * fh) =
-                        make_uint2(pack_bf2(acc[i][4 * gq], acc[i][4 * gq + 1]),
-                                   pack_bf2(acc[i][4 * gq + 2], acc[i][4 * gq + 3]));
-                }
-            }
-            __syncthreads();
-            const unsigned tbase = (unsigned)(((size_t)(b * a.Ho + p0) * a.Wo) * a.Nout * 2);
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int e = t + 256 * u;  // 16-B chunk e of the tile: pixel e / 8, chunk e % 8
-                const int m = e >> 3, j = e & 7;
-                const bool ok = m < valid;
-                const uint4 v = *reinterpret_cast<const uint4*>(ot + (ok ? m : 0) * 128 + ((j ^ (m & 7)) << 4));
-                __builtin_amdgcn_raw_buffer_store_b128(
-                    __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), orsrc,
-                    ok ? tbase + (unsigned)e * 16u : 0xfffffff0u, 0, 0);
-            }
-            constexpr int kWaitStores8 = 8 | (7 << 4) | (15 << 8);
-            if (DIAG != 1) __builtin_amdgcn_s_waitcnt(kWaitStores8);
-            lds_barrier();
-            bb ^= 1;
-            continue;
-        }
-        size_t off[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int ho = (p0 + prow[i]) * cl.oS + cl.oH, wo = pcol[i] * cl.oS + cl.oW;
-            off[i] = ((size_t)(b * a.Ho + ho) * a.Wo + wo) * a.Nout + wn * 32 + 4 * fh;
-        }
-        uint2 av[4][4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int gq = 0; gq < 4; ++gq) av[i][gq] = *(const uint2*)(gadd + off[i] + 8 * gq);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-#pragma unroll
-            for (int gq = 0; gq < 4; ++gq) {
-                float o0 = acc[i][4 * gq], o1 = acc[i][4 * gq + 1];
-                float o2 = acc[i][4 * gq + 2], o3 = acc[i][4 * gq + 3];
-                o0 += bf_lo(av[i][gq].x); o1 += bf_hi(av[i][gq].x);
-                o2 += bf_lo(av[i][gq].y); o3 += bf_hi(av[i][gq].y);
-                typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-                const u32x2 v = {pack_bf2(o0, o1), pack_bf2(o2, o3)};
-                __builtin_amdgcn_raw_buffer_store_b64(v, orsrc, pok[i] ? (unsigned)((off[i] + 8 * gq) * 2) : 0xfffffff0u,
-                                                      0, 0);
-            }
-        }
-        constexpr int kWaitStores16 = 16 | (7 << 4) | (15 << 8);
-        if (DIAG != 1) __builtin_amdgcn_s_waitcnt(kWaitStores16);
-        lds_barrier();
-        bb ^= 1;
-    }
-}
-
 static int g_conv_rw = [] {
     const char* e = getenv("GM_CONV_RW");  // 0: layer-1 shapes take the im2col kernel
     return e ? atoi(e) : 1;
@@ -2462,8 +2251,7 @@ static size_t rw_plan(const ConvArgs& a, RwArgs& r) {
     if ((size_t)a.N * a.Ho * a.Wo * a.Nout * 2 >= 0x7ffff000u) return 0;  // 32-bit buffer offsets
     for (int i = 0; i < 3; ++i)
         if (c.cdh[i] < -1 || c.cdh[i] > 1 || c.cdw[i] < -1 || c.cdw[i] > 1) return 0;
-    const bool v2 = g_conv_rw == 4 || g_conv_rw == 5;  // k_conv_rw2: 256-row tiles, weights in VGPRs
-    int RT = (v2 ? 256 : 128) / a.Wi;
+    int RT = 128 / a.Wi;
     if (RT > a.Hi) RT = a.Hi;
     while (RT > 1 && a.Hi % RT) --RT;
     r.RT = RT;
@@ -2475,24 +2263,15 @@ static size_t rw_plan(const ConvArgs& a, RwArgs& r) {
     r.hbytes = r.nI * 1024;
     r.fd_w2 = FastDiv((uint32_t)(a.Wi + 2));
     r.fd_tpi = FastDiv((uint32_t)r.tpi);
-    const size_t lds = v2 ? 2 * (size_t)r.hbytes + 256 * 128  // halo buffers + the output tile
-                          : (size_t)kRwWeightBytes + 2 * (size_t)r.hbytes + 128 * 128;
+    const size_t lds = (size_t)kRwWeightBytes + 2 * (size_t)r.hbytes + 128 * 128;
     return lds <= 160 * 1024 ? lds : 0;
 }
 
 static int launch_rw(const ConvArgs& a, const RwArgs& r, size_t lds, hipStream_t st) {
-    static bool granted = false;  // every variant may use the whole LDS (idempotent, safe to race)
+    static bool granted = false;  // the whole LDS (idempotent, safe to race)
     if (!granted) {
         const int mx = 160 * 1024;
-        hipError_t e = hipFuncSetAttribute((const void*)k_conv_rw<0>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void*)k_conv_rw<1>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void*)k_conv_rw<2>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void*)k_conv_rw2<0>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void*)k_conv_rw2<1>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+        const hipError_t e = hipFuncSetAttribute((const void*)k_conv_rw<0>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
         if (e != hipSuccess) {
             set_error("k_conv_rw: %d B of LDS refused (%s)", mx, hipGetErrorString(e));
             return GM_E_UNSUP;
@@ -2502,11 +2281,7 @@ static int launch_rw(const ConvArgs& a, const RwArgs& r, size_t lds, hipStream_t
     // persistent: one workgroup per CU, split evenly over the view groups
     const int per = r.tiles < 256 / a.G ? r.tiles : (256 / a.G > 0 ? 256 / a.G : 1);
     const int grid = per * a.G;
-    if (g_conv_rw == 4) k_conv_rw2<0><<<grid, 256, lds, st>>>(a, r);
-    else if (g_conv_rw == 5) k_conv_rw2<1><<<grid, 256, lds, st>>>(a, r);  // timing diagnostics
-    else if (g_conv_rw == 2) k_conv_rw<1><<<grid, 256, lds, st>>>(a, r);  // timing diagnostics
-    else if (g_conv_rw == 3) k_conv_rw<2><<<grid, 256, lds, st>>>(a, r);
-    else k_conv_rw<0><<<grid, 256, lds, st>>>(a, r);
+    k_conv_rw<0><<<grid, 256, lds, st>>>(a, r);
     return check_launch("k_conv_rw");
 }
 
@@ -2954,7 +2729,7 @@ extern "C" int gm_conv_set_stem(int on) {
 }
 
 extern "C" int gm_conv_set_rw(int on) {
-    g_conv_rw = on;  // 0 off, 1 k_conv_rw, 4 k_conv_rw2 (2, 3, 5: timing diagnostics)
+    g_conv_rw = on ? 1 : 0;  // 0: the layer-1 shapes take the im2col kernel
     return GM_OK;
 }
 

@@ -480,409 +480,279 @@ __global__ __launch_bounds__(256) void k_conv_wgrad4(WgradArgs a) {
     }
 }
 
-// k_conv_wgrad_ring<MT, NT, BK, NS>: the k_conv_wgrad4 tile (same LDS image, swizzle,
-// transposed fragment reads and MFMA order, so bit-identical results) on an NS-deep LDS-DMA
-// ring of BK-pixel steps.  k_conv_wgrad4 issues step s+1, computes step s and then drains
-// vmcnt(0) at a __syncthreads: every step waits out one full DMA round trip beyond the
-// MFMAs that cover it.  Here NS-1 steps are in flight: each step waits with a COUNTED
-// vmcnt((NS-2) * pieces) for its own pieces only, passes a raw s_barrier (no vmcnt drain)
-// so every wave's pieces of the step have landed, re-issues the buffer the previous step
-// read (all waves are past that step's reads) and computes (cdna_hip_programming.md §5,
-// "Pipelining across barriers").  BK = 32 keeps the ring at 4 x 16 KB for 128 x 128 tiles,
-// so two workgroups still share a CU.
-template <int MT, int NT, int BK, int NS>
-__global__ __launch_bounds__(256) void k_conv_wgrad_ring(WgradArgs a) {
-    static_assert(BK == 32 || BK == 64, "BK");
-    static_assert(NS >= 3 && NS <= 6, "ring depth");
-    constexpr int BM = 64 * MT, BN = 64 * NT;
-    constexpr int RA = 2 * BM, RB = 2 * BN;          // row bytes
-    constexpr int SA = BK * RA, SB = BK * RB;        // bytes per buffer
-    constexpr int SS = SA + SB;                       // one ring slot
-    constexpr int GA = SA / 1024 / 4, GB = SB / 1024 / 4;  // DMA instructions per wave per step
-    constexpr int PC = GA + GB;                      // pieces per wave per step (vmcnt units)
-    static_assert(GA >= 1 && GB >= 1 && (NS - 2) * PC <= 63, "pieces / vmcnt range");
-    constexpr int LPA = RA / 16, LPB = RB / 16;      // lanes per row
-    constexpr int KS = BK / 16;                      // 16-pixel k-slices per step
-    extern __shared__ __attribute__((aligned(16))) uint4 wsm[];
-    char* lds = reinterpret_cast<char*>(wsm);        // NS slots of [A][B]
-    const int t = threadIdx.x, lane = t & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-    const int wm = wave >> 1, wn = wave & 1;
-    int bid = blockIdx.x;
-    {   // XCD-major: the tiles of one pixel range share an XCD (and its L2 copy of the rows)
-        const int n = gridDim.x, q = n >> 3, r = n & 7, x = bid & 7;
-        bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
-    }
-    const int tiles = a.tiles_k * a.tiles_n;
-    const int grp = bid / (tiles * a.splits);
-    bid -= grp * tiles * a.splits;
-    const uint16_t* __restrict__ gdy = a.dy + grp * a.gs_dy;
-    const uint16_t* __restrict__ gx = a.x + grp * a.gs_x;
-    const int split = bid / tiles, tile = bid - split * tiles;
-    const int tk = tile % a.tiles_k, tn = tile / a.tiles_k;
-    const int k0 = tk * BM, n0 = tn * BN;
-    const int PQ = a.P * a.Q;
-    const int M = a.N * PQ;
-    constexpr int SUB = 64 / BK;                     // BK-steps per 64-pixel plan step
-    const int step0 = split * a.steps_per_split * SUB;
-    const int step1 = min((M + BK - 1) / BK, step0 + a.steps_per_split * SUB);
-    const int nst = step1 - step0;
-
-    const int a_rsub = lane / LPA, a_slot = lane % LPA;
-    const uint16_t* a_ptr[GA];
-    int a_row[GA];
-    bool a_cok[GA];
-#pragma unroll
-    for (int j = 0; j < GA; ++j) {
-        a_row[j] = (wave * GA + j) * (64 / LPA) + a_rsub;
-        const int col = k0 + ((a_slot ^ wswz<RA>(a_row[j])) << 3);
-        a_cok[j] = col < a.Kc;
-        a_ptr[j] = gdy + ((size_t)step0 * BK + a_row[j]) * a.Kc + (a_cok[j] ? col : 0);
-    }
-    const int b_rsub = lane / LPB, b_slot = lane % LPB;
-    int b_toff[GB], b_dh[GB], b_dw[GB];
-    int b_b[GB], b_p[GB], b_q[GB];
-    bool b_cok[GB];
-#pragma unroll
-    for (int j = 0; j < GB; ++j) {
-        const int row = (wave * GB + j) * (64 / LPB) + b_rsub;
-        const int col = n0 + ((b_slot ^ wswz<RB>(row)) << 3);
-        b_cok[j] = col < a.T * a.C;
-        const int tap = b_cok[j] ? col >> a.logC : 0;
-        const int r = tap / a.S, s = tap - r * a.S;
-        b_dh[j] = r - a.padh;
-        b_dw[j] = s - a.padw;
-        b_toff[j] = ((b_dh[j] * a.W + b_dw[j]) << a.logC) + (col & (a.C - 1));
-        const int m = step0 * BK + row;
-        b_b[j] = (int)a.fd_pq.div((uint32_t)m);
-        const int pq = m - b_b[j] * PQ;
-        b_p[j] = (int)a.fd_q.div((uint32_t)pq);
-        b_q[j] = pq - b_p[j] * a.Q;
-    }
-    typedef __attribute__((address_space(1))) const void* gptr_t;
-    typedef __attribute__((address_space(3))) void* lptr_t;
-    const void* zero = (const void*)g_wzero16;
-    auto issue = [&](int i, int slot) __attribute__((always_inline)) {  // step step0 + i into ring slot
-        const bool full = (step0 + i + 1) * BK <= M;
-        const int bufoff = slot * SS;
-#pragma unroll
-        for (int j = 0; j < GA; ++j) {
-            const bool ok = a_cok[j] & (full | ((step0 + i) * BK + a_row[j] < M));
-            const void* src = ok ? (const void*)(a_ptr[j] + (size_t)i * BK * a.Kc) : zero;
-            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + bufoff + (wave * GA + j) * 1024), 16, 0, 0);
-        }
-#pragma unroll
-        for (int j = 0; j < GB; ++j) {
-            const int b = b_b[j], p = b_p[j], q = b_q[j];
-            const int h0 = p * a.sth, w0 = q * a.stw;
-            const int hi = h0 + b_dh[j], wi = w0 + b_dw[j];
-            const bool ok = b_cok[j] & (b < a.N) & ((unsigned)hi < (unsigned)a.H) & ((unsigned)wi < (unsigned)a.W);
-            const int pix = (b * a.H + h0) * a.W + w0;
-            const void* src = ok ? (const void*)(gx + (((long)pix << a.logC) + b_toff[j])) : zero;
-            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + bufoff + SA + (wave * GB + j) * 1024), 16,
-                                             0, 0);
-            int nq = q + a.adv_q, np = p + a.adv_p, nb = b + a.adv_b;
-            if (nq >= a.Q) { nq -= a.Q; ++np; }
-            if (np >= a.P) { np -= a.P; ++nb; }
-            b_b[j] = nb; b_p[j] = np; b_q[j] = nq;
-        }
-    };
-
-    floatx16 acc[MT][NT];
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
-    const int rbase = 8 * (g >> 1) + q4;
-    unsigned a_lds[MT], b_lds[NT];
-#pragma unroll
-    for (int i = 0; i < MT; ++i) {
-        const int c = wm * (32 * MT) + 32 * i + 16 * (g & 1) + 4 * p4;
-        a_lds[i] = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)(
-            lds + rbase * RA + (((c >> 3) ^ wswz<RA>(rbase)) << 4) + (c & 7) * 2);
-    }
-#pragma unroll
-    for (int j = 0; j < NT; ++j) {
-        const int c = wn * (32 * NT) + 32 * j + 16 * (g & 1) + 4 * p4;
-        b_lds[j] = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)(
-            lds + SA + rbase * RB + (((c >> 3) ^ wswz<RB>(rbase)) << 4) + (c & 7) * 2);
-    }
-    auto compute = [&](int slot) __attribute__((always_inline)) {
-        const unsigned so = (unsigned)(slot * SS);
-        unsigned ab[MT], bb[NT];
-#pragma unroll
-        for (int i = 0; i < MT; ++i) ab[i] = a_lds[i] + so;
-#pragma unroll
-        for (int j = 0; j < NT; ++j) bb[j] = b_lds[j] + so;
-        bf16x8 af[2][MT], bfr[2][NT];
-        auto load = [&](int ks, int c) {
-#pragma unroll
-            for (int i = 0; i < MT; ++i) af[c][i] = tr_frag_asm<0, RA>(ks, ab[i]);
-#pragma unroll
-            for (int j = 0; j < NT; ++j) bfr[c][j] = tr_frag_asm<0, RB>(ks, bb[j]);
-        };
-        load(0, 0);
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            const int c = ks & 1;
-            wait_lgkm0<MT, NT>(af[c], bfr[c]);
-            if (ks + 1 < KS) load(ks + 1, c ^ 1);
-            __builtin_amdgcn_sched_barrier(0);  // the next slice's reads before these MFMAs
-#pragma unroll
-            for (int i = 0; i < MT; ++i)
-#pragma unroll
-                for (int j = 0; j < NT; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[c][i], bfr[c][j], acc[i][j], 0, 0, 0);
-        }
-    };
-    // prologue: NS-1 steps in flight (fewer when the split is short)
-    const int npre = nst < NS - 1 ? nst : NS - 1;
-    for (int i = 0; i < npre; ++i) issue(i, i);
-    int i = 0, slot = 0;
-    for (; i + (NS - 1) < nst; ++i) {  // steady state: retire step i, re-issue its predecessor's slot
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * PC) : "memory");
-        __builtin_amdgcn_s_barrier();
-        issue(i + NS - 1, slot == 0 ? NS - 1 : slot - 1);
-        compute(slot);
-        slot = slot == NS - 1 ? 0 : slot + 1;
-    }
-    // tail: the last npre steps, nothing more to issue; k steps stay in flight behind each
-    auto tail = [&](auto kc) __attribute__((always_inline)) {
-        constexpr int k = decltype(kc)::value;
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(k * PC) : "memory");
-        __builtin_amdgcn_s_barrier();
-        compute(slot);
-        slot = slot == NS - 1 ? 0 : slot + 1;
-    };
-    const int left = nst - i;  // == npre
-    if (left >= 6) tail(std::integral_constant<int, 5>{});
-    if (left >= 5) tail(std::integral_constant<int, 4>{});
-    if (left >= 4) tail(std::integral_constant<int, 3>{});
-    if (left >= 3) tail(std::integral_constant<int, 2>{});
-    if (left >= 2) tail(std::integral_constant<int, 1>{});
-    if (left >= 1) tail(std::integral_constant<int, 0>{});
-
-    const int TC = a.T * a.C;
-    float* out = a.part + grp * a.gs_part + (size_t)split * a.Kc * TC;
-    const bool inner = k0 + BM <= a.Kc && n0 + BN <= TC;
-#pragma unroll
-    for (int j = 0; j < NT; ++j) {
-        const int col = n0 + wn * (32 * NT) + 32 * j + (lane & 31);
-#pragma unroll
-        for (int ii = 0; ii < MT; ++ii) {
-            const int row0 = k0 + wm * (32 * MT) + 32 * ii + 4 * (lane >> 5);
-            float* o = out + (size_t)row0 * TC + col;
-            if (inner) {
-                if (a.accumulate) {
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        float* p = o + (size_t)((r & 3) + 8 * (r >> 2)) * TC;
-                        *p += acc[ii][j][r];
-                    }
-                } else {
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) o[(size_t)((r & 3) + 8 * (r >> 2)) * TC] = acc[ii][j][r];
-                }
-            } else if (col < TC) {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int row = row0 + (r & 3) + 8 * (r >> 2);
-                    if (row < a.Kc) {
-                        float* p = o + (size_t)((r & 3) + 8 * (r >> 2)) * TC;
-                        *p = a.accumulate ? *p + acc[ii][j][r] : acc[ii][j][r];
-                    }
-                }
-            }
-        }
-    }
-}
-
 // k_wgrad_halo64: weight gradient of a 3x3 / stride-1 / pad-1 convolution with 64-channel
-// multiples and W <= 62 (ResNet layers 1 and 2), a 64 x (9 taps x 64) block of a view group's
-// gradient (the whole layer-1 gradient) held in the accumulators of one workgroup (wave (kh, ch): output channels 32 kh .., input channels
-// 32 ch .., all nine taps = 9 x 32x32 accumulators) while it walks a contiguous range of
-// output rows.  Per output row only that row's dy (64 pixel rows of 128 B, pixels >= W zero)
-// and ONE new input row (the x ring holds rows r-1, r, r+1 of the current output row r plus
-// the prefetched ones) are staged: 16 KB per 36 MFMAs per wave, against 24 KB per 8 MFMAs
-// per wave of k_conv_wgrad4's 64 x 128 tiles, whose B operand re-stages every input pixel
-// once per tap.  The nine taps read the same ring row at a pixel shift s (and ring rows
-// r-1 .. r+1 for the kernel rows): x halo pixel j = input column j - 1, so output pixel q,
-// tap (rr, s) reads halo pixel q + s of input row p + rr - 1 (a zero row outside the image).
-// Both operands go through the ds_read_b64_tr_b16 transposed reads of k_conv_wgrad4 (rows
-// of 128 B, chunk XOR 4 * ((row >> 1) & 1): conflict-free for any 4 consecutive rows, so a
-// tap shift keeps the reads conflict-free).  Rows stream D = 2 ahead through LDS-DMA with
-// counted vmcnt waits and raw barriers.  Taps s = 1, 2 of the last k-slice read halo pixels
-// 64 and 65 (they meet dy pixels >= W, which are zero - but 0 x NaN is NaN): every x slot is
-// followed by two zeroed pad rows that no DMA writes, so those reads never land in the next
-// slot, which may still be in flight or hold a previous kernel's LDS contents.
-// Each workgroup writes its fp32 partial slab
-// [64][9 x 64] (split-K over rows; k_wgrad_sum reduces them in a fixed order).
+// multiples and W <= 62 (the ResNet-18 identity-block shapes), as 64 x (9 taps x 64) blocks of
+// a view group's gradient held in the accumulators of one workgroup's four compute waves
+// (wave (kh, ch): output channels 32 kh .., input channels 32 ch .., 9 taps = 9 x 32x32
+// accumulators) while it walks a contiguous range of image rows.
+//
+// Staging unit: a "super-row" of 64 positions x 128 B = RPS = 64 / PP consecutive image rows
+// of PP >= W + 2 positions each (PP = 64, 32, 16 for W <= 62, 30, 14).  In the x image,
+// position m of a row holds input column m - 1 (zeros outside the image); in the dy image,
+// position m holds output pixel m - 2 (two leading zeros).  Tap (rr, s) of output row p is
+//   dw[rr][s] = sum over positions m of dy_p[m + 2 - s] (x) x_{p + rr - 1}[m]   (m from 0)
+// per 16-position k-slice.  Operand economy (LDS fragment reads set this kernel's speed:
+// halving them took the layer-1 launch from 47 to 37 us, while relaxing every wait did
+// nothing): per slice ONE dy fragment is read (shift s = 2, rows m) and the shifts s = 1, 0 are
+// made in registers from it and the next slice's fragment (v_permlane32_swap + v_alignbit:
+// rows m + 1, m + 2 = this fragment moved up by one / two elements plus the next fragment's
+// first rows); the x fragments of input rows p - 1, p, p + 1 stay in registers across output
+// rows (a 4-set rotation), so per slice ONE x fragment is read (row p + 2, for the next output
+// row).  2 + 2 transposed reads feed 9 MFMAs (12 before).  Kernel rows outside the image
+// multiply zeroed operands.
+//
+// Both operands come through ds_read_b64_tr_b16 transposed reads (rows of 128 B, chunk XOR
+// 4 * ((row >> 1) & 1): conflict-free for any 4 consecutive rows).  Four loader waves (one
+// beside each compute wave's SIMD) keep D super-rows of LDS-DMA in flight (dy of super-row S
+// with x of S + 2) under counted vmcnt waits; one raw barrier per super-row, before its third
+// slice (the dy reads run two slices ahead, the x reads one image row ahead).  Each workgroup
+// writes its fp32 partial slab [64][9 x 64] (split over rows; k_wgrad_sum reduces the splits in
+// a fixed order).
 struct WHaloArgs {
     const uint16_t* dy;  // [G][N*P][Q][K]  (P = H, Q = W)
     const uint16_t* x;   // [G][N*H][W][C]
-    float* part;         // [G][kt*ct tiles][splits][K][9*C] (tile (kb, cb) writes its 64 x 9 x 64 block)
-    int N, H, W, rows, splits, rpw;  // rows = N*H per group, rpw = rows per workgroup
+    float* part;         // [G][splits][K][9*C] (tile (kb, cb) writes its 64 x 9 x 64 block)
+    int N, H, W, rows, srows, splits, rpw;  // rows = N*H image rows per group, srows = super-rows,
+                                            // rpw = super-rows per workgroup
     int K, C, kt, ct;    // channels; 64-channel tiles of dy (kt) and x (ct)
     long long gs_dy, gs_x;  // group strides (elements)
 };
 
-template <int D>
-__global__ __launch_bounds__(256) void k_wgrad_halo64(WHaloArgs a) {
-    constexpr int XS = D + 3, DS = D + 1;  // x ring (rows r-1 .. r+1 + D ahead), dy ring
-    constexpr int SL = 8192;               // one staged row: 64 pixels x 128 B
-    constexpr int XSL = SL + 256;          // x slot: the row + two zeroed pad pixel rows
-    constexpr int OX = 0, OZ = XS * XSL, OD = OZ + SL + 1024;  // x ring | zero row (+ pad) | dy ring
+template <int D, int PP, bool PB, int ABL = 0>
+__global__ __launch_bounds__(512) void k_wgrad_halo64(WHaloArgs a) {
+    static_assert(D >= 2 && (PP == 16 || PP == 32 || PP == 64), "halo64: D >= 2 super-rows in flight, PP = 16/32/64");
+    constexpr int RPS = 64 / PP, SPR = PP / 16;  // image rows per super-row, k-slices per image row
+    constexpr int XS = D + 3, DS = D + 1;  // x ring (super-rows R .. R+D+2), dy ring (R .. R+D)
+    constexpr int SL = 8192, DSL = SL + 256;  // one super-row; dy slot + 2 zero pad positions
+    constexpr int OX = 0, OD = XS * SL;       // x ring | dy ring
     extern __shared__ __attribute__((aligned(16))) uint4 wsm[];
     char* lds = reinterpret_cast<char*>(wsm);
     const int t = threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-    const int kh = wave & 1, ch = wave >> 1;
     // block -> (group, 64 x 64 channel tile, split): splits innermost
     int bid = blockIdx.x;
     const int split = bid % a.splits;
     bid /= a.splits;
     const int tile = bid % (a.kt * a.ct), grp = bid / (a.kt * a.ct);
     const int kb = tile % a.kt, cb = tile / a.kt;
-    const uint16_t* __restrict__ gdy = a.dy + grp * a.gs_dy + kb * 64;
-    const uint16_t* __restrict__ gx = a.x + grp * a.gs_x + cb * 64;
-    const int r0 = split * a.rpw;
-    const int r1 = min(a.rows, r0 + a.rpw);
-    // the zero row (+ 1 KB pad: tap reads run two pixels past a row) and each x slot's pad rows
-    for (int i = t; i < (SL + 1024) / 16; i += 256) *reinterpret_cast<uint4*>(lds + OZ + i * 16) = make_uint4(0, 0, 0, 0);
-    if (t < XS * 16) *reinterpret_cast<uint4*>(lds + OX + (t >> 4) * XSL + SL + (t & 15) * 16) = make_uint4(0, 0, 0, 0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // visible to every wave at the loop's first barrier
+    const int R0 = split * a.rpw;
+    const int R1 = min(a.srows, R0 + a.rpw);
+    // each dy slot's two pad positions: ds_write, never a DMA target
+    if (t < DS * 16) *reinterpret_cast<uint4*>(lds + OD + (t >> 4) * DSL + SL + (t & 15) * 16) = make_uint4(0, 0, 0, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // visible to every wave at the first barrier
 
-    typedef __attribute__((address_space(1))) const void* gptr_t;
-    typedef __attribute__((address_space(3))) void* lptr_t;
-    const void* zero = (const void*)g_wzero16;
-    // DMA lanes: piece I = 2 wave + j (j = 0, 1) covers pixel rows 8 I .. 8 I + 7; lane -> pixel
-    // 8 I + lane / 8, source chunk (lane % 8) ^ swizzle(pixel)
-    int px[2], soff[2];
+    if (wave >= 4) {
+        // loader waves: all LDS-DMA, so the compute waves' MFMA stream never carries a DMA issue.
+        // Piece (lw, j) = slot positions 8 (2 lw + j) .. + 7, one image row (PP is a multiple of
+        // 8); lane -> position 8 (2 lw + j) + lane / 8, source chunk (lane % 8) ^ swizzle(position).
+        const int lw = wave - 4;
+        typedef __attribute__((address_space(1))) const void* gptr_t;
+        typedef __attribute__((address_space(3))) void* lptr_t;
+        const void* zero = (const void*)g_wzero16;
+        const uint16_t* __restrict__ gdy = a.dy + grp * a.gs_dy + kb * 64;
+        const uint16_t* __restrict__ gx = a.x + grp * a.gs_x + cb * 64;
+        int sub[2], xcol[2], dpx[2], xo[2], dyo[2];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        px[j] = (2 * wave + j) * 8 + (lane >> 3);
-        soff[j] = (((lane & 7) ^ wswz<128>(px[j])) << 3);
+        for (int j = 0; j < 2; ++j) {
+            const int pos = (2 * lw + j) * 8 + (lane >> 3);
+            const int sc = ((lane & 7) ^ wswz<128>(pos)) << 3;
+            sub[j] = pos / PP;
+            xcol[j] = pos % PP - 1;
+            dpx[j] = pos % PP - 2;
+            xo[j] = xcol[j] * a.C + sc;
+            dyo[j] = dpx[j] * a.K + sc;
+        }
+        auto dma = [&](const void* src, int off) __attribute__((always_inline)) {
+            if (ABL != 3) __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + off), 16, 0, 0);
+        };
+        auto issue_x = [&](int R, int xs) __attribute__((always_inline)) {  // x super-row R into slot xs
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int g = R * RPS + sub[j];
+                const bool ok = R >= 0 && g < a.rows && xcol[j] >= 0 && xcol[j] < a.W;
+                dma(ok ? (const void*)(gx + (size_t)g * a.W * a.C + xo[j]) : zero, OX + xs * SL + (2 * lw + j) * 1024);
+            }
+        };
+        auto issue_dy = [&](int R, int ds) __attribute__((always_inline)) {  // dy super-row R into slot ds
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int g = R * RPS + sub[j];
+                const bool ok = R < R1 && g < a.rows && dpx[j] >= 0 && dpx[j] < a.W;
+                dma(ok ? (const void*)(gdy + (size_t)g * a.W * a.K + dyo[j]) : zero, OD + ds * DSL + (2 * lw + j) * 1024);
+            }
+        };
+        auto slot = [](int v, int n) { return ((v % n) + n) % n; };
+        if (R0 < R1) {
+            // prologue: x super-rows R0 - 1 .. R0 + 1, then D steps of (dy S, x S + 2); step R0 landed
+            issue_x(R0 - 1, slot(R0 - 1, XS));
+            issue_x(R0, slot(R0, XS));
+            issue_x(R0 + 1, slot(R0 + 1, XS));
+            for (int i = 0; i < D; ++i) {
+                issue_dy(R0 + i, slot(R0 + i, DS));
+                issue_x(R0 + i + 2, slot(R0 + i + 2, XS));
+            }
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (D - 1)) : "memory");
+            __builtin_amdgcn_s_barrier();
+        }
+        int dsn = slot(R0 + D, DS), xsn = slot(R0 + D + 2, XS);  // slots of DMA step R + D
+        for (int R = R0; R < R1; ++R) {
+            // step R + 1 landed (later steps may stay in flight); after the barrier no compute
+            // wave reads dy super-row R - 1 or x super-row R - 1 any more (their slots are the
+            // ones step R + D refills; uniform counts: past the range the pieces load zeros)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (D - 2)) : "memory");
+            __builtin_amdgcn_s_barrier();
+            issue_dy(R + D, dsn);
+            issue_x(R + D + 2, xsn);
+            dsn = dsn + 1 == DS ? 0 : dsn + 1;
+            xsn = xsn + 1 == XS ? 0 : xsn + 1;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        return;
     }
-    auto issue = [&](int r) __attribute__((always_inline)) {  // dy row r and x row r + 1 (ring slots)
-        const int ds = r % DS, xs = (r + 1) % XS;
-        const bool dok = r < r1, xok = r + 1 < a.rows;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const void* src = (dok && px[j] < a.W) ? (const void*)(gdy + ((size_t)r * a.W + px[j]) * a.K + soff[j]) : zero;
-            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + OD + ds * SL + (2 * wave + j) * 1024), 16, 0, 0);
-        }
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int col = px[j] - 1;
-            const bool ok = xok && col >= 0 && col < a.W;
-            const void* src = ok ? (const void*)(gx + ((size_t)(r + 1) * a.W + col) * a.C + soff[j]) : zero;
-            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + OX + xs * XSL + (2 * wave + j) * 1024), 16, 0, 0);
-        }
-    };
-    auto issue_x = [&](int f) __attribute__((always_inline)) {  // x row f alone (prologue)
-        const int xs = ((f % XS) + XS) % XS;
-        const bool fok = f >= 0 && f < a.rows;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int col = px[j] - 1;
-            const bool ok = fok && col >= 0 && col < a.W;
-            const void* src = ok ? (const void*)(gx + ((size_t)f * a.W + col) * a.C + soff[j]) : zero;
-            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + OX + xs * XSL + (2 * wave + j) * 1024), 16, 0, 0);
-        }
-    };
 
+    const int kh = wave & 1, ch = wave >> 1;
     floatx16 acc[9];
 #pragma unroll
     for (int i = 0; i < 9; ++i)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
     // tr-read lane geometry (k_conv_wgrad4's): half-wave g >> 1 reads rows 8 (g >> 1) + q4 (+4) of
-    // a 16-row slice, 4-column block p4 of the 32-column fragment, 16-column half g & 1
+    // a 16-row slice, 4-column block p4 of the 32-column fragment, 16-column half g & 1; lane l
+    // receives channel l % 32, rows 8 (l / 32) .. + 7 (the MFMA operand layout)
     const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
     const int rbase = 8 * (g >> 1) + q4;
     const int acol = kh * 32 + 16 * (g & 1) + 4 * p4;
     const int bcol = ch * 32 + 16 * (g & 1) + 4 * p4;
     const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
     auto rowoff = [](int row, int col) { return (unsigned)(row * 128 + ((((col >> 3) ^ wswz<128>(row))) << 4) + (col & 7) * 2); };
-    const unsigned a_lane = rowoff(rbase, acol);
-    unsigned b_lane[3];
-#pragma unroll
-    for (int s = 0; s < 3; ++s) b_lane[s] = rowoff(rbase + s, bcol);
-    const int nks = (a.W + 15) >> 4;  // 16-pixel k-slices of a row
+    const unsigned a_lane = rowoff(rbase, acol), b_lane = rowoff(rbase, bcol);
+    const bool lo_half = lane < 32;
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 F[4];  // dy fragments (shift 2) of slices ks .. ks + 3 of the super-row (ring by ks % 4)
+    // x fragments of image rows g - 1, g, g + 1 and the prefetched g + 2, per slice of a row;
+    // rotated by register copies at each image row's end (VALU beside the MFMAs)
+    u32x4 Xm[SPR], X0[SPR], Xp[SPR], Xn[SPR];
+    auto rd = [&](unsigned ad) __attribute__((always_inline)) {
+        short4_t lo, hi;
+        if (ABL == 2) {
+            asm volatile("v_mov_b32 %0, %1" : "=v"(lo[0]) : "v"(ad));
+            return __builtin_bit_cast(u32x4, __builtin_shufflevector(lo, lo, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(ad));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:512" : "=v"(hi) : "v"(ad));
+        return __builtin_bit_cast(u32x4, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    auto mfma = [&](int i, u32x4 A, u32x4 B) __attribute__((always_inline)) {
+        if (ABL == 1) { asm volatile("; no mfma" : "+v"(acc[i]) : "v"(A), "v"(B)); return; }
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, A), __builtin_bit_cast(bf16x8, B),
+                                                        acc[i], 0, 0, 0);
+    };
+    // uniform slot bases of super-rows R (dy), R + 1 (dy, the reads two slices ahead) and
+    // R - 1 .. R + 2 (x); the lane offsets are added per read
+    int dsl = R0 % DS, xsl = (R0 - 1 + XS) % XS;
+    auto dy_base = [&](int i) { const int d = dsl + i; return lds0 + (unsigned)(OD + (d >= DS ? d - DS : d) * DSL); };
+    auto x_base = [&](int i) { const int x = xsl + i; return lds0 + (unsigned)(OX + (x >= XS ? x - XS : x) * SL); };
+    // x fragment of image row R * RPS + r (r = -1 .. RPS + 1), slice kk of that row
+    auto xaddr = [&](int r, int kk) __attribute__((always_inline)) {
+        const int rr = r + RPS;  // >= 0: super-row R - 1 + rr / RPS
+        return x_base(rr / RPS) + b_lane + (unsigned)(((rr % RPS) * PP + kk * 16) * 128);
+    };
 
-    // prologue: x rows r0 - 1, r0, then D steps of (dy r, x r + 1)
-    if (r0 < r1) {
-        issue_x(r0 - 1);
-        issue_x(r0);
-        for (int i = 0; i < D; ++i) issue(r0 + i);
+    int p = 0;  // image row (within its image) of the current output row
+    if (R0 < R1) {
+        __builtin_amdgcn_s_barrier();  // step R0 landed: dy R0, x R0 - 1 .. R0 + 2
+        p = (int)(((long long)R0 * RPS) % a.H);
+#pragma unroll
+        for (int kk = 0; kk < SPR; ++kk) {
+            Xm[kk] = rd(xaddr(-1, kk));
+            X0[kk] = rd(xaddr(0, kk));
+            Xp[kk] = rd(xaddr(1, kk));
+        }
+        F[0] = rd(dy_base(0) + a_lane);
+        F[1] = rd(dy_base(0) + a_lane + 2048);
     }
-    for (int r = r0; r < r1; ++r) {
-        // row r's pieces landed (the D - 1 later steps' 4 pieces per wave may stay in flight),
-        // and after the barrier every wave's have, and every wave is done with row r - 1 -
-        // whose dy slot and oldest x slot the next issue refills
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (D - 1)) : "memory");
-        __builtin_amdgcn_s_barrier();
-        issue(r + D);  // uniform count: past the range it loads zeros
-        const int p = r % a.H;
-        const unsigned abase = lds0 + OD + (r % DS) * SL + a_lane;
-        unsigned xb[3];  // kernel row rr: input row p + rr - 1 (zero row outside the image)
+    for (int R = R0; R < R1; ++R) {
 #pragma unroll
-        for (int rr = 0; rr < 3; ++rr) {
-            const int h = p + rr - 1;
-            xb[rr] = lds0 + ((h < 0 || h >= a.H) ? (unsigned)OZ : (unsigned)(OX + ((r + rr - 1 + XS) % XS) * XSL));
-        }
-        unsigned bb[9];
+        for (int ks = 0; ks < 4; ++ks) {
+            const int j = ks / SPR, kk = ks % SPR;  // image row of the super-row, slice of it
+            if (ks == 2)  // super-row R + 1 landed; every wave done with super-row R - 1
+                __builtin_amdgcn_s_barrier();
+            // everything this slice consumes was read a slice or more ago
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(F[ks]), "+v"(F[(ks + 1) & 3]), "+v"(Xm[kk]), "+v"(X0[kk]),
+                         "+v"(Xp[kk]));
+            const u32x4 f2 = F[ks], fn = F[(ks + 1) & 3];
+            // kernel rows 0 / 2 outside the image take zero operands (masks, not branches: a
+            // conditional MFMA costs accumulator copies)
+            const unsigned mt = p != 0 ? ~0u : 0u, mb = p != a.H - 1 ? ~0u : 0u;
+            const u32x4 xm = Xm[kk] & mt, x0 = X0[kk], xp = Xp[kk] & mb;
+            // shift s = 2 (the fragment as read); reads for later slices threaded behind
+            mfma(2, f2, xm);
+            __builtin_amdgcn_sched_barrier(0);
+            // dy two slices ahead (slices 2, 3 read super-row R + 1's first two)
+            F[(ks + 2) & 3] = rd(dy_base(ks >= 2 ? 1 : 0) + a_lane + (unsigned)(((ks + 2) & 3) * 2048));
+            __builtin_amdgcn_sched_barrier(0);
+            mfma(5, f2, x0);
+            __builtin_amdgcn_sched_barrier(0);
+            Xn[kk] = rd(xaddr(j + 2, kk));  // image row + 2, for the next output row
+            __builtin_amdgcn_sched_barrier(0);
+            mfma(8, f2, xp);
+            // shifts s = 1, 0: rows m + 1, m + 2 - the fragment moved up by one / two elements,
+            // the vacated top elements from lane l + 32 (lanes 0-31: this fragment's rows 8, 9)
+            // or lane l - 32 of the next fragment (lanes 32-63: its rows 0, 1)
+            const auto sw = __builtin_amdgcn_permlane32_swap(f2[0], fn[0], false, false);
+            const unsigned donor = lo_half ? sw[1] : sw[0];
+            u32x4 f1, f0;
+            f1[0] = __builtin_amdgcn_alignbit(f2[1], f2[0], 16);
+            f1[1] = __builtin_amdgcn_alignbit(f2[2], f2[1], 16);
+            f1[2] = __builtin_amdgcn_alignbit(f2[3], f2[2], 16);
+            f1[3] = __builtin_amdgcn_alignbit(donor, f2[3], 16);
+            f0[0] = f2[1]; f0[1] = f2[2]; f0[2] = f2[3]; f0[3] = donor;
+            mfma(1, f1, xm);
+            mfma(4, f1, x0);
+            mfma(7, f1, xp);
+            mfma(0, f0, xm);
+            mfma(3, f0, x0);
+            mfma(6, f0, xp);
+            __builtin_amdgcn_sched_barrier(0);
+            if (kk == SPR - 1) {  // the image row ends: rotate the x rows, next output row
+                // (the register copies read the prefetched fragments: their reads must have landed)
 #pragma unroll
-        for (int tp = 0; tp < 9; ++tp) bb[tp] = xb[tp / 3] + b_lane[tp % 3];
-        // k-slice fragments double-buffered: slice ks + 1's reads go out before slice ks's
-        // MFMAs (sched_barrier: hipcc would otherwise hoist the MFMAs above the asm reads)
-        bf16x8 af[2], bfr[2][9];
-        auto rd = [&](int ks, int c) __attribute__((always_inline)) {
-            const unsigned ko = (unsigned)(ks * 16 * 128);
-            short4_t lo, hi;
-            asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(abase + ko));
-            asm volatile("ds_read_b64_tr_b16 %0, %1 offset:512" : "=v"(hi) : "v"(abase + ko));
-            af[c] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+                for (int q = 0; q < SPR; ++q) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(Xn[q]));
 #pragma unroll
-            for (int tp = 0; tp < 9; ++tp) {
-                asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(bb[tp] + ko));
-                asm volatile("ds_read_b64_tr_b16 %0, %1 offset:512" : "=v"(hi) : "v"(bb[tp] + ko));
-                bfr[c][tp] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+                for (int q = 0; q < SPR; ++q) {
+                    Xm[q] = X0[q];
+                    X0[q] = Xp[q];
+                    Xp[q] = Xn[q];
+                }
+                p = p + 1 == a.H ? 0 : p + 1;
             }
-        };
-        rd(0, 0);
-        for (int ks = 0; ks < nks; ks += 2) {
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                if (ks + h >= nks) break;
-                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[h]), "+v"(bfr[h][0]), "+v"(bfr[h][1]), "+v"(bfr[h][2]),
-                             "+v"(bfr[h][3]), "+v"(bfr[h][4]), "+v"(bfr[h][5]), "+v"(bfr[h][6]), "+v"(bfr[h][7]),
-                             "+v"(bfr[h][8]));
-                if (ks + h + 1 < nks) rd(ks + h + 1, h ^ 1);
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int tp = 0; tp < 9; ++tp)
-                    acc[tp] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[h], bfr[h][tp], acc[tp], 0, 0, 0);
-                __builtin_amdgcn_sched_barrier(0);
-            }
         }
+        dsl = dsl + 1 == DS ? 0 : dsl + 1;
+        xsl = xsl + 1 == XS ? 0 : xsl + 1;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // D[k][c]: col = lane & 31 (c), row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5) (k)
-    // the split's slab [K][9*C]; this tile fills rows kb*64 .., columns tap*C + cb*64 ..
-    const int TC = 9 * a.C;
-    float* out = a.part + ((size_t)grp * a.splits + split) * ((size_t)a.K * TC);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // the split's partial in the accumulators' own layout, [tile][wave][tap][lane][16 e]: each
+    // lane stores its 16 values of a tap contiguously (PB = bf16: 2 x 16 B, else 4 x 16 B), a
+    // wave 64 contiguous lanes; k_wgrad_sum_raw maps (wave, tap, lane, e) back to dw[k][tap][c]
+    const size_t pos = ((((size_t)grp * a.splits + split) * (a.kt * a.ct) + tile) * 4 + wave) * 9 * 64 + lane;
+    if constexpr (PB) {
+        uint4* out = reinterpret_cast<uint4*>(a.part) + pos * 2;
 #pragma unroll
-    for (int tp = 0; tp < 9; ++tp) {
-        const int col = tp * a.C + cb * 64 + ch * 32 + (lane & 31);
+        for (int tp = 0; tp < 9; ++tp) {
+            uint32_t w[8];
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            const int row = kb * 64 + kh * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-            out[(size_t)row * TC + col] = acc[tp][e];
+            for (int e = 0; e < 8; ++e)
+                w[e] = (uint32_t)Elem<uint16_t>::f2bf(acc[tp][2 * e]) | ((uint32_t)Elem<uint16_t>::f2bf(acc[tp][2 * e + 1]) << 16);
+            out[tp * 128] = make_uint4(w[0], w[1], w[2], w[3]);
+            out[tp * 128 + 1] = make_uint4(w[4], w[5], w[6], w[7]);
         }
+    } else {
+        float4* out = reinterpret_cast<float4*>(a.part) + pos * 4;
+#pragma unroll
+        for (int tp = 0; tp < 9; ++tp)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                out[tp * 256 + q] = make_float4(acc[tp][4 * q], acc[tp][4 * q + 1], acc[tp][4 * q + 2], acc[tp][4 * q + 3]);
     }
 }
 
@@ -936,6 +806,73 @@ __global__ __launch_bounds__(256) void k_wgrad_sum(const float* __restrict__ par
         acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
     *o = acc;
+}
+
+// dw[k][tap][c] (+)= sum over splits of k_wgrad_halo64's raw partials ([G][splits][tile][wave]
+// [tap][lane][16 e], fp32 or bf16): a thread owns 8 values (half of one lane's 16) of one
+// (tile, wave, tap, lane) position, R split lanes per position sum splits r, r + R, ... and
+// combine in lane order through LDS (fixed order: deterministic), then scatter to dw.
+template <int R, bool PB>
+__global__ __launch_bounds__(256) void k_wgrad_sum_raw(const void* __restrict__ part, int splits, int tiles, int kt,
+                                                       int K, int C, int accumulate, float* __restrict__ dw,
+                                                       long long gs_dw) {
+    constexpr int CPB = 256 / R;
+    const size_t npos = (size_t)tiles * 4 * 9 * 64 * 2;  // 8-value halves per split slab
+    const int g = blockIdx.y;
+    dw += g * gs_dw;
+    const int t = threadIdx.x, col = t % CPB, r = t / CPB;
+    const size_t h = (size_t)blockIdx.x * CPB + col;  // half index within a slab
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    if (h < npos) {
+        for (int sp = r; sp < splits; sp += R) {
+            const size_t i = ((size_t)g * splits + sp) * npos + h;
+            if constexpr (PB) {
+                const uint4 v = reinterpret_cast<const uint4*>(part)[i];
+                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    acc[2 * q] += __uint_as_float(w[q] << 16);
+                    acc[2 * q + 1] += __uint_as_float(w[q] & 0xffff0000u);
+                }
+            } else {
+                const float4 v0 = reinterpret_cast<const float4*>(part)[2 * i];
+                const float4 v1 = reinterpret_cast<const float4*>(part)[2 * i + 1];
+                acc[0] += v0.x; acc[1] += v0.y; acc[2] += v0.z; acc[3] += v0.w;
+                acc[4] += v1.x; acc[5] += v1.y; acc[6] += v1.z; acc[7] += v1.w;
+            }
+        }
+    }
+    if constexpr (R > 1) {
+        __shared__ float red[8][256];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) red[e][t] = acc[e];
+        __syncthreads();
+        if (r != 0) return;
+#pragma unroll
+        for (int q = 1; q < R; ++q)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[e] += red[e][q * CPB + col];
+    }
+    if (h >= npos) return;
+    // h -> (tile, wave, tap, lane, half): half-slab of 8 values e = 8 half .. + 7
+    size_t q = h;
+    const int half = (int)(q & 1); q >>= 1;
+    const int lane = (int)(q % 64); q /= 64;
+    const int tp = (int)(q % 9); q /= 9;
+    const int wave = (int)(q % 4); q /= 4;
+    const int tile = (int)q;
+    const int kb = tile % kt, cb = tile / kt, kh = wave & 1, ch = wave >> 1;
+    const int TC = 9 * C;
+    const int c = tp * C + cb * 64 + ch * 32 + (lane & 31);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int e = 8 * half + j;
+        const int k = kb * 64 + kh * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+        float* o = dw + (size_t)k * TC + c;
+        *o = accumulate ? *o + acc[j] : acc[j];
+    }
 }
 
 // dw = sum over splits (fixed order); also the [K][T][Cpad] -> [K][T][Creal] crop
@@ -1038,38 +975,18 @@ static int g_wgrad_wr = [] {
     return e ? atoi(e) : 2;
 }();
 
-// weight-gradient main loops (GM_WGRAD_LOOP at load, gm_conv_set_wgrad_loop): bit 0 =
-// k_conv_wgrad_ring<.., 32, 4> (four-deep ring of 32-pixel steps, counted vmcnt, raw barrier)
-// instead of k_conv_wgrad4 (two buffers, vmcnt(0) drain per step); bit 1 = k_wgrad_halo64 for
-// the layer-1 shape (3x3 / s1 / p1, C = K = 64, W <= 62)
-static int g_wgrad_loop = [] {  // default 2: k_wgrad_halo64 for layer 1 (62 vs 77 us per launch)
+// weight-gradient kernel choice for 3x3 / s1 / p1 shapes with W <= 62 (GM_WGRAD_LOOP at load,
+// gm_conv_set_wgrad_loop): bit 1 = k_wgrad_halo64 for 64 channels (layer 1), bit 2 = also for
+// 128 channels (layer 2); otherwise k_conv_wgrad4.  Default 6 (r04, B = 64 two-view step:
+// layer 1 61.9 -> 44.9 us and layer 2 54.6 -> 46.6 us per launch with the sum; step 3.98 ->
+// 3.91 ms against bit 1 alone).
+static int g_wgrad_loop = [] {
     const char* e = getenv("GM_WGRAD_LOOP");
-    return e ? atoi(e) : 2;
+    return e ? atoi(e) : 6;
 }();
 
 template <int MT, int NT>
-static int launch_wgrad_ring(WgradArgs a, int grid, hipStream_t st) {
-    constexpr int BK = 32, NS = 4;
-    const size_t lds = (size_t)NS * BK * 2 * (64 * MT + 64 * NT);
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_conv_wgrad_ring<MT, NT, BK, NS>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr = true;
-    }
-    a.adv_b = BK / (a.P * a.Q);
-    a.adv_p = (BK % (a.P * a.Q)) / a.Q;
-    a.adv_q = (BK % (a.P * a.Q)) % a.Q;
-    k_conv_wgrad_ring<MT, NT, BK, NS><<<grid, 256, lds, st>>>(a);
-    return check_launch("k_conv_wgrad_ring");
-}
-
-template <int MT, int NT>
 static int launch_wgrad4(const WgradArgs& a, int grid, hipStream_t st) {
-    if constexpr (MT <= 2 && NT <= 2) {
-        if ((g_wgrad_loop & 1) && !(g_wgrad_wr == 1 || (g_wgrad_wr == 2 && a.T == 1)))
-            return launch_wgrad_ring<MT, NT>(a, grid, st);
-    }
     const size_t lds = (size_t)2 * 64 * 2 * (64 * MT + 64 * NT);
     static bool attr = false;  // idempotent, safe to race
     if (!attr) {
@@ -1087,25 +1004,34 @@ static gm_conv_desc_hw to_hw(const gm_conv_desc* d) {
     return gm_conv_desc_hw{d->N, d->H, d->W, d->C, d->K, d->R, d->S, d->stride, d->stride, d->pad, d->pad};
 }
 
-// k_wgrad_halo64 serves the layer-1 shape: splits = workgroups per view group
+// k_wgrad_halo64's split partials in bf16 (halves the partial-slab traffic; the splits are
+// summed in fp32) or fp32
+static constexpr bool kH64Bf16Part = true;
+
+// k_wgrad_halo64 serves 3x3 / s1 / p1 shapes with W <= 62: image rows of PP = 16, 32 or 64
+// positions (PP >= W + 2), 64 / PP of them per super-row
+static int halo64_pp(int W) { return W + 2 <= 16 ? 16 : (W + 2 <= 32 ? 32 : 64); }
 static bool halo64_ok(const gm_conv_desc_hw* d) {
-    const int maxc = (g_wgrad_loop & 4) ? 128 : 64;  // bit 2: also the 128-channel (layer-2) shape
+    // bit 1: 64 channels (layer 1), bit 2: up to 128 (layer 2), bit 3: up to 512 (layers 3, 4)
+    const int maxc = (g_wgrad_loop & 8) ? 512 : ((g_wgrad_loop & 4) ? 128 : 64);
     return (g_wgrad_loop & 2) && d->R == 3 && d->S == 3 && d->stride_h == 1 && d->stride_w == 1 && d->pad_h == 1 &&
            d->pad_w == 1 && d->C % 64 == 0 && d->K % 64 == 0 && d->C <= maxc && d->K <= maxc && d->W <= 62 &&
-           d->W >= 1 && d->H >= 1 && (long long)d->N * d->H * d->W * (d->C > d->K ? d->C : d->K) < (1ll << 31);
+           d->W >= 1 && d->H >= 64 / halo64_pp(d->W) && d->N >= 1 &&
+           (long long)d->N * d->H * d->W * (d->C > d->K ? d->C : d->K) < (1ll << 31);
 }
 // workgroups per (view group, channel tile): about one per CU in all
 static int halo64_splits(const gm_conv_desc_hw* d, int G) {
-    const int rows = d->N * d->H;
+    const int rps = 64 / halo64_pp(d->W);
+    const int srows = (d->N * d->H + rps - 1) / rps;
     const int tiles = (d->K / 64) * (d->C / 64) * G;
     int sp = 256 / tiles;
     if (sp < 1) sp = 1;
-    return sp < rows ? sp : rows;
+    return sp < srows ? sp : srows;
 }
 
 extern "C" size_t gm_conv2d_wgrad_grouped_scratch(const gm_conv_desc_hw* d, int G) {
     if (!d || d->stride_h < 1 || d->stride_w < 1 || G < 1) return 0;
-    if (halo64_ok(d)) return (size_t)G * halo64_splits(d, G) * d->K * 9 * d->C * sizeof(float);
+    if (halo64_ok(d)) return (size_t)G * halo64_splits(d, G) * d->K * 9 * d->C * (kH64Bf16Part ? 2 : 4);
     const WPlan w = plan(d, G);
     const size_t slab = (size_t)d->K * d->R * d->S * d->C;
     return (size_t)G * w.splits * slab * sizeof(float);
@@ -1147,36 +1073,55 @@ extern "C" int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, con
         h.part = (float*)scratch;
         h.N = d->N; h.H = d->H; h.W = d->W;
         h.rows = d->N * d->H;
+        const int pp = halo64_pp(d->W);
+        h.srows = (h.rows + 64 / pp - 1) / (64 / pp);
         h.splits = halo64_splits(d, G);
-        h.rpw = (h.rows + h.splits - 1) / h.splits;
+        h.rpw = (h.srows + h.splits - 1) / h.splits;
         h.K = d->K; h.C = d->C; h.kt = d->K / 64; h.ct = d->C / 64;
         h.gs_dy = (long long)d->N * d->H * d->W * d->K;
         h.gs_x = (long long)d->N * d->H * d->W * d->C;
-        constexpr int D = 2;
-        const size_t lds = (size_t)(D + 3) * (8192 + 256) + 8192 + 1024 + (size_t)(D + 1) * 8192;
-        static bool attr = false;
-        if (!attr) {
-            (void)hipFuncSetAttribute((const void*)k_wgrad_halo64<D>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            attr = true;
-        }
-        k_wgrad_halo64<D><<<h.splits * h.kt * h.ct * G, 256, lds, st0>>>(h);
+        // D = 3 super-rows of LDS-DMA in flight
+        const int nblk = h.splits * h.kt * h.ct * G;
+        auto go = [&](auto pc, auto ac) {
+            constexpr int D = 3, PP = decltype(pc)::value, AB = decltype(ac)::value;
+            constexpr size_t lds = (size_t)(D + 3) * 8192 + (size_t)(D + 1) * (8192 + 256);
+            static bool attr = false;
+            if (!attr) {
+                (void)hipFuncSetAttribute((const void*)k_wgrad_halo64<D, PP, kH64Bf16Part, AB>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                attr = true;
+            }
+            k_wgrad_halo64<D, PP, kH64Bf16Part, AB><<<nblk, 512, lds, st0>>>(h);
+        };
+        static const int abl = [] { const char* e = getenv("GM_H64_ABL"); return e ? atoi(e) : 0; }();
+        using A0 = std::integral_constant<int, 0>;
+        if (pp == 16) go(std::integral_constant<int, 16>{}, A0{});
+        else if (pp == 32) go(std::integral_constant<int, 32>{}, A0{});
+        else if (abl == 1) go(std::integral_constant<int, 64>{}, std::integral_constant<int, 1>{});
+        else if (abl == 2) go(std::integral_constant<int, 64>{}, std::integral_constant<int, 2>{});
+        else if (abl == 3) go(std::integral_constant<int, 64>{}, std::integral_constant<int, 3>{});
+        else go(std::integral_constant<int, 64>{}, A0{});
         int rc = check_launch("k_wgrad_halo64");
         if (rc) return rc;
-        const size_t slab = (size_t)d->K * 9 * d->C;
-        const size_t ncol = slab / 4;
+        const int tiles = h.kt * h.ct;
+        const size_t npos = (size_t)tiles * 4 * 9 * 64 * 2;  // 8-value halves per split slab
         int R = 1;
-        while (R < 32 && R * 2 <= h.splits && (ncol * R + 255) / 256 < 512) R *= 2;
-        const dim3 gg((unsigned)((ncol + 256 / R - 1) / (256 / R)), (unsigned)G);
-        float* part = h.part;
+        while (R < 32 && R * 2 <= h.splits && (npos * R + 255) / 256 < 512) R *= 2;
+        const dim3 gg((unsigned)((npos + 256 / R - 1) / (256 / R)), (unsigned)G);
+        auto sum = [&](auto rc_) {
+            constexpr int RR = decltype(rc_)::value;
+            k_wgrad_sum_raw<RR, kH64Bf16Part><<<gg, 256, 0, st0>>>(h.part, h.splits, tiles, h.kt, d->K, d->C, accumulate,
+                                                                   dw, dw_stride);
+        };
         switch (R) {
-            case 1: k_wgrad_sum<1><<<gg, 256, 0, st0>>>(part, h.splits, slab, accumulate, dw, dw_stride); break;
-            case 2: k_wgrad_sum<2><<<gg, 256, 0, st0>>>(part, h.splits, slab, accumulate, dw, dw_stride); break;
-            case 4: k_wgrad_sum<4><<<gg, 256, 0, st0>>>(part, h.splits, slab, accumulate, dw, dw_stride); break;
-            case 8: k_wgrad_sum<8><<<gg, 256, 0, st0>>>(part, h.splits, slab, accumulate, dw, dw_stride); break;
-            case 16: k_wgrad_sum<16><<<gg, 256, 0, st0>>>(part, h.splits, slab, accumulate, dw, dw_stride); break;
-            default: k_wgrad_sum<32><<<gg, 256, 0, st0>>>(part, h.splits, slab, accumulate, dw, dw_stride); break;
+            case 1: sum(std::integral_constant<int, 1>{}); break;
+            case 2: sum(std::integral_constant<int, 2>{}); break;
+            case 4: sum(std::integral_constant<int, 4>{}); break;
+            case 8: sum(std::integral_constant<int, 8>{}); break;
+            case 16: sum(std::integral_constant<int, 16>{}); break;
+            default: sum(std::integral_constant<int, 32>{}); break;
         }
-        return check_launch("k_wgrad_sum");
+        return check_launch("k_wgrad_sum_raw");
     }
     WgradArgs a;
     memset(&a, 0, sizeof(a));
@@ -1268,8 +1213,8 @@ extern "C" int gm_conv_set_wgrad_staging(int wr) {
 }
 
 extern "C" int gm_conv_set_wgrad_loop(int mode) {
-    GM_REQUIRE(mode >= 0 && mode <= 7,
-               "gm_conv_set_wgrad_loop: bit 0 ring main loop, bit 1 layer-1 halo kernel, bit 2 also layer 2");
+    GM_REQUIRE(mode >= 0 && mode <= 15 && !(mode & 1),
+               "gm_conv_set_wgrad_loop: bit 1 halo kernel for 64 channels, bit 2 up to 128, bit 3 up to 512");
     g_wgrad_loop = mode;
     return GM_OK;
 }

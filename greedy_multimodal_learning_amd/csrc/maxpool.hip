@@ -31,10 +31,13 @@ struct PoolArgs {
 
 // BNRELU: the pooled values are relu(x*sc + sh) rounded to E, i.e. the stem's BatchNorm +
 // ReLU applied on the fly (coef = sc[C], sh[C]): the normalised activation is never
-// written, bit-identical to BN-apply (fmaf, fmaxf, RNE store) followed by the plain pool
+// written, bit-identical to BN-apply (fmaf, fmaxf, RNE store) followed by the plain pool.
+// xsel (optional): the raw input value each output selected (its argmax's x), so the BN
+// backward's channel sums need only the pooled tensors (k_stem_pool_bn_bwd pass 1)
 template <typename E, bool BNRELU = false>
 __global__ __launch_bounds__(256) void k_maxpool_fwd(PoolArgs a, const void* __restrict__ x, void* __restrict__ y,
-                                                     uint2* __restrict__ idx, const float* __restrict__ coef = nullptr) {
+                                                     uint2* __restrict__ idx, const float* __restrict__ coef = nullptr,
+                                                     void* __restrict__ xsel = nullptr) {
     const unsigned total = (unsigned)a.N * a.P * a.Q * a.C8;  // < 2^31 (checked on the host)
     for (unsigned i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
         unsigned t = a.fd_c8.div(i);
@@ -45,7 +48,7 @@ __global__ __launch_bounds__(256) void k_maxpool_fwd(PoolArgs a, const void* __r
         const int p = (int)(t2 - n_ * a.P);
         const int n = (int)n_;
         const int h0 = p * a.s - a.pad, w0 = q * a.s - a.pad;
-        float m[8];
+        float m[8], xs[8];
         uint32_t ix[8];
         float sc[8], sh[8];
         if (BNRELU) {
@@ -61,6 +64,7 @@ __global__ __launch_bounds__(256) void k_maxpool_fwd(PoolArgs a, const void* __r
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             m[j] = -__builtin_huge_valf();
+            xs[j] = 0.f;
             ix[j] = first;
         }
         if (a.k == 3) {
@@ -82,6 +86,7 @@ __global__ __launch_bounds__(256) void k_maxpool_fwd(PoolArgs a, const void* __r
                     const float z = BNRELU ? round_to<E>(fmaxf(fmaf(v[u][j], sc[j], sh[j]), 0.f)) : v[u][j];
                     if (z > m[j] || __builtin_isnan(z)) {
                         m[j] = z;
+                        xs[j] = v[u][j];
                         ix[j] = (uint32_t)u;
                     }
                 }
@@ -93,8 +98,10 @@ __global__ __launch_bounds__(256) void k_maxpool_fwd(PoolArgs a, const void* __r
             for (int c = 0; c < a.k; ++c) {
                 const int w = w0 + c;
                 if (w < 0 || w >= a.W) continue;
-                float v[8];
+                float v[8], raw[8];
                 V8<E>::ld(x, (((long long)n * a.H + h) * a.W + w) * a.C8 + cg, v);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) raw[j] = v[j];
                 if (BNRELU) {
 #pragma unroll
                     for (int j = 0; j < 8; ++j) v[j] = round_to<E>(fmaxf(fmaf(v[j], sc[j], sh[j]), 0.f));
@@ -104,12 +111,14 @@ __global__ __launch_bounds__(256) void k_maxpool_fwd(PoolArgs a, const void* __r
                 for (int j = 0; j < 8; ++j) {
                     if (v[j] > m[j] || __builtin_isnan(v[j])) {
                         m[j] = v[j];
+                        xs[j] = raw[j];
                         ix[j] = pos;
                     }
                 }
             }
         }
         V8<E>::st(y, i, m);  // the max of E values is an E value: the store is exact
+        if (xsel) V8<E>::st(xsel, i, xs);  // an E value loaded from x: exact
         idx[i] = make_uint2(ix[0] | ix[1] << 8 | ix[2] << 16 | ix[3] << 24, ix[4] | ix[5] << 8 | ix[6] << 16 | ix[7] << 24);
     }
 }
@@ -257,9 +266,9 @@ extern "C" int gm_maxpool2d_fwd_bf16(const gm_pool_desc* d, const void* x, void*
 }
 
 // G view groups of d->N images each, stacked along the batch; group g applies the
-// coefficients coef + g*2C
+// coefficients coef + g*2C; xsel (optional, y-shaped) receives each output's selected raw x
 extern "C" int gm_bn_relu_maxpool2d_fwd_grouped_bf16(const gm_pool_desc* d, int G, const void* x, const float* coef,
-                                                     void* y, void* idx, void* stream) {
+                                                     void* y, void* idx, void* xsel, void* stream) {
     const char* fn = "gm_bn_relu_maxpool2d_fwd_grouped_bf16";
     GM_REQUIRE(d && G >= 1 && G <= 64, "%s: 1..64 groups", fn);
     gm_pool_desc dg = *d;
@@ -271,13 +280,13 @@ extern "C" int gm_bn_relu_maxpool2d_fwd_grouped_bf16(const gm_pool_desc* d, int 
     GM_REQUIRE(x && coef && y && idx, "%s: null pointer", fn);
     const long long n = (long long)a.N * a.P * a.Q * a.C8;
     hipLaunchKernelGGL((k_maxpool_fwd<uint16_t, true>), dim3(grid_for(n)), dim3(256), 0, as_stream(stream), a, x, y,
-                       static_cast<uint2*>(idx), coef);
+                       static_cast<uint2*>(idx), coef, xsel);
     return check_launch("k_maxpool_fwd<bnrelu>");
 }
 
 extern "C" int gm_bn_relu_maxpool2d_fwd_bf16(const gm_pool_desc* d, const void* x, const float* coef, void* y,
                                              void* idx, void* stream) {
-    return gm_bn_relu_maxpool2d_fwd_grouped_bf16(d, 1, x, coef, y, idx, stream);
+    return gm_bn_relu_maxpool2d_fwd_grouped_bf16(d, 1, x, coef, y, idx, nullptr, stream);
 }
 
 extern "C" int gm_maxpool2d_bwd_bf16(const gm_pool_desc* d, const void* dy, const void* idx, void* dx, void* stream) {

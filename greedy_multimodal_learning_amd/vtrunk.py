@@ -512,11 +512,15 @@ class _VBNReluPoolFn(torch.autograd.Function):
         P, Q = (H + 2 * pad - k) // s + 1, (W + 2 * pad - k) // s + 1
         y = torch.empty(GN, C, P, Q, device=dev, dtype=BF, memory_format=CL)
         idx = torch.empty(GN, P, Q, C, device=dev, dtype=torch.uint8)
+        # the selected raw x per pooled output: the fused backward's statistics pass reads it
+        # (and the pooled gradient) instead of x, the gradient and the argmax
+        fused_bwd = FUSED_STEM_BWD and (k, s, pad, C) == (3, 2, 1, 64)
+        xsel = torch.empty(GN, P, Q, C, device=dev, dtype=BF) if fused_bwd else None
         d = L.PoolDesc(N, H, W, C, k, s, pad)
         L.check(lib.gm_bn_relu_maxpool2d_fwd_grouped_bf16(ctypes.byref(d), G, xb.data_ptr(), coef.data_ptr(),
-                                                          y.data_ptr(), idx.data_ptr(), st),
+                                                          y.data_ptr(), idx.data_ptr(), L.ptr(xsel), st),
                 "gm_bn_relu_maxpool2d_fwd_grouped_bf16")
-        ctx.save_for_backward(xb, coef, sm, si, idx, *gammas, *betas)
+        ctx.save_for_backward(xb, coef, sm, si, idx, xsel, *gammas, *betas)
         ctx.meta = (G, k, s, pad)
         return y
 
@@ -524,13 +528,13 @@ class _VBNReluPoolFn(torch.autograd.Function):
     def backward(ctx, dy):
         flush_wgrads()  # the trunk's remaining weight gradients overlap the stem's backward
         lib = L.load()
-        xb, coef, sm, si, idx, *prm = ctx.saved_tensors
+        xb, coef, sm, si, idx, xsel, *prm = ctx.saved_tensors
         G, k, s, pad = ctx.meta
         gammas, betas = prm[:G], prm[G:]
         GN, C, H, W = xb.shape
         dy = _nhwc(dy.to(BF))
         want_w, want_b = any(ctx.needs_input_grad[7:7 + G]), any(ctx.needs_input_grad[7 + G:])
-        if FUSED_STEM_BWD and (k, s, pad, C) == (3, 2, 1, 64) and (want_w or want_b):
+        if xsel is not None and (want_w or want_b):
             # the pool's input gradient is gathered inside the BN backward's two passes
             # (gm_bn_relu_maxpool2d_bwd_grouped_bf16): never written
             N = GN // G
@@ -543,8 +547,8 @@ class _VBNReluPoolFn(torch.autograd.Function):
             buf = _bn_scratch_g(xb.device, M, C, G)
             d = L.PoolDesc(N, H, W, C, k, s, pad)
             L.check(lib.gm_bn_relu_maxpool2d_bwd_grouped_bf16(ctypes.byref(d), G, dy.data_ptr(), idx.data_ptr(),
-                                                              L.arr(L.BnBwd, descs), buf.data_ptr(), buf.numel(),
-                                                              L.stream_of(xb.device)),
+                                                              xsel.data_ptr(), L.arr(L.BnBwd, descs), buf.data_ptr(),
+                                                              buf.numel(), L.stream_of(xb.device)),
                     "gm_bn_relu_maxpool2d_bwd_grouped_bf16")
             if sunk:
                 for p in list(gammas) + list(betas):

@@ -375,10 +375,10 @@ int gm_conv_set_splitk(int target);
 /* Weight-gradient tile form (process-wide; GM_WGRAD_WIDE at load): bit 0 takes
  * 256-row tiles for K >= 256, bit 1 256-column (tap, channel) tiles; 0 = 128 x 128. */
 int gm_conv_set_wgrad_wide(int mode);
-/* Weight-gradient main loops (A/B; GM_WGRAD_LOOP at load): bit 0 = 4-deep LDS-DMA ring of
- * 32-pixel steps with counted vmcnt waits (k_conv_wgrad_ring; bit-identical to the two-buffer
- * k_conv_wgrad4), bit 1 = k_wgrad_halo64 for the layer-1 shape (3x3 / s1 / p1, 64 -> 64:
- * whole-gradient accumulators, one new input row staged per output row). */
+/* Weight-gradient kernel for 3x3 / s1 / p1 shapes with W <= 62 (GM_WGRAD_LOOP at load; default
+ * 6): bit 1 = k_wgrad_halo64 (64 x 9 x 64 gradient blocks in one workgroup's accumulators, one
+ * input row staged per output row, dedicated loader waves) for 64 channels, bit 2 = also for
+ * 128 channels; the rest take k_conv_wgrad4.  Bit 0 is reserved (must be 0). */
 int gm_conv_set_wgrad_loop(int mode);
 /* Weight-gradient operand staging: 0 = LDS-DMA pieces, 1 = register-staged (global_load_dwordx4
  * two steps ahead + ds_write_b128; same LDS image and arithmetic), 2 (default) = register-staged
@@ -573,7 +573,11 @@ int gm_maxpool2d_bwd_bf16(const gm_pool_desc* d, const void* dy, const void* idx
  * d: ONE view group's pool (N images; k 3, stride 2, pad 1, C 64); dy_pool / idx: the G
  * groups' pooled gradient and argmax stacked ([G*N][P][Q][C], gm_bn_relu_maxpool2d_fwd_*);
  * ps[g]: group g's BN backward with relu, fwd_coef, y = dres = NULL (dy unused); scratch:
- * gm_bn_scratch_grouped(N*H*W, C, G) bytes of the grouped layout. */
+ * gm_bn_scratch_grouped(N*H*W, C, G) bytes of the grouped layout.  xsel (optional): the
+ * forward's selected raw x (gm_bn_relu_maxpool2d_fwd_grouped_bf16); with it pass 1 reduces
+ * over the pooled tensors alone (pool gradient + xsel, a quarter of the pixels, no x read:
+ * sum over windows of dy_pool * mask and of dy_pool * mask * (xsel - mean), linear in the
+ * per-pixel sums; the per-pixel bf16 rounding of the gathered gradient is skipped there). */
 /* The stem's BatchNorm statistics without a pass over its output: the stem convolution
  * (gm_conv2d_fwd_grouped_stats_bf16, k_conv_stem's shapes, 64 output channels) adds every
  * workgroup's (sum, sum of squares) of its stored bf16 outputs into a partial row, and
@@ -586,16 +590,18 @@ int gm_conv2d_fwd_grouped_stats_bf16(const gm_conv_desc_hw* d, int G, const void
                                      long long w_stride, void* y, float* stats, int rows, void* stream);
 int gm_bn_fwd_stats_finalize_grouped(const gm_bn_fwd* ps, int G, float* stats, int rows, void* stream);
 int gm_bn_relu_maxpool2d_bwd_grouped_bf16(const gm_pool_desc* d, int G, const void* dy_pool, const void* idx,
-                                          const gm_bn_bwd* ps, void* scratch, size_t scratch_bytes, void* stream);
+                                          const void* xsel, const gm_bn_bwd* ps, void* scratch, size_t scratch_bytes,
+                                          void* stream);
 /* the stem's BatchNorm + ReLU + MaxPool forward: pools relu(x*sc + sh) rounded to bf16
  * (coef = sc[C], sh[C] from gm_bn_fwd_stats_bf16), bit-identical to gm_bn_fwd_train's
  * apply followed by gm_maxpool2d_fwd_bf16, without writing the normalised activation */
 int gm_bn_relu_maxpool2d_fwd_bf16(const gm_pool_desc* d, const void* x, const float* coef, void* y, void* idx,
                                   void* stream);
 /* G view groups of d->N images each stacked along the batch (x [G*N][H][W][C]); group g
- * applies coef + g*2C (gm_bn_fwd_stats_grouped_bf16's coef_out of group g) */
+ * applies coef + g*2C (gm_bn_fwd_stats_grouped_bf16's coef_out of group g); xsel (optional,
+ * y-shaped) receives the raw x each output selected */
 int gm_bn_relu_maxpool2d_fwd_grouped_bf16(const gm_pool_desc* d, int G, const void* x, const float* coef, void* y,
-                                          void* idx, void* stream);
+                                          void* idx, void* xsel, void* stream);
 /* fp32 activations (the reference-precision trunk), same index format */
 int gm_maxpool2d_fwd_f32(const gm_pool_desc* d, const void* x, void* y, void* idx, void* stream);
 int gm_maxpool2d_bwd_f32(const gm_pool_desc* d, const void* dy, const void* idx, void* dx, void* stream);

@@ -41,7 +41,7 @@ MODEL_CASES = [
     dict(id="m224b2", B=2, H=224, W=224, seed=11),
     dict(id="m32c0", B=3, H=32, W=32, seed=2, cur=True, caring=0, gpu_tol=5e-3),
     dict(id="m32c1", B=3, H=32, W=32, seed=3, cur=True, caring=1, gpu_tol=5e-3),
-    dict(id="m224", B=1, H=224, W=224, seed=4, gpu_tol=1e-2),
+    dict(id="m224", B=1, H=224, W=224, seed=4, gpu_tol=1e-3),  # measured 5.6e-7 (r04)
 ]
 
 # F3 - gating trace through the reference's own Model_.train_loop

@@ -234,44 +234,6 @@ def test_conv_splitk_spin_timeout_never_silent(dev):
     assert torch.equal(G.conv_fwd(x, w, st, pad), ref)
 
 
-@pytest.mark.parametrize("shape", [(64, 64, 56, 56), (2, 64, 28, 28), (3, 64, 9, 11), (1, 64, 7, 7), (2, 64, 5, 40)],
-                         ids=lambda s: "x".join(map(str, s)))
-def test_conv_resident_weight_layer1(dev, shape):
-    """3x3/s1 64->64 convolutions (ResNet layer 1) run the resident-weight kernel: weights
-    held in LDS by a persistent workgroup, whole-row tiles with a double-buffered input
-    halo.  Forward, input gradient and the fused gradient join (addend) equal the fp32
-    reference and the im2col kernel within bf16 output rounding."""
-    from greedy_multimodal_learning_amd import _lib as L
-    from greedy_multimodal_learning_amd import conv as G
-    lib = L.load()
-    N, C, H, W = shape
-    g = torch.Generator(device="cuda").manual_seed(sum(shape))
-    CL = torch.channels_last
-    x = torch.randn(N, C, H, W, device=dev, generator=g).bfloat16().contiguous(memory_format=CL)
-    w = (torch.randn(C, C, 3, 3, device=dev, generator=g) / (C * 9) ** 0.5).bfloat16().contiguous(memory_format=CL)
-    dy = torch.randn(N, C, H, W, device=dev, generator=g).bfloat16().contiguous(memory_format=CL)
-    add = torch.randn(N, C, H, W, device=dev, generator=g).bfloat16().contiguous(memory_format=CL)
-    wt = w.permute(1, 0, 2, 3).contiguous(memory_format=CL)
-    outs = {}
-    try:
-        for rw in (0, 1):
-            L.check(lib.gm_conv_set_rw(rw), "gm_conv_set_rw")
-            outs[rw] = (G.conv_fwd(x, w, 1, 1), G.conv_dgrad_t(dy, wt, H, W, 1, 1),
-                        G.conv_dgrad_t(dy, wt, H, W, 1, 1, addend=add))
-        torch.cuda.synchronize()
-    finally:
-        lib.gm_conv_set_rw(1)
-    yr = F.conv2d(x.float(), w.float(), padding=1)
-    dxr = torch.ops.aten.convolution_backward(dy.float(), x.float(), w.float(), None, [1, 1], [1, 1], [1, 1],
-                                              False, [0, 0], 1, [True, False, False])[0]
-    y, dx, dxa = outs[1]
-    _close(y, yr, 1e-2)
-    _close(dx, dxr, 1e-2)
-    _close(dxa, dxr + add.float(), 1e-2)
-    for a_, b_ in zip(outs[1], outs[0]):
-        _close(a_, b_, 1e-2)
-
-
 @pytest.mark.parametrize("shape", [(4, 128, 28, 28, 128, 3, 3, 1, 1), (4, 64, 56, 56, 128, 3, 3, 2, 1),
                                    (64, 256, 14, 14, 256, 3, 3, 1, 1), (5, 128, 7, 7, 256, 1, 1, 2, 0),
                                    (4, 64, 56, 56, 64, 3, 3, 1, 1)],
@@ -403,11 +365,10 @@ def test_wgrad_staging_forms_bit_identical(dev, shape):
                                    (64, 512, 7, 7, 512, 3, 1, 1), (7, 256, 14, 14, 512, 1, 2, 0),
                                    (2, 8, 115, 115, 64, 7, 1, 0)],
                          ids=lambda s: "x".join(map(str, s)))
-def test_wgrad_ring_bit_identical(dev, shape):
-    """k_conv_wgrad_ring (4-deep LDS-DMA ring of 32-pixel steps, counted vmcnt) stages the
-    same LDS image and issues the same MFMAs in the same pixel order as k_conv_wgrad4:
-    bit-identical weight gradients, grouped over two views, split-K and ragged tails
-    included (B = 3, 5, 7)."""
+def test_wgrad4_grouped_vs_fp32(dev, shape):
+    """k_conv_wgrad4 (the im2col weight gradient every shape can take; the halo kernel off so
+    the 3x3 / s1 shapes take it too) grouped over two views, split-K and ragged tails included
+    (B = 3, 5, 7), plain and accumulating, against fp32 PyTorch per group."""
     import ctypes
     from greedy_multimodal_learning_amd import _lib as L
     from greedy_multimodal_learning_amd import conv as CV
@@ -419,84 +380,49 @@ def test_wgrad_ring_bit_identical(dev, shape):
     dy = torch.randn(G * N, P, Q, K, device=dev).bfloat16()
     lib = L.load()
     d = CV._desc_hw(N, H, W, C, K, R, R, st, st, pad, pad)
-    need = lib.gm_conv2d_wgrad_grouped_scratch(ctypes.byref(d), G)
-    scr = torch.empty(max(need, 16), device=dev, dtype=torch.uint8)
     outs = []
     try:
-        for ring in (0, 1):
-            L.check(lib.gm_conv_set_wgrad_loop(ring), "ring")
-            for acc in (0, 1):
-                dw = torch.full((G, K, R, R, C), 0.25, device=dev, dtype=torch.float32)
-                L.check(lib.gm_conv2d_wgrad_grouped_bf16(ctypes.byref(d), G, dy.data_ptr(), x.data_ptr(),
-                                                          dw.data_ptr(), K * R * R * C, C, acc, scr.data_ptr(),
-                                                          need, L.stream_of(dev)), "wgrad")
-                outs.append(dw)
+        L.check(lib.gm_conv_set_wgrad_loop(0), "loop")
+        need = lib.gm_conv2d_wgrad_grouped_scratch(ctypes.byref(d), G)
+        scr = torch.empty(max(need, 16), device=dev, dtype=torch.uint8)
+        for acc in (0, 1):
+            dw = torch.full((G, K, R, R, C), 0.25, device=dev, dtype=torch.float32)
+            L.check(lib.gm_conv2d_wgrad_grouped_bf16(ctypes.byref(d), G, dy.data_ptr(), x.data_ptr(),
+                                                      dw.data_ptr(), K * R * R * C, C, acc, scr.data_ptr(),
+                                                      need, L.stream_of(dev)), "wgrad")
+            outs.append(dw)
         torch.cuda.synchronize()
     finally:
-        L.check(lib.gm_conv_set_wgrad_loop(2), "ring")  # the default
-    assert torch.equal(outs[0], outs[2]) and torch.equal(outs[1], outs[3])
-    # and it is a weight gradient: group 0 against fp32 PyTorch
-    xr = x[:N].float().permute(0, 3, 1, 2)
-    gr = dy[:N].float().permute(0, 3, 1, 2)
-    ref = torch.nn.grad.conv2d_weight(xr, (K, C, R, R), gr, stride=st, padding=pad)
-    got = outs[0][0].permute(0, 3, 1, 2)
-    err = float((got - ref).abs().max() / ref.abs().max())
-    assert err < 2e-3, err
-
-
-@pytest.mark.parametrize("shape", [(64, 64, 56, 56), (2, 64, 28, 28), (3, 64, 9, 11), (1, 64, 7, 7), (2, 64, 5, 40)],
-                         ids=lambda s: "x".join(map(str, s)))
-def test_conv_rw2_bit_identical(dev, shape):
-    """k_conv_rw2 (weights resident in VGPRs, 256-row tiles, four accumulators per wave)
-    issues the same MFMAs in the same k order per output as k_conv_rw: forward, input
-    gradient and the fused gradient join (addend) are bit-identical; also as the two-view
-    grouped launch the view-batched trunk issues."""
-    import ctypes
-    from greedy_multimodal_learning_amd import _lib as L
-    from greedy_multimodal_learning_amd import conv as G
-    lib = L.load()
-    N, C, H, W = shape
-    g = torch.Generator(device="cuda").manual_seed(sum(shape) + 7)
-    CL = torch.channels_last
-    x = torch.randn(2 * N, C, H, W, device=dev, generator=g).bfloat16().contiguous(memory_format=CL)
-    w = (torch.randn(2, C, C, 3, 3, device=dev, generator=g) / (C * 9) ** 0.5).bfloat16()
-    dy = torch.randn(N, C, H, W, device=dev, generator=g).bfloat16().contiguous(memory_format=CL)
-    add = torch.randn(N, C, H, W, device=dev, generator=g).bfloat16().contiguous(memory_format=CL)
-    w0 = w[0].contiguous(memory_format=CL)
-    wt = w0.permute(1, 0, 2, 3).contiguous(memory_format=CL)
-    wg = w.permute(0, 1, 3, 4, 2).contiguous()  # [G][K][R][S][C]
-    d = G._desc_hw(N, H, W, C, C, 3, 3, 1, 1, 1, 1)
-    outs = {}
-    try:
-        for rw in (1, 4):
-            L.check(lib.gm_conv_set_rw(rw), "gm_conv_set_rw")
-            yg = torch.empty(2 * N, C, H, W, device=dev, dtype=torch.bfloat16).contiguous(memory_format=CL)
-            L.check(lib.gm_conv2d_fwd_grouped_bf16(ctypes.byref(d), 2, x.data_ptr(), wg.data_ptr(), C * 9 * C,
-                                                   yg.data_ptr(), 0, 0, L.stream_of(dev)), "grouped fwd")
-            outs[rw] = (G.conv_fwd(x[:N], w0, 1, 1), G.conv_dgrad_t(dy, wt, H, W, 1, 1),
-                        G.conv_dgrad_t(dy, wt, H, W, 1, 1, addend=add), yg)
-        torch.cuda.synchronize()
-    finally:
-        lib.gm_conv_set_rw(1)
-    for name, a_, b_ in zip(("fwd", "dgrad", "dgrad+addend", "grouped fwd"), outs[4], outs[1]):
-        assert torch.equal(a_, b_), name
+        L.check(lib.gm_conv_set_wgrad_loop(6), "loop")  # the default
+    for gi in range(G):
+        xr = x[gi * N:(gi + 1) * N].float().permute(0, 3, 1, 2)
+        gr = dy[gi * N:(gi + 1) * N].float().permute(0, 3, 1, 2)
+        ref = torch.nn.grad.conv2d_weight(xr, (K, C, R, R), gr, stride=st, padding=pad)
+        for acc, base in ((0, 0.0), (1, 0.25)):
+            got = outs[acc][gi].permute(0, 3, 1, 2) - base
+            err = float((got - ref).abs().max() / ref.abs().max())
+            assert err < 2e-3, (gi, acc, err)
 
 
 @pytest.mark.parametrize("shape", [(64, 56, 56, 64), (3, 56, 56, 64), (5, 20, 20, 64), (2, 9, 7, 64), (1, 3, 62, 64),
-                                   (64, 28, 28, 128), (3, 28, 28, 128), (2, 5, 9, 128)],
+                                   (64, 28, 28, 128), (3, 28, 28, 128), (2, 5, 9, 128), (3, 30, 30, 128),
+                                   (64, 14, 14, 256), (3, 14, 14, 256), (2, 6, 13, 128), (64, 7, 7, 512),
+                                   (3, 7, 7, 512), (1, 4, 14, 256), (2, 5, 9, 256)],
                          ids=lambda s: "x".join(map(str, s)))
 def test_wgrad_halo64_vs_fp32(dev, shape):
-    """k_wgrad_halo64 (layer-1 weight gradient: the whole 64 x 9 x 64 gradient in one
-    workgroup's accumulators, one input row staged per output row, rows split over the
-    workgroups, slabs summed in a fixed order) against fp32 PyTorch, grouped over two views,
-    plain and accumulating; and against k_conv_wgrad4 within fp32 summation-order noise."""
+    """k_wgrad_halo64 (3x3 / s1 weight gradient: 64 x 9 x 64 gradient blocks in one workgroup's
+    accumulators, super-rows of 64 / PP image rows staged once for all nine taps, rows split
+    over the workgroups, slabs summed in a fixed order; PP = 64, 32, 16 for layers 1, 2, 3-4)
+    against fp32 PyTorch, grouped over two views, plain and accumulating, ragged batches and
+    image heights that straddle super-rows included; and against k_conv_wgrad4 within the
+    bf16 split-partial rounding."""
     import ctypes
     from greedy_multimodal_learning_amd import _lib as L
     from greedy_multimodal_learning_amd import conv as CV
     N, H, W, C = shape
     K = C
     G = 2
-    mode = 2 if C == 64 else 6
+    mode = 2 if C == 64 else (6 if C == 128 else 14)
     torch.manual_seed(N * 1000 + H * 10 + W)
     x = torch.randn(G * N, H, W, C, device=dev).bfloat16()
     dy = torch.randn(G * N, H, W, K, device=dev).bfloat16()
@@ -518,7 +444,7 @@ def test_wgrad_halo64_vs_fp32(dev, shape):
             outs[m] = res
         torch.cuda.synchronize()
     finally:
-        L.check(lib.gm_conv_set_wgrad_loop(2), "loop")  # the default
+        L.check(lib.gm_conv_set_wgrad_loop(6), "loop")  # the default
     for gi in range(G):
         xr = x[gi * N:(gi + 1) * N].float().permute(0, 3, 1, 2)
         gr = dy[gi * N:(gi + 1) * N].float().permute(0, 3, 1, 2)
@@ -528,7 +454,9 @@ def test_wgrad_halo64_vs_fp32(dev, shape):
             err = float((got - ref).abs().max() / ref.abs().max())
             assert err < 2e-3, (gi, acc, err)
             old = outs[0][acc][gi].permute(0, 3, 1, 2) - base
-            assert float((got - old).abs().max() / ref.abs().max()) < 1e-4
+            # bf16 split partials (summed in fp32): ~2^-9 of a partial per split, far below the
+            # bf16 rounding PyTorch's own bf16 weight gradient carries
+            assert float((got - old).abs().max() / ref.abs().max()) < 2e-3
 
 
 def test_wgrad_halo64_beside_a_busy_neighbour(dev):
@@ -546,7 +474,7 @@ def test_wgrad_halo64_beside_a_busy_neighbour(dev):
     dy = torch.randn(G * N, H, W, C, device=dev).bfloat16()
     lib = L.load()
     d = CV._desc_hw(N, H, W, C, C, 3, 3, 1, 1, 1, 1)
-    L.check(lib.gm_conv_set_wgrad_loop(2), "loop")
+    L.check(lib.gm_conv_set_wgrad_loop(6), "loop")
     need = lib.gm_conv2d_wgrad_grouped_scratch(ctypes.byref(d), G)
     scr = torch.empty(need, device=dev, dtype=torch.uint8)
     side = torch.cuda.Stream()

@@ -188,5 +188,7 @@ def test_dp_bf16_hip_group_sums_match_oracle_mean_of_shards(tmp_path):
     e_g = np.abs(s0[1::2] - ref[1::2]) / ref[1::2]
     print(f"bf16 DP 2x64 vs oracle mean of shards: weight sums rel {e_w.max():.2e}, gradient sums rel {e_g}")
     assert e_w.max() < 1e-6
-    # statistical bound of the bf16 trunk (test_gpu_c2_bf16.py: 9.8e-3 measured on one shard)
-    assert e_g.max() < 3e-2
+    # the bf16 floor: PyTorch's own CPU bf16 autocast moves these sums by 4-8e-3 per branch
+    # (test_gpu_c2_bf16.py); measured here (r04) 7.1e-3 / 7.5e-5 / 1.4e-3 / 6.5e-4 - which
+    # branch lands high follows the weights (test_gpu_view_symmetry.py).  Bound: 2x the worst.
+    assert e_g.max() < 1.5e-2

@@ -252,9 +252,11 @@ def test_model_stacked_vs_per_view(dev, kind):
 @pytest.mark.parametrize("G,B,H", [(2, 4, 64), (3, 2, 38), (1, 2, 224)])
 def test_fused_stem_backward_matches_pool_then_bn(dev, G, B, H):
     """gm_bn_relu_maxpool2d_bwd_grouped_bf16 (pool gradient gathered inside the BN backward,
-    never written) against k_maxpool_bwd + the grouped BN backward: the same dz arithmetic
-    (bf16-rounded gathered sums), so dx agrees to the BN reductions' summation order
-    (<= 1 bf16 ulp) and dgamma / dbeta to fp32 rounding; ragged maps (38 -> 19x19 pool)."""
+    never written; its statistics pass over the pooled gradient and the forward's selected x)
+    against k_maxpool_bwd + the grouped BN backward.  dx takes the same dz arithmetic
+    (bf16-rounded gathered sums); dgamma / dbeta sum the window gradients in fp32 without the
+    per-pixel bf16 rounding the unfused pair's dz carries, so they agree to that rounding
+    (2^-9 relative per term: bound 4e-3 of the largest channel); ragged maps (38 -> 19x19)."""
     from greedy_multimodal_learning_amd import vtrunk
     from greedy_multimodal_learning_amd.resnet import resnet18
     torch.manual_seed(5 + G)
@@ -276,8 +278,8 @@ def test_fused_stem_backward_matches_pool_then_bn(dev, G, B, H):
         res[fused] = [(n.conv1.weight.grad.clone(), n.bn1.weight.grad.clone(), n.bn1.bias.grad.clone()) for n in nets]
     for g in range(G):
         (wf, gf, bf), (wu, gu, bu) = res[True][g], res[False][g]
-        _close(gf, gu, 1e-4, f"dgamma[{g}]")
-        _close(bf, bu, 1e-4, f"dbeta[{g}]")
+        _close(gf, gu, 4e-3, f"dgamma[{g}]")
+        _close(bf, bu, 4e-3, f"dbeta[{g}]")
         _close(wf, wu, 1e-2, f"stem dw[{g}]")
 
 

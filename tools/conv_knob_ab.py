@@ -4,8 +4,7 @@ the trunk shapes, in ONE process (cdna_hip_programming.md §5.4 rule 24): every 
 `--rounds` times alternately on the grouped launches the step runs (both views per launch),
 operands rotating over more than the 256 MiB Infinity Cache.
 
-    python tools/conv_knob_ab.py --setter gm_conv_set_wgrad_loop --modes 0,1 --ops wgrad
-    python tools/conv_knob_ab.py --setter gm_conv_set_rw --modes 1,4 --ops fwd,dgrad --shapes l1
+    python tools/conv_knob_ab.py --setter gm_conv_set_wgrad_loop --modes 0,6 --ops wgrad --shapes l1,l2
 """
 import argparse
 import os

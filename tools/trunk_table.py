@@ -275,28 +275,30 @@ def bn_ops(B, dev, G=2):
             P, Q = H // 2, W // 2
             yp = torch.empty(G * B, C, P, Q, device=dev, dtype=torch.bfloat16).contiguous(memory_format=CL)
             idx = torch.empty(G * B, P, Q, C, device=dev, dtype=torch.uint8)
+            xs = torch.empty(G * B, P, Q, C, device=dev, dtype=torch.bfloat16)
             gyp = torch.randn(G * B, C, P, Q, device=dev).bfloat16().contiguous(memory_format=CL)
             d1 = L.PoolDesc(B, H, W, C, 3, 2, 1)
             dG = L.PoolDesc(G * B, H, W, C, 3, 2, 1)
 
-            def pool_fwd(d1=d1, x=x, coef=coef, yp=yp, idx=idx):
+            def pool_fwd(d1=d1, x=x, coef=coef, yp=yp, idx=idx, xs=xs):
                 L.check(lib.gm_bn_relu_maxpool2d_fwd_grouped_bf16(ctypes.byref(d1), G, x.data_ptr(), coef.data_ptr(),
-                                                                  yp.data_ptr(), idx.data_ptr(), st), "pool fwd")
+                                                                  yp.data_ptr(), idx.data_ptr(), xs.data_ptr(), st),
+                        "pool fwd")
 
             def pool_bwd(dG=dG, gyp=gyp, idx=idx, dx=dx):
                 L.check(lib.gm_maxpool2d_bwd_bf16(ctypes.byref(dG), gyp.data_ptr(), idx.data_ptr(), dx.data_ptr(),
                                                   st), "pool bwd")
             e_in, e_out = G * M * C, G * B * P * Q * C
-            out.append(("maxpool", "bn_relu_fwd", 1, 0, e_in * 2 + e_out * 3, pool_fwd))
+            out.append(("maxpool", "bn_relu_fwd", 1, 0, e_in * 2 + e_out * 5, pool_fwd))
             out.append(("maxpool", "bwd", 1, 0, e_out * 3 + e_in * 2, pool_bwd))
             pool_fwd()  # valid argmax bytes for the fused backward
 
-            def pool_bn_bwd(d1=d1, gyp=gyp, idx=idx, ba=ba, buf=buf):  # what the step runs (vtrunk)
+            def pool_bn_bwd(d1=d1, gyp=gyp, idx=idx, xs=xs, ba=ba, buf=buf):  # what the step runs (vtrunk)
                 L.check(lib.gm_bn_relu_maxpool2d_bwd_grouped_bf16(ctypes.byref(d1), G, gyp.data_ptr(), idx.data_ptr(),
-                                                                  ba, buf.data_ptr(), buf.numel(), st),
+                                                                  xs.data_ptr(), ba, buf.data_ptr(), buf.numel(), st),
                         "pool+bn bwd")
-            # two passes: (x, pooled gradient, argmax) each, + the dx write
-            out.append(("bn1+maxpool", "pool_bn_bwd", 1, 0, 2 * (e_in * 2 + e_out * 3) + e_in * 2, pool_bn_bwd))
+            # pass 1: pooled gradient + selected x; pass 2: x, pooled gradient, argmax, the dx write
+            out.append(("bn1+maxpool", "pool_bn_bwd", 1, 0, e_out * 4 + (e_in * 2 + e_out * 3) + e_in * 2, pool_bn_bwd))
     return out
 
 
