@@ -55,7 +55,6 @@ EXPORTS = {
     "gm_mmtm_spatial_reduce": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_size_t,
                                        c_void_p]),
     "gm_mmtm_set_reduce_form": (c_int, [c_int, c_int]),
-    "gm_mmtm_set_reduce_dma": (c_int, [c_int]),
     "gm_mmtm_channel_scale": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "gm_gemm_f32": (c_int, [c_void_p, c_int, c_void_p]),
     "gm_gemm_set_form": (c_int, [c_int]),
@@ -351,8 +350,8 @@ EXPORTS.update({
     "gm_conv_set_h9_staging": (c_int, [c_int]),
     "gm_conv_set_wgrad_staging": (c_int, [c_int]),
     "gm_conv_set_splitk": (c_int, [c_int]),
-    "gm_conv_set_wgrad_wide": (c_int, [c_int]),
     "gm_conv_set_wgrad_loop": (c_int, [c_int]),
+    "gm_conv_set_1x1_gemm": (c_int, [c_int]),
     "gm_conv_set_rw": (c_int, [c_int]),
     "gm_conv_set_stem": (c_int, [c_int]),
 })

@@ -28,7 +28,6 @@ typedef short short8_t __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int kWTap = 49;
-constexpr int kPitch = 96;      // LDS row pitch in bf16 elements (192 B)
 
 struct WgradArgs {
     const uint16_t* dy;         // [N][P][Q][Kc]
@@ -99,100 +98,6 @@ __device__ __forceinline__ void wait_lgkm0(bf16x8 (&a)[MT], bf16x8 (&b)[NT]) {
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]));
 }
 
-__global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a) {
-    constexpr int BK = 64;  // pixels per step
-    __shared__ __attribute__((aligned(16))) uint16_t lds[2][2][BK * kPitch];  // [buf][A|B]
-    __shared__ int tapt[kWTap];
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int wm = wave >> 1, wn = wave & 1;
-    int bid = blockIdx.x;
-    const int split = bid % a.splits;
-    bid /= a.splits;
-    const int tk = bid % a.tiles_k, tn = bid / a.tiles_k;
-    const int k0 = tk * 64, n0 = tn * 64;
-#pragma unroll
-    for (int i = 0; i < kWTap; ++i)
-        if (t == i && i < a.T) tapt[i] = ((int)(a.dh[i] + 128)) | ((int)(a.dw[i] + 128) << 8);
-    __syncthreads();
-    const int PQ = a.P * a.Q;
-    const int M = a.N * PQ;
-    const int step0 = split * a.steps_per_split;
-    const int step1 = min((M + BK - 1) / BK, step0 + a.steps_per_split);
-    const int lchunk = t & 7, lrow = t >> 3;  // 8 loaders per 64-channel row, rows lrow, lrow+32
-    // B column chunk geometry (fixed for the workgroup): col = n0 + 8*lchunk -> (tap, c)
-    const int colk = n0 + lchunk * 8;
-    const int btap = colk >> a.logC, bc = colk & (a.C - 1);
-    const int te = tapt[btap < a.T ? btap : 0];
-    const int bdh = (te & 0xff) - 128, bdw = ((te >> 8) & 0xff) - 128;
-    const bool bcol_ok = colk < a.T * a.C;
-    const bool acol_ok = (k0 + lchunk * 8) < a.Kc;
-
-    uint4 ra[2], rb[2];
-    auto load = [&](int step) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int m = step * BK + lrow + 32 * i;
-            uint4 va = make_uint4(0, 0, 0, 0), vb = make_uint4(0, 0, 0, 0);
-            if (m < M) {
-                if (acol_ok) va = *(const uint4*)(a.dy + (size_t)m * a.Kc + k0 + lchunk * 8);
-                const int b = (int)a.fd_pq.div((uint32_t)m), pq = m - b * PQ;
-                const int p = (int)a.fd_q.div((uint32_t)pq), q = pq - p * a.Q;
-                const int hi = p * a.sth + bdh, wi = q * a.stw + bdw;
-                if (bcol_ok && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W)
-                    vb = *(const uint4*)(a.x + ((size_t)((b * a.H + hi) * a.W + wi) << a.logC) + bc);
-            }
-            ra[i] = va;
-            rb[i] = vb;
-        }
-    };
-    auto store = [&](int buf) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int row = lrow + 32 * i;
-            *(uint4*)&lds[buf][0][row * kPitch + lchunk * 8] = ra[i];
-            *(uint4*)&lds[buf][1][row * kPitch + lchunk * 8] = rb[i];
-        }
-    };
-    floatx16 acc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    // tr-read lane geometry: group g = lane>>4 reads rows 8*(g>>1)+q (+4), cols 16*(g&1)+4p
-    const int g = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
-    const int rbase = 8 * (g >> 1) + q4;
-    const int acol = wm * 32 + 16 * (g & 1) + 4 * p4;
-    const int bcol = wn * 32 + 16 * (g & 1) + 4 * p4;
-    if (step0 < step1) {
-        load(step0);
-        store(0);
-    }
-    __syncthreads();
-    for (int s = step0; s < step1; ++s) {
-        const int buf = (s - step0) & 1;
-        if (s + 1 < step1) load(s + 1);
-        const uint16_t* A = lds[buf][0];
-        const uint16_t* Bm = lds[buf][1];
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-            const int r0 = ks * 16 + rbase;
-            const bf16x8 af = tr_frag(A + r0 * kPitch + acol, A + (r0 + 4) * kPitch + acol);
-            const bf16x8 bf = tr_frag(Bm + r0 * kPitch + bcol, Bm + (r0 + 4) * kPitch + bcol);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, acc, 0, 0, 0);
-        }
-        if (s + 1 < step1) store(buf ^ 1);
-        __syncthreads();
-    }
-    // D[k][c]: col = lane&31 (c), row = (r&3) + 8(r>>2) + 4(lane>>5) (k)
-    const int TC = a.T * a.C;
-    float* out = a.part + (size_t)split * a.Kc * TC;
-    const int col = n0 + wn * 32 + (lane & 31);
-    if (col < TC) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int row = k0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-            if (row < a.Kc) out[(size_t)row * TC + col] = acc[r];
-        }
-    }
-}
 
 __device__ __attribute__((aligned(16))) const uint4 g_wzero16[1] = {{0u, 0u, 0u, 0u}};
 
@@ -897,29 +802,13 @@ static int ilog2w(int v) {
     return (1 << l) == v ? l : -1;
 }
 
-static int wgrad_version() {
-    static int v = [] {
-        const char* e = getenv("GM_WGRAD_V");  // 1: 64x64 register-staged kernel, 2: k_conv_wgrad4
-        return (e && e[0] == '1') ? 1 : 2;
-    }();
-    return v;
-}
-
 static int wgrad_target_wgs() {
     static int w = [] {
         const char* e = getenv("GM_WGRAD_WGS");
-        return e ? atoi(e) : (wgrad_version() == 2 ? 512 : 1024);
+        return e ? atoi(e) : 512;
     }();
     return w;
 }
-
-
-
-static int g_wgrad_wide = [] {
-    const char* e = getenv("GM_WGRAD_WIDE");
-    return e ? atoi(e) : 0;
-}();
-static int wgrad_wide() { return g_wgrad_wide; }
 
 struct WPlan {
     int P, Q, tiles_k, tiles_n, splits, sps, mt, nt;
@@ -932,26 +821,17 @@ static WPlan plan(const gm_conv_desc_hw* d, int G = 1) {
     const int M = d->N * w.P * w.Q;
     const int steps = (M + 63) / 64;
     const int TC = d->R * d->S * d->C;
-    w.mt = w.nt = 1;
-    if (wgrad_version() >= 2) {
-        w.mt = d->K >= 128 ? 2 : 1;
-        w.nt = TC >= 128 ? 2 : 1;
-        // wide tiles (one workgroup per CU): 256-row / 256-column tiles halve the
-        // staged bytes per MFMA of the dimension they widen (g_wgrad_wide bit 0: rows,
-        // bit 1: columns)
-        if ((wgrad_wide() & 1) && d->K >= 256 && w.mt == 2) w.mt = 4;
-        if ((wgrad_wide() & 2) && TC >= 256 && w.nt == 2) w.nt = 4;
-        // bit 2: 256-column tiles for the 64-row (K = 64) shapes only - layer 1, where a
-        // 64 x 128 tile gives each wave 8 MFMAs per 64-pixel step between barriers
-        if ((wgrad_wide() & 4) && d->K <= 64 && TC >= 256 && w.nt == 2) w.nt = 4;
-    }
+    // 128 x 128 tiles where the shape allows (256-row / 256-column tiles at one workgroup per
+    // CU measured 1.2-1.6x slower in round 2 and were dropped)
+    w.mt = d->K >= 128 ? 2 : 1;
+    w.nt = TC >= 128 ? 2 : 1;
     w.tiles_k = (d->K + 64 * w.mt - 1) / (64 * w.mt);
     w.tiles_n = (TC + 64 * w.nt - 1) / (64 * w.nt);
     const int tiles = w.tiles_k * w.tiles_n * G;  // the groups' tiles share the chip
-    const int target = wgrad_version() >= 2 ? wgrad_target_wgs() : 1024;
-    const int min_steps = wgrad_version() == 2 ? 8 : 4;
-    int want = wgrad_version() == 2 ? (target > tiles ? target / tiles : 1) : (target + tiles - 1) / tiles;
-    if (wgrad_version() == 2 && tiles >= 256) want = 1;  // the chip is full: no partial slabs
+    const int target = wgrad_target_wgs();
+    const int min_steps = 8;
+    int want = target > tiles ? target / tiles : 1;
+    if (tiles >= 256) want = 1;  // the chip is full: no partial slabs
     if (want > steps / min_steps) want = steps / min_steps > 0 ? steps / min_steps : 1;
     if (want < 1) want = 1;
     w.sps = (steps + want - 1) / want;
@@ -1047,6 +927,13 @@ extern "C" size_t gm_conv2d_wgrad_scratch(const gm_conv_desc* d) {
     return gm_conv2d_wgrad_hw_scratch(&h);
 }
 
+// 1x1 / s1 / p0 convolutions as plain GEMMs on hipBLASLt (conv1x1_lt.hip)
+namespace gm {
+bool conv1x1_lt_ok(int R, int S, int sh, int sw, int ph, int pw, long long M);
+int conv1x1_lt_wgrad(long long M, int C, int K, int G, const void* dy, long long gs_dy, const void* x, long long gs_x,
+                     float* dw, long long gs_dw, int accumulate, hipStream_t st);
+}  // namespace gm
+
 // G view groups in one launch: group g reads dy + g*N*P*Q*K and x + g*N*H*W*C (the views
 // stacked along the batch) and writes its weight gradient to dw + g*dw_stride (floats)
 extern "C" int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, const void* dy, const void* x,
@@ -1054,7 +941,6 @@ extern "C" int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, con
                                             void* scratch, size_t scratch_bytes, void* stream) {
     GM_REQUIRE(d && dy && x && dw, "conv wgrad: null pointer");
     GM_REQUIRE(G >= 1 && G <= 64, "conv wgrad: view groups must be 1..64 (got %d)", G);
-    GM_REQUIRE(wgrad_version() >= 2 || G == 1, "conv wgrad: view groups need k_conv_wgrad4");
     GM_REQUIRE(d->stride_h >= 1 && d->stride_w >= 1 && d->pad_h >= 0 && d->pad_w >= 0, "conv wgrad: bad stride/pad");
     GM_REQUIRE(d->R * d->S <= kWTap, "conv wgrad: at most %d taps", kWTap);
     GM_REQUIRE(ilog2w(d->C) >= 3, "conv wgrad: C must be a power of two >= 8");
@@ -1063,6 +949,11 @@ extern "C" int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, con
     const size_t slab_c = (size_t)d->K * d->R * d->S * (size_t)c_real;
     GM_REQUIRE(G == 1 || (dw_stride >= (long long)slab_c || dw_stride <= -(long long)slab_c),
                "conv wgrad: group gradient stride %lld overlaps one gradient", dw_stride);
+    const long long M = (long long)d->N * d->H * d->W;
+    if (gm::conv1x1_lt_ok(d->R, d->S, d->stride_h, d->stride_w, d->pad_h, d->pad_w, M) && c_real == d->C &&
+        (G == 1 || dw_stride > 0))
+        return gm::conv1x1_lt_wgrad(M, d->C, d->K, G, dy, M * d->K, x, M * d->C, dw, dw_stride, accumulate,
+                                    as_stream(stream));
     const size_t need = gm_conv2d_wgrad_grouped_scratch(d, G);
     GM_REQUIRE(scratch && scratch_bytes >= need, "conv wgrad: scratch %zu < %zu", scratch_bytes, need);
     hipStream_t st0 = as_stream(stream);
@@ -1150,30 +1041,20 @@ extern "C" int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, con
     hipStream_t st = as_stream(stream);
     const int grid = a.tiles_k * a.tiles_n * a.splits * G;
     int rc;
-    if (wgrad_version() >= 2) {
-        const bool direct = a.splits == 1 && c_real == d->C;
-        if (direct) {
-            a.part = dw;
-            a.gs_part = dw_stride;
-            a.accumulate = accumulate;
-        }
-        a.S = d->S;
-        a.padh = d->pad_h;
-        a.padw = d->pad_w;
-        if (w.mt == 4 && w.nt == 4) rc = launch_wgrad4<4, 4>(a, grid, st);
-        else if (w.mt == 4) rc = launch_wgrad4<4, 2>(a, grid, st);
-        else if (w.nt == 4 && w.mt == 2) rc = launch_wgrad4<2, 4>(a, grid, st);
-        else if (w.nt == 4) rc = launch_wgrad4<1, 4>(a, grid, st);
-        else if (w.mt == 2 && w.nt == 2) rc = launch_wgrad4<2, 2>(a, grid, st);
-        else if (w.mt == 2) rc = launch_wgrad4<2, 1>(a, grid, st);
-        else if (w.nt == 2) rc = launch_wgrad4<1, 2>(a, grid, st);
-        else rc = launch_wgrad4<1, 1>(a, grid, st);
-        if (rc || direct) return rc;
-    } else {
-        k_conv_wgrad<<<grid, 256, 0, st>>>(a);
-        rc = check_launch("k_conv_wgrad");
+    const bool direct = a.splits == 1 && c_real == d->C;
+    if (direct) {
+        a.part = dw;
+        a.gs_part = dw_stride;
+        a.accumulate = accumulate;
     }
-    if (rc) return rc;
+    a.S = d->S;
+    a.padh = d->pad_h;
+    a.padw = d->pad_w;
+    if (w.mt == 2 && w.nt == 2) rc = launch_wgrad4<2, 2>(a, grid, st);
+    else if (w.mt == 2) rc = launch_wgrad4<2, 1>(a, grid, st);
+    else if (w.nt == 2) rc = launch_wgrad4<1, 2>(a, grid, st);
+    else rc = launch_wgrad4<1, 1>(a, grid, st);
+    if (rc || direct) return rc;
     const size_t slab = (size_t)d->K * a.T * d->C;
     if (c_real == d->C) {  // one-launch split reduction (slab is a multiple of 4: K % 8 == 0)
         const size_t ncol = slab / 4;
@@ -1216,12 +1097,6 @@ extern "C" int gm_conv_set_wgrad_loop(int mode) {
     GM_REQUIRE(mode >= 0 && mode <= 15 && !(mode & 1),
                "gm_conv_set_wgrad_loop: bit 1 halo kernel for 64 channels, bit 2 up to 128, bit 3 up to 512");
     g_wgrad_loop = mode;
-    return GM_OK;
-}
-
-extern "C" int gm_conv_set_wgrad_wide(int mode) {
-    GM_REQUIRE(mode >= 0 && mode <= 3, "gm_conv_set_wgrad_wide: 0..3 (bit 0: 256-row tiles, bit 1: 256-column tiles)");
-    g_wgrad_wide = mode;
     return GM_OK;
 }
 

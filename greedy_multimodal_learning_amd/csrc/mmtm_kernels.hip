@@ -234,108 +234,6 @@ __global__ __launch_bounds__(NTH) void k_colreduce_nhwc(RedArgs a) {
     }
 }
 
-// The bf16 forward squeeze with the activations streamed by LDS-DMA (global_load_lds
-// dwordx4, nontemporal: aux 2) instead of vector loads into VGPRs: a workgroup's region
-// of one image (pixels [hw0, hw1) x all C channels, C*2 <= 4096 B so the region is ONE
-// contiguous byte range) flows through an NS-stage ring of 16 KB stages, NS - 2 stages in
-// flight across each barrier (counted vmcnt); each thread adds the 16-B chunks of its
-// fixed channel group out of LDS.  The DMA path streams HBM faster than register loads
-// (MI355X_MICROARCH.md price list: LDS-DMA 6.4-6.8 TB/s chip-wide with nt).  Same pixel
-// lanes and final LDS reduction as k_colreduce_nhwc (same summation order per thread
-// differs: the thread's chunks are now pixels t/tpp + 16KB/RB*i).
-constexpr int kDmaStage = 16384;
-template <int NS>
-__global__ __launch_bounds__(256) void k_colreduce_nhwc_dma(RedArgs a) {
-    constexpr int NTH = 256, N = 8;
-    extern __shared__ __attribute__((aligned(16))) uint4 dsm[];
-    char* ring = reinterpret_cast<char*>(dsm);                       // [NS][16 KB]
-    float* red = reinterpret_cast<float*>(ring + NS * kDmaStage);    // [256 * 8]
-    float* red2 = red + NTH * N;                                      // [256]
-    int pi = 0;
-#pragma unroll
-    for (int q = 1; q < kMaxProb; ++q)
-        if (q < a.nprob && (int)blockIdx.x >= a.p[q].wg_start) pi = q;
-    const RedProb& p = a.p[pi];
-    const int w = blockIdx.x - p.wg_start;
-    const int b = w / p.S, s = w - b * p.S;
-    const int CW = p.C, RB = CW * 2;    // one slab: the whole pixel row
-    const int tpp = CW / N;             // threads per pixel (16-B chunks per row)
-    const int ppi = NTH / tpp;          // pixel lanes
-    const int t = threadIdx.x, lane = t & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-    const int cc = t % tpp, pl = t / tpp;
-    const int hw0 = s * p.hw_per, hw1 = min(p.HW, hw0 + p.hw_per);
-    const char* src = (const char*)p.x + ((size_t)b * p.HW + hw0) * RB;
-    const long long nbytes = (long long)(hw1 - hw0) * RB;
-    const int nst = (int)((nbytes + kDmaStage - 1) / kDmaStage);
-    typedef __attribute__((address_space(1))) const void* gptr_t;
-    typedef __attribute__((address_space(3))) void* lptr_t;
-    auto issue = [&](int i) {  // stage i: wave w copies bytes [i*16K + w*4K, +4K) in 4 x 1 KB
-        char* dst = ring + (i % NS) * kDmaStage + wave * 4096;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const long long off = (long long)i * kDmaStage + wave * 4096 + j * 1024 + lane * 16;
-            const void* g = (const void*)(src + (off < nbytes ? off : 0));
-            __builtin_amdgcn_global_load_lds((gptr_t)g, (lptr_t)(dst + j * 1024), 16, 0, 2);
-        }
-    };
-    float acc[N];
-#pragma unroll
-    for (int j = 0; j < N; ++j) acc[j] = 0.f;
-#pragma unroll
-    for (int i = 0; i < NS - 1; ++i)
-        if (i < nst) issue(i);
-    for (int i = 0; i < nst; ++i) {
-        // stage i landed: NS - 2 younger stages (4 DMA instructions each) may stay in flight
-        if (i + NS - 2 < nst) {
-            if constexpr (NS == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-            else if constexpr (NS == 3) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __builtin_amdgcn_s_barrier();  // every wave's part of stage i landed; stage i-1 fully read
-        asm volatile("" ::: "memory");
-        if (i + NS - 1 < nst) issue(i + NS - 1);  // into the slot stage i-1 freed
-        const char* st = ring + (i % NS) * kDmaStage;
-        const long long base = (long long)i * kDmaStage;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int off = j * 4096 + t * 16;
-            if (base + off < nbytes) {
-                const uint4 v = *reinterpret_cast<const uint4*>(st + off);
-                acc[0] += bf_lo(v.x); acc[1] += bf_hi(v.x); acc[2] += bf_lo(v.y); acc[3] += bf_hi(v.y);
-                acc[4] += bf_lo(v.z); acc[5] += bf_hi(v.z); acc[6] += bf_lo(v.w); acc[7] += bf_hi(v.w);
-            }
-        }
-    }
-    // thread t's chunks all lie in channel group cc (4096 % RB == 0); its pixel lane is
-    // pl (mod ppi): the same [pl][CW] combine as k_colreduce_nhwc
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < N; ++j) red[pl * CW + cc * N + j] = acc[j];
-    __syncthreads();
-    const int R = CW <= NTH ? NTH / CW : 1;
-    if (R > 1) {
-        if (t < R * CW) {
-            const int c = t % CW, r = t / CW;
-            float v = 0.f;
-            for (int q = r; q < ppi; q += R) v += red[q * CW + c];
-            red2[r * CW + c] = v;
-        }
-        __syncthreads();
-    }
-    for (int c = t; c < CW; c += NTH) {
-        float v = 0.f;
-        if (R > 1) {
-            for (int r = 0; r < R; ++r) v += red2[r * CW + c];
-        } else {
-            for (int q = 0; q < ppi; ++q) v += red[q * CW + c];
-        }
-        if (p.S == 1) p.out[(size_t)b * p.ld_out + c] = epilogue(v, p, b, c, 1.f);
-        else p.part[((size_t)b * p.S + s) * p.C + c] = v;
-    }
-}
 
 __global__ __launch_bounds__(256) void k_reduce_partials(RedArgs a) {
     // grid: (ceil(maxC/256), B, nprob)
@@ -543,16 +441,6 @@ static int g_red_nt = [] {
     const char* e = getenv("GM_RED_NT");
     return e ? atoi(e) : 1;
 }();
-// LDS-DMA form of the bf16 forward squeeze: ring stages (3 or 4; 0 = off; GM_RED_DMA)
-static int g_red_dma = [] {
-    const char* e = getenv("GM_RED_DMA");
-    return e ? atoi(e) : 0;
-}();
-extern "C" int gm_mmtm_set_reduce_dma(int stages) {
-    GM_REQUIRE(stages == 0 || stages == 3 || stages == 4, "reduce DMA stages must be 0, 3 or 4 (got %d)", stages);
-    g_red_dma = stages;
-    return GM_OK;
-}
 extern "C" int gm_mmtm_set_reduce_form(int threads, int unroll) {
     g_red_nt = threads < 0;  // negative threads: nontemporal loads (forward, bf16; the default)
     if (threads < 0) threads = -threads;
@@ -688,22 +576,7 @@ static int spatial_reduce_impl(const gm_spatial_reduce* in, int nprob, int B, in
     if (bwd) k_colreduce_nhwc<T, true, U, NTH><<<nwg, NTH, 0, st>>>(a);      \
     else k_colreduce_nhwc<T, false, U, NTH><<<nwg, NTH, 0, st>>>(a);
     const int u = red_unroll(), wide = red_threads() == 1024;
-    bool dma_ok = dtype == GM_BF16 && !bwd && g_red_dma;
-    for (int i = 0; i < nprob; ++i) dma_ok = dma_ok && a.p[i].ncs == 1 && (a.p[i].C * 2) <= 4096 &&
-                                             4096 % (a.p[i].C * 2) == 0;
-    if (dma_ok) {
-        const size_t lds = (size_t)g_red_dma * kDmaStage + (256 * 8 + 256) * 4;
-        static bool attr = [] {  // > 64 KB of dynamic LDS
-            (void)hipFuncSetAttribute((const void*)k_colreduce_nhwc_dma<3>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 3 * kDmaStage + 9216);
-            (void)hipFuncSetAttribute((const void*)k_colreduce_nhwc_dma<4>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kDmaStage + 9216);
-            return true;
-        }();
-        (void)attr;
-        if (g_red_dma == 3) k_colreduce_nhwc_dma<3><<<nwg, 256, lds, st>>>(a);
-        else k_colreduce_nhwc_dma<4><<<nwg, 256, lds, st>>>(a);
-    } else if (dtype == GM_BF16 && !bwd && g_red_nt) {
+    if (dtype == GM_BF16 && !bwd && g_red_nt) {
         if (wide) k_colreduce_nhwc<uint16_t, false, 4, 1024, true><<<nwg, 1024, 0, st>>>(a);
         else if (u >= 8) k_colreduce_nhwc<uint16_t, false, 8, 256, true><<<nwg, 256, 0, st>>>(a);
         else k_colreduce_nhwc<uint16_t, false, 4, 256, true><<<nwg, 256, 0, st>>>(a);

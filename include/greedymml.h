@@ -114,9 +114,6 @@ int gm_mmtm_spatial_reduce(const gm_spatial_reduce* p, int nprob, int B, int dty
  * pixels whose 16-B loads one thread keeps in flight (4, 8 or 16; GM_RED_UNROLL).
  * Process-wide, not thread-safe. */
 int gm_mmtm_set_reduce_form(int threads, int unroll);
-/* A/B knob: the bf16 forward squeeze streamed by LDS-DMA through a 3- or 4-stage ring
- * (0 = off; GM_RED_DMA).  Process-wide. */
-int gm_mmtm_set_reduce_dma(int stages);
 
 /* ---------------------------------------------------------------------------
  * Channel re-scale: y[b,c,hw] = x[b,c,hw] * s[b*ld_s + c] (+ alpha * a[b*ld_a + c])
@@ -372,14 +369,14 @@ int gm_conv_set_h9_staging(int wr);
 /* Split-K target: workgroups wanted from splitting K of 128x128-tile convolutions whose
  * tiles alone do not fill the device (default 384, GM_CONV_SPLITK at load; 0 = never). */
 int gm_conv_set_splitk(int target);
-/* Weight-gradient tile form (process-wide; GM_WGRAD_WIDE at load): bit 0 takes
- * 256-row tiles for K >= 256, bit 1 256-column (tap, channel) tiles; 0 = 128 x 128. */
-int gm_conv_set_wgrad_wide(int mode);
 /* Weight-gradient kernel for 3x3 / s1 / p1 shapes with W <= 62 (GM_WGRAD_LOOP at load; default
  * 6): bit 1 = k_wgrad_halo64 (64 x 9 x 64 gradient blocks in one workgroup's accumulators, one
  * input row staged per output row, dedicated loader waves) for 64 channels, bit 2 = also for
  * 128 channels; the rest take k_conv_wgrad4.  Bit 0 is reserved (must be 0). */
 int gm_conv_set_wgrad_loop(int mode);
+/* 1x1 / stride-1 / pad-0 convolutions (forward, input and weight gradient) as plain GEMMs on
+ * hipBLASLt (default on; GM_CONV1X1_LT=0 at load or gm_conv_set_1x1_gemm(0): the im2col kernel). */
+int gm_conv_set_1x1_gemm(int on);
 /* Weight-gradient operand staging: 0 = LDS-DMA pieces, 1 = register-staged (global_load_dwordx4
  * two steps ahead + ds_write_b128; same LDS image and arithmetic), 2 (default) = register-staged
  * for 1x1 filters, LDS-DMA otherwise.  GM_WGRAD_WR at load. */

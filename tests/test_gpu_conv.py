@@ -492,3 +492,65 @@ def test_wgrad_halo64_beside_a_busy_neighbour(dev):
     assert torch.isfinite(outs[0]).all()
     for i, dw in enumerate(outs[1:], 1):
         assert torch.equal(dw, outs[0]), (i, int((~torch.isfinite(dw)).sum()))
+
+
+@pytest.mark.parametrize("shape", [(4, 256, 14, 14, 64), (2, 64, 56, 56, 256), (3, 512, 7, 7, 2048), (1, 8, 5, 3, 16),
+                                   (5, 1024, 14, 14, 256)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_conv1x1_gemm_vs_fp32(dev, shape):
+    """1x1 / s1 / p0 convolutions as plain GEMMs (hipBLASLt, conv1x1_lt.hip): forward, input
+    gradient with and without the fused addend, weight gradient plain and accumulating, as
+    the two-view grouped launches the trunk issues (the view groups as the GEMM batch) -
+    against fp32 PyTorch and against the im2col kernel (gm_conv_set_1x1_gemm(0))."""
+    import ctypes
+    from greedy_multimodal_learning_amd import _lib as L
+    from greedy_multimodal_learning_amd import conv as CV
+    N, C, H, W, K = shape
+    G = 2
+    torch.manual_seed(sum(shape))
+    x = torch.randn(G * N, H, W, C, device=dev).bfloat16()
+    dy = torch.randn(G * N, H, W, K, device=dev).bfloat16()
+    add = torch.randn(G * N, H, W, C, device=dev).bfloat16()
+    w = (torch.randn(G, K, C, device=dev) / C ** 0.5).bfloat16()  # [G][K][C] = KRSC, R = S = 1
+    wt = w.transpose(1, 2).contiguous()                          # [G][C][K]
+    lib = L.load()
+    st = L.stream_of(dev)
+    dh = CV._desc_hw(N, H, W, C, K, 1, 1, 1, 1, 0, 0)
+    dd = L.ConvDesc(N, H, W, C, K, 1, 1, 1, 0)
+    res = {}
+    try:
+        for mode in (1, 0):
+            L.check(lib.gm_conv_set_1x1_gemm(mode), "1x1 gemm")
+            y = torch.empty(G * N, H, W, K, device=dev, dtype=torch.bfloat16)
+            L.check(lib.gm_conv2d_fwd_grouped_bf16(ctypes.byref(dh), G, x.data_ptr(), w.data_ptr(), K * C,
+                                                   y.data_ptr(), 0, 0, st), "fwd")
+            dx = torch.empty(G * N, H, W, C, device=dev, dtype=torch.bfloat16)
+            L.check(lib.gm_conv2d_dgrad_grouped_bf16(ctypes.byref(dd), G, dy.data_ptr(), wt.data_ptr(), C * K,
+                                                     dx.data_ptr(), 0, 0, 0, st), "dgrad")
+            dxa = torch.empty_like(dx)
+            L.check(lib.gm_conv2d_dgrad_grouped_bf16(ctypes.byref(dd), G, dy.data_ptr(), wt.data_ptr(), C * K,
+                                                     dxa.data_ptr(), add.data_ptr(), 0, 0, st), "dgrad+addend")
+            need = lib.gm_conv2d_wgrad_grouped_scratch(ctypes.byref(dh), G)
+            scr = torch.empty(max(need, 16), device=dev, dtype=torch.uint8)
+            dws = []
+            for acc in (0, 1):
+                dw = torch.full((G, K, C), 0.5, device=dev)
+                L.check(lib.gm_conv2d_wgrad_grouped_bf16(ctypes.byref(dh), G, dy.data_ptr(), x.data_ptr(),
+                                                         dw.data_ptr(), K * C, C, acc, scr.data_ptr(), need, st),
+                        "wgrad")
+                dws.append(dw)
+            torch.cuda.synchronize()
+            res[mode] = (y, dx, dxa, dws)
+    finally:
+        L.check(lib.gm_conv_set_1x1_gemm(1), "1x1 gemm")  # the default
+    for g in range(G):
+        sl = slice(g * N, (g + 1) * N)
+        xf, dyf, wf = x[sl].float().reshape(-1, C), dy[sl].float().reshape(-1, K), w[g].float()
+        yr, dxr, dwr = xf @ wf.t(), dyf @ wf, dyf.t() @ xf
+        for mode in (1, 0):
+            y, dx, dxa, dws = res[mode]
+            _close(y[sl].reshape(-1, K), yr, 1e-2)
+            _close(dx[sl].reshape(-1, C), dxr, 1e-2)
+            _close(dxa[sl].reshape(-1, C), dxr + add[sl].float().reshape(-1, C), 1e-2)
+            _close(dws[0][g], dwr, 2e-3)
+            _close(dws[1][g] - 0.5, dwr, 2e-3)

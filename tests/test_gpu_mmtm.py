@@ -136,15 +136,13 @@ def test_mmtm_turnoff_squeeze_raises(dev):
           average_squeezemaps=[torch.zeros(8, device=dev), torch.zeros(8, device=dev)])
 
 
-@pytest.mark.parametrize("form", [(256, 4, 0), (-256, 4, 0), (-256, 8, 0), (1024, 4, 0), (-1024, 4, 0),
-                                  (-256, 4, 3), (-256, 4, 4)],
-                         ids=lambda f: f"t{abs(f[0])}u{f[1]}{'nt' if f[0] < 0 else ''}dma{f[2]}")
+@pytest.mark.parametrize("form", [(256, 4), (-256, 4), (-256, 8), (1024, 4), (-1024, 4)],
+                         ids=lambda f: f"t{abs(f[0])}u{f[1]}{'nt' if f[0] < 0 else ''}")
 @pytest.mark.parametrize("C,H,B", [(128, 28, 64), (256, 14, 64), (512, 7, 64), (128, 28, 256), (64, 9, 5)])
 def test_squeeze_forms_vs_torch(dev, form, C, H, B):
     """Every form of the NHWC bf16 squeeze (k_colreduce_nhwc: threads x pixels in flight,
-    nontemporal loads; k_colreduce_nhwc_dma: LDS-DMA ring of 3 / 4 stages) against the fp32
-    torch mean over the same bf16 activations, both modalities in one launch, incl. a
-    ragged map (9x9, a partial DMA stage) and the north-star batch 256."""
+    nontemporal loads) against the fp32 torch mean over the same bf16 activations, both
+    modalities in one launch, incl. a ragged map (9x9) and the north-star batch 256."""
     from greedy_multimodal_learning_amd import _lib as L
     from greedy_multimodal_learning_amd import ops
     lib = L.load()
@@ -154,13 +152,11 @@ def test_squeeze_forms_vs_torch(dev, form, C, H, B):
     sq = torch.empty(B, 2 * C, device=dev)
     try:
         L.check(lib.gm_mmtm_set_reduce_form(form[0], form[1]), "form")
-        L.check(lib.gm_mmtm_set_reduce_dma(form[2]), "dma")
         ops.spatial_reduce([dict(x=xs[0], C=C, HW=H * H, out=sq, ld_out=2 * C, scale=1.0 / (H * H)),
                             dict(x=xs[1], C=C, HW=H * H, out=sq, out_off=C, ld_out=2 * C, scale=1.0 / (H * H))],
                            B, L.GM_BF16, L.GM_NHWC, dev)
         torch.cuda.synchronize()
     finally:
         L.check(lib.gm_mmtm_set_reduce_form(-256, 4), "form")
-        L.check(lib.gm_mmtm_set_reduce_dma(0), "dma")
     ref = torch.cat([x.float().mean(dim=(2, 3)) for x in xs], dim=1)
     torch.testing.assert_close(sq, ref, rtol=1e-5, atol=1e-6)

@@ -39,8 +39,6 @@ def main():
     pipes = a.pipes.replace("+", ",").split(",")
 
     def select(p):  # "h", "h5", "h6": the halo kernel (+ diagnostics); "H...": 256-pixel halo tiles;
-        # "W<n>": halo kernel + weight-gradient tile form n (gm_conv_set_wgrad_wide)
-        L.check(lib.gm_conv_set_wgrad_wide(int(p[1:]) if p[0] == "W" else 0), "set_wgrad_wide")
         # "o": the halo kernel with run-time tap decode (k_conv_halo) instead of k_conv_h9;
         # "fBN.NB": k_conv_h9 forced to BN-channel tiles and an NB-stage weight ring
         # "s<n>": split-K target n (0: never split), auto form otherwise

@@ -82,16 +82,15 @@ def main():
     if a.mode == "ab":  # interleaved rounds of the unroll forms in one process
         from greedy_multimodal_learning_amd import _lib as L
         lib = L.load()
-        res = {u: [] for u in ((256, 4, 0), (-256, 4, 0), (-256, 4, 3), (-256, 4, 4))}
+        res = {u: [] for u in ((256, 4), (-256, 4), (-256, 8), (-1024, 4))}
         for _ in range(5):
             for u in res:
-                L.check(lib.gm_mmtm_set_reduce_form(*u[:2]), "set_reduce_form")
-                L.check(lib.gm_mmtm_set_reduce_dma(u[2]), "set_reduce_dma")
+                L.check(lib.gm_mmtm_set_reduce_form(*u), "set_reduce_form")
                 nb, secs, _ = measure(torch.device("cuda:0"), a.batch)
                 res[u].append(secs * 1e6)
         for u, ts in res.items():
             ts.sort()
-            print(f"threads, unroll, dma stages {u}: median {ts[len(ts) // 2]:.2f} us  min {ts[0]:.2f} us  "
+            print(f"threads (negative: nontemporal), unroll {u}: median {ts[len(ts) // 2]:.2f} us  min {ts[0]:.2f} us  "
                   f"-> {nb / ts[len(ts) // 2] / 1e3:.0f} GB/s ({nb / ts[len(ts) // 2] / 1e3 / 8000:.3f} of 8 TB/s)")
         return
     if a.mode == "run":
