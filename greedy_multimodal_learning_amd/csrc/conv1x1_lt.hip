@@ -13,8 +13,11 @@
 //   dgrad dX^T (C x M) = op_T(wt: K x C) . (dy: K x M)       (+ addend as the C matrix)
 //   wgrad dW^T (C x K) = (x: C x M) . op_T(dy: K x M)         (fp32 out, beta = accumulate)
 // The view groups are the GEMM batch (strided).  Algorithms come from hipBLASLt's heuristic
-// with no workspace (nothing allocated), cached per problem; the handle is created on first
-// use (eager warm-up steps run before any graph capture).
+// with no workspace (nothing allocated), cached per problem; a handle per stream, created on
+// first use (eager warm-up steps run before any graph capture).  OFF by default: the C5
+// training step faulted with it (an illegal address inside the step, r04) while every
+// isolated shape, the C5 ones at 12 view groups included, matches fp32 PyTorch
+// (test_conv1x1_gemm_vs_fp32); GM_CONV1X1_LT=1 / gm_conv_set_1x1_gemm(1) turn it on.
 #include <hipblaslt/hipblaslt.h>
 
 #include <cstdint>
@@ -29,31 +32,35 @@ namespace gm {
 namespace {
 
 int g_conv_lt = [] {
-    const char* e = getenv("GM_CONV1X1_LT");  // 0: the 1x1 shapes take the im2col kernel
-    return e ? atoi(e) : 1;
+    const char* e = getenv("GM_CONV1X1_LT");  // 1: the 1x1 shapes take hipBLASLt (default: im2col)
+    return e ? atoi(e) : 0;
 }();
 
-hipblasLtHandle_t lt_handle() {
-    static hipblasLtHandle_t h = [] {
-        hipblasLtHandle_t x = nullptr;
-        if (hipblasLtCreate(&x) != HIPBLAS_STATUS_SUCCESS) x = nullptr;
-        return x;
-    }();
-    return h;
+// one handle per stream: the step runs weight gradients on a side stream beside the main
+// chain, and a handle's internal state must not be shared by concurrent GEMMs
+std::mutex g_lt_mu;
+hipblasLtHandle_t lt_handle(hipStream_t st) {
+    static std::map<hipStream_t, hipblasLtHandle_t> hs;
+    std::lock_guard<std::mutex> g(g_lt_mu);
+    auto it = hs.find(st);
+    if (it != hs.end()) return it->second;
+    hipblasLtHandle_t x = nullptr;
+    if (hipblasLtCreate(&x) != HIPBLAS_STATUS_SUCCESS) x = nullptr;
+    hs[st] = x;
+    return x;
 }
 
 struct LtPlan {
     hipblasLtMatmulDesc_t op = nullptr;
     hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr, ld = nullptr;
     hipblasLtMatmulAlgo_t algo;
-    bool ok = false;
+    bool ok = false, bad = false;  // bad: no workspace-free algorithm (the caller falls back)
 };
 
 // (transA, transB, m, n, k, lda, ldb, ldc, batch, sa, sb, sc, d_f32, c_is_d)
 using LtKey = std::tuple<int, int, long long, long long, long long, long long, long long, long long, int, long long,
                          long long, long long, int>;
 
-std::mutex g_lt_mu;
 std::map<LtKey, LtPlan> g_lt_plans;
 
 hipblasLtMatrixLayout_t layout(hipDataType t, long long rows, long long cols, long long ld, int batch, long long stride) {
@@ -72,13 +79,14 @@ hipblasLtMatrixLayout_t layout(hipDataType t, long long rows, long long cols, lo
 int lt_gemm(bool ta, bool tb, long long m, long long n, long long k, const void* A, long long lda, long long sa,
             const void* B, long long ldb, long long sb, const void* C, void* D, long long ldc, long long sc,
             bool d_f32, int batch, float beta, hipStream_t st, const char* fn) {
-    hipblasLtHandle_t h = lt_handle();
+    hipblasLtHandle_t h = lt_handle(st);
     GM_REQUIRE(h != nullptr, "%s: hipblasLtCreate failed", fn);
     const LtKey key{ta, tb, m, n, k, lda, ldb, ldc, batch, sa, sb, sc, d_f32};
     LtPlan* pl;
     {
         std::lock_guard<std::mutex> g(g_lt_mu);
         pl = &g_lt_plans[key];
+        if (pl->bad) return GM_E_UNSUP;
         if (!pl->ok) {
             const hipDataType dt = d_f32 ? HIP_R_32F : HIP_R_16BF;
             GM_REQUIRE(hipblasLtMatmulDescCreate(&pl->op, HIPBLAS_COMPUTE_32F, HIP_R_32F) == HIPBLAS_STATUS_SUCCESS,
@@ -95,14 +103,22 @@ int lt_gemm(bool ta, bool tb, long long m, long long n, long long k, const void*
             hipblasLtMatmulPreferenceCreate(&pref);
             uint64_t ws = 0;  // no workspace: the library allocates nothing
             hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &ws, sizeof(ws));
-            hipblasLtMatmulHeuristicResult_t res[1];
+            // the first candidate that needs no workspace (the preference alone does not
+            // guarantee it: a solution with a workspace requirement would write through a
+            // null workspace)
+            hipblasLtMatmulHeuristicResult_t res[16];
             int found = 0;
             const hipblasStatus_t s =
-                hipblasLtMatmulAlgoGetHeuristic(h, pl->op, pl->la, pl->lb, pl->lc, pl->ld, pref, 1, res, &found);
+                hipblasLtMatmulAlgoGetHeuristic(h, pl->op, pl->la, pl->lb, pl->lc, pl->ld, pref, 16, res, &found);
             hipblasLtMatmulPreferenceDestroy(pref);
-            GM_REQUIRE(s == HIPBLAS_STATUS_SUCCESS && found > 0, "%s: no hipBLASLt algorithm for %lldx%lldx%lld", fn,
-                       m, n, k);
-            pl->algo = res[0].algo;
+            int pick = -1;
+            for (int i = 0; s == HIPBLAS_STATUS_SUCCESS && i < found && pick < 0; ++i)
+                if (res[i].state == HIPBLAS_STATUS_SUCCESS && res[i].workspaceSize == 0) pick = i;
+            if (pick < 0) {  // none: this problem takes the im2col kernel
+                pl->bad = true;
+                return GM_E_UNSUP;
+            }
+            pl->algo = res[pick].algo;
             pl->ok = true;
         }
     }

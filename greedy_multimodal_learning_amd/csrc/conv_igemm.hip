@@ -2755,8 +2755,10 @@ extern "C" int gm_conv2d_fwd_hw_bf16(const gm_conv_desc_hw* d, const void* x, co
     if (rc) return rc;
     GM_REQUIRE(x && w && y, "conv fwd: null pointer");
     const long long M = (long long)d->N * d->H * d->W;
-    if (gm::conv1x1_lt_ok(d->R, d->S, d->stride_h, d->stride_w, d->pad_h, d->pad_w, M))
-        return gm::conv1x1_lt_fwd(M, d->C, d->K, 1, x, 0, w, 0, y, 0, as_stream(stream));
+    if (gm::conv1x1_lt_ok(d->R, d->S, d->stride_h, d->stride_w, d->pad_h, d->pad_w, M)) {
+        const int lr = gm::conv1x1_lt_fwd(M, d->C, d->K, 1, x, 0, w, 0, y, 0, as_stream(stream));
+        if (lr != GM_E_UNSUP) return lr;  // no workspace-free GEMM: the im2col kernel
+    }
     ConvArgs a;
     fwd_setup(d, x, w, y, a);
     return pick_and_launch(a, as_stream(stream), nullptr, 0);
@@ -2769,8 +2771,10 @@ extern "C" int gm_conv2d_fwd_ex_bf16(const gm_conv_desc* d, const void* x, const
     GM_REQUIRE(x && w && y, "conv fwd: null pointer");
     const gm_conv_desc_hw h = to_hw(d);
     const long long M = (long long)d->N * d->H * d->W;
-    if (gm::conv1x1_lt_ok(d->R, d->S, d->stride, d->stride, d->pad, d->pad, M))
-        return gm::conv1x1_lt_fwd(M, d->C, d->K, 1, x, 0, w, 0, y, 0, as_stream(stream));
+    if (gm::conv1x1_lt_ok(d->R, d->S, d->stride, d->stride, d->pad, d->pad, M)) {
+        const int lr = gm::conv1x1_lt_fwd(M, d->C, d->K, 1, x, 0, w, 0, y, 0, as_stream(stream));
+        if (lr != GM_E_UNSUP) return lr;  // no workspace-free GEMM: the im2col kernel
+    }
     ConvArgs a;
     fwd_setup(&h, x, w, y, a);
     return pick_and_launch(a, as_stream(stream), ws, ws_bytes);
@@ -2792,8 +2796,10 @@ extern "C" int gm_conv2d_fwd_grouped_bf16(const gm_conv_desc_hw* d, int G, const
                    -w_stride >= (long long)d->K * d->R * d->S * d->C,
                "conv fwd: group weight stride %lld shorter than one weight", w_stride);
     const long long M = (long long)d->N * d->H * d->W;
-    if (gm::conv1x1_lt_ok(d->R, d->S, d->stride_h, d->stride_w, d->pad_h, d->pad_w, M) && (G == 1 || w_stride > 0))
-        return gm::conv1x1_lt_fwd(M, d->C, d->K, G, x, M * d->C, w, w_stride, y, M * d->K, as_stream(stream));
+    if (gm::conv1x1_lt_ok(d->R, d->S, d->stride_h, d->stride_w, d->pad_h, d->pad_w, M) && (G == 1 || w_stride > 0)) {
+        const int lr = gm::conv1x1_lt_fwd(M, d->C, d->K, G, x, M * d->C, w, w_stride, y, M * d->K, as_stream(stream));
+        if (lr != GM_E_UNSUP) return lr;  // no workspace-free GEMM: the im2col kernel
+    }
     ConvArgs a;
     fwd_setup(d, x, w, y, a);
     a.G = G;
@@ -2855,9 +2861,11 @@ extern "C" int gm_conv2d_dgrad_grouped_bf16(const gm_conv_desc* d, int G, const 
     const int P = (d->H + 2 * d->pad - d->R) / d->stride + 1;
     const int Q = (d->W + 2 * d->pad - d->S) / d->stride + 1;
     const long long M = (long long)d->N * d->H * d->W;
-    if (gm::conv1x1_lt_ok(d->R, d->S, d->stride, d->stride, d->pad, d->pad, M) && (G == 1 || wt_stride > 0))
-        return gm::conv1x1_lt_dgrad(M, d->C, d->K, G, dy, M * d->K, wt, wt_stride, dx, M * d->C, addend,
+    if (gm::conv1x1_lt_ok(d->R, d->S, d->stride, d->stride, d->pad, d->pad, M) && (G == 1 || wt_stride > 0)) {
+        const int lr = gm::conv1x1_lt_dgrad(M, d->C, d->K, G, dy, M * d->K, wt, wt_stride, dx, M * d->C, addend,
                                     as_stream(stream));
+        if (lr != GM_E_UNSUP) return lr;  // no workspace-free GEMM: the im2col kernel
+    }
     ConvArgs a;
     const bool full = dgrad_setup(d, dy, wt, dx, a);
     a.G = G;
@@ -2885,8 +2893,10 @@ extern "C" int gm_conv2d_dgrad_add_bf16(const gm_conv_desc* d, const void* dy, c
     // and stores that element from the same thread, and pixels no parity class covers
     // then simply keep the addend (no zero / copy pass)
     const long long M = (long long)d->N * d->H * d->W;
-    if (gm::conv1x1_lt_ok(d->R, d->S, d->stride, d->stride, d->pad, d->pad, M))
-        return gm::conv1x1_lt_dgrad(M, d->C, d->K, 1, dy, 0, wt, 0, dx, 0, addend, as_stream(stream));
+    if (gm::conv1x1_lt_ok(d->R, d->S, d->stride, d->stride, d->pad, d->pad, M)) {
+        const int lr = gm::conv1x1_lt_dgrad(M, d->C, d->K, 1, dy, 0, wt, 0, dx, 0, addend, as_stream(stream));
+        if (lr != GM_E_UNSUP) return lr;  // no workspace-free GEMM: the im2col kernel
+    }
     ConvArgs a;
     const bool full = dgrad_setup(d, dy, wt, dx, a);
     a.addend = (const uint16_t*)addend;

@@ -409,8 +409,8 @@ __global__ __launch_bounds__(256) void k_conv_wgrad4(WgradArgs a) {
 // Both operands come through ds_read_b64_tr_b16 transposed reads (rows of 128 B, chunk XOR
 // 4 * ((row >> 1) & 1): conflict-free for any 4 consecutive rows).  Four loader waves (one
 // beside each compute wave's SIMD) keep D super-rows of LDS-DMA in flight (dy of super-row S
-// with x of S + 2) under counted vmcnt waits; one raw barrier per super-row, before its third
-// slice (the dy reads run two slices ahead, the x reads one image row ahead).  Each workgroup
+// with x of S + 2) under counted vmcnt waits; one raw barrier per super-row, before its second
+// slice (the dy reads run three slices ahead, the x reads one image row ahead).  Each workgroup
 // writes its fp32 partial slab [64][9 x 64] (split over rows; k_wgrad_sum reduces the splits in
 // a fixed order).
 struct WHaloArgs {
@@ -423,7 +423,7 @@ struct WHaloArgs {
     long long gs_dy, gs_x;  // group strides (elements)
 };
 
-template <int D, int PP, bool PB, int ABL = 0>
+template <int D, int PP, int ABL = 0>
 __global__ __launch_bounds__(512) void k_wgrad_halo64(WHaloArgs a) {
     static_assert(D >= 2 && (PP == 16 || PP == 32 || PP == 64), "halo64: D >= 2 super-rows in flight, PP = 16/32/64");
     constexpr int RPS = 64 / PP, SPR = PP / 16;  // image rows per super-row, k-slices per image row
@@ -575,15 +575,18 @@ __global__ __launch_bounds__(512) void k_wgrad_halo64(WHaloArgs a) {
         }
         F[0] = rd(dy_base(0) + a_lane);
         F[1] = rd(dy_base(0) + a_lane + 2048);
+        F[2] = rd(dy_base(0) + a_lane + 4096);
     }
     for (int R = R0; R < R1; ++R) {
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
             const int j = ks / SPR, kk = ks % SPR;  // image row of the super-row, slice of it
-            if (ks == 2)  // super-row R + 1 landed; every wave done with super-row R - 1
+            if (ks == 1)  // super-row R + 1 landed; every wave done with super-row R - 1
                 __builtin_amdgcn_s_barrier();
-            // everything this slice consumes was read a slice or more ago
-            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(F[ks]), "+v"(F[(ks + 1) & 3]), "+v"(Xm[kk]), "+v"(X0[kk]),
+            // everything this slice consumes has landed: the last slice's reads were its x
+            // fragment, then the dy fragment three slices ahead - only that one may still fly
+            // (LDS reads return in order; no other LDS or scalar-memory op in this loop)
+            asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(F[ks]), "+v"(F[(ks + 1) & 3]), "+v"(Xm[kk]), "+v"(X0[kk]),
                          "+v"(Xp[kk]));
             const u32x4 f2 = F[ks], fn = F[(ks + 1) & 3];
             // kernel rows 0 / 2 outside the image take zero operands (masks, not branches: a
@@ -593,12 +596,12 @@ __global__ __launch_bounds__(512) void k_wgrad_halo64(WHaloArgs a) {
             // shift s = 2 (the fragment as read); reads for later slices threaded behind
             mfma(2, f2, xm);
             __builtin_amdgcn_sched_barrier(0);
-            // dy two slices ahead (slices 2, 3 read super-row R + 1's first two)
-            F[(ks + 2) & 3] = rd(dy_base(ks >= 2 ? 1 : 0) + a_lane + (unsigned)(((ks + 2) & 3) * 2048));
+            Xn[kk] = rd(xaddr(j + 2, kk));  // image row + 2, for the next output row
             __builtin_amdgcn_sched_barrier(0);
             mfma(5, f2, x0);
             __builtin_amdgcn_sched_barrier(0);
-            Xn[kk] = rd(xaddr(j + 2, kk));  // image row + 2, for the next output row
+            // dy three slices ahead (slices 1..3 read super-row R + 1's)
+            F[(ks + 3) & 3] = rd(dy_base(ks >= 1 ? 1 : 0) + a_lane + (unsigned)(((ks + 3) & 3) * 2048));
             __builtin_amdgcn_sched_barrier(0);
             mfma(8, f2, xp);
             // shifts s = 1, 0: rows m + 1, m + 2 - the fragment moved up by one / two elements,
@@ -622,7 +625,7 @@ __global__ __launch_bounds__(512) void k_wgrad_halo64(WHaloArgs a) {
             if (kk == SPR - 1) {  // the image row ends: rotate the x rows, next output row
                 // (the register copies read the prefetched fragments: their reads must have landed)
 #pragma unroll
-                for (int q = 0; q < SPR; ++q) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(Xn[q]));
+                for (int q = 0; q < SPR; ++q) asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(Xn[q]));
 #pragma unroll
                 for (int q = 0; q < SPR; ++q) {
                     Xm[q] = X0[q];
@@ -636,28 +639,20 @@ __global__ __launch_bounds__(512) void k_wgrad_halo64(WHaloArgs a) {
         xsl = xsl + 1 == XS ? 0 : xsl + 1;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    // the split's partial in the accumulators' own layout, [tile][wave][tap][lane][16 e]: each
-    // lane stores its 16 values of a tap contiguously (PB = bf16: 2 x 16 B, else 4 x 16 B), a
-    // wave 64 contiguous lanes; k_wgrad_sum_raw maps (wave, tap, lane, e) back to dw[k][tap][c]
-    const size_t pos = ((((size_t)grp * a.splits + split) * (a.kt * a.ct) + tile) * 4 + wave) * 9 * 64 + lane;
-    if constexpr (PB) {
-        uint4* out = reinterpret_cast<uint4*>(a.part) + pos * 2;
+    // D[k][c]: col = lane & 31 (c), row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5) (k)
+    // the split's slab [K][9*C]; this tile fills rows kb*64 .., columns tap*C + cb*64 ..
+    // (bf16 partials in the accumulators' own layout with 16-B stores measured no faster:
+    // l1 49.6 vs 49.4 us with the sum, r04)
+    const int TC = 9 * a.C;
+    float* out = a.part + ((size_t)grp * a.splits + split) * ((size_t)a.K * TC);
 #pragma unroll
-        for (int tp = 0; tp < 9; ++tp) {
-            uint32_t w[8];
+    for (int tp = 0; tp < 9; ++tp) {
+        const int col = tp * a.C + cb * 64 + ch * 32 + (lane & 31);
 #pragma unroll
-            for (int e = 0; e < 8; ++e)
-                w[e] = (uint32_t)Elem<uint16_t>::f2bf(acc[tp][2 * e]) | ((uint32_t)Elem<uint16_t>::f2bf(acc[tp][2 * e + 1]) << 16);
-            out[tp * 128] = make_uint4(w[0], w[1], w[2], w[3]);
-            out[tp * 128 + 1] = make_uint4(w[4], w[5], w[6], w[7]);
+        for (int e = 0; e < 16; ++e) {
+            const int row = kb * 64 + kh * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+            out[(size_t)row * TC + col] = acc[tp][e];
         }
-    } else {
-        float4* out = reinterpret_cast<float4*>(a.part) + pos * 4;
-#pragma unroll
-        for (int tp = 0; tp < 9; ++tp)
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                out[tp * 256 + q] = make_float4(acc[tp][4 * q], acc[tp][4 * q + 1], acc[tp][4 * q + 2], acc[tp][4 * q + 3]);
     }
 }
 
@@ -711,73 +706,6 @@ __global__ __launch_bounds__(256) void k_wgrad_sum(const float* __restrict__ par
         acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
     *o = acc;
-}
-
-// dw[k][tap][c] (+)= sum over splits of k_wgrad_halo64's raw partials ([G][splits][tile][wave]
-// [tap][lane][16 e], fp32 or bf16): a thread owns 8 values (half of one lane's 16) of one
-// (tile, wave, tap, lane) position, R split lanes per position sum splits r, r + R, ... and
-// combine in lane order through LDS (fixed order: deterministic), then scatter to dw.
-template <int R, bool PB>
-__global__ __launch_bounds__(256) void k_wgrad_sum_raw(const void* __restrict__ part, int splits, int tiles, int kt,
-                                                       int K, int C, int accumulate, float* __restrict__ dw,
-                                                       long long gs_dw) {
-    constexpr int CPB = 256 / R;
-    const size_t npos = (size_t)tiles * 4 * 9 * 64 * 2;  // 8-value halves per split slab
-    const int g = blockIdx.y;
-    dw += g * gs_dw;
-    const int t = threadIdx.x, col = t % CPB, r = t / CPB;
-    const size_t h = (size_t)blockIdx.x * CPB + col;  // half index within a slab
-    float acc[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
-    if (h < npos) {
-        for (int sp = r; sp < splits; sp += R) {
-            const size_t i = ((size_t)g * splits + sp) * npos + h;
-            if constexpr (PB) {
-                const uint4 v = reinterpret_cast<const uint4*>(part)[i];
-                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    acc[2 * q] += __uint_as_float(w[q] << 16);
-                    acc[2 * q + 1] += __uint_as_float(w[q] & 0xffff0000u);
-                }
-            } else {
-                const float4 v0 = reinterpret_cast<const float4*>(part)[2 * i];
-                const float4 v1 = reinterpret_cast<const float4*>(part)[2 * i + 1];
-                acc[0] += v0.x; acc[1] += v0.y; acc[2] += v0.z; acc[3] += v0.w;
-                acc[4] += v1.x; acc[5] += v1.y; acc[6] += v1.z; acc[7] += v1.w;
-            }
-        }
-    }
-    if constexpr (R > 1) {
-        __shared__ float red[8][256];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) red[e][t] = acc[e];
-        __syncthreads();
-        if (r != 0) return;
-#pragma unroll
-        for (int q = 1; q < R; ++q)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) acc[e] += red[e][q * CPB + col];
-    }
-    if (h >= npos) return;
-    // h -> (tile, wave, tap, lane, half): half-slab of 8 values e = 8 half .. + 7
-    size_t q = h;
-    const int half = (int)(q & 1); q >>= 1;
-    const int lane = (int)(q % 64); q /= 64;
-    const int tp = (int)(q % 9); q /= 9;
-    const int wave = (int)(q % 4); q /= 4;
-    const int tile = (int)q;
-    const int kb = tile % kt, cb = tile / kt, kh = wave & 1, ch = wave >> 1;
-    const int TC = 9 * C;
-    const int c = tp * C + cb * 64 + ch * 32 + (lane & 31);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const int e = 8 * half + j;
-        const int k = kb * 64 + kh * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-        float* o = dw + (size_t)k * TC + c;
-        *o = accumulate ? *o + acc[j] : acc[j];
-    }
 }
 
 // dw = sum over splits (fixed order); also the [K][T][Cpad] -> [K][T][Creal] crop
@@ -884,10 +812,6 @@ static gm_conv_desc_hw to_hw(const gm_conv_desc* d) {
     return gm_conv_desc_hw{d->N, d->H, d->W, d->C, d->K, d->R, d->S, d->stride, d->stride, d->pad, d->pad};
 }
 
-// k_wgrad_halo64's split partials in bf16 (halves the partial-slab traffic; the splits are
-// summed in fp32) or fp32
-static constexpr bool kH64Bf16Part = true;
-
 // k_wgrad_halo64 serves 3x3 / s1 / p1 shapes with W <= 62: image rows of PP = 16, 32 or 64
 // positions (PP >= W + 2), 64 / PP of them per super-row
 static int halo64_pp(int W) { return W + 2 <= 16 ? 16 : (W + 2 <= 32 ? 32 : 64); }
@@ -911,7 +835,7 @@ static int halo64_splits(const gm_conv_desc_hw* d, int G) {
 
 extern "C" size_t gm_conv2d_wgrad_grouped_scratch(const gm_conv_desc_hw* d, int G) {
     if (!d || d->stride_h < 1 || d->stride_w < 1 || G < 1) return 0;
-    if (halo64_ok(d)) return (size_t)G * halo64_splits(d, G) * d->K * 9 * d->C * (kH64Bf16Part ? 2 : 4);
+    if (halo64_ok(d)) return (size_t)G * halo64_splits(d, G) * d->K * 9 * d->C * 4;
     const WPlan w = plan(d, G);
     const size_t slab = (size_t)d->K * d->R * d->S * d->C;
     return (size_t)G * w.splits * slab * sizeof(float);
@@ -951,9 +875,11 @@ extern "C" int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, con
                "conv wgrad: group gradient stride %lld overlaps one gradient", dw_stride);
     const long long M = (long long)d->N * d->H * d->W;
     if (gm::conv1x1_lt_ok(d->R, d->S, d->stride_h, d->stride_w, d->pad_h, d->pad_w, M) && c_real == d->C &&
-        (G == 1 || dw_stride > 0))
-        return gm::conv1x1_lt_wgrad(M, d->C, d->K, G, dy, M * d->K, x, M * d->C, dw, dw_stride, accumulate,
+        (G == 1 || dw_stride > 0)) {
+        const int lr = gm::conv1x1_lt_wgrad(M, d->C, d->K, G, dy, M * d->K, x, M * d->C, dw, dw_stride, accumulate,
                                     as_stream(stream));
+        if (lr != GM_E_UNSUP) return lr;  // no workspace-free GEMM: the im2col kernel
+    }
     const size_t need = gm_conv2d_wgrad_grouped_scratch(d, G);
     GM_REQUIRE(scratch && scratch_bytes >= need, "conv wgrad: scratch %zu < %zu", scratch_bytes, need);
     hipStream_t st0 = as_stream(stream);
@@ -978,11 +904,11 @@ extern "C" int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, con
             constexpr size_t lds = (size_t)(D + 3) * 8192 + (size_t)(D + 1) * (8192 + 256);
             static bool attr = false;
             if (!attr) {
-                (void)hipFuncSetAttribute((const void*)k_wgrad_halo64<D, PP, kH64Bf16Part, AB>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                (void)hipFuncSetAttribute((const void*)k_wgrad_halo64<D, PP, AB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)lds);
                 attr = true;
             }
-            k_wgrad_halo64<D, PP, kH64Bf16Part, AB><<<nblk, 512, lds, st0>>>(h);
+            k_wgrad_halo64<D, PP, AB><<<nblk, 512, lds, st0>>>(h);
         };
         static const int abl = [] { const char* e = getenv("GM_H64_ABL"); return e ? atoi(e) : 0; }();
         using A0 = std::integral_constant<int, 0>;
@@ -994,25 +920,21 @@ extern "C" int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, con
         else go(std::integral_constant<int, 64>{}, A0{});
         int rc = check_launch("k_wgrad_halo64");
         if (rc) return rc;
-        const int tiles = h.kt * h.ct;
-        const size_t npos = (size_t)tiles * 4 * 9 * 64 * 2;  // 8-value halves per split slab
+        const size_t slab = (size_t)d->K * 9 * d->C;
+        const size_t ncol = slab / 4;
         int R = 1;
-        while (R < 32 && R * 2 <= h.splits && (npos * R + 255) / 256 < 512) R *= 2;
-        const dim3 gg((unsigned)((npos + 256 / R - 1) / (256 / R)), (unsigned)G);
-        auto sum = [&](auto rc_) {
-            constexpr int RR = decltype(rc_)::value;
-            k_wgrad_sum_raw<RR, kH64Bf16Part><<<gg, 256, 0, st0>>>(h.part, h.splits, tiles, h.kt, d->K, d->C, accumulate,
-                                                                   dw, dw_stride);
-        };
+        while (R < 32 && R * 2 <= h.splits && (ncol * R + 255) / 256 < 512) R *= 2;
+        const dim3 gg((unsigned)((ncol + 256 / R - 1) / (256 / R)), (unsigned)G);
+        float* part = h.part;
         switch (R) {
-            case 1: sum(std::integral_constant<int, 1>{}); break;
-            case 2: sum(std::integral_constant<int, 2>{}); break;
-            case 4: sum(std::integral_constant<int, 4>{}); break;
-            case 8: sum(std::integral_constant<int, 8>{}); break;
-            case 16: sum(std::integral_constant<int, 16>{}); break;
-            default: sum(std::integral_constant<int, 32>{}); break;
+            case 1: k_wgrad_sum<1><<<gg, 256, 0, st0>>>(part, h.splits, slab, accumulate, dw, dw_stride); break;
+            case 2: k_wgrad_sum<2><<<gg, 256, 0, st0>>>(part, h.splits, slab, accumulate, dw, dw_stride); break;
+            case 4: k_wgrad_sum<4><<<gg, 256, 0, st0>>>(part, h.splits, slab, accumulate, dw, dw_stride); break;
+            case 8: k_wgrad_sum<8><<<gg, 256, 0, st0>>>(part, h.splits, slab, accumulate, dw, dw_stride); break;
+            case 16: k_wgrad_sum<16><<<gg, 256, 0, st0>>>(part, h.splits, slab, accumulate, dw, dw_stride); break;
+            default: k_wgrad_sum<32><<<gg, 256, 0, st0>>>(part, h.splits, slab, accumulate, dw, dw_stride); break;
         }
-        return check_launch("k_wgrad_sum_raw");
+        return check_launch("k_wgrad_sum");
     }
     WgradArgs a;
     memset(&a, 0, sizeof(a));

@@ -41,6 +41,8 @@ ENABLED = os.environ.get("GM_VTRUNK", "1") != "0"
 # the stem's pool + BN backward in the gathered two-pass form (GM_FUSED_STEM_BWD=0: the
 # max-pool backward + BatchNorm backward pair, an A/B switch)
 FUSED_STEM_BWD = os.environ.get("GM_FUSED_STEM_BWD", "1") != "0"
+# its statistics pass over the pooled tensors (the forward's selected x) instead of x
+STEM_XSEL = os.environ.get("GM_STEM_XSEL", "1") != "0"
 # the stem BN's statistics from the stem convolution's epilogue (GM_FUSED_STEM_STATS=0: the
 # statistics pass over the convolution's output, an A/B switch)
 FUSED_STEM_STATS = os.environ.get("GM_FUSED_STEM_STATS", "1") != "0"
@@ -516,6 +518,7 @@ class _VBNReluPoolFn(torch.autograd.Function):
         # (and the pooled gradient) instead of x, the gradient and the argmax
         fused_bwd = FUSED_STEM_BWD and (k, s, pad, C) == (3, 2, 1, 64)
         xsel = torch.empty(GN, P, Q, C, device=dev, dtype=BF) if fused_bwd else None
+        ctx.xsel_on = STEM_XSEL
         d = L.PoolDesc(N, H, W, C, k, s, pad)
         L.check(lib.gm_bn_relu_maxpool2d_fwd_grouped_bf16(ctypes.byref(d), G, xb.data_ptr(), coef.data_ptr(),
                                                           y.data_ptr(), idx.data_ptr(), L.ptr(xsel), st),
@@ -547,7 +550,8 @@ class _VBNReluPoolFn(torch.autograd.Function):
             buf = _bn_scratch_g(xb.device, M, C, G)
             d = L.PoolDesc(N, H, W, C, k, s, pad)
             L.check(lib.gm_bn_relu_maxpool2d_bwd_grouped_bf16(ctypes.byref(d), G, dy.data_ptr(), idx.data_ptr(),
-                                                              xsel.data_ptr(), L.arr(L.BnBwd, descs), buf.data_ptr(),
+                                                              xsel.data_ptr() if ctx.xsel_on else 0,
+                                                              L.arr(L.BnBwd, descs), buf.data_ptr(),
                                                               buf.numel(), L.stream_of(xb.device)),
                     "gm_bn_relu_maxpool2d_bwd_grouped_bf16")
             if sunk:

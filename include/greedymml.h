@@ -375,7 +375,7 @@ int gm_conv_set_splitk(int target);
  * 128 channels; the rest take k_conv_wgrad4.  Bit 0 is reserved (must be 0). */
 int gm_conv_set_wgrad_loop(int mode);
 /* 1x1 / stride-1 / pad-0 convolutions (forward, input and weight gradient) as plain GEMMs on
- * hipBLASLt (default on; GM_CONV1X1_LT=0 at load or gm_conv_set_1x1_gemm(0): the im2col kernel). */
+ * hipBLASLt (default off: GM_CONV1X1_LT=1 at load or gm_conv_set_1x1_gemm(1) turn it on). */
 int gm_conv_set_1x1_gemm(int on);
 /* Weight-gradient operand staging: 0 = LDS-DMA pieces, 1 = register-staged (global_load_dwordx4
  * two steps ahead + ds_write_b128; same LDS image and arithmetic), 2 (default) = register-staged

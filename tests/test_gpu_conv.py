@@ -414,8 +414,8 @@ def test_wgrad_halo64_vs_fp32(dev, shape):
     accumulators, super-rows of 64 / PP image rows staged once for all nine taps, rows split
     over the workgroups, slabs summed in a fixed order; PP = 64, 32, 16 for layers 1, 2, 3-4)
     against fp32 PyTorch, grouped over two views, plain and accumulating, ragged batches and
-    image heights that straddle super-rows included; and against k_conv_wgrad4 within the
-    bf16 split-partial rounding."""
+    image heights that straddle super-rows included; and against k_conv_wgrad4 within fp32
+    summation-order noise."""
     import ctypes
     from greedy_multimodal_learning_amd import _lib as L
     from greedy_multimodal_learning_amd import conv as CV
@@ -454,9 +454,7 @@ def test_wgrad_halo64_vs_fp32(dev, shape):
             err = float((got - ref).abs().max() / ref.abs().max())
             assert err < 2e-3, (gi, acc, err)
             old = outs[0][acc][gi].permute(0, 3, 1, 2) - base
-            # bf16 split partials (summed in fp32): ~2^-9 of a partial per split, far below the
-            # bf16 rounding PyTorch's own bf16 weight gradient carries
-            assert float((got - old).abs().max() / ref.abs().max()) < 2e-3
+            assert float((got - old).abs().max() / ref.abs().max()) < 1e-4
 
 
 def test_wgrad_halo64_beside_a_busy_neighbour(dev):
@@ -494,8 +492,9 @@ def test_wgrad_halo64_beside_a_busy_neighbour(dev):
         assert torch.equal(dw, outs[0]), (i, int((~torch.isfinite(dw)).sum()))
 
 
-@pytest.mark.parametrize("shape", [(4, 256, 14, 14, 64), (2, 64, 56, 56, 256), (3, 512, 7, 7, 2048), (1, 8, 5, 3, 16),
-                                   (5, 1024, 14, 14, 256)],
+@pytest.mark.parametrize("shape", [(4, 256, 14, 14, 64), (2, 64, 56, 56, 256), (3, 512, 7, 7, 2048), (1, 64, 5, 3, 128),
+                                   (5, 1024, 14, 14, 256), (8, 256, 56, 56, 64, 12), (8, 64, 56, 56, 256, 12),
+                                   (8, 64, 56, 56, 64, 12), (8, 2048, 7, 7, 512, 12), (8, 512, 28, 28, 128, 12)],
                          ids=lambda s: "x".join(map(str, s)))
 def test_conv1x1_gemm_vs_fp32(dev, shape):
     """1x1 / s1 / p0 convolutions as plain GEMMs (hipBLASLt, conv1x1_lt.hip): forward, input
@@ -505,8 +504,8 @@ def test_conv1x1_gemm_vs_fp32(dev, shape):
     import ctypes
     from greedy_multimodal_learning_amd import _lib as L
     from greedy_multimodal_learning_amd import conv as CV
-    N, C, H, W, K = shape
-    G = 2
+    N, C, H, W, K = shape[:5]
+    G = shape[5] if len(shape) > 5 else 2  # 12: the C5 trunk's view groups
     torch.manual_seed(sum(shape))
     x = torch.randn(G * N, H, W, C, device=dev).bfloat16()
     dy = torch.randn(G * N, H, W, K, device=dev).bfloat16()
@@ -542,7 +541,7 @@ def test_conv1x1_gemm_vs_fp32(dev, shape):
             torch.cuda.synchronize()
             res[mode] = (y, dx, dxa, dws)
     finally:
-        L.check(lib.gm_conv_set_1x1_gemm(1), "1x1 gemm")  # the default
+        L.check(lib.gm_conv_set_1x1_gemm(0), "1x1 gemm")  # the default
     for g in range(G):
         sl = slice(g * N, (g + 1) * N)
         xf, dyf, wf = x[sl].float().reshape(-1, C), dy[sl].float().reshape(-1, K), w[g].float()

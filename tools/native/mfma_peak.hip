@@ -1,24 +1,44 @@
 // Calibration kernel (tools only): back-to-back v_mfma_f32_32x32x16_bf16 on register operands,
 // 8 independent accumulators per wave, `waves` waves per workgroup, one workgroup per CU slot.
 // Measures the MFMA rate the chip sustains under full load (clock included) - the practical
-// ceiling the trunk kernels' roofline fractions are read against.
+// ceiling the trunk kernels' roofline fractions are read against.  mode 0: constant operands;
+// 1: random operands, fixed per lane; 2: random operands changing every iteration (the power
+// draw of real data: MI355X clocks down under it).
 #include <hip/hip_runtime.h>
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-__global__ __launch_bounds__(512) void k_mfma_peak(float* out, int iters) {
+__device__ __forceinline__ unsigned hash(unsigned x) {
+    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+    return x;
+}
+// a random bf16 pair in [-2, 2) (exponent bits kept sane: no inf / nan)
+__device__ __forceinline__ unsigned rnd_pair(unsigned h) { return (h & 0x807f807fU) | 0x3f803f80U; }
+
+__global__ __launch_bounds__(512) void k_mfma_peak(float* out, int iters, int mode) {
     floatx16 acc[8];
     for (int i = 0; i < 8; ++i)
         for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
-    bf16x8 a, b;
-    for (int e = 0; e < 8; ++e) {
-        a[e] = (__bf16)(float)(threadIdx.x & 7);
-        b[e] = (__bf16)(float)(e + 1);
+    u32x4 a, b;
+    const unsigned seed = blockIdx.x * 1024 + threadIdx.x;
+    for (int q = 0; q < 4; ++q) {
+        a[q] = mode ? rnd_pair(hash(seed * 8 + q)) : 0x3f803f80U;
+        b[q] = mode ? rnd_pair(hash(seed * 8 + 4 + q)) : 0x40004000U;
     }
     for (int it = 0; it < iters; ++it) {
+        if (mode == 2) {  // new operand bits every iteration (sign and mantissa bits flip)
+            const unsigned f = hash(it + seed) & 0x807f807fU;
+            for (int q = 0; q < 4; ++q) {
+                a[q] ^= f;
+                b[q] ^= (f >> 1) & 0x807f807fU;
+            }
+        }
 #pragma unroll
-        for (int i = 0; i < 8; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[i], 0, 0, 0);
+        for (int i = 0; i < 8; ++i)
+            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b),
+                                                            acc[i], 0, 0, 0);
     }
     float s = 0.f;
     for (int i = 0; i < 8; ++i)
@@ -26,7 +46,7 @@ __global__ __launch_bounds__(512) void k_mfma_peak(float* out, int iters) {
     if (s == 12345.678f) out[threadIdx.x] = s;  // keep the loop alive
 }
 
-extern "C" int mfma_peak_launch(float* out, int blocks, int threads, int iters, void* stream) {
-    k_mfma_peak<<<blocks, threads, 0, (hipStream_t)stream>>>(out, iters);
+extern "C" int mfma_peak_launch(float* out, int blocks, int threads, int iters, int mode, void* stream) {
+    k_mfma_peak<<<blocks, threads, 0, (hipStream_t)stream>>>(out, iters, mode);
     return (int)hipGetLastError();
 }
