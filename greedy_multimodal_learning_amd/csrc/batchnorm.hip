@@ -517,6 +517,16 @@ struct StemPoolGeo {
     const uint4* xs;         // [G*Ng][P][Q][C] bf16 selected x (optional)
 };
 
+typedef unsigned u32x4v_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld_nt16(const uint4* p) {  // streamed once: nontemporal
+    const u32x4v_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4v_t*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st_nt16(uint4* p, uint4 v) {
+    const u32x4v_t w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<u32x4v_t*>(p));
+}
+
 template <bool APPLY>
 __global__ __launch_bounds__(kT) void k_stem_pool_bn_bwd(ReduceArgs a0, StemPoolGeo pg) {
     const ReduceArgs a = group_args(a0);
@@ -579,7 +589,7 @@ __global__ __launch_bounds__(kT) void k_stem_pool_bn_bwd(ReduceArgs a0, StemPool
         for (int q = 0; q < 4; ++q) {
             const int h = 2 * k + (q >> 1), w = 2 * l + (q & 1);
             const bool in = h < pg.H && w < pg.W;
-            it.xv[q] = X[(((long long)n * pg.H + (in ? h : 2 * k)) * pg.W + (in ? w : 2 * l)) * C8 + cg];
+            it.xv[q] = ld_nt16(&X[(((long long)n * pg.H + (in ? h : 2 * k)) * pg.W + (in ? w : 2 * l)) * C8 + cg]);
         }
     };
     auto compute = [&](const Item& it) {
@@ -619,7 +629,7 @@ __global__ __launch_bounds__(kT) void k_stem_pool_bn_bwd(ReduceArgs a0, StemPool
                 float o[8];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) o[j] = fmaf(ca[j], d[j], fmaf(cb[j], xf[j], cc[j]));
-                reinterpret_cast<uint4*>(a.yout)[(((long long)n * pg.H + h) * pg.W + w) * C8 + cg] = pack8(o);
+                st_nt16(&reinterpret_cast<uint4*>(a.yout)[(((long long)n * pg.H + h) * pg.W + w) * C8 + cg], pack8(o));
             } else {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
@@ -636,8 +646,17 @@ __global__ __launch_bounds__(kT) void k_stem_pool_bn_bwd(ReduceArgs a0, StemPool
     };
     if (APPLY) {
         // (the coefficient registers hold channel group cg0: a grid-stride step is a multiple of C8)
+        // two items' loads in flight per thread
         const long long stride = (long long)gridDim.x * kT;
-        for (long long i = (long long)blockIdx.x * kT + t; i < pg.items; i += stride) item(i);
+        long long i = (long long)blockIdx.x * kT + t;
+        for (; i + stride < pg.items; i += 2 * stride) {
+            Item u, v;
+            load(i, u);
+            load(i + stride, v);
+            compute(u);
+            compute(v);
+        }
+        if (i < pg.items) item(i);
         return;
     }
     const int rc = blockIdx.x;

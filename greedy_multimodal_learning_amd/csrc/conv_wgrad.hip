@@ -423,7 +423,7 @@ struct WHaloArgs {
     long long gs_dy, gs_x;  // group strides (elements)
 };
 
-template <int D, int PP, int ABL = 0>
+template <int D, int PP>
 __global__ __launch_bounds__(512) void k_wgrad_halo64(WHaloArgs a) {
     static_assert(D >= 2 && (PP == 16 || PP == 32 || PP == 64), "halo64: D >= 2 super-rows in flight, PP = 16/32/64");
     constexpr int RPS = 64 / PP, SPR = PP / 16;  // image rows per super-row, k-slices per image row
@@ -468,7 +468,7 @@ __global__ __launch_bounds__(512) void k_wgrad_halo64(WHaloArgs a) {
             dyo[j] = dpx[j] * a.K + sc;
         }
         auto dma = [&](const void* src, int off) __attribute__((always_inline)) {
-            if (ABL != 3) __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + off), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + off), 16, 0, 0);
         };
         auto issue_x = [&](int R, int xs) __attribute__((always_inline)) {  // x super-row R into slot xs
 #pragma unroll
@@ -539,16 +539,11 @@ __global__ __launch_bounds__(512) void k_wgrad_halo64(WHaloArgs a) {
     u32x4 Xm[SPR], X0[SPR], Xp[SPR], Xn[SPR];
     auto rd = [&](unsigned ad) __attribute__((always_inline)) {
         short4_t lo, hi;
-        if (ABL == 2) {
-            asm volatile("v_mov_b32 %0, %1" : "=v"(lo[0]) : "v"(ad));
-            return __builtin_bit_cast(u32x4, __builtin_shufflevector(lo, lo, 0, 1, 2, 3, 4, 5, 6, 7));
-        }
         asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(ad));
         asm volatile("ds_read_b64_tr_b16 %0, %1 offset:512" : "=v"(hi) : "v"(ad));
         return __builtin_bit_cast(u32x4, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
     };
     auto mfma = [&](int i, u32x4 A, u32x4 B) __attribute__((always_inline)) {
-        if (ABL == 1) { asm volatile("; no mfma" : "+v"(acc[i]) : "v"(A), "v"(B)); return; }
         acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, A), __builtin_bit_cast(bf16x8, B),
                                                         acc[i], 0, 0, 0);
     };
@@ -899,25 +894,20 @@ extern "C" int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, con
         h.gs_x = (long long)d->N * d->H * d->W * d->C;
         // D = 3 super-rows of LDS-DMA in flight
         const int nblk = h.splits * h.kt * h.ct * G;
-        auto go = [&](auto pc, auto ac) {
-            constexpr int D = 3, PP = decltype(pc)::value, AB = decltype(ac)::value;
+        auto go = [&](auto pc) {
+            constexpr int D = 3, PP = decltype(pc)::value;
             constexpr size_t lds = (size_t)(D + 3) * 8192 + (size_t)(D + 1) * (8192 + 256);
             static bool attr = false;
             if (!attr) {
-                (void)hipFuncSetAttribute((const void*)k_wgrad_halo64<D, PP, AB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                (void)hipFuncSetAttribute((const void*)k_wgrad_halo64<D, PP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                           (int)lds);
                 attr = true;
             }
-            k_wgrad_halo64<D, PP, AB><<<nblk, 512, lds, st0>>>(h);
+            k_wgrad_halo64<D, PP><<<nblk, 512, lds, st0>>>(h);
         };
-        static const int abl = [] { const char* e = getenv("GM_H64_ABL"); return e ? atoi(e) : 0; }();
-        using A0 = std::integral_constant<int, 0>;
-        if (pp == 16) go(std::integral_constant<int, 16>{}, A0{});
-        else if (pp == 32) go(std::integral_constant<int, 32>{}, A0{});
-        else if (abl == 1) go(std::integral_constant<int, 64>{}, std::integral_constant<int, 1>{});
-        else if (abl == 2) go(std::integral_constant<int, 64>{}, std::integral_constant<int, 2>{});
-        else if (abl == 3) go(std::integral_constant<int, 64>{}, std::integral_constant<int, 3>{});
-        else go(std::integral_constant<int, 64>{}, A0{});
+        if (pp == 16) go(std::integral_constant<int, 16>{});
+        else if (pp == 32) go(std::integral_constant<int, 32>{});
+        else go(std::integral_constant<int, 64>{});
         int rc = check_launch("k_wgrad_halo64");
         if (rc) return rc;
         const size_t slab = (size_t)d->K * 9 * d->C;
