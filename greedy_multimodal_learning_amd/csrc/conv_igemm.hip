@@ -19,6 +19,7 @@
 // so the ds_read_b128 fragment reads are conflict-free; fp32 accumulation; weights are
 // the MFMA A operand so each lane holds 4 consecutive output channels of one pixel and
 // the epilogue writes 8-B NHWC chunks directly.  Out-of-range taps read zeros.
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -1718,167 +1719,171 @@ __global__ __launch_bounds__(256) void k_conv_rw(ConvArgs a, RwArgs r) {
 }
 
 // ---------------------------------------------------------------------------------
-// Convolutions over 8-channel (16-byte) input elements with 64 output channels and
-// no padding - the ResNet stem on its pixel-pair view (conv.py: a 7 x 4 filter over
-// pairs, strides (2, 1), K = 224).  The im2col kernel re-stages every input element
-// R*S times through LDS-DMA for a 64-wide N tile; here a persistent workgroup keeps
-// the whole weight tensor in LDS (64 x T x 16 B, row pitch padded by 16 B) and walks
-// output rows: one output row's input is R consecutive input rows (contiguous in
-// NHWC), DMA'd as one block into the second of two buffers while the current row's
-// MFMAs run.  A k-step covers two taps (16 channels); output columns past Q are MFMA
-// padding.  LDS reads as asm one k-step ahead of the MFMAs; the output row leaves
-// through an LDS tile as whole 128-B pixel rows, with a counted store wait.
+// The ResNet stem on its pixel-pair view (conv.py: a 7 x 4 filter over 8-channel pairs,
+// strides (2, 1), K = 224, 64 output channels, no padding).  A workgroup walks a
+// contiguous run of output rows of one image, TWO rows per iteration:
+//  * the weights live in VGPRs (each lane its 2 x 14 B fragments, 112 VGPRs), so the
+//    LDS feeds only the pixel operand;
+//  * input rows stream through an LDS ring of "units" of two input rows (unit u = rows
+//    2u, 2u + 1, slot u % 8), fetched once per workgroup by register-staged global loads
+//    two iterations ahead (no LDS-DMA: every LDS access is compiler-visible, so its waits
+//    are exact);
+//  * output rows p, p + 1 share input rows (row p + 1's tap row r is row p's r + 2): one
+//    pixel fragment of input row j feeds row p's MFMAs (tap row j) and row p + 1's (tap
+//    row j - 2) - 18 fragment reads for 56 MFMAs per wave, where the row-at-a-time form
+//    with weights in LDS read 84;
+//  * wave w owns output columns 32 w .. 32 w + 31 and all 64 channels; its 8 KB output
+//    tile is private (no barrier between the MFMAs and the stores), leaving as whole
+//    128-B pixel rows.
+// One barrier per iteration (the ring).  The row-at-a-time kernel this replaces spent
+// 121 us per step: per-k-step address math and an LDS round trip + barrier per row.
+constexpr int kStemRing = 8;
 struct StemArgs {
-    int T, ksteps;      // taps (R * S, even), k-steps (T / 2)
-    int rows;           // output rows N * P (one tile each)
-    int hbytes, nI;     // one input block: R * Wi * 16 B rounded up to 1 KB, its DMA instructions
-    int blk;            // bytes of one input block (R * Wi * 16)
-    int wpitch;         // LDS bytes per output channel's weights (T * 16 + 16)
-    FastDiv fd_p;       // P
-    FastDiv fd_s;       // S
-    float* stats;       // optional: per-workgroup BatchNorm partial rows of the stored output
-                        // ([G][stats_rows][64 x (sum, sum of squares)] + 128 floats per group)
-    int stats_rows;     // workgroups per group (the rows of each group's partials)
+    int N, P;      // images, output rows per image
+    int cpi, L;    // chunks (workgroups) per image, output rows per chunk (even)
+    int uchunks;   // 16-B chunks per unit (2 * Wi)
+    int upitch;    // LDS bytes per ring slot (uchunks * 16)
+    int ichunks;   // 16-B chunks per image (Hi * Wi)
+    float* stats;  // optional: per-workgroup BatchNorm partial rows of the stored output
+                   // ([G][stats_rows][64 x (sum, sum of squares)] + 128 floats per group)
+    int stats_rows;  // workgroups per group (N * cpi: the rows of each group's partials)
 };
 
-__global__ __launch_bounds__(256) void k_conv_stem(ConvArgs a, StemArgs r) {
+template <int R, int S>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_conv_stem(ConvArgs a, StemArgs r) {
+    static_assert(S % 2 == 0 && R >= 2, "k_conv_stem: even pair-tap count per row");
+    constexpr int KS = R * S / 2;  // k-steps (two taps of 8 channels each)
+    constexpr int H2 = S / 2;      // k-steps per tap row
     extern __shared__ __attribute__((aligned(16))) uint4 smem[];
-    char* lds = reinterpret_cast<char*>(smem);  // [weights 64 x wpitch][block 0][block 1]
+    char* lds = reinterpret_cast<char*>(smem);  // [ring 8 x upitch][4 wave tiles x 8 KB]
     const ConvCls& cl = a.cls[0];
-    const int Wi = a.Wi, Q = cl.Q, P = cl.P;
+    const int Wi = a.Wi, Q = cl.Q;
     const int t = threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-    const int wm = wave >> 1, wn = wave & 1;
     const int fr = lane & 31, fh = lane >> 5;
-    const int WB = 64 * r.wpitch;
-    typedef __attribute__((address_space(1))) const void* gptr_t;
-    typedef __attribute__((address_space(3))) void* lptr_t;
-    // view groups: gridDim / G workgroups per group, each walking that group's output rows
-    int g = 0, tl = blockIdx.x, nwg = gridDim.x;
-    if (a.G > 1) {
-        nwg = gridDim.x / a.G;
-        g = tl / nwg;
-        tl -= g * nwg;
+    const int per = r.stats_rows;
+    const int g = blockIdx.x / per, wg = blockIdx.x - g * per;
+    if (g >= a.G) return;
+    const int b = wg / r.cpi, c = wg - b * r.cpi;
+    const int p0 = c * r.L, p1 = min(cl.P, p0 + r.L);
+    const uint4* const img = reinterpret_cast<const uint4*>(a.in + g * a.gs_in) + (size_t)b * r.ichunks;
+    char* const tile = lds + kStemRing * r.upitch + wave * 8192;
+
+    // weights -> VGPRs: fragment (k-step ks, channel block cb) = channel 32 cb + fr, tap 2 ks + fh
+    bf16x8 wf[KS][2];
+    {
+        const uint4* wsrc = reinterpret_cast<const uint4*>(a.wt + g * a.gs_wt);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb)
+                wf[ks][cb] = __builtin_bit_cast(bf16x8, wsrc[(cb * 32 + fr) * (2 * KS) + 2 * ks + fh]);
     }
-    const int wg = tl;  // this workgroup's index within its group (its BN partial row)
-    if (tl >= r.rows || g >= a.G) return;
-    const uint16_t* const gin = a.in + g * a.gs_in;
-    // BatchNorm statistics of the stored (bf16) output, per thread over its stores: every
-    // store of thread t is channel group t & 7 (k_bn_reduce's FWD accumulation)
+    // two units (u, u + 1: 2 * uchunks 16-B chunks, contiguous in the image) per iteration:
+    // thread t holds chunks t and t + 256 (2 * uchunks <= 512); zeros past the image
+    auto fetch = [&](int u, uint4 (&v)[2]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int cc = t + 256 * h;
+            const int gi = u * r.uchunks + cc;
+            v[h] = (cc < 2 * r.uchunks && gi < r.ichunks) ? img[gi] : make_uint4(0, 0, 0, 0);
+        }
+    };
+    auto stash = [&](int u, const uint4 (&v)[2]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int cc = t + 256 * h;
+            if (cc < 2 * r.uchunks) {
+                const int hi = cc >= r.uchunks;
+                const int uu = u + hi;
+                *reinterpret_cast<uint4*>(lds + (uu & (kStemRing - 1)) * r.upitch + (cc - hi * r.uchunks) * 16) = v[h];
+            }
+        }
+    };
+    // prologue: units p0 .. p0 + 4 into the ring (iteration 0's window), units of
+    // iterations 1 and 2 into the register stages
+    {
+        uint4 v0[2], v1[2], v2[2];
+        fetch(p0, v0);
+        fetch(p0 + 2, v1);
+        fetch(p0 + 4, v2);
+        stash(p0, v0);
+        stash(p0 + 2, v1);
+        stash(p0 + 4, v2);  // (unit p0 + 5 too: part of iteration 1's window, rewritten there)
+    }
+    uint4 sa[2], sb[2];  // register stages: units for iterations i + 1 (written at i) and i + 2
+    fetch(p0 + 5, sa);
+    fetch(p0 + 7, sb);
+
     float bs1[8], bs2[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) bs1[j] = bs2[j] = 0.f;
-
-    // weights [64][T][8] -> LDS rows of wpitch bytes (register path: the padded pitch
-    // is not lane-linear)
-    const uint4* wsrc = reinterpret_cast<const uint4*>(a.wt + g * a.gs_wt);
-    for (int e = t; e < 64 * r.T; e += 256) {
-        const int n = e / r.T, tp = e - n * r.T;
-        *reinterpret_cast<uint4*>(lds + n * r.wpitch + tp * 16) = wsrc[e];
-    }
-    // the R input rows of output row `row` (= image b, output row p): one contiguous block
-    auto issue_block = [&](int row, int bb) {
-        const int b = (int)r.fd_p.div((uint32_t)row), p = row - b * P;
-        const char* src = reinterpret_cast<const char*>(gin) + ((size_t)(b * a.Hi + p * a.sAh) * Wi) * 16;
-        char* base = lds + WB + bb * r.hbytes;
-        for (int I = wave; I < r.nI; I += 4) {
-            const int off = I * 1024 + lane * 16;
-            const void* s = off < r.blk ? (const void*)(src + off) : (const void*)g_zero16;
-            __builtin_amdgcn_global_load_lds((gptr_t)s, (lptr_t)(base + I * 1024), 16, 0, 0);
-        }
-    };
-    issue_block(tl, 0);
-
-    // tile-invariant geometry: MFMA row block i of this wave -> output column q
-    int qv[2];
-    bool qok[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int q = wm * 64 + i * 32 + fr;
-        qok[i] = q < Q;
-        qv[i] = qok[i] ? q : 0;
-    }
-    const int nb = wn * 32 + fr;
-    const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
-    const unsigned bbase = lds0 + (unsigned)(nb * r.wpitch + fh * 16);  // + 32 per k-step
-
-    constexpr int kWaitAll = (7 << 4) | (15 << 8);
-    constexpr int kStores = 4;  // 16-B output stores per thread per row (Q * 8 <= 1024 chunks)
-    constexpr int kWaitStores = kStores | (7 << 4) | (15 << 8);
-    __builtin_amdgcn_s_waitcnt(kWaitAll);
-    __syncthreads();  // weights (ds_write) and the first block (DMA) are in LDS
+    const int q = wave * 32 + fr;
+    const int qc = q < Q ? q : 0;
     const size_t out_bytes = (size_t)a.N * a.Ho * a.Wo * a.Nout * 2;
     const __amdgpu_buffer_rsrc_t orsrc =
         __builtin_amdgcn_make_buffer_rsrc(cl.out + g * a.gs_out, 0, (int)(out_bytes < 0x7fffffffu ? out_bytes : 0x7fffffffu),
                                           0x00020000);
 
-    int bb = 0;
-    for (; tl < r.rows; tl += nwg) {
-        const int nx = tl + nwg;
-        if (nx < r.rows) issue_block(nx, bb ^ 1);
-        const unsigned hoff = lds0 + (unsigned)(WB + bb * r.hbytes);
+    auto iteration = [&](int p, uint4 (&cur)[2]) __attribute__((always_inline)) {
+        __syncthreads();  // units p .. p + 4 are in the ring; iteration p - 2's reads are done
+        stash(p + 5, cur);  // iteration p + 2's new units into the slots of units p - 3, p - 2
+        fetch(p + 9, cur);  // ... and the iteration after next's into the registers
 
-        floatx16 acc[2];
+        floatx16 acc[2][2];
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
-        bf16x8 af[2][2], bfr[2];
-        // k-step k: taps 2k (fh = 0) and 2k + 1 (fh = 1); tap (rr, ss) reads input row rr,
-        // column q + ss of the block
-        auto load = [&](int k, int c) {
-            const int tp = 2 * k + fh;
-            const int rr = (int)r.fd_s.div((uint32_t)tp), ss = tp - rr * a.Sw;
+            for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-            for (int i = 0; i < 2; ++i) af[c][i] = lds_rd128<0>(hoff + (unsigned)((rr * Wi + qv[i] + ss) * 16));
-            bfr[c] = lds_rd128<0>(bbase + (unsigned)(k * 32));
-        };
-        // one k-step of fragments in flight under the MFMAs: wait for everything (lgkmcnt(0)),
-        // then issue the next k-step's reads, then this k-step's MFMAs.  (Counted waits that
-        // keep two k-steps in flight produced sporadic wrong tiles with two workgroups per CU:
-        // LDS returns are not relied on to be in order.)
-        load(0, 0);
-        for (int k0 = 0; k0 < r.ksteps; k0 += 2) {
+                for (int e = 0; e < 16; ++e) acc[i][cb][e] = 0.f;
+        unsigned sl[5];  // ring slot bases of units p .. p + 4
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int k = k0 + u;
-                if (k >= r.ksteps) break;
-                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[u][0]), "+v"(af[u][1]), "+v"(bfr[u]));
-                if (k + 1 < r.ksteps) load(k + 1, u ^ 1);
-                __builtin_amdgcn_sched_barrier(0);  // the next k-step's reads go out before these MFMAs
+        for (int d = 0; d < 5; ++d) sl[d] = (unsigned)(((p + d) & (kStemRing - 1)) * r.upitch);
+        // pixel fragment (input row j, tap pair h): lane (q, fh) <- pixel pair q + 2 h + fh
 #pragma unroll
-                for (int i = 0; i < 2; ++i)
-                    acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[u], af[u][i], acc[i], 0, 0, 0);
-                __builtin_amdgcn_sched_barrier(0);
+        for (int j = 0; j < R + 2; ++j) {
+#pragma unroll
+            for (int h = 0; h < H2; ++h) {
+                const bf16x8 af = *reinterpret_cast<const bf16x8*>(lds + sl[j >> 1] +
+                                                                   (((j & 1) * Wi + qc + 2 * h + fh) << 4));
+                if (j < R) {
+#pragma unroll
+                    for (int cb = 0; cb < 2; ++cb)
+                        acc[0][cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[j * H2 + h][cb], af, acc[0][cb], 0, 0, 0);
+                }
+                if (j >= 2) {
+#pragma unroll
+                    for (int cb = 0; cb < 2; ++cb)
+                        acc[1][cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[(j - 2) * H2 + h][cb], af, acc[1][cb],
+                                                                            0, 0, 0);
+                }
             }
         }
-
-        // epilogue through LDS: the row's [Q][64] bf16 tile is assembled in LDS (16-B chunks
-        // XOR-swizzled by pixel) and written as whole 128-B pixel rows with 16-B stores -
-        // the MFMA layout would store 8 B per lane at a 128-B stride
-        char* ot = lds + WB + 2 * r.hbytes;
+        // the wave's tile: [row i][pixel fr][64 channels] bf16, 16-B chunks XOR-swizzled by pixel
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int q = wm * 64 + i * 32 + fr;
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int gq = 0; gq < 4; ++gq) {
-                const int chunk = (wn * 4 + gq) ^ (q & 7);
-                *reinterpret_cast<uint2*>(ot + q * 128 + chunk * 16 + 8 * fh) =
-                    make_uint2(pack_bf2(acc[i][4 * gq], acc[i][4 * gq + 1]),
-                               pack_bf2(acc[i][4 * gq + 2], acc[i][4 * gq + 3]));
-            }
-        }
-        __syncthreads();
-        const int b = (int)r.fd_p.div((uint32_t)tl), p = tl - b * P;
-        const unsigned rowoff = (unsigned)(((size_t)(b * a.Ho + p) * a.Wo) * a.Nout * 2);
+            for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-        for (int u = 0; u < kStores; ++u) {
-            const int e = t + 256 * u;  // 16-B chunk e of the row: pixel e / 8, chunk e % 8
-            const int q = e >> 3, j = e & 7;
-            const bool ok = q < Q;
-            const uint4 v = *reinterpret_cast<const uint4*>(ot + (ok ? q : 0) * 128 + ((j ^ (q & 7)) << 4));
+                for (int gq = 0; gq < 4; ++gq) {
+                    const int chunk = (cb * 4 + gq) ^ (fr & 7);
+                    *reinterpret_cast<uint2*>(tile + (i * 32 + fr) * 128 + chunk * 16 + 8 * fh) =
+                        make_uint2(pack_bf2(acc[i][cb][4 * gq], acc[i][cb][4 * gq + 1]),
+                                   pack_bf2(acc[i][cb][4 * gq + 2], acc[i][cb][4 * gq + 3]));
+                }
+        // 8 KB = 64 pixel rows of 128 B: store u covers pixel rows 8 u .. 8 u + 7, lane ->
+        // (pixel row 8 u + lane / 8, chunk lane % 8): the channel group is lane % 8
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int pr = 8 * u + (lane >> 3), j = lane & 7;
+            const int i = pr >> 5, px = pr & 31;
+            const int qq = wave * 32 + px;
+            const bool ok = qq < Q && p + i < p1;
+            const uint4 v = *reinterpret_cast<const uint4*>(tile + pr * 128 + ((j ^ (px & 7)) << 4));
+            const unsigned off = (unsigned)((((size_t)(b * a.Ho + p + i) * a.Wo + qq) * 64 + j * 8) * 2);
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
-                                                   orsrc, ok ? rowoff + (unsigned)e * 16u : 0xfffffff0u, 0, 0);
+                                                   orsrc, ok ? off : 0xfffffff0u, 0, 0);
             if (r.stats) {
                 const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -1890,12 +1895,15 @@ __global__ __launch_bounds__(256) void k_conv_stem(ConvArgs a, StemArgs r) {
                 }
             }
         }
-        __builtin_amdgcn_s_waitcnt(kWaitStores);  // the next block has landed; stores may fly
-        lds_barrier();                            // and the LDS tile / block bb are free again
-        bb ^= 1;
+    };
+    // iterations alternate the two register stages (stage a: units written at even iterations)
+    for (int p = p0; p < p1; p += 4) {
+        iteration(p, sa);
+        if (p + 2 < p1) iteration(p + 2, sb);
     }
     if (r.stats) {  // the workgroup's partial row: [32 thread rows][64 channels][2] combined in LDS
-        float* red = reinterpret_cast<float*>(lds + WB + 2 * r.hbytes);  // the output tile (16 KB)
+        __syncthreads();
+        float* red = reinterpret_cast<float*>(lds);  // the ring (>= 16 KB)
         const int r0 = t >> 3, cg = t & 7;
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) {
@@ -2188,13 +2196,13 @@ static int g_conv_stem = [] {
     return e ? atoi(e) : 1;
 }();
 
-// k_conv_stem serves one-class forward convolutions over 8-channel elements with 64
-// output channels, no padding, unit column stride, output columns <= 128 and an even
-// tap count; returns its LDS bytes (0 = not eligible)
+// k_conv_stem serves the pixel-pair stem: one-class forward convolutions over 8-channel
+// elements with 64 output channels, no padding, strides (2, 1), a 7 x 4 filter and output
+// columns <= 128; returns its LDS bytes (0 = not eligible)
 static size_t stem_plan(const ConvArgs& a, StemArgs& r) {
-    if (!g_conv_stem || a.ncls != 1 || a.C != 8 || a.Nout != 64 || a.sAw != 1 || a.sAh < 1) return 0;
+    if (!g_conv_stem || a.ncls != 1 || a.C != 8 || a.Nout != 64 || a.sAw != 1 || a.sAh != 2) return 0;
     const ConvCls& c = a.cls[0];
-    if (c.oS != 1 || c.oH != 0 || c.oW != 0 || c.Q > 128 || c.ntap != a.T || (a.T & 1) || a.T > 64) return 0;
+    if (c.oS != 1 || c.oH != 0 || c.oW != 0 || c.Q > 128 || c.ntap != a.T || a.Sw != 4 || a.T != 28) return 0;
     for (int tp = 0; tp < c.ntap; ++tp) {  // forward taps without padding: (r, s) = (dh, dw), weight tap tp
         const int rr = tp / a.Sw, ss = tp - rr * a.Sw;
         if (c.tw[tp] != tp || c.dh[tp] != rr || c.dw[tp] != ss) return 0;
@@ -2202,36 +2210,38 @@ static size_t stem_plan(const ConvArgs& a, StemArgs& r) {
     const int R = a.T / a.Sw;
     if ((c.P - 1) * a.sAh + R > a.Hi || c.Q - 1 + a.Sw > a.Wi) return 0;
     if ((size_t)a.N * a.Ho * a.Wo * a.Nout * 2 >= 0x7ffff000u) return 0;
-    r.T = a.T;
-    r.ksteps = a.T / 2;
-    r.rows = a.N * c.P;
-    r.blk = R * a.Wi * 16;
-    r.nI = (r.blk + 1023) / 1024;
-    r.hbytes = r.nI * 1024;
-    r.wpitch = a.T * 16 + 16;
-    r.fd_p = FastDiv((uint32_t)c.P);
-    r.fd_s = FastDiv((uint32_t)a.Sw);
-    const size_t lds = (size_t)64 * r.wpitch + 2 * (size_t)r.hbytes + 128 * 128;  // + the output tile
+    if ((long long)a.Hi * a.Wi >= (1ll << 27)) return 0;
+    r.N = a.N;
+    r.P = c.P;
+    r.uchunks = 2 * a.Wi;
+    if (r.uchunks > 256) return 0;  // two units per iteration over 256 threads x 2 chunks
+    r.upitch = r.uchunks * 16;
+    r.ichunks = a.Hi * a.Wi;
+    // chunks of an even number of rows: about two workgroups per CU over all view groups
+    const int target = a.G > 0 ? 512 / a.G : 512;
+    const int cpi0 = std::max(1, std::min((c.P + 1) / 2, target / std::max(1, a.N)));
+    r.L = (c.P + cpi0 - 1) / cpi0;
+    r.L += r.L & 1;
+    r.cpi = (c.P + r.L - 1) / r.L;  // no empty chunk
+    r.stats_rows = a.N * r.cpi;
+    r.stats = nullptr;
+    const size_t lds = (size_t)kStemRing * r.upitch + 4 * 8192;
     return lds <= 80 * 1024 ? lds : 0;  // two workgroups per CU
 }
-
-static int stem_wgs(int rows, int G) { return rows < 512 / G ? rows : (512 / G > 0 ? 512 / G : 1); }
 
 static int launch_stem(const ConvArgs& a, const StemArgs& r, size_t lds, hipStream_t st) {
     static size_t granted = 0;
     if (lds > granted) {
         const hipError_t e =
-            hipFuncSetAttribute((const void*)k_conv_stem, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            hipFuncSetAttribute((const void*)k_conv_stem<7, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) {
             set_error("k_conv_stem: %zu B of LDS refused (%s)", lds, hipGetErrorString(e));
             return GM_E_UNSUP;
         }
         granted = lds;
     }
-    // persistent: two workgroups per CU, split evenly over the view groups
-    const int per = stem_wgs(r.rows, a.G);
-    const int grid = per * a.G;
-    k_conv_stem<<<grid, 256, lds, st>>>(a, r);
+    // N * cpi workgroups per view group (about two per CU in all)
+    k_conv_stem<7, 4><<<r.stats_rows * a.G, 256, lds, st>>>(a, r);
     return check_launch("k_conv_stem");
 }
 
@@ -2480,9 +2490,7 @@ static int pick_and_launch(ConvArgs& a, hipStream_t st, void* ws, size_t ws_byte
     {
         StemArgs r;
         const size_t lds = stem_plan(a, r);
-        r.stats = nullptr;
-        r.stats_rows = 0;
-        if (lds > 0) return launch_stem(a, r, lds, st);
+        if (lds > 0) return launch_stem(a, r, lds, st);  // (no statistics: r.stats null)
     }
     TilePick p = pick_tile(a);
     if (p.splits > 1 && (!ws || ws_bytes < splitk_bytes(p) || p.tiles > kMaxSplitTiles)) {  // the unsplit choice
@@ -2819,7 +2827,7 @@ extern "C" int gm_conv_stem_stats_rows(const gm_conv_desc_hw* d, int G) {
     a.G = G;
     StemArgs r;
     if (stem_plan(a, r) == 0 || a.Nout != 64) return 0;
-    return stem_wgs(r.rows, G);
+    return r.stats_rows;
 }
 
 extern "C" int gm_conv2d_fwd_grouped_stats_bf16(const gm_conv_desc_hw* d, int G, const void* x, const void* w,
@@ -2841,10 +2849,9 @@ extern "C" int gm_conv2d_fwd_grouped_stats_bf16(const gm_conv_desc_hw* d, int G,
     StemArgs r;
     const size_t lds = stem_plan(a, r);
     GM_REQUIRE(lds > 0 && a.Nout == 64, "conv fwd stats: only the stem kernel's shapes (64 output channels)");
-    GM_REQUIRE(stats_rows == stem_wgs(r.rows, G), "conv fwd stats: stats_rows %d != gm_conv_stem_stats_rows %d",
-               stats_rows, stem_wgs(r.rows, G));
+    GM_REQUIRE(stats_rows == r.stats_rows, "conv fwd stats: stats_rows %d != gm_conv_stem_stats_rows %d",
+               stats_rows, r.stats_rows);
     r.stats = stats;
-    r.stats_rows = stats_rows;
     return launch_stem(a, r, lds, as_stream(stream));
 }
 

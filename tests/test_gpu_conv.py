@@ -266,12 +266,14 @@ def test_conv_dgrad_fused_addend(dev, shape):
     assert torch.equal(dxi, dxa)
 
 
-@pytest.mark.parametrize("shape", [(64, 3, 224, 224), (3, 3, 37, 30), (2, 3, 64, 64), (5, 3, 250, 200)],
+@pytest.mark.parametrize("shape", [(64, 3, 224, 224), (3, 3, 37, 30), (2, 3, 64, 64), (5, 3, 250, 200),
+                                   (300, 3, 40, 36), (1, 3, 224, 224)],
                          ids=lambda s: "x".join(map(str, s)))
 def test_stem_resident_weight_kernel(dev, shape):
     """The pixel-pair stem (7x7/s2, 3 -> 64 channels) on the resident-weight kernel
-    (weights in LDS, one output row per step, double-buffered input rows) equals the
-    im2col kernel and the fp32 convolution."""
+    (weights in LDS, a workgroup per run of output rows, input rows streamed through an LDS
+    ring) equals the im2col kernel and the fp32 convolution: one chunk per image (N = 300),
+    one row per chunk (N = 1), ragged last chunks (P = 125, 19)."""
     from greedy_multimodal_learning_amd import _lib as L
     from greedy_multimodal_learning_amd import conv as G
     lib = L.load()

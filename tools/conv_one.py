@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--pipe", type=int, default=0)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--sets", type=int, default=1, help="grouped stem/wgrad: distinct operand sets cycled")
     a = ap.parse_args()
     from greedy_multimodal_learning_amd import _lib as L
     from greedy_multimodal_learning_amd import conv as G
@@ -38,6 +39,10 @@ def main():
     wt = w.permute(1, 0, 2, 3).contiguous(memory_format=CL)
     L.check(L.load().gm_conv_set_pipe(a.pipe), "set_pipe")
     fn = (lambda: G.conv_fwd(x, w, st, pad)) if a.op == "fwd" else (lambda: G.conv_dgrad_t(dy, wt, H, W, st, pad))
+    if a.shape == "conv1" and a.op == "fwd":  # the pixel-pair stem, grouped as in the step
+        fns = [T._make_bf16("fwd", B, dev, C, H, W, K, R, st, pad, P, Q, a.groups) for _ in range(a.sets)]
+        fn = fns[0] if a.sets == 1 else T._cycle(fns)
+        B = B * a.groups
     if a.op == "wgrad":  # the step's grouped launch (both views), as tools/trunk_table.py builds it
         if a.ring is not None:
             L.check(L.load().gm_conv_set_wgrad_loop(a.ring), "ring")
