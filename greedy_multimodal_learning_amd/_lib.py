@@ -354,4 +354,5 @@ EXPORTS.update({
     "gm_conv_set_1x1_gemm": (c_int, [c_int]),
     "gm_conv_set_rw": (c_int, [c_int]),
     "gm_conv_set_stem": (c_int, [c_int]),
+    "gm_conv_set_wgrad_stem": (c_int, [c_int]),
 })

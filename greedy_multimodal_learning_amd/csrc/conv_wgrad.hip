@@ -13,6 +13,7 @@
 // waves of 32x32, v_mfma_f32_32x32x16_bf16), double-buffered register-staged
 // loads, split-K over pixels into fp32 partial slabs, then a fixed-order reduce
 // (deterministic, no atomics).
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -651,6 +652,131 @@ __global__ __launch_bounds__(512) void k_wgrad_halo64(WHaloArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------------
+// Weight gradient of the pixel-pair stem (7 x 4 filter over 8-channel pairs, strides
+// (2, 1), 64 output channels, no padding): dw[n][r][s][c] = sum over output pixels
+// (b, p, q) of dy[b][p][q][n] x[b][2p + r][q + s][c].  A workgroup walks a contiguous
+// run of output rows of one image with ONE WAVE PER TAP ROW r (7 waves): per output row
+// the dy row (Q x 64 channels, 128-B pixel rows, XOR-swizzled 16-B chunks) and the input
+// rows 2p .. 2p + 6 (a ring of two-row units, as k_conv_stem) sit in LDS; wave r reduces
+// over the row's pixels in 16-pixel k-steps: A = dy^T (two 32-channel blocks), B = the
+// input row 2p + r read as the [q][(s, c)] matrix whose rows overlap (row q = pairs
+// q .. q + 3, 64 B at a 16-B pitch) - both by ds_read_b64_tr_b16, so one B fragment
+// feeds two MFMAs and the whole tap row (s, c) = 32 columns is one accumulator column
+// block.  Operands are register-staged two rows ahead (compiler-visible LDS accesses,
+// exact waits); each workgroup writes its fp32 [64][224] partial, k_wgrad_sum reduces
+// them in a fixed order.  The generic kernel (k_conv_wgrad4 <1, 2>) re-staged every
+// input pixel per tap through an im2col tile: 117 us alone, 142 us in the step.
+struct WStemArgs {
+    const uint16_t* dy;  // [G][N][P][Q][64]
+    const uint16_t* x;   // [G][N][Hi][Wi][8] (pixel pairs)
+    float* part;         // [G][splits][64][R * S * 8]
+    int P, Q, Wi;
+    int cpi, L, splits;  // chunks per image, output rows per chunk, workgroups per group (N * cpi)
+    int uchunks, upitch, ichunks;  // 16-B chunks per unit (two input rows), LDS slot bytes, chunks per image
+    long long gs_dy, gs_x;
+};
+
+template <int R, int S>
+__global__ __launch_bounds__(64 * R) void k_wgrad_stem(WStemArgs a) {
+    constexpr int NT = 64 * R;                // threads: one wave per tap row
+    constexpr int TC = R * S * 8;             // dw columns per output channel
+    constexpr int DPT = (1024 + NT - 1) / NT;  // dy chunks per thread per row (Q <= 128)
+    constexpr int RING = 8;
+    static_assert(S * 8 == 32, "k_wgrad_stem: one tap row = one 32-column accumulator block");
+    extern __shared__ __attribute__((aligned(16))) uint4 wsm[];
+    char* lds = reinterpret_cast<char*>(wsm);  // [dy tiles 2 x Q*128][ring 8 x upitch]
+    const int t = threadIdx.x, lane = t & 63;
+    const int rr = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int grp = blockIdx.x / a.splits, wg = blockIdx.x - grp * a.splits;
+    const int b = wg / a.cpi, c = wg - b * a.cpi;
+    const int p0 = c * a.L, p1 = min(a.P, p0 + a.L);
+    const int tileb = a.Q * 128, dchunks = a.Q * 8;
+    char* const ring = lds + 2 * tileb;
+    const uint4* const gdy = reinterpret_cast<const uint4*>(a.dy + grp * a.gs_dy) + (size_t)b * a.P * dchunks;
+    const uint4* const gx = reinterpret_cast<const uint4*>(a.x + grp * a.gs_x) + (size_t)b * a.ichunks;
+    struct Stage {
+        uint4 d[DPT];
+        uint4 x;
+    };
+    // dy row pr and input unit u (rows 2u, 2u + 1) -> registers; zeros past the image
+    auto fetch = [&](int pr, int u, Stage& st, bool with_dy = true) __attribute__((always_inline)) {
+#pragma unroll
+        for (int h = 0; h < DPT && with_dy; ++h) {
+            const int cc = t + NT * h;
+            st.d[h] = (cc < dchunks && pr < a.P) ? gdy[(size_t)pr * dchunks + cc] : make_uint4(0, 0, 0, 0);
+        }
+        const int gi = u * a.uchunks + t;
+        st.x = (t < a.uchunks && gi < a.ichunks) ? gx[gi] : make_uint4(0, 0, 0, 0);
+    };
+    auto stash = [&](int pr, int u, const Stage& st, bool with_dy = true) __attribute__((always_inline)) {
+        char* tile = lds + (pr & 1) * tileb;
+#pragma unroll
+        for (int h = 0; h < DPT && with_dy; ++h) {
+            const int cc = t + NT * h;
+            if (cc < dchunks) {
+                const int px = cc >> 3, j = cc & 7;
+                *reinterpret_cast<uint4*>(tile + px * 128 + ((j ^ wswz<128>(px)) << 4)) = st.d[h];
+            }
+        }
+        if (t < a.uchunks) *reinterpret_cast<uint4*>(ring + (u & (RING - 1)) * a.upitch + t * 16) = st.x;
+    };
+    {  // prologue: dy row p0 and units p0 .. p0 + 3 (row p0's window)
+        Stage s0, s1;
+        fetch(p0, p0, s0, true);
+        fetch(0, p0 + 1, s1, false);
+        stash(p0, p0, s0, true);
+        stash(0, p0 + 1, s1, false);
+        fetch(0, p0 + 2, s0, false);
+        fetch(0, p0 + 3, s1, false);
+        stash(0, p0 + 2, s0, false);
+        stash(0, p0 + 3, s1, false);
+    }
+    Stage sa, sb;  // iteration p stashes dy row p + 1 and unit p + 4, then fetches row p + 3, unit p + 6
+    fetch(p0 + 1, p0 + 4, sa);
+    fetch(p0 + 2, p0 + 5, sb);
+
+    floatx16 acc[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+    // tr-read lane geometry: 16-lane group g reads pixel rows 8 (g >> 1) + q4 (+ 4) of a
+    // 16-pixel slice, columns 16 (g & 1) + 4 p4 .. + 3; lane l receives column l % 32
+    const int g4 = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+    const int krow = 8 * (g4 >> 1) + q4, col = 16 * (g4 & 1) + 4 * p4;
+    auto rowoff = [](int row, int ch) { return row * 128 + ((((ch >> 3) ^ wswz<128>(row))) << 4) + (ch & 7) * 2; };
+    const int nks = a.Q >> 4;
+    auto iteration = [&](int p, Stage& st) __attribute__((always_inline)) {
+        __syncthreads();  // row p's dy tile and units p .. p + 3 are in LDS; row p - 1's reads are done
+        stash(p + 1, p + 4, st);
+        fetch(p + 3, p + 6, st);
+        const char* tile = lds + (p & 1) * tileb;
+        const char* xrow = ring + ((p + (rr >> 1)) & (RING - 1)) * a.upitch + (rr & 1) * a.Wi * 16;
+        for (int ks = 0; ks < nks; ++ks) {
+            const int px = 16 * ks + krow;
+            const bf16x8 A0 = tr_frag(reinterpret_cast<const uint16_t*>(tile + rowoff(px, col)),
+                                      reinterpret_cast<const uint16_t*>(tile + rowoff(px + 4, col)));
+            const bf16x8 A1 = tr_frag(reinterpret_cast<const uint16_t*>(tile + rowoff(px, 32 + col)),
+                                      reinterpret_cast<const uint16_t*>(tile + rowoff(px + 4, 32 + col)));
+            const char* xb = xrow + (px + (col >> 3)) * 16 + (col & 7) * 2;
+            const bf16x8 B = tr_frag(reinterpret_cast<const uint16_t*>(xb), reinterpret_cast<const uint16_t*>(xb + 64));
+            acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B, acc[0], 0, 0, 0);
+            acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, B, acc[1], 0, 0, 0);
+        }
+    };
+    for (int p = p0; p < p1; p += 2) {
+        iteration(p, sa);
+        if (p + 1 < p1) iteration(p + 1, sb);
+    }
+    // the partial: dw[channel][rr * 32 + (s, c)], lane -> column, registers -> channels
+    float* out = a.part + ((size_t)grp * a.splits + wg) * (64 * TC) + rr * 32 + (lane & 31);
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) out[(size_t)(nb * 32 + 8 * (e >> 2) + 4 * (lane >> 5) + (e & 3)) * TC] = acc[nb][e];
+}
+
 // dw[i] (+)= sum over splits of part[s][i] in ONE launch, for the uncropped case (Cp == Cr,
 // every layer but the RGB stem).  A block covers 256/R float4 columns with R split lanes
 // per column: lane r sums splits r, r+R, ... (four loads in flight), the R lane sums are
@@ -828,12 +954,44 @@ static int halo64_splits(const gm_conv_desc_hw* d, int G) {
     return sp < srows ? sp : srows;
 }
 
+// k_wgrad_stem serves the pixel-pair stem: 8-channel pairs, 64 output channels, a 7 x 4
+// filter, strides (2, 1), no padding, output rows of a multiple of 16 and <= 128 pixels
+static int g_wgrad_stem = [] {
+    const char* e = getenv("GM_WGRAD_STEM");  // 0: the stem's weight gradient takes k_conv_wgrad4
+    return e ? atoi(e) : 1;
+}();
+struct StemWPlan {
+    int P, Q, cpi, L, splits;
+};
+static bool stemw_plan(const gm_conv_desc_hw* d, int G, StemWPlan& w) {
+    if (!g_wgrad_stem || d->C != 8 || d->K != 64 || d->R != 7 || d->S != 4 || d->stride_h != 2 || d->stride_w != 1 ||
+        d->pad_h != 0 || d->pad_w != 0 || d->N < 1 || d->H < 7 || d->W < 4)
+        return false;
+    w.P = (d->H - 7) / 2 + 1;
+    w.Q = d->W - 3;
+    if (w.Q % 16 != 0 || w.Q > 128 || 2 * d->W > 448 || (long long)d->H * d->W >= (1ll << 27)) return false;
+    if ((long long)d->N * w.P * w.Q * 64 >= (1ll << 31)) return false;
+    const int target = 512 / G > 0 ? 512 / G : 1;
+    const int cpi0 = std::max(1, std::min(w.P, target / d->N));
+    w.L = (w.P + cpi0 - 1) / cpi0;
+    w.cpi = (w.P + w.L - 1) / w.L;
+    w.splits = d->N * w.cpi;
+    return true;
+}
+
 extern "C" size_t gm_conv2d_wgrad_grouped_scratch(const gm_conv_desc_hw* d, int G) {
     if (!d || d->stride_h < 1 || d->stride_w < 1 || G < 1) return 0;
+    StemWPlan sw;
+    if (stemw_plan(d, G, sw)) return (size_t)G * sw.splits * 64 * 224 * 4;
     if (halo64_ok(d)) return (size_t)G * halo64_splits(d, G) * d->K * 9 * d->C * 4;
     const WPlan w = plan(d, G);
     const size_t slab = (size_t)d->K * d->R * d->S * d->C;
     return (size_t)G * w.splits * slab * sizeof(float);
+}
+
+extern "C" int gm_conv_set_wgrad_stem(int on) {
+    g_wgrad_stem = on ? 1 : 0;
+    return GM_OK;
 }
 
 extern "C" size_t gm_conv2d_wgrad_hw_scratch(const gm_conv_desc_hw* d) {
@@ -878,6 +1036,49 @@ extern "C" int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, con
     const size_t need = gm_conv2d_wgrad_grouped_scratch(d, G);
     GM_REQUIRE(scratch && scratch_bytes >= need, "conv wgrad: scratch %zu < %zu", scratch_bytes, need);
     hipStream_t st0 = as_stream(stream);
+    auto split_sum = [&](float* part, int splits, size_t slab) {
+        const size_t ncol = slab / 4;
+        int R = 1;
+        while (R < 32 && R * 2 <= splits && (ncol * R + 255) / 256 < 512) R *= 2;
+        const dim3 gg((unsigned)((ncol + 256 / R - 1) / (256 / R)), (unsigned)G);
+        switch (R) {
+            case 1: k_wgrad_sum<1><<<gg, 256, 0, st0>>>(part, splits, slab, accumulate, dw, dw_stride); break;
+            case 2: k_wgrad_sum<2><<<gg, 256, 0, st0>>>(part, splits, slab, accumulate, dw, dw_stride); break;
+            case 4: k_wgrad_sum<4><<<gg, 256, 0, st0>>>(part, splits, slab, accumulate, dw, dw_stride); break;
+            case 8: k_wgrad_sum<8><<<gg, 256, 0, st0>>>(part, splits, slab, accumulate, dw, dw_stride); break;
+            case 16: k_wgrad_sum<16><<<gg, 256, 0, st0>>>(part, splits, slab, accumulate, dw, dw_stride); break;
+            default: k_wgrad_sum<32><<<gg, 256, 0, st0>>>(part, splits, slab, accumulate, dw, dw_stride); break;
+        }
+        return check_launch("k_wgrad_sum");
+    };
+    StemWPlan sw;
+    if (stemw_plan(d, G, sw) && c_real == d->C) {
+        WStemArgs s;
+        s.dy = (const uint16_t*)dy;
+        s.x = (const uint16_t*)x;
+        s.part = (float*)scratch;
+        s.P = sw.P; s.Q = sw.Q; s.Wi = d->W;
+        s.cpi = sw.cpi; s.L = sw.L; s.splits = sw.splits;
+        s.uchunks = 2 * d->W;
+        s.upitch = s.uchunks * 16;
+        s.ichunks = d->H * d->W;
+        s.gs_dy = (long long)d->N * sw.P * sw.Q * 64;
+        s.gs_x = (long long)d->N * d->H * d->W * 8;
+        const size_t lds = (size_t)2 * sw.Q * 128 + (size_t)8 * s.upitch;
+        static size_t granted = 0;
+        if (lds > granted) {
+            if (hipFuncSetAttribute((const void*)k_wgrad_stem<7, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+                hipSuccess) {
+                set_error("k_wgrad_stem: %zu B of LDS refused", lds);
+                return GM_E_UNSUP;
+            }
+            granted = lds;
+        }
+        k_wgrad_stem<7, 4><<<sw.splits * G, 448, lds, st0>>>(s);
+        const int rc = check_launch("k_wgrad_stem");
+        if (rc) return rc;
+        return split_sum(s.part, sw.splits, (size_t)64 * 224);
+    }
     if (halo64_ok(d) && c_real == d->C) {
         WHaloArgs h;
         h.dy = (const uint16_t*)dy;

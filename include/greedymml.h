@@ -385,10 +385,15 @@ int gm_conv_set_wgrad_staging(int wr);
  * layer 1, forward and input gradient; default on, GM_CONV_RW=0 at load or
  * gm_conv_set_rw(0) selects the im2col kernel for them). */
 int gm_conv_set_rw(int on);
-/* Resident-weight kernel for the pixel-pair stem (8-channel elements -> 64 channels, no
- * padding; default on, GM_CONV_STEM=0 at load or gm_conv_set_stem(0) selects the
- * im2col kernel). */
+/* Dedicated kernel for the pixel-pair stem's forward (8-channel elements -> 64 channels,
+ * 7 x 4 filter, strides (2, 1), no padding: weights in VGPRs, two output rows per
+ * iteration; default on, GM_CONV_STEM=0 at load or gm_conv_set_stem(0) selects the im2col
+ * kernel). */
 int gm_conv_set_stem(int on);
+/* Dedicated kernel for the pixel-pair stem's weight gradient (k_wgrad_stem: one wave per
+ * tap row, fp32 partials per workgroup + the split sum; default on, GM_WGRAD_STEM=0 at load
+ * or gm_conv_set_wgrad_stem(0) selects k_conv_wgrad4). */
+int gm_conv_set_wgrad_stem(int on);
 int gm_conv2d_fwd_ex_bf16(const gm_conv_desc* d, const void* x, const void* w, void* y, void* ws,
                           size_t ws_bytes, void* stream);
 int gm_conv2d_dgrad_ex_bf16(const gm_conv_desc* d, const void* dy, const void* wt, void* dx, void* ws,

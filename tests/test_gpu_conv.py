@@ -266,6 +266,54 @@ def test_conv_dgrad_fused_addend(dev, shape):
     assert torch.equal(dxi, dxa)
 
 
+@pytest.mark.parametrize("shape", [(64, 2, 224, 224), (8, 1, 224, 224), (3, 2, 64, 64), (2, 1, 96, 72),
+                                   (300, 1, 40, 38)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_stem_wgrad_kernel(dev, shape):
+    """The pixel-pair stem's weight gradient on k_wgrad_stem (one wave per tap row,
+    per-workgroup fp32 partials + the fixed-order split sum), G view groups in one launch,
+    equals k_conv_wgrad4 (same bf16 operands, fp32 sums in another order) and the fp32
+    weight gradient of the pair-view convolution; bit-identical on a second run."""
+    import ctypes
+    from greedy_multimodal_learning_amd import _lib as L
+    from greedy_multimodal_learning_amd import conv as CV
+    lib = L.load()
+    B, G, H, W = shape
+    K, R = 64, 7
+    P, Q, Sp, Hp, Wp = CV._stem_geom(H, W, R, R, 3)
+    g = torch.Generator(device="cuda").manual_seed(sum(shape))
+    xp = torch.empty(G * B, Hp, Wp // 2, 8, device=dev, dtype=torch.bfloat16)
+    for v in range(G):
+        x = torch.randn(B, 3, H, W, device=dev, generator=g)
+        CV.stem_pack(x, torch.randn(K, 3, R, R, device=dev, generator=g), 3, xp=xp[v * B:(v + 1) * B],
+                     wp=torch.empty(K, R, Sp, 8, device=dev, dtype=torch.bfloat16))
+    dy = torch.randn(G * B, P, Q, K, device=dev, generator=g).bfloat16()
+    d = CV._desc_hw(B, Hp, Wp // 2, 8, K, R, Sp, 2, 1, 0, 0)
+    n = K * R * Sp * 8
+
+    def run(on):
+        L.check(lib.gm_conv_set_wgrad_stem(on), "gm_conv_set_wgrad_stem")
+        need = lib.gm_conv2d_wgrad_grouped_scratch(ctypes.byref(d), G)
+        scr = torch.empty(max(need, 16), device=dev, dtype=torch.uint8)
+        dw = torch.full((G, K, R, Sp, 8), float("nan"), device=dev)
+        L.check(lib.gm_conv2d_wgrad_grouped_bf16(ctypes.byref(d), G, dy.data_ptr(), xp.data_ptr(), dw.data_ptr(), n, 8,
+                                                 0, scr.data_ptr(), need, L.stream_of(dev)), "wgrad")
+        torch.cuda.synchronize()
+        return dw
+    try:
+        d_new, d_new2, d_old = run(1), run(1), run(0)
+    finally:
+        lib.gm_conv_set_wgrad_stem(1)
+    assert torch.isfinite(d_new).all()
+    assert torch.equal(d_new, d_new2)
+    _close(d_new, d_old, 1e-5)
+    for v in range(G):  # fp32 reference on the pair view: [B, 8, Hp, Wp/2] x [64, 8, 7, 4], strides (2, 1)
+        xv = xp[v * B:(v + 1) * B].permute(0, 3, 1, 2).float()
+        dyv = dy[v * B:(v + 1) * B].permute(0, 3, 1, 2).float()
+        ref = torch.nn.grad.conv2d_weight(xv, (K, 8, R, Sp), dyv, stride=(2, 1))
+        _close(d_new[v].permute(0, 3, 1, 2), ref, 1e-5)
+
+
 @pytest.mark.parametrize("shape", [(64, 3, 224, 224), (3, 3, 37, 30), (2, 3, 64, 64), (5, 3, 250, 200),
                                    (300, 3, 40, 36), (1, 3, 224, 224)],
                          ids=lambda s: "x".join(map(str, s)))
