@@ -22,6 +22,7 @@ import os
 import torch
 import torch.nn as nn
 
+from .streams import scratch_key
 from . import _lib as L
 from .gradsink import sink_done, sink_target
 
@@ -47,7 +48,7 @@ def _get_scratch(device, M, C):
     two BN launches in flight must not share tickets."""
     need = L.load().gm_bn_scratch(M, C)
     idx = device.index if device.index is not None else torch.cuda.current_device()
-    key = (idx, torch.cuda.current_stream(idx).stream_id)
+    key = scratch_key(idx)
     buf = _scratch.get(key)
     if buf is None or buf.numel() < need:
         size = max(need, 1 << 20) if buf is None else max(need, 2 * buf.numel())

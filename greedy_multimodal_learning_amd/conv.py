@@ -21,6 +21,7 @@ import os
 import torch
 import torch.nn as nn
 
+from .streams import scratch_key
 from . import _lib as L
 from .gradsink import sink_done, sink_target
 
@@ -71,7 +72,7 @@ def _splitk(device, d, dgrad):
     if need == 0:
         return 0, 0
     idx = device.index if device.index is not None else torch.cuda.current_device()
-    key = (idx, torch.cuda.current_stream(idx).stream_id)
+    key = scratch_key(idx)
     buf = _splitk_ws.get(key)
     if buf is None or buf.numel() < need:
         buf = torch.zeros((need + (1 << 20) - 1) >> 20 << 20, device=device, dtype=torch.uint8)

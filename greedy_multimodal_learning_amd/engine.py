@@ -37,7 +37,7 @@ import torch.distributed as dist
 from .callbacks import GroupNorms
 from .gradsink import GradSink
 from .losses import blend_loss
-from .streams import all_side_streams, side_stream
+from .streams import alias_capture_stream, all_side_streams, side_stream
 from .streams import enabled as streams_enabled
 from .vtrunk import drop_pending_wgrads
 
@@ -522,8 +522,11 @@ class BalancedStep:
         # thread_local: the process group's watchdog thread keeps querying its events
         # while this thread captures (global mode would invalidate the capture)
         mode = "thread_local" if dp else "global"
+        eager_sid = torch.cuda.current_stream(self.device).stream_id
         try:
             with torch.cuda.graph(g, pool=self._gpool, capture_error_mode=mode):
+                alias_capture_stream(self.device.index if self.device.index is not None
+                                     else torch.cuda.current_device(), eager_sid)
                 loss, outs = self._fwd_bwd(*(inputs or self._static))
                 loss = loss.detach()
                 sums = None if (dp and not inline) else self.norms.sums(grad_scale=1.0 / self.world, lr=self.lr)

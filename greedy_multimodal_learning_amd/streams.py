@@ -37,6 +37,24 @@ def side_stream(device, i):
     return s
 
 
+# capture stream id -> the stream the step ran on before the capture (engine._capture): the
+# per-stream scratch caches (BN tickets, split-K turnstiles: zeroed once) then serve the
+# captured step from the buffers the eager warm-up steps created, instead of allocating
+# and zero-filling new ones inside the graph (a fill replayed every step)
+_capture_alias = {}
+
+
+def scratch_key(idx):
+    """(device, stream) key of the per-stream scratch caches, capture streams aliased."""
+    sid = torch.cuda.current_stream(idx).stream_id
+    return (idx, _capture_alias.get((idx, sid), sid))
+
+
+def alias_capture_stream(idx, eager_sid):
+    """Inside a capture: the current (capture) stream shares eager_sid's scratch buffers."""
+    _capture_alias[(idx, torch.cuda.current_stream(idx).stream_id)] = eager_sid
+
+
 def all_side_streams(device):
     idx = device.index if device.index is not None else torch.cuda.current_device()
     return [s for (d, _), s in sorted(_side.items(), key=lambda kv: kv[0]) if d == idx]

@@ -29,6 +29,7 @@ import os
 
 import torch
 
+from .streams import scratch_key
 from . import _lib as L
 from .bn import MASK_FROM_X
 from .conv import CL, _cpad, _desc, _desc_hw, _like_param, _prepped, _splitk_ws, _stem_geom, stem_pack
@@ -74,7 +75,7 @@ def _splitk_g(device, d, G, dgrad):
     if need == 0:
         return 0, 0
     idx = device.index if device.index is not None else torch.cuda.current_device()
-    key = (idx, torch.cuda.current_stream(idx).stream_id)
+    key = scratch_key(idx)
     buf = _splitk_ws.get(key)
     if buf is None or buf.numel() < need:
         buf = torch.zeros((need + (1 << 20) - 1) >> 20 << 20, device=device, dtype=torch.uint8)
@@ -90,7 +91,7 @@ def _bn_scratch_g(device, M, C, G):
     sit in fixed per-group headers: never shared with the ungrouped calls' buffers)."""
     need = L.load().gm_bn_scratch_grouped(M, C, G)
     idx = device.index if device.index is not None else torch.cuda.current_device()
-    key = (idx, torch.cuda.current_stream(idx).stream_id)
+    key = scratch_key(idx)
     buf = _bn_scratch.get(key)
     if buf is None or buf.numel() < need:
         size = max(need, 1 << 20) if buf is None else max(need, 2 * buf.numel())
