@@ -187,7 +187,8 @@ class StemPack(ctypes.Structure):
     _fields_ = [("x", c_void_p), ("dtype", c_int), ("N", c_int), ("C0", c_int), ("H", c_int), ("W", c_int),
                 ("pad", c_int), ("sn", ctypes.c_longlong), ("sc", ctypes.c_longlong), ("sh", ctypes.c_longlong),
                 ("sw", ctypes.c_longlong), ("Hp", c_int), ("Wp", c_int), ("xp", c_void_p), ("w", c_void_p),
-                ("K", c_int), ("R", c_int), ("S", c_int), ("wp", c_void_p)]
+                ("K", c_int), ("R", c_int), ("S", c_int), ("wp", c_void_p), ("wk", ctypes.c_longlong),
+                ("wc", ctypes.c_longlong), ("wr", ctypes.c_longlong), ("ws", ctypes.c_longlong)]
 
 
 EXPORTS.update({

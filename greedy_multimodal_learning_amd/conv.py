@@ -206,8 +206,8 @@ def stem_pack(x, weight, pad, xp=None, wp=None):
     if x.dtype not in (torch.float32, torch.bfloat16):
         x = x.float()
     w = weight.detach()
-    if w.dtype != torch.float32 or not w.is_contiguous():
-        w = w.float().contiguous()
+    if w.dtype != torch.float32:
+        w = w.float()
     if xp is None:
         xp = torch.empty(N, Hp, Wp // 2, 8, device=x.device, dtype=torch.bfloat16)
     if wp is None:
@@ -216,7 +216,7 @@ def stem_pack(x, weight, pad, xp=None, wp=None):
             or not wp.is_contiguous()):
         raise ValueError("stem_pack: output buffers must be dense [N,Hp,Wp/2,8] / [K,R,Sp,8]")
     p = L.StemPack(x.data_ptr(), L.GM_BF16 if x.dtype == torch.bfloat16 else L.GM_F32, N, C0, H, W, pad,
-                   *x.stride(), Hp, Wp, xp.data_ptr(), w.data_ptr(), K, R, S, wp.data_ptr())
+                   *x.stride(), Hp, Wp, xp.data_ptr(), w.data_ptr(), K, R, S, wp.data_ptr(), *w.stride())
     L.check(L.load().gm_stem_pack_bf16(ctypes.byref(p), L.stream_of(x.device)), "gm_stem_pack_bf16")
     return xp.permute(0, 3, 1, 2), wp.permute(0, 3, 1, 2)
 

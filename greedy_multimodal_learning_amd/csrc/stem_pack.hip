@@ -3,7 +3,8 @@
 //                   (zero outside the image and for c >= C0), bf16, from an fp32 or bf16
 //                   NCHW-strided x (e.g. x[:, view] of the [B, V, 3, H, W] batch), and
 //   the weight view wp[k][r][sq][8]  = {w[k, c, r, 2sq+j] : j in 0..1, c in 0..3}
-//                   (zero for s >= S or c >= C0), bf16 from the fp32 [K, C0, R, S] weight.
+//                   (zero for s >= S or c >= C0), bf16 from the fp32 [K, C0, R, S] weight at
+//                   any strides (the model's channels_last parameter, no contiguous copy).
 // Each thread writes one 16-B element (2 pixels x 4 channels); reads are coalesced per
 // channel plane.  Replaces the zero-fill + strided cast/copy PyTorch launches of the
 // input and of the weight (4 launches per view).
@@ -64,7 +65,8 @@ __global__ __launch_bounds__(kPT) void k_stem_pack(gm_stem_pack a, long long nx,
             const int s = 2 * sq + j;
             if (s < a.S)
                 for (int c = 0; c < a.C0; ++c)
-                    v[4 * j + c] = bf16_of(a.w[(((long long)k * a.C0 + c) * a.R + r) * a.S + s]);
+                    v[4 * j + c] = bf16_of(a.w[(long long)k * a.wk + (long long)c * a.wc + (long long)r * a.wr +
+                                               (long long)s * a.ws]);
         }
         uint4 o;
         o.x = v[0] | ((unsigned)v[1] << 16); o.y = v[2] | ((unsigned)v[3] << 16);
@@ -87,6 +89,14 @@ extern "C" int gm_stem_pack_bf16(const gm_stem_pack* p, void* stream) {
                p->W, p->pad);
     GM_REQUIRE(p->dtype == GM_F32 || p->dtype == GM_BF16, "gm_stem_pack_bf16: x must be fp32 or bf16");
     GM_REQUIRE(!p->w || (p->wp && p->K > 0 && p->R > 0 && p->S > 0), "gm_stem_pack_bf16: bad weight");
+    gm_stem_pack q = *p;
+    if (q.w && !q.wk && !q.wc && !q.wr && !q.ws) {  // contiguous [K, C0, R, S]
+        q.ws = 1;
+        q.wr = q.S;
+        q.wc = (long long)q.R * q.S;
+        q.wk = (long long)q.C0 * q.R * q.S;
+    }
+    p = &q;
     const long long nx = (long long)p->N * p->Hp * (p->Wp / 2);
     const int nw = p->w ? p->K * p->R * ((p->S + 1) / 2) : 0;
     const long long tot = nx + nw;

@@ -289,9 +289,10 @@ typedef struct gm_stem_pack {
     long long sn, sc, sh, sw;  /* element strides of x */
     int Hp, Wp;
     void* xp;
-    const float* w;            /* optional fp32 [K, C0, R, S] contiguous */
+    const float* w;            /* optional fp32 [K, C0, R, S] */
     int K, R, S;
     void* wp;
+    long long wk, wc, wr, ws;  /* element strides of w (all 0: contiguous [K, C0, R, S]) */
 } gm_stem_pack;
 
 int gm_stem_pack_bf16(const gm_stem_pack* p, void* stream);

@@ -200,6 +200,9 @@ def test_stem_pack_kernel_matches_torch_pack(dev, shape, dtype):
     xp, wp = G.stem_pack(x, w, pad)
     assert torch.equal(xp, G.stem_pack_input(x, R, S, pad))
     assert torch.equal(wp, G.stem_pack_weight(w))
+    # the model's channels_last weight parameter, read at its strides (no contiguous copy)
+    _, wp_cl = G.stem_pack(x, w.contiguous(memory_format=torch.channels_last), pad)
+    assert torch.equal(wp_cl, wp)
 
 
 def test_conv_splitk_spin_timeout_never_silent(dev):
