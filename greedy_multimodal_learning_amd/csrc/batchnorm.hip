@@ -597,6 +597,11 @@ __global__ __launch_bounds__(kT) void k_stem_pool_bn_bwd(ReduceArgs a0, StemPool
         float gv[4][8];
 #pragma unroll
         for (int u = 0; u < 4; ++u) unpack8(it.gq[u], gv[u]);
+        // a missing window's argmax bytes become 0xff (never a position 0..8): one select per
+        // window here instead of a mask AND per channel compare below
+        uint2 ivm[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) ivm[u] = ((it.okw >> u) & 1u) ? it.iv[u] : make_uint2(~0u, ~0u);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int dh = q >> 1, dw = q & 1;
@@ -609,13 +614,13 @@ __global__ __launch_bounds__(kT) void k_stem_pool_bn_bwd(ReduceArgs a0, StemPool
             for (int u = 0; u < 4; ++u) {
                 const int wr = u >> 1, wc = u & 1;
                 if (wr > dh || wc > dw) continue;
-                const bool okw = (it.okw >> u) & 1u;
                 // position of pixel (h, w) in window (k + wr, l + wc): rows 2(k+wr)-1 .., cols 2(l+wc)-1 ..
-                const uint32_t pos = (uint32_t)((h - (2 * (k + wr) - 1)) * 3 + (w - (2 * (l + wc) - 1)));
+                // (h - 2k = dh, w - 2l = dw: a compile-time constant per (q, u))
+                const uint32_t pos = (uint32_t)((dh - 2 * wr + 1) * 3 + (dw - 2 * wc + 1));
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    const uint32_t b = ((j < 4 ? it.iv[u].x : it.iv[u].y) >> (8 * (j & 3))) & 0xffu;
-                    if (okw && b == pos) d[j] += gv[u][j];
+                    const uint32_t b = ((j < 4 ? ivm[u].x : ivm[u].y) >> (8 * (j & 3))) & 0xffu;
+                    if (b == pos) d[j] += gv[u][j];
                 }
             }
             float xf[8];
