@@ -565,31 +565,37 @@ __global__ __launch_bounds__(kT) void k_stem_pool_bn_bwd(ReduceArgs a0, StemPool
         unsigned okw;  // bit u: window u exists (a select on the loaded value instead would
                        // make hipcc branch around the load and drain vmcnt per window)
     };
-    auto load = [&](long long i, Item& it) {
-        it.cg = (int)(i % C8);
-        const long long ob = i / C8;
-        it.l = (int)(ob % pg.Q);
-        const long long r1 = ob / pg.Q;
-        it.k = (int)(r1 % pg.P);
-        it.n = (int)(r1 / pg.P);
-        const int n = it.n, k = it.k, l = it.l, cg = it.cg;
+    // 32-bit index math (a group's pooled and input vectors are < 2^31: checked on the host)
+    const unsigned QC8 = (unsigned)pg.Q * C8, WC8 = (unsigned)pg.W * C8;
+    auto load = [&](long long i64, Item& it) {
+        const unsigned i = (unsigned)i64;
+        const unsigned ob = i / (unsigned)C8;
+        it.cg = (int)(i - ob * (unsigned)C8);
+        const unsigned r1 = ob / (unsigned)pg.Q;
+        it.l = (int)(ob - r1 * (unsigned)pg.Q);
+        const unsigned nn = r1 / (unsigned)pg.P;
+        it.k = (int)(r1 - nn * (unsigned)pg.P);
+        it.n = (int)nn;
+        const int k = it.k, l = it.l;
         // windows (k + wr, l + wc); pixel (dh, dw) of the block is covered by window
         // (k + wr, l + wc) iff wr <= dh and wc <= dw (and the window exists)
+        const unsigned o0 = i;  // the block's own window (k, l) = pooled vector i
         it.okw = 0u;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int wr = u >> 1, wc = u & 1;
             const bool ok = k + wr < pg.P && l + wc < pg.Q;
-            const long long o = (((long long)n * pg.P + (ok ? k + wr : k)) * pg.Q + (ok ? l + wc : l)) * C8 + cg;
+            const unsigned o = ok ? o0 + (unsigned)wr * QC8 + (unsigned)wc * (unsigned)C8 : o0;
             it.iv[u] = IDX[o];
             it.gq[u] = GP[o];
             it.okw |= ok ? (1u << u) : 0u;
         }
+        const unsigned x0 = ((nn * (unsigned)pg.H + 2u * (unsigned)k) * (unsigned)pg.W + 2u * (unsigned)l) * C8 + it.cg;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const int h = 2 * k + (q >> 1), w = 2 * l + (q & 1);
-            const bool in = h < pg.H && w < pg.W;
-            it.xv[q] = ld_nt16(&X[(((long long)n * pg.H + (in ? h : 2 * k)) * pg.W + (in ? w : 2 * l)) * C8 + cg]);
+            const int dh = q >> 1, dw = q & 1;
+            const bool in = 2 * k + dh < pg.H && 2 * l + dw < pg.W;
+            it.xv[q] = ld_nt16(&X[in ? x0 + (unsigned)dh * WC8 + (unsigned)dw * (unsigned)C8 : x0]);
         }
     };
     auto compute = [&](const Item& it) {
@@ -1867,6 +1873,7 @@ extern "C" int gm_bn_relu_maxpool2d_bwd_grouped_bf16(const gm_pool_desc* d, int 
     StemPoolGeo pg;
     pg.Ng = d->N; pg.H = d->H; pg.W = d->W; pg.P = P; pg.Q = Q;
     pg.items = (long long)d->N * P * Q * (d->C / 8);
+    GM_REQUIRE((long long)d->N * d->H * d->W * (d->C / 8) < (1ll << 31), "%s: a group's map exceeds 2^31 vectors", fn);
     // pass-1 partial rows: at most the plan's (the grouped scratch holds pl.nrc rows per group)
     int nrc = pl.nrc < kMaxRC ? pl.nrc : kMaxRC;
     pg.ipb = (pg.items + nrc - 1) / nrc;
