@@ -70,12 +70,17 @@ __global__ __launch_bounds__(256) void k_maxpool_fwd(PoolArgs a, const void* __r
         if (a.k == 3) {
             // 3 x 3 windows (the ResNet stem): the nine loads in flight at once, out-of-image
             // positions clamped to (hs, ws) and skipped in the row-major scan below
+            // 32-bit vector indices (the map has < 2^31 16-B vectors: checked on the host):
+            // the clamped corner (hs, ws) and the window origin, then constant offsets per tap
             float v[9][8];
+            const int xc = ((n * a.H + hs) * a.W + ws) * a.C8 + cg;
+            const int x00 = xc + ((h0 - hs) * a.W + (w0 - ws)) * a.C8;
+            const int WC8 = a.W * a.C8;
 #pragma unroll
             for (int u = 0; u < 9; ++u) {
                 const int h = h0 + u / 3, w = w0 + u % 3;
                 const bool in = h >= 0 && h < a.H && w >= 0 && w < a.W;
-                V8<E>::ld(x, (((long long)n * a.H + (in ? h : hs)) * a.W + (in ? w : ws)) * a.C8 + cg, v[u]);
+                V8<E>::ld(x, in ? x00 + (u / 3) * WC8 + (u % 3) * a.C8 : xc, v[u]);
             }
 #pragma unroll
             for (int u = 0; u < 9; ++u) {
