@@ -352,6 +352,7 @@ EXPORTS.update({
     "gm_conv_set_wgrad_staging": (c_int, [c_int]),
     "gm_conv_set_splitk": (c_int, [c_int]),
     "gm_conv_set_wgrad_loop": (c_int, [c_int]),
+    "gm_conv_set_wgrad_ring": (c_int, [c_int]),
     "gm_conv_set_1x1_gemm": (c_int, [c_int]),
     "gm_conv_set_rw": (c_int, [c_int]),
     "gm_conv_set_stem": (c_int, [c_int]),

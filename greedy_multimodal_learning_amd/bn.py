@@ -22,7 +22,7 @@ import os
 import torch
 import torch.nn as nn
 
-from .streams import scratch_key
+from .streams import zeroed_scratch
 from . import _lib as L
 from .gradsink import sink_done, sink_target
 
@@ -47,14 +47,8 @@ def _get_scratch(device, M, C):
     per stream: the trunks run on separate streams concurrently (streams.py), and
     two BN launches in flight must not share tickets."""
     need = L.load().gm_bn_scratch(M, C)
-    idx = device.index if device.index is not None else torch.cuda.current_device()
-    key = scratch_key(idx)
-    buf = _scratch.get(key)
-    if buf is None or buf.numel() < need:
-        size = max(need, 1 << 20) if buf is None else max(need, 2 * buf.numel())
-        buf = torch.zeros(size, device=device, dtype=torch.uint8)
-        _scratch[key] = buf
-    return buf
+    return zeroed_scratch(_scratch, device, need,
+                          lambda old: max(need, 1 << 20) if old is None else max(need, 2 * old.numel()))
 
 
 def _nhwc(t):

@@ -59,8 +59,7 @@ def build(force=False, verbose=False):
         if p.returncode != 0:
             raise RuntimeError("hipcc failed:\n" + " ".join(cmd) + "\n" + out.decode(errors="replace"))
     tmp = LIB + ".tmp"
-    # hipBLASLt: the 1x1 convolutions are plain GEMMs (conv1x1_lt.hip)
-    cmd = [cc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs + ["-L/opt/rocm/lib", "-lhipblaslt"]
+    cmd = [cc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
     if r.returncode != 0:
         raise RuntimeError("link failed:\n" + r.stdout.decode(errors="replace"))

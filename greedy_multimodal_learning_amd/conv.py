@@ -21,7 +21,7 @@ import os
 import torch
 import torch.nn as nn
 
-from .streams import scratch_key
+from .streams import zeroed_scratch
 from . import _lib as L
 from .gradsink import sink_done, sink_target
 
@@ -71,12 +71,7 @@ def _splitk(device, d, dgrad):
     need = L.load().gm_conv2d_splitk_ws_bytes(ctypes.byref(d), int(dgrad))
     if need == 0:
         return 0, 0
-    idx = device.index if device.index is not None else torch.cuda.current_device()
-    key = scratch_key(idx)
-    buf = _splitk_ws.get(key)
-    if buf is None or buf.numel() < need:
-        buf = torch.zeros((need + (1 << 20) - 1) >> 20 << 20, device=device, dtype=torch.uint8)
-        _splitk_ws[key] = buf
+    buf = zeroed_scratch(_splitk_ws, device, need, lambda old: (need + (1 << 20) - 1) >> 20 << 20)
     return buf.data_ptr(), buf.numel()
 
 

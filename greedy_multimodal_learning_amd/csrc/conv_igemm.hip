@@ -2741,6 +2741,13 @@ extern "C" int gm_conv_set_rw(int on) {
     return GM_OK;
 }
 
+// the 1x1 / s1 GEMM path (gm_conv_set_1x1_gemm): 0 = the im2col kernel for 1x1 shapes
+static int g_conv_1x1 = 0;
+extern "C" int gm_conv_set_1x1_gemm(int on) {
+    g_conv_1x1 = on ? 1 : 0;
+    return GM_OK;
+}
+
 extern "C" int gm_conv_set_pipe(int pipe) {
     GM_REQUIRE(pipe == 0 || pipe == 2 || pipe == 3 || (pipe >= 5 && pipe <= 8),
                "gm_conv_set_pipe: 0, 2, 3 (5..8: timing diagnostics)");
@@ -2748,25 +2755,12 @@ extern "C" int gm_conv_set_pipe(int pipe) {
     return GM_OK;
 }
 
-// 1x1 / s1 / p0 convolutions as plain GEMMs on hipBLASLt (conv1x1_lt.hip)
-namespace gm {
-bool conv1x1_lt_ok(int R, int S, int sh, int sw, int ph, int pw, long long M);
-int conv1x1_lt_fwd(long long M, int C, int K, int G, const void* x, long long gs_x, const void* w, long long gs_w,
-                   void* y, long long gs_y, hipStream_t st);
-int conv1x1_lt_dgrad(long long M, int C, int K, int G, const void* dy, long long gs_dy, const void* wt, long long gs_wt,
-                     void* dx, long long gs_dx, const void* addend, hipStream_t st);
-}  // namespace gm
 
 extern "C" int gm_conv2d_fwd_hw_bf16(const gm_conv_desc_hw* d, const void* x, const void* w, void* y,
                                      void* stream) {
     int rc = check_desc_hw(d);
     if (rc) return rc;
     GM_REQUIRE(x && w && y, "conv fwd: null pointer");
-    const long long M = (long long)d->N * d->H * d->W;
-    if (gm::conv1x1_lt_ok(d->R, d->S, d->stride_h, d->stride_w, d->pad_h, d->pad_w, M)) {
-        const int lr = gm::conv1x1_lt_fwd(M, d->C, d->K, 1, x, 0, w, 0, y, 0, as_stream(stream));
-        if (lr != GM_E_UNSUP) return lr;  // no workspace-free GEMM: the im2col kernel
-    }
     ConvArgs a;
     fwd_setup(d, x, w, y, a);
     return pick_and_launch(a, as_stream(stream), nullptr, 0);
@@ -2778,11 +2772,6 @@ extern "C" int gm_conv2d_fwd_ex_bf16(const gm_conv_desc* d, const void* x, const
     if (rc) return rc;
     GM_REQUIRE(x && w && y, "conv fwd: null pointer");
     const gm_conv_desc_hw h = to_hw(d);
-    const long long M = (long long)d->N * d->H * d->W;
-    if (gm::conv1x1_lt_ok(d->R, d->S, d->stride, d->stride, d->pad, d->pad, M)) {
-        const int lr = gm::conv1x1_lt_fwd(M, d->C, d->K, 1, x, 0, w, 0, y, 0, as_stream(stream));
-        if (lr != GM_E_UNSUP) return lr;  // no workspace-free GEMM: the im2col kernel
-    }
     ConvArgs a;
     fwd_setup(&h, x, w, y, a);
     return pick_and_launch(a, as_stream(stream), ws, ws_bytes);
@@ -2803,11 +2792,6 @@ extern "C" int gm_conv2d_fwd_grouped_bf16(const gm_conv_desc_hw* d, int G, const
     GM_REQUIRE(G == 1 || w_stride >= (long long)d->K * d->R * d->S * d->C ||
                    -w_stride >= (long long)d->K * d->R * d->S * d->C,
                "conv fwd: group weight stride %lld shorter than one weight", w_stride);
-    const long long M = (long long)d->N * d->H * d->W;
-    if (gm::conv1x1_lt_ok(d->R, d->S, d->stride_h, d->stride_w, d->pad_h, d->pad_w, M) && (G == 1 || w_stride > 0)) {
-        const int lr = gm::conv1x1_lt_fwd(M, d->C, d->K, G, x, M * d->C, w, w_stride, y, M * d->K, as_stream(stream));
-        if (lr != GM_E_UNSUP) return lr;  // no workspace-free GEMM: the im2col kernel
-    }
     ConvArgs a;
     fwd_setup(d, x, w, y, a);
     a.G = G;
@@ -2867,12 +2851,6 @@ extern "C" int gm_conv2d_dgrad_grouped_bf16(const gm_conv_desc* d, int G, const 
                "conv dgrad: group weight stride %lld shorter than one weight", wt_stride);
     const int P = (d->H + 2 * d->pad - d->R) / d->stride + 1;
     const int Q = (d->W + 2 * d->pad - d->S) / d->stride + 1;
-    const long long M = (long long)d->N * d->H * d->W;
-    if (gm::conv1x1_lt_ok(d->R, d->S, d->stride, d->stride, d->pad, d->pad, M) && (G == 1 || wt_stride > 0)) {
-        const int lr = gm::conv1x1_lt_dgrad(M, d->C, d->K, G, dy, M * d->K, wt, wt_stride, dx, M * d->C, addend,
-                                    as_stream(stream));
-        if (lr != GM_E_UNSUP) return lr;  // no workspace-free GEMM: the im2col kernel
-    }
     ConvArgs a;
     const bool full = dgrad_setup(d, dy, wt, dx, a);
     a.G = G;
@@ -2899,11 +2877,6 @@ extern "C" int gm_conv2d_dgrad_add_bf16(const gm_conv_desc* d, const void* dy, c
     // addend == dx (in place) is allowed: every epilogue loads an output element's addend
     // and stores that element from the same thread, and pixels no parity class covers
     // then simply keep the addend (no zero / copy pass)
-    const long long M = (long long)d->N * d->H * d->W;
-    if (gm::conv1x1_lt_ok(d->R, d->S, d->stride, d->stride, d->pad, d->pad, M)) {
-        const int lr = gm::conv1x1_lt_dgrad(M, d->C, d->K, 1, dy, 0, wt, 0, dx, 0, addend, as_stream(stream));
-        if (lr != GM_E_UNSUP) return lr;  // no workspace-free GEMM: the im2col kernel
-    }
     ConvArgs a;
     const bool full = dgrad_setup(d, dy, wt, dx, a);
     a.addend = (const uint16_t*)addend;

@@ -18,6 +18,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
+#include <utility>
 
 #include "gm_common.h"
 
@@ -652,6 +653,301 @@ __global__ __launch_bounds__(512) void k_wgrad_halo64(WHaloArgs a) {
     }
 }
 
+// k_wgrad_ring: weight gradient of a 3 x 3 convolution (any stride / padding) with K % 128 == 0
+// and C % 32 == 0 - the layer-2..4 shapes k_conv_wgrad4 served at 0.15-0.23 of the MFMA peak.
+// What bound k_conv_wgrad4: one 64-pixel step of LDS-DMA in flight per workgroup (issue ->
+// landed is ~1 us under load, MI355X_MICROARCH.md ldsdma rows) against 16 MFMAs per wave
+// (~0.25 us), so its two workgroups per CU took in ~35 GB/s; and every DMA issue sat in the
+// compute waves' MFMA stream.  Here, per CU ONE workgroup of 512 threads:
+//   * four LOADER waves own all LDS-DMA: an S-slot ring of 64-pixel steps, S - 1 steps in flight
+//     (104 KB at S = 3), one raw s_barrier per step after a counted vmcnt (the step about to be
+//     read has landed; the younger one stays in flight across the barrier);
+//   * four COMPUTE waves never touch VMEM in the loop: wave w owns output channels 32w .. 32w+31
+//     of the tile and all 9 column fragments (9 accumulators), ds_read_b64_tr_b16 fragments one
+//     k-slice ahead, 36 MFMAs per step between barriers (k_conv_wgrad4: 16);
+//   * tile 128 output channels x 288 (tap, channel) columns = 9 x 32 - every 3x3 shape with C % 32
+//     == 0 splits into whole tiles, and the trunk's layer-2..4 shapes give tiles x splits = 256
+//     workgroups exactly (one per CU, no tail); 88.6 FLOP per staged byte (128 x 128: 64).
+// LDS slot: B (x gathered per tap) as 9 blocks of [64 px][32 columns] (64-B rows: the tr reads of a
+// half-wave cover 4 rows x 64 B = all 64 banks, no swizzle), then A (dy) as 2 blocks of
+// [64 px][64 k] (128-B rows, chunk XOR 4 ((row >> 1) & 1): k_conv_wgrad4's image).  Splits over the
+// pixel steps write fp32 partial slabs that k_wgrad_sum reduces in a fixed order (deterministic);
+// one split writes (or accumulates into) the gradient directly.
+struct WRingArgs {
+    const uint16_t* dy;  // [G][M][K]  (M = N*P*Q)
+    const uint16_t* x;   // [G][N][H][W][C]
+    float* part;         // [G][splits][K][9C], or dw (one split)
+    int N, H, W, C, logC, K, P, Q, sth, stw, padh, padw, M;
+    int tiles_k, tiles_n, splits, sps;  // sps: 64-pixel steps per split
+    FastDiv fd_pq, fd_q;
+    int adv_b, adv_p, adv_q;            // one step of 64 pixels in (b, p, q)
+    long long gs_dy, gs_x, gs_part;     // group strides (elements)
+    int accumulate;
+};
+
+// slot of BK pixels: B = 9 blocks of BK x 64 B, then A = 2 blocks of BK x 128 B
+template <int BK> struct RingGeo {
+    static constexpr int BB = BK * 64, AB = BK * 128;  // bytes per B / A block
+    static constexpr int B = 9 * BB, A = 2 * AB, SLOT = B + A;
+    static constexpr int SLICES = BK / 16;             // 16-pixel k-slices per step
+};
+
+// one 32 x 16 fragment by two transposed reads at base + LO / + HI
+template <int LO, int HI>
+__device__ __forceinline__ bf16x8 ring_frag(unsigned base) {
+    const short4_t lo = tr_rd<LO>(base), hi = tr_rd<HI>(base);
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+// slice KS of the 9 B blocks (immediate offsets on one base register)
+template <int BK, int KS, int... J>
+__device__ __forceinline__ void ring_load_b(bf16x8 (&fb)[9], unsigned ba, std::integer_sequence<int, J...>) {
+    ((fb[J] = ring_frag<J * RingGeo<BK>::BB + KS * 1024, J * RingGeo<BK>::BB + KS * 1024 + 256>(ba)), ...);
+}
+template <int BK, int KS>
+__device__ __forceinline__ void ring_load(bf16x8& fa, bf16x8 (&fb)[9], unsigned aa, unsigned ba) {
+    fa = ring_frag<KS * 2048, KS * 2048 + 512>(aa);
+    ring_load_b<BK, KS>(fb, ba, std::make_integer_sequence<int, 9>{});
+}
+
+template <int S, int BK>
+__global__ __launch_bounds__(512) void k_wgrad_ring(WRingArgs a) {
+    static_assert(S >= 2 && (BK == 32 || BK == 64), "k_wgrad_ring: S >= 2 slots of 32 or 64 pixels");
+    using Geo = RingGeo<BK>;
+    constexpr int D = S - 1;  // steps in flight
+    extern __shared__ __attribute__((aligned(16))) uint4 wsm[];
+    char* lds = reinterpret_cast<char*>(wsm);
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    int bid = blockIdx.x;
+    {   // XCD-major: the tiles of one pixel range (split) share an XCD and its L2 copy of the rows
+        const int n = gridDim.x, q = n >> 3, r = n & 7, x = bid & 7;
+        bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+    }
+    const int tiles = a.tiles_k * a.tiles_n;
+    const int grp = bid / (tiles * a.splits);
+    bid -= grp * tiles * a.splits;
+    const int split = bid / tiles, tile = bid - split * tiles;
+    const int tk = tile % a.tiles_k, tn = tile / a.tiles_k;
+    const int k0 = tk * 128, n0 = tn * 288;
+    const int step0 = split * a.sps;
+    const int nst = max(0, min((a.M + BK - 1) / BK, step0 + a.sps) - step0);
+    const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
+
+    if (wave >= 4) {
+        // ---- loader waves ----
+        // BK = 64: every loader wave stages B rows 16 lw .. + 15 of the 9 blocks and A rows
+        //          16 lw .. + 15 of both blocks (9 + 4 pieces per step);
+        // BK = 32: waves 0, 1 stage B rows 16 lw .. + 15 (9 pieces), waves 2, 3 A rows
+        //          16 (lw - 2) .. + 15 of both blocks (4 pieces)
+        const int lw = wave - 4;
+        constexpr bool SPLITROLE = BK == 32;
+        const bool do_b = !SPLITROLE || lw < 2, do_a = !SPLITROLE || lw >= 2;
+        const int rb = SPLITROLE ? (lw & 1) : lw;  // 16-row band of this wave's pieces
+        typedef __attribute__((address_space(1))) const void* gptr_t;
+        typedef __attribute__((address_space(3))) void* lptr_t;
+        const void* zero = (const void*)g_wzero16;
+        const uint16_t* __restrict__ gdy = a.dy + grp * a.gs_dy;
+        const uint16_t* __restrict__ gx = a.x + grp * a.gs_x;
+        const int brow = 16 * rb + (lane >> 2), bc = (lane & 3) * 8;
+        int bdh[9], bdw[9], boff[9];
+#pragma unroll
+        for (int j = 0; j < 9; ++j) {
+            const int n = n0 + 32 * j + bc;
+            const int tap = n >> a.logC, c = n & (a.C - 1);
+            const int r = tap / 3, s = tap - 3 * r;
+            bdh[j] = r - a.padh;
+            bdw[j] = s - a.padw;
+            boff[j] = ((bdh[j] * a.W + bdw[j]) << a.logC) + c;
+        }
+        // A sources advance by BK pixel rows per step (no per-step 64-bit multiply)
+        int arow[2];
+        const uint16_t* ap[2][2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            arow[h] = 16 * rb + 8 * h + (lane >> 3);
+#pragma unroll
+            for (int ab = 0; ab < 2; ++ab)
+                ap[h][ab] = gdy + (size_t)(step0 * BK + arow[h]) * a.K + k0 + 64 * ab +
+                            (((lane & 7) ^ wswz<128>(arow[h])) << 3);
+        }
+        const size_t astep = (size_t)BK * a.K;
+        const int PQ = a.P * a.Q;
+        int m = step0 * BK + brow;
+        int b = (int)a.fd_pq.div((uint32_t)m);
+        int p = (int)a.fd_q.div((uint32_t)(m - b * PQ));
+        int q = m - b * PQ - p * a.Q;
+        auto dma = [&](const void* src, unsigned off) __attribute__((always_inline)) {
+            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + off), 16, 0, 0);
+        };
+        int slot = 0;
+        auto issue = [&](int i) __attribute__((always_inline)) {  // step step0 + i into the next slot
+            const unsigned sb = (unsigned)slot * Geo::SLOT;
+            const int ms = (step0 + i) * BK;
+            if (do_b) {
+                const int hi0 = p * a.sth, wi0 = q * a.stw;
+                const bool rok = ms + brow < a.M;
+                const long pix = ((long)(b * a.H + hi0) * a.W + wi0) << a.logC;
+#pragma unroll
+                for (int j = 0; j < 9; ++j) {
+                    const int hi = hi0 + bdh[j], wi = wi0 + bdw[j];
+                    const bool ok = rok & ((unsigned)hi < (unsigned)a.H) & ((unsigned)wi < (unsigned)a.W);
+                    dma(ok ? (const void*)(gx + pix + boff[j]) : zero, sb + j * Geo::BB + rb * 1024);
+                }
+                // next step's pixel: + BK = (adv_b, adv_p, adv_q), one carry per component at most
+                int nq = q + a.adv_q, np = p + a.adv_p, nb = b + a.adv_b;
+                if (nq >= a.Q) { nq -= a.Q; ++np; }
+                if (np >= a.P) { np -= a.P; ++nb; }
+                b = nb; p = np; q = nq;
+            }
+            if (do_a) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const bool ok = ms + arow[h] < a.M;
+#pragma unroll
+                    for (int ab = 0; ab < 2; ++ab) {
+                        dma(ok ? (const void*)ap[h][ab] : zero, sb + Geo::B + ab * Geo::AB + (2 * rb + h) * 1024);
+                        ap[h][ab] += astep;
+                    }
+                }
+            }
+            slot = slot + 1 == S ? 0 : slot + 1;
+        };
+        // pieces per step of this wave: the counted wait leaves the D - 1 younger steps in flight
+        auto wait_all_but = [&](bool younger) __attribute__((always_inline)) {
+            if (!younger) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            else if (!SPLITROLE) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(13 * (D - 1)) : "memory");
+            else if (do_b) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(9 * (D - 1)) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (D - 1)) : "memory");
+        };
+        for (int i = 0; i < D && i < nst; ++i) issue(i);
+        for (int i = 0; i < nst; ++i) {
+            // step i has landed (the younger steps may stay in flight; at the tail, where fewer
+            // than D - 1 younger ones exist, everything); after the barrier no compute wave reads
+            // step i - 1's slot any more: step i + D refills it.  No DMA past the range, so none
+            // is in flight once the last barrier has passed (the epilogue reuses the ring).
+            wait_all_but(i + D - 1 < nst);
+            __builtin_amdgcn_s_barrier();
+            if (i + D < nst) issue(i + D);
+        }
+        return;
+    }
+
+    // ---- compute waves ----
+    const int w = wave;
+    floatx16 acc[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+    // tr-read geometry (k_conv_wgrad4's): half-wave g >> 1 reads rows 8 (g >> 1) + q4 (+4) of a
+    // 16-row k-slice, 4-column block p4 of the 32-column fragment, 16-column half g & 1
+    const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+    const int rbase = 8 * (g >> 1) + q4;
+    const int ac = 32 * (w & 1) + 16 * (g & 1) + 4 * p4;
+    const unsigned a_lane =
+        Geo::B + (w >> 1) * Geo::AB + rbase * 128 + ((((ac >> 3) ^ wswz<128>(rbase))) << 4) + (ac & 7) * 2;
+    const unsigned b_lane = rbase * 64 + (16 * (g & 1) + 4 * p4) * 2;
+    bf16x8 fa[2], fb[2][9];
+    auto load = [&](int ks, int c, unsigned sb) __attribute__((always_inline)) {
+        switch (ks) {
+            case 0: ring_load<BK, 0>(fa[c], fb[c], sb + a_lane, sb + b_lane); break;
+            case 1: ring_load<BK, 1>(fa[c], fb[c], sb + a_lane, sb + b_lane); break;
+            case 2: ring_load<BK, 2 % Geo::SLICES>(fa[c], fb[c], sb + a_lane, sb + b_lane); break;
+            default: ring_load<BK, 3 % Geo::SLICES>(fa[c], fb[c], sb + a_lane, sb + b_lane); break;
+        }
+    };
+    // lgkmcnt(0), then every fragment of buffer c re-defined after it (asm reads are invisible
+    // to the compiler's own waits; the MFMAs must not be hoisted above the wait)
+    auto wait_frags = [&](int c) __attribute__((always_inline)) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        asm volatile("" : "+v"(fa[c]));
+#pragma unroll
+        for (int j = 0; j < 9; ++j) asm volatile("" : "+v"(fb[c][j]));
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    int slot = 0;
+    if (nst > 0) {
+        __builtin_amdgcn_s_barrier();  // step 0 landed
+        unsigned sb = lds0;
+        load(0, 0, sb);
+        for (int i = 0; i < nst; ++i) {
+#pragma unroll
+            for (int ks = 0; ks < Geo::SLICES; ++ks) {
+                const int c = ks & 1;
+                wait_frags(c);
+                if (ks + 1 < Geo::SLICES) {
+                    load(ks + 1, c ^ 1, sb);
+                } else if (i + 1 < nst) {
+                    // every read of this step is done: the barrier lets the loaders refill the
+                    // previous step's slot and tells us step i + 1 has landed - read its first
+                    // slice under this slice's MFMAs
+                    __builtin_amdgcn_s_barrier();
+                    slot = slot + 1 == S ? 0 : slot + 1;
+                    sb = lds0 + (unsigned)slot * Geo::SLOT;
+                    load(0, c ^ 1, sb);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int j = 0; j < 9; ++j)
+                    acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[c], fb[c][j], acc[j], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+    }
+    // Epilogue through LDS: per half (accumulator rows 16 h .. 16 h + 15) the wave stages its
+    // [16][288] fp32 block in a slot no wave reads any more (every slot but the last step's:
+    // all their reads finished before the last barrier, and no DMA is in flight) and leaves
+    // with 16-B stores - 18 dwordx4 instead of 72 dword stores per half.
+    // D[k][col]: col = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5)
+    constexpr int HB = 16 * 288 * 4;  // 18 KB per wave and half
+    static_assert(Geo::SLOT >= HB && (S - 1) * Geo::SLOT >= 4 * HB, "k_wgrad_ring: epilogue staging space");
+    unsigned stg;
+    if constexpr (Geo::SLOT >= 2 * HB) {  // two waves per free slot
+        const int s1 = slot + 1 + (w >> 1);
+        stg = (unsigned)((s1 % S) * Geo::SLOT + (w & 1) * HB);
+    } else {
+        const int s1 = slot + 1 + w;
+        stg = (unsigned)((s1 % S) * Geo::SLOT);
+    }
+    float* stgp = reinterpret_cast<float*>(lds + stg);
+    const int TC = 9 * a.C;
+    float* out = a.part + grp * a.gs_part + (size_t)split * a.K * TC + (size_t)(k0 + 32 * w) * TC + n0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int j = 0; j < 9; ++j)
+#pragma unroll
+            for (int e = 8 * h; e < 8 * h + 8; ++e)
+                stgp[((e & 3) + 8 * ((e >> 2) & 1) + 4 * (lane >> 5)) * 288 + 32 * j + (lane & 31)] = acc[j][e];
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's own staging writes done
+        __builtin_amdgcn_sched_barrier(0);
+        float4 v[18];
+#pragma unroll
+        for (int i = 0; i < 18; ++i) {
+            const int L = i * 64 + lane, row = L / 72, c4 = L - row * 72;
+            v[i] = reinterpret_cast<const float4*>(stgp)[row * 72 + c4];
+        }
+        float* oh = out + (size_t)(16 * h) * TC;
+        if (a.accumulate) {
+#pragma unroll
+            for (int i = 0; i < 18; ++i) {
+                const int L = i * 64 + lane, row = L / 72, c4 = L - row * 72;
+                float4* o = reinterpret_cast<float4*>(oh + (size_t)row * TC) + c4;
+                const float4 u = *o;
+                *o = make_float4(u.x + v[i].x, u.y + v[i].y, u.z + v[i].z, u.w + v[i].w);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 18; ++i) {
+                const int L = i * 64 + lane, row = L / 72, c4 = L - row * 72;
+                reinterpret_cast<float4*>(oh + (size_t)row * TC)[c4] = v[i];
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // the reads of this half done before the next half's writes
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 // ---------------------------------------------------------------------------------
 // Weight gradient of the pixel-pair stem (7 x 4 filter over 8-channel pairs, strides
 // (2, 1), 64 output channels, no padding): dw[n][r][s][c] = sum over output pixels
@@ -906,12 +1202,13 @@ static int g_wgrad_wr = [] {
 
 // weight-gradient kernel choice for 3x3 / s1 / p1 shapes with W <= 62 (GM_WGRAD_LOOP at load,
 // gm_conv_set_wgrad_loop): bit 1 = k_wgrad_halo64 for 64 channels (layer 1), bit 2 = also for
-// 128 channels (layer 2); otherwise k_conv_wgrad4.  Default 6 (r04, B = 64 two-view step:
-// layer 1 61.9 -> 44.9 us and layer 2 54.6 -> 46.6 us per launch with the sum; step 3.98 ->
-// 3.91 ms against bit 1 alone).
+// 128 channels (layer 2); bit 4 = k_wgrad_ring for the other 3x3 shapes it serves (K % 128 == 0,
+// C % 32 == 0: layers 3 / 4 and the strided first convolutions); otherwise k_conv_wgrad4.
+// Default 22 (bits 1, 2: r04, B = 64 two-view step: layer 1 61.9 -> 44.9 us and layer 2
+// 54.6 -> 46.6 us per launch with the sum; step 3.98 -> 3.91 ms against bit 1 alone).
 static int g_wgrad_loop = [] {
     const char* e = getenv("GM_WGRAD_LOOP");
-    return e ? atoi(e) : 6;
+    return e ? atoi(e) : 22;
 }();
 
 template <int MT, int NT>
@@ -954,6 +1251,50 @@ static int halo64_splits(const gm_conv_desc_hw* d, int G) {
     return sp < srows ? sp : srows;
 }
 
+// k_wgrad_ring serves 3x3 shapes (any stride / padding) with K % 128 == 0 and C a power of two
+// >= 32 (GM_WGRAD_LOOP bit 4, default on): tiles x splits sized to one workgroup per CU
+static int device_cus_w() {
+    static const int cus = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            return 256;
+        return n;
+    }();
+    return cus;
+}
+// k_wgrad_ring's form (GM_WGRAD_RING at load, gm_conv_set_wgrad_ring): 0 = 3 slots of 64 pixels,
+// 1 = 6 slots of 32 pixels (more bytes in flight, twice the barriers)
+static int g_ring_form = [] {
+    const char* e = getenv("GM_WGRAD_RING");
+    return e ? atoi(e) : 0;
+}();
+static int ring_bk() { return g_ring_form == 1 ? 32 : 64; }
+struct RingPlan {
+    int P, Q, M, tiles_k, tiles_n, splits, sps;
+};
+static bool ring_plan(const gm_conv_desc_hw* d, int G, RingPlan& r) {
+    if (!(g_wgrad_loop & 16) || d->R != 3 || d->S != 3 || d->K % 128 != 0 || d->C % 32 != 0 || ilog2w(d->C) < 5)
+        return false;
+    r.P = (d->H + 2 * d->pad_h - 3) / d->stride_h + 1;
+    r.Q = (d->W + 2 * d->pad_w - 3) / d->stride_w + 1;
+    if (r.P < 1 || r.Q < 1 || d->N < 1) return false;
+    const long long M = (long long)d->N * r.P * r.Q;
+    if (M * d->K >= (1ll << 31) || (long long)d->N * d->H * d->W * d->C >= (1ll << 31)) return false;
+    r.M = (int)M;
+    r.tiles_k = d->K / 128;
+    r.tiles_n = d->C / 32;  // 9 C / 288
+    const int tiles = r.tiles_k * r.tiles_n * G;
+    const int bk = ring_bk();
+    const int steps = (r.M + bk - 1) / bk;
+    int want = device_cus_w() / tiles;
+    if (want > steps / (512 / bk)) want = steps / (512 / bk);  // >= 512 pixels per split
+    if (want < 1) want = 1;
+    r.sps = (steps + want - 1) / want;
+    r.splits = (steps + r.sps - 1) / r.sps;
+    return true;
+}
+
 // k_wgrad_stem serves the pixel-pair stem: 8-channel pairs, 64 output channels, a 7 x 4
 // filter, strides (2, 1), no padding, output rows of a multiple of 16 and <= 128 pixels
 static int g_wgrad_stem = [] {
@@ -981,12 +1322,17 @@ static bool stemw_plan(const gm_conv_desc_hw* d, int G, StemWPlan& w) {
 
 extern "C" size_t gm_conv2d_wgrad_grouped_scratch(const gm_conv_desc_hw* d, int G) {
     if (!d || d->stride_h < 1 || d->stride_w < 1 || G < 1) return 0;
-    StemWPlan sw;
-    if (stemw_plan(d, G, sw)) return (size_t)G * sw.splits * 64 * 224 * 4;
-    if (halo64_ok(d)) return (size_t)G * halo64_splits(d, G) * d->K * 9 * d->C * 4;
+    // the launch takes the stem / halo kernels only when c_real == C and otherwise falls
+    // through to k_conv_wgrad4, which this query cannot tell apart: size for the larger plan
     const WPlan w = plan(d, G);
     const size_t slab = (size_t)d->K * d->R * d->S * d->C;
-    return (size_t)G * w.splits * slab * sizeof(float);
+    size_t need = (size_t)G * w.splits * slab * sizeof(float);
+    StemWPlan sw;
+    RingPlan rp;
+    if (stemw_plan(d, G, sw)) need = std::max(need, (size_t)G * sw.splits * 64 * 224 * 4);
+    else if (halo64_ok(d)) need = std::max(need, (size_t)G * halo64_splits(d, G) * d->K * 9 * d->C * 4);
+    else if (ring_plan(d, G, rp) && rp.splits > 1) need = std::max(need, (size_t)G * rp.splits * slab * sizeof(float));
+    return need;
 }
 
 extern "C" int gm_conv_set_wgrad_stem(int on) {
@@ -1004,12 +1350,6 @@ extern "C" size_t gm_conv2d_wgrad_scratch(const gm_conv_desc* d) {
     return gm_conv2d_wgrad_hw_scratch(&h);
 }
 
-// 1x1 / s1 / p0 convolutions as plain GEMMs on hipBLASLt (conv1x1_lt.hip)
-namespace gm {
-bool conv1x1_lt_ok(int R, int S, int sh, int sw, int ph, int pw, long long M);
-int conv1x1_lt_wgrad(long long M, int C, int K, int G, const void* dy, long long gs_dy, const void* x, long long gs_x,
-                     float* dw, long long gs_dw, int accumulate, hipStream_t st);
-}  // namespace gm
 
 // G view groups in one launch: group g reads dy + g*N*P*Q*K and x + g*N*H*W*C (the views
 // stacked along the batch) and writes its weight gradient to dw + g*dw_stride (floats)
@@ -1026,13 +1366,6 @@ extern "C" int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, con
     const size_t slab_c = (size_t)d->K * d->R * d->S * (size_t)c_real;
     GM_REQUIRE(G == 1 || (dw_stride >= (long long)slab_c || dw_stride <= -(long long)slab_c),
                "conv wgrad: group gradient stride %lld overlaps one gradient", dw_stride);
-    const long long M = (long long)d->N * d->H * d->W;
-    if (gm::conv1x1_lt_ok(d->R, d->S, d->stride_h, d->stride_w, d->pad_h, d->pad_w, M) && c_real == d->C &&
-        (G == 1 || dw_stride > 0)) {
-        const int lr = gm::conv1x1_lt_wgrad(M, d->C, d->K, G, dy, M * d->K, x, M * d->C, dw, dw_stride, accumulate,
-                                    as_stream(stream));
-        if (lr != GM_E_UNSUP) return lr;  // no workspace-free GEMM: the im2col kernel
-    }
     const size_t need = gm_conv2d_wgrad_grouped_scratch(d, G);
     GM_REQUIRE(scratch && scratch_bytes >= need, "conv wgrad: scratch %zu < %zu", scratch_bytes, need);
     hipStream_t st0 = as_stream(stream);
@@ -1127,6 +1460,50 @@ extern "C" int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, con
         }
         return check_launch("k_wgrad_sum");
     }
+    RingPlan rp;
+    if (c_real == d->C && ring_plan(d, G, rp)) {
+        WRingArgs r;
+        memset(&r, 0, sizeof(r));
+        r.dy = (const uint16_t*)dy;
+        r.x = (const uint16_t*)x;
+        r.N = d->N; r.H = d->H; r.W = d->W; r.C = d->C; r.logC = ilog2w(d->C); r.K = d->K;
+        r.P = rp.P; r.Q = rp.Q; r.sth = d->stride_h; r.stw = d->stride_w; r.padh = d->pad_h; r.padw = d->pad_w;
+        r.M = rp.M;
+        r.tiles_k = rp.tiles_k; r.tiles_n = rp.tiles_n; r.splits = rp.splits; r.sps = rp.sps;
+        r.fd_pq = FastDiv((uint32_t)(rp.P * rp.Q));
+        r.fd_q = FastDiv((uint32_t)rp.Q);
+        const int BK = ring_bk();
+        r.adv_b = BK / (rp.P * rp.Q);
+        r.adv_p = (BK % (rp.P * rp.Q)) / rp.Q;
+        r.adv_q = (BK % (rp.P * rp.Q)) % rp.Q;
+        r.gs_dy = (long long)rp.M * d->K;
+        r.gs_x = (long long)d->N * d->H * d->W * d->C;
+        const size_t slab = (size_t)d->K * 9 * d->C;
+        const bool direct = rp.splits == 1;
+        r.part = direct ? dw : (float*)scratch;
+        r.gs_part = direct ? dw_stride : (long long)rp.splits * (long long)slab;
+        r.accumulate = direct ? accumulate : 0;
+        const int grid = rp.tiles_k * rp.tiles_n * rp.splits * G;
+        auto go = [&](auto sc, auto bc) -> int {
+            constexpr int S = decltype(sc)::value, BK = decltype(bc)::value;
+            constexpr size_t lds = (size_t)S * RingGeo<BK>::SLOT;
+            static bool attr = false;
+            if (!attr) {
+                if (hipFuncSetAttribute((const void*)k_wgrad_ring<S, BK>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)lds) != hipSuccess) {
+                    set_error("k_wgrad_ring: %zu B of LDS refused", lds);
+                    return GM_E_UNSUP;
+                }
+                attr = true;
+            }
+            k_wgrad_ring<S, BK><<<grid, 512, lds, st0>>>(r);
+            return check_launch("k_wgrad_ring");
+        };
+        const int rc = g_ring_form == 1 ? go(std::integral_constant<int, 6>{}, std::integral_constant<int, 32>{})
+                                        : go(std::integral_constant<int, 3>{}, std::integral_constant<int, 64>{});
+        if (rc || direct) return rc;
+        return split_sum(r.part, rp.splits, slab);
+    }
     WgradArgs a;
     memset(&a, 0, sizeof(a));
     const WPlan w = plan(d, G);
@@ -1206,9 +1583,16 @@ extern "C" int gm_conv_set_wgrad_staging(int wr) {
     return GM_OK;
 }
 
+extern "C" int gm_conv_set_wgrad_ring(int form) {
+    GM_REQUIRE(form == 0 || form == 1, "gm_conv_set_wgrad_ring: 0 (3 slots of 64 pixels) or 1 (6 slots of 32)");
+    g_ring_form = form;
+    return GM_OK;
+}
+
 extern "C" int gm_conv_set_wgrad_loop(int mode) {
-    GM_REQUIRE(mode >= 0 && mode <= 15 && !(mode & 1),
-               "gm_conv_set_wgrad_loop: bit 1 halo kernel for 64 channels, bit 2 up to 128, bit 3 up to 512");
+    GM_REQUIRE(mode >= 0 && mode <= 31 && !(mode & 1),
+               "gm_conv_set_wgrad_loop: bit 1 halo kernel for 64 channels, bit 2 up to 128, bit 3 up to 512, "
+               "bit 4 the ring kernel for 3x3 shapes with K % 128 == 0, C % 32 == 0");
     g_wgrad_loop = mode;
     return GM_OK;
 }

@@ -63,7 +63,8 @@ __global__ void k_gate_strong(const double* __restrict__ s, gm_gate_state* st) {
 
 // N branches (C4 / C5): the host gate's N-branch rule (callbacks.bdr_values /
 // bdr_decision) in fp64 - M_main_i += g/w of group i, M_bypass_i += g/w of group nb+i,
-// BDR_i = log10(M_bypass_i / M_main_i), d = max - min, caring = argmax (first on ties)
+// BDR_i = log10(M_bypass_i / M_main_i), d = max - min (two branches: the signed
+// BDR_0 - BDR_1), caring = argmax (first on ties)
 __global__ void k_gate_strong_n(const double* __restrict__ s, gm_gate_state_n* st) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     gm_gate_state_n g = *st;
@@ -80,7 +81,9 @@ __global__ void k_gate_strong_n(const double* __restrict__ s, gm_gate_state_n* s
             if (i == 0 || b > mx) { mx = b; hi = i; }  // numpy argmax: first maximum
             if (i == 0 || b < mn) mn = b;
         }
-        g.d_bdr = mx - mn;
+        // two branches: the reference's signed BDR_0 - BDR_1 (src/callbacks.py:233), as the
+        // host gate and k_gate_strong log it; the decision (|d| > eps, caring = argmax) is the same
+        g.d_bdr = nb == 2 ? g.bdr[0] - g.bdr[1] : mx - mn;
     };
     if (g.unlock) {
         if (!g.curation_mode) {

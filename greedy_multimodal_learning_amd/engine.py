@@ -422,6 +422,9 @@ class BalancedStep:
             g.M_bypass = [float(v) for v in st.M_bypass[:nb]]
             g.M_main = [float(v) for v in st.M_main[:nb]]
             g.BDR = [float(v) for v in st.bdr[:nb]]
+            if nb == 2:  # the two-branch host mirrors, as the host gate keeps them
+                g.M_bypass_modal_0, g.M_bypass_modal_1 = g.M_bypass
+                g.M_main_modal_0, g.M_main_modal_1 = g.M_main
         else:
             g.M_bypass_modal_0, g.M_bypass_modal_1 = float(st.M[0]), float(st.M[1])
             g.M_main_modal_0, g.M_main_modal_1 = float(st.M[2]), float(st.M[3])
@@ -552,7 +555,12 @@ class BalancedStep:
             if slot is None:
                 st = self._static
                 if st is None or st[0].shape != x.shape or st[1].shape != y.shape or st[0].dtype != x.dtype:
+                    if self._graphs:  # (as above: no graph destroyed under a running replay)
+                        torch.cuda.synchronize(self.device)
                     self._graphs = {}
+                    # the destroyed graphs released the private pool; capturing into a released
+                    # pool trips the caching allocator (use_count == 0): start a fresh one
+                    self._gpool = None
                     self._static = st = (x.detach().clone(), y.detach().clone())
                 else:
                     if st[0].data_ptr() != x.data_ptr():
@@ -562,9 +570,15 @@ class BalancedStep:
             key = (self._graph_key(), None if slot is None else (x.data_ptr(), y.data_ptr()))
             entry, err = self._graphs.get(key), None
             if entry is None:
-                # a learning-rate change (ReduceLROnPlateau) makes the old-lr graphs dead weight
-                for k in [k for k in self._graphs if k[0][-1] != self.lr]:
+                # a learning-rate change (ReduceLROnPlateau) makes the old-lr graphs dead weight;
+                # the last replay may still be running: destroy nothing before it is done
+                stale = [k for k in self._graphs if k[0][-1] != self.lr]
+                if stale:
+                    torch.cuda.synchronize(self.device)
+                for k in stale:
                     del self._graphs[k]
+                if stale and not self._graphs:
+                    self._gpool = None  # (every graph of the pool destroyed: a fresh pool)
                 try:
                     entry = self._capture(key, slot)
                 except RuntimeError as e:  # capture refused on this system
@@ -583,6 +597,7 @@ class BalancedStep:
                           "collectives run eagerly behind each replay", file=sys.stderr, flush=True)
                     self.graph_collectives = False
                     self._graphs = {}
+                    self._gpool = None
                     torch.cuda.synchronize(self.device)
                     return self(x, y)
                 print(f"[greedy_multimodal_learning_amd] hipGraph capture failed ({err}); eager steps from now on",

@@ -55,6 +55,29 @@ def alias_capture_stream(idx, eager_sid):
     _capture_alias[(idx, torch.cuda.current_stream(idx).stream_id)] = eager_sid
 
 
+def zeroed_scratch(cache, device, need, size_of):
+    """The per-stream zero-initialised scratch buffer (uint8) of `cache` with >= need bytes.
+
+    Keyed by scratch_key: a capture stream reuses the eager stream's buffer when it is big
+    enough.  A buffer that must GROW inside a capture is never put under the aliased key - its
+    torch.zeros is only recorded into the graph, not run, so eager launches (a failed capture's
+    fallback) would then meet ticket words nobody zeroed; it goes under the capture stream's
+    own key instead, where the recorded fill runs before every use."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    key = scratch_key(idx)
+    buf = cache.get(key)
+    if buf is not None and buf.numel() >= need:
+        return buf
+    if torch.cuda.is_current_stream_capturing():
+        key = (idx, torch.cuda.current_stream(idx).stream_id)
+        buf = cache.get(key)
+        if buf is not None and buf.numel() >= need:
+            return buf
+    buf = torch.zeros(size_of(buf), device=device, dtype=torch.uint8)
+    cache[key] = buf
+    return buf
+
+
 def all_side_streams(device):
     idx = device.index if device.index is not None else torch.cuda.current_device()
     return [s for (d, _), s in sorted(_side.items(), key=lambda kv: kv[0]) if d == idx]

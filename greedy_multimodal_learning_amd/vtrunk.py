@@ -29,7 +29,7 @@ import os
 
 import torch
 
-from .streams import scratch_key
+from .streams import zeroed_scratch
 from . import _lib as L
 from .bn import MASK_FROM_X
 from .conv import CL, _cpad, _desc, _desc_hw, _like_param, _prepped, _splitk_ws, _stem_geom, stem_pack
@@ -74,12 +74,7 @@ def _splitk_g(device, d, G, dgrad):
     need = L.load().gm_conv2d_splitk_ws_bytes_grouped(ctypes.byref(d), G, int(dgrad))
     if need == 0:
         return 0, 0
-    idx = device.index if device.index is not None else torch.cuda.current_device()
-    key = scratch_key(idx)
-    buf = _splitk_ws.get(key)
-    if buf is None or buf.numel() < need:
-        buf = torch.zeros((need + (1 << 20) - 1) >> 20 << 20, device=device, dtype=torch.uint8)
-        _splitk_ws[key] = buf
+    buf = zeroed_scratch(_splitk_ws, device, need, lambda old: (need + (1 << 20) - 1) >> 20 << 20)
     return buf.data_ptr(), buf.numel()
 
 
@@ -90,14 +85,8 @@ def _bn_scratch_g(device, M, C, G):
     """Grouped-layout BatchNorm scratch per (device, stream), zeroed once (its ticket words
     sit in fixed per-group headers: never shared with the ungrouped calls' buffers)."""
     need = L.load().gm_bn_scratch_grouped(M, C, G)
-    idx = device.index if device.index is not None else torch.cuda.current_device()
-    key = scratch_key(idx)
-    buf = _bn_scratch.get(key)
-    if buf is None or buf.numel() < need:
-        size = max(need, 1 << 20) if buf is None else max(need, 2 * buf.numel())
-        buf = torch.zeros(size, device=device, dtype=torch.uint8)
-        _bn_scratch[key] = buf
-    return buf
+    return zeroed_scratch(_bn_scratch, device, need,
+                          lambda old: max(need, 1 << 20) if old is None else max(need, 2 * old.numel()))
 
 
 @L.on_fault_reset

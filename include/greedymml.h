@@ -370,11 +370,16 @@ int gm_conv_set_h9_staging(int wr);
 /* Split-K target: workgroups wanted from splitting K of 128x128-tile convolutions whose
  * tiles alone do not fill the device (default 384, GM_CONV_SPLITK at load; 0 = never). */
 int gm_conv_set_splitk(int target);
-/* Weight-gradient kernel for 3x3 / s1 / p1 shapes with W <= 62 (GM_WGRAD_LOOP at load; default
- * 6): bit 1 = k_wgrad_halo64 (64 x 9 x 64 gradient blocks in one workgroup's accumulators, one
- * input row staged per output row, dedicated loader waves) for 64 channels, bit 2 = also for
- * 128 channels; the rest take k_conv_wgrad4.  Bit 0 is reserved (must be 0). */
+/* Weight-gradient kernel choice (GM_WGRAD_LOOP at load; default 22): bit 1 = k_wgrad_halo64 (64 x 9 x 64
+ * gradient blocks in one workgroup's accumulators, one input row staged per output row, dedicated
+ * loader waves) for 3x3 / s1 shapes with 64 channels, bit 2 = also for 128 channels, bit 3 = up to
+ * 512; bit 4 = k_wgrad_ring for the other 3x3 shapes with K % 128 == 0 and C a power of two >= 32
+ * (loader waves feeding an LDS ring, one workgroup per CU); the rest take k_conv_wgrad4.  Bit 0 is
+ * reserved (must be 0). */
 int gm_conv_set_wgrad_loop(int mode);
+/* k_wgrad_ring's staging form (GM_WGRAD_RING at load): 0 (default) = 3 slots of 64 pixels,
+ * 1 = 6 slots of 32 pixels. */
+int gm_conv_set_wgrad_ring(int form);
 /* 1x1 / stride-1 / pad-0 convolutions (forward, input and weight gradient) as plain GEMMs on
  * hipBLASLt (default off: GM_CONV1X1_LT=1 at load or gm_conv_set_1x1_gemm(1) turn it on). */
 int gm_conv_set_1x1_gemm(int on);

@@ -12,6 +12,8 @@ import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 
+WGRAD_LOOP_DEFAULT = 22  # gm_conv_set_wgrad_loop's default (conv_wgrad.hip g_wgrad_loop)
+
 SHAPES = [  # N, C, H, W, K, R, S, stride, pad
     (2, 64, 56, 56, 64, 3, 3, 1, 1),
     (2, 64, 56, 56, 128, 3, 3, 2, 1),
@@ -446,7 +448,7 @@ def test_wgrad4_grouped_vs_fp32(dev, shape):
             outs.append(dw)
         torch.cuda.synchronize()
     finally:
-        L.check(lib.gm_conv_set_wgrad_loop(6), "loop")  # the default
+        L.check(lib.gm_conv_set_wgrad_loop(WGRAD_LOOP_DEFAULT), "loop")  # the default
     for gi in range(G):
         xr = x[gi * N:(gi + 1) * N].float().permute(0, 3, 1, 2)
         gr = dy[gi * N:(gi + 1) * N].float().permute(0, 3, 1, 2)
@@ -497,13 +499,66 @@ def test_wgrad_halo64_vs_fp32(dev, shape):
             outs[m] = res
         torch.cuda.synchronize()
     finally:
-        L.check(lib.gm_conv_set_wgrad_loop(6), "loop")  # the default
+        L.check(lib.gm_conv_set_wgrad_loop(WGRAD_LOOP_DEFAULT), "loop")  # the default
     for gi in range(G):
         xr = x[gi * N:(gi + 1) * N].float().permute(0, 3, 1, 2)
         gr = dy[gi * N:(gi + 1) * N].float().permute(0, 3, 1, 2)
         ref = torch.nn.grad.conv2d_weight(xr, (K, C, 3, 3), gr, stride=1, padding=1)
         for acc, base in ((0, 0.0), (1, 0.5)):
             got = outs[mode][acc][gi].permute(0, 3, 1, 2) - base
+            err = float((got - ref).abs().max() / ref.abs().max())
+            assert err < 2e-3, (gi, acc, err)
+            old = outs[0][acc][gi].permute(0, 3, 1, 2) - base
+            assert float((got - old).abs().max() / ref.abs().max()) < 1e-4
+
+
+@pytest.mark.parametrize("shape", [(64, 256, 14, 14, 256, 1, 2), (64, 512, 7, 7, 512, 1, 2), (64, 128, 28, 28, 256, 2, 2),
+                                   (64, 256, 14, 14, 512, 2, 2), (64, 64, 56, 56, 128, 2, 2), (3, 256, 14, 14, 256, 1, 2),
+                                   (5, 128, 9, 11, 128, 2, 2), (2, 32, 7, 5, 128, 1, 2), (1, 512, 7, 7, 512, 1, 2),
+                                   (4, 128, 28, 28, 128, 1, 2), (3, 256, 14, 14, 256, 1, 12)],
+                         ids=lambda s: "x".join(map(str, s)))
+@pytest.mark.parametrize("form", [0, 1], ids=["bk64", "bk32"])
+def test_wgrad_ring_vs_fp32(dev, shape, form):
+    """k_wgrad_ring (3x3 weight gradient, 128 x 288 tiles, loader waves feeding a 3-slot LDS ring,
+    splits over the pixel steps sized to one workgroup per CU, slabs summed in a fixed order; one
+    split writes the gradient directly) against fp32 PyTorch per view group, plain and
+    accumulating, strided and ragged shapes (M not a multiple of 64) included, 2 and 12 (C5) view
+    groups; and against k_conv_wgrad4 within fp32 summation-order noise."""
+    import ctypes
+    from greedy_multimodal_learning_amd import _lib as L
+    from greedy_multimodal_learning_amd import conv as CV
+    N, C, H, W, K, st, G = shape
+    P, Q = (H + 2 - 3) // st + 1, (W + 2 - 3) // st + 1
+    torch.manual_seed(N * 1000 + C + H * 10 + W + st)
+    x = torch.randn(G * N, H, W, C, device=dev).bfloat16()
+    dy = torch.randn(G * N, P, Q, K, device=dev).bfloat16()
+    lib = L.load()
+    d = CV._desc_hw(N, H, W, C, K, 3, 3, st, st, 1, 1)
+    outs = {}
+    try:
+        L.check(lib.gm_conv_set_wgrad_ring(form), "ring form")
+        for m in (0, 16):
+            L.check(lib.gm_conv_set_wgrad_loop(m), "loop")
+            need = lib.gm_conv2d_wgrad_grouped_scratch(ctypes.byref(d), G)
+            scr = torch.empty(max(need, 16), device=dev, dtype=torch.uint8)
+            res = []
+            for acc in (0, 1):
+                dw = torch.full((G, K, 3, 3, C), 0.5, device=dev, dtype=torch.float32)
+                L.check(lib.gm_conv2d_wgrad_grouped_bf16(ctypes.byref(d), G, dy.data_ptr(), x.data_ptr(),
+                                                          dw.data_ptr(), K * 9 * C, C, acc, scr.data_ptr(),
+                                                          need, L.stream_of(dev)), "wgrad")
+                res.append(dw)
+            outs[m] = res
+        torch.cuda.synchronize()
+    finally:
+        L.check(lib.gm_conv_set_wgrad_loop(WGRAD_LOOP_DEFAULT), "loop")
+        L.check(lib.gm_conv_set_wgrad_ring(0), "ring form")
+    for gi in range(G):
+        xr = x[gi * N:(gi + 1) * N].float().permute(0, 3, 1, 2)
+        gr = dy[gi * N:(gi + 1) * N].float().permute(0, 3, 1, 2)
+        ref = torch.nn.grad.conv2d_weight(xr, (K, C, 3, 3), gr, stride=st, padding=1)
+        for acc, base in ((0, 0.0), (1, 0.5)):
+            got = outs[16][acc][gi].permute(0, 3, 1, 2) - base
             err = float((got - ref).abs().max() / ref.abs().max())
             assert err < 2e-3, (gi, acc, err)
             old = outs[0][acc][gi].permute(0, 3, 1, 2) - base
@@ -525,7 +580,7 @@ def test_wgrad_halo64_beside_a_busy_neighbour(dev):
     dy = torch.randn(G * N, H, W, C, device=dev).bfloat16()
     lib = L.load()
     d = CV._desc_hw(N, H, W, C, C, 3, 3, 1, 1, 1, 1)
-    L.check(lib.gm_conv_set_wgrad_loop(6), "loop")
+    L.check(lib.gm_conv_set_wgrad_loop(WGRAD_LOOP_DEFAULT), "loop")
     need = lib.gm_conv2d_wgrad_grouped_scratch(ctypes.byref(d), G)
     scr = torch.empty(need, device=dev, dtype=torch.uint8)
     side = torch.cuda.Stream()

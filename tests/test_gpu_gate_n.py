@@ -11,7 +11,7 @@ pytestmark = pytest.mark.gpu
 V = 4
 
 
-def _run(device_gate, graphs, steps, dev):
+def _run(device_gate, graphs, steps, dev, V=V):
     from greedy_multimodal_learning_amd.callbacks import Bias_Mitigation_Strong
     from greedy_multimodal_learning_amd.engine import BalancedStep
     from greedy_multimodal_learning_amd.model import MMTM_MVCNN_N
@@ -40,11 +40,17 @@ def _run(device_gate, graphs, steps, dev):
     return m, st, trace
 
 
-@pytest.mark.parametrize("graphs", [False, True])
-def test_n_branch_device_gate_equals_host_gate(graphs):
+@pytest.mark.parametrize("graphs,views", [(False, V), (True, V), (True, 2)])
+def test_n_branch_device_gate_equals_host_gate(graphs, views):
+    """At two views the N-branch kernel must log the reference's SIGNED d_BDR = BDR_0 - BDR_1
+    (what the host gate's nb == 2 rule computes) and fill the two-branch host mirrors."""
     dev = torch.device("cuda:0")
-    m_h, _, tr_h = _run(False, False, 10, dev)
-    m_d, st_d, tr_d = _run(True, graphs, 10, dev)
+    m_h, st_h, tr_h = _run(False, False, 10, dev, views)
+    m_d, st_d, tr_d = _run(True, graphs, 10, dev, views)
+    if views == 2:
+        g_h, g_d = st_h.gate, st_d.gate
+        for k in ("M_bypass_modal_0", "M_bypass_modal_1", "M_main_modal_0", "M_main_modal_1"):
+            assert getattr(g_d, k) == pytest.approx(getattr(g_h, k), rel=1e-6), k
     assert {t[2] for t in tr_h} == {True, False}, "the trace should contain curation steps"
     assert len({t[3] for t in tr_h if t[2]}) >= 1
     if graphs:
@@ -115,3 +121,13 @@ def test_n_branch_gate_kernel_rule():
     state.copy_(torch.frombuffer(bytearray(bytes(st3)), dtype=torch.uint8))
     r = step()
     assert r.curation_mode == 0 and r.caring == 0 and r.d_bdr > 0.05
+    # two branches: the signed d = BDR_0 - BDR_1 (negative when branch 1 leads), caring 1
+    st4 = L.GateStateN()
+    st4.nb, st4.eps, st4.window, st4.unlock, st4.caring = 2, 0.05, 2, 1, -1
+    state.copy_(torch.frombuffer(bytearray(bytes(st4)), dtype=torch.uint8))
+    sums2 = torch.tensor([2.0, 2.0, 2.0, 2.0, 4.0, 4.0, 4.0, 16.0], dtype=torch.float64, device=dev)
+    L.check(lib.gm_gate_strong_step_n(sums2.data_ptr(), state.data_ptr(), L.stream_of(dev)), "gate_n")
+    torch.cuda.synchronize()
+    r = L.GateStateN.from_buffer_copy(state.cpu().numpy().tobytes())
+    assert r.d_bdr == pytest.approx(-math.log10(4.0), abs=1e-12)
+    assert r.curation_mode == 1 and r.caring == 1

@@ -131,3 +131,40 @@ def test_device_gate_equals_host_gate(graphs):
     for i in (2, 3, 4):
         a, b = getattr(m_h, f"mmtm{i}"), getattr(m_d, f"mmtm{i}")
         torch.testing.assert_close(b.running_avg_weight_visual, a.running_avg_weight_visual, rtol=1e-6, atol=1e-7)
+
+
+def test_larger_second_batch_under_capture():
+    """a batch larger than every earlier one is captured directly (no eager
+    warm-up at its shape), so the BN ticket / split-K turnstile scratch must grow INSIDE the
+    capture.  The grown buffers must not replace the eager stream's (their zero fill is only
+    recorded): graph steps over growing batches equal eager steps, and an eager step after
+    them (the failed-capture fallback's path) still runs on zeroed tickets."""
+    from greedy_multimodal_learning_amd.callbacks import Bias_Mitigation_Strong
+    from greedy_multimodal_learning_amd.engine import BalancedStep
+    from greedy_multimodal_learning_amd.model import MMTM_MVCNN
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(7)
+    sizes = [2, 2, 8, 8, 16]
+    xs = [torch.randn(b, 2, 3, 64, 64, device=dev, generator=g) for b in sizes]
+    ys = [torch.randint(0, 40, (b,), device=dev, generator=g) for b in sizes]
+
+    def run(graphs):
+        torch.manual_seed(0)
+        m = MMTM_MVCNN().to(dev)
+        gate = Bias_Mitigation_Strong(epsilon=2e-3, curation_windowsize=2,
+                                      branchnames=["net_view_0", "net_view_1"], starting_epoch=1)
+        st = BalancedStep(m, lr=0.05, gate=gate, graphs=graphs, device_gate=True)
+        st.on_epoch_begin(1)
+        losses = [float(st(x, y)) for x, y in zip(xs, ys)]
+        assert st.graphs == graphs, "a capture failed and the engine fell back to eager steps"
+        st.graphs = False  # one eager step after the captured ones, at the largest shape
+        losses.append(float(st(xs[-1], ys[-1])))
+        torch.cuda.synchronize()
+        return m, losses
+
+    m_e, l_e = run(False)
+    m_g, l_g = run(True)
+    assert l_g == pytest.approx(l_e, rel=1e-6, abs=1e-6)
+    se, sg = m_e.state_dict(), m_g.state_dict()
+    for k in se:
+        torch.testing.assert_close(sg[k], se[k], rtol=1e-6, atol=1e-6, msg=k)
