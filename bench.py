@@ -18,8 +18,16 @@ import os
 import sys
 import time
 
-import torch
-import torch.distributed as dist
+# A data-parallel rank runs more concurrent streams (main chain, weight gradients, the gradient
+# bucket stream, RCCL's own) than HIP's default 4 hardware queues.  Streams that share a queue
+# serialise: a long RCCL kernel would hold back every launch queued behind it on that queue
+# (tests/test_gpu_rccl_residency.py measured a 393 ms stall behind a CU-holding kernel on a shared
+# queue).  Set before the HIP runtime initialises; an operator's value wins.
+if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)

@@ -894,57 +894,27 @@ __global__ __launch_bounds__(512) void k_wgrad_ring(WRingArgs a) {
             }
         }
     }
-    // Epilogue through LDS: per half (accumulator rows 16 h .. 16 h + 15) the wave stages its
-    // [16][288] fp32 block in a slot no wave reads any more (every slot but the last step's:
-    // all their reads finished before the last barrier, and no DMA is in flight) and leaves
-    // with 16-B stores - 18 dwordx4 instead of 72 dword stores per half.
-    // D[k][col]: col = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5)
-    constexpr int HB = 16 * 288 * 4;  // 18 KB per wave and half
-    static_assert(Geo::SLOT >= HB && (S - 1) * Geo::SLOT >= 4 * HB, "k_wgrad_ring: epilogue staging space");
-    unsigned stg;
-    if constexpr (Geo::SLOT >= 2 * HB) {  // two waves per free slot
-        const int s1 = slot + 1 + (w >> 1);
-        stg = (unsigned)((s1 % S) * Geo::SLOT + (w & 1) * HB);
-    } else {
-        const int s1 = slot + 1 + w;
-        stg = (unsigned)((s1 % S) * Geo::SLOT);
-    }
-    float* stgp = reinterpret_cast<float*>(lds + stg);
+    // D[k][col]: col = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5).  Direct dword stores
+    // (an LDS-staged dwordx4 epilogue measured 3-4 us slower per launch: hipcc serialised its
+    // stores on vmcnt(0)); the accumulate test is hoisted out of the loops (a per-element select
+    // would branch and wait vmcnt(0) around every load)
     const int TC = 9 * a.C;
-    float* out = a.part + grp * a.gs_part + (size_t)split * a.K * TC + (size_t)(k0 + 32 * w) * TC + n0;
+    float* out = a.part + grp * a.gs_part + (size_t)split * a.K * TC + (size_t)(k0 + 32 * w + 4 * (lane >> 5)) * TC +
+                 n0 + (lane & 31);
+    if (a.accumulate) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+        for (int j = 0; j < 9; ++j) {
+            float v[16];
+#pragma unroll
+            for (int e = 0; e < 16; ++e) v[e] = out[(size_t)((e & 3) + 8 * (e >> 2)) * TC + 32 * j];
+#pragma unroll
+            for (int e = 0; e < 16; ++e) out[(size_t)((e & 3) + 8 * (e >> 2)) * TC + 32 * j] = v[e] + acc[j][e];
+        }
+    } else {
 #pragma unroll
         for (int j = 0; j < 9; ++j)
 #pragma unroll
-            for (int e = 8 * h; e < 8 * h + 8; ++e)
-                stgp[((e & 3) + 8 * ((e >> 2) & 1) + 4 * (lane >> 5)) * 288 + 32 * j + (lane & 31)] = acc[j][e];
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's own staging writes done
-        __builtin_amdgcn_sched_barrier(0);
-        float4 v[18];
-#pragma unroll
-        for (int i = 0; i < 18; ++i) {
-            const int L = i * 64 + lane, row = L / 72, c4 = L - row * 72;
-            v[i] = reinterpret_cast<const float4*>(stgp)[row * 72 + c4];
-        }
-        float* oh = out + (size_t)(16 * h) * TC;
-        if (a.accumulate) {
-#pragma unroll
-            for (int i = 0; i < 18; ++i) {
-                const int L = i * 64 + lane, row = L / 72, c4 = L - row * 72;
-                float4* o = reinterpret_cast<float4*>(oh + (size_t)row * TC) + c4;
-                const float4 u = *o;
-                *o = make_float4(u.x + v[i].x, u.y + v[i].y, u.z + v[i].z, u.w + v[i].w);
-            }
-        } else {
-#pragma unroll
-            for (int i = 0; i < 18; ++i) {
-                const int L = i * 64 + lane, row = L / 72, c4 = L - row * 72;
-                reinterpret_cast<float4*>(oh + (size_t)row * TC)[c4] = v[i];
-            }
-        }
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // the reads of this half done before the next half's writes
-        __builtin_amdgcn_sched_barrier(0);
+            for (int e = 0; e < 16; ++e) out[(size_t)((e & 3) + 8 * (e >> 2)) * TC + 32 * j] = acc[j][e];
     }
 }
 
@@ -1270,11 +1240,22 @@ static int g_ring_form = [] {
     return e ? atoi(e) : 0;
 }();
 static int ring_bk() { return g_ring_form == 1 ? 32 : 64; }
+// A/B knobs (GM_WGRAD_RING_WGS: workgroups the plan aims at, default one per CU;
+// GM_WGRAD_RING_MINK: the smallest K served, default 128)
+static int g_ring_wgs = [] {
+    const char* e = getenv("GM_WGRAD_RING_WGS");
+    return e ? atoi(e) : 0;
+}();
+static int g_ring_mink = [] {
+    const char* e = getenv("GM_WGRAD_RING_MINK");
+    return e ? atoi(e) : 128;
+}();
 struct RingPlan {
     int P, Q, M, tiles_k, tiles_n, splits, sps;
 };
 static bool ring_plan(const gm_conv_desc_hw* d, int G, RingPlan& r) {
-    if (!(g_wgrad_loop & 16) || d->R != 3 || d->S != 3 || d->K % 128 != 0 || d->C % 32 != 0 || ilog2w(d->C) < 5)
+    if (!(g_wgrad_loop & 16) || d->R != 3 || d->S != 3 || d->K % 128 != 0 || d->C % 32 != 0 || ilog2w(d->C) < 5 ||
+        d->K < g_ring_mink)
         return false;
     r.P = (d->H + 2 * d->pad_h - 3) / d->stride_h + 1;
     r.Q = (d->W + 2 * d->pad_w - 3) / d->stride_w + 1;
@@ -1287,7 +1268,7 @@ static bool ring_plan(const gm_conv_desc_hw* d, int G, RingPlan& r) {
     const int tiles = r.tiles_k * r.tiles_n * G;
     const int bk = ring_bk();
     const int steps = (r.M + bk - 1) / bk;
-    int want = device_cus_w() / tiles;
+    int want = (g_ring_wgs > 0 ? g_ring_wgs : device_cus_w()) / tiles;
     if (want > steps / (512 / bk)) want = steps / (512 / bk);  // >= 512 pixels per split
     if (want < 1) want = 1;
     r.sps = (steps + want - 1) / want;
@@ -1499,8 +1480,9 @@ extern "C" int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, con
             k_wgrad_ring<S, BK><<<grid, 512, lds, st0>>>(r);
             return check_launch("k_wgrad_ring");
         };
-        const int rc = g_ring_form == 1 ? go(std::integral_constant<int, 6>{}, std::integral_constant<int, 32>{})
-                                        : go(std::integral_constant<int, 3>{}, std::integral_constant<int, 64>{});
+        const int rc = g_ring_form == 1   ? go(std::integral_constant<int, 6>{}, std::integral_constant<int, 32>{})
+                       : g_ring_form == 2 ? go(std::integral_constant<int, 2>{}, std::integral_constant<int, 64>{})
+                                          : go(std::integral_constant<int, 3>{}, std::integral_constant<int, 64>{});
         if (rc || direct) return rc;
         return split_sum(r.part, rp.splits, slab);
     }
@@ -1584,7 +1566,8 @@ extern "C" int gm_conv_set_wgrad_staging(int wr) {
 }
 
 extern "C" int gm_conv_set_wgrad_ring(int form) {
-    GM_REQUIRE(form == 0 || form == 1, "gm_conv_set_wgrad_ring: 0 (3 slots of 64 pixels) or 1 (6 slots of 32)");
+    GM_REQUIRE(form >= 0 && form <= 2,
+               "gm_conv_set_wgrad_ring: 0 (3 slots of 64 pixels), 1 (6 slots of 32), 2 (2 slots of 64)");
     g_ring_form = form;
     return GM_OK;
 }

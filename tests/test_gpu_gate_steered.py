@@ -54,6 +54,25 @@ def _steer(r, target):
 
 @pytest.fixture(scope="module")
 def trace():
+    return _trace(EPS, TARGETS, MIN_DECIDING, FLOOR_STEPS)
+
+
+# training_guided.gin's own epsilon (configs/training_guided.gin:14): 0.01.  With the 1e-2 bf16
+# band no no-curation step can be judged (|d_BDR| < 0.01 lies inside the band of +-0.01), so the
+# targets put most steps far beyond it in both signs (judged: curate + which modality) and the rest
+# near 0 / near +-epsilon (reported: how often the bf16 step still matches there)
+EPS_GUIDED = 0.01
+TARGETS_GUIDED = [0.030, -0.030, 0.0, 0.025, -0.025, 0.012, -0.012, 0.040, -0.040, 0.004, 0.022, -0.022, 0.008,
+                  -0.006, 0.050, -0.050]
+MIN_DECIDING_GUIDED = 16
+
+
+@pytest.fixture(scope="module")
+def trace_guided():
+    return _trace(EPS_GUIDED, TARGETS_GUIDED, MIN_DECIDING_GUIDED, 0)
+
+
+def _trace(EPS, TARGETS, MIN_DECIDING, FLOOR_STEPS):
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     from greedy_multimodal_learning_amd.callbacks import Bias_Mitigation_Strong
@@ -143,3 +162,24 @@ def test_steered_gate_decisions_vs_oracle(trace):
         assert dec_h == dec_o, (t, dh, do, dec_h, dec_o)
     agree = sum(r[3] == r[4] for r in rows)
     print(f"decisions identical on {agree}/{len(rows)} deciding steps ({len(clear)} outside the band)")
+
+
+def test_steered_gate_decisions_at_guided_epsilon(trace_guided):
+    """The same teacher-forced, steered C2 bf16 step at training_guided.gin's epsilon = 0.01: every
+    step whose oracle d_BDR lies outside the bf16 band around +-epsilon (|d| > 0.02 here) must
+    curate the same modality; steps inside the band (every no-curation step at this epsilon)
+    are reported with the fraction that still decides like the fp32 reference."""
+    rows = trace_guided
+    eps = EPS_GUIDED
+    clear = [r for r in rows if abs(abs(r[2]) - eps) > BAND]
+    inside = [r for r in rows if abs(abs(r[2]) - eps) <= BAND]
+    assert len(clear) >= len(rows) // 2, (len(clear), len(rows))
+    assert {(True, 0), (True, 1)} <= {r[4] for r in clear}
+    for t, dh, do, dec_h, dec_o, _ in clear:
+        assert dec_h == dec_o, (t, dh, do, dec_h, dec_o)
+    agree_in = sum(r[3] == r[4] for r in inside)
+    diff = np.array([abs(r[1] - r[2]) for r in rows])
+    print(f"epsilon {eps}: decisions identical on {len(clear)}/{len(clear)} steps outside the band and "
+          f"{agree_in}/{len(inside)} inside it ({sum(r[4][0] is False for r in inside)} of those no-curation in the "
+          f"fp32 reference); d_BDR |hip - oracle| median {np.median(diff):.2e} max {diff.max():.2e}")
+    assert diff.max() < BAND
