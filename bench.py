@@ -72,7 +72,7 @@ def parse():
 
 def cpu_baseline(seconds, size):
     """Oracle (port) of the reference step on the host cores: config C1's
-    shape (B = 4) for ~`seconds`, then B = 64 (the GPU workload's batch) for a few steps.
+    shape (B = 4) for ~`seconds`, then B = 64 (the GPU workload's batch) for ten timed steps.
     Threads: torch's intra-op pool as the box configures it (OMP_NUM_THREADS = the CPU
     share of the job); os.cpu_count() reports the whole machine and is stated beside it."""
     from oracle import model_ref, step_ref, gating_ref, weights
@@ -98,7 +98,7 @@ def cpu_baseline(seconds, size):
 
     th = torch.get_num_threads()
     n4, dt4 = run(4, seconds, 200)
-    n64, dt64 = run(64, 0.0, 2)
+    n64, dt64 = run(64, 0.0, 10)  # ten timed steps at the bench batch (BASELINE.md quotes a median of 10)
     return {"value": round(n4 * 4 * 2 / dt4, 3), "unit": "view-images/s", "cores": th,
             "kind": "port", "ms_per_step": round(1e3 * dt4 / n4, 2),
             "b64": {"value": round(n64 * 64 * 2 / dt64, 3), "ms_per_step": round(1e3 * dt64 / n64, 1),

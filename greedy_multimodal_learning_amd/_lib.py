@@ -350,7 +350,6 @@ EXPORTS.update({
     "gm_conv_set_pipe": (c_int, [c_int]),
     "gm_conv_set_halo": (c_int, [c_int]),
     "gm_conv_set_h9": (c_int, [c_int]),
-    "gm_conv_set_h9_staging": (c_int, [c_int]),
     "gm_conv_set_wgrad_staging": (c_int, [c_int]),
     "gm_conv_set_splitk": (c_int, [c_int]),
     "gm_conv_set_wgrad_loop": (c_int, [c_int]),

@@ -417,9 +417,6 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
     constexpr int MT = BM / 64, NT = BN / 64;
     constexpr int SA = BM * 128, SB = BN * 128;  // bytes per stage
     constexpr int NST = PIPE == 3 ? 3 : 2;      // LDS stages
-    // diagnostics (timing only, outputs meaningless): PIPE 5 = the PIPE 2 loop without
-    // its LDS-DMA, PIPE 6 = without its MFMA/LDS reads
-    constexpr bool kDma = PIPE != 5, kMath = PIPE != 6;
     constexpr int G = AR + BR;                   // LDS-DMA instructions per wave per k-tile
     extern __shared__ __attribute__((aligned(16))) uint4 smem[];
     char* lds = reinterpret_cast<char*>(smem);   // [A0..A(NST-1)][B0..B(NST-1)]
@@ -618,19 +615,19 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
         // s_waitcnt immediates (gfx9 encoding: vmcnt[3:0] + [15:14], expcnt[6:4], lgkmcnt[11:8])
         constexpr int kWaitTile = (G & 15) | (7 << 4) | (15 << 8) | (((G >> 4) & 3) << 14);  // vmcnt(G)
         constexpr int kWaitAll = (7 << 4) | (15 << 8);                                       // vmcnt(0)
-        if (kDma) issue(0, 0);
-        if (kDma && NST == 3 && nk > 1) issue(1, 1);
+        issue(0, 0);
+        if (NST == 3 && nk > 1) issue(1, 1);
         int s = 0;  // stage of tile kt
         for (int kt = 0; kt < nk; ++kt) {
             if (NST == 3 && kt + 1 < nk) __builtin_amdgcn_s_waitcnt(kWaitTile);  // tile kt+1 stays in flight
             else __builtin_amdgcn_s_waitcnt(kWaitAll);
             __builtin_amdgcn_s_barrier();
-            if (kDma && kt + NST - 1 < nk) {
+            if (kt + NST - 1 < nk) {
                 int sn = s + NST - 1;
                 if (sn >= NST) sn -= NST;
                 issue(kt + NST - 1, sn);
             }
-            if (kMath) compute_pf(s);
+            compute_pf(s);
             if (++s == NST) s = 0;
         }
     }
@@ -749,11 +746,9 @@ struct HaloArgs {
 // LDS-DMA traffic of the BM = 128 form - halve; the halo is double-buffered and the
 // next chunk's halo is DMA'd in pieces under the current chunk's first eight k-tiles
 // (the BM = 128 form relies on its co-resident second workgroup to hide that load).
-template <int BM, int BN, int DIAG, int NB>
+template <int BM, int BN, int NB>
 __global__ __launch_bounds__(BM == 256 ? 512 : 256) void k_conv_halo(ConvArgs a, HaloArgs h) {
     constexpr int BK = 64;  // NB: stages of the weight (B) ring, 2 or 3
-    // DIAG (timing diagnostics, outputs meaningless): 5 = no DMA, 6 = no MFMA/LDS reads
-    constexpr bool kDma = DIAG != 5, kMath = DIAG != 6;
     constexpr bool kHB2 = BM == 256;  // double-buffered halo, prefetched in pieces
     constexpr int NW = BM == 256 ? 8 : 4;  // waves: (NW/2) x 2, each a 64x64 sub-tile
     constexpr int NT_ = NW * 64;           // threads
@@ -924,9 +919,9 @@ __global__ __launch_bounds__(BM == 256 ? 512 : 256) void k_conv_halo(ConvArgs a,
     };
 
     constexpr int kWaitAll = (7 << 4) | (15 << 8);  // s_waitcnt vmcnt(0)
-    if (kDma) issue_halo(kt0 / 9);
-    if (kDma) issue_b(0, 0);
-    if (kDma && NB == 3 && nk > 1) issue_b(1, 1);
+    issue_halo(kt0 / 9);
+    issue_b(0, 0);
+    if (NB == 3 && nk > 1) issue_b(1, 1);
     constexpr int kWaitB = (BR & 15) | (7 << 4) | (15 << 8);  // vmcnt(BR): the newest B stage stays in flight
     int sb = 0;  // B stage of k-tile kt
     for (int kt = 0; kt < nk; ++kt) {
@@ -935,7 +930,7 @@ __global__ __launch_bounds__(BM == 256 ? 512 : 256) void k_conv_halo(ConvArgs a,
         if (NB == 3 && kt + 1 < nk) __builtin_amdgcn_s_waitcnt(kWaitB);
         else __builtin_amdgcn_s_waitcnt(kWaitAll);
         __builtin_amdgcn_s_barrier();
-        if (!kHB2 && kDma && kt > 0 && tp == 0) {  // next channel chunk: every wave is done with the old halo
+        if (!kHB2 && kt > 0 && tp == 0) {  // next channel chunk: every wave is done with the old halo
             issue_halo(k / 9);
             __builtin_amdgcn_s_waitcnt(kWaitAll);
             __builtin_amdgcn_s_barrier();
@@ -943,20 +938,20 @@ __global__ __launch_bounds__(BM == 256 ? 512 : 256) void k_conv_halo(ConvArgs a,
         // kHB2: the next chunk's halo goes to the other buffer (last read by the previous
         // chunk, whose k-tiles every wave has passed at this barrier), issued before this
         // k-tile's B stage so the counted B waits stay valid, landed by the chunk's first wait
-        if (kHB2 && kDma && kt - tp + 9 < nk) {
+        if (kHB2 && kt - tp + 9 < nk) {
             // pieces [lo, hi): a split that starts mid-chunk issues the pieces it skipped
             const int lo = kt == 0 ? 0 : tp, hi = tp < 8 ? tp + 1 : 8;
             const int cn = k / 9 + 1;
             if (lo < hi) issue_halo_part(cn, cn & 1, lo * nIp, min(hi * nIp, nI));
         }
-        if (kDma && kt + NB - 1 < nk) {
+        if (kt + NB - 1 < nk) {
             int sn = sb + NB - 1;
             if (sn >= NB) sn -= NB;
             issue_b(kt + NB - 1, sn);
         }
         const int ti = tp / 3, tj = tp - ti * 3;
         const int dh = (int)((pk_dh >> (4 * ti)) & 15u) - 8, dw = (int)((pk_dw >> (4 * tj)) & 15u) - 8;
-        if (kMath) compute(sb, dh * W2 + dw, kHB2 ? ((k / 9) & 1) * HB : 0);
+        compute(sb, dh * W2 + dw, kHB2 ? ((k / 9) & 1) * HB : 0);
         if (++sb == NB) sb = 0;
     }
 
@@ -1043,19 +1038,11 @@ __global__ __launch_bounds__(BM == 256 ? 512 : 256) void k_conv_halo(ConvArgs a,
 // channels, 4 waves of 64x64 (v_mfma_f32_32x32x16_bf16), two workgroups per CU.
 constexpr int kH9MaxQ = 12;  // halo DMA instructions per wave (nI <= 48)
 
-// NB: weight-ring stages (NB - 2 stay in flight across a k-tile); DIAG (timing
-// diagnostics, outputs meaningless): 1 = no weight DMA in the k-loop, 2 = no MFMAs /
-// fragment reads, 3 = no barrier in the k-loop, 4 = no halo reload.
-// WR: how the operands reach LDS.  0: LDS-DMA (global_load_lds) for the weights and the
-// halo.  1: the weights register-staged - global_load_dwordx4 one k-tile ahead into VGPRs,
-// ds_write_b128 into the ring stage the previous k-tile freed - because an LDS-DMA piece
-// costs its wave ~60-185 issue cycles among MFMAs (MI355X_MICROARCH.md price table) where a
-// load + ds_write_b128 costs ~20; the halo stays LDS-DMA, reloaded at each chunk start.
-// 2: as 1, and the next chunk's halo is prefetched into VGPRs at the chunk start and
-// written to LDS at the next one, so no chunk start waits for a halo load.
-// 3: LDS-DMA as 0, with the next k-tile's weight pieces issued one after each k-slice's
-// MFMAs instead of back to back before them.
-template <int BN, int NB, int DIAG = 0, int WR = 0>
+// NB: weight-ring stages (NB - 2 stay in flight across a k-tile).  Weights and halo both by
+// LDS-DMA.  Measured and dropped (r03-r04): register-staged weights, a register prefetch of
+// the next chunk's halo, weight pieces spread between the k-slices' MFMAs (0.05-0.07 ms/step
+// slower or neutral).
+template <int BN, int NB>
 __global__ __launch_bounds__(256, 2) void k_conv_h9(ConvArgs a, HaloArgs h) {
     constexpr int BM = 128, MT = 2, NT = BN / 64, NW = 4;
     static_assert(NB >= 2 && NB <= 8, "ring depth");
@@ -1195,9 +1182,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_h9(ConvArgs a, HaloArgs h) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    // piece(ks) runs after k-slice ks's MFMAs (WR 3: the next k-tile's weight DMA pieces
-    // spread between the MFMAs instead of issued back to back before them)
-    auto compute = [&](int tp, int st, auto&& piece) {
+    auto compute = [&](int tp, int st) {
         bf16x8 af[2][MT], bfr[2][NT];
 #pragma unroll
         for (int i = 0; i < MT; ++i) af[0][i] = *reinterpret_cast<const bf16x8*>(lds + aad[tp][i]);
@@ -1219,25 +1204,21 @@ __global__ __launch_bounds__(256, 2) void k_conv_h9(ConvArgs a, HaloArgs h) {
 #pragma unroll
                 for (int j = 0; j < NT; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[c][j], af[c][i], acc[i][j], 0, 0, 0);
-            piece(ks);
         }
         constexpr int NR = MT + NT, NM = MT * NT;
-        if constexpr (WR != 3) {
-            // slice ks + 1's fragment reads are issued BEFORE slice ks's MFMAs (the compiler's
-            // counted lgkmcnt then waits for slice ks's reads only, slice ks + 1's stay in
-            // flight under the MFMAs).  The read/MFMA interleave this replaces issued each
-            // slice's last read after its MFMAs, into a register an MFMA had just released,
-            // and waited lgkmcnt(0) on it: one exposed LDS round trip per k-slice.
-            __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+        // slice ks + 1's fragment reads are issued BEFORE slice ks's MFMAs (the compiler's
+        // counted lgkmcnt then waits for slice ks's reads only, slice ks + 1's stay in
+        // flight under the MFMAs).  The read/MFMA interleave this replaces issued each
+        // slice's last read after its MFMAs, into a register an MFMA had just released,
+        // and waited lgkmcnt(0) on it: one exposed LDS round trip per k-slice.
+        __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
 #pragma unroll
-            for (int ks = 0; ks < 3; ++ks) {
-                __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
-            }
+        for (int ks = 0; ks < 3; ++ks) {
+            __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
             __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
         }
+        __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
     };
-    auto none = [](int) {};
 
     // vmcnt(n): all but the wave's n newest vector-memory operations done
     auto wait_vm = [](int n) {
@@ -1259,90 +1240,6 @@ __global__ __launch_bounds__(256, 2) void k_conv_h9(ConvArgs a, HaloArgs h) {
     };
     static_assert((NB - 2) * BR <= 12, "counted wait range");
     const int nkt = (c1 - c0) * 9;
-    if constexpr (WR == 1 || WR == 2) {
-        // register-staged weights (and, WR 2, halo): see the template comment
-        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));  // (a native vector: SROA-able)
-        u32x4 wreg[BR];
-        auto gload_b = [&](int cc, int tp) __attribute__((always_inline)) {
-            const int off = twc[tp] + (cc << 6);
-#pragma unroll
-            for (int j = 0; j < BR; ++j) wreg[j] = *reinterpret_cast<const u32x4*>(b_src[j] + off);
-        };
-        auto swrite_b = [&](int st) __attribute__((always_inline)) {
-#pragma unroll
-            for (int j = 0; j < BR; ++j)
-                *reinterpret_cast<u32x4*>(lds + HB + st * SB + (wave * BR + j) * 1024 + lane * 16) = wreg[j];
-        };
-        constexpr int HQ = WR == 2 ? kH9MaxQ : 1;
-        u32x4 hreg[HQ];
-        auto gload_halo = [&](int cc) __attribute__((always_inline)) {
-            const int cbase = cc << 6;
-#pragma unroll
-            for (int q = 0; q < HQ; ++q)
-                if (q < nq)
-                    hreg[q] = hsrc[q] >= 0 ? *reinterpret_cast<const u32x4*>(gin + hsrc[q] + cbase)
-                                           : u32x4{0u, 0u, 0u, 0u};
-        };
-        auto swrite_halo = [&]() __attribute__((always_inline)) {
-#pragma unroll
-            for (int q = 0; q < HQ; ++q)
-                if (q < nq) *reinterpret_cast<u32x4*>(lds + (wave + NW * q) * 1024 + lane * 16) = hreg[q];
-        };
-        // LDS stores drained, then the barrier; the memory clobber keeps the compiler from
-        // moving LDS accesses across it (the loads in flight into VGPRs stay in flight: the
-        // compiler waits for them where their registers are used)
-        auto bar = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
-        // prologue: the first chunk's halo and k-tiles 0 .. NB-2 in LDS, k-tile NB-1 in flight
-        if constexpr (WR == 2) {
-            gload_halo(c0);
-            swrite_halo();
-        } else {
-            issue_halo(c0);
-        }
-#pragma unroll
-        for (int k = 0; k < NB - 1; ++k) {
-            if (k < nkt) {
-                gload_b(c0 + k / 9, k % 9);
-                swrite_b(k);
-            }
-        }
-        if (NB - 1 < nkt) gload_b(c0 + (NB - 1) / 9, (NB - 1) % 9);
-        // a chunk-start iteration issues its next-k-tile loads, then (WR 2) the next chunk's
-        // halo loads; the compiler's counted waits let the halo loads stay in flight until
-        // the k-tile loads issued after them are consumed (two iterations later)
-        int sb = 0;
-        int kt = 0;
-        for (int cc = c0; cc < c1; ++cc) {
-            const bool pre = WR == 2 && cc + 1 < c1;  // this chunk prefetches the next one's halo
-#pragma clang loop unroll(full)
-            for (int tp = 0; tp < 9; ++tp, ++kt) {
-                if (WR == 1 && kt == 0) wait_vm(0);  // the prologue's halo DMA
-                bar();  // every wave's ds_writes of k-tile kt (and of the halo) are in LDS
-                if (tp == 0 && cc > c0) {  // every wave is done with the previous chunk's halo
-                    if constexpr (WR == 2) {
-                        swrite_halo();  // (the prefetch landed by tp 2 of the previous chunk)
-                    } else {
-                        issue_halo(cc);
-                        wait_vm(0);
-                    }
-                    bar();
-                }
-                compute(tp, sb, none);
-                if (kt + NB - 1 < nkt) {  // k-tile kt+NB-1 into the stage k-tile kt-1 freed
-                    int sn = sb + NB - 1;
-                    if (sn >= NB) sn -= NB;
-                    swrite_b(sn);
-                }
-                if (kt + NB < nkt) {
-                    if (tp + NB < 9) gload_b(cc, tp + NB);
-                    else gload_b(cc + 1, tp + NB - 9);
-                }
-                if constexpr (WR == 2)
-                    if (tp == 0 && pre) gload_halo(cc + 1);
-                if (++sb == NB) sb = 0;
-            }
-        }
-    } else {
     issue_halo(c0);
 #pragma unroll
     for (int k = 0; k < NB - 1; ++k)
@@ -1354,42 +1251,23 @@ __global__ __launch_bounds__(256, 2) void k_conv_h9(ConvArgs a, HaloArgs h) {
         for (int tp = 0; tp < 9; ++tp, ++kt) {
             // stages issued after k-tile kt: min(NB - 2, nkt - 1 - kt), left in flight
             const int ahead = min(NB - 2, nkt - 1 - kt);
-            if (DIAG == 1) wait_vm(0);
-            else wait_vm(ahead * BR);
-            if (DIAG != 3) __builtin_amdgcn_s_barrier();
-            if (DIAG != 4 && tp == 0 && cc > c0) {  // every wave is done with the previous chunk's halo
+            wait_vm(ahead * BR);
+            __builtin_amdgcn_s_barrier();
+            if (tp == 0 && cc > c0) {  // every wave is done with the previous chunk's halo
                 issue_halo(cc);
                 wait_vm(0);
                 __builtin_amdgcn_s_barrier();
             }
             int sn = sb + NB - 1;
             if (sn >= NB) sn -= NB;
-            const bool refill = DIAG != 1 && kt + NB - 1 < nkt;
-            if (WR != 3 && refill) {
+            if (kt + NB - 1 < nkt) {
                 if (tp + NB - 1 < 9) issue_b(cc, tp + NB - 1, sn);
                 else issue_b(cc + 1, tp + NB - 1 - 9, sn);
             }
-            // WR 3: piece j of the refill after k-slice j * 4 / BR's MFMAs
-            auto piece = [&](int ks) __attribute__((always_inline)) {
-                if constexpr (WR == 3) {
-                    if (refill && (ks * BR) % 4 == 0) {
-                        const int j = ks * BR / 4;
-                        const int ccn = tp + NB - 1 < 9 ? cc : cc + 1;
-                        const int tpn = tp + NB - 1 < 9 ? tp + NB - 1 : tp + NB - 1 - 9;
-                        const int off = twc[tpn] + (ccn << 6);
-#pragma unroll
-                        for (int r = 0; r < (BR >= 4 ? BR / 4 : 1); ++r)
-                            __builtin_amdgcn_global_load_lds(
-                                (gptr_t)(b_src[j + r] + off),
-                                (lptr_t)(lds + HB + sn * SB + (wave * BR + j + r) * 1024), 16, 0, 0);
-                    }
-                }
-            };
-            if (DIAG != 2) compute(tp, sb, piece);
+            compute(tp, sb);
             if (++sb == NB) sb = 0;
         }
     }
-    }  // WR
 
     if (a.splits > 1) {
         constexpr int NQ = MT * NT * 4;  // float4 groups of accumulators per lane
@@ -1476,7 +1354,7 @@ struct RwArgs {
 
 constexpr int kRwWeightBytes = 9 * 64 * 128;
 
-template <int DIAG>  // DIAG (timing diagnostics, outputs meaningless): 1 = no halo wait, 2 = no MFMA
+template <int Form = 0>  // one form (the template keeps the symbol of earlier profiles)
 __global__ __launch_bounds__(256) void k_conv_rw(ConvArgs a, RwArgs r) {
     extern __shared__ __attribute__((aligned(16))) uint4 smem[];
     char* lds = reinterpret_cast<char*>(smem);  // [weights][halo 0][halo 1]
@@ -1670,7 +1548,7 @@ __global__ __launch_bounds__(256) void k_conv_rw(ConvArgs a, RwArgs r) {
             }
             // the next tile's halo (issued before these stores) has landed; the stores may
             // still be in flight.  Then every wave is done with buffer bb and the LDS tile.
-            if (DIAG != 1) __builtin_amdgcn_s_waitcnt(kWaitStores4);
+            __builtin_amdgcn_s_waitcnt(kWaitStores4);
             lds_barrier();
             bb ^= 1;
             continue;
@@ -1712,7 +1590,7 @@ __global__ __launch_bounds__(256) void k_conv_rw(ConvArgs a, RwArgs r) {
         }
         // the next tile's halo (issued before these stores) has landed; the stores may
         // still be in flight.  Then every wave is done with buffer bb.
-        if (DIAG != 1) __builtin_amdgcn_s_waitcnt(kWaitStores);
+        __builtin_amdgcn_s_waitcnt(kWaitStores);
         lds_barrier();
         bb ^= 1;
     }
@@ -2007,8 +1885,6 @@ static int launch_igemm(ConvArgs& a, hipStream_t st) {
     if (a.C >= 64 && grid && lean_path()) {
         const int pipe = conv_pipe();
         if (pipe == 3) launch_ut<BM, BN, 3>(a, tiles * a.splits, st);
-        else if (pipe == 5) launch_ut<BM, BN, 5>(a, tiles * a.splits, st);
-        else if (pipe == 6) launch_ut<BM, BN, 6>(a, tiles * a.splits, st);
         else if (pipe == 2) launch_ut<BM, BN, 2>(a, tiles * a.splits, st);
         else launch_ut<BM, BN, 0>(a, tiles * a.splits, st);
     } else if (a.splits > 1) {
@@ -2164,7 +2040,7 @@ static int halo_bytes(const ConvArgs& a, int BM = 128) {
     return (maxpix + 7) / 8 * 1024;
 }
 
-template <int BN, int DIAG, int NB, int BM = 128>
+template <int BN, int NB, int BM = 128>
 static int launch_halo_v(ConvArgs& a, int hb, hipStream_t st) {
     ConvCls& c = a.cls[0];
     const int M = a.N * c.P * c.Q;
@@ -2179,7 +2055,7 @@ static int launch_halo_v(ConvArgs& a, int hb, hipStream_t st) {
     const size_t lds = (size_t)hb * (BM == 256 ? 2 : 1) + NB * (size_t)BN * 128;
     static size_t attr = 0;  // largest dynamic LDS granted so far (idempotent, safe to race)
     if (lds > attr) {
-        const hipError_t e = hipFuncSetAttribute((const void*)k_conv_halo<BM, BN, DIAG, NB>,
+        const hipError_t e = hipFuncSetAttribute((const void*)k_conv_halo<BM, BN, NB>,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) {
             set_error("k_conv_halo: %zu B of LDS refused (%s)", lds, hipGetErrorString(e));
@@ -2187,7 +2063,7 @@ static int launch_halo_v(ConvArgs& a, int hb, hipStream_t st) {
         }
         attr = lds;
     }
-    k_conv_halo<BM, BN, DIAG, NB><<<a.tiles_total * a.splits, BM == 256 ? 512 : 256, lds, st>>>(a, h);
+    k_conv_halo<BM, BN, NB><<<a.tiles_total * a.splits, BM == 256 ? 512 : 256, lds, st>>>(a, h);
     return check_launch("k_conv_halo");
 }
 
@@ -2299,13 +2175,6 @@ static int g_conv_h9 = [] {
     const char* e = getenv("GM_CONV_H9");  // 0: the halo shapes take k_conv_halo (A/B)
     return e ? atoi(e) : 1;
 }();
-// k_conv_h9's operand staging (its WR template argument): 0 LDS-DMA, 1 register-staged
-// weights, 2 register-staged weights + halo prefetch (GM_CONV_H9_WR at load)
-static int g_conv_h9_wr = [] {
-    const char* e = getenv("GM_CONV_H9_WR");
-    return e ? atoi(e) : 0;
-}();
-
 // k_conv_h9 when eligible: Nout a multiple of BN, at most 48 halo DMA instructions, the
 // halo + 3 weight stages within half the CU's LDS (two workgroups per CU), splits over
 // whole channel chunks.  Returns 0 when not taken.
@@ -2325,41 +2194,15 @@ static int launch_h9(ConvArgs& a, int hb, hipStream_t st) {
     const size_t lds = (size_t)hb + NB * (size_t)BN * 128;
     static size_t attr = 0;
     if (lds > attr) {
-        hipError_t e = hipSuccess;
-        for (const void* k : {(const void*)k_conv_h9<BN, NB, 0>, (const void*)k_conv_h9<BN, NB, 1>,
-                              (const void*)k_conv_h9<BN, NB, 2>, (const void*)k_conv_h9<BN, NB, 3>,
-                              (const void*)k_conv_h9<BN, NB, 4>, (const void*)k_conv_h9<BN, NB, 0, 1>,
-                              (const void*)k_conv_h9<BN, NB, 0, 2>, (const void*)k_conv_h9<BN, NB, 0, 3>})
-            if (e == hipSuccess) e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        const hipError_t e =
+            hipFuncSetAttribute((const void*)k_conv_h9<BN, NB>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) {
             set_error("k_conv_h9: %zu B of LDS refused (%s)", lds, hipGetErrorString(e));
             return GM_E_UNSUP;
         }
         attr = lds;
     }
-    const dim3 grid(a.tiles_total * a.splits);
-    if (g_conv_h9_wr == 1) {
-        k_conv_h9<BN, NB, 0, 1><<<grid, 256, lds, st>>>(a, h);
-        const int rc = check_launch("k_conv_h9<wr1>");
-        return rc == GM_OK ? 1 : rc;
-    }
-    if (g_conv_h9_wr == 2) {
-        k_conv_h9<BN, NB, 0, 2><<<grid, 256, lds, st>>>(a, h);
-        const int rc = check_launch("k_conv_h9<wr2>");
-        return rc == GM_OK ? 1 : rc;
-    }
-    if (g_conv_h9_wr == 3) {
-        k_conv_h9<BN, NB, 0, 3><<<grid, 256, lds, st>>>(a, h);
-        const int rc = check_launch("k_conv_h9<wr3>");
-        return rc == GM_OK ? 1 : rc;
-    }
-    switch (conv_pipe()) {  // 5..8: timing diagnostics (outputs meaningless)
-    case 5: k_conv_h9<BN, NB, 1><<<grid, 256, lds, st>>>(a, h); break;
-    case 6: k_conv_h9<BN, NB, 2><<<grid, 256, lds, st>>>(a, h); break;
-    case 7: k_conv_h9<BN, NB, 3><<<grid, 256, lds, st>>>(a, h); break;
-    case 8: k_conv_h9<BN, NB, 4><<<grid, 256, lds, st>>>(a, h); break;
-    default: k_conv_h9<BN, NB, 0><<<grid, 256, lds, st>>>(a, h);
-    }
+    k_conv_h9<BN, NB><<<dim3(a.tiles_total * a.splits), 256, lds, st>>>(a, h);
     const int rc = check_launch("k_conv_h9");
     return rc == GM_OK ? 1 : rc;
 }
@@ -2400,16 +2243,14 @@ static int try_h9(ConvArgs& a, int hb, hipStream_t st) {
 template <int BN>
 static int launch_halo(ConvArgs& a, int hb, hipStream_t st) {
     const int p = conv_pipe();
-    if (p == 0 || p == 3 || p >= 5) {
+    if (p == 0 || p == 3) {
         const int r = try_h9<BN>(a, hb, st);
         if (r == 1) return GM_OK;
         if (r != 0) return r;
     }
-    if (p == 5) return launch_halo_v<BN, 5, 2>(a, hb, st);
-    if (p == 6) return launch_halo_v<BN, 6, 2>(a, hb, st);
     // a third weight stage when two workgroups per CU still fit (or when asked: pipe 3)
-    if (p == 3 || hb + 3 * BN * 128 <= 80 * 1024 - 256) return launch_halo_v<BN, 0, 3>(a, hb, st);
-    return launch_halo_v<BN, 0, 2>(a, hb, st);
+    if (p == 3 || hb + 3 * BN * 128 <= 80 * 1024 - 256) return launch_halo_v<BN, 3>(a, hb, st);
+    return launch_halo_v<BN, 2>(a, hb, st);
 }
 
 // 256-pixel halo tiles (one workgroup per CU, BN = 128): eligible when the double
@@ -2466,11 +2307,7 @@ static int try_halo256(ConvArgs& a, hipStream_t st, void* ws, size_t ws_bytes) {
         a.flags = static_cast<unsigned*>(ws);
         a.ws = reinterpret_cast<float*>(static_cast<char*>(ws) + splitk_flag_bytes(tiles));
     }
-    const int p = conv_pipe();
-    int rc;
-    if (p == 5) rc = launch_halo_v<128, 5, 3, 256>(a, hb, st);
-    else if (p == 6) rc = launch_halo_v<128, 6, 3, 256>(a, hb, st);
-    else rc = launch_halo_v<128, 0, 3, 256>(a, hb, st);
+    const int rc = launch_halo_v<128, 3, 256>(a, hb, st);
     return rc == GM_OK ? 1 : rc;
 }
 
@@ -2719,12 +2556,6 @@ extern "C" int gm_conv_set_h9(int on) {
     return GM_OK;
 }
 
-extern "C" int gm_conv_set_h9_staging(int wr) {
-    GM_REQUIRE(wr >= 0 && wr <= 3, "gm_conv_set_h9_staging: 0 (LDS-DMA), 1 (register weights), 2 (+ halo "
-                                   "prefetch), 3 (LDS-DMA weight pieces between the MFMAs)");
-    g_conv_h9_wr = wr;
-    return GM_OK;
-}
 
 extern "C" int gm_conv_set_halo(int on) {
     g_conv_halo = on < 0 ? 0 : on > 2 ? 2 : on;
@@ -2749,8 +2580,7 @@ extern "C" int gm_conv_set_1x1_gemm(int on) {
 }
 
 extern "C" int gm_conv_set_pipe(int pipe) {
-    GM_REQUIRE(pipe == 0 || pipe == 2 || pipe == 3 || (pipe >= 5 && pipe <= 8),
-               "gm_conv_set_pipe: 0, 2, 3 (5..8: timing diagnostics)");
+    GM_REQUIRE(pipe == 0 || pipe == 2 || pipe == 3, "gm_conv_set_pipe: 0, 2 or 3");
     g_conv_pipe = pipe;
     return GM_OK;
 }

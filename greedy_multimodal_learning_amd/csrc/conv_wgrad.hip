@@ -1240,8 +1240,13 @@ static int g_ring_form = [] {
     return e ? atoi(e) : 0;
 }();
 static int ring_bk() { return g_ring_form == 1 ? 32 : 64; }
-// A/B knobs (GM_WGRAD_RING_WGS: workgroups the plan aims at, default one per CU;
-// GM_WGRAD_RING_MINK: the smallest K served, default 128)
+// GM_WGRAD_RING_WGS: workgroups the plan aims at.  Default: HALF the CUs.  The ring runs on the
+// weight-gradient stream beside the main chain's input-gradient convolutions and BatchNorms, and
+// a workgroup holds its CU's LDS (156 KB): one per CU starved the main chain (C2 step 3.94 ms
+// against 3.85 without the ring), half the CUs left the other half to it (3.75 ms; 64 / 96 /
+// 160 / 192 / 224: 3.77 / 3.77 / 3.80 / 3.80 / 3.80 ms, r05 interleaved A/B).  Alone a launch
+// then takes longer (conv family 0.218 vs 0.228 isolated).  GM_WGRAD_RING_MINK: the smallest
+// K served (default 128).
 static int g_ring_wgs = [] {
     const char* e = getenv("GM_WGRAD_RING_WGS");
     return e ? atoi(e) : 0;
@@ -1268,7 +1273,7 @@ static bool ring_plan(const gm_conv_desc_hw* d, int G, RingPlan& r) {
     const int tiles = r.tiles_k * r.tiles_n * G;
     const int bk = ring_bk();
     const int steps = (r.M + bk - 1) / bk;
-    int want = (g_ring_wgs > 0 ? g_ring_wgs : device_cus_w()) / tiles;
+    int want = (g_ring_wgs > 0 ? g_ring_wgs : device_cus_w() / 2) / tiles;
     if (want > steps / (512 / bk)) want = steps / (512 / bk);  // >= 512 pixels per split
     if (want < 1) want = 1;
     r.sps = (steps + want - 1) / want;

@@ -352,9 +352,7 @@ int gm_conv2d_dgrad_bf16(const gm_conv_desc* d, const void* dy, const void* wt, 
 size_t gm_conv2d_splitk_ws_bytes(const gm_conv_desc* d, int dgrad);
 /* Main-loop form of the implicit-GEMM kernel (process-wide; default GM_CONV_PIPE or 0):
  * 0 = two LDS stages drained at every barrier; 2 / 3 = a 2- / 3-stage LDS ring with one
- * barrier per k-tile and counted DMA waits (3: the next tile's DMA stays in flight);
- * 5 / 6 = timing diagnostics only (the 2-stage loop without its DMA / without its math;
- * outputs meaningless). */
+ * barrier per k-tile and counted DMA waits (3: the next tile's DMA stays in flight). */
 int gm_conv_set_pipe(int pipe);
 /* 3x3 / stride-1 / pad-1 convolutions (forward and input gradient, C % 64 == 0) stage
  * the input once per 64-channel chunk as a halo instead of once per tap (default on;
@@ -363,10 +361,6 @@ int gm_conv_set_halo(int on);
 /* The halo kernel with its nine taps unrolled (k_conv_h9; default on, GM_CONV_H9=0 at
  * load or gm_conv_set_h9(0) selects the run-time-decoded k_conv_halo, an A/B switch). */
 int gm_conv_set_h9(int on);
-/* k_conv_h9's operand staging: 0 = LDS-DMA (global_load_lds) weights and halo; 1 = weights
- * register-staged (global_load_dwordx4 one k-tile ahead + ds_write_b128); 2 = as 1, and the
- * next channel chunk's halo prefetched into registers (GM_CONV_H9_WR at load; A/B switch) */
-int gm_conv_set_h9_staging(int wr);
 /* Split-K target: workgroups wanted from splitting K of 128x128-tile convolutions whose
  * tiles alone do not fill the device (default 384, GM_CONV_SPLITK at load; 0 = never). */
 int gm_conv_set_splitk(int target);

@@ -214,7 +214,8 @@ def test_model_stacked_vs_per_view(dev, kind):
         e_pv = float((outs[False][i].cpu() - ref).abs().max()) / scale
         assert e_st <= max(3e-2, 2 * e_pv), (f"logits[{i}]", e_st, e_pv)
     worst = []
-    tot = [0.0, 0.0, 0.0]  # all parameters as one vector: stacked / per-view error^2, fp32 norm^2
+    tot = [0.0] * 5  # all parameters as one vector: stacked / per-view error^2, fp32 norm^2, direct
+    direct = []
     for (n, pa), (_, pb), (_, pc) in zip(a.named_parameters(), b.named_parameters(), c.named_parameters()):
         ga, gb, gc = pa.grad.double(), pb.grad.double(), pc.grad.double()
         den = gc.norm() + 1e-30
@@ -232,8 +233,25 @@ def test_model_stacked_vs_per_view(dev, kind):
         tot[0] += float((ga - gc).pow(2).sum())
         tot[1] += float((gb - gc).pow(2).sum())
         tot[2] += float(gc.pow(2).sum())
+        tot[3] += float((ga - gb).pow(2).sum())
+        tot[4] += float(gb.pow(2).sum())
+        # directly, bf16 against bf16: both paths run the same per-view
+        # kernels, so they share most of their rounding - they must agree far better than
+        # either agrees with fp32, also where the bf16 floor hides the fp32 comparison
+        direct.append((float((ga - gb).norm() / (gb.norm() + 1e-30)), eb, n))
     e_all, e_all_pv = (tot[0] / tot[2]) ** 0.5, (tot[1] / tot[2]) ** 0.5
+    e_direct = (tot[3] / tot[4]) ** 0.5
     assert e_all < max(2 * e_all_pv, 1e-2), ("all parameters", e_all, e_all_pv)
+    direct.sort(reverse=True)
+    print(f"stacked vs per-view directly: whole gradient {e_direct:.3e}; worst "
+          + ", ".join(f"{n} {d:.2e} (per-view vs fp32 {eb:.2e})" for d, eb, n in direct[:3]))
+    # (ResNet-50 excluded: at this batch its bf16 gradient carries no signal - against fp32 it
+    # is off by 1.28 in either path, and the two bf16 runs differ from each other by 0.99 at
+    # 64^2 and 1.04 at 128^2, r05; the ResNet-18 paths agree to 3e-4 / 1e-3)
+    if not kind.endswith("r50"):
+        assert e_direct < max(0.25 * e_all_pv, 1e-2), ("stacked vs per-view, whole gradient", e_direct, e_all_pv)
+        for d, eb, n in direct:
+            assert d < max(0.5 * eb, 5e-2), (n, d, eb)
     worst.sort(reverse=True)
     print(f"whole gradient vs fp32: stacked {e_all:.3e}, per-view {e_all_pv:.3e}")
     print("stacked vs per-view gradient error vs fp32 (worst 5):",

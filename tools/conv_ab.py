@@ -38,16 +38,14 @@ def main():
     B = a.batch
     pipes = a.pipes.replace("+", ",").split(",")
 
-    def select(p):  # "h", "h5", "h6": the halo kernel (+ diagnostics); "H...": 256-pixel halo tiles;
+    def select(p):  # "h": the halo kernel; "H...": 256-pixel halo tiles;
         # "o": the halo kernel with run-time tap decode (k_conv_halo) instead of k_conv_h9;
         # "fBN.NB": k_conv_h9 forced to BN-channel tiles and an NB-stage weight ring
         # "s<n>": split-K target n (0: never split), auto form otherwise
         L.check(lib.gm_conv_set_splitk(int(p[1:]) if p[0] == "s" else 384), "set_splitk")
-        # "r<n>": k_conv_h9 with operand staging n (gm_conv_set_h9_staging)
-        L.check(lib.gm_conv_set_h9_staging(int(p[1:]) if p[0] == "r" else 0), "set_h9_staging")
         # "g<n>": weight-gradient operand staging n (gm_conv_set_wgrad_staging)
         L.check(lib.gm_conv_set_wgrad_staging(int(p[1:]) if p[0] == "g" else 0), "set_wgrad_staging")
-        if p[0] in ("r", "g"):
+        if p[0] == "g":
             p = "h"
         if p[0] == "s":
             p = "h"
