@@ -132,12 +132,9 @@ class GroupNorms:
         self._table = None
         self._scratch = None
         self._out = None
-        self.wprep = None  # a conv.WeightPrep whose bf16 copies the SGD pass writes (set by the engine)
 
     def _build(self):
-        wp = self.wprep
-        key = tuple((p.data_ptr(), 0 if p.grad is None else p.grad.data_ptr()) for p in self.params) \
-            + ((id(wp), wp.table_key()) if wp is not None else ())
+        key = tuple((p.data_ptr(), 0 if p.grad is None else p.grad.data_ptr()) for p in self.params)
         if key == self._key:
             return
         for p in self.params:
@@ -149,11 +146,9 @@ class GroupNorms:
         n = len(self.params)
         tab = (L.Tensor * n)()
         off = 0
-        fused = self.wprep.fused_index() if self.wprep is not None else {}
         for i, p in enumerate(self.params):
-            # pad = 1 + the gm_wprep entry whose bf16 copies this weight's update also writes
             tab[i] = L.Tensor(p.data_ptr(), 0 if p.grad is None else p.grad.data_ptr(),
-                              p.numel(), off, self.masks[i], fused.get(p.data_ptr(), -1) + 1)
+                              p.numel(), off, self.masks[i], 0)
             off += p.numel()
         host = torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8)
         self._table = host.to(self.device)
@@ -169,14 +164,10 @@ class GroupNorms:
             raise L.GreedyMMLError("group norms run on HIP devices only (no CPU fallback)")
         self._build()
         out = torch.empty(2 * self.ngroups, dtype=torch.float64, device=self.device)
-        wp = self.wprep if lr != 0.0 else None
-        L.check(L.load().gm_group_sumsq_wprep(self._table.data_ptr(), len(self.params), self.total,
-                                              self.ngroups, float(grad_scale), float(lr),
-                                              wp.table.data_ptr() if wp is not None else None, out.data_ptr(),
-                                              self._scratch.data_ptr(), self._scratch.numel(),
-                                              L.stream_of(self.device)), "gm_group_sumsq")
-        if wp is not None:
-            wp.written_by_sgd()
+        L.check(L.load().gm_group_sumsq(self._table.data_ptr(), len(self.params), self.total,
+                                        self.ngroups, float(grad_scale), float(lr), out.data_ptr(),
+                                        self._scratch.data_ptr(), self._scratch.numel(),
+                                        L.stream_of(self.device)), "gm_group_sumsq")
         return out
 
 

@@ -305,10 +305,6 @@ class WeightPrep:
         self.tiles = tiles
         self.table = None
         self._ptrs = None
-        # the copies are fresh when the last thing that changed the fp32 weights was the fused
-        # norms+SGD pass, which writes them too (gm_group_sumsq_wprep); every in-place torch op on a
-        # parameter bumps its version counter, so a weight changed outside the step is caught
-        self._fresh_version = None
 
     def _refresh_table(self):
         """(Re)build the device table when parameter storage moved (FlatParams)."""
@@ -324,37 +320,8 @@ class WeightPrep:
         self.table = host.to(self.buf.device)
         self._ptrs = ptrs
 
-    def _version(self):
-        return tuple(w._version for (w, _, _) in self.copies)
-
-    def table_key(self):
-        self._refresh_table()
-        return self._ptrs
-
-    def fused_index(self):
-        """{weight data_ptr: gm_wprep index} of the weights the SGD pass can prepare itself:
-        KRSC fp32 with K and C multiples of 64, no channel padding, a transposed copy."""
-        self._refresh_table()
-        out = {}
-        for i, ((w, wb, wt), it) in enumerate(zip(self.copies, self.items)):
-            if wt is not None and it.K % 64 == 0 and it.C % 64 == 0 and it.C == it.Cp:
-                out[w.data_ptr()] = i
-        return out
-
-    def written_by_sgd(self):
-        """The fused SGD pass was enqueued: it leaves every fused weight's copies current (the
-        others are re-made by run() before each forward)."""
-        self._fresh_version = self._version()
-        self._all_fused = len(self.fused_index()) == len(self.copies)
-
-    def fresh(self):
-        return (self._fresh_version is not None and getattr(self, "_all_fused", False)
-                and self._fresh_version == self._version())
-
     def run(self):
-        """Make the bf16 copies from the fp32 weights (one launch) unless the last fused
-        norms+SGD pass already did."""
-        if not self.copies or self.fresh():
+        if not self.copies:
             return
         self._refresh_table()
         L.check(L.load().gm_conv_weight_prep_multi_bf16(self.table.data_ptr(), len(self.items), self.tiles,

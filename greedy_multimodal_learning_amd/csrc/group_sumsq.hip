@@ -105,74 +105,11 @@ __device__ __forceinline__ void stream_segment(const gm_tensor& T, long long tb,
     }
 }
 
-// A conv weight whose bf16 copies ride along with its SGD update (gm_group_sumsq_wprep, table
-// entry pad = 1 + its gm_wprep index; fp32 KRSC [K][RS][C] with K, C multiples of 64 and Cp == C):
-// the tensor is walked in 64(k) x 64(c) tiles of one tap instead of linearly, so besides the
-// update the workgroup writes the bf16 KRSC copy along c and, through an LDS transpose, the
-// channel-transposed [C][RS][K] copy along k - what k_wprep_multi did in its own pass at the start
-// of the next step (read 4 + write 4 B per weight there; 4 B more here, no re-read).  Tile j
-// (order: k-tile, tap, c-tile) belongs to the chunk holding its anchor element j * 4096, so the
-// chunks still partition the work; sums in a fixed order per chunk (deterministic).
-__device__ __forceinline__ void stream_tiles(const gm_tensor& T, const gm_wprep& E, long long tb, long long te,
-                                             float gscale, float lr, float& sw, float& sg,
-                                             uint16_t (*tile)[72]) {
-    float* __restrict__ p = T.param;
-    const float* __restrict__ gr = T.grad;
-    uint16_t* __restrict__ wb = static_cast<uint16_t*>(E.wb);
-    uint16_t* __restrict__ wt = static_cast<uint16_t*>(E.wt);
-    const int K = E.K, RS = E.RS, C = E.C, tc = C >> 6;
-    const int t = threadIdx.x, kk = t >> 2, c16 = (t & 3) * 16;
-    for (long long j = (tb + 4095) >> 12; (j << 12) < te; ++j) {
-        const int ct = (int)(j % tc), r = (int)(j / tc), tap = r % RS, kt = r / RS;
-        const long long base = ((long long)(kt * 64 + kk) * RS + tap) * C + ct * 64 + c16;
-        float4 w[4], g[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            w[u] = reinterpret_cast<const float4*>(p + base)[u];
-            g[u] = reinterpret_cast<const float4*>(gr + base)[u];
-        }
-        uint32_t h[8];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            sw = fmaf(w[u].x, w[u].x, sw); sw = fmaf(w[u].y, w[u].y, sw);
-            sw = fmaf(w[u].z, w[u].z, sw); sw = fmaf(w[u].w, w[u].w, sw);
-            g[u].x *= gscale; g[u].y *= gscale; g[u].z *= gscale; g[u].w *= gscale;
-            sg = fmaf(g[u].x, g[u].x, sg); sg = fmaf(g[u].y, g[u].y, sg);
-            sg = fmaf(g[u].z, g[u].z, sg); sg = fmaf(g[u].w, g[u].w, sg);
-            const float4 n = make_float4(fmaf(-lr, g[u].x, w[u].x), fmaf(-lr, g[u].y, w[u].y),
-                                         fmaf(-lr, g[u].z, w[u].z), fmaf(-lr, g[u].w, w[u].w));
-            reinterpret_cast<float4*>(p + base)[u] = n;
-            h[2 * u] = pack_bf2(n.x, n.y);
-            h[2 * u + 1] = pack_bf2(n.z, n.w);
-        }
-        reinterpret_cast<uint4*>(wb + base)[0] = make_uint4(h[0], h[1], h[2], h[3]);
-        reinterpret_cast<uint4*>(wb + base)[1] = make_uint4(h[4], h[5], h[6], h[7]);
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            tile[kk][c16 + 2 * u] = (uint16_t)(h[u] & 0xffffu);
-            tile[kk][c16 + 2 * u + 1] = (uint16_t)(h[u] >> 16);
-        }
-        __syncthreads();
-        // transposed copy: thread t writes row c = ct * 64 + (t >> 2), k = kt * 64 + c16 .. + 15
-        const int cc = t >> 2;
-        uint32_t o[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-            o[u] = (uint32_t)tile[c16 + 2 * u][cc] | ((uint32_t)tile[c16 + 2 * u + 1][cc] << 16);
-        uint16_t* dst = wt + ((long long)(ct * 64 + cc) * RS + tap) * K + kt * 64 + c16;
-        reinterpret_cast<uint4*>(dst)[0] = make_uint4(o[0], o[1], o[2], o[3]);
-        reinterpret_cast<uint4*>(dst)[1] = make_uint4(o[4], o[5], o[6], o[7]);
-        __syncthreads();  // the next tile overwrites the LDS tile
-    }
-}
-
 template <bool SGD, int MG>
 __global__ __launch_bounds__(256) void k_group_sumsq(const gm_tensor* __restrict__ tab, int nt,
                                                      long long total, int ngroups, float gscale,
-                                                     float lr, long long chunk, double* __restrict__ rows,
-                                                     const gm_wprep* __restrict__ wp) {
+                                                     float lr, long long chunk, double* __restrict__ rows) {
     __shared__ double sred[4][2 * MG];
-    __shared__ uint16_t tile[64][72];
     const long long e0 = (long long)blockIdx.x * chunk;
     const long long e1 = min(total, e0 + chunk);
     double gw[MG], gg[MG];
@@ -185,8 +122,7 @@ __global__ __launch_bounds__(256) void k_group_sumsq(const gm_tensor* __restrict
         const long long tb = e - T.offset;                       // first local element
         const long long te = min(T.n, e1 - T.offset);            // end (exclusive)
         float sw = 0.f, sg = 0.f;
-        if (SGD && wp && T.pad && T.grad) stream_tiles(T, wp[T.pad - 1], tb, te, gscale, lr, sw, sg, tile);
-        else stream_segment<SGD>(T, tb, te, gscale, lr, sw, sg);
+        stream_segment<SGD>(T, tb, te, gscale, lr, sw, sg);
         const unsigned m = T.group_mask;
 #pragma unroll
         for (int g = 0; g < MG; ++g)
@@ -234,11 +170,9 @@ __device__ __forceinline__ void flush_run(double& aw, double& ag, unsigned mask,
 template <bool SGD>
 __global__ __launch_bounds__(256) void k_group_sumsq_runs(const gm_tensor* __restrict__ tab, int nt,
                                                           long long total, int ngroups, float gscale,
-                                                          float lr, long long chunk, double* __restrict__ rows,
-                                                          const gm_wprep* __restrict__ wp) {
+                                                          float lr, long long chunk, double* __restrict__ rows) {
     __shared__ double sred[4][2];
     __shared__ double acc[2 * kMaxGroups];
-    __shared__ uint16_t tile[64][72];
     if (threadIdx.x < 2 * kMaxGroups) acc[threadIdx.x] = 0.0;
     const long long e0 = (long long)blockIdx.x * chunk;
     const long long e1 = min(total, e0 + chunk);
@@ -255,8 +189,7 @@ __global__ __launch_bounds__(256) void k_group_sumsq_runs(const gm_tensor* __res
         const long long tb = e - T.offset;
         const long long te = min(T.n, e1 - T.offset);
         float sw = 0.f, sg = 0.f;
-        if (SGD && wp && T.pad && T.grad) stream_tiles(T, wp[T.pad - 1], tb, te, gscale, lr, sw, sg, tile);
-        else stream_segment<SGD>(T, tb, te, gscale, lr, sw, sg);
+        stream_segment<SGD>(T, tb, te, gscale, lr, sw, sg);
         aw += (double)sw;
         ag += (double)sg;
         e = T.offset + te;
@@ -320,9 +253,8 @@ extern "C" size_t gm_group_sumsq_scratch(long long total) {
     return (size_t)nb * 2 * kMaxGroups * sizeof(double);
 }
 
-extern "C" int gm_group_sumsq_wprep(const gm_tensor* table, int nt, long long total, int ngroups, float gscale,
-                                    float lr, const gm_wprep* wprep, double* out, void* scratch,
-                                    size_t scratch_bytes, void* stream) {
+extern "C" int gm_group_sumsq(const gm_tensor* table, int nt, long long total, int ngroups, float gscale,
+                              float lr, double* out, void* scratch, size_t scratch_bytes, void* stream) {
     GM_REQUIRE(table && nt >= 1 && total >= 1, "group_sumsq: empty tensor table");
     GM_REQUIRE(ngroups >= 1 && ngroups <= kMaxGroups, "group_sumsq: ngroups must be 1..%d", kMaxGroups);
     GM_REQUIRE(out, "group_sumsq: null output");
@@ -335,25 +267,17 @@ extern "C" int gm_group_sumsq_wprep(const gm_tensor* table, int nt, long long to
     double* rows = (double*)scratch;
     if (ngroups <= 8) {
         if (lr != 0.f)
-            k_group_sumsq<true, 8><<<(int)nb, 256, 0, st>>>(table, nt, total, ngroups, gscale, lr, chunk, rows, wprep);
+            k_group_sumsq<true, 8><<<(int)nb, 256, 0, st>>>(table, nt, total, ngroups, gscale, lr, chunk, rows);
         else
-            k_group_sumsq<false, 8><<<(int)nb, 256, 0, st>>>(table, nt, total, ngroups, gscale, lr, chunk, rows,
-                                                              nullptr);
+            k_group_sumsq<false, 8><<<(int)nb, 256, 0, st>>>(table, nt, total, ngroups, gscale, lr, chunk, rows);
     } else {  // N-branch gates (C5: 12 branches -> 24 groups)
         if (lr != 0.f)
-            k_group_sumsq_runs<true><<<(int)nb, 256, 0, st>>>(table, nt, total, ngroups, gscale, lr, chunk, rows,
-                                                               wprep);
+            k_group_sumsq_runs<true><<<(int)nb, 256, 0, st>>>(table, nt, total, ngroups, gscale, lr, chunk, rows);
         else
-            k_group_sumsq_runs<false><<<(int)nb, 256, 0, st>>>(table, nt, total, ngroups, gscale, lr, chunk, rows,
-                                                                nullptr);
+            k_group_sumsq_runs<false><<<(int)nb, 256, 0, st>>>(table, nt, total, ngroups, gscale, lr, chunk, rows);
     }
     int rc = check_launch("k_group_sumsq");
     if (rc) return rc;
     k_group_finalize<<<1, kFinT, 0, st>>>(rows, (int)nb, ngroups, out);
     return check_launch("k_group_finalize");
-}
-
-extern "C" int gm_group_sumsq(const gm_tensor* table, int nt, long long total, int ngroups, float gscale,
-                              float lr, double* out, void* scratch, size_t scratch_bytes, void* stream) {
-    return gm_group_sumsq_wprep(table, nt, total, ngroups, gscale, lr, nullptr, out, scratch, scratch_bytes, stream);
 }

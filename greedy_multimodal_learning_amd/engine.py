@@ -286,9 +286,6 @@ class BalancedStep:
         if self.device.type == "cuda" and channels_last and compute_dtype == torch.bfloat16:
             from .conv import WeightPrep
             self.wprep = WeightPrep(model)
-            # the fused norms+SGD pass writes the next step's bf16 weight copies itself
-            # (gm_group_sumsq_wprep): no separate prep pass per step
-            self.norms.wprep = self.wprep
         # graphs under data parallelism: the per-rank compute (zero_grad, forward, loss,
         # backward) is ONE hipGraph; the gradient all-reduce and the fused norms+SGD pass
         # run eagerly behind each replay (no collective inside a graph)
@@ -611,12 +608,7 @@ class BalancedStep:
                 return self(x, y)
             g, loss, sums, outs = entry
             want = gate is not None and hasattr(gate, "needs_bdr") and gate.needs_bdr()
-            wp = self.wprep
-            if wp is not None and not wp.fresh():
-                wp.run()  # the weights changed outside the step: re-make the copies the graph reads
             g.replay()
-            if wp is not None and sums is not None:
-                wp.written_by_sgd()  # the replayed norms+SGD pass wrote them
             if self.buckets is not None and not self.graph_collectives:
                 self.buckets.reduce_all()
                 sums = self.norms.sums(grad_scale=1.0 / self.world, lr=self.lr)

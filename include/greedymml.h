@@ -422,14 +422,6 @@ typedef struct gm_wprep {
 } gm_wprep;
 int gm_wprep_tiles(int K, int RS, int Cp);
 int gm_conv_weight_prep_multi_bf16(const gm_wprep* table, int n, int total_tiles, void* stream);
-/* gm_group_sumsq whose SGD update (lr != 0) also writes the bf16 copies of the UPDATED conv
- * weights: a tensor entry with pad = 1 + i (and a gradient) is the weight of wprep[i] (a DEVICE
- * gm_wprep array; K and C multiples of 64, Cp == C), walked in 64 x 64 tiles per tap so both the
- * KRSC copy and the channel-transposed copy are written coalesced - the next step's
- * gm_conv_weight_prep_multi_bf16 pass is not needed.  pad = 0 entries as gm_group_sumsq. */
-int gm_group_sumsq_wprep(const gm_tensor* table, int ntensors, long long total_elems, int ngroups,
-                         float grad_scale, float lr, const gm_wprep* wprep, double* out, void* scratch,
-                         size_t scratch_bytes, void* stream);
 /* dw is fp32 [K][R][S][c_real]: the first c_real of the C (padded) input channels;
  * accumulate != 0 adds into dw (a parameter's gradient buffer written in place) */
 size_t gm_conv2d_wgrad_scratch(const gm_conv_desc* d);

@@ -209,56 +209,3 @@ def test_group_sumsq_long_chunks(dev, V):
     for (_, p), w in zip(params, want):
         torch.testing.assert_close(p.detach(), w, rtol=1e-6, atol=1e-7)
 
-
-@pytest.mark.parametrize("branches", [2, 12])
-def test_fused_sgd_writes_the_bf16_weight_copies(dev, branches):
-    """gm_group_sumsq_wprep: conv weights in the table (pad = 1 + their
-    gm_wprep entry) are updated tile by tile and their bf16 KRSC and channel-transposed copies
-    are written by the same pass.  The fp32 update is bit-identical to the plain pass, the copies
-    are bit-identical to k_wprep_multi run on the updated weights, and the group sums agree with
-    the plain pass within fp32 reduction order; tensors straddle the 16384-element chunks at
-    unaligned offsets (a 100-element tensor first), 2 and 12 branches (the 8- and 32-group
-    kernels)."""
-    from greedy_multimodal_learning_amd import _lib as L
-    from greedy_multimodal_learning_amd.callbacks import GroupNorms
-    from greedy_multimodal_learning_amd.conv import WeightPrep, GMConv2d
-    torch.manual_seed(2)
-    names = [f"net_view_{i}" for i in range(branches)]
-
-    class M(torch.nn.Module):
-        def __init__(self):
-            super().__init__()
-            self.head = torch.nn.Parameter(torch.randn(100))
-            self.convs = torch.nn.ModuleList([GMConv2d(64, 128, 3, bias=False), GMConv2d(128, 64, 1, bias=False),
-                                              GMConv2d(128, 256, 3, bias=False)])
-
-    def build():
-        torch.manual_seed(3)
-        m = M().to(dev).to(memory_format=torch.channels_last)
-        named = []
-        for i, (n, p) in enumerate(m.named_parameters()):
-            p.grad = torch.randn_like(p)
-            named.append((f"{names[i % branches]}.{n}", p))
-        return m, named
-
-    m0, named0 = build()
-    m1, named1 = build()
-    out0 = GroupNorms(named0, names, ["visual", "skeleton"]).sums(grad_scale=0.5, lr=0.1)
-    gn = GroupNorms(named1, names, ["visual", "skeleton"])
-    wp = WeightPrep(m1)
-    gn.wprep = wp
-    assert len(wp.fused_index()) == 3
-    out1 = gn.sums(grad_scale=0.5, lr=0.1)
-    assert wp.fresh()
-    copies = [(wb.clone(), wt.clone()) for (_, wb, wt) in wp.copies]
-    wp._fresh_version = None  # force the standalone pass on the updated weights
-    wp.run()
-    torch.cuda.synchronize()
-    for (p0, p1) in zip(m0.parameters(), m1.parameters()):
-        assert torch.equal(p0, p1)
-    for (wb, wt), (_, rb, rt) in zip(copies, wp.copies):
-        assert torch.equal(wb, rb) and torch.equal(wt, rt)
-    torch.testing.assert_close(out1, out0, rtol=1e-6, atol=0)
-    with torch.no_grad():  # an in-place change outside the step makes the copies stale
-        m1.convs[0].weight.mul_(2.0)
-    assert not wp.fresh()
