@@ -1,0 +1,300 @@
+// 1x1 / stride-1 / pad-0 convolutions in NHWC are plain NT GEMMs over the pixels: the ResNet-50
+// bottleneck's reduce / expand convolutions and their input gradients (C5 workload, SURVEY §8 row
+// f4; torchvision Bottleneck conv1 / conv3 + downsample of layer 1, autocast bf16).  The im2col
+// kernel ran them at 0.09-0.18 of the MFMA peak: most have a short reduction (K = 64-512), so a
+// 128 x 128 tile is one to eight 64-deep k-steps, each paid for with a DMA round trip, a barrier
+// and an epilogue - latency, not math or bytes.
+//
+//   Out[g][m][n] = sum_k A[g][m][k] * B[g][n][k]  (+ Addend[g][m][n]),  bf16 in/out, fp32 accumulate
+//   forward: A = x [M][C], B = w [K][C] (KRSC, R = S = 1),   Out = y  [M][K]
+//   dgrad:   A = dy [M][K], B = wt [C][K] (the transposed copy), Out = dx [M][C] (+ the join addend)
+//
+// k_gemm_ring: a PERSISTENT workgroup walks a strided list of output tiles; the (tile, k-step)
+// units of its list stream through an S-slot LDS ring filled by four LOADER waves (LDS-DMA,
+// S - 1 units in flight, one raw s_barrier per unit after a counted vmcnt - the pattern of
+// k_wgrad_ring), so a tile's DMA, the previous tile's epilogue stores and the MFMAs overlap
+// across tile boundaries; four COMPUTE waves (2 x 2, 64 pixels x BN/2 channels each) read
+// ds_read_b128 fragments from 128-B rows whose 16-B chunks are XOR-swizzled by (row >> 1) & 7
+// on the source side (conflict-free for the b128 lane groups), weights as the MFMA A operand
+// so each lane owns 4 consecutive output channels of one pixel: 8-byte NHWC stores through a
+// buffer resource (rows past M dropped by the hardware, addend loads in flight together).
+#include <cstdint>
+#include <cstring>
+
+#include "gm_common.h"
+
+namespace gm {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+struct RingGemmArgs {
+    const uint16_t* A;       // [G][M][Kr]
+    const uint16_t* B;       // [G][N][Kr]
+    uint16_t* out;           // [G][M][N]
+    const uint16_t* addend;  // [G][M][N] or null (may alias out)
+    int M, N, Kr;            // per group
+    int G, tiles_m, tiles_n, tiles;  // tiles = G * tiles_m * tiles_n
+    long long gsA, gsB, gsO; // group strides (elements; gsB may be negative)
+};
+
+__device__ __attribute__((aligned(16))) const uint4 g_rzero16[1] = {{0u, 0u, 0u, 0u}};
+
+template <int BN, int S>
+__global__ __launch_bounds__(512) void k_gemm_ring(RingGemmArgs a) {
+    static_assert(BN == 64 || BN == 128, "k_gemm_ring: 64 or 128 output channels per tile");
+    static_assert(S >= 2, "k_gemm_ring: at least two slots");
+    constexpr int BM = 128, D = S - 1;
+    constexpr int SA = BM * 128, SB = BN * 128, SLOT = SA + SB;  // bytes
+    constexpr int PA = SA / 1024 / 4, PB = SB / 1024 / 4;        // DMA pieces per loader wave per unit
+    constexpr int NT = BN / 64;                                  // 32-channel fragments per wave
+    extern __shared__ __attribute__((aligned(16))) uint4 gsm[];
+    char* lds = reinterpret_cast<char*>(gsm);
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int nk = a.Kr >> 6;  // 64-deep k-steps per tile
+    // this workgroup's tiles: blockIdx.x, + gridDim.x, ...; units = tiles x k-steps
+    const int ntiles = a.tiles > (int)blockIdx.x ? (a.tiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+    const int nunits = ntiles * nk;
+    auto tile_of = [&](int i, int& g, int& m0, int& n0) __attribute__((always_inline)) {
+        int tl = (int)blockIdx.x + i * (int)gridDim.x;
+        const int per = a.tiles_m * a.tiles_n;
+        g = tl / per;
+        tl -= g * per;
+        const int mt = tl / a.tiles_n;
+        m0 = mt * BM;
+        n0 = (tl - mt * a.tiles_n) * BN;
+    };
+
+    if (wave >= 4) {
+        // ---- loader waves: A rows 32 lw .. + 31 (4 pieces of 8 rows), B rows (BN / 4) lw .. ----
+        const int lw = wave - 4;
+        typedef __attribute__((address_space(1))) const void* gptr_t;
+        typedef __attribute__((address_space(3))) void* lptr_t;
+        const void* zero = (const void*)g_rzero16;
+        const int r8 = lane >> 3, ch = lane & 7;
+        int slot = 0, ut = 0, uk = 0;  // next unit to issue: tile index ut, k-step uk
+        int g = 0, m0 = 0, n0 = 0;
+        if (nunits > 0) tile_of(0, g, m0, n0);
+        auto issue = [&]() __attribute__((always_inline)) {
+            const unsigned sb = (unsigned)slot * SLOT;
+            const uint16_t* Ag = a.A + g * a.gsA;
+            const uint16_t* Bg = a.B + g * a.gsB;
+            const int k0 = uk << 6;
+#pragma unroll
+            for (int j = 0; j < PA; ++j) {
+                const int row = (lw * PA + j) * 8 + r8;
+                const int m = m0 + row;
+                const int c = (ch ^ ((row >> 1) & 7)) << 3;
+                const void* src = m < a.M ? (const void*)(Ag + (size_t)m * a.Kr + k0 + c) : zero;
+                __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + sb + (lw * PA + j) * 1024), 16, 0, 0);
+            }
+#pragma unroll
+            for (int j = 0; j < PB; ++j) {
+                const int row = (lw * PB + j) * 8 + r8;
+                const int c = (ch ^ ((row >> 1) & 7)) << 3;
+                __builtin_amdgcn_global_load_lds((gptr_t)(Bg + (size_t)(n0 + row) * a.Kr + k0 + c),
+                                                 (lptr_t)(lds + sb + SA + (lw * PB + j) * 1024), 16, 0, 0);
+            }
+            slot = slot + 1 == S ? 0 : slot + 1;
+            if (++uk == nk) {
+                uk = 0;
+                if (++ut < ntiles) tile_of(ut, g, m0, n0);
+            }
+        };
+        for (int i = 0; i < D && i < nunits; ++i) issue();
+        for (int i = 0; i < nunits; ++i) {
+            // unit i has landed (D - 1 younger ones may stay in flight; at the tail all of them)
+            if (i + D - 1 < nunits) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((PA + PB) * (D - 1)) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            if (i + D < nunits) issue();  // into the slot unit i - 1 used (every read of it is done)
+        }
+        return;
+    }
+
+    // ---- compute waves ----
+    const int wm = wave >> 1, wn = wave & 1;
+    const int fr = lane & 31, fh = lane >> 5;
+    // fragment row r, 16-B chunk of k-slice ks: (2 ks + fh) ^ ((r >> 1) & 7); the XOR term is
+    // per lane, the k-slice an XOR of (ks << 5) on the byte offset
+    unsigned aoff[2], boff[NT];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int r = wm * 64 + i * 32 + fr;
+        aoff[i] = (unsigned)(r * 128 + ((fh ^ ((r >> 1) & 7)) << 4));
+    }
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const int r = wn * (BN / 2) + j * 32 + fr;
+        boff[j] = (unsigned)(SA + r * 128 + ((fh ^ ((r >> 1) & 7)) << 4));
+    }
+    floatx16 acc[NT][2];
+    auto zero_acc = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) acc[j][i][e] = 0.f;
+    };
+    zero_acc();
+    bf16x8 fa[2][2], fb[2][NT];  // [buffer][fragment]: activations (MFMA B), weights (MFMA A)
+    auto load = [&](int ks, int c, const char* base) __attribute__((always_inline)) {
+        const unsigned x = (unsigned)ks << 5;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) fa[c][i] = *reinterpret_cast<const bf16x8*>(base + (aoff[i] ^ x));
+#pragma unroll
+        for (int j = 0; j < NT; ++j) fb[c][j] = *reinterpret_cast<const bf16x8*>(base + (boff[j] ^ x));
+    };
+    int slot = 0, g = 0, m0 = 0, n0 = 0;
+    if (nunits > 0) tile_of(0, g, m0, n0);
+    int uk = 0, ut = 0;
+    for (int i = 0; i < nunits; ++i) {
+        __builtin_amdgcn_s_barrier();  // unit i landed; every wave is done with unit i - 1's slot
+        const char* base = lds + slot * SLOT;
+        load(0, 0, base);
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            const int c = ks & 1;
+            if (ks < 3) load(ks + 1, c ^ 1, base);
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+#pragma unroll
+                for (int ii = 0; ii < 2; ++ii)
+                    acc[j][ii] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[c][j], fa[c][ii], acc[j][ii], 0, 0, 0);
+        }
+        // slice ks + 1's fragment reads go out BEFORE slice ks's MFMAs (k_conv_h9's schedule): the
+        // counted lgkmcnt then waits for slice ks's reads only
+        constexpr int NR = 2 + NT, NM = 2 * NT;
+        __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+#pragma unroll
+        for (int ks = 0; ks < 3; ++ks) {
+            __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
+        // every LDS read of this unit must be done before the next barrier lets the loaders refill
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        slot = slot + 1 == S ? 0 : slot + 1;
+        if (++uk == nk) {
+            // epilogue of tile ut: D[n][m] - lane: pixel m = m0 + 64 wm + 32 ii + fr, registers
+            // 4 q .. 4 q + 3: channels n0 + (BN / 2) wn + 32 j + 8 q + 4 fh + 0..3
+            uint16_t* outp = a.out + g * a.gsO;
+            const size_t obytes = (size_t)a.M * a.N * 2;
+            const auto orsrc = __builtin_amdgcn_make_buffer_rsrc(outp, 0, (int)obytes, 0x00020000);
+            typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+            unsigned off[2];
+#pragma unroll
+            for (int ii = 0; ii < 2; ++ii) {
+                const int m = m0 + wm * 64 + ii * 32 + fr;
+                off[ii] = m < a.M ? (unsigned)m * (unsigned)a.N * 2u : 0xfffffff0u;
+            }
+            auto bo = [&](int ii, int j, int q) {
+                return off[ii] == 0xfffffff0u ? 0xfffffff0u
+                                              : off[ii] + (unsigned)(n0 + wn * (BN / 2) + j * 32 + 8 * q + 4 * fh) * 2u;
+            };
+            // (the addend test hoisted out of the loops: a per-element one branches and waits
+            // vmcnt around every store)
+            if (a.addend) {
+                const auto arsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.addend + g * a.gsO), 0,
+                                                                     (int)obytes, 0x00020000);
+                u32x2 av[NT][2][4];
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+#pragma unroll
+                    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            av[j][ii][q] = __builtin_amdgcn_raw_buffer_load_b64(arsrc, bo(ii, j, q), 0, 0);
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+#pragma unroll
+                    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const u32x2 v = {pack_bf2(acc[j][ii][4 * q] + bf_lo(av[j][ii][q].x),
+                                                      acc[j][ii][4 * q + 1] + bf_hi(av[j][ii][q].x)),
+                                             pack_bf2(acc[j][ii][4 * q + 2] + bf_lo(av[j][ii][q].y),
+                                                      acc[j][ii][4 * q + 3] + bf_hi(av[j][ii][q].y))};
+                            __builtin_amdgcn_raw_buffer_store_b64(v, orsrc, bo(ii, j, q), 0, 0);
+                        }
+            } else {
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+#pragma unroll
+                    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const u32x2 v = {pack_bf2(acc[j][ii][4 * q], acc[j][ii][4 * q + 1]),
+                                             pack_bf2(acc[j][ii][4 * q + 2], acc[j][ii][4 * q + 3])};
+                            __builtin_amdgcn_raw_buffer_store_b64(v, orsrc, bo(ii, j, q), 0, 0);
+                        }
+            }
+            zero_acc();
+            uk = 0;
+            if (++ut < ntiles) tile_of(ut, g, m0, n0);
+        }
+    }
+}
+
+static int g_ring_cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+        return 256;
+    return n;
+}();
+
+// GM_CONV1X1 at load / gm_conv_set_1x1_gemm: 1 (default) = 1x1 / s1 shapes take k_gemm_ring,
+// 0 = the im2col kernel
+int g_conv_1x1 = [] {
+    const char* e = getenv("GM_CONV1X1");
+    return e ? atoi(e) : 1;
+}();
+
+bool conv1x1_ok(int R, int S, int sh, int sw, int ph, int pw, long long M, int Kr, int N) {
+    return g_conv_1x1 && R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0 && M >= 1 && Kr % 64 == 0 &&
+           Kr >= 64 && (N % 128 == 0 || N == 64) && M * (long long)(Kr > N ? Kr : N) < (1ll << 30);
+}
+
+// Out = A . B^T (+ addend) per group; the caller checked conv1x1_ok
+int conv1x1_gemm(long long M, int Kr, int N, int G, const void* A, long long gsA, const void* B, long long gsB,
+                 void* out, long long gsO, const void* addend, hipStream_t st, const char* fn) {
+    RingGemmArgs r;
+    memset(&r, 0, sizeof(r));
+    r.A = (const uint16_t*)A;
+    r.B = (const uint16_t*)B;
+    r.out = (uint16_t*)out;
+    r.addend = (const uint16_t*)addend;
+    r.M = (int)M; r.N = N; r.Kr = Kr; r.G = G;
+    const int BN = N % 128 == 0 ? 128 : 64;
+    r.tiles_m = (int)((M + 127) / 128);
+    r.tiles_n = N / BN;
+    r.tiles = G * r.tiles_m * r.tiles_n;
+    r.gsA = gsA; r.gsB = gsB; r.gsO = gsO;
+    const int grid = r.tiles < g_ring_cus ? r.tiles : g_ring_cus;  // persistent: one workgroup per CU
+    auto go = [&](auto bnc) -> int {
+        constexpr int BNt = decltype(bnc)::value, S = 4;
+        constexpr size_t lds = (size_t)S * (128 * 128 + BNt * 128);
+        static bool attr = false;
+        if (!attr) {
+            if (hipFuncSetAttribute((const void*)k_gemm_ring<BNt, S>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds) != hipSuccess) {
+                set_error("%s: %zu B of LDS refused", fn, lds);
+                return GM_E_UNSUP;
+            }
+            attr = true;
+        }
+        k_gemm_ring<BNt, S><<<grid, 512, lds, st>>>(r);
+        return check_launch(fn);
+    };
+    return BN == 128 ? go(std::integral_constant<int, 128>{}) : go(std::integral_constant<int, 64>{});
+}
+
+}  // namespace gm
+
+extern "C" int gm_conv_set_1x1_gemm(int on) {
+    gm::g_conv_1x1 = on ? 1 : 0;
+    return GM_OK;
+}

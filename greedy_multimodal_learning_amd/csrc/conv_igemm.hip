@@ -2572,13 +2572,6 @@ extern "C" int gm_conv_set_rw(int on) {
     return GM_OK;
 }
 
-// the 1x1 / s1 GEMM path (gm_conv_set_1x1_gemm): 0 = the im2col kernel for 1x1 shapes
-static int g_conv_1x1 = 0;
-extern "C" int gm_conv_set_1x1_gemm(int on) {
-    g_conv_1x1 = on ? 1 : 0;
-    return GM_OK;
-}
-
 extern "C" int gm_conv_set_pipe(int pipe) {
     GM_REQUIRE(pipe == 0 || pipe == 2 || pipe == 3, "gm_conv_set_pipe: 0, 2 or 3");
     g_conv_pipe = pipe;
@@ -2586,11 +2579,23 @@ extern "C" int gm_conv_set_pipe(int pipe) {
 }
 
 
+// 1x1 / s1 / p0 convolutions as plain GEMMs (conv1x1.hip, k_gemm_ring)
+namespace gm {
+bool conv1x1_ok(int R, int S, int sh, int sw, int ph, int pw, long long M, int Kr, int N);
+int conv1x1_gemm(long long M, int Kr, int N, int G, const void* A, long long gsA, const void* B, long long gsB,
+                 void* out, long long gsO, const void* addend, hipStream_t st, const char* fn);
+}  // namespace gm
+
 extern "C" int gm_conv2d_fwd_hw_bf16(const gm_conv_desc_hw* d, const void* x, const void* w, void* y,
                                      void* stream) {
     int rc = check_desc_hw(d);
     if (rc) return rc;
     GM_REQUIRE(x && w && y, "conv fwd: null pointer");
+    {
+        const long long M = (long long)d->N * d->H * d->W;
+        if (gm::conv1x1_ok(d->R, d->S, d->stride_h, d->stride_w, d->pad_h, d->pad_w, M, d->C, d->K))
+            return gm::conv1x1_gemm(M, d->C, d->K, 1, x, 0, w, 0, y, 0, nullptr, as_stream(stream), "conv1x1 fwd");
+    }
     ConvArgs a;
     fwd_setup(d, x, w, y, a);
     return pick_and_launch(a, as_stream(stream), nullptr, 0);
@@ -2602,6 +2607,11 @@ extern "C" int gm_conv2d_fwd_ex_bf16(const gm_conv_desc* d, const void* x, const
     if (rc) return rc;
     GM_REQUIRE(x && w && y, "conv fwd: null pointer");
     const gm_conv_desc_hw h = to_hw(d);
+    {
+        const long long M = (long long)d->N * d->H * d->W;
+        if (gm::conv1x1_ok(d->R, d->S, d->stride, d->stride, d->pad, d->pad, M, d->C, d->K))
+            return gm::conv1x1_gemm(M, d->C, d->K, 1, x, 0, w, 0, y, 0, nullptr, as_stream(stream), "conv1x1 fwd");
+    }
     ConvArgs a;
     fwd_setup(&h, x, w, y, a);
     return pick_and_launch(a, as_stream(stream), ws, ws_bytes);
@@ -2622,6 +2632,12 @@ extern "C" int gm_conv2d_fwd_grouped_bf16(const gm_conv_desc_hw* d, int G, const
     GM_REQUIRE(G == 1 || w_stride >= (long long)d->K * d->R * d->S * d->C ||
                    -w_stride >= (long long)d->K * d->R * d->S * d->C,
                "conv fwd: group weight stride %lld shorter than one weight", w_stride);
+    {
+        const long long M = (long long)d->N * d->H * d->W;
+        if (gm::conv1x1_ok(d->R, d->S, d->stride_h, d->stride_w, d->pad_h, d->pad_w, M, d->C, d->K))
+            return gm::conv1x1_gemm(M, d->C, d->K, G, x, M * d->C, w, w_stride, y, M * d->K, nullptr,
+                                    as_stream(stream), "conv1x1 fwd");
+    }
     ConvArgs a;
     fwd_setup(d, x, w, y, a);
     a.G = G;
@@ -2681,6 +2697,12 @@ extern "C" int gm_conv2d_dgrad_grouped_bf16(const gm_conv_desc* d, int G, const 
                "conv dgrad: group weight stride %lld shorter than one weight", wt_stride);
     const int P = (d->H + 2 * d->pad - d->R) / d->stride + 1;
     const int Q = (d->W + 2 * d->pad - d->S) / d->stride + 1;
+    {
+        const long long M = (long long)d->N * d->H * d->W;
+        if (gm::conv1x1_ok(d->R, d->S, d->stride, d->stride, d->pad, d->pad, M, d->K, d->C))
+            return gm::conv1x1_gemm(M, d->K, d->C, G, dy, M * d->K, wt, wt_stride, dx, M * d->C, addend,
+                                    as_stream(stream), "conv1x1 dgrad");
+    }
     ConvArgs a;
     const bool full = dgrad_setup(d, dy, wt, dx, a);
     a.G = G;
@@ -2707,6 +2729,12 @@ extern "C" int gm_conv2d_dgrad_add_bf16(const gm_conv_desc* d, const void* dy, c
     // addend == dx (in place) is allowed: every epilogue loads an output element's addend
     // and stores that element from the same thread, and pixels no parity class covers
     // then simply keep the addend (no zero / copy pass)
+    {
+        const long long M = (long long)d->N * d->H * d->W;
+        if (gm::conv1x1_ok(d->R, d->S, d->stride, d->stride, d->pad, d->pad, M, d->K, d->C))
+            return gm::conv1x1_gemm(M, d->K, d->C, 1, dy, 0, wt, 0, dx, 0, addend, as_stream(stream),
+                                    "conv1x1 dgrad");
+    }
     ConvArgs a;
     const bool full = dgrad_setup(d, dy, wt, dx, a);
     a.addend = (const uint16_t*)addend;

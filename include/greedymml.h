@@ -374,8 +374,10 @@ int gm_conv_set_wgrad_loop(int mode);
 /* k_wgrad_ring's staging form (GM_WGRAD_RING at load): 0 (default) = 3 slots of 64 pixels,
  * 1 = 6 slots of 32 pixels. */
 int gm_conv_set_wgrad_ring(int form);
-/* 1x1 / stride-1 / pad-0 convolutions (forward, input and weight gradient) as plain GEMMs on
- * hipBLASLt (default off: GM_CONV1X1_LT=1 at load or gm_conv_set_1x1_gemm(1) turn it on). */
+/* 1x1 / stride-1 / pad-0 forward and input-gradient convolutions as plain NT GEMMs on
+ * k_gemm_ring (conv1x1.hip: persistent, loader waves feeding a 4-slot LDS ring; C % 64 == 0 and
+ * the output channels % 128 == 0 or == 64).  Default on (GM_CONV1X1=0 at load or
+ * gm_conv_set_1x1_gemm(0) route them back to the im2col kernels). */
 int gm_conv_set_1x1_gemm(int on);
 /* Weight-gradient operand staging: 0 = LDS-DMA pieces, 1 = register-staged (global_load_dwordx4
  * two steps ahead + ds_write_b128; same LDS image and arithmetic), 2 (default) = register-staged

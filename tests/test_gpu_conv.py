@@ -605,10 +605,11 @@ def test_wgrad_halo64_beside_a_busy_neighbour(dev):
                                    (8, 64, 56, 56, 64, 12), (8, 2048, 7, 7, 512, 12), (8, 512, 28, 28, 128, 12)],
                          ids=lambda s: "x".join(map(str, s)))
 def test_conv1x1_gemm_vs_fp32(dev, shape):
-    """1x1 / s1 / p0 convolutions as plain GEMMs (hipBLASLt, conv1x1_lt.hip): forward, input
+    """1x1 / s1 / p0 convolutions as plain NT GEMMs (k_gemm_ring, conv1x1.hip): forward, input
     gradient with and without the fused addend, weight gradient plain and accumulating, as
-    the two-view grouped launches the trunk issues (the view groups as the GEMM batch) -
-    against fp32 PyTorch and against the im2col kernel (gm_conv_set_1x1_gemm(0))."""
+    the two-view grouped launches the trunk issues (the view groups as the GEMM batch; M not a
+    multiple of the 128-row tile at 5x3 and 7x7 maps) - against fp32 PyTorch and against the
+    im2col kernel (gm_conv_set_1x1_gemm(0))."""
     import ctypes
     from greedy_multimodal_learning_amd import _lib as L
     from greedy_multimodal_learning_amd import conv as CV
@@ -649,7 +650,7 @@ def test_conv1x1_gemm_vs_fp32(dev, shape):
             torch.cuda.synchronize()
             res[mode] = (y, dx, dxa, dws)
     finally:
-        L.check(lib.gm_conv_set_1x1_gemm(0), "1x1 gemm")  # the default
+        L.check(lib.gm_conv_set_1x1_gemm(1), "1x1 gemm")  # the default
     for g in range(G):
         sl = slice(g * N, (g + 1) * N)
         xf, dyf, wf = x[sl].float().reshape(-1, C), dy[sl].float().reshape(-1, K), w[g].float()

@@ -27,6 +27,7 @@
 #                (commas become spaces), summarised per kernel  -> gpurun_out/pmcone_SET.txt
 #   rp:FILE[,ARGS] rocprofv3 --kernel-trace --stats of python FILE ARGS -> gpurun_out/rp_FILE/
 #   py:FILE[,ARGS] python FILE ARGS (a tools/ script; commas become spaces) -> gpurun_out/py_FILE.log
+#   env:V=X,..   export the variables for the following steps (bench:* logs get the tag _V_X); env: clears
 set -o pipefail
 mkdir -p gpurun_out
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -66,8 +67,12 @@ for s in "$@"; do
       timeout -k 10 600 python -u bench.py --no-cpu-baseline > gpurun_out/benchq.log 2>&1 \
         || { tail -30 gpurun_out/benchq.log; exit 15; }
       tail -1 gpurun_out/benchq.log | cut -c1-400 ;;
+    env:*)
+      for v in $ENVSET; do unset "${v%%=*}"; done
+      ENVSET="${s#env:}"; ENVSET="${ENVSET//,/ }"; TAG=""
+      [ -n "$ENVSET" ] && { export $ENVSET; TAG="_$(echo "$ENVSET" | tr -c 'A-Za-z0-9\n' '_')"; } ;;
     bench:*)
-      a="${s#bench:}"; f="gpurun_out/bench_$(echo "$a" | tr -c 'A-Za-z0-9_=.\n-' '_').log"
+      a="${s#bench:}"; f="gpurun_out/bench_$(echo "$a" | tr -c 'A-Za-z0-9_=.\n-' '_')$TAG.log"
       timeout -k 10 600 python -u bench.py ${a//,/ } > "$f" 2>&1 || { tail -30 "$f"; exit 16; }
       tail -1 "$f" | cut -c1-400 ;;
     prof)
