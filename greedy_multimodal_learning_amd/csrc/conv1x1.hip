@@ -16,8 +16,9 @@
 // across tile boundaries; four COMPUTE waves (2 x 2, 64 pixels x BN/2 channels each) read
 // ds_read_b128 fragments from 128-B rows whose 16-B chunks are XOR-swizzled by (row >> 1) & 7
 // on the source side (conflict-free for the b128 lane groups), weights as the MFMA A operand
-// so each lane owns 4 consecutive output channels of one pixel: 8-byte NHWC stores through a
-// buffer resource (rows past M dropped by the hardware, addend loads in flight together).
+// so each lane owns 4 consecutive output channels of one pixel; the epilogue transposes each
+// wave's 32-pixel halves through private fp32 LDS rows into 16-B NHWC stores through a buffer
+// resource (rows past M dropped by the hardware, addend loads in flight together).
 #include <cstdint>
 #include <cstring>
 
@@ -53,11 +54,16 @@ __global__ __launch_bounds__(512) void k_gemm_ring(RingGemmArgs a) {
     const int t = threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const int nk = a.Kr >> 6;  // 64-deep k-steps per tile
-    // this workgroup's tiles: blockIdx.x, + gridDim.x, ...; units = tiles x k-steps
-    const int ntiles = a.tiles > (int)blockIdx.x ? (a.tiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+    // this workgroup's tiles: vb, vb + gridDim.x, ...; units = tiles x k-steps.  Workgroups are
+    // dealt round-robin over the 8 XCDs (b on XCD b % 8): vb gives each XCD a contiguous block of
+    // every round's tile ids, so the tiles_n output-channel tiles of one pixel block run together
+    // on one XCD and fetch its activation rows from HBM once (into that L2) instead of tiles_n times
+    const int nb = (int)gridDim.x, b = (int)blockIdx.x;
+    const int vb = nb % 8 == 0 ? (b & 7) * (nb >> 3) + (b >> 3) : b;
+    const int ntiles = a.tiles > vb ? (a.tiles - 1 - vb) / nb + 1 : 0;
     const int nunits = ntiles * nk;
     auto tile_of = [&](int i, int& g, int& m0, int& n0) __attribute__((always_inline)) {
-        int tl = (int)blockIdx.x + i * (int)gridDim.x;
+        int tl = vb + i * nb;
         const int per = a.tiles_m * a.tiles_n;
         g = tl / per;
         tl -= g * per;
@@ -178,58 +184,70 @@ __global__ __launch_bounds__(512) void k_gemm_ring(RingGemmArgs a) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         slot = slot + 1 == S ? 0 : slot + 1;
         if (++uk == nk) {
-            // epilogue of tile ut: D[n][m] - lane: pixel m = m0 + 64 wm + 32 ii + fr, registers
-            // 4 q .. 4 q + 3: channels n0 + (BN / 2) wn + 32 j + 8 q + 4 fh + 0..3
+            // epilogue of tile ut: lane (fr, fh) holds pixel 64 wm + 32 ii + fr, channels
+            // (BN / 2) wn + 32 j + 8 q + 4 fh + 0..3 in registers 4 q .. 4 q + 3.  Direct 8-B stores
+            // from that layout touch 32 rows per instruction and held the write-heavy shapes
+            // (K = 64 -> 256) at 3 TB/s; instead each 32-pixel half goes through the wave's own
+            // fp32 staging rows (16-B chunks XOR-swizzled) and leaves as 16-B stores, OPR lanes per
+            // contiguous row segment - the addend added in fp32 before the one rounding, as before.
+            constexpr int RB = NT * 128, OPR = 4 * NT, RPI = 64 / OPR;
+            char* stg = lds + S * SLOT + wave * (32 * RB);
+            auto swz = [](int r, int c) { return NT == 2 ? c ^ (r & 15) : c ^ ((r >> 1) & 7); };
             uint16_t* outp = a.out + g * a.gsO;
             const size_t obytes = (size_t)a.M * a.N * 2;
             const auto orsrc = __builtin_amdgcn_make_buffer_rsrc(outp, 0, (int)obytes, 0x00020000);
-            typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-            unsigned off[2];
+            const auto arsrc = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<uint16_t*>(a.addend ? a.addend + g * a.gsO : outp), 0, (int)obytes, 0x00020000);
+            typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+            const int o = lane % OPR, rr = lane / OPR;
+            const unsigned nb = (unsigned)(n0 + wn * (BN / 2) + 8 * o) * 2u;
 #pragma unroll
             for (int ii = 0; ii < 2; ++ii) {
-                const int m = m0 + wm * 64 + ii * 32 + fr;
-                off[ii] = m < a.M ? (unsigned)m * (unsigned)a.N * 2u : 0xfffffff0u;
-            }
-            auto bo = [&](int ii, int j, int q) {
-                return off[ii] == 0xfffffff0u ? 0xfffffff0u
-                                              : off[ii] + (unsigned)(n0 + wn * (BN / 2) + j * 32 + 8 * q + 4 * fh) * 2u;
-            };
-            // (the addend test hoisted out of the loops: a per-element one branches and waits
-            // vmcnt around every store)
-            if (a.addend) {
-                const auto arsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.addend + g * a.gsO), 0,
-                                                                     (int)obytes, 0x00020000);
-                u32x2 av[NT][2][4];
 #pragma unroll
                 for (int j = 0; j < NT; ++j)
 #pragma unroll
-                    for (int ii = 0; ii < 2; ++ii)
+                    for (int q = 0; q < 4; ++q) {
+                        const float4 v = {acc[j][ii][4 * q], acc[j][ii][4 * q + 1], acc[j][ii][4 * q + 2],
+                                          acc[j][ii][4 * q + 3]};
+                        *reinterpret_cast<float4*>(stg + fr * RB + swz(fr, 8 * j + 2 * q + fh) * 16) = v;
+                    }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                unsigned off[2 * NT];
 #pragma unroll
-                        for (int q = 0; q < 4; ++q)
-                            av[j][ii][q] = __builtin_amdgcn_raw_buffer_load_b64(arsrc, bo(ii, j, q), 0, 0);
+                for (int it = 0; it < 2 * NT; ++it) {
+                    const int m = m0 + wm * 64 + ii * 32 + it * RPI + rr;
+                    off[it] = m < a.M ? (unsigned)m * (unsigned)a.N * 2u + nb : 0xfffffff0u;
+                }
+                // (the addend test hoisted out of the loops: a per-element one branches and waits
+                // vmcnt around every store)
+                if (a.addend) {
+                    u32x4 av[2 * NT];
 #pragma unroll
-                for (int j = 0; j < NT; ++j)
+                    for (int it = 0; it < 2 * NT; ++it) av[it] = __builtin_amdgcn_raw_buffer_load_b128(arsrc, off[it], 0, 0);
 #pragma unroll
-                    for (int ii = 0; ii < 2; ++ii)
+                    for (int it = 0; it < 2 * NT; ++it) {
+                        const int row = it * RPI + rr;
+                        const float4 f0 = *reinterpret_cast<const float4*>(stg + row * RB + swz(row, 2 * o) * 16);
+                        const float4 f1 = *reinterpret_cast<const float4*>(stg + row * RB + swz(row, 2 * o + 1) * 16);
+                        const u32x4 v = {pack_bf2(f0.x + bf_lo(av[it].x), f0.y + bf_hi(av[it].x)),
+                                         pack_bf2(f0.z + bf_lo(av[it].y), f0.w + bf_hi(av[it].y)),
+                                         pack_bf2(f1.x + bf_lo(av[it].z), f1.y + bf_hi(av[it].z)),
+                                         pack_bf2(f1.z + bf_lo(av[it].w), f1.w + bf_hi(av[it].w))};
+                        __builtin_amdgcn_raw_buffer_store_b128(v, orsrc, off[it], 0, 0);
+                    }
+                } else {
 #pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            const u32x2 v = {pack_bf2(acc[j][ii][4 * q] + bf_lo(av[j][ii][q].x),
-                                                      acc[j][ii][4 * q + 1] + bf_hi(av[j][ii][q].x)),
-                                             pack_bf2(acc[j][ii][4 * q + 2] + bf_lo(av[j][ii][q].y),
-                                                      acc[j][ii][4 * q + 3] + bf_hi(av[j][ii][q].y))};
-                            __builtin_amdgcn_raw_buffer_store_b64(v, orsrc, bo(ii, j, q), 0, 0);
-                        }
-            } else {
-#pragma unroll
-                for (int j = 0; j < NT; ++j)
-#pragma unroll
-                    for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            const u32x2 v = {pack_bf2(acc[j][ii][4 * q], acc[j][ii][4 * q + 1]),
-                                             pack_bf2(acc[j][ii][4 * q + 2], acc[j][ii][4 * q + 3])};
-                            __builtin_amdgcn_raw_buffer_store_b64(v, orsrc, bo(ii, j, q), 0, 0);
-                        }
+                    for (int it = 0; it < 2 * NT; ++it) {
+                        const int row = it * RPI + rr;
+                        const float4 f0 = *reinterpret_cast<const float4*>(stg + row * RB + swz(row, 2 * o) * 16);
+                        const float4 f1 = *reinterpret_cast<const float4*>(stg + row * RB + swz(row, 2 * o + 1) * 16);
+                        const u32x4 v = {pack_bf2(f0.x, f0.y), pack_bf2(f0.z, f0.w), pack_bf2(f1.x, f1.y),
+                                         pack_bf2(f1.z, f1.w)};
+                        __builtin_amdgcn_raw_buffer_store_b128(v, orsrc, off[it], 0, 0);
+                    }
+                }
+                // the next half's staging writes after every read of this one
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             }
             zero_acc();
             uk = 0;
@@ -276,7 +294,8 @@ int conv1x1_gemm(long long M, int Kr, int N, int G, const void* A, long long gsA
     const int grid = r.tiles < g_ring_cus ? r.tiles : g_ring_cus;  // persistent: one workgroup per CU
     auto go = [&](auto bnc) -> int {
         constexpr int BNt = decltype(bnc)::value, S = 4;
-        constexpr size_t lds = (size_t)S * (128 * 128 + BNt * 128);
+        // the ring + four compute waves' fp32 staging rows (32 pixels x BN / 2 channels each)
+        constexpr size_t lds = (size_t)S * (128 * 128 + BNt * 128) + 4 * 32 * (BNt / 2) * 4;
         static bool attr = false;
         if (!attr) {
             if (hipFuncSetAttribute((const void*)k_gemm_ring<BNt, S>, hipFuncAttributeMaxDynamicSharedMemorySize,
