@@ -728,10 +728,10 @@ __global__ __launch_bounds__(kT) void k_stem_pool_bn_bwd(ReduceArgs a0, StemPool
 __global__ __launch_bounds__(kT) void k_bn_stats_finalize(ReduceArgs a0) {
     const ReduceArgs a = group_args(a0);
     __shared__ float red[kRedF + 4];
-    const int t = threadIdx.x;
+    const int t = threadIdx.x, cs = blockIdx.y;  // channel slice cs (64 channels)
     FinOps fo{};
-    if (t < a.SW) fo = fin_load<FWD>(a, t);
-    combine_finalize<FWD>(a, 0, red, fo);
+    if (t < a.SW) fo = fin_load<FWD>(a, cs * a.SW + t);
+    combine_finalize<FWD>(a, cs, red, fo);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1255,6 +1255,8 @@ struct ApplyArgs {
     const float* coef;   // [4][C]
     int C;
     const float* fcoef;  // bwd MASKX: the forward's sc[C], sh[C]
+    long long gvec;      // fwd apply, view groups (gridDim.y): group g's x / res / out gvec
+    long long cgs;       // vectors and its coefficients cgs floats after group 0's
 };
 
 __device__ __forceinline__ void load_coef(const float* p, int cg, float* c) {
@@ -1268,10 +1270,13 @@ __global__ __launch_bounds__(kT) void k_bn_apply(ApplyArgs a) {
     const long long stride = (long long)gridDim.x * kT;  // multiple of C/8
     long long v = (long long)blockIdx.x * kT + threadIdx.x;
     const int cg = (int)(v & ((1 << a.tpr_log) - 1));
+    const long long go = blockIdx.y * a.gvec;  // view group blockIdx.y
+    const float* coef = a.coef + blockIdx.y * a.cgs;
     float sc[8], sh[8];
-    load_coef(a.coef, cg, sc);
-    load_coef(a.coef + a.C, cg, sh);
+    load_coef(coef, cg, sc);
+    load_coef(coef + a.C, cg, sh);
     auto one = [&](long long i) {
+        i += go;
         float f[8];
         V8<E>::ld(a.x, i, f);
         float r[8];
@@ -1892,21 +1897,23 @@ extern "C" int gm_bn_relu_maxpool2d_bwd_grouped_bf16(const gm_pool_desc* d, int 
     return check_launch("k_stem_pool_bn_bwd<apply>");
 }
 
-// BatchNorm forward statistics from producer partial rows (gm_conv2d_fwd_grouped_stats_bf16):
-// stats = [G][rows + 1][128] floats (rows partial rows of 64 x (sum, sum of squares), then
-// 128 floats of coefficient scratch); ps[g] as for gm_bn_fwd_stats_grouped_bf16 (C = 64).
+// BatchNorm forward statistics from producer partial rows (gm_conv2d_fwd_grouped_bn_stats_bf16,
+// the stem's gm_conv2d_fwd_grouped_stats_bf16): stats = [G] x ([C / 64 slices][rows][64 x (sum,
+// sum of squares)] then 2C floats of coefficient scratch); ps[g] as for
+// gm_bn_fwd_stats_grouped_bf16 (C a multiple of 64).  One block per (slice, group).
 extern "C" int gm_bn_fwd_stats_finalize_grouped(const gm_bn_fwd* ps, int G, float* stats, int rows, void* stream) {
     const char* fn = "gm_bn_fwd_stats_finalize_grouped";
     int rc = check_groups_fwd(ps, G, fn);
     if (rc) return rc;
-    GM_REQUIRE(stats && rows >= 1 && ps[0].C == 64 && !ps[0].residual && ps[0].M >= 1,
-               "%s: C 64, no residual, rows >= 1", fn);
+    const int C = ps[0].C;
+    GM_REQUIRE(stats && rows >= 1 && C >= 64 && C % 64 == 0 && ps[0].M >= 1, "%s: C a multiple of 64, rows >= 1",
+               fn);
     ReduceArgs a{};
-    a.M = ps[0].M; a.C = 64; a.SW = 64; a.tpr_log = 3; a.nrc = rows;
+    a.M = ps[0].M; a.C = C; a.SW = 64; a.tpr_log = 3; a.nrc = rows;
     a.momentum = ps[0].momentum; a.eps = ps[0].eps;
     a.part = stats;
-    a.coef = stats + (size_t)rows * 128;
-    a.scr_stride = (unsigned long long)(rows + 1) * 128 * sizeof(float);
+    a.coef = stats + (size_t)rows * 2 * C;
+    a.scr_stride = (unsigned long long)(rows + 1) * 2 * C * sizeof(float);
     a.hdr_words = 0;
     for (int g = 0; g < G; ++g) {
         BnGroup& q = a.grp[g];
@@ -1917,6 +1924,47 @@ extern "C" int gm_bn_fwd_stats_finalize_grouped(const gm_bn_fwd* ps, int G, floa
         q.nbt = ps[g].num_batches_tracked;
         q.coef_out = ps[g].coef_out;
     }
-    hipLaunchKernelGGL(k_bn_stats_finalize, dim3(1, 1, G), dim3(kT), 0, as_stream(stream), a);
+    hipLaunchKernelGGL(k_bn_stats_finalize, dim3(1, C / 64, G), dim3(kT), 0, as_stream(stream), a);
     return check_launch("k_bn_stats_finalize");
+}
+
+// The apply after gm_bn_fwd_stats_finalize_grouped: y = relu?(x*sc + sh (+ residual)), the
+// coefficients read from the statistics buffer; one launch for the G groups when their
+// tensors are evenly strided (the view-batched trunk), else one per group.
+extern "C" int gm_bn_fwd_apply_grouped_bf16(const gm_bn_fwd* ps, int G, const float* stats, int rows, void* stream) {
+    const char* fn = "gm_bn_fwd_apply_grouped_bf16";
+    int rc = check_groups_fwd(ps, G, fn);
+    if (rc) return rc;
+    const gm_bn_fwd* p = ps;
+    const int C = p->C;
+    GM_REQUIRE(stats && rows >= 1 && C >= 64 && C % 64 == 0 && p->y, "%s: C a multiple of 64, rows >= 1, y", fn);
+    const long long gs = p->M * C;  // elements
+    bool strided = true;
+    for (int g = 1; g < G; ++g) {
+        const uint16_t* x0 = static_cast<const uint16_t*>(p->x);
+        strided = strided && ps[g].x == x0 + g * gs &&
+                  ps[g].y == static_cast<uint16_t*>(p->y) + g * gs &&
+                  (!p->residual || ps[g].residual == static_cast<const uint16_t*>(p->residual) + g * gs);
+    }
+    const long long cgs = (long long)(rows + 1) * 2 * C;
+    hipStream_t st = as_stream(stream);
+    const int ng = strided ? 1 : G;
+    for (int gi = 0; gi < ng; ++gi) {
+        ApplyArgs b{};
+        b.nvec = p->M * (C / 8); b.tpr_log = ilog2(C / 8); b.C = C; b.relu = p->relu;
+        b.x = ps[gi].x; b.res = ps[gi].residual; b.out = ps[gi].y;
+        b.coef = stats + gi * cgs + (size_t)rows * 2 * C;
+        b.gvec = strided ? gs / 8 : 0;
+        b.cgs = strided ? cgs : 0;
+        const dim3 g(apply_grid(b.nvec, C), strided ? G : 1);
+        if (p->residual) {
+            if (p->relu) hipLaunchKernelGGL((k_bn_apply<true, true, uint16_t>), g, dim3(kT), 0, st, b);
+            else hipLaunchKernelGGL((k_bn_apply<true, false, uint16_t>), g, dim3(kT), 0, st, b);
+        } else {
+            if (p->relu) hipLaunchKernelGGL((k_bn_apply<false, true, uint16_t>), g, dim3(kT), 0, st, b);
+            else hipLaunchKernelGGL((k_bn_apply<false, false, uint16_t>), g, dim3(kT), 0, st, b);
+        }
+        if ((rc = check_launch("k_bn_apply"))) return rc;
+    }
+    return GM_OK;
 }

@@ -37,7 +37,20 @@ struct RingGemmArgs {
     int M, N, Kr;            // per group
     int G, tiles_m, tiles_n, tiles;  // tiles = G * tiles_m * tiles_n
     long long gsA, gsB, gsO; // group strides (elements; gsB may be negative)
+    // forward, optional: BatchNorm partial rows of the stored output, as ConvArgs::stats
+    // (row = a wave's 64-pixel slab, group g at stats + g * 2 N (stats_rows + 1))
+    float* stats;
+    int stats_rows;
 };
+
+// sum over the lanes xor 8, 16, 32 (the lanes sharing lane % 8): DPP row rotate by 8, a
+// swizzle xor 16, a bpermute xor 32
+__device__ __forceinline__ float sum_lanes_8(float v) {
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false));
+    v += __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x401f));
+    v += __shfl_xor(v, 32);
+    return v;
+}
 
 __device__ __attribute__((aligned(16))) const uint4 g_rzero16[1] = {{0u, 0u, 0u, 0u}};
 
@@ -201,6 +214,9 @@ __global__ __launch_bounds__(512) void k_gemm_ring(RingGemmArgs a) {
             typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
             const int o = lane % OPR, rr = lane / OPR;
             const unsigned nb = (unsigned)(n0 + wn * (BN / 2) + 8 * o) * 2u;
+            float bs1[8], bs2[8];  // BatchNorm statistics (a.stats): channels 8 o .. + 7 of the wave
+#pragma unroll
+            for (int e = 0; e < 8; ++e) bs1[e] = bs2[e] = 0.f;
 #pragma unroll
             for (int ii = 0; ii < 2; ++ii) {
 #pragma unroll
@@ -244,10 +260,40 @@ __global__ __launch_bounds__(512) void k_gemm_ring(RingGemmArgs a) {
                         const u32x4 v = {pack_bf2(f0.x, f0.y), pack_bf2(f0.z, f0.w), pack_bf2(f1.x, f1.y),
                                          pack_bf2(f1.z, f1.w)};
                         __builtin_amdgcn_raw_buffer_store_b128(v, orsrc, off[it], 0, 0);
+                        if (a.stats) {  // the stored (bf16) values, rows past M out
+                            const bool ok = off[it] != 0xfffffff0u;
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) {
+                                const unsigned w = v[e >> 1];
+                                const float f = ok ? ((e & 1) ? bf_hi(w) : bf_lo(w)) : 0.f;
+                                bs1[e] += f;
+                                bs2[e] = fmaf(f, f, bs2[e]);
+                            }
+                        }
                     }
                 }
                 // the next half's staging writes after every read of this one
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            }
+            if (a.stats) {  // the wave's 64-pixel slab: partial row (m0 + 64 wm) / 64
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    if (NT == 1) {  // lanes sharing lane % 4: first fold xor 4
+                        bs1[e] += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(bs1[e]), 0x124, 0xf, 0xf, false));
+                        bs2[e] += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(bs2[e]), 0x124, 0xf, 0xf, false));
+                    }
+                    bs1[e] = sum_lanes_8(bs1[e]);
+                    bs2[e] = sum_lanes_8(bs2[e]);
+                }
+                if (rr == 0 && m0 + wm * 64 < a.M) {  // (a slab past M: no row)
+                    const int n = n0 + wn * (BN / 2) + 8 * o, row = (m0 + wm * 64) >> 6;
+                    float4* dst = reinterpret_cast<float4*>(a.stats + (size_t)g * 2 * a.N * (a.stats_rows + 1) +
+                                                            ((size_t)(n >> 6) * a.stats_rows + row) * 128 + (n & 63) * 2);
+                    dst[0] = make_float4(bs1[0], bs2[0], bs1[1], bs2[1]);
+                    dst[1] = make_float4(bs1[2], bs2[2], bs1[3], bs2[3]);
+                    dst[2] = make_float4(bs1[4], bs2[4], bs1[5], bs2[5]);
+                    dst[3] = make_float4(bs1[6], bs2[6], bs1[7], bs2[7]);
+                }
             }
             zero_acc();
             uk = 0;
@@ -278,7 +324,7 @@ bool conv1x1_ok(int R, int S, int sh, int sw, int ph, int pw, long long M, int K
 
 // Out = A . B^T (+ addend) per group; the caller checked conv1x1_ok
 int conv1x1_gemm(long long M, int Kr, int N, int G, const void* A, long long gsA, const void* B, long long gsB,
-                 void* out, long long gsO, const void* addend, hipStream_t st, const char* fn) {
+                 void* out, long long gsO, const void* addend, hipStream_t st, const char* fn, float* stats) {
     RingGemmArgs r;
     memset(&r, 0, sizeof(r));
     r.A = (const uint16_t*)A;
@@ -291,6 +337,8 @@ int conv1x1_gemm(long long M, int Kr, int N, int G, const void* A, long long gsA
     r.tiles_n = N / BN;
     r.tiles = G * r.tiles_m * r.tiles_n;
     r.gsA = gsA; r.gsB = gsB; r.gsO = gsO;
+    r.stats = addend ? nullptr : stats;
+    r.stats_rows = (int)((M + 63) / 64);
     const int grid = r.tiles < g_ring_cus ? r.tiles : g_ring_cus;  // persistent: one workgroup per CU
     auto go = [&](auto bnc) -> int {
         constexpr int BNt = decltype(bnc)::value, S = 4;

@@ -80,8 +80,30 @@ struct ConvArgs {
     // group g the tiles [g * tiles_g, (g + 1) * tiles_g), persistent ones gridDim / G workgroups
     int G, tiles_g;
     long long gs_in, gs_wt, gs_out;
+    // forward, optional: BatchNorm statistics of the stored (bf16) output from the epilogue -
+    // per group [Nout / 64 slices][stats_rows][64 channels][sum, sum of squares] fp32 partial
+    // rows (row = a wave's 64-pixel slab, (m0 + wm * BM / 2) / 64), then 2 Nout floats of
+    // coefficient area: group g at stats + g * 2 Nout (stats_rows + 1)
+    // (gm_bn_fwd_stats_finalize_grouped combines them)
+    float* stats;
+    int stats_rows;
     ConvCls cls[kMaxCls];
 };
+
+// sum over the 32 lanes of each half-wave (lanes 0-31, 32-63), in every lane of the half:
+// quad xor 1, quad xor 2, half-row mirror, row mirror (DPP adds), then the two rows of the
+// half through a swizzle (xor 16)
+template <int CTRL>
+__device__ __forceinline__ float dpp_add(float v) {
+    return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float half_wave_sum(float v) {
+    v = dpp_add<0xb1>(v);
+    v = dpp_add<0x4e>(v);
+    v = dpp_add<0x141>(v);
+    v = dpp_add<0x140>(v);
+    return v + __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x401f));
+}
 
 // sticky fault word of this translation unit (gm_device_faults): a split whose
 // turnstile wait timed out
@@ -124,7 +146,9 @@ __device__ __forceinline__ unsigned span_mask(int x, int d0, int s, int n, int l
 // addend loads are all in flight together instead of one dependent round trip per store.
 template <int MT, int NT, int BM, int BN>
 __device__ __forceinline__ void store_tile(const ConvArgs& a, const ConvCls& cl, int m0, int n0, int wm, int wn,
-                                           int fr, int fh, int M, floatx16 (&acc)[MT][NT], long long goff = 0) {
+                                           int fr, int fh, int M, floatx16 (&acc)[MT][NT], long long goff = 0,
+                                           int grp = 0) {
+    static_assert(BM / 2 == MT * 32, "store_tile: a wave holds BM / 2 pixels");
     const int PQ = cl.P * cl.Q;
     uint16_t* const outp = cl.out + goff;  // this group's output (and addend)
     const uint16_t* const addp = a.addend ? a.addend + goff : nullptr;
@@ -175,6 +199,43 @@ __device__ __forceinline__ void store_tile(const ConvArgs& a, const ConvCls& cl,
                     const u32x2 v = {pack_bf2(o0, o1), pack_bf2(o2, o3)};
                     __builtin_amdgcn_raw_buffer_store_b64(v, orsrc, boff(i, j, gq), 0, 0);
                 }
+        if (a.stats) {
+            // BatchNorm statistics of the stored values: per channel, the wave's pixels (lanes
+            // fr, fragments i) summed - the bf16-rounded outputs, zero outside the tile
+            float* const sp = a.stats + (size_t)grp * 2 * a.Nout * (a.stats_rows + 1);
+            const int row = (m0 + wm * (BM / 2)) / (BM / 2);
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+#pragma unroll
+                for (int gq = 0; gq < 4; ++gq) {
+                    float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int i = 0; i < MT; ++i) {
+                        const bool ok = boff(i, j, gq) != 0xfffffff0u;
+                        const unsigned w0 = pack_bf2(acc[i][j][4 * gq], acc[i][j][4 * gq + 1]);
+                        const unsigned w1 = pack_bf2(acc[i][j][4 * gq + 2], acc[i][j][4 * gq + 3]);
+                        const float f[4] = {ok ? bf_lo(w0) : 0.f, ok ? bf_hi(w0) : 0.f, ok ? bf_lo(w1) : 0.f,
+                                            ok ? bf_hi(w1) : 0.f};
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            s1[e] += f[e];
+                            s2[e] = fmaf(f[e], f[e], s2[e]);
+                        }
+                    }
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        s1[e] = half_wave_sum(s1[e]);
+                        s2[e] = half_wave_sum(s2[e]);
+                    }
+                    const int n = n0 + wn * (BN / 2) + j * 32 + 8 * gq + 4 * fh;
+                    if (fr == 0 && n < a.Nout && row < a.stats_rows) {  // (a slab past M: no row)
+                        float4* dst = reinterpret_cast<float4*>(
+                            sp + ((size_t)(n >> 6) * a.stats_rows + row) * 128 + (n & 63) * 2);
+                        dst[0] = make_float4(s1[0], s2[0], s1[1], s2[1]);
+                        dst[1] = make_float4(s1[2], s2[2], s1[3], s2[3]);
+                    }
+                }
+        }
         return;
     }
 #pragma unroll
@@ -692,7 +753,7 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
         if (t == 0) __hip_atomic_store(a.flags + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 
-    store_tile<MT, NT, BM, BN>(a, cl, m0, n0, wm, wn, fr, fh, M, acc, g * a.gs_out);
+    store_tile<MT, NT, BM, BN>(a, cl, m0, n0, wm, wn, fr, fh, M, acc, g * a.gs_out, g);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1328,7 +1389,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_h9(ConvArgs a, HaloArgs h) {
         }
         if (t == 0) __hip_atomic_store(a.flags + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    store_tile<MT, NT, 128, BN>(a, cl, m0, n0, wm, wn, fr, fh, M, acc, g * a.gs_out);
+    store_tile<MT, NT, 128, BN>(a, cl, m0, n0, wm, wn, fr, fh, M, acc, g * a.gs_out, g);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1454,6 +1515,12 @@ __global__ __launch_bounds__(256) void k_conv_rw(ConvArgs a, RwArgs r) {
         __builtin_amdgcn_make_buffer_rsrc(cl.out + g * a.gs_out, 0, (int)(out_bytes < 0x7fffffffu ? out_bytes : 0x7fffffffu),
                                           0x00020000);
 
+    // BatchNorm statistics (a.stats, forward): this thread's channel group t % 8 summed over
+    // the pixels it stores, combined over the workgroup after the last tile (partial row wg)
+    const int wg = tl;
+    float bs1[8], bs2[8];
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) bs1[jj] = bs2[jj] = 0.f;
     int bb = 0;
     for (; tl < r.tiles; tl += nwg) {
         const int nx = tl + nwg;
@@ -1545,6 +1612,15 @@ __global__ __launch_bounds__(256) void k_conv_rw(ConvArgs a, RwArgs r) {
                 __builtin_amdgcn_raw_buffer_store_b128(
                     __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), orsrc,
                     ok ? tbase + (unsigned)e * 16u : 0xfffffff0u, 0, 0);
+                if (a.stats) {
+                    const unsigned w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (int jj = 0; jj < 8; ++jj) {
+                        const float f = ok ? ((jj & 1) ? bf_hi(w4[jj >> 1]) : bf_lo(w4[jj >> 1])) : 0.f;
+                        bs1[jj] += f;
+                        bs2[jj] = fmaf(f, f, bs2[jj]);
+                    }
+                }
             }
             // the next tile's halo (issued before these stores) has landed; the stores may
             // still be in flight.  Then every wave is done with buffer bb and the LDS tile.
@@ -1593,6 +1669,21 @@ __global__ __launch_bounds__(256) void k_conv_rw(ConvArgs a, RwArgs r) {
         __builtin_amdgcn_s_waitcnt(kWaitStores);
         lds_barrier();
         bb ^= 1;
+    }
+    if (a.stats) {  // the partial row: [32 thread rows][64 channels][2] combined in the free LDS tile
+        float* red = reinterpret_cast<float*>(lds + WB + 2 * r.hbytes);  // 16 KB
+        const int r0 = t >> 3, cg = t & 7;
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+            red[r0 * 128 + (cg * 8 + jj) * 2] = bs1[jj];
+            red[r0 * 128 + (cg * 8 + jj) * 2 + 1] = bs2[jj];
+        }
+        __syncthreads();
+        if (t < 128) {
+            float s = 0.f;
+            for (int i = 0; i < 32; ++i) s += red[i * 128 + t];
+            a.stats[((size_t)g * (a.stats_rows + 1) + wg) * 128 + t] = s;
+        }
     }
 }
 
@@ -2153,6 +2244,10 @@ static size_t rw_plan(const ConvArgs& a, RwArgs& r) {
     return lds <= 160 * 1024 ? lds : 0;
 }
 
+// persistent: one workgroup per CU, split evenly over the view groups (workgroups per group)
+static int rw_per(const ConvArgs& a, const RwArgs& r) {
+    return r.tiles < 256 / a.G ? r.tiles : (256 / a.G > 0 ? 256 / a.G : 1);
+}
 static int launch_rw(const ConvArgs& a, const RwArgs& r, size_t lds, hipStream_t st) {
     static bool granted = false;  // the whole LDS (idempotent, safe to race)
     if (!granted) {
@@ -2164,9 +2259,7 @@ static int launch_rw(const ConvArgs& a, const RwArgs& r, size_t lds, hipStream_t
         }
         granted = true;
     }
-    // persistent: one workgroup per CU, split evenly over the view groups
-    const int per = r.tiles < 256 / a.G ? r.tiles : (256 / a.G > 0 ? 256 / a.G : 1);
-    const int grid = per * a.G;
+    const int grid = rw_per(a, r) * a.G;
     k_conv_rw<0><<<grid, 256, lds, st>>>(a, r);
     return check_launch("k_conv_rw");
 }
@@ -2314,7 +2407,12 @@ static int try_halo256(ConvArgs& a, hipStream_t st, void* ws, size_t ws_bytes) {
 static int pick_and_launch(ConvArgs& a, hipStream_t st, void* ws, size_t ws_bytes) {
     const bool three = stages() == 3;
     if (a.G < 1) a.G = 1;
+    // BatchNorm statistics (a.stats, forward): the partial rows of the kernel picked below -
+    // a wave's pixel slab for the tiled kernels (store_tile), a workgroup for the persistent ones
+    const long long Mg = (long long)a.N * a.cls[0].P * a.cls[0].Q;
+    auto slab_rows = [&](int slab) { a.stats_rows = (int)((Mg + slab - 1) / slab); };
     if (a.G == 1) {
+        slab_rows(64);
         const int r = try_halo256(a, st, ws, ws_bytes);
         if (r == 1) return GM_OK;
         if (r != 0) return r;
@@ -2322,12 +2420,19 @@ static int pick_and_launch(ConvArgs& a, hipStream_t st, void* ws, size_t ws_byte
     {
         RwArgs r;
         const size_t lds = rw_plan(a, r);
-        if (lds > 0) return launch_rw(a, r, lds, st);
+        if (lds > 0) {
+            a.stats_rows = rw_per(a, r);
+            return launch_rw(a, r, lds, st);
+        }
     }
     {
         StemArgs r;
         const size_t lds = stem_plan(a, r);
-        if (lds > 0) return launch_stem(a, r, lds, st);  // (no statistics: r.stats null)
+        if (lds > 0) {
+            r.stats = a.stats;  // the stem's own partial-row epilogue (same layout, C = 64)
+            a.stats_rows = r.stats_rows;
+            return launch_stem(a, r, lds, st);
+        }
     }
     TilePick p = pick_tile(a);
     if (p.splits > 1 && (!ws || ws_bytes < splitk_bytes(p) || p.tiles > kMaxSplitTiles)) {  // the unsplit choice
@@ -2343,6 +2448,7 @@ static int pick_and_launch(ConvArgs& a, hipStream_t st, void* ws, size_t ws_byte
         a.ws = reinterpret_cast<float*>(static_cast<char*>(ws) + splitk_flag_bytes(p.tiles));
     }
     const int hb = halo_bytes(a);
+    slab_rows(64);
     if (hb > 0 && hb + 2 * 128 * 128 <= 160 * 1024 && a.G > 1) {
         // view groups: k_conv_h9 when it takes the shape, else the lean kernel below
         if (p.tile != T128x128) a.splits = 1;
@@ -2356,6 +2462,7 @@ static int pick_and_launch(ConvArgs& a, hipStream_t st, void* ws, size_t ws_byte
         if (a.Nout >= 128) return launch_halo<128>(a, hb, st);
         return launch_halo<64>(a, hb, st);
     }
+    slab_rows(p.tile == T64x64 ? 32 : 64);
     switch (p.tile) {
     case T128x128: return three ? launch_igemm<128, 128, 3>(a, st) : launch_igemm<128, 128, 2>(a, st);
     case T128x64: return three ? launch_igemm<128, 64, 3>(a, st) : launch_igemm<128, 64, 2>(a, st);
@@ -2583,7 +2690,8 @@ extern "C" int gm_conv_set_pipe(int pipe) {
 namespace gm {
 bool conv1x1_ok(int R, int S, int sh, int sw, int ph, int pw, long long M, int Kr, int N);
 int conv1x1_gemm(long long M, int Kr, int N, int G, const void* A, long long gsA, const void* B, long long gsB,
-                 void* out, long long gsO, const void* addend, hipStream_t st, const char* fn);
+                 void* out, long long gsO, const void* addend, hipStream_t st, const char* fn,
+                 float* stats = nullptr);
 }  // namespace gm
 
 extern "C" int gm_conv2d_fwd_hw_bf16(const gm_conv_desc_hw* d, const void* x, const void* w, void* y,
@@ -2650,6 +2758,56 @@ extern "C" int gm_conv2d_fwd_grouped_bf16(const gm_conv_desc_hw* d, int G, const
 // The stem convolution (k_conv_stem's shapes) with the BatchNorm statistics of its output
 // accumulated in its epilogue: partial rows per workgroup, finalized by
 // gm_bn_fwd_stats_finalize_grouped (no statistics pass over the 205 MB output).
+// Forward convolution + the BatchNorm statistics of its stored output from the epilogue
+// (include/greedymml.h).  The statistics buffer: an upper bound of the partial rows any kernel
+// takes for the shape (the smallest pixel slab is 32; persistent kernels use <= 256 rows).
+extern "C" size_t gm_conv2d_fwd_bn_stats_floats(const gm_conv_desc_hw* d, int G) {
+    if (check_desc_hw(d) || G < 1 || G > 64) return 0;
+    ConvArgs a;
+    fwd_setup(d, reinterpret_cast<const void*>(16), reinterpret_cast<const void*>(16), reinterpret_cast<void*>(16), a);
+    a.G = G;
+    const long long M = (long long)d->N * a.cls[0].P * a.cls[0].Q;
+    long long rows = (M + 31) / 32;
+    if (rows < 256) rows = 256;
+    StemArgs r;
+    if (stem_plan(a, r) > 0 && r.stats_rows > rows) rows = r.stats_rows;
+    return (size_t)G * 2 * d->K * (size_t)(rows + 1);
+}
+
+extern "C" int gm_conv2d_fwd_grouped_bn_stats_bf16(const gm_conv_desc_hw* d, int G, const void* x, const void* w,
+                                                   long long w_stride, void* y, float* stats, size_t stats_floats,
+                                                   int* rows_out, void* ws, size_t ws_bytes, void* stream) {
+    int rc = check_desc_hw(d);
+    if (rc) return rc;
+    GM_REQUIRE(x && w && y && stats && rows_out, "conv fwd bn stats: null pointer");
+    GM_REQUIRE(G >= 1 && G <= 64, "conv fwd bn stats: view groups must be 1..64 (got %d)", G);
+    GM_REQUIRE(G == 1 || w_stride >= (long long)d->K * d->R * d->S * d->C ||
+                   -w_stride >= (long long)d->K * d->R * d->S * d->C,
+               "conv fwd bn stats: group weight stride %lld shorter than one weight", w_stride);
+    const size_t need = gm_conv2d_fwd_bn_stats_floats(d, G);
+    GM_REQUIRE(stats_floats >= need, "conv fwd bn stats: %zu floats < %zu", stats_floats, need);
+    ConvArgs a;
+    fwd_setup(d, x, w, y, a);
+    const long long M = (long long)d->N * a.cls[0].P * a.cls[0].Q;
+    if (d->K % 64 != 0 || (size_t)M * d->K * 2 >= 0x7ffff000u) {
+        set_error("conv fwd bn stats: K %% 64 != 0 or a group's output past 32-bit offsets");
+        return GM_E_UNSUP;
+    }
+    if (gm::conv1x1_ok(d->R, d->S, d->stride_h, d->stride_w, d->pad_h, d->pad_w, M, d->C, d->K)) {
+        *rows_out = (int)((M + 63) / 64);
+        return gm::conv1x1_gemm(M, d->C, d->K, G, x, M * d->C, w, w_stride, y, M * d->K, nullptr,
+                                as_stream(stream), "conv1x1 fwd", stats);
+    }
+    a.G = G;
+    a.gs_in = (long long)d->N * d->H * d->W * d->C;
+    a.gs_wt = w_stride;
+    a.gs_out = M * d->K;
+    a.stats = stats;
+    rc = pick_and_launch(a, as_stream(stream), ws, ws_bytes);
+    *rows_out = a.stats_rows;
+    return rc;
+}
+
 extern "C" int gm_conv_stem_stats_rows(const gm_conv_desc_hw* d, int G) {
     if (check_desc_hw(d) || G < 1 || G > 64) return 0;
     ConvArgs a;

@@ -47,6 +47,11 @@ STEM_XSEL = os.environ.get("GM_STEM_XSEL", "1") != "0"
 # the stem BN's statistics from the stem convolution's epilogue (GM_FUSED_STEM_STATS=0: the
 # statistics pass over the convolution's output, an A/B switch)
 FUSED_STEM_STATS = os.environ.get("GM_FUSED_STEM_STATS", "1") != "0"
+# every other BatchNorm's statistics from its producing convolution's epilogue, then a finalize
+# and a streaming apply instead of the single-launch BatchNorm's statistics read
+# (GM_EPI_BN_STATS=0: the single-launch BatchNorm)
+EPI_BN_STATS = os.environ.get("GM_EPI_BN_STATS", "1") != "0"
+_GM_E_UNSUP = -3
 
 
 def _nhwc(t):
@@ -190,7 +195,9 @@ class _VConvFn(torch.autograd.Function):
     """y = conv(X_g, W_g) for every view group g of the stacked X, one launch per pass."""
 
     @staticmethod
-    def forward(ctx, X, G, stride, pad, join, *weights):
+    def forward(ctx, X, G, stride, pad, join, stats, *weights):
+        """stats (optional dict): receives the BatchNorm statistics partial rows of the output
+        from the epilogue (gm_conv2d_fwd_grouped_bn_stats_bf16) when the kernel has them."""
         lib = L.load()
         ctx.join = join
         GN, C, H, W = X.shape
@@ -206,8 +213,21 @@ class _VConvFn(torch.autograd.Function):
         y = torch.empty(GN, K, P, Q, device=X.device, dtype=BF, memory_format=CL)
         d = _desc_hw(N, H, W, C, K, R, S, stride, stride, pad, pad)
         ws, nb = _splitk_g(X.device, _desc(N, H, W, C, K, R, S, stride, pad), G, False)
-        L.check(lib.gm_conv2d_fwd_grouped_bf16(ctypes.byref(d), G, xb.data_ptr(), wb.data_ptr(), sb, y.data_ptr(),
-                                               ws, nb, L.stream_of(X.device)), "gm_conv2d_fwd_grouped_bf16")
+        rc = _GM_E_UNSUP
+        if stats is not None and EPI_BN_STATS and K % 64 == 0:
+            nf = lib.gm_conv2d_fwd_bn_stats_floats(ctypes.byref(d), G)
+            part = torch.empty(max(nf, 1), device=X.device, dtype=torch.float32)
+            rows = ctypes.c_int(0)
+            rc = lib.gm_conv2d_fwd_grouped_bn_stats_bf16(ctypes.byref(d), G, xb.data_ptr(), wb.data_ptr(), sb,
+                                                         y.data_ptr(), part.data_ptr(), nf, ctypes.byref(rows), ws,
+                                                         nb, L.stream_of(X.device))
+            if rc == 0:
+                stats["part"], stats["rows"] = part, rows.value
+            elif rc != _GM_E_UNSUP:
+                L.check(rc, "gm_conv2d_fwd_grouped_bn_stats_bf16")
+        if rc != 0:
+            L.check(lib.gm_conv2d_fwd_grouped_bf16(ctypes.byref(d), G, xb.data_ptr(), wb.data_ptr(), sb, y.data_ptr(),
+                                                   ws, nb, L.stream_of(X.device)), "gm_conv2d_fwd_grouped_bf16")
         ctx.save_for_backward(xb, wt, *weights)
         ctx.meta = (G, N, stride, pad, st)
         return y
@@ -237,7 +257,7 @@ class _VConvFn(torch.autograd.Function):
                 return out
             dx = ctx.join.contribute(dgrad) if ctx.join is not None else dgrad(None)
         grads = [None] * G
-        want = [ctx.needs_input_grad[5 + g] for g in range(G)]
+        want = [ctx.needs_input_grad[6 + g] for g in range(G)]
         if any(want):
             dh = _desc_hw(N, H, W, C, K, R, S, stride, stride, pad, pad)
             tg = [sink_target(w) if wn else None for w, wn in zip(weights, want)]
@@ -273,11 +293,13 @@ class _VConvFn(torch.autograd.Function):
                                                          need, L.stream_of(dev)), "gm_conv2d_wgrad_grouped_bf16")
                 grads = [_like_param(dw[g].permute(0, 3, 1, 2), w) if wn else None
                          for g, (w, wn) in enumerate(zip(weights, want))]
-        return (dx, None, None, None, None, *grads)
+        return (dx, None, None, None, None, None, *grads)
 
 
-def vconv(X, convs, join=None):
-    """The G GMConv2d modules `convs` (one per view, same shape) over the stacked X."""
+def vconv(X, convs, join=None, stats=None):
+    """The G GMConv2d modules `convs` (one per view, same shape) over the stacked X; `stats`
+    (a dict) receives the output's BatchNorm partial rows for vbn(..., stats=) when the
+    convolution's kernel produces them."""
     c0 = convs[0]
     if not c0._hip_ok():
         raise L.GreedyMMLError("vtrunk conv: only the ResNet trunk's convolutions")
@@ -286,7 +308,7 @@ def vconv(X, convs, join=None):
     else:
         join = None
     with torch.autocast("cuda", enabled=False):
-        return _VConvFn.apply(X, len(convs), c0.stride[0], c0.padding[0], join, *[c.weight for c in convs])
+        return _VConvFn.apply(X, len(convs), c0.stride[0], c0.padding[0], join, stats, *[c.weight for c in convs])
 
 
 # ---- BatchNorm ---------------------------------------------------------------------
@@ -340,7 +362,7 @@ class _VBNFn(torch.autograd.Function):
     """relu?(BatchNorm_g(X_g) (+ residual_g)) per view group g of the stacked X."""
 
     @staticmethod
-    def forward(ctx, X, residual, G, bns, relu, join, *params):
+    def forward(ctx, X, residual, G, bns, relu, join, stats, *params):
         lib = L.load()
         ctx.join = join
         gammas, betas = params[:G], params[G:]
@@ -365,9 +387,17 @@ class _VBNFn(torch.autograd.Function):
                                  L.ptr(bn.running_var), float(bn.momentum), float(bn.eps), sm[g].data_ptr(),
                                  si[g].data_ptr(), L.ptr(bn.num_batches_tracked),
                                  coef[g].data_ptr() if maskx else 0))
-        buf = _bn_scratch_g(dev, M, C, G)
-        L.check(lib.gm_bn_fwd_train_grouped_bf16(L.arr(L.BnFwd, descs), G, buf.data_ptr(), buf.numel(),
-                                                 L.stream_of(dev)), "gm_bn_fwd_train_grouped_bf16")
+        if stats is not None and "part" in stats:  # partial rows from the convolution's epilogue
+            part, rows = stats.pop("part"), stats.pop("rows")
+            st = L.stream_of(dev)
+            L.check(lib.gm_bn_fwd_stats_finalize_grouped(L.arr(L.BnFwd, descs), G, part.data_ptr(), rows, st),
+                    "gm_bn_fwd_stats_finalize_grouped")
+            L.check(lib.gm_bn_fwd_apply_grouped_bf16(L.arr(L.BnFwd, descs), G, part.data_ptr(), rows, st),
+                    "gm_bn_fwd_apply_grouped_bf16")
+        else:
+            buf = _bn_scratch_g(dev, M, C, G)
+            L.check(lib.gm_bn_fwd_train_grouped_bf16(L.arr(L.BnFwd, descs), G, buf.data_ptr(), buf.numel(),
+                                                     L.stream_of(dev)), "gm_bn_fwd_train_grouped_bf16")
         ctx.save_for_backward(xb, y if relu and not maskx else coef, sm, si, *gammas, *betas)
         ctx.meta = (G, maskx, relu, residual is not None)
         return y
@@ -380,13 +410,13 @@ class _VBNFn(torch.autograd.Function):
         y, coef = (None, yc) if maskx else (yc, None)
         want_dres = has_res and ctx.needs_input_grad[1]
         dx, dres, gw, gb = _bn_backward(dy, y, xb, G, gammas, betas, sm, si, relu, want_dres, coef,
-                                        any(ctx.needs_input_grad[6:6 + G]), any(ctx.needs_input_grad[6 + G:]))
+                                        any(ctx.needs_input_grad[7:7 + G]), any(ctx.needs_input_grad[7 + G:]))
         if dres is not None and ctx.join is not None:
             dres = ctx.join.contribute(lambda add: dres if add is None else dres + add)
-        return (dx if ctx.needs_input_grad[0] else None, dres, None, None, None, None, *gw, *gb)
+        return (dx if ctx.needs_input_grad[0] else None, dres, None, None, None, None, None, *gw, *gb)
 
 
-def vbn(X, bns, residual=None, relu=False, residual_join=None):
+def vbn(X, bns, residual=None, relu=False, residual_join=None, stats=None):
     """The G GMBatchNorm2d modules `bns` (training mode) over the stacked X."""
     b0 = bns[0]
     if any(b.momentum is None or b.momentum != b0.momentum or b.eps != b0.eps for b in bns):
@@ -396,7 +426,7 @@ def vbn(X, bns, residual=None, relu=False, residual_join=None):
         residual_join.register()
         join = residual_join
     with torch.autocast("cuda", enabled=False):
-        return _VBNFn.apply(X, residual, len(bns), bns, bool(relu), join,
+        return _VBNFn.apply(X, residual, len(bns), bns, bool(relu), join, stats,
                             *[b.weight for b in bns], *[b.bias for b in bns])
 
 
@@ -582,16 +612,20 @@ def vblock(blocks, X):
     b0 = blocks[0]
     join = GradJoin()
     ds = b0.downsample is not None
+
+    def cbn(x, convs, bns, cjoin=None, **kw):  # conv -> BatchNorm, statistics from the conv's epilogue
+        st = {}
+        return vbn(vconv(x, convs, cjoin, stats=st), bns, stats=st, **kw)
     if ds:
-        idt = vbn(vconv(X, [b.downsample[0] for b in blocks], join), [b.downsample[1] for b in blocks])
+        idt = cbn(X, [b.downsample[0] for b in blocks], [b.downsample[1] for b in blocks], join)
     else:
         idt = X
-    out = vbn(vconv(X, [b.conv1 for b in blocks], join), [b.bn1 for b in blocks], relu=True)
+    out = cbn(X, [b.conv1 for b in blocks], [b.bn1 for b in blocks], join, relu=True)
     if hasattr(b0, "conv3"):  # Bottleneck
-        out = vbn(vconv(out, [b.conv2 for b in blocks]), [b.bn2 for b in blocks], relu=True)
-        return vbn(vconv(out, [b.conv3 for b in blocks]), [b.bn3 for b in blocks], residual=idt, relu=True,
+        out = cbn(out, [b.conv2 for b in blocks], [b.bn2 for b in blocks], relu=True)
+        return cbn(out, [b.conv3 for b in blocks], [b.bn3 for b in blocks], residual=idt, relu=True,
                    residual_join=None if ds else join)
-    return vbn(vconv(out, [b.conv2 for b in blocks]), [b.bn2 for b in blocks], residual=idt, relu=True,
+    return cbn(out, [b.conv2 for b in blocks], [b.bn2 for b in blocks], residual=idt, relu=True,
                residual_join=None if ds else join)
 
 

@@ -1,0 +1,92 @@
+"""BatchNorm statistics from the producing convolution's epilogue:
+gm_conv2d_fwd_grouped_bn_stats_bf16 -> gm_bn_fwd_stats_finalize_grouped -> gm_bn_fwd_apply_grouped_bf16
+against the single-launch BatchNorm forward (gm_bn_fwd_train_grouped_bf16) over the SAME
+convolution output, for every kernel family that writes the partial rows: k_conv_rw (layer 1),
+k_conv_h9 (3x3 view groups), k_conv_igemm_ut (strided 3x3 and 1x1, 128x128 / 64x64 tiles),
+k_gemm_ring (1x1 / s1), k_conv_halo (one group).  Checked: the statistics path was taken (partial
+rows exist), the convolution output is bit-identical, y / saved statistics / running statistics /
+num_batches_tracked / backward dx and parameter gradients agree to the two summation orders'
+rounding (the reference's own semantics: torchvision conv -> BatchNorm2d in training mode,
+/root/reference/src/model.py:65-76)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+CL = torch.channels_last
+
+SHAPES = [  # N per view, C, H, W, K, R, S, stride, pad, G
+    (4, 64, 56, 56, 64, 3, 3, 1, 1, 2),     # k_conv_rw
+    (8, 128, 28, 28, 128, 3, 3, 1, 1, 2),   # k_conv_h9
+    (8, 256, 14, 14, 256, 3, 3, 1, 1, 2),   # k_conv_h9 (split-K candidate)
+    (8, 512, 7, 7, 512, 3, 3, 1, 1, 2),     # layer 4
+    (4, 64, 56, 56, 128, 3, 3, 2, 1, 2),    # strided 3x3 (igemm_ut)
+    (4, 128, 28, 28, 256, 1, 1, 2, 0, 2),   # downsample 1x1 / s2
+    (2, 64, 9, 11, 128, 3, 3, 2, 1, 2),     # ragged, small M: 64x64 tiles
+    (4, 256, 14, 14, 64, 1, 1, 1, 0, 2),    # 1x1 / s1 reduce: k_gemm_ring BN = 64
+    (4, 64, 28, 28, 256, 1, 1, 1, 0, 3),    # 1x1 / s1 expand: k_gemm_ring BN = 128, 3 groups
+    (4, 128, 28, 28, 128, 3, 3, 1, 1, 1),   # one group: k_conv_halo
+]
+
+
+def _close(a, b, tol, what):
+    a, b = a.detach().float().cpu(), b.detach().float().cpu()
+    err = float((a - b).abs().max()) / (float(b.abs().max()) + 1e-12)
+    assert err <= tol, f"{what}: max |diff| / max |ref| = {err:.3e} > {tol}"
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
+@pytest.mark.parametrize("mode", ["res_relu", "relu"])
+def test_epilogue_statistics_match_single_launch_bn(shape, mode):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from greedy_multimodal_learning_amd.bn import GMBatchNorm2d
+    from greedy_multimodal_learning_amd.conv import GMConv2d
+    from greedy_multimodal_learning_amd.vtrunk import vbn, vconv
+    dev = torch.device("cuda:0")
+    N, C, H, W, K, R, S, st, pad, G = shape
+    g = torch.Generator().manual_seed(sum(shape) + len(mode))
+    x = torch.randn(G * N, C, H, W, generator=g).bfloat16().to(dev).contiguous(memory_format=CL)
+    convs = []
+    for _ in range(G):
+        m = GMConv2d(C, K, (R, S), stride=st, padding=pad, bias=False).to(dev)
+        with torch.no_grad():
+            m.weight.copy_(torch.randn(K, C, R, S, generator=g) / (C * R * S) ** 0.5 + 0.02)  # mean != 0
+        convs.append(m.to(memory_format=CL))
+    P, Q = (H + 2 * pad - R) // st + 1, (W + 2 * pad - S) // st + 1
+    res = torch.randn(G * N, K, P, Q, generator=g).bfloat16().to(dev).contiguous(memory_format=CL)
+    gy = torch.randn(G * N, K, P, Q, generator=g).bfloat16().to(dev).contiguous(memory_format=CL)
+    out = {}
+    for path in ("epi", "fused"):
+        bns = []
+        for i in range(G):
+            b = GMBatchNorm2d(K).to(dev)
+            gb = torch.Generator().manual_seed(i)
+            with torch.no_grad():
+                b.weight.copy_(torch.rand(K, generator=gb) + 0.5)
+                b.bias.copy_(torch.rand(K, generator=gb) - 0.5)
+                b.running_mean.copy_(torch.rand(K, generator=gb) * 0.2 - 0.1)
+            bns.append(b.train())
+        xs = x.clone().requires_grad_(True)
+        stats = {} if path == "epi" else None
+        y0 = vconv(xs, convs, stats=stats)
+        if path == "epi":
+            assert "part" in stats and stats["rows"] >= 1, "no partial rows from the convolution's epilogue"
+        y = vbn(y0, bns, residual=res if mode == "res_relu" else None, relu=True, stats=stats)
+        y.backward(gy)
+        out[path] = dict(y0=y0.detach().clone(), y=y.detach().clone(), dx=xs.grad.clone(),
+                         rm=[b.running_mean.clone() for b in bns], rv=[b.running_var.clone() for b in bns],
+                         nbt=[int(b.num_batches_tracked) for b in bns],
+                         dg=[b.weight.grad.clone() for b in bns], db=[b.bias.grad.clone() for b in bns])
+        for c in convs:
+            c.weight.grad = None
+    a, b = out["epi"], out["fused"]
+    assert torch.equal(a["y0"], b["y0"]), "the statistics epilogue changed the convolution output"
+    _close(a["y"], b["y"], 8e-3, "y")
+    for i in range(G):
+        _close(a["rm"][i], b["rm"][i], 1e-5, f"running_mean[{i}]")
+        _close(a["rv"][i], b["rv"][i], 1e-5, f"running_var[{i}]")
+        assert a["nbt"][i] == b["nbt"][i] == 1
+        _close(a["dg"][i], b["dg"][i], 5e-3, f"dgamma[{i}]")
+        _close(a["db"][i], b["db"][i], 5e-3, f"dbeta[{i}]")
+    _close(a["dx"], b["dx"], 2e-2, "dx")
