@@ -725,13 +725,43 @@ __global__ __launch_bounds__(kT) void k_stem_pool_bn_bwd(ReduceArgs a0, StemPool
 // the producer (k_conv_stem's epilogue): one block per view group combines the rows in fp64
 // (fixed order) and finalizes as k_bn_reduce's last block does.  a0.part / a0.coef: group 0's
 // rows and coefficient area, the groups scr_stride bytes apart.
-__global__ __launch_bounds__(kT) void k_bn_stats_finalize(ReduceArgs a0) {
+// 1024 threads per (64-channel slice, group): 32 lanes per partial row (one float4 each), 32
+// row groups with 8 rows' loads in flight each (the producers' rows are many - a 3x3 layer-2
+// convolution writes one per 64-pixel slab - and the combine sits on the forward's critical
+// path), fp64, then the row groups combined in a fixed order.
+constexpr int kFinT = 1024;
+__global__ __launch_bounds__(kFinT) void k_bn_stats_finalize(ReduceArgs a0) {
     const ReduceArgs a = group_args(a0);
-    __shared__ float red[kRedF + 4];
+    __shared__ double rd[kFinT / 32][128];
     const int t = threadIdx.x, cs = blockIdx.y;  // channel slice cs (64 channels)
+    const int lv = t & 31, rg = t >> 5;
     FinOps fo{};
-    if (t < a.SW) fo = fin_load<FWD>(a, cs * a.SW + t);
-    combine_finalize<FWD>(a, cs, red, fo);
+    if (t < 64) fo = fin_load<FWD>(a, cs * 64 + t);
+    if (a.nbt && cs == 0 && t == 0) *a.nbt += 1;
+    const float4* rows = reinterpret_cast<const float4*>(a.part + (size_t)cs * a.nrc * 128);
+    double d0 = 0.0, d1 = 0.0, d2 = 0.0, d3 = 0.0;
+    for (int i0 = rg; i0 < a.nrc; i0 += 8 * 32) {
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = i0 + u * 32;
+            v[u] = i < a.nrc ? rows[(size_t)i * 32 + lv] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            d0 += (double)v[u].x; d1 += (double)v[u].y; d2 += (double)v[u].z; d3 += (double)v[u].w;
+        }
+    }
+    rd[rg][4 * lv] = d0; rd[rg][4 * lv + 1] = d1; rd[rg][4 * lv + 2] = d2; rd[rg][4 * lv + 3] = d3;
+    __syncthreads();
+    if (t < 64) {
+        double S1 = 0.0, S2 = 0.0;
+        for (int i = 0; i < kFinT / 32; ++i) {
+            S1 += rd[i][2 * t];
+            S2 += rd[i][2 * t + 1];
+        }
+        finalize<FWD>(a, cs * 64 + t, S1, S2, 1.0 / (double)a.M, fo);
+    }
 }
 
 // ---------------------------------------------------------------------------------
@@ -1924,7 +1954,7 @@ extern "C" int gm_bn_fwd_stats_finalize_grouped(const gm_bn_fwd* ps, int G, floa
         q.nbt = ps[g].num_batches_tracked;
         q.coef_out = ps[g].coef_out;
     }
-    hipLaunchKernelGGL(k_bn_stats_finalize, dim3(1, C / 64, G), dim3(kT), 0, as_stream(stream), a);
+    hipLaunchKernelGGL(k_bn_stats_finalize, dim3(1, C / 64, G), dim3(kFinT), 0, as_stream(stream), a);
     return check_launch("k_bn_stats_finalize");
 }
 

@@ -80,30 +80,14 @@ struct ConvArgs {
     // group g the tiles [g * tiles_g, (g + 1) * tiles_g), persistent ones gridDim / G workgroups
     int G, tiles_g;
     long long gs_in, gs_wt, gs_out;
-    // forward, optional: BatchNorm statistics of the stored (bf16) output from the epilogue -
-    // per group [Nout / 64 slices][stats_rows][64 channels][sum, sum of squares] fp32 partial
-    // rows (row = a wave's 64-pixel slab, (m0 + wm * BM / 2) / 64), then 2 Nout floats of
-    // coefficient area: group g at stats + g * 2 Nout (stats_rows + 1)
-    // (gm_bn_fwd_stats_finalize_grouped combines them)
+    // forward, optional (k_conv_rw): BatchNorm statistics of the stored (bf16) output from the
+    // epilogue - per group [Nout / 64 slices][stats_rows][64 channels][sum, sum of squares] fp32
+    // partial rows (one per persistent workgroup), then 2 Nout floats of coefficient area: group
+    // g at stats + g * 2 Nout (stats_rows + 1) (gm_bn_fwd_stats_finalize_grouped combines them)
     float* stats;
     int stats_rows;
     ConvCls cls[kMaxCls];
 };
-
-// sum over the 32 lanes of each half-wave (lanes 0-31, 32-63), in every lane of the half:
-// quad xor 1, quad xor 2, half-row mirror, row mirror (DPP adds), then the two rows of the
-// half through a swizzle (xor 16)
-template <int CTRL>
-__device__ __forceinline__ float dpp_add(float v) {
-    return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
-}
-__device__ __forceinline__ float half_wave_sum(float v) {
-    v = dpp_add<0xb1>(v);
-    v = dpp_add<0x4e>(v);
-    v = dpp_add<0x141>(v);
-    v = dpp_add<0x140>(v);
-    return v + __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x401f));
-}
 
 // sticky fault word of this translation unit (gm_device_faults): a split whose
 // turnstile wait timed out
@@ -146,9 +130,7 @@ __device__ __forceinline__ unsigned span_mask(int x, int d0, int s, int n, int l
 // addend loads are all in flight together instead of one dependent round trip per store.
 template <int MT, int NT, int BM, int BN>
 __device__ __forceinline__ void store_tile(const ConvArgs& a, const ConvCls& cl, int m0, int n0, int wm, int wn,
-                                           int fr, int fh, int M, floatx16 (&acc)[MT][NT], long long goff = 0,
-                                           int grp = 0) {
-    static_assert(BM / 2 == MT * 32, "store_tile: a wave holds BM / 2 pixels");
+                                           int fr, int fh, int M, floatx16 (&acc)[MT][NT], long long goff = 0) {
     const int PQ = cl.P * cl.Q;
     uint16_t* const outp = cl.out + goff;  // this group's output (and addend)
     const uint16_t* const addp = a.addend ? a.addend + goff : nullptr;
@@ -199,43 +181,6 @@ __device__ __forceinline__ void store_tile(const ConvArgs& a, const ConvCls& cl,
                     const u32x2 v = {pack_bf2(o0, o1), pack_bf2(o2, o3)};
                     __builtin_amdgcn_raw_buffer_store_b64(v, orsrc, boff(i, j, gq), 0, 0);
                 }
-        if (a.stats) {
-            // BatchNorm statistics of the stored values: per channel, the wave's pixels (lanes
-            // fr, fragments i) summed - the bf16-rounded outputs, zero outside the tile
-            float* const sp = a.stats + (size_t)grp * 2 * a.Nout * (a.stats_rows + 1);
-            const int row = (m0 + wm * (BM / 2)) / (BM / 2);
-#pragma unroll
-            for (int j = 0; j < NT; ++j)
-#pragma unroll
-                for (int gq = 0; gq < 4; ++gq) {
-                    float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                    for (int i = 0; i < MT; ++i) {
-                        const bool ok = boff(i, j, gq) != 0xfffffff0u;
-                        const unsigned w0 = pack_bf2(acc[i][j][4 * gq], acc[i][j][4 * gq + 1]);
-                        const unsigned w1 = pack_bf2(acc[i][j][4 * gq + 2], acc[i][j][4 * gq + 3]);
-                        const float f[4] = {ok ? bf_lo(w0) : 0.f, ok ? bf_hi(w0) : 0.f, ok ? bf_lo(w1) : 0.f,
-                                            ok ? bf_hi(w1) : 0.f};
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            s1[e] += f[e];
-                            s2[e] = fmaf(f[e], f[e], s2[e]);
-                        }
-                    }
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        s1[e] = half_wave_sum(s1[e]);
-                        s2[e] = half_wave_sum(s2[e]);
-                    }
-                    const int n = n0 + wn * (BN / 2) + j * 32 + 8 * gq + 4 * fh;
-                    if (fr == 0 && n < a.Nout && row < a.stats_rows) {  // (a slab past M: no row)
-                        float4* dst = reinterpret_cast<float4*>(
-                            sp + ((size_t)(n >> 6) * a.stats_rows + row) * 128 + (n & 63) * 2);
-                        dst[0] = make_float4(s1[0], s2[0], s1[1], s2[1]);
-                        dst[1] = make_float4(s1[2], s2[2], s1[3], s2[3]);
-                    }
-                }
-        }
         return;
     }
 #pragma unroll
@@ -753,7 +698,7 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
         if (t == 0) __hip_atomic_store(a.flags + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 
-    store_tile<MT, NT, BM, BN>(a, cl, m0, n0, wm, wn, fr, fh, M, acc, g * a.gs_out, g);
+    store_tile<MT, NT, BM, BN>(a, cl, m0, n0, wm, wn, fr, fh, M, acc, g * a.gs_out);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1389,7 +1334,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_h9(ConvArgs a, HaloArgs h) {
         }
         if (t == 0) __hip_atomic_store(a.flags + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    store_tile<MT, NT, 128, BN>(a, cl, m0, n0, wm, wn, fr, fh, M, acc, g * a.gs_out, g);
+    store_tile<MT, NT, 128, BN>(a, cl, m0, n0, wm, wn, fr, fh, M, acc, g * a.gs_out);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1518,9 +1463,10 @@ __global__ __launch_bounds__(256) void k_conv_rw(ConvArgs a, RwArgs r) {
     // BatchNorm statistics (a.stats, forward): this thread's channel group t % 8 summed over
     // the pixels it stores, combined over the workgroup after the last tile (partial row wg)
     const int wg = tl;
-    float bs1[8], bs2[8];
+    typedef float f32x2 __attribute__((ext_vector_type(2)));  // channel pairs: packed fp32 math
+    f32x2 bs1[4], bs2[4];
 #pragma unroll
-    for (int jj = 0; jj < 8; ++jj) bs1[jj] = bs2[jj] = 0.f;
+    for (int k = 0; k < 4; ++k) bs1[k] = bs2[k] = f32x2{0.f, 0.f};
     int bb = 0;
     for (; tl < r.tiles; tl += nwg) {
         const int nx = tl + nwg;
@@ -1603,22 +1549,31 @@ __global__ __launch_bounds__(256) void k_conv_rw(ConvArgs a, RwArgs r) {
             }
             __syncthreads();
             const unsigned tbase = (unsigned)(((size_t)(b * a.Ho + p0) * a.Wo) * a.Nout * 2);
+            uint4 vv[4];  // the four reads together, then the stores (then the statistics)
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int e = t + 256 * u;  // 16-B chunk e of the tile: pixel e / 8, chunk e % 8
                 const int m = e >> 3, j = e & 7;
-                const bool ok = m < valid;
-                const uint4 v = *reinterpret_cast<const uint4*>(ot + (ok ? m : 0) * 128 + ((j ^ (m & 7)) << 4));
-                __builtin_amdgcn_raw_buffer_store_b128(
-                    __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), orsrc,
-                    ok ? tbase + (unsigned)e * 16u : 0xfffffff0u, 0, 0);
-                if (a.stats) {
-                    const unsigned w4[4] = {v.x, v.y, v.z, v.w};
+                vv[u] = *reinterpret_cast<const uint4*>(ot + (m < valid ? m : 0) * 128 + ((j ^ (m & 7)) << 4));
+            }
 #pragma unroll
-                    for (int jj = 0; jj < 8; ++jj) {
-                        const float f = ok ? ((jj & 1) ? bf_hi(w4[jj >> 1]) : bf_lo(w4[jj >> 1])) : 0.f;
-                        bs1[jj] += f;
-                        bs2[jj] = fmaf(f, f, bs2[jj]);
+            for (int u = 0; u < 4; ++u) {
+                const int e = t + 256 * u;
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, vv[u]), orsrc,
+                    (e >> 3) < valid ? tbase + (unsigned)e * 16u : 0xfffffff0u, 0, 0);
+            }
+            if (a.stats) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const bool ok = ((t + 256 * u) >> 3) < valid;
+                    const unsigned w4[4] = {ok ? vv[u].x : 0u, ok ? vv[u].y : 0u, ok ? vv[u].z : 0u,
+                                            ok ? vv[u].w : 0u};
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const f32x2 f = {bf_lo(w4[k]), bf_hi(w4[k])};
+                        bs1[k] += f;
+                        bs2[k] = __builtin_elementwise_fma(f, f, bs2[k]);
                     }
                 }
             }
@@ -1674,9 +1629,11 @@ __global__ __launch_bounds__(256) void k_conv_rw(ConvArgs a, RwArgs r) {
         float* red = reinterpret_cast<float*>(lds + WB + 2 * r.hbytes);  // 16 KB
         const int r0 = t >> 3, cg = t & 7;
 #pragma unroll
-        for (int jj = 0; jj < 8; ++jj) {
-            red[r0 * 128 + (cg * 8 + jj) * 2] = bs1[jj];
-            red[r0 * 128 + (cg * 8 + jj) * 2 + 1] = bs2[jj];
+        for (int k = 0; k < 4; ++k) {
+            red[r0 * 128 + (cg * 8 + 2 * k) * 2] = bs1[k].x;
+            red[r0 * 128 + (cg * 8 + 2 * k) * 2 + 1] = bs2[k].x;
+            red[r0 * 128 + (cg * 8 + 2 * k + 1) * 2] = bs1[k].y;
+            red[r0 * 128 + (cg * 8 + 2 * k + 1) * 2 + 1] = bs2[k].y;
         }
         __syncthreads();
         if (t < 128) {
@@ -2407,12 +2364,7 @@ static int try_halo256(ConvArgs& a, hipStream_t st, void* ws, size_t ws_bytes) {
 static int pick_and_launch(ConvArgs& a, hipStream_t st, void* ws, size_t ws_bytes) {
     const bool three = stages() == 3;
     if (a.G < 1) a.G = 1;
-    // BatchNorm statistics (a.stats, forward): the partial rows of the kernel picked below -
-    // a wave's pixel slab for the tiled kernels (store_tile), a workgroup for the persistent ones
-    const long long Mg = (long long)a.N * a.cls[0].P * a.cls[0].Q;
-    auto slab_rows = [&](int slab) { a.stats_rows = (int)((Mg + slab - 1) / slab); };
     if (a.G == 1) {
-        slab_rows(64);
         const int r = try_halo256(a, st, ws, ws_bytes);
         if (r == 1) return GM_OK;
         if (r != 0) return r;
@@ -2421,18 +2373,14 @@ static int pick_and_launch(ConvArgs& a, hipStream_t st, void* ws, size_t ws_byte
         RwArgs r;
         const size_t lds = rw_plan(a, r);
         if (lds > 0) {
-            a.stats_rows = rw_per(a, r);
+            a.stats_rows = rw_per(a, r);  // (a.stats: one partial row per workgroup)
             return launch_rw(a, r, lds, st);
         }
     }
     {
         StemArgs r;
         const size_t lds = stem_plan(a, r);
-        if (lds > 0) {
-            r.stats = a.stats;  // the stem's own partial-row epilogue (same layout, C = 64)
-            a.stats_rows = r.stats_rows;
-            return launch_stem(a, r, lds, st);
-        }
+        if (lds > 0) return launch_stem(a, r, lds, st);  // (no statistics: r.stats null)
     }
     TilePick p = pick_tile(a);
     if (p.splits > 1 && (!ws || ws_bytes < splitk_bytes(p) || p.tiles > kMaxSplitTiles)) {  // the unsplit choice
@@ -2448,7 +2396,6 @@ static int pick_and_launch(ConvArgs& a, hipStream_t st, void* ws, size_t ws_byte
         a.ws = reinterpret_cast<float*>(static_cast<char*>(ws) + splitk_flag_bytes(p.tiles));
     }
     const int hb = halo_bytes(a);
-    slab_rows(64);
     if (hb > 0 && hb + 2 * 128 * 128 <= 160 * 1024 && a.G > 1) {
         // view groups: k_conv_h9 when it takes the shape, else the lean kernel below
         if (p.tile != T128x128) a.splits = 1;
@@ -2462,7 +2409,6 @@ static int pick_and_launch(ConvArgs& a, hipStream_t st, void* ws, size_t ws_byte
         if (a.Nout >= 128) return launch_halo<128>(a, hb, st);
         return launch_halo<64>(a, hb, st);
     }
-    slab_rows(p.tile == T64x64 ? 32 : 64);
     switch (p.tile) {
     case T128x128: return three ? launch_igemm<128, 128, 3>(a, st) : launch_igemm<128, 128, 2>(a, st);
     case T128x64: return three ? launch_igemm<128, 64, 3>(a, st) : launch_igemm<128, 64, 2>(a, st);
@@ -2759,16 +2705,16 @@ extern "C" int gm_conv2d_fwd_grouped_bf16(const gm_conv_desc_hw* d, int G, const
 // accumulated in its epilogue: partial rows per workgroup, finalized by
 // gm_bn_fwd_stats_finalize_grouped (no statistics pass over the 205 MB output).
 // Forward convolution + the BatchNorm statistics of its stored output from the epilogue
-// (include/greedymml.h).  The statistics buffer: an upper bound of the partial rows any kernel
-// takes for the shape (the smallest pixel slab is 32; persistent kernels use <= 256 rows).
+// (include/greedymml.h).  The statistics buffer: an upper bound of the partial rows either
+// statistics kernel takes for the shape.
 extern "C" size_t gm_conv2d_fwd_bn_stats_floats(const gm_conv_desc_hw* d, int G) {
     if (check_desc_hw(d) || G < 1 || G > 64) return 0;
     ConvArgs a;
     fwd_setup(d, reinterpret_cast<const void*>(16), reinterpret_cast<const void*>(16), reinterpret_cast<void*>(16), a);
     a.G = G;
     const long long M = (long long)d->N * a.cls[0].P * a.cls[0].Q;
-    long long rows = (M + 31) / 32;
-    if (rows < 256) rows = 256;
+    long long rows = (M + 63) / 64;  // k_gemm_ring: one row per 64-pixel slab
+    if (rows < 256) rows = 256;       // k_conv_rw, k_conv_stem: one per workgroup
     StemArgs r;
     if (stem_plan(a, r) > 0 && r.stats_rows > rows) rows = r.stats_rows;
     return (size_t)G * 2 * d->K * (size_t)(rows + 1);
@@ -2802,10 +2748,20 @@ extern "C" int gm_conv2d_fwd_grouped_bn_stats_bf16(const gm_conv_desc_hw* d, int
     a.gs_in = (long long)d->N * d->H * d->W * d->C;
     a.gs_wt = w_stride;
     a.gs_out = M * d->K;
-    a.stats = stats;
-    rc = pick_and_launch(a, as_stream(stream), ws, ws_bytes);
-    *rows_out = a.stats_rows;
-    return rc;
+    // the kernels whose epilogue stages the output tile anyway (k_conv_rw; k_gemm_ring above):
+    // there the sums are a few VALU per stored 16-B chunk.  The tiled 3x3 / strided kernels
+    // (k_conv_h9, k_conv_igemm_ut) store from the MFMA layout, where the per-channel sums need
+    // a 32-lane reduction per value: measured +4-10 us per launch (10-15 %) and one partial row
+    // per 64-pixel slab (a 1.5k-row combine) - more than the statistics read they replace
+    RwArgs rw;
+    if (a.G > 1 && rw_plan(a, rw) > 0) {
+        a.stats = stats;
+        rc = pick_and_launch(a, as_stream(stream), ws, ws_bytes);
+        *rows_out = a.stats_rows;
+        return rc;
+    }
+    set_error("conv fwd bn stats: no statistics epilogue for this shape's kernel");
+    return GM_E_UNSUP;
 }
 
 extern "C" int gm_conv_stem_stats_rows(const gm_conv_desc_hw* d, int G) {

@@ -593,14 +593,16 @@ int gm_conv_stem_stats_rows(const gm_conv_desc_hw* d, int G);
 int gm_conv2d_fwd_grouped_stats_bf16(const gm_conv_desc_hw* d, int G, const void* x, const void* w,
                                      long long w_stride, void* y, float* stats, int rows, void* stream);
 int gm_bn_fwd_stats_finalize_grouped(const gm_bn_fwd* ps, int G, float* stats, int rows, void* stream);
-/* The same for every trunk convolution whose BatchNorm follows it (replaces the statistics read
- * of the single-launch BatchNorm forward, gm_bn_fwd_train_grouped_bf16): the convolution's
- * epilogue (k_conv_rw, k_conv_h9, k_conv_igemm_ut / halo, k_gemm_ring) sums each wave's pixel
- * slab - or each persistent workgroup's pixels - of its stored bf16 outputs per channel
- * (fp32), writing per group [K / 64 slices][rows][64 x (sum, sum of squares)] then 2K floats
- * of coefficient area (group g at stats + g * 2K (rows + 1)).  stats holds stats_floats >=
- * gm_conv2d_fwd_bn_stats_floats(d, G) floats; *rows_out receives the rows of the kernel picked.
- * GM_E_UNSUP (nothing launched) when K % 64 != 0 or a group's output needs 64-bit offsets.
+/* The same for the trunk convolutions whose kernel stages its output tile anyway (replaces the
+ * statistics read of the single-launch BatchNorm forward, gm_bn_fwd_train_grouped_bf16): the
+ * layer-1 resident-weight kernel (k_conv_rw, view groups G >= 2: one partial row per persistent
+ * workgroup) and the 1x1 / s1 GEMM (k_gemm_ring: one per wave's 64-pixel slab) sum their
+ * stored bf16 outputs per channel (fp32), writing per group [K / 64 slices][rows][64 x (sum,
+ * sum of squares)] then 2K floats of coefficient area (group g at stats + g * 2K (rows + 1)).
+ * stats holds stats_floats >= gm_conv2d_fwd_bn_stats_floats(d, G) floats; *rows_out receives
+ * the rows of the kernel picked.  GM_E_UNSUP (nothing launched) for any other shape (the MFMA-
+ * layout epilogues of k_conv_h9 / k_conv_igemm_ut would need a 32-lane reduction per value:
+ * measured slower than the statistics read), K % 64 != 0 or 64-bit output offsets.
  * Then gm_bn_fwd_stats_finalize_grouped(ps, G, stats, rows) (C = K, any multiple of 64, residual
  * allowed) and gm_bn_fwd_apply_grouped_bf16: y = relu?(x*sc + sh (+ residual)) from the
  * coefficients it left in stats, one launch for evenly strided groups.  Replaces

@@ -197,19 +197,27 @@ def test_model_stacked_vs_per_view(dev, kind):
     y = torch.randint(0, 40, (B,), device=dev)
     assert vtrunk.usable(a, [getattr(a, f"net_view_{i}") for i in range(V)], x)
     outs = {}
-    # a: the stacked trunk as the step runs it; d: the same with the single-launch BatchNorm
-    # statistics (GM_EPI_BN_STATS=0) - the per-view trunk's BatchNorm kernels and summation
-    # order, so that the direct bf16-vs-bf16 comparison below isolates the stacking (the
-    # epilogue statistics differ from them by summation order only: test_gpu_bn_epi.py)
-    for m, on, epi in ((a, True, True), (b, False, True), (d, True, False)):
+    # a: the stacked trunk as the step runs it.  The direct bf16-vs-bf16 comparison below must
+    # isolate the stacking from summation order, which at this batch decides ReLU masks and
+    # with them tens of percent of the gradient: b (per-view) and d (stacked) both run the
+    # two-kernel BatchNorm (gm_bn_set_fused_mode(0): its partition depends on (M, C) alone,
+    # where the single-launch one sizes its grid for the launch's view groups and the
+    # residency plan) and d takes the BatchNorm statistics from that reduction instead of
+    # the convolution epilogue (GM_EPI_BN_STATS=0; the epilogue statistics differ from it
+    # by summation order only: test_gpu_bn_epi.py)
+    from greedy_multimodal_learning_amd import _lib as L
+    lib = L.load()
+    for m, on, epi, fused in ((a, True, True, 2), (b, False, True, 0), (d, True, False, 0)):
         old, old_epi = vtrunk.ENABLED, vtrunk.EPI_BN_STATS
         vtrunk.ENABLED, vtrunk.EPI_BN_STATS = on, epi
+        L.check(lib.gm_bn_set_fused_mode(fused), "gm_bn_set_fused_mode")
         try:
             with torch.autocast("cuda", dtype=torch.bfloat16):
                 _, o, _, _ = m(x)
             blend_loss([t.float() for t in o], y).backward()
         finally:
             vtrunk.ENABLED, vtrunk.EPI_BN_STATS = old, old_epi
+            L.check(lib.gm_bn_set_fused_mode(2), "gm_bn_set_fused_mode")  # the default
         if epi:
             outs[on] = [t.detach().float() for t in o]
     _, o, _, _ = c(x.float())
