@@ -136,9 +136,9 @@ def conv_roofline(conv, traffic, dtype="bf16", workload="C2"):
             "C4": "every ResNet-18 trunk shape, the 4 views per launch (the view-batched trunk)",
             "C5": "every ResNet-50 trunk shape, the 12 views per launch (the view-batched trunk)"}[workload]
     return {"kernel": "trunk convolutions (bf16 MFMA: k_conv_stem pixel-pair stem, k_conv_rw layer-1 "
-                      "resident-weight, k_conv_h9 3x3 halo, k_conv_igemm_ut strided/1x1 fwd + input "
-                      "grad, k_conv_wgrad4 + k_wgrad_sum weight grad; " + what + " at the step's batch, "
-                      "tools/trunk_table.py)",
+                      "resident-weight, k_conv_h9 3x3 halo, k_conv_igemm_ut strided fwd + input grad, "
+                      "k_gemm_ring 1x1/s1 fwd + input grad, k_wgrad_ring / k_wgrad_halo64 / k_conv_wgrad4 + "
+                      "k_wgrad_sum weight grad; " + what + " at the step's batch, tools/trunk_table.py)",
             "bound": "mfma", "achieved": round(flops / secs / 1e12, 1), "peak": MFMA_PEAK_TFS, "unit": "TFLOP/s",
             "frac": round(flops / secs / 1e12 / MFMA_PEAK_TFS, 4), "traffic": traffic,
             "alg_flops_per_launch": round(flops / launches), "avg_launch_us": round(secs / launches * 1e6, 2)}
@@ -340,7 +340,9 @@ def main():
             "vs_baseline": None,
             "dtype": a.dtype,
             "data": f"synthetic N(0,1) [B,{V},3,224,224] + uniform labels, resident in HBM; random-init weights",
-            "config": {"workload": WL["desc"] + ", guided gating (training_guided.gin eps 0.01, window 5, unlocked)",
+            "config": {"workload": WL["desc"] + ", guided gating (training_guided.gin eps 0.01, window 5, unlocked;"
+                                   " decided on bf16-trunk gradients: d_BDR within ~6.5e-3 of eps may decide"
+                                   " unlike fp32, INTEGRATION.md section 3)",
                        "params": step.flat.total,
                        "global_batch": B * world, "per_gpu_batch": B, "image": a.size,
                        "parallelism": f"dp{world}", "samples_per_s": round(world * B * a.steps / elapsed, 2),
