@@ -14,7 +14,7 @@ LIB_PATH = os.path.join(_PKG, "libgreedymml_hip.so")
 
 GM_F32, GM_BF16 = 0, 1
 GM_NCHW, GM_NHWC = 0, 1
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 c_int, c_float, c_void_p, c_size_t = ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
 c_float_p = ctypes.c_void_p  # device pointers are opaque
@@ -217,14 +217,15 @@ class BnFwd(ctypes.Structure):
                 ("residual", c_void_p), ("y", c_void_p), ("gamma", c_void_p), ("beta", c_void_p),
                 ("running_mean", c_void_p), ("running_var", c_void_p), ("momentum", c_float),
                 ("eps", c_float), ("save_mean", c_void_p), ("save_invstd", c_void_p),
-                ("num_batches_tracked", c_void_p), ("coef_out", c_void_p)]
+                ("num_batches_tracked", c_void_p), ("coef_out", c_void_p), ("relu_mask", c_void_p)]
 
 
 class BnBwd(ctypes.Structure):
     _fields_ = [("M", ctypes.c_longlong), ("C", c_int), ("relu", c_int), ("dy", c_void_p),
                 ("y", c_void_p), ("x", c_void_p), ("gamma", c_void_p), ("save_mean", c_void_p),
                 ("save_invstd", c_void_p), ("dx", c_void_p), ("dres", c_void_p), ("dgamma", c_void_p),
-                ("dbeta", c_void_p), ("accumulate", c_int), ("pad", c_int), ("fwd_coef", c_void_p)]
+                ("dbeta", c_void_p), ("accumulate", c_int), ("pad", c_int), ("fwd_coef", c_void_p),
+                ("relu_mask", c_void_p)]
 
 
 EXPORTS.update({

@@ -92,6 +92,27 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
     return make_uint4(pack_bf2(f[0], f[1]), pack_bf2(f[2], f[3]), pack_bf2(f[4], f[5]), pack_bf2(f[6], f[7]));
 }
 
+// The ReLU mask of 8 stored bf16 values as one byte (bit j: value j > 0, i.e. the bf16 half as a
+// signed 16-bit integer is positive - exactly the backward's y > 0 test on the stored y), and
+// back as 8 bf16 values (1.0 where set) that the y-mask code paths test unchanged
+__device__ __forceinline__ unsigned mask_byte(uint4 w) {
+    const unsigned v[4] = {w.x, w.y, w.z, w.w};
+    unsigned b = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        b |= ((int)(short)(v[k] & 0xffffu) > 0 ? 1u : 0u) << (2 * k);
+        b |= ((int)v[k] > 0x0000ffff ? 1u : 0u) << (2 * k + 1);
+    }
+    return b;
+}
+__device__ __forceinline__ uint4 mask_vals(unsigned b) {
+    unsigned v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        v[k] = ((b >> (2 * k)) & 1u ? 0x3f80u : 0u) | ((b >> (2 * k + 1)) & 1u ? 0x3f800000u : 0u);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
 // Per-view-group operands: a grouped launch (gm_bn_*_grouped_bf16) normalises G views
 // stacked along the batch, each with its own parameters, statistics and scratch, in one
 // grid (blockIdx.z = group); every kernel starts from group_args().
@@ -114,6 +135,8 @@ struct BnGroup {
     const uint4* res;
     uint4* yout;
     uint4* dres_out;
+    uint8_t* mask_out;      // fwd (relu + residual), optional: the ReLU mask, one byte per 8 channels
+    const uint8_t* ymask;   // bwd: that mask in place of y (k_bn_bwd_fused<BWD_RELU, ..., YM>)
 };
 
 struct ReduceArgs {
@@ -143,6 +166,8 @@ struct ReduceArgs {
     const uint4* res;    // fused fwd: residual
     uint4* yout;         // fused fwd: output / fused bwd: dx
     uint4* dres_out;     // fused bwd: dres
+    uint8_t* mask_out;   // fused fwd, optional: ReLU mask bytes (bit j: channel 8 v + j of vector v > 0)
+    const uint8_t* ymask;  // fused bwd: the mask in place of y
     unsigned spin_limit; // fused: poll budget of the coefficient hand-off
     int redundant;       // fused, small maps: every block combines the partial rows itself
     unsigned long long scr_stride;  // bytes between the groups' coefficient + partial areas
@@ -162,6 +187,7 @@ __device__ __forceinline__ ReduceArgs group_args(const ReduceArgs& a0) {
     a.dgamma = q.dgamma; a.dbeta = q.dbeta; a.nbt = q.nbt;
     a.coef_out = q.coef_out; a.fcoef = q.fcoef;
     a.res = q.res; a.yout = q.yout; a.dres_out = q.dres_out;
+    a.mask_out = q.mask_out; a.ymask = q.ymask;
     const unsigned long long off = (unsigned long long)g * a0.scr_stride;
     a.counter = a0.counter + g * a0.hdr_words;
     a.coef = reinterpret_cast<float*>(reinterpret_cast<char*>(a0.coef) + off);
@@ -1074,7 +1100,9 @@ __global__ __launch_bounds__(kT, NR == 16 ? 2 : NR == 8 ? 3 : 4) void k_bn_fwd_f
             f[j] = RELU ? fmaxf(zz, 0.f) : zz;
             if (!fresh) f[j] = __builtin_nanf("");  // poisoned (fmaxf would turn NaN into 0)
         }
-        a.yout[i] = pack8(f);
+        const uint4 w = pack8(f);
+        a.yout[i] = w;
+        if (RES && RELU && a.mask_out) a.mask_out[i] = (uint8_t)mask_byte(w);
     };
     if (NR > 0) {
 #pragma unroll
@@ -1099,7 +1127,7 @@ __global__ __launch_bounds__(kT, NR == 16 ? 2 : NR == 8 ? 3 : 4) void k_bn_fwd_f
 // Fused backward, same scheme as k_bn_fwd_fused: the block holds its x / dy (/ y)
 // strip in registers (NR 4 or 8) or re-reads it (NR 0), the slice's last block
 // publishes (a, b, c) and every block writes dx = a*dz + b*x + c (and dres = dz).
-template <int MODE, bool DRES, int NR>
+template <int MODE, bool DRES, int NR, bool YM = false>
 __global__ __launch_bounds__(kT, NR == 8 ? 2 : 3) void k_bn_bwd_fused(ReduceArgs a0) {
     const ReduceArgs a = group_args(a0);
     __shared__ float red[kRedF + 4];
@@ -1119,6 +1147,8 @@ __global__ __launch_bounds__(kT, NR == 8 ? 2 : 3) void k_bn_bwd_fused(ReduceArgs
     const uint4* X = static_cast<const uint4*>(a.x);
     const uint4* DY = static_cast<const uint4*>(a.dy);
     const uint4* Y = static_cast<const uint4*>(a.y);
+    // y for the ReLU mask, or (YM) the forward's mask byte expanded to 1.0 / 0 bf16 values
+    auto ldy = [&](long long i) { return YM ? mask_vals(a.ymask[i]) : Y[i]; };
     float mu[8], fsc[8], fsh[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -1147,7 +1177,7 @@ __global__ __launch_bounds__(kT, NR == 8 ? 2 : 3) void k_bn_bwd_fused(ReduceArgs
             const uint4 wx = X[i], wd = DY[i];
             vx[u] = r < rend ? wx : z;
             vd[u] = r < rend ? wd : z;
-            if (MODE == BWD_RELU) vy[u] = Y[i];
+            if (MODE == BWD_RELU) vy[u] = ldy(i);
         }
 #pragma unroll
         for (int u = 0; u < NV; ++u)
@@ -1162,14 +1192,14 @@ __global__ __launch_bounds__(kT, NR == 8 ? 2 : 3) void k_bn_bwd_fused(ReduceArgs
                 const long long i = r * vpr + cv + u * st;
                 wx[u] = X[i];
                 wd[u] = DY[i];
-                if (MODE == BWD_RELU) wy[u] = Y[i];
+                if (MODE == BWD_RELU) wy[u] = ldy(i);
             }
 #pragma unroll
             for (int u = 0; u < US; ++u) accum_vals<MODE>(wx[u], wd[u], MODE == BWD_RELU ? wy[u] : z, mu, s1, s2, fsc, fsh);
         }
         for (; r < rend; r += rpp) {
             const long long i = r * vpr + cv;
-            accum_vals<MODE>(X[i], DY[i], MODE == BWD_RELU ? Y[i] : z, mu, s1, s2, fsc, fsh);
+            accum_vals<MODE>(X[i], DY[i], MODE == BWD_RELU ? ldy(i) : z, mu, s1, s2, fsc, fsh);
         }
     }
 
@@ -1261,14 +1291,14 @@ __global__ __launch_bounds__(kT, NR == 8 ? 2 : 3) void k_bn_bwd_fused(ReduceArgs
                 const long long i = r * vpr + cv + u * st;
                 wx[u] = X[i];
                 wd[u] = DY[i];
-                if (MODE == BWD_RELU) wy[u] = Y[i];
+                if (MODE == BWD_RELU) wy[u] = ldy(i);
             }
 #pragma unroll
             for (int u = 0; u < US; ++u) out(wx[u], wd[u], MODE == BWD_RELU ? wy[u] : z, r * vpr + cv + u * st);
         }
         for (; r < rend; r += rpp) {
             const long long i = r * vpr + cv;
-            out(X[i], DY[i], MODE == BWD_RELU ? Y[i] : z, i);
+            out(X[i], DY[i], MODE == BWD_RELU ? ldy(i) : z, i);
         }
     }
 }
@@ -1287,6 +1317,7 @@ struct ApplyArgs {
     const float* fcoef;  // bwd MASKX: the forward's sc[C], sh[C]
     long long gvec;      // fwd apply, view groups (gridDim.y): group g's x / res / out gvec
     long long cgs;       // vectors and its coefficients cgs floats after group 0's
+    uint8_t* mask_out;   // fwd (relu + residual), optional: the ReLU mask bytes (as gvec)
 };
 
 __device__ __forceinline__ void load_coef(const float* p, int cg, float* c) {
@@ -1318,6 +1349,7 @@ __global__ __launch_bounds__(kT) void k_bn_apply(ApplyArgs a) {
             f[j] = RELU ? fmaxf(z, 0.f) : z;
         }
         V8<E>::st(a.out, i, f);
+        if (RES && RELU && std::is_same<E, uint16_t>::value && a.mask_out) a.mask_out[i] = (uint8_t)mask_byte(pack8(f));
     };
     for (; v + stride < a.nvec; v += 2 * stride) {
         one(v);
@@ -1434,7 +1466,8 @@ const Occ& occupancy() {
 #define GM_F(NR) occ_min({k_bn_fwd_fused<true, true, NR>, k_bn_fwd_fused<true, false, NR>, \
                           k_bn_fwd_fused<false, true, NR>, k_bn_fwd_fused<false, false, NR>})
 #define GM_B(NR) occ_min({k_bn_bwd_fused<BWD_RELUX, false, NR>, k_bn_bwd_fused<BWD_RELU, true, NR>, \
-                          k_bn_bwd_fused<BWD_RELU, false, NR>, k_bn_bwd_fused<BWD, false, NR>})
+                          k_bn_bwd_fused<BWD_RELU, false, NR>, k_bn_bwd_fused<BWD, false, NR>,       \
+                          k_bn_bwd_fused<BWD_RELU, true, NR, true>, k_bn_bwd_fused<BWD_RELU, false, NR, true>})
         r.fwd[0] = GM_F(4); r.fwd[1] = GM_F(8); r.fwd[2] = GM_F(16); r.fwd[3] = GM_F(0);
         r.bwd[0] = GM_B(4); r.bwd[1] = GM_B(8); r.bwd[2] = GM_B(0);
 #undef GM_F
@@ -1620,6 +1653,7 @@ void fill_fwd(ReduceArgs& a, const gm_bn_fwd* ps, int G, bool grouped, const Pla
         q.coef_out = ps[g].coef_out;
         q.res = static_cast<const uint4*>(ps[g].residual);
         q.yout = static_cast<uint4*>(ps[g].y);
+        q.mask_out = static_cast<uint8_t*>(ps[g].relu_mask);
     }
     BnGroup& q = a.grp[0];  // the single-group fields (host bookkeeping only: kernels read grp[])
     a.x = q.x; a.gamma = q.gamma; a.beta = q.beta; a.rmean = q.rmean; a.rvar = q.rvar;
@@ -1669,6 +1703,7 @@ int bn_fwd_train(const gm_bn_fwd* ps, int G, bool grouped, void* scratch, size_t
         ApplyArgs b{};
         b.nvec = p->M * (p->C / 8); b.tpr_log = ilog2(p->C / 8); b.C = p->C; b.relu = p->relu;
         b.x = ps[gi].x; b.res = ps[gi].residual; b.out = ps[gi].y;
+        b.mask_out = static_cast<uint8_t*>(ps[gi].relu_mask);
         b.coef = reinterpret_cast<float*>(reinterpret_cast<char*>(a.coef) + gi * a.scr_stride);
         const int g = apply_grid(b.nvec, p->C);
         if (p->residual) {
@@ -1733,6 +1768,7 @@ int bn_bwd(const gm_bn_bwd* ps, int G, bool grouped, void* scratch, size_t bytes
         q.fcoef = ps[g].fwd_coef;
         q.yout = static_cast<uint4*>(ps[g].dx);
         q.dres_out = static_cast<uint4*>(ps[g].dres);
+        q.ymask = static_cast<const uint8_t*>(ps[g].relu_mask);
     }
     hipStream_t st = as_stream(stream);
     Plan fp;
@@ -1745,10 +1781,13 @@ int bn_bwd(const gm_bn_bwd* ps, int G, bool grouped, void* scratch, size_t bytes
         a.spin_limit = spin_limit();
         a.redundant = redundant_ok(a.nrc);
         const dim3 g(fp.nrc, fp.nslice, G);
-#define GM_BN_BWD_FUSED_LAUNCH(NR)                                                                           \
-    if (maskx) hipLaunchKernelGGL((k_bn_bwd_fused<BWD_RELUX, false, NR>), g, dim3(kT), 0, st, a);            \
-    else if (p->relu && p->dres) hipLaunchKernelGGL((k_bn_bwd_fused<BWD_RELU, true, NR>), g, dim3(kT), 0, st, a); \
-    else if (p->relu) hipLaunchKernelGGL((k_bn_bwd_fused<BWD_RELU, false, NR>), g, dim3(kT), 0, st, a);    \
+        const bool ym = p->relu && p->relu_mask && !maskx;  // the forward's mask bytes in place of y
+#define GM_BN_BWD_FUSED_LAUNCH(NR)                                                                                  \
+    if (maskx) hipLaunchKernelGGL((k_bn_bwd_fused<BWD_RELUX, false, NR>), g, dim3(kT), 0, st, a);                   \
+    else if (ym && p->dres) hipLaunchKernelGGL((k_bn_bwd_fused<BWD_RELU, true, NR, true>), g, dim3(kT), 0, st, a);  \
+    else if (ym) hipLaunchKernelGGL((k_bn_bwd_fused<BWD_RELU, false, NR, true>), g, dim3(kT), 0, st, a);            \
+    else if (p->relu && p->dres) hipLaunchKernelGGL((k_bn_bwd_fused<BWD_RELU, true, NR>), g, dim3(kT), 0, st, a);   \
+    else if (p->relu) hipLaunchKernelGGL((k_bn_bwd_fused<BWD_RELU, false, NR>), g, dim3(kT), 0, st, a);             \
     else hipLaunchKernelGGL((k_bn_bwd_fused<BWD, false, NR>), g, dim3(kT), 0, st, a);
         if (nr < 0) { GM_BN_BWD_FUSED_LAUNCH(0) }
         else if (nr == 4) { GM_BN_BWD_FUSED_LAUNCH(4) }
@@ -1974,7 +2013,8 @@ extern "C" int gm_bn_fwd_apply_grouped_bf16(const gm_bn_fwd* ps, int G, const fl
         const uint16_t* x0 = static_cast<const uint16_t*>(p->x);
         strided = strided && ps[g].x == x0 + g * gs &&
                   ps[g].y == static_cast<uint16_t*>(p->y) + g * gs &&
-                  (!p->residual || ps[g].residual == static_cast<const uint16_t*>(p->residual) + g * gs);
+                  (!p->residual || ps[g].residual == static_cast<const uint16_t*>(p->residual) + g * gs) &&
+                  (!p->relu_mask || ps[g].relu_mask == static_cast<uint8_t*>(p->relu_mask) + g * gs / 8);
     }
     const long long cgs = (long long)(rows + 1) * 2 * C;
     hipStream_t st = as_stream(stream);
@@ -1983,6 +2023,7 @@ extern "C" int gm_bn_fwd_apply_grouped_bf16(const gm_bn_fwd* ps, int G, const fl
         ApplyArgs b{};
         b.nvec = p->M * (C / 8); b.tpr_log = ilog2(C / 8); b.C = C; b.relu = p->relu;
         b.x = ps[gi].x; b.res = ps[gi].residual; b.out = ps[gi].y;
+        b.mask_out = static_cast<uint8_t*>(ps[gi].relu_mask);
         b.coef = stats + gi * cgs + (size_t)rows * 2 * C;
         b.gvec = strided ? gs / 8 : 0;
         b.cgs = strided ? cgs : 0;

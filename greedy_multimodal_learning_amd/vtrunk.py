@@ -51,6 +51,9 @@ FUSED_STEM_STATS = os.environ.get("GM_FUSED_STEM_STATS", "1") != "0"
 # and a streaming apply instead of the single-launch BatchNorm's statistics read
 # (GM_EPI_BN_STATS=0: the single-launch BatchNorm)
 EPI_BN_STATS = os.environ.get("GM_EPI_BN_STATS", "1") != "0"
+# the block-output BatchNorm (+ residual + ReLU) writes its ReLU mask as bits (1/16 of y) and the
+# backward reads them in place of y (GM_BN_RELU_MASK=0: the backward reads y)
+BN_RELU_MASK = os.environ.get("GM_BN_RELU_MASK", "1") != "0"
 _GM_E_UNSUP = -3
 
 
@@ -332,8 +335,9 @@ def _bn_param_grads(gammas, betas, want_w, want_b):
             [torch.empty(C, device=dev, dtype=torch.float32) for _ in range(G)], False, False)
 
 
-def _bn_backward(dz, y, xb, G, gammas, betas, sm, si, relu, want_dres, coef, want_w, want_b):
-    """Grouped BN backward; returns (dx, dres, grads_w[G], grads_b[G])."""
+def _bn_backward(dz, y, xb, G, gammas, betas, sm, si, relu, want_dres, coef, want_w, want_b, ymask=None):
+    """Grouped BN backward; returns (dx, dres, grads_w[G], grads_b[G]).  ymask: the forward's
+    ReLU mask bytes (read in place of y by the single-launch backward)."""
     lib = L.load()
     GN, C, H, W = xb.shape
     M = (GN // G) * H * W
@@ -347,7 +351,8 @@ def _bn_backward(dz, y, xb, G, gammas, betas, sm, si, relu, want_dres, coef, wan
         descs.append(L.BnBwd(M, C, int(relu), dz[r].data_ptr(), y[r].data_ptr() if (relu and y is not None) else 0,
                              xb[r].data_ptr(), gammas[g].data_ptr(), sm[g].data_ptr(), si[g].data_ptr(),
                              dx[r].data_ptr(), dres[r].data_ptr() if dres is not None else 0, dgs[g].data_ptr(),
-                             dbs[g].data_ptr(), int(acc), 0, coef[g].data_ptr() if coef is not None else 0))
+                             dbs[g].data_ptr(), int(acc), 0, coef[g].data_ptr() if coef is not None else 0,
+                             ymask[g * (M * C // 8):].data_ptr() if ymask is not None else 0))
     buf = _bn_scratch_g(xb.device, M, C, G)
     L.check(lib.gm_bn_bwd_grouped_bf16(L.arr(L.BnBwd, descs), G, buf.data_ptr(), buf.numel(),
                                        L.stream_of(xb.device)), "gm_bn_bwd_grouped_bf16")
@@ -378,6 +383,8 @@ class _VBNFn(torch.autograd.Function):
         sm = torch.empty(G, C, device=dev, dtype=torch.float32)
         si = torch.empty(G, C, device=dev, dtype=torch.float32)
         coef = torch.empty(G, 2 * C, device=dev, dtype=torch.float32) if maskx else None
+        ymask = (torch.empty(GN * H * W * C // 8, device=dev, dtype=torch.uint8)
+                 if relu and residual is not None and BN_RELU_MASK else None)
         descs = []
         for g, bn in enumerate(bns):
             r = slice(g * N, (g + 1) * N)
@@ -386,7 +393,8 @@ class _VBNFn(torch.autograd.Function):
                                  gammas[g].data_ptr(), betas[g].data_ptr(), L.ptr(bn.running_mean),
                                  L.ptr(bn.running_var), float(bn.momentum), float(bn.eps), sm[g].data_ptr(),
                                  si[g].data_ptr(), L.ptr(bn.num_batches_tracked),
-                                 coef[g].data_ptr() if maskx else 0))
+                                 coef[g].data_ptr() if maskx else 0,
+                                 ymask[g * (M * C // 8):].data_ptr() if ymask is not None else 0))
         if stats is not None and "part" in stats:  # partial rows from the convolution's epilogue
             part, rows = stats.pop("part"), stats.pop("rows")
             st = L.stream_of(dev)
@@ -398,19 +406,20 @@ class _VBNFn(torch.autograd.Function):
             buf = _bn_scratch_g(dev, M, C, G)
             L.check(lib.gm_bn_fwd_train_grouped_bf16(L.arr(L.BnFwd, descs), G, buf.data_ptr(), buf.numel(),
                                                      L.stream_of(dev)), "gm_bn_fwd_train_grouped_bf16")
-        ctx.save_for_backward(xb, y if relu and not maskx else coef, sm, si, *gammas, *betas)
+        ctx.save_for_backward(xb, y if relu and not maskx else coef, sm, si, ymask, *gammas, *betas)
         ctx.meta = (G, maskx, relu, residual is not None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        xb, yc, sm, si, *prm = ctx.saved_tensors
+        xb, yc, sm, si, ymask, *prm = ctx.saved_tensors
         G, maskx, relu, has_res = ctx.meta
         gammas, betas = prm[:G], prm[G:]
         y, coef = (None, yc) if maskx else (yc, None)
         want_dres = has_res and ctx.needs_input_grad[1]
         dx, dres, gw, gb = _bn_backward(dy, y, xb, G, gammas, betas, sm, si, relu, want_dres, coef,
-                                        any(ctx.needs_input_grad[7:7 + G]), any(ctx.needs_input_grad[7 + G:]))
+                                        any(ctx.needs_input_grad[7:7 + G]), any(ctx.needs_input_grad[7 + G:]),
+                                        ymask)
         if dres is not None and ctx.join is not None:
             dres = ctx.join.contribute(lambda add: dres if add is None else dres + add)
         return (dx if ctx.needs_input_grad[0] else None, dres, None, None, None, None, None, *gw, *gb)

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define GM_ABI_VERSION 2
+#define GM_ABI_VERSION 3
 
 /* activation element types */
 #define GM_F32  0
@@ -511,6 +511,9 @@ typedef struct gm_bn_fwd {
     float* save_invstd;
     long long* num_batches_tracked;  /* train: += 1 if non-NULL (nn.BatchNorm2d counter) */
     float* coef_out;                 /* train, optional: the affine coefficients sc[C], sh[C] (fp32) */
+    void* relu_mask;                 /* train, relu with residual, optional (bf16): the ReLU mask, one byte
+                                        per 8 channels of a pixel (bit j: channel 8v + j of y's 16-B
+                                        vector v is > 0), M*C/8 bytes - for gm_bn_bwd.relu_mask */
 } gm_bn_fwd;
 
 typedef struct gm_bn_bwd {
@@ -530,6 +533,9 @@ typedef struct gm_bn_bwd {
     int pad;
     const float* fwd_coef;  /* relu without residual: the forward's coef_out; y may then be NULL and
                                the relu mask is recomputed from x (x*sc + sh > 0, the forward's value) */
+    const void* relu_mask;  /* relu (bf16), optional: the forward's relu_mask, read in place of y by the
+                               single-launch backward (1/16 of y's bytes; y is still required for the
+                               two-launch fallback) */
 } gm_bn_bwd;
 
 size_t gm_bn_scratch(long long M, int C);

@@ -89,3 +89,51 @@ def test_epilogue_statistics_match_single_launch_bn(shape, mode):
         _close(a["dg"][i], b["dg"][i], 5e-3, f"dgamma[{i}]")
         _close(a["db"][i], b["db"][i], 5e-3, f"dbeta[{i}]")
     _close(a["dx"], b["dx"], 2e-2, "dx")
+
+
+@pytest.mark.parametrize("shape", [(8, 64, 56, 56), (8, 256, 14, 14), (8, 512, 7, 7), (3, 64, 9, 11)],
+                         ids=lambda s: "x".join(map(str, s)))
+@pytest.mark.parametrize("epi", [False, True], ids=["single_launch_fwd", "epilogue_stats_fwd"])
+def test_relu_mask_bits_backward_bit_identical(shape, epi):
+    """The block-output BatchNorm (+ residual + ReLU) writes its ReLU mask as one byte per 8
+    channels (k_bn_fwd_fused / k_bn_apply) and the single-launch backward reads it in place of
+    y (k_bn_bwd_fused<BWD_RELU, DRES, NR, YM>): bit-identical to the y-reading backward - the
+    mask is the stored bf16 y > 0 - for the streaming and register-held backward plans and
+    both forward paths (statistics from the BN's own read or from a k_conv_rw epilogue)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from greedy_multimodal_learning_amd import vtrunk
+    from greedy_multimodal_learning_amd.bn import GMBatchNorm2d
+    from greedy_multimodal_learning_amd.conv import GMConv2d
+    from greedy_multimodal_learning_amd.vtrunk import vbn, vconv
+    dev = torch.device("cuda:0")
+    N, C, H, W = shape
+    G = 2
+    g = torch.Generator().manual_seed(C + H + int(epi))
+    x = torch.randn(G * N, C, H, W, generator=g).bfloat16().to(dev).contiguous(memory_format=CL)
+    res = torch.randn(G * N, C, H, W, generator=g).bfloat16().to(dev).contiguous(memory_format=CL)
+    gy = torch.randn(G * N, C, H, W, generator=g).bfloat16().to(dev).contiguous(memory_format=CL)
+    convs = []
+    for _ in range(G):
+        m = GMConv2d(C, C, 3, padding=1, bias=False).to(dev)
+        with torch.no_grad():
+            m.weight.copy_(torch.randn(C, C, 3, 3, generator=g) / (9 * C) ** 0.5)
+        convs.append(m.to(memory_format=CL))
+    out = {}
+    old = vtrunk.BN_RELU_MASK
+    try:
+        for mask in (True, False):
+            vtrunk.BN_RELU_MASK = mask
+            bns = [GMBatchNorm2d(C).to(dev).train() for _ in range(G)]
+            xs, rs = x.clone().requires_grad_(True), res.clone().requires_grad_(True)
+            stats = {} if epi else None
+            h = vconv(xs, convs, stats=stats) if epi else xs
+            y = vbn(h, bns, residual=rs, relu=True, stats=stats)
+            y.backward(gy)
+            out[mask] = [y.detach(), xs.grad, rs.grad] + [b.weight.grad for b in bns] + [b.bias.grad for b in bns]
+            for c in convs:
+                c.weight.grad = None
+    finally:
+        vtrunk.BN_RELU_MASK = old
+    for i, (a, b) in enumerate(zip(out[True], out[False])):
+        assert torch.equal(a, b), f"output {i} differs with the mask bits"
