@@ -1044,29 +1044,41 @@ __global__ __launch_bounds__(64 * R) void k_wgrad_stem(WStemArgs a) {
 }
 
 // dw[i] (+)= sum over splits of part[s][i] in ONE launch, for the uncropped case (Cp == Cr,
-// every layer but the RGB stem).  A block covers 256/R float4 columns with R split lanes
-// per column: lane r sums splits r, r+R, ... (four loads in flight), the R lane sums are
-// then combined in lane order through LDS - a fixed summation order for a given shape,
-// so the result is deterministic.  R is picked on the host so that small slabs (layer 1:
-// 9k float4 columns x 100 splits) still spread over hundreds of blocks.
+// every layer but the RGB stem).  A wave covers 64/R float4 columns with R split lanes per
+// column (lane r sums splits r, r+R, ..., eight loads in flight), and the R lane sums are
+// combined inside the wave by a fixed xor tree (DPP row rotate, swizzle, bpermute) - a fixed
+// summation order for a given shape (deterministic) and NO LDS: these sums run on the weight-
+// gradient stream beside LDS-heavy kernels (k_wgrad_halo64, k_wgrad_stem hold most of a CU's
+// LDS), where the former LDS combine could not place its workgroups (the stem's sum: 6.3 us
+// alone, 34 us in the step).  R is picked on the host so that small slabs still spread over
+// hundreds of waves.
+template <int C>
+__device__ __forceinline__ float wsum_dpp(float v) {
+    return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), C, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float wsum_x16(float v) {
+    return v + __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x401f));
+}
 template <int R>
 __global__ __launch_bounds__(256) void k_wgrad_sum(const float* __restrict__ part, int splits, size_t slab,
                                                    int accumulate, float* __restrict__ dw, long long gs_dw) {
-    constexpr int CPB = 256 / R;
+    static_assert(R == 1 || R == 2 || R == 4 || R == 8, "k_wgrad_sum: 1, 2, 4 or 8 split lanes");
+    constexpr int CPW = 64 / R, CPB = 4 * CPW;
     part += (size_t)blockIdx.y * splits * slab;  // view group blockIdx.y
     dw += blockIdx.y * gs_dw;
-    const int t = threadIdx.x, col = t % CPB, r = t / CPB;
-    const size_t i4 = ((size_t)blockIdx.x * CPB + col) * 4;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int r = lane / CPW, cw = lane - r * CPW;
+    const size_t i4 = ((size_t)blockIdx.x * CPB + wave * CPW + cw) * 4;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     if (i4 < slab) {
         const float* p = part + i4;
         int s = r;
-        for (; s + 3 * R < splits; s += 4 * R) {
-            float4 v[4];
+        for (; s + 7 * R < splits; s += 8 * R) {
+            float4 v[8];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = *(const float4*)(p + (size_t)(s + j * R) * slab);
+            for (int j = 0; j < 8; ++j) v[j] = *(const float4*)(p + (size_t)(s + j * R) * slab);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
+            for (int j = 0; j < 8; ++j) {
                 acc.x += v[j].x; acc.y += v[j].y; acc.z += v[j].z; acc.w += v[j].w;
             }
         }
@@ -1075,18 +1087,19 @@ __global__ __launch_bounds__(256) void k_wgrad_sum(const float* __restrict__ par
             acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
         }
     }
-    if constexpr (R > 1) {
-        __shared__ float4 red[256];
-        red[t] = acc;
-        __syncthreads();
-        if (r != 0) return;
-#pragma unroll
-        for (int q = 1; q < R; ++q) {
-            const float4 v = red[q * CPB + col];
-            acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-        }
+    // the split lanes of a column are lanes cw + CPW q: xor 8 (row rotate 8), 16, 32
+    if constexpr (R >= 8) {
+        acc.x = wsum_dpp<0x128>(acc.x); acc.y = wsum_dpp<0x128>(acc.y);
+        acc.z = wsum_dpp<0x128>(acc.z); acc.w = wsum_dpp<0x128>(acc.w);
     }
-    if (i4 >= slab) return;
+    if constexpr (R >= 4) {
+        acc.x = wsum_x16(acc.x); acc.y = wsum_x16(acc.y); acc.z = wsum_x16(acc.z); acc.w = wsum_x16(acc.w);
+    }
+    if constexpr (R >= 2) {
+        acc.x += __shfl_xor(acc.x, 32); acc.y += __shfl_xor(acc.y, 32);
+        acc.z += __shfl_xor(acc.z, 32); acc.w += __shfl_xor(acc.w, 32);
+    }
+    if (r != 0 || i4 >= slab) return;
     float4* o = (float4*)(dw + i4);
     if (accumulate) {
         const float4 v = *o;
@@ -1337,6 +1350,23 @@ extern "C" size_t gm_conv2d_wgrad_scratch(const gm_conv_desc* d) {
 }
 
 
+// the split sum of every split weight-gradient kernel: k_wgrad_sum with R split lanes per
+// column (at most 8, inside one wave), enough waves for small slabs
+static int launch_wgrad_sum(const float* part, int splits, size_t slab, int accumulate, float* dw, long long gs,
+                            int G, hipStream_t st) {
+    const size_t ncol = slab / 4;
+    int R = 1;
+    while (R < 8 && R * 2 <= splits && (ncol * R + 255) / 256 < 512) R *= 2;
+    const dim3 gg((unsigned)((ncol + 256 / R - 1) / (256 / R)), (unsigned)G);
+    switch (R) {
+        case 1: k_wgrad_sum<1><<<gg, 256, 0, st>>>(part, splits, slab, accumulate, dw, gs); break;
+        case 2: k_wgrad_sum<2><<<gg, 256, 0, st>>>(part, splits, slab, accumulate, dw, gs); break;
+        case 4: k_wgrad_sum<4><<<gg, 256, 0, st>>>(part, splits, slab, accumulate, dw, gs); break;
+        default: k_wgrad_sum<8><<<gg, 256, 0, st>>>(part, splits, slab, accumulate, dw, gs); break;
+    }
+    return check_launch("k_wgrad_sum");
+}
+
 // G view groups in one launch: group g reads dy + g*N*P*Q*K and x + g*N*H*W*C (the views
 // stacked along the batch) and writes its weight gradient to dw + g*dw_stride (floats)
 extern "C" int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, const void* dy, const void* x,
@@ -1356,19 +1386,7 @@ extern "C" int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, con
     GM_REQUIRE(scratch && scratch_bytes >= need, "conv wgrad: scratch %zu < %zu", scratch_bytes, need);
     hipStream_t st0 = as_stream(stream);
     auto split_sum = [&](float* part, int splits, size_t slab) {
-        const size_t ncol = slab / 4;
-        int R = 1;
-        while (R < 32 && R * 2 <= splits && (ncol * R + 255) / 256 < 512) R *= 2;
-        const dim3 gg((unsigned)((ncol + 256 / R - 1) / (256 / R)), (unsigned)G);
-        switch (R) {
-            case 1: k_wgrad_sum<1><<<gg, 256, 0, st0>>>(part, splits, slab, accumulate, dw, dw_stride); break;
-            case 2: k_wgrad_sum<2><<<gg, 256, 0, st0>>>(part, splits, slab, accumulate, dw, dw_stride); break;
-            case 4: k_wgrad_sum<4><<<gg, 256, 0, st0>>>(part, splits, slab, accumulate, dw, dw_stride); break;
-            case 8: k_wgrad_sum<8><<<gg, 256, 0, st0>>>(part, splits, slab, accumulate, dw, dw_stride); break;
-            case 16: k_wgrad_sum<16><<<gg, 256, 0, st0>>>(part, splits, slab, accumulate, dw, dw_stride); break;
-            default: k_wgrad_sum<32><<<gg, 256, 0, st0>>>(part, splits, slab, accumulate, dw, dw_stride); break;
-        }
-        return check_launch("k_wgrad_sum");
+        return launch_wgrad_sum(part, splits, slab, accumulate, dw, dw_stride, G, st0);
     };
     StemWPlan sw;
     if (stemw_plan(d, G, sw) && c_real == d->C) {
@@ -1430,21 +1448,7 @@ extern "C" int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, con
         else go(std::integral_constant<int, 64>{});
         int rc = check_launch("k_wgrad_halo64");
         if (rc) return rc;
-        const size_t slab = (size_t)d->K * 9 * d->C;
-        const size_t ncol = slab / 4;
-        int R = 1;
-        while (R < 32 && R * 2 <= h.splits && (ncol * R + 255) / 256 < 512) R *= 2;
-        const dim3 gg((unsigned)((ncol + 256 / R - 1) / (256 / R)), (unsigned)G);
-        float* part = h.part;
-        switch (R) {
-            case 1: k_wgrad_sum<1><<<gg, 256, 0, st0>>>(part, h.splits, slab, accumulate, dw, dw_stride); break;
-            case 2: k_wgrad_sum<2><<<gg, 256, 0, st0>>>(part, h.splits, slab, accumulate, dw, dw_stride); break;
-            case 4: k_wgrad_sum<4><<<gg, 256, 0, st0>>>(part, h.splits, slab, accumulate, dw, dw_stride); break;
-            case 8: k_wgrad_sum<8><<<gg, 256, 0, st0>>>(part, h.splits, slab, accumulate, dw, dw_stride); break;
-            case 16: k_wgrad_sum<16><<<gg, 256, 0, st0>>>(part, h.splits, slab, accumulate, dw, dw_stride); break;
-            default: k_wgrad_sum<32><<<gg, 256, 0, st0>>>(part, h.splits, slab, accumulate, dw, dw_stride); break;
-        }
-        return check_launch("k_wgrad_sum");
+        return launch_wgrad_sum(h.part, h.splits, (size_t)d->K * 9 * d->C, accumulate, dw, dw_stride, G, st0);
     }
     RingPlan rp;
     if (c_real == d->C && ring_plan(d, G, rp)) {
@@ -1533,22 +1537,8 @@ extern "C" int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, con
     else rc = launch_wgrad4<1, 1>(a, grid, st);
     if (rc || direct) return rc;
     const size_t slab = (size_t)d->K * a.T * d->C;
-    if (c_real == d->C) {  // one-launch split reduction (slab is a multiple of 4: K % 8 == 0)
-        const size_t ncol = slab / 4;
-        int R = 1;  // split lanes per column: aim for >= 512 blocks without idle lanes
-        while (R < 32 && R * 2 <= a.splits && (ncol * R + 255) / 256 < 512) R *= 2;
-        const dim3 g((unsigned)((ncol + 256 / R - 1) / (256 / R)), (unsigned)G);
-        const long long gs = dw_stride;
-        switch (R) {
-            case 1: k_wgrad_sum<1><<<g, 256, 0, st>>>(a.part, a.splits, slab, accumulate, dw, gs); break;
-            case 2: k_wgrad_sum<2><<<g, 256, 0, st>>>(a.part, a.splits, slab, accumulate, dw, gs); break;
-            case 4: k_wgrad_sum<4><<<g, 256, 0, st>>>(a.part, a.splits, slab, accumulate, dw, gs); break;
-            case 8: k_wgrad_sum<8><<<g, 256, 0, st>>>(a.part, a.splits, slab, accumulate, dw, gs); break;
-            case 16: k_wgrad_sum<16><<<g, 256, 0, st>>>(a.part, a.splits, slab, accumulate, dw, gs); break;
-            default: k_wgrad_sum<32><<<g, 256, 0, st>>>(a.part, a.splits, slab, accumulate, dw, gs); break;
-        }
-        return check_launch("k_wgrad_sum");
-    }
+    if (c_real == d->C)  // one-launch split reduction (slab is a multiple of 4: K % 8 == 0)
+        return launch_wgrad_sum(a.part, a.splits, slab, accumulate, dw, dw_stride, G, st);
     const size_t n = (size_t)d->K * a.T * c_real;
     int g = (int)((n + 255) / 256);
     if (g > 4096) g = 4096;
