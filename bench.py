@@ -98,7 +98,7 @@ def cpu_baseline(seconds, size):
 
     th = torch.get_num_threads()
     n4, dt4 = run(4, seconds, 200)
-    n64, dt64 = run(64, 0.0, 10)  # ten timed steps at the bench batch (BASELINE.md quotes a median of 10)
+    n64, dt64 = run(64, float("inf"), 10)  # ten timed steps at the bench batch (a median of 10)
     return {"value": round(n4 * 4 * 2 / dt4, 3), "unit": "view-images/s", "cores": th,
             "kind": "port", "ms_per_step": round(1e3 * dt4 / n4, 2),
             "b64": {"value": round(n64 * 64 * 2 / dt64, 3), "ms_per_step": round(1e3 * dt64 / n64, 1),
