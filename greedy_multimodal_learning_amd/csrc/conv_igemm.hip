@@ -211,6 +211,111 @@ __device__ __forceinline__ void store_tile(const ConvArgs& a, const ConvCls& cl,
     }
 }
 
+// The same epilogue through LDS for the 256-thread tiled kernels (2 x 2 waves of MT x NT
+// fragments, the k-loop's LDS idle: every DMA has landed, the caller's barrier-free reads
+// end at the __syncthreads below): the tile's BM pixel rows of BN channels are assembled in
+// LDS - bf16, or fp32 with the fused gradient-join addend (added before the one rounding) -
+// 16-B chunks XOR-swizzled by pixel, and leave as 16-B stores, BN / 8 lanes per contiguous
+// pixel row segment.  The direct 8-B stores from the MFMA layout touch 32 pixel rows per
+// instruction: 13 % of the layer-3 halo launch (41.4 us with, 36.0 without them).  Falls
+// back to store_tile when the LDS is too small or the output needs 64-bit offsets.
+template <int MT, int NT, int BM, int BN>
+__device__ __forceinline__ void store_tile_lds(const ConvArgs& a, const ConvCls& cl, int m0, int n0, int wm, int wn,
+                                               int fr, int fh, int M, floatx16 (&acc)[MT][NT], long long goff,
+                                               char* lds, int lds_bytes, int t) {
+    static_assert(BM == 64 * MT && BN == 64 * NT, "store_tile_lds: 2 x 2 waves of MT x NT fragments");
+    const size_t out_bytes = (size_t)a.N * a.Ho * a.Wo * a.Nout * 2;
+    const bool f32 = a.addend != nullptr;
+    if (out_bytes >= 0x7ffff000u || BM * BN * (f32 ? 4 : 2) > lds_bytes) {
+        store_tile<MT, NT, BM, BN>(a, cl, m0, n0, wm, wn, fr, fh, M, acc, goff);
+        return;
+    }
+    constexpr int CH = BN / 8, CF = BN / 4;  // bf16 / fp32 16-B chunks per pixel row
+    constexpr int NU = BM * CH / 256;          // output chunks per thread
+    __syncthreads();  // every wave is done with the k-loop's LDS
+    if (f32) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+#pragma unroll
+                for (int gq = 0; gq < 4; ++gq) {
+                    const int px = wm * (BM / 2) + i * 32 + fr, c = wn * (CF / 2) + 8 * j + 2 * gq + fh;
+                    *reinterpret_cast<float4*>(lds + px * (BN * 4) + ((c ^ (px & (CF - 1))) << 4)) =
+                        make_float4(acc[i][j][4 * gq], acc[i][j][4 * gq + 1], acc[i][j][4 * gq + 2], acc[i][j][4 * gq + 3]);
+                }
+    } else {
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+#pragma unroll
+                for (int gq = 0; gq < 4; ++gq) {
+                    const int px = wm * (BM / 2) + i * 32 + fr, c = wn * (CH / 2) + 4 * j + gq;
+                    *reinterpret_cast<uint2*>(lds + px * (BN * 2) + ((c ^ (px & (CH - 1))) << 4) + 8 * fh) =
+                        make_uint2(pack_bf2(acc[i][j][4 * gq], acc[i][j][4 * gq + 1]),
+                                   pack_bf2(acc[i][j][4 * gq + 2], acc[i][j][4 * gq + 3]));
+                }
+    }
+    __syncthreads();
+    // this thread's chunks: pixel row px = e / CH, chunk c = e % CH of e = t + 256 u
+    const int PQ = cl.P * cl.Q;
+    // dense classes (forward, stride-1 input gradient): output pixel m is NHWC row m
+    const bool dense = cl.oS == 1 && cl.oH == 0 && cl.oW == 0 && cl.P == a.Ho && cl.Q == a.Wo;
+    unsigned off[NU];  // (computed branch-free per lane: a per-lane branch in these unrolled loops
+                       // serialises them)
+    if (dense) {
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+            const int e = t + 256 * u, px = e / CH, c = e - px * CH;
+            const int m = m0 + px, n = n0 + 8 * c;
+            const unsigned o = (unsigned)m * (unsigned)a.Nout * 2u + (unsigned)n * 2u;
+            off[u] = (m < M) & (n < a.Nout) ? o : 0xfffffff0u;
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+            const int e = t + 256 * u, px = e / CH, c = e - px * CH;
+            const int n = n0 + 8 * c;
+            const int m = min(m0 + px, M - 1);
+            const int b = (int)cl.fd_pq.div((uint32_t)m), pq = m - b * PQ;
+            const int p = (int)cl.fd_q.div((uint32_t)pq), q = pq - p * cl.Q;
+            const unsigned o = (unsigned)((((b * a.Ho + p * cl.oS + cl.oH) * a.Wo + q * cl.oS + cl.oW) * a.Nout + n) * 2);
+            off[u] = (m0 + px < M) & (n < a.Nout) ? o : 0xfffffff0u;
+        }
+    }
+    uint16_t* const outp = cl.out + goff;
+    const auto orsrc = __builtin_amdgcn_make_buffer_rsrc(outp, 0, (int)out_bytes, 0x00020000);
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    if (f32) {
+        const auto arsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.addend + goff), 0, (int)out_bytes,
+                                                             0x00020000);
+        u32x4 av[NU];
+#pragma unroll
+        for (int u = 0; u < NU; ++u) av[u] = __builtin_amdgcn_raw_buffer_load_b128(arsrc, off[u], 0, 0);
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+            const int e = t + 256 * u, px = e / CH, c = e - px * CH;
+            const float4 f0 = *reinterpret_cast<const float4*>(lds + px * (BN * 4) + (((2 * c) ^ (px & (CF - 1))) << 4));
+            const float4 f1 = *reinterpret_cast<const float4*>(lds + px * (BN * 4) + (((2 * c + 1) ^ (px & (CF - 1))) << 4));
+            const u32x4 o = {pack_bf2(f0.x + bf_lo(av[u].x), f0.y + bf_hi(av[u].x)),
+                             pack_bf2(f0.z + bf_lo(av[u].y), f0.w + bf_hi(av[u].y)),
+                             pack_bf2(f1.x + bf_lo(av[u].z), f1.y + bf_hi(av[u].z)),
+                             pack_bf2(f1.z + bf_lo(av[u].w), f1.w + bf_hi(av[u].w))};
+            __builtin_amdgcn_raw_buffer_store_b128(o, orsrc, off[u], 0, 0);
+        }
+        return;
+    }
+    u32x4 v[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        const int e = t + 256 * u, px = e / CH, c = e - px * CH;
+        v[u] = *reinterpret_cast<const u32x4*>(lds + px * (BN * 2) + ((c ^ (px & (CH - 1))) << 4));
+    }
+#pragma unroll
+    for (int u = 0; u < NU; ++u) __builtin_amdgcn_raw_buffer_store_b128(v[u], orsrc, off[u], 0, 0);
+}
+
 template <int BM, int BN, bool UT, int ST>
 __global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
     constexpr int BK = 64;
@@ -698,7 +803,7 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
         if (t == 0) __hip_atomic_store(a.flags + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 
-    store_tile<MT, NT, BM, BN>(a, cl, m0, n0, wm, wn, fr, fh, M, acc, g * a.gs_out);
+    store_tile_lds<MT, NT, BM, BN>(a, cl, m0, n0, wm, wn, fr, fh, M, acc, g * a.gs_out, lds, NST * (SA + SB), t);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1334,85 +1439,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_h9(ConvArgs a, HaloArgs h) {
         }
         if (t == 0) __hip_atomic_store(a.flags + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    const size_t out_bytes = (size_t)a.N * a.Ho * a.Wo * a.Nout * 2;
-    if (cl.oS != 1 || cl.oH != 0 || cl.oW != 0 || cl.P != a.Ho || cl.Q != a.Wo || out_bytes >= 0x7ffff000u ||
-        (a.addend && 128 * BN * 4 > HB + NB * SB)) {
-        store_tile<MT, NT, 128, BN>(a, cl, m0, n0, wm, wn, fr, fh, M, acc, g * a.gs_out);
-        return;
-    }
-    // Epilogue through LDS (output pixel m is NHWC row m): the tile's 128 pixel rows of BN
-    // channels are assembled in the (now idle) halo / weight LDS - 16-B chunks XOR-swizzled by
-    // pixel - and leave as 16-B stores, BN / 8 lanes per contiguous row segment.  The direct
-    // 8-B stores from the MFMA layout (32 pixel rows per instruction) cost 13 % of the layer-3
-    // launch (41.4 us with, 36.0 without them; staged: l2 50.2 -> 44.6, l3 41.4 -> 38.9 us).  Every DMA has landed (the last k-tile waited
-    // vmcnt(0)); the barrier ends every wave's reads of the ring.
-    constexpr int CH = BN / 8;  // 16-B chunks per pixel row
-    __syncthreads();
-    const auto orsrc = __builtin_amdgcn_make_buffer_rsrc(cl.out + g * a.gs_out, 0, (int)out_bytes, 0x00020000);
-    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-    if (a.addend) {
-        // the fused gradient join: the tile staged in fp32 (rows of BN * 4 B, 16-B chunks of 4
-        // channels XOR-swizzled by pixel), the addend added in fp32 before the one rounding
-        constexpr int CF = BN / 4;  // fp32 chunks per pixel row
-#pragma unroll
-        for (int i = 0; i < MT; ++i)
-#pragma unroll
-            for (int j = 0; j < NT; ++j)
-#pragma unroll
-                for (int gq = 0; gq < 4; ++gq) {
-                    const int px = wm * 64 + i * 32 + fr, c = wn * (CF / 2) + 8 * j + 2 * gq + fh;
-                    *reinterpret_cast<float4*>(lds + px * (BN * 4) + ((c ^ (px & (CF - 1))) << 4)) =
-                        make_float4(acc[i][j][4 * gq], acc[i][j][4 * gq + 1], acc[i][j][4 * gq + 2], acc[i][j][4 * gq + 3]);
-                }
-        __syncthreads();
-        const auto arsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.addend + g * a.gs_out), 0,
-                                                             (int)out_bytes, 0x00020000);
-        unsigned off[CH / 2];
-        u32x4 av[CH / 2];
-#pragma unroll
-        for (int u = 0; u < CH / 2; ++u) {
-            const int e = t + 256 * u, px = e / CH, c = e - px * CH;
-            off[u] = m0 + px < M ? (unsigned)(((size_t)(m0 + px) * a.Nout + n0 + 8 * c) * 2) : 0xfffffff0u;
-            av[u] = __builtin_amdgcn_raw_buffer_load_b128(arsrc, off[u], 0, 0);
-        }
-#pragma unroll
-        for (int u = 0; u < CH / 2; ++u) {
-            const int e = t + 256 * u, px = e / CH, c = e - px * CH;
-            const float4 f0 = *reinterpret_cast<const float4*>(lds + px * (BN * 4) + (((2 * c) ^ (px & (CF - 1))) << 4));
-            const float4 f1 = *reinterpret_cast<const float4*>(lds + px * (BN * 4) + (((2 * c + 1) ^ (px & (CF - 1))) << 4));
-            const u32x4 o = {pack_bf2(f0.x + bf_lo(av[u].x), f0.y + bf_hi(av[u].x)),
-                             pack_bf2(f0.z + bf_lo(av[u].y), f0.w + bf_hi(av[u].y)),
-                             pack_bf2(f1.x + bf_lo(av[u].z), f1.y + bf_hi(av[u].z)),
-                             pack_bf2(f1.z + bf_lo(av[u].w), f1.w + bf_hi(av[u].w))};
-            __builtin_amdgcn_raw_buffer_store_b128(o, orsrc, off[u], 0, 0);
-        }
-        return;
-    }
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-#pragma unroll
-            for (int gq = 0; gq < 4; ++gq) {
-                const int px = wm * 64 + i * 32 + fr, c = wn * (CH / 2) + 4 * j + gq;
-                *reinterpret_cast<uint2*>(lds + px * (BN * 2) + ((c ^ (px & (CH - 1))) << 4) + 8 * fh) =
-                    make_uint2(pack_bf2(acc[i][j][4 * gq], acc[i][j][4 * gq + 1]),
-                               pack_bf2(acc[i][j][4 * gq + 2], acc[i][j][4 * gq + 3]));
-            }
-    __syncthreads();
-    u32x4 v[CH / 2];
-#pragma unroll
-    for (int u = 0; u < CH / 2; ++u) {
-        const int e = t + 256 * u, px = e / CH, c = e - px * CH;
-        v[u] = *reinterpret_cast<const u32x4*>(lds + px * (BN * 2) + ((c ^ (px & (CH - 1))) << 4));
-    }
-#pragma unroll
-    for (int u = 0; u < CH / 2; ++u) {
-        const int e = t + 256 * u, px = e / CH, c = e - px * CH;
-        const int m = m0 + px;
-        __builtin_amdgcn_raw_buffer_store_b128(
-            v[u], orsrc, m < M ? (unsigned)(((size_t)m * a.Nout + n0 + 8 * c) * 2) : 0xfffffff0u, 0, 0);
-    }
+    store_tile_lds<MT, NT, 128, BN>(a, cl, m0, n0, wm, wn, fr, fh, M, acc, g * a.gs_out, lds, HB + NB * SB, t);
 }
 
 // ---------------------------------------------------------------------------------
