@@ -80,10 +80,11 @@ struct ConvArgs {
     // group g the tiles [g * tiles_g, (g + 1) * tiles_g), persistent ones gridDim / G workgroups
     int G, tiles_g;
     long long gs_in, gs_wt, gs_out;
-    // forward, optional (k_conv_rw): BatchNorm statistics of the stored (bf16) output from the
-    // epilogue - per group [Nout / 64 slices][stats_rows][64 channels][sum, sum of squares] fp32
-    // partial rows (one per persistent workgroup), then 2 Nout floats of coefficient area: group
-    // g at stats + g * 2 Nout (stats_rows + 1) (gm_bn_fwd_stats_finalize_grouped combines them)
+    // forward, optional: BatchNorm statistics of the stored (bf16) output from the epilogue -
+    // per group [Nout / 64 slices][stats_rows][64 channels][sum, sum of squares] fp32 partial
+    // rows (k_conv_rw: one per persistent workgroup; store_tile_lds: one per output tile), then
+    // 2 Nout floats of coefficient area: group g at stats + g * 2 Nout (stats_rows + 1)
+    // (gm_bn_fwd_stats_finalize_grouped combines them)
     float* stats;
     int stats_rows;
     ConvCls cls[kMaxCls];
@@ -222,11 +223,11 @@ __device__ __forceinline__ void store_tile(const ConvArgs& a, const ConvCls& cl,
 template <int MT, int NT, int BM, int BN>
 __device__ __forceinline__ void store_tile_lds(const ConvArgs& a, const ConvCls& cl, int m0, int n0, int wm, int wn,
                                                int fr, int fh, int M, floatx16 (&acc)[MT][NT], long long goff,
-                                               char* lds, int lds_bytes, int t) {
+                                               char* lds, int lds_bytes, int t, int grp) {
     static_assert(BM == 64 * MT && BN == 64 * NT, "store_tile_lds: 2 x 2 waves of MT x NT fragments");
     const size_t out_bytes = (size_t)a.N * a.Ho * a.Wo * a.Nout * 2;
     const bool f32 = a.addend != nullptr;
-    if (out_bytes >= 0x7ffff000u || BM * BN * (f32 ? 4 : 2) > lds_bytes) {
+    if (out_bytes >= 0x7ffff000u || BM * BN * (f32 ? 4 : 2) + 4 * (BN / 8) * 64 > lds_bytes) {
         store_tile<MT, NT, BM, BN>(a, cl, m0, n0, wm, wn, fr, fh, M, acc, goff);
         return;
     }
@@ -314,6 +315,63 @@ __device__ __forceinline__ void store_tile_lds(const ConvArgs& a, const ConvCls&
     }
 #pragma unroll
     for (int u = 0; u < NU; ++u) __builtin_amdgcn_raw_buffer_store_b128(v[u], orsrc, off[u], 0, 0);
+    if (a.stats) {
+        // BatchNorm statistics of the stored values (forward): this thread's chunk c = t % CH
+        // (8 channels) over its NU pixels, then the lanes sharing c (c + CH k: xor 8 / 16 / 32)
+        // and the four waves (LDS past the tile) - one partial row per output tile, row m0 / BM
+        typedef float f32x2 __attribute__((ext_vector_type(2)));
+        f32x2 s1[4], s2[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s1[k] = s2[k] = f32x2{0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+            const bool ok = off[u] != 0xfffffff0u;
+            const unsigned w4[4] = {ok ? v[u].x : 0u, ok ? v[u].y : 0u, ok ? v[u].z : 0u, ok ? v[u].w : 0u};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const f32x2 f = {bf_lo(w4[k]), bf_hi(w4[k])};
+                s1[k] += f;
+                s2[k] = __builtin_elementwise_fma(f, f, s2[k]);
+            }
+        }
+        float r[16];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            r[4 * k] = s1[k].x; r[4 * k + 1] = s2[k].x; r[4 * k + 2] = s1[k].y; r[4 * k + 3] = s2[k].y;
+        }
+        const int lane = t & 63, wave = t >> 6;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            float x = r[q];
+            if (CH == 8) x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x128, 0xf, 0xf, false));
+            x += __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(x), 0x401f));
+            x += __shfl_xor(x, 32);
+            r[q] = x;
+        }
+        float* red = reinterpret_cast<float*>(lds + BM * BN * 2);  // [4 waves][CH chunks][16]
+        if (lane < CH) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                *reinterpret_cast<float4*>(red + (wave * CH + lane) * 16 + 4 * q) =
+                    make_float4(r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]);
+        }
+        __syncthreads();
+        if (t < BN) {  // channel n0 + t: chunk t / 8, channel j = t % 8 of it
+            const int c = t >> 3, j = t & 7;
+            float S1 = 0.f, S2 = 0.f;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                S1 += red[(w * CH + c) * 16 + 2 * j];
+                S2 += red[(w * CH + c) * 16 + 2 * j + 1];
+            }
+            const int n = n0 + t;
+            if (n < a.Nout) {
+                float* sp = a.stats + (size_t)grp * 2 * a.Nout * (a.stats_rows + 1);
+                *reinterpret_cast<float2*>(sp + ((size_t)(n >> 6) * a.stats_rows + m0 / BM) * 128 + (n & 63) * 2) =
+                    make_float2(S1, S2);
+            }
+        }
+    }
 }
 
 template <int BM, int BN, bool UT, int ST>
@@ -803,7 +861,7 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
         if (t == 0) __hip_atomic_store(a.flags + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 
-    store_tile_lds<MT, NT, BM, BN>(a, cl, m0, n0, wm, wn, fr, fh, M, acc, g * a.gs_out, lds, NST * (SA + SB), t);
+    store_tile_lds<MT, NT, BM, BN>(a, cl, m0, n0, wm, wn, fr, fh, M, acc, g * a.gs_out, lds, NST * (SA + SB), t, g);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1439,7 +1497,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_h9(ConvArgs a, HaloArgs h) {
         }
         if (t == 0) __hip_atomic_store(a.flags + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    store_tile_lds<MT, NT, 128, BN>(a, cl, m0, n0, wm, wn, fr, fh, M, acc, g * a.gs_out, lds, HB + NB * SB, t);
+    store_tile_lds<MT, NT, 128, BN>(a, cl, m0, n0, wm, wn, fr, fh, M, acc, g * a.gs_out, lds, HB + NB * SB, t, g);
 }
 
 // ---------------------------------------------------------------------------------
@@ -2501,6 +2559,8 @@ static int pick_and_launch(ConvArgs& a, hipStream_t st, void* ws, size_t ws_byte
         a.ws = reinterpret_cast<float*>(static_cast<char*>(ws) + splitk_flag_bytes(p.tiles));
     }
     const int hb = halo_bytes(a);
+    const long long Mg = (long long)a.N * a.cls[0].P * a.cls[0].Q;
+    a.stats_rows = (int)((Mg + 127) / 128);  // (a.stats: one partial row per 128-pixel tile)
     if (hb > 0 && hb + 2 * 128 * 128 <= 160 * 1024 && a.G > 1) {
         // view groups: k_conv_h9 when it takes the shape, else the lean kernel below
         if (p.tile != T128x128) a.splits = 1;
@@ -2514,6 +2574,7 @@ static int pick_and_launch(ConvArgs& a, hipStream_t st, void* ws, size_t ws_byte
         if (a.Nout >= 128) return launch_halo<128>(a, hb, st);
         return launch_halo<64>(a, hb, st);
     }
+    if (p.tile == T64x64) a.stats_rows = (int)((Mg + 63) / 64);
     switch (p.tile) {
     case T128x128: return three ? launch_igemm<128, 128, 3>(a, st) : launch_igemm<128, 128, 2>(a, st);
     case T128x64: return three ? launch_igemm<128, 64, 3>(a, st) : launch_igemm<128, 64, 2>(a, st);
@@ -2818,7 +2879,7 @@ extern "C" size_t gm_conv2d_fwd_bn_stats_floats(const gm_conv_desc_hw* d, int G)
     fwd_setup(d, reinterpret_cast<const void*>(16), reinterpret_cast<const void*>(16), reinterpret_cast<void*>(16), a);
     a.G = G;
     const long long M = (long long)d->N * a.cls[0].P * a.cls[0].Q;
-    long long rows = (M + 63) / 64;  // k_gemm_ring: one row per 64-pixel slab
+    long long rows = (M + 63) / 64;  // k_gemm_ring, 64-pixel tiles: one row per 64 pixels
     if (rows < 256) rows = 256;       // k_conv_rw, k_conv_stem: one per workgroup
     StemArgs r;
     if (stem_plan(a, r) > 0 && r.stats_rows > rows) rows = r.stats_rows;
@@ -2853,20 +2914,18 @@ extern "C" int gm_conv2d_fwd_grouped_bn_stats_bf16(const gm_conv_desc_hw* d, int
     a.gs_in = (long long)d->N * d->H * d->W * d->C;
     a.gs_wt = w_stride;
     a.gs_out = M * d->K;
-    // the kernels whose epilogue stages the output tile anyway (k_conv_rw; k_gemm_ring above):
-    // there the sums are a few VALU per stored 16-B chunk.  The tiled 3x3 / strided kernels
-    // (k_conv_h9, k_conv_igemm_ut) store from the MFMA layout, where the per-channel sums need
-    // a 32-lane reduction per value: measured +4-10 us per launch (10-15 %) and one partial row
-    // per 64-pixel slab (a 1.5k-row combine) - more than the statistics read they replace
-    RwArgs rw;
-    if (a.G > 1 && rw_plan(a, rw) > 0) {
-        a.stats = stats;
-        rc = pick_and_launch(a, as_stream(stream), ws, ws_bytes);
-        *rows_out = a.stats_rows;
-        return rc;
+    // every view-grouped forward kernel stages its output tile through LDS (k_conv_rw,
+    // store_tile_lds of k_conv_h9 / k_conv_igemm_ut; k_gemm_ring above), where the sums are a
+    // few VALU per stored 16-B chunk.  (Summed in the MFMA layout instead - a 32-lane reduction
+    // per value, one row per 64-pixel slab - they cost more than the statistics read: r05.)
+    if (a.G < 2) {
+        set_error("conv fwd bn stats: view groups (G >= 2) only");
+        return GM_E_UNSUP;
     }
-    set_error("conv fwd bn stats: no statistics epilogue for this shape's kernel");
-    return GM_E_UNSUP;
+    a.stats = stats;
+    rc = pick_and_launch(a, as_stream(stream), ws, ws_bytes);
+    *rows_out = a.stats_rows;
+    return rc;
 }
 
 extern "C" int gm_conv_stem_stats_rows(const gm_conv_desc_hw* d, int G) {

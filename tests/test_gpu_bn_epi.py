@@ -1,10 +1,11 @@
 """BatchNorm statistics from the producing convolution's epilogue:
 gm_conv2d_fwd_grouped_bn_stats_bf16 -> gm_bn_fwd_stats_finalize_grouped -> gm_bn_fwd_apply_grouped_bf16
 against the single-launch BatchNorm forward (gm_bn_fwd_train_grouped_bf16) over the SAME
-convolution output, for the kernels that write the partial rows - k_conv_rw (layer 1, view
-groups) and k_gemm_ring (1x1 / s1, ragged M) - and, for every other kernel family (k_conv_h9,
-k_conv_igemm_ut, k_conv_halo), that the call declines (GM_E_UNSUP, nothing launched) and the
-trunk falls back to the single-launch BatchNorm.  Checked: which path was taken, the convolution
+convolution output, for every view-grouped kernel that writes the partial rows - k_conv_rw
+(layer 1), k_conv_h9 and k_conv_igemm_ut through their LDS-staged epilogue (store_tile_lds:
+3x3, strided 3x3, 1x1 / s2, 128x128 and 64x64 tiles, split-K) and k_gemm_ring (1x1 / s1,
+ragged M) - and that a single-group call declines (GM_E_UNSUP, nothing launched) so the trunk
+falls back to the single-launch BatchNorm.  Checked: which path was taken, the convolution
 output is bit-identical, y / running statistics / num_batches_tracked / backward dx and parameter
 gradients agree to the two summation orders' rounding (the reference's own semantics:
 torchvision conv -> BatchNorm2d in training mode, /root/reference/src/model.py:65-76)."""
@@ -20,10 +21,13 @@ SHAPES = [  # N per view, C, H, W, K, R, S, stride, pad, G, statistics from the 
     (3, 64, 20, 20, 64, 3, 3, 1, 1, 4, True),      # k_conv_rw, 4 groups
     (4, 256, 14, 14, 64, 1, 1, 1, 0, 2, True),     # 1x1 / s1 reduce: k_gemm_ring BN = 64, ragged M
     (4, 64, 28, 28, 256, 1, 1, 1, 0, 3, True),     # 1x1 / s1 expand: k_gemm_ring BN = 128, 3 groups
-    (8, 128, 28, 28, 128, 3, 3, 1, 1, 2, False),   # k_conv_h9: declined
-    (4, 64, 56, 56, 128, 3, 3, 2, 1, 2, False),    # strided 3x3 (igemm_ut): declined
-    (4, 128, 28, 28, 256, 1, 1, 2, 0, 2, False),   # downsample 1x1 / s2: declined
-    (4, 64, 56, 56, 64, 3, 3, 1, 1, 1, False),     # one group (k_conv_rw needs G >= 2): declined
+    (8, 128, 28, 28, 128, 3, 3, 1, 1, 2, True),    # k_conv_h9 (store_tile_lds)
+    (8, 256, 14, 14, 256, 3, 3, 1, 1, 2, True),    # k_conv_h9, split-K candidate
+    (8, 512, 7, 7, 512, 3, 3, 1, 1, 2, True),      # layer 4
+    (4, 64, 56, 56, 128, 3, 3, 2, 1, 2, True),     # strided 3x3 (k_conv_igemm_ut)
+    (4, 128, 28, 28, 256, 1, 1, 2, 0, 2, True),    # downsample 1x1 / s2 (k_conv_igemm_ut)
+    (2, 64, 9, 11, 128, 3, 3, 2, 1, 2, True),      # ragged, small M: 64 x 64 tiles
+    (4, 64, 56, 56, 64, 3, 3, 1, 1, 1, False),     # one group: declined (view groups only)
 ]
 
 
