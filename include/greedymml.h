@@ -599,16 +599,16 @@ int gm_conv_stem_stats_rows(const gm_conv_desc_hw* d, int G);
 int gm_conv2d_fwd_grouped_stats_bf16(const gm_conv_desc_hw* d, int G, const void* x, const void* w,
                                      long long w_stride, void* y, float* stats, int rows, void* stream);
 int gm_bn_fwd_stats_finalize_grouped(const gm_bn_fwd* ps, int G, float* stats, int rows, void* stream);
-/* The same for the trunk convolutions whose kernel stages its output tile anyway (replaces the
- * statistics read of the single-launch BatchNorm forward, gm_bn_fwd_train_grouped_bf16): the
- * layer-1 resident-weight kernel (k_conv_rw, view groups G >= 2: one partial row per persistent
- * workgroup) and the 1x1 / s1 GEMM (k_gemm_ring: one per wave's 64-pixel slab) sum their
+/* The same for the view-grouped trunk convolutions (replaces the statistics read of the
+ * single-launch BatchNorm forward, gm_bn_fwd_train_grouped_bf16): every kernel that stages its
+ * output tile - k_conv_rw (layer 1: one partial row per persistent workgroup), k_conv_h9 and
+ * k_conv_igemm_ut through their LDS-staged epilogue (one row per output tile, split-K
+ * included) and the 1x1 / s1 GEMM k_gemm_ring (one per wave's 64-pixel slab) - sums its
  * stored bf16 outputs per channel (fp32), writing per group [K / 64 slices][rows][64 x (sum,
  * sum of squares)] then 2K floats of coefficient area (group g at stats + g * 2K (rows + 1)).
  * stats holds stats_floats >= gm_conv2d_fwd_bn_stats_floats(d, G) floats; *rows_out receives
- * the rows of the kernel picked.  GM_E_UNSUP (nothing launched) for any other shape (the MFMA-
- * layout epilogues of k_conv_h9 / k_conv_igemm_ut would need a 32-lane reduction per value:
- * measured slower than the statistics read), K % 64 != 0 or 64-bit output offsets.
+ * the rows of the kernel picked.  GM_E_UNSUP (nothing launched) for G < 2, K % 64 != 0, 64-bit
+ * output offsets or a kernel without the staged epilogue (k_conv_halo / k_conv_igemm).
  * Then gm_bn_fwd_stats_finalize_grouped(ps, G, stats, rows) (C = K, any multiple of 64, residual
  * allowed) and gm_bn_fwd_apply_grouped_bf16: y = relu?(x*sc + sh (+ residual)) from the
  * coefficients it left in stats, one launch for evenly strided groups.  Replaces
