@@ -261,6 +261,13 @@ EXPORTS.update({
     "gm_conv2d_fwd_grouped_bn_stats_bf16": (c_int, [c_void_p, c_int, c_void_p, c_void_p, ctypes.c_longlong, c_void_p,
                                                     c_void_p, c_size_t, c_void_p, c_void_p, c_size_t, c_void_p]),
     "gm_bn_fwd_apply_grouped_bf16": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p]),
+    "gm_conv2d_dgrad_bn_stats_floats": (c_size_t, [c_void_p, c_int]),
+    "gm_conv2d_dgrad_grouped_bn_stats_bf16": (c_int, [c_void_p, c_int, c_void_p, c_void_p, ctypes.c_longlong,
+                                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                                      c_void_p, c_void_p, c_size_t, c_void_p]),
+    "gm_bn_bwd_stats_coef_offset": (c_size_t, [c_int, c_int, c_int]),
+    "gm_bn_bwd_stats_finalize_grouped": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p]),
+    "gm_bn_bwd_apply_grouped_bf16": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p]),
     "gm_maxpool2d_bwd_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
 })
 

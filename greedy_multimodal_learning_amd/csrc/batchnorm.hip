@@ -790,6 +790,45 @@ __global__ __launch_bounds__(kFinT) void k_bn_stats_finalize(ReduceArgs a0) {
     }
 }
 
+// The backward's statistics (sum dz, sum dz * (x - mean) per channel) from producer partial
+// rows (the input-gradient convolution's epilogue, gm_conv2d_dgrad_grouped_bn_stats_bf16):
+// combined like k_bn_stats_finalize, then finalize<BWD> - dgamma / dbeta (accumulate) and the
+// apply's coefficients ca, cb, cc at coef0 + g * cstride (the partial rows' group blocks are
+// packed: no room for 3 C coefficients at their end).
+__global__ __launch_bounds__(kFinT) void k_bn_bwd_stats_finalize(ReduceArgs a0, float* coef0, long long cstride) {
+    ReduceArgs a = group_args(a0);
+    a.coef = coef0 + blockIdx.z * cstride;
+    __shared__ double rd[kFinT / 32][128];
+    const int t = threadIdx.x, cs = blockIdx.y;
+    const int lv = t & 31, rg = t >> 5;
+    FinOps fo{};
+    if (t < 64) fo = fin_load<BWD>(a, cs * 64 + t);
+    const float4* rows = reinterpret_cast<const float4*>(a.part + (size_t)cs * a.nrc * 128);
+    double d0 = 0.0, d1 = 0.0, d2 = 0.0, d3 = 0.0;
+    for (int i0 = rg; i0 < a.nrc; i0 += 8 * 32) {
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = i0 + u * 32;
+            v[u] = i < a.nrc ? rows[(size_t)i * 32 + lv] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            d0 += (double)v[u].x; d1 += (double)v[u].y; d2 += (double)v[u].z; d3 += (double)v[u].w;
+        }
+    }
+    rd[rg][4 * lv] = d0; rd[rg][4 * lv + 1] = d1; rd[rg][4 * lv + 2] = d2; rd[rg][4 * lv + 3] = d3;
+    __syncthreads();
+    if (t < 64) {
+        double S1 = 0.0, S2 = 0.0;
+        for (int i = 0; i < kFinT / 32; ++i) {
+            S1 += rd[i][2 * t];
+            S2 += rd[i][2 * t + 1];
+        }
+        finalize<BWD>(a, cs * 64 + t, S1, S2, 1.0 / (double)a.M, fo);
+    }
+}
+
 // ---------------------------------------------------------------------------------
 // Redundant-finalize hand-off of the single-launch kernels for small maps (a.redundant):
 // the last-arriving block no longer combines, finalizes, publishes the coefficients and a
@@ -1315,8 +1354,9 @@ struct ApplyArgs {
     const float* coef;   // [4][C]
     int C;
     const float* fcoef;  // bwd MASKX: the forward's sc[C], sh[C]
-    long long gvec;      // fwd apply, view groups (gridDim.y): group g's x / res / out gvec
+    long long gvec;      // view groups (gridDim.y): group g's x / res / dy / out / out2 gvec
     long long cgs;       // vectors and its coefficients cgs floats after group 0's
+    long long fcgs;      // bwd MASKX: group g's fcoef fcgs floats after group 0's
     uint8_t* mask_out;   // fwd (relu + residual), optional: the ReLU mask bytes (as gvec)
 };
 
@@ -1364,16 +1404,19 @@ __global__ __launch_bounds__(kT) void k_bn_apply_bwd(ApplyArgs a) {
     const long long stride = (long long)gridDim.x * kT;
     long long v = (long long)blockIdx.x * kT + threadIdx.x;
     const int cg = (int)(v & ((1 << a.tpr_log) - 1));
+    const long long go = blockIdx.y * a.gvec;  // view group blockIdx.y
+    const float* coef = a.coef + blockIdx.y * a.cgs;
     float ca[8], cb[8], cc[8], fs[8], fh[8], mu[8];
-    load_coef(a.coef, cg, ca);
-    load_coef(a.coef + a.C, cg, cb);
-    load_coef(a.coef + 2 * a.C, cg, cc);
-    if (CENTER) load_coef(a.coef + 3 * a.C, cg, mu);
+    load_coef(coef, cg, ca);
+    load_coef(coef + a.C, cg, cb);
+    load_coef(coef + 2 * a.C, cg, cc);
+    if (CENTER) load_coef(coef + 3 * a.C, cg, mu);
     if (MASKX) {
-        load_coef(a.fcoef, cg, fs);
-        load_coef(a.fcoef + a.C, cg, fh);
+        load_coef(a.fcoef + blockIdx.y * a.fcgs, cg, fs);
+        load_coef(a.fcoef + blockIdx.y * a.fcgs + a.C, cg, fh);
     }
     auto one = [&](long long i) {
+        i += go;
         float d[8], xf[8];
         V8<E>::ld(a.dy, i, d);
         V8<E>::ld(a.x, i, xf);
@@ -2036,6 +2079,85 @@ extern "C" int gm_bn_fwd_apply_grouped_bf16(const gm_bn_fwd* ps, int G, const fl
             else hipLaunchKernelGGL((k_bn_apply<false, false, uint16_t>), g, dim3(kT), 0, st, b);
         }
         if ((rc = check_launch("k_bn_apply"))) return rc;
+    }
+    return GM_OK;
+}
+
+// The BatchNorm backward from producer statistics (include/greedymml.h): stats as written by
+// gm_conv2d_dgrad_grouped_bn_stats_bf16 - [G] x ([C / 64][rows][64 x (sum dz, sum dz (x - mean))]
+// + 2C floats), then G x 4C floats of backward coefficients.  ps[g]: the backward descriptor
+// (relu with fwd_coef - the mask recomputed from x - or no relu; no dres), C a multiple of 64.
+extern "C" size_t gm_bn_bwd_stats_coef_offset(int C, int G, int rows) {
+    return (size_t)G * 2 * C * (size_t)(rows + 1);
+}
+
+static int check_bwd_from_stats(const gm_bn_bwd* ps, int G, const float* stats, int rows, const char* fn) {
+    int rc = check_groups_bwd(ps, G, fn);
+    if (rc) return rc;
+    const int C = ps[0].C;
+    GM_REQUIRE(stats && rows >= 1 && C >= 64 && C % 64 == 0 && ps[0].M >= 1, "%s: C a multiple of 64, rows >= 1",
+               fn);
+    GM_REQUIRE(!ps[0].dres && (!ps[0].relu || ps[0].fwd_coef),
+               "%s: relu needs fwd_coef (mask from x); no residual gradient", fn);
+    return GM_OK;
+}
+
+extern "C" int gm_bn_bwd_stats_finalize_grouped(const gm_bn_bwd* ps, int G, float* stats, int rows, void* stream) {
+    const char* fn = "gm_bn_bwd_stats_finalize_grouped";
+    int rc = check_bwd_from_stats(ps, G, stats, rows, fn);
+    if (rc) return rc;
+    const int C = ps[0].C;
+    ReduceArgs a{};
+    a.M = ps[0].M; a.C = C; a.SW = 64; a.tpr_log = 3; a.nrc = rows;
+    a.accumulate = ps[0].accumulate;
+    a.part = stats;
+    a.coef = stats;
+    a.scr_stride = (unsigned long long)(rows + 1) * 2 * C * sizeof(float);
+    a.hdr_words = 0;
+    for (int g = 0; g < G; ++g) {
+        BnGroup& q = a.grp[g];
+        q.x = ps[g].x; q.dy = ps[g].dy;
+        q.gamma = ps[g].gamma;
+        q.save_mean = const_cast<float*>(ps[g].save_mean);
+        q.save_invstd = const_cast<float*>(ps[g].save_invstd);
+        q.dgamma = ps[g].dgamma; q.dbeta = ps[g].dbeta;
+    }
+    float* coef0 = stats + gm_bn_bwd_stats_coef_offset(C, G, rows);
+    hipLaunchKernelGGL(k_bn_bwd_stats_finalize, dim3(1, C / 64, G), dim3(kFinT), 0, as_stream(stream), a, coef0,
+                       (long long)4 * C);
+    return check_launch("k_bn_bwd_stats_finalize");
+}
+
+extern "C" int gm_bn_bwd_apply_grouped_bf16(const gm_bn_bwd* ps, int G, const float* stats, int rows, void* stream) {
+    const char* fn = "gm_bn_bwd_apply_grouped_bf16";
+    int rc = check_bwd_from_stats(ps, G, stats, rows, fn);
+    if (rc) return rc;
+    const gm_bn_bwd* p = ps;
+    const int C = p->C;
+    GM_REQUIRE(p->dx && p->dy && p->x, "%s: null argument (dx, dy, x)", fn);
+    const long long gs = p->M * C;
+    bool strided = true;
+    for (int g = 1; g < G; ++g)
+        strided = strided && ps[g].x == static_cast<const uint16_t*>(p->x) + g * gs &&
+                  ps[g].dy == static_cast<const uint16_t*>(p->dy) + g * gs &&
+                  ps[g].dx == static_cast<uint16_t*>(p->dx) + g * gs &&
+                  (!p->relu || ps[g].fwd_coef == p->fwd_coef + (size_t)g * 2 * C);
+    const float* coef0 = stats + gm_bn_bwd_stats_coef_offset(C, G, rows);
+    hipStream_t st = as_stream(stream);
+    const int ng = strided ? 1 : G;
+    for (int gi = 0; gi < ng; ++gi) {
+        ApplyArgs b{};
+        b.nvec = p->M * (C / 8); b.tpr_log = ilog2(C / 8); b.C = C; b.relu = p->relu;
+        b.x = ps[gi].x; b.dy = ps[gi].dy; b.out = ps[gi].dx;
+        b.coef = coef0 + (size_t)gi * 4 * C;
+        b.fcoef = ps[gi].fwd_coef;
+        b.gvec = strided ? gs / 8 : 0;
+        b.cgs = strided ? 4 * C : 0;
+        b.fcgs = strided ? 2 * C : 0;
+        const dim3 g(apply_grid(b.nvec, C), strided ? G : 1);
+        if (p->relu) hipLaunchKernelGGL((k_bn_apply_bwd<true, false, true, uint16_t>), g, dim3(kT), 0, st, b);
+        else hipLaunchKernelGGL((k_bn_apply_bwd<false, false, false, uint16_t>), g, dim3(kT), 0, st, b);
+        if ((rc = check_launch("k_bn_apply_bwd"))) return rc;
     }
     return GM_OK;
 }

@@ -41,6 +41,11 @@ struct RingGemmArgs {
     // (row = a wave's 64-pixel slab, group g at stats + g * 2 N (stats_rows + 1))
     float* stats;
     int stats_rows;
+    // input gradient, optional (with stats): the BatchNorm backward's statistics instead
+    // (ConvArgs::bnx): dz = out where x sc + sh > 0, sums of dz and dz (x - mean)
+    const uint16_t* bnx;
+    const float* bncoef;  // [G][2 N]
+    const float* bnmean;  // [G][N]
 };
 
 // sum over the lanes xor 8, 16, 32 (the lanes sharing lane % 8): DPP row rotate by 8, a
@@ -217,6 +222,23 @@ __global__ __launch_bounds__(512) void k_gemm_ring(RingGemmArgs a) {
             float bs1[8], bs2[8];  // BatchNorm statistics (a.stats): channels 8 o .. + 7 of the wave
 #pragma unroll
             for (int e = 0; e < 8; ++e) bs1[e] = bs2[e] = 0.f;
+            float bsc[8], bsh[8], bmu[8];  // backward statistics (a.bnx): the BN's coefficients
+            if (a.stats && a.bnx) {
+                const int n = n0 + wn * (BN / 2) + 8 * o;
+                const float* cf = a.bncoef + (size_t)g * 2 * a.N + n;
+                const float* mu = a.bnmean + (size_t)g * a.N + n;
+#pragma unroll
+                for (int e = 0; e < 8; e += 4) {
+                    const float4 c0 = *reinterpret_cast<const float4*>(cf + e);
+                    const float4 c1 = *reinterpret_cast<const float4*>(cf + a.N + e);
+                    const float4 c2 = *reinterpret_cast<const float4*>(mu + e);
+                    bsc[e] = c0.x; bsc[e + 1] = c0.y; bsc[e + 2] = c0.z; bsc[e + 3] = c0.w;
+                    bsh[e] = c1.x; bsh[e + 1] = c1.y; bsh[e + 2] = c1.z; bsh[e + 3] = c1.w;
+                    bmu[e] = c2.x; bmu[e + 1] = c2.y; bmu[e + 2] = c2.z; bmu[e + 3] = c2.w;
+                }
+            }
+            const auto xrsrc = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<uint16_t*>(a.bnx ? a.bnx + g * a.gsO : outp), 0, (int)obytes, 0x00020000);
 #pragma unroll
             for (int ii = 0; ii < 2; ++ii) {
 #pragma unroll
@@ -250,6 +272,28 @@ __global__ __launch_bounds__(512) void k_gemm_ring(RingGemmArgs a) {
                                          pack_bf2(f1.x + bf_lo(av[it].z), f1.y + bf_hi(av[it].z)),
                                          pack_bf2(f1.z + bf_lo(av[it].w), f1.w + bf_hi(av[it].w))};
                         __builtin_amdgcn_raw_buffer_store_b128(v, orsrc, off[it], 0, 0);
+                    }
+                } else if (a.stats && a.bnx) {
+                    u32x4 xv[2 * NT];  // the BN input's chunks at the stored positions (rows past M: 0)
+#pragma unroll
+                    for (int it = 0; it < 2 * NT; ++it) xv[it] = __builtin_amdgcn_raw_buffer_load_b128(xrsrc, off[it], 0, 0);
+#pragma unroll
+                    for (int it = 0; it < 2 * NT; ++it) {
+                        const int row = it * RPI + rr;
+                        const float4 f0 = *reinterpret_cast<const float4*>(stg + row * RB + swz(row, 2 * o) * 16);
+                        const float4 f1 = *reinterpret_cast<const float4*>(stg + row * RB + swz(row, 2 * o + 1) * 16);
+                        const u32x4 v = {pack_bf2(f0.x, f0.y), pack_bf2(f0.z, f0.w), pack_bf2(f1.x, f1.y),
+                                         pack_bf2(f1.z, f1.w)};
+                        __builtin_amdgcn_raw_buffer_store_b128(v, orsrc, off[it], 0, 0);
+                        const bool ok = off[it] != 0xfffffff0u;
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) {  // dz = dy where x sc + sh > 0 (the forward's ReLU)
+                            const unsigned w = v[e >> 1], xw = xv[it][e >> 1];
+                            const float x = (e & 1) ? bf_hi(xw) : bf_lo(xw);
+                            const float d = ok && fmaf(x, bsc[e], bsh[e]) > 0.f ? ((e & 1) ? bf_hi(w) : bf_lo(w)) : 0.f;
+                            bs1[e] += d;
+                            bs2[e] = fmaf(d, x - bmu[e], bs2[e]);
+                        }
                     }
                 } else {
 #pragma unroll
@@ -324,7 +368,8 @@ bool conv1x1_ok(int R, int S, int sh, int sw, int ph, int pw, long long M, int K
 
 // Out = A . B^T (+ addend) per group; the caller checked conv1x1_ok
 int conv1x1_gemm(long long M, int Kr, int N, int G, const void* A, long long gsA, const void* B, long long gsB,
-                 void* out, long long gsO, const void* addend, hipStream_t st, const char* fn, float* stats) {
+                 void* out, long long gsO, const void* addend, hipStream_t st, const char* fn, float* stats,
+                 const uint16_t* bnx, const float* bncoef, const float* bnmean) {
     RingGemmArgs r;
     memset(&r, 0, sizeof(r));
     r.A = (const uint16_t*)A;
@@ -338,6 +383,9 @@ int conv1x1_gemm(long long M, int Kr, int N, int G, const void* A, long long gsA
     r.tiles = G * r.tiles_m * r.tiles_n;
     r.gsA = gsA; r.gsB = gsB; r.gsO = gsO;
     r.stats = addend ? nullptr : stats;
+    r.bnx = r.stats ? bnx : nullptr;
+    r.bncoef = bncoef;
+    r.bnmean = bnmean;
     r.stats_rows = (int)((M + 63) / 64);
     const int grid = r.tiles < g_ring_cus ? r.tiles : g_ring_cus;  // persistent: one workgroup per CU
     auto go = [&](auto bnc) -> int {

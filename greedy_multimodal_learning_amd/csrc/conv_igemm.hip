@@ -87,8 +87,55 @@ struct ConvArgs {
     // (gm_bn_fwd_stats_finalize_grouped combines them)
     float* stats;
     int stats_rows;
+    // input gradient, optional (with stats): the statistics of the BatchNorm backward whose dy
+    // this launch writes - the BN's input x (out's layout), its forward coefficients sc, sh
+    // ([G][2 Nout]) and save_mean ([G][Nout]): partial rows of (sum dz, sum dz (x - mean)) with
+    // dz = dy where x sc + sh > 0 (the forward's ReLU; gm_bn_bwd_stats_finalize_grouped)
+    const uint16_t* bnx;
+    const float* bncoef;
+    const float* bnmean;
     ConvCls cls[kMaxCls];
 };
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));  // channel pairs: packed fp32 math
+
+// BatchNorm statistics of one stored 16-B chunk (8 channels) into s1 / s2 (channel pairs):
+// forward - sum y, sum y^2 of the stored values v; backward (BnB) - sum dz, sum dz (x - mean)
+// of the stored input gradient v with x's chunk xv.  Invalid chunks arrive as zeros (no sum).
+struct BnB {
+    f32x2 sc[4], sh[4], mu[4];
+};
+__device__ __forceinline__ void bnb_load(const ConvArgs& a, int grp, int n, BnB& q) {
+    const float* cf = a.bncoef + (size_t)grp * 2 * a.Nout + n;
+    const float* mu = a.bnmean + (size_t)grp * a.Nout + n;
+    const float4 s0 = *reinterpret_cast<const float4*>(cf), s1 = *reinterpret_cast<const float4*>(cf + 4);
+    const float4 h0 = *reinterpret_cast<const float4*>(cf + a.Nout), h1 = *reinterpret_cast<const float4*>(cf + a.Nout + 4);
+    const float4 m0 = *reinterpret_cast<const float4*>(mu), m1 = *reinterpret_cast<const float4*>(mu + 4);
+    q.sc[0] = {s0.x, s0.y}; q.sc[1] = {s0.z, s0.w}; q.sc[2] = {s1.x, s1.y}; q.sc[3] = {s1.z, s1.w};
+    q.sh[0] = {h0.x, h0.y}; q.sh[1] = {h0.z, h0.w}; q.sh[2] = {h1.x, h1.y}; q.sh[3] = {h1.z, h1.w};
+    q.mu[0] = {m0.x, m0.y}; q.mu[1] = {m0.z, m0.w}; q.mu[2] = {m1.x, m1.y}; q.mu[3] = {m1.z, m1.w};
+}
+__device__ __forceinline__ void bn_acc_fwd(const unsigned (&v)[4], f32x2 (&s1)[4], f32x2 (&s2)[4]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const f32x2 f = {bf_lo(v[k]), bf_hi(v[k])};
+        s1[k] += f;
+        s2[k] = __builtin_elementwise_fma(f, f, s2[k]);
+    }
+}
+__device__ __forceinline__ void bn_acc_bwd(const unsigned (&v)[4], const unsigned (&xv)[4], const BnB& q,
+                                           f32x2 (&s1)[4], f32x2 (&s2)[4]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        f32x2 d = {bf_lo(v[k]), bf_hi(v[k])};
+        const f32x2 x = {bf_lo(xv[k]), bf_hi(xv[k])};
+        const f32x2 z = __builtin_elementwise_fma(x, q.sc[k], q.sh[k]);  // fmaf(x, sc, sh) > 0: the
+        d.x = z.x > 0.f ? d.x : 0.f;                                       // single-launch backward's mask
+        d.y = z.y > 0.f ? d.y : 0.f;
+        s1[k] += d;
+        s2[k] = __builtin_elementwise_fma(d, x - q.mu[k], s2[k]);
+    }
+}
 
 // sticky fault word of this translation unit (gm_device_faults): a split whose
 // turnstile wait timed out
@@ -316,22 +363,35 @@ __device__ __forceinline__ void store_tile_lds(const ConvArgs& a, const ConvCls&
 #pragma unroll
     for (int u = 0; u < NU; ++u) __builtin_amdgcn_raw_buffer_store_b128(v[u], orsrc, off[u], 0, 0);
     if (a.stats) {
-        // BatchNorm statistics of the stored values (forward): this thread's chunk c = t % CH
-        // (8 channels) over its NU pixels, then the lanes sharing c (c + CH k: xor 8 / 16 / 32)
-        // and the four waves (LDS past the tile) - one partial row per output tile, row m0 / BM
-        typedef float f32x2 __attribute__((ext_vector_type(2)));
+        // BatchNorm statistics of the stored values (forward: y; input gradient: the BN
+        // backward's dz against x): this thread's chunk c = t % CH (8 channels) over its NU
+        // pixels, then the lanes sharing c (c + CH k: xor 8 / 16 / 32) and the four waves (LDS
+        // past the tile) - one partial row per output tile, row m0 / BM
         f32x2 s1[4], s2[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) s1[k] = s2[k] = f32x2{0.f, 0.f};
+        if (a.bnx) {
+            const auto xrsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.bnx + goff), 0,
+                                                                 (int)out_bytes, 0x00020000);
+            u32x4 xv[NU];
 #pragma unroll
-        for (int u = 0; u < NU; ++u) {
-            const bool ok = off[u] != 0xfffffff0u;
-            const unsigned w4[4] = {ok ? v[u].x : 0u, ok ? v[u].y : 0u, ok ? v[u].z : 0u, ok ? v[u].w : 0u};
+            for (int u = 0; u < NU; ++u) xv[u] = __builtin_amdgcn_raw_buffer_load_b128(xrsrc, off[u], 0, 0);
+            const int n = n0 + 8 * (t % CH);
+            BnB q;
+            bnb_load(a, grp, n < a.Nout ? n : 0, q);
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const f32x2 f = {bf_lo(w4[k]), bf_hi(w4[k])};
-                s1[k] += f;
-                s2[k] = __builtin_elementwise_fma(f, f, s2[k]);
+            for (int u = 0; u < NU; ++u) {
+                const bool ok = off[u] != 0xfffffff0u;
+                const unsigned w4[4] = {ok ? v[u].x : 0u, ok ? v[u].y : 0u, ok ? v[u].z : 0u, ok ? v[u].w : 0u};
+                const unsigned x4[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
+                bn_acc_bwd(w4, x4, q, s1, s2);
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < NU; ++u) {
+                const bool ok = off[u] != 0xfffffff0u;
+                const unsigned w4[4] = {ok ? v[u].x : 0u, ok ? v[u].y : 0u, ok ? v[u].z : 0u, ok ? v[u].w : 0u};
+                bn_acc_fwd(w4, s1, s2);
             }
         }
         float r[16];
@@ -1623,16 +1683,35 @@ __global__ __launch_bounds__(256) void k_conv_rw(ConvArgs a, RwArgs r) {
         __builtin_amdgcn_make_buffer_rsrc(cl.out + g * a.gs_out, 0, (int)(out_bytes < 0x7fffffffu ? out_bytes : 0x7fffffffu),
                                           0x00020000);
 
-    // BatchNorm statistics (a.stats, forward): this thread's channel group t % 8 summed over
-    // the pixels it stores, combined over the workgroup after the last tile (partial row wg)
+    // BatchNorm statistics (a.stats; forward: y, input gradient: the BN backward's dz against
+    // a.bnx): this thread's channel group t % 8 summed over the pixels it stores, combined over
+    // the workgroup after the last tile (partial row wg)
     const int wg = tl;
-    typedef float f32x2 __attribute__((ext_vector_type(2)));  // channel pairs: packed fp32 math
     f32x2 bs1[4], bs2[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) bs1[k] = bs2[k] = f32x2{0.f, 0.f};
+    BnB bq;
+    if (a.stats && a.bnx) bnb_load(a, g, 8 * (t & 7), bq);
+    const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint16_t*>(a.bnx ? a.bnx + g * a.gs_out : cl.out), 0,
+        (int)(out_bytes < 0x7fffffffu ? out_bytes : 0x7fffffffu), 0x00020000);
     int bb = 0;
     for (; tl < r.tiles; tl += nwg) {
         const int nx = tl + nwg;
+        const int b = (int)r.fd_tpi.div((uint32_t)tl);
+        const int p0 = (tl - b * r.tpi) * r.RT;
+        const unsigned tbase = (unsigned)(((size_t)(b * a.Ho + p0) * a.Wo) * a.Nout * 2);
+        // backward statistics: the BN input's chunks of this tile, loaded under the MFMAs
+        // (issued before the next halo's DMA so their wait does not include it)
+        __attribute__((ext_vector_type(4))) unsigned xv[4];
+        if (a.stats && a.bnx && !a.addend) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int e = t + 256 * u;
+                xv[u] = __builtin_amdgcn_raw_buffer_load_b128(xrsrc, (e >> 3) < valid ? tbase + (unsigned)e * 16u
+                                                                                     : 0xfffffff0u, 0, 0);
+            }
+        }
         if (nx < r.tiles) issue_halo(nx, bb ^ 1);  // buffer bb^1 was released by the last barrier
         const int hoff = WB + bb * r.hbytes;
 
@@ -1692,8 +1771,6 @@ __global__ __launch_bounds__(256) void k_conv_rw(ConvArgs a, RwArgs r) {
             __builtin_amdgcn_sched_barrier(0);
         }
 
-        const int b = (int)r.fd_tpi.div((uint32_t)tl);
-        const int p0 = (tl - b * r.tpi) * r.RT;
         if (!a.addend) {
             // epilogue through LDS: the tile's RT whole image rows are one contiguous NHWC
             // block, assembled in LDS (16-B chunks XOR-swizzled by pixel) and written with
@@ -1711,7 +1788,6 @@ __global__ __launch_bounds__(256) void k_conv_rw(ConvArgs a, RwArgs r) {
                 }
             }
             __syncthreads();
-            const unsigned tbase = (unsigned)(((size_t)(b * a.Ho + p0) * a.Wo) * a.Nout * 2);
             uint4 vv[4];  // the four reads together, then the stores (then the statistics)
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -1726,18 +1802,22 @@ __global__ __launch_bounds__(256) void k_conv_rw(ConvArgs a, RwArgs r) {
                     __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, vv[u]), orsrc,
                     (e >> 3) < valid ? tbase + (unsigned)e * 16u : 0xfffffff0u, 0, 0);
             }
-            if (a.stats) {
+            if (a.stats && a.bnx) {
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const bool ok = ((t + 256 * u) >> 3) < valid;
                     const unsigned w4[4] = {ok ? vv[u].x : 0u, ok ? vv[u].y : 0u, ok ? vv[u].z : 0u,
                                             ok ? vv[u].w : 0u};
+                    const unsigned x4[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
+                    bn_acc_bwd(w4, x4, bq, bs1, bs2);
+                }
+            } else if (a.stats) {
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const f32x2 f = {bf_lo(w4[k]), bf_hi(w4[k])};
-                        bs1[k] += f;
-                        bs2[k] = __builtin_elementwise_fma(f, f, bs2[k]);
-                    }
+                for (int u = 0; u < 4; ++u) {
+                    const bool ok = ((t + 256 * u) >> 3) < valid;
+                    const unsigned w4[4] = {ok ? vv[u].x : 0u, ok ? vv[u].y : 0u, ok ? vv[u].z : 0u,
+                                            ok ? vv[u].w : 0u};
+                    bn_acc_fwd(w4, bs1, bs2);
                 }
             }
             // the next tile's halo (issued before these stores) has landed; the stores may
@@ -2803,7 +2883,8 @@ namespace gm {
 bool conv1x1_ok(int R, int S, int sh, int sw, int ph, int pw, long long M, int Kr, int N);
 int conv1x1_gemm(long long M, int Kr, int N, int G, const void* A, long long gsA, const void* B, long long gsB,
                  void* out, long long gsO, const void* addend, hipStream_t st, const char* fn,
-                 float* stats = nullptr);
+                 float* stats = nullptr, const uint16_t* bnx = nullptr, const float* bncoef = nullptr,
+                 const float* bnmean = nullptr);
 }  // namespace gm
 
 extern "C" int gm_conv2d_fwd_hw_bf16(const gm_conv_desc_hw* d, const void* x, const void* w, void* y,
@@ -2997,6 +3078,65 @@ extern "C" int gm_conv2d_dgrad_grouped_bf16(const gm_conv_desc* d, int G, const 
         if (rc) return rc;
     }
     return pick_and_launch(a, s, ws, ws_bytes);
+}
+
+// Input gradient + the statistics of the BatchNorm backward that consumes it (include/
+// greedymml.h): the partial rows of (sum dz, sum dz (x - mean)) from the LDS-staged epilogue
+// (k_conv_rw, k_conv_h9, k_conv_igemm_ut), then G x 4C floats for the backward's coefficients
+// (gm_bn_bwd_stats_finalize_grouped / gm_bn_bwd_apply_grouped_bf16).
+extern "C" size_t gm_conv2d_dgrad_bn_stats_floats(const gm_conv_desc* d, int G) {
+    if (check_desc(d) || G < 1 || G > 64) return 0;
+    const long long M = (long long)d->N * d->H * d->W;
+    long long rows = (M + 63) / 64;  // 64 x 64 tiles: one row per 64 pixels
+    if (rows < 256) rows = 256;      // k_conv_rw: one per workgroup
+    return (size_t)G * 2 * d->C * (size_t)(rows + 1) + (size_t)G * 4 * d->C;
+}
+
+extern "C" int gm_conv2d_dgrad_grouped_bn_stats_bf16(const gm_conv_desc* d, int G, const void* dy, const void* wt,
+                                                     long long wt_stride, void* dx, const void* bn_x,
+                                                     const float* bn_coef, const float* bn_mean, float* stats,
+                                                     size_t stats_floats, int* rows_out, void* ws, size_t ws_bytes,
+                                                     void* stream) {
+    int rc = check_dgrad(d);
+    if (rc) return rc;
+    GM_REQUIRE(dy && wt && dx && bn_x && bn_coef && bn_mean && stats && rows_out, "conv dgrad bn stats: null pointer");
+    GM_REQUIRE(G >= 1 && G <= 64, "conv dgrad bn stats: view groups must be 1..64 (got %d)", G);
+    GM_REQUIRE(G == 1 || wt_stride >= (long long)d->K * d->R * d->S * d->C ||
+                   -wt_stride >= (long long)d->K * d->R * d->S * d->C,
+               "conv dgrad bn stats: group weight stride %lld shorter than one weight", wt_stride);
+    const size_t need = gm_conv2d_dgrad_bn_stats_floats(d, G);
+    GM_REQUIRE(stats_floats >= need, "conv dgrad bn stats: %zu floats < %zu", stats_floats, need);
+    const long long M = (long long)d->N * d->H * d->W;
+    // one dense output class (stride 1: the parity classes of a strided input gradient would
+    // share tile rows), view groups, 64-channel slices, 32-bit offsets
+    if (d->stride != 1 || G < 2 || d->C % 64 != 0 || (size_t)M * d->C * 2 >= 0x7ffff000u) {
+        set_error("conv dgrad bn stats: stride 1, G >= 2, C %% 64 == 0, 32-bit offsets only");
+        return GM_E_UNSUP;
+    }
+    if (gm::conv1x1_ok(d->R, d->S, d->stride, d->stride, d->pad, d->pad, M, d->K, d->C)) {  // k_gemm_ring
+        *rows_out = (int)((M + 63) / 64);
+        return gm::conv1x1_gemm(M, d->K, d->C, G, dy, M * d->K, wt, wt_stride, dx, M * d->C, nullptr,
+                                as_stream(stream), "conv1x1 dgrad", stats, static_cast<const uint16_t*>(bn_x),
+                                bn_coef, bn_mean);
+    }
+    ConvArgs a;
+    const bool full = dgrad_setup(d, dy, wt, dx, a);
+    StemArgs sr;
+    if (!full || a.ncls != 1 || stem_plan(a, sr) > 0) {
+        set_error("conv dgrad bn stats: one dense output class only");
+        return GM_E_UNSUP;
+    }
+    a.G = G;
+    a.gs_in = M * d->K;
+    a.gs_wt = wt_stride;
+    a.gs_out = M * d->C;
+    a.stats = stats;
+    a.bnx = static_cast<const uint16_t*>(bn_x);
+    a.bncoef = bn_coef;
+    a.bnmean = bn_mean;
+    rc = pick_and_launch(a, as_stream(stream), ws, ws_bytes);
+    *rows_out = a.stats_rows;
+    return rc;
 }
 
 extern "C" int gm_conv2d_dgrad_add_bf16(const gm_conv_desc* d, const void* dy, const void* wt, void* dx,

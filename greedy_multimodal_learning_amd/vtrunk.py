@@ -54,6 +54,10 @@ EPI_BN_STATS = os.environ.get("GM_EPI_BN_STATS", "1") != "0"
 # the block-output BatchNorm (+ residual + ReLU) writes its ReLU mask as bits (1/16 of y) and the
 # backward reads them in place of y (GM_BN_RELU_MASK=0: the backward reads y)
 BN_RELU_MASK = os.environ.get("GM_BN_RELU_MASK", "1") != "0"
+# the ReLU-after-BN backward (bn1 / bn2 of a block) takes its statistics from the input-gradient
+# epilogue of the convolution it feeds, then one finalize + one streaming apply
+# (GM_EPI_BN_BWD_STATS=0: the single-launch backward)
+EPI_BN_BWD_STATS = os.environ.get("GM_EPI_BN_BWD_STATS", "1") != "0"
 _GM_E_UNSUP = -3
 
 
@@ -203,6 +207,9 @@ class _VConvFn(torch.autograd.Function):
         from the epilogue (gm_conv2d_fwd_grouped_bn_stats_bf16) when the kernel has them."""
         lib = L.load()
         ctx.join = join
+        # the BatchNorm that produced X (vblock: bn1 -> relu -> conv2), for its backward
+        # statistics from this convolution's input-gradient epilogue
+        ctx.dlink = stats.get("dgrad_link") if stats is not None else None
         GN, C, H, W = X.shape
         N = GN // G
         K, C0, R, S = weights[0].shape
@@ -254,6 +261,22 @@ class _VConvFn(torch.autograd.Function):
                     raise ValueError("vtrunk conv dgrad: addend must be bf16 channels_last shaped like dx")
                 out = add if add is not None else torch.empty(GN, C, H, W, device=dev, dtype=BF, memory_format=CL)
                 ws, nb = _splitk_g(dev, d, G, True)
+                lk = ctx.dlink
+                if add is None and lk is not None and "bn" in lk and EPI_BN_BWD_STATS:
+                    bx, bcoef, bmean = lk.pop("bn")
+                    if tuple(bx.shape) == (GN, C, H, W):
+                        nf = lib.gm_conv2d_dgrad_bn_stats_floats(ctypes.byref(d), G)
+                        part = torch.empty(max(nf, 1), device=dev, dtype=torch.float32)
+                        rows = ctypes.c_int(0)
+                        rc = lib.gm_conv2d_dgrad_grouped_bn_stats_bf16(
+                            ctypes.byref(d), G, gy.data_ptr(), wt.data_ptr(), st, out.data_ptr(), bx.data_ptr(),
+                            bcoef.data_ptr(), bmean.data_ptr(), part.data_ptr(), nf, ctypes.byref(rows), ws, nb,
+                            L.stream_of(dev))
+                        if rc == 0:
+                            lk["part"], lk["rows"], lk["dy"] = part, rows.value, out
+                            return out
+                        if rc != _GM_E_UNSUP:
+                            L.check(rc, "gm_conv2d_dgrad_grouped_bn_stats_bf16")
                 L.check(lib.gm_conv2d_dgrad_grouped_bf16(ctypes.byref(d), G, gy.data_ptr(), wt.data_ptr(), st,
                                                          out.data_ptr(), L.ptr(add), ws, nb, L.stream_of(dev)),
                         "gm_conv2d_dgrad_grouped_bf16")
@@ -363,6 +386,32 @@ def _bn_backward(dz, y, xb, G, gammas, betas, sm, si, relu, want_dres, coef, wan
     return dx, dres, [d if want_w else None for d in dgs], [d if want_b else None for d in dbs]
 
 
+def _bn_backward_from_stats(dz, xb, G, gammas, betas, sm, si, coef, part, rows, want_w, want_b):
+    """The ReLU-after-BN backward with its statistics from the input-gradient epilogue of the
+    convolution that consumed the BN's output (gm_conv2d_dgrad_grouped_bn_stats_bf16): an fp64
+    finalize and one streaming apply.  Returns (dx, grads_w[G], grads_b[G])."""
+    lib = L.load()
+    GN, C, H, W = xb.shape
+    M = (GN // G) * H * W
+    dx = torch.empty_like(xb, memory_format=CL)
+    dgs, dbs, acc, sunk = _bn_param_grads(gammas, betas, want_w, want_b)
+    descs = []
+    for g in range(G):
+        r = slice(g * (GN // G), (g + 1) * (GN // G))
+        descs.append(L.BnBwd(M, C, 1, dz[r].data_ptr(), 0, xb[r].data_ptr(), gammas[g].data_ptr(),
+                             sm[g].data_ptr(), si[g].data_ptr(), dx[r].data_ptr(), 0, dgs[g].data_ptr(),
+                             dbs[g].data_ptr(), int(acc), 0, coef[g].data_ptr(), 0))
+    st = L.stream_of(xb.device)
+    arr = L.arr(L.BnBwd, descs)
+    L.check(lib.gm_bn_bwd_stats_finalize_grouped(arr, G, part.data_ptr(), rows, st), "gm_bn_bwd_stats_finalize_grouped")
+    L.check(lib.gm_bn_bwd_apply_grouped_bf16(arr, G, part.data_ptr(), rows, st), "gm_bn_bwd_apply_grouped_bf16")
+    if sunk:
+        for p in list(gammas) + list(betas):
+            sink_done(p)
+        return dx, [None] * G, [None] * G
+    return dx, [d if want_w else None for d in dgs], [d if want_b else None for d in dbs]
+
+
 class _VBNFn(torch.autograd.Function):
     """relu?(BatchNorm_g(X_g) (+ residual_g)) per view group g of the stacked X."""
 
@@ -408,6 +457,9 @@ class _VBNFn(torch.autograd.Function):
                                                      L.stream_of(dev)), "gm_bn_fwd_train_grouped_bf16")
         ctx.save_for_backward(xb, y if relu and not maskx else coef, sm, si, ymask, *gammas, *betas)
         ctx.meta = (G, maskx, relu, residual is not None)
+        ctx.blink = stats.get("bn_link") if stats is not None else None
+        if ctx.blink is not None and maskx and G >= 2 and C % 64 == 0:
+            ctx.blink["bn"] = (xb, coef, sm)  # for the consuming convolution's input-gradient epilogue
         return y
 
     @staticmethod
@@ -417,9 +469,17 @@ class _VBNFn(torch.autograd.Function):
         gammas, betas = prm[:G], prm[G:]
         y, coef = (None, yc) if maskx else (yc, None)
         want_dres = has_res and ctx.needs_input_grad[1]
+        lk = ctx.blink
+        want_w, want_b = any(ctx.needs_input_grad[7:7 + G]), any(ctx.needs_input_grad[7 + G:])
+        if lk is not None and "part" in lk:  # statistics from the consuming convolution's dgrad
+            part, rows, pdy = lk.pop("part"), lk.pop("rows"), lk.pop("dy")
+            lk.pop("bn", None)
+            if maskx and not want_dres and dy.data_ptr() == pdy.data_ptr() and dy.shape == pdy.shape:
+                dx, gw, gb = _bn_backward_from_stats(pdy, xb, G, gammas, betas, sm, si, coef, part, rows,
+                                                     want_w, want_b)
+                return (dx if ctx.needs_input_grad[0] else None, None, None, None, None, None, None, *gw, *gb)
         dx, dres, gw, gb = _bn_backward(dy, y, xb, G, gammas, betas, sm, si, relu, want_dres, coef,
-                                        any(ctx.needs_input_grad[7:7 + G]), any(ctx.needs_input_grad[7 + G:]),
-                                        ymask)
+                                        want_w, want_b, ymask)
         if dres is not None and ctx.join is not None:
             dres = ctx.join.contribute(lambda add: dres if add is None else dres + add)
         return (dx if ctx.needs_input_grad[0] else None, dres, None, None, None, None, None, *gw, *gb)
@@ -622,19 +682,24 @@ def vblock(blocks, X):
     join = GradJoin()
     ds = b0.downsample is not None
 
-    def cbn(x, convs, bns, cjoin=None, **kw):  # conv -> BatchNorm, statistics from the conv's epilogue
-        st = {}
+    def cbn(x, convs, bns, cjoin=None, link_in=None, link_out=None, **kw):
+        # conv -> BatchNorm, the forward statistics from the conv's epilogue; link_out: this
+        # BN (+ ReLU) feeds the next conv, whose input-gradient epilogue then sums this BN's
+        # backward statistics (link_in of that conv)
+        st = {"dgrad_link": link_in, "bn_link": link_out}
         return vbn(vconv(x, convs, cjoin, stats=st), bns, stats=st, **kw)
     if ds:
         idt = cbn(X, [b.downsample[0] for b in blocks], [b.downsample[1] for b in blocks], join)
     else:
         idt = X
-    out = cbn(X, [b.conv1 for b in blocks], [b.bn1 for b in blocks], join, relu=True)
+    l1 = {}
+    out = cbn(X, [b.conv1 for b in blocks], [b.bn1 for b in blocks], join, link_out=l1, relu=True)
     if hasattr(b0, "conv3"):  # Bottleneck
-        out = cbn(out, [b.conv2 for b in blocks], [b.bn2 for b in blocks], relu=True)
-        return cbn(out, [b.conv3 for b in blocks], [b.bn3 for b in blocks], residual=idt, relu=True,
+        l2 = {}
+        out = cbn(out, [b.conv2 for b in blocks], [b.bn2 for b in blocks], link_in=l1, link_out=l2, relu=True)
+        return cbn(out, [b.conv3 for b in blocks], [b.bn3 for b in blocks], link_in=l2, residual=idt, relu=True,
                    residual_join=None if ds else join)
-    return cbn(out, [b.conv2 for b in blocks], [b.bn2 for b in blocks], residual=idt, relu=True,
+    return cbn(out, [b.conv2 for b in blocks], [b.bn2 for b in blocks], link_in=l1, residual=idt, relu=True,
                residual_join=None if ds else join)
 
 

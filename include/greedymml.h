@@ -618,6 +618,27 @@ int gm_conv2d_fwd_grouped_bn_stats_bf16(const gm_conv_desc_hw* d, int G, const v
                                         long long w_stride, void* y, float* stats, size_t stats_floats,
                                         int* rows_out, void* ws, size_t ws_bytes, void* stream);
 int gm_bn_fwd_apply_grouped_bf16(const gm_bn_fwd* ps, int G, const float* stats, int rows, void* stream);
+/* The BatchNorm backward's statistics from the input-gradient convolution that produces its
+ * dy (replaces the statistics pass of gm_bn_bwd_grouped_bf16 for the ReLU-after-BN of the
+ * torchvision blocks, conv1 -> bn1 -> relu -> conv2: /root/reference/src/model.py:65-76 via
+ * resnet.py).  gm_conv2d_dgrad_grouped_bn_stats_bf16 computes dx = dgrad(dy) like
+ * gm_conv2d_dgrad_grouped_bf16 (no addend) and, in the same epilogue, per channel of dx the
+ * sums of dz and dz * (x - mean) with dz = dx where x * sc + sh > 0: bn_x is the BatchNorm's
+ * input (dx's layout, groups at the same stride), bn_coef its forward coef_out ([G][2C]),
+ * bn_mean its save_mean ([G][C]).  stats: stats_floats >= gm_conv2d_dgrad_bn_stats_floats(d, G)
+ * floats, *rows_out the partial rows per 64-channel slice.  GM_E_UNSUP (nothing launched) for
+ * stride != 1, G < 2, C % 64 != 0, 1x1 shapes or 64-bit offsets.  Then
+ * gm_bn_bwd_stats_finalize_grouped (dgamma / dbeta, accumulate honoured, coefficients into
+ * stats) and gm_bn_bwd_apply_grouped_bf16 (dx_bn = ca dz + cb x + cc, one launch for evenly
+ * strided groups); ps[g] as for gm_bn_bwd_grouped_bf16 with relu + fwd_coef (or no relu), no dres. */
+size_t gm_conv2d_dgrad_bn_stats_floats(const gm_conv_desc* d, int G);
+int gm_conv2d_dgrad_grouped_bn_stats_bf16(const gm_conv_desc* d, int G, const void* dy, const void* wt,
+                                          long long wt_stride, void* dx, const void* bn_x, const float* bn_coef,
+                                          const float* bn_mean, float* stats, size_t stats_floats, int* rows_out,
+                                          void* ws, size_t ws_bytes, void* stream);
+size_t gm_bn_bwd_stats_coef_offset(int C, int G, int rows);
+int gm_bn_bwd_stats_finalize_grouped(const gm_bn_bwd* ps, int G, float* stats, int rows, void* stream);
+int gm_bn_bwd_apply_grouped_bf16(const gm_bn_bwd* ps, int G, const float* stats, int rows, void* stream);
 int gm_bn_relu_maxpool2d_bwd_grouped_bf16(const gm_pool_desc* d, int G, const void* dy_pool, const void* idx,
                                           const void* xsel, const gm_bn_bwd* ps, void* scratch, size_t scratch_bytes,
                                           void* stream);

@@ -141,3 +141,85 @@ def test_relu_mask_bits_backward_bit_identical(shape, epi):
         vtrunk.BN_RELU_MASK = old
     for i, (a, b) in enumerate(zip(out[True], out[False])):
         assert torch.equal(a, b), f"output {i} differs with the mask bits"
+
+
+BWD_SHAPES = [  # N per view, C, H, W, conv2 (R, stride), G, statistics from the dgrad epilogue
+    (4, 64, 56, 56, 3, 1, 2, True),      # layer 1: k_conv_rw input gradient
+    (8, 128, 28, 28, 3, 1, 2, True),     # k_conv_h9
+    (8, 256, 14, 14, 3, 1, 3, True),     # k_conv_h9, 3 groups
+    (8, 512, 7, 7, 3, 1, 2, True),       # layer 4
+    (2, 64, 9, 11, 3, 1, 2, True),       # ragged, small M: 64 x 64 tiles (k_conv_igemm_ut)
+    (4, 128, 28, 28, 3, 2, 2, False),    # strided conv2 (Bottleneck .0): parity classes, declined
+    (4, 256, 14, 14, 1, 1, 2, True),     # 1x1 conv3 (k_gemm_ring, BN = 128)
+    (4, 64, 28, 28, 1, 1, 3, True),      # 1x1, 64 channels (k_gemm_ring, BN = 64), 3 groups
+    (3, 128, 9, 13, 1, 1, 2, True),      # 1x1, ragged M
+]
+
+
+@pytest.mark.parametrize("shape", BWD_SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_bn_backward_statistics_from_dgrad_epilogue(shape, monkeypatch):
+    """conv1 -> bn1 -> relu -> conv2 (the torchvision blocks, /root/reference/src/model.py:65-76
+    via resnet.py): the ReLU-after-BN backward with its statistics summed in conv2's input-
+    gradient epilogue (gm_conv2d_dgrad_grouped_bn_stats_bf16 -> gm_bn_bwd_stats_finalize_grouped
+    -> gm_bn_bwd_apply_grouped_bf16) against the single-launch backward: conv2's input
+    gradient bit-identical, the input / weight / BN parameter gradients within the two
+    summation orders' rounding; for k_conv_rw, k_conv_h9, k_conv_igemm_ut and k_gemm_ring
+    (1x1 conv3); a strided conv2 declines (single-launch backward)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from greedy_multimodal_learning_amd import vtrunk
+    from greedy_multimodal_learning_amd.bn import GMBatchNorm2d
+    from greedy_multimodal_learning_amd.conv import GMConv2d
+    from greedy_multimodal_learning_amd.vtrunk import vbn, vconv
+    dev = torch.device("cuda:0")
+    N, C, H, W, R2, s2, G, epi = shape
+    g = torch.Generator().manual_seed(sum(shape))
+    x = torch.randn(G * N, C, H, W, generator=g).bfloat16().to(dev).contiguous(memory_format=CL)
+    convs1, convs2 = [], []
+    for _ in range(G):
+        m1 = GMConv2d(C, C, 3, padding=1, bias=False).to(dev)
+        m2 = GMConv2d(C, C, R2, stride=s2, padding=R2 // 2, bias=False).to(dev)
+        with torch.no_grad():
+            m1.weight.copy_(torch.randn(C, C, 3, 3, generator=g) / (9 * C) ** 0.5)
+            m2.weight.copy_(torch.randn(C, C, R2, R2, generator=g) / (R2 * R2 * C) ** 0.5)
+        convs1.append(m1.to(memory_format=CL))
+        convs2.append(m2.to(memory_format=CL))
+    P, Q = (H + 2 * (R2 // 2) - R2) // s2 + 1, (W + 2 * (R2 // 2) - R2) // s2 + 1
+    gy = torch.randn(G * N, C, P, Q, generator=g).bfloat16().to(dev).contiguous(memory_format=CL)
+    calls = []
+    real = vtrunk._bn_backward_from_stats
+    monkeypatch.setattr(vtrunk, "_bn_backward_from_stats", lambda *a: calls.append(1) or real(*a))
+    out = {}
+    for path in (True, False):
+        monkeypatch.setattr(vtrunk, "EPI_BN_BWD_STATS", path)
+        calls.clear()
+        bns = []
+        for i in range(G):
+            b = GMBatchNorm2d(C).to(dev)
+            gb = torch.Generator().manual_seed(i)
+            with torch.no_grad():
+                b.weight.copy_(torch.rand(C, generator=gb) + 0.5)
+                b.bias.copy_(torch.rand(C, generator=gb) - 0.5)
+            bns.append(b.train())
+        xs = x.clone().requires_grad_(True)
+        link = {}
+        st1 = {"dgrad_link": None, "bn_link": link}
+        a = vbn(vconv(xs, convs1, stats=st1), bns, relu=True, stats=st1)
+        da = []
+        a.register_hook(lambda t: da.append(t.detach().clone()))
+        y = vconv(a, convs2, stats={"dgrad_link": link, "bn_link": None})
+        y.backward(gy)
+        assert bool(calls) == (epi and path), f"statistics from the dgrad epilogue: {bool(calls)}"
+        out[path] = dict(da=da[0], dx=xs.grad.clone(), dg=[b.weight.grad.clone() for b in bns],
+                         db=[b.bias.grad.clone() for b in bns], w1=[c.weight.grad.clone() for c in convs1],
+                         w2=[c.weight.grad.clone() for c in convs2])
+        for c in convs1 + convs2:
+            c.weight.grad = None
+    a_, b_ = out[True], out[False]
+    assert torch.equal(a_["da"], b_["da"]), "the statistics epilogue changed conv2's input gradient"
+    for i in range(G):
+        _close(a_["dg"][i], b_["dg"][i], 5e-3, f"dgamma[{i}]")
+        _close(a_["db"][i], b_["db"][i], 5e-3, f"dbeta[{i}]")
+        _close(a_["w1"][i], b_["w1"][i], 2e-2, f"conv1 dW[{i}]")
+        assert torch.equal(a_["w2"][i], b_["w2"][i]), f"conv2 dW[{i}]"
+    _close(a_["dx"], b_["dx"], 2e-2, "dx")
