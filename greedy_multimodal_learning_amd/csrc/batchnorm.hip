@@ -1415,32 +1415,74 @@ __global__ __launch_bounds__(kT) void k_bn_apply_bwd(ApplyArgs a) {
         load_coef(a.fcoef + blockIdx.y * a.fcgs, cg, fs);
         load_coef(a.fcoef + blockIdx.y * a.fcgs + a.C, cg, fh);
     }
-    auto one = [&](long long i) {
-        i += go;
-        float d[8], xf[8];
-        V8<E>::ld(a.dy, i, d);
-        V8<E>::ld(a.x, i, xf);
+    constexpr bool YR = RELU && !MASKX;  // the mask read from y
+    auto ld = [&](long long i, float* d, float* xf, float* yf) {
+        V8<E>::ld(a.dy, go + i, d);
+        V8<E>::ld(a.x, go + i, xf);
+        if (YR) V8<E>::ld(a.res, go + i, yf);
+    };
+    auto out = [&](long long i, float* d, const float* xf, const float* yf) {
         if (RELU && MASKX) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) d[j] = fmaf(xf[j], fs[j], fh[j]) > 0.f ? d[j] : 0.f;
         } else if (RELU) {
-            float yf[8];
-            V8<E>::ld(a.res, i, yf);
 #pragma unroll
             for (int j = 0; j < 8; ++j) d[j] = yf[j] > 0.f ? d[j] : 0.f;
         }
-        if (DRES) V8<E>::st(a.out2, i, d);
+        if (DRES) V8<E>::st(a.out2, go + i, d);
         float o[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j)
             o[j] = CENTER ? fmaf(ca[j], d[j], fmaf(cb[j], xf[j] - mu[j], cc[j])) : fmaf(ca[j], d[j], fmaf(cb[j], xf[j], cc[j]));
-        V8<E>::st(a.out, i, o);
+        V8<E>::st(a.out, go + i, o);
     };
-    for (; v + stride < a.nvec; v += 2 * stride) {
-        one(v);
-        one(v + stride);
+    // U vectors' loads issued before the first store (the pointers may alias as far as the
+    // compiler knows: one vector at a time serialised load -> wait -> store, 32 B in flight)
+    constexpr int U = 4;
+    if constexpr (std::is_same<E, uint16_t>::value) {  // raw 16-B loads first, unpacked after
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4* DY = static_cast<const u32x4*>(a.dy) + go;
+        const u32x4* XX = static_cast<const u32x4*>(a.x) + go;
+        const u32x4* YY = static_cast<const u32x4*>(a.res) + go;
+        auto u4 = [](u32x4 w) { return make_uint4(w.x, w.y, w.z, w.w); };
+        for (; v + (U - 1) * stride < a.nvec; v += U * stride) {
+            u32x4 rd[U], rx[U], ry[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                rd[u] = DY[v + u * stride];
+                rx[u] = XX[v + u * stride];
+                if (YR) ry[u] = YY[v + u * stride];
+            }
+            // every load issued before the first use (the compiler otherwise sinks each load to
+            // its use: one vector's 32 B in flight per thread)
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                asm volatile("" : "+v"(rd[u]), "+v"(rx[u]));
+                if (YR) asm volatile("" : "+v"(ry[u]));
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                float d[8], xf[8], yf[8];
+                unpack8(u4(rd[u]), d);
+                unpack8(u4(rx[u]), xf);
+                if (YR) unpack8(u4(ry[u]), yf);
+                out(v + u * stride, d, xf, yf);
+            }
+        }
+    } else {
+        for (; v + (U - 1) * stride < a.nvec; v += U * stride) {
+            float d[U][8], xf[U][8], yf[U][YR ? 8 : 1];
+#pragma unroll
+            for (int u = 0; u < U; ++u) ld(v + u * stride, d[u], xf[u], yf[u]);
+#pragma unroll
+            for (int u = 0; u < U; ++u) out(v + u * stride, d[u], xf[u], yf[u]);
+        }
     }
-    if (v < a.nvec) one(v);
+    for (; v < a.nvec; v += stride) {
+        float d[8], xf[8], yf[YR ? 8 : 1];
+        ld(v, d, xf, yf);
+        out(v, d, xf, yf);
+    }
 }
 
 __global__ void k_bn_infer_coef(int C, const float* gamma, const float* beta, const float* rm, const float* rv,

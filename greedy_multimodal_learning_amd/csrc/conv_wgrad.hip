@@ -1224,12 +1224,21 @@ static bool halo64_ok(const gm_conv_desc_hw* d) {
            d->W >= 1 && d->H >= 64 / halo64_pp(d->W) && d->N >= 1 &&
            (long long)d->N * d->H * d->W * (d->C > d->K ? d->C : d->K) < (1ll << 31);
 }
-// workgroups per (view group, channel tile): about one per CU in all
+// workgroups per (view group, channel tile): GM_WGRAD_HALO64_WGS in all (default 256, about one
+// per CU; the launch runs on the weight-gradient stream beside the input-gradient chain)
+static int halo64_wgs() {
+    static const int w = [] {
+        const char* e = getenv("GM_WGRAD_HALO64_WGS");
+        const int v = e ? atoi(e) : 256;
+        return v < 8 ? 8 : v;
+    }();
+    return w;
+}
 static int halo64_splits(const gm_conv_desc_hw* d, int G) {
     const int rps = 64 / halo64_pp(d->W);
     const int srows = (d->N * d->H + rps - 1) / rps;
     const int tiles = (d->K / 64) * (d->C / 64) * G;
-    int sp = 256 / tiles;
+    int sp = halo64_wgs() / tiles;
     if (sp < 1) sp = 1;
     return sp < srows ? sp : srows;
 }
