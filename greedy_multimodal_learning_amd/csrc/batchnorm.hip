@@ -1376,12 +1376,7 @@ __global__ __launch_bounds__(kT) void k_bn_apply(ApplyArgs a) {
     float sc[8], sh[8];
     load_coef(coef, cg, sc);
     load_coef(coef + a.C, cg, sh);
-    auto one = [&](long long i) {
-        i += go;
-        float f[8];
-        V8<E>::ld(a.x, i, f);
-        float r[8];
-        if (RES) V8<E>::ld(a.res, i, r);
+    auto fin = [&](long long i, float* f, const float* r) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             float z = fmaf(f[j], sc[j], sh[j]);
@@ -1391,6 +1386,43 @@ __global__ __launch_bounds__(kT) void k_bn_apply(ApplyArgs a) {
         V8<E>::st(a.out, i, f);
         if (RES && RELU && std::is_same<E, uint16_t>::value && a.mask_out) a.mask_out[i] = (uint8_t)mask_byte(pack8(f));
     };
+    auto one = [&](long long i) {
+        i += go;
+        float f[8];
+        V8<E>::ld(a.x, i, f);
+        float r[8];
+        if (RES) V8<E>::ld(a.res, i, r);
+        fin(i, f, r);
+    };
+    if constexpr (std::is_same<E, uint16_t>::value) {
+        // four vectors' 16-B loads issued before the first use (as k_bn_apply_bwd)
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        constexpr int U = 4;
+        const u32x4* XX = static_cast<const u32x4*>(a.x) + go;
+        const u32x4* RR = static_cast<const u32x4*>(a.res) + go;
+        for (; v + (U - 1) * stride < a.nvec; v += U * stride) {
+            u32x4 rx[U], rr[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                rx[u] = XX[v + u * stride];
+                if (RES) rr[u] = RR[v + u * stride];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                asm volatile("" : "+v"(rx[u]));
+                if (RES) asm volatile("" : "+v"(rr[u]));
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                float f[8], r[8];
+                unpack8(make_uint4(rx[u].x, rx[u].y, rx[u].z, rx[u].w), f);
+                if (RES) unpack8(make_uint4(rr[u].x, rr[u].y, rr[u].z, rr[u].w), r);
+                fin(go + v + u * stride, f, r);
+            }
+        }
+        for (; v < a.nvec; v += stride) one(v);
+        return;
+    }
     for (; v + stride < a.nvec; v += 2 * stride) {
         one(v);
         one(v + stride);

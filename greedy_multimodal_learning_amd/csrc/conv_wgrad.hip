@@ -1224,12 +1224,15 @@ static bool halo64_ok(const gm_conv_desc_hw* d) {
            d->W >= 1 && d->H >= 64 / halo64_pp(d->W) && d->N >= 1 &&
            (long long)d->N * d->H * d->W * (d->C > d->K ? d->C : d->K) < (1ll << 31);
 }
-// workgroups per (view group, channel tile): GM_WGRAD_HALO64_WGS in all (default 256, about one
-// per CU; the launch runs on the weight-gradient stream beside the input-gradient chain)
+// workgroups per (view group, channel tile): GM_WGRAD_HALO64_WGS in all, default 128 - half the
+// CUs: the launch runs on the weight-gradient stream beside the input-gradient chain, and one
+// workgroup per CU (512 threads, 81 KB of LDS) left no room on any CU for that chain's BN
+// finalize / apply launches (C2, in the step: 64 / 96 / 128 / 160 / 256 workgroups = 3.80 /
+// 3.67 / 3.63 / 3.63 / 3.70 ms; as k_wgrad_ring's half-CU grid)
 static int halo64_wgs() {
     static const int w = [] {
         const char* e = getenv("GM_WGRAD_HALO64_WGS");
-        const int v = e ? atoi(e) : 256;
+        const int v = e ? atoi(e) : 128;
         return v < 8 ? 8 : v;
     }();
     return w;
