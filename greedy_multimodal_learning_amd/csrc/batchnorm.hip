@@ -113,6 +113,17 @@ __device__ __forceinline__ uint4 mask_vals(unsigned b) {
     return make_uint4(v[0], v[1], v[2], v[3]);
 }
 
+// Pin loaded values at this point: every load issued before is complete here, and none is sunk
+// past it to its first use (the compiler otherwise issues a streaming loop's loads one round
+// trip at a time - the ReLU mask bytes after the 16-B vectors had landed)
+typedef unsigned pin_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void pin(uint4& v) {
+    pin_u32x4 w = {v.x, v.y, v.z, v.w};
+    asm volatile("" : "+v"(w));
+    v = make_uint4(w.x, w.y, w.z, w.w);
+}
+__device__ __forceinline__ void pin(unsigned& v) { asm volatile("" : "+v"(v)); }
+
 // Per-view-group operands: a grouped launch (gm_bn_*_grouped_bf16) normalises G views
 // stacked along the batch, each with its own parameters, statistics and scratch, in one
 // grid (blockIdx.z = group); every kernel starts from group_args().
@@ -1203,7 +1214,8 @@ __global__ __launch_bounds__(kT, NR == 8 ? 2 : 3) void k_bn_bwd_fused(ReduceArgs
     const uint4 z = make_uint4(0u, 0u, 0u, 0u);
     constexpr int NV = NR > 0 ? NR : 1;
     constexpr int NY = MODE == BWD_RELU ? NV : 1;
-    constexpr int US = MODE == BWD_RELU ? 2 : 4;  // streaming rows in flight (register budget)
+    // streaming rows in flight (register budget: y's vectors; the mask bytes (YM) cost one each)
+    constexpr int US = MODE == BWD_RELU && !YM ? 2 : 4;
     uint4 vx[NV], vd[NV], vy[NY];
     float s1[8], s2[8];
 #pragma unroll
@@ -1226,15 +1238,26 @@ __global__ __launch_bounds__(kT, NR == 8 ? 2 : 3) void k_bn_bwd_fused(ReduceArgs
         const long long st = (long long)rpp * vpr;
         for (; r + (US - 1) * rpp < rend; r += US * rpp) {
             uint4 wx[US], wd[US], wy[US];
+            unsigned wm[US];
 #pragma unroll
             for (int u = 0; u < US; ++u) {
                 const long long i = r * vpr + cv + u * st;
                 wx[u] = X[i];
                 wd[u] = DY[i];
-                if (MODE == BWD_RELU) wy[u] = ldy(i);
+                if (MODE == BWD_RELU && YM) wm[u] = a.ymask[i];
+                else if (MODE == BWD_RELU) wy[u] = Y[i];
             }
 #pragma unroll
-            for (int u = 0; u < US; ++u) accum_vals<MODE>(wx[u], wd[u], MODE == BWD_RELU ? wy[u] : z, mu, s1, s2, fsc, fsh);
+            for (int u = 0; u < US; ++u) {
+                pin(wx[u]);
+                pin(wd[u]);
+                if (MODE == BWD_RELU && YM) pin(wm[u]);
+                else if (MODE == BWD_RELU) pin(wy[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < US; ++u)
+                accum_vals<MODE>(wx[u], wd[u], MODE == BWD_RELU ? (YM ? mask_vals(wm[u]) : wy[u]) : z, mu, s1, s2, fsc,
+                                 fsh);
         }
         for (; r < rend; r += rpp) {
             const long long i = r * vpr + cv;
@@ -1325,15 +1348,25 @@ __global__ __launch_bounds__(kT, NR == 8 ? 2 : 3) void k_bn_bwd_fused(ReduceArgs
         const long long st = (long long)rpp * vpr;
         for (; r + (US - 1) * rpp < rend; r += US * rpp) {
             uint4 wx[US], wd[US], wy[US];
+            unsigned wm[US];
 #pragma unroll
             for (int u = 0; u < US; ++u) {
                 const long long i = r * vpr + cv + u * st;
                 wx[u] = X[i];
                 wd[u] = DY[i];
-                if (MODE == BWD_RELU) wy[u] = ldy(i);
+                if (MODE == BWD_RELU && YM) wm[u] = a.ymask[i];
+                else if (MODE == BWD_RELU) wy[u] = Y[i];
             }
 #pragma unroll
-            for (int u = 0; u < US; ++u) out(wx[u], wd[u], MODE == BWD_RELU ? wy[u] : z, r * vpr + cv + u * st);
+            for (int u = 0; u < US; ++u) {
+                pin(wx[u]);
+                pin(wd[u]);
+                if (MODE == BWD_RELU && YM) pin(wm[u]);
+                else if (MODE == BWD_RELU) pin(wy[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < US; ++u)
+                out(wx[u], wd[u], MODE == BWD_RELU ? (YM ? mask_vals(wm[u]) : wy[u]) : z, r * vpr + cv + u * st);
         }
         for (; r < rend; r += rpp) {
             const long long i = r * vpr + cv;
