@@ -181,7 +181,7 @@ __device__ __forceinline__ void seg_any(int vec, floatx4& acc, const gm_operand&
 struct GemmForm { int nw, u; };
 // forms 4 / 5: timing diagnostics of form 1 (outputs meaningless): arguments and one
 // store only / everything but the operand loads and MFMAs
-constexpr GemmForm kForms[] = {{4, 8}, {4, 16}, {8, 16}, {16, 8}, {4, 16}, {4, 16}};
+constexpr GemmForm kForms[] = {{4, 8}, {4, 16}, {8, 16}, {16, 8}};
 static int g_gemm_form = 1, g_gemm_vec = 1;
 
 // The MMTM GEMMs are dependent-latency chains (kernel arguments -> operand loads ->
@@ -189,7 +189,7 @@ static int g_gemm_form = 1, g_gemm_vec = 1;
 // the problem index is the grid's y (no tile-table lookup before the argument loads),
 // the epilogue's operands (bias, relu mask, accumulated C) are loaded together with the
 // first operand round, and a wave's K range is at most two load rounds.
-template <int NW, int U, int DIAG = 0>
+template <int NW, int U>
 __global__ __launch_bounds__(NW * 64) void k_gemm_f32(GemmArgs a) {
     __shared__ floatx4 red[NW][64];
     const int pi = blockIdx.y;
@@ -198,10 +198,6 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_f32(GemmArgs a) {
     const int TM = cfg & 31, TN = (cfg >> 5) & 31, KS = (cfg >> 10) & 31;
     const int wg = blockIdx.x;
     if (wg >= a.tile_start[pi + 1] - a.tile_start[pi]) return;
-    if (DIAG == 1) {  // timing diagnostic: arguments only, one store
-        if (threadIdx.x == 0 && wg == 0) p.C[0] = (float)cfg;
-        return;
-    }
     const int wm = wg / a.tiles_n[pi], wn = wg - wm * a.tiles_n[pi];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tile = wave / KS, ks = wave - tile * KS;
@@ -229,8 +225,8 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_f32(GemmArgs a) {
         }
     }
     floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-    if (DIAG != 2) seg_any<U>(a.vec, acc, p.A[0], p.B[0], mm, nn, mrow, ncol, lk, kb, min(ke, K0));
-    if (DIAG != 2 && p.K[1] > 0)
+    seg_any<U>(a.vec, acc, p.A[0], p.B[0], mm, nn, mrow, ncol, lk, kb, min(ke, K0));
+    if (p.K[1] > 0)
         seg_any<U>(a.vec, acc, p.A[1], p.B[1], mm, nn, mrow, ncol, lk, max(kb, K0) - K0, ke - K0);
     if (KS > 1) {
         red[wave][lane] = acc;
@@ -304,9 +300,7 @@ extern "C" int gm_gemm_f32(const gm_gemm* in, int nprob, void* stream) {
         case 0: k_gemm_f32<4, 8><<<grid, 256, 0, st>>>(a); break;
         case 1: k_gemm_f32<4, 16><<<grid, 256, 0, st>>>(a); break;
         case 2: k_gemm_f32<8, 16><<<grid, 512, 0, st>>>(a); break;
-        case 3: k_gemm_f32<16, 8><<<grid, 1024, 0, st>>>(a); break;
-        case 4: k_gemm_f32<4, 16, 1><<<grid, 256, 0, st>>>(a); break;  // diagnostics
-        default: k_gemm_f32<4, 16, 2><<<grid, 256, 0, st>>>(a); break;
+        default: k_gemm_f32<16, 8><<<grid, 1024, 0, st>>>(a); break;
     }
     return check_launch("k_gemm_f32");
 }
@@ -314,7 +308,7 @@ extern "C" int gm_gemm_f32(const gm_gemm* in, int nprob, void* stream) {
 extern "C" int gm_gemm_set_form(int form) {
     g_gemm_vec = !(form & 256);  // bit 8: scalar k-steps only
     form &= 255;
-    GM_REQUIRE(form >= 0 && form < (int)(sizeof(kForms) / sizeof(kForms[0])), "gemm form must be 0..5 (got %d)",
+    GM_REQUIRE(form >= 0 && form < (int)(sizeof(kForms) / sizeof(kForms[0])), "gemm form must be 0..3 (got %d)",
                form);
     g_gemm_form = form;
     return GM_OK;

@@ -167,8 +167,8 @@ typedef struct gm_gemm {
 
 int gm_gemm_f32(const gm_gemm* p, int nprob, void* stream);
 /* A/B knob: fp32 GEMM form, waves per workgroup x k-steps per load round:
- * 0 = 4 x 8, 1 = 4 x 16 (default), 2 = 8 x 16, 3 = 16 x 8; + 256: no float4 k-segments
- * (4, 5: timing diagnostics).  Process-wide. */
+ * 0 = 4 x 8, 1 = 4 x 16 (default), 2 = 8 x 16, 3 = 16 x 8; + 256: no float4 k-segments.
+ * Process-wide. */
 int gm_gemm_set_form(int form);
 
 /* ---------------------------------------------------------------------------
