@@ -772,20 +772,26 @@ __global__ __launch_bounds__(kFinT) void k_bn_stats_finalize(ReduceArgs a0) {
     __shared__ double rd[kFinT / 32][128];
     const int t = threadIdx.x, cs = blockIdx.y;  // channel slice cs (64 channels)
     const int lv = t & 31, rg = t >> 5;
-    FinOps fo{};
-    if (t < 64) fo = fin_load<FWD>(a, cs * 64 + t);
-    if (a.nbt && cs == 0 && t == 0) *a.nbt += 1;
+    FinOps fo;
+    {  // every thread, no branch (a conditional load here cost wave 0 a waited round trip
+       // before its row loads); threads t >= 64 load channel t % 64's again, unused
+        const int c = cs * 64 + (t & 63);
+        const float* rm = a.rmean ? a.rmean : a.gamma;
+        const float* rv = a.rmean ? a.rvar : a.gamma;
+        fo.g = a.gamma[c];
+        fo.b = a.beta[c];
+        fo.rm = rm[c];
+        fo.rv = rv[c];
+    }
     const float4* rows = reinterpret_cast<const float4*>(a.part + (size_t)cs * a.nrc * 128);
     double d0 = 0.0, d1 = 0.0, d2 = 0.0, d3 = 0.0;
     for (int i0 = rg; i0 < a.nrc; i0 += 8 * 32) {
-        float4 v[8];
+        float4 v[8];  // clamped rows, all eight loads in flight, then the value select (a
+#pragma unroll    // conditional load compiled to a branch and a full wait per row)
+        for (int u = 0; u < 8; ++u) v[u] = rows[(size_t)min(i0 + u * 32, a.nrc - 1) * 32 + lv];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            const int i = i0 + u * 32;
-            v[u] = i < a.nrc ? rows[(size_t)i * 32 + lv] : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
+            if (i0 + u * 32 >= a.nrc) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
             d0 += (double)v[u].x; d1 += (double)v[u].y; d2 += (double)v[u].z; d3 += (double)v[u].w;
         }
     }
@@ -797,7 +803,8 @@ __global__ __launch_bounds__(kFinT) void k_bn_stats_finalize(ReduceArgs a0) {
             S1 += rd[i][2 * t];
             S2 += rd[i][2 * t + 1];
         }
-        finalize<FWD>(a, cs * 64 + t, S1, S2, 1.0 / (double)a.M, fo);
+        finalize<FWD>(a, cs * 64 + t, S1, S2, 1.0 / (double)a.M, fo);  // (rm / rv unused without rmean)
+        if (a.nbt && cs == 0 && t == 0) *a.nbt += 1;
     }
 }
 
@@ -812,19 +819,16 @@ __global__ __launch_bounds__(kFinT) void k_bn_bwd_stats_finalize(ReduceArgs a0, 
     __shared__ double rd[kFinT / 32][128];
     const int t = threadIdx.x, cs = blockIdx.y;
     const int lv = t & 31, rg = t >> 5;
-    FinOps fo{};
-    if (t < 64) fo = fin_load<BWD>(a, cs * 64 + t);
+    const FinOps fo = fin_load<BWD>(a, cs * 64 + (t & 63));  // every thread: no branch, no early wait
     const float4* rows = reinterpret_cast<const float4*>(a.part + (size_t)cs * a.nrc * 128);
     double d0 = 0.0, d1 = 0.0, d2 = 0.0, d3 = 0.0;
     for (int i0 = rg; i0 < a.nrc; i0 += 8 * 32) {
-        float4 v[8];
+        float4 v[8];  // clamped rows, all eight loads in flight, then the value select (a
+#pragma unroll    // conditional load compiled to a branch and a full wait per row)
+        for (int u = 0; u < 8; ++u) v[u] = rows[(size_t)min(i0 + u * 32, a.nrc - 1) * 32 + lv];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            const int i = i0 + u * 32;
-            v[u] = i < a.nrc ? rows[(size_t)i * 32 + lv] : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
+            if (i0 + u * 32 >= a.nrc) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
             d0 += (double)v[u].x; d1 += (double)v[u].y; d2 += (double)v[u].z; d3 += (double)v[u].w;
         }
     }
