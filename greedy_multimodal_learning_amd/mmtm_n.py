@@ -81,6 +81,9 @@ class _MMTMNStackedFn(torch.autograd.Function):
 
 
 def _mmtmn_forward(ctx, cfg, w_sq, b_sq, xs, w_e, b_e, ys=None):
+    # no zero-filled gradients for the non-differentiable side outputs (the N excitations and
+    # the squeeze): autograd otherwise materialises them, 3 x (N + 1) fills per C5 step
+    ctx.set_materialize_grads(False)
     N = cfg["N"]
     dev = xs[0].device
     B = xs[0].shape[0]
