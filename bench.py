@@ -205,6 +205,24 @@ def spawn_ranks(n, script, argv, poll_s=0.2):
     return rc
 
 
+def dp_info(step, dist_on):
+    """What the communicator saw: the backend and world size as the process
+    groups report them, the gradient buckets in all-reduce order and whether the all-reduces were
+    captured inside the step graph - so the driver's N > 1 record proves N RCCL ranks took part."""
+    info = {"dist_backend": None, "world_size": 1, "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES")}
+    if not dist_on:
+        return info
+    pg = step.pg
+    info.update(dist_backend=dist.get_backend(pg), world_size=dist.get_world_size(pg),
+                collectives_in_graph=bool(step.graph_collectives),
+                capture_group_size=(dist.get_world_size(step._capture_pg) if step._capture_pg is not None
+                                    else None),
+                nccl_max_nchannels=os.environ.get("NCCL_MAX_NCHANNELS"))
+    if step.buckets is not None:
+        info["buckets_mb"] = [round((e - s) * 4 / 2 ** 20, 2) for s, e, _ in step.buckets.buckets]
+    return info
+
+
 def main():
     a = parse()
     if "RANK" not in os.environ and a.gpus > 1:
@@ -347,7 +365,8 @@ def main():
                        "global_batch": B * world, "per_gpu_batch": B, "image": a.size,
                        "parallelism": f"dp{world}", "samples_per_s": round(world * B * a.steps / elapsed, 2),
                        "hipgraph": bool(step.graphs), "device_gate": bool(step.device_gate),
-                       "curation_steps_timed": curation_steps, "final_loss": round(loss, 4)},
+                       "curation_steps_timed": curation_steps, "final_loss": round(loss, 4),
+                       "dp": dp_info(step, dist_on)},
             "roofline": conv_roofline(conv, conv_traffic if a.dtype == "bf16" and a.workload == "C2" else None,
                                       a.dtype, a.workload),
             "roofline_hbm": {"kernel": "k_group_sumsq<SGD> (fused per-branch norms + SGD, gm_group_sumsq)",

@@ -92,16 +92,17 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
     return make_uint4(pack_bf2(f[0], f[1]), pack_bf2(f[2], f[3]), pack_bf2(f[4], f[5]), pack_bf2(f[6], f[7]));
 }
 
-// The ReLU mask of 8 stored bf16 values as one byte (bit j: value j > 0, i.e. the bf16 half as a
-// signed 16-bit integer is positive - exactly the backward's y > 0 test on the stored y), and
-// back as 8 bf16 values (1.0 where set) that the y-mask code paths test unchanged
+// The ReLU mask of 8 stored bf16 values as one byte (bit j: value j > 0 - the bf16 half in
+// 0x0001 .. 0x7f80, positive and not NaN: exactly the backward's y > 0 test on the stored y, also
+// for the NaN poison a spin timeout writes), and back as 8 bf16 values (1.0 where set) that the
+// y-mask code paths test unchanged
 __device__ __forceinline__ unsigned mask_byte(uint4 w) {
     const unsigned v[4] = {w.x, w.y, w.z, w.w};
     unsigned b = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        b |= ((int)(short)(v[k] & 0xffffu) > 0 ? 1u : 0u) << (2 * k);
-        b |= ((int)v[k] > 0x0000ffff ? 1u : 0u) << (2 * k + 1);
+        b |= ((v[k] & 0xffffu) - 1u < 0x7f80u ? 1u : 0u) << (2 * k);
+        b |= ((v[k] >> 16) - 1u < 0x7f80u ? 1u : 0u) << (2 * k + 1);
     }
     return b;
 }

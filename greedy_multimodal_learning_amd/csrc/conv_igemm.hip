@@ -153,6 +153,15 @@ __device__ __forceinline__ int block_id(int xcd) {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
 }
 
+// The same bijection over [0, n) for a block ordinal l inside a range of n blocks that starts at
+// any fixed offset: the blocks whose l agree mod 8 sit on one XCD ((start + l) % 8), and they get one
+// contiguous tile range.  Applied per split of a split-K launch (blocks [s T, (s + 1) T)), it keeps the
+// split-major dispatch order the turnstile relies on: tile t is block l in every split.
+__device__ __forceinline__ int xcd_range(int l, int n) {
+    const int q = n >> 3, r = n & 7, x = l & 7;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (l >> 3);
+}
+
 __device__ __attribute__((aligned(16))) const uint4 g_zero16[1] = {{0u, 0u, 0u, 0u}};
 
 // bits i in [0, n) with 0 <= x + d0 + s*i < lim (s = +-1): one contiguous range
@@ -650,12 +659,17 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint4 smem[];
     char* lds = reinterpret_cast<char*>(smem);   // [A0..A(NST-1)][B0..B(NST-1)]
 
-    int bid = block_id(a.xcd);
+    // xcd 1: each XCD a contiguous tile range, tm fastest (one weight slice per XCD; unsplit only);
+    // xcd 2: each XCD a contiguous tile range of every split, tn fastest - the column tiles of one
+    // pixel range (one im2col A block, re-read by every column tile) share an L2, and a group's
+    // tiles stay on its own XCDs
+    int bid = a.xcd == 1 ? block_id(1) : (int)blockIdx.x;
     int split = 0;
     if (a.splits > 1) {
         split = bid / a.tiles_total;
         bid -= split * a.tiles_total;
     }
+    if (a.xcd == 2) bid = xcd_range(bid, a.splits > 1 ? a.tiles_total : (int)gridDim.x);
     const int tid = bid;  // launch-wide tile index: split-K slab and turnstile word
     int g = 0;            // view group
     if (a.G > 1) {
@@ -675,8 +689,8 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
     // with a power-of-two column count the round-robin XCD dealing (block b on XCD b % 8)
     // keeps each weight slice on the same XCD(s) - L2-resident instead of re-fetched
     const int tiles_n = (a.Nout + BN - 1) / BN;
-    const int tm = a.xcd ? wgid % cl.tiles_m : wgid / tiles_n;
-    const int tn = a.xcd ? wgid / cl.tiles_m : wgid - tm * tiles_n;
+    const int tm = a.xcd == 1 ? wgid % cl.tiles_m : wgid / tiles_n;
+    const int tn = a.xcd == 1 ? wgid / cl.tiles_m : wgid - tm * tiles_n;
     const int m0 = tm * BM, n0 = tn * BN;
     const int PQ = cl.P * cl.Q;
     const int M = a.N * PQ;
@@ -2200,13 +2214,13 @@ static int stages() {
     return s;
 }
 
-static int xcd_remap() {
-    static int on = [] {
-        const char* e = getenv("GM_CONV_XCD");  // off by default: measured no gain
-        return (e && e[0] == '1') ? 1 : 0;
-    }();
-    return on;
-}
+// GM_CONV_XCD (k_conv_igemm_ut's tile order over the XCDs): 0 = dispatch order, 1 = tm fastest per
+// XCD (measured no gain, r01), 2 = tn fastest per XCD, split-K included
+static int g_xcd_mode = [] {
+    const char* e = getenv("GM_CONV_XCD");
+    return e ? atoi(e) : 0;
+}();
+static int xcd_remap() { return g_xcd_mode; }
 
 static int tile_bias() {
     static int b = [] {
@@ -2632,7 +2646,8 @@ static int pick_and_launch(ConvArgs& a, hipStream_t st, void* ws, size_t ws_byte
         p = {M / 128 * ((a.Nout + 63) / 64) >= tile_bias() * 3 / 4 ? T128x64 : T64x64, 1, 0};
     }
     a.splits = p.splits;
-    a.xcd = p.splits > 1 ? 0 : xcd_remap();  // split-K relies on split-major dispatch order
+    // (mode 1 only unsplit: split-K relies on split-major dispatch order, which mode 2 keeps)
+    a.xcd = xcd_remap() == 2 ? 2 : (p.splits > 1 ? 0 : (xcd_remap() == 1));
     if (p.splits > 1) {
         a.spin_limit = spin_limit();
         a.flags = static_cast<unsigned*>(ws);
@@ -3003,9 +3018,18 @@ extern "C" int gm_conv2d_fwd_grouped_bn_stats_bf16(const gm_conv_desc_hw* d, int
         set_error("conv fwd bn stats: view groups (G >= 2) only");
         return GM_E_UNSUP;
     }
+    StemArgs sr;
+    if (stem_plan(a, sr) > 0) {  // the stem's statistics come from gm_conv2d_fwd_grouped_stats_bf16
+        set_error("conv fwd bn stats: stem shapes take the stem statistics entry point");
+        return GM_E_UNSUP;
+    }
     a.stats = stats;
     rc = pick_and_launch(a, as_stream(stream), ws, ws_bytes);
     *rows_out = a.stats_rows;
+    if (rc == GM_OK && a.stats_rows == 0) {  // a kernel without the staged epilogue ran
+        set_error("conv fwd bn stats: the kernel chosen for this shape writes no statistics");
+        return GM_E_UNSUP;
+    }
     return rc;
 }
 

@@ -709,7 +709,130 @@ __device__ __forceinline__ void ring_load(bf16x8& fa, bf16x8 (&fb)[9], unsigned 
     ring_load_b<BK, KS>(fb, ba, std::make_integer_sequence<int, 9>{});
 }
 
+// k_wgrad_ring's compute waves in the CW = 1 form (see the kernel): wave w = kh + 2 ch.
+template <int S, int BK, int CH>
+__device__ __forceinline__ void ring_compute_split_ch(const WRingArgs& a, int w, int lane, unsigned lds0, int nst,
+                                                      int grp, int split, int k0, int n0) {
+    using Geo = RingGeo<BK>;
+    const int kh = w & 1;
+    floatx16 acc[9];  // [4 i + jj]: k-block 2 kh + i x column block 5 CH + jj; [8]: (2 kh + CH, 4)
+#pragma unroll
+    for (int j = 0; j < 9; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+    // tr-read geometry as CW = 0: half-wave g >> 1 reads rows 8 (g >> 1) + q4 (+4) of a 16-row k-slice,
+    // 4-column block p4 of the 32-column fragment, 16-column half g & 1.  The A image's chunk swizzle
+    // (XOR 4 on odd row pairs) flips the 64-column half's bit, so the two A fragments of a lane sit
+    // at +-64 B of each other by row: two base registers.
+    const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+    const int rbase = 8 * (g >> 1) + q4;
+    const int cin = 16 * (g & 1) + 4 * p4;
+    unsigned a_l[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int ac = 32 * i + cin;
+        a_l[i] = Geo::B + kh * Geo::AB + rbase * 128 + ((((ac >> 3) ^ wswz<128>(rbase))) << 4) + (ac & 7) * 2;
+    }
+    const unsigned b_l = rbase * 64 + cin * 2 + 5 * CH * Geo::BB, b_4 = rbase * 64 + cin * 2 + 4 * Geo::BB;
+    bf16x8 fa[2][2], fb[2][5];
+    auto load_ks = [&](auto ksc, int c, unsigned sb) __attribute__((always_inline)) {
+        constexpr int KS = decltype(ksc)::value;
+        fa[c][0] = ring_frag<KS * 2048, KS * 2048 + 512>(sb + a_l[0]);
+        fa[c][1] = ring_frag<KS * 2048, KS * 2048 + 512>(sb + a_l[1]);
+        fb[c][0] = ring_frag<0 * Geo::BB + KS * 1024, 0 * Geo::BB + KS * 1024 + 256>(sb + b_l);
+        fb[c][1] = ring_frag<1 * Geo::BB + KS * 1024, 1 * Geo::BB + KS * 1024 + 256>(sb + b_l);
+        fb[c][2] = ring_frag<2 * Geo::BB + KS * 1024, 2 * Geo::BB + KS * 1024 + 256>(sb + b_l);
+        fb[c][3] = ring_frag<3 * Geo::BB + KS * 1024, 3 * Geo::BB + KS * 1024 + 256>(sb + b_l);
+        fb[c][4] = ring_frag<KS * 1024, KS * 1024 + 256>(sb + b_4);
+    };
+    auto load = [&](int ks, int c, unsigned sb) __attribute__((always_inline)) {
+        switch (ks) {
+            case 0: load_ks(std::integral_constant<int, 0>{}, c, sb); break;
+            case 1: load_ks(std::integral_constant<int, 1>{}, c, sb); break;
+            case 2: load_ks(std::integral_constant<int, 2 % Geo::SLICES>{}, c, sb); break;
+            default: load_ks(std::integral_constant<int, 3 % Geo::SLICES>{}, c, sb); break;
+        }
+    };
+    auto wait_frags = [&](int c) __attribute__((always_inline)) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        asm volatile("" : "+v"(fa[c][0]), "+v"(fa[c][1]));
+#pragma unroll
+        for (int j = 0; j < 5; ++j) asm volatile("" : "+v"(fb[c][j]));
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    int slot = 0;
+    if (nst > 0) {
+        __builtin_amdgcn_s_barrier();  // step 0 landed
+        unsigned sb = lds0;
+        load(0, 0, sb);
+        for (int i = 0; i < nst; ++i) {
+#pragma unroll
+            for (int ks = 0; ks < Geo::SLICES; ++ks) {
+                const int c = ks & 1;
+                wait_frags(c);
+                if (ks + 1 < Geo::SLICES) {
+                    load(ks + 1, c ^ 1, sb);
+                } else if (i + 1 < nst) {
+                    __builtin_amdgcn_s_barrier();  // (as CW = 0)
+                    slot = slot + 1 == S ? 0 : slot + 1;
+                    sb = lds0 + (unsigned)slot * Geo::SLOT;
+                    load(0, c ^ 1, sb);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj)
+                        acc[4 * ii + jj] =
+                            __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[c][ii], fb[c][jj], acc[4 * ii + jj], 0, 0, 0);
+                acc[8] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[c][CH], fb[c][4], acc[8], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+    }
+    // D[k][col]: col = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5); direct dword stores (CW = 0)
+    const int TC = 9 * a.C;
+    float* base = a.part + grp * a.gs_part + (size_t)split * a.K * TC + (size_t)(k0 + 4 * (lane >> 5)) * TC + n0 +
+                  (lane & 31);
+    auto out_of = [&](int j) __attribute__((always_inline)) -> float* {
+        const int kb = j < 8 ? 2 * kh + (j >> 2) : 2 * kh + CH;
+        const int cb = j < 8 ? 5 * CH + (j & 3) : 4;
+        return base + (size_t)(32 * kb) * TC + 32 * cb;
+    };
+    if (a.accumulate) {
+#pragma unroll
+        for (int j = 0; j < 9; ++j) {
+            float* out = out_of(j);
+            float v[16];
+#pragma unroll
+            for (int e = 0; e < 16; ++e) v[e] = out[(size_t)((e & 3) + 8 * (e >> 2)) * TC];
+#pragma unroll
+            for (int e = 0; e < 16; ++e) out[(size_t)((e & 3) + 8 * (e >> 2)) * TC] = v[e] + acc[j][e];
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 9; ++j) {
+            float* out = out_of(j);
+#pragma unroll
+            for (int e = 0; e < 16; ++e) out[(size_t)((e & 3) + 8 * (e >> 2)) * TC] = acc[j][e];
+        }
+    }
+}
+
 template <int S, int BK>
+__device__ __forceinline__ void ring_compute_split(const WRingArgs& a, int w, int lane, unsigned lds0, int nst,
+                                                   int grp, int split, int k0, int n0) {
+    if (w >> 1) ring_compute_split_ch<S, BK, 1>(a, w, lane, lds0, nst, grp, split, k0, n0);
+    else ring_compute_split_ch<S, BK, 0>(a, w, lane, lds0, nst, grp, split, k0, n0);
+}
+
+// The compute waves' share of the 4 x 9 grid of 32 x 32 blocks (4 k-blocks of the 128 output channels
+// x 9 column blocks of the 288 (tap, channel) columns).  CW = 0: wave w owns k-block w x all 9 column
+// blocks - 1 A + 9 B fragments (20 transposed reads) per 9 MFMAs, every B fragment read by all four
+// waves.  CW = 1: wave w owns k-blocks {2 kh, 2 kh + 1} (kh = w & 1) x column blocks 5 ch .. 5 ch + 3
+// (ch = w >> 1) plus the single cell (2 kh + ch, 4) of the middle column block - still 9 MFMAs per
+// wave, but 2 A + 5 B fragments (14 reads): 56 instead of 80 transposed reads per k-slice and CU.
+template <int S, int BK, int CW = 0>
 __global__ __launch_bounds__(512) void k_wgrad_ring(WRingArgs a) {
     static_assert(S >= 2 && (BK == 32 || BK == 64), "k_wgrad_ring: S >= 2 slots of 32 or 64 pixels");
     using Geo = RingGeo<BK>;
@@ -834,6 +957,10 @@ __global__ __launch_bounds__(512) void k_wgrad_ring(WRingArgs a) {
 
     // ---- compute waves ----
     const int w = wave;
+    if constexpr (CW == 1) {
+        ring_compute_split<S, BK>(a, w, lane, lds0, nst, grp, split, k0, n0);
+        return;
+    }
     floatx16 acc[9];
 #pragma unroll
     for (int j = 0; j < 9; ++j)
@@ -1259,7 +1386,8 @@ static int device_cus_w() {
     return cus;
 }
 // k_wgrad_ring's form (GM_WGRAD_RING at load, gm_conv_set_wgrad_ring): 0 = 3 slots of 64 pixels,
-// 1 = 6 slots of 32 pixels (more bytes in flight, twice the barriers)
+// 1 = 6 slots of 32 pixels (more bytes in flight, twice the barriers), 3 = 3 slots of 64 pixels with
+// the split-column compute waves (CW = 1)
 static int g_ring_form = [] {
     const char* e = getenv("GM_WGRAD_RING");
     return e ? atoi(e) : 0;
@@ -1486,24 +1614,27 @@ extern "C" int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, con
         r.gs_part = direct ? dw_stride : (long long)rp.splits * (long long)slab;
         r.accumulate = direct ? accumulate : 0;
         const int grid = rp.tiles_k * rp.tiles_n * rp.splits * G;
-        auto go = [&](auto sc, auto bc) -> int {
-            constexpr int S = decltype(sc)::value, BK = decltype(bc)::value;
+        auto go = [&](auto sc, auto bc, auto cwc) -> int {
+            constexpr int S = decltype(sc)::value, BK = decltype(bc)::value, CW = decltype(cwc)::value;
             constexpr size_t lds = (size_t)S * RingGeo<BK>::SLOT;
             static bool attr = false;
             if (!attr) {
-                if (hipFuncSetAttribute((const void*)k_wgrad_ring<S, BK>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                if (hipFuncSetAttribute((const void*)k_wgrad_ring<S, BK, CW>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         (int)lds) != hipSuccess) {
                     set_error("k_wgrad_ring: %zu B of LDS refused", lds);
                     return GM_E_UNSUP;
                 }
                 attr = true;
             }
-            k_wgrad_ring<S, BK><<<grid, 512, lds, st0>>>(r);
+            k_wgrad_ring<S, BK, CW><<<grid, 512, lds, st0>>>(r);
             return check_launch("k_wgrad_ring");
         };
-        const int rc = g_ring_form == 1   ? go(std::integral_constant<int, 6>{}, std::integral_constant<int, 32>{})
-                       : g_ring_form == 2 ? go(std::integral_constant<int, 2>{}, std::integral_constant<int, 64>{})
-                                          : go(std::integral_constant<int, 3>{}, std::integral_constant<int, 64>{});
+        using I = std::integral_constant<int, 0>;
+        const int rc =
+            g_ring_form == 1   ? go(std::integral_constant<int, 6>{}, std::integral_constant<int, 32>{}, I{})
+            : g_ring_form == 3 ? go(std::integral_constant<int, 3>{}, std::integral_constant<int, 64>{},
+                                    std::integral_constant<int, 1>{})
+                               : go(std::integral_constant<int, 3>{}, std::integral_constant<int, 64>{}, I{});
         if (rc || direct) return rc;
         return split_sum(r.part, rp.splits, slab);
     }
@@ -1573,8 +1704,8 @@ extern "C" int gm_conv_set_wgrad_staging(int wr) {
 }
 
 extern "C" int gm_conv_set_wgrad_ring(int form) {
-    GM_REQUIRE(form >= 0 && form <= 2,
-               "gm_conv_set_wgrad_ring: 0 (3 slots of 64 pixels), 1 (6 slots of 32), 2 (2 slots of 64)");
+    GM_REQUIRE(form >= 0 && form <= 3,
+               "gm_conv_set_wgrad_ring: 0 (3 slots of 64 pixels), 1 (6 slots of 32), 3 (split-column waves)");
     g_ring_form = form;
     return GM_OK;
 }

@@ -37,7 +37,8 @@ import torch.distributed as dist
 from .callbacks import GroupNorms
 from .gradsink import GradSink
 from .losses import blend_loss
-from .streams import alias_capture_stream, all_side_streams, side_stream
+from .streams import alias_capture_stream, all_side_streams, capture_dropped, capture_replayed, \
+    release_rng_capture_state, side_stream
 from .streams import enabled as streams_enabled
 from .vtrunk import drop_pending_wgrads
 
@@ -46,6 +47,30 @@ _DEBUG_BUCKETS = os.environ.get("GM_DEBUG_BUCKETS", "0") == "1"
 
 # RCCL channels bound = CUs reserved for RCCL's kernels beside the spin hand-off kernels.
 RCCL_CHANNELS_DEFAULT = 64
+
+
+# hardware queues a data-parallel rank needs: the trunk stream, the weight-gradient stream, the
+# gradient-bucket (comm) stream and RCCL's own stream must not share a queue - a stream queued
+# behind a long RCCL kernel on a shared queue stalls (test_gpu_rccl_residency.py measured 393 ms
+# behind a CU-holding kernel at HIP's default of 4); 8 leaves headroom (the pool's cap is 32)
+DP_HW_QUEUES = 8
+
+
+def check_hw_queues():
+    """Warn when a data-parallel engine runs with fewer than DP_HW_QUEUES hardware queues.
+    GPU_MAX_HW_QUEUES is read once, when the HIP runtime initialises - set it before the first
+    HIP call of the rank (bench.py does, before importing torch)."""
+    try:
+        q = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+    except ValueError:
+        q = 4
+    if q < DP_HW_QUEUES:
+        import warnings
+        warnings.warn(f"data-parallel BalancedStep with GPU_MAX_HW_QUEUES={q} (< {DP_HW_QUEUES}): the trunk, "
+                      "weight-gradient, gradient-bucket and RCCL streams share hardware queues and can stall "
+                      "behind each other; export GPU_MAX_HW_QUEUES=8 before the rank's first HIP call",
+                      RuntimeWarning, stacklevel=3)
+    return q
 
 
 def bound_rccl_channels():
@@ -298,6 +323,8 @@ class BalancedStep:
         # compute is the graph and the all-reduce + norms/SGD run eagerly behind it.
         self.graph_collectives = False
         self._capture_pg = None
+        if self.buckets is not None and self.device.type == "cuda":
+            check_hw_queues()
         if self.buckets is not None and self.graphs:
             backend = dist.get_backend(process_group)
             self.graph_collectives = (backend == "nccl"
@@ -316,6 +343,7 @@ class BalancedStep:
             self._plan_residency(model)
         self._graphs = {}
         self._gpool = None
+        self.capture_failures = []  # messages of failed captures (each one fell back, see __call__)
         self._static = None
         self._slots = {}
         from .balanced_mmtm import MMTM_mitigate
@@ -583,11 +611,15 @@ class BalancedStep:
                     entry = self._capture(key, slot)
                 except RuntimeError as e:  # capture refused on this system
                     entry, err = None, e
+                    self.capture_failures.append(str(e))
+                    capture_dropped()  # (scratch grown in the failed capture was never zeroed)
+                    release_rng_capture_state(self.device)
                 if self.buckets is not None and self.world > 1 and not self._agree(entry is not None):
                     # every rank takes the same fallback, so the ranks' collective sequences
                     # stay identical (a rank replaying in-graph collectives beside one that
                     # reduces eagerly would hang or sum the wrong buffers)
                     self._graphs.pop(key, None)
+                    capture_dropped()
                     entry = None
                     err = err or RuntimeError("graph capture failed on another rank")
             if entry is None:
@@ -609,6 +641,7 @@ class BalancedStep:
             g, loss, sums, outs = entry
             want = gate is not None and hasattr(gate, "needs_bdr") and gate.needs_bdr()
             g.replay()
+            capture_replayed()
             if self.buckets is not None and not self.graph_collectives:
                 self.buckets.reduce_all()
                 sums = self.norms.sums(grad_scale=1.0 / self.world, lr=self.lr)

@@ -68,14 +68,65 @@ def zeroed_scratch(cache, device, need, size_of):
     buf = cache.get(key)
     if buf is not None and buf.numel() >= need:
         return buf
-    if torch.cuda.is_current_stream_capturing():
+    capturing = torch.cuda.is_current_stream_capturing()
+    if capturing:
         key = (idx, torch.cuda.current_stream(idx).stream_id)
         buf = cache.get(key)
         if buf is not None and buf.numel() >= need:
             return buf
     buf = torch.zeros(size_of(buf), device=device, dtype=torch.uint8)
     cache[key] = buf
+    if capturing:
+        _grown_in_capture.append((cache, key, buf))
     return buf
+
+
+# buffers grown inside a capture whose graph has not been replayed yet: their zero fill exists
+# only as a node of that graph.  If the capture fails or its graph is dropped unreplayed, a later
+# capture on the same (default capture) stream would find them big enough and record no fill -
+# its BN tickets / split-K turnstiles would start on memory nobody zeroed.
+_grown_in_capture = []
+
+
+def capture_dropped():
+    """The capture that grew scratch buffers failed, or its graph is dropped before any replay:
+    evict those buffers, so the next capture grows (and zero-fills) its own."""
+    for cache, key, buf in _grown_in_capture:
+        if cache.get(key) is buf:
+            del cache[key]
+    _grown_in_capture.clear()
+
+
+def capture_replayed():
+    """A graph holding the recorded fills has run: the grown buffers are zeroed (every kernel
+    using them leaves its tickets re-zeroed), so later captures may reuse them without a fill."""
+    _grown_in_capture.clear()
+
+
+def release_rng_capture_state(device):
+    """After a failed capture, end the default generator's capture state.
+
+    torch.cuda.CUDAGraph.capture_begin puts the default CUDA generator into its capture state
+    (capture_prologue) BEFORE it asks the allocator for the private pool and begins the stream
+    capture, and only capture_end's epilogue takes it out again - after hipStreamEndCapture
+    succeeded.  A capture refused in capture_begin (e.g. a released private pool) or invalidated
+    in its body therefore leaves the generator believing it is captured, and the next eager
+    random op anywhere in the process raises "Offset increment outside graph capture
+    encountered unexpectedly" (the round-5 test_xent_bad_label_is_nan failure).  One complete
+    capture of a trivial kernel on a private stream runs prologue + epilogue and restores it;
+    the graph is never replayed, so the generator's offset does not move."""
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream(device=device)
+    t = torch.zeros(1, device=device)
+    s.wait_stream(torch.cuda.current_stream(device))
+    with torch.cuda.stream(s):
+        g.capture_begin()
+        try:
+            t.add_(1)
+        finally:
+            g.capture_end()
+    torch.cuda.current_stream(device).wait_stream(s)
+    del g
 
 
 def all_side_streams(device):

@@ -116,6 +116,8 @@ def test_relu_mask_bits_backward_bit_identical(shape, epi):
     g = torch.Generator().manual_seed(C + H + int(epi))
     x = torch.randn(G * N, C, H, W, generator=g).bfloat16().to(dev).contiguous(memory_format=CL)
     res = torch.randn(G * N, C, H, W, generator=g).bfloat16().to(dev).contiguous(memory_format=CL)
+    res[0, 5, 1, 1] = float("inf")    # y = +inf (bf16 0x7f80): the mask's largest set value
+    res[1, 6, 0, 1] = float("-inf")   # y = 0 after the ReLU
     gy = torch.randn(G * N, C, H, W, generator=g).bfloat16().to(dev).contiguous(memory_format=CL)
     convs = []
     for _ in range(G):

@@ -517,7 +517,7 @@ def test_wgrad_halo64_vs_fp32(dev, shape):
                                    (5, 128, 9, 11, 128, 2, 2), (2, 32, 7, 5, 128, 1, 2), (1, 512, 7, 7, 512, 1, 2),
                                    (4, 128, 28, 28, 128, 1, 2), (3, 256, 14, 14, 256, 1, 12)],
                          ids=lambda s: "x".join(map(str, s)))
-@pytest.mark.parametrize("form", [0, 1], ids=["bk64", "bk32"])
+@pytest.mark.parametrize("form", [0, 1, 3], ids=["bk64", "bk32", "split"])
 def test_wgrad_ring_vs_fp32(dev, shape, form):
     """k_wgrad_ring (3x3 weight gradient, 128 x 288 tiles, loader waves feeding a 3-slot LDS ring,
     splits over the pixel steps sized to one workgroup per CU, slabs summed in a fixed order; one

@@ -168,3 +168,110 @@ def test_larger_second_batch_under_capture():
     se, sg = m_e.state_dict(), m_g.state_dict()
     for k in se:
         torch.testing.assert_close(sg[k], se[k], rtol=1e-6, atol=1e-6, msg=k)
+
+
+def test_failed_capture_then_recapture():
+    """a capture that grows the BN ticket / split-K turnstile scratch and then fails
+    must not leave those buffers (whose zero fill exists only in the dropped graph) for the next
+    capture on the same stream; and the failure must not leave the default CUDA generator in its
+    capture state.  A failure is injected at the end of the first capture's
+    body; the engine falls back to eager steps; graphs are then re-enabled and the step is
+    captured again.  Losses and parameters equal an all-eager run."""
+    from greedy_multimodal_learning_amd import streams
+    from greedy_multimodal_learning_amd.callbacks import Bias_Mitigation_Strong
+    from greedy_multimodal_learning_amd.engine import BalancedStep
+    from greedy_multimodal_learning_amd.model import MMTM_MVCNN
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(11)
+    sizes = [2, 24, 24, 24]  # 24: larger than any batch an earlier test ran, so scratch grows
+    xs = [torch.randn(b, 2, 3, 64, 64, device=dev, generator=g) for b in sizes]
+    ys = [torch.randint(0, 40, (b,), device=dev, generator=g) for b in sizes]
+
+    def build(graphs):
+        torch.manual_seed(0)
+        m = MMTM_MVCNN().to(dev)
+        gate = Bias_Mitigation_Strong(epsilon=2e-3, curation_windowsize=2,
+                                      branchnames=["net_view_0", "net_view_1"], starting_epoch=1)
+        st = BalancedStep(m, lr=0.05, gate=gate, graphs=graphs, device_gate=True)
+        st.on_epoch_begin(1)
+        return m, st
+
+    m_e, st_e = build(False)
+    l_e = [float(st_e(x, y)) for x, y in zip(xs, ys)]
+
+    from greedy_multimodal_learning_amd import bn, conv, vtrunk
+    caches = (vtrunk._bn_scratch, conv._splitk_ws, bn._scratch)
+
+    def shrink():  # every cached scratch buffer too small for the next call: a capture must grow it
+        torch.cuda.synchronize()
+        for cache in caches:
+            for k in list(cache):
+                cache[k] = torch.zeros(16, dtype=torch.uint8, device=dev)
+
+    m_g, st_g = build(True)
+    l_g = [float(st_g(xs[0], ys[0]))]  # eager first step (B = 2)
+    shrink()
+    orig = st_g._fwd_bwd
+    injected = []
+
+    def failing(*a):
+        out = orig(*a)
+        if torch.cuda.is_current_stream_capturing() and not injected:
+            injected.append(len(streams._grown_in_capture))
+            raise RuntimeError("injected capture failure")
+        return out
+
+    st_g._fwd_bwd = failing
+    l_g.append(float(st_g(xs[1], ys[1])))  # capture at B = 24 fails -> eager fallback
+    assert injected and injected[0] > 0, "no scratch grew inside the failed capture"
+    assert st_g.capture_failures and not st_g.graphs
+    assert streams._grown_in_capture == []
+    cap_key = (0, torch.cuda.graph.default_capture_stream.stream_id)
+    assert all(cap_key not in c for c in caches), "scratch grown in the failed capture was kept"
+    torch.randn(1, device=dev)  # the default generator is usable outside a capture
+    st_g._fwd_bwd = orig
+    shrink()  # the retry's capture grows again: under the capture key, with its own recorded fill
+    st_g.graphs = True  # the retry: capture again on the same capture stream
+    l_g += [float(st_g(x, y)) for x, y in zip(xs[2:], ys[2:])]
+    assert st_g.graphs and len(st_g._graphs) == 1
+    torch.cuda.synchronize()
+    assert l_g == pytest.approx(l_e, rel=1e-6, abs=1e-6)
+    se, sg = m_e.state_dict(), m_g.state_dict()
+    for k in se:
+        torch.testing.assert_close(sg[k], se[k], rtol=1e-6, atol=1e-6, msg=k)
+
+
+def test_released_pool_capture_leaves_generator_usable():
+    """The round-5 cause, reproduced: a capture into a private pool whose graphs were all
+    destroyed is refused inside capture_begin, after torch put the default generator into its
+    capture state.  streams.release_rng_capture_state (which the engine runs after every failed
+    capture) takes it out again; the default generator then works eagerly."""
+    from greedy_multimodal_learning_amd.streams import release_rng_capture_state
+    dev = torch.device("cuda:0")
+    s = torch.cuda.Stream(device=dev)
+    pool = torch.cuda.graph_pool_handle()
+    t = torch.zeros(4, device=dev)
+    g1 = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g1, pool=pool, stream=s):
+        t.add_(1)
+    g1.replay()
+    torch.cuda.synchronize()
+    del g1  # releases the pool
+    refused, stuck = None, None
+    g2 = torch.cuda.CUDAGraph()
+    try:
+        with torch.cuda.graph(g2, pool=pool, stream=s):
+            t.add_(1)
+    except RuntimeError as e:
+        refused = str(e).splitlines()[0][:160]
+    del g2
+    torch.cuda.synchronize()
+    state = torch.cuda.get_rng_state()
+    try:
+        torch.empty(1, device=dev).uniform_()
+    except RuntimeError as e:
+        stuck = str(e).splitlines()[0][:160]
+    print(f"released-pool capture refused: {refused!r}; eager RNG afterwards: {stuck!r}")
+    release_rng_capture_state(dev)
+    torch.empty(1, device=dev).uniform_()
+    torch.cuda.set_rng_state(state)
