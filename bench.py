@@ -279,12 +279,6 @@ def main():
         return buf.permute(1, 0, 4, 2, 3)
     xs = [batch() for _ in range(2)]
     ys = [torch.randint(0, 40, (B,), device=dev, generator=g) for _ in range(2)]
-    # GM_BENCH_BIND=1: the two resident batches become the engine's double-buffered
-    # graph inputs (no input copy per step).  Measured slower than one graph plus the
-    # 38 MB copy (5.32-5.38 vs 5.29-5.30 ms/step): alternating two graphs costs more.
-    if os.environ.get("GM_BENCH_BIND", "0") != "0":
-        step.bind_batches(*zip(xs, ys))
-
     for i in range(a.warmup):
         step(xs[i % 2], ys[i % 2])
     torch.cuda.synchronize()

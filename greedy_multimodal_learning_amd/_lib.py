@@ -298,7 +298,6 @@ EXPORTS.update({
     "gm_bn_set_fused_mode": (c_int, [c_int]),
     "gm_set_residency": (c_int, [c_int, c_int, c_int]),
     "gm_get_residency": (c_int, [ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
-    "gm_test_hold_cus": (c_int, [c_int, c_int, c_int, ctypes.c_uint, c_void_p]),
 })
 
 
@@ -363,7 +362,6 @@ EXPORTS.update({
     "gm_conv_set_wgrad_staging": (c_int, [c_int]),
     "gm_conv_set_splitk": (c_int, [c_int]),
     "gm_conv_set_wgrad_loop": (c_int, [c_int]),
-    "gm_conv_set_wgrad_ring": (c_int, [c_int]),
     "gm_conv_set_1x1_gemm": (c_int, [c_int]),
     "gm_conv_set_rw": (c_int, [c_int]),
     "gm_conv_set_stem": (c_int, [c_int]),

@@ -17,7 +17,6 @@ PyTorch batch_norm path: CPU tensors raise.  Reference: torchvision ResNet
 BasicBlock/Bottleneck as used by src/model.py:53-56,65-106.
 """
 import ctypes
-import os
 
 import torch
 import torch.nn as nn
@@ -33,12 +32,12 @@ _scratch = {}
 # ReLU BNs without a residual keep the forward's fp32 affine coefficients (2C floats)
 # instead of y: the backward recomputes the mask x*sc + sh > 0 from x, which it reads
 # anyway, so y is never read back (one bf16 activation read fewer in each of the two
-# backward kernels).  GM_BN_MASKX=0 keeps the y mask.
-MASK_FROM_X = os.environ.get("GM_BN_MASKX", "1") != "0"
+# backward kernels).  (False keeps the y mask.)
+MASK_FROM_X = True
 
 # The stem's BN + ReLU + max-pool in one statistics launch and one pool launch
-# (GMBatchNorm2d.relu_maxpool); GM_BN_FUSE_POOL=0 composes the two modules.
-FUSE_POOL = os.environ.get("GM_BN_FUSE_POOL", "1") != "0"
+# (GMBatchNorm2d.relu_maxpool); False composes the two modules.
+FUSE_POOL = True
 
 
 def _get_scratch(device, M, C):

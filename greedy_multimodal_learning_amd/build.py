@@ -39,6 +39,7 @@ def needs_build():
 
 def build(force=False, verbose=False):
     if not force and not needs_build():
+        build_testkit()
         return LIB
     objs = []
     bdir = os.path.join(PKG, "csrc", "build")
@@ -64,7 +65,28 @@ def build(force=False, verbose=False):
     if r.returncode != 0:
         raise RuntimeError("link failed:\n" + r.stdout.decode(errors="replace"))
     os.replace(tmp, LIB)
+    build_testkit(force=True, verbose=verbose)
     return LIB
+
+
+TESTKIT_SRC = os.path.join(ROOT, "tests", "native", "testkit.hip")
+TESTKIT = os.path.join(ROOT, "tests", "native", "libgm_testkit.so")
+
+
+def build_testkit(force=False, verbose=False):
+    """The test-only kernel library (CU-holding kernel of the residency tests), kept out of the
+    product ABI: tests/native/libgm_testkit.so."""
+    if not os.path.exists(TESTKIT_SRC):
+        return None
+    if not force and os.path.exists(TESTKIT) and os.path.getmtime(TESTKIT) >= os.path.getmtime(TESTKIT_SRC):
+        return TESTKIT
+    cmd = [hipcc(), "-O3", "-std=c++17", "-fPIC", "-shared", f"--offload-arch={ARCH}", TESTKIT_SRC, "-o", TESTKIT]
+    if verbose:
+        print(" ".join(cmd))
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    if r.returncode != 0:
+        raise RuntimeError("testkit build failed:\n" + r.stdout.decode(errors="replace"))
+    return TESTKIT
 
 
 if __name__ == "__main__":

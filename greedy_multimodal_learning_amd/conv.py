@@ -16,7 +16,6 @@ place through the gradient sink).  There is no vendor-library path: a CPU tensor
 or an unsupported configuration raises.
 """
 import ctypes
-import os
 
 import torch
 import torch.nn as nn
@@ -484,7 +483,7 @@ class GMConv2d(nn.Conv2d):
     """nn.Conv2d whose bf16 path runs on libgreedymml_hip.so (groups=1, no bias,
     square stride/padding, dilation 1 - the ResNet trunk's convolutions)."""
 
-    pair_stem = os.environ.get("GM_STEM_PAIR", "1") != "0"
+    pair_stem = True
 
     def _hip_ok(self):
         return (self.groups == 1 and self.bias is None and self.dilation == (1, 1)

@@ -37,15 +37,6 @@ int usable_cus(int cus) {
     return u > cus / 4 ? u : cus / 4;
 }
 
-// one workgroup per CU when lds_bytes is the whole LDS: spins on the 100 MHz real-time
-// counter, sleeping between polls, until `usec` have passed
-__global__ void k_hold_cus(unsigned long long ticks) {
-    extern __shared__ int lds[];
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
-    if (threadIdx.x == 0) lds[0] = 0;
-}
-
 }  // namespace gm
 
 extern "C" int gm_abi_version(void) { return GM_ABI_VERSION; }
@@ -82,16 +73,4 @@ extern "C" int gm_get_residency(int* streams, int* sharers, int* reserved_cus) {
     *sharers = gm::g_res.sharers;
     *reserved_cus = gm::g_res.reserved_cus;
     return GM_OK;
-}
-
-extern "C" int gm_test_hold_cus(int blocks, int threads, int lds_bytes, unsigned usec, void* stream) {
-    GM_REQUIRE(blocks >= 1 && blocks <= 4096 && threads >= 64 && threads <= 1024 && lds_bytes >= 4 &&
-                   lds_bytes <= 160 * 1024 && usec <= 10000000u,
-               "gm_test_hold_cus: bad arguments");
-    if (lds_bytes > 64 * 1024)
-        hipFuncSetAttribute(reinterpret_cast<const void*>(gm::k_hold_cus), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            lds_bytes);
-    hipLaunchKernelGGL(gm::k_hold_cus, dim3(blocks), dim3(threads), lds_bytes, gm::as_stream(stream),
-                       (unsigned long long)usec * 100ull);
-    return gm::check_launch("gm_test_hold_cus");
 }

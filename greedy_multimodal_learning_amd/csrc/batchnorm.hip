@@ -55,8 +55,7 @@ inline int ilog2(int v) {
 
 inline int bn_blocks() {
     static int b = [] {
-        const char* e = getenv("GM_BN_BLOCKS");
-        return e ? atoi(e) : 512;
+        return 512;
     }();
     return b;
 }
@@ -1583,19 +1582,17 @@ constexpr int kGenOff = 32;  // generation words: header words [32, 32 + nslice)
 // the occupancy MEASURED for the kernel instantiations that can be launched
 // (hipOccupancyMaxActiveBlocksPerMultiprocessor, the minimum over their variants) and
 // the concurrency set by the caller (gm_bn_set_concurrency: the number of trunk streams
-// that run concurrently plus headroom; default 4, GM_BN_FUSE_STREAMS at load).  A grid
+// that run concurrently plus headroom; default 4).  A grid
 // that could exceed the resident capacity would let spinning blocks wait on blocks that
 // cannot be scheduled (the spin is bounded and then faults loudly, see wait_generation).
 // Returns NR (pl rewritten), -1 for the streaming variant (x re-read by the apply phase;
-// GM_BN_FUSED=1 disables it) or 0: use the two-kernel path.  GM_BN_FUSED=0 disables it.
+// gm_bn_set_fused_mode(1) disables it) or 0: use the two-kernel path (gm_bn_set_fused_mode(0)).
 int g_concurrency = [] {
-    const char* e = getenv("GM_BN_FUSE_STREAMS");
-    const int v = e ? atoi(e) : 4;
+    const int v = 4;
     return v >= 1 ? v : 4;  // 0 / garbage: the default (never a division by zero)
 }();
 int g_fused_env = [] {
-    const char* e = getenv("GM_BN_FUSED");  // read once; 0 = two-kernel path, 1 = no streaming variant
-    return e ? atoi(e) : 2;
+    return 2;  // read once; 0 = two-kernel path, 1 = no streaming variant
 }();
 
 template <typename K>
@@ -1644,10 +1641,9 @@ int device_cus() {
 }
 
 // the redundant-finalize hand-off (every block combines the partial rows): small maps only,
-// where a block's extra partial-row reads are a few KB (GM_BN_REDUNDANT=0: the publish form)
+// where a block's extra partial-row reads are a few KB
 static int g_bn_redundant_max = [] {
-    const char* e = getenv("GM_BN_REDUNDANT");
-    return e ? atoi(e) : 16;  // measured: 8 / 16 help layer 4 (~1-1.3 us a launch), 32+ slow layer 3
+    return 16;  // measured: 8 / 16 help layer 4 (~1-1.3 us a launch), 32+ slow layer 3
 }();
 inline int redundant_ok(int nrc) { return nrc <= g_bn_redundant_max ? 1 : 0; }
 

@@ -354,11 +354,10 @@ static int g_ring_cus = [] {
     return n;
 }();
 
-// GM_CONV1X1 at load / gm_conv_set_1x1_gemm: 1 (default) = 1x1 / s1 shapes take k_gemm_ring,
+// gm_conv_set_1x1_gemm: 1 (default) = 1x1 / s1 shapes take k_gemm_ring,
 // 0 = the im2col kernel
 int g_conv_1x1 = [] {
-    const char* e = getenv("GM_CONV1X1");
-    return e ? atoi(e) : 1;
+    return 1;
 }();
 
 bool conv1x1_ok(int R, int S, int sh, int sw, int ph, int pw, long long M, int Kr, int N) {

@@ -153,15 +153,6 @@ __device__ __forceinline__ int block_id(int xcd) {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
 }
 
-// The same bijection over [0, n) for a block ordinal l inside a range of n blocks that starts at
-// any fixed offset: the blocks whose l agree mod 8 sit on one XCD ((start + l) % 8), and they get one
-// contiguous tile range.  Applied per split of a split-K launch (blocks [s T, (s + 1) T)), it keeps the
-// split-major dispatch order the turnstile relies on: tile t is block l in every split.
-__device__ __forceinline__ int xcd_range(int l, int n) {
-    const int q = n >> 3, r = n & 7, x = l & 7;
-    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (l >> 3);
-}
-
 __device__ __attribute__((aligned(16))) const uint4 g_zero16[1] = {{0u, 0u, 0u, 0u}};
 
 // bits i in [0, n) with 0 <= x + d0 + s*i < lim (s = +-1): one contiguous range
@@ -659,17 +650,12 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint4 smem[];
     char* lds = reinterpret_cast<char*>(smem);   // [A0..A(NST-1)][B0..B(NST-1)]
 
-    // xcd 1: each XCD a contiguous tile range, tm fastest (one weight slice per XCD; unsplit only);
-    // xcd 2: each XCD a contiguous tile range of every split, tn fastest - the column tiles of one
-    // pixel range (one im2col A block, re-read by every column tile) share an L2, and a group's
-    // tiles stay on its own XCDs
-    int bid = a.xcd == 1 ? block_id(1) : (int)blockIdx.x;
+    int bid = block_id(a.xcd);
     int split = 0;
     if (a.splits > 1) {
         split = bid / a.tiles_total;
         bid -= split * a.tiles_total;
     }
-    if (a.xcd == 2) bid = xcd_range(bid, a.splits > 1 ? a.tiles_total : (int)gridDim.x);
     const int tid = bid;  // launch-wide tile index: split-K slab and turnstile word
     int g = 0;            // view group
     if (a.G > 1) {
@@ -689,8 +675,8 @@ __global__ __launch_bounds__(256) void k_conv_igemm_ut(ConvArgs a) {
     // with a power-of-two column count the round-robin XCD dealing (block b on XCD b % 8)
     // keeps each weight slice on the same XCD(s) - L2-resident instead of re-fetched
     const int tiles_n = (a.Nout + BN - 1) / BN;
-    const int tm = a.xcd == 1 ? wgid % cl.tiles_m : wgid / tiles_n;
-    const int tn = a.xcd == 1 ? wgid / cl.tiles_m : wgid - tm * tiles_n;
+    const int tm = a.xcd ? wgid % cl.tiles_m : wgid / tiles_n;
+    const int tn = a.xcd ? wgid / cl.tiles_m : wgid - tm * tiles_n;
     const int m0 = tm * BM, n0 = tn * BN;
     const int PQ = cl.P * cl.Q;
     const int M = a.N * PQ;
@@ -2131,8 +2117,7 @@ using namespace gm;
 
 static bool lean_path() {
     static bool on = [] {
-        const char* e = getenv("GM_CONV_LEAN");
-        return !(e && e[0] == '0');
+        return true;
     }();
     return on;
 }
@@ -2140,11 +2125,10 @@ static bool lean_path() {
 static bool grid_ok(const ConvCls& c, int S);
 static void pack_grid(ConvCls& c, int S);
 
-// main-loop form of the lean kernel (k_conv_igemm_ut PIPE); GM_CONV_PIPE at load,
+// main-loop form of the lean kernel (k_conv_igemm_ut PIPE);
 // gm_conv_set_pipe() at run time (A/B in one process)
 static int g_conv_pipe = [] {
-    const char* e = getenv("GM_CONV_PIPE");
-    return e ? atoi(e) : 0;
+    return 0;
 }();
 static int conv_pipe() { return g_conv_pipe; }
 
@@ -2208,38 +2192,31 @@ static int launch_igemm(ConvArgs& a, hipStream_t st) {
 
 static int stages() {
     static int s = [] {
-        const char* e = getenv("GM_CONV_STAGES");
-        return (e && e[0] == '3') ? 3 : 2;
+        return 2;  // (3 stages: one workgroup per CU, slower)
     }();
     return s;
 }
 
-// GM_CONV_XCD (k_conv_igemm_ut's tile order over the XCDs): 0 = dispatch order, 1 = tm fastest per
-// XCD (measured no gain, r01), 2 = tn fastest per XCD, split-K included
-static int g_xcd_mode = [] {
-    const char* e = getenv("GM_CONV_XCD");
-    return e ? atoi(e) : 0;
-}();
-static int xcd_remap() { return g_xcd_mode; }
+// XCD remap of the tile order (ConvArgs::xcd: each XCD a contiguous tile range, tm fastest, so one
+// weight slice stays in one L2): measured no gain (r01; r06: a split-aware tn-fastest remap, whose
+// XCDs share each pixel range's im2col rows, 3.62 vs 3.59 ms/step) - off
+static int xcd_remap() { return 0; }
 
 static int tile_bias() {
     static int b = [] {
-        const char* e = getenv("GM_CONV_TILE_WGS");
-        return e ? atoi(e) : 1024;
+        return 1024;
     }();
     return b;
 }
 
 static int g_splitk_target = [] {
-    const char* e = getenv("GM_CONV_SPLITK");  // workgroups wanted from split-K; 0 disables it
-    return e ? atoi(e) : 384;
+    return 384;  // workgroups wanted from split-K; 0 disables it
 }();
 static int splitk_target() { return g_splitk_target; }
 
 static int splitk_mink() {
     static int t = [] {
-        const char* e = getenv("GM_CONV_SPLITK_MINK");  // minimum k-tiles per split
-        return e ? atoi(e) : 16;
+        return 16;  // minimum k-tiles per split
     }();
     return t;
 }
@@ -2316,8 +2293,7 @@ static size_t splitk_bytes(const TilePick& p) {
 }
 
 static int g_conv_halo = [] {
-    const char* e = getenv("GM_CONV_HALO");
-    return e ? atoi(e) : 1;
+    return 1;
 }();
 
 // the halo kernel serves one-class, 3x3 tap grids with offsets in [-1, 1] at stride 1
@@ -2373,8 +2349,7 @@ static int launch_halo_v(ConvArgs& a, int hb, hipStream_t st) {
 }
 
 static int g_conv_stem = [] {
-    const char* e = getenv("GM_CONV_STEM");  // 0: the pixel-pair stem takes the im2col kernel
-    return e ? atoi(e) : 1;
+    return 1;  // 0: the pixel-pair stem takes the im2col kernel
 }();
 
 // k_conv_stem serves the pixel-pair stem: one-class forward convolutions over 8-channel
@@ -2427,8 +2402,7 @@ static int launch_stem(const ConvArgs& a, const StemArgs& r, size_t lds, hipStre
 }
 
 static int g_conv_rw = [] {
-    const char* e = getenv("GM_CONV_RW");  // 0: layer-1 shapes take the im2col kernel
-    return e ? atoi(e) : 1;
+    return 1;  // 0: layer-1 shapes take the im2col kernel
 }();
 
 // the resident-weight kernel serves one-class 3x3 / stride-1 / same-size convolutions with
@@ -2479,8 +2453,7 @@ static int launch_rw(const ConvArgs& a, const RwArgs& r, size_t lds, hipStream_t
 }
 
 static int g_conv_h9 = [] {
-    const char* e = getenv("GM_CONV_H9");  // 0: the halo shapes take k_conv_halo (A/B)
-    return e ? atoi(e) : 1;
+    return 1;  // 0: the halo shapes take k_conv_halo (A/B)
 }();
 // k_conv_h9 when eligible: Nout a multiple of BN, at most 48 halo DMA instructions, the
 // halo + 3 weight stages within half the CU's LDS (two workgroups per CU), splits over
@@ -2570,14 +2543,10 @@ struct Halo256Plan {
     size_t ws = 0;     // split-K workspace bytes (turnstile words + 256x128 fp32 slabs)
 };
 
-static int halo256_env(const char* name, int dflt) {
-    const char* e = getenv(name);
-    return e ? atoi(e) : dflt;
-}
-// GM_HALO256_MINTILES: shapes with fewer 256x128 tiles keep the 128-pixel form;
-// GM_HALO256_SPLIT=0: never split K
-static const int g_h256_mintiles = halo256_env("GM_HALO256_MINTILES", 192);
-static const int g_h256_split = halo256_env("GM_HALO256_SPLIT", 1);
+// the 256-pixel form (gm_conv_set_halo(2)): shapes with fewer 256x128 tiles keep the 128-pixel form;
+// K is split when the tiles do not fill the chip
+static const int g_h256_mintiles = 192;
+static const int g_h256_split = 1;
 
 static Halo256Plan halo256_plan(const ConvArgs& a) {
     Halo256Plan p;
@@ -2646,8 +2615,7 @@ static int pick_and_launch(ConvArgs& a, hipStream_t st, void* ws, size_t ws_byte
         p = {M / 128 * ((a.Nout + 63) / 64) >= tile_bias() * 3 / 4 ? T128x64 : T64x64, 1, 0};
     }
     a.splits = p.splits;
-    // (mode 1 only unsplit: split-K relies on split-major dispatch order, which mode 2 keeps)
-    a.xcd = xcd_remap() == 2 ? 2 : (p.splits > 1 ? 0 : (xcd_remap() == 1));
+    a.xcd = p.splits > 1 ? 0 : xcd_remap();  // split-K relies on split-major dispatch order
     if (p.splits > 1) {
         a.spin_limit = spin_limit();
         a.flags = static_cast<unsigned*>(ws);

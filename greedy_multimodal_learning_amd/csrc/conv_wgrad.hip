@@ -659,20 +659,25 @@ __global__ __launch_bounds__(512) void k_wgrad_halo64(WHaloArgs a) {
 // landed is ~1 us under load, MI355X_MICROARCH.md ldsdma rows) against 16 MFMAs per wave
 // (~0.25 us), so its two workgroups per CU took in ~35 GB/s; and every DMA issue sat in the
 // compute waves' MFMA stream.  Here, per CU ONE workgroup of 512 threads:
-//   * four LOADER waves own all LDS-DMA: an S-slot ring of 64-pixel steps, S - 1 steps in flight
-//     (104 KB at S = 3), one raw s_barrier per step after a counted vmcnt (the step about to be
-//     read has landed; the younger one stays in flight across the barrier);
-//   * four COMPUTE waves never touch VMEM in the loop: wave w owns output channels 32w .. 32w+31
-//     of the tile and all 9 column fragments (9 accumulators), ds_read_b64_tr_b16 fragments one
-//     k-slice ahead, 36 MFMAs per step between barriers (k_conv_wgrad4: 16);
-//   * tile 128 output channels x 288 (tap, channel) columns = 9 x 32 - every 3x3 shape with C % 32
-//     == 0 splits into whole tiles, and the trunk's layer-2..4 shapes give tiles x splits = 256
-//     workgroups exactly (one per CU, no tail); 88.6 FLOP per staged byte (128 x 128: 64).
+//   * four LOADER waves own all LDS-DMA: a 3-slot ring of 64-pixel steps, 2 steps in flight
+//     (156 KB), one raw s_barrier per step after a counted vmcnt (the step about to be read has
+//     landed; the younger one stays in flight across the barrier);
+//   * four COMPUTE waves never touch VMEM in the loop.  The workgroup tile is 128 output channels
+//     x 288 (tap, channel) columns = a 4 x 9 grid of 32 x 32 blocks (k-block kb, column block cb);
+//     compute wave w = kh + 2 ch owns k-blocks {2 kh, 2 kh + 1} x column blocks 5 ch .. 5 ch + 3
+//     plus the single cell (2 kh + ch, 4) of the middle column: 9 accumulators and 9 MFMAs per
+//     16-pixel k-slice, fed by 2 A + 5 B fragments (14 ds_read_b64_tr_b16) read one k-slice
+//     ahead.  (r05's layout - wave w owning k-block w x all 9 column blocks - read 1 A + 9 B
+//     fragments per wave, every B fragment by all four waves: 80 instead of 56 transposed reads
+//     per k-slice and CU, 2.22 instead of 1.56 LDS instructions per MFMA (PMC), 2.5 % slower.)
+//   * every 3x3 shape with C % 32 == 0 splits into whole tiles; 88.6 FLOP per staged byte.
 // LDS slot: B (x gathered per tap) as 9 blocks of [64 px][32 columns] (64-B rows: the tr reads of a
 // half-wave cover 4 rows x 64 B = all 64 banks, no swizzle), then A (dy) as 2 blocks of
 // [64 px][64 k] (128-B rows, chunk XOR 4 ((row >> 1) & 1): k_conv_wgrad4's image).  Splits over the
 // pixel steps write fp32 partial slabs that k_wgrad_sum reduces in a fixed order (deterministic);
 // one split writes (or accumulates into) the gradient directly.
+// What bounds it now (r06 A/B): the LDS-DMA feed - 52 KB staged per 64-pixel step, ~38 GB/s per CU
+// at half the CUs - not the LDS reads (30 % fewer of them bought 2.5 %).
 struct WRingArgs {
     const uint16_t* dy;  // [G][M][K]  (M = N*P*Q)
     const uint16_t* x;   // [G][N][H][W][C]
@@ -685,12 +690,13 @@ struct WRingArgs {
     int accumulate;
 };
 
-// slot of BK pixels: B = 9 blocks of BK x 64 B, then A = 2 blocks of BK x 128 B
-template <int BK> struct RingGeo {
-    static constexpr int BB = BK * 64, AB = BK * 128;  // bytes per B / A block
-    static constexpr int B = 9 * BB, A = 2 * AB, SLOT = B + A;
-    static constexpr int SLICES = BK / 16;             // 16-pixel k-slices per step
-};
+namespace ring {
+constexpr int S = 3, BK = 64;                      // ring slots, pixels per step
+constexpr int BB = BK * 64, AB = BK * 128;         // bytes per B / A block
+constexpr int B = 9 * BB, A = 2 * AB, SLOT = B + A;
+constexpr int SLICES = BK / 16;                    // 16-pixel k-slices per step
+constexpr size_t LDS = (size_t)S * SLOT;
+}  // namespace ring
 
 // one 32 x 16 fragment by two transposed reads at base + LO / + HI
 template <int LO, int HI>
@@ -698,32 +704,22 @@ __device__ __forceinline__ bf16x8 ring_frag(unsigned base) {
     const short4_t lo = tr_rd<LO>(base), hi = tr_rd<HI>(base);
     return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 }
-// slice KS of the 9 B blocks (immediate offsets on one base register)
-template <int BK, int KS, int... J>
-__device__ __forceinline__ void ring_load_b(bf16x8 (&fb)[9], unsigned ba, std::integer_sequence<int, J...>) {
-    ((fb[J] = ring_frag<J * RingGeo<BK>::BB + KS * 1024, J * RingGeo<BK>::BB + KS * 1024 + 256>(ba)), ...);
-}
-template <int BK, int KS>
-__device__ __forceinline__ void ring_load(bf16x8& fa, bf16x8 (&fb)[9], unsigned aa, unsigned ba) {
-    fa = ring_frag<KS * 2048, KS * 2048 + 512>(aa);
-    ring_load_b<BK, KS>(fb, ba, std::make_integer_sequence<int, 9>{});
-}
 
-// k_wgrad_ring's compute waves in the CW = 1 form (see the kernel): wave w = kh + 2 ch.
-template <int S, int BK, int CH>
-__device__ __forceinline__ void ring_compute_split_ch(const WRingArgs& a, int w, int lane, unsigned lds0, int nst,
-                                                      int grp, int split, int k0, int n0) {
-    using Geo = RingGeo<BK>;
+// the compute waves (see above): wave w = kh + 2 CH
+template <int CH>
+__device__ __forceinline__ void ring_compute(const WRingArgs& a, int w, int lane, unsigned lds0, int nst, int grp,
+                                             int split, int k0, int n0) {
+    using namespace ring;
     const int kh = w & 1;
     floatx16 acc[9];  // [4 i + jj]: k-block 2 kh + i x column block 5 CH + jj; [8]: (2 kh + CH, 4)
 #pragma unroll
     for (int j = 0; j < 9; ++j)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
-    // tr-read geometry as CW = 0: half-wave g >> 1 reads rows 8 (g >> 1) + q4 (+4) of a 16-row k-slice,
-    // 4-column block p4 of the 32-column fragment, 16-column half g & 1.  The A image's chunk swizzle
-    // (XOR 4 on odd row pairs) flips the 64-column half's bit, so the two A fragments of a lane sit
-    // at +-64 B of each other by row: two base registers.
+    // tr-read geometry (k_conv_wgrad4's): half-wave g >> 1 reads rows 8 (g >> 1) + q4 (+4) of a
+    // 16-row k-slice, 4-column block p4 of the 32-column fragment, 16-column half g & 1.  The A
+    // image's chunk swizzle (XOR 4 on odd row pairs) flips the 64-column half's bit, so the two A
+    // fragments of a lane sit at +-64 B of each other by row: two base registers.
     const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
     const int rbase = 8 * (g >> 1) + q4;
     const int cin = 16 * (g & 1) + 4 * p4;
@@ -731,28 +727,30 @@ __device__ __forceinline__ void ring_compute_split_ch(const WRingArgs& a, int w,
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int ac = 32 * i + cin;
-        a_l[i] = Geo::B + kh * Geo::AB + rbase * 128 + ((((ac >> 3) ^ wswz<128>(rbase))) << 4) + (ac & 7) * 2;
+        a_l[i] = B + kh * AB + rbase * 128 + ((((ac >> 3) ^ wswz<128>(rbase))) << 4) + (ac & 7) * 2;
     }
-    const unsigned b_l = rbase * 64 + cin * 2 + 5 * CH * Geo::BB, b_4 = rbase * 64 + cin * 2 + 4 * Geo::BB;
+    const unsigned b_l = rbase * 64 + cin * 2 + 5 * CH * BB, b_4 = rbase * 64 + cin * 2 + 4 * BB;
     bf16x8 fa[2][2], fb[2][5];
     auto load_ks = [&](auto ksc, int c, unsigned sb) __attribute__((always_inline)) {
         constexpr int KS = decltype(ksc)::value;
         fa[c][0] = ring_frag<KS * 2048, KS * 2048 + 512>(sb + a_l[0]);
         fa[c][1] = ring_frag<KS * 2048, KS * 2048 + 512>(sb + a_l[1]);
-        fb[c][0] = ring_frag<0 * Geo::BB + KS * 1024, 0 * Geo::BB + KS * 1024 + 256>(sb + b_l);
-        fb[c][1] = ring_frag<1 * Geo::BB + KS * 1024, 1 * Geo::BB + KS * 1024 + 256>(sb + b_l);
-        fb[c][2] = ring_frag<2 * Geo::BB + KS * 1024, 2 * Geo::BB + KS * 1024 + 256>(sb + b_l);
-        fb[c][3] = ring_frag<3 * Geo::BB + KS * 1024, 3 * Geo::BB + KS * 1024 + 256>(sb + b_l);
+        fb[c][0] = ring_frag<0 * BB + KS * 1024, 0 * BB + KS * 1024 + 256>(sb + b_l);
+        fb[c][1] = ring_frag<1 * BB + KS * 1024, 1 * BB + KS * 1024 + 256>(sb + b_l);
+        fb[c][2] = ring_frag<2 * BB + KS * 1024, 2 * BB + KS * 1024 + 256>(sb + b_l);
+        fb[c][3] = ring_frag<3 * BB + KS * 1024, 3 * BB + KS * 1024 + 256>(sb + b_l);
         fb[c][4] = ring_frag<KS * 1024, KS * 1024 + 256>(sb + b_4);
     };
     auto load = [&](int ks, int c, unsigned sb) __attribute__((always_inline)) {
         switch (ks) {
             case 0: load_ks(std::integral_constant<int, 0>{}, c, sb); break;
             case 1: load_ks(std::integral_constant<int, 1>{}, c, sb); break;
-            case 2: load_ks(std::integral_constant<int, 2 % Geo::SLICES>{}, c, sb); break;
-            default: load_ks(std::integral_constant<int, 3 % Geo::SLICES>{}, c, sb); break;
+            case 2: load_ks(std::integral_constant<int, 2>{}, c, sb); break;
+            default: load_ks(std::integral_constant<int, 3>{}, c, sb); break;
         }
     };
+    // lgkmcnt(0), then every fragment of buffer c re-defined after it (asm reads are invisible
+    // to the compiler's own waits; the MFMAs must not be hoisted above the wait)
     auto wait_frags = [&](int c) __attribute__((always_inline)) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         asm volatile("" : "+v"(fa[c][0]), "+v"(fa[c][1]));
@@ -767,15 +765,18 @@ __device__ __forceinline__ void ring_compute_split_ch(const WRingArgs& a, int w,
         load(0, 0, sb);
         for (int i = 0; i < nst; ++i) {
 #pragma unroll
-            for (int ks = 0; ks < Geo::SLICES; ++ks) {
+            for (int ks = 0; ks < SLICES; ++ks) {
                 const int c = ks & 1;
                 wait_frags(c);
-                if (ks + 1 < Geo::SLICES) {
+                if (ks + 1 < SLICES) {
                     load(ks + 1, c ^ 1, sb);
                 } else if (i + 1 < nst) {
-                    __builtin_amdgcn_s_barrier();  // (as CW = 0)
+                    // every read of this step is done: the barrier lets the loaders refill the
+                    // previous step's slot and tells us step i + 1 has landed - read its first
+                    // slice under this slice's MFMAs
+                    __builtin_amdgcn_s_barrier();
                     slot = slot + 1 == S ? 0 : slot + 1;
-                    sb = lds0 + (unsigned)slot * Geo::SLOT;
+                    sb = lds0 + (unsigned)slot * SLOT;
                     load(0, c ^ 1, sb);
                 }
                 __builtin_amdgcn_sched_barrier(0);
@@ -790,7 +791,10 @@ __device__ __forceinline__ void ring_compute_split_ch(const WRingArgs& a, int w,
             }
         }
     }
-    // D[k][col]: col = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5); direct dword stores (CW = 0)
+    // D[k][col]: col = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5).  Direct dword stores
+    // (an LDS-staged dwordx4 epilogue measured 3-4 us slower per launch: hipcc serialised its
+    // stores on vmcnt(0)); the accumulate test is hoisted out of the loops (a per-element select
+    // would branch and wait vmcnt(0) around every load)
     const int TC = 9 * a.C;
     float* base = a.part + grp * a.gs_part + (size_t)split * a.K * TC + (size_t)(k0 + 4 * (lane >> 5)) * TC + n0 +
                   (lane & 31);
@@ -819,23 +823,8 @@ __device__ __forceinline__ void ring_compute_split_ch(const WRingArgs& a, int w,
     }
 }
 
-template <int S, int BK>
-__device__ __forceinline__ void ring_compute_split(const WRingArgs& a, int w, int lane, unsigned lds0, int nst,
-                                                   int grp, int split, int k0, int n0) {
-    if (w >> 1) ring_compute_split_ch<S, BK, 1>(a, w, lane, lds0, nst, grp, split, k0, n0);
-    else ring_compute_split_ch<S, BK, 0>(a, w, lane, lds0, nst, grp, split, k0, n0);
-}
-
-// The compute waves' share of the 4 x 9 grid of 32 x 32 blocks (4 k-blocks of the 128 output channels
-// x 9 column blocks of the 288 (tap, channel) columns).  CW = 0: wave w owns k-block w x all 9 column
-// blocks - 1 A + 9 B fragments (20 transposed reads) per 9 MFMAs, every B fragment read by all four
-// waves.  CW = 1: wave w owns k-blocks {2 kh, 2 kh + 1} (kh = w & 1) x column blocks 5 ch .. 5 ch + 3
-// (ch = w >> 1) plus the single cell (2 kh + ch, 4) of the middle column block - still 9 MFMAs per
-// wave, but 2 A + 5 B fragments (14 reads): 56 instead of 80 transposed reads per k-slice and CU.
-template <int S, int BK, int CW = 0>
 __global__ __launch_bounds__(512) void k_wgrad_ring(WRingArgs a) {
-    static_assert(S >= 2 && (BK == 32 || BK == 64), "k_wgrad_ring: S >= 2 slots of 32 or 64 pixels");
-    using Geo = RingGeo<BK>;
+    using namespace ring;
     constexpr int D = S - 1;  // steps in flight
     extern __shared__ __attribute__((aligned(16))) uint4 wsm[];
     char* lds = reinterpret_cast<char*>(wsm);
@@ -856,192 +845,89 @@ __global__ __launch_bounds__(512) void k_wgrad_ring(WRingArgs a) {
     const int nst = max(0, min((a.M + BK - 1) / BK, step0 + a.sps) - step0);
     const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
 
-    if (wave >= 4) {
-        // ---- loader waves ----
-        // BK = 64: every loader wave stages B rows 16 lw .. + 15 of the 9 blocks and A rows
-        //          16 lw .. + 15 of both blocks (9 + 4 pieces per step);
-        // BK = 32: waves 0, 1 stage B rows 16 lw .. + 15 (9 pieces), waves 2, 3 A rows
-        //          16 (lw - 2) .. + 15 of both blocks (4 pieces)
-        const int lw = wave - 4;
-        constexpr bool SPLITROLE = BK == 32;
-        const bool do_b = !SPLITROLE || lw < 2, do_a = !SPLITROLE || lw >= 2;
-        const int rb = SPLITROLE ? (lw & 1) : lw;  // 16-row band of this wave's pieces
-        typedef __attribute__((address_space(1))) const void* gptr_t;
-        typedef __attribute__((address_space(3))) void* lptr_t;
-        const void* zero = (const void*)g_wzero16;
-        const uint16_t* __restrict__ gdy = a.dy + grp * a.gs_dy;
-        const uint16_t* __restrict__ gx = a.x + grp * a.gs_x;
-        const int brow = 16 * rb + (lane >> 2), bc = (lane & 3) * 8;
-        int bdh[9], bdw[9], boff[9];
-#pragma unroll
-        for (int j = 0; j < 9; ++j) {
-            const int n = n0 + 32 * j + bc;
-            const int tap = n >> a.logC, c = n & (a.C - 1);
-            const int r = tap / 3, s = tap - 3 * r;
-            bdh[j] = r - a.padh;
-            bdw[j] = s - a.padw;
-            boff[j] = ((bdh[j] * a.W + bdw[j]) << a.logC) + c;
-        }
-        // A sources advance by BK pixel rows per step (no per-step 64-bit multiply)
-        int arow[2];
-        const uint16_t* ap[2][2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            arow[h] = 16 * rb + 8 * h + (lane >> 3);
-#pragma unroll
-            for (int ab = 0; ab < 2; ++ab)
-                ap[h][ab] = gdy + (size_t)(step0 * BK + arow[h]) * a.K + k0 + 64 * ab +
-                            (((lane & 7) ^ wswz<128>(arow[h])) << 3);
-        }
-        const size_t astep = (size_t)BK * a.K;
-        const int PQ = a.P * a.Q;
-        int m = step0 * BK + brow;
-        int b = (int)a.fd_pq.div((uint32_t)m);
-        int p = (int)a.fd_q.div((uint32_t)(m - b * PQ));
-        int q = m - b * PQ - p * a.Q;
-        auto dma = [&](const void* src, unsigned off) __attribute__((always_inline)) {
-            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + off), 16, 0, 0);
-        };
-        int slot = 0;
-        auto issue = [&](int i) __attribute__((always_inline)) {  // step step0 + i into the next slot
-            const unsigned sb = (unsigned)slot * Geo::SLOT;
-            const int ms = (step0 + i) * BK;
-            if (do_b) {
-                const int hi0 = p * a.sth, wi0 = q * a.stw;
-                const bool rok = ms + brow < a.M;
-                const long pix = ((long)(b * a.H + hi0) * a.W + wi0) << a.logC;
-#pragma unroll
-                for (int j = 0; j < 9; ++j) {
-                    const int hi = hi0 + bdh[j], wi = wi0 + bdw[j];
-                    const bool ok = rok & ((unsigned)hi < (unsigned)a.H) & ((unsigned)wi < (unsigned)a.W);
-                    dma(ok ? (const void*)(gx + pix + boff[j]) : zero, sb + j * Geo::BB + rb * 1024);
-                }
-                // next step's pixel: + BK = (adv_b, adv_p, adv_q), one carry per component at most
-                int nq = q + a.adv_q, np = p + a.adv_p, nb = b + a.adv_b;
-                if (nq >= a.Q) { nq -= a.Q; ++np; }
-                if (np >= a.P) { np -= a.P; ++nb; }
-                b = nb; p = np; q = nq;
-            }
-            if (do_a) {
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const bool ok = ms + arow[h] < a.M;
-#pragma unroll
-                    for (int ab = 0; ab < 2; ++ab) {
-                        dma(ok ? (const void*)ap[h][ab] : zero, sb + Geo::B + ab * Geo::AB + (2 * rb + h) * 1024);
-                        ap[h][ab] += astep;
-                    }
-                }
-            }
-            slot = slot + 1 == S ? 0 : slot + 1;
-        };
-        // pieces per step of this wave: the counted wait leaves the D - 1 younger steps in flight
-        auto wait_all_but = [&](bool younger) __attribute__((always_inline)) {
-            if (!younger) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            else if (!SPLITROLE) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(13 * (D - 1)) : "memory");
-            else if (do_b) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(9 * (D - 1)) : "memory");
-            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (D - 1)) : "memory");
-        };
-        for (int i = 0; i < D && i < nst; ++i) issue(i);
-        for (int i = 0; i < nst; ++i) {
-            // step i has landed (the younger steps may stay in flight; at the tail, where fewer
-            // than D - 1 younger ones exist, everything); after the barrier no compute wave reads
-            // step i - 1's slot any more: step i + D refills it.  No DMA past the range, so none
-            // is in flight once the last barrier has passed (the epilogue reuses the ring).
-            wait_all_but(i + D - 1 < nst);
-            __builtin_amdgcn_s_barrier();
-            if (i + D < nst) issue(i + D);
-        }
+    if (wave < 4) {
+        if (wave >> 1) ring_compute<1>(a, wave, lane, lds0, nst, grp, split, k0, n0);
+        else ring_compute<0>(a, wave, lane, lds0, nst, grp, split, k0, n0);
         return;
     }
-
-    // ---- compute waves ----
-    const int w = wave;
-    if constexpr (CW == 1) {
-        ring_compute_split<S, BK>(a, w, lane, lds0, nst, grp, split, k0, n0);
-        return;
+    // ---- loader waves: wave 4 + lw stages B rows 16 lw .. + 15 of the 9 blocks and A rows
+    // 16 lw .. + 15 of both blocks (9 + 4 pieces per step) ----
+    const int lw = wave - 4;
+    typedef __attribute__((address_space(1))) const void* gptr_t;
+    typedef __attribute__((address_space(3))) void* lptr_t;
+    const void* zero = (const void*)g_wzero16;
+    const uint16_t* __restrict__ gdy = a.dy + grp * a.gs_dy;
+    const uint16_t* __restrict__ gx = a.x + grp * a.gs_x;
+    const int brow = 16 * lw + (lane >> 2), bc = (lane & 3) * 8;
+    int bdh[9], bdw[9], boff[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+        const int n = n0 + 32 * j + bc;
+        const int tap = n >> a.logC, c = n & (a.C - 1);
+        const int r = tap / 3, s = tap - 3 * r;
+        bdh[j] = r - a.padh;
+        bdw[j] = s - a.padw;
+        boff[j] = ((bdh[j] * a.W + bdw[j]) << a.logC) + c;
     }
-    floatx16 acc[9];
+    // A sources advance by BK pixel rows per step (no per-step 64-bit multiply)
+    int arow[2];
+    const uint16_t* ap[2][2];
 #pragma unroll
-    for (int j = 0; j < 9; ++j)
+    for (int h = 0; h < 2; ++h) {
+        arow[h] = 16 * lw + 8 * h + (lane >> 3);
 #pragma unroll
-        for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
-    // tr-read geometry (k_conv_wgrad4's): half-wave g >> 1 reads rows 8 (g >> 1) + q4 (+4) of a
-    // 16-row k-slice, 4-column block p4 of the 32-column fragment, 16-column half g & 1
-    const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
-    const int rbase = 8 * (g >> 1) + q4;
-    const int ac = 32 * (w & 1) + 16 * (g & 1) + 4 * p4;
-    const unsigned a_lane =
-        Geo::B + (w >> 1) * Geo::AB + rbase * 128 + ((((ac >> 3) ^ wswz<128>(rbase))) << 4) + (ac & 7) * 2;
-    const unsigned b_lane = rbase * 64 + (16 * (g & 1) + 4 * p4) * 2;
-    bf16x8 fa[2], fb[2][9];
-    auto load = [&](int ks, int c, unsigned sb) __attribute__((always_inline)) {
-        switch (ks) {
-            case 0: ring_load<BK, 0>(fa[c], fb[c], sb + a_lane, sb + b_lane); break;
-            case 1: ring_load<BK, 1>(fa[c], fb[c], sb + a_lane, sb + b_lane); break;
-            case 2: ring_load<BK, 2 % Geo::SLICES>(fa[c], fb[c], sb + a_lane, sb + b_lane); break;
-            default: ring_load<BK, 3 % Geo::SLICES>(fa[c], fb[c], sb + a_lane, sb + b_lane); break;
-        }
-    };
-    // lgkmcnt(0), then every fragment of buffer c re-defined after it (asm reads are invisible
-    // to the compiler's own waits; the MFMAs must not be hoisted above the wait)
-    auto wait_frags = [&](int c) __attribute__((always_inline)) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        asm volatile("" : "+v"(fa[c]));
-#pragma unroll
-        for (int j = 0; j < 9; ++j) asm volatile("" : "+v"(fb[c][j]));
-        __builtin_amdgcn_sched_barrier(0);
+        for (int ab = 0; ab < 2; ++ab)
+            ap[h][ab] = gdy + (size_t)(step0 * BK + arow[h]) * a.K + k0 + 64 * ab +
+                        (((lane & 7) ^ wswz<128>(arow[h])) << 3);
+    }
+    const size_t astep = (size_t)BK * a.K;
+    const int PQ = a.P * a.Q;
+    int m = step0 * BK + brow;
+    int b = (int)a.fd_pq.div((uint32_t)m);
+    int p = (int)a.fd_q.div((uint32_t)(m - b * PQ));
+    int q = m - b * PQ - p * a.Q;
+    auto dma = [&](const void* src, unsigned off) __attribute__((always_inline)) {
+        __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + off), 16, 0, 0);
     };
     int slot = 0;
-    if (nst > 0) {
-        __builtin_amdgcn_s_barrier();  // step 0 landed
-        unsigned sb = lds0;
-        load(0, 0, sb);
-        for (int i = 0; i < nst; ++i) {
-#pragma unroll
-            for (int ks = 0; ks < Geo::SLICES; ++ks) {
-                const int c = ks & 1;
-                wait_frags(c);
-                if (ks + 1 < Geo::SLICES) {
-                    load(ks + 1, c ^ 1, sb);
-                } else if (i + 1 < nst) {
-                    // every read of this step is done: the barrier lets the loaders refill the
-                    // previous step's slot and tells us step i + 1 has landed - read its first
-                    // slice under this slice's MFMAs
-                    __builtin_amdgcn_s_barrier();
-                    slot = slot + 1 == S ? 0 : slot + 1;
-                    sb = lds0 + (unsigned)slot * Geo::SLOT;
-                    load(0, c ^ 1, sb);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int j = 0; j < 9; ++j)
-                    acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[c], fb[c][j], acc[j], 0, 0, 0);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-    }
-    // D[k][col]: col = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5).  Direct dword stores
-    // (an LDS-staged dwordx4 epilogue measured 3-4 us slower per launch: hipcc serialised its
-    // stores on vmcnt(0)); the accumulate test is hoisted out of the loops (a per-element select
-    // would branch and wait vmcnt(0) around every load)
-    const int TC = 9 * a.C;
-    float* out = a.part + grp * a.gs_part + (size_t)split * a.K * TC + (size_t)(k0 + 32 * w + 4 * (lane >> 5)) * TC +
-                 n0 + (lane & 31);
-    if (a.accumulate) {
+    auto issue = [&](int i) __attribute__((always_inline)) {  // step step0 + i into the next slot
+        const unsigned sb = (unsigned)slot * SLOT;
+        const int ms = (step0 + i) * BK;
+        const int hi0 = p * a.sth, wi0 = q * a.stw;
+        const bool rok = ms + brow < a.M;
+        const long pix = ((long)(b * a.H + hi0) * a.W + wi0) << a.logC;
 #pragma unroll
         for (int j = 0; j < 9; ++j) {
-            float v[16];
-#pragma unroll
-            for (int e = 0; e < 16; ++e) v[e] = out[(size_t)((e & 3) + 8 * (e >> 2)) * TC + 32 * j];
-#pragma unroll
-            for (int e = 0; e < 16; ++e) out[(size_t)((e & 3) + 8 * (e >> 2)) * TC + 32 * j] = v[e] + acc[j][e];
+            const int hi = hi0 + bdh[j], wi = wi0 + bdw[j];
+            const bool ok = rok & ((unsigned)hi < (unsigned)a.H) & ((unsigned)wi < (unsigned)a.W);
+            dma(ok ? (const void*)(gx + pix + boff[j]) : zero, sb + j * BB + lw * 1024);
         }
-    } else {
+        // next step's pixel: + BK = (adv_b, adv_p, adv_q), one carry per component at most
+        int nq = q + a.adv_q, np = p + a.adv_p, nb = b + a.adv_b;
+        if (nq >= a.Q) { nq -= a.Q; ++np; }
+        if (np >= a.P) { np -= a.P; ++nb; }
+        b = nb; p = np; q = nq;
 #pragma unroll
-        for (int j = 0; j < 9; ++j)
+        for (int h = 0; h < 2; ++h) {
+            const bool ok = ms + arow[h] < a.M;
 #pragma unroll
-            for (int e = 0; e < 16; ++e) out[(size_t)((e & 3) + 8 * (e >> 2)) * TC + 32 * j] = acc[j][e];
+            for (int ab = 0; ab < 2; ++ab) {
+                dma(ok ? (const void*)ap[h][ab] : zero, sb + B + ab * AB + (2 * lw + h) * 1024);
+                ap[h][ab] += astep;
+            }
+        }
+        slot = slot + 1 == S ? 0 : slot + 1;
+    };
+    for (int i = 0; i < D && i < nst; ++i) issue(i);
+    for (int i = 0; i < nst; ++i) {
+        // step i has landed (13 pieces per step per loader wave; the D - 1 younger steps may stay
+        // in flight, at the tail everything); after the barrier no compute wave reads step i - 1's
+        // slot any more: step i + D refills it.  No DMA past the range, so none is in flight once
+        // the last barrier has passed.
+        if (i + D - 1 < nst) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(13 * (D - 1)) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (i + D < nst) issue(i + D);
     }
 }
 
@@ -1259,8 +1145,7 @@ static int ilog2w(int v) {
 
 static int wgrad_target_wgs() {
     static int w = [] {
-        const char* e = getenv("GM_WGRAD_WGS");
-        return e ? atoi(e) : 512;
+        return 512;
     }();
     return w;
 }
@@ -1298,7 +1183,7 @@ static WPlan plan(const gm_conv_desc_hw* d, int G = 1) {
 
 using namespace gm;
 
-// operand staging of k_conv_wgrad4 (its WR argument; GM_WGRAD_WR at load): 0 LDS-DMA,
+// operand staging of k_conv_wgrad4 (its WR argument; gm_conv_set_wgrad_staging): 0 LDS-DMA,
 // 1 register-staged, 2 (default) register-staged for 1x1 filters only.  Isolated
 // (tools/trunk_table.py) the register-staged form is faster on the 1x1/s2 downsample
 // gradients (16.6-18.7 vs 18.0-19.6 us) and slower on every 3x3 shape (layer 4 64.6 ->
@@ -1306,19 +1191,17 @@ using namespace gm;
 // the input-gradient chain, the all-register form measured 0.4 % faster on average over
 // nine interleaved pairs, within the box-to-box noise.
 static int g_wgrad_wr = [] {
-    const char* e = getenv("GM_WGRAD_WR");
-    return e ? atoi(e) : 2;
+    return 2;
 }();
 
-// weight-gradient kernel choice for 3x3 / s1 / p1 shapes with W <= 62 (GM_WGRAD_LOOP at load,
+// weight-gradient kernel choice for 3x3 / s1 / p1 shapes with W <= 62 (gm_conv_set_wgrad_loop,
 // gm_conv_set_wgrad_loop): bit 1 = k_wgrad_halo64 for 64 channels (layer 1), bit 2 = also for
 // 128 channels (layer 2); bit 4 = k_wgrad_ring for the other 3x3 shapes it serves (K % 128 == 0,
 // C % 32 == 0: layers 3 / 4 and the strided first convolutions); otherwise k_conv_wgrad4.
 // Default 22 (bits 1, 2: r04, B = 64 two-view step: layer 1 61.9 -> 44.9 us and layer 2
 // 54.6 -> 46.6 us per launch with the sum; step 3.98 -> 3.91 ms against bit 1 alone).
 static int g_wgrad_loop = [] {
-    const char* e = getenv("GM_WGRAD_LOOP");
-    return e ? atoi(e) : 22;
+    return 22;
 }();
 
 template <int MT, int NT>
@@ -1351,15 +1234,14 @@ static bool halo64_ok(const gm_conv_desc_hw* d) {
            d->W >= 1 && d->H >= 64 / halo64_pp(d->W) && d->N >= 1 &&
            (long long)d->N * d->H * d->W * (d->C > d->K ? d->C : d->K) < (1ll << 31);
 }
-// workgroups per (view group, channel tile): GM_WGRAD_HALO64_WGS in all, default 128 - half the
+// workgroups per (view group, channel tile): 128 in all - half the
 // CUs: the launch runs on the weight-gradient stream beside the input-gradient chain, and one
 // workgroup per CU (512 threads, 81 KB of LDS) left no room on any CU for that chain's BN
 // finalize / apply launches (C2, in the step: 64 / 96 / 128 / 160 / 256 workgroups = 3.80 /
 // 3.67 / 3.63 / 3.63 / 3.70 ms; as k_wgrad_ring's half-CU grid)
 static int halo64_wgs() {
     static const int w = [] {
-        const char* e = getenv("GM_WGRAD_HALO64_WGS");
-        const int v = e ? atoi(e) : 128;
+        const int v = 128;
         return v < 8 ? 8 : v;
     }();
     return w;
@@ -1374,7 +1256,7 @@ static int halo64_splits(const gm_conv_desc_hw* d, int G) {
 }
 
 // k_wgrad_ring serves 3x3 shapes (any stride / padding) with K % 128 == 0 and C a power of two
-// >= 32 (GM_WGRAD_LOOP bit 4, default on): tiles x splits sized to one workgroup per CU
+// >= 32 (gm_conv_set_wgrad_loop bit 4, default on): tiles x splits sized to one workgroup per CU
 static int device_cus_w() {
     static const int cus = [] {
         int dev = 0, n = 0;
@@ -1385,35 +1267,18 @@ static int device_cus_w() {
     }();
     return cus;
 }
-// k_wgrad_ring's form (GM_WGRAD_RING at load, gm_conv_set_wgrad_ring): 0 = 3 slots of 64 pixels,
-// 1 = 6 slots of 32 pixels (more bytes in flight, twice the barriers), 3 = 3 slots of 64 pixels with
-// the split-column compute waves (CW = 1)
-static int g_ring_form = [] {
-    const char* e = getenv("GM_WGRAD_RING");
-    return e ? atoi(e) : 0;
-}();
-static int ring_bk() { return g_ring_form == 1 ? 32 : 64; }
-// GM_WGRAD_RING_WGS: workgroups the plan aims at.  Default: HALF the CUs.  The ring runs on the
-// weight-gradient stream beside the main chain's input-gradient convolutions and BatchNorms, and
-// a workgroup holds its CU's LDS (156 KB): one per CU starved the main chain (C2 step 3.94 ms
-// against 3.85 without the ring), half the CUs left the other half to it (3.75 ms; 64 / 96 /
-// 160 / 192 / 224: 3.77 / 3.77 / 3.80 / 3.80 / 3.80 ms, r05 interleaved A/B).  Alone a launch
-// then takes longer (conv family 0.218 vs 0.228 isolated).  GM_WGRAD_RING_MINK: the smallest
-// K served (default 128).
-static int g_ring_wgs = [] {
-    const char* e = getenv("GM_WGRAD_RING_WGS");
-    return e ? atoi(e) : 0;
-}();
-static int g_ring_mink = [] {
-    const char* e = getenv("GM_WGRAD_RING_MINK");
-    return e ? atoi(e) : 128;
-}();
+// k_wgrad_ring's grid: HALF the CUs.  The ring runs on the weight-gradient stream beside the main
+// chain's input-gradient convolutions and BatchNorms, and a workgroup holds its CU's LDS (156 KB):
+// one per CU starved the main chain (C2 step 3.94 ms against 3.85 without the ring), half the CUs
+// left the other half to it (3.75 ms; 64 / 96 / 160 / 192 / 224 workgroups: 3.77 / 3.77 / 3.80 /
+// 3.80 / 3.80 ms, r05 interleaved A/B).  Alone a launch then takes longer (conv family 0.218 vs
+// 0.228 isolated).  Measured and dropped (r05): 6 slots of 32 pixels (+0.06-0.24 ms/step), 2 slots.
 struct RingPlan {
     int P, Q, M, tiles_k, tiles_n, splits, sps;
 };
 static bool ring_plan(const gm_conv_desc_hw* d, int G, RingPlan& r) {
     if (!(g_wgrad_loop & 16) || d->R != 3 || d->S != 3 || d->K % 128 != 0 || d->C % 32 != 0 || ilog2w(d->C) < 5 ||
-        d->K < g_ring_mink)
+        d->K < 128)
         return false;
     r.P = (d->H + 2 * d->pad_h - 3) / d->stride_h + 1;
     r.Q = (d->W + 2 * d->pad_w - 3) / d->stride_w + 1;
@@ -1424,9 +1289,9 @@ static bool ring_plan(const gm_conv_desc_hw* d, int G, RingPlan& r) {
     r.tiles_k = d->K / 128;
     r.tiles_n = d->C / 32;  // 9 C / 288
     const int tiles = r.tiles_k * r.tiles_n * G;
-    const int bk = ring_bk();
+    constexpr int bk = ring::BK;
     const int steps = (r.M + bk - 1) / bk;
-    int want = (g_ring_wgs > 0 ? g_ring_wgs : device_cus_w() / 2) / tiles;
+    int want = (device_cus_w() / 2) / tiles;
     if (want > steps / (512 / bk)) want = steps / (512 / bk);  // >= 512 pixels per split
     if (want < 1) want = 1;
     r.sps = (steps + want - 1) / want;
@@ -1437,8 +1302,7 @@ static bool ring_plan(const gm_conv_desc_hw* d, int G, RingPlan& r) {
 // k_wgrad_stem serves the pixel-pair stem: 8-channel pairs, 64 output channels, a 7 x 4
 // filter, strides (2, 1), no padding, output rows of a multiple of 16 and <= 128 pixels
 static int g_wgrad_stem = [] {
-    const char* e = getenv("GM_WGRAD_STEM");  // 0: the stem's weight gradient takes k_conv_wgrad4
-    return e ? atoi(e) : 1;
+    return 1;  // 0: the stem's weight gradient takes k_conv_wgrad4
 }();
 struct StemWPlan {
     int P, Q, cpi, L, splits;
@@ -1602,7 +1466,7 @@ extern "C" int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, con
         r.tiles_k = rp.tiles_k; r.tiles_n = rp.tiles_n; r.splits = rp.splits; r.sps = rp.sps;
         r.fd_pq = FastDiv((uint32_t)(rp.P * rp.Q));
         r.fd_q = FastDiv((uint32_t)rp.Q);
-        const int BK = ring_bk();
+        constexpr int BK = ring::BK;
         r.adv_b = BK / (rp.P * rp.Q);
         r.adv_p = (BK % (rp.P * rp.Q)) / rp.Q;
         r.adv_q = (BK % (rp.P * rp.Q)) % rp.Q;
@@ -1614,27 +1478,17 @@ extern "C" int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, con
         r.gs_part = direct ? dw_stride : (long long)rp.splits * (long long)slab;
         r.accumulate = direct ? accumulate : 0;
         const int grid = rp.tiles_k * rp.tiles_n * rp.splits * G;
-        auto go = [&](auto sc, auto bc, auto cwc) -> int {
-            constexpr int S = decltype(sc)::value, BK = decltype(bc)::value, CW = decltype(cwc)::value;
-            constexpr size_t lds = (size_t)S * RingGeo<BK>::SLOT;
-            static bool attr = false;
-            if (!attr) {
-                if (hipFuncSetAttribute((const void*)k_wgrad_ring<S, BK, CW>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)lds) != hipSuccess) {
-                    set_error("k_wgrad_ring: %zu B of LDS refused", lds);
-                    return GM_E_UNSUP;
-                }
-                attr = true;
+        static bool attr = false;
+        if (!attr) {
+            if (hipFuncSetAttribute((const void*)k_wgrad_ring, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)ring::LDS) != hipSuccess) {
+                set_error("k_wgrad_ring: %zu B of LDS refused", ring::LDS);
+                return GM_E_UNSUP;
             }
-            k_wgrad_ring<S, BK, CW><<<grid, 512, lds, st0>>>(r);
-            return check_launch("k_wgrad_ring");
-        };
-        using I = std::integral_constant<int, 0>;
-        const int rc =
-            g_ring_form == 1   ? go(std::integral_constant<int, 6>{}, std::integral_constant<int, 32>{}, I{})
-            : g_ring_form == 3 ? go(std::integral_constant<int, 3>{}, std::integral_constant<int, 64>{},
-                                    std::integral_constant<int, 1>{})
-                               : go(std::integral_constant<int, 3>{}, std::integral_constant<int, 64>{}, I{});
+            attr = true;
+        }
+        k_wgrad_ring<<<grid, 512, ring::LDS, st0>>>(r);
+        const int rc = check_launch("k_wgrad_ring");
         if (rc || direct) return rc;
         return split_sum(r.part, rp.splits, slab);
     }
@@ -1700,13 +1554,6 @@ extern "C" int gm_conv_set_wgrad_staging(int wr) {
     GM_REQUIRE(wr >= 0 && wr <= 2,
                "gm_conv_set_wgrad_staging: 0 (LDS-DMA), 1 (register-staged), 2 (register-staged for 1x1 filters)");
     g_wgrad_wr = wr;
-    return GM_OK;
-}
-
-extern "C" int gm_conv_set_wgrad_ring(int form) {
-    GM_REQUIRE(form >= 0 && form <= 3,
-               "gm_conv_set_wgrad_ring: 0 (3 slots of 64 pixels), 1 (6 slots of 32), 3 (split-column waves)");
-    g_ring_form = form;
     return GM_OK;
 }
 

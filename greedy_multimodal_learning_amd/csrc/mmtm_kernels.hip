@@ -421,25 +421,22 @@ using namespace gm;
 // ======================= host entry points =======================
 
 // k_colreduce_nhwc form: pixels in flight per thread (4, 8, 16) and threads per workgroup
-// (256, 1024); GM_RED_UNROLL / GM_RED_THREADS / gm_mmtm_set_reduce_form, an A/B knob
+// (256, 1024); gm_mmtm_set_reduce_form, an A/B knob
 static int g_red_unroll = -1, g_red_threads = -1;
 static int red_unroll() {
     if (g_red_unroll < 0) {
-        const char* e = getenv("GM_RED_UNROLL");
-        g_red_unroll = e ? atoi(e) : 4;
+        g_red_unroll = 4;
     }
     return g_red_unroll;
 }
 static int red_threads() {
     if (g_red_threads < 0) {
-        const char* e = getenv("GM_RED_THREADS");
-        g_red_threads = e ? atoi(e) : 256;
+        g_red_threads = 256;
     }
     return g_red_threads;
 }
 static int g_red_nt = [] {
-    const char* e = getenv("GM_RED_NT");
-    return e ? atoi(e) : 1;
+    return 1;
 }();
 extern "C" int gm_mmtm_set_reduce_form(int threads, int unroll) {
     g_red_nt = threads < 0;  // negative threads: nontemporal loads (forward, bf16; the default)
@@ -453,10 +450,10 @@ extern "C" int gm_mmtm_set_reduce_form(int threads, int unroll) {
 
 static int red_wgs() {
     static int w = [] {
-        const char* e = getenv("GM_MMTM_RED_WGS");  // workgroups wanted for the NHWC squeeze
+        // workgroups wanted for the NHWC squeeze:
         // 128: from B = 64 up one workgroup per (sample, view) and no partials pass (measured
         // 25-30 us/step faster at C2 than 512, which split each map 4 ways at B = 64)
-        return e ? atoi(e) : 128;
+        return 128;
     }();
     return w;
 }

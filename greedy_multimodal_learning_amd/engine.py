@@ -300,7 +300,7 @@ class BalancedStep:
         # lazy_zero: no zero-fill of the flat gradient buffer per step (gradsink.py)
         self.sink = GradSink(self.flat.slices.keys(),
                              on_ready=self.buckets._on_sink if self.buckets is not None else None,
-                             lazy_zero=os.environ.get("GM_LAZY_ZERO", "1") != "0")
+                             lazy_zero=True)
         if self.buckets is not None:
             self.sink.on_pending = self.buckets._on_pending
         self.last_loss = None

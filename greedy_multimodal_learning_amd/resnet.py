@@ -10,7 +10,6 @@ config C5.  Convolutions are `conv.GMConv2d` (bf16 MFMA kernels on HIP); batch
 norms are `bn.GMBatchNorm2d`, which take the block's residual add and ReLU as
 fused arguments (`relu` modules are kept for name/structure parity).
 """
-import os
 
 import torch
 import torch.nn as nn
@@ -19,7 +18,7 @@ from .bn import GMBatchNorm2d
 from .conv import GMConv2d
 from .gradsink import GradJoin
 
-_JOIN = os.environ.get("GM_GRAD_JOIN", "1") != "0"
+_JOIN = True
 
 
 def _join():

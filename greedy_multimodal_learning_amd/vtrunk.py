@@ -39,25 +39,25 @@ BF = torch.bfloat16
 ENABLED = os.environ.get("GM_VTRUNK", "1") != "0"
 
 
-# the stem's pool + BN backward in the gathered two-pass form (GM_FUSED_STEM_BWD=0: the
-# max-pool backward + BatchNorm backward pair, an A/B switch)
-FUSED_STEM_BWD = os.environ.get("GM_FUSED_STEM_BWD", "1") != "0"
+# the stem's pool + BN backward in the gathered two-pass form (False: the max-pool backward +
+# BatchNorm backward pair; module switches below are A/B and test switches)
+FUSED_STEM_BWD = True
 # its statistics pass over the pooled tensors (the forward's selected x) instead of x
-STEM_XSEL = os.environ.get("GM_STEM_XSEL", "1") != "0"
-# the stem BN's statistics from the stem convolution's epilogue (GM_FUSED_STEM_STATS=0: the
-# statistics pass over the convolution's output, an A/B switch)
-FUSED_STEM_STATS = os.environ.get("GM_FUSED_STEM_STATS", "1") != "0"
+STEM_XSEL = True
+# the stem BN's statistics from the stem convolution's epilogue (False: the statistics pass over
+# the convolution's output)
+FUSED_STEM_STATS = True
 # every other BatchNorm's statistics from its producing convolution's epilogue, then a finalize
 # and a streaming apply instead of the single-launch BatchNorm's statistics read
-# (GM_EPI_BN_STATS=0: the single-launch BatchNorm)
-EPI_BN_STATS = os.environ.get("GM_EPI_BN_STATS", "1") != "0"
+# (False: the single-launch BatchNorm)
+EPI_BN_STATS = True
 # the block-output BatchNorm (+ residual + ReLU) writes its ReLU mask as bits (1/16 of y) and the
-# backward reads them in place of y (GM_BN_RELU_MASK=0: the backward reads y)
-BN_RELU_MASK = os.environ.get("GM_BN_RELU_MASK", "1") != "0"
+# backward reads them in place of y (False: the backward reads y)
+BN_RELU_MASK = True
 # the ReLU-after-BN backward (bn1 / bn2 of a block) takes its statistics from the input-gradient
 # epilogue of the convolution it feeds, then one finalize + one streaming apply
-# (GM_EPI_BN_BWD_STATS=0: the single-launch backward)
-EPI_BN_BWD_STATS = os.environ.get("GM_EPI_BN_BWD_STATS", "1") != "0"
+# (False: the single-launch backward)
+EPI_BN_BWD_STATS = True
 _GM_E_UNSUP = -3
 
 
@@ -110,15 +110,15 @@ def _reset_bn_scratch():
 
 # ---- convolution -------------------------------------------------------------------
 
-WGRAD_STREAM = os.environ.get("GM_WGRAD_STREAM", "1") != "0"
+WGRAD_STREAM = True
 _WGRAD_SIDE = 64  # streams.side_stream index of the weight-gradient stream
 # Weight-gradient launches are handed to the wgrad stream in batches of WGRAD_BATCH (one
-# stream fork per batch, GM_WGRAD_BATCH; 1 = a fork per convolution).  In a replayed
+# stream fork per batch; 1 = a fork per convolution).  In a replayed
 # hipGraph every fork makes the main chain's next node start on another hardware queue,
 # ~15-25 us of idle GPU per hop (profiles/r03e_step_listing.txt, tools/trace_gaps.py).
 # A batch is flushed when full, by the stem's backward (the trunk's last), and at the end
 # of the backward pass (autograd queue_callback), so no launch is ever left pending.
-WGRAD_BATCH = max(1, int(os.environ.get("GM_WGRAD_BATCH", "8")))
+WGRAD_BATCH = 8
 _PENDING = []  # (launch, weights, tensors to keep alive, device)
 
 

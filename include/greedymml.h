@@ -61,7 +61,7 @@ int gm_set_spin_limit(unsigned polls);
 /* Co-residency of the single-launch BatchNorm: at most `n` such launches are assumed
  * to run at once (one per concurrently running trunk stream, plus headroom for other
  * kernels); the fused grid is capped at CUs x (measured blocks per CU) / n, else the
- * two-launch path runs.  Default 4 (GM_BN_FUSE_STREAMS overrides at load). */
+ * two-launch path runs.  Default 4. */
 int gm_bn_set_concurrency(int n);
 /* Device residency plan for every kernel whose workgroups wait on other workgroups of
  * the same launch (single-launch BatchNorm, split-K turnstile).  Such a launch is only
@@ -77,12 +77,8 @@ int gm_bn_set_concurrency(int n);
  * The engine sets it per process (engine.BalancedStep).  gm_get_residency reads it. */
 int gm_set_residency(int streams, int sharers, int reserved_cus);
 int gm_get_residency(int* streams, int* sharers, int* reserved_cus);
-/* Test hook: `blocks` workgroups of `threads` threads, each holding `lds_bytes` of LDS
- * (up to 160 KiB: one workgroup per CU), spinning for `usec` microseconds (s_sleep +
- * the 100 MHz real-time counter) - a stand-in for a resident collective kernel. */
-int gm_test_hold_cus(int blocks, int threads, int lds_bytes, unsigned usec, void* stream);
 /* 0: always the two-launch path; 1: single launch with register-held strips only;
- * 2 (default): also the streaming single-launch variant.  GM_BN_FUSED at load. */
+ * 2 (default): also the streaming single-launch variant. */
 int gm_bn_set_fused_mode(int mode);
 
 /* ---------------------------------------------------------------------------
@@ -109,9 +105,9 @@ typedef struct gm_spatial_reduce {
 size_t gm_spatial_reduce_scratch(const gm_spatial_reduce* p, int nprob, int B, int dtype, int layout);
 int gm_mmtm_spatial_reduce(const gm_spatial_reduce* p, int nprob, int B, int dtype, int layout,
                            void* scratch, size_t scratch_bytes, void* stream);
-/* A/B knob of the NHWC squeeze: threads per workgroup (256 or 1024; GM_RED_THREADS; negative:
- * nontemporal loads in the bf16 forward, GM_RED_NT) and
- * pixels whose 16-B loads one thread keeps in flight (4, 8 or 16; GM_RED_UNROLL).
+/* A/B knob of the NHWC squeeze: threads per workgroup (256 or 1024; negative:
+ * nontemporal loads in the bf16 forward) and
+ * pixels whose 16-B loads one thread keeps in flight (4, 8 or 16).
  * Process-wide, not thread-safe. */
 int gm_mmtm_set_reduce_form(int threads, int unroll);
 
@@ -350,51 +346,48 @@ int gm_conv2d_dgrad_bf16(const gm_conv_desc* d, const void* dy, const void* wt, 
  * this shape; ws may then be NULL), ZEROED ONCE before first use (the kernel leaves
  * its turnstile words at zero); calls sharing one ws must be stream-ordered. */
 size_t gm_conv2d_splitk_ws_bytes(const gm_conv_desc* d, int dgrad);
-/* Main-loop form of the implicit-GEMM kernel (process-wide; default GM_CONV_PIPE or 0):
+/* Main-loop form of the implicit-GEMM kernel (process-wide; default 0):
  * 0 = two LDS stages drained at every barrier; 2 / 3 = a 2- / 3-stage LDS ring with one
  * barrier per k-tile and counted DMA waits (3: the next tile's DMA stays in flight). */
 int gm_conv_set_pipe(int pipe);
 /* 3x3 / stride-1 / pad-1 convolutions (forward and input gradient, C % 64 == 0) stage
  * the input once per 64-channel chunk as a halo instead of once per tap (default on;
- * GM_CONV_HALO=0 or gm_conv_set_halo(0) selects the im2col kernel for them). */
+ * gm_conv_set_halo(0) selects the im2col kernel for them). */
 int gm_conv_set_halo(int on);
-/* The halo kernel with its nine taps unrolled (k_conv_h9; default on, GM_CONV_H9=0 at
- * load or gm_conv_set_h9(0) selects the run-time-decoded k_conv_halo, an A/B switch). */
+/* The halo kernel with its nine taps unrolled (k_conv_h9; default on,
+ * gm_conv_set_h9(0) selects the run-time-decoded k_conv_halo, an A/B switch). */
 int gm_conv_set_h9(int on);
 /* Split-K target: workgroups wanted from splitting K of 128x128-tile convolutions whose
- * tiles alone do not fill the device (default 384, GM_CONV_SPLITK at load; 0 = never). */
+ * tiles alone do not fill the device (default 384; 0 = never). */
 int gm_conv_set_splitk(int target);
-/* Weight-gradient kernel choice (GM_WGRAD_LOOP at load; default 22): bit 1 = k_wgrad_halo64 (64 x 9 x 64
+/* Weight-gradient kernel choice (default 22): bit 1 = k_wgrad_halo64 (64 x 9 x 64
  * gradient blocks in one workgroup's accumulators, one input row staged per output row, dedicated
  * loader waves) for 3x3 / s1 shapes with 64 channels, bit 2 = also for 128 channels, bit 3 = up to
  * 512; bit 4 = k_wgrad_ring for the other 3x3 shapes with K % 128 == 0 and C a power of two >= 32
  * (loader waves feeding an LDS ring, one workgroup per CU); the rest take k_conv_wgrad4.  Bit 0 is
  * reserved (must be 0). */
 int gm_conv_set_wgrad_loop(int mode);
-/* k_wgrad_ring's staging form (GM_WGRAD_RING at load): 0 (default) = 3 slots of 64 pixels,
- * 1 = 6 slots of 32 pixels. */
-int gm_conv_set_wgrad_ring(int form);
 /* 1x1 / stride-1 / pad-0 forward and input-gradient convolutions as plain NT GEMMs on
  * k_gemm_ring (conv1x1.hip: persistent, loader waves feeding a 4-slot LDS ring; C % 64 == 0 and
- * the output channels % 128 == 0 or == 64).  Default on (GM_CONV1X1=0 at load or
+ * the output channels % 128 == 0 or == 64).  Default on (
  * gm_conv_set_1x1_gemm(0) route them back to the im2col kernels). */
 int gm_conv_set_1x1_gemm(int on);
 /* Weight-gradient operand staging: 0 = LDS-DMA pieces, 1 = register-staged (global_load_dwordx4
  * two steps ahead + ds_write_b128; same LDS image and arithmetic), 2 (default) = register-staged
- * for 1x1 filters, LDS-DMA otherwise.  GM_WGRAD_WR at load. */
+ * for 1x1 filters, LDS-DMA otherwise. */
 int gm_conv_set_wgrad_staging(int wr);
 /* Resident-weight kernel for 3x3 / stride-1 convolutions with 64 -> 64 channels (ResNet
- * layer 1, forward and input gradient; default on, GM_CONV_RW=0 at load or
+ * layer 1, forward and input gradient; default on,
  * gm_conv_set_rw(0) selects the im2col kernel for them). */
 int gm_conv_set_rw(int on);
 /* Dedicated kernel for the pixel-pair stem's forward (8-channel elements -> 64 channels,
  * 7 x 4 filter, strides (2, 1), no padding: weights in VGPRs, two output rows per
- * iteration; default on, GM_CONV_STEM=0 at load or gm_conv_set_stem(0) selects the im2col
+ * iteration; default on, gm_conv_set_stem(0) selects the im2col
  * kernel). */
 int gm_conv_set_stem(int on);
 /* Dedicated kernel for the pixel-pair stem's weight gradient (k_wgrad_stem: one wave per
- * tap row, fp32 partials per workgroup + the split sum; default on, GM_WGRAD_STEM=0 at load
- * or gm_conv_set_wgrad_stem(0) selects k_conv_wgrad4). */
+ * tap row, fp32 partials per workgroup + the split sum; default on,
+ * gm_conv_set_wgrad_stem(0) selects k_conv_wgrad4). */
 int gm_conv_set_wgrad_stem(int on);
 int gm_conv2d_fwd_ex_bf16(const gm_conv_desc* d, const void* x, const void* w, void* y, void* ws,
                           size_t ws_bytes, void* stream);

@@ -517,8 +517,7 @@ def test_wgrad_halo64_vs_fp32(dev, shape):
                                    (5, 128, 9, 11, 128, 2, 2), (2, 32, 7, 5, 128, 1, 2), (1, 512, 7, 7, 512, 1, 2),
                                    (4, 128, 28, 28, 128, 1, 2), (3, 256, 14, 14, 256, 1, 12)],
                          ids=lambda s: "x".join(map(str, s)))
-@pytest.mark.parametrize("form", [0, 1, 3], ids=["bk64", "bk32", "split"])
-def test_wgrad_ring_vs_fp32(dev, shape, form):
+def test_wgrad_ring_vs_fp32(dev, shape):
     """k_wgrad_ring (3x3 weight gradient, 128 x 288 tiles, loader waves feeding a 3-slot LDS ring,
     splits over the pixel steps sized to one workgroup per CU, slabs summed in a fixed order; one
     split writes the gradient directly) against fp32 PyTorch per view group, plain and
@@ -536,7 +535,6 @@ def test_wgrad_ring_vs_fp32(dev, shape, form):
     d = CV._desc_hw(N, H, W, C, K, 3, 3, st, st, 1, 1)
     outs = {}
     try:
-        L.check(lib.gm_conv_set_wgrad_ring(form), "ring form")
         for m in (0, 16):
             L.check(lib.gm_conv_set_wgrad_loop(m), "loop")
             need = lib.gm_conv2d_wgrad_grouped_scratch(ctypes.byref(d), G)
@@ -552,7 +550,6 @@ def test_wgrad_ring_vs_fp32(dev, shape, form):
         torch.cuda.synchronize()
     finally:
         L.check(lib.gm_conv_set_wgrad_loop(WGRAD_LOOP_DEFAULT), "loop")
-        L.check(lib.gm_conv_set_wgrad_ring(0), "ring form")
     for gi in range(G):
         xr = x[gi * N:(gi + 1) * N].float().permute(0, 3, 1, 2)
         gr = dy[gi * N:(gi + 1) * N].float().permute(0, 3, 1, 2)

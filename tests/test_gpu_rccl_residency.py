@@ -73,7 +73,8 @@ def _worker(rank, port, out_dir):
             e0, e_hold, e_work = (torch.cuda.Event(enable_timing=True) for _ in range(3))
             e0.record()
             hs.wait_stream(torch.cuda.current_stream())
-            L.check(lib.gm_test_hold_cus(HOLD_CUS, 256, 160 * 1024, HOLD_US, hs.cuda_stream), "gm_test_hold_cus")
+            import testkit
+            testkit.hold_cus(HOLD_CUS, 256, 160 * 1024, HOLD_US, hs.cuda_stream)
             e_hold.record(hs)
             torch.cuda._sleep(2_000_000)  # the holding workgroups land first
         out = [st(xs[i % 2], ys[i % 2]) for i in range(3, 7)]

@@ -58,7 +58,8 @@ def test_spin_launches_beside_a_cu_holding_kernel(lib):
     e_work = torch.cuda.Event(enable_timing=True)
     e0.record()
     hold.wait_stream(torch.cuda.current_stream())
-    L.check(L.load().gm_test_hold_cus(HOLD_CUS, 256, 160 * 1024, HOLD_US, hold.cuda_stream), "gm_test_hold_cus")
+    import testkit
+    testkit.hold_cus(HOLD_CUS, 256, 160 * 1024, HOLD_US, hold.cuda_stream)
     e_hold.record(hold)
     torch.cuda._sleep(2_000_000)  # let the holding workgroups land first
     out = work()

@@ -203,7 +203,7 @@ def test_model_stacked_vs_per_view(dev, kind):
     # two-kernel BatchNorm (gm_bn_set_fused_mode(0): its partition depends on (M, C) alone,
     # where the single-launch one sizes its grid for the launch's view groups and the
     # residency plan) and d takes the BatchNorm statistics from that reduction instead of
-    # the convolution epilogue (GM_EPI_BN_STATS=0; the epilogue statistics differ from it
+    # the convolution epilogue (vtrunk.EPI_BN_STATS = False; the epilogue statistics differ from it
     # by summation order only: test_gpu_bn_epi.py)
     from greedy_multimodal_learning_amd import _lib as L
     lib = L.load()

@@ -21,7 +21,6 @@ def main():
     ap.add_argument("--op", default="fwd", choices=["fwd", "dgrad", "wgrad"])
     ap.add_argument("--groups", type=int, default=2, help="wgrad: views per grouped launch")
     ap.add_argument("--ring", type=int, default=None, help="wgrad: gm_conv_set_wgrad_loop mode")
-    ap.add_argument("--form", type=int, default=None, help="wgrad: gm_conv_set_wgrad_ring form")
     ap.add_argument("--pipe", type=int, default=0)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--reps", type=int, default=50)
@@ -47,8 +46,6 @@ def main():
     if a.op == "wgrad":  # the step's grouped launch (both views), as tools/trunk_table.py builds it
         if a.ring is not None:
             L.check(L.load().gm_conv_set_wgrad_loop(a.ring), "ring")
-        if a.form is not None:
-            L.check(L.load().gm_conv_set_wgrad_ring(a.form), "ring form")
         fn = T._make_bf16("wgrad", B, dev, C, H, W, K, R, st, pad, P, Q, a.groups)
         B = B * a.groups
     t = T._time(fn, a.reps)

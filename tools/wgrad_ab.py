@@ -31,13 +31,11 @@ def main():
     from greedy_multimodal_learning_amd import _lib as L
     lib = L.load()
     dev = torch.device("cuda:0")
-    # a mode is LOOP or LOOP/FORM (gm_conv_set_wgrad_loop, gm_conv_set_wgrad_ring)
+    # a mode is a gm_conv_set_wgrad_loop value
     modes = a.modes.replace(":", ",").split(",")
 
     def set_mode(m):
-        loop, _, form = m.partition("/")
-        L.check(lib.gm_conv_set_wgrad_loop(int(loop)), "loop")
-        L.check(lib.gm_conv_set_wgrad_ring(int(form or 0)), "ring")
+        L.check(lib.gm_conv_set_wgrad_loop(int(m)), "loop")
     trunk = dict(T.TRUNKS[a.arch])
     B, G = a.batch, a.groups
     print(f"{a.arch} wgrad, G={G}, B={B}, modes {modes}, {a.rounds} rounds x {a.reps} reps", flush=True)
