@@ -102,14 +102,17 @@ class _Flags:
 
 class FlatParams:
     """All parameters of `model` as views of ONE flat fp32 buffer and their
-    gradients as views of a second one (same offsets), in reverse registration
-    order (~ the order backward produces gradients).  Conv weights keep the
-    model's memory format (KRSC when channels_last)."""
+    gradients as views of a second one (same offsets), in the order backward produces
+    the gradients (model.grad_order(), else reverse registration order).  Conv weights
+    keep the model's memory format (KRSC when channels_last)."""
 
     def __init__(self, model, channels_last=False):
         self.device = next(model.parameters()).device
-        named = list(model.named_parameters())
-        params = [p for _, p in named][::-1]
+        order = getattr(model, "grad_order", None)
+        # the model's backward-production order when it states one (model.grad_order: views
+        # interleaved per layer), else reverse registration order
+        params = list(order()) if callable(order) else [p for _, p in model.named_parameters()][::-1]
+        assert len(params) == len(list(model.parameters())), "grad_order must list every parameter once"
         total = sum(p.numel() for p in params)
         self.param = torch.empty(total, device=self.device, dtype=torch.float32)
         self.grad = torch.zeros(total, device=self.device, dtype=torch.float32)

@@ -27,6 +27,43 @@ CLASSNAMES = ['airplane', 'bathtub', 'bed', 'bench', 'bookshelf', 'bottle', 'bow
               'stool', 'table', 'tent', 'toilet', 'tv_stand', 'vase', 'wardrobe', 'xbox']
 
 
+def grad_order(model):
+    """The model's parameters in the order the view-batched backward produces their gradients:
+    the heads (`net_view_*.fc`), the MMTM site after layer 4, layer 4 of every view, the site
+    after layer 3, layer 3, ..., layer 1, the stems.  Inside a stage: reversed registration order
+    of the per-view name, views interleaved (the grouped launches write every view's gradient of
+    a layer together).  The engine lays its flat gradient buffer out in this order, so each
+    data-parallel all-reduce bucket (a contiguous slice) completes as early as backward allows -
+    with the reverse registration order, net_view_1's whole trunk sat between net_view_0's layer-4
+    and stem gradients, and half of C2's 95 MB could only be reduced after the stem."""
+    named = list(model.named_parameters())
+
+    def split(n):
+        head, _, rest = n.partition(".")
+        if head.startswith("net_view_") and head[9:].isdigit():
+            return int(head[9:]), rest
+        return -1, n
+
+    def stage(n):
+        v, rest = split(n)
+        if v >= 0:
+            sub = rest.split(".")[0]
+            if sub == "fc":
+                return 100
+            if sub.startswith("layer") and sub[5:].isdigit():
+                return 10 * int(sub[5:])
+            return 0  # stem: conv1, bn1
+        head = n.split(".")[0]
+        if head.startswith("mmtm") and head[4:].isdigit():
+            return 10 * int(head[4:]) + 5
+        return 100
+    first = {}  # per-view name -> its registration index within the view (or the global index)
+    for i, (n, _) in enumerate(named):
+        first.setdefault(split(n)[1], i)
+    keyed = sorted(named, key=lambda np_: (-stage(np_[0]), -first[split(np_[0])[1]], split(np_[0])[0]))
+    return [p for _, p in keyed]
+
+
 @configurable
 class MMTM_MVCNN(nn.Module):
     def __init__(self, nclasses=40, num_views=2, pretraining=False, mmtm_off=False,
@@ -97,6 +134,10 @@ class MMTM_MVCNN(nn.Module):
             x0, x1 = self._head(nets[0], X[:B]), self._head(nets[1], X[B:])
         mean = None if getattr(self, "_no_mean", False) else (x0 + x1) / 2
         return mean, [x0, x1], scales, squeezed
+
+    def grad_order(self):
+        """Parameters in backward-production order (module function grad_order)."""
+        return grad_order(self)
 
     def forward(self, x, curation_mode=False, caring_modality=None):
         if vtrunk.usable(self, [self.net_view_0, self.net_view_1], x):
@@ -195,6 +236,10 @@ class MMTM_MVCNN_N(nn.Module):
             outs = [MMTM_MVCNN._head(n, X[i * B:(i + 1) * B]) for i, n in enumerate(nets)]
         mean = None if getattr(self, "_no_mean", False) else sum(outs) / len(outs)
         return mean, outs, scales, squeezed
+
+    def grad_order(self):
+        """Parameters in backward-production order (module function grad_order)."""
+        return grad_order(self)
 
     def forward(self, x, curation_mode=False, caring_modality=None):
         nets = [getattr(self, f"net_view_{i}") for i in range(self.num_views)]

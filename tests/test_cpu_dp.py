@@ -65,3 +65,33 @@ def test_dp_gloo_world2_matches_mean_of_shards(golden, tmp_path, bucket_mb):
     np.testing.assert_allclose(g0, fix["ddp/gn"], rtol=2e-4, atol=1e-9)
     nb = int(np.load(tmp_path / "nb_0.npy"))
     assert nb >= (20 if bucket_mb == 2.0 else 4)
+
+
+def test_flat_layout_follows_backward_order():
+    """The flat gradient buffer (engine.FlatParams) is laid out in the order the view-batched
+    backward produces gradients (model.grad_order): heads, MMTM site 4, layer 4 of every view,
+    site 3, layer 3, ... stems - so every all-reduce bucket but the last completes before the
+    stem's backward (with reverse registration order net_view_1's whole trunk sat between
+    net_view_0's layer-4 and stem gradients)."""
+    from greedy_multimodal_learning_amd import engine as E
+    from greedy_multimodal_learning_amd.model import MMTM_MVCNN, MMTM_MVCNN_N
+
+    def stage(n):
+        head, _, rest = n.partition(".")
+        if head.startswith("net_view_"):
+            sub = rest.split(".")[0]
+            return 100 if sub == "fc" else (10 * int(sub[5:]) if sub.startswith("layer") else 0)
+        return 10 * int(head[4:]) + 5
+
+    for m in (MMTM_MVCNN(), MMTM_MVCNN_N(num_views=4, trunk="resnet18")):
+        fp = E.FlatParams(m)
+        names = {id(p): n for n, p in m.named_parameters()}
+        order = [names[id(p)] for p, _ in sorted(fp.slices.items(), key=lambda kv: kv[1][0])]
+        assert sorted(order) == sorted(names.values())
+        st = [stage(n) for n in order]
+        assert st == sorted(st, reverse=True), "stages out of backward order"
+        b = E.GradBuckets(fp, None, bucket_mb=25.0)
+        last = b.buckets[-1]
+        early = [names[id(p)] for s, e, ps in b.buckets[:-1] for p in ps]
+        assert not any(stage(n) in (0, 10) for n in early), "a bucket before the last waits for layer 1 / stem"
+        assert sum(e - s for s, e, _ in b.buckets[:-1]) > 0.85 * fp.total
