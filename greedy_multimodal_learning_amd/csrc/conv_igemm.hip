@@ -968,7 +968,6 @@ __device__ __forceinline__ bf16x8 lds_rd128(unsigned addr) {
 
 struct HaloArgs {
     int halo_bytes;           // LDS bytes of the halo region (multiple of 1 KB)
-    int diag;                 // DIAG
     FastDiv fd_w2, fd_h1;     // W + 2, H + 1
 };
 
@@ -1483,7 +1482,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_h9(ConvArgs a, HaloArgs h) {
             const int ahead = min(NB - 2, nkt - 1 - kt);
             wait_vm(ahead * BR);
             __builtin_amdgcn_s_barrier();
-            if (tp == 0 && cc > c0 && !h.diag) {  // every wave is done with the previous chunk's halo
+            if (tp == 0 && cc > c0) {  // every wave is done with the previous chunk's halo
                 issue_halo(cc);
                 wait_vm(0);
                 __builtin_amdgcn_s_barrier();
@@ -2332,7 +2331,6 @@ static int launch_halo_v(ConvArgs& a, int hb, hipStream_t st) {
     if (a.splits < 1) a.splits = 1;
     HaloArgs h;
     h.halo_bytes = hb;
-    h.diag = conv_pipe() == 7;
     h.fd_w2 = FastDiv((uint32_t)(a.Wi + 2));
     h.fd_h1 = FastDiv((uint32_t)(a.Hi + 1));
     const size_t lds = (size_t)hb * (BM == 256 ? 2 : 1) + NB * (size_t)BN * 128;
@@ -2471,7 +2469,6 @@ static int launch_h9(ConvArgs& a, int hb, hipStream_t st) {
     if (a.splits < 1) a.splits = 1;
     HaloArgs h;
     h.halo_bytes = hb;
-    h.diag = conv_pipe() == 7;
     h.fd_w2 = FastDiv((uint32_t)(a.Wi + 2));
     h.fd_h1 = FastDiv((uint32_t)(a.Hi + 1));
     const size_t lds = (size_t)hb + NB * (size_t)BN * 128;
@@ -2526,7 +2523,7 @@ static int try_h9(ConvArgs& a, int hb, hipStream_t st) {
 template <int BN>
 static int launch_halo(ConvArgs& a, int hb, hipStream_t st) {
     const int p = conv_pipe();
-    if (p == 0 || p == 3 || p == 7) {
+    if (p == 0 || p == 3) {
         const int r = try_h9<BN>(a, hb, st);
         if (r == 1) return GM_OK;
         if (r != 0) return r;
@@ -2858,7 +2855,7 @@ extern "C" int gm_conv_set_rw(int on) {
 }
 
 extern "C" int gm_conv_set_pipe(int pipe) {
-    GM_REQUIRE(pipe == 0 || pipe == 2 || pipe == 3 || pipe == 7, "gm_conv_set_pipe: 0, 2 or 3");
+    GM_REQUIRE(pipe == 0 || pipe == 2 || pipe == 3, "gm_conv_set_pipe: 0, 2 or 3");
     g_conv_pipe = pipe;
     return GM_OK;
 }

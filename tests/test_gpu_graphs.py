@@ -241,37 +241,38 @@ def test_failed_capture_then_recapture():
         torch.testing.assert_close(sg[k], se[k], rtol=1e-6, atol=1e-6, msg=k)
 
 
-def test_released_pool_capture_leaves_generator_usable():
-    """The round-5 cause, reproduced: a capture into a private pool whose graphs were all
-    destroyed is refused inside capture_begin, after torch put the default generator into its
-    capture state.  streams.release_rng_capture_state (which the engine runs after every failed
-    capture) takes it out again; the default generator then works eagerly."""
+def test_invalidated_capture_leaves_generator_usable():
+    """The round-5 failure mechanism, reproduced: a capture that fails after torch put the default
+    CUDA generator into its capture state (capture_begin's prologue) - here a stream synchronize
+    inside the capture invalidates it, so capture_end's hipStreamEndCapture fails before the
+    epilogue - leaves the generator "capturing", and the next eager random op raises "Offset
+    increment outside graph capture encountered unexpectedly" (test_xent_bad_label_is_nan's
+    "RuntimeError: Off..." in round 5).  streams.release_rng_capture_state, which the engine runs
+    after every failed capture, takes it out again."""
     from greedy_multimodal_learning_amd.streams import release_rng_capture_state
     dev = torch.device("cuda:0")
     s = torch.cuda.Stream(device=dev)
-    pool = torch.cuda.graph_pool_handle()
     t = torch.zeros(4, device=dev)
-    g1 = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g1, pool=pool, stream=s):
-        t.add_(1)
-    g1.replay()
     torch.cuda.synchronize()
-    del g1  # releases the pool
-    refused, stuck = None, None
-    g2 = torch.cuda.CUDAGraph()
+    failed = None
+    g = torch.cuda.CUDAGraph()
     try:
-        with torch.cuda.graph(g2, pool=pool, stream=s):
+        with torch.cuda.graph(g, stream=s):
             t.add_(1)
+            s.synchronize()  # not capturable: invalidates the capture
     except RuntimeError as e:
-        refused = str(e).splitlines()[0][:160]
-    del g2
+        failed = str(e).splitlines()[0][:160]
+    del g
     torch.cuda.synchronize()
     state = torch.cuda.get_rng_state()
+    stuck = None
     try:
         torch.empty(1, device=dev).uniform_()
     except RuntimeError as e:
         stuck = str(e).splitlines()[0][:160]
-    print(f"released-pool capture refused: {refused!r}; eager RNG afterwards: {stuck!r}")
+    print(f"invalidated capture: {failed!r}; eager RNG afterwards: {stuck!r}")
     release_rng_capture_state(dev)
     torch.empty(1, device=dev).uniform_()
     torch.cuda.set_rng_state(state)
+    if failed is not None:
+        assert stuck is not None and stuck.startswith("Off"), "torch no longer leaves the generator capturing"
