@@ -182,7 +182,7 @@ struct GemmForm { int nw, u; };
 // forms 4 / 5: timing diagnostics of form 1 (outputs meaningless): arguments and one
 // store only / everything but the operand loads and MFMAs
 constexpr GemmForm kForms[] = {{4, 8}, {4, 16}, {8, 16}, {16, 8}};
-static int g_gemm_form = 1, g_gemm_vec = 1;
+static int g_gemm_form = 1, g_gemm_vec = 1, g_gemm_outer = 1;
 
 // The MMTM GEMMs are dependent-latency chains (kernel arguments -> operand loads ->
 // MFMAs -> epilogue loads -> store), not MFMA work: every round trip costs ~1-2 us.  So
@@ -251,12 +251,157 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_f32(GemmArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------------
+// Outer-product shapes: K <= 128 with a large M x N output - the MMTM weight gradients at C5
+// (fc_squeeze: dW[2048][24576] = dz^T[2048][32] . sq[32][24576], 201 MB of fp32 output written,
+// and read back when accumulating).  k_gemm_f32 gives each wave one 16 x 16 tile and its
+// epilogue stores 64-B row segments: 0.5 TB/s on that shape (407 us).  Here a 256-thread
+// workgroup owns a 64 x 256 output tile; every thread keeps 8 rows x 8 columns (two float4
+// column chunks 128 floats apart, so a wave's stores are whole 512-B row segments) in registers
+// and runs an in-order fmaf chain over k, its operands loaded straight from global memory as
+// float4s (A: the 8 rows of the thread's row group - the same address across the 32 lanes of
+// the group; B: the thread's 8 columns), 4 k-steps in flight.  No LDS: the kernel runs beside
+// the weight-gradient stream's one-workgroup-per-CU 156 KB ring kernels, which an LDS-staged
+// form (40 KB per workgroup) kept off the CUs - C5 +0.5 ms/step in an A/B although its own
+// launches were faster.  Bound: the output write (+ read when accumulating).
+constexpr int kOM = 64, kON = 256, kOU = 4;
+
+struct OuterArgs {
+    gm_gemm p[kMaxGemm];
+    int tiles_m[kMaxGemm];
+    int tile_start[kMaxGemm + 1];
+};
+
+__global__ __launch_bounds__(256) void k_gemm_outer(OuterArgs a) {
+    const int pi = blockIdx.y;
+    const gm_gemm& p = a.p[pi];
+    const int wg = blockIdx.x;
+    if (wg >= a.tile_start[pi + 1] - a.tile_start[pi]) return;
+    const int tm = wg % a.tiles_m[pi], tn = wg / a.tiles_m[pi];  // tm fastest: neighbours share B
+    const int t = threadIdx.x, cg = t & 31, rg = t >> 5;
+    const int m0 = tm * kOM + 8 * rg, n0 = tn * kON + 4 * cg;
+    const int K = p.K[0];
+    // A[m][k] = A.ptr[m + k * ld1] (ld0 == 1), B[k][n] = B.ptr[k * ld0 + n] (ld1 == 1); rows / columns
+    // past M / N read a clamped in-range float4 and are never stored
+    const float* pa = p.A[0].ptr + min(m0, p.M - 8);
+    const long sa = p.A[0].ld1;
+    const float* pb0 = p.B[0].ptr + min(n0, p.N - 4);
+    const float* pb1 = p.B[0].ptr + min(n0 + 128, p.N - 4);
+    const long sb = p.B[0].ld0;
+    float acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = 0.f;
+    auto fma8 = [&](const float4& a0, const float4& a1, const float4& b0, const float4& b1) __attribute__((always_inline)) {
+        const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[i][j] = fmaf(av[i], bv[j], acc[i][j]);
+    };
+    int k = 0;
+    for (; k + kOU <= K; k += kOU) {  // kOU k-steps' loads in flight, then their FMAs in k order
+        float4 a0[kOU], a1[kOU], b0[kOU], b1[kOU];
+#pragma unroll
+        for (int u = 0; u < kOU; ++u) {
+            const long ka = (long)(k + u) * sa, kb = (long)(k + u) * sb;
+            a0[u] = *reinterpret_cast<const float4*>(pa + ka);
+            a1[u] = *reinterpret_cast<const float4*>(pa + ka + 4);
+            b0[u] = *reinterpret_cast<const float4*>(pb0 + kb);
+            b1[u] = *reinterpret_cast<const float4*>(pb1 + kb);
+        }
+#pragma unroll
+        for (int u = 0; u < kOU; ++u) fma8(a0[u], a1[u], b0[u], b1[u]);
+    }
+    for (; k < K; ++k) {
+        const float4 a0 = *reinterpret_cast<const float4*>(pa + (long)k * sa);
+        const float4 a1 = *reinterpret_cast<const float4*>(pa + (long)k * sa + 4);
+        const float4 b0 = *reinterpret_cast<const float4*>(pb0 + (long)k * sb);
+        const float4 b1 = *reinterpret_cast<const float4*>(pb1 + (long)k * sb);
+        fma8(a0, a1, b0, b1);
+    }
+    // the clamped rows / columns: the thread's registers hold rows min(m0, M - 8) + i and columns
+    // min(n0, N - 4) + j; store only the thread's own in-range outputs
+    const int mb = min(m0, p.M - 8), nb0 = min(n0, p.N - 4), nb1 = min(n0 + 128, p.N - 4);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int m = mb + i;
+        if (m < m0 || m >= m0 + 8) continue;  // (a clamped row group: rows another group owns)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int nb = h ? nb1 : nb0, n = n0 + 128 * h;
+            if (n >= p.N) continue;
+            float* c = p.C + (size_t)m * p.ld_c + nb;
+            float4 v = make_float4(acc[i][4 * h], acc[i][4 * h + 1], acc[i][4 * h + 2], acc[i][4 * h + 3]);
+            if (nb == n) {  // a whole float4 chunk of this thread
+                if (p.accumulate) {
+                    const float4 o = *reinterpret_cast<const float4*>(c);
+                    v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+                }
+                *reinterpret_cast<float4*>(c) = v;
+            } else {  // the last, clamped chunk: columns nb + q >= n are this thread's
+                const float vv[4] = {v.x, v.y, v.z, v.w};
+                for (int q = n - nb; q < 4; ++q) c[q] = (p.accumulate ? c[q] : 0.f) + vv[q];
+            }
+        }
+    }
+}
+
+// a problem the outer-product kernel takes: one K segment of at most 128, a large output, no
+// bias / activation / mask, row-contiguous operands (A[m][k] = A[m + k ld1], B[k][n] = B[k ld0 + n]),
+// M >= 8 and N >= 4, float4-aligned operand rows and C rows
+static bool outer_ok(const gm_gemm& p) {
+    const gm_operand& A = p.A[0];
+    const gm_operand& B = p.B[0];
+    return p.K[1] == 0 && p.K[0] >= 1 && p.K[0] <= 128 && (long long)p.M * p.N >= (1ll << 20) && p.M >= 8 &&
+           p.N >= 4 && !p.bias && !p.mask && p.act == 0 && A.ptr && A.ld0 == 1 && (A.ld1 & 3) == 0 &&
+           ((uintptr_t)A.ptr & 15) == 0 && B.ld1 == 1 && (B.ld0 & 3) == 0 && ((uintptr_t)B.ptr & 15) == 0 &&
+           (p.ld_c & 3) == 0 && ((uintptr_t)p.C & 15) == 0;
+}
+
 }  // namespace gm
 
 using namespace gm;
 
+static int launch_gemm_f32(const gm_gemm* in, int nprob, hipStream_t st);
+
 extern "C" int gm_gemm_f32(const gm_gemm* in, int nprob, void* stream) {
     GM_REQUIRE(in && nprob >= 1 && nprob <= kMaxGemm, "gemm_f32: nprob must be 1..%d", kMaxGemm);
+    hipStream_t st = as_stream(stream);
+    // the outer-product problems (k_gemm_outer) and the rest (k_gemm_f32): independent problems,
+    // two launches on one stream
+    gm_gemm rest[kMaxGemm];
+    int nrest = 0;
+    OuterArgs o;
+    memset(&o, 0, sizeof(o));
+    int nout = 0, maxt = 0;
+    for (int i = 0; i < nprob; ++i) {
+        const gm_gemm& p = in[i];
+        if (g_gemm_outer && p.M >= 1 && p.N >= 1 && p.C && p.ld_c >= p.N && p.A[0].ptr && p.B[0].ptr && outer_ok(p)) {
+            o.p[nout] = p;
+            o.tiles_m[nout] = (p.M + kOM - 1) / kOM;
+            const int t = o.tiles_m[nout] * ((p.N + kON - 1) / kON);
+            o.tile_start[nout + 1] = o.tile_start[nout] + t;
+            maxt = t > maxt ? t : maxt;
+            ++nout;
+        } else {
+            rest[nrest++] = p;
+        }
+    }
+    if (nrest) {
+        const int rc = launch_gemm_f32(rest, nrest, st);
+        if (rc) return rc;
+    }
+    if (nout) {
+        k_gemm_outer<<<dim3(maxt, nout), 256, 0, st>>>(o);
+        return check_launch("k_gemm_outer");
+    }
+    return GM_OK;
+}
+
+static int launch_gemm_f32(const gm_gemm* in, int nprob, hipStream_t st) {
     GemmArgs a;
     memset(&a, 0, sizeof(a));
     a.nprob = nprob;
@@ -295,7 +440,6 @@ extern "C" int gm_gemm_f32(const gm_gemm* in, int nprob, void* stream) {
     a.tile_start[nprob] = tiles;
     a.vec = g_gemm_vec;
     const dim3 grid(maxt, nprob);
-    hipStream_t st = as_stream(stream);
     switch (g_gemm_form) {
         case 0: k_gemm_f32<4, 8><<<grid, 256, 0, st>>>(a); break;
         case 1: k_gemm_f32<4, 16><<<grid, 256, 0, st>>>(a); break;
@@ -306,7 +450,8 @@ extern "C" int gm_gemm_f32(const gm_gemm* in, int nprob, void* stream) {
 }
 
 extern "C" int gm_gemm_set_form(int form) {
-    g_gemm_vec = !(form & 256);  // bit 8: scalar k-steps only
+    g_gemm_vec = !(form & 256);    // bit 8: scalar k-steps only
+    g_gemm_outer = !(form & 512);  // bit 9: no outer-product kernel (every problem on k_gemm_f32)
     form &= 255;
     GM_REQUIRE(form >= 0 && form < (int)(sizeof(kForms) / sizeof(kForms[0])), "gemm form must be 0..3 (got %d)",
                form);

@@ -616,7 +616,10 @@ class BalancedStep:
                     entry, err = None, e
                     self.capture_failures.append(str(e))
                     capture_dropped()  # (scratch grown in the failed capture was never zeroed)
-                    release_rng_capture_state(self.device)
+                    try:
+                        release_rng_capture_state(self.device)
+                    except RuntimeError as e2:  # best effort: the fallback below still runs
+                        self.capture_failures.append(f"release_rng_capture_state: {e2}")
                 if self.buckets is not None and self.world > 1 and not self._agree(entry is not None):
                     # every rank takes the same fallback, so the ranks' collective sequences
                     # stay identical (a rank replaying in-graph collectives beside one that

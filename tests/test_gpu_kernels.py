@@ -54,6 +54,38 @@ def test_gemm_segments_strides_ones_mask_accumulate(dev):
     np.testing.assert_allclose(out.cpu().numpy()[0], mask.sum(0).numpy(), rtol=1e-6)
 
 
+@pytest.mark.parametrize("M,N,K,acc", [(2048, 24576, 32, 1), (300, 5000, 32, 0), (1004, 1028, 100, 1),
+                                       (64, 16384, 7, 0), (1000, 1027, 100, 1)])
+def test_gemm_outer_product_shapes(dev, M, N, K, acc):
+    """The outer-product kernel (k_gemm_outer: K <= 128, M x N >= 2^20 - the C5 MMTM weight
+    gradients, fc_squeeze's dW[2048][24576] = dz^T . sq at K = B = 32) against fp64, with the
+    strided A^T operand the MMTM backward passes (Op(dz, 1, M)), accumulating into C, ragged
+    edges (a partial row group, a partial column chunk), a K tail, and a shape whose unaligned
+    rows fall back to k_gemm_f32; equal within fp32 summation order to k_gemm_f32 (form bit 9)."""
+    from greedy_multimodal_learning_amd import _lib as L
+    from greedy_multimodal_learning_amd import ops
+    from greedy_multimodal_learning_amd.ops import Op
+    g = torch.Generator().manual_seed(M + N + K)
+    dz = torch.randn(K, M, generator=g)        # the GEMM's A = dz^T (A[m, k] = dz[k, m])
+    sq = torch.randn(K, N, generator=g)
+    c0 = torch.randn(M, N, generator=g) if acc else torch.zeros(M, N)
+    ref = c0.double() + dz.double().T @ sq.double()
+    outs = []
+    try:
+        for form in (1, 1 | 512):
+            L.check(L.load().gm_gemm_set_form(form), "gemm form")
+            C = c0.to(dev).contiguous()
+            ops.gemm([dict(M=M, N=N, segs=[(K, Op(dz.to(dev), 1, M), Op(sq.to(dev), N, 1))], C=C, ld_c=N,
+                           accumulate=acc)], dev)
+            outs.append(C.cpu())
+    finally:
+        L.check(L.load().gm_gemm_set_form(1), "gemm form")
+    scale = float(ref.abs().max())
+    for o in outs:
+        assert float((o.double() - ref).abs().max()) <= 1e-5 * scale
+    assert float((outs[0] - outs[1]).abs().max()) <= 1e-5 * scale
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("layout", ["nchw", "nhwc"])
 @pytest.mark.parametrize("B,C,H,W", [(2, 128, 28, 28), (3, 256, 14, 14), (64, 512, 7, 7),

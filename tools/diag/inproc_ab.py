@@ -1,0 +1,50 @@
+"""Interleaved in-process A/B on the bench (one box, one process, alternating arms):
+
+    python tools/diag/inproc_ab.py ARMSET ROUNDS [bench args ...]
+
+ARMSET: layout      - flat parameter layout: model.grad_order vs reverse registration order
+        gemm_outer  - the outer-product GEMM kernel on vs off (gm_gemm_set_form bit 9)
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+
+
+def arms(name):
+    from greedy_multimodal_learning_amd import _lib as L
+    from greedy_multimodal_learning_amd import model as M
+    if name == "layout":
+        orig = {c: c.grad_order for c in (M.MMTM_MVCNN, M.MMTM_MVCNN_N)}
+
+        def setl(on):
+            for c, f in orig.items():
+                if on:
+                    c.grad_order = f
+                elif hasattr(c, "grad_order"):
+                    del c.grad_order
+        return [("grad_order", lambda: setl(True)), ("reverse_registration", lambda: setl(False))]
+    if name == "gemm_outer":
+        def setg(form):
+            L.check(L.load().gm_gemm_set_form(form), "gemm form")
+        return [("outer_on", lambda: setg(1)), ("outer_off", lambda: setg(1 | 512))]
+    raise SystemExit(f"unknown arm set {name}")
+
+
+def main():
+    name, rounds = sys.argv[1], int(sys.argv[2])
+    extra = sys.argv[3:] or ["--no-cpu-baseline", "--steps", "40"]
+    import bench
+    sets = arms(name)
+    for r in range(rounds):
+        for arm, apply in sets:
+            apply()
+            print(f"round {r} {arm}", flush=True)
+            sys.argv = ["bench.py"] + extra
+            bench.main()
+    sets[0][1]()
+
+
+if __name__ == "__main__":
+    main()
