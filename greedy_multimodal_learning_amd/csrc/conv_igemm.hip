@@ -2125,11 +2125,11 @@ static bool lean_path() {
 static bool grid_ok(const ConvCls& c, int S);
 static void pack_grid(ConvCls& c, int S);
 
-// main-loop form of the lean kernel (k_conv_igemm_ut PIPE);
-// gm_conv_set_pipe() at run time (A/B in one process)
-static int g_conv_pipe = [] {
-    return 0;
-}();
+// main-loop form of the lean kernel (k_conv_igemm_ut PIPE); gm_conv_set_pipe() at run time (A/B in
+// one process).  -1 (default): PIPE 2 - one raw barrier per k-tile with a counted wait - which
+// measured 2-6 % faster than PIPE 0 on the strided first convolutions of layers 2-4 as the step
+// launches them (r06, profiles/r06_strided_ab.txt); the halo kernels stay eligible
+static int g_conv_pipe = -1;
 static int conv_pipe() { return g_conv_pipe; }
 
 template <int BM, int BN, int PIPE>
@@ -2172,7 +2172,7 @@ static int launch_igemm(ConvArgs& a, hipStream_t st) {
     bool grid = true;
     for (int i = 0; i < a.ncls; ++i) grid = grid && grid_ok(a.cls[i], a.Sw);
     if (a.C >= 64 && grid && lean_path()) {
-        const int pipe = conv_pipe();
+        const int pipe = conv_pipe() < 0 ? 2 : conv_pipe();
         if (pipe == 3) launch_ut<BM, BN, 3>(a, tiles * a.splits, st);
         else if (pipe == 2) launch_ut<BM, BN, 2>(a, tiles * a.splits, st);
         else launch_ut<BM, BN, 0>(a, tiles * a.splits, st);
@@ -2523,7 +2523,7 @@ static int try_h9(ConvArgs& a, int hb, hipStream_t st) {
 template <int BN>
 static int launch_halo(ConvArgs& a, int hb, hipStream_t st) {
     const int p = conv_pipe();
-    if (p == 0 || p == 3) {
+    if (p <= 0 || p == 3) {
         const int r = try_h9<BN>(a, hb, st);
         if (r == 1) return GM_OK;
         if (r != 0) return r;
@@ -2855,7 +2855,7 @@ extern "C" int gm_conv_set_rw(int on) {
 }
 
 extern "C" int gm_conv_set_pipe(int pipe) {
-    GM_REQUIRE(pipe == 0 || pipe == 2 || pipe == 3, "gm_conv_set_pipe: 0, 2 or 3");
+    GM_REQUIRE(pipe == -1 || pipe == 0 || pipe == 2 || pipe == 3, "gm_conv_set_pipe: -1 (default), 0, 2 or 3");
     g_conv_pipe = pipe;
     return GM_OK;
 }

@@ -346,7 +346,7 @@ int gm_conv2d_dgrad_bf16(const gm_conv_desc* d, const void* dy, const void* wt, 
  * this shape; ws may then be NULL), ZEROED ONCE before first use (the kernel leaves
  * its turnstile words at zero); calls sharing one ws must be stream-ordered. */
 size_t gm_conv2d_splitk_ws_bytes(const gm_conv_desc* d, int dgrad);
-/* Main-loop form of the implicit-GEMM kernel (process-wide; default 0):
+/* Main-loop form of the implicit-GEMM kernel (process-wide): -1 (default) = 2;
  * 0 = two LDS stages drained at every barrier; 2 / 3 = a 2- / 3-stage LDS ring with one
  * barrier per k-tile and counted DMA waits (3: the next tile's DMA stays in flight). */
 int gm_conv_set_pipe(int pipe);

@@ -21,7 +21,7 @@ def main():
     ap.add_argument("--op", default="fwd", choices=["fwd", "dgrad", "wgrad"])
     ap.add_argument("--groups", type=int, default=2, help="wgrad: views per grouped launch")
     ap.add_argument("--ring", type=int, default=None, help="wgrad: gm_conv_set_wgrad_loop mode")
-    ap.add_argument("--pipe", type=int, default=0)
+    ap.add_argument("--pipe", type=int, default=-1)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--sets", type=int, default=1, help="grouped stem/wgrad: distinct operand sets cycled")

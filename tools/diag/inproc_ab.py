@@ -4,6 +4,7 @@
 
 ARMSET: layout      - flat parameter layout: model.grad_order vs reverse registration order
         gemm_outer  - the outer-product GEMM kernel on vs off (gm_gemm_set_form bit 9)
+        pipe        - k_conv_igemm_ut main loop: PIPE 2 (default) vs PIPE 0 (gm_conv_set_pipe)
 """
 import os
 import sys
@@ -29,6 +30,10 @@ def arms(name):
         def setg(form):
             L.check(L.load().gm_gemm_set_form(form), "gemm form")
         return [("outer_on", lambda: setg(1)), ("outer_off", lambda: setg(1 | 512))]
+    if name == "pipe":
+        def setp(p):
+            L.check(L.load().gm_conv_set_pipe(p), "pipe")
+        return [("pipe2", lambda: setp(-1)), ("pipe0", lambda: setp(0))]
     raise SystemExit(f"unknown arm set {name}")
 
 
