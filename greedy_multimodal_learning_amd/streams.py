@@ -103,20 +103,25 @@ def capture_replayed():
     _grown_in_capture.clear()
 
 
+_repair_stream = {}
+
+
 def release_rng_capture_state(device):
     """After a failed capture, end the default generator's capture state.
 
     torch.cuda.CUDAGraph.capture_begin puts the default CUDA generator into its capture state
     (capture_prologue) BEFORE it asks the allocator for the private pool and begins the stream
     capture, and only capture_end's epilogue takes it out again - after hipStreamEndCapture
-    succeeded.  A capture refused in capture_begin (e.g. a released private pool) or invalidated
-    in its body therefore leaves the generator believing it is captured, and the next eager
+    succeeded.  A capture refused in capture_begin after the prologue, or invalidated in its body,
+    therefore leaves the generator believing it is captured, and the next eager
     random op anywhere in the process raises "Offset increment outside graph capture
     encountered unexpectedly" (the round-5 test_xent_bad_label_is_nan failure).  One complete
     capture of a trivial kernel on a private stream runs prologue + epilogue and restores it;
     the graph is never replayed, so the generator's offset does not move."""
     g = torch.cuda.CUDAGraph()
-    s = torch.cuda.Stream(device=device)
+    s = _repair_stream.get(device)
+    if s is None:  # one private stream for the process (a new stream per call would shift HIP's
+        s = _repair_stream[device] = torch.cuda.Stream(device=device)  # stream-to-queue mapping)
     t = torch.zeros(1, device=device)
     s.wait_stream(torch.cuda.current_stream(device))
     with torch.cuda.stream(s):
@@ -134,15 +139,7 @@ def all_side_streams(device):
     return [s for (d, _), s in sorted(_side.items(), key=lambda kv: kv[0]) if d == idx]
 
 
-def _env_int(name, default):
-    try:
-        v = int(os.environ.get(name, default))
-    except ValueError:
-        return default
-    return v if v >= 1 else default
-
-
-_bn_concurrency = [_env_int("GM_BN_FUSE_STREAMS", 4)]  # the library's value at load
+_bn_concurrency = [4]  # the library's default (gm_bn_set_concurrency)
 
 
 def reserve_concurrency(n):
