@@ -68,7 +68,7 @@ def c2_run(dev):
     od = gating_ref.BDRState(0.01, 5).update(osums)
     flat = [v for i in range(2) for v in (osums["wn_main"][i], osums["gn_main"][i])] + \
            [v for i in range(2) for v in (osums["wn_bypass"][i], osums["gn_bypass"][i])]
-    ref = dict(loss=float(oloss), d_BDR=od, sums=np.asarray(flat, np.float64), mean=om.detach().numpy(),
+    ref = dict(loss=float(oloss.detach()), d_BDR=od, sums=np.asarray(flat, np.float64), mean=om.detach().numpy(),
                outs=[t.detach().numpy() for t in oo])
     # the bf16 floor: the same oracle under PyTorch's own CPU bf16 autocast (its convolutions
     # and matmuls in bf16, as the HIP trunk computes) against the fp32 oracle

@@ -120,7 +120,7 @@ def test_model_vs_reference(golden, dev, case):
             assert q.grad is not None, n
             idx = spec.sample_idx(n, q.numel())
             r64 = g64[n].reshape(-1)[idx].numpy()
-            scale = np.abs(g64[n]).max().item() + 1e-30
+            scale = float(g64[n].abs().max()) + 1e-30
             es_ref.append(np.abs(fix[key] - r64) / scale)
             es_gpu.append(np.abs(q.grad.reshape(-1)[idx].cpu().double().numpy() - r64) / scale)
         else:
