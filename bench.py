@@ -63,7 +63,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture of the step")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_group_sumsq.json"))
-    ap.add_argument("--conv-traffic-file", default=os.path.join(ROOT, "profiles", "r05b_traffic_conv_family.json"))
+    ap.add_argument("--conv-traffic-file", default=os.path.join(ROOT, "profiles", "r06_traffic_conv_family.json"))
     ap.add_argument("--mmtm-traffic-file", default=os.path.join(ROOT, "profiles", "r03_traffic_mmtm.json"))
     ap.add_argument("--profile", action="store_true",
                     help="steps only (no roofline / cpu_baseline measurements): for rocprofv3 runs")
