@@ -157,7 +157,17 @@ EXPORTS.update({
                                              c_int, c_int, c_void_p, c_size_t, c_void_p]),
     "gm_conv2d_wgrad_hw_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
                                         c_size_t, c_void_p]),
+    "gm_conv2d_wgrad_stem_bn_ok": (c_int, [c_void_p, c_int]),
+    "gm_conv2d_wgrad_stem_bn_grouped_bf16": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                                                     ctypes.c_longlong, c_int, c_void_p, c_size_t, c_void_p]),
 })
+
+
+class StemBnSrc(ctypes.Structure):
+    """gm_stem_bn_src: the stem BatchNorm + ReLU + max-pool backward's operands, for the stem
+    weight gradient that forms its dy in the loader"""
+    _fields_ = [("y", c_void_p), ("dy_pool", c_void_p), ("idx", c_void_p), ("fcoef", c_void_p),
+                ("fcoef_gs", ctypes.c_longlong), ("bcoef", c_void_p), ("bcoef_gs", ctypes.c_longlong)]
 
 
 class WPrep(ctypes.Structure):
@@ -253,6 +263,9 @@ EXPORTS.update({
                                                       c_void_p, c_void_p]),
     "gm_bn_relu_maxpool2d_bwd_grouped_bf16": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                                       c_void_p, c_size_t, c_void_p]),
+    "gm_bn_relu_maxpool2d_bwd_stats_grouped_bf16": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                                                            c_void_p, c_void_p, c_size_t, c_void_p, c_void_p,
+                                                            c_void_p]),
     "gm_conv_stem_stats_rows": (c_int, [c_void_p, c_int]),
     "gm_conv2d_fwd_grouped_stats_bf16": (c_int, [c_void_p, c_int, c_void_p, c_void_p, ctypes.c_longlong, c_void_p,
                                                  c_void_p, c_int, c_void_p]),

@@ -2062,10 +2062,11 @@ extern "C" int gm_bn_bwd_f32(const gm_bn_bwd* p, void* scratch, size_t bytes, vo
 // The stem's BatchNorm + ReLU + max-pool backward in two launches (k_stem_pool_bn_bwd):
 // d describes one view group's pool (N images, k 3, stride 2, pad 1, C 64); ps[g] the BN
 // backward of group g with relu, fwd_coef (the mask from x) and no y / dres; ps[g].dy unused.
-extern "C" int gm_bn_relu_maxpool2d_bwd_grouped_bf16(const gm_pool_desc* d, int G, const void* dy_pool,
-                                                     const void* idx, const void* xsel, const gm_bn_bwd* ps,
-                                                     void* scratch, size_t bytes, void* stream) {
-    const char* fn = "gm_bn_relu_maxpool2d_bwd_grouped_bf16";
+// apply = false: pass 1 only (statistics, dgamma / dbeta, the coefficients ca, cb, cc); the
+// weight gradient of the stem then forms dx itself (gm_conv2d_wgrad_stem_bn_grouped_bf16).
+static int stem_pool_bwd(const gm_pool_desc* d, int G, const void* dy_pool, const void* idx, const void* xsel,
+                         const gm_bn_bwd* ps, void* scratch, size_t bytes, bool apply, const float** bcoef,
+                         long long* bcoef_gs, void* stream, const char* fn) {
     GM_REQUIRE(d && dy_pool && idx && ps && G >= 1 && G <= kMaxBnG, "%s: bad arguments", fn);
     GM_REQUIRE(d->k == 3 && d->stride == 2 && d->pad == 1 && d->C == 64 && d->N >= 1 && d->H >= 2 && d->W >= 2,
                "%s: the stem's pool only (k 3, stride 2, pad 1, C 64)", fn);
@@ -2074,7 +2075,7 @@ extern "C" int gm_bn_relu_maxpool2d_bwd_grouped_bf16(const gm_pool_desc* d, int 
     for (int g = 0; g < G; ++g) {
         const gm_bn_bwd& p = ps[g];
         GM_REQUIRE(p.M == (long long)d->N * d->H * d->W && p.C == d->C && p.relu && p.fwd_coef && !p.y && !p.dres &&
-                       p.x && p.dx && p.gamma && p.save_mean && p.save_invstd && p.dgamma && p.dbeta &&
+                       p.x && (p.dx || !apply) && p.gamma && p.save_mean && p.save_invstd && p.dgamma && p.dbeta &&
                        p.accumulate == ps[0].accumulate,
                    "%s: group %d: BN backward must be M = N*H*W, C, relu with fwd_coef, no y / dres", fn, g);
     }
@@ -2111,10 +2112,31 @@ extern "C" int gm_bn_relu_maxpool2d_bwd_grouped_bf16(const gm_pool_desc* d, int 
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL((k_stem_pool_bn_bwd<false>), dim3(nrc, 1, G), dim3(kT), 0, st, a, pg);
     if ((rc = check_launch("k_stem_pool_bn_bwd<reduce>"))) return rc;
+    if (!apply) {  // group g's ca, cb, cc: a.coef + g * scr_stride bytes (group_args)
+        *bcoef = a.coef;
+        *bcoef_gs = (long long)(a.scr_stride / sizeof(float));
+        return GM_OK;
+    }
     long long grid = (pg.items + kT - 1) / kT;
     if (grid > 4096) grid = 4096;
     hipLaunchKernelGGL((k_stem_pool_bn_bwd<true>), dim3((unsigned)grid, 1, G), dim3(kT), 0, st, a, pg);
     return check_launch("k_stem_pool_bn_bwd<apply>");
+}
+
+extern "C" int gm_bn_relu_maxpool2d_bwd_grouped_bf16(const gm_pool_desc* d, int G, const void* dy_pool,
+                                                     const void* idx, const void* xsel, const gm_bn_bwd* ps,
+                                                     void* scratch, size_t bytes, void* stream) {
+    return stem_pool_bwd(d, G, dy_pool, idx, xsel, ps, scratch, bytes, true, nullptr, nullptr, stream,
+                         "gm_bn_relu_maxpool2d_bwd_grouped_bf16");
+}
+
+extern "C" int gm_bn_relu_maxpool2d_bwd_stats_grouped_bf16(const gm_pool_desc* d, int G, const void* dy_pool,
+                                                           const void* idx, const void* xsel, const gm_bn_bwd* ps,
+                                                           void* scratch, size_t bytes, const float** bcoef,
+                                                           long long* bcoef_gs, void* stream) {
+    const char* fn = "gm_bn_relu_maxpool2d_bwd_stats_grouped_bf16";
+    GM_REQUIRE(bcoef && bcoef_gs, "%s: null coefficient outputs", fn);
+    return stem_pool_bwd(d, G, dy_pool, idx, xsel, ps, scratch, bytes, false, bcoef, bcoef_gs, stream, fn);
 }
 
 // BatchNorm forward statistics from producer partial rows (gm_conv2d_fwd_grouped_bn_stats_bf16,

@@ -947,24 +947,102 @@ __global__ __launch_bounds__(512) void k_wgrad_ring(WRingArgs a) {
 // them in a fixed order.  The generic kernel (k_conv_wgrad4 <1, 2>) re-staged every
 // input pixel per tap through an im2col tile: 117 us alone, 142 us in the step.
 struct WStemArgs {
-    const uint16_t* dy;  // [G][N][P][Q][64]
+    const uint16_t* dy;  // [G][N][P][Q][64]: the output gradient, or (BN) the stem output y
     const uint16_t* x;   // [G][N][Hi][Wi][8] (pixel pairs)
     float* part;         // [G][splits][64][R * S * 8]
     int P, Q, Wi;
     int cpi, L, splits;  // chunks per image, output rows per chunk, workgroups per group (N * cpi)
     int uchunks, upitch, ichunks;  // 16-B chunks per unit (two input rows), LDS slot bytes, chunks per image
     long long gs_dy, gs_x;
+    // BN (k_wgrad_stem<R, S, true>): dy formed in the loader from the stem's BatchNorm + ReLU +
+    // max-pool backward (gm_conv2d_wgrad_stem_bn_grouped_bf16)
+    const uint4* gp;     // [G][N][Pp][Qp][64] bf16 pool gradient
+    const uint2* pidx;   // [G][N][Pp][Qp][64] window-relative argmax bytes
+    const float* fcoef;  // group g: fcoef + g * fcoef_gs = sc[64], sh[64]
+    const float* bcoef;  // group g: bcoef + g * bcoef_gs = ca[64], cb[64], cc[64]
+    long long fcoef_gs, bcoef_gs, gs_pool;  // floats, floats, 16-B vectors
+    int Pp, Qp;
 };
 
-template <int R, int S>
+// BN: the stem BatchNorm + ReLU + max-pool backward of the 8-channel chunks cg of the stem output y
+// at row s, columns 2 pp and 2 pp + 1 (y0, y1), exactly as k_stem_pool_bn_bwd<true> forms dx
+// (batchnorm.hip): the fp32 sum, in window order, of the pool gradients whose argmax is the
+// element, rounded to bf16, masked by relu(y * sc + sh), then ca * d + (cb * y + cc) rounded to
+// bf16.  Both columns lie in pool column pp (the odd one also in pp + 1), so each window's data is
+// read once for the pair.  pool_g / pool_i: the two LDS slots of pooled rows (slot k & 1: gradient
+// [Qp][64] bf16, argmax bytes [Qp][64]); cf: sc, sh, ca, cb, cc [64] each.
+__device__ __forceinline__ void stem_bn_dx2(uint4& y0, uint4& y1, int s, int pp, int cg, const char* pool_g,
+                                            const char* pool_i, const float* cf, int Pp, int Qp) {
+    const int k0 = s >> 1, dh = s & 1;
+    const uint32_t yw[2][4] = {{y0.x, y0.y, y0.z, y0.w}, {y1.x, y1.y, y1.z, y1.w}};
+    uint32_t ow[2][4];
+    const bool right = pp + 1 < Qp;
+    // two halves of four channels, one after the other
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        float d0[4] = {0.f, 0.f, 0.f, 0.f}, d1[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int wr = 0; wr < 2; ++wr) {
+            const int k = k0 + wr;
+            if (wr > dh || k >= Pp) continue;  // uniform
+            const int rb = (dh - 2 * wr + 1) * 3;  // window row of row s, times 3
+            const char* gk = pool_g + (k & 1) * Qp * 128 + cg * 16 + h * 8;
+            const char* ik = pool_i + (k & 1) * Qp * 64 + cg * 8 + h * 4;
+            const uint2 ga = *reinterpret_cast<const uint2*>(gk + pp * 128);
+            const uint32_t ia = *reinterpret_cast<const uint32_t*>(ik + pp * 64);
+            uint2 gb = make_uint2(0, 0);
+            uint32_t ib = ~0u;  // no window right of the last pool column: never a position
+            if (right) {
+                gb = *reinterpret_cast<const uint2*>(gk + (pp + 1) * 128);
+                ib = *reinterpret_cast<const uint32_t*>(ik + (pp + 1) * 64);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t ba = (ia >> (8 * i)) & 0xffu, bb = (ib >> (8 * i)) & 0xffu;
+                const float va = (i & 1) ? bf_hi(i < 2 ? ga.x : ga.y) : bf_lo(i < 2 ? ga.x : ga.y);
+                const float vb = (i & 1) ? bf_hi(i < 2 ? gb.x : gb.y) : bf_lo(i < 2 ? gb.x : gb.y);
+                // column 2pp: window (k, pp) at window column 1; column 2pp + 1: window (k, pp) at
+                // column 2, then window (k, pp + 1) at column 0 (the reference's window order)
+                if (ba == (uint32_t)(rb + 1)) d0[i] += va;
+                if (ba == (uint32_t)(rb + 2)) d1[i] += va;
+                if (bb == (uint32_t)rb) d1[i] += vb;
+            }
+        }
+        const float4* c4 = reinterpret_cast<const float4*>(cf + cg * 8 + 4 * h);
+        const float4 sc = c4[0], sh = c4[16], ca = c4[32], cb = c4[48], cc = c4[64];
+        const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
+        const float cav[4] = {ca.x, ca.y, ca.z, ca.w}, cbv[4] = {cb.x, cb.y, cb.z, cb.w};
+        const float ccv[4] = {cc.x, cc.y, cc.z, cc.w};
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            float o[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int j = 4 * h + i;
+                const float xf = (j & 1) ? bf_hi(yw[c][j >> 1]) : bf_lo(yw[c][j >> 1]);
+                const float dr = __uint_as_float((uint32_t)Elem<uint16_t>::f2bf(c ? d1[i] : d0[i]) << 16);
+                const float dm = fmaf(xf, scv[i], shv[i]) > 0.f ? dr : 0.f;
+                o[i] = fmaf(cav[i], dm, fmaf(cbv[i], xf, ccv[i]));
+            }
+            ow[c][2 * h] = pack_bf2(o[0], o[1]);
+            ow[c][2 * h + 1] = pack_bf2(o[2], o[3]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    y0 = make_uint4(ow[0][0], ow[0][1], ow[0][2], ow[0][3]);
+    y1 = make_uint4(ow[1][0], ow[1][1], ow[1][2], ow[1][3]);
+}
+
+template <int R, int S, bool BN = false>
 __global__ __launch_bounds__(64 * R) void k_wgrad_stem(WStemArgs a) {
     constexpr int NT = 64 * R;                // threads: one wave per tap row
     constexpr int TC = R * S * 8;             // dw columns per output channel
-    constexpr int DPT = (1024 + NT - 1) / NT;  // dy chunks per thread per row (Q <= 128)
+    // dy chunks per thread per row (Q <= 128; BN: Q * 8 <= 2 * NT, checked on the host)
+    constexpr int DPT = BN ? 2 : (1024 + NT - 1) / NT;
     constexpr int RING = 8;
     static_assert(S * 8 == 32, "k_wgrad_stem: one tap row = one 32-column accumulator block");
     extern __shared__ __attribute__((aligned(16))) uint4 wsm[];
-    char* lds = reinterpret_cast<char*>(wsm);  // [dy tiles 2 x Q*128][ring 8 x upitch]
+    char* lds = reinterpret_cast<char*>(wsm);  // [dy tiles 2 x Q*128][ring 8 x upitch] (BN: [pooled 2 x Qp*192][coef])
     const int t = threadIdx.x, lane = t & 63;
     const int rr = __builtin_amdgcn_readfirstlane(t >> 6);
     const int grp = blockIdx.x / a.splits, wg = blockIdx.x - grp * a.splits;
@@ -974,46 +1052,108 @@ __global__ __launch_bounds__(64 * R) void k_wgrad_stem(WStemArgs a) {
     char* const ring = lds + 2 * tileb;
     const uint4* const gdy = reinterpret_cast<const uint4*>(a.dy + grp * a.gs_dy) + (size_t)b * a.P * dchunks;
     const uint4* const gx = reinterpret_cast<const uint4*>(a.x + grp * a.gs_x) + (size_t)b * a.ichunks;
+    // BN: two slots of pooled rows (slot k & 1), the coefficients; this image's pooled rows
+    char* const pool_g = ring + RING * a.upitch;
+    char* const pool_i = pool_g + 2 * a.Qp * 128;
+    float* const cf = reinterpret_cast<float*>(pool_i + 2 * a.Qp * 64);
+    const size_t pimg = BN ? (size_t)b * a.Pp * a.Qp * 8 : 0;
+    const uint4* const gpp = BN ? a.gp + grp * a.gs_pool + pimg : nullptr;
+    const uint2* const gpi = BN ? a.pidx + grp * a.gs_pool + pimg : nullptr;
     struct Stage {
         uint4 d[DPT];
         uint4 x;
+        uint4 pg;  // BN: one pooled row's gradient vector and argmax bytes (thread t: vector t)
+        uint2 pi;
     };
-    // dy row pr and input unit u (rows 2u, 2u + 1) -> registers; zeros past the image
-    auto fetch = [&](int pr, int u, Stage& st, bool with_dy = true) __attribute__((always_inline)) {
+    // dy row pr and input unit u (rows 2u, 2u + 1) -> registers; zeros past the image;
+    // BN: pooled row pk too when pk >= 0
+    auto fetch = [&](int pr, int u, Stage& st, bool with_dy = true, int pk = -1) __attribute__((always_inline)) {
 #pragma unroll
         for (int h = 0; h < DPT && with_dy; ++h) {
-            const int cc = t + NT * h;
+            // BN: thread t holds columns 2 (t >> 3) + h of channel chunk t & 7 (a pool column's pair)
+            const int cc = BN ? (2 * (t >> 3) + h) * 8 + (t & 7) : t + NT * h;
             st.d[h] = (cc < dchunks && pr < a.P) ? gdy[(size_t)pr * dchunks + cc] : make_uint4(0, 0, 0, 0);
         }
         const int gi = u * a.uchunks + t;
         st.x = (t < a.uchunks && gi < a.ichunks) ? gx[gi] : make_uint4(0, 0, 0, 0);
-    };
-    auto stash = [&](int pr, int u, const Stage& st, bool with_dy = true) __attribute__((always_inline)) {
-        char* tile = lds + (pr & 1) * tileb;
-#pragma unroll
-        for (int h = 0; h < DPT && with_dy; ++h) {
-            const int cc = t + NT * h;
-            if (cc < dchunks) {
-                const int px = cc >> 3, j = cc & 7;
-                *reinterpret_cast<uint4*>(tile + px * 128 + ((j ^ wswz<128>(px)) << 4)) = st.d[h];
+        if constexpr (BN) {
+            if (pk >= 0) {
+                const bool ok = pk < a.Pp && t < a.Qp * 8;
+                const size_t o = (size_t)pk * a.Qp * 8 + t;
+                st.pg = ok ? gpp[o] : make_uint4(0, 0, 0, 0);
+                st.pi = ok ? gpi[o] : make_uint2(0, 0);
             }
         }
+    };
+    // dy row pr (BN: formed from y row pr and the pooled rows in LDS) into tile pr & 1
+    auto stash_dy = [&](int pr, const Stage& st) __attribute__((always_inline)) {
+        char* tile = lds + (pr & 1) * tileb;
+        if constexpr (BN) {
+            const int pp = t >> 3, j = t & 7;
+            if (2 * pp < a.Q) {
+                uint4 v0 = st.d[0], v1 = st.d[1];
+                stem_bn_dx2(v0, v1, pr, pp, j, pool_g, pool_i, cf, a.Pp, a.Qp);
+                const int px = 2 * pp;
+                *reinterpret_cast<uint4*>(tile + px * 128 + ((j ^ wswz<128>(px)) << 4)) = v0;
+                *reinterpret_cast<uint4*>(tile + (px + 1) * 128 + ((j ^ wswz<128>(px + 1)) << 4)) = v1;
+            }
+        } else {
+#pragma unroll
+            for (int h = 0; h < DPT; ++h) {
+                const int cc = t + NT * h;
+                if (cc < dchunks) {
+                    const int px = cc >> 3, j = cc & 7;
+                    *reinterpret_cast<uint4*>(tile + px * 128 + ((j ^ wswz<128>(px)) << 4)) = st.d[h];
+                }
+            }
+        }
+    };
+    auto stash_unit = [&](int u, const Stage& st) __attribute__((always_inline)) {
         if (t < a.uchunks) *reinterpret_cast<uint4*>(ring + (u & (RING - 1)) * a.upitch + t * 16) = st.x;
     };
-    {  // prologue: dy row p0 and units p0 .. p0 + 3 (row p0's window)
+    auto stash_pool = [&](int pk, const Stage& st) __attribute__((always_inline)) {
+        if (t < a.Qp * 8) {
+            *reinterpret_cast<uint4*>(pool_g + (pk & 1) * a.Qp * 128 + t * 16) = st.pg;
+            *reinterpret_cast<uint2*>(pool_i + (pk & 1) * a.Qp * 64 + t * 8) = st.pi;
+        }
+    };
+    const int k0 = p0 >> 1;  // BN: p0 is even (the host plan's L is)
+    {  // prologue: dy row p0 and units p0 .. p0 + 3 (row p0's window); BN: pooled rows k0, k0 + 1
         Stage s0, s1;
-        fetch(p0, p0, s0, true);
-        fetch(0, p0 + 1, s1, false);
-        stash(p0, p0, s0, true);
-        stash(0, p0 + 1, s1, false);
+        fetch(p0, p0, s0, true, k0);
+        fetch(0, p0 + 1, s1, false, k0 + 1);
+        if constexpr (!BN) stash_dy(p0, s0);
+        stash_unit(p0, s0);
+        stash_unit(p0 + 1, s1);
+        if constexpr (BN) {
+            stash_pool(k0, s0);
+            stash_pool(k0 + 1, s1);
+            if (t < 64) {
+                const float* fc = a.fcoef + grp * a.fcoef_gs;
+                const float* bc = a.bcoef + grp * a.bcoef_gs;
+                cf[t] = fc[t];
+                cf[64 + t] = fc[64 + t];
+                cf[128 + t] = bc[t];
+                cf[192 + t] = bc[64 + t];
+                cf[256 + t] = bc[128 + t];
+            }
+        }
         fetch(0, p0 + 2, s0, false);
         fetch(0, p0 + 3, s1, false);
-        stash(0, p0 + 2, s0, false);
-        stash(0, p0 + 3, s1, false);
+        stash_unit(p0 + 2, s0);
+        stash_unit(p0 + 3, s1);
+        if constexpr (BN) {
+            __syncthreads();  // pooled rows k0, k0 + 1 and the coefficients are in LDS
+            stash_dy(p0, s0);
+        }
     }
-    Stage sa, sb;  // iteration p stashes dy row p + 1 and unit p + 4, then fetches row p + 3, unit p + 6
+    // iteration p stashes dy row p + 1 and unit p + 4, then fetches row p + 3, unit p + 6.  BN:
+    // pooled row j is fetched in iteration 2j - 5 and stashed in iteration 2j - 3 (both odd: stage
+    // sb), one iteration before row 2j - 1 - its first reader - is formed, after the last reader of
+    // row j - 2 (its slot) - row 2j - 3, formed in iteration 2j - 4
+    Stage sa, sb;
     fetch(p0 + 1, p0 + 4, sa);
-    fetch(p0 + 2, p0 + 5, sb);
+    fetch(p0 + 2, p0 + 5, sb, true, k0 + 2);
 
     floatx16 acc[2];
 #pragma unroll
@@ -1026,10 +1166,14 @@ __global__ __launch_bounds__(64 * R) void k_wgrad_stem(WStemArgs a) {
     const int krow = 8 * (g4 >> 1) + q4, col = 16 * (g4 & 1) + 4 * p4;
     auto rowoff = [](int row, int ch) { return row * 128 + ((((ch >> 3) ^ wswz<128>(row))) << 4) + (ch & 7) * 2; };
     const int nks = a.Q >> 4;
-    auto iteration = [&](int p, Stage& st) __attribute__((always_inline)) {
+    auto iteration = [&](int p, Stage& st, auto odd) __attribute__((always_inline)) {
+        constexpr bool ODD = decltype(odd)::value;
         __syncthreads();  // row p's dy tile and units p .. p + 3 are in LDS; row p - 1's reads are done
-        stash(p + 1, p + 4, st);
-        fetch(p + 3, p + 6, st);
+        // (the unit and the pooled row first: their registers are free before dy is formed)
+        stash_unit(p + 4, st);
+        if constexpr (BN && ODD) stash_pool((p + 3) >> 1, st);
+        stash_dy(p + 1, st);
+        fetch(p + 3, p + 6, st, true, (BN && ODD) ? (p + 5) >> 1 : -1);
         const char* tile = lds + (p & 1) * tileb;
         const char* xrow = ring + ((p + (rr >> 1)) & (RING - 1)) * a.upitch + (rr & 1) * a.Wi * 16;
         for (int ks = 0; ks < nks; ++ks) {
@@ -1045,8 +1189,8 @@ __global__ __launch_bounds__(64 * R) void k_wgrad_stem(WStemArgs a) {
         }
     };
     for (int p = p0; p < p1; p += 2) {
-        iteration(p, sa);
-        if (p + 1 < p1) iteration(p + 1, sb);
+        iteration(p, sa, std::false_type{});
+        if (p + 1 < p1) iteration(p + 1, sb, std::true_type{});
     }
     // the partial: dw[channel][rr * 32 + (s, c)], lane -> column, registers -> channels
     float* out = a.part + ((size_t)grp * a.splits + wg) * (64 * TC) + rr * 32 + (lane & 31);
@@ -1318,6 +1462,7 @@ static bool stemw_plan(const gm_conv_desc_hw* d, int G, StemWPlan& w) {
     const int target = 512 / G > 0 ? 512 / G : 1;
     const int cpi0 = std::max(1, std::min(w.P, target / d->N));
     w.L = (w.P + cpi0 - 1) / cpi0;
+    w.L += w.L & 1;  // even: the BN form's pooled-row schedule starts on an even row
     w.cpi = (w.P + w.L - 1) / w.L;
     w.splits = d->N * w.cpi;
     return true;
@@ -1353,6 +1498,37 @@ extern "C" size_t gm_conv2d_wgrad_scratch(const gm_conv_desc* d) {
     return gm_conv2d_wgrad_hw_scratch(&h);
 }
 
+
+static WStemArgs stem_args(const gm_conv_desc_hw* d, const StemWPlan& sw, const void* dy, const void* x,
+                           void* scratch) {
+    WStemArgs s{};
+    s.dy = (const uint16_t*)dy;
+    s.x = (const uint16_t*)x;
+    s.part = (float*)scratch;
+    s.P = sw.P; s.Q = sw.Q; s.Wi = d->W;
+    s.cpi = sw.cpi; s.L = sw.L; s.splits = sw.splits;
+    s.uchunks = 2 * d->W;
+    s.upitch = s.uchunks * 16;
+    s.ichunks = d->H * d->W;
+    s.gs_dy = (long long)d->N * sw.P * sw.Q * 64;
+    s.gs_x = (long long)d->N * d->H * d->W * 8;
+    return s;
+}
+
+template <bool BN>
+static int launch_wgrad_stem(const WStemArgs& s, const StemWPlan& sw, int G, size_t lds, hipStream_t st) {
+    static size_t granted = 0;
+    if (lds > granted) {
+        if (hipFuncSetAttribute((const void*)k_wgrad_stem<7, 4, BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds) != hipSuccess) {
+            set_error("k_wgrad_stem: %zu B of LDS refused", lds);
+            return GM_E_UNSUP;
+        }
+        granted = lds;
+    }
+    k_wgrad_stem<7, 4, BN><<<sw.splits * G, 448, lds, st>>>(s);
+    return check_launch(BN ? "k_wgrad_stem<bn>" : "k_wgrad_stem");
+}
 
 // the split sum of every split weight-gradient kernel: k_wgrad_sum with R split lanes per
 // column (at most 8, inside one wave), enough waves for small slabs
@@ -1394,29 +1570,8 @@ extern "C" int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, con
     };
     StemWPlan sw;
     if (stemw_plan(d, G, sw) && c_real == d->C) {
-        WStemArgs s;
-        s.dy = (const uint16_t*)dy;
-        s.x = (const uint16_t*)x;
-        s.part = (float*)scratch;
-        s.P = sw.P; s.Q = sw.Q; s.Wi = d->W;
-        s.cpi = sw.cpi; s.L = sw.L; s.splits = sw.splits;
-        s.uchunks = 2 * d->W;
-        s.upitch = s.uchunks * 16;
-        s.ichunks = d->H * d->W;
-        s.gs_dy = (long long)d->N * sw.P * sw.Q * 64;
-        s.gs_x = (long long)d->N * d->H * d->W * 8;
-        const size_t lds = (size_t)2 * sw.Q * 128 + (size_t)8 * s.upitch;
-        static size_t granted = 0;
-        if (lds > granted) {
-            if (hipFuncSetAttribute((const void*)k_wgrad_stem<7, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
-                hipSuccess) {
-                set_error("k_wgrad_stem: %zu B of LDS refused", lds);
-                return GM_E_UNSUP;
-            }
-            granted = lds;
-        }
-        k_wgrad_stem<7, 4><<<sw.splits * G, 448, lds, st0>>>(s);
-        const int rc = check_launch("k_wgrad_stem");
+        const WStemArgs s = stem_args(d, sw, dy, x, scratch);
+        int rc = launch_wgrad_stem<false>(s, sw, G, (size_t)2 * sw.Q * 128 + (size_t)8 * s.upitch, st0);
         if (rc) return rc;
         return split_sum(s.part, sw.splits, (size_t)64 * 224);
     }
@@ -1542,6 +1697,52 @@ extern "C" int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, con
     k_wgrad_reduce<<<dim3(g, G), 256, 0, st>>>(a.part, a.splits, d->K, a.T, d->C, c_real, accumulate, dw,
                                                dw_stride);
     return check_launch("k_wgrad_reduce");
+}
+
+
+// The stem's weight gradient with dy formed in the loader (greedymml.h: the stem BatchNorm +
+// ReLU + max-pool backward, never written): k_wgrad_stem<7, 4, true> on the k_wgrad_stem plan
+static bool stem_bn_plan(const gm_conv_desc_hw* d, int G, StemWPlan& sw) {
+    return d && G >= 1 && G <= 64 && stemw_plan(d, G, sw) && sw.Q * 8 <= 2 * 448 && ((sw.Q + 1) / 2) * 8 <= 448 &&
+           !(sw.L & 1);
+}
+
+extern "C" int gm_conv2d_wgrad_stem_bn_ok(const gm_conv_desc_hw* d, int G) {
+    StemWPlan sw;
+    return stem_bn_plan(d, G, sw) ? 1 : 0;
+}
+
+extern "C" int gm_conv2d_wgrad_stem_bn_grouped_bf16(const gm_conv_desc_hw* d, int G, const gm_stem_bn_src* src,
+                                                    const void* x, float* dw, long long dw_stride, int accumulate,
+                                                    void* scratch, size_t scratch_bytes, void* stream) {
+    const char* fn = "gm_conv2d_wgrad_stem_bn_grouped_bf16";
+    GM_REQUIRE(d && src && src->y && src->dy_pool && src->idx && src->fcoef && src->bcoef && x && dw,
+               "%s: null pointer", fn);
+    GM_REQUIRE(G >= 1 && G <= 64, "%s: view groups must be 1..64 (got %d)", fn, G);
+    StemWPlan sw;
+    if (!stem_bn_plan(d, G, sw)) {
+        set_error("%s: not the pixel-pair stem shape of k_wgrad_stem with Q <= 112", fn);
+        return GM_E_UNSUP;
+    }
+    const int Pp = (sw.P + 1) / 2, Qp = (sw.Q + 1) / 2;
+    GM_REQUIRE(G == 1 || dw_stride >= 64 * 224 || dw_stride <= -64 * 224, "%s: group gradient stride overlaps", fn);
+    const size_t need = gm_conv2d_wgrad_grouped_scratch(d, G);
+    GM_REQUIRE(scratch && scratch_bytes >= need, "%s: scratch %zu < %zu", fn, scratch_bytes, need);
+    WStemArgs s = stem_args(d, sw, src->y, x, scratch);
+    s.gp = static_cast<const uint4*>(src->dy_pool);
+    s.pidx = static_cast<const uint2*>(src->idx);
+    s.fcoef = src->fcoef;
+    s.bcoef = src->bcoef;
+    s.fcoef_gs = src->fcoef_gs;
+    s.bcoef_gs = src->bcoef_gs;
+    s.gs_pool = (long long)d->N * Pp * Qp * 8;
+    s.Pp = Pp;
+    s.Qp = Qp;
+    hipStream_t st = as_stream(stream);
+    const size_t lds = (size_t)2 * sw.Q * 128 + (size_t)8 * s.upitch + (size_t)2 * Qp * 192 + 5 * 64 * sizeof(float);
+    int rc = launch_wgrad_stem<true>(s, sw, G, lds, st);
+    if (rc) return rc;
+    return launch_wgrad_sum(s.part, sw.splits, (size_t)64 * 224, accumulate, dw, dw_stride, G, st);
 }
 
 extern "C" int gm_conv2d_wgrad_hw_bf16(const gm_conv_desc_hw* d, const void* dy, const void* x, float* dw,

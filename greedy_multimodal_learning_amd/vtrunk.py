@@ -44,6 +44,10 @@ ENABLED = os.environ.get("GM_VTRUNK", "1") != "0"
 FUSED_STEM_BWD = True
 # its statistics pass over the pooled tensors (the forward's selected x) instead of x
 STEM_XSEL = True
+# with it, the stem's weight gradient forms its dy in the loader from the pool + BN operands, so
+# the BN's input gradient (the stem's dy, 205 MB at C2) is never written nor read (False: the
+# BN backward's apply pass writes it, the weight gradient reads it)
+FUSED_STEM_WGRAD = True
 # the stem BN's statistics from the stem convolution's epilogue (False: the statistics pass over
 # the convolution's output)
 FUSED_STEM_STATS = True
@@ -532,6 +536,11 @@ class _VStemFn(torch.autograd.Function):
                                                    y.data_ptr(), 0, 0, L.stream_of(dev)), "gm_conv2d_fwd_grouped_bf16")
         ctx.save_for_backward(xp, *weights)
         ctx.meta = (G, B, R, S, Sp)
+        # the stem BN + ReLU + max-pool backward hands its operands over (stats["bwd"]) instead of
+        # writing dy when the weight gradient can form dy itself (gm_conv2d_wgrad_stem_bn_ok)
+        ctx.link = stats
+        if stats is not None:
+            stats["stem_bn_ok"] = FUSED_STEM_WGRAD and lib.gm_conv2d_wgrad_stem_bn_ok(ctypes.byref(d), G) == 1
         return y
 
     @staticmethod
@@ -542,7 +551,9 @@ class _VStemFn(torch.autograd.Function):
         if not any(want):
             return (None, None, None, None, *[None] * G)
         lib = L.load()
-        gy = _nhwc(gy.to(BF))
+        bw = ctx.link.pop("bwd", None) if ctx.link is not None else None
+        if bw is None:
+            gy = _nhwc(gy.to(BF))
         dev = gy.device
         _, Hp, Wq, _ = xp.shape
         K, C0 = weights[0].shape[0], weights[0].shape[1]
@@ -550,9 +561,17 @@ class _VStemFn(torch.autograd.Function):
         need = lib.gm_conv2d_wgrad_grouped_scratch(ctypes.byref(d), G)
         scratch = torch.empty(max(need, 16), device=dev, dtype=torch.uint8)
         dwp = torch.empty(G, K, R, Sp, 8, device=dev, dtype=torch.float32)
-        L.check(lib.gm_conv2d_wgrad_grouped_bf16(ctypes.byref(d), G, gy.data_ptr(), xp.data_ptr(), dwp.data_ptr(),
-                                                 K * R * Sp * 8, 8, 0, scratch.data_ptr(), need, L.stream_of(dev)),
-                "gm_conv2d_wgrad_grouped_bf16")
+        if bw is not None:  # gy is a placeholder: dy is formed from the BN + pool operands
+            src = L.StemBnSrc(bw["y"].data_ptr(), bw["dy_pool"].data_ptr(), bw["idx"].data_ptr(),
+                              bw["fcoef"].data_ptr(), bw["fcoef"].stride(0), bw["bcoef"], bw["bcoef_gs"])
+            L.check(lib.gm_conv2d_wgrad_stem_bn_grouped_bf16(ctypes.byref(d), G, ctypes.byref(src), xp.data_ptr(),
+                                                             dwp.data_ptr(), K * R * Sp * 8, 0, scratch.data_ptr(),
+                                                             need, L.stream_of(dev)),
+                    "gm_conv2d_wgrad_stem_bn_grouped_bf16")
+        else:
+            L.check(lib.gm_conv2d_wgrad_grouped_bf16(ctypes.byref(d), G, gy.data_ptr(), xp.data_ptr(),
+                                                     dwp.data_ptr(), K * R * Sp * 8, 8, 0, scratch.data_ptr(), need,
+                                                     L.stream_of(dev)), "gm_conv2d_wgrad_grouped_bf16")
         grads = []
         for g, w in enumerate(weights):
             if not want[g]:
@@ -614,6 +633,7 @@ class _VBNReluPoolFn(torch.autograd.Function):
                 "gm_bn_relu_maxpool2d_fwd_grouped_bf16")
         ctx.save_for_backward(xb, coef, sm, si, idx, xsel, *gammas, *betas)
         ctx.meta = (G, k, s, pad)
+        ctx.link = stats
         return y
 
     @staticmethod
@@ -628,21 +648,37 @@ class _VBNReluPoolFn(torch.autograd.Function):
         want_w, want_b = any(ctx.needs_input_grad[7:7 + G]), any(ctx.needs_input_grad[7 + G:])
         if xsel is not None and (want_w or want_b):
             # the pool's input gradient is gathered inside the BN backward's two passes
-            # (gm_bn_relu_maxpool2d_bwd_grouped_bf16): never written
+            # (gm_bn_relu_maxpool2d_bwd_grouped_bf16): never written.  With the stem's fused weight
+            # gradient (ctx.link["stem_bn_ok"]) only the statistics pass runs here and dx is never
+            # written at all: the stem's backward forms it in its loader from the operands handed
+            # over in ctx.link["bwd"]; the gradient returned for X is a placeholder it does not read
             N = GN // G
             M = N * H * W
-            dx = torch.empty_like(xb, memory_format=CL)
+            link = ctx.link if (ctx.needs_input_grad[0] and ctx.link is not None
+                                and ctx.link.get("stem_bn_ok")) else None
+            dx = None if link is not None else torch.empty_like(xb, memory_format=CL)
             dgs, dbs, acc, sunk = _bn_param_grads(gammas, betas, want_w, want_b)
             descs = [L.BnBwd(M, C, 1, 0, 0, xb[g * N:(g + 1) * N].data_ptr(), gammas[g].data_ptr(), sm[g].data_ptr(),
-                             si[g].data_ptr(), dx[g * N:(g + 1) * N].data_ptr(), 0, dgs[g].data_ptr(),
-                             dbs[g].data_ptr(), int(acc), 0, coef[g].data_ptr()) for g in range(G)]
+                             si[g].data_ptr(), dx[g * N:(g + 1) * N].data_ptr() if dx is not None else 0, 0,
+                             dgs[g].data_ptr(), dbs[g].data_ptr(), int(acc), 0, coef[g].data_ptr())
+                     for g in range(G)]
             buf = _bn_scratch_g(xb.device, M, C, G)
             d = L.PoolDesc(N, H, W, C, k, s, pad)
-            L.check(lib.gm_bn_relu_maxpool2d_bwd_grouped_bf16(ctypes.byref(d), G, dy.data_ptr(), idx.data_ptr(),
-                                                              xsel.data_ptr() if ctx.xsel_on else 0,
-                                                              L.arr(L.BnBwd, descs), buf.data_ptr(),
-                                                              buf.numel(), L.stream_of(xb.device)),
-                    "gm_bn_relu_maxpool2d_bwd_grouped_bf16")
+            if link is not None:
+                bcoef, bgs = ctypes.c_void_p(), ctypes.c_longlong()
+                L.check(lib.gm_bn_relu_maxpool2d_bwd_stats_grouped_bf16(
+                    ctypes.byref(d), G, dy.data_ptr(), idx.data_ptr(), xsel.data_ptr() if ctx.xsel_on else 0,
+                    L.arr(L.BnBwd, descs), buf.data_ptr(), buf.numel(), ctypes.byref(bcoef), ctypes.byref(bgs),
+                    L.stream_of(xb.device)), "gm_bn_relu_maxpool2d_bwd_stats_grouped_bf16")
+                link["bwd"] = dict(y=xb, dy_pool=dy, idx=idx, fcoef=coef, bcoef=bcoef.value, bcoef_gs=bgs.value,
+                                   keep=buf)
+                dx = torch.empty((), device=xb.device, dtype=xb.dtype).expand(xb.shape)
+            else:
+                L.check(lib.gm_bn_relu_maxpool2d_bwd_grouped_bf16(ctypes.byref(d), G, dy.data_ptr(), idx.data_ptr(),
+                                                                  xsel.data_ptr() if ctx.xsel_on else 0,
+                                                                  L.arr(L.BnBwd, descs), buf.data_ptr(),
+                                                                  buf.numel(), L.stream_of(xb.device)),
+                        "gm_bn_relu_maxpool2d_bwd_grouped_bf16")
             if sunk:
                 for p in list(gammas) + list(betas):
                     sink_done(p)

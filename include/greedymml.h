@@ -441,6 +441,32 @@ size_t gm_conv2d_wgrad_grouped_scratch(const gm_conv_desc_hw* d, int G);
 int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, const void* dy, const void* x, float* dw,
                                  long long dw_stride, int c_real, int accumulate, void* scratch,
                                  size_t scratch_bytes, void* stream);
+/* The pixel-pair stem's weight gradient (the shape gm_conv2d_wgrad_grouped_bf16 serves with
+ * k_wgrad_stem: 7 x 4 filter over 8-channel pairs, strides (2, 1), K 64, Q <= 112) with dy NOT
+ * materialised: the loader forms dy = the stem BatchNorm + ReLU + max-pool backward (reference
+ * src/model.py:65-106 through torchvision's conv1 -> bn1 -> relu -> maxpool) per element,
+ *   d  = sum over the pool windows whose argmax is the element of dy_pool (fp32, window order),
+ *        rounded to bf16, zero where y * fsc + fsh <= 0;
+ *   dy = bf16(ca * d + (cb * y + cc)),
+ * bit-identical to gm_bn_relu_maxpool2d_bwd_grouped_bf16's dx followed by
+ * gm_conv2d_wgrad_grouped_bf16.  y: the stem output [G][N][P][Q][64] bf16 (the BatchNorm's x);
+ * dy_pool / idx: the pool's gradient and argmax bytes [G][N][(P+1)/2][(Q+1)/2][64];
+ * fcoef: the forward's sc[64], sh[64] of group g at fcoef + g * fcoef_gs; bcoef: ca, cb, cc
+ * [3][64] of group g at bcoef + g * bcoef_gs (gm_bn_relu_maxpool2d_bwd_stats_grouped_bf16).
+ * Scratch: gm_conv2d_wgrad_grouped_scratch(d, G).  GM_E_UNSUP (nothing launched) for other shapes. */
+typedef struct gm_stem_bn_src {
+    const void* y;
+    const void* dy_pool;
+    const void* idx;
+    const float* fcoef;
+    long long fcoef_gs;
+    const float* bcoef;
+    long long bcoef_gs;
+} gm_stem_bn_src;
+int gm_conv2d_wgrad_stem_bn_ok(const gm_conv_desc_hw* d, int G); /* 1: the call below takes this shape */
+int gm_conv2d_wgrad_stem_bn_grouped_bf16(const gm_conv_desc_hw* d, int G, const gm_stem_bn_src* src, const void* x,
+                                         float* dw, long long dw_stride, int accumulate, void* scratch,
+                                         size_t scratch_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Reference-precision (fp32) trunk convolutions: the same three passes on the exact
@@ -635,6 +661,13 @@ int gm_bn_bwd_apply_grouped_bf16(const gm_bn_bwd* ps, int G, const float* stats,
 int gm_bn_relu_maxpool2d_bwd_grouped_bf16(const gm_pool_desc* d, int G, const void* dy_pool, const void* idx,
                                           const void* xsel, const gm_bn_bwd* ps, void* scratch, size_t scratch_bytes,
                                           void* stream);
+/* its statistics pass only (dgamma / dbeta; ps[g].dx may be null): *bcoef receives group 0's
+ * backward coefficients ca, cb, cc ([3][C] floats, inside scratch), *bcoef_gs the floats between
+ * groups - the input of gm_conv2d_wgrad_stem_bn_grouped_bf16, which forms dx in its loader */
+int gm_bn_relu_maxpool2d_bwd_stats_grouped_bf16(const gm_pool_desc* d, int G, const void* dy_pool, const void* idx,
+                                                const void* xsel, const gm_bn_bwd* ps, void* scratch,
+                                                size_t scratch_bytes, const float** bcoef, long long* bcoef_gs,
+                                                void* stream);
 /* the stem's BatchNorm + ReLU + MaxPool forward: pools relu(x*sc + sh) rounded to bf16
  * (coef = sc[C], sh[C] from gm_bn_fwd_stats_bf16), bit-identical to gm_bn_fwd_train's
  * apply followed by gm_maxpool2d_fwd_bf16, without writing the normalised activation */

@@ -61,6 +61,7 @@ def test_struct_layouts_match_header(tmp_path):
              ("gm_channel_scale", L.ChannelScale), ("gm_gemm", L.Gemm), ("gm_conv_desc", L.ConvDesc),
              ("gm_bn_fwd", L.BnFwd), ("gm_bn_bwd", L.BnBwd), ("gm_pool_desc", L.PoolDesc),
              ("gm_conv_f32", L.ConvF32), ("gm_conv_desc_hw", L.ConvDescHW), ("gm_stem_pack", L.StemPack),
+             ("gm_stem_bn_src", L.StemBnSrc),
              ("gm_wprep", L.WPrep), ("gm_views_norm", L.ViewsNorm), ("gm_gate_state", L.GateState),
              ("gm_gate_state_n", L.GateStateN)]
     # every struct the header declares has a mirror in this list

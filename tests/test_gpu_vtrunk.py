@@ -344,3 +344,48 @@ def test_fused_stem_statistics_match_stats_pass(dev, G, B, H):
         _close(nets[g].bn1.running_mean, ref[g].bn1.running_mean, 1e-5, f"running_mean[{g}]")
         _close(nets[g].bn1.running_var, ref[g].bn1.running_var, 1e-5, f"running_var[{g}]")
         assert int(nets[g].bn1.num_batches_tracked) == int(ref[g].bn1.num_batches_tracked) == 1
+
+
+@pytest.mark.parametrize("G,B,H,W", [(2, 4, 64, 64), (2, 3, 224, 224), (1, 2, 96, 96), (2, 2, 62, 64)])
+def test_stem_wgrad_forms_bn_pool_dy(dev, G, B, H, W):
+    """The stem's weight gradient with dy formed in its loader from the BN + ReLU + max-pool
+    backward's operands (gm_conv2d_wgrad_stem_bn_grouped_bf16: the BN's input gradient never
+    written) against the BN backward's apply pass writing dy + the weight gradient reading it:
+    the same per-element arithmetic and the same MFMA order, so bit-identical; dgamma / dbeta
+    come from the same statistics pass.  Ragged: 62 -> 31 rows (odd pooled tail), Q 32 / 48 / 112."""
+    import ctypes
+    from greedy_multimodal_learning_amd import _lib as L
+    from greedy_multimodal_learning_amd import vtrunk
+    from greedy_multimodal_learning_amd.conv import _desc_hw, _stem_geom
+    from greedy_multimodal_learning_amd.resnet import resnet18
+    P, Q, Sp, Hp, Wp = _stem_geom(H, W, 7, 7, 3)
+    assert L.load().gm_conv2d_wgrad_stem_bn_ok(ctypes.byref(_desc_hw(B, Hp, Wp // 2, 8, 64, 7, Sp, 2, 1, 0, 0)), G)
+    torch.manual_seed(11 + G)
+    nets = [resnet18().to(dev).to(memory_format=CL).train() for _ in range(G)]
+    for n in nets:  # BN parameters away from the identity (signs of gamma both ways)
+        with torch.no_grad():
+            n.bn1.weight.uniform_(-1.5, 1.5)
+            n.bn1.bias.uniform_(-0.5, 0.5)
+    init = [{k: v.clone() for k, v in n.state_dict().items()} for n in nets]
+    x = torch.randn(B, G, 3, H, W, device=dev).bfloat16()
+    res = {}
+    for fused in (True, False):
+        for n, sd in zip(nets, init):
+            n.load_state_dict(sd)
+            for p in n.parameters():
+                p.grad = None
+        old = vtrunk.FUSED_STEM_WGRAD
+        vtrunk.FUSED_STEM_WGRAD = fused
+        try:
+            Y = vtrunk.vstem(x, nets)
+            gY = torch.randn(Y.shape, generator=torch.Generator(device=dev).manual_seed(9), device=dev).bfloat16()
+            Y.backward(gY.contiguous(memory_format=CL))
+        finally:
+            vtrunk.FUSED_STEM_WGRAD = old
+        torch.cuda.synchronize()
+        res[fused] = [(n.conv1.weight.grad.clone(), n.bn1.weight.grad.clone(), n.bn1.bias.grad.clone()) for n in nets]
+    assert L.device_faults(clear=True) == 0
+    for g in range(G):
+        for a, b, name in zip(res[True][g], res[False][g], ("stem dw", "dgamma", "dbeta")):
+            assert torch.equal(a, b), (g, name, float((a - b).abs().max()))
+        assert float(res[True][g][0].abs().max()) > 0

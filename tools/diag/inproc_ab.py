@@ -5,6 +5,9 @@
 ARMSET: layout      - flat parameter layout: model.grad_order vs reverse registration order
         gemm_outer  - the outer-product GEMM kernel on vs off (gm_gemm_set_form bit 9)
         pipe        - k_conv_igemm_ut main loop: PIPE 2 (default) vs PIPE 0 (gm_conv_set_pipe)
+        wgrad_batch - weight-gradient launches handed to the side stream in batches of 8 / 4 / 2
+        stem_wgrad  - the stem weight gradient forming its dy from the BN + pool backward's operands
+                      (vtrunk.FUSED_STEM_WGRAD) vs the BN apply pass writing dy
 """
 import os
 import sys
@@ -34,6 +37,18 @@ def arms(name):
         def setp(p):
             L.check(L.load().gm_conv_set_pipe(p), "pipe")
         return [("pipe2", lambda: setp(-1)), ("pipe0", lambda: setp(0))]
+    if name == "stem_wgrad":
+        from greedy_multimodal_learning_amd import vtrunk
+
+        def setw(on):
+            vtrunk.FUSED_STEM_WGRAD = on
+        return [("fused", lambda: setw(True)), ("apply_pass", lambda: setw(False))]
+    if name == "wgrad_batch":
+        from greedy_multimodal_learning_amd import vtrunk
+
+        def setb(n):
+            vtrunk.WGRAD_BATCH = n
+        return [(f"batch{n}", (lambda n=n: setb(n))) for n in (8, 4, 2)]
     raise SystemExit(f"unknown arm set {name}")
 
 
