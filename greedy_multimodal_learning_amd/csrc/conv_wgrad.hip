@@ -1033,16 +1033,15 @@ __device__ __forceinline__ void stem_bn_dx2(uint4& y0, uint4& y1, int s, int pp,
     y1 = make_uint4(ow[1][0], ow[1][1], ow[1][2], ow[1][3]);
 }
 
-template <int R, int S, bool BN = false>
+template <int R, int S>
 __global__ __launch_bounds__(64 * R) void k_wgrad_stem(WStemArgs a) {
     constexpr int NT = 64 * R;                // threads: one wave per tap row
     constexpr int TC = R * S * 8;             // dw columns per output channel
-    // dy chunks per thread per row (Q <= 128; BN: Q * 8 <= 2 * NT, checked on the host)
-    constexpr int DPT = BN ? 2 : (1024 + NT - 1) / NT;
+    constexpr int DPT = (1024 + NT - 1) / NT;  // dy chunks per thread per row (Q <= 128)
     constexpr int RING = 8;
     static_assert(S * 8 == 32, "k_wgrad_stem: one tap row = one 32-column accumulator block");
     extern __shared__ __attribute__((aligned(16))) uint4 wsm[];
-    char* lds = reinterpret_cast<char*>(wsm);  // [dy tiles 2 x Q*128][ring 8 x upitch] (BN: [pooled 2 x Qp*192][coef])
+    char* lds = reinterpret_cast<char*>(wsm);  // [dy tiles 2 x Q*128][ring 8 x upitch]
     const int t = threadIdx.x, lane = t & 63;
     const int rr = __builtin_amdgcn_readfirstlane(t >> 6);
     const int grp = blockIdx.x / a.splits, wg = blockIdx.x - grp * a.splits;
@@ -1052,108 +1051,46 @@ __global__ __launch_bounds__(64 * R) void k_wgrad_stem(WStemArgs a) {
     char* const ring = lds + 2 * tileb;
     const uint4* const gdy = reinterpret_cast<const uint4*>(a.dy + grp * a.gs_dy) + (size_t)b * a.P * dchunks;
     const uint4* const gx = reinterpret_cast<const uint4*>(a.x + grp * a.gs_x) + (size_t)b * a.ichunks;
-    // BN: two slots of pooled rows (slot k & 1), the coefficients; this image's pooled rows
-    char* const pool_g = ring + RING * a.upitch;
-    char* const pool_i = pool_g + 2 * a.Qp * 128;
-    float* const cf = reinterpret_cast<float*>(pool_i + 2 * a.Qp * 64);
-    const size_t pimg = BN ? (size_t)b * a.Pp * a.Qp * 8 : 0;
-    const uint4* const gpp = BN ? a.gp + grp * a.gs_pool + pimg : nullptr;
-    const uint2* const gpi = BN ? a.pidx + grp * a.gs_pool + pimg : nullptr;
     struct Stage {
         uint4 d[DPT];
         uint4 x;
-        uint4 pg;  // BN: one pooled row's gradient vector and argmax bytes (thread t: vector t)
-        uint2 pi;
     };
-    // dy row pr and input unit u (rows 2u, 2u + 1) -> registers; zeros past the image;
-    // BN: pooled row pk too when pk >= 0
-    auto fetch = [&](int pr, int u, Stage& st, bool with_dy = true, int pk = -1) __attribute__((always_inline)) {
+    // dy row pr and input unit u (rows 2u, 2u + 1) -> registers; zeros past the image
+    auto fetch = [&](int pr, int u, Stage& st, bool with_dy = true) __attribute__((always_inline)) {
 #pragma unroll
         for (int h = 0; h < DPT && with_dy; ++h) {
-            // BN: thread t holds columns 2 (t >> 3) + h of channel chunk t & 7 (a pool column's pair)
-            const int cc = BN ? (2 * (t >> 3) + h) * 8 + (t & 7) : t + NT * h;
+            const int cc = t + NT * h;
             st.d[h] = (cc < dchunks && pr < a.P) ? gdy[(size_t)pr * dchunks + cc] : make_uint4(0, 0, 0, 0);
         }
         const int gi = u * a.uchunks + t;
         st.x = (t < a.uchunks && gi < a.ichunks) ? gx[gi] : make_uint4(0, 0, 0, 0);
-        if constexpr (BN) {
-            if (pk >= 0) {
-                const bool ok = pk < a.Pp && t < a.Qp * 8;
-                const size_t o = (size_t)pk * a.Qp * 8 + t;
-                st.pg = ok ? gpp[o] : make_uint4(0, 0, 0, 0);
-                st.pi = ok ? gpi[o] : make_uint2(0, 0);
-            }
-        }
     };
-    // dy row pr (BN: formed from y row pr and the pooled rows in LDS) into tile pr & 1
-    auto stash_dy = [&](int pr, const Stage& st) __attribute__((always_inline)) {
+    auto stash = [&](int pr, int u, const Stage& st, bool with_dy = true) __attribute__((always_inline)) {
         char* tile = lds + (pr & 1) * tileb;
-        if constexpr (BN) {
-            const int pp = t >> 3, j = t & 7;
-            if (2 * pp < a.Q) {
-                uint4 v0 = st.d[0], v1 = st.d[1];
-                stem_bn_dx2(v0, v1, pr, pp, j, pool_g, pool_i, cf, a.Pp, a.Qp);
-                const int px = 2 * pp;
-                *reinterpret_cast<uint4*>(tile + px * 128 + ((j ^ wswz<128>(px)) << 4)) = v0;
-                *reinterpret_cast<uint4*>(tile + (px + 1) * 128 + ((j ^ wswz<128>(px + 1)) << 4)) = v1;
-            }
-        } else {
 #pragma unroll
-            for (int h = 0; h < DPT; ++h) {
-                const int cc = t + NT * h;
-                if (cc < dchunks) {
-                    const int px = cc >> 3, j = cc & 7;
-                    *reinterpret_cast<uint4*>(tile + px * 128 + ((j ^ wswz<128>(px)) << 4)) = st.d[h];
-                }
+        for (int h = 0; h < DPT && with_dy; ++h) {
+            const int cc = t + NT * h;
+            if (cc < dchunks) {
+                const int px = cc >> 3, j = cc & 7;
+                *reinterpret_cast<uint4*>(tile + px * 128 + ((j ^ wswz<128>(px)) << 4)) = st.d[h];
             }
         }
-    };
-    auto stash_unit = [&](int u, const Stage& st) __attribute__((always_inline)) {
         if (t < a.uchunks) *reinterpret_cast<uint4*>(ring + (u & (RING - 1)) * a.upitch + t * 16) = st.x;
     };
-    auto stash_pool = [&](int pk, const Stage& st) __attribute__((always_inline)) {
-        if (t < a.Qp * 8) {
-            *reinterpret_cast<uint4*>(pool_g + (pk & 1) * a.Qp * 128 + t * 16) = st.pg;
-            *reinterpret_cast<uint2*>(pool_i + (pk & 1) * a.Qp * 64 + t * 8) = st.pi;
-        }
-    };
-    const int k0 = p0 >> 1;  // BN: p0 is even (the host plan's L is)
-    {  // prologue: dy row p0 and units p0 .. p0 + 3 (row p0's window); BN: pooled rows k0, k0 + 1
+    {  // prologue: dy row p0 and units p0 .. p0 + 3 (row p0's window)
         Stage s0, s1;
-        fetch(p0, p0, s0, true, k0);
-        fetch(0, p0 + 1, s1, false, k0 + 1);
-        if constexpr (!BN) stash_dy(p0, s0);
-        stash_unit(p0, s0);
-        stash_unit(p0 + 1, s1);
-        if constexpr (BN) {
-            stash_pool(k0, s0);
-            stash_pool(k0 + 1, s1);
-            if (t < 64) {
-                const float* fc = a.fcoef + grp * a.fcoef_gs;
-                const float* bc = a.bcoef + grp * a.bcoef_gs;
-                cf[t] = fc[t];
-                cf[64 + t] = fc[64 + t];
-                cf[128 + t] = bc[t];
-                cf[192 + t] = bc[64 + t];
-                cf[256 + t] = bc[128 + t];
-            }
-        }
+        fetch(p0, p0, s0, true);
+        fetch(0, p0 + 1, s1, false);
+        stash(p0, p0, s0, true);
+        stash(0, p0 + 1, s1, false);
         fetch(0, p0 + 2, s0, false);
         fetch(0, p0 + 3, s1, false);
-        stash_unit(p0 + 2, s0);
-        stash_unit(p0 + 3, s1);
-        if constexpr (BN) {
-            __syncthreads();  // pooled rows k0, k0 + 1 and the coefficients are in LDS
-            stash_dy(p0, s0);
-        }
+        stash(0, p0 + 2, s0, false);
+        stash(0, p0 + 3, s1, false);
     }
-    // iteration p stashes dy row p + 1 and unit p + 4, then fetches row p + 3, unit p + 6.  BN:
-    // pooled row j is fetched in iteration 2j - 5 and stashed in iteration 2j - 3 (both odd: stage
-    // sb), one iteration before row 2j - 1 - its first reader - is formed, after the last reader of
-    // row j - 2 (its slot) - row 2j - 3, formed in iteration 2j - 4
-    Stage sa, sb;
+    Stage sa, sb;  // iteration p stashes dy row p + 1 and unit p + 4, then fetches row p + 3, unit p + 6
     fetch(p0 + 1, p0 + 4, sa);
-    fetch(p0 + 2, p0 + 5, sb, true, k0 + 2);
+    fetch(p0 + 2, p0 + 5, sb);
 
     floatx16 acc[2];
 #pragma unroll
@@ -1166,14 +1103,10 @@ __global__ __launch_bounds__(64 * R) void k_wgrad_stem(WStemArgs a) {
     const int krow = 8 * (g4 >> 1) + q4, col = 16 * (g4 & 1) + 4 * p4;
     auto rowoff = [](int row, int ch) { return row * 128 + ((((ch >> 3) ^ wswz<128>(row))) << 4) + (ch & 7) * 2; };
     const int nks = a.Q >> 4;
-    auto iteration = [&](int p, Stage& st, auto odd) __attribute__((always_inline)) {
-        constexpr bool ODD = decltype(odd)::value;
+    auto iteration = [&](int p, Stage& st) __attribute__((always_inline)) {
         __syncthreads();  // row p's dy tile and units p .. p + 3 are in LDS; row p - 1's reads are done
-        // (the unit and the pooled row first: their registers are free before dy is formed)
-        stash_unit(p + 4, st);
-        if constexpr (BN && ODD) stash_pool((p + 3) >> 1, st);
-        stash_dy(p + 1, st);
-        fetch(p + 3, p + 6, st, true, (BN && ODD) ? (p + 5) >> 1 : -1);
+        stash(p + 1, p + 4, st);
+        fetch(p + 3, p + 6, st);
         const char* tile = lds + (p & 1) * tileb;
         const char* xrow = ring + ((p + (rr >> 1)) & (RING - 1)) * a.upitch + (rr & 1) * a.Wi * 16;
         for (int ks = 0; ks < nks; ++ks) {
@@ -1189,8 +1122,8 @@ __global__ __launch_bounds__(64 * R) void k_wgrad_stem(WStemArgs a) {
         }
     };
     for (int p = p0; p < p1; p += 2) {
-        iteration(p, sa, std::false_type{});
-        if (p + 1 < p1) iteration(p + 1, sb, std::true_type{});
+        iteration(p, sa);
+        if (p + 1 < p1) iteration(p + 1, sb);
     }
     // the partial: dw[channel][rr * 32 + (s, c)], lane -> column, registers -> channels
     float* out = a.part + ((size_t)grp * a.splits + wg) * (64 * TC) + rr * 32 + (lane & 31);
@@ -1200,6 +1133,198 @@ __global__ __launch_bounds__(64 * R) void k_wgrad_stem(WStemArgs a) {
         for (int e = 0; e < 16; ++e) out[(size_t)(nb * 32 + 8 * (e >> 2) + 4 * (lane >> 5) + (e & 3)) * TC] = acc[nb][e];
 }
 
+// k_wgrad_stem_bn: k_wgrad_stem with dy formed in the loader (stem_bn_dx2 above) - the stem's
+// BatchNorm + ReLU + max-pool backward is never written (gm_conv2d_wgrad_stem_bn_grouped_bf16).
+// Forming dy costs ~450 VALU instructions per wave and row, so the MFMA waves of ONE workgroup
+// would serialise it with their MFMAs (barrier per row); here a workgroup is FOUR waves (tap rows
+// {2w, 2w + 1}, wave 3 row 6 only: the busiest SIMD issues the same 28 MFMAs per row as
+// k_wgrad_stem's), so two workgroups fit a CU (81 KB of LDS each, 2 waves per SIMD: up to 256
+// VGPRs) and one's dy forming overlaps the other's MFMAs.  The A fragments (dy) of a k-slice feed
+// both of a wave's tap rows.  Rows are prefetched three iterations ahead.  Same MFMA operands and
+// order as k_wgrad_stem on the same tiles: bit-identical partials.
+template <int R, int S>
+__global__ __launch_bounds__(256) void k_wgrad_stem_bn(WStemArgs a) {
+    constexpr int NT = 256;
+    constexpr int TC = R * S * 8;
+    constexpr int RING = 8;
+    static_assert(S * 8 == 32 && R == 7, "k_wgrad_stem_bn: the 7 x 4 pixel-pair stem");
+    extern __shared__ __attribute__((aligned(16))) uint4 wsm[];
+    char* lds = reinterpret_cast<char*>(wsm);  // [dy tiles 2][unit ring 8][pooled 2 x (grad, argmax)][coef]
+    const int t = threadIdx.x, lane = t & 63;
+    const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int grp = blockIdx.x / a.splits, wg = blockIdx.x - grp * a.splits;
+    const int b = wg / a.cpi, c = wg - b * a.cpi;
+    const int p0 = c * a.L, p1 = min(a.P, p0 + a.L);
+    const int tileb = a.Q * 128, dchunks = a.Q * 8;
+    const int npair = a.Q * 4;   // (column pair, channel chunk) items per row, <= 2 NT (host)
+    const int npool = a.Qp * 8;  // pooled vectors per row, <= 2 NT (host)
+    char* const ring = lds + 2 * tileb;
+    char* const pool_g = ring + RING * a.upitch;
+    char* const pool_i = pool_g + 2 * a.Qp * 128;
+    float* const cf = reinterpret_cast<float*>(pool_i + 2 * a.Qp * 64);
+    const uint4* const gy = reinterpret_cast<const uint4*>(a.dy + grp * a.gs_dy) + (size_t)b * a.P * dchunks;
+    const uint4* const gx = reinterpret_cast<const uint4*>(a.x + grp * a.gs_x) + (size_t)b * a.ichunks;
+    const size_t pimg = (size_t)b * a.Pp * a.Qp * 8;
+    const uint4* const gpp = a.gp + grp * a.gs_pool + pimg;
+    const uint2* const gpi = a.pidx + grp * a.gs_pool + pimg;
+    const int cg = t & 7;  // the channel chunk of every item of this thread (NT % 8 == 0)
+    struct Stage {
+        uint4 y[2][2];  // item h = t + NT h: columns 2 pp, 2 pp + 1 of chunk cg (pp = item >> 3)
+        uint4 x;        // unit chunk t
+    };
+    struct Pool {
+        uint4 g[2];  // pooled vector t + NT h
+        uint2 i[2];
+    };
+    auto fetch = [&](int pr, int u, Stage& st) __attribute__((always_inline)) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int it = t + NT * h;
+            const bool ok = it < npair && pr < a.P;
+            const size_t o = (size_t)pr * dchunks + (size_t)(it >> 3) * 16 + cg;
+            st.y[h][0] = ok ? gy[o] : make_uint4(0, 0, 0, 0);
+            st.y[h][1] = ok ? gy[o + 8] : make_uint4(0, 0, 0, 0);
+        }
+        const int gi = u * a.uchunks + t;
+        st.x = (t < a.uchunks && gi < a.ichunks) ? gx[gi] : make_uint4(0, 0, 0, 0);
+    };
+    auto fetch_pool = [&](int pk, Pool& pq) __attribute__((always_inline)) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int v = t + NT * h;
+            const bool ok = pk < a.Pp && v < npool;
+            const size_t o = (size_t)pk * npool + v;
+            pq.g[h] = ok ? gpp[o] : make_uint4(0, 0, 0, 0);
+            pq.i[h] = ok ? gpi[o] : make_uint2(0, 0);
+        }
+    };
+    auto stash_pool = [&](int pk, const Pool& pq) __attribute__((always_inline)) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int v = t + NT * h;
+            if (v < npool) {
+                *reinterpret_cast<uint4*>(pool_g + (pk & 1) * a.Qp * 128 + v * 16) = pq.g[h];
+                *reinterpret_cast<uint2*>(pool_i + (pk & 1) * a.Qp * 64 + v * 8) = pq.i[h];
+            }
+        }
+    };
+    auto stash_unit = [&](int u, const Stage& st) __attribute__((always_inline)) {
+        if (t < a.uchunks) *reinterpret_cast<uint4*>(ring + (u & (RING - 1)) * a.upitch + t * 16) = st.x;
+    };
+    // dy row pr from y row pr (registers) and the pooled rows in LDS, into tile pr & 1
+    auto stash_dy = [&](int pr, const Stage& st) __attribute__((always_inline)) {
+        char* tile = lds + (pr & 1) * tileb;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int it = t + NT * h;
+            if (it < npair) {
+                const int pp = it >> 3;
+                uint4 v0 = st.y[h][0], v1 = st.y[h][1];
+                stem_bn_dx2(v0, v1, pr, pp, cg, pool_g, pool_i, cf, a.Pp, a.Qp);
+                const int px = 2 * pp;
+                *reinterpret_cast<uint4*>(tile + px * 128 + ((cg ^ wswz<128>(px)) << 4)) = v0;
+                *reinterpret_cast<uint4*>(tile + (px + 1) * 128 + ((cg ^ wswz<128>(px + 1)) << 4)) = v1;
+            }
+        }
+    };
+    const int k0 = p0 >> 1;  // p0 is even (the host plan's L is)
+    Pool pq;
+    {  // prologue: units p0 .. p0 + 3, pooled rows k0, k0 + 1, the coefficients; then dy row p0
+        Stage s0, s1;
+        fetch(p0, p0, s0);
+        fetch(a.P, p0 + 1, s1);
+        fetch_pool(k0, pq);
+        stash_unit(p0, s0);
+        stash_unit(p0 + 1, s1);
+        stash_pool(k0, pq);
+        fetch_pool(k0 + 1, pq);
+        if (t < 64) {
+            const float* fc = a.fcoef + grp * a.fcoef_gs;
+            const float* bc = a.bcoef + grp * a.bcoef_gs;
+            cf[t] = fc[t];
+            cf[64 + t] = fc[64 + t];
+            cf[128 + t] = bc[t];
+            cf[192 + t] = bc[64 + t];
+            cf[256 + t] = bc[128 + t];
+        }
+        stash_pool(k0 + 1, pq);
+        fetch(a.P, p0 + 2, s1);
+        stash_unit(p0 + 2, s1);
+        fetch(a.P, p0 + 3, s1);
+        stash_unit(p0 + 3, s1);
+        __syncthreads();  // pooled rows k0, k0 + 1 and the coefficients are in LDS
+        stash_dy(p0, s0);
+    }
+    // iteration p stashes dy row p + 1 and unit p + 4, then fetches row p + 4, unit p + 7.  Pooled
+    // row j is fetched in iteration 2j - 5 and stashed in iteration 2j - 3 (odd iterations, one
+    // register set), one iteration before row 2j - 1 - its first reader - is formed, after the
+    // last reader of row j - 2 (its slot) - row 2j - 3, formed in iteration 2j - 4
+    Stage sa, sb, sc;
+    fetch(p0 + 1, p0 + 4, sa);
+    fetch(p0 + 2, p0 + 5, sb);
+    fetch(p0 + 3, p0 + 6, sc);
+    fetch_pool(k0 + 2, pq);
+
+    floatx16 acc[2][2];  // [tap row of the wave][channel block]
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[r][i][e] = 0.f;
+    const bool two = w < 3;  // wave 3: tap row 6 only
+    const int g4 = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+    const int krow = 8 * (g4 >> 1) + q4, col = 16 * (g4 & 1) + 4 * p4;
+    auto rowoff = [](int row, int ch) { return row * 128 + ((((ch >> 3) ^ wswz<128>(row))) << 4) + (ch & 7) * 2; };
+    const int nks = a.Q >> 4;
+    auto iteration = [&](int p, Stage& st) __attribute__((always_inline)) {
+        __syncthreads();  // row p's dy tile and units p .. p + 3 are in LDS; row p - 1's reads are done
+        stash_unit(p + 4, st);
+        if (p & 1) {
+            stash_pool((p + 3) >> 1, pq);
+            fetch_pool((p + 5) >> 1, pq);
+        }
+        stash_dy(p + 1, st);
+        fetch(p + 4, p + 7, st);
+        const char* tile = lds + (p & 1) * tileb;
+        // tap rows 2w, 2w + 1 read input rows 2(p + w), 2(p + w) + 1: one unit
+        const char* xrow = ring + ((p + w) & (RING - 1)) * a.upitch;
+        for (int ks = 0; ks < nks; ++ks) {
+            const int px = 16 * ks + krow;
+            const bf16x8 A0 = tr_frag(reinterpret_cast<const uint16_t*>(tile + rowoff(px, col)),
+                                      reinterpret_cast<const uint16_t*>(tile + rowoff(px + 4, col)));
+            const bf16x8 A1 = tr_frag(reinterpret_cast<const uint16_t*>(tile + rowoff(px, 32 + col)),
+                                      reinterpret_cast<const uint16_t*>(tile + rowoff(px + 4, 32 + col)));
+            const char* xb = xrow + (px + (col >> 3)) * 16 + (col & 7) * 2;
+            const bf16x8 B0 = tr_frag(reinterpret_cast<const uint16_t*>(xb), reinterpret_cast<const uint16_t*>(xb + 64));
+            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B0, acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, B0, acc[0][1], 0, 0, 0);
+            if (two) {
+                const char* xb1 = xb + a.Wi * 16;
+                const bf16x8 B1 = tr_frag(reinterpret_cast<const uint16_t*>(xb1),
+                                          reinterpret_cast<const uint16_t*>(xb1 + 64));
+                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B1, acc[1][0], 0, 0, 0);
+                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, B1, acc[1][1], 0, 0, 0);
+            }
+        }
+    };
+    for (int p = p0; p < p1; p += 3) {
+        iteration(p, sa);
+        if (p + 1 < p1) iteration(p + 1, sb);
+        if (p + 2 < p1) iteration(p + 2, sc);
+    }
+    // the partial: dw[channel][rr * 32 + (s, c)] for the wave's tap rows rr = 2w (+ 1)
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        if (r == 1 && !two) break;
+        float* out = a.part + ((size_t)grp * a.splits + wg) * (64 * TC) + (2 * w + r) * 32 + (lane & 31);
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+            for (int e = 0; e < 16; ++e)
+                out[(size_t)(nb * 32 + 8 * (e >> 2) + 4 * (lane >> 5) + (e & 3)) * TC] = acc[r][nb][e];
+    }
+}
 // dw[i] (+)= sum over splits of part[s][i] in ONE launch, for the uncropped case (Cp == Cr,
 // every layer but the RGB stem).  A wave covers 64/R float4 columns with R split lanes per
 // column (lane r sums splits r, r+R, ..., eight loads in flight), and the R lane sums are
@@ -1518,16 +1643,17 @@ static WStemArgs stem_args(const gm_conv_desc_hw* d, const StemWPlan& sw, const 
 template <bool BN>
 static int launch_wgrad_stem(const WStemArgs& s, const StemWPlan& sw, int G, size_t lds, hipStream_t st) {
     static size_t granted = 0;
+    const void* fn = BN ? (const void*)k_wgrad_stem_bn<7, 4> : (const void*)k_wgrad_stem<7, 4>;
     if (lds > granted) {
-        if (hipFuncSetAttribute((const void*)k_wgrad_stem<7, 4, BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)lds) != hipSuccess) {
+        if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
             set_error("k_wgrad_stem: %zu B of LDS refused", lds);
             return GM_E_UNSUP;
         }
         granted = lds;
     }
-    k_wgrad_stem<7, 4, BN><<<sw.splits * G, 448, lds, st>>>(s);
-    return check_launch(BN ? "k_wgrad_stem<bn>" : "k_wgrad_stem");
+    if (BN) k_wgrad_stem_bn<7, 4><<<sw.splits * G, 256, lds, st>>>(s);
+    else k_wgrad_stem<7, 4><<<sw.splits * G, 448, lds, st>>>(s);
+    return check_launch(BN ? "k_wgrad_stem_bn" : "k_wgrad_stem");
 }
 
 // the split sum of every split weight-gradient kernel: k_wgrad_sum with R split lanes per
@@ -1703,8 +1829,10 @@ extern "C" int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, con
 // The stem's weight gradient with dy formed in the loader (greedymml.h: the stem BatchNorm +
 // ReLU + max-pool backward, never written): k_wgrad_stem<7, 4, true> on the k_wgrad_stem plan
 static bool stem_bn_plan(const gm_conv_desc_hw* d, int G, StemWPlan& sw) {
-    return d && G >= 1 && G <= 64 && stemw_plan(d, G, sw) && sw.Q * 8 <= 2 * 448 && ((sw.Q + 1) / 2) * 8 <= 448 &&
-           !(sw.L & 1);
+    // k_wgrad_stem_bn: two (column pair, chunk) items and two pooled vectors per thread, a unit
+    // chunk per thread
+    return d && G >= 1 && G <= 64 && stemw_plan(d, G, sw) && sw.Q * 4 <= 2 * 256 && ((sw.Q + 1) / 2) * 8 <= 2 * 256 &&
+           2 * d->W <= 256 && !(sw.L & 1);
 }
 
 extern "C" int gm_conv2d_wgrad_stem_bn_ok(const gm_conv_desc_hw* d, int G) {
