@@ -5,6 +5,7 @@
 ARMSET: layout      - flat parameter layout: model.grad_order vs reverse registration order
         gemm_outer  - the outer-product GEMM kernel on vs off (gm_gemm_set_form bit 9)
         pipe        - k_conv_igemm_ut main loop: PIPE 2 (default) vs PIPE 0 (gm_conv_set_pipe)
+        bind        - resident batches bound as graph inputs vs copied into the static buffers (bench args)
         wgrad_batch - weight-gradient launches handed to the side stream in batches of 8 / 4 / 2
         stem_wgrad  - the stem weight gradient forming its dy from the BN + pool backward's operands
                       (vtrunk.FUSED_STEM_WGRAD) vs the BN apply pass writing dy
@@ -49,6 +50,8 @@ def arms(name):
         def setb(n):
             vtrunk.WGRAD_BATCH = n
         return [(f"batch{n}", (lambda n=n: setb(n))) for n in (8, 4, 2)]
+    if name == "bind":
+        return [("bound", lambda: None), ("copied", lambda: None)]
     raise SystemExit(f"unknown arm set {name}")
 
 
@@ -61,7 +64,7 @@ def main():
         for arm, apply in sets:
             apply()
             print(f"round {r} {arm}", flush=True)
-            sys.argv = ["bench.py"] + extra
+            sys.argv = ["bench.py"] + extra + (["--copy-inputs"] if arm == "copied" else [])
             bench.main()
     sets[0][1]()
 
