@@ -3225,7 +3225,7 @@ extern "C" int gm_conv_weight_prep_bf16(const float* w, int K, int RS, int C, in
 // along c, the bf16 KRSC copy written along c, the tile transposed through LDS so the
 // [C][RS][K] dgrad copy is also written along k.
 __global__ __launch_bounds__(256) void k_wprep_multi(const gm_wprep* __restrict__ tab, int n) {
-    __shared__ uint16_t tile[64][66];
+    __shared__ uint16_t tile[64][66];  // 132-B rows: the transposed column reads are conflict-free
     const int blk = blockIdx.x;
     int lo = 0, hi = n - 1;  // last entry whose tile_start <= blk (uniform: scalar loads)
     while (lo < hi) {
@@ -3242,20 +3242,60 @@ __global__ __launch_bounds__(256) void k_wprep_multi(const gm_wprep* __restrict_
     const int ci = r % tc;
     r /= tc;
     const int tap = r % RS, k0 = (r / RS) * 64, c0 = ci * 64;
-    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
-        const int kk = i >> 6, cc = i & 63;
-        const int k = k0 + kk, c = c0 + cc;
-        const float v = (k < K && c < C) ? w[((size_t)k * RS + tap) * C + c] : 0.f;
-        const uint16_t h = gm::Elem<uint16_t>::f2bf(v);
-        if (k < K && c < Cp) wb[((size_t)k * RS + tap) * Cp + c] = h;
-        tile[kk][cc] = h;
+    // 8 consecutive elements per thread and step: two float4 loads along c, one 16-B bf16 store
+    // (vector forms where the whole run is in range and aligned, element-wise otherwise)
+    const bool vc = (C & 3) == 0 && (Cp & 7) == 0 && ((uintptr_t)w & 15) == 0 && ((uintptr_t)wb & 15) == 0;
+    for (int i = threadIdx.x; i < 64 * 8; i += 256) {
+        const int kk = i >> 3, cq = (i & 7) * 8;
+        const int k = k0 + kk, c = c0 + cq;
+        uint16_t h[8];
+        const float* src = w + ((size_t)k * RS + tap) * C + c;
+        if (vc && k < K && c + 8 <= C) {
+            const float4 u0 = reinterpret_cast<const float4*>(src)[0], u1 = reinterpret_cast<const float4*>(src)[1];
+            const float f[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) h[j] = gm::Elem<uint16_t>::f2bf(f[j]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) h[j] = gm::Elem<uint16_t>::f2bf((k < K && c + j < C) ? src[j] : 0.f);
+        }
+        if (k < K) {
+            uint16_t* dst = wb + ((size_t)k * RS + tap) * Cp + c;
+            if (vc && c + 8 <= Cp) {
+                *reinterpret_cast<uint4*>(dst) =
+                    make_uint4(h[0] | (uint32_t)h[1] << 16, h[2] | (uint32_t)h[3] << 16, h[4] | (uint32_t)h[5] << 16,
+                               h[6] | (uint32_t)h[7] << 16);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (c + j < Cp) dst[j] = h[j];
+            }
+        }
+        uint32_t* row = reinterpret_cast<uint32_t*>(&tile[kk][cq]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) row[j] = h[2 * j] | (uint32_t)h[2 * j + 1] << 16;
     }
     if (!wt) return;
     __syncthreads();
-    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
-        const int cc = i >> 6, kk = i & 63;
-        const int k = k0 + kk, c = c0 + cc;
-        if (k < K && c < Cp) wt[((size_t)c * RS + tap) * K + k] = tile[kk][cc];
+    // the [C][RS][K] copy: 8 consecutive k of one c per thread and step, one 16-B store
+    const bool vk = (K & 7) == 0 && ((uintptr_t)wt & 15) == 0;
+    for (int i = threadIdx.x; i < 64 * 8; i += 256) {
+        const int cc = i >> 3, kq = (i & 7) * 8;
+        const int k = k0 + kq, c = c0 + cc;
+        if (c >= Cp) continue;
+        uint16_t h[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) h[j] = tile[kq + j][cc];
+        uint16_t* dst = wt + ((size_t)c * RS + tap) * K + k;
+        if (vk && k + 8 <= K) {
+            *reinterpret_cast<uint4*>(dst) =
+                make_uint4(h[0] | (uint32_t)h[1] << 16, h[2] | (uint32_t)h[3] << 16, h[4] | (uint32_t)h[5] << 16,
+                           h[6] | (uint32_t)h[7] << 16);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (k + j < K) dst[j] = h[j];
+        }
     }
 }
 

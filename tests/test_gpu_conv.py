@@ -113,8 +113,10 @@ def test_weight_prep_multi_matches_single(dev):
     net = torch.nn.Sequential(GMConv2d(3, 64, 7, stride=2, padding=3, bias=False),
                               GMConv2d(64, 128, 3, padding=1, bias=False),
                               GMConv2d(128, 256, 1, stride=2, bias=False),
-                              GMConv2d(256, 72, 3, padding=1, bias=False)).to(dev).to(memory_format=CL)
-    assert net[0].uses_pair_stem() and len(WeightPrep(net).copies) == 3  # the pair-view stem packs its own
+                              GMConv2d(256, 72, 3, padding=1, bias=False),
+                              GMConv2d(72, 70, 1, bias=False)).to(dev).to(memory_format=CL)
+    # (ragged tiles: K 72 and 70 - element-wise transposed stores -, C 3 - element-wise loads)
+    assert net[0].uses_pair_stem() and len(WeightPrep(net).copies) == 4  # the pair-view stem packs its own
     net[0].pair_stem = False
     wp = WeightPrep(net)
     wp.run()
