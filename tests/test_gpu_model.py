@@ -195,7 +195,7 @@ def test_guided_trace_vs_reference(golden, dev):
             opt.step()
             logs = {}
             gate.on_batch_end(step, logs)
-            rows.append((float(loss), logs["d_BDR"], logs["curation_mode"],
+            rows.append((float(loss.detach()), logs["d_BDR"], logs["curation_mode"],
                          -1 if logs["caring_modality"] is None else logs["caring_modality"], *accs))
         m.eval()
         with torch.no_grad():
