@@ -65,6 +65,8 @@ EXPORTS = {
     "gm_group_sumsq_scratch": (c_size_t, [ctypes.c_longlong]),
     "gm_group_sumsq": (c_int, [c_void_p, c_int, ctypes.c_longlong, c_int, c_float, c_float,
                                c_void_p, c_void_p, c_size_t, c_void_p]),
+    "gm_group_sumsq_gate": (c_int, [c_void_p, c_int, ctypes.c_longlong, c_int, c_float, c_float,
+                                    c_void_p, c_void_p, c_size_t, c_void_p, c_int, c_void_p]),
 }
 
 _lib = None

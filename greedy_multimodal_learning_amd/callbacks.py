@@ -158,16 +158,21 @@ class GroupNorms:
             self._scratch = torch.empty(need, dtype=torch.uint8, device=self.device)
             self._out = torch.empty(2 * self.ngroups, dtype=torch.float64, device=self.device)
 
-    def sums(self, grad_scale=1.0, lr=0.0):
+    def sums(self, grad_scale=1.0, lr=0.0, gate=None, gate_n=False):
+        """The step's group sums (and the fused SGD when lr != 0); gate (a device gm_gate_state /
+        gm_gate_state_n tensor): the on-device gate's step runs in the same finalize launch."""
         L.load()
         if not self.params[0].is_cuda:
             raise L.GreedyMMLError("group norms run on HIP devices only (no CPU fallback)")
         self._build()
         out = torch.empty(2 * self.ngroups, dtype=torch.float64, device=self.device)
-        L.check(L.load().gm_group_sumsq(self._table.data_ptr(), len(self.params), self.total,
-                                        self.ngroups, float(grad_scale), float(lr), out.data_ptr(),
-                                        self._scratch.data_ptr(), self._scratch.numel(),
-                                        L.stream_of(self.device)), "gm_group_sumsq")
+        args = (self._table.data_ptr(), len(self.params), self.total, self.ngroups, float(grad_scale), float(lr),
+                out.data_ptr(), self._scratch.data_ptr(), self._scratch.numel())
+        if gate is not None:
+            L.check(L.load().gm_group_sumsq_gate(*args, gate.data_ptr(), int(bool(gate_n)),
+                                                 L.stream_of(self.device)), "gm_group_sumsq_gate")
+        else:
+            L.check(L.load().gm_group_sumsq(*args, L.stream_of(self.device)), "gm_group_sumsq")
         return out
 
 

@@ -11,6 +11,7 @@
 // pass adds the rows in fixed order.  HBM bytes/step: 8*N (read p, g) without the
 // update, 12*N with it (read p, g; write p).  Deterministic.
 #include "gm_common.h"
+#include "gate_rule.h"
 
 namespace gm {
 
@@ -206,9 +207,13 @@ __global__ __launch_bounds__(256) void k_group_sumsq_runs(const gm_tensor* __res
 // the C2 step for 1451 rows).  Then per column 32 fixed partial sums of its slots and
 // their fixed-order total => deterministic.  (Threads t >= S hold 0 and take no part.)
 constexpr int kFinT = 1024;
+// gate (optional): the on-device gate's state - gm_gate_state (gate_n 0) or gm_gate_state_n (1) -
+// whose step rule thread 0 applies to the finished sums (gm_group_sumsq_gate: no gate launch)
 __global__ __launch_bounds__(kFinT) void k_group_finalize(const double* __restrict__ rows, int nrows,
-                                                          int ngroups, double* __restrict__ out) {
+                                                          int ngroups, double* __restrict__ out,
+                                                          void* gate = nullptr, int gate_n = 0) {
     __shared__ double s[kFinT];
+    __shared__ double tot_s[2 * kMaxGroups];
     __shared__ double part[32 * 2 * kMaxGroups];
     const int w = 2 * ngroups;
     const int S = (kFinT / w) * w, R = S / w;  // R row slots per column
@@ -240,6 +245,13 @@ __global__ __launch_bounds__(kFinT) void k_group_finalize(const double* __restri
         double tot = 0.0;
         for (int q = 0; q < P; ++q) tot += part[q * w + t];
         out[t] = tot;
+        tot_s[t] = tot;
+    }
+    if (gate == nullptr) return;  // (uniform)
+    __syncthreads();
+    if (t == 0) {
+        if (gate_n) gate_strong_rule_n(tot_s, static_cast<gm_gate_state_n*>(gate));
+        else gate_strong_rule(tot_s, static_cast<gm_gate_state*>(gate));
     }
 }
 
@@ -253,8 +265,8 @@ extern "C" size_t gm_group_sumsq_scratch(long long total) {
     return (size_t)nb * 2 * kMaxGroups * sizeof(double);
 }
 
-extern "C" int gm_group_sumsq(const gm_tensor* table, int nt, long long total, int ngroups, float gscale,
-                              float lr, double* out, void* scratch, size_t scratch_bytes, void* stream) {
+static int group_sumsq(const gm_tensor* table, int nt, long long total, int ngroups, float gscale, float lr,
+                       double* out, void* scratch, size_t scratch_bytes, void* gate, int gate_n, void* stream) {
     GM_REQUIRE(table && nt >= 1 && total >= 1, "group_sumsq: empty tensor table");
     GM_REQUIRE(ngroups >= 1 && ngroups <= kMaxGroups, "group_sumsq: ngroups must be 1..%d", kMaxGroups);
     GM_REQUIRE(out, "group_sumsq: null output");
@@ -278,6 +290,23 @@ extern "C" int gm_group_sumsq(const gm_tensor* table, int nt, long long total, i
     }
     int rc = check_launch("k_group_sumsq");
     if (rc) return rc;
-    k_group_finalize<<<1, kFinT, 0, st>>>(rows, (int)nb, ngroups, out);
+    k_group_finalize<<<1, kFinT, 0, st>>>(rows, (int)nb, ngroups, out, gate, gate_n);
     return check_launch("k_group_finalize");
+}
+
+extern "C" int gm_group_sumsq(const gm_tensor* table, int nt, long long total, int ngroups, float gscale,
+                              float lr, double* out, void* scratch, size_t scratch_bytes, void* stream) {
+    return group_sumsq(table, nt, total, ngroups, gscale, lr, out, scratch, scratch_bytes, nullptr, 0, stream);
+}
+
+extern "C" int gm_group_sumsq_gate(const gm_tensor* table, int nt, long long total, int ngroups, float gscale,
+                                   float lr, double* out, void* scratch, size_t scratch_bytes, void* gate,
+                                   int gate_n, void* stream) {
+    GM_REQUIRE(gate, "group_sumsq_gate: null gate state");
+    // (main, bypass) groups per branch: 4 for the two-branch gate, 2 nb for the N-branch one (nb in
+    // the state: the rule reads 4 nb sums)
+    GM_REQUIRE(gate_n ? (ngroups >= 4 && ngroups % 2 == 0) : ngroups == 4,
+               "group_sumsq_gate: %d groups do not match the %s gate", ngroups, gate_n ? "N-branch" : "two-branch");
+    return group_sumsq(table, nt, total, ngroups, gscale, lr, out, scratch, scratch_bytes, gate, gate_n ? 1 : 0,
+                       stream);
 }

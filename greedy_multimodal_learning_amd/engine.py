@@ -416,14 +416,13 @@ class BalancedStep:
         self.residency = L.set_residency(streams=max(1, streams), sharers=max(1, sharers), reserved_cus=reserved)
 
     # ---------------- on-device gate ----------------
-    def _gate_step(self, sums):
-        from . import _lib as L
-        if self.gate_n:
-            L.check(L.load().gm_gate_strong_step_n(sums.data_ptr(), self.gate_state.data_ptr(),
-                                                   L.stream_of(self.device)), "gm_gate_strong_step_n")
-            return
-        L.check(L.load().gm_gate_strong_step(sums.data_ptr(), self.gate_state.data_ptr(),
-                                             L.stream_of(self.device)), "gm_gate_strong_step")
+    def _sums_and_gate(self):
+        """The fused norms+SGD pass; with the on-device gate its step rides in the same finalize
+        launch (gm_group_sumsq_gate)."""
+        if self.device_gate:
+            return self.norms.sums(grad_scale=1.0 / self.world, lr=self.lr, gate=self.gate_state,
+                                   gate_n=self.gate_n)
+        return self.norms.sums(grad_scale=1.0 / self.world, lr=self.lr)
 
     def gate_struct(self):
         """The device gate state as its ctypes mirror (GateState / GateStateN); a host sync."""
@@ -563,9 +562,7 @@ class BalancedStep:
                                      else torch.cuda.current_device(), eager_sid)
                 loss, outs = self._fwd_bwd(*(inputs or self._static))
                 loss = loss.detach()
-                sums = None if (dp and not inline) else self.norms.sums(grad_scale=1.0 / self.world, lr=self.lr)
-                if sums is not None and self.device_gate:
-                    self._gate_step(sums)
+                sums = None if (dp and not inline) else self._sums_and_gate()
         finally:
             if dp:
                 self.buckets.deferred = False
@@ -650,9 +647,7 @@ class BalancedStep:
             capture_replayed()
             if self.buckets is not None and not self.graph_collectives:
                 self.buckets.reduce_all()
-                sums = self.norms.sums(grad_scale=1.0 / self.world, lr=self.lr)
-                if self.device_gate:
-                    self._gate_step(sums)
+                sums = self._sums_and_gate()
             for m in self._mmtms:
                 m.step += 1
                 m._step_mirror = m.step
@@ -668,9 +663,7 @@ class BalancedStep:
             ev0 = torch.cuda.Event(enable_timing=True)
             ev1 = torch.cuda.Event(enable_timing=True)
             ev0.record()
-        sums = self.norms.sums(grad_scale=1.0 / self.world, lr=self.lr)
-        if self.device_gate:
-            self._gate_step(sums)
+        sums = self._sums_and_gate()
         if t is not None:
             ev1.record()
             t.append((ev0, ev1))

@@ -308,6 +308,11 @@ int gm_xent_bwd(const float* logits, const float* lse, int nbranch, int B, int N
 int gm_group_sumsq(const gm_tensor* table, int ntensors, long long total_elems, int ngroups,
                    float grad_scale, float lr, double* out, void* scratch, size_t scratch_bytes,
                    void* stream);
+/* gm_group_sumsq + the on-device gate's step (gm_gate_strong_step / _n) in the same finalize
+ * launch: gate -> gm_gate_state (gate_n 0, ngroups 4) or gm_gate_state_n (gate_n 1, ngroups 2 nb);
+ * identical sums and state to the two calls */
+int gm_group_sumsq_gate(const gm_tensor* table, int nt, long long total, int ngroups, float gscale, float lr,
+                        double* out, void* scratch, size_t scratch_bytes, void* gate, int gate_n, void* stream);
 
 /* ---------------------------------------------------------------------------
  * ResNet trunk convolutions (torchvision resnet18/50 Conv2d, bias=False; called

@@ -131,3 +131,57 @@ def test_n_branch_gate_kernel_rule():
     r = L.GateStateN.from_buffer_copy(state.cpu().numpy().tobytes())
     assert r.d_bdr == pytest.approx(-math.log10(4.0), abs=1e-12)
     assert r.curation_mode == 1 and r.caring == 1
+
+
+@pytest.mark.parametrize("nb", [2, 5])
+def test_group_sumsq_gate_matches_two_launches(nb):
+    """gm_group_sumsq_gate (the gate's step rule run by the group-sum finalize's thread 0, no gate
+    launch) == gm_group_sumsq followed by gm_gate_strong_step / _n: the same sums, the same
+    updated parameters (fused SGD) and a bit-identical gate state, over several steps (the
+    two-branch state for nb = 2 through the 4-group table, the N-branch state for nb = 5)."""
+    from greedy_multimodal_learning_amd import _lib as L
+    from greedy_multimodal_learning_amd.callbacks import GroupNorms
+    dev = torch.device("cuda:0")
+    torch.manual_seed(nb)
+    branches = [f"net_view_{i}" for i in range(nb)]
+    mods = [f"mod{i}" for i in range(nb)]
+    names = [f"net_view_{i}.conv{k}.weight" for i in range(nb) for k in range(3)] + \
+            [f"mmtm{k}.fc_{m}.weight" for m in mods for k in range(2)]
+    params = []
+    for i, _ in enumerate(names):
+        p = torch.randn(1000 + 37 * i, device=dev)
+        params.append((p, torch.randn_like(p) * (0.1 + 0.05 * (i % 7))))
+    lib = L.load()
+    two = nb == 2
+
+    def new_state():
+        st = L.GateState() if two else L.GateStateN()
+        if not two:
+            st.nb = nb
+        st.eps, st.window, st.unlock, st.caring = 1e-3, 2, 1, -1
+        return torch.frombuffer(bytearray(bytes(st)), dtype=torch.uint8).to(dev)
+
+    out = {}
+    for fused in (True, False):
+        ps = [torch.nn.Parameter(p.clone()) for p, _ in params]
+        for q, (_, gr) in zip(ps, params):
+            q.grad = gr.clone()
+        norms = GroupNorms(list(zip(names, ps)), branches, mods)
+        state = new_state()
+        sums_seen = []
+        for _ in range(4):
+            if fused:
+                s = norms.sums(lr=0.01, gate=state, gate_n=not two)
+            else:
+                s = norms.sums(lr=0.01)
+                fn = lib.gm_gate_strong_step if two else lib.gm_gate_strong_step_n
+                L.check(fn(s.data_ptr(), state.data_ptr(), L.stream_of(dev)), "gate")
+            sums_seen.append(s.clone())
+        torch.cuda.synchronize()
+        out[fused] = (sums_seen, [p.detach().clone() for p in ps], state.cpu().clone())
+    a, b = out[True], out[False]
+    for x, y in zip(a[0], b[0]):
+        assert torch.equal(x, y)
+    for x, y in zip(a[1], b[1]):
+        assert torch.equal(x, y)
+    assert torch.equal(a[2], b[2]), "gate state differs"
