@@ -219,6 +219,7 @@ EXPORTS.update({
     "gm_mmtm_spatial_reduce_gated": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_size_t,
                                              c_void_p]),
     "gm_stem_pack_bf16": (c_int, [c_void_p, c_void_p]),
+    "gm_stem_pack_grouped_bf16": (c_int, [c_void_p, c_int, c_void_p]),
     "gm_xent_fwd": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "gm_xent_bwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
 })

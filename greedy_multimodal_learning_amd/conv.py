@@ -215,6 +215,32 @@ def stem_pack(x, weight, pad, xp=None, wp=None):
     return xp.permute(0, 3, 1, 2), wp.permute(0, 3, 1, 2)
 
 
+def stem_pack_grouped(xs, weights, pad, xp, wp):
+    """stem_pack for G views in ONE launch (gm_stem_pack_grouped_bf16): view g's input xs[g]
+    [N,C0,H,W] (any strides, fp32 or bf16, every view the same) and fp32 weight weights[g] into
+    xp[g*N:(g+1)*N] ([G*N,Hp,Wp/2,8] dense bf16) and wp[g] ([G,K,R,Sp,8])."""
+    G = len(xs)
+    N, C0, H, W = xs[0].shape
+    K, _, R, S = weights[0].shape
+    P, Q, Sp, Hp, Wp = _stem_geom(H, W, R, S, pad)
+    if tuple(xp.shape) != (G * N, Hp, Wp // 2, 8) or tuple(wp.shape) != (G, K, R, Sp, 8) or \
+            not xp.is_contiguous() or not wp.is_contiguous():
+        raise ValueError("stem_pack_grouped: outputs must be dense [G*N,Hp,Wp/2,8] / [G,K,R,Sp,8]")
+    descs, keep = [], []
+    for g, (x, w) in enumerate(zip(xs, weights)):
+        if x.dtype not in (torch.float32, torch.bfloat16):
+            x = x.float()
+        w = w.detach()
+        if w.dtype != torch.float32:
+            w = w.float()
+        keep += [x, w]
+        descs.append(L.StemPack(x.data_ptr(), L.GM_BF16 if x.dtype == torch.bfloat16 else L.GM_F32, N, C0, H, W,
+                                pad, *x.stride(), Hp, Wp, xp[g * N:(g + 1) * N].data_ptr(), w.data_ptr(), K, R, S,
+                                wp[g].data_ptr(), *w.stride()))
+    L.check(L.load().gm_stem_pack_grouped_bf16(L.arr(L.StemPack, descs), G, L.stream_of(xs[0].device)),
+            "gm_stem_pack_grouped_bf16")
+
+
 def stem_fwd(xp, wp, P, Q):
     lib = L.load()
     N, _, Hp, Wq = xp.shape

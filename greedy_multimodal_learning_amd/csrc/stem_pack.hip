@@ -8,6 +8,8 @@
 // Each thread writes one 16-B element (2 pixels x 4 channels); reads are coalesced per
 // channel plane.  Replaces the zero-fill + strided cast/copy PyTorch launches of the
 // input and of the weight (4 launches per view).
+#include <cstdint>
+
 #include "gm_common.h"
 
 namespace gm {
@@ -75,6 +77,102 @@ __global__ __launch_bounds__(kPT) void k_stem_pack(gm_stem_pack a, long long nx,
     }
 }
 
+// G view groups in one launch (gm_stem_pack_grouped_bf16), one wave per padded input row:
+// the row's W x C0 elements are read as whole 16-B vectors when the view is channels-last
+// RGB bf16 (the bench's resident batch; element loads otherwise), staged in LDS as
+// [W][4] bf16, and the row's Wp / 2 pixel pairs leave as one 16-B store each.  The
+// per-group weight views follow in the last blocks (as k_stem_pack).  Same values as
+// k_stem_pack, bit for bit.
+constexpr int kMaxPackG = 4, kRowW = 512;
+struct StemPackG {
+    gm_stem_pack p[kMaxPackG];
+    long long rows;  // N * Hp (every group)
+    int row_blocks;  // ceil(rows / 4)
+    int nw;          // weight elements per group
+};
+
+template <bool BF16, int C0T>  // C0T: the channels at compile time (3: RGB), 0 = p.C0 at run time
+__global__ __launch_bounds__(256) void k_stem_pack_rows(StemPackG a) {
+    __shared__ uint2 px[4][kRowW];  // [row of the wave][w]: 4 bf16 channels
+    const gm_stem_pack& p = a.p[blockIdx.y];
+    const int C0 = C0T ? C0T : p.C0;
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+    if ((int)blockIdx.x >= a.row_blocks) {  // weights (uniform per block)
+        const int e = ((int)blockIdx.x - a.row_blocks) * 256 + t;
+        if (e >= a.nw || !p.w) return;
+        const int Sq = (p.S + 1) >> 1;
+        const int k = e / (p.R * Sq), rs = e - k * p.R * Sq, r = rs / Sq, sq = rs - r * Sq;
+        unsigned short v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int s = 2 * sq + j;
+            if (s < p.S)
+                for (int c = 0; c < p.C0; ++c)
+                    v[4 * j + c] = bf16_of(p.w[(long long)k * p.wk + (long long)c * p.wc + (long long)r * p.wr +
+                                               (long long)s * p.ws]);
+        }
+        reinterpret_cast<uint4*>(p.wp)[e] = make_uint4(v[0] | ((unsigned)v[1] << 16), v[2] | ((unsigned)v[3] << 16),
+                                                       v[4] | ((unsigned)v[5] << 16), v[6] | ((unsigned)v[7] << 16));
+        return;
+    }
+    const long long row = (long long)blockIdx.x * 4 + wave;  // (n, hp)
+    const bool live = row < a.rows;
+    const int n = live ? (int)(row / p.Hp) : 0, hp = live ? (int)(row - (long long)n * p.Hp) : 0;
+    const int h = hp - p.pad;
+    const bool inrow = live && h >= 0 && h < p.H;
+    uint16_t* rp = reinterpret_cast<uint16_t*>(px[wave]);
+    if (inrow) {
+        const long long base = (long long)n * p.sn + (long long)h * p.sh;
+        const int E = p.W * C0;
+        // zero the row first (channels C0 .. 3 stay zero); the fill below writes other lanes'
+        // pixels, so the wave's LDS writes are ordered by a wave barrier
+        for (int w = lane; w < p.W; w += 64) px[wave][w] = make_uint2(0u, 0u);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // channels-last bf16 rows (sc 1, sw C0) whose start is 16-B aligned: whole vectors
+        const bool vec = BF16 && p.sc == 1 && p.sw == C0 &&
+                         (((uintptr_t)p.x + (uintptr_t)base * 2) & 15) == 0;
+        if (vec) {
+            const uint4* src = reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(p.x) + base);
+            for (int q = lane; q * 8 < E; q += 64) {
+                const uint4 u = src[q];
+                const unsigned uw[4] = {u.x, u.y, u.z, u.w};
+                int w = (q * 8) / C0, c = q * 8 - w * C0;  // element q * 8 + k: carried, no division per k
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    if (q * 8 + k < E) rp[w * 4 + c] = (unsigned short)(uw[k >> 1] >> (16 * (k & 1)));
+                    if (++c == C0) { c = 0; ++w; }
+                }
+            }
+        } else {
+            for (int e = lane; e < E; e += 64) {
+                const int w = e / C0, c = e - w * C0;
+                rp[w * 4 + c] = load_bf16<BF16>(p.x, base + (long long)c * p.sc + (long long)w * p.sw);
+            }
+        }
+    }
+    __syncthreads();
+    if (!live) return;
+    const int Wq = p.Wp >> 1;
+    uint4* dst = reinterpret_cast<uint4*>(p.xp) + row * Wq;
+    for (int wq = lane; wq < Wq; wq += 64) {
+        unsigned v[4] = {0u, 0u, 0u, 0u};
+        if (inrow) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int w = 2 * wq + j - p.pad;
+                if (w >= 0 && w < p.W) {
+                    const uint2 q = px[wave][w];
+                    v[2 * j] = q.x;
+                    v[2 * j + 1] = q.y;
+                }
+            }
+        }
+        dst[wq] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+}
+
 }  // namespace
 }  // namespace gm
 
@@ -106,4 +204,41 @@ extern "C" int gm_stem_pack_bf16(const gm_stem_pack* p, void* stream) {
     else
         hipLaunchKernelGGL(k_stem_pack<false>, g, dim3(kPT), 0, as_stream(stream), *p, nx, nw);
     return check_launch("k_stem_pack");
+}
+
+extern "C" int gm_stem_pack_grouped_bf16(const gm_stem_pack* ps, int G, void* stream) {
+    const char* fn = "gm_stem_pack_grouped_bf16";
+    GM_REQUIRE(ps && G >= 1 && G <= kMaxPackG, "%s: 1..%d view groups", fn, kMaxPackG);
+    StemPackG a{};
+    for (int g = 0; g < G; ++g) {
+        gm_stem_pack q = ps[g];
+        GM_REQUIRE(q.x && q.xp, "%s: group %d: null argument", fn, g);
+        GM_REQUIRE(q.C0 >= 1 && q.C0 <= 4 && q.N > 0 && q.H > 0 && q.W > 0 && q.W <= kRowW && q.pad >= 0,
+                   "%s: group %d: need 1 <= C0 <= 4, 1 <= W <= %d", fn, g, kRowW);
+        GM_REQUIRE(q.Hp >= q.H + q.pad && q.Wp >= q.W + q.pad && (q.Wp & 1) == 0, "%s: group %d: pair view", fn, g);
+        GM_REQUIRE(q.dtype == ps[0].dtype && (q.dtype == GM_F32 || q.dtype == GM_BF16), "%s: dtypes", fn);
+        GM_REQUIRE(q.N == ps[0].N && q.H == ps[0].H && q.W == ps[0].W && q.C0 == ps[0].C0 && q.pad == ps[0].pad &&
+                       q.Hp == ps[0].Hp && q.Wp == ps[0].Wp && (q.w != nullptr) == (ps[0].w != nullptr) &&
+                       q.K == ps[0].K && q.R == ps[0].R && q.S == ps[0].S,
+                   "%s: the groups must share their geometry", fn);
+        GM_REQUIRE(!q.w || (q.wp && q.K > 0 && q.R > 0 && q.S > 0), "%s: group %d: bad weight", fn, g);
+        if (q.w && !q.wk && !q.wc && !q.wr && !q.ws) {  // contiguous [K, C0, R, S]
+            q.ws = 1;
+            q.wr = q.S;
+            q.wc = (long long)q.R * q.S;
+            q.wk = (long long)q.C0 * q.R * q.S;
+        }
+        a.p[g] = q;
+    }
+    a.rows = (long long)ps[0].N * ps[0].Hp;
+    GM_REQUIRE(a.rows / 4 < (1ll << 30), "%s: too many rows", fn);
+    a.row_blocks = (int)((a.rows + 3) / 4);
+    a.nw = ps[0].w ? ps[0].K * ps[0].R * ((ps[0].S + 1) / 2) : 0;
+    const dim3 grid((unsigned)(a.row_blocks + (a.nw + 255) / 256), (unsigned)G);
+    const bool bf = ps[0].dtype == GM_BF16, rgb = ps[0].C0 == 3;
+    if (bf && rgb) hipLaunchKernelGGL((k_stem_pack_rows<true, 3>), grid, dim3(256), 0, as_stream(stream), a);
+    else if (bf) hipLaunchKernelGGL((k_stem_pack_rows<true, 0>), grid, dim3(256), 0, as_stream(stream), a);
+    else if (rgb) hipLaunchKernelGGL((k_stem_pack_rows<false, 3>), grid, dim3(256), 0, as_stream(stream), a);
+    else hipLaunchKernelGGL((k_stem_pack_rows<false, 0>), grid, dim3(256), 0, as_stream(stream), a);
+    return check_launch("k_stem_pack_rows");
 }

@@ -32,7 +32,8 @@ import torch
 from .streams import zeroed_scratch
 from . import _lib as L
 from .bn import MASK_FROM_X
-from .conv import CL, _cpad, _desc, _desc_hw, _like_param, _prepped, _splitk_ws, _stem_geom, stem_pack
+from .conv import CL, _cpad, _desc, _desc_hw, _like_param, _prepped, _splitk_ws, _stem_geom, stem_pack, \
+    stem_pack_grouped
 from .gradsink import GradJoin, sink_done, sink_pending, sink_target
 
 BF = torch.bfloat16
@@ -520,8 +521,11 @@ class _VStemFn(torch.autograd.Function):
         dev = x.device
         xp = torch.empty(G * B, Hp, Wp // 2, 8, device=dev, dtype=BF)
         wp = torch.empty(G, K, R, Sp, 8, device=dev, dtype=BF)
-        for g in range(G):
-            stem_pack(x[:, g], weights[g], pad, xp=xp[g * B:(g + 1) * B], wp=wp[g])
+        if G <= 4:
+            stem_pack_grouped([x[:, g] for g in range(G)], weights, pad, xp, wp)  # one launch
+        else:
+            for g in range(G):
+                stem_pack(x[:, g], weights[g], pad, xp=xp[g * B:(g + 1) * B], wp=wp[g])
         y = torch.empty(G * B, K, P, Q, device=dev, dtype=BF, memory_format=CL)
         d = _desc_hw(B, Hp, Wp // 2, 8, K, R, Sp, 2, 1, 0, 0)
         rows = lib.gm_conv_stem_stats_rows(ctypes.byref(d), G) if (stats is not None and FUSED_STEM_STATS) else 0

@@ -292,6 +292,9 @@ typedef struct gm_stem_pack {
 } gm_stem_pack;
 
 int gm_stem_pack_bf16(const gm_stem_pack* p, void* stream);
+/* G (<= 4) view groups sharing their geometry (N, H, W, C0, pad, Hp, Wp, K, R, S, dtype) in one
+ * launch, ps[g] each with its own pointers and strides; bit-identical to G gm_stem_pack_bf16 calls */
+int gm_stem_pack_grouped_bf16(const gm_stem_pack* ps, int G, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Branch-summed cross-entropy (reference train.py:22-29 blend_loss: sum over the
