@@ -159,6 +159,7 @@ EXPORTS.update({
                                              c_int, c_int, c_void_p, c_size_t, c_void_p]),
     "gm_conv2d_wgrad_hw_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
                                         c_size_t, c_void_p]),
+    "gm_stem_dw_crop": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
     "gm_conv2d_wgrad_stem_bn_ok": (c_int, [c_void_p, c_int]),
     "gm_conv2d_wgrad_stem_bn_grouped_bf16": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                                                      ctypes.c_longlong, c_int, c_void_p, c_size_t, c_void_p]),

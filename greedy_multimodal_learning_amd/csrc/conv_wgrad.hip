@@ -1325,6 +1325,32 @@ __global__ __launch_bounds__(256) void k_wgrad_stem_bn(WStemArgs a) {
                 out[(size_t)(nb * 32 + 8 * (e >> 2) + 4 * (lane >> 5) + (e & 3)) * TC] = acc[r][nb][e];
     }
 }
+// The stem's weight gradient from its padded pixel-pair layout [G][K][R][Sp][2][4] (fp32) into each
+// view's parameter gradient [K][R][S][C0] (the channels_last [K, C0, R, S] parameter): one launch
+// for every view instead of a strided copy per view (gm_stem_dw_crop)
+constexpr int kCropG = 16;
+struct StemCropArgs {
+    const float* dwp;
+    float* dst[kCropG];
+    int K, R, S, C0, Sp, accumulate;
+};
+
+__global__ __launch_bounds__(256) void k_stem_dw_crop(StemCropArgs a) {
+    const int g = blockIdx.y;
+    const int n = a.K * a.R * a.S * a.C0;
+    const int o = blockIdx.x * 256 + threadIdx.x;
+    if (o >= n) return;
+    int t = o;
+    const int c = t % a.C0;
+    t /= a.C0;
+    const int s = t % a.S;
+    t /= a.S;
+    const int r = t % a.R, k = t / a.R;
+    const float v = a.dwp[(size_t)g * a.K * a.R * a.Sp * 8 + ((size_t)(k * a.R + r) * a.Sp + (s >> 1)) * 8 + (s & 1) * 4 + c];
+    float* d = a.dst[g] + o;
+    *d = a.accumulate ? *d + v : v;
+}
+
 // dw[i] (+)= sum over splits of part[s][i] in ONE launch, for the uncropped case (Cp == Cr,
 // every layer but the RGB stem).  A wave covers 64/R float4 columns with R split lanes per
 // column (lane r sums splits r, r+R, ..., eight loads in flight), and the R lane sums are
@@ -1899,4 +1925,21 @@ extern "C" int gm_conv2d_wgrad_bf16(const gm_conv_desc* d, const void* dy, const
     GM_REQUIRE(d, "conv wgrad: null pointer");
     const gm_conv_desc_hw h = to_hw(d);
     return gm_conv2d_wgrad_hw_bf16(&h, dy, x, dw, c_real, accumulate, scratch, scratch_bytes, stream);
+}
+
+extern "C" int gm_stem_dw_crop(const float* dwp, int G, int K, int R, int S, int C0, int Sp, float* const* dst,
+                               int accumulate, void* stream) {
+    GM_REQUIRE(dwp && dst && G >= 1 && G <= kCropG && K > 0 && R > 0 && S > 0 && C0 >= 1 && C0 <= 4 &&
+                   Sp == (S + 1) / 2,
+               "gm_stem_dw_crop: bad arguments");
+    StemCropArgs a{};
+    a.dwp = dwp;
+    for (int g = 0; g < G; ++g) {
+        GM_REQUIRE(dst[g], "gm_stem_dw_crop: null destination %d", g);
+        a.dst[g] = dst[g];
+    }
+    a.K = K; a.R = R; a.S = S; a.C0 = C0; a.Sp = Sp; a.accumulate = accumulate ? 1 : 0;
+    const int n = K * R * S * C0;
+    k_stem_dw_crop<<<dim3((unsigned)((n + 255) / 256), (unsigned)G), 256, 0, as_stream(stream)>>>(a);
+    return check_launch("k_stem_dw_crop");
 }

@@ -576,13 +576,23 @@ class _VStemFn(torch.autograd.Function):
             L.check(lib.gm_conv2d_wgrad_grouped_bf16(ctypes.byref(d), G, gy.data_ptr(), xp.data_ptr(),
                                                      dwp.data_ptr(), K * R * Sp * 8, 8, 0, scratch.data_ptr(), need,
                                                      L.stream_of(dev)), "gm_conv2d_wgrad_grouped_bf16")
+        tgts = [sink_target(w) if want[g] else None for g, w in enumerate(weights)]
+        if all(t is not None and t[1] == tgts[0][1] and t[0].dtype == torch.float32
+               and t[0].is_contiguous(memory_format=CL) for t in tgts):
+            # every view's gradient sink at once: one crop launch into the [K][R][S][C0] memory
+            ptrs = (ctypes.c_void_p * G)(*[t[0].data_ptr() for t in tgts])
+            L.check(lib.gm_stem_dw_crop(dwp.data_ptr(), G, K, R, S, C0, Sp, ptrs, int(bool(tgts[0][1])),
+                                        L.stream_of(dev)), "gm_stem_dw_crop")
+            for w in weights:
+                sink_done(w)
+            return (None, None, None, None, *[None] * G)
         grads = []
         for g, w in enumerate(weights):
             if not want[g]:
                 grads.append(None)
                 continue
             dw = dwp[g].view(K, R, 2 * Sp, 4)[:, :, :S, :C0].permute(0, 3, 1, 2)  # [K,C0,R,S]
-            tgt = sink_target(w)
+            tgt = tgts[g]  # (sink_target marks the gradient written: called once per step above)
             if tgt is not None:
                 if tgt[1]:
                     tgt[0].add_(dw)

@@ -471,6 +471,11 @@ typedef struct gm_stem_bn_src {
     const float* bcoef;
     long long bcoef_gs;
 } gm_stem_bn_src;
+/* the pixel-pair stem's weight gradient dwp [G][K][R][Sp][2][4] fp32 (as the wgrad calls above write
+ * it for the stem) into each view's [K][R][S][C0] gradient dst[g] (the channels_last [K, C0, R, S]
+ * parameter's memory), += when accumulate; one launch for every view (G <= 16) */
+int gm_stem_dw_crop(const float* dwp, int G, int K, int R, int S, int C0, int Sp, float* const* dst, int accumulate,
+                    void* stream);
 int gm_conv2d_wgrad_stem_bn_ok(const gm_conv_desc_hw* d, int G); /* 1: the call below takes this shape */
 int gm_conv2d_wgrad_stem_bn_grouped_bf16(const gm_conv_desc_hw* d, int G, const gm_stem_bn_src* src, const void* x,
                                          float* dw, long long dw_stride, int accumulate, void* scratch,

@@ -92,7 +92,7 @@ def test_engine_bf16_step_vs_oracle(trunk, V, B):
     assert not missing, missing
     o.train(True)
     _, outs_ref, _, _ = o(x.float())
-    ref = float(gating_ref.blend_loss(outs_ref, y))
+    ref = float(gating_ref.blend_loss(outs_ref, y).detach())
     m = m.to(dev)
     xd, yd = x.to(dev), y.to(dev)
     m.train(True)
