@@ -1142,6 +1142,7 @@ __global__ __launch_bounds__(64 * R) void k_wgrad_stem(WStemArgs a) {
 // VGPRs) and one's dy forming overlaps the other's MFMAs.  The A fragments (dy) of a k-slice feed
 // both of a wave's tap rows.  Rows are prefetched three iterations ahead.  Same MFMA operands and
 // order as k_wgrad_stem on the same tiles: bit-identical partials.
+constexpr int kStemBnDepth = 3;  // rows of y in flight (registers; 2: 216 VGPRs, room for a split-sum wave beside it - equal in the step, profiles/r06_stem_wgrad_ab.txt)
 template <int R, int S>
 __global__ __launch_bounds__(256) void k_wgrad_stem_bn(WStemArgs a) {
     constexpr int NT = 256;
@@ -1262,7 +1263,7 @@ __global__ __launch_bounds__(256) void k_wgrad_stem_bn(WStemArgs a) {
     Stage sa, sb, sc;
     fetch(p0 + 1, p0 + 4, sa);
     fetch(p0 + 2, p0 + 5, sb);
-    fetch(p0 + 3, p0 + 6, sc);
+    if constexpr (kStemBnDepth == 3) fetch(p0 + 3, p0 + 6, sc);
     fetch_pool(k0 + 2, pq);
 
     floatx16 acc[2][2];  // [tap row of the wave][channel block]
@@ -1285,7 +1286,7 @@ __global__ __launch_bounds__(256) void k_wgrad_stem_bn(WStemArgs a) {
             fetch_pool((p + 5) >> 1, pq);
         }
         stash_dy(p + 1, st);
-        fetch(p + 4, p + 7, st);
+        fetch(p + kStemBnDepth + 1, p + kStemBnDepth + 4, st);
         const char* tile = lds + (p & 1) * tileb;
         // tap rows 2w, 2w + 1 read input rows 2(p + w), 2(p + w) + 1: one unit
         const char* xrow = ring + ((p + w) & (RING - 1)) * a.upitch;
@@ -1308,10 +1309,17 @@ __global__ __launch_bounds__(256) void k_wgrad_stem_bn(WStemArgs a) {
             }
         }
     };
-    for (int p = p0; p < p1; p += 3) {
-        iteration(p, sa);
-        if (p + 1 < p1) iteration(p + 1, sb);
-        if (p + 2 < p1) iteration(p + 2, sc);
+    if constexpr (kStemBnDepth == 3) {
+        for (int p = p0; p < p1; p += 3) {
+            iteration(p, sa);
+            if (p + 1 < p1) iteration(p + 1, sb);
+            if (p + 2 < p1) iteration(p + 2, sc);
+        }
+    } else {
+        for (int p = p0; p < p1; p += 2) {
+            iteration(p, sa);
+            if (p + 1 < p1) iteration(p + 1, sb);
+        }
     }
     // the partial: dw[channel][rr * 32 + (s, c)] for the wave's tap rows rr = 2w (+ 1)
 #pragma unroll
