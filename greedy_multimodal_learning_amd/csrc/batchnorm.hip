@@ -1151,7 +1151,7 @@ __global__ __launch_bounds__(kT, NR == 16 ? 2 : NR == 8 ? 3 : 4) void k_bn_fwd_f
         for (int j = 0; j < 8; ++j) {
             float zz = fmaf(f[j], sc[j], sh[j]);
             if (RES) zz += q[j];
-            f[j] = RELU ? fmaxf(zz, 0.f) : zz;
+            f[j] = RELU ? relu_nan(zz) : zz;
             if (!fresh) f[j] = __builtin_nanf("");  // poisoned (fmaxf would turn NaN into 0)
         }
         const uint4 w = pack8(f);
@@ -1418,7 +1418,7 @@ __global__ __launch_bounds__(kT) void k_bn_apply(ApplyArgs a) {
         for (int j = 0; j < 8; ++j) {
             float z = fmaf(f[j], sc[j], sh[j]);
             if (RES) z += r[j];
-            f[j] = RELU ? fmaxf(z, 0.f) : z;
+            f[j] = RELU ? relu_nan(z) : z;
         }
         V8<E>::st(a.out, i, f);
         if (RES && RELU && std::is_same<E, uint16_t>::value && a.mask_out) a.mask_out[i] = (uint8_t)mask_byte(pack8(f));

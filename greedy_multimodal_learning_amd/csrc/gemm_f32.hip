@@ -244,7 +244,7 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_f32(GemmArgs a) {
     for (int r = 0; r < 4; ++r) {
         const int m = m0 + lk * 4 + r;
         float v = acc[r] + bias;
-        if (p.act == 1) v = v > 0.f ? v : 0.f;
+        if (p.act == 1) v = relu_nan(v);
         else if (p.act == 2) v = 1.0f / (1.0f + expf(-v));
         v = mk[r] > 0.f ? v : 0.f;
         if (m < p.M) p.C[(size_t)m * p.ld_c + n] = co[r] + v;

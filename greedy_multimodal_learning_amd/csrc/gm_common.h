@@ -40,6 +40,10 @@ template <> struct Elem<uint16_t> {
     }
 };
 
+// ReLU with PyTorch's NaN semantics (torch.relu = clamp_min propagates NaN; fmaxf(NaN, 0) would
+// return 0 and hide a diverged activation from the NaN-loss stop)
+__device__ __forceinline__ float relu_nan(float z) { return (z > 0.f || z != z) ? z : 0.f; }
+
 __device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {

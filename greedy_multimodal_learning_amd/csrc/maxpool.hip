@@ -88,7 +88,7 @@ __global__ __launch_bounds__(256) void k_maxpool_fwd(PoolArgs a, const void* __r
                 if (h < 0 || h >= a.H || w < 0 || w >= a.W) continue;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    const float z = BNRELU ? round_to<E>(fmaxf(fmaf(v[u][j], sc[j], sh[j]), 0.f)) : v[u][j];
+                    const float z = BNRELU ? round_to<E>(relu_nan(fmaf(v[u][j], sc[j], sh[j]))) : v[u][j];
                     if (z > m[j] || __builtin_isnan(z)) {
                         m[j] = z;
                         xs[j] = v[u][j];
@@ -109,7 +109,7 @@ __global__ __launch_bounds__(256) void k_maxpool_fwd(PoolArgs a, const void* __r
                 for (int j = 0; j < 8; ++j) raw[j] = v[j];
                 if (BNRELU) {
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) v[j] = round_to<E>(fmaxf(fmaf(v[j], sc[j], sh[j]), 0.f));
+                    for (int j = 0; j < 8; ++j) v[j] = round_to<E>(relu_nan(fmaf(v[j], sc[j], sh[j])));
                 }
                 const uint32_t pos = (uint32_t)(r * a.k + c);
 #pragma unroll

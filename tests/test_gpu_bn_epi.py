@@ -118,6 +118,7 @@ def test_relu_mask_bits_backward_bit_identical(shape, epi):
     res = torch.randn(G * N, C, H, W, generator=g).bfloat16().to(dev).contiguous(memory_format=CL)
     res[0, 5, 1, 1] = float("inf")    # y = +inf (bf16 0x7f80): the mask's largest set value
     res[1, 6, 0, 1] = float("-inf")   # y = 0 after the ReLU
+    res[2, 7, 1, 0] = float("nan")    # y = NaN: no gradient through it on either backward
     gy = torch.randn(G * N, C, H, W, generator=g).bfloat16().to(dev).contiguous(memory_format=CL)
     convs = []
     for _ in range(G):
@@ -142,7 +143,10 @@ def test_relu_mask_bits_backward_bit_identical(shape, epi):
     finally:
         vtrunk.BN_RELU_MASK = old
     for i, (a, b) in enumerate(zip(out[True], out[False])):
-        assert torch.equal(a, b), f"output {i} differs with the mask bits"
+        assert torch.equal(a.isnan(), b.isnan()), f"output {i}: NaN positions differ with the mask bits"
+        assert torch.equal(a.nan_to_num(), b.nan_to_num()), f"output {i} differs with the mask bits"
+    assert int(out[True][0].isnan().sum()) == 1 and all(not t.isnan().any() for t in out[True][1:]), \
+        "the NaN of y must stay in y (its gradient is dropped by the ReLU mask)"
 
 
 BWD_SHAPES = [  # N per view, C, H, W, conv2 (R, stride), G, statistics from the dgrad epilogue
