@@ -153,6 +153,8 @@ EXPORTS.update({
                                            c_void_p, c_size_t, c_void_p]),
     "gm_conv2d_dgrad_grouped_bf16": (c_int, [c_void_p, c_int, c_void_p, c_void_p, ctypes.c_longlong, c_void_p,
                                              c_void_p, c_void_p, c_size_t, c_void_p]),
+    "gm_conv2d_dgrad_grouped_masked_bf16": (c_int, [c_void_p, c_int, c_void_p, c_void_p, ctypes.c_longlong,
+                                                    c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "gm_conv2d_splitk_ws_bytes_grouped": (c_size_t, [c_void_p, c_int, c_int]),
     "gm_conv2d_wgrad_grouped_scratch": (c_size_t, [c_void_p, c_int]),
     "gm_conv2d_wgrad_grouped_bf16": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, ctypes.c_longlong,

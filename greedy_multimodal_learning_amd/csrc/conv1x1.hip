@@ -34,6 +34,7 @@ struct RingGemmArgs {
     const uint16_t* B;       // [G][N][Kr]
     uint16_t* out;           // [G][M][N]
     const uint16_t* addend;  // [G][M][N] or null (may alias out)
+    const uint8_t* amask;    // with it, optional: its 1-bit mask (mask_bf2), [G][M * N / 8]
     int M, N, Kr;            // per group
     int G, tiles_m, tiles_n, tiles;  // tiles = G * tiles_m * tiles_n
     long long gsA, gsB, gsO; // group strides (elements; gsB may be negative)
@@ -262,6 +263,21 @@ __global__ __launch_bounds__(512) void k_gemm_ring(RingGemmArgs a) {
                     u32x4 av[2 * NT];
 #pragma unroll
                     for (int it = 0; it < 2 * NT; ++it) av[it] = __builtin_amdgcn_raw_buffer_load_b128(arsrc, off[it], 0, 0);
+                    if (a.amask) {  // one mask byte per 16-B chunk: byte off / 16 (past the range: 0)
+                        const auto mrsrc = __builtin_amdgcn_make_buffer_rsrc(
+                            const_cast<uint8_t*>(a.amask + g * a.gsO / 8), 0, (int)(obytes >> 4), 0x00020000);
+                        unsigned mb[2 * NT];
+#pragma unroll
+                        for (int it = 0; it < 2 * NT; ++it)
+                            mb[it] = __builtin_amdgcn_raw_buffer_load_b8(mrsrc, off[it] >> 4, 0, 0);
+#pragma unroll
+                        for (int it = 0; it < 2 * NT; ++it) {
+                            av[it].x = mask_bf2(av[it].x, mb[it]);
+                            av[it].y = mask_bf2(av[it].y, mb[it] >> 2);
+                            av[it].z = mask_bf2(av[it].z, mb[it] >> 4);
+                            av[it].w = mask_bf2(av[it].w, mb[it] >> 6);
+                        }
+                    }
 #pragma unroll
                     for (int it = 0; it < 2 * NT; ++it) {
                         const int row = it * RPI + rr;
@@ -368,13 +384,14 @@ bool conv1x1_ok(int R, int S, int sh, int sw, int ph, int pw, long long M, int K
 // Out = A . B^T (+ addend) per group; the caller checked conv1x1_ok
 int conv1x1_gemm(long long M, int Kr, int N, int G, const void* A, long long gsA, const void* B, long long gsB,
                  void* out, long long gsO, const void* addend, hipStream_t st, const char* fn, float* stats,
-                 const uint16_t* bnx, const float* bncoef, const float* bnmean) {
+                 const uint16_t* bnx, const float* bncoef, const float* bnmean, const uint8_t* amask) {
     RingGemmArgs r;
     memset(&r, 0, sizeof(r));
     r.A = (const uint16_t*)A;
     r.B = (const uint16_t*)B;
     r.out = (uint16_t*)out;
     r.addend = (const uint16_t*)addend;
+    r.amask = addend ? amask : nullptr;
     r.M = (int)M; r.N = N; r.Kr = Kr; r.G = G;
     const int BN = N % 128 == 0 ? 128 : 64;
     r.tiles_m = (int)((M + 127) / 128);

@@ -71,6 +71,9 @@ struct ConvArgs {
     // on in order 0 -> 1 -> ... -> S-1 through ws (turnstile flags[tile], zero between
     // launches); the last split writes the output.  Deterministic (fixed order).
     const uint16_t* addend;   // dgrad, optional: out = conv + addend (same layout as out)
+    // with it, optional: the addend's 1-bit mask (mask_bf2; group g at amask + g * gs_out / 8) -
+    // out = conv + (addend where the bit is set), the addend never aliasing out
+    const uint8_t* amask;
     int splits, tiles_total;
     float* ws;                // [tiles][MT*NT*16/4][256] float4
     unsigned* flags;          // [tiles]
@@ -176,7 +179,10 @@ __device__ __forceinline__ unsigned span_mask(int x, int d0, int s, int n, int l
 // whole tile with no per-element branch: out-of-tile positions get an offset past the
 // buffer's range, which the hardware drops (stores) or reads as zero (loads), so the
 // addend loads are all in flight together instead of one dependent round trip per store.
-template <int MT, int NT, int BM, int BN>
+// MASK: the masked addend (a.amask) is handled here - store_tile_lds's fallback; the kernels that
+// store through store_tile directly (k_conv_igemm, k_conv_halo) get their masked addend
+// materialised in dx before the launch (demask) and so keep their registers.
+template <int MT, int NT, int BM, int BN, bool MASK = false>
 __device__ __forceinline__ void store_tile(const ConvArgs& a, const ConvCls& cl, int m0, int n0, int wm, int wn,
                                            int fr, int fh, int M, floatx16 (&acc)[MT][NT], long long goff = 0) {
     const int PQ = cl.P * cl.Q;
@@ -213,6 +219,22 @@ __device__ __forceinline__ void store_tile(const ConvArgs& a, const ConvCls& cl,
 #pragma unroll
                     for (int gq = 0; gq < 4; ++gq)
                         av[i][j][gq] = __builtin_amdgcn_raw_buffer_load_b64(arsrc, boff(i, j, gq), 0, 0);
+            if (MASK && a.amask) {  // (Nout % 32 == 0) one mask dword per 32 channels: gq's byte, fh's nibble
+                const auto mrsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.amask + goff / 8), 0,
+                                                                     (int)(out_bytes >> 4), 0x00020000);
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+#pragma unroll
+                    for (int j = 0; j < NT; ++j) {
+                        const unsigned w = __builtin_amdgcn_raw_buffer_load_b32(mrsrc, (boff(i, j, 0) - 8u * fh) >> 4,
+                                                                                0, 0) >> (4 * fh);
+#pragma unroll
+                        for (int gq = 0; gq < 4; ++gq) {
+                            av[i][j][gq].x = mask_bf2(av[i][j][gq].x, w >> (8 * gq));
+                            av[i][j][gq].y = mask_bf2(av[i][j][gq].y, w >> (8 * gq + 2));
+                        }
+                    }
+            }
         }
 #pragma unroll
         for (int i = 0; i < MT; ++i)
@@ -248,7 +270,13 @@ __device__ __forceinline__ void store_tile(const ConvArgs& a, const ConvCls& cl,
                 float o0 = acc[i][j][4 * gq], o1 = acc[i][j][4 * gq + 1];
                 float o2 = acc[i][j][4 * gq + 2], o3 = acc[i][j][4 * gq + 3];
                 if (a.addend) {
-                    const uint2 av = *(const uint2*)(addp + (dst - outp) + n);
+                    uint2 av = *(const uint2*)(addp + (dst - outp) + n);
+                    if (MASK && a.amask) {
+                        const size_t e = (size_t)goff + (size_t)(dst - outp) + n;
+                        const unsigned b = (unsigned)a.amask[e >> 3] >> (e & 4);
+                        av.x = mask_bf2(av.x, b);
+                        av.y = mask_bf2(av.y, b >> 2);
+                    }
                     o0 += bf_lo(av.x); o1 += bf_hi(av.x); o2 += bf_lo(av.y); o3 += bf_hi(av.y);
                 }
                 uint2 v;
@@ -275,7 +303,7 @@ __device__ __forceinline__ void store_tile_lds(const ConvArgs& a, const ConvCls&
     const size_t out_bytes = (size_t)a.N * a.Ho * a.Wo * a.Nout * 2;
     const bool f32 = a.addend != nullptr;
     if (out_bytes >= 0x7ffff000u || BM * BN * (f32 ? 4 : 2) + 4 * (BN / 8) * 64 > lds_bytes) {
-        store_tile<MT, NT, BM, BN>(a, cl, m0, n0, wm, wn, fr, fh, M, acc, goff);
+        store_tile<MT, NT, BM, BN, true>(a, cl, m0, n0, wm, wn, fr, fh, M, acc, goff);
         return;
     }
     constexpr int CH = BN / 8, CF = BN / 4;  // bf16 / fp32 16-B chunks per pixel row
@@ -341,6 +369,20 @@ __device__ __forceinline__ void store_tile_lds(const ConvArgs& a, const ConvCls&
         u32x4 av[NU];
 #pragma unroll
         for (int u = 0; u < NU; ++u) av[u] = __builtin_amdgcn_raw_buffer_load_b128(arsrc, off[u], 0, 0);
+        if (a.amask) {  // one mask byte per 16-B chunk: byte off / 16 (past the range: 0)
+            const auto mrsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.amask + goff / 8), 0,
+                                                                 (int)(out_bytes >> 4), 0x00020000);
+            unsigned mb[NU];
+#pragma unroll
+            for (int u = 0; u < NU; ++u) mb[u] = __builtin_amdgcn_raw_buffer_load_b8(mrsrc, off[u] >> 4, 0, 0);
+#pragma unroll
+            for (int u = 0; u < NU; ++u) {
+                av[u].x = mask_bf2(av[u].x, mb[u]);
+                av[u].y = mask_bf2(av[u].y, mb[u] >> 2);
+                av[u].z = mask_bf2(av[u].z, mb[u] >> 4);
+                av[u].w = mask_bf2(av[u].w, mb[u] >> 6);
+            }
+        }
 #pragma unroll
         for (int u = 0; u < NU; ++u) {
             const int e = t + 256 * u, px = e / CH, c = e - px * CH;
@@ -1843,6 +1885,18 @@ __global__ __launch_bounds__(256) void k_conv_rw(ConvArgs a, RwArgs r) {
 #pragma unroll
                 for (int gq = 0; gq < 4; ++gq)
                     av[i][gq] = *(const uint2*)(gadd + off[i] + 8 * gq);  // rows past RT*W read row 0
+            if (a.amask) {  // element e's bit: byte e / 8, nibble (e / 4) & 1
+                const uint8_t* const gm = a.amask + g * a.gs_out / 8;
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int gq = 0; gq < 4; ++gq) {
+                        const size_t e = off[i] + 8 * gq;
+                        const unsigned b = (unsigned)gm[e >> 3] >> (e & 4);
+                        av[i][gq].x = mask_bf2(av[i][gq].x, b);
+                        av[i][gq].y = mask_bf2(av[i][gq].y, b >> 2);
+                    }
+            }
         }
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
@@ -2090,10 +2144,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
 // zero the output pixels no dgrad class covers (e.g. odd pixels of a 1x1/s2 dgrad), or
 // copy the addend there when the dgrad is fused with a gradient join
-__global__ void k_zero_bf16(uint16_t* p, size_t n, const uint16_t* src) {
+__global__ void k_zero_bf16(uint16_t* p, size_t n, const uint16_t* src, const uint8_t* msk = nullptr) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; i * 8 < n; i += (size_t)gridDim.x * blockDim.x)
-        *(uint4*)(p + i * 8) = src ? *(const uint4*)(src + i * 8) : make_uint4(0, 0, 0, 0);
+    for (; i * 8 < n; i += (size_t)gridDim.x * blockDim.x) {
+        uint4 v = src ? *(const uint4*)(src + i * 8) : make_uint4(0, 0, 0, 0);
+        if (msk) {  // the masked addend: byte i covers these 8 elements
+            const unsigned b = msk[i];
+            v.x = mask_bf2(v.x, b); v.y = mask_bf2(v.y, b >> 2); v.z = mask_bf2(v.z, b >> 4); v.w = mask_bf2(v.w, b >> 6);
+        }
+        *(uint4*)(p + i * 8) = v;
+    }
 }
 
 // W[Co][T][Ci] -> Wt[Ci][T][Co] (bf16), for the input-gradient convolution
@@ -2145,8 +2205,22 @@ static void launch_ut(const ConvArgs& a, int grid, hipStream_t st) {
     k_conv_igemm_ut<BM, BN, PIPE><<<grid, 256, lds, st>>>(a);
 }
 
+// the masked addend materialised over dx (k_zero_bf16's masked copy; every group, contiguous),
+// which then is the addend in place - for the kernels whose epilogue reads no mask
+static int demask(ConvArgs& a, hipStream_t st) {
+    if (!a.amask) return GM_OK;
+    const size_t n = (size_t)(a.G > 1 ? a.G : 1) * a.N * a.Ho * a.Wo * a.Nout;
+    uint16_t* dx = a.cls[0].out;
+    k_zero_bf16<<<(int)((n / 8 + 255) / 256 < 4096 ? (n / 8 + 255) / 256 : 4096), 256, 0, st>>>(dx, n, a.addend,
+                                                                                               a.amask);
+    a.addend = dx;
+    a.amask = nullptr;
+    return check_launch("k_zero_bf16");
+}
+
 template <int BM, int BN, int ST>
 static int launch_igemm(ConvArgs& a, hipStream_t st) {
+    if (int rc = demask(a, st)) return rc;
     int tiles = 0;
     for (int i = 0; i < a.ncls; ++i) {
         ConvCls& c = a.cls[i];
@@ -2323,6 +2397,7 @@ static int halo_bytes(const ConvArgs& a, int BM = 128) {
 
 template <int BN, int NB, int BM = 128>
 static int launch_halo_v(ConvArgs& a, int hb, hipStream_t st) {
+    if (int rc = demask(a, st)) return rc;
     ConvCls& c = a.cls[0];
     const int M = a.N * c.P * c.Q;
     c.tiles_m = (M + BM - 1) / BM;
@@ -2867,7 +2942,7 @@ bool conv1x1_ok(int R, int S, int sh, int sw, int ph, int pw, long long M, int K
 int conv1x1_gemm(long long M, int Kr, int N, int G, const void* A, long long gsA, const void* B, long long gsB,
                  void* out, long long gsO, const void* addend, hipStream_t st, const char* fn,
                  float* stats = nullptr, const uint16_t* bnx = nullptr, const float* bncoef = nullptr,
-                 const float* bnmean = nullptr);
+                 const float* bnmean = nullptr, const uint8_t* amask = nullptr);
 }  // namespace gm
 
 extern "C" int gm_conv2d_fwd_hw_bf16(const gm_conv_desc_hw* d, const void* x, const void* w, void* y,
@@ -3036,9 +3111,30 @@ extern "C" int gm_conv2d_fwd_grouped_stats_bf16(const gm_conv_desc_hw* d, int G,
     return launch_stem(a, r, lds, as_stream(stream));
 }
 
+// The input gradient with a masked gradient-join addend: dx = dgrad + (addend where the 1-bit mask
+// is set) - the identity branch's dz = dy . [y > 0] of a block-output ReLU read from its dy and the
+// BatchNorm forward's mask bits (batchnorm.hip) instead of a materialised dres.  dx != addend.
+static int dgrad_grouped(const gm_conv_desc* d, int G, const void* dy, const void* wt, long long wt_stride, void* dx,
+                         const void* addend, const uint8_t* amask, void* ws, size_t ws_bytes, void* stream);
+
+extern "C" int gm_conv2d_dgrad_grouped_masked_bf16(const gm_conv_desc* d, int G, const void* dy, const void* wt,
+                                                   long long wt_stride, void* dx, const void* addend,
+                                                   const void* addend_mask, void* ws, size_t ws_bytes, void* stream) {
+    GM_REQUIRE(addend && addend_mask, "conv dgrad masked: null addend or mask");
+    GM_REQUIRE(addend != dx, "conv dgrad masked: the addend must not alias dx");
+    GM_REQUIRE(d && d->C % 32 == 0, "conv dgrad masked: C must be a multiple of 32 (one mask dword per 32 channels)");
+    return dgrad_grouped(d, G, dy, wt, wt_stride, dx, addend, static_cast<const uint8_t*>(addend_mask), ws, ws_bytes,
+                         stream);
+}
+
 extern "C" int gm_conv2d_dgrad_grouped_bf16(const gm_conv_desc* d, int G, const void* dy, const void* wt,
                                             long long wt_stride, void* dx, const void* addend, void* ws,
                                             size_t ws_bytes, void* stream) {
+    return dgrad_grouped(d, G, dy, wt, wt_stride, dx, addend, nullptr, ws, ws_bytes, stream);
+}
+
+static int dgrad_grouped(const gm_conv_desc* d, int G, const void* dy, const void* wt, long long wt_stride, void* dx,
+                         const void* addend, const uint8_t* amask, void* ws, size_t ws_bytes, void* stream) {
     int rc = check_dgrad(d);
     if (rc) return rc;
     GM_REQUIRE(dy && wt && dx, "conv dgrad: null pointer");
@@ -3052,7 +3148,7 @@ extern "C" int gm_conv2d_dgrad_grouped_bf16(const gm_conv_desc* d, int G, const 
         const long long M = (long long)d->N * d->H * d->W;
         if (gm::conv1x1_ok(d->R, d->S, d->stride, d->stride, d->pad, d->pad, M, d->K, d->C))
             return gm::conv1x1_gemm(M, d->K, d->C, G, dy, M * d->K, wt, wt_stride, dx, M * d->C, addend,
-                                    as_stream(stream), "conv1x1 dgrad");
+                                    as_stream(stream), "conv1x1 dgrad", nullptr, nullptr, nullptr, nullptr, amask);
     }
     ConvArgs a;
     const bool full = dgrad_setup(d, dy, wt, dx, a);
@@ -3061,11 +3157,12 @@ extern "C" int gm_conv2d_dgrad_grouped_bf16(const gm_conv_desc* d, int G, const 
     a.gs_wt = wt_stride;
     a.gs_out = (long long)d->N * d->H * d->W * d->C;
     a.addend = (const uint16_t*)addend;
+    a.amask = addend ? amask : nullptr;
     hipStream_t s = as_stream(stream);
     if (!full && addend != dx) {  // the groups are contiguous: one pass zeroes (or copies) them all
         const size_t n = (size_t)G * d->N * d->H * d->W * d->C;
         k_zero_bf16<<<(int)((n / 8 + 255) / 256 < 4096 ? (n / 8 + 255) / 256 : 4096), 256, 0, s>>>(
-            (uint16_t*)dx, n, (const uint16_t*)addend);
+            (uint16_t*)dx, n, (const uint16_t*)addend, a.amask);
         rc = check_launch("k_zero_bf16");
         if (rc) return rc;
     }

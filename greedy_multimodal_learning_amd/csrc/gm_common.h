@@ -44,6 +44,13 @@ template <> struct Elem<uint16_t> {
 // return 0 and hide a diverged activation from the NaN-loss stop)
 __device__ __forceinline__ float relu_nan(float z) { return (z > 0.f || z != z) ? z : 0.f; }
 
+// The gradient join's masked addend (a ReLU output's dz = dy where the forward's mask bit is set;
+// batchnorm.hip's 1-bit mask: bit e of byte i is element 8 i + e): the bf16 pair x keeps the
+// halves whose bits (b & 1: low, b & 2: high) are set - exactly the dres the BN backward wrote
+__device__ __forceinline__ uint32_t mask_bf2(uint32_t x, uint32_t b) {
+    return x & ((b & 1u ? 0x0000ffffu : 0u) | (b & 2u ? 0xffff0000u : 0u));
+}
+
 __device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {

@@ -114,9 +114,16 @@ class GradJoin:
         self.n = 0
         self.done = 0
         self.pending = None
+        # every consumer that may come last accepts a MaskedAddend (the view-batched trunk's
+        # identity blocks: vtrunk.vblock sets it)
+        self.masked_ok = False
 
     def register(self):
         self.n += 1
+
+    def first_of_many(self):
+        """True when the next contribution is stored as the pending addend (not the last)."""
+        return self.pending is None and self.done + 1 < self.n
 
     def contribute(self, compute):
         self.done += 1
@@ -127,3 +134,14 @@ class GradJoin:
             return g
         self.pending = g
         return None
+
+
+class MaskedAddend:
+    """A pending join addend kept as (dy, 1-bit mask): dz = dy where the mask bit is set - the
+    identity branch's gradient of a block-output ReLU, which the consuming convolution's dgrad
+    epilogue forms itself (gm_conv2d_dgrad_grouped_masked_bf16) instead of reading a dres tensor
+    that the BatchNorm backward would have written."""
+
+    def __init__(self, dy, mask):
+        self.dy = dy
+        self.mask = mask

@@ -34,7 +34,7 @@ from . import _lib as L
 from .bn import MASK_FROM_X
 from .conv import CL, _cpad, _desc, _desc_hw, _like_param, _prepped, _splitk_ws, _stem_geom, stem_pack, \
     stem_pack_grouped
-from .gradsink import GradJoin, sink_done, sink_pending, sink_target
+from .gradsink import GradJoin, MaskedAddend, sink_done, sink_pending, sink_target
 
 BF = torch.bfloat16
 ENABLED = os.environ.get("GM_VTRUNK", "1") != "0"
@@ -59,6 +59,12 @@ EPI_BN_STATS = True
 # the block-output BatchNorm (+ residual + ReLU) writes its ReLU mask as bits (1/16 of y) and the
 # backward reads them in place of y (False: the backward reads y)
 BN_RELU_MASK = True
+# with it, a downsample block's residual BN backward reads the block output BN's dy and ReLU mask
+# (the fused backward's mask mode) instead of the dres = dz tensor that BN would otherwise write
+DS_DZ_LINK = True
+# and an identity block's: the block input's gradient join hands conv1's dgrad the pending addend as
+# (dy, mask) (gradsink.MaskedAddend; gm_conv2d_dgrad_grouped_masked_bf16) - no dres either
+IDT_MASKED_ADDEND = True
 # the ReLU-after-BN backward (bn1 / bn2 of a block) takes its statistics from the input-gradient
 # epilogue of the convolution it feeds, then one finalize + one streaming apply
 # (False: the single-launch backward)
@@ -261,9 +267,20 @@ class _VConvFn(torch.autograd.Function):
             d = _desc(N, H, W, C, K, R, S, stride, pad)
 
             def dgrad(add):
-                if add is not None and (tuple(add.shape) != (GN, C, H, W) or add.dtype != BF
-                                        or not add.is_contiguous(memory_format=CL)):
+                madd = add if isinstance(add, MaskedAddend) else None
+                at = madd.dy if madd is not None else add
+                if at is not None and (tuple(at.shape) != (GN, C, H, W) or at.dtype != BF
+                                       or not at.is_contiguous(memory_format=CL)):
                     raise ValueError("vtrunk conv dgrad: addend must be bf16 channels_last shaped like dx")
+                if madd is not None:  # dx = dgrad + dy where the block output's ReLU passed
+                    if madd.mask.numel() * 8 != at.numel():
+                        raise ValueError("vtrunk conv dgrad: addend mask must hold one bit per element")
+                    out = torch.empty(GN, C, H, W, device=dev, dtype=BF, memory_format=CL)
+                    ws, nb = _splitk_g(dev, d, G, True)
+                    L.check(lib.gm_conv2d_dgrad_grouped_masked_bf16(
+                        ctypes.byref(d), G, gy.data_ptr(), wt.data_ptr(), st, out.data_ptr(), at.data_ptr(),
+                        madd.mask.data_ptr(), ws, nb, L.stream_of(dev)), "gm_conv2d_dgrad_grouped_masked_bf16")
+                    return out
                 out = add if add is not None else torch.empty(GN, C, H, W, device=dev, dtype=BF, memory_format=CL)
                 ws, nb = _splitk_g(dev, d, G, True)
                 lk = ctx.dlink
@@ -463,6 +480,10 @@ class _VBNFn(torch.autograd.Function):
         ctx.save_for_backward(xb, y if relu and not maskx else coef, sm, si, ymask, *gammas, *betas)
         ctx.meta = (G, maskx, relu, residual is not None)
         ctx.blink = stats.get("bn_link") if stats is not None else None
+        # res_link (block output BN): the residual's BN backward takes this BN's dy and ReLU
+        # mask instead of a materialised dres; dz_link (that residual BN): where it finds them
+        ctx.rlink = stats.get("res_link") if stats is not None and ymask is not None else None
+        ctx.zlink = stats.get("dz_link") if stats is not None and not relu and residual is None else None
         if ctx.blink is not None and maskx and G >= 2 and C % 64 == 0:
             ctx.blink["bn"] = (xb, coef, sm)  # for the consuming convolution's input-gradient epilogue
         return y
@@ -483,6 +504,30 @@ class _VBNFn(torch.autograd.Function):
                 dx, gw, gb = _bn_backward_from_stats(pdy, xb, G, gammas, betas, sm, si, coef, part, rows,
                                                      want_w, want_b)
                 return (dx if ctx.needs_input_grad[0] else None, None, None, None, None, None, None, *gw, *gb)
+        zl = ctx.zlink
+        if zl is not None and "dz" in zl:  # dy is the block output's: dz = dy where its ReLU passed
+            dyo, yo, mo = zl.pop("dz")
+            if dy.data_ptr() != dyo.data_ptr() or dy.shape != dyo.shape:
+                raise L.GreedyMMLError("vtrunk BatchNorm: the residual's gradient is not the block output's dy")
+            dx, _, gw, gb = _bn_backward(dyo, yo, xb, G, gammas, betas, sm, si, True, False, None,
+                                         want_w, want_b, mo)
+            return (dx if ctx.needs_input_grad[0] else None, None, None, None, None, None, None, *gw, *gb)
+        join = ctx.join
+        if (want_dres and join is not None and ymask is not None and IDT_MASKED_ADDEND and join.masked_ok
+                and join.first_of_many()):
+            # the identity branch: the block input's other consumer (conv1) forms dz = dy . mask
+            # in its dgrad epilogue; no dres written here
+            dyb = _nhwc(dy.to(BF))
+            dx, _, gw, gb = _bn_backward(dyb, y, xb, G, gammas, betas, sm, si, relu, False, coef,
+                                         want_w, want_b, ymask)
+            join.contribute(lambda add: MaskedAddend(dyb, ymask))
+            return (dx if ctx.needs_input_grad[0] else None, None, None, None, None, None, None, *gw, *gb)
+        if want_dres and ctx.rlink is not None and DS_DZ_LINK:
+            dyb = _nhwc(dy.to(BF))
+            ctx.rlink["dz"] = (dyb, y, ymask)
+            dx, _, gw, gb = _bn_backward(dyb, y, xb, G, gammas, betas, sm, si, relu, False, coef,
+                                         want_w, want_b, ymask)
+            return (dx if ctx.needs_input_grad[0] else None, dyb, None, None, None, None, None, *gw, *gb)
         dx, dres, gw, gb = _bn_backward(dy, y, xb, G, gammas, betas, sm, si, relu, want_dres, coef,
                                         want_w, want_b, ymask)
         if dres is not None and ctx.join is not None:
@@ -731,15 +776,18 @@ def vblock(blocks, X):
     b0 = blocks[0]
     join = GradJoin()
     ds = b0.downsample is not None
+    join.masked_ok = not ds  # its consumers: conv1 (vconv takes a MaskedAddend) and the output BN
 
-    def cbn(x, convs, bns, cjoin=None, link_in=None, link_out=None, **kw):
+    def cbn(x, convs, bns, cjoin=None, link_in=None, link_out=None, res_link=None, **kw):
         # conv -> BatchNorm, the forward statistics from the conv's epilogue; link_out: this
         # BN (+ ReLU) feeds the next conv, whose input-gradient epilogue then sums this BN's
-        # backward statistics (link_in of that conv)
-        st = {"dgrad_link": link_in, "bn_link": link_out}
+        # backward statistics (link_in of that conv); res_link: the downsample BN <-> the block
+        # output BN whose residual it is (its only consumer)
+        st = {"dgrad_link": link_in, "bn_link": link_out, "dz_link": res_link, "res_link": res_link}
         return vbn(vconv(x, convs, cjoin, stats=st), bns, stats=st, **kw)
+    rl = {} if ds else None
     if ds:
-        idt = cbn(X, [b.downsample[0] for b in blocks], [b.downsample[1] for b in blocks], join)
+        idt = cbn(X, [b.downsample[0] for b in blocks], [b.downsample[1] for b in blocks], join, res_link=rl)
     else:
         idt = X
     l1 = {}
@@ -748,9 +796,9 @@ def vblock(blocks, X):
         l2 = {}
         out = cbn(out, [b.conv2 for b in blocks], [b.bn2 for b in blocks], link_in=l1, link_out=l2, relu=True)
         return cbn(out, [b.conv3 for b in blocks], [b.bn3 for b in blocks], link_in=l2, residual=idt, relu=True,
-                   residual_join=None if ds else join)
+                   residual_join=None if ds else join, res_link=rl)
     return cbn(out, [b.conv2 for b in blocks], [b.bn2 for b in blocks], link_in=l1, residual=idt, relu=True,
-               residual_join=None if ds else join)
+               residual_join=None if ds else join, res_link=rl)
 
 
 def vlayer(nets, i, X):

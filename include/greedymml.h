@@ -444,6 +444,15 @@ int gm_conv2d_fwd_grouped_bf16(const gm_conv_desc_hw* d, int G, const void* x, c
                                void* y, void* ws, size_t ws_bytes, void* stream);
 int gm_conv2d_dgrad_grouped_bf16(const gm_conv_desc* d, int G, const void* dy, const void* wt, long long wt_stride,
                                  void* dx, const void* addend, void* ws, size_t ws_bytes, void* stream);
+/* The same with a MASKED addend: dx = dgrad + (addend where addend_mask's bit is set) - the
+ * identity branch's gradient dz = dy . [y > 0] of a block-output ReLU (reference resnet.py
+ * BasicBlock/Bottleneck `out += identity; out = relu(out)`) formed in the epilogue from that
+ * ReLU's dy and the BatchNorm forward's 1-bit mask (gm_bn_fwd: relu_mask; bit e of byte i =
+ * element 8 i + e, group g's at addend_mask + g*N*H*W*C/8) instead of a dres tensor the BN
+ * backward would write and this launch read.  addend != dx; C a multiple of 8. */
+int gm_conv2d_dgrad_grouped_masked_bf16(const gm_conv_desc* d, int G, const void* dy, const void* wt,
+                                        long long wt_stride, void* dx, const void* addend, const void* addend_mask,
+                                        void* ws, size_t ws_bytes, void* stream);
 size_t gm_conv2d_splitk_ws_bytes_grouped(const gm_conv_desc* d, int G, int dgrad);
 size_t gm_conv2d_wgrad_grouped_scratch(const gm_conv_desc_hw* d, int G);
 int gm_conv2d_wgrad_grouped_bf16(const gm_conv_desc_hw* d, int G, const void* dy, const void* x, float* dw,

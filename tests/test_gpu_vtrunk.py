@@ -389,3 +389,100 @@ def test_stem_wgrad_forms_bn_pool_dy(dev, G, B, H, W):
         for a, b, name in zip(res[True][g], res[False][g], ("stem dw", "dgamma", "dbeta")):
             assert torch.equal(a, b), (g, name, float((a - b).abs().max()))
         assert float(res[True][g][0].abs().max()) > 0
+
+
+def _masked(add, mask):
+    """The dres the BN backward writes: add where the mask bit is set (bit e of byte i = element
+    8 i + e of the channels-last storage order), else 0."""
+    flat = add.permute(0, 2, 3, 1).reshape(-1)
+    bits = ((mask.to(torch.int32)[:, None] >> torch.arange(8, device=mask.device)) & 1).reshape(-1).bool()
+    out = torch.where(bits, flat, torch.zeros((), dtype=flat.dtype, device=flat.device))
+    N, C, H, W = add.shape
+    return out.reshape(N, H, W, C).permute(0, 3, 1, 2).contiguous(memory_format=CL)
+
+
+MASKED_SHAPES = CONV_SHAPES + [
+    (4, 256, 14, 14, 64, 1, 1, 1, 0),    # 1x1 s1 input gradient: k_gemm_ring (the bottleneck's conv1)
+    (4, 64, 28, 28, 256, 1, 1, 1, 0),    # k_gemm_ring, 64 output channels
+]
+
+
+@pytest.mark.parametrize("G", [2, 1])
+@pytest.mark.parametrize("shape", MASKED_SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_masked_addend_dgrad_is_exact(dev, shape, G):
+    """gm_conv2d_dgrad_grouped_masked_bf16 (the identity branch's dz = dy . mask formed in the
+    input-gradient epilogue: k_conv_rw, k_conv_h9 / k_conv_igemm_ut via store_tile_lds, k_gemm_ring,
+    the strided zero/copy pass, and - G = 1 - the halo / lean kernels through the materialised
+    copy) against the plain fused addend holding the masked values: bit-identical."""
+    from greedy_multimodal_learning_amd.conv import GMConv2d
+    from greedy_multimodal_learning_amd.gradsink import GradJoin, MaskedAddend
+    from greedy_multimodal_learning_amd.vtrunk import vconv
+    N, C, H, W, K, R, S, st, pad = shape
+    if C % 32:
+        pytest.skip("the masked addend needs C % 32 == 0")
+    g = torch.Generator().manual_seed(sum(shape) + 7 * G)
+    x = torch.randn(G * N, C, H, W, generator=g).bfloat16().to(dev).contiguous(memory_format=CL)
+    mods = []
+    for _ in range(G):
+        m = GMConv2d(C, K, (R, S), stride=st, padding=pad, bias=False).to(dev)
+        with torch.no_grad():
+            m.weight.copy_(torch.randn(K, C, R, S, generator=g) / (C * R * S) ** 0.5)
+        mods.append(m.to(memory_format=CL))
+    P, Q = (H + 2 * pad - R) // st + 1, (W + 2 * pad - S) // st + 1
+    gy = torch.randn(G * N, K, P, Q, generator=g).bfloat16().to(dev).contiguous(memory_format=CL)
+    add = torch.randn(G * N, C, H, W, generator=g).bfloat16().to(dev).contiguous(memory_format=CL)
+    mask = torch.randint(0, 256, (add.numel() // 8,), generator=g, dtype=torch.uint8).to(dev)
+    grads = []
+    for masked in (True, False):
+        xd = x.clone().requires_grad_(True)
+        jn = GradJoin()
+        jn.masked_ok = True
+        y = vconv(xd, mods, jn)
+        jn.register()
+        assert jn.first_of_many()
+        pend = MaskedAddend(add, mask) if masked else _masked(add, mask)
+        assert jn.contribute(lambda a: pend) is None
+        y.backward(gy)
+        torch.cuda.synchronize()
+        grads.append(xd.grad.clone())
+    assert torch.equal(grads[0], grads[1]), float((grads[0].float() - grads[1].float()).abs().max())
+    assert float(grads[0].float().abs().max()) > 0
+
+
+@pytest.mark.parametrize("arch", ["resnet18", "resnet50"])
+def test_block_dres_elision_is_exact(dev, arch):
+    """The block-output BN backward writes no dres: identity blocks hand conv1's dgrad (dy, ReLU
+    mask) as a masked join addend, downsample blocks' residual BN backward reads dy and the mask
+    itself (vtrunk.IDT_MASKED_ADDEND / DS_DZ_LINK) - every gradient bit-identical to the dres path
+    over layer1..layer4 of two views."""
+    from greedy_multimodal_learning_amd import vtrunk
+    from greedy_multimodal_learning_amd import resnet
+    torch.manual_seed(21)
+    nets = [getattr(resnet, arch)().to(dev).to(memory_format=CL).train() for _ in range(2)]
+    init = [{k: v.clone() for k, v in n.state_dict().items()} for n in nets]
+    B, H = 3, 32
+    x = torch.randn(2 * B, 64, H, H, device=dev).bfloat16().contiguous(memory_format=CL)
+    res = {}
+    for on in (True, False):
+        for n, sd in zip(nets, init):
+            n.load_state_dict(sd)
+            for p in n.parameters():
+                p.grad = None
+        old = (vtrunk.IDT_MASKED_ADDEND, vtrunk.DS_DZ_LINK)
+        vtrunk.IDT_MASKED_ADDEND = vtrunk.DS_DZ_LINK = on
+        try:
+            X = x.clone().requires_grad_(True)
+            Y = X
+            for i in (1, 2, 3, 4):
+                Y = vtrunk.vlayer(nets, i, Y)
+            gY = torch.randn(Y.shape, generator=torch.Generator(device=dev).manual_seed(4), device=dev).bfloat16()
+            Y.backward(gY.contiguous(memory_format=CL))
+        finally:
+            vtrunk.IDT_MASKED_ADDEND, vtrunk.DS_DZ_LINK = old
+        torch.cuda.synchronize()
+        res[on] = (X.grad.clone(), [(k, p.grad.clone()) for n in nets for k, p in n.named_parameters()
+                                    if p.grad is not None])
+    assert torch.equal(res[True][0], res[False][0]), "input gradient"
+    assert len(res[True][1]) == len(res[False][1]) > 0
+    for (k, a), (_, b) in zip(res[True][1], res[False][1]):
+        assert torch.equal(a, b), (k, float((a - b).abs().max()))
