@@ -9,6 +9,8 @@ ARMSET: layout      - flat parameter layout: model.grad_order vs reverse registr
         wgrad_batch - weight-gradient launches handed to the side stream in batches of 8 / 4 / 2
         stem_wgrad  - the stem weight gradient forming its dy from the BN + pool backward's operands
                       (vtrunk.FUSED_STEM_WGRAD) vs the BN apply pass writing dy
+        dres        - the block-output BN backward without dres (vtrunk.IDT_MASKED_ADDEND + DS_DZ_LINK)
+                      vs writing it
 """
 import os
 import sys
@@ -50,6 +52,12 @@ def arms(name):
         def setb(n):
             vtrunk.WGRAD_BATCH = n
         return [(f"batch{n}", (lambda n=n: setb(n))) for n in (8, 4, 2)]
+    if name == "dres":
+        from greedy_multimodal_learning_amd import vtrunk
+
+        def setd(on):
+            vtrunk.IDT_MASKED_ADDEND = vtrunk.DS_DZ_LINK = on
+        return [("no_dres", lambda: setd(True)), ("dres", lambda: setd(False))]
     if name == "bind":
         return [("bound", lambda: None), ("copied", lambda: None)]
     raise SystemExit(f"unknown arm set {name}")
