@@ -11,6 +11,7 @@ ARMSET: layout      - flat parameter layout: model.grad_order vs reverse registr
                       (vtrunk.FUSED_STEM_WGRAD) vs the BN apply pass writing dy
         dres        - the block-output BN backward without dres (vtrunk.IDT_MASKED_ADDEND + DS_DZ_LINK)
                       vs writing it
+        bnchunk     - the single-launch BN backward over view chunks of <= 112 / 56 MB of x + dy vs one launch
 """
 import os
 import sys
@@ -58,6 +59,13 @@ def arms(name):
         def setd(on):
             vtrunk.IDT_MASKED_ADDEND = vtrunk.DS_DZ_LINK = on
         return [("no_dres", lambda: setd(True)), ("dres", lambda: setd(False))]
+    if name == "bnchunk":
+        from greedy_multimodal_learning_amd import vtrunk
+
+        def setc(n):
+            vtrunk.BN_BWD_CHUNK_BYTES = n
+        return [("chunk112", lambda: setc(112 << 20)), ("one_launch", lambda: setc(0)),
+                ("chunk56", lambda: setc(56 << 20))]
     if name == "bind":
         return [("bound", lambda: None), ("copied", lambda: None)]
     raise SystemExit(f"unknown arm set {name}")
