@@ -267,3 +267,29 @@ def test_losses_match_oracle():
     assert float(blend_loss(outs, y)) == pytest.approx(float(gating_ref.blend_loss(outs, y)), rel=1e-6)
     assert float(acc(outs, y)) == float(gating_ref.acc(outs, y))
     assert float(acc(outs[0], y[:2])) == float(gating_ref.acc(outs[0], y[:2]))
+
+
+def test_grad_join_order_and_masked_pending():
+    """gradsink.GradJoin (the block-input gradient join): every consumer but the last leaves its
+    gradient pending and gets None; the last one's compute receives it; first_of_many() says when
+    a consumer's contribution will be left pending (the block-output BN then hands a MaskedAddend
+    instead of writing dres); the join resets for the next backward."""
+    import torch
+    from greedy_multimodal_learning_amd.gradsink import GradJoin, MaskedAddend
+    jn = GradJoin()
+    assert not jn.masked_ok
+    jn.register()
+    jn.register()
+    for _ in range(2):  # two backward passes through the same join
+        assert jn.first_of_many()
+        dy, mask = torch.ones(2, 8), torch.full((2,), 0xA5, dtype=torch.uint8)
+        assert jn.contribute(lambda add: MaskedAddend(dy, mask) if add is None else None) is None
+        assert not jn.first_of_many()
+        seen = []
+        out = jn.contribute(lambda add: seen.append(add) or "dx")
+        assert out == "dx" and isinstance(seen[0], MaskedAddend) and seen[0].dy is dy and seen[0].mask is mask
+        assert jn.pending is None and jn.done == 0
+    single = GradJoin()
+    single.register()
+    assert not single.first_of_many()  # a lone consumer is always the last
+    assert single.contribute(lambda add: add) is None
