@@ -35,6 +35,9 @@ struct RingGemmArgs {
     uint16_t* out;           // [G][M][N]
     const uint16_t* addend;  // [G][M][N] or null (may alias out)
     const uint8_t* amask;    // with it, optional: its 1-bit mask (mask_bf2), [G][M * N / 8]
+    // A rows gathered from a strided 1x1 convolution's input (forward, stride sst > 0): row m =
+    // output pixel (b, p, q) of [.][sP][sQ] reads input pixel (b, sst p, sst q) of [.][sH][sW]
+    int sst, sH, sW, sP, sQ;
     int M, N, Kr;            // per group
     int G, tiles_m, tiles_n, tiles;  // tiles = G * tiles_m * tiles_n
     long long gsA, gsB, gsO; // group strides (elements; gsB may be negative)
@@ -100,7 +103,23 @@ __global__ __launch_bounds__(512) void k_gemm_ring(RingGemmArgs a) {
         const int r8 = lane >> 3, ch = lane & 7;
         int slot = 0, ut = 0, uk = 0;  // next unit to issue: tile index ut, k-step uk
         int g = 0, m0 = 0, n0 = 0;
-        if (nunits > 0) tile_of(0, g, m0, n0);
+        long long ar[PA];  // this tile's A row offsets (elements; -1: past M), once per tile
+        auto rows_of = [&]() __attribute__((always_inline)) {
+#pragma unroll
+            for (int j = 0; j < PA; ++j) {
+                const int m = m0 + (lw * PA + j) * 8 + r8;
+                long long o = (long long)m;
+                if (a.sst) {
+                    const int PQ = a.sP * a.sQ, b = m / PQ, pq = m - b * PQ, p = pq / a.sQ, q = pq - p * a.sQ;
+                    o = ((long long)b * a.sH + (long long)a.sst * p) * a.sW + (long long)a.sst * q;
+                }
+                ar[j] = m < a.M ? o * a.Kr : -1;
+            }
+        };
+        if (nunits > 0) {
+            tile_of(0, g, m0, n0);
+            rows_of();
+        }
         auto issue = [&]() __attribute__((always_inline)) {
             const unsigned sb = (unsigned)slot * SLOT;
             const uint16_t* Ag = a.A + g * a.gsA;
@@ -109,9 +128,8 @@ __global__ __launch_bounds__(512) void k_gemm_ring(RingGemmArgs a) {
 #pragma unroll
             for (int j = 0; j < PA; ++j) {
                 const int row = (lw * PA + j) * 8 + r8;
-                const int m = m0 + row;
                 const int c = (ch ^ ((row >> 1) & 7)) << 3;
-                const void* src = m < a.M ? (const void*)(Ag + (size_t)m * a.Kr + k0 + c) : zero;
+                const void* src = ar[j] >= 0 ? (const void*)(Ag + ar[j] + k0 + c) : zero;
                 __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(lds + sb + (lw * PA + j) * 1024), 16, 0, 0);
             }
 #pragma unroll
@@ -124,7 +142,10 @@ __global__ __launch_bounds__(512) void k_gemm_ring(RingGemmArgs a) {
             slot = slot + 1 == S ? 0 : slot + 1;
             if (++uk == nk) {
                 uk = 0;
-                if (++ut < ntiles) tile_of(ut, g, m0, n0);
+                if (++ut < ntiles) {
+                    tile_of(ut, g, m0, n0);
+                    rows_of();
+                }
             }
         };
         for (int i = 0; i < D && i < nunits; ++i) issue();
@@ -370,11 +391,16 @@ static int g_ring_cus = [] {
     return n;
 }();
 
-// gm_conv_set_1x1_gemm: 1 (default) = 1x1 / s1 shapes take k_gemm_ring,
-// 0 = the im2col kernel
+// gm_conv_set_1x1_gemm: 2 (default) = 1x1 / s1 shapes and 1x1 / s2 forwards (the downsamples, A rows
+// gathered) take k_gemm_ring, 1 = the s1 shapes only, 0 = the im2col kernel
 int g_conv_1x1 = [] {
-    return 1;
+    return 2;
 }();
+
+bool conv1x1s_ok(int R, int S, int sh, int sw, int ph, int pw, long long M, int Kr, int N) {
+    return g_conv_1x1 >= 2 && R == 1 && S == 1 && sh == 2 && sw == 2 && ph == 0 && pw == 0 && M >= 1 &&
+           Kr % 64 == 0 && Kr >= 64 && (N % 128 == 0 || N == 64) && M * (long long)(Kr > N ? Kr : N) < (1ll << 30);
+}
 
 bool conv1x1_ok(int R, int S, int sh, int sw, int ph, int pw, long long M, int Kr, int N) {
     return g_conv_1x1 && R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0 && M >= 1 && Kr % 64 == 0 &&
@@ -384,9 +410,13 @@ bool conv1x1_ok(int R, int S, int sh, int sw, int ph, int pw, long long M, int K
 // Out = A . B^T (+ addend) per group; the caller checked conv1x1_ok
 int conv1x1_gemm(long long M, int Kr, int N, int G, const void* A, long long gsA, const void* B, long long gsB,
                  void* out, long long gsO, const void* addend, hipStream_t st, const char* fn, float* stats,
-                 const uint16_t* bnx, const float* bncoef, const float* bnmean, const uint8_t* amask) {
+                 const uint16_t* bnx, const float* bncoef, const float* bnmean, const uint8_t* amask,
+                 const int* sgeo) {
     RingGemmArgs r;
     memset(&r, 0, sizeof(r));
+    if (sgeo) {  // {stride, H, W, P, Q}: A rows gathered from the strided input
+        r.sst = sgeo[0]; r.sH = sgeo[1]; r.sW = sgeo[2]; r.sP = sgeo[3]; r.sQ = sgeo[4];
+    }
     r.A = (const uint16_t*)A;
     r.B = (const uint16_t*)B;
     r.out = (uint16_t*)out;
@@ -426,6 +456,6 @@ int conv1x1_gemm(long long M, int Kr, int N, int G, const void* A, long long gsA
 }  // namespace gm
 
 extern "C" int gm_conv_set_1x1_gemm(int on) {
-    gm::g_conv_1x1 = on ? 1 : 0;
+    gm::g_conv_1x1 = on < 0 ? 2 : on > 2 ? 2 : on;
     return GM_OK;
 }

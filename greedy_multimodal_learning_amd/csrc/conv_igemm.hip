@@ -2939,10 +2939,11 @@ extern "C" int gm_conv_set_pipe(int pipe) {
 // 1x1 / s1 / p0 convolutions as plain GEMMs (conv1x1.hip, k_gemm_ring)
 namespace gm {
 bool conv1x1_ok(int R, int S, int sh, int sw, int ph, int pw, long long M, int Kr, int N);
+bool conv1x1s_ok(int R, int S, int sh, int sw, int ph, int pw, long long M, int Kr, int N);
 int conv1x1_gemm(long long M, int Kr, int N, int G, const void* A, long long gsA, const void* B, long long gsB,
                  void* out, long long gsO, const void* addend, hipStream_t st, const char* fn,
                  float* stats = nullptr, const uint16_t* bnx = nullptr, const float* bncoef = nullptr,
-                 const float* bnmean = nullptr, const uint8_t* amask = nullptr);
+                 const float* bnmean = nullptr, const uint8_t* amask = nullptr, const int* sgeo = nullptr);
 }  // namespace gm
 
 extern "C" int gm_conv2d_fwd_hw_bf16(const gm_conv_desc_hw* d, const void* x, const void* w, void* y,
@@ -2996,6 +2997,15 @@ extern "C" int gm_conv2d_fwd_grouped_bf16(const gm_conv_desc_hw* d, int G, const
         if (gm::conv1x1_ok(d->R, d->S, d->stride_h, d->stride_w, d->pad_h, d->pad_w, M, d->C, d->K))
             return gm::conv1x1_gemm(M, d->C, d->K, G, x, M * d->C, w, w_stride, y, M * d->K, nullptr,
                                     as_stream(stream), "conv1x1 fwd");
+        const int P = (d->H - 1) / 2 + 1, Q = (d->W - 1) / 2 + 1;
+        const long long Mo = (long long)d->N * P * Q;
+        if (gm::conv1x1s_ok(d->R, d->S, d->stride_h, d->stride_w, d->pad_h, d->pad_w, Mo, d->C, d->K) &&
+            M * d->C < (1ll << 30)) {  // the downsample: A rows gathered at stride 2
+            const int geo[5] = {2, d->H, d->W, P, Q};
+            return gm::conv1x1_gemm(Mo, d->C, d->K, G, x, M * d->C, w, w_stride, y, Mo * d->K, nullptr,
+                                    as_stream(stream), "conv1x1/s2 fwd", nullptr, nullptr, nullptr, nullptr, nullptr,
+                                    geo);
+        }
     }
     ConvArgs a;
     fwd_setup(d, x, w, y, a);
@@ -3048,6 +3058,17 @@ extern "C" int gm_conv2d_fwd_grouped_bn_stats_bf16(const gm_conv_desc_hw* d, int
         *rows_out = (int)((M + 63) / 64);
         return gm::conv1x1_gemm(M, d->C, d->K, G, x, M * d->C, w, w_stride, y, M * d->K, nullptr,
                                 as_stream(stream), "conv1x1 fwd", stats);
+    }
+    {
+        const long long Mi = (long long)d->N * d->H * d->W;
+        if (gm::conv1x1s_ok(d->R, d->S, d->stride_h, d->stride_w, d->pad_h, d->pad_w, M, d->C, d->K) &&
+            Mi * d->C < (1ll << 30)) {  // the downsample: A rows gathered at stride 2 (M = output pixels)
+            const int geo[5] = {2, d->H, d->W, a.cls[0].P, a.cls[0].Q};
+            *rows_out = (int)((M + 63) / 64);
+            return gm::conv1x1_gemm(M, d->C, d->K, G, x, Mi * d->C, w, w_stride, y, M * d->K, nullptr,
+                                    as_stream(stream), "conv1x1/s2 fwd", stats, nullptr, nullptr, nullptr, nullptr,
+                                    geo);
+        }
     }
     a.G = G;
     a.gs_in = (long long)d->N * d->H * d->W * d->C;

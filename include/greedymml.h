@@ -377,8 +377,9 @@ int gm_conv_set_splitk(int target);
 int gm_conv_set_wgrad_loop(int mode);
 /* 1x1 / stride-1 / pad-0 forward and input-gradient convolutions as plain NT GEMMs on
  * k_gemm_ring (conv1x1.hip: persistent, loader waves feeding a 4-slot LDS ring; C % 64 == 0 and
- * the output channels % 128 == 0 or == 64).  Default on (
- * gm_conv_set_1x1_gemm(0) route them back to the im2col kernels). */
+ * the output channels % 128 == 0 or == 64).  Mode 2 (default) also runs the grouped 1x1 / stride-2 /
+ * pad-0 forwards (the ResNet downsamples) there, the A rows gathered at stride 2; 1 = stride-1 shapes
+ * only; 0 = every 1x1 back on the im2col kernels. */
 int gm_conv_set_1x1_gemm(int on);
 /* Weight-gradient operand staging: 0 = LDS-DMA pieces, 1 = register-staged (global_load_dwordx4
  * two steps ahead + ds_write_b128; same LDS image and arithmetic), 2 (default) = register-staged

@@ -649,7 +649,7 @@ def test_conv1x1_gemm_vs_fp32(dev, shape):
             torch.cuda.synchronize()
             res[mode] = (y, dx, dxa, dws)
     finally:
-        L.check(lib.gm_conv_set_1x1_gemm(1), "1x1 gemm")  # the default
+        L.check(lib.gm_conv_set_1x1_gemm(2), "1x1 gemm")  # the default
     for g in range(G):
         sl = slice(g * N, (g + 1) * N)
         xf, dyf, wf = x[sl].float().reshape(-1, C), dy[sl].float().reshape(-1, K), w[g].float()
@@ -661,6 +661,57 @@ def test_conv1x1_gemm_vs_fp32(dev, shape):
             _close(dxa[sl].reshape(-1, C), dxr + add[sl].float().reshape(-1, C), 1e-2)
             _close(dws[0][g], dwr, 2e-3)
             _close(dws[1][g] - 0.5, dwr, 2e-3)
+
+
+@pytest.mark.parametrize("shape", [(2, 256, 56, 56, 512, 2), (3, 64, 28, 28, 128, 2), (2, 1024, 14, 14, 2048, 3),
+                                   (1, 64, 15, 13, 128, 2), (2, 512, 28, 28, 1024, 12)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_conv1x1_s2_forward_gathers_rows(dev, shape):
+    """The 1x1 / s2 downsample forward on k_gemm_ring with its A rows gathered at stride 2
+    (gm_conv_set_1x1_gemm(2), the default) - plain and with the BatchNorm statistics epilogue -
+    against fp32 PyTorch and the im2col kernel (mode 1); odd maps (15 x 13 -> 8 x 7)."""
+    import ctypes
+    from greedy_multimodal_learning_amd import _lib as L
+    from greedy_multimodal_learning_amd import conv as CV
+    N, C, H, W, K, G = shape
+    P, Q = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    torch.manual_seed(sum(shape))
+    x = torch.randn(G * N, H, W, C, device=dev).bfloat16()
+    w = (torch.randn(G, K, C, device=dev) / C ** 0.5).bfloat16()
+    lib = L.load()
+    st = L.stream_of(dev)
+    dh = CV._desc_hw(N, H, W, C, K, 1, 1, 2, 2, 0, 0)
+    nf = lib.gm_conv2d_fwd_bn_stats_floats(ctypes.byref(dh), G)
+    res = {}
+    try:
+        for mode in (2, 1):
+            L.check(lib.gm_conv_set_1x1_gemm(mode), "1x1 gemm")
+            y = torch.empty(G * N, P, Q, K, device=dev, dtype=torch.bfloat16)
+            L.check(lib.gm_conv2d_fwd_grouped_bf16(ctypes.byref(dh), G, x.data_ptr(), w.data_ptr(), K * C,
+                                                   y.data_ptr(), 0, 0, st), "fwd")
+            ys = torch.empty_like(y)
+            part = torch.zeros(max(nf, 1), device=dev)
+            rows = ctypes.c_int(0)
+            rc = lib.gm_conv2d_fwd_grouped_bn_stats_bf16(ctypes.byref(dh), G, x.data_ptr(), w.data_ptr(), K * C,
+                                                         ys.data_ptr(), part.data_ptr(), nf, ctypes.byref(rows),
+                                                         0, 0, st)
+            torch.cuda.synchronize()
+            res[mode] = (y, ys if rc == 0 else None, part, rows.value)
+    finally:
+        L.check(lib.gm_conv_set_1x1_gemm(2), "1x1 gemm")
+    y2, ys2, part2, rows2 = res[2]
+    assert ys2 is not None and torch.equal(ys2, y2)
+    for g in range(G):
+        sl = slice(g * N, (g + 1) * N)
+        xs = x[sl, ::2, ::2, :].float().reshape(-1, C)
+        yr = xs @ w[g].float().t()
+        for mode in (2, 1):
+            _close(res[mode][0][sl].reshape(-1, K), yr, 1e-2)
+        # the epilogue's partial rows: per 64-channel slice, rows x [64][sum, sum of squares]
+        pg = part2[g * 2 * K * (rows2 + 1):][:K * rows2 * 2].view(K // 64, rows2, 64, 2).sum(1).reshape(K, 2)
+        yv = y2[sl].float().reshape(-1, K)
+        _close(pg[:, 0], yv.sum(0), 1e-4)
+        _close(pg[:, 1], (yv * yv).sum(0), 1e-4)
 
 
 @pytest.mark.parametrize("case", [("bf16_cl", 2, 4, 224, 224), ("bf16_cl", 3, 2, 37, 30), ("f32_nchw", 2, 3, 64, 64),

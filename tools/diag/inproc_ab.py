@@ -11,6 +11,7 @@ ARMSET: layout      - flat parameter layout: model.grad_order vs reverse registr
                       (vtrunk.FUSED_STEM_WGRAD) vs the BN apply pass writing dy
         dres        - the block-output BN backward without dres (vtrunk.IDT_MASKED_ADDEND + DS_DZ_LINK)
                       vs writing it
+        ds1x1       - the 1x1 / s2 downsample forwards on k_gemm_ring (gathered A rows) vs k_conv_igemm_ut
         bnchunk     - the single-launch BN backward over view chunks of <= 112 / 56 MB of x + dy vs one launch
 """
 import os
@@ -66,6 +67,10 @@ def arms(name):
             vtrunk.BN_BWD_CHUNK_BYTES = n
         return [("chunk112", lambda: setc(112 << 20)), ("one_launch", lambda: setc(0)),
                 ("chunk56", lambda: setc(56 << 20))]
+    if name == "ds1x1":
+        def setm(m):
+            L.check(L.load().gm_conv_set_1x1_gemm(m), "1x1 gemm")
+        return [("ring_s2", lambda: setm(2)), ("igemm_s2", lambda: setm(1))]
     if name == "bind":
         return [("bound", lambda: None), ("copied", lambda: None)]
     raise SystemExit(f"unknown arm set {name}")
