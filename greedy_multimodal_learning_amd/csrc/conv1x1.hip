@@ -36,8 +36,11 @@ struct RingGemmArgs {
     const uint16_t* addend;  // [G][M][N] or null (may alias out)
     const uint8_t* amask;    // with it, optional: its 1-bit mask (mask_bf2), [G][M * N / 8]
     // A rows gathered from a strided 1x1 convolution's input (forward, stride sst > 0): row m =
-    // output pixel (b, p, q) of [.][sP][sQ] reads input pixel (b, sst p, sst q) of [.][sH][sW]
-    int sst, sH, sW, sP, sQ;
+    // output pixel (b, p, q) of [.][sP][sQ] reads input pixel (b, sst p, sst q) of [.][sH][sW];
+    // scatter (input gradient): A = dy rows read densely, out row m written to input pixel
+    // (b, sst p, sst q) of the [orows = M / (sP sQ) * sH * sW][N] output
+    int sst, sH, sW, sP, sQ, scatter;
+    long long orows;
     int M, N, Kr;            // per group
     int G, tiles_m, tiles_n, tiles;  // tiles = G * tiles_m * tiles_n
     long long gsA, gsB, gsO; // group strides (elements; gsB may be negative)
@@ -109,7 +112,7 @@ __global__ __launch_bounds__(512) void k_gemm_ring(RingGemmArgs a) {
             for (int j = 0; j < PA; ++j) {
                 const int m = m0 + (lw * PA + j) * 8 + r8;
                 long long o = (long long)m;
-                if (a.sst) {
+                if (a.sst && !a.scatter) {
                     const int PQ = a.sP * a.sQ, b = m / PQ, pq = m - b * PQ, p = pq / a.sQ, q = pq - p * a.sQ;
                     o = ((long long)b * a.sH + (long long)a.sst * p) * a.sW + (long long)a.sst * q;
                 }
@@ -234,7 +237,7 @@ __global__ __launch_bounds__(512) void k_gemm_ring(RingGemmArgs a) {
             char* stg = lds + S * SLOT + wave * (32 * RB);
             auto swz = [](int r, int c) { return NT == 2 ? c ^ (r & 15) : c ^ ((r >> 1) & 7); };
             uint16_t* outp = a.out + g * a.gsO;
-            const size_t obytes = (size_t)a.M * a.N * 2;
+            const size_t obytes = (size_t)a.orows * a.N * 2;
             const auto orsrc = __builtin_amdgcn_make_buffer_rsrc(outp, 0, (int)obytes, 0x00020000);
             const auto arsrc = __builtin_amdgcn_make_buffer_rsrc(
                 const_cast<uint16_t*>(a.addend ? a.addend + g * a.gsO : outp), 0, (int)obytes, 0x00020000);
@@ -276,7 +279,12 @@ __global__ __launch_bounds__(512) void k_gemm_ring(RingGemmArgs a) {
 #pragma unroll
                 for (int it = 0; it < 2 * NT; ++it) {
                     const int m = m0 + wm * 64 + ii * 32 + it * RPI + rr;
-                    off[it] = m < a.M ? (unsigned)m * (unsigned)a.N * 2u + nb : 0xfffffff0u;
+                    unsigned orow = (unsigned)m;
+                    if (a.scatter) {  // the strided input gradient: output pixel -> input pixel row
+                        const int PQ = a.sP * a.sQ, b = m / PQ, pq = m - b * PQ, p = pq / a.sQ, q = pq - p * a.sQ;
+                        orow = (unsigned)((b * a.sH + a.sst * p) * a.sW + a.sst * q);
+                    }
+                    off[it] = m < a.M ? orow * (unsigned)a.N * 2u + nb : 0xfffffff0u;
                 }
                 // (the addend test hoisted out of the loops: a per-element one branches and waits
                 // vmcnt around every store)
@@ -414,8 +422,10 @@ int conv1x1_gemm(long long M, int Kr, int N, int G, const void* A, long long gsA
                  const int* sgeo) {
     RingGemmArgs r;
     memset(&r, 0, sizeof(r));
-    if (sgeo) {  // {stride, H, W, P, Q}: A rows gathered from the strided input
-        r.sst = sgeo[0]; r.sH = sgeo[1]; r.sW = sgeo[2]; r.sP = sgeo[3]; r.sQ = sgeo[4];
+    r.orows = M;
+    if (sgeo) {  // {stride, H, W, P, Q, scatter}: A rows gathered from / out rows scattered to the strided map
+        r.sst = sgeo[0]; r.sH = sgeo[1]; r.sW = sgeo[2]; r.sP = sgeo[3]; r.sQ = sgeo[4]; r.scatter = sgeo[5];
+        if (r.scatter) r.orows = M / ((long long)r.sP * r.sQ) * r.sH * r.sW;
     }
     r.A = (const uint16_t*)A;
     r.B = (const uint16_t*)B;
@@ -428,7 +438,7 @@ int conv1x1_gemm(long long M, int Kr, int N, int G, const void* A, long long gsA
     r.tiles_n = N / BN;
     r.tiles = G * r.tiles_m * r.tiles_n;
     r.gsA = gsA; r.gsB = gsB; r.gsO = gsO;
-    r.stats = addend ? nullptr : stats;
+    r.stats = addend || r.scatter ? nullptr : stats;
     r.bnx = r.stats ? bnx : nullptr;
     r.bncoef = bncoef;
     r.bnmean = bnmean;

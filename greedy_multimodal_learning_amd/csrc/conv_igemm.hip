@@ -3001,7 +3001,7 @@ extern "C" int gm_conv2d_fwd_grouped_bf16(const gm_conv_desc_hw* d, int G, const
         const long long Mo = (long long)d->N * P * Q;
         if (gm::conv1x1s_ok(d->R, d->S, d->stride_h, d->stride_w, d->pad_h, d->pad_w, Mo, d->C, d->K) &&
             M * d->C < (1ll << 30)) {  // the downsample: A rows gathered at stride 2
-            const int geo[5] = {2, d->H, d->W, P, Q};
+            const int geo[6] = {2, d->H, d->W, P, Q, 0};
             return gm::conv1x1_gemm(Mo, d->C, d->K, G, x, M * d->C, w, w_stride, y, Mo * d->K, nullptr,
                                     as_stream(stream), "conv1x1/s2 fwd", nullptr, nullptr, nullptr, nullptr, nullptr,
                                     geo);
@@ -3063,7 +3063,7 @@ extern "C" int gm_conv2d_fwd_grouped_bn_stats_bf16(const gm_conv_desc_hw* d, int
         const long long Mi = (long long)d->N * d->H * d->W;
         if (gm::conv1x1s_ok(d->R, d->S, d->stride_h, d->stride_w, d->pad_h, d->pad_w, M, d->C, d->K) &&
             Mi * d->C < (1ll << 30)) {  // the downsample: A rows gathered at stride 2 (M = output pixels)
-            const int geo[5] = {2, d->H, d->W, a.cls[0].P, a.cls[0].Q};
+            const int geo[6] = {2, d->H, d->W, a.cls[0].P, a.cls[0].Q, 0};
             *rows_out = (int)((M + 63) / 64);
             return gm::conv1x1_gemm(M, d->C, d->K, G, x, Mi * d->C, w, w_stride, y, M * d->K, nullptr,
                                     as_stream(stream), "conv1x1/s2 fwd", stats, nullptr, nullptr, nullptr, nullptr,
@@ -3170,6 +3170,23 @@ static int dgrad_grouped(const gm_conv_desc* d, int G, const void* dy, const voi
         if (gm::conv1x1_ok(d->R, d->S, d->stride, d->stride, d->pad, d->pad, M, d->K, d->C))
             return gm::conv1x1_gemm(M, d->K, d->C, G, dy, M * d->K, wt, wt_stride, dx, M * d->C, addend,
                                     as_stream(stream), "conv1x1 dgrad", nullptr, nullptr, nullptr, nullptr, amask);
+        const long long Mo = (long long)d->N * P * Q;
+        if (d->stride == 2 && gm::conv1x1s_ok(d->R, d->S, 2, 2, d->pad, d->pad, Mo, d->K, d->C) &&
+            M * d->C < (1ll << 30)) {
+            // the downsample's input gradient: dy rows dense, out rows scattered to the even pixels; the
+            // others hold the (masked) addend or zero - one pass over dx unless the addend is dx itself
+            hipStream_t s = as_stream(stream);
+            if (addend != dx) {
+                const size_t n = (size_t)G * M * d->C;
+                k_zero_bf16<<<(int)((n / 8 + 255) / 256 < 4096 ? (n / 8 + 255) / 256 : 4096), 256, 0, s>>>(
+                    (uint16_t*)dx, n, (const uint16_t*)addend, addend ? amask : nullptr);
+                if ((rc = check_launch("k_zero_bf16"))) return rc;
+            }
+            const int geo[6] = {2, d->H, d->W, P, Q, 1};
+            return gm::conv1x1_gemm(Mo, d->K, d->C, G, dy, Mo * d->K, wt, wt_stride, dx, M * d->C,
+                                    addend ? dx : nullptr, s, "conv1x1/s2 dgrad", nullptr, nullptr, nullptr, nullptr,
+                                    nullptr, geo);
+        }
     }
     ConvArgs a;
     const bool full = dgrad_setup(d, dy, wt, dx, a);

@@ -714,6 +714,61 @@ def test_conv1x1_s2_forward_gathers_rows(dev, shape):
         _close(pg[:, 1], (yv * yv).sum(0), 1e-4)
 
 
+@pytest.mark.parametrize("shape", [(2, 256, 56, 56, 512, 2), (3, 64, 28, 28, 128, 2), (1, 64, 15, 13, 128, 2),
+                                   (2, 512, 28, 28, 1024, 12)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_conv1x1_s2_input_gradient_scatters_rows(dev, shape):
+    """The 1x1 / s2 downsample's input gradient on k_gemm_ring: dy rows read densely, output rows
+    scattered to the even pixels, the odd ones zero / the join addend (plain, masked, in place) -
+    against fp32 PyTorch and the im2col kernel (mode 1); the odd pixels exactly zero / the addend."""
+    import ctypes
+    from greedy_multimodal_learning_amd import _lib as L
+    N, C, H, W, K, G = shape
+    P, Q = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    torch.manual_seed(sum(shape) + 1)
+    dy = torch.randn(G * N, P, Q, K, device=dev).bfloat16()
+    w = (torch.randn(G, K, C, device=dev) / K ** 0.5).bfloat16()
+    wt = w.transpose(1, 2).contiguous()  # [G][C][K]
+    add = torch.randn(G * N, H, W, C, device=dev).bfloat16()
+    mask = torch.randint(0, 256, (add.numel() // 8,), device=dev, dtype=torch.uint8)
+    lib = L.load()
+    st = L.stream_of(dev)
+    dd = L.ConvDesc(N, H, W, C, K, 1, 1, 2, 0)
+    res = {}
+    try:
+        for mode in (2, 1):
+            L.check(lib.gm_conv_set_1x1_gemm(mode), "1x1 gemm")
+            dx = torch.full((G * N, H, W, C), 7.0, device=dev, dtype=torch.bfloat16)
+            L.check(lib.gm_conv2d_dgrad_grouped_bf16(ctypes.byref(dd), G, dy.data_ptr(), wt.data_ptr(), C * K,
+                                                     dx.data_ptr(), 0, 0, 0, st), "dgrad")
+            dxa = add.clone()  # in place
+            L.check(lib.gm_conv2d_dgrad_grouped_bf16(ctypes.byref(dd), G, dy.data_ptr(), wt.data_ptr(), C * K,
+                                                     dxa.data_ptr(), dxa.data_ptr(), 0, 0, st), "dgrad in place")
+            dxm = torch.empty_like(dx)
+            L.check(lib.gm_conv2d_dgrad_grouped_masked_bf16(ctypes.byref(dd), G, dy.data_ptr(), wt.data_ptr(),
+                                                            C * K, dxm.data_ptr(), add.data_ptr(), mask.data_ptr(),
+                                                            0, 0, st), "dgrad masked")
+            torch.cuda.synchronize()
+            res[mode] = (dx, dxa, dxm)
+    finally:
+        L.check(lib.gm_conv_set_1x1_gemm(2), "1x1 gemm")
+    bits = ((mask.to(torch.int32)[:, None] >> torch.arange(8, device=dev)) & 1).reshape(add.shape).bool()
+    madd = torch.where(bits, add, torch.zeros((), dtype=add.dtype, device=dev))
+    for i in range(3):  # (the im2col kernel may split K: another fp32 order)
+        _close(res[2][i], res[1][i], 8e-3)
+    for g in range(G):
+        sl = slice(g * N, (g + 1) * N)
+        ref = torch.zeros(N, H, W, C, device=dev)
+        ref[:, ::2, ::2, :] = (dy[sl].float().reshape(-1, K) @ w[g].float()).reshape(N, P, Q, C)
+        _close(res[2][0][sl], ref, 1e-2)
+        _close(res[2][1][sl], ref + add[sl].float(), 1e-2)
+        _close(res[2][2][sl], ref + madd[sl].float(), 1e-2)
+        odd = torch.ones(H, W, dtype=torch.bool, device=dev)
+        odd[::2, ::2] = False
+        assert torch.equal(res[2][0][sl][:, odd], torch.zeros_like(res[2][0][sl][:, odd]))
+        assert torch.equal(res[2][2][sl][:, odd], madd[sl][:, odd])
+
+
 @pytest.mark.parametrize("case", [("bf16_cl", 2, 4, 224, 224), ("bf16_cl", 3, 2, 37, 30), ("f32_nchw", 2, 3, 64, 64),
                                   ("bf16_nchw", 2, 2, 31, 40), ("f32_cl", 4, 1, 19, 22)],
                          ids=lambda c: "x".join(map(str, c)))
