@@ -66,7 +66,7 @@ def parse():
                     help="copy each step's resident batch into the engine's static input buffers (the pre-r06 "
                          "form) instead of binding the two resident batches as graph inputs")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_group_sumsq.json"))
-    ap.add_argument("--conv-traffic-file", default=os.path.join(ROOT, "profiles", "r06_traffic_conv_family.json"))
+    ap.add_argument("--conv-traffic-file", default=os.path.join(ROOT, "profiles", "r06g_traffic_conv_family.json"))
     ap.add_argument("--mmtm-traffic-file", default=os.path.join(ROOT, "profiles", "r03_traffic_mmtm.json"))
     ap.add_argument("--profile", action="store_true",
                     help="steps only (no roofline / cpu_baseline measurements): for rocprofv3 runs")
